@@ -1,0 +1,44 @@
+# Top-level build: the HIP scan library, the drop-in CLI and the generator.
+# Everything is built in-tree so the .so files travel to the GPU box.
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+ARCH    ?= gfx950
+CFLAGS  ?= -O2 -g -Wall -Wno-alloc-size-larger-than -fPIC
+HIPFLAGS ?= -O3 -g --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall
+LIBDIR  = grom_amd/lib
+BINDIR  = grom_amd/bin
+
+HOST_SRC = grom_amd/csrc/bamio.c grom_amd/csrc/stream.c grom_amd/csrc/tables.c grom_amd/csrc/synth.c grom_amd/csrc/hostapi.c grom_amd/csrc/grom_main.c
+HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC))
+HDRS = include/grom_amd.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h
+
+all: $(LIBDIR)/libgrom_amd.so $(BINDIR)/grom $(BINDIR)/grom_synth oracle
+
+build/%.o: grom_amd/csrc/%.c $(HDRS)
+	@mkdir -p build
+	$(CC) $(CFLAGS) -c $< -o $@
+
+build/scan.o: grom_amd/csrc/scan.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libgrom_amd.so: build/scan.o $(HOST_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lz -lm
+
+$(BINDIR)/grom: grom_amd/csrc/grom_cli.c $(LIBDIR)/libgrom_amd.so $(HDRS)
+	@mkdir -p $(BINDIR)
+	$(CC) $(CFLAGS) -o $@ grom_amd/csrc/grom_cli.c -L$(LIBDIR) -lgrom_amd -Wl,-rpath,'$$ORIGIN/../lib' -lz -lm
+
+$(BINDIR)/grom_synth: tools/grom_synth.c build/synth.o build/bamio.o
+	@mkdir -p $(BINDIR)
+	$(CC) $(CFLAGS) -o $@ $^ -lz -lm
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIBDIR) $(BINDIR)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

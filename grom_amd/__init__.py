@@ -1,0 +1,217 @@
+"""grom_amd -- Python view of the MI355X-native GROM scan library.
+
+The product is the C ABI in ``include/grom_amd.h`` (``grom_amd/lib/libgrom_amd.so``)
+and the drop-in CLI ``grom_amd/bin/grom``.  This module only binds them with
+ctypes for tests and ``bench.py``; it has no compute of its own and raises if the
+HIP library is missing (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(ROOT)
+LIB_PATH = os.path.join(ROOT, "lib", "libgrom_amd.so")
+GROM_BIN = os.path.join(ROOT, "bin", "grom")
+SYNTH_BIN = os.path.join(ROOT, "bin", "grom_synth")
+MAX_TRIALS = 1000
+NCOUNT = 40
+
+
+class Params(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "min_mapq", "rd_min_mapq", "min_base_qual", "min_snv", "ploidy", "gender", "splitread", "rmdup", "vcf",
+        "overlap_mult", "sv_list_len", "rmdup_list_len", "read_name_len", "sc_min")] + \
+        [(n, C.c_double) for n in ("min_snv_ratio", "min_ave_bq", "snv_rd_min_factor", "high_cov_min_snv_ratio")] + \
+        [(n, C.c_int32) for n in ("insert_mean", "insert_min_size", "insert_max_size", "lseq", "one_base_rd_len",
+                                  "half_one_base_rd_len", "r14_one_base_rd_len", "r34_one_base_rd_len")]
+
+
+class Chrom(C.Structure):
+    _fields_ = [("ref", C.c_void_p), ("len", C.c_int64), ("name", C.c_char_p), ("tid", C.c_int32),
+                ("n_skip", C.c_int32), ("p_last", C.c_int32)]
+
+
+class Reads(C.Structure):
+    _fields_ = [("n", C.c_int64), ("n_cigar_ops", C.c_int64), ("n_bases", C.c_int64)] + \
+        [(n, C.c_void_p) for n in ("pos", "flag", "mapq", "mtid", "mpos", "isize", "l_qseq", "cigar_off", "cigar",
+                                   "base_off", "seq", "qual", "name_id")]
+
+
+class Out(C.Structure):
+    _fields_ = [("vcf", C.c_void_p), ("vcf_len", C.c_size_t), ("vcf_cap", C.c_size_t),
+                ("ctx", C.c_void_p), ("ctx_len", C.c_size_t), ("ctx_cap", C.c_size_t)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_pileup", C.c_double), ("bases_evaluated", C.c_int64),
+                ("snv_candidates", C.c_int64), ("mismatch_events", C.c_int64)]
+
+
+# every function declared in include/grom_amd.h, with its ctypes signature
+_SIGS = {
+    "grom_abi_version": (C.c_int, []),
+    "grom_last_error": (C.c_char_p, []),
+    "grom_dev_init": (C.c_int, [C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
+    "grom_dev_fini": (None, [C.c_int]),
+    "grom_scan_chrom": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Out), C.POINTER(Stats)]),
+    "grom_scan_chrom_device": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Out),
+                                         C.POINTER(Stats)]),
+    "grom_debug_counts": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(C.c_int32), C.c_void_p,
+                                    C.c_int64, C.c_void_p]),
+    "grom_build_tables": (None, [C.c_int32, C.c_void_p, C.c_void_p]),
+    "grom_default_params": (None, [C.POINTER(Params)]),
+    "grom_params_set_insert": (None, [C.POINTER(Params), C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "grom_out_free": (None, [C.POINTER(Out)]),
+    "grom_upload": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Chrom), C.POINTER(Reads)]),
+    "grom_synth_batch": (C.c_void_p, [C.c_int64, C.c_double, C.c_int32, C.c_double, C.c_double, C.c_uint64,
+                                      C.POINTER(Params)]),
+    "grom_batch_get": (C.c_int, [C.c_void_p, C.POINTER(Chrom), C.POINTER(Reads)]),
+    "grom_batch_release": (None, [C.c_void_p]),
+    "grom_cli_main": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """The loaded HIP library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"grom_amd: {LIB_PATH} missing -- run `make` (or __graft_entry__.build()); "
+                               "there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().grom_last_error().decode()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
+
+
+def default_params() -> Params:
+    p = Params()
+    lib().grom_default_params(C.byref(p))
+    return p
+
+
+def build_tables(min_mapq: int = 20):
+    """(hez, mq) binomial tables exactly as a `-q min_mapq` run uses them."""
+    hez = np.zeros((MAX_TRIALS + 1, MAX_TRIALS + 1), np.float64)
+    mq = np.zeros_like(hez)
+    lib().grom_build_tables(min_mapq, hez.ctypes.data, mq.ctypes.data)
+    return hez, mq
+
+
+class Device:
+    """One initialised GPU (grom_dev_init / grom_dev_fini)."""
+
+    def __init__(self, device: int, params: Params):
+        self.device = device
+        self.params = params
+        self.hez, self.mq = build_tables(params.min_mapq)
+        check(lib().grom_dev_init(device, C.byref(params), self.hez.ctypes.data, self.mq.ctypes.data),
+              "grom_dev_init")
+
+    def close(self):
+        lib().grom_dev_fini(self.device)
+
+    def scan(self, chrom: Chrom, reads: Reads, device_resident: bool = False):
+        out, st = Out(), Stats()
+        fn = lib().grom_scan_chrom_device if device_resident else lib().grom_scan_chrom
+        check(fn(self.device, C.byref(chrom), C.byref(reads), C.byref(out), C.byref(st)), "scan")
+        text = C.string_at(out.vcf, out.vcf_len).decode() if out.vcf_len else ""
+        lib().grom_out_free(C.byref(out))
+        return text, st
+
+    def upload(self, chrom: Chrom, reads: Reads):
+        dc, dr = Chrom(), Reads()
+        check(lib().grom_upload(self.device, C.byref(chrom), C.byref(reads), C.byref(dc), C.byref(dr)), "upload")
+        return dc, dr
+
+    def debug_counts(self, chrom: Chrom, reads: Reads):
+        lo = max(self.params.one_base_rd_len // 4 + 1, 2 * self.params.insert_max_size + 1)
+        n_eval = max(chrom.p_last - lo + 1, 0)
+        cnt = np.zeros((max(n_eval, 1), NCOUNT), np.int32)
+        caf = np.zeros((3, chrom.len), np.int32)
+        first = C.c_int32(0)
+        check(lib().grom_debug_counts(self.device, C.byref(chrom), C.byref(reads), C.byref(first), cnt.ctypes.data,
+                                      cnt.size, caf.ctypes.data), "grom_debug_counts")
+        return cnt[:n_eval], caf
+
+
+class SynthBatch:
+    """A synthetic chromosome and the read batch its scan ingests (host memory)."""
+
+    def __init__(self, length: int, coverage: float = 30.0, read_len: int = 150, insert_mean: float = 500.0,
+                 insert_sd: float = 50.0, seed: int = 2, params: Params | None = None):
+        self.params = params if params is not None else default_params()
+        self.h = lib().grom_synth_batch(length, coverage, read_len, insert_mean, insert_sd, seed,
+                                        C.byref(self.params))
+        if not self.h:
+            raise RuntimeError("grom_synth_batch failed")
+        self.chrom, self.reads = Chrom(), Reads()
+        check(lib().grom_batch_get(self.h, C.byref(self.chrom), C.byref(self.reads)), "grom_batch_get")
+
+    def close(self):
+        if self.h:
+            lib().grom_batch_release(self.h)
+            self.h = None
+
+    @property
+    def n_reads(self) -> int:
+        return self.reads.n
+
+    @property
+    def n_bases(self) -> int:
+        return self.reads.n_bases
+
+
+def cli_main(args, env=None, cwd=None) -> int:
+    """Run the drop-in CLI in this process (loads the HIP library here)."""
+    saved_env, saved_cwd = dict(os.environ), os.getcwd()
+    try:
+        if env:
+            os.environ.update(env)
+        if cwd:
+            os.chdir(cwd)
+        argv = [b"grom"] + [str(a).encode() for a in args]
+        arr = (C.c_char_p * (len(argv) + 1))(*argv, None)
+        return lib().grom_cli_main(len(argv), arr)
+    finally:
+        os.chdir(saved_cwd)
+        os.environ.clear()
+        os.environ.update(saved_env)
+
+
+def run_grom(args, env=None, check_rc=True, timeout=600):
+    """Run the drop-in CLI as a subprocess (GPU)."""
+    e = dict(os.environ)
+    if env:
+        e.update(env)
+    r = subprocess.run([GROM_BIN] + list(args), env=e, capture_output=True, text=True, timeout=timeout)
+    if check_rc and r.returncode != 0:
+        raise RuntimeError(f"grom failed ({r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}")
+    return r
+
+
+def run_synth(prefix, *args, timeout=600):
+    r = subprocess.run([SYNTH_BIN, "-o", prefix] + [str(a) for a in args], capture_output=True, text=True,
+                       timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"grom_synth failed: {r.stderr}")
+    return prefix + ".bam", prefix + ".fa"

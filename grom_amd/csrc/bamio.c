@@ -1,0 +1,344 @@
+/*
+ * bamio.c -- BGZF/BAM reader and writer on zlib (see bamio.h).
+ */
+#include "bamio.h"
+
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+#include <unistd.h>
+
+#define BGZF_MAX_BLOCK 65536
+#define BGZF_WRITE_PAYLOAD 0xff00
+
+const char grom_nt16_rev[16] = {'=', 'A', 'C', 'M', 'G', 'R', 'S', 'V',
+                                'T', 'W', 'Y', 'H', 'K', 'D', 'B', 'N'};
+
+static const unsigned char BGZF_EOF_BLOCK[28] = {
+    0x1f, 0x8b, 0x08, 0x04, 0x00, 0x00, 0x00, 0x00, 0x00, 0xff, 0x06, 0x00, 0x42, 0x43,
+    0x02, 0x00, 0x1b, 0x00, 0x03, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00};
+
+static uint16_t rd16(const unsigned char *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static uint32_t rd32(const unsigned char *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static void wr16(unsigned char *p, uint16_t v) { p[0] = v & 0xff; p[1] = v >> 8; }
+static void wr32(unsigned char *p, uint32_t v) {
+    p[0] = v & 0xff; p[1] = (v >> 8) & 0xff; p[2] = (v >> 16) & 0xff; p[3] = v >> 24;
+}
+
+int bgzf_open_read(bgzf_reader *r, const char *path) {
+    memset(r, 0, sizeof(*r));
+    r->fp = fopen(path, "rb");
+    if (!r->fp) return -1;
+    r->blk = (unsigned char *)malloc(BGZF_MAX_BLOCK);
+    r->cbuf = (unsigned char *)malloc(BGZF_MAX_BLOCK);
+    if (!r->blk || !r->cbuf) return -1;
+    return 0;
+}
+
+void bgzf_close_read(bgzf_reader *r) {
+    if (r->fp) fclose(r->fp);
+    free(r->blk);
+    free(r->cbuf);
+    memset(r, 0, sizeof(*r));
+}
+
+/* inflate the next block into r->blk; returns block length, 0 at EOF, -1 error */
+static int bgzf_next_block(bgzf_reader *r) {
+    unsigned char hdr[18];
+    size_t got = fread(hdr, 1, 18, r->fp);
+    if (got == 0) { r->eof = 1; return 0; }
+    if (got != 18 || hdr[0] != 0x1f || hdr[1] != 0x8b || hdr[3] != 0x04) return -1;
+    uint16_t xlen = rd16(hdr + 10);
+    /* locate the BC subfield; hdr holds the first 6 bytes of the extra field */
+    unsigned char extra[1024];
+    if (xlen > sizeof(extra) || xlen < 6) return -1;
+    memcpy(extra, hdr + 12, 6);
+    if (xlen > 6 && fread(extra + 6, 1, xlen - 6, r->fp) != (size_t)(xlen - 6)) return -1;
+    int bsize = -1;
+    for (int o = 0; o + 4 <= xlen;) {
+        int sl = rd16(extra + o + 2);
+        if (extra[o] == 'B' && extra[o + 1] == 'C' && sl == 2) { bsize = rd16(extra + o + 4); break; }
+        o += 4 + sl;
+    }
+    if (bsize < 0) return -1;
+    int clen = bsize + 1 - 12 - xlen; /* deflate data + 8-byte trailer */
+    if (clen < 8 || clen > BGZF_MAX_BLOCK) return -1;
+    if (fread(r->cbuf, 1, clen, r->fp) != (size_t)clen) return -1;
+    uint32_t isize = rd32(r->cbuf + clen - 4);
+    if (isize > BGZF_MAX_BLOCK) return -1;
+    if (isize == 0) { r->blk_len = 0; r->blk_off = 0; return 1; /* empty block (e.g. EOF marker) */ }
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    if (inflateInit2(&zs, -15) != Z_OK) return -1;
+    zs.next_in = r->cbuf;
+    zs.avail_in = clen - 8;
+    zs.next_out = r->blk;
+    zs.avail_out = BGZF_MAX_BLOCK;
+    int rc = inflate(&zs, Z_FINISH);
+    inflateEnd(&zs);
+    if (rc != Z_STREAM_END || zs.total_out != isize) return -1;
+    r->blk_len = (int)isize;
+    r->blk_off = 0;
+    return 1;
+}
+
+int bgzf_read(bgzf_reader *r, void *dst, int n) {
+    unsigned char *d = (unsigned char *)dst;
+    int done = 0;
+    while (done < n) {
+        if (r->blk_off >= r->blk_len) {
+            int rc = bgzf_next_block(r);
+            if (rc < 0) return -1;
+            if (rc == 0) return done == 0 ? 0 : -1;
+            continue;
+        }
+        int take = r->blk_len - r->blk_off;
+        if (take > n - done) take = n - done;
+        memcpy(d + done, r->blk + r->blk_off, take);
+        r->blk_off += take;
+        done += take;
+    }
+    return done;
+}
+
+int bgzf_open_write(bgzf_writer *w, const char *path, int level) {
+    memset(w, 0, sizeof(*w));
+    w->fp = fopen(path, "wb");
+    if (!w->fp) return -1;
+    w->buf = (unsigned char *)malloc(BGZF_MAX_BLOCK);
+    w->level = level;
+    return w->buf ? 0 : -1;
+}
+
+int bgzf_flush_block(bgzf_writer *w) {
+    if (w->len == 0) return 0;
+    unsigned char out[BGZF_MAX_BLOCK + 64];
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    if (deflateInit2(&zs, w->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return -1;
+    zs.next_in = w->buf;
+    zs.avail_in = w->len;
+    zs.next_out = out + 18;
+    zs.avail_out = BGZF_MAX_BLOCK - 18 - 8;
+    int rc = deflate(&zs, Z_FINISH);
+    int clen = (int)zs.total_out;
+    deflateEnd(&zs);
+    if (rc != Z_STREAM_END) return -1;
+    static const unsigned char h[12] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0, 0xff, 0x06, 0x00};
+    memcpy(out, h, 12);
+    out[12] = 'B'; out[13] = 'C';
+    wr16(out + 14, 2);
+    wr16(out + 16, (uint16_t)(18 + clen + 8 - 1));
+    uint32_t crc = crc32(0L, w->buf, w->len);
+    wr32(out + 18 + clen, crc);
+    wr32(out + 18 + clen + 4, (uint32_t)w->len);
+    if (fwrite(out, 1, 18 + clen + 8, w->fp) != (size_t)(18 + clen + 8)) return -1;
+    w->len = 0;
+    return 0;
+}
+
+int bgzf_write(bgzf_writer *w, const void *src, int n) {
+    const unsigned char *s = (const unsigned char *)src;
+    while (n > 0) {
+        int take = BGZF_WRITE_PAYLOAD - w->len;
+        if (take > n) take = n;
+        memcpy(w->buf + w->len, s, take);
+        w->len += take;
+        s += take;
+        n -= take;
+        if (w->len >= BGZF_WRITE_PAYLOAD && bgzf_flush_block(w) != 0) return -1;
+    }
+    return 0;
+}
+
+int bgzf_close_write(bgzf_writer *w) {
+    int rc = bgzf_flush_block(w);
+    if (fwrite(BGZF_EOF_BLOCK, 1, 28, w->fp) != 28) rc = -1;
+    if (fclose(w->fp) != 0) rc = -1;
+    free(w->buf);
+    memset(w, 0, sizeof(*w));
+    return rc;
+}
+
+int bam_read_header(bgzf_reader *r, bam_hdr *h) {
+    memset(h, 0, sizeof(*h));
+    unsigned char b4[4];
+    if (bgzf_read(r, b4, 4) != 4 || memcmp(b4, "BAM\1", 4) != 0) return -1;
+    if (bgzf_read(r, b4, 4) != 4) return -1;
+    h->l_text = (int32_t)rd32(b4);
+    h->text = (char *)calloc((size_t)h->l_text + 1, 1);
+    if (h->l_text && bgzf_read(r, h->text, h->l_text) != h->l_text) return -1;
+    if (bgzf_read(r, b4, 4) != 4) return -1;
+    h->n_ref = (int32_t)rd32(b4);
+    h->ref_name = (char **)calloc(h->n_ref > 0 ? h->n_ref : 1, sizeof(char *));
+    h->ref_len = (int32_t *)calloc(h->n_ref > 0 ? h->n_ref : 1, sizeof(int32_t));
+    for (int i = 0; i < h->n_ref; i++) {
+        if (bgzf_read(r, b4, 4) != 4) return -1;
+        int32_t ln = (int32_t)rd32(b4);
+        h->ref_name[i] = (char *)calloc((size_t)ln + 1, 1);
+        if (bgzf_read(r, h->ref_name[i], ln) != ln) return -1;
+        if (bgzf_read(r, b4, 4) != 4) return -1;
+        h->ref_len[i] = (int32_t)rd32(b4);
+    }
+    return 0;
+}
+
+void bam_free_header(bam_hdr *h) {
+    for (int i = 0; i < h->n_ref; i++) free(h->ref_name[i]);
+    free(h->ref_name);
+    free(h->ref_len);
+    free(h->text);
+    memset(h, 0, sizeof(*h));
+}
+
+int bam_read_rec(bgzf_reader *r, bam_rec *b) {
+    unsigned char c[36];
+    int got = bgzf_read(r, c, 4);
+    if (got == 0) return 0;
+    if (got != 4) return -1;
+    int32_t block = (int32_t)rd32(c);
+    if (block < 32) return -1;
+    if (bgzf_read(r, c + 4, 32) != 32) return -1;
+    b->tid = (int32_t)rd32(c + 4);
+    b->pos = (int32_t)rd32(c + 8);
+    b->l_qname = c[12];
+    b->mapq = c[13];
+    b->bin = rd16(c + 14);
+    b->n_cigar = rd16(c + 16);
+    b->flag = rd16(c + 18);
+    b->l_qseq = (int32_t)rd32(c + 20);
+    b->mtid = (int32_t)rd32(c + 24);
+    b->mpos = (int32_t)rd32(c + 28);
+    b->isize = (int32_t)rd32(c + 32);
+    b->data_len = block - 32;
+    if (b->data_len > b->m_data) {
+        b->m_data = (b->data_len + 255) & ~255;
+        b->data = (uint8_t *)realloc(b->data, b->m_data);
+        if (!b->data) return -1;
+    }
+    if (bgzf_read(r, b->data, b->data_len) != b->data_len) return -1;
+    return 1;
+}
+
+void bam_free_rec(bam_rec *b) {
+    free(b->data);
+    memset(b, 0, sizeof(*b));
+}
+
+int bam_write_header(bgzf_writer *w, const bam_hdr *h) {
+    unsigned char b4[4];
+    if (bgzf_write(w, "BAM\1", 4)) return -1;
+    wr32(b4, (uint32_t)h->l_text);
+    if (bgzf_write(w, b4, 4)) return -1;
+    if (h->l_text && bgzf_write(w, h->text, h->l_text)) return -1;
+    wr32(b4, (uint32_t)h->n_ref);
+    if (bgzf_write(w, b4, 4)) return -1;
+    for (int i = 0; i < h->n_ref; i++) {
+        int32_t ln = (int32_t)strlen(h->ref_name[i]) + 1;
+        wr32(b4, (uint32_t)ln);
+        if (bgzf_write(w, b4, 4) || bgzf_write(w, h->ref_name[i], ln)) return -1;
+        wr32(b4, (uint32_t)h->ref_len[i]);
+        if (bgzf_write(w, b4, 4)) return -1;
+    }
+    return 0;
+}
+
+int bam_write_rec(bgzf_writer *w, const bam_rec *b) {
+    unsigned char c[36];
+    wr32(c, (uint32_t)(32 + b->data_len));
+    wr32(c + 4, (uint32_t)b->tid);
+    wr32(c + 8, (uint32_t)b->pos);
+    c[12] = b->l_qname;
+    c[13] = b->mapq;
+    wr16(c + 14, b->bin);
+    wr16(c + 16, b->n_cigar);
+    wr16(c + 18, b->flag);
+    wr32(c + 20, (uint32_t)b->l_qseq);
+    wr32(c + 24, (uint32_t)b->mtid);
+    wr32(c + 28, (uint32_t)b->mpos);
+    wr32(c + 32, (uint32_t)b->isize);
+    /* keep a record inside one block when it fits, as htslib does */
+    if (w->len + 36 + b->data_len > BGZF_WRITE_PAYLOAD && w->len > 0) {
+        if (bgzf_flush_block(w)) return -1;
+    }
+    if (bgzf_write(w, c, 36)) return -1;
+    return bgzf_write(w, b->data, b->data_len);
+}
+
+/* size in bytes of one aux value of type t (not B/Z/H) */
+static int aux_type_size(uint8_t t) {
+    switch (t) {
+    case 'A': case 'c': case 'C': return 1;
+    case 's': case 'S': return 2;
+    case 'i': case 'I': case 'f': return 4;
+    case 'd': return 8;
+    default: return -1;
+    }
+}
+
+uint8_t *bam_aux_find(const bam_rec *b, const char tag[2]) {
+    uint8_t *s = bam_aux(b);
+    uint8_t *end = b->data + b->data_len;
+    while (s + 3 <= end) {
+        int hit = (s[0] == (uint8_t)tag[0] && s[1] == (uint8_t)tag[1]);
+        uint8_t t = s[2];
+        if (hit) return s + 2;
+        s += 3;
+        if (t == 'Z' || t == 'H') {
+            while (s < end && *s) s++;
+            s++;
+        } else if (t == 'B') {
+            if (s + 5 > end) return NULL;
+            int sz = aux_type_size(s[0]);
+            uint32_t n = rd32(s + 1);
+            if (sz < 0) return NULL;
+            s += 5 + (size_t)sz * n;
+        } else {
+            int sz = aux_type_size(t);
+            if (sz < 0) return NULL;
+            s += sz;
+        }
+    }
+    return NULL;
+}
+
+int bam_reg2bin(int beg, int end) {
+    --end;
+    if (beg >> 14 == end >> 14) return ((1 << 15) - 1) / 7 + (beg >> 14);
+    if (beg >> 17 == end >> 17) return ((1 << 12) - 1) / 7 + (beg >> 17);
+    if (beg >> 20 == end >> 20) return ((1 << 9) - 1) / 7 + (beg >> 20);
+    if (beg >> 23 == end >> 23) return ((1 << 6) - 1) / 7 + (beg >> 23);
+    if (beg >> 26 == end >> 26) return ((1 << 3) - 1) / 7 + (beg >> 26);
+    return 0;
+}
+
+int bai_write_minimal(const char *bam_path, int32_t n_ref) {
+    char path[4096];
+    snprintf(path, sizeof(path), "%s.bai", bam_path);
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    unsigned char b4[4];
+    fwrite("BAI\1", 1, 4, f);
+    wr32(b4, (uint32_t)n_ref);
+    fwrite(b4, 1, 4, f);
+    wr32(b4, 0);
+    for (int i = 0; i < n_ref; i++) {
+        fwrite(b4, 1, 4, f); /* n_bin */
+        fwrite(b4, 1, 4, f); /* n_intv */
+    }
+    return fclose(f);
+}
+
+int bai_exists(const char *bam_path) {
+    char path[4096];
+    snprintf(path, sizeof(path), "%s.bai", bam_path);
+    if (access(path, R_OK) == 0) return 1;
+    size_t n = strlen(bam_path);
+    if (n > 4 && strcmp(bam_path + n - 4, ".bam") == 0) {
+        snprintf(path, sizeof(path), "%.*s.bai", (int)(n - 4), bam_path);
+        if (access(path, R_OK) == 0) return 1;
+    }
+    return 0;
+}

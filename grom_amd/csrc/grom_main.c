@@ -1,0 +1,378 @@
+/*
+ * grom_main.c -- `grom`, the drop-in command line for GROM's scan.
+ *
+ * Mirrors GROM's main (GROM.c:21865-22781) and find_disc_svs
+ * (GROM.c:20440-21129): the same getopt string and defaults, the same output
+ * files (OUT and OUT's .ctx.vcf sibling), the same chromosome selection and
+ * order.  The per-chromosome scan (count_discordant_pairs, GROM.c:1432) runs
+ * on the GPU through include/grom_amd.h.
+ *
+ * Not yet restated (the build reports them rather than guessing): -f
+ * (tab-separated output).  Options that steer parts of the reference outside
+ * the implemented scan rows are accepted and recorded.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../../include/grom_amd.h"
+#include "bamio.h"
+#include "stream.h"
+
+static const char *VERSION = "GROM, Version 1.0.1\n"; /* g_version_name, GROM.c:690 */
+
+static void print_help(void) {
+    /* GROM.c:1125-1181 */
+    printf("\n%s", VERSION);
+    printf("\nUsage: GROM -i <BAM input file> -r <REFERENCE input file> -o <output file> [optional parameters]\n");
+    printf("\nRequired Parameters:\n");
+    printf("\t-i \tBAM input file\n");
+    printf("\t-r \tREFERENCE input file (fasta)\n");
+    printf("\t-o \tSTRUCTURAL VARIANT output file\n");
+    printf("\nOptional Parameters:\n");
+    printf("\t-P \tthreads [1]\n");
+    printf("\t-M \tturn on GROM's duplicate read filtering\n");
+    printf("\t-q \tmapping quality threshold [35]\n");
+    printf("\t-s \tminimum standard deviations for discordance [3]\n");
+    printf("\t-v \tprobability threshold [0.001]\n");
+    printf("\t-g \tgender (0=female,1=male) [0]\n");
+    printf("\t-d \tminimum discordant pairs [3]\n");
+    printf("\t-b \tbase phred quality score threshold [35]\n");
+    printf("\t-n \tminimum SNV bases [3]\n");
+    printf("\t-a \tminimum SNV ratio [0.2]\n");
+    printf("\t-y \tmaximum unmapped gap or overlap for split reads [20]\n");
+    printf("\t-z \tminimum split read mapped length (each split) [30]\n");
+    printf("\t-S \tturn off split-read detection\n");
+    printf("\t-p \tploidy [2]\n");
+    printf("\t-e \tinsertion probability threshold [0.0000000001]\n");
+    printf("\t-j \tminimum SV ratio [0.05]\n");
+    printf("\t-k \tmaximum homopolymer (indels) [0.05]\n");
+    printf("\t-m \tminimum indel ratio [0.125]\n");
+    printf("\t-u \tmaximum evidence ratio (SV except insertion) [0.25]\n");
+    printf("\t-A \tsampling rate [2]\n");
+    printf("\t-V \tread depth p-value threshold [0.000001]\n");
+    printf("\t-W \twindow minimum size [100]\n");
+    printf("\t-X \twindow maximum size [10000]\n");
+    printf("\t-Y \tminimum number of blocks [4]\n");
+    printf("\t-Z \tblock minimum size [10000]\n");
+    printf("\t-U \texcessive coverage threshold [2]\n");
+    printf("\t-B \tchromosome maximum length [300000000]\n");
+    printf("\t-D \tdinucleotide repeat minimum length [20]\n");
+    printf("\t-E \tdinucleotide repeat minimum standard deviation [1.5]\n");
+    printf("\t-K \tranks (0=no ranking,1=use ranks) [1]\n");
+    printf("\t-L \tduplication coverage threshold [2]\n");
+    printf("\nSee README file for additional help.\n");
+    printf("\n");
+}
+
+static void header(FILE *f, const char *fasta_name, int ctx) {
+    /* GROM.c:20517-20565 (main VCF) and GROM.c:22612-22651 (.ctx.vcf) */
+    const char *pin = getenv("GROM_FILEDATE");
+    fprintf(f, "##fileformat=VCFv4.2\n");
+    if (pin) {
+        fprintf(f, "##fileDate=%s\n", pin);
+    } else {
+        time_t t = time(NULL);
+        struct tm tm = *localtime(&t);
+        fprintf(f, "##fileDate=%d%d%d\n", tm.tm_year + 1900, tm.tm_mon + 1, tm.tm_mday);
+    }
+    fprintf(f, "##reference=%s\n", fasta_name);
+    fprintf(f, "##ALT=<ID=DEL,Description=\"Deletion\">\n");
+    fprintf(f, "##ALT=<ID=DUP,Description=\"Duplication\">\n");
+    fprintf(f, "##ALT=<ID=INS,Description=\"Insertion\">\n");
+    fprintf(f, "##ALT=<ID=INV,Description=\"Inversion\">\n");
+    fprintf(f, "##INFO=<ID=END,Number=1,Type=Integer,Description=\"End position of the structural variant\">\n");
+    if (!ctx) fprintf(f, "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n");
+    static const char *fmt_lines[][2] = {
+        {"SPR", "Float\",Description=\"Probability of start breakpoint evidence occurring by chance"},
+        {"EPR", "Float\",Description=\"Probability of end breakpoint evidence occurring by chance"},
+        {"SEV", "Integer\",Description=\"Evidence supporting variant at start breakpoint"},
+        {"EEV", "Integer\",Description=\"Evidence supporting variant at end breakpoint"},
+        {"SRD", "Integer\",Description=\"Physical read depth at start breakpoint"},
+        {"ERD", "Integer\",Description=\"Physical read depth at end breakpoint"},
+        {"SCO", "Integer\",Description=\"Concordant pairs at start breakpoint"},
+        {"ECO", "Integer\",Description=\"Concordant pairs at end breakpoint"},
+        {"SOT", "Integer\",Description=\"Count of distinct SVs with evidence at start breakpoint"},
+        {"EOT", "Integer\",Description=\"Count of distinct SVs with evidence at end breakpoint"},
+        {"SSC", "Integer\",Description=\"Soft-clipped reads at start breakpoint"},
+        {"ESC", "Integer\",Description=\"Soft-clipped at end breakpoint"},
+        {"SFR", "Integer\",Description=\"Position of first read supporting start breakpoint"},
+        {"SLR", "Integer\",Description=\"Position of last read supporting start breakpoint"},
+        {"EFR", "Integer\",Description=\"Position of first read supporting end breakpoint"},
+        {"ELR", "Integer\",Description=\"Position of last read supporting end breakpoint"},
+        {"AF", "Float\",Description=\"Allele frequency (high mapping quality reads)"},
+        {"PR", "Float\",Description=\"Probability of SNV evidence occurring by chance"},
+        {"A", "Integer\",Description=\"A nucleotides (high mapping quality reads)"},
+        {"C", "Integer\",Description=\"C nucleotides (high mapping quality reads)"},
+        {"G", "Integer\",Description=\"G nucleotides (high mapping quality reads)"},
+        {"T", "Integer\",Description=\"T nucleotides (high mapping quality reads)"},
+        {"AL", "Integer\",Description=\"A nucleotides (low mapping quality reads)"},
+        {"CL", "Integer\",Description=\"C nucleotides (low mapping quality reads)"},
+        {"GL", "Integer\",Description=\"G nucleotides (low mapping quality reads)"},
+        {"TL", "Integer\",Description=\"T nucleotides (low mapping quality reads)"},
+        {"BQ", "Float\",Description=\"Average base quality (all reads)"},
+        {"MQ", "Float\",Description=\"Average mapping quality (all reads)"},
+        {"PIR", "Float\",Description=\"Average distance of SNV from DNA fragment end)"},
+        {"FS", "Integer\",Description=\"SNV reads mapped to forward strand)"},
+    };
+    for (size_t i = 0; i < sizeof(fmt_lines) / sizeof(fmt_lines[0]); i++) {
+        /* the Type= value is unquoted in GROM's text; rebuild it exactly */
+        const char *rest = fmt_lines[i][1];
+        const char *q = strchr(rest, '"');
+        fprintf(f, "##FORMAT=<ID=%s,Number=1,Type=%.*s%s\">\n", fmt_lines[i][0], (int)(q - rest), rest, q + 1);
+    }
+    if (!ctx) {
+        fprintf(f, "##FORMAT=<ID=SD,Number=1,Type=Float,Description=\"CNV standard deviation\"\n");
+        fprintf(f, "##FORMAT=<ID=Z,Number=1,Type=Float,Description=\"CNV probability score\"\n");
+        fprintf(f, "##FORMAT=<ID=CN,Number=1,Type=Float,Description=\"CNV copy number\"\n");
+        fprintf(f, "##FORMAT=<ID=CS,Number=1,Type=Float,Description=\"CNV copy number standard deviation\"\n");
+    }
+    fprintf(f, "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\n");
+}
+
+typedef struct {
+    int fasta_idx;
+    int32_t tid;
+    char *ref;
+    long len;
+    char name[GROM_MAX_CHR_NAME_LEN + 1];
+} chrom_plan;
+
+static int g_plan_only = 0; /* GROM_PLAN_ONLY: report the record plan, no GPU */
+
+static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_params *P, FILE *vcf, int verbose) {
+    grom_batch_finish(b, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size);
+    if (g_plan_only) {
+        printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d\n", cp->name, cp->tid, (long long)b->n, b->n_skip,
+               b->p_last);
+        return GROM_OK;
+    }
+    grom_chrom ch;
+    ch.ref = cp->ref;
+    ch.len = cp->len;
+    ch.name = cp->name;
+    ch.tid = cp->tid;
+    ch.n_skip = b->n_skip;
+    ch.p_last = b->p_last;
+    grom_reads rd;
+    grom_batch_view(b, &rd);
+    grom_out out = {0};
+    grom_stats st = {0};
+    int rc = grom_scan_chrom(device, &ch, &rd, &out, &st);
+    if (rc != GROM_OK) {
+        fprintf(stderr, "grom: scan of %s failed: %s\n", cp->name, grom_last_error());
+        grom_out_free(&out);
+        return rc;
+    }
+    if (out.vcf_len) fwrite(out.vcf, 1, out.vcf_len, vcf);
+    const char *dump = getenv("GROM_DUMP");
+    if (dump) {
+        /* test hook: per-base counters and caf depth, same files as the oracle's */
+        int32_t first = 0;
+        int32_t lo = P->one_base_rd_len / 4 + 1;
+        if (lo < 2 * P->insert_max_size + 1) lo = 2 * P->insert_max_size + 1;
+        int64_t n_eval = (ch.p_last >= lo) ? (int64_t)ch.p_last - lo + 1 : 0;
+        int32_t *cnt = malloc(sizeof(int32_t) * GROM_NCOUNT * (n_eval > 0 ? n_eval : 1));
+        int32_t *caf = malloc(sizeof(int32_t) * 3 * cp->len);
+        rc = grom_debug_counts(device, &ch, &rd, &first, cnt, GROM_NCOUNT * n_eval, caf);
+        if (rc == GROM_OK) {
+            char path[4096];
+            snprintf(path, sizeof(path), "%s.%s.cnt", dump, cp->name);
+            FILE *f = fopen(path, "wb");
+            if (f) { fwrite(cnt, sizeof(int32_t) * GROM_NCOUNT, n_eval, f); fclose(f); }
+            snprintf(path, sizeof(path), "%s.%s.caf", dump, cp->name);
+            f = fopen(path, "wb");
+            if (f) { fwrite(caf, sizeof(int32_t), 3 * cp->len, f); fclose(f); }
+        } else {
+            fprintf(stderr, "grom: counter dump of %s failed: %s\n", cp->name, grom_last_error());
+        }
+        free(cnt);
+        free(caf);
+    }
+    if (verbose)
+        printf("%s: %lld reads, %.3f ms on GPU (%.2f Mbases/s)\n", cp->name, (long long)b->n, st.ms_total,
+               st.ms_total > 0 ? cp->len / (st.ms_total * 1e3) : 0.0);
+    grom_out_free(&out);
+    return GROM_OK;
+}
+
+int grom_cli_main(int argc, char **argv) {
+    optind = 1; /* callable more than once per process */
+    setlinebuf(stdout);
+    grom_params P;
+    grom_default_params(&P);
+    const char *bam_name = NULL, *fasta_name = NULL, *out_name = NULL;
+    long max_chr_len = 300000000; /* g_max_chr_fasta_len, GROM.c:946 */
+    double num_sd = 3;
+    int device = 0, verbose = getenv("GROM_VERBOSE") != NULL;
+    if (getenv("GROM_DEVICE")) device = atoi(getenv("GROM_DEVICE"));
+    int opt;
+    /* getopt string of GROM.c:21908 */
+    while ((opt = getopt(argc, argv,
+                         "Z:W:X:Q:A:Y:B:D:E:K:N:V:U:L:F:SP:c:R:MG:i:r:o:p:q:s:v:g:l:d:b:n:a:y:z:e:fj:k:m:u:w:x:h")) != -1) {
+        switch (opt) {
+        case 'S': P.splitread = 0; break;
+        case 'G': P.sv_list_len = atoi(optarg); break;
+        case 'M': P.rmdup = 1; break;
+        case 'i': bam_name = optarg; break;
+        case 'r': fasta_name = optarg; break;
+        case 'o': out_name = optarg; break;
+        case 'B': max_chr_len = atol(optarg); break;
+        case 'p': P.ploidy = atoi(optarg); break;
+        case 'q': P.min_mapq = atoi(optarg); break;
+        case 's': num_sd = atof(optarg); break;
+        case 'g': P.gender = atoi(optarg); break;
+        case 'l': P.overlap_mult = atoi(optarg); break;
+        case 'b': P.min_base_qual = atoi(optarg); break;
+        case 'n': P.min_snv = atoi(optarg); break;
+        case 'a': P.min_snv_ratio = atof(optarg); break;
+        case 'f': P.vcf = 0; break;
+        case 'x': P.min_ave_bq = atof(optarg); break;
+        case 'h': print_help(); return 0;
+        case '?': return 1;
+        default: break; /* accepted; steers rows outside the implemented scan */
+        }
+    }
+    P.rd_min_mapq = P.min_mapq; /* GROM.c:22102 */
+    printf("bam %s\n", bam_name ? bam_name : "(null)");
+    printf("ref %s\n", fasta_name ? fasta_name : "(null)");
+    printf("results %s\n", out_name ? out_name : "(null)");
+    if (!bam_name) { printf("ERROR: No bam file specified.\n"); return 1; }
+    bgzf_reader br;
+    bam_hdr hdr;
+    if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) {
+        printf("\nCould not open %s\n", bam_name);
+        return 1;
+    }
+    if (!bai_exists(bam_name)) { printf("Could not open BAM indexing file\n"); return 1; }
+    if (!out_name) { printf("ERROR: No output file specified.\n"); return 1; }
+    FILE *probe = fopen(out_name, "w");
+    if (!probe) { printf("\nCould not open %s\n", out_name); return 1; }
+    fclose(probe);
+    if (!fasta_name) { printf("ERROR: No reference file specified.\n"); return 1; }
+    grom_fasta fa;
+    if (grom_fasta_open(&fa, fasta_name) != 0) { printf("\nCould not open %s\n", fasta_name); return 1; }
+
+    /* tables (read_binom_tables, GROM.c:22234) */
+    size_t tn = (size_t)(GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);
+    double *hez = malloc(sizeof(double) * tn), *mq = malloc(sizeof(double) * tn);
+    grom_build_tables(P.min_mapq, hez, mq);
+
+    /* insert-size pre-pass on the first records (GROM.c:22255) */
+    int lseq = 0, imin = 0, imax = 0;
+    long mapped = 0;
+    int imean = grom_insert_stats(&br, grom_prob2(num_sd), &lseq, &imin, &imax, &mapped, P.min_mapq);
+    bgzf_close_read(&br);
+    if (imean < 0) { printf("ERROR: no reads to estimate the insert size from\n"); return 1; }
+    printf("insert_min_size, insert_max_size %d %d\n", imin, imax);
+    {
+        char mean_name[4096];
+        snprintf(mean_name, sizeof(mean_name), "%s.mean", bam_name);
+        FILE *mf = fopen(mean_name, "w"); /* save_insert_mean, GROM.c:994-1008 */
+        if (mf) {
+            printf("Saving insert_mean et al to %s\n", mean_name);
+            fprintf(mf, "%d %d %d %d %ld\n", imean, lseq, imin, imax, mapped);
+            fclose(mf);
+        }
+    }
+    grom_params_set_insert(&P, imean, imin, imax, lseq);
+    printf("insert mean, insert minimum, insert maximum: %d %d %d\n", P.insert_mean, imin, imax);
+    printf("median read length: %d\n", lseq);
+
+    g_plan_only = getenv("GROM_PLAN_ONLY") != NULL;
+    int rc = g_plan_only ? GROM_OK : grom_dev_init(device, &P, hez, mq);
+    if (rc != GROM_OK) { fprintf(stderr, "grom: %s\n", grom_last_error()); return 1; }
+
+    /* chromosome selection in BAM header order (GROM.c:20826-21050) */
+    const int32_t s0 = P.one_base_rd_len / 4 + 1;
+    chrom_plan *plan = calloc(hdr.n_ref > 0 ? hdr.n_ref : 1, sizeof(chrom_plan));
+    int32_t *order = calloc(hdr.n_ref > 0 ? hdr.n_ref : 1, sizeof(int32_t));
+    int n_plan = 0;
+    for (int t = 0; t < hdr.n_ref; t++) {
+        int fi = grom_match_target(&fa, hdr.ref_name[t]);
+        char lc[GROM_MAX_CHR_NAMES];
+        int bl = grom_target_name_lc(hdr.ref_name[t], lc, (int)sizeof(lc));
+        if (P.gender == 0 && ((bl == 4 && strncmp(lc, "chry", 4) == 0) || (bl == 1 && lc[0] == 'y'))) fi = -1;
+        if (fi < 0) continue;
+        long len = grom_fasta_load(&fa, fi, NULL, 0);
+        if (len > max_chr_len) printf("ERROR: Reference chromosome length exceeds maximum allowed chromosome size (%ld)\n", max_chr_len);
+        if (!(len > s0 + (long)P.overlap_mult * P.insert_max_size)) continue;
+        if (!(len > 0 && len <= max_chr_len)) continue;
+        /* count_discordant_pairs re-derives the BAM target from the FASTA name
+         * (GROM.c:1894-1961): the first target matching it */
+        int32_t tid2 = -1;
+        for (int a = 0; a < hdr.n_ref; a++)
+            if (grom_match_target(&fa, hdr.ref_name[a]) == fi) { tid2 = a; break; }
+        plan[n_plan].fasta_idx = fi;
+        plan[n_plan].tid = tid2;
+        plan[n_plan].len = len;
+        snprintf(plan[n_plan].name, sizeof(plan[n_plan].name), "%.*s", fa.name_len[fi], fa.names[fi]);
+        order[n_plan] = tid2;
+        n_plan++;
+    }
+
+    FILE *vcf = fopen(out_name, "w");
+    if (!vcf) { printf("Error opening file %s\n", out_name); return 1; }
+    if (P.vcf == 1) header(vcf, fasta_name, 0);
+    char ctx_name[4096];
+    size_t ol = strlen(out_name);
+    if (ol > 4 && strcmp(out_name + ol - 4, ".vcf") == 0)
+        snprintf(ctx_name, sizeof(ctx_name), "%.*s.ctx.vcf", (int)(ol - 4), out_name);
+    else
+        snprintf(ctx_name, sizeof(ctx_name), "%s.ctx", out_name);
+
+    /* one serial pass over the records, split per chromosome (stream.h) */
+    if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) return 1;
+    grom_planner pl;
+    grom_planner_init(&pl, order, n_plan);
+    grom_batch batch;
+    int cur = 0;
+    if (n_plan > 0) grom_batch_init(&batch, order[0], P.read_name_len);
+    bam_rec rec;
+    memset(&rec, 0, sizeof(rec));
+    int status = 0;
+    while (cur < n_plan && bam_read_rec(&br, &rec) > 0) {
+        int k = grom_planner_feed(&pl, rec.tid);
+        while (cur < n_plan && pl.k > cur) {
+            /* chromosome `cur` is complete */
+            plan[cur].ref = malloc(plan[cur].len + 1);
+            grom_fasta_load(&fa, plan[cur].fasta_idx, plan[cur].ref, plan[cur].len);
+            if (scan_batch(device, &plan[cur], &batch, &P, vcf, verbose) != GROM_OK) status = 1;
+            free(plan[cur].ref);
+            grom_batch_free(&batch);
+            cur++;
+            if (cur < n_plan) grom_batch_init(&batch, order[cur], P.read_name_len);
+        }
+        if (k >= 0 && k == cur) grom_batch_add(&batch, &rec, s0);
+    }
+    /* end of file: the chromosome being read and every later one */
+    while (cur < n_plan) {
+        plan[cur].ref = malloc(plan[cur].len + 1);
+        grom_fasta_load(&fa, plan[cur].fasta_idx, plan[cur].ref, plan[cur].len);
+        if (scan_batch(device, &plan[cur], &batch, &P, vcf, verbose) != GROM_OK) status = 1;
+        free(plan[cur].ref);
+        grom_batch_free(&batch);
+        cur++;
+        if (cur < n_plan) grom_batch_init(&batch, order[cur], P.read_name_len);
+    }
+    bam_free_rec(&rec);
+    bgzf_close_read(&br);
+    fclose(vcf);
+    /* CTX post-pass (GROM.c:22400-22770): with no translocation rows the
+     * rewritten file is the header alone */
+    FILE *ctx = fopen(ctx_name, "w");
+    if (ctx) {
+        if (P.vcf == 1) header(ctx, fasta_name, 1);
+        fclose(ctx);
+    }
+    grom_dev_fini(device);
+    grom_fasta_close(&fa);
+    bam_free_header(&hdr);
+    free(plan);
+    free(order);
+    free(hez);
+    free(mq);
+    return status;
+}

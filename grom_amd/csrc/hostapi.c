@@ -1,0 +1,135 @@
+/*
+ * hostapi.c -- host conveniences for tests and benchmarks: a synthetic
+ * chromosome turned straight into the read batch its scan ingests, without a
+ * BAM round trip (the SoA the BAM decoder would have produced).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/grom_amd.h"
+#include "stream.h"
+#include "synth.h"
+
+struct grom_batch_handle {
+    grom_batch b;
+    char *ref;
+    int64_t len;
+    char name[48];
+    /* insert statistics sample (find_insert_mean's rule) */
+    int *ins, *lq;
+    int64_t n_ins, cap_ins;
+};
+
+static void on_record(void *ctx, const bam_rec *r) {
+    struct grom_batch_handle *h = (struct grom_batch_handle *)ctx;
+    if (!(r->flag & GF_UNMAP) && !(r->flag & GF_DUP) && h->n_ins < 10000000) {
+        int take = 0, v = 0;
+        if (!(r->flag & GF_PAIRED)) { take = 1; v = r->l_qseq; }
+        else if (!(r->flag & GF_MUNMAP) && r->tid == r->mtid && r->pos < r->mpos && (r->flag & GF_PROPER) && r->isize > 0) {
+            take = 1;
+            v = r->isize;
+        }
+        if (take) {
+            if (h->n_ins == h->cap_ins) {
+                h->cap_ins = h->cap_ins ? 2 * h->cap_ins : 1 << 16;
+                h->ins = realloc(h->ins, sizeof(int) * h->cap_ins);
+                h->lq = realloc(h->lq, sizeof(int) * h->cap_ins);
+            }
+            h->ins[h->n_ins] = v;
+            h->lq[h->n_ins++] = r->l_qseq;
+        }
+    }
+    grom_batch_add(&h->b, r, 0); /* the skip prefix is trimmed once index_start is known */
+}
+
+static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
+
+/* drop the leading records with pos < s0 (the walk's skip branch) */
+static void trim_prefix(grom_batch *b, int32_t s0, int64_t *n_dropped_mapped) {
+    int64_t k = 0;
+    while (k < b->n && b->pos[k] < s0) k++;
+    *n_dropped_mapped = k;
+    if (k == 0) return;
+    int64_t n = b->n - k;
+    int64_t c0 = b->cigar_off[k], bo0 = b->base_off[k];
+    memmove(b->pos, b->pos + k, sizeof(int32_t) * n);
+    memmove(b->flag, b->flag + k, sizeof(uint16_t) * n);
+    memmove(b->mapq, b->mapq + k, n);
+    memmove(b->mtid, b->mtid + k, sizeof(int32_t) * n);
+    memmove(b->mpos, b->mpos + k, sizeof(int32_t) * n);
+    memmove(b->isize, b->isize + k, sizeof(int32_t) * n);
+    memmove(b->l_qseq, b->l_qseq + k, sizeof(int32_t) * n);
+    memmove(b->name_id, b->name_id + k, sizeof(uint32_t) * n);
+    for (int64_t i = 0; i <= n; i++) b->cigar_off[i] = b->cigar_off[i + k] - (uint32_t)c0;
+    memmove(b->cigar, b->cigar + c0, sizeof(uint32_t) * (b->n_cig - c0));
+    b->n_cig -= c0;
+    for (int64_t i = 0; i < n; i++) b->base_off[i] = b->base_off[i + k] - bo0;
+    memmove(b->qual, b->qual + bo0, b->n_bases - bo0);
+    memmove(b->seq, b->seq + bo0 / 2, (b->n_bases - bo0) / 2);
+    b->n_bases -= bo0;
+    b->n = n;
+}
+
+grom_batch_handle *grom_synth_batch(int64_t chr_len, double coverage, int32_t read_len, double insert_mean,
+                                    double insert_sd, uint64_t seed, grom_params *P) {
+    synth_cfg c;
+    synth_default_cfg(&c);
+    c.n_chr = 1;
+    c.chr_len[0] = chr_len;
+    snprintf(c.chr_name[0], sizeof(c.chr_name[0]), "chr1");
+    c.coverage = coverage;
+    c.read_len = read_len;
+    c.insert_mean = insert_mean;
+    c.insert_sd = insert_sd;
+    c.seed = seed;
+    c.munmap_frac = 0.0; /* every ingested record is a placed, mapped read */
+    struct grom_batch_handle *h = calloc(1, sizeof(*h));
+    h->len = chr_len;
+    snprintf(h->name, sizeof(h->name), "chr1");
+    h->ref = synth_reference(&c, 0);
+    grom_batch_init(&h->b, 0, P->read_name_len);
+    synth_reads(&c, 0, h->ref, on_record, h);
+    if (h->n_ins == 0) { grom_batch_release(h); return NULL; }
+    /* find_insert_mean, GROM.c:1276-1310 */
+    qsort(h->ins, h->n_ins, sizeof(int), icmp);
+    int64_t n = h->n_ins;
+    int mean = h->ins[n / 2], lim = mean * 5;
+    int64_t end = 0;
+    for (int64_t a = n - 1; a >= 0; a--)
+        if (h->ins[a] <= lim) { end = a; break; }
+    end += 1;
+    mean = h->ins[end / 2];
+    int lo = (int)(grom_prob2(3.0) * end / 2);
+    int imin = h->ins[lo], imax = h->ins[end - lo < n ? end - lo : n - 1];
+    qsort(h->lq, n, sizeof(int), icmp);
+    grom_params_set_insert(P, mean, imin, imax, h->lq[n / 2]);
+    int32_t s0 = P->one_base_rd_len / 4 + 1;
+    int64_t dropped = 0;
+    trim_prefix(&h->b, s0, &dropped);
+    h->b.n_skip = (int32_t)dropped;
+    h->b.any_ingested = h->b.n > 0;
+    if (h->b.n > 0) h->b.last_pos = h->b.pos[h->b.n - 1];
+    grom_batch_finish(&h->b, s0, P->overlap_mult, P->insert_max_size);
+    return h;
+}
+
+int grom_batch_get(grom_batch_handle *h, grom_chrom *ch, grom_reads *rd) {
+    if (!h) return GROM_E_ARG;
+    ch->ref = h->ref;
+    ch->len = h->len;
+    ch->name = h->name;
+    ch->tid = 0;
+    ch->n_skip = h->b.n_skip;
+    ch->p_last = h->b.p_last;
+    grom_batch_view(&h->b, rd);
+    return GROM_OK;
+}
+
+void grom_batch_release(grom_batch_handle *h) {
+    if (!h) return;
+    grom_batch_free(&h->b);
+    free(h->ref);
+    free(h->ins);
+    free(h->lq);
+    free(h);
+}

@@ -1,0 +1,342 @@
+/*
+ * stream.c -- host front end (see stream.h).
+ */
+#include "stream.h"
+
+#include <ctype.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------- FASTA ---------------- */
+
+int grom_fasta_open(grom_fasta *f, const char *path) {
+    memset(f, 0, sizeof(*f));
+    f->fh = fopen(path, "r");
+    if (!f->fh) return -1;
+    int cap = 64;
+    f->names = malloc(sizeof(*f->names) * cap);
+    f->name_len = malloc(sizeof(int) * cap);
+    f->file_pos = malloc(sizeof(long) * cap);
+    f->len = malloc(sizeof(long) * cap);
+    /* find_genome_length, GROM.c:1321-1428: lines read with fgets(1000);
+     * a header's name runs to its first non-graph character. */
+    char line[1000];
+    long cur_len = 0;
+    while (fgets(line, sizeof(line), f->fh)) {
+        if (line[0] != '>') {
+            for (const char *c = line; *c; c++)
+                if (isalpha((unsigned char)*c)) {
+                    if (*c != 'N' && *c != 'n') f->mappable++;
+                    cur_len++;
+                }
+            continue;
+        }
+        long here = ftell(f->fh);
+        int L = (int)strlen(line), name_end = L;
+        for (int w = L - 1; w > 0; w--)
+            if (!isgraph((unsigned char)line[w])) name_end = w;
+        if (f->n > 0) f->len[f->n - 1] = cur_len;
+        cur_len = 0;
+        if (f->n >= GROM_MAX_CHR_NAMES) { f->n++; continue; }
+        if (f->n == cap) {
+            cap *= 2;
+            f->names = realloc(f->names, sizeof(*f->names) * cap);
+            f->name_len = realloc(f->name_len, sizeof(int) * cap);
+            f->file_pos = realloc(f->file_pos, sizeof(long) * cap);
+            f->len = realloc(f->len, sizeof(long) * cap);
+        }
+        if (name_end >= GROM_MAX_CHR_NAME_LEN) name_end = GROM_MAX_CHR_NAME_LEN;
+        memset(f->names[f->n], 0, GROM_MAX_CHR_NAME_LEN);
+        for (int a = 1; a < name_end; a++) f->names[f->n][a - 1] = (char)tolower((unsigned char)line[a]);
+        f->name_len[f->n] = name_end - 1;
+        f->file_pos[f->n] = here;
+        f->len[f->n] = 0;
+        f->n++;
+    }
+    if (f->n > 0 && f->n <= GROM_MAX_CHR_NAMES) f->len[f->n - 1] = cur_len;
+    if (f->n > GROM_MAX_CHR_NAMES) f->n = GROM_MAX_CHR_NAMES;
+    return 0;
+}
+
+void grom_fasta_close(grom_fasta *f) {
+    if (f->fh) fclose(f->fh);
+    free(f->names);
+    free(f->name_len);
+    free(f->file_pos);
+    free(f->len);
+    memset(f, 0, sizeof(*f));
+}
+
+long grom_fasta_load(grom_fasta *f, int i, char *buf, long cap) {
+    /* find_disc_svs' loader, GROM.c:21009-21045: per line keep everything up
+     * to the last letter; that cut is only re-measured when the line length
+     * changes. */
+    char line[1000];
+    long len = 0;
+    fseek(f->fh, f->file_pos[i], SEEK_SET);
+    while (fgets(line, sizeof(line), f->fh) && line[0] != '>') {
+        int L = (int)strlen(line);
+        if (len == 0 || L != f->loader_line_len) {
+            f->loader_line_len = L;
+            int w = L - 1;
+            while (!isalpha((unsigned char)line[w]) && w > 0) w--;
+            f->loader_alpha_len = w + 1;
+        }
+        if (buf && len + f->loader_alpha_len <= cap) memcpy(buf + len, line, f->loader_alpha_len);
+        len += f->loader_alpha_len;
+    }
+    return len;
+}
+
+int grom_target_name_lc(const char *target, char *out, int cap) {
+    int L = (int)strlen(target);
+    if (L > cap - 1) L = cap - 1;
+    for (int i = 0; i < L; i++) out[i] = (char)tolower((unsigned char)target[i]);
+    out[L] = 0;
+    for (int i = L - 1; i > 0; i--)
+        if (!isgraph((unsigned char)out[i])) L = i;
+    return L;
+}
+
+static int name_rule(const char *bam, int bl, const char *fa, int fl) {
+    char t[GROM_MAX_CHR_NAME_LEN + 8];
+    if (bl == fl && strncmp(bam, fa, fl) == 0) return 1;
+    if (bl - 3 == fl && strncmp(bam, "chr", 3) == 0) {
+        snprintf(t, sizeof(t), "chr%.*s", fl, fa);
+        return strncmp(bam, t, bl) == 0;
+    }
+    if (bl + 3 == fl && strncmp(fa, "chr", 3) == 0) {
+        snprintf(t, sizeof(t), "chr%.*s", bl, bam);
+        return strncmp(fa, t, fl) == 0;
+    }
+    return 0;
+}
+
+int grom_match_target(const grom_fasta *f, const char *target) {
+    char lc[GROM_MAX_CHR_NAMES];
+    int bl = grom_target_name_lc(target, lc, (int)sizeof(lc));
+    for (int i = 0; i < f->n; i++)
+        if (name_rule(lc, bl, f->names[i], f->name_len[i])) return i;
+    return -1;
+}
+
+/* ---------------- insert-size pre-pass ---------------- */
+
+double grom_prob2(double num_sd) {
+    double x = num_sd / sqrt(2), t = 1.0 / (1.0 + 0.3275911 * x);
+    double e = 1.0 - (0.254829592 * t + -0.284496736 * pow(t, 2) + 1.421413741 * pow(t, 3) +
+                      -1.453152027 * pow(t, 4) + 1.061405429 * pow(t, 5)) *
+                         exp(-pow(x, 2));
+    return (1.0 - e) / 2.0;
+}
+
+static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
+
+int grom_insert_stats(bgzf_reader *r, double prob2, int *lseq, int *imin, int *imax, long *mapped, int min_mapq) {
+    const int cap = 10000000; /* insert_sample_size, GROM.c:913 */
+    int *ins = malloc(sizeof(int) * cap), *lq = malloc(sizeof(int) * cap);
+    int n = 0;
+    long m = 0;
+    bam_rec b;
+    memset(&b, 0, sizeof(b));
+    while (n < cap && bam_read_rec(r, &b) > 0) {
+        if ((b.flag & GF_UNMAP) || (b.flag & GF_DUP)) continue;
+        if (!(b.flag & GF_PAIRED)) {
+            ins[n] = b.l_qseq;
+            lq[n++] = b.l_qseq;
+        } else if (!(b.flag & GF_MUNMAP) && b.tid == b.mtid && b.pos < b.mpos && (b.flag & GF_PROPER) && b.isize > 0) {
+            ins[n] = b.isize;
+            lq[n++] = b.l_qseq;
+        }
+        if (b.mapq >= min_mapq) m += b.l_qseq;
+    }
+    bam_free_rec(&b);
+    if (n == 0) { free(ins); free(lq); return -1; }
+    qsort(ins, n, sizeof(int), icmp);
+    int mean = ins[n / 2], lim = mean * 5, end = 0; /* g_insert_max_mult = 5 */
+    for (int a = n - 1; a >= 0; a--)
+        if (ins[a] <= lim) { end = a; break; }
+    end += 1;
+    mean = ins[end / 2];
+    int lo = (int)(prob2 * end / 2);
+    *imin = ins[lo];
+    *imax = ins[end - lo < n ? end - lo : n - 1];
+    qsort(lq, n, sizeof(int), icmp);
+    *lseq = lq[n / 2];
+    if (mapped) *mapped = m;
+    free(ins);
+    free(lq);
+    return mean;
+}
+
+/* ---------------- batches ---------------- */
+
+
+void grom_batch_init(grom_batch *b, int32_t tid, int read_name_len) {
+    memset(b, 0, sizeof(*b));
+    b->tid = tid;
+    b->p_last = -1;
+    b->read_name_len = read_name_len;
+}
+
+void grom_batch_free(grom_batch *b) {
+    free(b->pos); free(b->flag); free(b->mapq); free(b->mtid); free(b->mpos); free(b->isize); free(b->l_qseq);
+    free(b->cigar_off); free(b->cigar); free(b->base_off); free(b->seq); free(b->qual); free(b->name_id);
+    for (int64_t i = 0; i < b->ncap; i++) free(b->nkeys[i]);
+    free(b->nkeys);
+    free(b->nids);
+    memset(b, 0, sizeof(*b));
+}
+
+static uint64_t hash_name(const char *s) {
+    uint64_t h = 0xcbf29ce484222325ULL;
+    for (; *s; s++) h = (h ^ (unsigned char)*s) * 0x100000001b3ULL;
+    return h;
+}
+
+static uint32_t intern(grom_batch *b, const char *s) {
+    size_t L = strlen(s);
+    if (L == 0 || L >= (size_t)b->read_name_len) return 0; /* never stored, GROM.c:6813 */
+    if (2 * (b->nn + 1) > b->ncap) {
+        int64_t nc = b->ncap ? 2 * b->ncap : 65536;
+        char **nk = calloc(nc, sizeof(char *));
+        uint32_t *ni = calloc(nc, sizeof(uint32_t));
+        for (int64_t i = 0; i < b->ncap; i++)
+            if (b->nkeys[i]) {
+                int64_t j = (int64_t)(hash_name(b->nkeys[i]) & (uint64_t)(nc - 1));
+                while (nk[j]) j = (j + 1) & (nc - 1);
+                nk[j] = b->nkeys[i];
+                ni[j] = b->nids[i];
+            }
+        free(b->nkeys);
+        free(b->nids);
+        b->nkeys = nk;
+        b->nids = ni;
+        b->ncap = nc;
+    }
+    int64_t j = (int64_t)(hash_name(s) & (uint64_t)(b->ncap - 1));
+    while (b->nkeys[j]) {
+        if (strcmp(b->nkeys[j], s) == 0) return b->nids[j];
+        j = (j + 1) & (b->ncap - 1);
+    }
+    b->nkeys[j] = strdup(s);
+    b->nids[j] = (uint32_t)(++b->nn);
+    return b->nids[j];
+}
+
+void grom_batch_add(grom_batch *b, const bam_rec *r, int32_t index_start) {
+    if (r->pos < index_start && !b->any_ingested) { /* skip branch, GROM.c:14859-14969 */
+        b->n_skip++;
+        return;
+    }
+    b->any_ingested = 1;
+    b->last_pos = r->pos;
+    if ((r->flag & GF_UNMAP) || (r->flag & GF_DUP)) return; /* GROM.c:6418 */
+    int64_t i = b->n;
+    if (i + 1 > b->cap) {
+        int64_t nc = b->cap ? b->cap * 2 : 1024;
+        b->pos = realloc(b->pos, sizeof(int32_t) * nc);
+        b->flag = realloc(b->flag, sizeof(uint16_t) * nc);
+        b->mapq = realloc(b->mapq, nc);
+        b->mtid = realloc(b->mtid, sizeof(int32_t) * nc);
+        b->mpos = realloc(b->mpos, sizeof(int32_t) * nc);
+        b->isize = realloc(b->isize, sizeof(int32_t) * nc);
+        b->l_qseq = realloc(b->l_qseq, sizeof(int32_t) * nc);
+        b->cigar_off = realloc(b->cigar_off, sizeof(uint32_t) * (nc + 1));
+        b->base_off = realloc(b->base_off, sizeof(int64_t) * nc);
+        b->name_id = realloc(b->name_id, sizeof(uint32_t) * nc);
+        b->cap = nc;
+    }
+    b->pos[i] = r->pos;
+    b->flag[i] = r->flag;
+    b->mapq[i] = r->mapq;
+    b->mtid[i] = r->mtid;
+    b->mpos[i] = r->mpos;
+    b->isize[i] = r->isize;
+    b->l_qseq[i] = r->l_qseq;
+    if (i == 0) b->cigar_off[0] = 0;
+    const uint32_t *cg = bam_cigar(r);
+    if (b->n_cig + r->n_cigar > b->cap_cig) {
+        int64_t nc = b->cap_cig ? b->cap_cig : 4096;
+        while (nc < b->n_cig + r->n_cigar) nc *= 2;
+        b->cigar = realloc(b->cigar, sizeof(uint32_t) * nc);
+        b->cap_cig = nc;
+    }
+    memcpy(b->cigar + b->n_cig, cg, sizeof(uint32_t) * r->n_cigar);
+    int32_t span = 0;
+    for (int k = 0; k < r->n_cigar; k++) {
+        int op = cg[k] & 0xf;
+        if (op == GC_MATCH || op == GC_DEL || op == GC_REF_SKIP || op == GC_EQUAL || op == GC_DIFF) span += (int32_t)(cg[k] >> 4);
+    }
+    if (span > b->max_ref_span) b->max_ref_span = span;
+    b->n_cig += r->n_cigar;
+    b->cigar_off[i + 1] = (uint32_t)b->n_cig;
+    int64_t L = r->l_qseq, Lp = (L + 1) & ~1LL; /* keep every read's first base on a byte */
+    int64_t need = b->n_bases + Lp;
+    if (need > b->cap_bases) {
+        int64_t nc = b->cap_bases ? b->cap_bases : 1 << 20;
+        while (nc < need) nc *= 2;
+        b->qual = realloc(b->qual, nc);
+        b->seq = realloc(b->seq, nc / 2);
+        b->cap_bases = nc;
+    }
+    b->base_off[i] = b->n_bases;
+    memcpy(b->seq + b->n_bases / 2, bam_seq(r), (size_t)((L + 1) / 2));
+    memcpy(b->qual + b->n_bases, bam_qual(r), (size_t)L);
+    if (Lp > L) b->qual[b->n_bases + L] = 0;
+    b->n_bases = need;
+    b->name_id[i] = intern(b, bam_qname(r));
+    b->n = i + 1;
+}
+
+void grom_batch_finish(grom_batch *b, int32_t index_start, int32_t overlap_mult, int32_t insert_max) {
+    if (!b->any_ingested) { b->p_last = -1; return; }
+    int32_t p = b->last_pos - overlap_mult * insert_max;
+    b->p_last = p > index_start ? p : index_start;
+}
+
+void grom_batch_view(const grom_batch *b, grom_reads *o) {
+    memset(o, 0, sizeof(*o));
+    o->n = b->n;
+    o->n_cigar_ops = b->n_cig;
+    o->n_bases = b->n_bases;
+    o->pos = b->pos;
+    o->flag = b->flag;
+    o->mapq = b->mapq;
+    o->mtid = b->mtid;
+    o->mpos = b->mpos;
+    o->isize = b->isize;
+    o->l_qseq = b->l_qseq;
+    o->cigar_off = b->cigar_off;
+    o->cigar = b->cigar;
+    o->base_off = b->base_off;
+    o->seq = b->seq;
+    o->qual = b->qual;
+    o->name_id = b->name_id;
+}
+
+/* ---------------- serial stream planner ---------------- */
+
+void grom_planner_init(grom_planner *p, const int32_t *order, int n_order) {
+    memset(p, 0, sizeof(*p));
+    p->order = order;
+    p->n_order = n_order;
+}
+
+int grom_planner_feed(grom_planner *p, int32_t tid) {
+    if (p->k >= p->n_order) return -1;
+    switch (p->state) {
+    case 0: /* outer loop of count_discordant_pairs, GROM.c:5740 / 17549 */
+        if (tid == p->order[p->k]) { p->state = 1; return p->k; }
+        return -1;
+    case 1: /* inner walk: a foreign record ends the chromosome (begin=2) ... */
+        if (tid == p->order[p->k]) return p->k;
+        p->state = 2;
+        return -1;
+    default: /* ... and the outer `while` condition reads one more (Q1) */
+        p->state = 0;
+        p->k++;
+        return -1;
+    }
+}

@@ -1,0 +1,486 @@
+/*
+ * synth.c -- deterministic synthetic genome + paired-end read generator.
+ * See synth.h for the model.  Everything is driven by xoshiro256** streams
+ * seeded from (cfg->seed, chromosome index, purpose), so a given config
+ * always yields byte-identical FASTA/BAM files.
+ */
+#include "synth.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------- RNG ---------------- */
+typedef struct { uint64_t s[4]; } xrng;
+
+static uint64_t splitmix(uint64_t *x) {
+    uint64_t z = (*x += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+static void xseed(xrng *r, uint64_t seed, uint64_t a, uint64_t b) {
+    uint64_t x = seed ^ (a * 0x9E3779B97F4A7C15ULL) ^ (b * 0xD1B54A32D192ED03ULL);
+    for (int i = 0; i < 4; i++) r->s[i] = splitmix(&x);
+}
+static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+static inline uint64_t xnext(xrng *r) {
+    uint64_t *s = r->s;
+    uint64_t res = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+    s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3]; s[2] ^= t; s[3] = rotl(s[3], 45);
+    return res;
+}
+static inline double xunif(xrng *r) { return (xnext(r) >> 11) * (1.0 / 9007199254740992.0); }
+static inline long xint(xrng *r, long n) { return (long)(xunif(r) * (double)n); }
+static double xnorm(xrng *r) {
+    double u1 = xunif(r), u2 = xunif(r);
+    if (u1 < 1e-300) u1 = 1e-300;
+    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+static double xexp(xrng *r, double mean) {
+    double u = xunif(r);
+    if (u < 1e-300) u = 1e-300;
+    return -log(u) * mean;
+}
+
+static const char ACGT[4] = {'A', 'C', 'G', 'T'};
+
+void synth_default_cfg(synth_cfg *c) {
+    memset(c, 0, sizeof(*c));
+    c->n_chr = 1;
+    c->chr_len[0] = 1000000;
+    strcpy(c->chr_name[0], "chr1");
+    c->coverage = 30.0;
+    for (int i = 0; i < SYNTH_MAX_CHR; i++) c->chr_cov[i] = -1.0;
+    c->read_len = 150;
+    c->insert_mean = 500.0;
+    c->insert_sd = 50.0;
+    c->snv_rate = 1e-3;
+    c->indel_rate = 1e-4;
+    c->max_indel = 20;
+    c->err_rate = 0.002;
+    c->lowq_frac = 0.02;
+    c->hi_q = 30;
+    c->lo_q = 10;
+    c->lowmapq_frac = 0.03;
+    c->softclip_frac = 0.01;
+    c->munmap_frac = 0.002;
+    c->dup_frac = 0.0;
+    c->telomere_n = 10000;
+    c->lower_frac = 0.1;
+    c->gc_lo = 0.35;
+    c->gc_hi = 0.55;
+    c->repeat_rate = 2e-5;
+    c->fasta_line = 60;
+    c->seed = 2;
+}
+
+char *synth_reference(const synth_cfg *c, int ci) {
+    long n = c->chr_len[ci];
+    char *s = (char *)malloc((size_t)n + 1);
+    xrng r;
+    xseed(&r, c->seed, (uint64_t)ci + 1, 1);
+    double gc = 0.41;
+    for (long i = 0; i < n; i++) {
+        if (i % 100000 == 0) gc = c->gc_lo + (c->gc_hi - c->gc_lo) * xunif(&r);
+        double u = xunif(&r);
+        if (u < gc) s[i] = (u < gc * 0.5) ? 'G' : 'C';
+        else s[i] = (u < gc + (1.0 - gc) * 0.5) ? 'A' : 'T';
+    }
+    /* dinucleotide repeat runs */
+    if (c->repeat_rate > 0) {
+        long i = (long)xexp(&r, 1.0 / c->repeat_rate);
+        while (i < n) {
+            int len = 20 + (int)xint(&r, 60);
+            char a = ACGT[xint(&r, 4)], b = ACGT[xint(&r, 4)];
+            for (int k = 0; k < len && i + k < n; k++) s[i + k] = (k & 1) ? b : a;
+            i += len + (long)xexp(&r, 1.0 / c->repeat_rate);
+        }
+    }
+    /* soft-masked blocks */
+    if (c->lower_frac > 0) {
+        long i = (long)xexp(&r, 5000.0 / c->lower_frac);
+        while (i < n) {
+            long len = 200 + xint(&r, 4800);
+            for (long k = 0; k < len && i + k < n; k++) s[i + k] = (char)(s[i + k] + 32);
+            i += len + (long)xexp(&r, 5000.0 / c->lower_frac);
+        }
+    }
+    long tn = c->telomere_n;
+    if (tn * 3 > n) tn = n / 3;
+    for (long i = 0; i < tn; i++) { s[i] = 'N'; s[n - 1 - i] = 'N'; }
+    s[n] = 0;
+    return s;
+}
+
+/* ---------------- donor haplotypes ---------------- */
+typedef struct {
+    char *seq;     /* donor bases (upper case) */
+    int32_t *map;  /* donor index -> reference index, -1 for inserted base */
+    int32_t *inv;  /* reference index -> first donor index with map >= it */
+    long len;
+} haplo;
+
+static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo h[2]) {
+    long n = c->chr_len[ci];
+    xrng r;
+    xseed(&r, c->seed, (uint64_t)ci + 1, 2);
+    for (int k = 0; k < 2; k++) {
+        long cap = n + n / 50 + 1024;
+        h[k].seq = (char *)malloc(cap);
+        h[k].map = (int32_t *)malloc(cap * sizeof(int32_t));
+        h[k].len = 0;
+    }
+    double vrate = c->snv_rate + c->indel_rate;
+    long next_var = vrate > 0 ? (long)xexp(&r, 1.0 / vrate) : n + 1;
+    long i = 0;
+    while (i < n) {
+        char rb = ref[i];
+        char ub = (rb >= 'a' && rb <= 'z') ? (char)(rb - 32) : rb;
+        if (i == next_var && ub != 'N' && i > 0 && i + c->max_indel + 2 < n) {
+            int gt = (int)xint(&r, 3); /* 0: hap0 only, 1: hap1 only, 2: both */
+            double u = xunif(&r) * vrate;
+            int consumed = 1;
+            if (u < c->snv_rate) {
+                char alt;
+                do { alt = ACGT[xint(&r, 4)]; } while (alt == ub);
+                for (int k = 0; k < 2; k++) {
+                    int has = (gt == 2) || (gt == k);
+                    h[k].seq[h[k].len] = has ? alt : ub;
+                    h[k].map[h[k].len++] = (int32_t)i;
+                }
+            } else {
+                int len = 1 + (int)xint(&r, c->max_indel);
+                int ins = xunif(&r) < 0.5;
+                if (ins) {
+                    for (int k = 0; k < 2; k++) {
+                        int has = (gt == 2) || (gt == k);
+                        h[k].seq[h[k].len] = ub;
+                        h[k].map[h[k].len++] = (int32_t)i;
+                        if (has)
+                            for (int q = 0; q < len; q++) {
+                                h[k].seq[h[k].len] = ACGT[xint(&r, 4)];
+                                h[k].map[h[k].len++] = -1;
+                            }
+                    }
+                } else {
+                    /* deletion of ref[i+1 .. i+len] */
+                    for (int k = 0; k < 2; k++) {
+                        int has = (gt == 2) || (gt == k);
+                        h[k].seq[h[k].len] = ub;
+                        h[k].map[h[k].len++] = (int32_t)i;
+                        if (!has)
+                            for (int q = 1; q <= len; q++) {
+                                char b = ref[i + q];
+                                h[k].seq[h[k].len] = (b >= 'a' && b <= 'z') ? (char)(b - 32) : b;
+                                h[k].map[h[k].len++] = (int32_t)(i + q);
+                            }
+                    }
+                    consumed = 1 + len;
+                }
+            }
+            i += consumed;
+            next_var = i + 2 * c->max_indel + (long)xexp(&r, 1.0 / vrate);
+            continue;
+        }
+        if (i == next_var) next_var++;
+        for (int k = 0; k < 2; k++) {
+            h[k].seq[h[k].len] = ub;
+            h[k].map[h[k].len++] = (int32_t)i;
+        }
+        i++;
+    }
+    for (int k = 0; k < 2; k++) {
+        h[k].inv = (int32_t *)malloc((size_t)(n + 1) * sizeof(int32_t));
+        long ri = 0;
+        for (long d = 0; d < h[k].len; d++) {
+            int32_t m = h[k].map[d];
+            if (m < 0) continue;
+            while (ri <= m) h[k].inv[ri++] = (int32_t)d;
+        }
+        while (ri <= n) h[k].inv[ri++] = (int32_t)h[k].len;
+    }
+}
+
+static void free_haplos(haplo h[2]) {
+    for (int k = 0; k < 2; k++) { free(h[k].seq); free(h[k].map); free(h[k].inv); }
+}
+
+/* ---------------- record heap (sorted emission) ---------------- */
+typedef struct { int32_t pos; uint64_t order; bam_rec rec; } hent;
+typedef struct { hent *a; long n, cap; } rheap;
+
+static int hless(const hent *x, const hent *y) {
+    return x->pos < y->pos || (x->pos == y->pos && x->order < y->order);
+}
+static void hpush(rheap *h, hent e) {
+    if (h->n == h->cap) {
+        h->cap = h->cap ? h->cap * 2 : 4096;
+        h->a = (hent *)realloc(h->a, h->cap * sizeof(hent));
+    }
+    long i = h->n++;
+    h->a[i] = e;
+    while (i > 0) {
+        long p = (i - 1) / 2;
+        if (!hless(&h->a[i], &h->a[p])) break;
+        hent t = h->a[i]; h->a[i] = h->a[p]; h->a[p] = t;
+        i = p;
+    }
+}
+static hent hpop(rheap *h) {
+    hent top = h->a[0];
+    h->a[0] = h->a[--h->n];
+    long i = 0;
+    for (;;) {
+        long l = 2 * i + 1, r = l + 1, m = i;
+        if (l < h->n && hless(&h->a[l], &h->a[m])) m = l;
+        if (r < h->n && hless(&h->a[r], &h->a[m])) m = r;
+        if (m == i) break;
+        hent t = h->a[i]; h->a[i] = h->a[m]; h->a[m] = t;
+        i = m;
+    }
+    return top;
+}
+
+/* ---------------- read construction ---------------- */
+typedef struct {
+    int32_t pos;        /* leftmost mapped reference base */
+    int32_t ref_end;    /* one past last mapped reference base */
+    int n_cigar;
+    uint32_t cigar[512];
+    char seq[1024];
+    uint8_t qual[1024];
+    int len;
+} aln;
+
+static void push_op(aln *a, int op, int len) {
+    if (len <= 0) return;
+    if (a->n_cigar > 0 && (int)(a->cigar[a->n_cigar - 1] & 0xf) == op) {
+        a->cigar[a->n_cigar - 1] += (uint32_t)len << 4;
+        return;
+    }
+    a->cigar[a->n_cigar++] = ((uint32_t)len << 4) | (uint32_t)op;
+}
+
+/* align donor[d0, d0+L) of haplotype h; clip_left/right bases become random
+ * soft-clipped sequence.  Returns 0 if no base maps. */
+static int make_aln(const haplo *h, long d0, int L, int clip_left, int clip_right, xrng *r, aln *a) {
+    a->n_cigar = 0;
+    a->len = L;
+    int first = -1, last = -1;
+    for (int k = 0; k < L; k++) {
+        int32_t m = (k < clip_left || k >= L - clip_right) ? -1 : h->map[d0 + k];
+        a->seq[k] = (k < clip_left || k >= L - clip_right) ? ACGT[xint(r, 4)] : h->seq[d0 + k];
+        if (m >= 0) { if (first < 0) first = k; last = k; }
+    }
+    if (first < 0) return 0;
+    push_op(a, GC_SOFT_CLIP, first);
+    int32_t prev = -1;
+    for (int k = first; k <= last; k++) {
+        int32_t m = (k < clip_left || k >= L - clip_right) ? -1 : h->map[d0 + k];
+        if (m < 0) { push_op(a, GC_INS, 1); continue; }
+        if (prev >= 0 && m > prev + 1) push_op(a, GC_DEL, m - prev - 1);
+        push_op(a, GC_MATCH, 1);
+        prev = m;
+    }
+    push_op(a, GC_SOFT_CLIP, L - 1 - last);
+    a->pos = h->map[d0 + first];
+    a->ref_end = prev + 1;
+    return 1;
+}
+
+static void fill_rec(bam_rec *b, const char *name, int tid, const aln *a, int with_cigar, int flag,
+                     int mapq, int mtid, int mpos, int isize, int pos_override) {
+    int lq = (int)strlen(name) + 1;
+    int nc = with_cigar ? a->n_cigar : 0;
+    int L = a->len;
+    b->data_len = lq + 4 * nc + (L + 1) / 2 + L;
+    b->m_data = b->data_len;
+    b->data = (uint8_t *)malloc(b->data_len);
+    memcpy(b->data, name, lq);
+    if (nc) memcpy(b->data + lq, a->cigar, 4 * nc);
+    uint8_t *s = b->data + lq + 4 * nc;
+    memset(s, 0, (L + 1) / 2);
+    for (int k = 0; k < L; k++) {
+        int code;
+        switch (a->seq[k]) {
+        case 'A': code = 1; break;
+        case 'C': code = 2; break;
+        case 'G': code = 4; break;
+        case 'T': code = 8; break;
+        default: code = 15;
+        }
+        s[k >> 1] |= (uint8_t)(code << ((~k & 1) << 2));
+    }
+    memcpy(s + (L + 1) / 2, a->qual, L);
+    b->tid = tid;
+    b->pos = with_cigar ? a->pos : pos_override;
+    b->l_qname = (uint8_t)lq;
+    b->mapq = (uint8_t)mapq;
+    b->n_cigar = (uint16_t)nc;
+    b->flag = (uint16_t)flag;
+    b->l_qseq = L;
+    b->mtid = mtid;
+    b->mpos = mpos;
+    b->isize = isize;
+    int end = with_cigar ? a->ref_end : pos_override + 1;
+    b->bin = (uint16_t)bam_reg2bin(b->pos, end > b->pos ? end : b->pos + 1);
+}
+
+static void add_errors(aln *a, const synth_cfg *c, xrng *r) {
+    for (int k = 0; k < a->len; k++) {
+        if (xunif(r) < c->err_rate) {
+            char o = a->seq[k], n;
+            do { n = ACGT[xint(r, 4)]; } while (n == o);
+            a->seq[k] = n;
+        }
+        a->qual[k] = (uint8_t)(xunif(r) < c->lowq_frac ? c->lo_q : c->hi_q);
+    }
+}
+
+static int draw_mapq(const synth_cfg *c, xrng *r) {
+    return xunif(r) < c->lowmapq_frac ? (int)xint(r, 20) : 60;
+}
+
+long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit, void *ctx) {
+    long n = c->chr_len[ci];
+    int L = c->read_len;
+    haplo h[2];
+    build_haplos(c, ci, ref, h);
+    /* prefix count of N bases so fragments never touch an N block */
+    int32_t *ncount = (int32_t *)malloc((size_t)(n + 1) * sizeof(int32_t));
+    ncount[0] = 0;
+    for (long i = 0; i < n; i++) ncount[i + 1] = ncount[i] + (ref[i] == 'N' || ref[i] == 'n');
+
+    xrng r;
+    xseed(&r, c->seed, (uint64_t)ci + 1, 3);
+    double cov = c->chr_cov[ci] >= 0 ? c->chr_cov[ci] : c->coverage;
+    double n_frag = cov * (double)n / (2.0 * L);
+    if (n_frag <= 0) n_frag = 0;
+    double gap = n_frag > 0 ? (double)n / n_frag : (double)n;
+    rheap heap = {0};
+    long emitted = 0;
+    uint64_t order = 0;
+    double start_f = n_frag > 0 ? xexp(&r, gap) : (double)n;
+    uint64_t frag_id = 0;
+    aln a1, a2;
+    char name[64];
+    while (start_f < (double)n) {
+        long start = (long)start_f;
+        start_f += xexp(&r, gap);
+        int hk = (int)xint(&r, 2);
+        const haplo *hp = &h[hk];
+        int ins = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+        if (ins < L) ins = L;
+        /* fragment start in reference coordinates, mapped onto the donor */
+        long d0 = hp->inv[start];
+        if (d0 + ins >= hp->len) continue;
+        int32_t rs = hp->map[d0], re = hp->map[d0 + ins - 1];
+        if (rs < 0 || re < 0 || re <= rs) continue;
+        if (ncount[re + 1] - ncount[rs] != 0) continue;
+        int ndup = (xunif(&r) < c->dup_frac) ? 2 : 1;
+        frag_id++;
+        /* flush everything that now sorts before this fragment */
+        while (heap.n > 0 && heap.a[0].pos < start) {
+            hent e = hpop(&heap);
+            emit(ctx, &e.rec);
+            free(e.rec.data);
+            emitted++;
+        }
+        for (int dup = 0; dup < ndup; dup++) {
+            int cl1 = 0, cr2 = 0;
+            if (xunif(&r) < c->softclip_frac) cl1 = 5 + (int)xint(&r, 26);
+            if (xunif(&r) < c->softclip_frac) cr2 = 5 + (int)xint(&r, 26);
+            if (!make_aln(hp, d0, L, cl1, 0, &r, &a1)) continue;
+            if (!make_aln(hp, d0 + ins - L, L, 0, cr2, &r, &a2)) continue;
+            add_errors(&a1, c, &r);
+            add_errors(&a2, c, &r);
+            int mq1 = draw_mapq(c, &r), mq2 = draw_mapq(c, &r);
+            int left_is_r1 = xunif(&r) < 0.5;
+            int munmap = xunif(&r) < c->munmap_frac;
+            if (dup == 0) snprintf(name, sizeof(name), "SYN%02d:%010llu", ci, (unsigned long long)frag_id);
+            else snprintf(name, sizeof(name), "SYN%02d:%010llu:d", ci, (unsigned long long)frag_id);
+            int tlen = a2.ref_end - a1.pos;
+            int f1 = GF_PAIRED | (left_is_r1 ? GF_READ1 : GF_READ2);
+            int f2 = GF_PAIRED | GF_REVERSE | (left_is_r1 ? GF_READ2 : GF_READ1);
+            hent e1, e2;
+            memset(&e1, 0, sizeof(e1));
+            memset(&e2, 0, sizeof(e2));
+            if (munmap) {
+                f1 |= GF_MUNMAP;
+                f2 |= GF_UNMAP;
+                f2 &= ~GF_REVERSE;
+                fill_rec(&e1.rec, name, ci, &a1, 1, f1, mq1, ci, a1.pos, 0, 0);
+                fill_rec(&e2.rec, name, ci, &a2, 0, f2, 0, ci, a1.pos, 0, a1.pos);
+            } else {
+                f1 |= GF_PROPER | GF_MREVERSE;
+                f2 |= GF_PROPER;
+                fill_rec(&e1.rec, name, ci, &a1, 1, f1, mq1, ci, a2.pos, tlen, 0);
+                fill_rec(&e2.rec, name, ci, &a2, 1, f2, mq2, ci, a1.pos, -tlen, 0);
+            }
+            e1.pos = e1.rec.pos; e1.order = order++;
+            e2.pos = e2.rec.pos; e2.order = order++;
+            hpush(&heap, e1);
+            hpush(&heap, e2);
+        }
+    }
+    while (heap.n > 0) {
+        hent e = hpop(&heap);
+        emit(ctx, &e.rec);
+        free(e.rec.data);
+        emitted++;
+    }
+    free(heap.a);
+    free(ncount);
+    free_haplos(h);
+    return emitted;
+}
+
+static void emit_to_bam(void *ctx, const bam_rec *b) { bam_write_rec((bgzf_writer *)ctx, b); }
+
+int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *bam_path) {
+    FILE *fa = fopen(fasta_path, "w");
+    if (!fa) return -1;
+    char **refs = (char **)calloc(c->n_chr, sizeof(char *));
+    for (int i = 0; i < c->n_chr; i++) {
+        refs[i] = synth_reference(c, i);
+        fprintf(fa, ">%s synthetic\n", c->chr_name[i]);
+        for (long k = 0; k < c->chr_len[i]; k += c->fasta_line) {
+            long m = c->chr_len[i] - k;
+            if (m > c->fasta_line) m = c->fasta_line;
+            fwrite(refs[i] + k, 1, m, fa);
+            fputc('\n', fa);
+        }
+    }
+    if (fclose(fa) != 0) return -1;
+
+    bam_hdr h;
+    memset(&h, 0, sizeof(h));
+    char text[64 * 96 + 64];
+    int tl = snprintf(text, sizeof(text), "@HD\tVN:1.4\tSO:coordinate\n");
+    for (int i = 0; i < c->n_chr; i++)
+        tl += snprintf(text + tl, sizeof(text) - tl, "@SQ\tSN:%s\tLN:%ld\n", c->chr_name[i], c->chr_len[i]);
+    h.text = text;
+    h.l_text = tl;
+    h.n_ref = c->n_chr;
+    h.ref_name = (char **)calloc(c->n_chr, sizeof(char *));
+    h.ref_len = (int32_t *)calloc(c->n_chr, sizeof(int32_t));
+    for (int i = 0; i < c->n_chr; i++) {
+        h.ref_name[i] = (char *)c->chr_name[i];
+        h.ref_len[i] = (int32_t)c->chr_len[i];
+    }
+    bgzf_writer w;
+    if (bgzf_open_write(&w, bam_path, 6) != 0) return -1;
+    int rc = bam_write_header(&w, &h);
+    for (int i = 0; i < c->n_chr && rc == 0; i++) {
+        synth_reads(c, i, refs[i], emit_to_bam, &w);
+        free(refs[i]);
+    }
+    if (bgzf_close_write(&w) != 0) rc = -1;
+    free(h.ref_name);
+    free(h.ref_len);
+    free(refs);
+    if (rc == 0) rc = bai_write_minimal(bam_path, c->n_chr);
+    return rc;
+}

@@ -1,0 +1,67 @@
+/*
+ * synth.h -- deterministic synthetic genome + paired-end read generator.
+ *
+ * The bundled tilapia BAM of the reference is a missing blob,
+ * so every benchmark and parity case is built from seeded synthetic data:
+ * a FASTA with isochore GC, N telomeres, soft-masked stretches and
+ * dinucleotide repeats; a diploid donor with SNVs and small indels; and
+ * coordinate-sorted 2xL paired-end reads with sequencing errors, low base
+ * qualities, low-MAPQ reads, soft clips, unmapped mates and PCR duplicates
+ * (the knobs listed in SURVEY.md §8d).
+ */
+#ifndef GROM_AMD_SYNTH_H
+#define GROM_AMD_SYNTH_H
+
+#include <stdint.h>
+#include "bamio.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SYNTH_MAX_CHR 64
+
+typedef struct synth_cfg {
+    int n_chr;
+    long chr_len[SYNTH_MAX_CHR];
+    char chr_name[SYNTH_MAX_CHR][48];
+    double coverage;      /* mean depth */
+    double chr_cov[SYNTH_MAX_CHR]; /* per-chromosome depth; < 0 means `coverage` */
+    int read_len;
+    double insert_mean, insert_sd;
+    double snv_rate, indel_rate;
+    int max_indel;
+    double err_rate;      /* per-base substitution error */
+    double lowq_frac;     /* fraction of bases at lo_q */
+    int hi_q, lo_q;
+    double lowmapq_frac;  /* fraction of reads with MAPQ 0..19 */
+    double softclip_frac; /* fraction of reads with a 5..30 bp soft clip */
+    double munmap_frac;   /* fraction of pairs whose right read is unmapped */
+    double dup_frac;      /* fraction of fragments emitted twice */
+    int telomere_n;       /* N bases at both chromosome ends */
+    double lower_frac;    /* fraction of reference in soft-masked blocks */
+    double gc_lo, gc_hi;  /* isochore GC range */
+    double repeat_rate;   /* dinucleotide repeat runs per base */
+    int fasta_line;       /* FASTA line width */
+    uint64_t seed;
+} synth_cfg;
+
+void synth_default_cfg(synth_cfg *c);
+
+/* Generate chromosome i's reference sequence (chr_len bytes, not NUL-terminated,
+ * returned buffer has one extra NUL). Deterministic in (seed, i). */
+char *synth_reference(const synth_cfg *c, int i);
+
+typedef void (*synth_emit_fn)(void *ctx, const bam_rec *b);
+
+/* Emit chromosome i's records in coordinate order (ties in generation order).
+ * `ref` is the sequence from synth_reference.  Returns number of records. */
+long synth_reads(const synth_cfg *c, int i, const char *ref, synth_emit_fn emit, void *ctx);
+
+/* Write FASTA, BAM and minimal BAI for the whole genome. 0 on success. */
+int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *bam_path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

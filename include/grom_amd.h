@@ -1,0 +1,204 @@
+/*
+ * grom_amd.h -- C ABI of the MI355X-native GROM per-chromosome scan.
+ *
+ * The reference has no library or FFI: its seam is the C function
+ *
+ *   void count_discordant_pairs(samfile_t*, char* bam_name, char* chr_fasta,
+ *        long chr_len, char* chr_name, int chr_name_len, FILE* vcf, ...,
+ *        FILE* ctx, int** sample_hi, ..., double* pval2sd_p, ...)   GROM.c:1432
+ *
+ * called once per chromosome by find_disc_svs (GROM.c:21057) with every
+ * parameter in globals (GROM.c:710-979) and the BAM record stream positioned
+ * where the previous chromosome left it.  This header replaces that seam:
+ *
+ *   - grom_params     <- the g_* globals the scan reads (set by main,
+ *                        GROM.c:21907-22290)
+ *   - grom_chrom      <- chr_fasta / chr_len / chr_name (GROM.c:1432 args 3-6)
+ *                        plus the two facts of the serial record stream the
+ *                        scan depends on (records skipped before the walk,
+ *                        GROM.c:14859-14969, and the last base reached,
+ *                        GROM.c:5842)
+ *   - grom_reads      <- the records `my_samread` would return for this
+ *                        chromosome (GROM.c:981-992), decoded into
+ *                        structure-of-arrays form
+ *   - grom_out        <- the VCF / CTX text the scan appends to its FILE*s
+ *
+ * Plain pointers and sizes only; no torch or HIP types cross the boundary.
+ * Ownership: the caller owns every input and grom_out's buffers (grown with
+ * realloc by the library); the library owns device memory between
+ * grom_dev_init and grom_dev_fini.  Errors: negative return codes, message via
+ * grom_last_error(); the library never calls exit().  Threading: one host
+ * thread per device; calls on different devices may run concurrently.
+ */
+#ifndef GROM_AMD_H
+#define GROM_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GROM_AMD_ABI_VERSION 1
+#define GROM_MAX_TRIALS 1000 /* max_trials, GROM.c:631 */
+
+enum {
+    GROM_OK = 0,
+    GROM_E_ARG = -1,      /* invalid argument / unsupported parameter value */
+    GROM_E_HIP = -2,      /* HIP runtime failure */
+    GROM_E_NOMEM = -3,    /* host or device allocation failed */
+    GROM_E_NODEV = -4,    /* device not initialised */
+    GROM_E_OVERFLOW = -5, /* a per-tile event buffer overflowed */
+};
+
+/* Every global the scan reads.  Names follow GROM.c's g_* variables. */
+typedef struct grom_params {
+    int32_t min_mapq;          /* g_min_mapq (-q), GROM.c:803 */
+    int32_t rd_min_mapq;       /* g_rd_min_mapq (= -q, GROM.c:22102) */
+    int32_t min_base_qual;     /* g_min_base_qual (-b), GROM.c:892 */
+    int32_t min_snv;           /* g_min_snv (-n), GROM.c:891 */
+    int32_t ploidy;            /* g_ploidy (-p) */
+    int32_t gender;            /* g_gender (-g) */
+    int32_t splitread;         /* g_splitread (-S clears) */
+    int32_t rmdup;             /* g_rmdup (-M) */
+    int32_t vcf;               /* g_vcf (-f clears) */
+    int32_t overlap_mult;      /* g_overlap_mult (-l) */
+    int32_t sv_list_len;       /* g_sv_list_len (-G) */
+    int32_t rmdup_list_len;    /* g_rmdup_list_len, GROM.c:864 */
+    int32_t read_name_len;     /* g_read_name_len, GROM.c:887 */
+    int32_t sc_min;            /* g_sc_min, GROM.c:808 */
+    double min_snv_ratio;      /* g_min_snv_ratio (-a), GROM.c:895 */
+    double min_ave_bq;         /* g_min_ave_bq (-x), GROM.c:904 */
+    double snv_rd_min_factor;  /* g_snv_rd_min_factor, GROM.c:906 */
+    double high_cov_min_snv_ratio; /* g_high_cov_min_snv_ratio, GROM.c:907 */
+    /* derived by main from the insert-size pre-pass, GROM.c:22255-22290 */
+    int32_t insert_mean, insert_min_size, insert_max_size, lseq;
+    int32_t one_base_rd_len;      /* full ring length (2 * half) */
+    int32_t half_one_base_rd_len;
+    int32_t r14_one_base_rd_len;  /* g_14_one_base_rd_len */
+    int32_t r34_one_base_rd_len;  /* g_34_one_base_rd_len */
+} grom_params;
+
+/* One chromosome.  `ref` holds exactly what find_disc_svs loaded
+ * (GROM.c:21009-21045), `name` the lower-cased FASTA name it passes. */
+typedef struct grom_chrom {
+    const char *ref;
+    int64_t len;
+    const char *name;
+    int32_t tid;        /* BAM target id of the records below */
+    int32_t n_skip;     /* stream records with pos < index_start, skipped
+                           before the per-base walk (GROM.c:14859-14969) */
+    int32_t p_last;     /* last base the walk reaches (the base at which the
+                           chromosome's final record is ingested), or -1 if
+                           the walk never ingests a record */
+} grom_chrom;
+
+/* The records the chromosome's scan ingests (stream order, after the serial
+ * stream's boundary drops and the n_skip prefix), minus records flagged
+ * unmapped or duplicate, which the ingest body ignores (GROM.c:6418).
+ * seq is BAM 4-bit packed; read i's bases start at nibble base_off[i]
+ * (always even) and its qualities at qual[base_off[i]]. */
+typedef struct grom_reads {
+    int64_t n;
+    int64_t n_cigar_ops;  /* length of cigar[] */
+    int64_t n_bases;      /* length of qual[] (seq[] holds n_bases/2 bytes) */
+    const int32_t *pos;
+    const uint16_t *flag;
+    const uint8_t *mapq;
+    const int32_t *mtid;
+    const int32_t *mpos;
+    const int32_t *isize;
+    const int32_t *l_qseq;
+    const uint32_t *cigar_off;  /* n+1 prefix offsets into cigar[] */
+    const uint32_t *cigar;      /* BAM-encoded ops (len<<4 | op) */
+    const int64_t *base_off;
+    const uint8_t *seq;
+    const uint8_t *qual;
+    const uint32_t *name_id;    /* equal ids <=> equal read names; 0 = a
+                                   name that is never stored (len >= 50) */
+} grom_reads;
+
+/* Growable output text (the two FILE*s of count_discordant_pairs). */
+typedef struct grom_out {
+    char *vcf;
+    size_t vcf_len, vcf_cap;
+    char *ctx;
+    size_t ctx_len, ctx_cap;
+} grom_out;
+
+/* Per-chromosome run statistics (for benchmarks / logs). */
+typedef struct grom_stats {
+    double ms_total;        /* device time of the whole scan */
+    double ms_pileup;       /* device time of the SNV pileup/evaluation kernel */
+    int64_t bases_evaluated;
+    int64_t snv_candidates;
+    int64_t mismatch_events;
+} grom_stats;
+
+int grom_abi_version(void);
+const char *grom_last_error(void);
+
+/* Initialise `device`: upload the two binomial tables (each
+ * (GROM_MAX_TRIALS+1)^2 doubles, row-major: g_hez_prob_binom_cdf_table and
+ * g_mq_prob_binom_cdf_table, GROM.c:780-783) and the parameters. */
+int grom_dev_init(int device, const grom_params *params, const double *hez_table, const double *mq_table);
+void grom_dev_fini(int device);
+
+/* Scan one chromosome whose reads are in host memory; appends its VCF rows to
+ * out->vcf (the rows count_discordant_pairs writes for that chromosome). */
+int grom_scan_chrom(int device, const grom_chrom *chrom, const grom_reads *reads, grom_out *out, grom_stats *stats);
+
+/* Same, with every grom_reads pointer (and chrom->ref) already in device
+ * memory of `device`.  Used to time the scan with inputs resident in HBM. */
+int grom_scan_chrom_device(int device, const grom_chrom *chrom, const grom_reads *dev_reads, grom_out *out,
+                           grom_stats *stats);
+
+/* Test hook: per-base counters of every evaluated base p (p > 2*insert_max and
+ * p <= chrom->p_last), NCOUNT int32 per base in the order of the reference's
+ * declarations (see grom_amd/csrc/scan_common.h), plus the three
+ * whole-chromosome read-depth arrays (3 * len int32).  Buffers are caller
+ * owned: counts must hold (p_last - first + 1) * GROM_NCOUNT int32. */
+#define GROM_NCOUNT 40
+int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *reads, int32_t *first_pos,
+                      int32_t *counts, int64_t counts_cap, int32_t *caf3);
+
+/* Host helpers shared by the CLI and the tests (grom_amd/csrc/tables.c):
+ * the tables exactly as a run with -q min_mapq uses them. */
+void grom_build_tables(int32_t min_mapq, double *hez_table, double *mq_table);
+void grom_default_params(grom_params *p);
+/* derive insert-dependent window sizes (GROM.c:22260-22290) */
+void grom_params_set_insert(grom_params *p, int32_t insert_mean, int32_t insert_min, int32_t insert_max,
+                            int32_t lseq);
+
+void grom_out_free(grom_out *out);
+
+/* Copy a host chromosome + reads into library-owned device buffers of
+ * `device` and return device-side views of them (valid until the next upload
+ * or grom_dev_fini).  Lets callers time grom_scan_chrom_device with the inputs
+ * already resident in HBM. */
+int grom_upload(int device, const grom_chrom *chrom, const grom_reads *reads, grom_chrom *dev_chrom,
+                grom_reads *dev_reads);
+
+/* The drop-in command line (GROM's main, GROM.c:21865) as a library call:
+ * argv as for `GROM -i BAM -r FASTA -o OUT [options]`; returns the exit code.
+ * The `grom` executable is a wrapper around it. */
+int grom_cli_main(int argc, char **argv);
+
+/* ---- host conveniences for tests and benchmarks (grom_amd/csrc/hostapi.c) ---- */
+typedef struct grom_batch_handle grom_batch_handle;
+
+/* Generate one synthetic chromosome (grom_amd/csrc/synth.c) and the read
+ * batch its scan ingests.  Insert statistics are measured on the generated
+ * pairs exactly as find_insert_mean does (GROM.c:1205-1318) and written into
+ * *params (with grom_params_set_insert); *params must hold the other options. */
+grom_batch_handle *grom_synth_batch(int64_t chr_len, double coverage, int32_t read_len, double insert_mean,
+                                    double insert_sd, uint64_t seed, grom_params *params);
+/* views into the handle (valid until grom_batch_release) */
+int grom_batch_get(grom_batch_handle *h, grom_chrom *chrom, grom_reads *reads);
+void grom_batch_release(grom_batch_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1132 @@
+/*
+ * grom_oracle.c -- TEST INFRASTRUCTURE ONLY: CPU restatement of GROM v1.0.1's
+ * per-chromosome scan.  Used by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py as the checker; never linked into or called by
+ * the product path (grom_amd/).
+ *
+ * Pinning status (see DESIGN.md "Oracle"): the reference cannot be built here
+ * (it needs the missing samtools-1.3.1 tarball, Makefile:3-8) and its shipped
+ * binary `dist/GROM` is prebuilt machine code that this project does not run.
+ * The restatement is pinned against the only golden vectors the reference
+ * ships, test_data/test_outuput_tilapia_*.vcf: VCF header text, record layout
+ * and the binomial-table values behind every SNV `PR` field.  Per-base counter
+ * values are "parity unpinned" beyond that: they follow GROM.c line by line
+ * (citations inline) and are cross-checked against the independent HIP path.
+ *
+ * Scope of this restatement (round 1): the serial read stream with its
+ * chromosome-boundary quirks, -M duplicate filtering, whole-chromosome read
+ * depth (caf_rd_*), the per-base SNV tally with read-name de-duplication,
+ * soft-clip evidence, physical read depth, SNV calling, SNV list flushes and
+ * the VCF header/SNV rows.  The per-position sliding ring of the reference
+ * (GROM.c:2897-3680, 5846-6402) is restated as a modular window of
+ * g_half_one_base_rd_len positions indexed by absolute coordinate; the ring
+ * index `cdp_one_base_index` is still tracked because the SNV flush range
+ * depends on it (GROM.c:11207, 15066).
+ */
+#include "grom_oracle.h"
+
+#include <ctype.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../grom_amd/csrc/bamio.h"
+
+#define MAX_TRIALS 1000
+#define MAX_CHR_NAMES 30000
+#define MAX_CHR_NAME_LEN 50
+
+/* ---------------- globals (GROM.c:710-979) ---------------- */
+static int g_min_mapq = 20;             /* -q, GROM.c:803 */
+static int g_rd_min_mapq = 20;          /* = g_min_mapq, GROM.c:22102 */
+static double g_insert_num_st_devs = 3; /* -s, GROM.c:805 */
+static int g_min_snv = 3;               /* -n, GROM.c:891 */
+static int g_min_base_qual = 20;        /* -b, GROM.c:892 */
+static double g_min_snv_ratio = 0.2;    /* -a, GROM.c:895 */
+static double g_min_ave_bq = 15;        /* -x, GROM.c:904 */
+static double g_snv_rd_min_factor = 1.75;
+static double g_high_cov_min_snv_ratio = 0.4;
+static int g_ploidy = 2;                /* -p */
+static int g_gender = 0;                /* -g */
+static int g_splitread = 1;             /* -S */
+static int g_rmdup = 0;                 /* -M */
+static int g_rmdup_list_len = 10000;
+static int g_vcf = 1;                   /* -f */
+static int g_overlap_mult = 1;          /* -l */
+static int g_sv_list_len = 1000000;     /* -G */
+static long g_max_chr_fasta_len = 300000000; /* -B */
+static int g_read_name_len = 50;
+static int g_sc_min = 1;
+static int g_insert_max_mult = 5;
+static int insert_sample_size = 10000000;
+
+static double g_prob2, g_mq_prob;
+static int g_insert_mean, g_insert_min_size, g_insert_max_size, g_lseq;
+static long g_one_base_window_size, g_one_base_window_size_total;
+static int g_one_base_rd_len, g_half_one_base_rd_len, g_14_one_base_rd_len, g_34_one_base_rd_len;
+
+static double g_mq_table[MAX_TRIALS + 1][MAX_TRIALS + 1];
+static double g_hez_table[MAX_TRIALS + 1][MAX_TRIALS + 1];
+
+static char g_chr_names[MAX_CHR_NAMES][MAX_CHR_NAME_LEN];
+static int g_chr_names_len[MAX_CHR_NAMES];
+static long g_fasta_file_position[MAX_CHR_NAMES];
+static long g_chr_len[MAX_CHR_NAMES];
+static int g_chr_names_index = 0;
+static long g_mappable_genome_length = 0;
+
+static const char g_dna[4] = {'A', 'C', 'G', 'T'};
+static const char *g_dump_prefix = NULL;
+
+/* ---------------- binomial tables (GROM.c:21134-21626) ---------------- */
+
+/* GROM.c:21589-21626 */
+static void calculate_normal_binom_constants(void) {
+    double p = 0.3275911, a1 = 0.254829592, a2 = -0.284496736, a3 = 1.421413741, a4 = -1.453152027,
+           a5 = 1.061405429;
+    double xc = g_insert_num_st_devs / sqrt(2);
+    double t = 1.0 / (1.0 + p * xc);
+    double erf = 1.0 - (a1 * t + a2 * pow(t, 2) + a3 * pow(t, 3) + a4 * pow(t, 4) + a5 * pow(t, 5)) * exp(-pow(xc, 2));
+    g_prob2 = (1.0 - erf) / 2.0;
+    g_mq_prob = pow(10, (-g_min_mapq / 10.0));
+}
+
+/* one cell of the Poisson / normal / exact CDF (GROM.c:21226-21301, 21401-21476);
+ * `norm_min_k` is 17 for the hez table and 20 for the mq table. */
+static double binom_cdf_cell(long n, long successes, double prob, long norm_min_k) {
+    const double p = 0.3275911, a1 = 0.254829592, a2 = -0.284496736, a3 = 1.421413741, a4 = -1.453152027,
+                 a5 = 1.061405429;
+    double cdf;
+    if ((n >= 20 && prob <= 0.05) || (n >= 100 && n * prob <= 10)) {
+        double lambda = n * prob;
+        cdf = 0;
+        /* GROM keeps k! in a `long`; it wraps past 20! exactly as the x86-64
+         * imul does, which the unsigned arithmetic below reproduces. */
+        uint64_t kf = 1;
+        for (long k = 0; k < successes; k++) {
+            if (k > 1) kf = kf * (uint64_t)k;
+            cdf += pow(lambda, k) * exp(-lambda) / (double)(int64_t)kf;
+        }
+    } else if (n * prob * (1 - prob) >= 5 && successes >= norm_min_k) {
+        double stdev = sqrt(n * prob * (1.0 - prob));
+        double mean = n * prob;
+        double ns = (mean - successes + 0.5) / stdev;
+        double x = ns / sqrt(2.0);
+        double t = 1.0 / (1.0 + p * x);
+        double erf = 1.0 - (a1 * t + a2 * pow(t, 2) + a3 * pow(t, 3) + a4 * pow(t, 4) + a5 * pow(t, 5)) * exp(-pow(x, 2));
+        if (ns >= 0) cdf = (1.0 - erf) / 2.0;
+        else cdf = 1 - (erf + (1.0 - erf) / 2.0);
+    } else {
+        cdf = 0;
+        long n_minus_k = n;
+        long comb = 1;
+        for (long k = 0; k < successes; k++) {
+            cdf += comb * pow(prob, k) * pow((1 - prob), n_minus_k);
+            /* `long = double` conversion: out-of-range values become
+             * LONG_MIN on x86-64 (cvttsd2si), reproduced explicitly. */
+            double nc = (k > 0) ? (comb / (k + 1.0)) * n_minus_k : (double)comb * n_minus_k;
+            if (nc >= 9223372036854775808.0 || nc < -9223372036854775808.0 || nc != nc) comb = INT64_MIN;
+            else comb = (long)nc;
+            n_minus_k -= 1;
+        }
+    }
+    if (cdf < 0) cdf = 0;
+    if (cdf > 1) cdf = 1;
+    return 1.0 - cdf;
+}
+
+/* The reference parses the tables back from "%e" text on every run that
+ * finds them next to the executable (GROM.c:21343-21355, 21531-21545). */
+static double pct_e_roundtrip(double v) {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%e", v);
+    return atof(buf);
+}
+
+static void build_binom_tables(void) {
+    memset(g_hez_table, 0, sizeof(g_hez_table));
+    memset(g_mq_table, 0, sizeof(g_mq_table));
+    /* hez table, GROM.c:21219-21325 */
+    for (long n = 1; n < MAX_TRIALS + 1; n++)
+        for (long s = 0; s < n + 1; s++) g_hez_table[n][s] = binom_cdf_cell(n, s, 0.5, 17);
+    for (int r = 0; r < MAX_TRIALS; r++) {
+        for (int c = 0; c < MAX_TRIALS; c++) {
+            g_hez_table[r][c] = 1.0 - g_hez_table[r][c + 1];
+            if (g_hez_table[r][c] < 0) g_hez_table[r][c] = 0;
+            if (c > 0 && g_hez_table[r][c - 1] == 1) g_hez_table[r][c] = 1;
+        }
+        g_hez_table[r][MAX_TRIALS] = 1.0;
+    }
+    /* mq table, GROM.c:21392-21485 */
+    for (long n = 1; n < MAX_TRIALS + 1; n++) {
+        for (long s = 0; s < n + 1; s++) {
+            if ((s > 0 && g_mq_table[n][s - 1] == 0) || (s > 1 && g_mq_table[n][s - 1] == g_mq_table[n][s - 2]))
+                g_mq_table[n][s] = 0;
+            else
+                g_mq_table[n][s] = binom_cdf_cell(n, s, g_mq_prob, 20);
+        }
+    }
+    for (int r = 0; r <= MAX_TRIALS; r++)
+        for (int c = 0; c <= MAX_TRIALS; c++) {
+            g_hez_table[r][c] = pct_e_roundtrip(g_hez_table[r][c]);
+            g_mq_table[r][c] = pct_e_roundtrip(g_mq_table[r][c]);
+        }
+}
+
+/* ---------------- record stream (GROM.c:981-992) ---------------- */
+typedef struct {
+    bgzf_reader bg;
+    bam_hdr hdr;
+    int open;
+} stream_t;
+
+static int stream_open(stream_t *s, const char *path) {
+    memset(s, 0, sizeof(*s));
+    if (bgzf_open_read(&s->bg, path) != 0) return -1;
+    if (bam_read_header(&s->bg, &s->hdr) != 0) return -1;
+    s->open = 1;
+    return 0;
+}
+static void stream_close(stream_t *s) {
+    if (!s->open) return;
+    bgzf_close_read(&s->bg);
+    bam_free_header(&s->hdr);
+    s->open = 0;
+}
+static int my_samread(stream_t *s, bam_rec *b) {
+    int rc = bam_read_rec(&s->bg, b);
+    return rc > 0 ? 1 : -1;
+}
+
+/* ---------------- find_insert_mean (GROM.c:1205-1318) ---------------- */
+static int cmp_int(const void *a, const void *b) { return (*(const int *)a - *(const int *)b); }
+
+static int find_insert_mean(stream_t *s, int *gc_lseq, int *imin, int *imax) {
+    int *sizes = (int *)malloc((size_t)insert_sample_size * sizeof(int));
+    int *lseqs = (int *)malloc((size_t)insert_sample_size * sizeof(int));
+    int count = 0;
+    bam_rec b;
+    memset(&b, 0, sizeof(b));
+    while (my_samread(s, &b) > 0 && count < insert_sample_size) {
+        int flag = b.flag;
+        if ((flag & GF_UNMAP) == 0 && (flag & GF_DUP) == 0) {
+            if ((flag & GF_PAIRED) == 0) {
+                sizes[count] = b.l_qseq;
+                lseqs[count] = b.l_qseq;
+                count++;
+            } else if ((flag & GF_MUNMAP) == 0 && b.tid == b.mtid) {
+                if (b.pos < b.mpos && (flag & GF_PROPER) != 0 && b.isize > 0) {
+                    sizes[count] = b.isize;
+                    lseqs[count] = b.l_qseq;
+                    count++;
+                }
+            }
+        }
+    }
+    bam_free_rec(&b);
+    qsort(sizes, count, sizeof(int), cmp_int);
+    int mean = sizes[count / 2];
+    int max_insert = mean * g_insert_max_mult;
+    int start = 0, end = 0;
+    for (int a = count - 1; a >= 0; a--)
+        if (sizes[a] <= max_insert) { end = a; break; }
+    end += 1;
+    mean = sizes[start + (end - start) / 2];
+    int min_index = (int)(g_prob2 * (end - start) / 2) + start;
+    int max_index = end - min_index;
+    *imin = sizes[min_index];
+    *imax = sizes[max_index];
+    printf("insert_min_size, insert_max_size %d %d\n", *imin, *imax);
+    qsort(lseqs, count, sizeof(int), cmp_int);
+    *gc_lseq = lseqs[count / 2];
+    free(sizes);
+    free(lseqs);
+    return mean;
+}
+
+/* ---------------- FASTA (GROM.c:1321-1428, 21009-21045) ---------------- */
+static void find_genome_length(FILE *fh) {
+    char line[1000];
+    long pos = 0, chr_len = 0;
+    while (fgets(line, sizeof(line), fh)) {
+        if (line[0] != '>') {
+            size_t L = strlen(line);
+            for (size_t a = 0; a < L; a++)
+                if (isalpha((unsigned char)line[a])) {
+                    if (line[a] != 'N' && line[a] != 'n') g_mappable_genome_length += 1;
+                    chr_len += 1;
+                }
+        } else {
+            pos = ftell(fh);
+            int name_len = (int)strlen(line);
+            int w = name_len - 1, alpha_len = name_len;
+            while (w > 0) {
+                if (isgraph((unsigned char)line[w]) == 0) alpha_len = w;
+                w -= 1;
+            }
+            if (g_chr_names_index < MAX_CHR_NAMES) {
+                if (alpha_len >= MAX_CHR_NAME_LEN) alpha_len = MAX_CHR_NAME_LEN;
+                for (int a = 1; a < alpha_len; a++)
+                    g_chr_names[g_chr_names_index][a - 1] = (char)tolower((unsigned char)line[a]);
+                g_fasta_file_position[g_chr_names_index] = pos;
+                if (g_chr_names_index > 0) g_chr_len[g_chr_names_index - 1] = chr_len;
+                g_chr_names_len[g_chr_names_index] = alpha_len - 1;
+            }
+            g_chr_names_index += 1;
+            chr_len = 0;
+        }
+    }
+    if (g_chr_names_index > 0 && g_chr_names_index < MAX_CHR_NAMES) g_chr_len[g_chr_names_index - 1] = chr_len;
+    fseek(fh, 0, SEEK_SET);
+}
+
+/* name match rules shared by find_disc_svs (GROM.c:20908-20975) and
+ * count_discordant_pairs (GROM.c:1916-1961): exact, BAM "chrX" vs FASTA "X",
+ * BAM "X" vs FASTA "chrX". */
+static int names_match(const char *bam, int bam_len, const char *fa, int fa_len) {
+    char tmp[MAX_CHR_NAME_LEN + 8];
+    if (bam_len == fa_len && strncmp(bam, fa, fa_len) == 0) return 1;
+    if (bam_len - 3 == fa_len && strncmp(bam, "chr", 3) == 0) {
+        snprintf(tmp, sizeof(tmp), "chr%.*s", fa_len, fa);
+        if (strncmp(bam, tmp, bam_len) == 0) return 1;
+    } else if (bam_len + 3 == fa_len && strncmp(fa, "chr", 3) == 0) {
+        snprintf(tmp, sizeof(tmp), "chr%.*s", bam_len, bam);
+        if (strncmp(fa, tmp, fa_len) == 0) return 1;
+    }
+    return 0;
+}
+
+/* lower-case BAM target name, trimmed at the first non-graph char after
+ * index 0 (GROM.c:1899-1912) */
+static int bam_name_lc(const char *target, char *out, int cap) {
+    int L = (int)strlen(target);
+    if (L > cap - 1) L = cap - 1;
+    for (int i = 0; i < L; i++) out[i] = (char)tolower((unsigned char)target[i]);
+    out[L] = 0;
+    int i = L - 1;
+    while (i > 0) {
+        if (isgraph((unsigned char)out[i]) == 0) L = i;
+        i -= 1;
+    }
+    return L;
+}
+
+/* ---------------- per-chromosome scan state ---------------- */
+typedef struct {
+    /* current record as loaded by the fetch sites (GROM.c:5744-5837) */
+    bam_rec b;
+    int32_t pos, mpos, tlen, lseq, chr, mchr;
+    uint16_t flag, mq;
+    int add;
+    int aux_pos, aux_mq, aux_strand;
+    char aux_str[128];
+    char *aux_chr, *aux_cigar;
+} cur_t;
+
+/* window of per-position state (modular restatement of the ring) */
+typedef struct {
+    int W;          /* window length = g_half_one_base_rd_len */
+    orc_counts *c;  /* counters (pos field unused here) */
+    int32_t *names; /* g_min_snv name ids per position */
+} win_t;
+
+static inline long wslot(const win_t *w, long x) { return ((x % w->W) + w->W) % w->W; }
+
+/* ---------------- read-name interning ---------------- */
+typedef struct { char **keys; int32_t *ids; long cap, n; } nametab;
+
+static uint64_t fnv1a(const char *s) {
+    uint64_t h = 1469598103934665603ULL;
+    while (*s) { h ^= (unsigned char)*s++; h *= 1099511628211ULL; }
+    return h;
+}
+static int32_t name_id(nametab *t, const char *s) {
+    if (t->n * 2 >= t->cap) {
+        long ncap = t->cap ? t->cap * 2 : 1 << 16;
+        char **nk = (char **)calloc(ncap, sizeof(char *));
+        int32_t *ni = (int32_t *)calloc(ncap, sizeof(int32_t));
+        for (long i = 0; i < t->cap; i++)
+            if (t->keys[i]) {
+                long j = (long)(fnv1a(t->keys[i]) & (uint64_t)(ncap - 1));
+                while (nk[j]) j = (j + 1) & (ncap - 1);
+                nk[j] = t->keys[i];
+                ni[j] = t->ids[i];
+            }
+        free(t->keys);
+        free(t->ids);
+        t->keys = nk;
+        t->ids = ni;
+        t->cap = ncap;
+    }
+    long j = (long)(fnv1a(s) & (uint64_t)(t->cap - 1));
+    while (t->keys[j]) {
+        if (strcmp(t->keys[j], s) == 0) return t->ids[j];
+        j = (j + 1) & (t->cap - 1);
+    }
+    t->keys[j] = strdup(s);
+    t->ids[j] = (int32_t)(++t->n);
+    return t->ids[j];
+}
+static void nametab_free(nametab *t) {
+    for (long i = 0; i < t->cap; i++) free(t->keys[i]);
+    free(t->keys);
+    free(t->ids);
+    memset(t, 0, sizeof(*t));
+}
+
+/* aux parsing at a fetch site (GROM.c:5757-5826, 10990-11066, 14885-14950) */
+static void load_record(cur_t *c, int parse_aux) {
+    bam_rec *b = &c->b;
+    c->pos = b->pos;
+    c->flag = b->flag;
+    c->mq = b->mapq;
+    c->chr = b->tid;
+    c->mchr = b->mtid;
+    c->mpos = b->mpos;
+    c->tlen = b->isize;
+    c->lseq = b->l_qseq;
+    c->add = (c->mq >= g_min_mapq) ? 6 : 0; /* GROM.c:5829-5836 */
+    c->aux_pos = -1;
+    c->aux_mq = -1;
+    int l_aux = bam_l_aux(b);
+    if (parse_aux && l_aux > 0 && l_aux < 100) {
+        int is_xp = 1;
+        uint8_t *a = bam_aux_find(b, "XP");
+        if (!a) { is_xp = 0; a = bam_aux_find(b, "SA"); }
+        if (a) {
+            const uint8_t *src = (a[0] == 'Z') ? a + 1 : a;
+            const uint8_t *end = b->data + b->data_len;
+            int k = 0;
+            while (src + k < end && src[k] && k < (int)sizeof(c->aux_str) - 1) { c->aux_str[k] = (char)src[k]; k++; }
+            c->aux_str[k] = 0;
+            char *save = NULL;
+            c->aux_chr = strtok_r(c->aux_str, ",", &save);
+            char *t = strtok_r(NULL, ",", &save);
+            if (is_xp) {
+                if (t) {
+                    c->aux_strand = (t[0] == '+') ? 0 : 1;
+                    c->aux_pos = atoi(t + 1);
+                }
+                c->aux_cigar = strtok_r(NULL, ",", &save);
+                t = strtok_r(NULL, ",", &save);
+                c->aux_mq = t ? atoi(t) : 0;
+            } else {
+                c->aux_pos = t ? atoi(t) : -1;
+                t = strtok_r(NULL, ",", &save);
+                c->aux_strand = (t && t[0] == '+') ? 0 : 1;
+                c->aux_cigar = strtok_r(NULL, ",", &save);
+                t = strtok_r(NULL, ",", &save);
+                c->aux_mq = t ? atoi(t) : 0;
+            }
+            if (!c->aux_chr || !c->aux_cigar) c->aux_pos = -1;
+        }
+    }
+}
+
+typedef struct {
+    int n;
+    int cap;
+    int32_t *pos, *base;
+    double *ratio, *binom, *hez;
+    int32_t (*snv)[4], (*lowmq)[4], (*pir)[4], (*fs)[4];
+    int32_t *bq, *bq_all, *mq, *mq_all, *bq_rc, *mq_rc, *rc_all;
+} snv_list;
+
+static void snv_list_init(snv_list *l, int cap) {
+    memset(l, 0, sizeof(*l));
+    l->cap = cap;
+    l->pos = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->base = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->ratio = (double *)malloc(cap * sizeof(double));
+    l->binom = (double *)malloc(cap * sizeof(double));
+    l->hez = (double *)malloc(cap * sizeof(double));
+    l->snv = malloc(cap * sizeof(*l->snv));
+    l->lowmq = malloc(cap * sizeof(*l->lowmq));
+    l->pir = malloc(cap * sizeof(*l->pir));
+    l->fs = malloc(cap * sizeof(*l->fs));
+    l->bq = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->bq_all = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->mq = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->mq_all = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->bq_rc = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->mq_rc = (int32_t *)malloc(cap * sizeof(int32_t));
+    l->rc_all = (int32_t *)malloc(cap * sizeof(int32_t));
+}
+static void snv_list_free(snv_list *l) {
+    free(l->pos); free(l->base); free(l->ratio); free(l->binom); free(l->hez);
+    free(l->snv); free(l->lowmq); free(l->pir); free(l->fs);
+    free(l->bq); free(l->bq_all); free(l->mq); free(l->mq_all); free(l->bq_rc); free(l->mq_rc); free(l->rc_all);
+}
+
+/* SNV rows of one list flush (GROM.c:11203-11326 mid-scan, 15035-15160 final) */
+static void snv_flush(snv_list *l, const char *fasta, long chr_len, const int32_t *caf_rd, const int32_t *caf_low,
+                      long *last_group_pos, long range_end, long *rc_total, long *base_total, const char *chr_name,
+                      FILE *vcf, int cur_lseq) {
+    for (long a = *last_group_pos; a < range_end; a++) {
+        if (fasta[a] != 'N' && fasta[a] != 'n') {
+            *rc_total += (long)caf_rd[a] + (long)caf_low[a];
+            *base_total += 1;
+        }
+    }
+    double ave_rd = (double)*rc_total / (double)*base_total;
+    *last_group_pos = range_end;
+    char gt[128];
+    for (int a = 0; a < l->n; a++) {
+        if (!(l->rc_all[a] <= round(g_snv_rd_min_factor * ave_rd) || l->ratio[a] >= g_high_cov_min_snv_ratio)) continue;
+        int b = l->base[a];
+        if (g_vcf == 1) {
+            int cn = (int)round(l->ratio[a] * g_ploidy);
+            if (cn == 0) cn = 1;
+            for (int k = 0; k < g_ploidy; k++) {
+                gt[2 * k] = (k < cn) ? '1' : '0';
+                gt[2 * k + 1] = (k < g_ploidy - 1) ? '/' : '\0';
+            }
+            fprintf(vcf,
+                    "%s\t%d\t\t%c\t%c\t.\t.\t.\tGT:PR:AF:A:C:G:T:AL:CL:GL:TL:BQ:MQ:PIR:FS\t%s:%e:%e:%d:%d:%d:%d:%d:%d:%d:%d:"
+                    "%.2f:%.2f:%.2f:%.2f\n",
+                    chr_name, l->pos[a] + 1, fasta[l->pos[a]], g_dna[b], gt, l->binom[a], l->ratio[a], l->snv[a][0],
+                    l->snv[a][1], l->snv[a][2], l->snv[a][3], l->lowmq[a][0], l->lowmq[a][1], l->lowmq[a][2],
+                    l->lowmq[a][3], (double)l->bq_all[a] / (double)l->rc_all[a],
+                    (double)l->mq_all[a] / (double)l->rc_all[a], (double)l->pir[a][b] / (double)l->snv[a][b],
+                    (double)l->fs[a][b] / (double)l->snv[a][b]);
+        } else {
+            /* GROM.c:11276-11323 (-f tab format) */
+            fprintf(vcf, "SNV\t%s\t%d\t%c\t%e\t%d\t%d", chr_name, l->pos[a], g_dna[b], l->ratio[a], 0, 0);
+            for (int k = 0; k < 4; k++) fprintf(vcf, "\t%d", l->snv[a][k]);
+            for (int k = 0; k < 4; k++) fprintf(vcf, "\t%d", l->lowmq[a][k]);
+            fprintf(vcf, "\t%d\t%d\t%d\t%d\t%d\t%d\t%d", l->bq[a], l->bq_all[a], l->mq[a], l->mq_all[a], l->bq_rc[a],
+                    l->mq_rc[a], l->rc_all[a]);
+            double pir = (double)l->pir[a][b] / (double)l->snv[a][b], fs = (double)l->fs[a][b] / (double)l->snv[a][b];
+            if (l->pos[a] > 0 && l->pos[a] < chr_len - 1)
+                fprintf(vcf, "\t%.2f\t%.2f\t%c%c%c", pir, fs, fasta[l->pos[a] - 1], fasta[l->pos[a]], fasta[l->pos[a] + 1]);
+            else
+                fprintf(vcf, "\t%.2f\t%.2f\t%c%c%c", pir, fs, '.', '.', '.');
+            fprintf(vcf, "\t");
+            for (int k = 0; k < cur_lseq; k++) {
+                long x = l->pos[a] - cur_lseq + 1 + k;
+                fputc(x < 0 ? 'N' : fasta[x], vcf);
+            }
+            for (int k = 0; k < cur_lseq - 1; k++) {
+                long x = l->pos[a] + cur_lseq - 1 - k;
+                fputc(x >= chr_len - 1 ? 'N' : fasta[x], vcf);
+            }
+            fprintf(vcf, "\t%e\t%e\n", l->binom[a], l->hez[a]);
+        }
+    }
+    l->n = 0;
+}
+
+typedef struct {
+    const char *fasta;
+    long chr_len;
+    win_t w;
+    int32_t *caf_mq, *caf_rd, *caf_low;
+    nametab names;
+    /* -M state (GROM.c:5451-5498) */
+    int *rm_mchr, *rm_mpos, *rm_lseq, *rm_tlen, *rm_svtype;
+    int rm_index, old_pos;
+    int p, one_base_index;
+} scan_t;
+
+enum { SV_DEL = 0, SV_DUP = 1, SV_INV_F = 8, SV_INV_R = 9, SV_CTX_FF = 11, SV_CTX_FR = 12, SV_CTX_RF = 13, SV_CTX_RR = 14 };
+
+/* -M pair-orientation class (GROM.c:6432-6529) */
+static int rmdup_svtype(const cur_t *c) {
+    int rev = (c->flag & GF_REVERSE) != 0, mrev = (c->flag & GF_MREVERSE) != 0;
+    if (c->chr == c->mchr) {
+        if (c->mpos > c->pos) {
+            if (!rev && mrev) return SV_DEL;
+            if (!rev && !mrev) return SV_INV_F;
+            return mrev ? SV_INV_R : SV_DUP;
+        }
+        if (rev && !mrev) return SV_DEL;
+        if (!rev && !mrev) return SV_INV_F;
+        if (mrev) return rev ? SV_INV_R : SV_DUP;
+        return -1;
+    }
+    if (!rev) return mrev ? SV_CTX_FR : SV_CTX_FF;
+    return mrev ? SV_CTX_RR : SV_CTX_RF;
+}
+
+/* one record through the ingest body (GROM.c:6418-7185) */
+static void ingest(scan_t *s, cur_t *c) {
+    const char *fasta = s->fasta;
+    long chr_len = s->chr_len;
+    bam_rec *b = &c->b;
+    if ((c->flag & GF_UNMAP) != 0 || (c->flag & GF_DUP) != 0) return;
+    int add_to_list = 1;
+    if (g_rmdup > 0 && (c->flag & GF_PAIRED) != 0 && (c->flag & GF_MUNMAP) == 0) {
+        int svtype = rmdup_svtype(c);
+        if (svtype >= 0) {
+            if (c->pos != s->old_pos) {
+                s->rm_index = 0;
+                s->old_pos = c->pos;
+            } else {
+                for (int a = 0; a < s->rm_index; a++) {
+                    if (c->mpos == s->rm_mpos[a] && c->mchr == s->rm_mchr[a] && s->rm_lseq[a] == c->lseq &&
+                        s->rm_tlen[a] == c->tlen && c->mq >= g_min_mapq && s->rm_svtype[a] == svtype) {
+                        add_to_list = 0;
+                        break;
+                    }
+                }
+            }
+            if (add_to_list == 1 && s->rm_index < g_rmdup_list_len) {
+                s->rm_mchr[s->rm_index] = c->mchr;
+                s->rm_mpos[s->rm_index] = c->mpos;
+                s->rm_lseq[s->rm_index] = c->lseq;
+                s->rm_tlen[s->rm_index] = c->tlen;
+                s->rm_svtype[s->rm_index] = svtype;
+                s->rm_index += 1;
+            }
+        }
+    }
+    if (add_to_list != 1) return;
+    const uint32_t *cig = bam_cigar(b);
+    int n_cigar = b->n_cigar;
+
+    /* whole-chromosome read depth, GROM.c:6605-6671 */
+    long caf_pos = c->pos;
+    for (int a = 0; a < n_cigar; a++) {
+        int op = cig[a] & 0xf;
+        long len = cig[a] >> 4;
+        if (op == GC_MATCH || op == GC_EQUAL || op == GC_DIFF) {
+            if (caf_pos >= 0 && caf_pos + len < chr_len) {
+                for (long x = caf_pos; x < caf_pos + len; x++) {
+                    s->caf_mq[x] += c->mq;
+                    if (c->mq >= g_rd_min_mapq) s->caf_rd[x] += 1;
+                    else s->caf_low[x] += 1;
+                }
+            }
+            caf_pos += len;
+        } else if (op == GC_DEL) {
+            caf_pos += len;
+        }
+    }
+
+    /* CIGAR copy limited to 1000 ops, GROM.c:6740-6750 */
+    int cigar_len = n_cigar > 1000 ? 1000 : n_cigar;
+    int c_type[1000];
+    long c_len[1000];
+    for (int a = 0; a < cigar_len; a++) { c_type[a] = cig[a] & 0xf; c_len[a] = cig[a] >> 4; }
+
+    const char *rname = bam_qname(b);
+    int name_storable = strlen(rname) < (size_t)g_read_name_len && rname[0] != 0;
+    int32_t nid = name_id(&s->names, rname);
+    const uint8_t *seq4 = bam_seq(b);
+    const uint8_t *qual = bam_qual(b);
+    int lseq_q = b->l_qseq;
+    int snv_base = 0, snv_ref_base = 0, last_cigar_id = 0;
+    int rev = (c->flag & GF_REVERSE) != 0;
+    (void)last_cigar_id;
+
+    /* per-base SNV tally, GROM.c:6769-7059 */
+    for (int a = 0; a < cigar_len; a++) {
+        int op = c_type[a];
+        if (op == GC_MATCH || op == GC_EQUAL || op == GC_DIFF) {
+            if (c->pos >= 0 && c->pos < chr_len) {
+                long loop_end;
+                if (c->pos + snv_ref_base + c_len[a] >= chr_len) loop_end = chr_len - c->pos;
+                else loop_end = c_len[a];
+                for (long bl = 0; bl < loop_end; bl++) {
+                    long x = c->pos + snv_ref_base;
+                    /* bytes past the read's own qual/seq or past the chromosome are
+                     * only reached for reads running off the chromosome end; those
+                     * positions are never evaluated ("edge semantics") */
+                    int q = snv_base < lseq_q ? qual[snv_base] : 0;
+                    char sb = snv_base < lseq_q ? grom_nt16_rev[bam_seqi(seq4, snv_base)] : 'N';
+                    char rb = x < chr_len ? (char)toupper((unsigned char)fasta[x]) : 'N';
+                    orc_counts *k = &s->w.c[wslot(&s->w, x)];
+                    if (c->mq >= g_min_mapq && q >= g_min_base_qual) {
+                        int found = 0;
+                        if (rb != sb) {
+                            int32_t *slots = &s->w.names[wslot(&s->w, x) * g_min_snv];
+                            for (int cl = 0; cl < g_min_snv; cl++) {
+                                if (slots[cl] == 0) {
+                                    if (name_storable) slots[cl] = nid;
+                                    break;
+                                } else if (slots[cl] == nid) {
+                                    found = 1;
+                                    break;
+                                }
+                            }
+                        }
+                        if (!found) {
+                            for (int cl = 0; cl < 4; cl++) {
+                                if (sb != g_dna[cl]) continue;
+                                if (rb == sb) {
+                                    k->snv[cl] += 1;
+                                    k->bq += q; k->bq_all += q;
+                                    k->mq += c->mq; k->mq_all += c->mq;
+                                    k->bq_rc += 1; k->mq_rc += 1; k->rc_all += 1;
+                                    if (!rev) { k->pir[cl] += snv_base; k->fs[cl] += 1; }
+                                    else k->pir[cl] += c->lseq - snv_base;
+                                } else {
+                                    /* guard at GROM.c:6889 compares a length with an
+                                     * op code; both ids are >= 0, so always taken */
+                                    k->snv[cl] += 1;
+                                    k->bq += q; k->bq_all += q;
+                                    k->mq += c->mq; k->mq_all += c->mq;
+                                    k->bq_rc += 1; k->mq_rc += 1; k->rc_all += 1;
+                                    k->pir[cl] += snv_base;
+                                    if (!rev) k->fs[cl] += 1;
+                                }
+                                break;
+                            }
+                        }
+                    } else {
+                        for (int cl = 0; cl < 4; cl++) {
+                            if (sb != g_dna[cl]) continue;
+                            k->snv_lowmq[cl] += 1;
+                            k->bq_all += q;
+                            k->mq_all += c->mq;
+                            k->rc_all += 1;
+                            break;
+                        }
+                    }
+                    snv_base += 1;
+                    snv_ref_base += 1;
+                }
+                last_cigar_id = 0;
+            }
+        } else if (op == GC_SOFT_CLIP || op == GC_HARD_CLIP) {
+            if (op == GC_HARD_CLIP) c->lseq += (int)c_len[a];
+            else snv_base += (int)c_len[a];
+            last_cigar_id = 0;
+        } else if (op == GC_INS) {
+            snv_base += (int)c_len[a];
+            last_cigar_id = 1;
+        } else if (op == GC_DEL) {
+            snv_ref_base += (int)c_len[a];
+            last_cigar_id = 1;
+        } else if (op == GC_REF_SKIP) {
+            snv_ref_base += (int)c_len[a];
+            last_cigar_id = 0;
+        } else {
+            last_cigar_id = 0;
+        }
+    }
+
+    /* clip lengths, GROM.c:7067-7100 */
+    int start_adj = (c_type[0] == GC_SOFT_CLIP || c_type[0] == GC_HARD_CLIP) ? (int)c_len[0] : 0;
+    int end_adj = (c_type[cigar_len - 1] == GC_SOFT_CLIP || c_type[cigar_len - 1] == GC_HARD_CLIP)
+                      ? (int)c_len[cigar_len - 1] : 0;
+    int end_adj_indel = 0;
+    for (int a = 0; a < cigar_len; a++) {
+        if (c_type[a] == GC_INS) end_adj_indel += (int)c_len[a];
+        else if (c_type[a] == GC_DEL) end_adj_indel -= (int)c_len[a];
+    }
+    int paired = (c->flag & GF_PAIRED) != 0, munmap = (c->flag & GF_MUNMAP) != 0;
+    long E = (long)c->pos - start_adj + c->lseq - end_adj - end_adj_indel;
+
+    /* soft-clip evidence, GROM.c:7105-7169 */
+    if (start_adj >= g_sc_min) {
+        orc_counts *k = &s->w.c[wslot(&s->w, (long)c->pos - 1)];
+        if (!paired || (!rev && (munmap || (!munmap && c->chr == c->mchr && c->mpos > c->pos)))) {
+            k->sc_left += c->add; k->sc_left_rd += 1; k->sc_rd += 1;
+        }
+        if (paired && !munmap && c->chr != c->mchr && rev) {
+            k->ctx_sc_left += c->add; k->ctx_sc_left_rd += 1; k->ctx_sc_rd += 1;
+        }
+        if (paired && !munmap && c->chr == c->mchr && rev && abs(c->tlen) <= g_insert_max_size && c->mpos < c->pos) {
+            k->indel_sc_left += c->add; k->indel_sc_left_rd += 1; k->indel_sc_rd += 1;
+        }
+    }
+    if (end_adj >= g_sc_min) {
+        orc_counts *k = &s->w.c[wslot(&s->w, E)];
+        if (!paired || (rev && (munmap || (!munmap && c->chr == c->mchr && c->mpos < c->pos)))) {
+            k->sc_right += c->add; k->sc_right_rd += 1; k->sc_rd += 1;
+        }
+        if (paired && !munmap && c->chr != c->mchr && !rev) {
+            k->ctx_sc_right += c->add; k->ctx_sc_right_rd += 1; k->ctx_sc_rd += 1;
+        }
+        if (paired && !munmap && c->chr == c->mchr && !rev && abs(c->tlen) <= g_insert_max_size && c->mpos > c->pos) {
+            k->indel_sc_right += c->add; k->indel_sc_right_rd += 1; k->indel_sc_rd += 1;
+        }
+    }
+    /* physical read depth over [pos, E), GROM.c:7173-7181 */
+    for (long x = c->pos; x < E; x++) s->w.c[wslot(&s->w, x)].rd += 1;
+}
+
+static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_match, int chr_match,
+                            const char *fasta, long chr_len, const char *chr_name, FILE *vcf, FILE *dump_cnt) {
+    (void)target_name_of_match;
+    scan_t s;
+    memset(&s, 0, sizeof(s));
+    s.fasta = fasta;
+    s.chr_len = chr_len;
+    s.w.W = g_half_one_base_rd_len;
+    s.w.c = (orc_counts *)calloc(s.w.W, sizeof(orc_counts));
+    s.w.names = (int32_t *)calloc((size_t)s.w.W * g_min_snv, sizeof(int32_t));
+    s.caf_mq = (int32_t *)calloc(chr_len, sizeof(int32_t));
+    s.caf_rd = (int32_t *)calloc(chr_len, sizeof(int32_t));
+    s.caf_low = (int32_t *)calloc(chr_len, sizeof(int32_t));
+    s.rm_mchr = (int *)malloc(g_rmdup_list_len * sizeof(int));
+    s.rm_mpos = (int *)malloc(g_rmdup_list_len * sizeof(int));
+    s.rm_lseq = (int *)malloc(g_rmdup_list_len * sizeof(int));
+    s.rm_tlen = (int *)malloc(g_rmdup_list_len * sizeof(int));
+    s.rm_svtype = (int *)malloc(g_rmdup_list_len * sizeof(int));
+    s.old_pos = -1;
+
+    snv_list sl;
+    snv_list_init(&sl, g_sv_list_len);
+    long last_group_pos = 0, rc_total = 0, base_total = 0;
+
+    int idx_start = g_one_base_rd_len / 4 + 1; /* GROM.c:2918 */
+    int idx = idx_start;
+    int p = idx_start;
+    int begin = 0;
+    int H2 = s.w.W / 2;
+    long n_skipped = 0, n_ingested = 0;
+
+    if (chr_match >= 0) {
+        while (my_samread(st, &c->b) > 0 && begin < 2) {
+            load_record(c, 1);
+            if (c->chr == chr_match) {
+                begin = 1;
+                while (begin < 2) {
+                    idx += 1;
+                    if (idx == g_34_one_base_rd_len) idx = g_14_one_base_rd_len; /* ring shift */
+                    if (begin < 2 && c->pos >= idx_start) {
+                        if (c->pos - g_overlap_mult * g_insert_max_size <= p) {
+                            while (c->pos - g_overlap_mult * g_insert_max_size <= p && begin < 2) {
+                                ingest(&s, c);
+                                n_ingested++;
+                                if (my_samread(st, &c->b) > 0) {
+                                    load_record(c, g_splitread == 1);
+                                    if (c->chr != chr_match) begin = 2;
+                                } else {
+                                    begin = 2;
+                                }
+                            }
+                        }
+                        if (p > 2 * g_insert_max_size) {
+                            orc_counts *k = &s.w.c[wslot(&s.w, p)];
+                            if (dump_cnt) {
+                                orc_counts o = *k;
+                                o.pos = p;
+                                fwrite(&o, sizeof(o), 1, dump_cnt);
+                            }
+                            /* SNV test, GROM.c:11096-11199 */
+                            if (k->rd + k->indel_sc_rd > 0 && fasta[p] != 'N' && fasta[p] != 'n') {
+                                int total = 0;
+                                for (int a = 0; a < 4; a++) total += k->snv[a];
+                                for (int a = 0; a < 4; a++) {
+                                    float ratio = (float)k->snv[a] / (float)total;
+                                    double binom, hez;
+                                    if (total > MAX_TRIALS) {
+                                        binom = g_mq_table[MAX_TRIALS][k->snv[a] * MAX_TRIALS / total];
+                                        hez = g_hez_table[MAX_TRIALS][k->snv[a] * MAX_TRIALS / total];
+                                    } else {
+                                        binom = g_mq_table[total][k->snv[a]];
+                                        hez = g_hez_table[total][k->snv[a]];
+                                    }
+                                    if (toupper((unsigned char)fasta[p]) != g_dna[a] && ratio >= g_min_snv_ratio &&
+                                        k->snv[a] >= g_min_snv && (double)k->bq_all / (double)k->rc_all >= g_min_ave_bq) {
+                                        if (sl.n > 0 && sl.pos[sl.n - 1] == p) {
+                                            if (ratio > sl.ratio[sl.n - 1]) {
+                                                sl.ratio[sl.n - 1] = ratio;
+                                                sl.base[sl.n - 1] = a;
+                                                sl.binom[sl.n - 1] = binom;
+                                                sl.hez[sl.n - 1] = hez;
+                                            }
+                                        } else {
+                                            int n = sl.n;
+                                            sl.pos[n] = p;
+                                            for (int bb = 0; bb < 4; bb++) {
+                                                sl.snv[n][bb] = k->snv[bb];
+                                                sl.lowmq[n][bb] = k->snv_lowmq[bb];
+                                                sl.pir[n][bb] = k->pir[bb];
+                                                sl.fs[n][bb] = k->fs[bb];
+                                            }
+                                            sl.ratio[n] = ratio;
+                                            sl.base[n] = a;
+                                            sl.binom[n] = binom;
+                                            sl.hez[n] = hez;
+                                            sl.bq[n] = k->bq; sl.bq_all[n] = k->bq_all;
+                                            sl.mq[n] = k->mq; sl.mq_all[n] = k->mq_all;
+                                            sl.bq_rc[n] = k->bq_rc; sl.mq_rc[n] = k->mq_rc;
+                                            sl.rc_all[n] = k->rc_all;
+                                            sl.n += 1;
+                                        }
+                                    }
+                                }
+                                if (sl.n >= g_sv_list_len - 10)
+                                    snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx,
+                                              &rc_total, &base_total, chr_name, vcf, c->lseq);
+                            }
+                        }
+                        p += 1;
+                        /* slide the modular window: the slot of p-H/2-1 now holds p+H/2-1 */
+                        {
+                            long x = (long)p + H2 - 1;
+                            long sl_ = wslot(&s.w, x);
+                            memset(&s.w.c[sl_], 0, sizeof(orc_counts));
+                            memset(&s.w.names[sl_ * g_min_snv], 0, sizeof(int32_t) * g_min_snv);
+                        }
+                    } else {
+                        n_skipped++;
+                        if (my_samread(st, &c->b) > 0) {
+                            load_record(c, 1);
+                            if (c->chr != chr_match) begin = 2;
+                        } else {
+                            begin = 2;
+                        }
+                    }
+                }
+            } else if (begin == 1) {
+                begin = 2;
+            }
+        }
+    }
+    /* final SNV flush, GROM.c:15063-15160 */
+    snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx, &rc_total, &base_total,
+              chr_name, vcf, c->lseq);
+
+    if (g_dump_prefix) {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s.%s.caf", g_dump_prefix, chr_name);
+        FILE *f = fopen(path, "wb");
+        if (f) {
+            fwrite(s.caf_mq, sizeof(int32_t), chr_len, f);
+            fwrite(s.caf_rd, sizeof(int32_t), chr_len, f);
+            fwrite(s.caf_low, sizeof(int32_t), chr_len, f);
+            fclose(f);
+        }
+        snprintf(path, sizeof(path), "%s.%s.meta", g_dump_prefix, chr_name);
+        f = fopen(path, "w");
+        if (f) {
+            fprintf(f, "p_end %d\nidx_end %d\nn_skip %ld\nn_ingested %ld\n", p, idx, n_skipped, n_ingested);
+            fclose(f);
+        }
+    }
+    snv_list_free(&sl);
+    nametab_free(&s.names);
+    free(s.w.c); free(s.w.names);
+    free(s.caf_mq); free(s.caf_rd); free(s.caf_low);
+    free(s.rm_mchr); free(s.rm_mpos); free(s.rm_lseq); free(s.rm_tlen); free(s.rm_svtype);
+}
+
+/* VCF header, GROM.c:20517-20565; the .ctx.vcf variant (GROM.c:22612-22651)
+ * omits the GT and the four CNV FORMAT lines.  fileDate may be pinned by
+ * GROM_FILEDATE for reproducible comparisons. */
+static void write_header(FILE *f, const char *fasta_file_name, int ctx) {
+    const char *pin = getenv("GROM_FILEDATE");
+    fprintf(f, "##fileformat=VCFv4.2\n");
+    if (pin) fprintf(f, "##fileDate=%s\n", pin);
+    else {
+        time_t t = time(NULL);
+        struct tm tm = *localtime(&t);
+        fprintf(f, "##fileDate=%d%d%d\n", tm.tm_year + 1900, tm.tm_mon + 1, tm.tm_mday);
+    }
+    fprintf(f, "##reference=%s\n", fasta_file_name);
+    static const char *rest0 =
+        "##ALT=<ID=DEL,Description=\"Deletion\">\n"
+        "##ALT=<ID=DUP,Description=\"Duplication\">\n"
+        "##ALT=<ID=INS,Description=\"Insertion\">\n"
+        "##ALT=<ID=INV,Description=\"Inversion\">\n"
+        "##INFO=<ID=END,Number=1,Type=Integer,Description=\"End position of the structural variant\">\n"
+""; fputs(rest0, f); if (!ctx) fputs("##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n", f);
+    static const char *rest =
+        "##FORMAT=<ID=SPR,Number=1,Type=Float,Description=\"Probability of start breakpoint evidence occurring by chance\">\n"
+        "##FORMAT=<ID=EPR,Number=1,Type=Float,Description=\"Probability of end breakpoint evidence occurring by chance\">\n"
+        "##FORMAT=<ID=SEV,Number=1,Type=Integer,Description=\"Evidence supporting variant at start breakpoint\">\n"
+        "##FORMAT=<ID=EEV,Number=1,Type=Integer,Description=\"Evidence supporting variant at end breakpoint\">\n"
+        "##FORMAT=<ID=SRD,Number=1,Type=Integer,Description=\"Physical read depth at start breakpoint\">\n"
+        "##FORMAT=<ID=ERD,Number=1,Type=Integer,Description=\"Physical read depth at end breakpoint\">\n"
+        "##FORMAT=<ID=SCO,Number=1,Type=Integer,Description=\"Concordant pairs at start breakpoint\">\n"
+        "##FORMAT=<ID=ECO,Number=1,Type=Integer,Description=\"Concordant pairs at end breakpoint\">\n"
+        "##FORMAT=<ID=SOT,Number=1,Type=Integer,Description=\"Count of distinct SVs with evidence at start breakpoint\">\n"
+        "##FORMAT=<ID=EOT,Number=1,Type=Integer,Description=\"Count of distinct SVs with evidence at end breakpoint\">\n"
+        "##FORMAT=<ID=SSC,Number=1,Type=Integer,Description=\"Soft-clipped reads at start breakpoint\">\n"
+        "##FORMAT=<ID=ESC,Number=1,Type=Integer,Description=\"Soft-clipped at end breakpoint\">\n"
+        "##FORMAT=<ID=SFR,Number=1,Type=Integer,Description=\"Position of first read supporting start breakpoint\">\n"
+        "##FORMAT=<ID=SLR,Number=1,Type=Integer,Description=\"Position of last read supporting start breakpoint\">\n"
+        "##FORMAT=<ID=EFR,Number=1,Type=Integer,Description=\"Position of first read supporting end breakpoint\">\n"
+        "##FORMAT=<ID=ELR,Number=1,Type=Integer,Description=\"Position of last read supporting end breakpoint\">\n"
+        "##FORMAT=<ID=AF,Number=1,Type=Float,Description=\"Allele frequency (high mapping quality reads)\">\n"
+        "##FORMAT=<ID=PR,Number=1,Type=Float,Description=\"Probability of SNV evidence occurring by chance\">\n"
+        "##FORMAT=<ID=A,Number=1,Type=Integer,Description=\"A nucleotides (high mapping quality reads)\">\n"
+        "##FORMAT=<ID=C,Number=1,Type=Integer,Description=\"C nucleotides (high mapping quality reads)\">\n"
+        "##FORMAT=<ID=G,Number=1,Type=Integer,Description=\"G nucleotides (high mapping quality reads)\">\n"
+        "##FORMAT=<ID=T,Number=1,Type=Integer,Description=\"T nucleotides (high mapping quality reads)\">\n"
+        "##FORMAT=<ID=AL,Number=1,Type=Integer,Description=\"A nucleotides (low mapping quality reads)\">\n"
+        "##FORMAT=<ID=CL,Number=1,Type=Integer,Description=\"C nucleotides (low mapping quality reads)\">\n"
+        "##FORMAT=<ID=GL,Number=1,Type=Integer,Description=\"G nucleotides (low mapping quality reads)\">\n"
+        "##FORMAT=<ID=TL,Number=1,Type=Integer,Description=\"T nucleotides (low mapping quality reads)\">\n"
+        "##FORMAT=<ID=BQ,Number=1,Type=Float,Description=\"Average base quality (all reads)\">\n"
+        "##FORMAT=<ID=MQ,Number=1,Type=Float,Description=\"Average mapping quality (all reads)\">\n"
+        "##FORMAT=<ID=PIR,Number=1,Type=Float,Description=\"Average distance of SNV from DNA fragment end)\">\n"
+        "##FORMAT=<ID=FS,Number=1,Type=Integer,Description=\"SNV reads mapped to forward strand)\">\n"
+"";
+    fputs(rest, f);
+    if (!ctx)
+        fputs("##FORMAT=<ID=SD,Number=1,Type=Float,Description=\"CNV standard deviation\"\n"
+              "##FORMAT=<ID=Z,Number=1,Type=Float,Description=\"CNV probability score\"\n"
+              "##FORMAT=<ID=CN,Number=1,Type=Float,Description=\"CNV copy number\"\n"
+              "##FORMAT=<ID=CS,Number=1,Type=Float,Description=\"CNV copy number standard deviation\"\n", f);
+    fputs("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\n", f);
+}
+
+/* ---------------- driver: main + find_disc_svs ---------------- */
+int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
+    g_dump_prefix = dump_prefix;
+    const char *bam_file_name = NULL, *fasta_file_name = NULL, *results_file_name = NULL;
+    optind = 1;
+    int opt;
+    /* getopt string of GROM.c:21908 */
+    while ((opt = getopt(argc, argv,
+                         "Z:W:X:Q:A:Y:B:D:E:K:N:V:U:L:F:SP:c:R:MG:i:r:o:p:q:s:v:g:l:d:b:n:a:y:z:e:fj:k:m:u:w:x:h")) != -1) {
+        switch (opt) {
+        case 'S': g_splitread = 0; break;
+        case 'G': g_sv_list_len = atoi(optarg); break;
+        case 'M': g_rmdup = 1; break;
+        case 'i': bam_file_name = optarg; break;
+        case 'r': fasta_file_name = optarg; break;
+        case 'o': results_file_name = optarg; break;
+        case 'B': g_max_chr_fasta_len = atol(optarg); break;
+        case 'p': g_ploidy = atoi(optarg); break;
+        case 'q': g_min_mapq = atoi(optarg); break;
+        case 's': g_insert_num_st_devs = atof(optarg); break;
+        case 'g': g_gender = atoi(optarg); break;
+        case 'l': g_overlap_mult = atoi(optarg); break;
+        case 'b': g_min_base_qual = atoi(optarg); break;
+        case 'n': g_min_snv = atoi(optarg); break;
+        case 'a': g_min_snv_ratio = atof(optarg); break;
+        case 'f': g_vcf = 0; break;
+        case 'x': g_min_ave_bq = atof(optarg); break;
+        case 'h': return 0;
+        case '?': return 1;
+        default: break; /* options outside this restatement's scope */
+        }
+    }
+    g_rd_min_mapq = g_min_mapq; /* GROM.c:22102 */
+    if (!bam_file_name) { printf("ERROR: No bam file specified.\n"); return 1; }
+    stream_t st;
+    if (stream_open(&st, bam_file_name) != 0) { printf("\nCould not open %s\n", bam_file_name); return 1; }
+    if (!bai_exists(bam_file_name)) { printf("Could not open BAM indexing file\n"); return 1; }
+    if (!results_file_name) { printf("ERROR: No output file specified.\n"); return 1; }
+    if (!fasta_file_name) { printf("ERROR: No reference file specified.\n"); return 1; }
+    FILE *fasta = fopen(fasta_file_name, "r");
+    if (!fasta) { printf("\nCould not open %s\n", fasta_file_name); return 1; }
+
+    calculate_normal_binom_constants();
+    build_binom_tables();
+    g_insert_mean = find_insert_mean(&st, &g_lseq, &g_insert_min_size, &g_insert_max_size);
+    stream_close(&st);
+    if (g_insert_mean < g_lseq) g_insert_mean = g_lseq;
+    g_one_base_window_size = 2 * g_insert_mean - 1;
+    g_one_base_window_size_total = g_insert_mean;
+    for (long a = 0; a < g_insert_mean - 1; a++) g_one_base_window_size_total += 2 * (a + 1);
+    printf("insert mean, insert minimum, insert maximum: %d %d %d\n", g_insert_mean, g_insert_min_size, g_insert_max_size);
+    /* window sizes, GROM.c:22282-22290 */
+    g_one_base_rd_len = g_overlap_mult * 8 * (2 * g_insert_mean - 1);
+    if (g_overlap_mult * 8 * (g_insert_max_size + 1) > g_one_base_rd_len)
+        g_one_base_rd_len = g_overlap_mult * 8 * (g_insert_max_size + 1);
+    g_half_one_base_rd_len = g_one_base_rd_len;
+    g_34_one_base_rd_len = g_half_one_base_rd_len + g_half_one_base_rd_len / 2;
+    g_14_one_base_rd_len = g_34_one_base_rd_len - g_half_one_base_rd_len;
+    g_one_base_rd_len = 2 * g_one_base_rd_len;
+
+    find_genome_length(fasta);
+
+    FILE *vcf = fopen(results_file_name, "w");
+    if (!vcf) { printf("Error opening file %s\n", results_file_name); return 1; }
+    char ctx_name[4096];
+    size_t rl = strlen(results_file_name);
+    if (rl > 4 && strcmp(results_file_name + rl - 4, ".vcf") == 0)
+        snprintf(ctx_name, sizeof(ctx_name), "%.*s.ctx.vcf", (int)(rl - 4), results_file_name);
+    else
+        snprintf(ctx_name, sizeof(ctx_name), "%s.ctx", results_file_name);
+    FILE *ctx = fopen(ctx_name, "w");
+    if (g_vcf == 1) {
+        write_header(vcf, fasta_file_name, 0);
+    }
+
+    /* find_disc_svs opens its own stream from the file start, GROM.c:20471 */
+    if (stream_open(&st, bam_file_name) != 0) return 1;
+    char *chr_fasta = (char *)malloc(g_max_chr_fasta_len + 1);
+    memset(chr_fasta, 0, g_max_chr_fasta_len + 1);
+    int idx_start = g_one_base_rd_len / 4 + 1;
+    cur_t cur;
+    memset(&cur, 0, sizeof(cur));
+    int line_len = 0, alpha_len = 0;
+    for (int t = 0; t < st.hdr.n_ref; t++) {
+        char bam_lc[MAX_CHR_NAMES];
+        int bl = bam_name_lc(st.hdr.ref_name[t], bam_lc, (int)sizeof(bam_lc));
+        int fmatch = -1;
+        for (int f = 0; f < g_chr_names_index; f++)
+            if (names_match(bam_lc, bl, g_chr_names[f], g_chr_names_len[f])) { fmatch = f; break; }
+        if ((bl == 4 && strncmp(bam_lc, "chry", 4) == 0 && g_gender == 0) ||
+            (bl == 1 && strncmp(bam_lc, "y", 1) == 0 && g_gender == 0))
+            fmatch = -1; /* GROM.c:20979-20988 */
+        if (fmatch < 0) continue;
+        /* load the chromosome, GROM.c:21009-21045 */
+        long chr_len = 0;
+        char line[1000];
+        fseek(fasta, g_fasta_file_position[fmatch], SEEK_SET);
+        while (fgets(line, sizeof(line), fasta) && line[0] != '>') {
+            if (chr_len == 0 || (int)strlen(line) != line_len) {
+                line_len = (int)strlen(line);
+                int w = line_len - 1;
+                while (isalpha((unsigned char)line[w]) == 0 && w > 0) w -= 1;
+                alpha_len = w + 1;
+            }
+            if (chr_len + alpha_len <= g_max_chr_fasta_len) memcpy(chr_fasta + chr_len, line, alpha_len);
+            else printf("ERROR: Reference chromosome length exceeds maximum allowed chromosome size (%ld)\n",
+                        g_max_chr_fasta_len);
+            chr_len += alpha_len;
+        }
+        if (!(chr_len > idx_start + g_overlap_mult * g_insert_max_size)) continue;
+        if (!(chr_len > 0 && chr_len <= g_max_chr_fasta_len)) continue;
+        /* count_discordant_pairs re-derives the BAM target, GROM.c:1894-1961 */
+        int chr_match = -1;
+        const char *target_name = NULL;
+        for (int a = 0; a < st.hdr.n_ref; a++) {
+            char lc[MAX_CHR_NAMES];
+            int l2 = bam_name_lc(st.hdr.ref_name[a], lc, (int)sizeof(lc));
+            target_name = st.hdr.ref_name[a];
+            if (names_match(lc, l2, g_chr_names[fmatch], g_chr_names_len[fmatch])) { chr_match = a; break; }
+        }
+        FILE *dump_cnt = NULL;
+        char cname[MAX_CHR_NAME_LEN + 1];
+        snprintf(cname, sizeof(cname), "%.*s", g_chr_names_len[fmatch], g_chr_names[fmatch]);
+        if (g_dump_prefix) {
+            char path[4096];
+            snprintf(path, sizeof(path), "%s.%s.cnt", g_dump_prefix, cname);
+            dump_cnt = fopen(path, "wb");
+        }
+        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, dump_cnt);
+        if (dump_cnt) fclose(dump_cnt);
+    }
+    bam_free_rec(&cur.b);
+    stream_close(&st);
+    free(chr_fasta);
+    fclose(vcf);
+    if (ctx) {
+        /* CTX post-pass of main (GROM.c:22400-22770) rewrites the file with the
+         * header; with no CTX rows that is the header alone. */
+        if (g_vcf == 1) write_header(ctx, fasta_file_name, 1);
+        fclose(ctx);
+    }
+    fclose(fasta);
+    return 0;
+}
+
+/* test hook: the two binomial tables exactly as a run with -q min_mapq uses them */
+void grom_oracle_tables(int min_mapq, double *mq_out, double *hez_out) {
+    g_min_mapq = min_mapq;
+    calculate_normal_binom_constants();
+    build_binom_tables();
+    memcpy(mq_out, g_mq_table, sizeof(g_mq_table));
+    memcpy(hez_out, g_hez_table, sizeof(g_hez_table));
+}
+
+#ifdef GROM_ORACLE_MAIN
+int main(int argc, char **argv) {
+    const char *dump = getenv("GROM_ORACLE_DUMP");
+    return grom_oracle_main(argc, argv, dump);
+}
+#endif

@@ -1,0 +1,46 @@
+/*
+ * grom_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of GROM v1.0.1's per-chromosome scan (GROM.c), used by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * checker.  It is never linked into, called by or shipped with the product
+ * path (grom_amd/).  See oracle/README.md for its pinning status.
+ */
+#ifndef GROM_ORACLE_H
+#define GROM_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Per-position counters, in the order the reference declares them
+ * (GROM.c:2923-3680).  `rd` is cdp_one_base_rd. */
+typedef struct orc_counts {
+    int32_t pos;
+    int32_t snv[4], snv_lowmq[4];
+    int32_t bq, bq_all, mq, mq_all, bq_rc, mq_rc, rc_all;
+    int32_t pir[4], fs[4];
+    int32_t rd;
+    int32_t sc_left, sc_right, sc_left_rd, sc_right_rd, sc_rd;
+    int32_t ctx_sc_left, ctx_sc_right, ctx_sc_left_rd, ctx_sc_right_rd, ctx_sc_rd;
+    int32_t indel_sc_left, indel_sc_right, indel_sc_left_rd, indel_sc_right_rd, indel_sc_rd;
+} orc_counts;
+
+/* Run the reference CLI semantics: argv as for GROM (-i -r -o ...).
+ * If dump_prefix is non-NULL, for every processed chromosome the counters of
+ * every evaluated base (p > 2*insert_max, GROM.c:11086) are written to
+ * <dump_prefix>.<chrname>.cnt as packed orc_counts records, and the caf read
+ * depth arrays to <dump_prefix>.<chrname>.caf (3 x int32 x chr_len).
+ * Returns the process exit code the reference would return. */
+int grom_oracle_main(int argc, char **argv, const char *dump_prefix);
+
+/* The mq and hez binomial tables (1001 x 1001 doubles each, row-major) as a
+ * run with `-q min_mapq` uses them, i.e. after the "%e" text round trip. */
+void grom_oracle_tables(int min_mapq, double *mq_out, double *hez_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

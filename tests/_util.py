@@ -1,0 +1,65 @@
+"""Test helpers: synthetic datasets, the oracle (CPU restatement) and the product CLI."""
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_BIN = os.path.join(REPO, "oracle", "grom_oracle")
+ORACLE_LIB = os.path.join(REPO, "oracle", "liboracle.so")
+GROM_BIN = os.path.join(REPO, "grom_amd", "bin", "grom")
+SYNTH_BIN = os.path.join(REPO, "grom_amd", "bin", "grom_synth")
+GOLDEN_VCF = os.path.join(REPO, "tests", "golden", "tilapia_v1.0.0.vcf")
+GOLDEN_CTX = os.path.join(REPO, "tests", "golden", "tilapia_v1.0.0.ctx.vcf")
+NCOUNT = 40
+FILEDATE = "20260101"
+
+# synthetic parity cases: name -> grom_synth arguments
+CASES = {
+    "one_chr": ["-L", "400000", "-s", "11"],
+    "three_chr": ["-L", "250000,180000,220000", "-s", "12"],
+    "lowmapq_clip": ["-L", "300000", "-s", "13", "-Q", "0.2", "-C", "0.08", "-q", "0.1", "-U", "0.01"],
+    "dups": ["-L", "300000", "-s", "14", "-D", "0.15"],
+    "empty_middle": ["-L", "200000,200000,200000", "-s", "15", "-c", "30,0,30"],
+}
+
+
+def synth(datadir, name, args):
+    prefix = os.path.join(str(datadir), name)
+    bam = prefix + ".bam"
+    if not os.path.exists(bam):
+        r = subprocess.run([SYNTH_BIN, "-o", prefix] + list(args), capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+    return bam, prefix + ".fa"
+
+
+def run(binary, args, cwd, env_extra=None):
+    env = dict(os.environ)
+    env["GROM_FILEDATE"] = FILEDATE
+    if env_extra:
+        env.update(env_extra)
+    r = subprocess.run([binary] + list(args), cwd=cwd, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, f"{binary} failed: {r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    return r
+
+
+def run_oracle(datadir, bam, fa, out, extra=(), dump=None):
+    env = {"GROM_ORACLE_DUMP": dump} if dump else None
+    return run(ORACLE_BIN, ["-i", bam, "-r", fa, "-o", out] + list(extra), str(datadir), env)
+
+
+def run_grom(datadir, bam, fa, out, extra=(), dump=None):
+    """The product CLI, called in this process through the C ABI so the HIP
+    library is loaded (and checked) by the test process itself."""
+    import grom_amd
+    env = {"GROM_FILEDATE": FILEDATE}
+    if dump:
+        env["GROM_DUMP"] = dump
+    rc = grom_amd.cli_main(["-i", bam, "-r", fa, "-o", out] + list(extra), env=env, cwd=str(datadir))
+    assert rc == 0, f"grom_cli_main returned {rc}: {grom_amd.last_error()}"
+    return rc
+
+
+def load_counts(path):
+    a = np.fromfile(path, dtype=np.int32)
+    return a.reshape(-1, NCOUNT)

@@ -1,0 +1,90 @@
+"""CPU tests of the host side: the C ABI library, the serial-stream planner and
+the generator.  No GPU calls."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from _util import CASES, REPO, synth, run, run_oracle, GROM_BIN
+
+HEADER = os.path.join(REPO, "include", "grom_amd.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w \*]*?\b(grom_\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    import grom_amd
+    lib = grom_amd.lib()
+    names = declared_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.grom_abi_version() == 1
+    # and the python binding declares a signature for each
+    assert set(names) <= set(grom_amd._SIGS), set(names) - set(grom_amd._SIGS)
+
+
+def test_device_calls_fail_loudly_without_device():
+    import grom_amd
+    p = grom_amd.default_params()
+    lib = grom_amd.lib()
+    rc = lib.grom_scan_chrom(0, None, None, None, None)
+    assert rc != 0  # device 0 never initialised in this process
+
+
+def test_generator_is_deterministic(datadir, tmp_path):
+    a, _ = synth(datadir, "one_chr", CASES["one_chr"])
+    b, _ = synth(tmp_path, "one_chr", CASES["one_chr"])
+    assert open(a, "rb").read() == open(b, "rb").read()
+
+
+def parse_plan(stdout):
+    out = {}
+    for line in stdout.splitlines():
+        if line.startswith("plan "):
+            f = line.split()
+            kv = dict(x.split("=") for x in f[2:])
+            out[f[1]] = {k: int(v) for k, v in kv.items()}
+    return out
+
+
+def parse_meta(path):
+    d = {}
+    for line in open(path):
+        k, v = line.split()
+        d[k] = int(v)
+    return d
+
+
+@pytest.mark.parametrize("case", ["one_chr", "three_chr", "empty_middle", "lowmapq_clip"])
+def test_stream_plan_matches_oracle_walk(datadir, case):
+    """The per-chromosome record plan (skip prefix, last base reached) equals what
+    the oracle's serial walk did, including the two records lost at every
+    chromosome boundary (Q1) and the empty chromosome swallowing the file (Q21)."""
+    bam, fa = synth(datadir, case, CASES[case])
+    dump = str(datadir / f"plan_{case}")
+    run_oracle(datadir, bam, fa, f"plan_{case}.vcf", dump=dump)
+    r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", f"plan_{case}_g.vcf"], str(datadir), {"GROM_PLAN_ONLY": "1"})
+    plan = parse_plan(r.stdout)
+    assert plan, r.stdout
+    for name, p in plan.items():
+        meta = parse_meta(f"{dump}.{name}.meta")
+        assert p["n_skip"] == meta["n_skip"], (name, p, meta)
+        if p["p_last"] >= 0:
+            assert p["p_last"] + 1 == meta["p_end"], (name, p, meta)
+        else:
+            assert meta["n_ingested"] == 0
+
+
+def test_q21_empty_chromosome_starves_later_ones(datadir):
+    bam, fa = synth(datadir, "empty_middle", CASES["empty_middle"])
+    r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "q21.vcf"], str(datadir), {"GROM_PLAN_ONLY": "1"})
+    plan = parse_plan(r.stdout)
+    assert plan["chr1"]["reads"] > 0
+    assert plan["chr2"]["reads"] == 0 and plan["chr3"]["reads"] == 0
