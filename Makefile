@@ -4,7 +4,7 @@ HIPCC   ?= /opt/rocm/bin/hipcc
 CC      ?= gcc
 ARCH    ?= gfx950
 CFLAGS  ?= -O2 -g -Wall -Wno-alloc-size-larger-than -fPIC
-HIPFLAGS ?= -O3 -g --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall
+HIPFLAGS ?= -O3 -g --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -pthread
 LIBDIR  = grom_amd/lib
 BINDIR  = grom_amd/bin
 

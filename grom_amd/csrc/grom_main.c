@@ -199,7 +199,7 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
 }
 
 int grom_cli_main(int argc, char **argv) {
-    optind = 1; /* callable more than once per process */
+    optind = 0; /* GNU getopt: 0 fully re-initialises, so this is callable again */
     setlinebuf(stdout);
     grom_params P;
     grom_default_params(&P);

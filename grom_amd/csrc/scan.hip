@@ -7,16 +7,16 @@
 // (GROM.c:11086-13553).  Here the chromosome is cut into tiles of GROM_TILE
 // absolute positions; one workgroup owns a tile and builds every counter of
 // its positions in LDS from all reads overlapping it, then evaluates them.
-// Counters that are plain sums are accumulated with LDS atomics in any order;
-// the order-dependent step -- read-name de-duplication of mismatching bases
-// (GROM.c:6805-6824) -- is turned into an event list that is sorted by read
-// order per position and folded by the position's owning thread.
+// Each lane owns one position and folds the tile's reads into registers in
+// read order, which is the order the reference's ring sees them, so even the
+// order-dependent read-name de-duplication of mismatching bases
+// (GROM.c:6805-6824) is a plain sequential fold (k_scan_tile.h).
 //
 // Kernels (one launch each per chromosome):
 //   k_span        longest reference extent of any read (tile halo)
 //   k_tile_ranges per-tile [first,last) read range, from the sorted positions
 //   k_rmdup       -M duplicate filter (GROM.c:6432-6588), per start position
-//   k_pileup      the tile kernel: caf read depth, SNV tally, soft-clip
+//   k_scan_tile   the tile kernel: caf read depth, SNV tally, soft-clip
 //                 evidence, physical read depth, SNV test, flush sums
 //   k_flush_sum   read-depth sum for mid-scan SNV list flushes (rare)
 
@@ -28,6 +28,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/grom_amd.h"
@@ -175,7 +177,7 @@ __global__ void k_rmdup(int64_t n, int32_t tid, const int32_t *__restrict__ pos,
 }
 
 // ---------------------------------------------------------------------------
-// k_pileup: the tile kernel
+// k_scan_tile: the tile kernel (k_scan_tile.h)
 // ---------------------------------------------------------------------------
 struct ReadArrays {
     const int32_t *pos;
@@ -205,444 +207,7 @@ struct PileOut {
     uint32_t *n_events;             // total events (stats)
 };
 
-// event word x: [0..9] position in tile, [10..12] kind, [13] forward strand,
-// [16..23] base quality, [24..31] MAPQ.  kind 0..3: mismatching A/C/G/T,
-// 4: mismatching non-ACGT, 5: left soft clip, 6: right soft clip.
-// y: read index.  z: read-name id (mismatch) or category bits | add<<8 (clip).
-// w: query offset of the base (mismatch).
-enum { EV_CLIP_L = 5, EV_CLIP_R = 6 };
-
-struct __align__(16) PileLds {
-    unsigned long long snvfs[4][T];  // lo32: cdp_one_base_snv, hi32: fstrand
-    unsigned long long bqmq_hi[T];   // lo32: bq, hi32: mq  (MAPQ >= q && BQ >= b)
-    unsigned long long bqmq_lo[T];   // lo32: bq, hi32: mq  (the other bases)
-    uint32_t lowmq[4][T];
-    uint32_t pir[4][T];
-    int32_t diff[4][T + 1];          // rd, caf_mq, caf_rd, caf_low difference arrays
-    uint4 ev[GROM_EVENT_CAP];
-    uint16_t ev_sorted[GROM_EVENT_CAP];
-    uint32_t ev_cnt[T];
-    uint32_t ev_fill[T];
-    char ref[T];
-    int32_t wsum[NWAVES][5];
-    unsigned long long red[NWAVES][2];
-    uint32_t nev;
-    int32_t r0, r1;
-};
-
-__device__ __forceinline__ void push_event(PileLds &L, uint4 e) {
-    uint32_t k = atomicAdd(&L.nev, 1u);
-    if (k < GROM_EVENT_CAP) L.ev[k] = e;
-}
-
-// inclusive scan of L.diff[0..3][0..T) and exclusive scan of L.ev_cnt,
-// 256 threads x 2 consecutive elements
-__device__ void tile_scans(PileLds &L) {
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    int32_t v[5][2], excl[5];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        v[k][0] = L.diff[k][2 * t];
-        v[k][1] = L.diff[k][2 * t + 1];
-    }
-    const int32_t c0 = (int32_t)L.ev_cnt[2 * t], c1 = (int32_t)L.ev_cnt[2 * t + 1];
-    v[4][0] = c0;
-    v[4][1] = c1;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        v[k][1] += v[k][0];
-        int32_t s = v[k][1];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            int32_t u = __shfl_up(s, o, 64);
-            if (lane >= o) s += u;
-        }
-        excl[k] = s - v[k][1];
-        if (lane == 63) L.wsum[w][k] = s;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        int32_t off = excl[k];
-        for (int ww = 0; ww < w; ww++) off += L.wsum[ww][k];
-        v[k][0] += off;
-        v[k][1] += off;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        L.diff[k][2 * t] = v[k][0];
-        L.diff[k][2 * t + 1] = v[k][1];
-    }
-    L.ev_cnt[2 * t] = (uint32_t)(v[4][0] - c0);
-    L.ev_cnt[2 * t + 1] = (uint32_t)(v[4][1] - c1);
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(NTHR) void k_pileup(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
-                                                  const int32_t *__restrict__ tile_lo,
-                                                  const int32_t *__restrict__ tile_hi, PileOut O,
-                                                  const double *__restrict__ mq_tab,
-                                                  const double *__restrict__ hez_tab) {
-    __shared__ PileLds L;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t t0 = (int64_t)blockIdx.x * T;
-
-    // ---- phase 0: clear, stage the reference tile ----
-    for (int i = tid; i < T; i += NTHR) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            L.snvfs[k][i] = 0;
-            L.lowmq[k][i] = 0;
-            L.pir[k][i] = 0;
-            L.diff[k][i] = 0;
-        }
-        L.bqmq_hi[i] = 0;
-        L.bqmq_lo[i] = 0;
-        L.ev_cnt[i] = 0;
-        L.ev_fill[i] = 0;
-        int64_t x = t0 + i;
-        L.ref[i] = (x < a.chr_len) ? upcase(ref[x]) : 'N';
-    }
-    if (tid < 4) L.diff[tid][T] = 0;
-    if (tid == 0) {
-        L.nev = 0;
-        L.r0 = tile_lo[blockIdx.x];
-        L.r1 = tile_hi[blockIdx.x];
-    }
-    __syncthreads();
-    const int32_t r0 = L.r0, r1 = L.r1;
-    // positions of this tile that are evaluated (GROM.c:11086, 5842)
-    const int64_t ev_lo = max((int64_t)a.eval_lo, t0), ev_hi = min((int64_t)a.eval_hi, t0 + T - 1);
-    const bool tile_evals = ev_lo <= ev_hi;
-
-    // ---- phase 1: every read overlapping the tile, one wave per read ----
-    for (int32_t r = r0 + wave; r < r1; r += NWAVES) {
-        const int32_t p0 = R.pos[r];
-        const uint16_t fl = R.flag[r];
-        const int mq = R.mapq[r];
-        if (R.keep && R.keep[r] == 0) continue;
-        const uint32_t c0 = R.cig_off[r], c1 = R.cig_off[r + 1];
-        const int64_t bo = R.base_off[r];
-        const int lq = R.lqseq[r];
-        const bool fwd = !(fl & 0x10);
-        const bool hq_read = mq >= a.min_mapq;
-        const int add = hq_read ? 6 : 0;  // cdp_add, GROM.c:5829-5836
-        const uint32_t nid = R.name_id[r];
-        const bool pos_ok = p0 >= 0 && p0 < a.chr_len;
-        int snv_base = 0, snv_ref_base = 0, lseq_mod = lq, end_adj_indel = 0;
-        int64_t caf_pos = p0;
-        int first_op = -1, first_len = 0, last_op = -1, last_len = 0;
-        const uint32_t ncap = (c1 - c0 > 1000u) ? c0 + 1000u : c1;  // cdp_c_type_len, GROM.c:6743
-        for (uint32_t k = c0; k < c1; k++) {
-            const uint32_t cg = R.cigar[k];
-            const int op = cg & 15;
-            const int len = (int)(cg >> 4);
-            const bool in_cap = k < ncap;
-            if (op == 0 || op == 7 || op == 8) {
-                // whole-chromosome read depth, GROM.c:6605-6671 (every op)
-                if (caf_pos >= 0 && caf_pos + len < a.chr_len) {
-                    int64_t lo = max(caf_pos, t0), hi = min(caf_pos + len, t0 + T);
-                    if (lo < hi && lane == 0) {
-                        atomicAdd(&L.diff[1][lo - t0], mq);
-                        atomicSub(&L.diff[1][hi - t0], mq);
-                        int which = (mq >= a.rd_min_mapq) ? 2 : 3;
-                        atomicAdd(&L.diff[which][lo - t0], 1);
-                        atomicSub(&L.diff[which][hi - t0], 1);
-                    }
-                }
-                caf_pos += len;
-                if (!in_cap) continue;
-                if (pos_ok) {
-                    // SNV tally, GROM.c:6769-7059
-                    const int64_t xb = (int64_t)p0 + snv_ref_base;
-                    const int loop_end = (xb + len >= a.chr_len) ? (int)(a.chr_len - p0) : len;
-                    int64_t blo = max((int64_t)0, max(ev_lo, t0) - xb);
-                    int64_t bhi = min((int64_t)loop_end, ev_hi + 1 - xb);
-                    if (tile_evals)
-                        for (int64_t b = blo + lane; b < bhi; b += 64) {
-                            const int64_t x = xb + b;
-                            const int xl = (int)(x - t0);
-                            const int qi = snv_base + (int)b;
-                            int q = 0, s4 = 15;
-                            if (qi < lq) {
-                                const int64_t nib = bo + qi;
-                                q = R.qual[nib];
-                                s4 = (R.seq[nib >> 1] >> ((~nib & 1) << 2)) & 15;
-                            }
-                            const char sb = c_nt16[s4];
-                            const int code = c_nt16_acgt[s4];
-                            const char rb = L.ref[xl];
-                            if (hq_read && q >= a.min_base_qual) {
-                                if (rb != sb) {
-                                    uint4 e;
-                                    e.x = (uint32_t)xl | ((uint32_t)code << 10) | ((uint32_t)fwd << 13) |
-                                          ((uint32_t)q << 16) | ((uint32_t)mq << 24);
-                                    e.y = (uint32_t)r;
-                                    e.z = nid;
-                                    e.w = (uint32_t)qi;
-                                    push_event(L, e);
-                                } else if (code < 4) {
-                                    atomicAdd(&L.snvfs[code][xl], 1ull | ((unsigned long long)fwd << 32));
-                                    atomicAdd(&L.bqmq_hi[xl], (unsigned long long)q | ((unsigned long long)mq << 32));
-                                    atomicAdd(&L.pir[code][xl], (uint32_t)(fwd ? qi : lseq_mod - qi));
-                                }
-                            } else if (code < 4) {
-                                atomicAdd(&L.lowmq[code][xl], 1u);
-                                atomicAdd(&L.bqmq_lo[xl], (unsigned long long)q | ((unsigned long long)mq << 32));
-                            }
-                        }
-                    snv_base += loop_end;
-                    snv_ref_base += loop_end;
-                }
-            } else if (op == 2) {
-                caf_pos += len;
-                if (!in_cap) continue;
-                snv_ref_base += len;
-                end_adj_indel -= len;
-            } else if (in_cap) {
-                if (op == 4) snv_base += len;
-                else if (op == 5) lseq_mod += len;
-                else if (op == 1) { snv_base += len; end_adj_indel += len; }
-                else if (op == 3) snv_ref_base += len;
-            } else {
-                continue;
-            }
-            if (first_op < 0) { first_op = op; first_len = len; }
-            last_op = op;
-            last_len = len;
-        }
-        // clip lengths and reference end, GROM.c:7067-7100
-        const int start_adj = (first_op == 4 || first_op == 5) ? first_len : 0;
-        const int end_adj = (last_op == 4 || last_op == 5) ? last_len : 0;
-        const int64_t E = (int64_t)p0 - start_adj + lseq_mod - end_adj - end_adj_indel;
-        // physical read depth over [pos, E), GROM.c:7173-7181
-        if (lane == 0 && E > p0) {
-            int64_t lo = max((int64_t)p0, t0), hi = min(E, t0 + T);
-            if (lo < hi) {
-                atomicAdd(&L.diff[0][lo - t0], 1);
-                atomicSub(&L.diff[0][hi - t0], 1);
-            }
-        }
-        // soft-clip evidence, GROM.c:7105-7169
-        if (lane == 0 && tile_evals) {
-            const bool paired = fl & 0x1, munmap = fl & 0x8, rev = fl & 0x10;
-            const int32_t mtid = R.mtid[r], mp = R.mpos[r], tl = R.isize[r];
-            // the read's own chromosome is the scanned one; its mate is on it iff mtid == tid
-            if (start_adj >= a.sc_min) {
-                const int64_t x = (int64_t)p0 - 1;
-                if (x >= ev_lo && x <= ev_hi) {
-                    const bool same_chr = (mtid == a.chr_tid);
-                    uint32_t cat = 0;
-                    if (!paired || (!rev && (munmap || (!munmap && same_chr && mp > p0)))) cat |= 1;
-                    if (paired && !munmap && !same_chr && rev) cat |= 2;
-                    if (paired && !munmap && same_chr && rev && abs(tl) <= a.insert_max && mp < p0) cat |= 4;
-                    if (cat) push_event(L, make_uint4((uint32_t)(x - t0) | ((uint32_t)EV_CLIP_L << 10), (uint32_t)r,
-                                                      cat | ((uint32_t)add << 8), 0));
-                }
-            }
-            if (end_adj >= a.sc_min) {
-                const int64_t x = E;
-                if (x >= ev_lo && x <= ev_hi) {
-                    const bool same_chr = (mtid == a.chr_tid);
-                    uint32_t cat = 0;
-                    if (!paired || (rev && (munmap || (!munmap && same_chr && mp < p0)))) cat |= 1;
-                    if (paired && !munmap && !same_chr && !rev) cat |= 2;
-                    if (paired && !munmap && same_chr && !rev && abs(tl) <= a.insert_max && mp > p0) cat |= 4;
-                    if (cat) push_event(L, make_uint4((uint32_t)(x - t0) | ((uint32_t)EV_CLIP_R << 10), (uint32_t)r,
-                                                      cat | ((uint32_t)add << 8), 0));
-                }
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- phase 2: bucket events by position ----
-    const uint32_t nev = L.nev;
-    if (nev > GROM_EVENT_CAP) {
-        if (tid == 0) {
-            if (atomicAdd(&O.status[0], 1u) == 0) O.status[1] = blockIdx.x;
-        }
-        return;  // whole block exits together; the host reports the overflow
-    }
-    if (tid == 0) atomicAdd(O.n_events, nev);
-    for (uint32_t e = tid; e < nev; e += NTHR) atomicAdd(&L.ev_cnt[L.ev[e].x & 1023], 1u);
-    __syncthreads();
-    tile_scans(L);
-    for (uint32_t e = tid; e < nev; e += NTHR) {
-        const uint32_t xl = L.ev[e].x & 1023;
-        const uint32_t s = atomicAdd(&L.ev_fill[xl], 1u);
-        L.ev_sorted[L.ev_cnt[xl] + s] = (uint16_t)e;
-    }
-    __syncthreads();
-
-    // ---- phase 3: per position fold, evaluation, outputs ----
-    unsigned long long fsum = 0, fcnt = 0;
-    for (int xl = tid; xl < T; xl += NTHR) {
-        const int64_t x = t0 + xl;
-        if (x >= a.chr_len) break;
-        const int32_t rd = L.diff[0][xl];
-        O.caf_mq[x] = L.diff[1][xl];
-        O.caf_rd[x] = L.diff[2][xl];
-        O.caf_low[x] = L.diff[3][xl];
-        const char rb = L.ref[xl];
-        if (x < a.flush_end && rb != 'N') {
-            fsum += (unsigned long long)((int64_t)L.diff[2][xl] + (int64_t)L.diff[3][xl]);
-            fcnt += 1;
-        }
-        if (x < ev_lo || x > ev_hi) continue;
-        // fold this position's events in read order
-        const uint32_t es = L.ev_cnt[xl], en = L.ev_fill[xl];
-        uint16_t *seg = &L.ev_sorted[es];
-        for (uint32_t i = 1; i < en; i++) {  // insertion sort by (read, kind)
-            uint16_t v = seg[i];
-            unsigned long long kv = ((unsigned long long)L.ev[v].y << 8) | ((L.ev[v].x >> 10) & 7);
-            uint32_t j = i;
-            while (j > 0) {
-                uint16_t u = seg[j - 1];
-                unsigned long long ku = ((unsigned long long)L.ev[u].y << 8) | ((L.ev[u].x >> 10) & 7);
-                if (ku <= kv) break;
-                seg[j] = u;
-                j--;
-            }
-            seg[j] = v;
-        }
-        uint32_t slots[GROM_MAX_NAME_SLOTS];
-#pragma unroll
-        for (int k = 0; k < GROM_MAX_NAME_SLOTS; k++) slots[k] = 0;
-        int32_t sc[15];
-#pragma unroll
-        for (int k = 0; k < 15; k++) sc[k] = 0;
-        for (uint32_t i = 0; i < en; i++) {
-            const uint4 e = L.ev[seg[i]];
-            const int kind = (e.x >> 10) & 7;
-            if (kind <= 4) {
-                // read-name slots, GROM.c:6805-6824
-                bool found = false;
-                for (int k = 0; k < a.min_snv; k++) {
-                    if (slots[k] == 0) {
-                        if (e.z != 0) slots[k] = e.z;
-                        break;
-                    } else if (slots[k] == e.z) {
-                        found = true;
-                        break;
-                    }
-                }
-                if (found || kind == 4) continue;
-                const uint32_t fw = (e.x >> 13) & 1, q = (e.x >> 16) & 255, m = e.x >> 24;
-                L.snvfs[kind][xl] += 1ull | ((unsigned long long)fw << 32);
-                L.bqmq_hi[xl] += (unsigned long long)q | ((unsigned long long)m << 32);
-                L.pir[kind][xl] += e.w;  // mismatches add the query offset on both strands (GROM.c:6896)
-            } else {
-                const uint32_t cat = e.z & 7;
-                const int32_t ad = (int32_t)(e.z >> 8);
-                const int base = (kind == EV_CLIP_L) ? 0 : 1;  // left / right
-                for (int c = 0; c < 3; c++)
-                    if (cat & (1u << c)) {
-                        sc[c * 5 + base] += ad;       // sc_left / sc_right
-                        sc[c * 5 + 2 + base] += 1;    // *_left_rd / *_right_rd
-                        sc[c * 5 + 4] += 1;           // *_sc_rd
-                    }
-            }
-        }
-        int32_t snv[4], fs[4], low[4], pir[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            snv[k] = (int32_t)(L.snvfs[k][xl] & 0xffffffffu);
-            fs[k] = (int32_t)(L.snvfs[k][xl] >> 32);
-            low[k] = (int32_t)L.lowmq[k][xl];
-            pir[k] = (int32_t)L.pir[k][xl];
-        }
-        const int32_t bq_hi = (int32_t)(L.bqmq_hi[xl] & 0xffffffffu), mq_hi = (int32_t)(L.bqmq_hi[xl] >> 32);
-        const int32_t bq_lo = (int32_t)(L.bqmq_lo[xl] & 0xffffffffu), mq_lo = (int32_t)(L.bqmq_lo[xl] >> 32);
-        const int32_t total = snv[0] + snv[1] + snv[2] + snv[3];
-        const int32_t rc_all = total + low[0] + low[1] + low[2] + low[3];
-        const int32_t bq_all = bq_hi + bq_lo, mq_all = mq_hi + mq_lo;
-        if (O.dbg) {
-            int32_t *d = O.dbg + (size_t)(x - a.eval_lo) * GC_COUNT;
-            d[GC_POS] = (int32_t)x;
-            for (int k = 0; k < 4; k++) {
-                d[GC_SNV + k] = snv[k];
-                d[GC_SNV_LOWMQ + k] = low[k];
-                d[GC_PIR + k] = pir[k];
-                d[GC_FS + k] = fs[k];
-            }
-            d[GC_BQ] = bq_hi;
-            d[GC_BQ_ALL] = bq_all;
-            d[GC_MQ] = mq_hi;
-            d[GC_MQ_ALL] = mq_all;
-            d[GC_BQ_RC] = total;
-            d[GC_MQ_RC] = total;
-            d[GC_RC_ALL] = rc_all;
-            d[GC_RD] = rd;
-            for (int k = 0; k < 15; k++) d[GC_SC_LEFT + k] = sc[k];
-        }
-        // SNV test, GROM.c:11096-11199
-        if (rd + sc[14] <= 0 || rb == 'N') continue;
-        int best = -1;
-        float best_ratio = 0.f;
-        for (int k = 0; k < 4; k++) {
-            const float ratio = (float)snv[k] / (float)total;
-            if (rb != c_acgt[k] && (double)ratio >= a.min_snv_ratio && snv[k] >= a.min_snv &&
-                (double)bq_all / (double)rc_all >= a.min_ave_bq) {
-                if (best < 0 || ratio > best_ratio) {
-                    best = k;
-                    best_ratio = ratio;
-                }
-            }
-        }
-        if (best < 0) continue;
-        const uint32_t ci = atomicAdd(O.n_cands, 1u);
-        if (ci >= O.cand_cap) continue;  // host sees n_cands > cap and re-runs with room
-        grom_snv_cand c;
-        c.pos = (int32_t)x;
-        c.base = best;
-        c.ratio = best_ratio;
-        c.ref_base = (int32_t)(unsigned char)ref[x];
-        size_t ti = (total > GROM_MAX_TRIALS)
-                        ? (size_t)GROM_MAX_TRIALS * (GROM_MAX_TRIALS + 1) + snv[best] * GROM_MAX_TRIALS / total
-                        : (size_t)total * (GROM_MAX_TRIALS + 1) + snv[best];
-        c.binom = mq_tab[ti];
-        c.hez = hez_tab[ti];
-        for (int k = 0; k < 4; k++) {
-            c.snv[k] = snv[k];
-            c.lowmq[k] = low[k];
-            c.pir[k] = pir[k];
-            c.fs[k] = fs[k];
-        }
-        c.bq = bq_hi;
-        c.bq_all = bq_all;
-        c.mq = mq_hi;
-        c.mq_all = mq_all;
-        c.bq_rc = total;
-        c.mq_rc = total;
-        c.rc_all = rc_all;
-        c.pad1 = 0;
-        O.cands[ci] = c;
-    }
-    // flush-range read-depth sums (GROM.c:15066-15073)
-    for (int o = 32; o > 0; o >>= 1) {
-        fsum += __shfl_xor(fsum, o, 64);
-        fcnt += __shfl_xor(fcnt, o, 64);
-    }
-    if (lane == 0) {
-        L.red[wave][0] = fsum;
-        L.red[wave][1] = fcnt;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long s = 0, c = 0;
-        for (int w = 0; w < NWAVES; w++) {
-            s += L.red[w][0];
-            c += L.red[w][1];
-        }
-        if (c) {
-            atomicAdd(&O.flush_acc[0], s);
-            atomicAdd(&O.flush_acc[1], c);
-        }
-    }
-}
+#include "k_scan_tile.h"
 
 // sums of caf_rd + caf_low over non-N bases of [0, e) for mid-scan flushes
 __global__ void k_flush_sum(int64_t e, const char *__restrict__ ref, const int32_t *__restrict__ rd,
@@ -737,12 +302,11 @@ struct Text {
 };
 
 // SNV rows of one list flush (GROM.c:11203-11274 mid-scan, 15063-15107 final)
-static void snv_rows(const grom_params &P, const grom_chrom *ch, const grom_snv_cand *c, size_t n, double ave_rd,
-                     Text &out) {
+static void snv_rows_range(const grom_params &P, const char *name, const grom_snv_cand *c, size_t lo, size_t hi,
+                           double lim, std::string &out) {
     static const char dna[4] = {'A', 'C', 'G', 'T'};
     char line[1024], gt[128];
-    const double lim = round(P.snv_rd_min_factor * ave_rd);
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = lo; i < hi; i++) {
         const grom_snv_cand &s = c[i];
         const double ratio = (double)s.ratio;
         if (!(s.rc_all <= lim || ratio >= P.high_cov_min_snv_ratio)) continue;
@@ -756,12 +320,30 @@ static void snv_rows(const grom_params &P, const grom_chrom *ch, const grom_snv_
         int w = snprintf(line, sizeof(line),
                          "%s\t%d\t\t%c\t%c\t.\t.\t.\tGT:PR:AF:A:C:G:T:AL:CL:GL:TL:BQ:MQ:PIR:FS\t%s:%e:%e:%d:%d:%d:%d:%d:%d:%d:"
                          "%d:%.2f:%.2f:%.2f:%.2f\n",
-                         ch->name, s.pos + 1, (char)s.ref_base, dna[b], gt, s.binom, ratio, s.snv[0], s.snv[1], s.snv[2],
+                         name, s.pos + 1, (char)s.ref_base, dna[b], gt, s.binom, ratio, s.snv[0], s.snv[1], s.snv[2],
                          s.snv[3], s.lowmq[0], s.lowmq[1], s.lowmq[2], s.lowmq[3],
                          (double)s.bq_all / (double)s.rc_all, (double)s.mq_all / (double)s.rc_all,
                          (double)s.pir[b] / (double)s.snv[b], (double)s.fs[b] / (double)s.snv[b]);
-        out.add(line, (size_t)w);
+        out.append(line, (size_t)w);
     }
+}
+
+// rows of one flush; large lists are formatted by host threads in parallel
+// (printf's %e/%.2f conversions are the host's cost) and joined in order
+static void snv_rows(const grom_params &P, const grom_chrom *ch, const grom_snv_cand *c, size_t n, double ave_rd,
+                     Text &out) {
+    const double lim = round(P.snv_rd_min_factor * ave_rd);
+    unsigned nt = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < 8192) nt = 1;
+    std::vector<std::string> parts(nt);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++) {
+        size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+        if (nt == 1) snv_rows_range(P, ch->name, c, lo, hi, lim, parts[t]);
+        else th.emplace_back(snv_rows_range, std::cref(P), ch->name, c, lo, hi, lim, std::ref(parts[t]));
+    }
+    for (auto &t : th) t.join();
+    for (auto &s : parts) out.add(s.data(), s.size());
 }
 
 static int check_params(const grom_params &p) {
@@ -874,7 +456,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                    (grom_snv_cand *)C.cands.p, d_ncand, cand_cap, d_facc,
                    want_dbg ? (int32_t *)C.dbg.p : nullptr, d_status, d_nev};
         HIPCHK(hipEventRecord(C.ep0, st));
-        hipLaunchKernelGGL(k_pileup, dim3((unsigned)n_tiles), dim3(NTHR), 0, st, a, ch->ref, ra,
+        hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)n_tiles), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
                            (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(C.ep1, st));

@@ -7,7 +7,7 @@
 #include <stdint.h>
 
 /* positions per tile of the pileup kernel and threads per tile */
-#define GROM_TILE 512
+#define GROM_TILE 256
 #define GROM_TILE_THREADS 256
 /* per-tile LDS event capacity (mismatches needing read-name de-duplication
  * plus soft-clip evidence); overflow is reported, never silently dropped */

@@ -974,7 +974,7 @@ static void write_header(FILE *f, const char *fasta_file_name, int ctx) {
 int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
     g_dump_prefix = dump_prefix;
     const char *bam_file_name = NULL, *fasta_file_name = NULL, *results_file_name = NULL;
-    optind = 1;
+    optind = 0; /* GNU getopt: full re-initialisation */
     int opt;
     /* getopt string of GROM.c:21908 */
     while ((opt = getopt(argc, argv,
