@@ -56,18 +56,7 @@ static void set_err(const char *fmt, ...) {
         }                                                                                       \
     } while (0)
 
-// htslib bam_nt16_rev_table
-__constant__ char c_nt16[16] = {'=', 'A', 'C', 'M', 'G', 'R', 'S', 'V', 'T', 'W', 'Y', 'H', 'K', 'D', 'B', 'N'};
-// 4-bit code -> index into "ACGT", 4 for anything else
-__constant__ int8_t c_nt16_acgt[16] = {4, 0, 1, 4, 2, 4, 4, 4, 3, 4, 4, 4, 4, 4, 4, 4};
-__constant__ char c_acgt[4] = {'A', 'C', 'G', 'T'};
-
-__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
-    int64_t q = a / b;
-    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
-}
-
-__device__ __forceinline__ char upcase(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; }
+#include "device_common.h"
 
 // ---------------------------------------------------------------------------
 // k_span: reads' M/D/N/=/X extent; the tile halo
@@ -179,34 +168,6 @@ __global__ void k_rmdup(int64_t n, int32_t tid, const int32_t *__restrict__ pos,
 // ---------------------------------------------------------------------------
 // k_scan_tile: the tile kernel (k_scan_tile.h)
 // ---------------------------------------------------------------------------
-struct ReadArrays {
-    const int32_t *pos;
-    const uint16_t *flag;
-    const uint8_t *mapq;
-    const int32_t *mtid;
-    const int32_t *mpos;
-    const int32_t *isize;
-    const int32_t *lqseq;
-    const uint32_t *cig_off;
-    const uint32_t *cigar;
-    const int64_t *base_off;
-    const uint8_t *seq;
-    const uint8_t *qual;
-    const uint32_t *name_id;
-    const uint8_t *keep;  // nullable (-M off)
-};
-
-struct PileOut {
-    int32_t *caf_mq, *caf_rd, *caf_low;
-    grom_snv_cand *cands;
-    uint32_t *n_cands;
-    uint32_t cand_cap;
-    unsigned long long *flush_acc;  // [0] sum of caf rd, [1] non-N bases
-    int32_t *dbg;                   // nullable: GC_COUNT int32 per evaluated base
-    uint32_t *status;               // [0] event overflow count, [1] first overflowing tile
-    uint32_t *n_events;             // total events (stats)
-};
-
 #include "k_scan_tile.h"
 
 // sums of caf_rd + caf_low over non-N bases of [0, e) for mid-scan flushes
@@ -432,6 +393,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
 
     for (int attempt = 0; attempt < 2; attempt++) {
         if ((rc = ensure(C.cands, sizeof(grom_snv_cand) * (size_t)cand_cap))) return rc;
+        (void)hipGetLastError();  // drop any stale error of an earlier, reported failure
         HIPCHK(hipMemsetAsync(C.misc.p, 0, 128, st));
         HIPCHK(hipEventRecord(C.e0, st));
         if (n > 0) {
@@ -456,8 +418,9 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                    (grom_snv_cand *)C.cands.p, d_ncand, cand_cap, d_facc,
                    want_dbg ? (int32_t *)C.dbg.p : nullptr, d_status, d_nev};
         HIPCHK(hipEventRecord(C.ep0, st));
-        hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)n_tiles), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
-                           (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez);
+        hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)(((n_tiles + 7) / 8) * 8)), dim3(GROM_TILE), 0, st, a,
+                           ch->ref, ra, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez,
+                           n_tiles);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(C.ep1, st));
         uint32_t hdr[4];
@@ -550,10 +513,12 @@ static int upload(Ctx &C, const grom_chrom *ch, const grom_reads *h, grom_chrom 
     hipStream_t st = C.st;
     int rc;
     const int64_t n = h->n;
+    static const uint32_t zero_off[1] = {0};
+    const uint32_t *coff = (n > 0 && h->cigar_off) ? h->cigar_off : zero_off;  // an empty batch may hold no array
     if ((rc = up(C.r_pos, h->pos, n, st)) || (rc = up(C.r_flag, h->flag, n, st)) ||
         (rc = up(C.r_mapq, h->mapq, n, st)) || (rc = up(C.r_mtid, h->mtid, n, st)) ||
         (rc = up(C.r_mpos, h->mpos, n, st)) || (rc = up(C.r_isize, h->isize, n, st)) ||
-        (rc = up(C.r_lq, h->l_qseq, n, st)) || (rc = up(C.r_coff, h->cigar_off, n + 1, st)) ||
+        (rc = up(C.r_lq, h->l_qseq, n, st)) || (rc = up(C.r_coff, coff, n + 1, st)) ||
         (rc = up(C.r_cig, h->cigar, h->n_cigar_ops, st)) || (rc = up(C.r_boff, h->base_off, n, st)) ||
         (rc = up(C.r_seq, h->seq, (h->n_bases + 1) / 2, st)) || (rc = up(C.r_qual, h->qual, h->n_bases, st)) ||
         (rc = up(C.r_nid, h->name_id, n, st)) || (rc = up(C.ref, ch->ref, ch->len, st)))

@@ -150,7 +150,9 @@ void grom_dev_fini(int device);
 int grom_scan_chrom(int device, const grom_chrom *chrom, const grom_reads *reads, grom_out *out, grom_stats *stats);
 
 /* Same, with every grom_reads pointer (and chrom->ref) already in device
- * memory of `device`.  Used to time the scan with inputs resident in HBM. */
+ * memory of `device`.  Used to time the scan with inputs resident in HBM.
+ * qual and seq must be 4-byte aligned and readable 16 bytes past their end
+ * (the kernel copies them in 32-bit words); grom_upload guarantees both. */
 int grom_scan_chrom_device(int device, const grom_chrom *chrom, const grom_reads *dev_reads, grom_out *out,
                            grom_stats *stats);
 

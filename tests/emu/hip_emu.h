@@ -1,0 +1,124 @@
+// hip_emu.h -- TEST INFRASTRUCTURE ONLY.
+//
+// Runs the unmodified HIP sources of grom_amd (scan.hip and the kernels it
+// includes) on the host so kernels can be checked against the oracle -- and
+// under AddressSanitizer -- without a GPU.  A launch executes its blocks one
+// after another; each block runs blockDim host threads that meet at real
+// barriers for __syncthreads, so LDS (`__shared__`, here a static) is shared by
+// the block exactly as on the device.  Wave-level intrinsics assume the
+// wave-uniform control flow the kernels already guarantee.  Never linked into
+// the product library.
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <barrier>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __constant__ static const
+#define __launch_bounds__(...)
+#define __align__(n) alignas(n)
+#define __shared__ static
+
+struct dim3 {
+    unsigned x, y, z;
+    dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+struct emu_idx { unsigned x, y, z; };
+extern thread_local emu_idx threadIdx, blockIdx;
+extern emu_idx blockDim, gridDim;
+
+using std::max;
+using std::min;
+
+// ---- synchronisation within the emulated block ----
+struct emu_block_sync {
+    std::barrier<> *bar = nullptr;
+    std::atomic<int> count{0};
+    std::vector<unsigned long long> xch;
+};
+extern emu_block_sync *g_emu_sync;
+inline void __syncthreads() { g_emu_sync->bar->arrive_and_wait(); }
+inline int __syncthreads_count(int p) {
+    if (p) g_emu_sync->count.fetch_add(1);
+    g_emu_sync->bar->arrive_and_wait();
+    int v = g_emu_sync->count.load();
+    g_emu_sync->bar->arrive_and_wait();
+    if (threadIdx.x == 0) g_emu_sync->count.store(0);
+    g_emu_sync->bar->arrive_and_wait();
+    return v;
+}
+template <typename T>
+inline T __shfl_xor(T v, int off, int width = 64) {
+    (void)width;
+    unsigned t = threadIdx.x;
+    unsigned long long u = 0;
+    std::memcpy(&u, &v, sizeof(T));
+    g_emu_sync->xch[t] = u;
+    g_emu_sync->bar->arrive_and_wait();
+    unsigned long long r = g_emu_sync->xch[t ^ (unsigned)off];
+    g_emu_sync->bar->arrive_and_wait();
+    T out;
+    std::memcpy(&out, &r, sizeof(T));
+    return out;
+}
+inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
+
+// ---- atomics ----
+template <typename T, typename U>
+inline T atomicAdd(T *p, U v) { return __atomic_fetch_add(p, (T)v, __ATOMIC_SEQ_CST); }
+template <typename T, typename U>
+inline T atomicSub(T *p, U v) { return __atomic_fetch_sub(p, (T)v, __ATOMIC_SEQ_CST); }
+template <typename T, typename U>
+inline T atomicMax(T *p, U v) {
+    T old = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+    while (old < (T)v && !__atomic_compare_exchange_n(p, &old, (T)v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
+    }
+    return old;
+}
+
+// ---- runtime API subset used by scan.hip ----
+typedef int hipError_t;
+typedef void *hipStream_t;
+typedef void *hipEvent_t;
+enum { hipSuccess = 0, hipErrorInvalidValue = 1 };
+enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice };
+#define hipStreamNonBlocking 1
+inline const char *hipGetErrorString(hipError_t) { return "emulated error"; }
+inline hipError_t hipGetLastError() { return hipSuccess; }
+inline hipError_t hipSetDevice(int) { return hipSuccess; }
+inline hipError_t hipMalloc(void **p, size_t n) {
+    *p = std::malloc(n);
+    return *p ? hipSuccess : hipErrorInvalidValue;
+}
+template <typename T>
+inline hipError_t hipMalloc(T **p, size_t n) { return hipMalloc((void **)p, n); }
+inline hipError_t hipFree(void *p) { std::free(p); return hipSuccess; }
+inline hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) { std::memcpy(d, s, n); return hipSuccess; }
+inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t) {
+    return hipMemcpy(d, s, n, k);
+}
+inline hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t) { std::memset(d, v, n); return hipSuccess; }
+inline hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) { *s = (void *)1; return hipSuccess; }
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventCreate(hipEvent_t *e) { *e = (void *)1; return hipSuccess; }
+inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipEventElapsedTime(float *ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+
+void emu_run_grid(dim3 grid, dim3 block, const std::function<void()> &body);
+
+#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
+    emu_run_grid(dim3(grid), dim3(block), [=]() { kernel(__VA_ARGS__); })
