@@ -2,6 +2,7 @@
 # Everything is built in-tree so the .so files travel to the GPU box.
 HIPCC   ?= /opt/rocm/bin/hipcc
 CC      ?= gcc
+CXX     ?= g++
 ARCH    ?= gfx950
 CFLAGS  ?= -O2 -g -Wall -Wno-alloc-size-larger-than -fPIC
 HIPFLAGS ?= -O3 -g --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -pthread
@@ -9,8 +10,9 @@ LIBDIR  = grom_amd/lib
 BINDIR  = grom_amd/bin
 
 HOST_SRC = grom_amd/csrc/bamio.c grom_amd/csrc/stream.c grom_amd/csrc/tables.c grom_amd/csrc/synth.c grom_amd/csrc/hostapi.c grom_amd/csrc/grom_main.c
-HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC))
+HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC)) build/snvfmt.o
 HDRS = include/grom_amd.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h
+KHDRS = grom_amd/csrc/k_scan_tile.h grom_amd/csrc/device_common.h grom_amd/csrc/snvfmt.h
 
 all: $(LIBDIR)/libgrom_amd.so $(BINDIR)/grom $(BINDIR)/grom_synth oracle
 
@@ -18,7 +20,11 @@ build/%.o: grom_amd/csrc/%.c $(HDRS)
 	@mkdir -p build
 	$(CC) $(CFLAGS) -c $< -o $@
 
-build/scan.o: grom_amd/csrc/scan.hip $(HDRS)
+build/snvfmt.o: grom_amd/csrc/snvfmt.cpp grom_amd/csrc/snvfmt.h $(HDRS)
+	@mkdir -p build
+	$(CXX) -O2 -g -Wall -fPIC -std=c++17 -pthread -c $< -o $@
+
+build/scan.o: grom_amd/csrc/scan.hip $(HDRS) $(KHDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -37,8 +43,15 @@ $(BINDIR)/grom_synth: tools/grom_synth.c build/synth.o build/bamio.o
 oracle:
 	$(MAKE) -C oracle
 
+# kernel tuning variants, loaded with GROM_AMD_LIB=...:
+#   make variant V=w4 VFLAGS=-DGROM_WAVES_PER_EU=4  ->  build/variants/libgrom_amd_w4.so
+variant: $(HOST_OBJ)
+	@mkdir -p build/variants
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c grom_amd/csrc/scan.hip -o build/variants/scan_$(V).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o build/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o $(HOST_OBJ) -lz -lm
+
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle variant

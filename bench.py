@@ -8,7 +8,7 @@ GPU) every rank scans its own chromosome: chromosomes shard with no data-path
 collective, so scaling is weak and `value` is all bases scanned / max-rank time.
 
 The JSON line also carries
-  roofline      k_pileup's algorithmic bytes per launch / its mean duration
+  roofline      k_scan_tile's algorithmic bytes per launch / its mean duration
                 (HIP events on the library's stream) against 8 TB/s HBM,
                 with PMC-measured traffic when profiles/pmc_<tag>.json exists;
   cpu_baseline  the CPU restatement of the reference (oracle/, "port"), one
@@ -33,7 +33,7 @@ CPU_SAMPLE_LEN = 6_000_000
 
 
 def algorithmic_bytes(batch) -> int:
-    """Bytes k_pileup must move once per launch: every read record it ingests
+    """Bytes k_scan_tile must move once per launch: every read record it ingests
     (SoA metadata, CIGAR, packed bases, qualities), the reference, and the three
     whole-chromosome read-depth arrays it writes ('Roofline')."""
     r = batch.reads
@@ -120,7 +120,7 @@ def main():
     pmc = os.path.join(REPO, "profiles", f"pmc_{tag}.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("k_pileup_hbm_bytes_per_launch")
+            traffic = json.load(open(pmc)).get("k_scan_tile_hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -151,7 +151,7 @@ def main():
                 "host_generate_s": round(t_gen, 1),
             },
             "roofline": {
-                "bound": "hbm", "kernel": "k_pileup",
+                "bound": "hbm", "kernel": "k_scan_tile",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "bytes_per_launch": abytes, "launch_ms": round(pile_s * 1e3, 3),

@@ -15,7 +15,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(ROOT)
-LIB_PATH = os.path.join(ROOT, "lib", "libgrom_amd.so")
+# GROM_AMD_LIB selects another build of the same library (kernel tuning variants)
+LIB_PATH = os.environ.get("GROM_AMD_LIB") or os.path.join(ROOT, "lib", "libgrom_amd.so")
 GROM_BIN = os.path.join(ROOT, "bin", "grom")
 SYNTH_BIN = os.path.join(ROOT, "bin", "grom_synth")
 MAX_TRIALS = 1000
@@ -67,6 +68,7 @@ _SIGS = {
     "grom_default_params": (None, [C.POINTER(Params)]),
     "grom_params_set_insert": (None, [C.POINTER(Params), C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "grom_out_free": (None, [C.POINTER(Out)]),
+    "grom_fmt_selftest": (C.c_int64, [C.c_int64, C.c_uint64]),
     "grom_upload": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Chrom), C.POINTER(Reads)]),
     "grom_synth_batch": (C.c_void_p, [C.c_int64, C.c_double, C.c_int32, C.c_double, C.c_double, C.c_uint64,
                                       C.POINTER(Params)]),

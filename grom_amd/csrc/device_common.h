@@ -43,6 +43,7 @@ struct PileOut {
     grom_snv_cand *cands;
     uint32_t *n_cands;
     uint32_t cand_cap;
+    uint32_t *run_base, *run_cnt;  // per tile: first candidate slot, candidates
     unsigned long long *flush_acc;  // [0] sum of caf rd, [1] non-N bases
     int32_t *dbg;                   // nullable: GC_COUNT int32 per evaluated base
     uint32_t *status;               // reserved

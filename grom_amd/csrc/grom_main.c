@@ -324,6 +324,7 @@ int grom_cli_main(int argc, char **argv) {
         snprintf(ctx_name, sizeof(ctx_name), "%s.ctx", out_name);
 
     /* one serial pass over the records, split per chromosome (stream.h) */
+    bam_free_header(&hdr);
     if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) return 1;
     grom_planner pl;
     grom_planner_init(&pl, order, n_plan);

@@ -2,36 +2,85 @@
 //
 // One workgroup owns GROM_TILE consecutive reference positions and one thread
 // owns one position.  The reads that can touch the tile (sorted by position,
-// GROM's file order) are staged in LDS in chunks -- metadata, CIGAR words and
-// the contiguous run of their qualities and packed bases, copied with wide
-// coalesced loads -- and every wave then walks them in order while each lane
-// folds the read's contribution to *its* position into registers.  That
-// per-position, in-read-order fold is exactly the order in which the
-// reference's ring accumulates a base (GROM.c:6406-7185), so the
-// order-dependent read-name de-duplication of mismatching bases
-// (GROM.c:6805-6824) needs no sorting and no atomics, and every counter stays in
-// a register until the base is evaluated in place (GROM.c:11096-11199).
+// GROM's file order) are staged in LDS in chunks -- their packed metadata
+// records (k_prep), CIGAR words, and the contiguous run of their qualities and
+// packed bases, all copied with 16-byte loads issued together.  Each wave then
+// takes the chunk 64 reads at a time: lane j holds read j's record in
+// registers, a ballot picks the reads that touch the wave's 64 positions, and
+// the wave walks those in order with the record broadcast by v_readlane (no
+// LDS round trip per read) while each lane folds the read's contribution to
+// *its* position into registers.  That per-position, in-read-order fold is
+// exactly the order in which the reference's ring accumulates a base
+// (GROM.c:6406-7185), so the order-dependent read-name de-duplication of
+// mismatching bases (GROM.c:6805-6824) needs no sorting and no atomics, and
+// every counter stays in a register until the base is evaluated in place
+// (GROM.c:11096-11199).  Reads whose CIGAR is one M/=/X op (the common case)
+// take a fast path whose LDS base fetch is issued one read ahead.
 //
-// Tiles are mapped so that consecutive tiles run on one XCD (blocks are dealt
-// round-robin over the 8 XCDs): a read straddling two tiles is then fetched
-// from HBM once and served to the second tile from that XCD's L2.
+// Positions are int32 (BAM positions are; scan_device rejects longer
+// chromosomes).  Tiles are mapped so that consecutive tiles run on one XCD
+// (blocks are dealt round-robin over the 8 XCDs): a read straddling two tiles
+// is then fetched from HBM once and served to the second tile from that XCD's
+// L2.
 
 #define TG GROM_TILE
-#define RCHUNK 192
+#define RCHUNK 128
 #define CIGCAP 1024
-#define QBYTES 16384  // staged qualities per chunk (bytes)
+#define QBYTES 12288                 // staged qualities per chunk (bytes)
+#define QV (QBYTES / 16 + 2)          // uint4 slots for qualities
+#define SV (QBYTES / 32 + 2)          // uint4 slots for packed bases
+#define QLOADS ((QV + TG - 1) / TG)   // 16-byte loads per thread
+#define SLOADS ((SV + TG - 1) / TG)
+
+// Packed per-read record written by k_prep (3 x 16 bytes):
+//   a: pos, ext (one past the furthest position the read can touch), l_qseq, name id
+//   b: cigar offset, n_cigar | flag << 16, mapq | keep << 8, base offset (low 32)
+//   c: base offset (high 32), mate tid, mate pos, isize
+struct ReadMeta {
+    uint4 a, b, c;
+};
+
+// k_prep: one record per read, and the tile halo (max ext - pos)
+__global__ void k_prep(int64_t n, ReadArrays R, ReadMeta *__restrict__ meta, int32_t *__restrict__ halo) {
+    int32_t best = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t cb = R.cig_off[i], ce = R.cig_off[i + 1];
+        const int32_t p = R.pos[i], lq = R.lqseq[i];
+        // tally extent (M/D/N/=/X) or the clip / depth end
+        // E = pos - start_adj + lseq - end_adj - (I - D), whichever is larger
+        int32_t s = 0, e = lq;
+        for (uint32_t k = cb; k < ce; k++) {
+            const uint32_t cw = R.cigar[k];
+            const int op = cw & 15;
+            const int32_t len = (int32_t)(cw >> 4);
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) s += len;
+            if (op == 2 || op == 5) e += len;
+        }
+        const int32_t span = max(s, e) + 1;
+        best = max(best, span);
+        const int64_t bo = R.base_off[i];
+        const uint32_t keep = R.keep ? R.keep[i] : 1u;
+        ReadMeta m;
+        m.a = make_uint4((uint32_t)p, (uint32_t)(p + span), (uint32_t)lq, R.name_id[i]);
+        m.b = make_uint4(cb, (ce - cb) | ((uint32_t)R.flag[i] << 16), (uint32_t)R.mapq[i] | (keep << 8),
+                         (uint32_t)(bo & 0xffffffffu));
+        m.c = make_uint4((uint32_t)((uint64_t)bo >> 32), (uint32_t)R.mtid[i], (uint32_t)R.mpos[i],
+                         (uint32_t)R.isize[i]);
+        meta[i] = m;
+    }
+    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(halo, best);
+}
 
 struct __align__(16) ScanLds {
-    int64_t boff[RCHUNK];
-    int32_t pos[RCHUNK], lq[RCHUNK], ext[RCHUNK], mtid[RCHUNK], mpos[RCHUNK], isize[RCHUNK];
-    uint32_t coff[RCHUNK], cend[RCHUNK], nid[RCHUNK];
-    uint16_t flag[RCHUNK];
-    uint8_t mapq[RCHUNK], keep[RCHUNK];
+    ReadMeta meta[RCHUNK];
+    uint4 qual[QV];
+    uint4 seq[SV];
     uint32_t cig[CIGCAP];
-    uint32_t qual[QBYTES / 4 + 2];
-    uint32_t seq[QBYTES / 8 + 2];
     char ref[TG];
     unsigned long long red[TG / 64][2];
+    uint32_t wcnt[TG / 64];  // candidates per wave
+    uint32_t cbase;          // the tile's first candidate slot
     int32_t m2;  // reads of the chunk that fit the staging budgets
 };
 
@@ -41,50 +90,69 @@ struct LaneCounts {
     int32_t bq_hi, mq_hi, bq_lo, mq_lo;
 };
 
-#define GROM_ADD4(cnt, f, code, v)                    \
-    do {                                              \
-        cnt.f##0 += ((code) == 0) ? (v) : 0;          \
-        cnt.f##1 += ((code) == 1) ? (v) : 0;          \
-        cnt.f##2 += ((code) == 2) ? (v) : 0;          \
-        cnt.f##3 += ((code) == 3) ? (v) : 0;          \
+#define GROM_ADD4(cnt, f, code, v)           \
+    do {                                     \
+        cnt.f##0 += ((code) == 0) ? (v) : 0; \
+        cnt.f##1 += ((code) == 1) ? (v) : 0; \
+        cnt.f##2 += ((code) == 2) ? (v) : 0; \
+        cnt.f##3 += ((code) == 3) ? (v) : 0; \
     } while (0)
+
+// bases matching the reference base of the lane (the common case), counted
+// without selecting a counter by base code; folded into LaneCounts at the end
+struct MatchCounts {
+    int32_t cnt, fs, pir, low;
+};
+
+// 4-bit BAM code -> index into "ACGT" (A=1, C=2, G=4, T=8), 4 for anything else
+__device__ __forceinline__ int acgt_code(int s4) {
+    return (s4 != 0 && (s4 & (s4 - 1)) == 0) ? __builtin_ctz((unsigned)s4) : 4;
+}
 
 // one aligned base of a read at this lane's position: the SNV tally body of
 // GROM.c:6800-6992 (high-quality branch with read-name slots) and
-// GROM.c:6995-7040 (low-quality branch)
-__device__ __forceinline__ void tally_base(LaneCounts &c, uint32_t (&slot)[GROM_MAX_NAME_SLOTS], int min_snv,
-                                           bool hq, int q, int s4, char rb, bool fwd, int qi, int lseq_mod, int mq,
-                                           uint32_t nid) {
-    const char sb = c_nt16[s4];
-    const int code = c_nt16_acgt[s4];
-    // branch-free updates: every counter is touched with a 0/1 increment, so
-    // the counters stay in registers (no select of addresses)
+// GROM.c:6995-7040 (low-quality branch).  rb4 is the 4-bit code whose
+// character (bam_nt16_rev_table) equals the reference base, or 16 if none, so
+// `s4 == rb4` is the reference's `ref != read base` test negated; mv says the
+// reference base is one of ACGT.
+__device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, uint32_t (&slot)[GROM_MAX_NAME_SLOTS],
+                                           int min_snv, bool hq, bool mv, int q, int s4, int rb4, bool fwd, int qi,
+                                           int lseq_mod, int mq, uint32_t nid) {
+    if (s4 == rb4) {
+        const bool h = hq && mv, l = !hq && mv;
+        m.cnt += h ? 1 : 0;
+        m.fs += (h && fwd) ? 1 : 0;
+        m.pir += h ? (fwd ? qi : lseq_mod - qi) : 0;
+        m.low += l ? 1 : 0;
+        c.bq_hi += h ? q : 0;
+        c.mq_hi += h ? mq : 0;
+        c.bq_lo += l ? q : 0;
+        c.mq_lo += l ? mq : 0;
+        return;
+    }
+    const int code = acgt_code(s4);
     bool count = hq && code < 4;
-    int32_t pv = fwd ? qi : lseq_mod - qi;
-    {
-        if (hq && rb != sb) {
-            // first empty slot takes the name (names >= 50 chars are never
-            // stored); a slot holding the name marks the base as seen.  Written
-            // with selects so the slots stay in registers.
-            bool done = false, found = false;
+    if (hq) {
+        // first empty slot takes the name (names >= 50 chars are never
+        // stored); a slot holding the name marks the base as seen.  Written
+        // with selects so the slots stay in registers.
+        bool done = false, found = false;
 #pragma unroll
-            for (int s = 0; s < GROM_MAX_NAME_SLOTS; s++) {
-                const bool active = !done && s < min_snv;
-                const bool empty = active && slot[s] == 0;
-                const bool match = active && !empty && slot[s] == nid;
-                slot[s] = (empty && nid != 0) ? nid : slot[s];
-                found = found || match;
-                done = done || empty || match;
-            }
-            count = count && !found;
-            pv = qi;  // mismatches add the offset on both strands (GROM.c:6896)
+        for (int s = 0; s < GROM_MAX_NAME_SLOTS; s++) {
+            const bool active = !done && s < min_snv;
+            const bool empty = active && slot[s] == 0;
+            const bool match = active && !empty && slot[s] == nid;
+            slot[s] = (empty && nid != 0) ? nid : slot[s];
+            found = found || match;
+            done = done || empty || match;
         }
+        count = count && !found;
     }
     const bool low = !hq && code < 4;
     const int32_t ch = count ? 1 : 0, cl = low ? 1 : 0;
     GROM_ADD4(c, snv, code, ch);
     GROM_ADD4(c, fs, code, fwd ? ch : 0);
-    GROM_ADD4(c, pir, code, count ? pv : 0);
+    GROM_ADD4(c, pir, code, count ? qi : 0);  // mismatches add the offset on both strands (GROM.c:6896)
     GROM_ADD4(c, low, code, cl);
     c.bq_hi += count ? q : 0;
     c.mq_hi += count ? mq : 0;
@@ -92,33 +160,61 @@ __device__ __forceinline__ void tally_base(LaneCounts &c, uint32_t (&slot)[GROM_
     c.mq_lo += low ? mq : 0;
 }
 
-// a CIGAR word of the current chunk: from LDS when the chunk was staged,
-// else (a read too large to stage) from global memory
-__device__ __forceinline__ uint32_t cigar_word(const ScanLds &L, const ReadArrays &R, bool staged, uint32_t k,
-                                               uint32_t cf) {
-    uint32_t w;
-    if (staged) w = L.cig[k - cf];
-    else w = R.cigar[k];
-    return w;
+// lane i's value of v, as a wave-uniform (scalar) value
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, int i) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, i);
 }
 
-// quality and 4-bit base of global base offset `nib` (BAM nibble order)
-__device__ __forceinline__ void load_base(const ScanLds &L, const ReadArrays &R, bool staged, int64_t qb0,
-                                          int64_t sb0, int64_t nib, int &q, int &s4) {
-    uint32_t qv, sv;
-    if (staged) {
-        const int64_t qo = nib - qb0, so = (nib >> 1) - sb0;
-        qv = (L.qual[qo >> 2] >> ((qo & 3) * 8)) & 255u;
-        sv = (L.seq[so >> 2] >> ((so & 3) * 8)) & 255u;
-    } else {
-        qv = R.qual[nib];
-        sv = R.seq[nib >> 1];
-    }
-    q = (int)qv;
-    s4 = (int)((sv >> ((~nib & 1) << 2)) & 15u);
+// lane j's registers: read g + j of the chunk
+struct GroupRegs {
+    uint32_t p0, lq, nid, cb, nf, mk, bo, cw0;
+};
+
+// the scalar view of read g + i
+struct ReadView {
+    int32_t p0, lq, bo;  // bo: base offset relative to the staged window
+    uint32_t cw0, ncig, fl, mq, nid, cb;
+    int i;
+};
+
+__device__ __forceinline__ ReadView view_of(const GroupRegs &G, int i) {
+    ReadView v;
+    v.i = i;
+    v.p0 = (int32_t)lane_get(G.p0, i);
+    v.lq = (int32_t)lane_get(G.lq, i);
+    v.bo = (int32_t)lane_get(G.bo, i);
+    v.cw0 = lane_get(G.cw0, i);
+    const uint32_t nf = lane_get(G.nf, i);
+    v.ncig = nf & 0xffffu;
+    v.fl = nf >> 16;
+    v.mq = lane_get(G.mk, i) & 255u;
+    v.nid = lane_get(G.nid, i);
+    v.cb = lane_get(G.cb, i);
+    return v;
 }
 
-__global__ __launch_bounds__(TG) void k_scan_tile(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
+__device__ __forceinline__ bool fast_read(const ReadView &v) {
+    const uint32_t op = v.cw0 & 15u;
+    return v.ncig == 1 && (op == 0 || op == 7 || op == 8);
+}
+
+// quality byte and 4-bit base (BAM nibble order) of staged base `rel`
+// (relative to the window start, which is a multiple of 16)
+__device__ __forceinline__ void staged_base(const uint8_t *lq8, const uint8_t *ls8, int32_t soff, int32_t rel,
+                                            uint32_t &q, uint32_t &sbyte) {
+    q = lq8[rel];
+    sbyte = ls8[soff + (rel >> 1)];
+}
+
+// GROM_WAVES_PER_EU: occupancy target (register budget) for tuning builds
+#ifdef GROM_WAVES_PER_EU
+#define GROM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GROM_WAVES_PER_EU)))
+#else
+#define GROM_OCCUPANCY
+#endif
+
+__global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
+                                                  const ReadMeta *__restrict__ meta,
                                                   const int32_t *__restrict__ tile_lo,
                                                   const int32_t *__restrict__ tile_hi, PileOut O,
                                                   const double *__restrict__ mq_tab,
@@ -131,22 +227,33 @@ __global__ __launch_bounds__(TG) void k_scan_tile(grom_scan_args a, const char *
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t t0 = tile * TG;
-    const int64_t x = t0 + tid;         // this lane's reference position
-    const int64_t x0 = t0 + wave * 64;  // first position of this wave
+    const int32_t clen = (int32_t)a.chr_len;
+    const int32_t t0 = (int32_t)(tile * TG);
+    const int32_t x = t0 + tid;         // this lane's reference position
+    const int32_t x0 = t0 + wave * 64;  // first position of this wave
     const int32_t r0 = tile_lo[tile], r1 = tile_hi[tile];
-    L.ref[tid] = (x < a.chr_len) ? upcase(ref[x]) : 'N';
+    L.ref[tid] = (x < clen) ? upcase(ref[x]) : 'N';
     const char rb = L.ref[tid];
+    int rb4 = 16;  // the 4-bit code printed as rb (GROM compares characters)
+    for (int k = 0; k < 16; k++) rb4 = (c_nt16[k] == rb) ? k : rb4;
+    const int rcode = (rb4 < 16) ? acgt_code(rb4) : 4;
+    const bool mv = rcode < 4;
     const bool evals = x >= a.eval_lo && x <= a.eval_hi;  // GROM.c:11086, 5842
+    const uint8_t *lq8 = reinterpret_cast<const uint8_t *>(L.qual);
+    const uint8_t *ls8 = reinterpret_cast<const uint8_t *>(L.seq);
 
     LaneCounts c = {};
+    MatchCounts mc = {0, 0, 0, 0};
     int32_t rd = 0, caf_mq = 0, caf_rd = 0, caf_low = 0;
-    int32_t sc[15];
-#pragma unroll
-    for (int k = 0; k < 15; k++) sc[k] = 0;
+    // soft-clip evidence per category (plain, ctx, indel) x side (L, R):
+    // reads with mapq >= -q (each adds 6, GROM.c:5829-5836) and all reads
+    int32_t sch[6] = {0, 0, 0, 0, 0, 0}, scn[6] = {0, 0, 0, 0, 0, 0};
     uint32_t slot[GROM_MAX_NAME_SLOTS];
 #pragma unroll
     for (int k = 0; k < GROM_MAX_NAME_SLOTS; k++) slot[k] = 0;
+
+    const uint4 *gq4 = reinterpret_cast<const uint4 *>(R.qual);
+    const uint4 *gs4 = reinterpret_cast<const uint4 *>(R.seq);
 
     int32_t c0 = r0;
     while (c0 < r1) {
@@ -154,194 +261,246 @@ __global__ __launch_bounds__(TG) void k_scan_tile(grom_scan_args a, const char *
         __syncthreads();  // previous chunk fully consumed
         if (tid == 0) L.m2 = 0;
         __syncthreads();
-        // ---- stage metadata ----
-        bool fits = false;
+        // ---- stage the packed records; find the prefix within the budgets ----
         if (tid < m) {
-            const int32_t r = c0 + tid;
-            const uint32_t cb = R.cig_off[r], ce = R.cig_off[r + 1];
-            const int32_t p = R.pos[r], lq = R.lqseq[r];
-            const int64_t bo = R.base_off[r];
-            L.pos[tid] = p;
-            L.lq[tid] = lq;
-            L.coff[tid] = cb;
-            L.cend[tid] = ce;
-            L.boff[tid] = bo;
-            L.nid[tid] = R.name_id[r];
-            L.flag[tid] = R.flag[r];
-            L.mapq[tid] = R.mapq[r];
-            L.keep[tid] = R.keep ? R.keep[r] : 1;
-            L.mtid[tid] = R.mtid[r];
-            L.mpos[tid] = R.mpos[r];
-            L.isize[tid] = R.isize[r];
-            // furthest position the read can touch (tally extent, or the
-            // clip / depth end E = pos - start_adj + lseq - end_adj - (I - D))
-            int32_t s = 0, e = lq;
-            for (uint32_t k = cb; k < ce; k++) {
-                const uint32_t cw = R.cigar[k];
-                const int op = cw & 15;
-                const int32_t len = (int32_t)(cw >> 4);
-                if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) s += len;
-                if (op == 2 || op == 5) e += len;
-            }
-            L.ext[tid] = p + max(s, e) + 1;
-            // reads are contiguous in cigar[] and in qual/seq, so these budgets
-            // hold for a prefix of the chunk
-            fits = (bo + lq - R.base_off[c0]) <= (int64_t)QBYTES - 16 && ce - R.cig_off[c0] <= CIGCAP;
+            const ReadMeta rm = meta[c0 + tid];
+            L.meta[tid] = rm;
+            const ReadMeta f = meta[c0];
+            const int64_t bo = ((int64_t)rm.c.x << 32) | rm.b.w, b0 = ((int64_t)f.c.x << 32) | f.b.w;
+            const uint32_t ce = rm.b.x + (rm.b.y & 0xffffu);
+            // reads are contiguous in cigar[] and in qual/seq, so this holds
+            // for a prefix of the chunk
+            if (bo + (int32_t)rm.a.z - b0 <= (int64_t)QBYTES - 64 && ce - f.b.x <= CIGCAP) atomicMax(&L.m2, tid + 1);
         }
-        if (fits) atomicMax(&L.m2, tid + 1);
         __syncthreads();
         int32_t m2 = min(L.m2, m);
         const bool staged = m2 > 0;
         if (!staged) m2 = 1;  // one oversized read: served from global memory
-        const int64_t b0 = L.boff[0];
-        const uint32_t cf = L.coff[0], cl = L.cend[m2 - 1];
+        const ReadMeta &first = L.meta[0], &last = L.meta[m2 - 1];
+        const int64_t b0 = ((int64_t)first.c.x << 32) | first.b.w;
+        const int64_t bend = (((int64_t)last.c.x << 32) | last.b.w) + (int32_t)last.a.z;
+        const uint32_t cf = first.b.x, cl = last.b.x + (last.b.y & 0xffffu);
         // ---- stage CIGAR words, qualities and packed bases ----
-        const int64_t qw0 = b0 >> 2, sw0 = (b0 >> 1) >> 2;  // first qual / seq word
+        const int64_t qv0 = b0 >> 4, sv0 = b0 >> 5;  // first 16-byte slot of each
         if (staged) {
-            const int64_t bend = L.boff[m2 - 1] + L.lq[m2 - 1];
-            const int64_t qw1 = min((bend + 3) >> 2, qw0 + (int64_t)(QBYTES / 4 + 2));
-            const int64_t sw1 = min((((bend + 1) >> 1) + 3) >> 2, sw0 + (int64_t)(QBYTES / 8 + 2));
-            const uint32_t nc = min(cl - cf, (uint32_t)CIGCAP);  // guards only; the budget check implies them
+            const int64_t qv1 = min((bend + 15) >> 4, qv0 + (int64_t)QV);
+            const int64_t sv1 = min((((bend + 1) >> 1) + 15) >> 4, sv0 + (int64_t)SV);
+            uint4 vq[QLOADS], vs[SLOADS];
+            // clamped indices: every load is unconditional and all are in
+            // flight before the first LDS store
+#pragma unroll
+            for (int k = 0; k < QLOADS; k++) vq[k] = gq4[min(qv0 + tid + k * TG, qv1 - 1)];
+#pragma unroll
+            for (int k = 0; k < SLOADS; k++) vs[k] = gs4[min(sv0 + tid + k * TG, sv1 - 1)];
+            const uint32_t nc = min(cl - cf, (uint32_t)CIGCAP);
             for (uint32_t k = tid; k < nc; k += TG) L.cig[k] = R.cigar[cf + k];
-            const uint32_t *gq = (const uint32_t *)R.qual;
-            for (int64_t w = qw0 + tid; w < qw1; w += TG) L.qual[w - qw0] = gq[w];
-            const uint32_t *gs = (const uint32_t *)R.seq;
-            for (int64_t w = sw0 + tid; w < sw1; w += TG) L.seq[w - sw0] = gs[w];
+#pragma unroll
+            for (int k = 0; k < QLOADS; k++) {
+                const int64_t w = qv0 + tid + k * TG;
+                if (w < qv1) L.qual[w - qv0] = vq[k];
+            }
+#pragma unroll
+            for (int k = 0; k < SLOADS; k++) {
+                const int64_t w = sv0 + tid + k * TG;
+                if (w < sv1) L.seq[w - sv0] = vs[k];
+            }
         }
         __syncthreads();
-        const int64_t qb0 = qw0 << 2, sb0 = sw0 << 2;  // global byte offsets of L.qual[0] / L.seq[0]
+        // window: base qb0 + rel has its quality at L.qual byte rel and its
+        // packed base at L.seq byte soff + (rel >> 1) (qb0 is a multiple of 16)
+        const int64_t qb0 = qv0 << 4;
+        const int32_t soff = (int32_t)((qb0 >> 1) - (sv0 << 4));
 
-        for (int i = 0; i < m2; i++) {
-            const int32_t p0 = L.pos[i];
-            // wave-uniform overlap test with [x0, x0+64): contributions span
-            // [pos-1 (left clip), ext)
-            if (p0 - 1 > x0 + 63 || L.ext[i] < x0) continue;
-            if (L.keep[i] == 0) continue;  // -M duplicate (GROM.c:6590)
-            const uint16_t fl = L.flag[i];
-            const int mq = L.mapq[i];
-            const int lq = L.lq[i];
-            const int64_t bo = L.boff[i];
-            const uint32_t nid = L.nid[i];
-            const uint32_t cb = L.coff[i], ce = L.cend[i];
-            const bool fwd = !(fl & 0x10);
-            const bool hq_read = mq >= a.min_mapq;
-            const bool pos_ok = p0 >= 0 && p0 < a.chr_len;
-            const uint32_t cw0 = (ce > cb) ? cigar_word(L, R, staged, cb, cf) : 0u;
-            const int op0 = cw0 & 15;
-            if (ce - cb == 1 && (op0 == 0 || op0 == 7 || op0 == 8)) {
-                // ---- fast path: a single M/=/X op ----
-                const int len = (int)(cw0 >> 4);
-                if (p0 >= 0 && (int64_t)p0 + len < a.chr_len && x >= p0 && x < (int64_t)p0 + len) {
-                    caf_mq += mq;
-                    if (mq >= a.rd_min_mapq) caf_rd += 1;
-                    else caf_low += 1;
-                }
-                if (pos_ok && evals) {
-                    const int loop_end = ((int64_t)p0 + len >= a.chr_len) ? (int)(a.chr_len - p0) : len;
-                    if (x >= p0 && x < (int64_t)p0 + loop_end) {
-                        const int qi = (int)(x - p0);
-                        int q = 0, s4 = 15;
-                        if (qi < lq) load_base(L, R, staged, qb0, sb0, bo + qi, q, s4);
-                        tally_base(c, slot, a.min_snv, hq_read && q >= a.min_base_qual, q, s4, rb, fwd, qi, lq, mq,
-                                   nid);
-                    }
-                }
-                if (x >= p0 && x < (int64_t)p0 + lq) rd += 1;  // E = pos + l_qseq
-                continue;
+        for (int g = 0; g < m2; g += 64) {
+            // ---- lane j holds read g + j of the chunk ----
+            const int j = g + lane;
+            GroupRegs G = {0, 0, 0, 0, 0, 0, 0, 0};
+            bool rel = false;
+            if (j < m2) {
+                const ReadMeta rm = L.meta[j];
+                G.p0 = rm.a.x;
+                G.lq = rm.a.z;
+                G.nid = rm.a.w;
+                G.cb = rm.b.x;
+                G.nf = rm.b.y;
+                G.mk = rm.b.z;
+                G.bo = (uint32_t)((((int64_t)rm.c.x << 32) | rm.b.w) - qb0);
+                G.cw0 = (staged && (rm.b.y & 0xffffu) != 0) ? L.cig[rm.b.x - cf] : 0u;
+                // touches [x0, x0+64)?  contributions span [pos-1 (left clip), ext)
+                rel = ((rm.b.z >> 8) & 255u) != 0 &&  // -M duplicate (GROM.c:6590)
+                      (int32_t)rm.a.x - 1 <= x0 + 63 && (int32_t)rm.a.y > x0;
             }
-            // ---- general CIGAR walk ----
-            int snv_base = 0, srb = 0, lseq_mod = lq, eai = 0;
-            int64_t caf_pos = p0;
-            int first_op = -1, first_len = 0, last_op = -1, last_len = 0;
-            const uint32_t ncap = (ce - cb > 1000u) ? cb + 1000u : ce;  // GROM.c:6743
-            for (uint32_t k = cb; k < ce; k++) {
-                const uint32_t cg = cigar_word(L, R, staged, k, cf);
-                const int op = cg & 15;
-                const int len = (int)(cg >> 4);
-                const bool in_cap = k < ncap;
-                if (op == 0 || op == 7 || op == 8) {
-                    // whole-chromosome read depth, GROM.c:6605-6671 (all ops)
-                    if (caf_pos >= 0 && caf_pos + len < a.chr_len && x >= caf_pos && x < caf_pos + len) {
+            uint64_t mask = __ballot(rel);
+            if (!mask) continue;
+            ReadView v = view_of(G, __builtin_ctzll(mask));
+            // the fast path's quality / base of read v at this lane, fetched
+            // one read ahead (clamped to a valid LDS byte when unused)
+            uint32_t qn, sn;
+            {
+                const int32_t qi = x - v.p0;
+                const int32_t rr = (staged && (uint32_t)qi < (uint32_t)v.lq) ? v.bo + qi : 0;
+                staged_base(lq8, ls8, soff, rr, qn, sn);
+            }
+            while (true) {
+                const ReadView u = v;
+                const uint32_t qv = qn, sv = sn;
+                mask &= mask - 1;
+                if (mask) {
+                    v = view_of(G, __builtin_ctzll(mask));
+                    const int32_t qi = x - v.p0;
+                    const int32_t rr = (staged && (uint32_t)qi < (uint32_t)v.lq) ? v.bo + qi : 0;
+                    staged_base(lq8, ls8, soff, rr, qn, sn);
+                }
+                const int32_t p0 = u.p0;
+                const int mq = (int)u.mq;
+                const bool fwd = !(u.fl & 0x10);
+                const bool hq_read = mq >= a.min_mapq;
+                const bool pos_ok = p0 >= 0 && p0 < clen;
+                const bool fastr = staged && fast_read(u);  // wave-uniform
+                // the read's base at this lane's position, if the SNV tally
+                // takes one: read offset and the hard-clip-extended length
+                int32_t hit_qi = -1, hit_lsm = u.lq;
+                if (fastr) {
+                    // ---- fast path: a single M/=/X op ----
+                    const int32_t len = (int32_t)(u.cw0 >> 4);
+                    const uint32_t dx = (uint32_t)(x - p0);
+                    if (p0 >= 0 && len < clen - p0 && dx < (uint32_t)len) {
                         caf_mq += mq;
-                        if (mq >= a.rd_min_mapq) caf_rd += 1;
-                        else caf_low += 1;
+                        caf_rd += (mq >= a.rd_min_mapq) ? 1 : 0;
+                        caf_low += (mq >= a.rd_min_mapq) ? 0 : 1;
                     }
-                    caf_pos += len;
-                    if (!in_cap) continue;
-                    if (pos_ok) {
-                        // SNV tally, GROM.c:6769-7059
-                        const int64_t xb = (int64_t)p0 + srb;
-                        const int loop_end = (xb + len >= a.chr_len) ? (int)(a.chr_len - p0) : len;
-                        if (evals && x >= xb && x < xb + loop_end) {
-                            const int qi = snv_base + (int)(x - xb);
-                            int q = 0, s4 = 15;
-                            if (qi < lq) load_base(L, R, staged, qb0, sb0, bo + qi, q, s4);
-                            tally_base(c, slot, a.min_snv, hq_read && q >= a.min_base_qual, q, s4, rb, fwd, qi,
-                                       lseq_mod, mq, nid);
-                        }
-                        snv_base += loop_end;
-                        srb += loop_end;
-                    }
-                } else if (op == 2) {
-                    caf_pos += len;
-                    if (!in_cap) continue;
-                    srb += len;
-                    eai -= len;
-                } else if (in_cap) {
-                    if (op == 4) snv_base += len;
-                    else if (op == 5) lseq_mod += len;
-                    else if (op == 1) { snv_base += len; eai += len; }
-                    else if (op == 3) srb += len;
+                    if (pos_ok && evals && dx < (uint32_t)min(len, clen - p0)) hit_qi = (int32_t)dx;
+                    rd += (dx < (uint32_t)u.lq) ? 1 : 0;  // E = pos + l_qseq
                 } else {
-                    continue;
+                    // ---- general CIGAR walk (rare: int64 arithmetic) ----
+                    const uint32_t cb = u.cb, ce = u.cb + u.ncig;
+                    int snv_base = 0, srb = 0, lseq_mod = u.lq, eai = 0;
+                    int64_t caf_pos = p0;
+                    int first_op = -1, first_len = 0, last_op = -1, last_len = 0;
+                    const uint32_t ncap = (ce - cb > 1000u) ? cb + 1000u : ce;  // GROM.c:6743
+                    for (uint32_t k = cb; k < ce; k++) {
+                        const uint32_t cg = staged ? L.cig[k - cf] : R.cigar[k];
+                        const int op = cg & 15;
+                        const int len = (int)(cg >> 4);
+                        const bool in_cap = k < ncap;
+                        if (op == 0 || op == 7 || op == 8) {
+                            // whole-chromosome read depth, GROM.c:6605-6671 (all ops)
+                            if (caf_pos >= 0 && caf_pos + len < clen && x >= caf_pos && x < caf_pos + len) {
+                                caf_mq += mq;
+                                if (mq >= a.rd_min_mapq) caf_rd += 1;
+                                else caf_low += 1;
+                            }
+                            caf_pos += len;
+                            if (!in_cap) continue;
+                            if (pos_ok) {
+                                // SNV tally, GROM.c:6769-7059: blocks advance
+                                // monotonically, so at most one covers x
+                                const int64_t xb = (int64_t)p0 + srb;
+                                const int loop_end = (xb + len >= clen) ? (int)(clen - p0) : len;
+                                if (evals && x >= xb && x < xb + loop_end) {
+                                    hit_qi = snv_base + (int)(x - xb);
+                                    hit_lsm = lseq_mod;
+                                }
+                                snv_base += loop_end;
+                                srb += loop_end;
+                            }
+                        } else if (op == 2) {
+                            caf_pos += len;
+                            if (!in_cap) continue;
+                            srb += len;
+                            eai -= len;
+                        } else if (in_cap) {
+                            if (op == 4) snv_base += len;
+                            else if (op == 5) lseq_mod += len;
+                            else if (op == 1) { snv_base += len; eai += len; }
+                            else if (op == 3) srb += len;
+                        } else {
+                            continue;
+                        }
+                        if (first_op < 0) { first_op = op; first_len = len; }
+                        last_op = op;
+                        last_len = len;
+                    }
+                    // clip lengths and the aligned end E, GROM.c:7067-7100
+                    const int start_adj = (first_op == 4 || first_op == 5) ? first_len : 0;
+                    const int end_adj = (last_op == 4 || last_op == 5) ? last_len : 0;
+                    const int64_t E = (int64_t)p0 - start_adj + lseq_mod - end_adj - eai;
+                    if (x >= p0 && x < E) rd += 1;  // physical read depth, GROM.c:7173-7181
+                    // soft-clip evidence, GROM.c:7105-7169
+                    const bool at_l = start_adj >= a.sc_min && x == p0 - 1;
+                    const bool at_r = end_adj >= a.sc_min && x == E;
+                    if (evals && (at_l || at_r)) {
+                        const uint4 mate = L.meta[g + u.i].c;
+                        const uint32_t fl = u.fl;
+                        const bool paired = fl & 0x1, munmap = fl & 0x8, rev = fl & 0x10;
+                        const bool same_chr = (int32_t)mate.y == a.chr_tid;
+                        const int32_t mp = (int32_t)mate.z, tl = (int32_t)mate.w;
+                        const int h = hq_read ? 1 : 0;
+                        // category: plain (mate unmapped / proper orientation),
+                        // ctx (mate on another chromosome), indel (close mate)
+                        if (at_l) {
+                            if (!paired || (!rev && (munmap || (!munmap && same_chr && mp > p0)))) {
+                                sch[0] += h; scn[0] += 1;
+                            }
+                            if (paired && !munmap && !same_chr && rev) { sch[2] += h; scn[2] += 1; }
+                            if (paired && !munmap && same_chr && rev && abs(tl) <= a.insert_max && mp < p0) {
+                                sch[4] += h; scn[4] += 1;
+                            }
+                        }
+                        if (at_r) {
+                            if (!paired || (rev && (munmap || (!munmap && same_chr && mp < p0)))) {
+                                sch[1] += h; scn[1] += 1;
+                            }
+                            if (paired && !munmap && !same_chr && !rev) { sch[3] += h; scn[3] += 1; }
+                            if (paired && !munmap && same_chr && !rev && abs(tl) <= a.insert_max && mp > p0) {
+                                sch[5] += h; scn[5] += 1;
+                            }
+                        }
+                    }
                 }
-                if (first_op < 0) { first_op = op; first_len = len; }
-                last_op = op;
-                last_len = len;
-            }
-            // clip lengths and the aligned end E, GROM.c:7067-7100
-            const int start_adj = (first_op == 4 || first_op == 5) ? first_len : 0;
-            const int end_adj = (last_op == 4 || last_op == 5) ? last_len : 0;
-            const int64_t E = (int64_t)p0 - start_adj + lseq_mod - end_adj - eai;
-            if (x >= p0 && x < E) rd += 1;  // physical read depth, GROM.c:7173-7181
-            // soft-clip evidence, GROM.c:7105-7169
-            const bool at_l = start_adj >= a.sc_min && x == (int64_t)p0 - 1;
-            const bool at_r = end_adj >= a.sc_min && x == E;
-            if (evals && (at_l || at_r)) {
-                const bool paired = fl & 0x1, munmap = fl & 0x8, rev = fl & 0x10;
-                const bool same_chr = L.mtid[i] == a.chr_tid;
-                const int32_t mp = L.mpos[i], tl = L.isize[i];
-                const int add = hq_read ? 6 : 0;  // cdp_add, GROM.c:5829-5836
-                if (at_l) {
-                    if (!paired || (!rev && (munmap || (!munmap && same_chr && mp > p0)))) {
-                        sc[0] += add; sc[2] += 1; sc[4] += 1;
+                // ---- SNV tally of the base at this lane (one per read) ----
+                if (hit_qi >= 0) {
+                    int q = 0, s4 = 15;
+                    if (hit_qi < u.lq) {
+                        uint32_t qb = qv, sbv = sv;  // fetched one read ahead (fast path)
+                        int odd = (u.bo + hit_qi) & 1;
+                        if (!fastr) {
+                            if (staged) {
+                                staged_base(lq8, ls8, soff, u.bo + hit_qi, qb, sbv);
+                            } else {
+                                const int64_t nib = qb0 + u.bo + (int64_t)hit_qi;
+                                qb = R.qual[nib];
+                                sbv = R.seq[nib >> 1];
+                                odd = (int)(nib & 1);
+                            }
+                        }
+                        q = (int)qb;
+                        s4 = (int)((sbv >> ((odd ^ 1) << 2)) & 15u);
                     }
-                    if (paired && !munmap && !same_chr && rev) {
-                        sc[5] += add; sc[7] += 1; sc[9] += 1;
-                    }
-                    if (paired && !munmap && same_chr && rev && abs(tl) <= a.insert_max && mp < p0) {
-                        sc[10] += add; sc[12] += 1; sc[14] += 1;
-                    }
+                    tally_base(c, mc, slot, a.min_snv, hq_read && q >= a.min_base_qual, mv, q, s4, rb4, fwd, hit_qi,
+                               hit_lsm, mq, u.nid);
                 }
-                if (at_r) {
-                    if (!paired || (rev && (munmap || (!munmap && same_chr && mp < p0)))) {
-                        sc[1] += add; sc[3] += 1; sc[4] += 1;
-                    }
-                    if (paired && !munmap && !same_chr && !rev) {
-                        sc[6] += add; sc[8] += 1; sc[9] += 1;
-                    }
-                    if (paired && !munmap && same_chr && !rev && abs(tl) <= a.insert_max && mp > p0) {
-                        sc[11] += add; sc[13] += 1; sc[14] += 1;
-                    }
-                }
+                if (!mask) break;
             }
         }
         c0 += m2;
     }
 
+    // matched bases go to the reference base's counters
+    GROM_ADD4(c, snv, rcode, mc.cnt);
+    GROM_ADD4(c, fs, rcode, mc.fs);
+    GROM_ADD4(c, pir, rcode, mc.pir);
+    GROM_ADD4(c, low, rcode, mc.low);
+
+    // soft-clip counters in the reference's order (GC_SC_LEFT..GC_INDEL_SC+4)
+    int32_t sc[15];
+    sc[0] = 6 * sch[0]; sc[1] = 6 * sch[1]; sc[2] = scn[0]; sc[3] = scn[1]; sc[4] = scn[0] + scn[1];
+    sc[5] = 6 * sch[2]; sc[6] = 6 * sch[3]; sc[7] = scn[2]; sc[8] = scn[3]; sc[9] = scn[2] + scn[3];
+    sc[10] = 6 * sch[4]; sc[11] = 6 * sch[5]; sc[12] = scn[4]; sc[13] = scn[5]; sc[14] = scn[4] + scn[5];
+
     // ---- outputs of this position ----
     unsigned long long fsum = 0, fcnt = 0;
-    if (x < a.chr_len) {
+    if (x < clen) {
         O.caf_mq[x] = caf_mq;
         O.caf_rd[x] = caf_rd;
         O.caf_low[x] = caf_low;
@@ -350,13 +509,15 @@ __global__ __launch_bounds__(TG) void k_scan_tile(grom_scan_args a, const char *
             fcnt = 1;
         }
     }
+    int best = -1;  // candidate base of this position, if any
+    float best_ratio = 0.f;
     if (evals) {
         const int32_t total = c.snv0 + c.snv1 + c.snv2 + c.snv3;
         const int32_t rc_all = total + c.low0 + c.low1 + c.low2 + c.low3;
         const int32_t bq_all = c.bq_hi + c.bq_lo, mq_all = c.mq_hi + c.mq_lo;
         if (O.dbg) {
             int32_t *d = O.dbg + (size_t)(x - a.eval_lo) * GC_COUNT;
-            d[GC_POS] = (int32_t)x;
+            d[GC_POS] = x;
             d[GC_SNV + 0] = c.snv0; d[GC_SNV + 1] = c.snv1; d[GC_SNV + 2] = c.snv2; d[GC_SNV + 3] = c.snv3;
             d[GC_SNV_LOWMQ + 0] = c.low0; d[GC_SNV_LOWMQ + 1] = c.low1;
             d[GC_SNV_LOWMQ + 2] = c.low2; d[GC_SNV_LOWMQ + 3] = c.low3;
@@ -376,8 +537,6 @@ __global__ __launch_bounds__(TG) void k_scan_tile(grom_scan_args a, const char *
         // SNV test, GROM.c:11096-11199
         if (rd + sc[14] > 0 && rb != 'N') {
             const int32_t snv[4] = {c.snv0, c.snv1, c.snv2, c.snv3};
-            int best = -1;
-            float best_ratio = 0.f;
             const bool bq_ok = (double)bq_all / (double)rc_all >= a.min_ave_bq;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -389,37 +548,12 @@ __global__ __launch_bounds__(TG) void k_scan_tile(grom_scan_args a, const char *
                     }
                 }
             }
-            if (best >= 0) {
-                const uint32_t ci = atomicAdd(O.n_cands, 1u);
-                if (ci < O.cand_cap) {  // else the host sees n_cands > cap and re-runs with room
-                    grom_snv_cand cd;
-                    cd.pos = (int32_t)x;
-                    cd.base = best;
-                    cd.ratio = best_ratio;
-                    cd.ref_base = (int32_t)(unsigned char)ref[x];
-                    const int32_t sk = best == 0 ? c.snv0 : best == 1 ? c.snv1 : best == 2 ? c.snv2 : c.snv3;
-                    const size_t ti = (total > GROM_MAX_TRIALS)
-                                          ? (size_t)GROM_MAX_TRIALS * (GROM_MAX_TRIALS + 1) + sk * GROM_MAX_TRIALS / total
-                                          : (size_t)total * (GROM_MAX_TRIALS + 1) + sk;
-                    cd.binom = mq_tab[ti];
-                    cd.hez = hez_tab[ti];
-                    cd.snv[0] = c.snv0; cd.snv[1] = c.snv1; cd.snv[2] = c.snv2; cd.snv[3] = c.snv3;
-                    cd.lowmq[0] = c.low0; cd.lowmq[1] = c.low1; cd.lowmq[2] = c.low2; cd.lowmq[3] = c.low3;
-                    cd.pir[0] = c.pir0; cd.pir[1] = c.pir1; cd.pir[2] = c.pir2; cd.pir[3] = c.pir3;
-                    cd.fs[0] = c.fs0; cd.fs[1] = c.fs1; cd.fs[2] = c.fs2; cd.fs[3] = c.fs3;
-                    cd.bq = c.bq_hi;
-                    cd.bq_all = bq_all;
-                    cd.mq = c.mq_hi;
-                    cd.mq_all = mq_all;
-                    cd.bq_rc = total;
-                    cd.mq_rc = total;
-                    cd.rc_all = rc_all;
-                    cd.pad1 = 0;
-                    O.cands[ci] = cd;
-                }
-            }
         }
     }
+    // ---- block totals: flush depth sums and the tile's candidate run ----
+    // Candidates of a tile are written contiguously in position order at a
+    // base taken with one atomic per tile; k_run_* put the runs in tile order.
+    const uint64_t cmask = __ballot(best >= 0);
     for (int o = 32; o > 0; o >>= 1) {
         fsum += __shfl_xor(fsum, o, 64);
         fcnt += __shfl_xor(fcnt, o, 64);
@@ -427,18 +561,127 @@ __global__ __launch_bounds__(TG) void k_scan_tile(grom_scan_args a, const char *
     if (lane == 0) {
         L.red[wave][0] = fsum;
         L.red[wave][1] = fcnt;
+        L.wcnt[wave] = (uint32_t)__popcll(cmask);
     }
     __syncthreads();
     if (tid == 0) {
         unsigned long long s = 0, cc = 0;
+        uint32_t nc = 0;
         for (int w = 0; w < TG / 64; w++) {
             s += L.red[w][0];
             cc += L.red[w][1];
+            nc += L.wcnt[w];
         }
         if (cc) {
             atomicAdd(&O.flush_acc[0], s);
             atomicAdd(&O.flush_acc[1], cc);
         }
+        const uint32_t base = nc ? atomicAdd(O.n_cands, nc) : 0u;
+        L.cbase = base;
+        O.run_base[tile] = base;
+        O.run_cnt[tile] = nc;
+    }
+    __syncthreads();
+    if (best >= 0) {
+        uint32_t ci = L.cbase + (uint32_t)__popcll(cmask & ((1ull << lane) - 1));
+        for (int w = 0; w < wave; w++) ci += L.wcnt[w];
+        if (ci < O.cand_cap) {  // else the host sees n_cands > cap and re-runs with room
+            const int32_t total = c.snv0 + c.snv1 + c.snv2 + c.snv3;
+            grom_snv_cand cd;
+            cd.pos = x;
+            cd.base = best;
+            cd.ratio = best_ratio;
+            cd.ref_base = (int32_t)(unsigned char)ref[x];
+            const int32_t sk = best == 0 ? c.snv0 : best == 1 ? c.snv1 : best == 2 ? c.snv2 : c.snv3;
+            const size_t ti = (total > GROM_MAX_TRIALS)
+                                  ? (size_t)GROM_MAX_TRIALS * (GROM_MAX_TRIALS + 1) + sk * GROM_MAX_TRIALS / total
+                                  : (size_t)total * (GROM_MAX_TRIALS + 1) + sk;
+            cd.binom = mq_tab[ti];
+            cd.hez = hez_tab[ti];
+            cd.snv[0] = c.snv0; cd.snv[1] = c.snv1; cd.snv[2] = c.snv2; cd.snv[3] = c.snv3;
+            cd.lowmq[0] = c.low0; cd.lowmq[1] = c.low1; cd.lowmq[2] = c.low2; cd.lowmq[3] = c.low3;
+            cd.pir[0] = c.pir0; cd.pir[1] = c.pir1; cd.pir[2] = c.pir2; cd.pir[3] = c.pir3;
+            cd.fs[0] = c.fs0; cd.fs[1] = c.fs1; cd.fs[2] = c.fs2; cd.fs[3] = c.fs3;
+            cd.bq = c.bq_hi;
+            cd.bq_all = c.bq_hi + c.bq_lo;
+            cd.mq = c.mq_hi;
+            cd.mq_all = c.mq_hi + c.mq_lo;
+            cd.bq_rc = total;
+            cd.mq_rc = total;
+            cd.rc_all = total + c.low0 + c.low1 + c.low2 + c.low3;
+            cd.pad1 = 0;
+            O.cands[ci] = cd;
+        }
+    }
+}
+
+// ---- candidate runs in tile order: exclusive scan of run_cnt, then gather ----
+#define RUN_ITEMS 8
+#define RUN_SEG (256 * RUN_ITEMS)
+
+// exclusive scan of v over a 256-thread block; *total = block sum
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += t;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int w = 0; w < 4; w++) {
+        off += (w < wave) ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+// per RUN_SEG-tile segment: the number of candidates
+__global__ __launch_bounds__(256) void k_run_sums(int64_t n_tiles, const uint32_t *__restrict__ cnt,
+                                                  uint32_t *__restrict__ seg_sum) {
+    __shared__ uint32_t wsum[4];
+    const int64_t t0 = (int64_t)blockIdx.x * RUN_SEG + threadIdx.x * RUN_ITEMS;
+    uint32_t s = 0;
+    for (int k = 0; k < RUN_ITEMS; k++) s += (t0 + k < n_tiles) ? cnt[t0 + k] : 0u;
+    uint32_t tot;
+    (void)block_scan_excl(s, wsum, &tot);
+    if (threadIdx.x == 0) seg_sum[blockIdx.x] = tot;
+}
+
+// exclusive scan of the segment sums (one block)
+__global__ __launch_bounds__(256) void k_run_scan(int64_t n_seg, uint32_t *__restrict__ seg_sum) {
+    __shared__ uint32_t wsum[4];
+    uint32_t carry = 0;
+    for (int64_t b = 0; b < n_seg; b += 256) {
+        const int64_t i = b + threadIdx.x;
+        const uint32_t v = (i < n_seg) ? seg_sum[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_scan_excl(v, wsum, &tot);
+        if (i < n_seg) seg_sum[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+// copy each tile's run to its place in position order
+__global__ __launch_bounds__(256) void k_run_gather(int64_t n_tiles, const uint32_t *__restrict__ base,
+                                                    const uint32_t *__restrict__ cnt,
+                                                    const uint32_t *__restrict__ seg_off,
+                                                    const grom_snv_cand *__restrict__ src,
+                                                    grom_snv_cand *__restrict__ dst) {
+    __shared__ uint32_t wsum[4];
+    const int64_t t0 = (int64_t)blockIdx.x * RUN_SEG + threadIdx.x * RUN_ITEMS;
+    uint32_t s = 0;
+    for (int k = 0; k < RUN_ITEMS; k++) s += (t0 + k < n_tiles) ? cnt[t0 + k] : 0u;
+    uint32_t tot;
+    uint32_t o = seg_off[blockIdx.x] + block_scan_excl(s, wsum, &tot);
+    for (int k = 0; k < RUN_ITEMS; k++) {
+        if (t0 + k >= n_tiles) break;
+        const uint32_t n = cnt[t0 + k], b = base[t0 + k];
+        for (uint32_t j = 0; j < n; j++) dst[o + j] = src[b + j];
+        o += n;
     }
 }
 

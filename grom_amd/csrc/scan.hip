@@ -5,17 +5,17 @@
 // read into a sliding ring of per-position counters (GROM.c:6406-10966) and
 // evaluating each base once every read that can touch it has been ingested
 // (GROM.c:11086-13553).  Here the chromosome is cut into tiles of GROM_TILE
-// absolute positions; one workgroup owns a tile and builds every counter of
-// its positions in LDS from all reads overlapping it, then evaluates them.
-// Each lane owns one position and folds the tile's reads into registers in
+// absolute positions; one workgroup owns a tile, stages the reads overlapping
+// it in LDS and evaluates its positions.  Each lane owns one position and folds the tile's reads into registers in
 // read order, which is the order the reference's ring sees them, so even the
 // order-dependent read-name de-duplication of mismatching bases
 // (GROM.c:6805-6824) is a plain sequential fold (k_scan_tile.h).
 //
 // Kernels (one launch each per chromosome):
-//   k_span        longest reference extent of any read (tile halo)
-//   k_tile_ranges per-tile [first,last) read range, from the sorted positions
 //   k_rmdup       -M duplicate filter (GROM.c:6432-6588), per start position
+//   k_prep        packs each read's metadata into one 48-byte record and
+//                 finds the longest reference extent (tile halo)
+//   k_tile_ranges per-tile [first,last) read range, from the sorted positions
 //   k_scan_tile   the tile kernel: caf read depth, SNV tally, soft-clip
 //                 evidence, physical read depth, SNV test, flush sums
 //   k_flush_sum   read-depth sum for mid-scan SNV list flushes (rare)
@@ -34,6 +34,7 @@
 
 #include "../../include/grom_amd.h"
 #include "scan_common.h"
+#include "snvfmt.h"
 
 #define T GROM_TILE
 #define NTHR GROM_TILE_THREADS
@@ -57,29 +58,6 @@ static void set_err(const char *fmt, ...) {
     } while (0)
 
 #include "device_common.h"
-
-// ---------------------------------------------------------------------------
-// k_span: reads' M/D/N/=/X extent; the tile halo
-// ---------------------------------------------------------------------------
-__global__ void k_span(int64_t n, const uint32_t *__restrict__ cig_off, const uint32_t *__restrict__ cigar,
-                       const int32_t *__restrict__ lqseq, int32_t *__restrict__ out_max) {
-    int32_t best = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        // reference extent of the tally (M/D/N/=/X) and a bound on the end
-        // E = pos - start_adj + lseq - end_adj - (I - D) used for clips/depth
-        int32_t s = 0, e = lqseq[i];
-        for (uint32_t k = cig_off[i]; k < cig_off[i + 1]; k++) {
-            uint32_t c = cigar[k];
-            int op = c & 15;
-            int32_t len = (int32_t)(c >> 4);
-            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) s += len;
-            if (op == 2 || op == 5) e += len;
-        }
-        best = max(best, max(s, e) + 1);
-    }
-    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(out_max, best);
-}
 
 // ---------------------------------------------------------------------------
 // k_tile_ranges: lo[t] = lower_bound(pos, t*T - halo), hi[t] = lower_bound(pos, t*T + T + 1)
@@ -204,10 +182,10 @@ struct DevBuf {
 static int ensure(DevBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return GROM_OK;
-    if (b.p) hipFree(b.p);
+    if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.cap = 0;
-    size_t want = bytes + bytes / 8;
+    size_t want = bytes + bytes / 8 + 64;  // slack: kernels read whole 16-byte words
     if (hipMalloc(&b.p, want) != hipSuccess) {
         set_err("hipMalloc(%zu) failed", want);
         return GROM_E_NOMEM;
@@ -225,7 +203,9 @@ struct Ctx {
     // reads (used when the caller passes host memory)
     DevBuf r_pos, r_flag, r_mapq, r_mtid, r_mpos, r_isize, r_lq, r_coff, r_cig, r_boff, r_seq, r_qual, r_nid, ref;
     // scan scratch
-    DevBuf keep, tlo, thi, caf_mq, caf_rd, caf_low, cands, misc, dbg;
+    DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg;
+    grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
+    size_t h_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, ep0 = nullptr, ep1 = nullptr;
 };
 
@@ -262,48 +242,11 @@ struct Text {
     }
 };
 
-// SNV rows of one list flush (GROM.c:11203-11274 mid-scan, 15063-15107 final)
-static void snv_rows_range(const grom_params &P, const char *name, const grom_snv_cand *c, size_t lo, size_t hi,
-                           double lim, std::string &out) {
-    static const char dna[4] = {'A', 'C', 'G', 'T'};
-    char line[1024], gt[128];
-    for (size_t i = lo; i < hi; i++) {
-        const grom_snv_cand &s = c[i];
-        const double ratio = (double)s.ratio;
-        if (!(s.rc_all <= lim || ratio >= P.high_cov_min_snv_ratio)) continue;
-        int cn = (int)round(ratio * P.ploidy);
-        if (cn == 0) cn = 1;
-        for (int k = 0; k < P.ploidy; k++) {
-            gt[2 * k] = (k < cn) ? '1' : '0';
-            gt[2 * k + 1] = (k < P.ploidy - 1) ? '/' : '\0';
-        }
-        const int b = s.base;
-        int w = snprintf(line, sizeof(line),
-                         "%s\t%d\t\t%c\t%c\t.\t.\t.\tGT:PR:AF:A:C:G:T:AL:CL:GL:TL:BQ:MQ:PIR:FS\t%s:%e:%e:%d:%d:%d:%d:%d:%d:%d:"
-                         "%d:%.2f:%.2f:%.2f:%.2f\n",
-                         name, s.pos + 1, (char)s.ref_base, dna[b], gt, s.binom, ratio, s.snv[0], s.snv[1], s.snv[2],
-                         s.snv[3], s.lowmq[0], s.lowmq[1], s.lowmq[2], s.lowmq[3],
-                         (double)s.bq_all / (double)s.rc_all, (double)s.mq_all / (double)s.rc_all,
-                         (double)s.pir[b] / (double)s.snv[b], (double)s.fs[b] / (double)s.snv[b]);
-        out.append(line, (size_t)w);
-    }
-}
-
-// rows of one flush; large lists are formatted by host threads in parallel
-// (printf's %e/%.2f conversions are the host's cost) and joined in order
+// rows of one SNV list flush (snvfmt.cpp), appended in order
 static void snv_rows(const grom_params &P, const grom_chrom *ch, const grom_snv_cand *c, size_t n, double ave_rd,
                      Text &out) {
-    const double lim = round(P.snv_rd_min_factor * ave_rd);
-    unsigned nt = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-    if (n < 8192) nt = 1;
-    std::vector<std::string> parts(nt);
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; t++) {
-        size_t lo = n * t / nt, hi = n * (t + 1) / nt;
-        if (nt == 1) snv_rows_range(P, ch->name, c, lo, hi, lim, parts[t]);
-        else th.emplace_back(snv_rows_range, std::cref(P), ch->name, c, lo, hi, lim, std::ref(parts[t]));
-    }
-    for (auto &t : th) t.join();
+    std::vector<std::string> parts;
+    snv_rows_format(P, ch->name, c, n, round(P.snv_rd_min_factor * ave_rd), parts);
     for (auto &s : parts) out.add(s.data(), s.size());
 }
 
@@ -342,6 +285,11 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     const int64_t n_tiles = (ch->len + T - 1) / T;
     const int32_t s0 = P.one_base_rd_len / 4 + 1; /* cdp_one_base_index_start, GROM.c:2918 */
 
+    if (ch->len < 0 || ch->len > (int64_t)INT32_MAX - (1 << 24)) {
+        set_err("chromosome %s: length %lld outside the BAM position range", ch->name ? ch->name : "?",
+                (long long)ch->len);
+        return GROM_E_ARG;
+    }
     grom_scan_args a{};
     a.chr_len = ch->len;
     a.n_reads = n;
@@ -375,7 +323,10 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     if ((rc = ensure(C.tlo, sizeof(int32_t) * n_tiles)) || (rc = ensure(C.thi, sizeof(int32_t) * n_tiles)) ||
         (rc = ensure(C.caf_mq, sizeof(int32_t) * ch->len)) || (rc = ensure(C.caf_rd, sizeof(int32_t) * ch->len)) ||
         (rc = ensure(C.caf_low, sizeof(int32_t) * ch->len)) || (rc = ensure(C.misc, 256)) ||
-        (rc = ensure(C.keep, (size_t)std::max<int64_t>(n, 1))))
+        (rc = ensure(C.keep, (size_t)std::max<int64_t>(n, 1))) ||
+        (rc = ensure(C.meta, sizeof(ReadMeta) * (size_t)std::max<int64_t>(n, 1))) ||
+        (rc = ensure(C.runb, sizeof(uint32_t) * n_tiles)) || (rc = ensure(C.runc, sizeof(uint32_t) * n_tiles)) ||
+        (rc = ensure(C.segs, sizeof(uint32_t) * (size_t)((n_tiles + RUN_SEG - 1) / RUN_SEG + 1))))
         return rc;
     if (want_dbg && (rc = ensure(C.dbg, sizeof(int32_t) * GC_COUNT * std::max<int64_t>(n_eval, 1)))) return rc;
     uint32_t cand_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, ch->len / 256), (int64_t)1 << 26);
@@ -392,19 +343,12 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     unsigned long long *d_macc = (unsigned long long *)(misc + 64);
 
     for (int attempt = 0; attempt < 2; attempt++) {
-        if ((rc = ensure(C.cands, sizeof(grom_snv_cand) * (size_t)cand_cap))) return rc;
+        if ((rc = ensure(C.cands, sizeof(grom_snv_cand) * (size_t)cand_cap)) ||
+            (rc = ensure(C.cands2, sizeof(grom_snv_cand) * (size_t)cand_cap)))
+            return rc;
         (void)hipGetLastError();  // drop any stale error of an earlier, reported failure
         HIPCHK(hipMemsetAsync(C.misc.p, 0, 128, st));
         HIPCHK(hipEventRecord(C.e0, st));
-        if (n > 0) {
-            int g = (int)std::min<int64_t>((n + 255) / 256, 4096);
-            hipLaunchKernelGGL(k_span, dim3(g), dim3(256), 0, st, n, R->cigar_off, R->cigar, R->l_qseq, d_halo);
-        }
-        {
-            int g = (int)std::min<int64_t>((n + 1 + 255) / 256, 8192);
-            hipLaunchKernelGGL(k_tile_ranges, dim3(g), dim3(256), 0, st, n, R->pos, d_halo, n_tiles,
-                               (int32_t *)C.tlo.p, (int32_t *)C.thi.p);
-        }
         const uint8_t *keep = nullptr;
         if (P.rmdup && n > 0) {
             int g = (int)std::min<int64_t>((n + 255) / 256, 8192);
@@ -414,12 +358,21 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         }
         ReadArrays ra{R->pos, R->flag, R->mapq, R->mtid, R->mpos, R->isize, R->l_qseq, R->cigar_off, R->cigar,
                       R->base_off, R->seq, R->qual, R->name_id, keep};
+        if (n > 0) {
+            int g = (int)std::min<int64_t>((n + 255) / 256, 8192);
+            hipLaunchKernelGGL(k_prep, dim3(g), dim3(256), 0, st, n, ra, (ReadMeta *)C.meta.p, d_halo);
+        }
+        {
+            int g = (int)std::min<int64_t>((n + 1 + 255) / 256, 8192);
+            hipLaunchKernelGGL(k_tile_ranges, dim3(g), dim3(256), 0, st, n, R->pos, d_halo, n_tiles,
+                               (int32_t *)C.tlo.p, (int32_t *)C.thi.p);
+        }
         PileOut po{(int32_t *)C.caf_mq.p, (int32_t *)C.caf_rd.p, (int32_t *)C.caf_low.p,
-                   (grom_snv_cand *)C.cands.p, d_ncand, cand_cap, d_facc,
+                   (grom_snv_cand *)C.cands.p, d_ncand, cand_cap, (uint32_t *)C.runb.p, (uint32_t *)C.runc.p, d_facc,
                    want_dbg ? (int32_t *)C.dbg.p : nullptr, d_status, d_nev};
         HIPCHK(hipEventRecord(C.ep0, st));
         hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)(((n_tiles + 7) / 8) * 8)), dim3(GROM_TILE), 0, st, a,
-                           ch->ref, ra, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez,
+                           ch->ref, ra, (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez,
                            n_tiles);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(C.ep1, st));
@@ -436,9 +389,29 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             continue;
         }
         uint32_t ncand = hdr[0];
-        std::vector<grom_snv_cand> cands(ncand);
+        if (ncand > C.h_cap) {
+            if (C.h_cands) (void)hipHostFree(C.h_cands);
+            C.h_cands = nullptr;
+            C.h_cap = 0;
+            const size_t want = (size_t)ncand + ncand / 4 + 1024;
+            HIPCHK(hipHostMalloc((void **)&C.h_cands, sizeof(grom_snv_cand) * want, 0));
+            C.h_cap = want;
+        }
+        const grom_snv_cand *cands = C.h_cands;
         unsigned long long facc[2];
-        if (ncand) HIPCHK(hipMemcpyAsync(cands.data(), C.cands.p, sizeof(grom_snv_cand) * ncand, hipMemcpyDeviceToHost, st));
+        if (ncand) {
+            // tile runs -> position order on the device, then one pinned copy
+            const int64_t n_seg = (n_tiles + RUN_SEG - 1) / RUN_SEG;
+            uint32_t *segs = (uint32_t *)C.segs.p;
+            hipLaunchKernelGGL(k_run_sums, dim3((unsigned)n_seg), dim3(256), 0, st, n_tiles, (const uint32_t *)C.runc.p,
+                               segs);
+            hipLaunchKernelGGL(k_run_scan, dim3(1), dim3(256), 0, st, n_seg, segs);
+            hipLaunchKernelGGL(k_run_gather, dim3((unsigned)n_seg), dim3(256), 0, st, n_tiles,
+                               (const uint32_t *)C.runb.p, (const uint32_t *)C.runc.p, (const uint32_t *)segs,
+                               (const grom_snv_cand *)C.cands.p, (grom_snv_cand *)C.cands2.p);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(C.h_cands, C.cands2.p, sizeof(grom_snv_cand) * ncand, hipMemcpyDeviceToHost, st));
+        }
         HIPCHK(hipMemcpyAsync(facc, d_facc, 16, hipMemcpyDeviceToHost, st));
         if (want_dbg) {
             if (n_eval * GC_COUNT > dbg_cap) {
@@ -455,8 +428,6 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             if (dbg_first) *dbg_first = a.eval_lo;
         }
         HIPCHK(hipStreamSynchronize(st));
-        std::sort(cands.begin(), cands.end(),
-                  [](const grom_snv_cand &x, const grom_snv_cand &y) { return x.pos < y.pos; });
 
         // SNV list with its flushes (GROM.c:11201-11326, 15063-15160)
         Text vt{&out->vcf, &out->vcf_len, &out->vcf_cap};
@@ -475,19 +446,19 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                 HIPCHK(hipMemcpyAsync(m, d_macc, 16, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
             }
-            snv_rows(P, ch, cands.data() + done, (size_t)thr, (double)(int64_t)m[0] / (double)(int64_t)m[1], vt);
+            snv_rows(P, ch, cands + done, (size_t)thr, (double)(int64_t)m[0] / (double)(int64_t)m[1], vt);
             done += (size_t)thr;
         }
-        snv_rows(P, ch, cands.data() + done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1], vt);
+        snv_rows(P, ch, cands + done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1], vt);
 
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
         if (stats) {
             float ms = 0, msp = 0;
-            hipEventElapsedTime(&ms, C.e0, C.e1);
-            hipEventElapsedTime(&msp, C.ep0, C.ep1);
+            (void)hipEventElapsedTime(&ms, C.e0, C.e1);
+            (void)hipEventElapsedTime(&msp, C.ep0, C.ep1);
             uint32_t nev = 0;
-            hipMemcpy(&nev, d_nev, 4, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(&nev, d_nev, 4, hipMemcpyDeviceToHost);
             stats->ms_total = ms;
             stats->ms_pileup = msp;
             stats->bases_evaluated = n_eval;
@@ -579,17 +550,19 @@ void grom_dev_fini(int device) {
     (void)hipSetDevice(device);
     (void)hipStreamSynchronize(C.st);
     DevBuf *all[] = {&C.r_pos, &C.r_flag, &C.r_mapq, &C.r_mtid, &C.r_mpos, &C.r_isize, &C.r_lq, &C.r_coff,
-                     &C.r_cig, &C.r_boff, &C.r_seq, &C.r_qual, &C.r_nid, &C.ref, &C.keep, &C.tlo, &C.thi,
-                     &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands, &C.misc, &C.dbg};
+                     &C.r_cig, &C.r_boff, &C.r_seq, &C.r_qual, &C.r_nid, &C.ref, &C.keep, &C.meta, &C.cands2,
+                     &C.runb, &C.runc, &C.segs, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
+                     &C.misc, &C.dbg};
     for (DevBuf *b : all)
-        if (b->p) hipFree(b->p);
-    hipFree(C.d_mq);
-    hipFree(C.d_hez);
-    hipEventDestroy(C.e0);
-    hipEventDestroy(C.e1);
-    hipEventDestroy(C.ep0);
-    hipEventDestroy(C.ep1);
-    hipStreamDestroy(C.st);
+        if (b->p) (void)hipFree(b->p);
+    if (C.h_cands) (void)hipHostFree(C.h_cands);
+    (void)hipFree(C.d_mq);
+    (void)hipFree(C.d_hez);
+    (void)hipEventDestroy(C.e0);
+    (void)hipEventDestroy(C.e1);
+    (void)hipEventDestroy(C.ep0);
+    (void)hipEventDestroy(C.ep1);
+    (void)hipStreamDestroy(C.st);
     g_ctx[device] = Ctx();
 }
 
@@ -610,6 +583,10 @@ int grom_scan_chrom_device(int device, const grom_chrom *chrom, const grom_reads
     Ctx *C = ctx_of(device);
     if (!C) return GROM_E_NODEV;
     if (!chrom || !dev_reads || !out) { set_err("grom_scan_chrom_device: null argument"); return GROM_E_ARG; }
+    if (((uintptr_t)dev_reads->qual | (uintptr_t)dev_reads->seq) & 15) {
+        set_err("grom_scan_chrom_device: qual and seq must be 16-byte aligned");
+        return GROM_E_ARG;
+    }
     HIPCHK(hipSetDevice(device));
     return scan_device(*C, chrom, dev_reads, out, stats, nullptr, nullptr, 0, nullptr);
 }

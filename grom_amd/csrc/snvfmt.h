@@ -1,0 +1,26 @@
+// snvfmt.h -- host-side VCF text of the SNV rows (GROM.c:11203-11274 mid-scan
+// flushes, 15063-15107 final flush), formatted without printf on the hot path.
+#ifndef GROM_AMD_SNVFMT_H
+#define GROM_AMD_SNVFMT_H
+
+#include <stddef.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/grom_amd.h"
+#include "scan_common.h"
+
+// Rows of one SNV list flush: candidates c[0..n) (position order) whose
+// rc_all passes the flush's depth limit `lim` (or whose ratio passes
+// high_cov_min_snv_ratio).  Large lists are split over up to 16 host threads;
+// the text of part t goes to parts[t] (join in order).
+void snv_rows_format(const grom_params &P, const char *chr_name, const grom_snv_cand *c, size_t n, double lim,
+                     std::vector<std::string> &parts);
+
+// Byte-identical replacement for printf("%.2f", v) (glibc semantics: the
+// exact binary value, rounded half to even).  `out` must hold 400 bytes.
+// Returns the length written.
+int fmt_2f(char *out, double v);
+
+#endif

@@ -151,8 +151,9 @@ int grom_scan_chrom(int device, const grom_chrom *chrom, const grom_reads *reads
 
 /* Same, with every grom_reads pointer (and chrom->ref) already in device
  * memory of `device`.  Used to time the scan with inputs resident in HBM.
- * qual and seq must be 4-byte aligned and readable 16 bytes past their end
- * (the kernel copies them in 32-bit words); grom_upload guarantees both. */
+ * qual and seq must be 16-byte aligned and readable up to the next 16-byte
+ * boundary past their end (the kernel copies them in 16-byte words);
+ * grom_upload guarantees both. */
 int grom_scan_chrom_device(int device, const grom_chrom *chrom, const grom_reads *dev_reads, grom_out *out,
                            grom_stats *stats);
 
@@ -174,6 +175,10 @@ void grom_params_set_insert(grom_params *p, int32_t insert_mean, int32_t insert_
                             int32_t lseq);
 
 void grom_out_free(grom_out *out);
+
+/* Test hook: checks the VCF writer's exact "%.2f" conversion against printf
+ * on n pseudo-random integer ratios (plus edge cases); returns mismatches. */
+int64_t grom_fmt_selftest(int64_t n, uint64_t seed);
 
 /* Copy a host chromosome + reads into library-owned device buffers of
  * `device` and return device-side views of them (valid until the next upload

@@ -34,6 +34,8 @@ struct dim3 {
     unsigned x, y, z;
     dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
 };
+struct alignas(16) uint4 { unsigned x, y, z, w; };
+inline uint4 make_uint4(unsigned x, unsigned y, unsigned z, unsigned w) { return uint4{x, y, z, w}; }
 struct emu_idx { unsigned x, y, z; };
 extern thread_local emu_idx threadIdx, blockIdx;
 extern emu_idx blockDim, gridDim;
@@ -44,6 +46,7 @@ using std::min;
 // ---- synchronisation within the emulated block ----
 struct emu_block_sync {
     std::barrier<> *bar = nullptr;
+    std::vector<std::barrier<> *> wave_bar;  // one per 64-lane wave
     std::atomic<int> count{0};
     std::vector<unsigned long long> xch;
 };
@@ -58,19 +61,52 @@ inline int __syncthreads_count(int p) {
     g_emu_sync->bar->arrive_and_wait();
     return v;
 }
+// cross-lane operations exchange through xch under the wave's own barrier,
+// so (as on the GPU) they need only the 64 lanes of one wave to be converged
+inline unsigned long long emu_lane_xch(unsigned long long u, unsigned src) {
+    const unsigned t = threadIdx.x;
+    std::barrier<> *wb = g_emu_sync->wave_bar[t / 64];
+    g_emu_sync->xch[t] = u;
+    wb->arrive_and_wait();
+    const unsigned long long r = g_emu_sync->xch[(t & ~63u) | (src & 63u)];
+    wb->arrive_and_wait();
+    return r;
+}
 template <typename T>
 inline T __shfl_xor(T v, int off, int width = 64) {
     (void)width;
-    unsigned t = threadIdx.x;
     unsigned long long u = 0;
     std::memcpy(&u, &v, sizeof(T));
-    g_emu_sync->xch[t] = u;
-    g_emu_sync->bar->arrive_and_wait();
-    unsigned long long r = g_emu_sync->xch[t ^ (unsigned)off];
-    g_emu_sync->bar->arrive_and_wait();
+    const unsigned long long r = emu_lane_xch(u, (threadIdx.x & 63u) ^ (unsigned)off);
     T out;
     std::memcpy(&out, &r, sizeof(T));
     return out;
+}
+template <typename T>
+inline T __shfl_up(T v, unsigned d, int width = 64) {
+    (void)width;
+    unsigned long long u = 0;
+    std::memcpy(&u, &v, sizeof(T));
+    const unsigned l = threadIdx.x & 63u;
+    const unsigned long long r = emu_lane_xch(u, l >= d ? l - d : l);
+    T out;
+    std::memcpy(&out, &r, sizeof(T));
+    return out;
+}
+inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
+inline int __builtin_amdgcn_readlane(int v, int i) {
+    return (int)(unsigned)emu_lane_xch((unsigned)v, (unsigned)i);
+}
+inline unsigned long long __ballot(int p) {
+    const unsigned t = threadIdx.x;
+    std::barrier<> *wb = g_emu_sync->wave_bar[t / 64];
+    g_emu_sync->xch[t] = p ? 1 : 0;
+    wb->arrive_and_wait();
+    unsigned long long m = 0;
+    for (unsigned k = 0; k < 64 && (t & ~63u) + k < g_emu_sync->xch.size(); k++)
+        if (g_emu_sync->xch[(t & ~63u) + k]) m |= 1ull << k;
+    wb->arrive_and_wait();
+    return m;
 }
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 
@@ -104,6 +140,11 @@ inline hipError_t hipMalloc(void **p, size_t n) {
 template <typename T>
 inline hipError_t hipMalloc(T **p, size_t n) { return hipMalloc((void **)p, n); }
 inline hipError_t hipFree(void *p) { std::free(p); return hipSuccess; }
+inline hipError_t hipHostMalloc(void **p, size_t n, unsigned) {
+    *p = std::malloc(n);
+    return *p ? hipSuccess : hipErrorInvalidValue;
+}
+inline hipError_t hipHostFree(void *p) { std::free(p); return hipSuccess; }
 inline hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) { std::memcpy(d, s, n); return hipSuccess; }
 inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t) {
     return hipMemcpy(d, s, n, k);

@@ -88,3 +88,10 @@ def test_q21_empty_chromosome_starves_later_ones(datadir):
     plan = parse_plan(r.stdout)
     assert plan["chr1"]["reads"] > 0
     assert plan["chr2"]["reads"] == 0 and plan["chr3"]["reads"] == 0
+
+
+def test_fmt_2f_matches_printf():
+    """The VCF writer's exact %.2f (snvfmt.cpp) against glibc printf on 400k
+    integer ratios, exact binary ties and edge cases (inf, nan, -0.0)."""
+    import grom_amd
+    assert grom_amd.lib().grom_fmt_selftest(200000, 12345) == 0
