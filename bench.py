@@ -15,6 +15,7 @@ The JSON line also carries
                 thread, on a bounded sample of the same workload (rank 0, N=1).
 """
 import argparse
+import ctypes
 import json
 import os
 import subprocess
@@ -98,13 +99,15 @@ def main():
     pile_ms = []
     tot_ms = []
     rows = 0
+    out = grom_amd.Out()  # the VCF text buffer, reused across steps (grom_out)
     for _ in range(args.steps):
-        text, st = dev.scan(dchrom, dreads, device_resident=True)
+        vcf_len, st = dev.scan(dchrom, dreads, device_resident=True, out=out)
         pile_ms.append(st.ms_pileup)
         tot_ms.append(st.ms_total)
-        rows = text.count("\n")
     barrier()
     dt = time.perf_counter() - t0
+    rows = ctypes.string_at(out.vcf, vcf_len).count(b"\n") if vcf_len else 0
+    grom_amd.lib().grom_out_free(ctypes.byref(out))
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -132,10 +132,21 @@ class Device:
     def close(self):
         lib().grom_dev_fini(self.device)
 
-    def scan(self, chrom: Chrom, reads: Reads, device_resident: bool = False):
-        out, st = Out(), Stats()
+    def scan(self, chrom: Chrom, reads: Reads, device_resident: bool = False, out: "Out | None" = None):
+        """Scan one chromosome; returns (VCF text, Stats).  With a caller-owned
+        `out` (reused across calls, freed with grom_out_free) the text stays
+        in out.vcf and the first element is its length instead."""
+        own = out is None
+        if own:
+            out = Out()
+        else:
+            out.vcf_len = 0
+            out.ctx_len = 0
+        st = Stats()
         fn = lib().grom_scan_chrom_device if device_resident else lib().grom_scan_chrom
         check(fn(self.device, C.byref(chrom), C.byref(reads), C.byref(out), C.byref(st)), "scan")
+        if not own:
+            return out.vcf_len, st
         text = C.string_at(out.vcf, out.vcf_len).decode() if out.vcf_len else ""
         lib().grom_out_free(C.byref(out))
         return text, st

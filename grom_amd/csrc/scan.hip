@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -276,20 +277,21 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     const grom_params &P = C.prm;
     int rc = check_params(P);
     if (rc) return rc;
-    if (ch->len <= 0 || ch->len >= (int64_t)1 << 31) {
+    // int32 positions in the kernels, with room for read extents past the end
+    if (ch->len <= 0 || ch->len > (int64_t)INT32_MAX - (1 << 24)) {
         set_err("chromosome length %lld out of range", (long long)ch->len);
         return GROM_E_ARG;
     }
     hipStream_t st = C.st;
+    const bool timing = getenv("GROM_TIMING") != nullptr;  // per-phase host clock on stderr
+    const auto t_start = std::chrono::steady_clock::now();
+    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     const int64_t n = R->n;
     const int64_t n_tiles = (ch->len + T - 1) / T;
     const int32_t s0 = P.one_base_rd_len / 4 + 1; /* cdp_one_base_index_start, GROM.c:2918 */
 
-    if (ch->len < 0 || ch->len > (int64_t)INT32_MAX - (1 << 24)) {
-        set_err("chromosome %s: length %lld outside the BAM position range", ch->name ? ch->name : "?",
-                (long long)ch->len);
-        return GROM_E_ARG;
-    }
     grom_scan_args a{};
     a.chr_len = ch->len;
     a.n_reads = n;
@@ -379,6 +381,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         uint32_t hdr[4];
         HIPCHK(hipMemcpyAsync(hdr, misc + 4, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        const double t_kernels = ms_since(t_start);
         if (hdr[1] != 0) {
             set_err("per-tile event buffer overflow in %u tile(s), first tile %u (position %lld)", hdr[1], hdr[2],
                     (long long)hdr[2] * T);
@@ -428,6 +431,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             if (dbg_first) *dbg_first = a.eval_lo;
         }
         HIPCHK(hipStreamSynchronize(st));
+        const double t_copied = ms_since(t_start);
 
         // SNV list with its flushes (GROM.c:11201-11326, 15063-15160)
         Text vt{&out->vcf, &out->vcf_len, &out->vcf_cap};
@@ -451,6 +455,9 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         }
         snv_rows(P, ch, cands + done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1], vt);
 
+        if (timing)
+            fprintf(stderr, "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms, rows %.3f ms (%u candidates)\n",
+                    ch->name ? ch->name : "?", t_kernels, t_copied - t_kernels, ms_since(t_start) - t_copied, ncand);
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
         if (stats) {
