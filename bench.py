@@ -80,6 +80,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import grom_amd
+    from grom_amd.shard import max_over_ranks, timed_steps
 
     t_gen = time.perf_counter()
     batch = grom_amd.SynthBatch(args.chrom_len, COVERAGE, READ_LEN, 500.0, 50.0, seed=1000 + rank)
@@ -94,24 +95,21 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
     pile_ms = []
     tot_ms = []
-    rows = 0
     out = grom_amd.Out()  # the VCF text buffer, reused across steps (grom_out)
-    for _ in range(args.steps):
+    last = [0]
+
+    def step():
         vcf_len, st = dev.scan(dchrom, dreads, device_resident=True, out=out)
         pile_ms.append(st.ms_pileup)
         tot_ms.append(st.ms_total)
-    barrier()
-    dt = time.perf_counter() - t0
-    rows = ctypes.string_at(out.vcf, vcf_len).count(b"\n") if vcf_len else 0
+        last[0] = vcf_len
+
+    dt = timed_steps(step, args.steps, barrier)
+    rows = ctypes.string_at(out.vcf, last[0]).count(b"\n") if last[0] else 0
     grom_amd.lib().grom_out_free(ctypes.byref(out))
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(dt, device="cuda")
 
     bases = args.chrom_len * world * args.steps
     value = bases / dt / 1e6

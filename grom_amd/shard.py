@@ -1,0 +1,51 @@
+"""Chromosome sharding and multi-rank timing (one process per GPU).
+
+The scan has no cross-chromosome state (every array of
+count_discordant_pairs is local to one call, GROM.c:1432), so ranks split the
+chromosomes and never exchange data on the scan path.  torch.distributed (RCCL
+on the GPU box, gloo in the CPU tests) carries only the barrier around the
+timed region and the max-over-ranks of its duration.
+"""
+import time
+from typing import Callable, List, Sequence
+
+
+def assign_chromosomes(lengths: Sequence[int], world: int) -> List[List[int]]:
+    """Longest-processing-time assignment of chromosome indices to ranks.
+
+    The reference already processes chromosomes longest-first
+    (GROM.c:22318-22336); each chromosome goes to the least-loaded rank, ties
+    to the lower rank, so the result is deterministic."""
+    if world < 1:
+        raise ValueError("world size must be >= 1")
+    order = sorted(range(len(lengths)), key=lambda i: (-lengths[i], i))
+    load = [0] * world
+    shards: List[List[int]] = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        shards[r].append(i)
+        load[r] += lengths[i]
+    for s in shards:
+        s.sort()
+    return shards
+
+
+def timed_steps(step: Callable[[], None], steps: int, barrier: Callable[[], None]) -> float:
+    """Seconds for exactly `steps` calls of step(), bracketed by barrier()."""
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Max of `value` over all ranks (identity without a process group)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
