@@ -29,12 +29,16 @@ class Params(C.Structure):
         "overlap_mult", "sv_list_len", "rmdup_list_len", "read_name_len", "sc_min")] + \
         [(n, C.c_double) for n in ("min_snv_ratio", "min_ave_bq", "snv_rd_min_factor", "high_cov_min_snv_ratio")] + \
         [(n, C.c_int32) for n in ("insert_mean", "insert_min_size", "insert_max_size", "lseq", "one_base_rd_len",
-                                  "half_one_base_rd_len", "r14_one_base_rd_len", "r34_one_base_rd_len")]
+                                  "half_one_base_rd_len", "r14_one_base_rd_len", "r34_one_base_rd_len",
+                                  "ranks_stdev", "chr_rd_threshold_factor")] + \
+        [(n, C.c_int64) for n in ("min_repeat", "min_blocks", "block_min", "min_rd_window_len", "max_rd_window_len",
+                                  "windows_sampling_factor", "dup_threshold_factor")] + \
+        [(n, C.c_double) for n in ("min_repeat_stdev", "rd_pval_threshold", "mapq_factor")]
 
 
 class Chrom(C.Structure):
     _fields_ = [("ref", C.c_void_p), ("len", C.c_int64), ("name", C.c_char_p), ("tid", C.c_int32),
-                ("n_skip", C.c_int32), ("p_last", C.c_int32)]
+                ("n_skip", C.c_int32), ("p_last", C.c_int32), ("cnv", C.c_int32), ("seed", C.c_uint32)]
 
 
 class Reads(C.Structure):
@@ -49,13 +53,15 @@ class Out(C.Structure):
 
 
 class Stats(C.Structure):
-    _fields_ = [("ms_total", C.c_double), ("ms_pileup", C.c_double), ("bases_evaluated", C.c_int64),
+    _fields_ = [("ms_total", C.c_double), ("ms_pileup", C.c_double), ("ms_cnv", C.c_double),
+                ("cnv_rows", C.c_int64), ("bases_evaluated", C.c_int64),
                 ("snv_candidates", C.c_int64), ("mismatch_events", C.c_int64)]
 
 
 # every function declared in include/grom_amd.h, with its ctypes signature
 _SIGS = {
     "grom_abi_version": (C.c_int, []),
+    "grom_abi_struct_size": (C.c_size_t, [C.c_int]),
     "grom_last_error": (C.c_char_p, []),
     "grom_dev_init": (C.c_int, [C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
     "grom_dev_fini": (None, [C.c_int]),

@@ -1,0 +1,1604 @@
+// cnv.hip -- MI355X (gfx950) implementation of GROM's read-depth CNV path,
+// SURVEY.md §8 rows A14-A16, run per chromosome after the pileup
+// (scan.hip) has filled the three whole-chromosome depth arrays.
+//
+//   reference step                              here
+//   GC/ACGT triangular windows   GROM.c:1770    k_cnv_gc: two LDS prefix scans per
+//                                               4096-base tile give the weighted
+//                                               window sum in closed form
+//   dinucleotide repeat runs     GROM.c:1727    k_cnv_gc (pair type) + k_cnv_repeats
+//   mapq/depth division, 10 kb   GROM.c:16637,  k_cnv_blocks (one workgroup per
+//   blocks, chromosome depth     16651, 16811   10 kb block, exact integer sums)
+//   GC-bin sampling, sort/merge  GROM.c:18373   host (≈G/250 samples), gathered
+//   bins, bin statistics         -18641         by k_cnv_gather
+//   low-ACGT/thin-bin flags      GROM.c:18654   k_cnv_tile_last + k_cnv_carry +
+//                                               k_cnv_flags: the "last high/low
+//                                               MAPQ class" state is a last-value
+//                                               scan (tile summary, carry, apply)
+//   per-base z score             GROM.c:18740   k_cnv_z (same scan for its own
+//                                               state, then bisect + pval2sd)
+//   window means per length      GROM.c:18967   k_cnv_windows (one lane per
+//                                               10 kb window, sequential double
+//                                               sums in reference order) +
+//                                               k_cnv_window_sq (one lane per
+//                                               window length)
+//   DEL/DUP window search        GROM.c:19359   k_cnv_walk: the data-dependent
+//                                               walk, chunked and run
+//                                               speculatively (one lane per
+//                                               chunk), then reconciled
+//   copy number, p value, rows   GROM.c:20024,  host, on gathered call ranges
+//                                17139
+//
+// Exactness: every double the VCF depends on is produced with the reference's
+// operation order (sequential sums stay sequential, one lane each; this file
+// is compiled with -ffp-contract=off so no multiply-add is fused).  The one
+// order-dependent sum computed differently is the chromosome depth variance
+// of GROM.c:16664-16677; it only feeds the repeat-bias comparison
+// (GROM.c:16765) and is summed from an exact depth histogram.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cnv.h"
+
+namespace {
+
+// ---- fixed parameters of the reference (not on its command line) ----
+constexpr int NBINS = 101;                 // g_num_gc_bins, GROM.c:947
+constexpr int REP_SEGS = 10;               // g_repeat_segments, GROM.c:732
+constexpr long SAMPLE_LEN = 100000;        // g_sample_lists_len, GROM.c:725
+constexpr long REDUCTION = 1;              // g_genome_reduction_factor, GROM.c:726
+constexpr long BLOCK_FACTOR = 4;           // g_block_factor, GROM.c:738
+constexpr long BLOCK_UNIT = 10000;         // g_block_unit_size, GROM.c:740
+constexpr int MIN_ACGT = 99;               // g_insert_min_acgt, GROM.c:926
+constexpr long NO_COMBINE = 100;           // g_rd_no_combine_min_windows, GROM.c:929
+constexpr long RD_MIN_WINDOWS = 20;        // g_rd_min_windows, GROM.c:928
+constexpr int RD_MAX_MAPQ = 60;            // g_rd_max_mapq, GROM.c:718
+constexpr long MIN_RD_LOW_STDEV = 3;       // g_one_base_read_depth_min_rd_low_stdev, GROM.c:935
+constexpr double MAX_LOW_ACGT = 2;         // g_max_rd_low_acgt_or_windows, GROM.c:937
+constexpr double PLOIDY_NUM = 0.6;         // g_ploidy_threshold_numerator, GROM.c:939
+constexpr double STDEV_STEP = 0.01;        // g_stdev_step, GROM.c:940
+constexpr long MAX_DIST_LAST_GOOD = 10500; // default -X + 500, set before getopt (GROM.c:21898)
+constexpr int MAX_BLOCK_LIST = 10000;      // max_block_list_len, GROM.c:633
+
+constexpr int GC_TP = 4096;                // positions per k_cnv_gc tile
+constexpr int GC_MMAX = 1536;              // largest insert mean the LDS tile holds
+constexpr int GC_LEN = GC_TP + 2 * GC_MMAX + 2;
+constexpr int SCAN_K = 16;                 // positions per lane in the state scans
+constexpr int SCAN_TP = 256 * SCAN_K;      // positions per scan tile
+constexpr int HIST_MAX = 4096;             // exact depth histogram for the chromosome variance
+constexpr int64_t WALK_CHUNK = 16384;      // positions per speculative walk lane
+
+// flag byte per position
+constexpr uint8_t F_LOW = 1;    // ddd_rd_low_acgt_or_windows_list != 0
+constexpr uint8_t F_GUARD = 2;  // z-scored / windowed base (GROM.c:18765 condition)
+
+struct Tables {  // device copy of the per-chromosome bin statistics
+    int32_t off[2][NBINS], cnt[2][NBINS];
+    int64_t wins[2][NBINS];
+    double ave[2][NBINS], sdv[2][NBINS], thr[2][2][NBINS];  // thr[0]=del, thr[1]=dup
+    double p2s_p[1001], p2s_sd[1001];
+    int32_t n_p2s;
+};
+
+struct Args {
+    int64_t len, lo, hi;  // [lo, hi) = [insert_mean-1, len - window_size)
+    int32_t min_mapq, ranks_stdev;
+    double mapq_factor, dup_factor;
+};
+
+__device__ __forceinline__ int gc_class(char ch) {  // bit0 GC, bit1 ACGT (GROM.c:1591-1592)
+    switch (ch) {
+    case 'C': case 'G': case 'c': case 'g': return 3;
+    case 'A': case 'T': case 'a': case 't': return 2;
+    default: return 0;
+    }
+}
+
+// dinucleotide class of (x, y), GROM.c:1656-1657, 1729-1737: unordered pair of
+// two upper-case or two lower-case ACGT bases, 10 for anything else
+__device__ __forceinline__ int pair_type(char x, char y) {
+    auto code = [](char c, int lower) -> int {
+        char u = lower ? (char)(c - 32) : c;
+        return u == 'A' ? 0 : u == 'C' ? 1 : u == 'G' ? 2 : u == 'T' ? 3 : -1;
+    };
+    int lx = (x >= 'a' && x <= 'z'), ly = (y >= 'a' && y <= 'z');
+    if (lx != ly) return 10;
+    int a = code(x, lx), b = code(y, ly);
+    if (a < 0 || b < 0) return 10;
+    if (a > b) { int t = a; a = b; b = t; }
+    const int base[4] = {0, 4, 7, 9};
+    return base[a] + (b - a);
+}
+
+// exclusive prefix sum of a[0..n) in place, one 256-thread block
+__device__ void block_excl_scan(int *a, int n, int *tmp) {
+    const int tid = threadIdx.x, per = (n + 255) / 256;
+    const int lo = min(n, tid * per), hi = min(n, lo + per);
+    int s = 0;
+    for (int i = lo; i < hi; i++) s += a[i];
+    tmp[tid] = s;
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int t = 0; t < 256; t++) { int v = tmp[t]; tmp[t] = acc; acc += v; }
+    }
+    __syncthreads();
+    int acc = tmp[tid];
+    for (int i = lo; i < hi; i++) { int v = a[i]; a[i] = acc; acc += v; }
+    __syncthreads();
+}
+
+// Weighted GC / ACGT percent and dinucleotide class per base (GROM.c:1684-1861).
+// The reference's rolling sums equal, for p in [m-1, len-2m+1),
+//   T(p) = sum_{|q-p|<m} g(q) (m - |q-p|) = Q[p+m+1] - 2 Q[p+1] + Q[p-m+1]
+// with P the prefix count of g and Q the prefix sum of P (exact integers).
+__global__ __launch_bounds__(256) void k_cnv_gc(const char *__restrict__ ref, Args A, int m, int64_t total,
+                                                uint8_t *__restrict__ gcw, uint8_t *__restrict__ acw,
+                                                uint8_t *__restrict__ rtype) {
+    __shared__ int P[GC_LEN + 1];
+    __shared__ int Q[GC_LEN + 1];
+    __shared__ uint8_t cls[GC_LEN];
+    __shared__ int tmp[256];
+    const int64_t t0 = (int64_t)blockIdx.x * GC_TP;
+    const int64_t base = t0 - m;
+    const int L = GC_TP + 2 * m + 1;
+    for (int i = threadIdx.x; i < L; i += 256) {
+        int64_t q = base + i;
+        cls[i] = (q >= 0 && q < A.len) ? (uint8_t)gc_class(ref[q]) : 0;
+    }
+    __syncthreads();
+    for (int pass = 0; pass < 2; pass++) {
+        for (int i = threadIdx.x; i <= L; i += 256) P[i] = (i < L) ? ((cls[i] >> pass) & 1) : 0;
+        __syncthreads();
+        block_excl_scan(P, L + 1, tmp);
+        for (int i = threadIdx.x; i <= L; i += 256) Q[i] = P[i];
+        __syncthreads();
+        block_excl_scan(Q, L + 1, tmp);
+        uint8_t *out = pass == 0 ? gcw : acw;
+        for (int j = threadIdx.x; j < GC_TP; j += 256) {
+            int64_t p = t0 + j;
+            if (p >= A.len) break;
+            uint8_t w = 0;
+            if (p >= A.lo && p < A.hi) {
+                int lp = j + m;
+                int64_t Tv = (int64_t)Q[lp + m + 1] - 2 * (int64_t)Q[lp + 1] + (int64_t)Q[lp - m + 1];
+                w = (uint8_t)(100 * Tv / total);
+            }
+            out[p] = w;
+        }
+        __syncthreads();
+    }
+    for (int j = threadIdx.x; j < GC_TP; j += 256) {
+        int64_t p = t0 + j;
+        if (p >= A.len) break;
+        rtype[p] = (p >= A.lo && p < A.hi) ? (uint8_t)pair_type(ref[p], ref[p + 1]) : (uint8_t)10;
+    }
+}
+
+struct RepeatRec {
+    int64_t start, end, rd;  // [start, end), depth sum over it
+    int32_t type, pad;
+};
+
+// Repeat runs (GROM.c:1727-1768): a maximal run of one class, closed before
+// the last scanned base, of at least g_min_repeat bases.
+__global__ void k_cnv_repeats(const uint8_t *__restrict__ rtype, const int32_t *__restrict__ rd,
+                              const int32_t *__restrict__ low, Args A, int64_t min_repeat, RepeatRec *out,
+                              uint32_t *n_out, uint32_t cap) {
+    int64_t p = A.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.hi) return;
+    int t = rtype[p];
+    if (t == 10 || (p > A.lo && rtype[p - 1] == t)) return;
+    int64_t e = p;
+    while (e + 1 < A.hi && rtype[e + 1] == t) e++;
+    if (e + 1 >= A.hi) return;  // still open when the scan loop ends: never written
+    if (e - p < min_repeat - 1) return;
+    int64_t s = 0;
+    for (int64_t q = p; q <= e; q++) s += rd[q] + low[q];
+    uint32_t k = atomicAdd(n_out, 1u);
+    if (k < cap) out[k] = RepeatRec{p, e + 1, s, t, 0};
+}
+
+struct BlockSums {
+    unsigned long long blk_total[1];  // placeholder for alignment
+};
+
+// One workgroup per 10 kb block (plus one for the tail): divides the mapq sum
+// by the depth in place (GROM.c:16637-16643), the block depth sums of
+// GROM.c:16811-16829 and the chromosome depth sums of GROM.c:16651-16662.
+__global__ __launch_bounds__(256) void k_cnv_blocks(const char *__restrict__ ref, Args A,
+                                                    int32_t *__restrict__ mq, const int32_t *__restrict__ rd,
+                                                    const int32_t *__restrict__ low,
+                                                    const uint8_t *__restrict__ acw, int64_t *blk_total,
+                                                    unsigned long long *acc, unsigned int *hist) {
+    __shared__ unsigned int h[HIST_MAX + 1];
+    __shared__ unsigned long long s_tot, s_acgt_tot, s_acgt_n, s_chr_tot, s_chr_n;
+    for (int i = threadIdx.x; i <= HIST_MAX; i += 256) h[i] = 0;
+    if (threadIdx.x == 0) s_tot = s_acgt_tot = s_acgt_n = s_chr_tot = s_chr_n = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * BLOCK_UNIT;
+    const int64_t b1 = min<int64_t>(b0 + BLOCK_UNIT, A.len);
+    unsigned long long tot = 0, at = 0, an = 0, ct = 0, cn = 0;
+    for (int64_t p = b0 + threadIdx.x; p < b1; p += 256) {
+        int r = rd[p] + low[p];
+        if (r > 0) mq[p] = mq[p] / r;
+        tot += r;
+        if (gc_class(ref[p])) { at += r; an += 1; }
+        if (p >= A.lo && p < A.hi && acw[p] >= MIN_ACGT) {
+            ct += r;
+            cn += 1;
+            atomicAdd(&h[min(r, HIST_MAX)], 1u);
+        }
+    }
+    atomicAdd(&s_tot, tot);
+    atomicAdd(&s_acgt_tot, at);
+    atomicAdd(&s_acgt_n, an);
+    atomicAdd(&s_chr_tot, ct);
+    atomicAdd(&s_chr_n, cn);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        blk_total[blockIdx.x] = (int64_t)s_tot;
+        if (s_acgt_tot) atomicAdd(&acc[0], s_acgt_tot);
+        if (s_acgt_n) atomicAdd(&acc[1], s_acgt_n);
+        if (s_chr_tot) atomicAdd(&acc[2], s_chr_tot);
+        if (s_chr_n) atomicAdd(&acc[3], s_chr_n);
+    }
+    for (int i = threadIdx.x; i <= HIST_MAX; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+struct GatherRange {
+    int64_t start, count, stride, out;
+};
+
+// per-position values for host-side steps (sampling, copy number)
+__global__ void k_cnv_gather(const GatherRange *__restrict__ rg, int n_rg, const uint8_t *__restrict__ gcw,
+                             const uint8_t *__restrict__ acw, const int32_t *__restrict__ mq,
+                             const int32_t *__restrict__ rd, const int32_t *__restrict__ low,
+                             const uint8_t *__restrict__ flag, int64_t total, uint8_t *o_gc, uint8_t *o_ac,
+                             int32_t *o_mq, int32_t *o_rd, int32_t *o_low, uint8_t *o_flag) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = n_rg - 1;
+        while (lo < hi) {  // range holding output slot i
+            int mid = (lo + hi + 1) / 2;
+            if (rg[mid].out <= i) lo = mid; else hi = mid - 1;
+        }
+        const GatherRange r = rg[lo];
+        int64_t p = r.start + (i - r.out) * r.stride;
+        o_gc[i] = gcw[p];
+        o_ac[i] = acw[p];
+        o_mq[i] = mq[p];
+        o_rd[i] = rd[p];
+        o_low[i] = low[p];
+        o_flag[i] = flag ? flag[p] : 0;
+    }
+}
+
+// ---- the "last MAPQ class" state scans ----
+// e1(p): GROM.c:18662-18677 -- ACGT-rich base with depth: its class
+__device__ __forceinline__ int ev1(const Args &A, int64_t p, const uint8_t *acw, const int32_t *mq,
+                                   const int32_t *rd, const int32_t *low) {
+    if (p < A.lo || p >= A.hi || acw[p] < MIN_ACGT) return -1;
+    int r = rd[p] + low[p];
+    if (r == 0) return -1;
+    return mq[p] >= A.min_mapq ? 0 : 1;
+}
+// e2(p): GROM.c:18765-18784 -- guarded base that sets the class
+__device__ __forceinline__ int ev2(const Args &A, int64_t p, const uint8_t *flag, const int32_t *mq,
+                                   const int32_t *rd, const int32_t *low) {
+    if (!(flag[p] & F_GUARD)) return -1;
+    if (mq[p] >= A.min_mapq) return 0;
+    if (rd[p] + low[p] == 0) return -1;
+    return 1;
+}
+
+// block-wide "last defined value before me" over the 256 lanes' own last values
+__device__ int block_last_excl(int mine, int carry, int *sh) {
+    const int tid = threadIdx.x;
+    sh[tid] = mine;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        int v = (tid >= d) ? sh[tid - d] : -1;
+        __syncthreads();
+        if (v != -1 && sh[tid] == -1) sh[tid] = v;
+        __syncthreads();
+    }
+    int r = (tid > 0) ? sh[tid - 1] : -1;
+    __syncthreads();
+    return r != -1 ? r : carry;
+}
+
+template <int WHICH>
+__global__ __launch_bounds__(256) void k_cnv_tile_last(Args A, const uint8_t *acw, const uint8_t *flag,
+                                                       const int32_t *mq, const int32_t *rd, const int32_t *low,
+                                                       int8_t *tile_last) {
+    __shared__ int best;
+    if (threadIdx.x == 0) best = -1;
+    __syncthreads();
+    const int64_t p0 = (int64_t)blockIdx.x * SCAN_TP + (int64_t)threadIdx.x * SCAN_K;
+    int last = -1;
+    for (int k = 0; k < SCAN_K; k++) {
+        int64_t p = p0 + k;
+        if (p >= A.len) break;
+        int e = WHICH == 1 ? ev1(A, p, acw, mq, rd, low) : ev2(A, p, flag, mq, rd, low);
+        if (e != -1) last = e;
+    }
+    if (last != -1) atomicMax(&best, (int)threadIdx.x * 4 + last);
+    __syncthreads();
+    if (threadIdx.x == 0) tile_last[blockIdx.x] = best < 0 ? (int8_t)-1 : (int8_t)(best & 3);
+}
+
+// carry[t] = last defined tile value before tile t (0 before the first)
+__global__ __launch_bounds__(1024) void k_cnv_carry(const int8_t *tile_last, int64_t n, int8_t *carry) {
+    __shared__ int seg[1024];
+    const int tid = threadIdx.x;
+    const int64_t per = (n + 1023) / 1024, lo = min<int64_t>(n, tid * per), hi = min<int64_t>(n, lo + per);
+    int l = -1;
+    for (int64_t i = lo; i < hi; i++) if (tile_last[i] != -1) l = tile_last[i];
+    seg[tid] = l;
+    __syncthreads();
+    if (tid == 0) {
+        int c = 0;  // ddd_last_low_mq = 0 at the start (GROM.c:18650, 18740)
+        for (int t = 0; t < 1024; t++) { int v = seg[t]; seg[t] = c; if (v != -1) c = v; }
+    }
+    __syncthreads();
+    int c = seg[tid];
+    for (int64_t i = lo; i < hi; i++) { carry[i] = (int8_t)c; if (tile_last[i] != -1) c = tile_last[i]; }
+}
+
+// flags (GROM.c:18654-18712) and the guard bit of GROM.c:18765
+__global__ __launch_bounds__(256) void k_cnv_flags(Args A, const uint8_t *__restrict__ acw,
+                                                   const uint8_t *__restrict__ gcw, const int32_t *__restrict__ mq,
+                                                   const int32_t *__restrict__ rd, const int32_t *__restrict__ low,
+                                                   const int8_t *__restrict__ carry, const Tables *__restrict__ T,
+                                                   uint8_t *__restrict__ flag) {
+    __shared__ int sh[256];
+    const int64_t p0 = (int64_t)blockIdx.x * SCAN_TP + (int64_t)threadIdx.x * SCAN_K;
+    int mine = -1;
+    for (int k = 0; k < SCAN_K; k++) {
+        int64_t p = p0 + k;
+        if (p >= A.len) break;
+        int e = ev1(A, p, acw, mq, rd, low);
+        if (e != -1) mine = e;
+    }
+    int last = block_last_excl(mine, carry[blockIdx.x], sh);
+    for (int k = 0; k < SCAN_K; k++) {
+        int64_t p = p0 + k;
+        if (p >= A.len) break;
+        uint8_t f = F_LOW;
+        if (p >= A.lo && p < A.hi && acw[p] >= MIN_ACGT) {
+            int r = rd[p] + low[p], mqi;
+            if (r == 0) mqi = last;
+            else if (mq[p] >= A.min_mapq) { mqi = 0; last = 0; }
+            else { mqi = 1; last = 1; }
+            f = (T->wins[mqi][gcw[p]] < NO_COMBINE) ? F_LOW : 0;
+        }
+        if (f == 0) {
+            int g = gcw[p];
+            if ((mq[p] >= A.min_mapq && T->wins[0][g] > 1) || (mq[p] < A.min_mapq && T->wins[1][g] > 1)) f |= F_GUARD;
+        }
+        flag[p] = f;
+    }
+}
+
+// GROM.c:21630-21860, exact
+__device__ long d_bisect_left(const int *l, int rd, long s, long e) {
+    int found = 0;
+    long i = s + (e - s) / 2, lo = s, hi = e;
+    while (found == 0) {
+        if (i <= s) { i = (rd <= l[s]) ? s : s + 1; found = 1; }
+        else if (i >= e - 1) { i = (rd <= l[e - 1]) ? e - 1 : e; found = 1; }
+        else if (rd <= l[i]) { hi = i; i = lo + (i - lo) / 2; if (hi == i) { found = 1; i += 1; } }
+        else { lo = i; i = i + (hi - i) / 2; if (lo == i) { found = 1; i += 1; } }
+    }
+    return i;
+}
+__device__ long d_bisect_right(const int *l, int rd, long s, long e) {
+    int found = 0;
+    long i = s + (e - s) / 2, lo = s, hi = e;
+    while (found == 0) {
+        if (i <= s) { i = (rd < l[s]) ? s : s + 1; found = 1; }
+        else if (i >= e - 1) { i = (rd < l[e - 1]) ? e - 1 : e; found = 1; }
+        else if (rd < l[i]) { hi = i; i = lo + (i - lo) / 2; if (hi == i) { found = 1; i += 1; } }
+        else { lo = i; i = i + (hi - i) / 2; if (lo == i) { found = 1; i += 1; } }
+    }
+    return i;
+}
+__device__ long d_bisect_right_double(const double *l, double p, long s, long e) {
+    int found = 0;
+    long i = s + (e - s) / 2, lo = s, hi = e;
+    while (found == 0) {
+        if (i <= s) { i = (p < l[s]) ? s : s + 1; found = 1; }
+        else if (i >= e - 1) { i = (p < l[e - 1]) ? e - 1 : e; found = 1; }
+        else if (p < l[i]) { hi = i; i = lo + (i - lo) / 2; if (hi == i) { found = 1; i += 1; } }
+        else { lo = i; i = i + (hi - i) / 2; if (lo == i) { found = 1; i += 1; } }
+    }
+    return i;
+}
+
+// per-base z score, GROM.c:18740-18963 (g_normal == 0)
+__global__ __launch_bounds__(256) void k_cnv_z(Args A, const uint8_t *__restrict__ gcw,
+                                               const int32_t *__restrict__ mq, const int32_t *__restrict__ rd,
+                                               const int32_t *__restrict__ low, const uint8_t *__restrict__ flag,
+                                               const int8_t *__restrict__ carry, const Tables *__restrict__ T,
+                                               const int32_t *__restrict__ samples, double *__restrict__ sd) {
+    __shared__ int sh[256];
+    const int64_t p0 = (int64_t)blockIdx.x * SCAN_TP + (int64_t)threadIdx.x * SCAN_K;
+    int mine = -1;
+    for (int k = 0; k < SCAN_K; k++) {
+        int64_t p = p0 + k;
+        if (p >= A.len) break;
+        int e = ev2(A, p, flag, mq, rd, low);
+        if (e != -1) mine = e;
+    }
+    int last = block_last_excl(mine, carry[blockIdx.x], sh);
+    for (int k = 0; k < SCAN_K; k++) {
+        int64_t p = p0 + k;
+        if (p >= A.len) break;
+        double z = 0.0;
+        if (flag[p] & F_GUARD) {
+            const int r = rd[p] + low[p], q = mq[p];
+            int mqi;
+            if (q >= A.min_mapq) { mqi = 0; last = 0; }
+            else if (r == 0) mqi = last;
+            else { mqi = 1; last = 1; }
+            const int bin = gcw[p];
+            const long ge = T->cnt[mqi][bin];
+            if (ge > 0) {
+                const int *list = samples + T->off[mqi][bin];
+                const double ave = T->ave[mqi][bin], sdv = T->sdv[mqi][bin];
+                const double mqf = A.mapq_factor + (1.0 - A.mapq_factor) * (q - A.min_mapq) / (double)(RD_MAX_MAPQ - A.min_mapq);
+                long i1, i2;
+                double d1, d2, prob;
+                if (r < ave) {
+                    i1 = d_bisect_right(list, r, 0, ge);
+                    i2 = d_bisect_left(list, r, 0, ge);
+                    d1 = (i1 <= 0) ? 0.5 : (double)i1;
+                    d2 = (i2 <= 0) ? 0.5 : (double)i2;
+                    prob = (d1 + d2) / (2 * ge);
+                    i1 = d_bisect_right_double(T->p2s_p, prob, 0, T->n_p2s);
+                    if (i1 < 0) i1 = 0; else if (i1 >= T->n_p2s) i1 = T->n_p2s - 1;
+                    if (A.ranks_stdev == 0) z = (q >= A.min_mapq ? mqf : A.mapq_factor) * (ave - rd[p] - low[p]) / sdv;
+                    else z = (q >= A.min_mapq ? mqf : A.mapq_factor) * T->p2s_sd[i1];
+                } else {
+                    const bool over = r > A.dup_factor * ave;
+                    if (over) {
+                        i1 = d_bisect_left(list, (int)(A.dup_factor * ave), 0, ge);  // Q11 truncation
+                        i2 = d_bisect_right(list, r, 0, ge);
+                    } else {
+                        i1 = d_bisect_left(list, r, 0, ge);
+                        i2 = d_bisect_right(list, r, 0, ge);
+                    }
+                    i1 = ge - i1;
+                    i2 = ge - i2;
+                    d1 = (i1 <= 0) ? 0.5 : (double)i1;
+                    d2 = (i2 <= 0) ? 0.5 : (double)i2;
+                    prob = (d1 + d2) / (2 * ge);
+                    i1 = d_bisect_right_double(T->p2s_p, prob, 0, T->n_p2s);
+                    if (i1 < 0) i1 = 0; else if (i1 >= T->n_p2s) i1 = T->n_p2s - 1;
+                    if (A.ranks_stdev == 0) {
+                        if (over) z = (q >= A.min_mapq ? mqf : A.mapq_factor) * (A.dup_factor - 1) * (-ave) / sdv;
+                        else z = (q >= A.min_mapq ? mqf : A.mapq_factor) * (ave - rd[p] - low[p]) / sdv;
+                    } else {
+                        z = -(q >= A.min_mapq ? mqf : A.mapq_factor) * T->p2s_sd[i1];
+                    }
+                }
+            }
+        }
+        sd[p] = z;
+    }
+}
+
+// Window means for every length of one sampled window (GROM.c:18967-19018):
+// one lane per window, its sum accumulated in the reference's order.  A
+// window is up to 3 pieces of consecutive bases (it can straddle the
+// sampling passes of a block).  out row: [min_len..len] means, NaN = none.
+struct WinDesc {
+    int64_t p0, n0, p1, n1, p2, n2;
+    int64_t row;
+};
+__global__ void k_cnv_windows(const WinDesc *__restrict__ wd, int64_t n_win, const uint8_t *__restrict__ flag,
+                              const double *__restrict__ sd, int64_t L, int64_t min_len, double *__restrict__ out) {
+    int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= n_win) return;
+    const WinDesc d = wd[w];
+    double *row = out + d.row * (L + 1);
+    double tot = 0.0;
+    long cnt = 0, ftot = 0, wl = 0;
+    const int64_t ps[3] = {d.p0, d.p1, d.p2}, ns[3] = {d.n0, d.n1, d.n2};
+    for (int s = 0; s < 3; s++) {
+        const int64_t pb = ps[s];
+        for (int64_t k = 0; k < ns[s]; k++) {
+            const int64_t p = pb + k;
+            const uint8_t f = flag[p];
+            if (f & F_GUARD) { tot += sd[p]; cnt += 1; }
+            ftot += (f & F_LOW);
+            wl += 1;
+            if (wl >= min_len) {
+                double v = __builtin_nan("");
+                if ((ftot / (double)wl) < MAX_LOW_ACGT && cnt > 0) v = tot / (double)cnt;
+                row[wl] = v;
+            }
+        }
+    }
+}
+
+// per window length: the sum of squared window means in window order
+// (GROM.c:19162-19170), one lane per length
+__global__ void k_cnv_window_sq(const double *__restrict__ rows, int64_t n_rows, const int64_t *__restrict__ row_len,
+                                int64_t L, int64_t min_len, double *__restrict__ tot, int64_t *__restrict__ cnt) {
+    int64_t l = min_len + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l > L) return;
+    double s = 0.0;
+    int64_t c = 0;
+    for (int64_t r = 0; r < n_rows; r++) {
+        if (row_len[r] < l) continue;
+        double v = rows[r * (L + 1) + l];
+        if (v != v) continue;
+        s += v * v;
+        c += 1;
+    }
+    tot[l] = s;
+    cnt[l] = c;
+}
+
+// ---------------- DEL / DUP window search (GROM.c:19359-20020) ----------------
+struct CallRec {
+    int64_t p, ce;
+    double stdevs;
+    int32_t m, pad;
+};
+
+struct WalkIn {
+    const uint8_t *gcw, *flag;
+    const int32_t *mq, *rd, *low;
+    const double *sd, *wsd;
+    const Tables *T;
+    int64_t len, start, end, L, min_len;
+    int32_t min_mapq;
+};
+
+template <int KIND>
+struct Walk {
+    WalkIn W;
+    __device__ __forceinline__ int rt(int64_t p) const { return W.rd[p] + W.low[p]; }
+    __device__ __forceinline__ bool pass(int64_t p, int m) const {
+        const double t = W.T->thr[KIND][m][W.gcw[p]];
+        return KIND == 0 ? (rt(p) <= t) : (rt(p) >= t);
+    }
+    __device__ __forceinline__ void add(double &x, double v) const { if (KIND == 0) x += v; else x -= v; }
+    __device__ __forceinline__ void sub(double &x, double v) const { if (KIND == 0) x -= v; else x += v; }
+    __device__ __forceinline__ bool lowf(int64_t p) const { return (W.flag[p] & F_LOW) != 0; }
+    // update at a visited base; returns the class (== the state after it)
+    __device__ __forceinline__ int visit(int64_t pos, int &last) const {
+        if (W.mq[pos] >= W.min_mapq) { last = 0; return 0; }
+        if (rt(pos) > 0) { last = 1; return 1; }
+        return last;
+    }
+    // the body of the reference's `if` at a base that passes the threshold:
+    // returns the position the walk continues from (before its `pos += 1`)
+    __device__ int64_t block(int64_t pos, int mqi, CallRec &call, bool &is_call) const {
+        const int64_t L = W.L, ML = W.min_len, end = W.end;
+        const double *wsd = W.wsd;
+        int begin = 0, stop = 0;
+        int64_t cs = 0, ce = 0, last_good = 0, temp_pos = pos, pa, pb, wl = 0, cnt = 0, cnt2 = 0;
+        double stdevs = 0.0, tot = 0.0;
+        for (pa = pos; pa < pos + ML; pa++) {
+            wl += 1;
+            if (!lowf(pa)) {
+                if (W.mq[pa] >= W.min_mapq) mqi = 0;
+                else if (rt(pa) > 0) mqi = 1;
+                if (pass(pa, mqi)) cnt2 += 1;
+                else if ((2 * cnt2) < wl) { stop = 1; temp_pos = pa; break; }
+            } else if ((2 * cnt2) < wl) { stop = 1; temp_pos = pa; break; }
+        }
+        if (stop == 0) {
+            cnt = ML;
+            tot = 0;
+            for (int64_t a = pos; a < pos + ML; a++) {
+                cnt -= (W.flag[a] & F_LOW);
+                add(tot, W.sd[a]);
+            }
+        }
+        if (stop == 0 && cnt > 0 && wsd[ML] > 0 && (tot / (cnt * wsd[ML])) >= MIN_RD_LOW_STDEV &&
+            ((ML - cnt) / ((double)ML)) <= MAX_LOW_ACGT) {
+            begin = 1;
+            cs = pos;
+            last_good = pos + ML;
+            ce = pos + ML;
+            stdevs = tot / (cnt * wsd[ML]);
+        }
+        if (stop == 0) {
+            for (pa = pos + ML; pa < pos + L; pa++) {
+                wl += 1;
+                if (pa < end) {
+                    if (!lowf(pa)) {
+                        if (W.mq[pa] >= W.min_mapq) mqi = 0;
+                        else if (rt(pa) > 0) mqi = 1;
+                        add(tot, W.sd[pa]);
+                        cnt += 1;
+                        if (pass(pa, mqi)) {
+                            cnt2 += 1;
+                            if (wsd[wl] > 0 && (tot / (cnt * wsd[wl])) >= MIN_RD_LOW_STDEV &&
+                                ((wl - cnt) / ((double)wl)) <= MAX_LOW_ACGT) {
+                                last_good = pa;
+                                if (begin == 0) {
+                                    begin = 1;
+                                    cs = pos;
+                                    ce = pa;
+                                    stdevs = tot / (cnt * wsd[wl]);
+                                } else {
+                                    double ts = tot / (cnt * wsd[wl]);
+                                    ce = pa;
+                                    if (ts > stdevs) stdevs = ts;
+                                }
+                            }
+                        } else if ((2 * cnt2) < wl) { stop = 1; break; }
+                    } else if ((2 * cnt2) < wl) { stop = 1; break; }
+                } else { stop = 1; break; }
+            }
+        }
+        if (stop == 0 && begin == 1) {
+            pa = pos + L;
+            tot = 0;
+            cnt = 0;
+            int mqb = mqi;
+            while (pa < W.len && (pa - last_good) <= MAX_DIST_LAST_GOOD) {
+                if (pa == pos + L) {
+                    for (pb = pa - L + 1; pb < pa + 1; pb++) {
+                        if (W.mq[pb] >= W.min_mapq) mqb = 0;
+                        else if (rt(pb) > 0) mqb = 1;
+                        if (!lowf(pb) && W.T->wins[mqb][W.gcw[pb]] > 1) { add(tot, W.sd[pb]); cnt += 1; }
+                    }
+                } else {
+                    pb = pa - L;
+                    if (W.mq[pb] >= W.min_mapq) mqb = 0;
+                    else if (rt(pb) > 0) mqb = 1;
+                    if (!lowf(pb) && W.T->wins[mqb][W.gcw[pb]] > 1) { sub(tot, W.sd[pb]); cnt -= 1; }
+                    if (W.mq[pa] >= W.min_mapq) mqi = 0;
+                    else if (rt(pa) > 0) mqi = 1;
+                    if (!lowf(pa) && W.T->wins[mqi][W.gcw[pa]] > 1) { add(tot, W.sd[pa]); cnt += 1; }
+                }
+                if (cnt > 0 && wsd[L] > 0 && (tot / (cnt * wsd[L])) >= MIN_RD_LOW_STDEV &&
+                    ((L - cnt) / ((double)L)) <= MAX_LOW_ACGT) {
+                    last_good = pa;
+                    ce = pa;
+                    double ts = tot / (cnt * wsd[L]);
+                    if (ts > stdevs) stdevs = ts;
+                }
+                pa += 1;
+            }
+        }
+        is_call = begin == 1;
+        if (begin == 1) {
+            int64_t p = ce;
+            while (p > cs + ML) {
+                if (W.mq[p] >= W.min_mapq) mqi = 0;
+                else if (rt(p) > 0) mqi = 1;
+                if (!pass(p, mqi)) {
+                    p -= 1;
+                    ce = p;
+                } else {
+                    int64_t c2 = 0, c3 = 0;
+                    pa = ce;
+                    int stop_while = 0, mqa = mqi;
+                    while (pa > cs + ML && stop_while == 0) {
+                        if (!lowf(pa)) {
+                            if (W.mq[pa] >= W.min_mapq) mqa = 0;
+                            else if (rt(pa) > 0) mqa = 1;
+                            c3 += 1;
+                            if (pass(pa, mqa)) c2 += 1;
+                        }
+                        if (c3 == 0 || (c3 > 0 && (c2 / ((double)c3)) < 0.5) ||
+                            ((ce - pa + 1 - c3) / ((double)ce - (double)pa + 1.0)) > MAX_LOW_ACGT) {
+                            ce = pa - 1;
+                            stop_while = 1;
+                        }
+                        pa -= 1;
+                    }
+                    p = pa;
+                }
+            }
+            call.p = cs;
+            call.ce = ce;
+            call.stdevs = stdevs;
+            return ce + 1;
+        }
+        return stop == 1 ? temp_pos : pos;
+    }
+};
+
+struct ChunkState {
+    int64_t x1;  // W1 exit position
+    int64_t x2;  // W2/W3 exit position (NOMERGE / redone chunks)
+    int32_t l1, l2, status, pad;
+};
+enum { ST_MERGED = 0, ST_NOMERGE = 1, ST_PASSTHRU = 2, ST_FIRST = 3 };
+
+template <int KIND>
+__device__ void emit_call(const CallRec &c, int m, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
+    uint32_t k = atomicAdd(n_calls, 1u);
+    if (k < cap) {
+        calls[k] = c;
+        calls[k].m = m;
+    }
+}
+
+// walk [from, chunk end) from state (from, last); mode 0: speculative first
+// pass (marks, calls); mode 1: reconciliation of chunk k from the previous
+// chunk's speculative exit.  vis[p] = 1 + class for every visited base.
+template <int KIND>
+__global__ void k_cnv_walk(WalkIn W, int mode, int64_t n_chunks, int64_t chunk, uint8_t *__restrict__ vis,
+                           ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_chunks) return;
+    Walk<KIND> w{W};
+    const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
+    if (mode == 0) {
+        int64_t pos = c0;
+        int last = 0;  // a guess except for chunk 0 (GROM.c:19366-19367)
+        while (pos < c1) {
+            int m = w.visit(pos, last);
+            vis[pos] = (uint8_t)(1 + m);
+            if (w.pass(pos, m)) {
+                CallRec c;
+                bool is_call = false;
+                pos = w.block(pos, m, c, is_call);
+                if (is_call) emit_call<KIND>(c, m, calls, n_calls, cap);
+            }
+            pos += 1;
+        }
+        cs[k].x1 = pos;
+        cs[k].l1 = last;
+        cs[k].status = k == 0 ? ST_FIRST : ST_MERGED;
+        return;
+    }
+    if (k == 0) return;
+    // mode 1: enter from chunk k-1's speculative exit
+    const int64_t x = cs[k - 1].x1;
+    const int l = cs[k - 1].l1;
+    if (x >= c1) {  // chunk k lies inside a jump of chunk k-1
+        for (int64_t p = c0; p < c1; p++) vis[p] = 0;
+        cs[k].status = ST_PASSTHRU;
+        return;
+    }
+    // pass 1: find the first base both walks visit in the same state
+    int64_t pos = x, merge = -1;
+    int last = l;
+    while (pos < c1) {
+        int m = w.visit(pos, last);
+        if (vis[pos] == 1 + m) { merge = pos; break; }
+        if (w.pass(pos, m)) {
+            CallRec c;
+            bool is_call = false;
+            pos = w.block(pos, m, c, is_call);
+        }
+        pos += 1;
+    }
+    const int64_t stop_at = merge >= 0 ? merge : c1;
+    for (int64_t p = c0; p < stop_at; p++) vis[p] = 0;
+    // pass 2: the true walk up to the merge point, with marks and calls
+    pos = x;
+    last = l;
+    while (pos < stop_at) {
+        int m = w.visit(pos, last);
+        vis[pos] = (uint8_t)(1 + m);
+        if (w.pass(pos, m)) {
+            CallRec c;
+            bool is_call = false;
+            pos = w.block(pos, m, c, is_call);
+            if (is_call) emit_call<KIND>(c, m, calls, n_calls, cap);
+        }
+        pos += 1;
+    }
+    if (merge >= 0) {
+        cs[k].status = ST_MERGED;
+    } else {
+        cs[k].status = ST_NOMERGE;
+        cs[k].x2 = pos;
+        cs[k].l2 = last;
+    }
+}
+
+// sequential repair of one chunk from a known-true entry (rare: only after a
+// pass-through or a chunk whose walks never met)
+template <int KIND>
+__global__ void k_cnv_walk_fix(WalkIn W, int64_t k, int64_t chunk, int64_t x, int l, uint8_t *__restrict__ vis,
+                               ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    Walk<KIND> w{W};
+    const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
+    for (int64_t p = c0; p < c1; p++) vis[p] = 0;
+    int64_t pos = x;
+    int last = l;
+    while (pos < c1) {
+        int m = w.visit(pos, last);
+        vis[pos] = (uint8_t)(1 + m);
+        if (w.pass(pos, m)) {
+            CallRec c;
+            bool is_call = false;
+            pos = w.block(pos, m, c, is_call);
+            if (is_call) emit_call<KIND>(c, m, calls, n_calls, cap);
+        }
+        pos += 1;
+    }
+    cs[k].x2 = pos;
+    cs[k].l2 = last;
+}
+
+// a call is on the true walk iff its start was visited in its class
+__global__ void k_cnv_calls_valid(const CallRec *calls, uint32_t n, const uint8_t *vis, uint8_t *ok) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    ok[i] = vis[calls[i].p] == 1 + calls[i].m;
+}
+
+// ---------------- host side ----------------
+struct Buf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+}  // namespace
+
+struct CnvScratch {
+    Buf gcw, acw, rtype, flag, sd, vis, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
+        rowlen, wtot, wcnt, wsd, calls, ok;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+namespace {
+
+#define CK(x)                                                                                       \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) {                                                                     \
+            snprintf(err, errlen, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return GROM_E_HIP;                                                                      \
+        }                                                                                           \
+    } while (0)
+
+static int grow(Buf &b, size_t bytes, char *err, size_t errlen) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return GROM_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = bytes + bytes / 8 + 256;
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        snprintf(err, errlen, "hipMalloc(%zu) failed in the CNV path", want);
+        return GROM_E_NOMEM;
+    }
+    b.cap = want;
+    return GROM_OK;
+}
+
+// glibc random()/rand() (TYPE_3, stdlib/random_r.c) for grom_rand, GROM.c:1185
+struct GlibcRand {
+    int32_t st[31];
+    int f = 3, r = 0;
+    explicit GlibcRand(uint32_t seed) {
+        if (seed == 0) seed = 1;
+        st[0] = (int32_t)seed;
+        long word = seed;
+        for (int i = 1; i < 31; i++) {
+            long hi = word / 127773, lo = word % 127773;
+            word = 16807 * lo - 2836 * hi;
+            if (word < 0) word += 2147483647;
+            st[i] = (int32_t)word;
+        }
+        for (int i = 0; i < 310; i++) next();
+    }
+    int next() {
+        uint32_t v = (uint32_t)st[f] + (uint32_t)st[r];
+        st[f] = (int32_t)v;
+        if (++f >= 31) { f = 0; ++r; } else if (++r >= 31) r = 0;
+        return (int)(v >> 1);
+    }
+    long grom_rand(long mx) {  // GROM.c:1185-1201
+        long v = 0, c = 1, t;
+        while (c < mx) {
+            t = (next() % 10) * c;
+            while (t + v >= mx) t = (next() % 10) * c;
+            v += t;
+            c *= 10;
+        }
+        return v;
+    }
+};
+
+// qsort(double[], cmpfunc) of glibc 2.12 (msort.c) with the reference's int
+// comparator reading each double's low 32 bits
+static int dcmp_lo(double a, double b) {
+    uint32_t x, y;
+    memcpy(&x, &a, 4);
+    memcpy(&y, &b, 4);
+    return (int32_t)(x - y);
+}
+static void msort_lo(double *b, size_t n, double *t) {
+    if (n <= 1) return;
+    size_t n1 = n / 2, n2 = n - n1;
+    double *b1 = b, *b2 = b + n1;
+    msort_lo(b1, n1, t);
+    msort_lo(b2, n2, t);
+    double *o = t;
+    while (n1 > 0 && n2 > 0) {
+        if (dcmp_lo(*b1, *b2) <= 0) { *o++ = *b1++; --n1; }
+        else { *o++ = *b2++; --n2; }
+    }
+    if (n1 > 0) memcpy(o, b1, n1 * sizeof(double));
+    memcpy(b, t, (n - n2) * sizeof(double));
+}
+
+struct Gathered {
+    std::vector<uint8_t> gc, ac, flag;
+    std::vector<int32_t> mq, rt, rd, low;
+};
+
+static int gather(CnvScratch *S, hipStream_t st, const std::vector<GatherRange> &rg, int64_t total, const uint8_t *gcw,
+                  const uint8_t *acw, const int32_t *mq, const int32_t *rd, const int32_t *low, const uint8_t *flag,
+                  Gathered &g, char *err, size_t errlen) {
+    g.gc.resize(total);
+    g.ac.resize(total);
+    g.flag.resize(total);
+    g.mq.resize(total);
+    g.rt.resize(total);
+    g.rd.resize(total);
+    g.low.resize(total);
+    if (total == 0 || rg.empty()) return GROM_OK;
+    int rc;
+    if ((rc = grow(S->gat_rg, sizeof(GatherRange) * rg.size(), err, errlen)) ||
+        (rc = grow(S->gat, (size_t)total * 15, err, errlen)))
+        return rc;
+    CK(hipMemcpyAsync(S->gat_rg.p, rg.data(), sizeof(GatherRange) * rg.size(), hipMemcpyHostToDevice, st));
+    uint8_t *o = (uint8_t *)S->gat.p;
+    int32_t *o_mq = (int32_t *)o, *o_rd = o_mq + total, *o_low = o_rd + total;
+    uint8_t *o_gc = (uint8_t *)(o_low + total), *o_ac = o_gc + total, *o_f = o_ac + total;
+    int g_ = (int)std::min<int64_t>((total + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_cnv_gather, dim3(g_), dim3(256), 0, st, (const GatherRange *)S->gat_rg.p, (int)rg.size(), gcw,
+                       acw, mq, rd, low, flag, total, o_gc, o_ac, o_mq, o_rd, o_low, o_f);
+    CK(hipGetLastError());
+    CK(hipMemcpyAsync(g.mq.data(), o_mq, 4 * total, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(g.rd.data(), o_rd, 4 * total, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(g.low.data(), o_low, 4 * total, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(g.gc.data(), o_gc, total, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(g.ac.data(), o_ac, total, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(g.flag.data(), o_f, total, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    for (int64_t i = 0; i < total; i++) g.rt[i] = g.rd[i] + g.low[i];
+    return GROM_OK;
+}
+
+}  // namespace
+
+CnvScratch *cnv_scratch_new() { return new CnvScratch(); }
+
+void cnv_scratch_free(CnvScratch *S) {
+    if (!S) return;
+    Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->rep, &S->misc, &S->blk, &S->hist,
+                  &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
+                  &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok};
+    for (Buf *b : all)
+        if (b->p) (void)hipFree(b->p);
+    if (S->e0) (void)hipEventDestroy(S->e0);
+    if (S->e1) (void)hipEventDestroy(S->e1);
+    delete S;
+}
+
+int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed, const char *chr_name,
+              const char *d_ref, int64_t len, int32_t *d_mq, const int32_t *d_rd, const int32_t *d_low,
+              std::string &rows, CnvTiming *timing, char *err, size_t errlen) {
+    const auto t_host0 = std::chrono::steady_clock::now();
+    int rc;
+    const int64_t m = P.insert_mean, W = 2 * (int64_t)m - 1;
+    const int64_t total_w = (int64_t)m * m;  // g_one_base_window_size_total, GROM.c:22265-22269
+    if (m < 1 || m > GC_MMAX) {
+        snprintf(err, errlen, "insert mean %lld outside the CNV kernels' range 1..%d", (long long)m, GC_MMAX);
+        return GROM_E_ARG;
+    }
+    if (P.max_rd_window_len < P.min_rd_window_len || P.min_rd_window_len < 1 || P.windows_sampling_factor < 1 ||
+        P.max_rd_window_len > 1000000) {
+        snprintf(err, errlen, "unsupported CNV window parameters (-W %lld -X %lld -A %lld)",
+                 (long long)P.min_rd_window_len, (long long)P.max_rd_window_len, (long long)P.windows_sampling_factor);
+        return GROM_E_ARG;
+    }
+    if (!S->e0) {
+        CK(hipEventCreate(&S->e0));
+        CK(hipEventCreate(&S->e1));
+    }
+    GlibcRand rng(seed);
+    Args A{};
+    A.len = len;
+    A.lo = m - 1;
+    A.hi = std::max<int64_t>(A.lo, len - W);
+    A.min_mapq = P.rd_min_mapq;
+    A.ranks_stdev = P.ranks_stdev;
+    A.mapq_factor = P.mapq_factor;
+    A.dup_factor = (double)P.dup_threshold_factor;
+    const int64_t n_blk = len / BLOCK_UNIT;
+    const int64_t n_scan = (len + SCAN_TP - 1) / SCAN_TP;
+    if ((rc = grow(S->gcw, len, err, errlen)) || (rc = grow(S->acw, len, err, errlen)) ||
+        (rc = grow(S->rtype, len, err, errlen)) || (rc = grow(S->flag, len, err, errlen)) ||
+        (rc = grow(S->sd, 8 * len, err, errlen)) || (rc = grow(S->vis, len, err, errlen)) ||
+        (rc = grow(S->misc, 4096, err, errlen)) || (rc = grow(S->blk, 8 * (n_blk + 1), err, errlen)) ||
+        (rc = grow(S->hist, 4 * (HIST_MAX + 1), err, errlen)) || (rc = grow(S->tiles, n_scan, err, errlen)) ||
+        (rc = grow(S->carry, n_scan, err, errlen)) || (rc = grow(S->tabs, sizeof(Tables), err, errlen)))
+        return rc;
+    uint8_t *gcw = (uint8_t *)S->gcw.p, *acw = (uint8_t *)S->acw.p, *rtype = (uint8_t *)S->rtype.p,
+            *flag = (uint8_t *)S->flag.p;
+    double *sd = (double *)S->sd.p;
+    char *misc = (char *)S->misc.p;
+    unsigned long long *acc = (unsigned long long *)misc;  // [0..3] block/chromosome sums
+    uint32_t *n_rep = (uint32_t *)(misc + 64), *n_calls = (uint32_t *)(misc + 68);
+    CK(hipEventRecord(S->e0, st));
+    CK(hipMemsetAsync(misc, 0, 128, st));
+    CK(hipMemsetAsync(S->hist.p, 0, 4 * (HIST_MAX + 1), st));
+
+    // ---- A14: weighted GC / ACGT and repeat classes ----
+    hipLaunchKernelGGL(k_cnv_gc, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, st, d_ref, A, (int)m,
+                       total_w, gcw, acw, rtype);
+    CK(hipGetLastError());
+    // ---- A15: mapq division, blocks, chromosome depth ----
+    hipLaunchKernelGGL(k_cnv_blocks, dim3((unsigned)(n_blk + 1)), dim3(256), 0, st, d_ref, A, d_mq, d_rd, d_low, acw,
+                       (int64_t *)S->blk.p, acc, (unsigned int *)S->hist.p);
+    CK(hipGetLastError());
+    uint32_t rep_cap = (uint32_t)std::min<int64_t>(len / std::max<int64_t>(P.min_repeat, 1) + 1, 1 << 24);
+    if ((rc = grow(S->rep, sizeof(RepeatRec) * rep_cap, err, errlen))) return rc;
+    if (A.hi > A.lo)
+        hipLaunchKernelGGL(k_cnv_repeats, dim3((unsigned)((A.hi - A.lo + 255) / 256)), dim3(256), 0, st, rtype, d_rd,
+                           d_low, A, P.min_repeat, (RepeatRec *)S->rep.p, n_rep, rep_cap);
+    CK(hipGetLastError());
+    unsigned long long hacc[4];
+    uint32_t hnrep = 0;
+    std::vector<int64_t> blk_total(n_blk + 1);
+    std::vector<unsigned int> hist(HIST_MAX + 1);
+    CK(hipMemcpyAsync(hacc, acc, 32, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(&hnrep, n_rep, 4, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(blk_total.data(), S->blk.p, 8 * (n_blk + 1), hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(hist.data(), S->hist.p, 4 * (HIST_MAX + 1), hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    if (hnrep > rep_cap) {
+        snprintf(err, errlen, "repeat list overflow (%u > %u)", hnrep, rep_cap);
+        return GROM_E_OVERFLOW;
+    }
+    std::vector<RepeatRec> reps(hnrep);
+    if (hnrep) CK(hipMemcpy(reps.data(), S->rep.p, sizeof(RepeatRec) * hnrep, hipMemcpyDeviceToHost));
+    std::sort(reps.begin(), reps.end(), [](const RepeatRec &a, const RepeatRec &b) { return a.start < b.start; });
+
+    // chromosome depth mean / stdev over ACGT-rich bases, GROM.c:16645-16684
+    double chr_ave = 0, chr_sd = 0;
+    const long chr_cnt = (long)hacc[3];
+    if (chr_cnt > 0) chr_ave = (double)hacc[2] / chr_cnt;
+    if (hist[HIST_MAX] != 0 && 2 * chr_ave > HIST_MAX) {
+        snprintf(err, errlen, "read depth above %d: outside the CNV histogram", HIST_MAX);
+        return GROM_E_ARG;
+    }
+    for (int v = 0; v < HIST_MAX; v++) {
+        if (!hist[v]) continue;
+        double term = (v < 2 * chr_ave) ? (v - chr_ave) * (v - chr_ave) : chr_ave * chr_ave;
+        chr_sd += term * hist[v];
+    }
+    chr_sd += (double)hist[HIST_MAX] * chr_ave * chr_ave;
+    chr_sd = chr_cnt > 1 ? sqrt(chr_sd / ((double)chr_cnt - 1.0)) : 0;
+    // repeat-type depth and the most biased repeat, GROM.c:16686-16775
+    double rave[10] = {0}, rsd[10] = {0};
+    long rcnt[10] = {0};
+    std::vector<double> rrl(reps.size());
+    for (size_t i = 0; i < reps.size(); i++) {
+        rrl[i] = (double)reps[i].rd / (reps[i].end - reps[i].start);
+        rave[reps[i].type] += (rrl[i] < 2 * chr_ave) ? rrl[i] : 2 * chr_ave;
+        rcnt[reps[i].type] += 1;
+    }
+    for (int t = 0; t < 10; t++) rave[t] = rave[t] / (double)rcnt[t];
+    for (size_t i = 0; i < reps.size(); i++) {
+        int t = reps[i].type;
+        double v = (rrl[i] < 2 * chr_ave) ? rrl[i] : 2 * chr_ave;
+        rsd[t] += (v - rave[t]) * (v - rave[t]);
+    }
+    for (int t = 0; t < 10; t++) rsd[t] = rcnt[t] > 1 ? sqrt(rsd[t] / ((double)rcnt[t] - 1.0)) : 0;
+    int biased = -1;
+    long biased_cnt = 0;
+    for (int t = 0; t < 10; t++)
+        if (rcnt[t] > NO_COMBINE && (rave[t] + (P.min_repeat_stdev * rsd[t])) < chr_ave &&
+            (chr_ave - (P.min_repeat_stdev * chr_sd)) > rave[t] && rcnt[t] > biased_cnt) {
+            biased = t;
+            biased_cnt = rcnt[t];
+        }
+    // 10 kb blocks over twice the mean depth -> low-variance sample blocks, GROM.c:16784-16993
+    const double chr_rd_ave = (double)hacc[0] / (double)hacc[1];
+    const double chr_rd_thr = P.chr_rd_threshold_factor * chr_rd_ave;
+    std::vector<long> over;
+    for (int64_t b = 0; b < n_blk; b++)
+        if (blk_total[b] / (double)BLOCK_UNIT > chr_rd_thr) over.push_back((long)b);
+    std::vector<long> bs(MAX_BLOCK_LIST), be(MAX_BLOCK_LIST);
+    long tb = 0, tbs = 0, tbe = 0, nbk = 0;
+    for (size_t a = 1; a < over.size(); a++) {
+        if (tb == 0) {
+            if ((tb + 1) > ((over[a] - over[a - 1]) / BLOCK_FACTOR)) { tbe = over[a] + 1; tb += 1; }
+            else tbe = over[a - 1] + 1;
+            tbs = over[a - 1];
+            tb += 1;
+        } else {
+            if ((tb + 1) > ((over[a - 1] - tbs) / BLOCK_FACTOR)) { tbe = over[a - 1] + 1; tb += 1; }
+            else {
+                if (tb >= P.min_blocks) nbk += 1;
+                tb = 1;
+                tbs = over[a - 1];
+                tbe = over[a - 1] + 1;
+            }
+            if (tb >= P.min_blocks && nbk < MAX_BLOCK_LIST) {
+                bs[nbk] = tbs * BLOCK_UNIT;
+                be[nbk] = tbe * BLOCK_UNIT;
+            }
+        }
+    }
+    if (tb >= P.min_blocks) nbk += 1;
+    std::vector<long> ls(1, 0), le;
+    for (long a = 0; a < nbk && a < MAX_BLOCK_LIST; a++)
+        if (be[a] - bs[a] >= P.block_min) { le.push_back(bs[a]); ls.push_back(be[a]); }
+    le.push_back(len);
+    for (size_t k = 0; k < ls.size(); k++) {
+        for (long *v : {&ls[k], &le[k]}) {
+            if (*v < m - 1) *v = m - 1;
+            else if (*v >= len - W) *v = len - W;
+        }
+    }
+    std::vector<long> ss, se;  // g_lowvar_block_sample_*_list
+    for (size_t k = 0; k < ls.size(); k++)
+        if (!(le[k] - ls[k] < P.min_rd_window_len)) { ss.push_back(ls[k]); se.push_back(le[k]); }
+
+    // ---- A16: GC-bin samples every insert_mean/2 bases, GROM.c:18373-18456 ----
+    const long half = m / 2;
+    Tables T{};
+    std::vector<std::vector<int>> smp[2];
+    smp[0].assign(NBINS, {});
+    smp[1].assign(NBINS, {});
+    long idx[2][NBINS] = {{0}}, all[2][NBINS] = {{0}};
+    {
+        std::vector<GatherRange> rg;
+        int64_t tot = 0;
+        for (size_t b = 0; b < ss.size(); b++) {
+            if (se[b] <= ss[b] || half <= 0) continue;
+            int64_t c = (se[b] - ss[b] + half - 1) / half;
+            rg.push_back(GatherRange{ss[b], c, half, tot});
+            tot += c;
+        }
+        Gathered g;
+        if ((rc = gather(S, st, rg, tot, gcw, acw, d_mq, d_rd, d_low, nullptr, g, err, errlen))) return rc;
+        int last_low = 0;
+        auto push = [&](int k, int bin, int v) {
+            if (idx[k][bin] < SAMPLE_LEN) {
+                smp[k][bin].push_back(v);
+                idx[k][bin] += 1;
+                all[k][bin] += 1;
+            } else {
+                if (rng.grom_rand(all[k][bin]) == 0) smp[k][bin][rng.grom_rand(idx[k][bin])] = v;
+                all[k][bin] += 1;
+            }
+        };
+        // (the most-biased-repeat samples come first in the reference and draw
+        // from the same generator, GROM.c:18284-18330)
+        std::vector<std::vector<int>> rsmp(REP_SEGS);
+        long mb_idx[REP_SEGS] = {0}, mb_all[REP_SEGS] = {0};
+        Gathered rgth;
+        std::vector<GatherRange> rrg;
+        if (biased != -1) {
+            int64_t rt_ = 0;
+            for (auto &r : reps)
+                if (r.type == biased) {
+                    rrg.push_back(GatherRange{r.start - half, r.end - r.start + 2 * half, 1, rt_});
+                    rt_ += r.end - r.start + 2 * half;
+                }
+            if ((rc = gather(S, st, rrg, rt_, gcw, acw, d_mq, d_rd, d_low, nullptr, rgth, err, errlen))) return rc;
+            for (auto &x : rrg) {
+                const int64_t rs = x.start + half, re = x.start + x.count - half;
+                for (int64_t i = 0; i < x.count; i++) {
+                    const int64_t pos = x.start + i, o = x.out + i;
+                    if (rgth.ac[o] < MIN_ACGT) continue;
+                    int seg;
+                    if (pos < rs) seg = (int)((REP_SEGS - 1) * (pos - (rs - half)) / half);
+                    else if (pos >= re) seg = (int)((REP_SEGS - 1) * ((re + half) - pos) / half);
+                    else seg = REP_SEGS - 1;
+                    if (mb_idx[seg] < SAMPLE_LEN) {
+                        rsmp[seg].push_back(rgth.rt[o]);
+                        mb_idx[seg]++;
+                        mb_all[seg]++;
+                    } else {
+                        if (rng.grom_rand(mb_all[seg]) == 0) rsmp[seg][rng.grom_rand(mb_idx[seg])] = rgth.rt[o];
+                        mb_all[seg]++;
+                    }
+                }
+            }
+        }
+        for (int64_t i = 0; i < tot; i++) {
+            if (g.ac[i] < MIN_ACGT) continue;
+            const int bin = g.gc[i], v = g.rt[i];
+            if (v == 0) push(last_low, bin, v);
+            else if (g.mq[i] >= P.rd_min_mapq) { push(0, bin, v); last_low = 0; }
+            else { push(1, bin, v); last_low = 1; }
+        }
+        for (int k = 0; k < 2; k++)
+            for (int b = 0; b < NBINS; b++) std::sort(smp[k][b].begin(), smp[k][b].end());
+        // thin bins borrow their +-2 neighbours' samples, GROM.c:18480-18548
+        for (int k = 0; k < 2; k++) {
+            std::vector<std::vector<int>> add(NBINS);
+            bool thin[NBINS];
+            for (int b = 0; b < NBINS; b++)
+                thin[b] = b >= 2 && b < NBINS - 2 && idx[k][b] >= RD_MIN_WINDOWS && idx[k][b] < NO_COMBINE;
+            for (int b = 0; b < NBINS; b++) {
+                if (!thin[b]) continue;
+                long n = idx[k][b];
+                for (int a = b - 2; a <= b + 2; a++)
+                    if (a != b)
+                        for (long j = 0; j < idx[k][a] && n < SAMPLE_LEN; j++, n++) add[b].push_back(smp[k][a][j]);
+            }
+            for (int b = 0; b < NBINS; b++)
+                if (thin[b]) {
+                    smp[k][b].insert(smp[k][b].end(), add[b].begin(), add[b].end());
+                    idx[k][b] = (long)smp[k][b].size();
+                    std::sort(smp[k][b].begin(), smp[k][b].end());
+                }
+        }
+        // repeat-segment statistics, GROM.c:18336-18367 (only with a biased repeat)
+        double rp_ave[REP_SEGS] = {0}, rp_sd[REP_SEGS] = {0};
+        if (biased != -1) {
+            for (int r = 0; r < REP_SEGS; r++) {
+                std::sort(rsmp[r].begin(), rsmp[r].end());
+                if (mb_idx[r] > 0) {
+                    long s0 = mb_idx[r] / 20, e0 = mb_idx[r] - s0, n0 = e0 - s0;
+                    for (long a = s0; a < e0; a++) rp_ave[r] += rsmp[r][a];
+                    rp_ave[r] = rp_ave[r] / n0;
+                    for (long a = s0; a < e0; a++) rp_sd[r] += pow((rsmp[r][a] - rp_ave[r]), 2);
+                    if (n0 > 1) rp_sd[r] = sqrt(rp_sd[r] / (n0 - 1));
+                }
+            }
+        }
+        // bin statistics, GROM.c:18560-18641
+        const double del_f = (1.0 - PLOIDY_NUM / P.ploidy), dup_f = (1.0 + PLOIDY_NUM / P.ploidy);
+        std::vector<int32_t> flat;
+        for (int k = 0; k < 2; k++)
+            for (int b = 0; b < NBINS; b++) {
+                const long n = idx[k][b];
+                const std::vector<int> &l = smp[k][b];
+                T.off[k][b] = (int32_t)flat.size();
+                T.cnt[k][b] = (int32_t)n;
+                flat.insert(flat.end(), l.begin(), l.end());
+                if (n > 0) {
+                    double a = 0.0;
+                    for (long j = 0; j < n; j++) a += l[j];
+                    a = a / n;
+                    double s = 0.0;
+                    for (long j = 0; j < n; j++) s += pow((l[j] - a), 2);
+                    if (n > 1) s = sqrt(s / (n - 1));
+                    T.ave[k][b] = a;
+                    T.sdv[k][b] = s;
+                    T.thr[0][k][b] = del_f * a;
+                    T.thr[1][k][b] = dup_f * a;
+                    T.wins[k][b] = n;
+                }
+            }
+        // pval2sd, find_disc_svs GROM.c:20705-20748
+        {
+            const double pp = 0.3275911, a1 = 0.254829592, a2 = -0.284496736, a3 = 1.421413741, a4 = -1.453152027,
+                         a5 = 1.061405429, sd_max = 10.0;
+            int n = (int)(sd_max / STDEV_STEP + 0.5) + 1;
+            T.n_p2s = n;
+            for (int k = 0; k < n; k++) {
+                double s = sd_max - k * STDEV_STEP;
+                if (s < 0) s = 0;
+                double x = s / sqrt(2.0), t = 1.0 / (1.0 + pp * x);
+                double e = 1.0 - ((a1 * t + a2 * pow(t, 2) + a3 * pow(t, 3) + a4 * pow(t, 4) + a5 * pow(t, 5)) *
+                                  exp(-pow(x, 2)));
+                T.p2s_p[k] = (1.0 - e) / 2.0;
+                T.p2s_sd[k] = s;
+            }
+        }
+        if ((rc = grow(S->samples, 4 * (flat.size() + 1), err, errlen))) return rc;
+        if (!flat.empty())
+            CK(hipMemcpyAsync(S->samples.p, flat.data(), 4 * flat.size(), hipMemcpyHostToDevice, st));
+        CK(hipMemcpyAsync(S->tabs.p, &T, sizeof(Tables), hipMemcpyHostToDevice, st));
+        const Tables *dT = (const Tables *)S->tabs.p;
+
+        // ---- flags, z scores ----
+        int8_t *tl = (int8_t *)S->tiles.p, *cr = (int8_t *)S->carry.p;
+        hipLaunchKernelGGL(k_cnv_tile_last<1>, dim3((unsigned)n_scan), dim3(256), 0, st, A, acw, flag, d_mq, d_rd,
+                           d_low, tl);
+        hipLaunchKernelGGL(k_cnv_carry, dim3(1), dim3(1024), 0, st, tl, n_scan, cr);
+        hipLaunchKernelGGL(k_cnv_flags, dim3((unsigned)n_scan), dim3(256), 0, st, A, acw, gcw, d_mq, d_rd, d_low, cr,
+                           dT, flag);
+        hipLaunchKernelGGL(k_cnv_tile_last<2>, dim3((unsigned)n_scan), dim3(256), 0, st, A, acw, flag, d_mq, d_rd,
+                           d_low, tl);
+        hipLaunchKernelGGL(k_cnv_carry, dim3(1), dim3(1024), 0, st, tl, n_scan, cr);
+        hipLaunchKernelGGL(k_cnv_z, dim3((unsigned)n_scan), dim3(256), 0, st, A, gcw, d_mq, d_rd, d_low, flag, cr, dT,
+                           (const int32_t *)S->samples.p, sd);
+        CK(hipGetLastError());
+
+        // ---- window means by length, GROM.c:18967-19018 ----
+        const int64_t L = P.max_rd_window_len, F = P.windows_sampling_factor, ML = P.min_rd_window_len;
+        std::vector<WinDesc> wds;
+        std::vector<int64_t> rlen;
+        long twc = 0;  // ddd_temp_win_count carries across blocks
+        for (size_t b = 0; b < ss.size(); b++) {
+            std::vector<std::pair<int64_t, int64_t>> segs;  // (start, count) of each sampling pass
+            for (int64_t s = 0; s < F; s++) {
+                int64_t a = ss[b] + s * L / F;
+                if (a < se[b]) segs.push_back({a, se[b] - a});
+            }
+            // chop the concatenation into windows of L
+            size_t si = 0;
+            int64_t so = 0;
+            while (si < segs.size()) {
+                WinDesc d{};
+                int64_t need = L, got = 0;
+                int np = 0;
+                int64_t *pp[3] = {&d.p0, &d.p1, &d.p2}, *nn[3] = {&d.n0, &d.n1, &d.n2};
+                while (need > 0 && si < segs.size()) {
+                    int64_t take = std::min(need, segs[si].second - so);
+                    if (np == 3) break;
+                    *pp[np] = segs[si].first + so;
+                    *nn[np] = take;
+                    np++;
+                    so += take;
+                    need -= take;
+                    got += take;
+                    if (so == segs[si].second) { si++; so = 0; }
+                }
+                if (np == 3 && need > 0 && si < segs.size()) {
+                    snprintf(err, errlen, "CNV window spans more than 3 sampling pieces (block too short for -A)");
+                    return GROM_E_ARG;
+                }
+                if (twc == 0 && got >= ML) {
+                    d.row = (int64_t)wds.size();
+                    wds.push_back(d);
+                    rlen.push_back(got);
+                }
+                if (got == L) { twc += 1; if (twc == REDUCTION) twc = 0; }
+            }
+        }
+        const int64_t n_win = (int64_t)wds.size();
+        if ((rc = grow(S->wd, sizeof(WinDesc) * (n_win + 1), err, errlen)) ||
+            (rc = grow(S->rows, 8 * (size_t)std::max<int64_t>(n_win, 1) * (L + 1), err, errlen)) ||
+            (rc = grow(S->rowlen, 8 * (n_win + 1), err, errlen)) || (rc = grow(S->wtot, 8 * (L + 1), err, errlen)) ||
+            (rc = grow(S->wcnt, 8 * (L + 1), err, errlen)) || (rc = grow(S->wsd, 8 * (L + 1), err, errlen)))
+            return rc;
+        std::vector<double> wtot(L + 1, 0.0), wsd(L + 1, 0.0);
+        std::vector<int64_t> wcnt(L + 1, 0);
+        if (n_win > 0) {
+            CK(hipMemcpyAsync(S->wd.p, wds.data(), sizeof(WinDesc) * n_win, hipMemcpyHostToDevice, st));
+            CK(hipMemcpyAsync(S->rowlen.p, rlen.data(), 8 * n_win, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_cnv_windows, dim3((unsigned)((n_win + 63) / 64)), dim3(64), 0, st,
+                               (const WinDesc *)S->wd.p, n_win, flag, sd, L, ML, (double *)S->rows.p);
+            hipLaunchKernelGGL(k_cnv_window_sq, dim3((unsigned)((L - ML + 1 + 63) / 64)), dim3(64), 0, st,
+                               (const double *)S->rows.p, n_win, (const int64_t *)S->rowlen.p, L, ML,
+                               (double *)S->wtot.p, (int64_t *)S->wcnt.p);
+            CK(hipGetLastError());
+            CK(hipMemcpyAsync(wtot.data(), S->wtot.p, 8 * (L + 1), hipMemcpyDeviceToHost, st));
+            CK(hipMemcpyAsync(wcnt.data(), S->wcnt.p, 8 * (L + 1), hipMemcpyDeviceToHost, st));
+            CK(hipStreamSynchronize(st));
+        }
+        for (int64_t l = ML; l <= L; l++) wsd[l] = wcnt[l] > 1 ? sqrt(wtot[l] / (wcnt[l] - 1)) : 0.0;  // GROM.c:19162
+
+        // ---- most-biased repeat z override, GROM.c:19022-19150 ----
+        if (biased != -1 && !rrg.empty()) {
+            Gathered rg2;
+            int64_t rt_ = rrg.back().out + rrg.back().count;
+            if ((rc = gather(S, st, rrg, rt_, gcw, acw, d_mq, d_rd, d_low, flag, rg2, err, errlen))) return rc;
+            std::vector<double> zv(rt_);
+            std::vector<int64_t> zp(rt_);
+            int64_t nz = 0;
+            for (auto &x : rrg) {
+                const int64_t rs = x.start + half, re = x.start + x.count - half;
+                for (int64_t i = 0; i < x.count; i++) {
+                    const int64_t pos = x.start + i, o = x.out + i;
+                    int seg;
+                    if (pos < rs) seg = (int)((REP_SEGS - 1) * (pos - (rs - half)) / half);
+                    else if (pos >= re) seg = (int)((REP_SEGS - 1) * ((re + half) - pos) / half);
+                    else seg = REP_SEGS - 1;
+                    if (rg2.flag[o] & F_LOW) continue;
+                    const long n = mb_idx[seg];
+                    const int *l = rsmp[seg].data();
+                    const int r = rg2.rt[o];
+                    auto bl = [&](int v) { long s_ = 0, e_ = n; int fd = 0; long i_ = s_ + (e_ - s_) / 2, lo = s_, hi = e_;
+                        while (!fd) { if (i_ <= s_) { i_ = (v <= l[s_]) ? s_ : s_ + 1; fd = 1; } else if (i_ >= e_ - 1) { i_ = (v <= l[e_ - 1]) ? e_ - 1 : e_; fd = 1; }
+                            else if (v <= l[i_]) { hi = i_; i_ = lo + (i_ - lo) / 2; if (hi == i_) { fd = 1; i_ += 1; } }
+                            else { lo = i_; i_ = i_ + (hi - i_) / 2; if (lo == i_) { fd = 1; i_ += 1; } } } return i_; };
+                    auto br = [&](int v) { long s_ = 0, e_ = n; int fd = 0; long i_ = s_ + (e_ - s_) / 2, lo = s_, hi = e_;
+                        while (!fd) { if (i_ <= s_) { i_ = (v < l[s_]) ? s_ : s_ + 1; fd = 1; } else if (i_ >= e_ - 1) { i_ = (v < l[e_ - 1]) ? e_ - 1 : e_; fd = 1; }
+                            else if (v < l[i_]) { hi = i_; i_ = lo + (i_ - lo) / 2; if (hi == i_) { fd = 1; i_ += 1; } }
+                            else { lo = i_; i_ = i_ + (hi - i_) / 2; if (lo == i_) { fd = 1; i_ += 1; } } } return i_; };
+                    auto brd = [&](double v) { long s_ = 0, e_ = T.n_p2s; int fd = 0; long i_ = s_ + (e_ - s_) / 2, lo = s_, hi = e_; const double *q = T.p2s_p;
+                        while (!fd) { if (i_ <= s_) { i_ = (v < q[s_]) ? s_ : s_ + 1; fd = 1; } else if (i_ >= e_ - 1) { i_ = (v < q[e_ - 1]) ? e_ - 1 : e_; fd = 1; }
+                            else if (v < q[i_]) { hi = i_; i_ = lo + (i_ - lo) / 2; if (hi == i_) { fd = 1; i_ += 1; } }
+                            else { lo = i_; i_ = i_ + (hi - i_) / 2; if (lo == i_) { fd = 1; i_ += 1; } } } return i_; };
+                    long i1, i2;
+                    double z;
+                    if (r < rp_ave[seg]) {
+                        i1 = br(r);
+                        i2 = bl(r);
+                        double d1 = (i1 <= 0) ? 0.5 : (double)i1, d2 = (i2 <= 0) ? 0.5 : (double)i2;
+                        i1 = brd((d1 + d2) / (2 * n));
+                        if (i1 < 0) i1 = 0; else if (i1 >= T.n_p2s) i1 = T.n_p2s - 1;
+                        z = P.ranks_stdev == 0 ? (rp_ave[seg] - rg2.rd[o] - rg2.low[o]) / rp_sd[seg] : T.p2s_sd[i1];
+                    } else {
+                        const bool ov = r > A.dup_factor * rp_ave[seg];
+                        if (ov) { i1 = bl((int)(A.dup_factor * rp_ave[seg])); i2 = br(r); }
+                        else { i1 = bl(r); i2 = br(r); }
+                        i1 = n - i1;
+                        i2 = n - i2;
+                        double d1 = (i1 <= 0) ? 0.5 : (double)i1, d2 = (i2 <= 0) ? 0.5 : (double)i2;
+                        i1 = brd((d1 + d2) / (2 * n));
+                        if (i1 < 0) i1 = 0; else if (i1 >= T.n_p2s) i1 = T.n_p2s - 1;
+                        if (P.ranks_stdev == 0)
+                            z = ov ? (A.dup_factor - 1) * (-rp_ave[seg]) / rp_sd[seg]
+                                   : (rp_ave[seg] - rg2.rd[o] - rg2.low[o]) / rp_sd[seg];
+                        else z = -T.p2s_sd[i1];
+                    }
+                    zp[nz] = pos;
+                    zv[nz] = z;
+                    nz++;
+                }
+            }
+            // later writes win, as in the reference's loop order
+            for (int64_t i = 0; i < nz; i++) CK(hipMemcpyAsync(sd + zp[i], &zv[i], 8, hipMemcpyHostToDevice, st));
+            CK(hipStreamSynchronize(st));
+        }
+        CK(hipMemcpyAsync(S->wsd.p, wsd.data(), 8 * (L + 1), hipMemcpyHostToDevice, st));
+
+        // ---- DEL then DUP walk over the one lowvar block [m-1, len-W) ----
+        WalkIn WI{gcw, flag, d_mq, d_rd, d_low, sd, (const double *)S->wsd.p, dT, len, m - 1,
+                  (len - W) - ML, L, ML, P.rd_min_mapq};
+        const int64_t span = std::max<int64_t>(0, WI.end - WI.start);
+        const int64_t n_ch = (span + WALK_CHUNK - 1) / WALK_CHUNK;
+        uint32_t call_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, len / 1000), 1 << 24);
+        std::vector<CallRec> found[2];
+        for (int kind = 0; kind < 2 && n_ch > 0; kind++) {
+            for (int attempt = 0; attempt < 2; attempt++) {
+                if ((rc = grow(S->calls, sizeof(CallRec) * call_cap, err, errlen)) ||
+                    (rc = grow(S->ok, call_cap, err, errlen)) ||
+                    (rc = grow(S->tiles, sizeof(ChunkState) * n_ch, err, errlen)))
+                    return rc;
+                ChunkState *dcs = (ChunkState *)S->tiles.p;
+                CallRec *dcalls = (CallRec *)S->calls.p;
+                uint8_t *vis = (uint8_t *)S->vis.p;
+                CK(hipMemsetAsync(n_calls, 0, 4, st));
+                CK(hipMemsetAsync(vis, 0, len, st));
+                const unsigned gch = (unsigned)((n_ch + 63) / 64);
+                if (kind == 0) {
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                } else {
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                }
+                CK(hipGetLastError());
+                std::vector<ChunkState> hcs(n_ch);
+                CK(hipMemcpyAsync(hcs.data(), dcs, sizeof(ChunkState) * n_ch, hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+                // reconcile: the true exit of each chunk, in order (GROM.c's walk is one pass)
+                int64_t tx = hcs[0].x1;
+                int tl_ = hcs[0].l1;
+                for (int64_t k = 1; k < n_ch; k++) {
+                    const bool entry_ok = tx == hcs[k - 1].x1 && tl_ == hcs[k - 1].l1;
+                    const int64_t c1 = std::min<int64_t>(WI.end, WI.start + (k + 1) * WALK_CHUNK);
+                    if (entry_ok && hcs[k].status == ST_MERGED) { tx = hcs[k].x1; tl_ = hcs[k].l1; continue; }
+                    if (entry_ok && hcs[k].status == ST_NOMERGE) { tx = hcs[k].x2; tl_ = hcs[k].l2; continue; }
+                    if (tx >= c1) {  // the true walk jumps over this chunk
+                        CK(hipMemsetAsync(vis + (WI.start + k * WALK_CHUNK), 0, c1 - (WI.start + k * WALK_CHUNK), st));
+                        continue;
+                    }
+                    if (kind == 0)
+                        hipLaunchKernelGGL(k_cnv_walk_fix<0>, dim3(1), dim3(64), 0, st, WI, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
+                    else
+                        hipLaunchKernelGGL(k_cnv_walk_fix<1>, dim3(1), dim3(64), 0, st, WI, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
+                    CK(hipGetLastError());
+                    ChunkState one;
+                    CK(hipMemcpyAsync(&one, dcs + k, sizeof(ChunkState), hipMemcpyDeviceToHost, st));
+                    CK(hipStreamSynchronize(st));
+                    tx = one.x2;
+                    tl_ = one.l2;
+                }
+                uint32_t nc = 0;
+                CK(hipMemcpyAsync(&nc, n_calls, 4, hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+                if (nc > call_cap) { call_cap = nc + nc / 4 + 1024; continue; }
+                std::vector<CallRec> hc(nc);
+                std::vector<uint8_t> ok(nc);
+                if (nc) {
+                    hipLaunchKernelGGL(k_cnv_calls_valid, dim3((nc + 255) / 256), dim3(256), 0, st, dcalls, nc, vis,
+                                       (uint8_t *)S->ok.p);
+                    CK(hipMemcpyAsync(hc.data(), dcalls, sizeof(CallRec) * nc, hipMemcpyDeviceToHost, st));
+                    CK(hipMemcpyAsync(ok.data(), S->ok.p, nc, hipMemcpyDeviceToHost, st));
+                    CK(hipStreamSynchronize(st));
+                }
+                for (uint32_t i = 0; i < nc; i++)
+                    if (ok[i]) found[kind].push_back(hc[i]);
+                std::sort(found[kind].begin(), found[kind].end(),
+                          [](const CallRec &a, const CallRec &b) { return a.p < b.p; });
+                found[kind].erase(std::unique(found[kind].begin(), found[kind].end(),
+                                              [](const CallRec &a, const CallRec &b) { return a.p == b.p; }),
+                                  found[kind].end());
+                break;
+            }
+        }
+        CK(hipEventRecord(S->e1, st));
+
+        // ---- p value (Q8), filter, copy number, rows: GROM.c:17139-17300, 20024-20228 ----
+        const double pp = 0.3275911, a1 = 0.254829592, a2 = -0.284496736, a3 = 1.421413741, a4 = -1.453152027,
+                     a5 = 1.061405429;
+        int64_t n_rows = 0;
+        for (int kind = 0; kind < 2; kind++) {
+            std::vector<std::pair<size_t, double>> keep;
+            for (size_t i = 0; i < found[kind].size(); i++) {
+                double x = fabs(found[kind][i].stdevs) / sqrt(2.0);
+                double t = 1.0 / (1.0 + pp + x);
+                double e = 1.0 - ((a1 * t + a2 * pow(t, 2) + a3 * pow(t, 3) + a4 * pow(t, 4) + a5 * pow(t, 5)) *
+                                  exp(-pow(x, 2)));
+                double pv = (1.0 - e) / 2.0;
+                if (pv < P.rd_pval_threshold) keep.push_back({i, pv});
+            }
+            std::vector<GatherRange> rg;
+            int64_t tot = 0;
+            for (auto &kp : keep) {
+                const CallRec &c = found[kind][kp.first];
+                int64_t n = std::max<int64_t>(0, c.ce - c.p);
+                rg.push_back(GatherRange{c.p, n, 1, tot});
+                tot += n;
+            }
+            Gathered g;
+            if ((rc = gather(S, st, rg, tot, gcw, acw, d_mq, d_rd, d_low, flag, g, err, errlen))) return rc;
+            std::vector<double> pl, tmp;
+            for (size_t j = 0; j < keep.size(); j++) {
+                const CallRec &c = found[kind][keep[j].first];
+                pl.clear();
+                for (int64_t i = 0; i < rg[j].count; i++) {
+                    const int64_t o = rg[j].out + i;
+                    if (g.flag[o] & F_LOW) continue;
+                    const int k = g.mq[o] >= P.rd_min_mapq ? 0 : 1;
+                    if (T.ave[k][g.gc[o]] > 0) pl.push_back((double)g.rt[o] / T.ave[k][g.gc[o]]);
+                }
+                double cn = -1, cns = 0;
+                const long pc = (long)pl.size();
+                if (pc > 0) {
+                    tmp.resize(pc);
+                    msort_lo(pl.data(), pl.size(), tmp.data());
+                    long s0 = 0.1 * pc, e0 = pc - s0;
+                    double sum = 0.0;
+                    for (long i = s0; i < e0; i++) sum += pl[i];
+                    if (e0 - s0 > 0) {
+                        cn = (sum / (e0 - s0)) * P.ploidy;
+                        cns = 0;
+                        for (long i = 0; i < pc; i++) cns += pow((P.ploidy * pl[i] - cn), 2);
+                        cns = sqrt(cns / pc);
+                    }
+                }
+                char line[512];
+                int nl = snprintf(line, sizeof(line), "%s\t%lld\t.\t.\t%s\t.\t.\tEND=%lld\tSD:Z:CN:CS\t%e:%e:%.2f:%e\n",
+                                  chr_name, (long long)c.p + 1, kind == 0 ? "<DEL>" : "<DUP>", (long long)c.ce + 1,
+                                  c.stdevs, keep[j].second, cn, cns);
+                rows.append(line, (size_t)nl);
+                n_rows++;
+            }
+        }
+        if (timing) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, S->e0, S->e1);
+            timing->ms_device = ms;
+            timing->del_calls = (int64_t)found[0].size();
+            timing->dup_calls = (int64_t)found[1].size();
+            timing->rows = n_rows;
+        }
+    }
+    if (timing)
+        timing->ms_host =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+    return GROM_OK;
+}

@@ -156,6 +156,12 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
     ch.tid = cp->tid;
     ch.n_skip = b->n_skip;
     ch.p_last = b->p_last;
+    ch.cnv = cp->tid >= 0; /* detect_del_dup runs for a matched target, GROM.c:16633 */
+    {
+        /* srand(time()) per chromosome, GROM.c:1584; GROM_SEED pins it */
+        const char *e = getenv("GROM_SEED");
+        ch.seed = e ? (uint32_t)strtoul(e, NULL, 10) : (uint32_t)time(NULL);
+    }
     grom_reads rd;
     grom_batch_view(b, &rd);
     grom_out out = {0};
@@ -230,6 +236,24 @@ int grom_cli_main(int argc, char **argv) {
         case 'a': P.min_snv_ratio = atof(optarg); break;
         case 'f': P.vcf = 0; break;
         case 'x': P.min_ave_bq = atof(optarg); break;
+        case 'Z': P.block_min = atol(optarg); break;
+        case 'W': P.min_rd_window_len = atol(optarg); break;
+        case 'X': P.max_rd_window_len = atol(optarg); break;
+        case 'A': P.windows_sampling_factor = atol(optarg); break;
+        case 'Y': P.min_blocks = atol(optarg); break;
+        case 'D': P.min_repeat = atol(optarg); break;
+        case 'E': P.min_repeat_stdev = atof(optarg); break;
+        case 'K': P.ranks_stdev = atoi(optarg); break;
+        case 'V': P.rd_pval_threshold = atof(optarg); break;
+        case 'U': P.chr_rd_threshold_factor = atoi(optarg); break;
+        case 'L': P.dup_threshold_factor = atol(optarg); break;
+        case 'F': P.mapq_factor = atof(optarg); break;
+        case 'N':
+            if (atol(optarg) > 0) {
+                printf("ERROR: -N (.1000gen side file) is not supported by this build\n");
+                return 1;
+            }
+            break;
         case 'h': print_help(); return 0;
         case '?': return 1;
         default: break; /* accepted; steers rows outside the implemented scan */

@@ -121,6 +121,8 @@ int grom_batch_get(grom_batch_handle *h, grom_chrom *ch, grom_reads *rd) {
     ch->tid = 0;
     ch->n_skip = h->b.n_skip;
     ch->p_last = h->b.p_last;
+    ch->cnv = 1;
+    ch->seed = 1;
     grom_batch_view(&h->b, rd);
     return GROM_OK;
 }

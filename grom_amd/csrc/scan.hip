@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../../include/grom_amd.h"
+#include "cnv.h"
 #include "scan_common.h"
 #include "snvfmt.h"
 
@@ -208,6 +209,7 @@ struct Ctx {
     grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
     size_t h_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, ep0 = nullptr, ep1 = nullptr;
+    CnvScratch *cnv = nullptr;  // read-depth CNV path (cnv.hip)
 };
 
 static Ctx g_ctx[64];
@@ -454,10 +456,31 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             done += (size_t)thr;
         }
         snv_rows(P, ch, cands + done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1], vt);
+        const double t_snv = ms_since(t_start);
+
+        // read-depth CNV path after the SV rows (GROM.c:16633-17300); the
+        // reference runs it only when the FASTA name matched a BAM target
+        CnvTiming ct{};
+        if (ch->cnv && !want_dbg) {
+            if (!C.cnv) C.cnv = cnv_scratch_new();
+            std::string crow;
+            char cerr[512] = {0};
+            rc = cnv_chrom(C.cnv, st, P, ch->seed, ch->name, ch->ref, ch->len, (int32_t *)C.caf_mq.p,
+                           (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, crow, &ct, cerr, sizeof(cerr));
+            if (rc != GROM_OK) {
+                set_err("%s", cerr);
+                return rc;
+            }
+            vt.add(crow.data(), crow.size());
+        }
 
         if (timing)
-            fprintf(stderr, "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms, rows %.3f ms (%u candidates)\n",
-                    ch->name ? ch->name : "?", t_kernels, t_copied - t_kernels, ms_since(t_start) - t_copied, ncand);
+            fprintf(stderr,
+                    "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms, rows %.3f ms (%u candidates), "
+                    "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows)\n",
+                    ch->name ? ch->name : "?", t_kernels, t_copied - t_kernels, t_snv - t_copied, ncand,
+                    ms_since(t_start) - t_snv, ct.ms_device, (long long)ct.del_calls, (long long)ct.dup_calls,
+                    (long long)ct.rows);
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
         if (stats) {
@@ -468,6 +491,8 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             (void)hipMemcpy(&nev, d_nev, 4, hipMemcpyDeviceToHost);
             stats->ms_total = ms;
             stats->ms_pileup = msp;
+            stats->ms_cnv = ct.ms_device;
+            stats->cnv_rows = ct.rows;
             stats->bases_evaluated = n_eval;
             stats->snv_candidates = ncand;
             stats->mismatch_events = nev;
@@ -525,6 +550,16 @@ static int upload(Ctx &C, const grom_chrom *ch, const grom_reads *h, grom_chrom 
 extern "C" {
 
 int grom_abi_version(void) { return GROM_AMD_ABI_VERSION; }
+size_t grom_abi_struct_size(int which) {
+    switch (which) {
+    case 0: return sizeof(grom_params);
+    case 1: return sizeof(grom_chrom);
+    case 2: return sizeof(grom_reads);
+    case 3: return sizeof(grom_out);
+    case 4: return sizeof(grom_stats);
+    default: return 0;
+    }
+}
 const char *grom_last_error(void) { return g_err; }
 
 int grom_dev_init(int device, const grom_params *params, const double *hez, const double *mq) {
@@ -563,6 +598,7 @@ void grom_dev_fini(int device) {
     for (DevBuf *b : all)
         if (b->p) (void)hipFree(b->p);
     if (C.h_cands) (void)hipHostFree(C.h_cands);
+    cnv_scratch_free(C.cnv);
     (void)hipFree(C.d_mq);
     (void)hipFree(C.d_hez);
     (void)hipEventDestroy(C.e0);

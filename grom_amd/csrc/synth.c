@@ -73,6 +73,9 @@ void synth_default_cfg(synth_cfg *c) {
     c->gc_hi = 0.55;
     c->repeat_rate = 2e-5;
     c->fasta_line = 60;
+    c->cnv_rate = 0.0;
+    c->cnv_min = 10000;
+    c->cnv_max = 300000;
     c->seed = 2;
 }
 
@@ -343,6 +346,36 @@ static int draw_mapq(const synth_cfg *c, xrng *r) {
     return xunif(r) < c->lowmapq_frac ? (int)xint(r, 20) : 60;
 }
 
+/* Copy-number regions of chromosome ci: fragment start rate is multiplied
+ * by the region's depth factor (0 = homozygous loss, 0.5, 1.5, 2).  Regions
+ * are sorted and disjoint; drawn from their own stream so that a genome with
+ * no regions reads exactly as before. */
+typedef struct { long start, end; double f; } cnv_reg;
+static int synth_cnv_regions(const synth_cfg *c, int ci, cnv_reg **out) {
+    long n = c->chr_len[ci];
+    int k = (int)(c->cnv_rate * (double)n + 0.5);
+    *out = NULL;
+    if (k <= 0 || c->cnv_max <= 0) return 0;
+    static const double fs[4] = {0.0, 0.5, 1.5, 2.0};
+    cnv_reg *r = (cnv_reg *)malloc(sizeof(cnv_reg) * k);
+    xrng g;
+    xseed(&g, c->seed, (uint64_t)ci + 1, 7);
+    long span = n / k;
+    int m = 0;
+    for (int i = 0; i < k; i++) {
+        long lo = (long)i * span + c->telomere_n, hi = (long)(i + 1) * span - c->telomere_n;
+        long len = c->cnv_min + xint(&g, c->cnv_max - c->cnv_min + 1);
+        if (hi - lo <= len + 2) continue;
+        long s = lo + xint(&g, hi - lo - len);
+        r[m].start = s;
+        r[m].end = s + len;
+        r[m].f = fs[xint(&g, 4)];
+        m++;
+    }
+    *out = r;
+    return m;
+}
+
 long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit, void *ctx) {
     long n = c->chr_len[ci];
     int L = c->read_len;
@@ -364,11 +397,20 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
     uint64_t order = 0;
     double start_f = n_frag > 0 ? xexp(&r, gap) : (double)n;
     uint64_t frag_id = 0;
+    cnv_reg *creg;
+    int n_creg = synth_cnv_regions(c, ci, &creg), ic = 0;
     aln a1, a2;
     char name[64];
     while (start_f < (double)n) {
         long start = (long)start_f;
-        start_f += xexp(&r, gap);
+        double f = 1.0;
+        while (ic < n_creg && creg[ic].end <= start) ic++;
+        if (ic < n_creg && creg[ic].start <= start) f = creg[ic].f;
+        if (f == 0.0) {
+            start_f = (double)creg[ic].end + xexp(&r, gap);
+            continue;
+        }
+        start_f += (f == 1.0) ? xexp(&r, gap) : xexp(&r, gap / f);
         int hk = (int)xint(&r, 2);
         const haplo *hp = &h[hk];
         int ins = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
@@ -432,6 +474,7 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
         emitted++;
     }
     free(heap.a);
+    free(creg);
     free(ncount);
     free_haplos(h);
     return emitted;

@@ -43,6 +43,8 @@ typedef struct synth_cfg {
     double gc_lo, gc_hi;  /* isochore GC range */
     double repeat_rate;   /* dinucleotide repeat runs per base */
     int fasta_line;       /* FASTA line width */
+    double cnv_rate;      /* copy-number regions per base (0 = none) */
+    long cnv_min, cnv_max;/* copy-number region length range */
     uint64_t seed;
 } synth_cfg;
 

@@ -121,6 +121,18 @@ void grom_default_params(grom_params *p) {
     p->min_ave_bq = 15;
     p->snv_rd_min_factor = 1.75;
     p->high_cov_min_snv_ratio = 0.4;
+    p->ranks_stdev = 1;
+    p->chr_rd_threshold_factor = 2;
+    p->min_repeat = 20;
+    p->min_blocks = 4;
+    p->block_min = 10000;
+    p->min_rd_window_len = 100;
+    p->max_rd_window_len = 10000;
+    p->windows_sampling_factor = 2;
+    p->dup_threshold_factor = 2;
+    p->min_repeat_stdev = 1.5;
+    p->rd_pval_threshold = 0.000000001;
+    p->mapq_factor = 0.5;
 }
 
 void grom_params_set_insert(grom_params *p, int32_t mean, int32_t imin, int32_t imax, int32_t lseq) {

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GROM_AMD_ABI_VERSION 1
+#define GROM_AMD_ABI_VERSION 2
 #define GROM_MAX_TRIALS 1000 /* max_trials, GROM.c:631 */
 
 enum {
@@ -78,6 +78,19 @@ typedef struct grom_params {
     int32_t half_one_base_rd_len;
     int32_t r14_one_base_rd_len;  /* g_14_one_base_rd_len */
     int32_t r34_one_base_rd_len;  /* g_34_one_base_rd_len */
+    /* read-depth CNV path (detect_del_dup and its callers) */
+    int32_t ranks_stdev;          /* g_ranks_stdev (-K), GROM.c:925 */
+    int32_t chr_rd_threshold_factor; /* g_chr_rd_threshold_factor (-U), GROM.c:737 */
+    int64_t min_repeat;           /* g_min_repeat (-D), GROM.c:733 */
+    int64_t min_blocks;           /* g_min_blocks (-Y), GROM.c:739 */
+    int64_t block_min;            /* g_block_min (-Z), GROM.c:758 */
+    int64_t min_rd_window_len;    /* g_min_rd_window_len (-W), GROM.c:931 */
+    int64_t max_rd_window_len;    /* g_max_rd_window_len (-X), GROM.c:933 */
+    int64_t windows_sampling_factor; /* g_windows_sampling_factor (-A), GROM.c:727 */
+    int64_t dup_threshold_factor; /* g_dup_threshold_factor (-L), GROM.c:731 */
+    double min_repeat_stdev;      /* g_min_repeat_stdev (-E), GROM.c:734 */
+    double rd_pval_threshold;     /* g_rd_pval_threshold (-V), GROM.c:722 */
+    double mapq_factor;           /* g_mapq_factor (-F), GROM.c:719 */
 } grom_params;
 
 /* One chromosome.  `ref` holds exactly what find_disc_svs loaded
@@ -92,6 +105,10 @@ typedef struct grom_chrom {
     int32_t p_last;     /* last base the walk reaches (the base at which the
                            chromosome's final record is ingested), or -1 if
                            the walk never ingests a record */
+    int32_t cnv;        /* 1: run the read-depth CNV path (the reference runs it
+                           when the FASTA name matched a BAM target) */
+    uint32_t seed;      /* CNV sampling seed: replaces srand(time()) at
+                           GROM.c:1584 */
 } grom_chrom;
 
 /* The records the chromosome's scan ingests (stream order, after the serial
@@ -131,12 +148,17 @@ typedef struct grom_out {
 typedef struct grom_stats {
     double ms_total;        /* device time of the whole scan */
     double ms_pileup;       /* device time of the SNV pileup/evaluation kernel */
+    double ms_cnv;          /* device time of the CNV kernels */
+    int64_t cnv_rows;       /* <DEL>/<DUP> rows written */
     int64_t bases_evaluated;
     int64_t snv_candidates;
     int64_t mismatch_events;
 } grom_stats;
 
 int grom_abi_version(void);
+/* sizeof of the ABI structs, for bindings to check their layout:
+ * 0 grom_params, 1 grom_chrom, 2 grom_reads, 3 grom_out, 4 grom_stats */
+size_t grom_abi_struct_size(int which);
 const char *grom_last_error(void);
 
 /* Initialise `device`: upload the two binomial tables (each

@@ -314,6 +314,8 @@ static int bam_name_lc(const char *target, char *out, int cap) {
     return L;
 }
 
+#include "cnv_oracle.c"
+
 /* ---------------- per-chromosome scan state ---------------- */
 typedef struct {
     /* current record as loaded by the fetch sites (GROM.c:5744-5837) */
@@ -755,6 +757,13 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     (void)target_name_of_match;
     scan_t s;
     memset(&s, 0, sizeof(s));
+    /* srand(time()) per chromosome, GROM.c:1584; GROM_SEED pins it */
+    {
+        const char *e = getenv("GROM_SEED");
+        glibc_srand(&g_rng, e ? (unsigned)strtoul(e, NULL, 10) : (unsigned)time(NULL));
+    }
+    cnv_pre pre;
+    cnv_prepass(fasta, chr_len, &pre); /* GROM.c:1586-1881 */
     s.fasta = fasta;
     s.chr_len = chr_len;
     s.w.W = g_half_one_base_rd_len;
@@ -885,6 +894,9 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx, &rc_total, &base_total,
               chr_name, vcf, c->lseq);
 
+    /* read-depth CNV path, GROM.c:16633-17300 (only for a matched target) */
+    if (chr_match != -1) cnv_chromosome(chr_len, fasta, &pre, s.caf_mq, s.caf_rd, s.caf_low, chr_name, vcf);
+
     if (g_dump_prefix) {
         char path[4096];
         snprintf(path, sizeof(path), "%s.%s.caf", g_dump_prefix, chr_name);
@@ -902,6 +914,7 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
             fclose(f);
         }
     }
+    cnv_pre_free(&pre);
     snv_list_free(&sl);
     nametab_free(&s.names);
     free(s.w.c); free(s.w.names);
@@ -997,6 +1010,18 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
         case 'a': g_min_snv_ratio = atof(optarg); break;
         case 'f': g_vcf = 0; break;
         case 'x': g_min_ave_bq = atof(optarg); break;
+        case 'Z': g_block_min = atol(optarg); break;
+        case 'W': g_min_rd_window_len = atol(optarg); break;
+        case 'X': g_max_rd_window_len = atol(optarg); break;
+        case 'A': g_windows_sampling_factor = atol(optarg); break;
+        case 'Y': g_min_blocks = atol(optarg); break;
+        case 'D': g_min_repeat = atol(optarg); break;
+        case 'E': g_min_repeat_stdev = atof(optarg); break;
+        case 'K': g_ranks_stdev = atoi(optarg); break;
+        case 'V': g_rd_pval_threshold = atof(optarg); break;
+        case 'U': g_chr_rd_threshold_factor = atoi(optarg); break;
+        case 'L': g_dup_threshold_factor = atol(optarg); break;
+        case 'F': g_mapq_factor = atof(optarg); break;
         case 'h': return 0;
         case '?': return 1;
         default: break; /* options outside this restatement's scope */
@@ -1044,6 +1069,14 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
     if (g_vcf == 1) {
         write_header(vcf, fasta_file_name, 0);
     }
+
+    build_pval2sd(); /* GROM.c:20705-20748 */
+    for (int g = 0; g < G_NUM_GC_BINS; g++) {
+        if (!g_sample_hi[g]) g_sample_hi[g] = (int *)malloc(g_sample_lists_len * sizeof(int));
+        if (!g_sample_lo[g]) g_sample_lo[g] = (int *)malloc(g_sample_lists_len * sizeof(int));
+    }
+    for (int g = 0; g < G_REPEAT_SEGMENTS; g++)
+        if (!g_sample_rep[g]) g_sample_rep[g] = (int *)malloc(g_sample_lists_len * sizeof(int));
 
     /* find_disc_svs opens its own stream from the file start, GROM.c:20471 */
     if (stream_open(&st, bam_file_name) != 0) return 1;

@@ -13,6 +13,7 @@ GOLDEN_VCF = os.path.join(REPO, "tests", "golden", "tilapia_v1.0.0.vcf")
 GOLDEN_CTX = os.path.join(REPO, "tests", "golden", "tilapia_v1.0.0.ctx.vcf")
 NCOUNT = 40
 FILEDATE = "20260101"
+SEED = "7"  # GROM_SEED: pins the CNV sampling generator (srand(time()) at GROM.c:1584)
 
 # synthetic parity cases: name -> grom_synth arguments
 CASES = {
@@ -21,6 +22,9 @@ CASES = {
     "lowmapq_clip": ["-L", "300000", "-s", "13", "-Q", "0.2", "-C", "0.08", "-q", "0.1", "-U", "0.01"],
     "dups": ["-L", "300000", "-s", "14", "-D", "0.15"],
     "empty_middle": ["-L", "200000,200000,200000", "-s", "15", "-c", "30,0,30"],
+    # copy-number regions (0x, 0.5x, 1.5x, 2x depth) for the read-depth CNV path
+    "cnv": ["-L", "1500000", "-s", "16", "-V", "0.000004", "-W", "20000,150000", "-Q", "0.05"],
+    "cnv_multi": ["-L", "700000,900000", "-s", "17", "-V", "0.000005", "-W", "15000,80000", "-Q", "0.08"],
 }
 
 
@@ -36,6 +40,7 @@ def synth(datadir, name, args):
 def run(binary, args, cwd, env_extra=None):
     env = dict(os.environ)
     env["GROM_FILEDATE"] = FILEDATE
+    env["GROM_SEED"] = SEED
     if env_extra:
         env.update(env_extra)
     r = subprocess.run([binary] + list(args), cwd=cwd, env=env, capture_output=True, text=True, timeout=900)
@@ -52,7 +57,7 @@ def run_grom(datadir, bam, fa, out, extra=(), dump=None):
     """The product CLI, called in this process through the C ABI so the HIP
     library is loaded (and checked) by the test process itself."""
     import grom_amd
-    env = {"GROM_FILEDATE": FILEDATE}
+    env = {"GROM_FILEDATE": FILEDATE, "GROM_SEED": SEED}
     if dump:
         env["GROM_DUMP"] = dump
     rc = grom_amd.cli_main(["-i", bam, "-r", fa, "-o", out] + list(extra), env=env, cwd=str(datadir))

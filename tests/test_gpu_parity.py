@@ -26,6 +26,17 @@ RUNS = [
     ("one_chr", ["-G", "40"]),  # forces mid-scan SNV list flushes (GROM.c:11201)
 ]
 
+# read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call
+# (the default 1e-9 p-value cut removes most)
+CNV_RUNS = [
+    ("cnv", []),
+    ("cnv", ["-V", "1"]),
+    ("cnv", ["-V", "1", "-K", "0"]),
+    ("cnv", ["-V", "1", "-A", "3", "-X", "4000", "-W", "60", "-L", "3", "-F", "0.3"]),
+    ("cnv_multi", ["-V", "1", "-p", "3"]),
+    ("cnv_multi", ["-V", "1", "-M", "-U", "1", "-Y", "2", "-Z", "20000"]),
+]
+
 
 def _names(datadir, tag):
     return sorted(f.split(".")[-2] for f in os.listdir(datadir) if f.startswith(tag + ".") and f.endswith(".cnt"))
@@ -55,6 +66,18 @@ def test_counters_and_vcf_bit_exact(datadir, case, extra):
     assert ov.count("\n") > 46
     assert ov == gv
     assert filecmp.cmp(datadir / f"o_{tag}.ctx.vcf", datadir / f"g_{tag}.ctx.vcf", shallow=False)
+
+
+@pytest.mark.parametrize("case,extra", CNV_RUNS, ids=[f"{c}{''.join(e)}" for c, e in CNV_RUNS])
+def test_cnv_rows_bit_exact(datadir, case, extra):
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"{case}{''.join(extra).replace('-', '_').replace('.', 'p')}"
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra)
+    ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"g_{tag}.vcf").read()
+    if "-V" in extra:
+        assert ov.count("<DEL>") + ov.count("<DUP>") > 0
+    assert ov == gv
 
 
 def test_device_resident_path_matches_host_path():
