@@ -72,8 +72,8 @@ constexpr int MAX_BLOCK_LIST = 10000;      // max_block_list_len, GROM.c:633
 constexpr int GC_TP = 4096;                // positions per k_cnv_gc tile
 constexpr int GC_MMAX = 1536;              // largest insert mean the LDS tile holds
 constexpr int GC_LEN = GC_TP + 2 * GC_MMAX + 2;
-constexpr int SCAN_K = 16;                 // positions per lane in the state scans
-constexpr int SCAN_TP = 256 * SCAN_K;      // positions per scan tile
+constexpr int SEG_W = 4096;                // positions per wave in the state scans
+constexpr int ZT_MAX = 1024;               // depths with a precomputed z rank index
 constexpr int HIST_MAX = 4096;             // exact depth histogram for the chromosome variance
 constexpr int64_t WALK_CHUNK = 16384;      // positions per speculative walk lane
 
@@ -301,40 +301,33 @@ __device__ __forceinline__ int ev2(const Args &A, int64_t p, const uint8_t *flag
     return 1;
 }
 
-// block-wide "last defined value before me" over the 256 lanes' own last values
-__device__ int block_last_excl(int mine, int carry, int *sh) {
-    const int tid = threadIdx.x;
-    sh[tid] = mine;
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {
-        int v = (tid >= d) ? sh[tid - d] : -1;
-        __syncthreads();
-        if (v != -1 && sh[tid] == -1) sh[tid] = v;
-        __syncthreads();
-    }
-    int r = (tid > 0) ? sh[tid - 1] : -1;
-    __syncthreads();
-    return r != -1 ? r : carry;
+// "last defined value at or before me" across the 64 lanes of a wave, with
+// `c` for lanes that have none before them
+__device__ __forceinline__ int wave_last_incl(int e, int c) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long m = __ballot(e != -1);
+    const unsigned long long mine = m & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const int src = mine ? 63 - __clzll(mine) : 0;
+    const int v = __shfl(e, src);
+    return mine ? v : c;
 }
 
+// Each wave owns SEG_W consecutive positions, read 64 at a time (coalesced).
 template <int WHICH>
-__global__ __launch_bounds__(256) void k_cnv_tile_last(Args A, const uint8_t *acw, const uint8_t *flag,
-                                                       const int32_t *mq, const int32_t *rd, const int32_t *low,
-                                                       int8_t *tile_last) {
-    __shared__ int best;
-    if (threadIdx.x == 0) best = -1;
-    __syncthreads();
-    const int64_t p0 = (int64_t)blockIdx.x * SCAN_TP + (int64_t)threadIdx.x * SCAN_K;
-    int last = -1;
-    for (int k = 0; k < SCAN_K; k++) {
-        int64_t p = p0 + k;
-        if (p >= A.len) break;
-        int e = WHICH == 1 ? ev1(A, p, acw, mq, rd, low) : ev2(A, p, flag, mq, rd, low);
-        if (e != -1) last = e;
+__global__ __launch_bounds__(256) void k_cnv_seg_last(Args A, const uint8_t *acw, const uint8_t *flag,
+                                                      const int32_t *mq, const int32_t *rd, const int32_t *low,
+                                                      int8_t *seg_last) {
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t p0 = wave * SEG_W;
+    int c = -1;
+    for (int r = 0; r < SEG_W / 64; r++) {
+        const int64_t p = p0 + r * 64 + lane;
+        int e = -1;
+        if (p < A.len) e = WHICH == 1 ? ev1(A, p, acw, mq, rd, low) : ev2(A, p, flag, mq, rd, low);
+        c = __builtin_amdgcn_readlane(wave_last_incl(e, c), 63);
     }
-    if (last != -1) atomicMax(&best, (int)threadIdx.x * 4 + last);
-    __syncthreads();
-    if (threadIdx.x == 0) tile_last[blockIdx.x] = best < 0 ? (int8_t)-1 : (int8_t)(best & 3);
+    if (lane == 0 && p0 < A.len) seg_last[wave] = (int8_t)c;
 }
 
 // carry[t] = last defined tile value before tile t (0 before the first)
@@ -355,35 +348,29 @@ __global__ __launch_bounds__(1024) void k_cnv_carry(const int8_t *tile_last, int
     for (int64_t i = lo; i < hi; i++) { carry[i] = (int8_t)c; if (tile_last[i] != -1) c = tile_last[i]; }
 }
 
+
 // flags (GROM.c:18654-18712) and the guard bit of GROM.c:18765
 __global__ __launch_bounds__(256) void k_cnv_flags(Args A, const uint8_t *__restrict__ acw,
                                                    const uint8_t *__restrict__ gcw, const int32_t *__restrict__ mq,
                                                    const int32_t *__restrict__ rd, const int32_t *__restrict__ low,
                                                    const int8_t *__restrict__ carry, const Tables *__restrict__ T,
                                                    uint8_t *__restrict__ flag) {
-    __shared__ int sh[256];
-    const int64_t p0 = (int64_t)blockIdx.x * SCAN_TP + (int64_t)threadIdx.x * SCAN_K;
-    int mine = -1;
-    for (int k = 0; k < SCAN_K; k++) {
-        int64_t p = p0 + k;
-        if (p >= A.len) break;
-        int e = ev1(A, p, acw, mq, rd, low);
-        if (e != -1) mine = e;
-    }
-    int last = block_last_excl(mine, carry[blockIdx.x], sh);
-    for (int k = 0; k < SCAN_K; k++) {
-        int64_t p = p0 + k;
-        if (p >= A.len) break;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t p0 = wave * SEG_W;
+    if (p0 >= A.len) return;
+    int c = carry[wave];
+    for (int r = 0; r < SEG_W / 64; r++) {
+        const int64_t p = p0 + r * 64 + lane;
+        const bool in = p < A.len;
+        const int e = in ? ev1(A, p, acw, mq, rd, low) : -1;
+        const int mqi = wave_last_incl(e, c);  // own class, or the last one before (depth 0)
+        c = __builtin_amdgcn_readlane(mqi, 63);
+        if (!in) continue;
         uint8_t f = F_LOW;
-        if (p >= A.lo && p < A.hi && acw[p] >= MIN_ACGT) {
-            int r = rd[p] + low[p], mqi;
-            if (r == 0) mqi = last;
-            else if (mq[p] >= A.min_mapq) { mqi = 0; last = 0; }
-            else { mqi = 1; last = 1; }
-            f = (T->wins[mqi][gcw[p]] < NO_COMBINE) ? F_LOW : 0;
-        }
+        if (p >= A.lo && p < A.hi && acw[p] >= MIN_ACGT) f = (T->wins[mqi][gcw[p]] < NO_COMBINE) ? F_LOW : 0;
         if (f == 0) {
-            int g = gcw[p];
+            const int g = gcw[p];
             if ((mq[p] >= A.min_mapq && T->wins[0][g] > 1) || (mq[p] < A.min_mapq && T->wins[1][g] > 1)) f |= F_GUARD;
         }
         flag[p] = f;
@@ -425,73 +412,87 @@ __device__ long d_bisect_right_double(const double *l, double p, long s, long e)
     return i;
 }
 
+// z-score rank index for every (class, bin, depth < ZT_MAX) (ranks mode):
+// the two bisects into the sorted bin sample and the pval2sd bisect of
+// GROM.c:18800-18940 depend on nothing else.  Entry: +/-(pval2sd index + 1)
+// (sign: the depth-above-mean branch), 0: no z (empty bin).
+__device__ int z_rank_index(const Tables *T, const int32_t *samples, int mqi, int bin, int r, double dup_factor) {
+    const long ge = T->cnt[mqi][bin];
+    if (ge <= 0) return 0;
+    const int *list = samples + T->off[mqi][bin];
+    const double ave = T->ave[mqi][bin];
+    long i1, i2;
+    double d1, d2, prob;
+    int sign = 1;
+    if (r < ave) {
+        i1 = d_bisect_right(list, r, 0, ge);
+        i2 = d_bisect_left(list, r, 0, ge);
+    } else {
+        sign = -1;
+        if (r > dup_factor * ave) {
+            i1 = d_bisect_left(list, (int)(dup_factor * ave), 0, ge);  // Q11 truncation
+            i2 = d_bisect_right(list, r, 0, ge);
+        } else {
+            i1 = d_bisect_left(list, r, 0, ge);
+            i2 = d_bisect_right(list, r, 0, ge);
+        }
+        i1 = ge - i1;
+        i2 = ge - i2;
+    }
+    d1 = (i1 <= 0) ? 0.5 : (double)i1;
+    d2 = (i2 <= 0) ? 0.5 : (double)i2;
+    prob = (d1 + d2) / (2 * ge);
+    i1 = d_bisect_right_double(T->p2s_p, prob, 0, T->n_p2s);
+    if (i1 < 0) i1 = 0;
+    else if (i1 >= T->n_p2s) i1 = T->n_p2s - 1;
+    return sign * (int)(i1 + 1);
+}
+
+__global__ void k_cnv_ztab(const Tables *__restrict__ T, const int32_t *__restrict__ samples, double dup_factor,
+                           int16_t *__restrict__ ztab) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * NBINS * ZT_MAX) return;
+    const int r = i % ZT_MAX, bin = (i / ZT_MAX) % NBINS, mqi = i / (ZT_MAX * NBINS);
+    ztab[i] = (int16_t)z_rank_index(T, samples, mqi, bin, r, dup_factor);
+}
+
 // per-base z score, GROM.c:18740-18963 (g_normal == 0)
 __global__ __launch_bounds__(256) void k_cnv_z(Args A, const uint8_t *__restrict__ gcw,
                                                const int32_t *__restrict__ mq, const int32_t *__restrict__ rd,
                                                const int32_t *__restrict__ low, const uint8_t *__restrict__ flag,
                                                const int8_t *__restrict__ carry, const Tables *__restrict__ T,
-                                               const int32_t *__restrict__ samples, double *__restrict__ sd) {
-    __shared__ int sh[256];
-    const int64_t p0 = (int64_t)blockIdx.x * SCAN_TP + (int64_t)threadIdx.x * SCAN_K;
-    int mine = -1;
-    for (int k = 0; k < SCAN_K; k++) {
-        int64_t p = p0 + k;
-        if (p >= A.len) break;
-        int e = ev2(A, p, flag, mq, rd, low);
-        if (e != -1) mine = e;
-    }
-    int last = block_last_excl(mine, carry[blockIdx.x], sh);
-    for (int k = 0; k < SCAN_K; k++) {
-        int64_t p = p0 + k;
-        if (p >= A.len) break;
+                                               const int32_t *__restrict__ samples, const int16_t *__restrict__ ztab,
+                                               double *__restrict__ sd) {
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t p0 = wave * SEG_W;
+    if (p0 >= A.len) return;
+    int c = carry[wave];
+    for (int r0 = 0; r0 < SEG_W / 64; r0++) {
+        const int64_t p = p0 + r0 * 64 + lane;
+        const bool in = p < A.len;
+        const int e = in ? ev2(A, p, flag, mq, rd, low) : -1;
+        const int mqi = wave_last_incl(e, c);
+        c = __builtin_amdgcn_readlane(mqi, 63);
+        if (!in) continue;
         double z = 0.0;
         if (flag[p] & F_GUARD) {
             const int r = rd[p] + low[p], q = mq[p];
-            int mqi;
-            if (q >= A.min_mapq) { mqi = 0; last = 0; }
-            else if (r == 0) mqi = last;
-            else { mqi = 1; last = 1; }
             const int bin = gcw[p];
-            const long ge = T->cnt[mqi][bin];
-            if (ge > 0) {
-                const int *list = samples + T->off[mqi][bin];
-                const double ave = T->ave[mqi][bin], sdv = T->sdv[mqi][bin];
-                const double mqf = A.mapq_factor + (1.0 - A.mapq_factor) * (q - A.min_mapq) / (double)(RD_MAX_MAPQ - A.min_mapq);
-                long i1, i2;
-                double d1, d2, prob;
-                if (r < ave) {
-                    i1 = d_bisect_right(list, r, 0, ge);
-                    i2 = d_bisect_left(list, r, 0, ge);
-                    d1 = (i1 <= 0) ? 0.5 : (double)i1;
-                    d2 = (i2 <= 0) ? 0.5 : (double)i2;
-                    prob = (d1 + d2) / (2 * ge);
-                    i1 = d_bisect_right_double(T->p2s_p, prob, 0, T->n_p2s);
-                    if (i1 < 0) i1 = 0; else if (i1 >= T->n_p2s) i1 = T->n_p2s - 1;
-                    if (A.ranks_stdev == 0) z = (q >= A.min_mapq ? mqf : A.mapq_factor) * (ave - rd[p] - low[p]) / sdv;
-                    else z = (q >= A.min_mapq ? mqf : A.mapq_factor) * T->p2s_sd[i1];
-                } else {
-                    const bool over = r > A.dup_factor * ave;
-                    if (over) {
-                        i1 = d_bisect_left(list, (int)(A.dup_factor * ave), 0, ge);  // Q11 truncation
-                        i2 = d_bisect_right(list, r, 0, ge);
-                    } else {
-                        i1 = d_bisect_left(list, r, 0, ge);
-                        i2 = d_bisect_right(list, r, 0, ge);
-                    }
-                    i1 = ge - i1;
-                    i2 = ge - i2;
-                    d1 = (i1 <= 0) ? 0.5 : (double)i1;
-                    d2 = (i2 <= 0) ? 0.5 : (double)i2;
-                    prob = (d1 + d2) / (2 * ge);
-                    i1 = d_bisect_right_double(T->p2s_p, prob, 0, T->n_p2s);
-                    if (i1 < 0) i1 = 0; else if (i1 >= T->n_p2s) i1 = T->n_p2s - 1;
-                    if (A.ranks_stdev == 0) {
-                        if (over) z = (q >= A.min_mapq ? mqf : A.mapq_factor) * (A.dup_factor - 1) * (-ave) / sdv;
-                        else z = (q >= A.min_mapq ? mqf : A.mapq_factor) * (ave - rd[p] - low[p]) / sdv;
-                    } else {
-                        z = -(q >= A.min_mapq ? mqf : A.mapq_factor) * T->p2s_sd[i1];
-                    }
+            const double f = q >= A.min_mapq
+                                 ? A.mapq_factor + (1.0 - A.mapq_factor) * (q - A.min_mapq) / (double)(RD_MAX_MAPQ - A.min_mapq)
+                                 : A.mapq_factor;
+            if (A.ranks_stdev == 0) {
+                if (T->cnt[mqi][bin] > 0) {
+                    const double ave = T->ave[mqi][bin], sdv = T->sdv[mqi][bin];
+                    if (r < ave || !(r > A.dup_factor * ave)) z = f * (ave - rd[p] - low[p]) / sdv;
+                    else z = f * (A.dup_factor - 1) * (-ave) / sdv;
                 }
+            } else {
+                const int zi = r < ZT_MAX ? ztab[(mqi * NBINS + bin) * ZT_MAX + r]
+                                          : z_rank_index(T, samples, mqi, bin, r, A.dup_factor);
+                if (zi > 0) z = f * T->p2s_sd[zi - 1];
+                else if (zi < 0) z = -f * T->p2s_sd[-zi - 1];
             }
         }
         sd[p] = z;
@@ -516,17 +517,29 @@ __global__ void k_cnv_windows(const WinDesc *__restrict__ wd, int64_t n_win, con
     long cnt = 0, ftot = 0, wl = 0;
     const int64_t ps[3] = {d.p0, d.p1, d.p2}, ns[3] = {d.n0, d.n1, d.n2};
     for (int s = 0; s < 3; s++) {
-        const int64_t pb = ps[s];
-        for (int64_t k = 0; k < ns[s]; k++) {
-            const int64_t p = pb + k;
-            const uint8_t f = flag[p];
-            if (f & F_GUARD) { tot += sd[p]; cnt += 1; }
-            ftot += (f & F_LOW);
-            wl += 1;
-            if (wl >= min_len) {
-                double v = __builtin_nan("");
-                if ((ftot / (double)wl) < MAX_LOW_ACGT && cnt > 0) v = tot / (double)cnt;
-                row[wl] = v;
+        const int64_t pb = ps[s], n = ns[s];
+        for (int64_t k0 = 0; k0 < n; k0 += 8) {
+            // 8 loads in flight, then the sequential sum in reference order
+            uint8_t f[8];
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const bool ok = k0 + j < n;
+                f[j] = ok ? flag[pb + k0 + j] : (uint8_t)0xff;
+                v[j] = ok ? sd[pb + k0 + j] : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (f[j] != 0xff) {
+                    if (f[j] & F_GUARD) { tot += v[j]; cnt += 1; }
+                    ftot += (f[j] & F_LOW);
+                    wl += 1;
+                    if (wl >= min_len) {
+                        double x = __builtin_nan("");
+                        if ((ftot / (double)wl) < MAX_LOW_ACGT && cnt > 0) x = tot / (double)cnt;
+                        row[wl] = x;
+                    }
+                }
             }
         }
     }
@@ -540,12 +553,20 @@ __global__ void k_cnv_window_sq(const double *__restrict__ rows, int64_t n_rows,
     if (l > L) return;
     double s = 0.0;
     int64_t c = 0;
-    for (int64_t r = 0; r < n_rows; r++) {
-        if (row_len[r] < l) continue;
-        double v = rows[r * (L + 1) + l];
-        if (v != v) continue;
-        s += v * v;
-        c += 1;
+    for (int64_t r0 = 0; r0 < n_rows; r0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int64_t r = r0 + j;
+            v[j] = (r < n_rows && row_len[r] >= l) ? rows[r * (L + 1) + l] : __builtin_nan("");
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (v[j] == v[j]) {
+                s += v[j] * v[j];
+                c += 1;
+            }
+        }
     }
     tot[l] = s;
     cnt[l] = c;
@@ -558,115 +579,260 @@ struct CallRec {
     int32_t m, pad;
 };
 
+// per-position bit word the walk reads (one uint16 instead of five arrays)
+constexpr uint32_t B_LOW = 1, B_HI = 2, B_RTP = 4, B_DEL0 = 8, B_DUP0 = 32, B_W0 = 128;
+
+__global__ void k_cnv_wbits(Args A, const uint8_t *__restrict__ gcw, const int32_t *__restrict__ mq,
+                            const int32_t *__restrict__ rd, const int32_t *__restrict__ low,
+                            const uint8_t *__restrict__ flag, const Tables *__restrict__ T, uint16_t *__restrict__ wb) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < A.len; p += (int64_t)gridDim.x * blockDim.x) {
+        const int r = rd[p] + low[p], g = gcw[p];
+        uint32_t b = (flag[p] & F_LOW) ? B_LOW : 0;
+        if (mq[p] >= A.min_mapq) b |= B_HI;
+        if (r > 0) b |= B_RTP;
+        for (int m = 0; m < 2; m++) {
+            if (r <= T->thr[0][m][g]) b |= B_DEL0 << m;  // GROM.c:19373 (DEL), 19688 (DUP)
+            if (r >= T->thr[1][m][g]) b |= B_DUP0 << m;
+            if (T->wins[m][g] > 1) b |= B_W0 << m;
+        }
+        wb[p] = (uint16_t)b;
+    }
+}
+
 struct WalkIn {
-    const uint8_t *gcw, *flag;
-    const int32_t *mq, *rd, *low;
+    const uint16_t *wb;
     const double *sd, *wsd;
-    const Tables *T;
     int64_t len, start, end, L, min_len;
-    int32_t min_mapq;
 };
+
+__device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) {
+    uint64_t u = ((uint64_t)hi << 32) | lo;
+    double d;
+    __builtin_memcpy(&d, &u, 8);
+    return d;
+}
+
+// The walk is one serial computation.  A wave runs it with every lane
+// executing the same uniform statements; per-position inputs come from a
+// 64-position register window (lane i holds position base+i) that is refilled
+// by one coalesced load whenever the walk leaves it, and read with readlane.
+struct Win {
+    const uint16_t *wb;
+    const double *sd;
+    const uint8_t *vis;
+    int64_t len;
+    int64_t base;
+    uint32_t b_l, s_lo, s_hi, v_l;
+    __device__ void fill(int64_t b) {
+        base = b;
+        const int64_t q = b + (int64_t)(threadIdx.x & 63);
+        const bool ok = q >= 0 && q < len;
+        b_l = ok ? wb[q] : 0u;
+        double v = ok ? sd[q] : 0.0;
+        uint64_t u;
+        __builtin_memcpy(&u, &v, 8);
+        s_lo = (uint32_t)u;
+        s_hi = (uint32_t)(u >> 32);
+        v_l = (ok && vis) ? vis[q] : 0u;
+    }
+    __device__ __forceinline__ int slot(int64_t p) {
+        if (p >= base + 64) fill(p);
+        else if (p < base) fill(p - 63);
+        return (int)(p - base);
+    }
+    __device__ __forceinline__ uint32_t bits(int64_t p) {
+        int i = slot(p);
+        return (uint32_t)__builtin_amdgcn_readlane((int)b_l, i);
+    }
+    __device__ __forceinline__ double z(int64_t p) {
+        int i = slot(p);
+        return dbl_of((uint32_t)__builtin_amdgcn_readlane((int)s_lo, i), (uint32_t)__builtin_amdgcn_readlane((int)s_hi, i));
+    }
+    __device__ __forceinline__ uint32_t mark(int64_t p) {
+        int i = slot(p);
+        return (uint32_t)__builtin_amdgcn_readlane((int)v_l, i);
+    }
+};
+
+// state after the first two phases of the window search at one base
+struct PreAB {
+    int64_t temp_pos, ce, last_good;
+    double stdevs;
+    int32_t stop, begin, mqi, pad;
+};
+
+// phases A (first min-window) and B (extension to L) of the window search at
+// a base that passes the threshold (GROM.c:19370-19470 DEL, 19685-19785 DUP);
+// Acc provides bits(p) and z(p)
+template <int KIND, class Acc>
+__device__ PreAB phase_ab(Acc &c, const WalkIn &W, int64_t pos, int mqi) {
+    const int64_t L = W.L, ML = W.min_len, end = W.end;
+    const double *wsd = W.wsd;
+    int begin = 0, stop = 0;
+    int64_t ce = 0, last_good = 0, temp_pos = pos, pa, wl = 0, cnt = 0, cnt2 = 0;
+    double stdevs = 0.0, tot = 0.0;
+    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    auto cls = [](uint32_t b, int m) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : m; };
+    for (pa = pos; pa < pos + ML; pa++) {
+        wl += 1;
+        const uint32_t b = c.bits(pa);
+        if (!(b & B_LOW)) {
+            mqi = cls(b, mqi);
+            if (b & (pb0 << mqi)) cnt2 += 1;
+            else if ((2 * cnt2) < wl) { stop = 1; temp_pos = pa; break; }
+        } else if ((2 * cnt2) < wl) { stop = 1; temp_pos = pa; break; }
+    }
+    if (stop == 0) {
+        cnt = ML;
+        tot = 0;
+        for (int64_t a = pos; a < pos + ML; a++) {
+            cnt -= (c.bits(a) & B_LOW);
+            if (KIND == 0) tot += c.z(a); else tot -= c.z(a);
+        }
+    }
+    if (stop == 0 && cnt > 0 && wsd[ML] > 0 && (tot / (cnt * wsd[ML])) >= MIN_RD_LOW_STDEV &&
+        ((ML - cnt) / ((double)ML)) <= MAX_LOW_ACGT) {
+        begin = 1;
+        last_good = pos + ML;
+        ce = pos + ML;
+        stdevs = tot / (cnt * wsd[ML]);
+    }
+    if (stop == 0) {
+        for (pa = pos + ML; pa < pos + L; pa++) {
+            wl += 1;
+            if (pa < end) {
+                const uint32_t b = c.bits(pa);
+                if (!(b & B_LOW)) {
+                    mqi = cls(b, mqi);
+                    if (KIND == 0) tot += c.z(pa); else tot -= c.z(pa);
+                    cnt += 1;
+                    if (b & (pb0 << mqi)) {
+                        cnt2 += 1;
+                        if (wsd[wl] > 0 && (tot / (cnt * wsd[wl])) >= MIN_RD_LOW_STDEV &&
+                            ((wl - cnt) / ((double)wl)) <= MAX_LOW_ACGT) {
+                            last_good = pa;
+                            if (begin == 0) {
+                                begin = 1;
+                                ce = pa;
+                                stdevs = tot / (cnt * wsd[wl]);
+                            } else {
+                                double ts = tot / (cnt * wsd[wl]);
+                                ce = pa;
+                                if (ts > stdevs) stdevs = ts;
+                            }
+                        }
+                    } else if ((2 * cnt2) < wl) { stop = 1; break; }
+                } else if ((2 * cnt2) < wl) { stop = 1; break; }
+            } else { stop = 1; break; }
+        }
+    }
+    PreAB r;
+    r.temp_pos = temp_pos;
+    r.ce = ce;
+    r.last_good = last_good;
+    r.stdevs = stdevs;
+    r.stop = stop;
+    r.begin = begin;
+    r.mqi = mqi;
+    r.pad = 0;
+    return r;
+}
+
+struct GAcc {  // direct loads (one lane per base)
+    const uint16_t *wb;
+    const double *sd;
+    __device__ __forceinline__ uint32_t bits(int64_t p) const { return wb[p]; }
+    __device__ __forceinline__ double z(int64_t p) const { return sd[p]; }
+};
+
+// a base's first two phases, for every base and class the walk can meet it in:
+// nxt[m][p] = the position the walk continues from (before its +1), or
+// -(k+2) for a call whose record pre[k] the walk completes (phases C, D)
+template <int KIND>
+__global__ void k_cnv_pre(WalkIn W, int32_t *__restrict__ nxt, PreAB *__restrict__ pre, uint32_t *n_pre, uint32_t cap,
+                          int64_t *__restrict__ pre_pos) {
+    const int64_t p = W.start + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= W.end) return;
+    GAcc c{W.wb, W.sd};
+    const uint32_t b = c.bits(p);
+    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    for (int m = 0; m < 2; m++) {
+        int32_t out = (int32_t)p;
+        const bool reach = (b & B_HI) ? m == 0 : (b & B_RTP) ? m == 1 : true;  // classes the walk can be in here
+        if (reach && (b & (pb0 << m))) {
+            PreAB r = phase_ab<KIND>(c, W, p, m);
+            if (r.begin == 1) {
+                uint32_t k = atomicAdd(n_pre, 1u);
+                if (k < cap) {
+                    pre[k] = r;
+                    pre_pos[k] = p;
+                    out = -(int32_t)k - 2;
+                }  // else: overflow, the host re-runs with a larger buffer
+            } else if (r.stop == 1) {
+                out = (int32_t)r.temp_pos;
+            }
+        }
+        nxt[m * W.len + p] = out;
+    }
+}
 
 template <int KIND>
 struct Walk {
     WalkIn W;
-    __device__ __forceinline__ int rt(int64_t p) const { return W.rd[p] + W.low[p]; }
-    __device__ __forceinline__ bool pass(int64_t p, int m) const {
-        const double t = W.T->thr[KIND][m][W.gcw[p]];
-        return KIND == 0 ? (rt(p) <= t) : (rt(p) >= t);
+    Win c;
+    const int32_t *nxt;
+    const PreAB *pre;
+    __device__ Walk(const WalkIn &w, const uint8_t *vis, const int32_t *nx, const PreAB *pr) : W(w), nxt(nx), pre(pr) {
+        c.wb = w.wb;
+        c.sd = w.sd;
+        c.vis = vis;
+        c.len = w.len;
+        c.base = INT64_MIN / 4;
+    }
+    __device__ __forceinline__ bool pass(uint32_t b, int m) const {
+        return (b & ((KIND == 0 ? B_DEL0 : B_DUP0) << m)) != 0;
     }
     __device__ __forceinline__ void add(double &x, double v) const { if (KIND == 0) x += v; else x -= v; }
     __device__ __forceinline__ void sub(double &x, double v) const { if (KIND == 0) x -= v; else x += v; }
-    __device__ __forceinline__ bool lowf(int64_t p) const { return (W.flag[p] & F_LOW) != 0; }
+    // mq >= -q -> class 0, else depth > 0 -> class 1, else unchanged
+    __device__ __forceinline__ static int cls(uint32_t b, int m) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : m; }
     // update at a visited base; returns the class (== the state after it)
-    __device__ __forceinline__ int visit(int64_t pos, int &last) const {
-        if (W.mq[pos] >= W.min_mapq) { last = 0; return 0; }
-        if (rt(pos) > 0) { last = 1; return 1; }
+    __device__ __forceinline__ int visit(int64_t pos, int &last) {
+        last = cls(c.bits(pos), last);
         return last;
     }
-    // the body of the reference's `if` at a base that passes the threshold:
-    // returns the position the walk continues from (before its `pos += 1`)
-    __device__ int64_t block(int64_t pos, int mqi, CallRec &call, bool &is_call) const {
-        const int64_t L = W.L, ML = W.min_len, end = W.end;
+    // the reference's `if` body at a base that passes the threshold: phases A
+    // and B come precomputed; a call is completed here (phase C: the sliding
+    // extension past L, phase D: trimming the end).  Returns the position the
+    // walk continues from (before its `pos += 1`).
+    __device__ int64_t block(int64_t pos, int mqi, CallRec &call, bool &is_call) {
+        const int32_t n = nxt[mqi * W.len + pos];
+        is_call = n < -1;
+        if (!is_call) return n;
+        const PreAB r = pre[-n - 2];
+        const int64_t L = W.L, ML = W.min_len, cs = pos;
         const double *wsd = W.wsd;
-        int begin = 0, stop = 0;
-        int64_t cs = 0, ce = 0, last_good = 0, temp_pos = pos, pa, pb, wl = 0, cnt = 0, cnt2 = 0;
-        double stdevs = 0.0, tot = 0.0;
-        for (pa = pos; pa < pos + ML; pa++) {
-            wl += 1;
-            if (!lowf(pa)) {
-                if (W.mq[pa] >= W.min_mapq) mqi = 0;
-                else if (rt(pa) > 0) mqi = 1;
-                if (pass(pa, mqi)) cnt2 += 1;
-                else if ((2 * cnt2) < wl) { stop = 1; temp_pos = pa; break; }
-            } else if ((2 * cnt2) < wl) { stop = 1; temp_pos = pa; break; }
-        }
-        if (stop == 0) {
-            cnt = ML;
-            tot = 0;
-            for (int64_t a = pos; a < pos + ML; a++) {
-                cnt -= (W.flag[a] & F_LOW);
-                add(tot, W.sd[a]);
-            }
-        }
-        if (stop == 0 && cnt > 0 && wsd[ML] > 0 && (tot / (cnt * wsd[ML])) >= MIN_RD_LOW_STDEV &&
-            ((ML - cnt) / ((double)ML)) <= MAX_LOW_ACGT) {
-            begin = 1;
-            cs = pos;
-            last_good = pos + ML;
-            ce = pos + ML;
-            stdevs = tot / (cnt * wsd[ML]);
-        }
-        if (stop == 0) {
-            for (pa = pos + ML; pa < pos + L; pa++) {
-                wl += 1;
-                if (pa < end) {
-                    if (!lowf(pa)) {
-                        if (W.mq[pa] >= W.min_mapq) mqi = 0;
-                        else if (rt(pa) > 0) mqi = 1;
-                        add(tot, W.sd[pa]);
-                        cnt += 1;
-                        if (pass(pa, mqi)) {
-                            cnt2 += 1;
-                            if (wsd[wl] > 0 && (tot / (cnt * wsd[wl])) >= MIN_RD_LOW_STDEV &&
-                                ((wl - cnt) / ((double)wl)) <= MAX_LOW_ACGT) {
-                                last_good = pa;
-                                if (begin == 0) {
-                                    begin = 1;
-                                    cs = pos;
-                                    ce = pa;
-                                    stdevs = tot / (cnt * wsd[wl]);
-                                } else {
-                                    double ts = tot / (cnt * wsd[wl]);
-                                    ce = pa;
-                                    if (ts > stdevs) stdevs = ts;
-                                }
-                            }
-                        } else if ((2 * cnt2) < wl) { stop = 1; break; }
-                    } else if ((2 * cnt2) < wl) { stop = 1; break; }
-                } else { stop = 1; break; }
-            }
-        }
-        if (stop == 0 && begin == 1) {
+        int64_t ce = r.ce, last_good = r.last_good, pa, pb, cnt = 0;
+        double stdevs = r.stdevs, tot = 0.0;
+        mqi = r.mqi;
+        if (r.stop == 0) {
             pa = pos + L;
-            tot = 0;
-            cnt = 0;
             int mqb = mqi;
             while (pa < W.len && (pa - last_good) <= MAX_DIST_LAST_GOOD) {
                 if (pa == pos + L) {
                     for (pb = pa - L + 1; pb < pa + 1; pb++) {
-                        if (W.mq[pb] >= W.min_mapq) mqb = 0;
-                        else if (rt(pb) > 0) mqb = 1;
-                        if (!lowf(pb) && W.T->wins[mqb][W.gcw[pb]] > 1) { add(tot, W.sd[pb]); cnt += 1; }
+                        const uint32_t b = c.bits(pb);
+                        mqb = cls(b, mqb);
+                        if (!(b & B_LOW) && (b & (B_W0 << mqb))) { add(tot, c.z(pb)); cnt += 1; }
                     }
                 } else {
                     pb = pa - L;
-                    if (W.mq[pb] >= W.min_mapq) mqb = 0;
-                    else if (rt(pb) > 0) mqb = 1;
-                    if (!lowf(pb) && W.T->wins[mqb][W.gcw[pb]] > 1) { sub(tot, W.sd[pb]); cnt -= 1; }
-                    if (W.mq[pa] >= W.min_mapq) mqi = 0;
-                    else if (rt(pa) > 0) mqi = 1;
-                    if (!lowf(pa) && W.T->wins[mqi][W.gcw[pa]] > 1) { add(tot, W.sd[pa]); cnt += 1; }
+                    const uint32_t bb = c.bits(pb);
+                    mqb = cls(bb, mqb);
+                    if (!(bb & B_LOW) && (bb & (B_W0 << mqb))) { sub(tot, c.z(pb)); cnt -= 1; }
+                    const uint32_t ba = c.bits(pa);
+                    mqi = cls(ba, mqi);
+                    if (!(ba & B_LOW) && (ba & (B_W0 << mqi))) { add(tot, c.z(pa)); cnt += 1; }
                 }
                 if (cnt > 0 && wsd[L] > 0 && (tot / (cnt * wsd[L])) >= MIN_RD_LOW_STDEV &&
                     ((L - cnt) / ((double)L)) <= MAX_LOW_ACGT) {
@@ -678,42 +844,38 @@ struct Walk {
                 pa += 1;
             }
         }
-        is_call = begin == 1;
-        if (begin == 1) {
-            int64_t p = ce;
-            while (p > cs + ML) {
-                if (W.mq[p] >= W.min_mapq) mqi = 0;
-                else if (rt(p) > 0) mqi = 1;
-                if (!pass(p, mqi)) {
-                    p -= 1;
-                    ce = p;
-                } else {
-                    int64_t c2 = 0, c3 = 0;
-                    pa = ce;
-                    int stop_while = 0, mqa = mqi;
-                    while (pa > cs + ML && stop_while == 0) {
-                        if (!lowf(pa)) {
-                            if (W.mq[pa] >= W.min_mapq) mqa = 0;
-                            else if (rt(pa) > 0) mqa = 1;
-                            c3 += 1;
-                            if (pass(pa, mqa)) c2 += 1;
-                        }
-                        if (c3 == 0 || (c3 > 0 && (c2 / ((double)c3)) < 0.5) ||
-                            ((ce - pa + 1 - c3) / ((double)ce - (double)pa + 1.0)) > MAX_LOW_ACGT) {
-                            ce = pa - 1;
-                            stop_while = 1;
-                        }
-                        pa -= 1;
+        int64_t p = ce;
+        while (p > cs + ML) {
+            const uint32_t b = c.bits(p);
+            mqi = cls(b, mqi);
+            if (!pass(b, mqi)) {
+                p -= 1;
+                ce = p;
+            } else {
+                int64_t c2 = 0, c3 = 0;
+                pa = ce;
+                int stop_while = 0, mqa = mqi;
+                while (pa > cs + ML && stop_while == 0) {
+                    const uint32_t ba = c.bits(pa);
+                    if (!(ba & B_LOW)) {
+                        mqa = cls(ba, mqa);
+                        c3 += 1;
+                        if (pass(ba, mqa)) c2 += 1;
                     }
-                    p = pa;
+                    if (c3 == 0 || (c3 > 0 && (c2 / ((double)c3)) < 0.5) ||
+                        ((ce - pa + 1 - c3) / ((double)ce - (double)pa + 1.0)) > MAX_LOW_ACGT) {
+                        ce = pa - 1;
+                        stop_while = 1;
+                    }
+                    pa -= 1;
                 }
+                p = pa;
             }
-            call.p = cs;
-            call.ce = ce;
-            call.stdevs = stdevs;
-            return ce + 1;
         }
-        return stop == 1 ? temp_pos : pos;
+        call.p = cs;
+        call.ce = ce;
+        call.stdevs = stdevs;
+        return ce + 1;
     }
 };
 
@@ -724,115 +886,157 @@ struct ChunkState {
 };
 enum { ST_MERGED = 0, ST_NOMERGE = 1, ST_PASSTHRU = 2, ST_FIRST = 3 };
 
-template <int KIND>
-__device__ void emit_call(const CallRec &c, int m, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
-    uint32_t k = atomicAdd(n_calls, 1u);
-    if (k < cap) {
-        calls[k] = c;
-        calls[k].m = m;
+__device__ __forceinline__ void emit_call(const CallRec &c, int m, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
+    if ((threadIdx.x & 63) == 0) {
+        uint32_t k = atomicAdd(n_calls, 1u);
+        if (k < cap) {
+            calls[k] = c;
+            calls[k].m = m;
+        }
     }
 }
+__device__ __forceinline__ void put_mark(uint8_t *vis, int64_t p, int v) {
+    if ((threadIdx.x & 63) == 0) vis[p] = (uint8_t)v;
+}
 
-// walk [from, chunk end) from state (from, last); mode 0: speculative first
-// pass (marks, calls); mode 1: reconciliation of chunk k from the previous
-// chunk's speculative exit.  vis[p] = 1 + class for every visited base.
+// One wave per chunk.  mode 0: speculative first pass from (chunk start,
+// class 0) -- exact for chunk 0 -- leaving marks vis[p] = 1 + class at every
+// visited base and the calls it finds; mode 1: reconciliation of chunk k from
+// chunk k-1's speculative exit up to the first base both walks visit in the
+// same state (from there the walks are identical).
 template <int KIND>
-__global__ void k_cnv_walk(WalkIn W, int mode, int64_t n_chunks, int64_t chunk, uint8_t *__restrict__ vis,
-                           ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64) void k_cnv_walk(WalkIn W, const int32_t *nxt, const PreAB *pre, int mode,
+                                                 int64_t n_chunks, int64_t chunk, uint8_t *__restrict__ vis,
+                                                 ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
+                                                 uint32_t cap) {
+    const int64_t k = blockIdx.x;
     if (k >= n_chunks) return;
-    Walk<KIND> w{W};
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
     if (mode == 0) {
+        Walk<KIND> w(W, nullptr, nxt, pre);
         int64_t pos = c0;
-        int last = 0;  // a guess except for chunk 0 (GROM.c:19366-19367)
+        int last = 0;  // exact for chunk 0 (GROM.c:19366-19367), a guess elsewhere
         while (pos < c1) {
             int m = w.visit(pos, last);
-            vis[pos] = (uint8_t)(1 + m);
-            if (w.pass(pos, m)) {
+            put_mark(vis, pos, 1 + m);
+            if (w.pass(w.c.bits(pos), m)) {
                 CallRec c;
                 bool is_call = false;
                 pos = w.block(pos, m, c, is_call);
-                if (is_call) emit_call<KIND>(c, m, calls, n_calls, cap);
+                if (is_call) emit_call(c, m, calls, n_calls, cap);
             }
             pos += 1;
         }
-        cs[k].x1 = pos;
-        cs[k].l1 = last;
-        cs[k].status = k == 0 ? ST_FIRST : ST_MERGED;
+        if ((threadIdx.x & 63) == 0) {
+            cs[k].x1 = pos;
+            cs[k].l1 = last;
+            cs[k].status = k == 0 ? ST_FIRST : ST_MERGED;
+        }
         return;
     }
     if (k == 0) return;
-    // mode 1: enter from chunk k-1's speculative exit
     const int64_t x = cs[k - 1].x1;
     const int l = cs[k - 1].l1;
     if (x >= c1) {  // chunk k lies inside a jump of chunk k-1
-        for (int64_t p = c0; p < c1; p++) vis[p] = 0;
-        cs[k].status = ST_PASSTHRU;
+        for (int64_t p = c0 + (threadIdx.x & 63); p < c1; p += 64) vis[p] = 0;
+        if ((threadIdx.x & 63) == 0) cs[k].status = ST_PASSTHRU;
         return;
     }
-    // pass 1: find the first base both walks visit in the same state
-    int64_t pos = x, merge = -1;
-    int last = l;
-    while (pos < c1) {
-        int m = w.visit(pos, last);
-        if (vis[pos] == 1 + m) { merge = pos; break; }
-        if (w.pass(pos, m)) {
-            CallRec c;
-            bool is_call = false;
-            pos = w.block(pos, m, c, is_call);
+    // pass 1: the first base both walks visit in the same state
+    int64_t merge = -1;
+    {
+        Walk<KIND> w(W, vis, nxt, pre);
+        int64_t pos = x;
+        int last = l;
+        while (pos < c1) {
+            int m = w.visit(pos, last);
+            if (w.c.mark(pos) == (uint32_t)(1 + m)) { merge = pos; break; }
+            if (w.pass(w.c.bits(pos), m)) {
+                CallRec c;
+                bool is_call = false;
+                pos = w.block(pos, m, c, is_call);
+            }
+            pos += 1;
         }
-        pos += 1;
     }
     const int64_t stop_at = merge >= 0 ? merge : c1;
-    for (int64_t p = c0; p < stop_at; p++) vis[p] = 0;
+    for (int64_t p = c0 + (threadIdx.x & 63); p < stop_at; p += 64) vis[p] = 0;
+    __syncthreads();
     // pass 2: the true walk up to the merge point, with marks and calls
-    pos = x;
-    last = l;
+    Walk<KIND> w(W, nullptr, nxt, pre);
+    int64_t pos = x;
+    int last = l;
     while (pos < stop_at) {
         int m = w.visit(pos, last);
-        vis[pos] = (uint8_t)(1 + m);
-        if (w.pass(pos, m)) {
+        put_mark(vis, pos, 1 + m);
+        if (w.pass(w.c.bits(pos), m)) {
             CallRec c;
             bool is_call = false;
             pos = w.block(pos, m, c, is_call);
-            if (is_call) emit_call<KIND>(c, m, calls, n_calls, cap);
+            if (is_call) emit_call(c, m, calls, n_calls, cap);
         }
         pos += 1;
     }
-    if (merge >= 0) {
-        cs[k].status = ST_MERGED;
-    } else {
-        cs[k].status = ST_NOMERGE;
-        cs[k].x2 = pos;
-        cs[k].l2 = last;
+    if ((threadIdx.x & 63) == 0) {
+        if (merge >= 0) {
+            cs[k].status = ST_MERGED;
+        } else {
+            cs[k].status = ST_NOMERGE;
+            cs[k].x2 = pos;
+            cs[k].l2 = last;
+        }
     }
 }
 
-// sequential repair of one chunk from a known-true entry (rare: only after a
-// pass-through or a chunk whose walks never met)
+// repair of one chunk from a known-true entry (x, l): like mode 1, it walks
+// until it meets a base that an earlier walk of this chunk visited in the
+// same state (from there that walk's marks, calls and exit hold) and reports
+// in cs[k].status whether it met one (ST_MERGED) or walked the chunk to its
+// end (ST_NOMERGE, exit in x2/l2)
 template <int KIND>
-__global__ void k_cnv_walk_fix(WalkIn W, int64_t k, int64_t chunk, int64_t x, int l, uint8_t *__restrict__ vis,
-                               ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    Walk<KIND> w{W};
+__global__ __launch_bounds__(64) void k_cnv_walk_fix(WalkIn W, const int32_t *nxt, const PreAB *pre, int64_t k,
+                                                     int64_t chunk, int64_t x, int l, uint8_t *__restrict__ vis,
+                                                     ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
+                                                     uint32_t cap) {
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
-    for (int64_t p = c0; p < c1; p++) vis[p] = 0;
+    int64_t merge = -1;
+    {
+        Walk<KIND> w(W, vis, nxt, pre);
+        int64_t pos = x;
+        int last = l;
+        while (pos < c1) {
+            int m = w.visit(pos, last);
+            if (w.c.mark(pos) == (uint32_t)(1 + m)) { merge = pos; break; }
+            if (w.pass(w.c.bits(pos), m)) {
+                CallRec c;
+                bool is_call = false;
+                pos = w.block(pos, m, c, is_call);
+            }
+            pos += 1;
+        }
+    }
+    const int64_t stop_at = merge >= 0 ? merge : c1;
+    for (int64_t p = c0 + (threadIdx.x & 63); p < stop_at; p += 64) vis[p] = 0;
+    __syncthreads();
+    Walk<KIND> w(W, nullptr, nxt, pre);
     int64_t pos = x;
     int last = l;
-    while (pos < c1) {
+    while (pos < stop_at) {
         int m = w.visit(pos, last);
-        vis[pos] = (uint8_t)(1 + m);
-        if (w.pass(pos, m)) {
+        put_mark(vis, pos, 1 + m);
+        if (w.pass(w.c.bits(pos), m)) {
             CallRec c;
             bool is_call = false;
             pos = w.block(pos, m, c, is_call);
-            if (is_call) emit_call<KIND>(c, m, calls, n_calls, cap);
+            if (is_call) emit_call(c, m, calls, n_calls, cap);
         }
         pos += 1;
     }
-    cs[k].x2 = pos;
-    cs[k].l2 = last;
+    if ((threadIdx.x & 63) == 0) {
+        cs[k].status = merge >= 0 ? ST_MERGED : ST_NOMERGE;
+        cs[k].x2 = pos;
+        cs[k].l2 = last;
+    }
 }
 
 // a call is on the true walk iff its start was visited in its class
@@ -851,7 +1055,7 @@ struct Buf {
 }  // namespace
 
 struct CnvScratch {
-    Buf gcw, acw, rtype, flag, sd, vis, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
+    Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
 };
@@ -984,7 +1188,8 @@ CnvScratch *cnv_scratch_new() { return new CnvScratch(); }
 
 void cnv_scratch_free(CnvScratch *S) {
     if (!S) return;
-    Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->rep, &S->misc, &S->blk, &S->hist,
+    Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre,
+                  &S->prepos, &S->rep, &S->misc, &S->blk, &S->hist,
                   &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
                   &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok};
     for (Buf *b : all)
@@ -1025,20 +1230,21 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     A.mapq_factor = P.mapq_factor;
     A.dup_factor = (double)P.dup_threshold_factor;
     const int64_t n_blk = len / BLOCK_UNIT;
-    const int64_t n_scan = (len + SCAN_TP - 1) / SCAN_TP;
+    const int64_t n_seg = (len + SEG_W - 1) / SEG_W;
     if ((rc = grow(S->gcw, len, err, errlen)) || (rc = grow(S->acw, len, err, errlen)) ||
         (rc = grow(S->rtype, len, err, errlen)) || (rc = grow(S->flag, len, err, errlen)) ||
         (rc = grow(S->sd, 8 * len, err, errlen)) || (rc = grow(S->vis, len, err, errlen)) ||
+        (rc = grow(S->wbits, 2 * len, err, errlen)) ||
         (rc = grow(S->misc, 4096, err, errlen)) || (rc = grow(S->blk, 8 * (n_blk + 1), err, errlen)) ||
-        (rc = grow(S->hist, 4 * (HIST_MAX + 1), err, errlen)) || (rc = grow(S->tiles, n_scan, err, errlen)) ||
-        (rc = grow(S->carry, n_scan, err, errlen)) || (rc = grow(S->tabs, sizeof(Tables), err, errlen)))
+        (rc = grow(S->hist, 4 * (HIST_MAX + 1), err, errlen)) || (rc = grow(S->tiles, n_seg, err, errlen)) ||
+        (rc = grow(S->carry, n_seg, err, errlen)) || (rc = grow(S->ztab, 2 * 2 * NBINS * ZT_MAX, err, errlen)) || (rc = grow(S->tabs, sizeof(Tables), err, errlen)))
         return rc;
     uint8_t *gcw = (uint8_t *)S->gcw.p, *acw = (uint8_t *)S->acw.p, *rtype = (uint8_t *)S->rtype.p,
             *flag = (uint8_t *)S->flag.p;
     double *sd = (double *)S->sd.p;
     char *misc = (char *)S->misc.p;
     unsigned long long *acc = (unsigned long long *)misc;  // [0..3] block/chromosome sums
-    uint32_t *n_rep = (uint32_t *)(misc + 64), *n_calls = (uint32_t *)(misc + 68);
+    uint32_t *n_rep = (uint32_t *)(misc + 64), *n_calls = (uint32_t *)(misc + 72), *n_pre = (uint32_t *)(misc + 76);
     CK(hipEventRecord(S->e0, st));
     CK(hipMemsetAsync(misc, 0, 128, st));
     CK(hipMemsetAsync(S->hist.p, 0, 4 * (HIST_MAX + 1), st));
@@ -1310,16 +1516,17 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
 
         // ---- flags, z scores ----
         int8_t *tl = (int8_t *)S->tiles.p, *cr = (int8_t *)S->carry.p;
-        hipLaunchKernelGGL(k_cnv_tile_last<1>, dim3((unsigned)n_scan), dim3(256), 0, st, A, acw, flag, d_mq, d_rd,
-                           d_low, tl);
-        hipLaunchKernelGGL(k_cnv_carry, dim3(1), dim3(1024), 0, st, tl, n_scan, cr);
-        hipLaunchKernelGGL(k_cnv_flags, dim3((unsigned)n_scan), dim3(256), 0, st, A, acw, gcw, d_mq, d_rd, d_low, cr,
-                           dT, flag);
-        hipLaunchKernelGGL(k_cnv_tile_last<2>, dim3((unsigned)n_scan), dim3(256), 0, st, A, acw, flag, d_mq, d_rd,
-                           d_low, tl);
-        hipLaunchKernelGGL(k_cnv_carry, dim3(1), dim3(1024), 0, st, tl, n_scan, cr);
-        hipLaunchKernelGGL(k_cnv_z, dim3((unsigned)n_scan), dim3(256), 0, st, A, gcw, d_mq, d_rd, d_low, flag, cr, dT,
-                           (const int32_t *)S->samples.p, sd);
+        const unsigned sblk = (unsigned)((n_seg + 3) / 4);  // 4 waves per block
+        hipLaunchKernelGGL(k_cnv_seg_last<1>, dim3(sblk), dim3(256), 0, st, A, acw, flag, d_mq, d_rd, d_low, tl);
+        hipLaunchKernelGGL(k_cnv_carry, dim3(1), dim3(1024), 0, st, tl, n_seg, cr);
+        hipLaunchKernelGGL(k_cnv_flags, dim3(sblk), dim3(256), 0, st, A, acw, gcw, d_mq, d_rd, d_low, cr, dT, flag);
+        hipLaunchKernelGGL(k_cnv_seg_last<2>, dim3(sblk), dim3(256), 0, st, A, acw, flag, d_mq, d_rd, d_low, tl);
+        hipLaunchKernelGGL(k_cnv_carry, dim3(1), dim3(1024), 0, st, tl, n_seg, cr);
+        if (P.ranks_stdev != 0)
+            hipLaunchKernelGGL(k_cnv_ztab, dim3((2 * NBINS * ZT_MAX + 255) / 256), dim3(256), 0, st, dT,
+                               (const int32_t *)S->samples.p, A.dup_factor, (int16_t *)S->ztab.p);
+        hipLaunchKernelGGL(k_cnv_z, dim3(sblk), dim3(256), 0, st, A, gcw, d_mq, d_rd, d_low, flag, cr, dT,
+                           (const int32_t *)S->samples.p, (const int16_t *)S->ztab.p, sd);
         CK(hipGetLastError());
 
         // ---- window means by length, GROM.c:18967-19018 ----
@@ -1454,30 +1661,44 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CK(hipMemcpyAsync(S->wsd.p, wsd.data(), 8 * (L + 1), hipMemcpyHostToDevice, st));
 
         // ---- DEL then DUP walk over the one lowvar block [m-1, len-W) ----
-        WalkIn WI{gcw, flag, d_mq, d_rd, d_low, sd, (const double *)S->wsd.p, dT, len, m - 1,
-                  (len - W) - ML, L, ML, P.rd_min_mapq};
+        hipLaunchKernelGGL(k_cnv_wbits, dim3((unsigned)std::min<int64_t>((len + 255) / 256, 65536)), dim3(256), 0, st,
+                           A, gcw, d_mq, d_rd, d_low, flag, dT, (uint16_t *)S->wbits.p);
+        CK(hipGetLastError());
+        WalkIn WI{(const uint16_t *)S->wbits.p, sd, (const double *)S->wsd.p, len, m - 1, (len - W) - ML, L, ML};
         const int64_t span = std::max<int64_t>(0, WI.end - WI.start);
         const int64_t n_ch = (span + WALK_CHUNK - 1) / WALK_CHUNK;
         uint32_t call_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, len / 1000), 1 << 24);
+        uint32_t pre_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, len / 64), 1 << 26);
         std::vector<CallRec> found[2];
         for (int kind = 0; kind < 2 && n_ch > 0; kind++) {
             for (int attempt = 0; attempt < 2; attempt++) {
-                if ((rc = grow(S->calls, sizeof(CallRec) * call_cap, err, errlen)) ||
+                if ((rc = grow(S->nxt, 8 * (size_t)len, err, errlen)) ||
+                    (rc = grow(S->pre, sizeof(PreAB) * pre_cap, err, errlen)) ||
+                    (rc = grow(S->prepos, 8 * (size_t)pre_cap, err, errlen)) ||
+                    (rc = grow(S->calls, sizeof(CallRec) * call_cap, err, errlen)) ||
                     (rc = grow(S->ok, call_cap, err, errlen)) ||
                     (rc = grow(S->tiles, sizeof(ChunkState) * n_ch, err, errlen)))
                     return rc;
                 ChunkState *dcs = (ChunkState *)S->tiles.p;
                 CallRec *dcalls = (CallRec *)S->calls.p;
                 uint8_t *vis = (uint8_t *)S->vis.p;
-                CK(hipMemsetAsync(n_calls, 0, 4, st));
+                CK(hipMemsetAsync(n_calls, 0, 8, st));  // n_calls, n_pre
                 CK(hipMemsetAsync(vis, 0, len, st));
-                const unsigned gch = (unsigned)((n_ch + 63) / 64);
+                int32_t *nxt = (int32_t *)S->nxt.p;
+                PreAB *pre = (PreAB *)S->pre.p;
+                const unsigned gpre = (unsigned)((span + 255) / 256);
+                if (kind == 0)
+                    hipLaunchKernelGGL(k_cnv_pre<0>, dim3(gpre), dim3(256), 0, st, WI, nxt, pre, n_pre, pre_cap, (int64_t *)S->prepos.p);
+                else
+                    hipLaunchKernelGGL(k_cnv_pre<1>, dim3(gpre), dim3(256), 0, st, WI, nxt, pre, n_pre, pre_cap, (int64_t *)S->prepos.p);
+                CK(hipGetLastError());
+                const unsigned gch = (unsigned)n_ch;  // one wave per chunk
                 if (kind == 0) {
-                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
                 } else {
-                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
                 }
                 CK(hipGetLastError());
                 std::vector<ChunkState> hcs(n_ch);
@@ -1486,30 +1707,45 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 // reconcile: the true exit of each chunk, in order (GROM.c's walk is one pass)
                 int64_t tx = hcs[0].x1;
                 int tl_ = hcs[0].l1;
+                int64_t n_fix = 0;
                 for (int64_t k = 1; k < n_ch; k++) {
                     const bool entry_ok = tx == hcs[k - 1].x1 && tl_ == hcs[k - 1].l1;
-                    const int64_t c1 = std::min<int64_t>(WI.end, WI.start + (k + 1) * WALK_CHUNK);
-                    if (entry_ok && hcs[k].status == ST_MERGED) { tx = hcs[k].x1; tl_ = hcs[k].l1; continue; }
-                    if (entry_ok && hcs[k].status == ST_NOMERGE) { tx = hcs[k].x2; tl_ = hcs[k].l2; continue; }
+                    const int64_t c0 = WI.start + k * WALK_CHUNK, c1 = std::min<int64_t>(WI.end, c0 + WALK_CHUNK);
+                    // the exit of the walk whose marks this chunk holds after its mode-1 pass
+                    const int64_t ex = hcs[k].status == ST_NOMERGE ? hcs[k].x2 : hcs[k].x1;
+                    const int el = hcs[k].status == ST_NOMERGE ? hcs[k].l2 : hcs[k].l1;
+                    if (entry_ok && hcs[k].status != ST_PASSTHRU) { tx = ex; tl_ = el; continue; }
                     if (tx >= c1) {  // the true walk jumps over this chunk
-                        CK(hipMemsetAsync(vis + (WI.start + k * WALK_CHUNK), 0, c1 - (WI.start + k * WALK_CHUNK), st));
+                        CK(hipMemsetAsync(vis + c0, 0, c1 - c0, st));
                         continue;
                     }
                     if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_walk_fix<0>, dim3(1), dim3(64), 0, st, WI, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
+                        hipLaunchKernelGGL(k_cnv_walk_fix<0>, dim3(1), dim3(64), 0, st, WI, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
                     else
-                        hipLaunchKernelGGL(k_cnv_walk_fix<1>, dim3(1), dim3(64), 0, st, WI, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
+                        hipLaunchKernelGGL(k_cnv_walk_fix<1>, dim3(1), dim3(64), 0, st, WI, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
                     CK(hipGetLastError());
                     ChunkState one;
                     CK(hipMemcpyAsync(&one, dcs + k, sizeof(ChunkState), hipMemcpyDeviceToHost, st));
                     CK(hipStreamSynchronize(st));
-                    tx = one.x2;
-                    tl_ = one.l2;
+                    n_fix++;
+                    if (one.status == ST_MERGED && hcs[k].status != ST_PASSTHRU) { tx = ex; tl_ = el; }
+                    else { tx = one.x2; tl_ = one.l2; }
                 }
+                if (getenv("GROM_TIMING"))
+                    fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired\n", kind == 0 ? "DEL" : "DUP",
+                            (long long)n_ch, (long long)n_fix);
                 uint32_t nc = 0;
                 CK(hipMemcpyAsync(&nc, n_calls, 4, hipMemcpyDeviceToHost, st));
                 CK(hipStreamSynchronize(st));
-                if (nc > call_cap) { call_cap = nc + nc / 4 + 1024; continue; }
+                uint32_t npre = 0;
+                CK(hipMemcpyAsync(&npre, n_pre, 4, hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+                if (npre > pre_cap || nc > call_cap) {
+                    pre_cap = std::max(pre_cap, npre + npre / 4 + 1024);
+                    call_cap = std::max(call_cap, nc + nc / 4 + 1024);
+                    found[kind].clear();
+                    continue;
+                }
                 std::vector<CallRec> hc(nc);
                 std::vector<uint8_t> ok(nc);
                 if (nc) {

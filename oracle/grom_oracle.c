@@ -894,9 +894,6 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx, &rc_total, &base_total,
               chr_name, vcf, c->lseq);
 
-    /* read-depth CNV path, GROM.c:16633-17300 (only for a matched target) */
-    if (chr_match != -1) cnv_chromosome(chr_len, fasta, &pre, s.caf_mq, s.caf_rd, s.caf_low, chr_name, vcf);
-
     if (g_dump_prefix) {
         char path[4096];
         snprintf(path, sizeof(path), "%s.%s.caf", g_dump_prefix, chr_name);
@@ -914,6 +911,9 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
             fclose(f);
         }
     }
+    /* read-depth CNV path, GROM.c:16633-17300 (only for a matched target);
+     * after the dump above, since it divides caf_mq in place */
+    if (chr_match != -1) cnv_chromosome(chr_len, fasta, &pre, s.caf_mq, s.caf_rd, s.caf_low, chr_name, vcf);
     cnv_pre_free(&pre);
     snv_list_free(&sl);
     nametab_free(&s.names);

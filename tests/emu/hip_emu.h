@@ -94,6 +94,17 @@ inline T __shfl_up(T v, unsigned d, int width = 64) {
     return out;
 }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
+inline int __clzll(unsigned long long v) { return v ? __builtin_clzll(v) : 64; }
+template <typename T>
+inline T __shfl(T v, int src, int width = 64) {
+    (void)width;
+    unsigned long long u = 0;
+    std::memcpy(&u, &v, sizeof(T));
+    const unsigned long long r = emu_lane_xch(u, (unsigned)src & 63u);
+    T out;
+    std::memcpy(&out, &r, sizeof(T));
+    return out;
+}
 inline int __builtin_amdgcn_readlane(int v, int i) {
     return (int)(unsigned)emu_lane_xch((unsigned)v, (unsigned)i);
 }
