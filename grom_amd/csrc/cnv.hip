@@ -620,9 +620,11 @@ struct Win {
     const uint16_t *wb;
     const double *sd;
     const uint8_t *vis;
+    const int32_t *nxt;
     int64_t len;
     int64_t base;
     uint32_t b_l, s_lo, s_hi, v_l;
+    int32_t n0, n1;  // nxt[0][p], nxt[1][p]
     __device__ void fill(int64_t b) {
         base = b;
         const int64_t q = b + (int64_t)(threadIdx.x & 63);
@@ -634,6 +636,8 @@ struct Win {
         s_lo = (uint32_t)u;
         s_hi = (uint32_t)(u >> 32);
         v_l = (ok && vis) ? vis[q] : 0u;
+        n0 = (ok && nxt) ? nxt[q] : 0;
+        n1 = (ok && nxt) ? nxt[len + q] : 0;
     }
     __device__ __forceinline__ int slot(int64_t p) {
         if (p >= base + 64) fill(p);
@@ -647,10 +651,6 @@ struct Win {
     __device__ __forceinline__ double z(int64_t p) {
         int i = slot(p);
         return dbl_of((uint32_t)__builtin_amdgcn_readlane((int)s_lo, i), (uint32_t)__builtin_amdgcn_readlane((int)s_hi, i));
-    }
-    __device__ __forceinline__ uint32_t mark(int64_t p) {
-        int i = slot(p);
-        return (uint32_t)__builtin_amdgcn_readlane((int)v_l, i);
     }
 };
 
@@ -786,6 +786,7 @@ struct Walk {
         c.wb = w.wb;
         c.sd = w.sd;
         c.vis = vis;
+        c.nxt = nx;
         c.len = w.len;
         c.base = INT64_MIN / 4;
     }
@@ -805,8 +806,7 @@ struct Walk {
     // and B come precomputed; a call is completed here (phase C: the sliding
     // extension past L, phase D: trimming the end).  Returns the position the
     // walk continues from (before its `pos += 1`).
-    __device__ int64_t block(int64_t pos, int mqi, CallRec &call, bool &is_call) {
-        const int32_t n = nxt[mqi * W.len + pos];
+    __device__ int64_t block(int64_t pos, int mqi, int32_t n, CallRec &call, bool &is_call) {
         is_call = n < -1;
         if (!is_call) return n;
         const PreAB r = pre[-n - 2];
@@ -895,8 +895,53 @@ __device__ __forceinline__ void emit_call(const CallRec &c, int m, CallRec *call
         }
     }
 }
-__device__ __forceinline__ void put_mark(uint8_t *vis, int64_t p, int v) {
-    if ((threadIdx.x & 63) == 0) vis[p] = (uint8_t)v;
+
+// The walk from (pos, last) while pos < lim.  Bases that do not pass the
+// threshold only update the class state, so the wave fast-forwards over them
+// 64 at a time: lane i takes base+i, the class each base sees is a
+// last-value scan over the window, and a ballot finds the first base that
+// passes (or, with merge_check, whose mark from an earlier walk equals its
+// class -- from there both walks are identical).  Marks are stored
+// coalesced; calls are completed serially (Walk::block).  Returns the exit
+// position; *merge = the merge base or -1.
+template <int KIND>
+__device__ int64_t walk_run(Walk<KIND> &w, int64_t pos, int &last, int64_t lim, uint8_t *vis_out, bool merge_check,
+                            int64_t *merge, CallRec *calls, uint32_t *n_calls, uint32_t cap, bool emit) {
+    const int lane = threadIdx.x & 63;
+    *merge = -1;
+    while (pos < lim) {
+        const int i0 = w.c.slot(pos);
+        const int64_t base = w.c.base;
+        const int limi = (int)min<int64_t>(64, lim - base);
+        const bool in = lane >= i0 && lane < limi;
+        const uint32_t b = w.c.b_l;
+        const int e = in ? ((b & B_HI) ? 0 : (b & B_RTP) ? 1 : -1) : -1;
+        const int mi = wave_last_incl(e, last);
+        const bool ps = in && w.pass(b, mi);
+        const bool mg = merge_check && in && w.c.v_l == (uint32_t)(1 + mi);
+        const unsigned long long stop_m = __ballot(ps || mg);
+        const unsigned long long mg_m = __ballot(mg);
+        const int j = stop_m ? __ffsll((long long)stop_m) - 1 : limi - 1;
+        const bool merged_here = stop_m && ((mg_m >> j) & 1ull);
+        if (vis_out && in && lane <= j && !(merged_here && lane == j)) vis_out[base + lane] = (uint8_t)(1 + mi);
+        last = __builtin_amdgcn_readlane(mi, j);
+        if (!stop_m) {
+            pos = base + limi;
+            continue;
+        }
+        pos = base + j;
+        if (merged_here) {
+            *merge = pos;
+            return pos;
+        }
+        const int32_t n = __builtin_amdgcn_readlane(last == 0 ? w.c.n0 : w.c.n1, j);
+        CallRec c;
+        bool is_call = false;
+        pos = w.block(pos, last, n, c, is_call);
+        if (is_call && emit) emit_call(c, last, calls, n_calls, cap);
+        pos += 1;
+    }
+    return pos;
 }
 
 // One wave per chunk.  mode 0: speculative first pass from (chunk start,
@@ -912,21 +957,11 @@ __global__ __launch_bounds__(64) void k_cnv_walk(WalkIn W, const int32_t *nxt, c
     const int64_t k = blockIdx.x;
     if (k >= n_chunks) return;
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
+    int64_t merge;
     if (mode == 0) {
         Walk<KIND> w(W, nullptr, nxt, pre);
-        int64_t pos = c0;
         int last = 0;  // exact for chunk 0 (GROM.c:19366-19367), a guess elsewhere
-        while (pos < c1) {
-            int m = w.visit(pos, last);
-            put_mark(vis, pos, 1 + m);
-            if (w.pass(w.c.bits(pos), m)) {
-                CallRec c;
-                bool is_call = false;
-                pos = w.block(pos, m, c, is_call);
-                if (is_call) emit_call(c, m, calls, n_calls, cap);
-            }
-            pos += 1;
-        }
+        const int64_t pos = walk_run<KIND>(w, c0, last, c1, vis, false, &merge, calls, n_calls, cap, true);
         if ((threadIdx.x & 63) == 0) {
             cs[k].x1 = pos;
             cs[k].l1 = last;
@@ -942,41 +977,19 @@ __global__ __launch_bounds__(64) void k_cnv_walk(WalkIn W, const int32_t *nxt, c
         if ((threadIdx.x & 63) == 0) cs[k].status = ST_PASSTHRU;
         return;
     }
-    // pass 1: the first base both walks visit in the same state
-    int64_t merge = -1;
-    {
+    {  // pass 1: find the merge base
         Walk<KIND> w(W, vis, nxt, pre);
-        int64_t pos = x;
         int last = l;
-        while (pos < c1) {
-            int m = w.visit(pos, last);
-            if (w.c.mark(pos) == (uint32_t)(1 + m)) { merge = pos; break; }
-            if (w.pass(w.c.bits(pos), m)) {
-                CallRec c;
-                bool is_call = false;
-                pos = w.block(pos, m, c, is_call);
-            }
-            pos += 1;
-        }
+        walk_run<KIND>(w, x, last, c1, nullptr, true, &merge, calls, n_calls, cap, false);
     }
     const int64_t stop_at = merge >= 0 ? merge : c1;
     for (int64_t p = c0 + (threadIdx.x & 63); p < stop_at; p += 64) vis[p] = 0;
     __syncthreads();
-    // pass 2: the true walk up to the merge point, with marks and calls
+    // pass 2: the true walk up to the merge base, with marks and calls
     Walk<KIND> w(W, nullptr, nxt, pre);
-    int64_t pos = x;
     int last = l;
-    while (pos < stop_at) {
-        int m = w.visit(pos, last);
-        put_mark(vis, pos, 1 + m);
-        if (w.pass(w.c.bits(pos), m)) {
-            CallRec c;
-            bool is_call = false;
-            pos = w.block(pos, m, c, is_call);
-            if (is_call) emit_call(c, m, calls, n_calls, cap);
-        }
-        pos += 1;
-    }
+    int64_t m2;
+    const int64_t pos = walk_run<KIND>(w, x, last, stop_at, vis, false, &m2, calls, n_calls, cap, true);
     if ((threadIdx.x & 63) == 0) {
         if (merge >= 0) {
             cs[k].status = ST_MERGED;
@@ -999,39 +1012,19 @@ __global__ __launch_bounds__(64) void k_cnv_walk_fix(WalkIn W, const int32_t *nx
                                                      ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
                                                      uint32_t cap) {
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
-    int64_t merge = -1;
+    int64_t merge;
     {
         Walk<KIND> w(W, vis, nxt, pre);
-        int64_t pos = x;
         int last = l;
-        while (pos < c1) {
-            int m = w.visit(pos, last);
-            if (w.c.mark(pos) == (uint32_t)(1 + m)) { merge = pos; break; }
-            if (w.pass(w.c.bits(pos), m)) {
-                CallRec c;
-                bool is_call = false;
-                pos = w.block(pos, m, c, is_call);
-            }
-            pos += 1;
-        }
+        walk_run<KIND>(w, x, last, c1, nullptr, true, &merge, calls, n_calls, cap, false);
     }
     const int64_t stop_at = merge >= 0 ? merge : c1;
     for (int64_t p = c0 + (threadIdx.x & 63); p < stop_at; p += 64) vis[p] = 0;
     __syncthreads();
     Walk<KIND> w(W, nullptr, nxt, pre);
-    int64_t pos = x;
     int last = l;
-    while (pos < stop_at) {
-        int m = w.visit(pos, last);
-        put_mark(vis, pos, 1 + m);
-        if (w.pass(w.c.bits(pos), m)) {
-            CallRec c;
-            bool is_call = false;
-            pos = w.block(pos, m, c, is_call);
-            if (is_call) emit_call(c, m, calls, n_calls, cap);
-        }
-        pos += 1;
-    }
+    int64_t m2;
+    const int64_t pos = walk_run<KIND>(w, x, last, stop_at, vis, false, &m2, calls, n_calls, cap, true);
     if ((threadIdx.x & 63) == 0) {
         cs[k].status = merge >= 0 ? ST_MERGED : ST_NOMERGE;
         cs[k].x2 = pos;

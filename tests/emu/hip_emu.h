@@ -95,6 +95,7 @@ inline T __shfl_up(T v, unsigned d, int width = 64) {
 }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 inline int __clzll(unsigned long long v) { return v ? __builtin_clzll(v) : 64; }
+inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 template <typename T>
 inline T __shfl(T v, int src, int width = 64) {
     (void)width;
