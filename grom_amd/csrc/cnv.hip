@@ -121,19 +121,24 @@ __device__ __forceinline__ int pair_type(char x, char y) {
 
 // exclusive prefix sum of a[0..n) in place, one 256-thread block
 __device__ void block_excl_scan(int *a, int n, int *tmp) {
-    const int tid = threadIdx.x, per = (n + 255) / 256;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, per = (n + 255) / 256;
     const int lo = min(n, tid * per), hi = min(n, lo + per);
     int s = 0;
     for (int i = lo; i < hi; i++) s += a[i];
-    tmp[tid] = s;
-    __syncthreads();
-    if (tid == 0) {
-        int acc = 0;
-        for (int t = 0; t < 256; t++) { int v = tmp[t]; tmp[t] = acc; acc += v; }
+    int x = s;  // inclusive scan within the wave
+    for (int d = 1; d < 64; d <<= 1) {
+        int y = __shfl_up(x, d);
+        if (lane >= d) x += y;
     }
+    if (lane == 63) tmp[wv] = x;
     __syncthreads();
-    int acc = tmp[tid];
-    for (int i = lo; i < hi; i++) { int v = a[i]; a[i] = acc; acc += v; }
+    int acc = x - s;
+    for (int w = 0; w < wv; w++) acc += tmp[w];
+    for (int i = lo; i < hi; i++) {
+        int v = a[i];
+        a[i] = acc;
+        acc += v;
+    }
     __syncthreads();
 }
 
@@ -512,24 +517,24 @@ __global__ void k_cnv_windows(const WinDesc *__restrict__ wd, int64_t n_win, con
     int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= n_win) return;
     const WinDesc d = wd[w];
-    double *row = out + d.row * (L + 1);
+    double *row = out + d.row;  // out[l * n_win + row]: lanes of a wave store adjacent words
     double tot = 0.0;
     long cnt = 0, ftot = 0, wl = 0;
     const int64_t ps[3] = {d.p0, d.p1, d.p2}, ns[3] = {d.n0, d.n1, d.n2};
     for (int s = 0; s < 3; s++) {
         const int64_t pb = ps[s], n = ns[s];
-        for (int64_t k0 = 0; k0 < n; k0 += 8) {
-            // 8 loads in flight, then the sequential sum in reference order
-            uint8_t f[8];
-            double v[8];
+        for (int64_t k0 = 0; k0 < n; k0 += 32) {
+            // 32 loads in flight, then the sequential sum in reference order
+            uint8_t f[32];
+            double v[32];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
+            for (int j = 0; j < 32; j++) {
                 const bool ok = k0 + j < n;
                 f[j] = ok ? flag[pb + k0 + j] : (uint8_t)0xff;
                 v[j] = ok ? sd[pb + k0 + j] : 0.0;
             }
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
+            for (int j = 0; j < 32; j++) {
                 if (f[j] != 0xff) {
                     if (f[j] & F_GUARD) { tot += v[j]; cnt += 1; }
                     ftot += (f[j] & F_LOW);
@@ -537,7 +542,7 @@ __global__ void k_cnv_windows(const WinDesc *__restrict__ wd, int64_t n_win, con
                     if (wl >= min_len) {
                         double x = __builtin_nan("");
                         if ((ftot / (double)wl) < MAX_LOW_ACGT && cnt > 0) x = tot / (double)cnt;
-                        row[wl] = x;
+                        row[wl * n_win] = x;
                     }
                 }
             }
@@ -551,17 +556,18 @@ __global__ void k_cnv_window_sq(const double *__restrict__ rows, int64_t n_rows,
                                 int64_t L, int64_t min_len, double *__restrict__ tot, int64_t *__restrict__ cnt) {
     int64_t l = min_len + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (l > L) return;
+    const double *row = rows + l * n_rows;  // this length's means, in window order
     double s = 0.0;
     int64_t c = 0;
-    for (int64_t r0 = 0; r0 < n_rows; r0 += 8) {
-        double v[8];
+    for (int64_t r0 = 0; r0 < n_rows; r0 += 48) {
+        double v[48];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < 48; j++) {
             const int64_t r = r0 + j;
-            v[j] = (r < n_rows && row_len[r] >= l) ? rows[r * (L + 1) + l] : __builtin_nan("");
+            v[j] = (r < n_rows && row_len[r] >= l) ? row[r] : __builtin_nan("");
         }
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < 48; j++) {
             if (v[j] == v[j]) {
                 s += v[j] * v[j];
                 c += 1;
@@ -616,6 +622,11 @@ __device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) {
 // executing the same uniform statements; per-position inputs come from a
 // 64-position register window (lane i holds position base+i) that is refilled
 // by one coalesced load whenever the walk leaves it, and read with readlane.
+struct WinRegs {
+    uint32_t b, s_lo, s_hi, v;
+    int32_t n0, n1;  // nxt[0][p], nxt[1][p]
+};
+
 struct Win {
     const uint16_t *wb;
     const double *sd;
@@ -623,34 +634,46 @@ struct Win {
     const int32_t *nxt;
     int64_t len;
     int64_t base;
-    uint32_t b_l, s_lo, s_hi, v_l;
-    int32_t n0, n1;  // nxt[0][p], nxt[1][p]
-    __device__ void fill(int64_t b) {
-        base = b;
+    WinRegs r, nx;  // the window [base, base+64) and, already in flight, [base+64, base+128)
+    __device__ void load(int64_t b, WinRegs &o) const {
         const int64_t q = b + (int64_t)(threadIdx.x & 63);
         const bool ok = q >= 0 && q < len;
-        b_l = ok ? wb[q] : 0u;
+        o.b = ok ? wb[q] : 0u;
         double v = ok ? sd[q] : 0.0;
         uint64_t u;
         __builtin_memcpy(&u, &v, 8);
-        s_lo = (uint32_t)u;
-        s_hi = (uint32_t)(u >> 32);
-        v_l = (ok && vis) ? vis[q] : 0u;
-        n0 = (ok && nxt) ? nxt[q] : 0;
-        n1 = (ok && nxt) ? nxt[len + q] : 0;
+        o.s_lo = (uint32_t)u;
+        o.s_hi = (uint32_t)(u >> 32);
+        o.v = (ok && vis) ? vis[q] : 0u;
+        o.n0 = (ok && nxt) ? nxt[q] : 0;
+        o.n1 = (ok && nxt) ? nxt[len + q] : 0;
+    }
+    __device__ void fill(int64_t b) {
+        base = b;
+        load(b, r);
+        load(b + 64, nx);  // prefetch: the walk mostly moves forward
     }
     __device__ __forceinline__ int slot(int64_t p) {
-        if (p >= base + 64) fill(p);
-        else if (p < base) fill(p - 63);
+        if (p >= base + 64) {
+            if (p < base + 128) {
+                base += 64;
+                r = nx;
+                load(base + 64, nx);
+            } else {
+                fill(p);
+            }
+        } else if (p < base) {
+            fill(p - 63);
+        }
         return (int)(p - base);
     }
     __device__ __forceinline__ uint32_t bits(int64_t p) {
         int i = slot(p);
-        return (uint32_t)__builtin_amdgcn_readlane((int)b_l, i);
+        return (uint32_t)__builtin_amdgcn_readlane((int)r.b, i);
     }
     __device__ __forceinline__ double z(int64_t p) {
         int i = slot(p);
-        return dbl_of((uint32_t)__builtin_amdgcn_readlane((int)s_lo, i), (uint32_t)__builtin_amdgcn_readlane((int)s_hi, i));
+        return dbl_of((uint32_t)__builtin_amdgcn_readlane((int)r.s_lo, i), (uint32_t)__builtin_amdgcn_readlane((int)r.s_hi, i));
     }
 };
 
@@ -658,7 +681,9 @@ struct Win {
 struct PreAB {
     int64_t temp_pos, ce, last_good;
     double stdevs;
-    int32_t stop, begin, mqi, pad;
+    int32_t stop, begin, mqi, done;  // done: ce/stdevs below are the finished call
+    int64_t ce_final;
+    double stdevs_final;
 };
 
 // phases A (first min-window) and B (extension to L) of the window search at
@@ -734,8 +759,99 @@ __device__ PreAB phase_ab(Acc &c, const WalkIn &W, int64_t pos, int mqi) {
     r.stop = stop;
     r.begin = begin;
     r.mqi = mqi;
-    r.pad = 0;
+    r.done = 0;
+    r.ce_final = 0;
+    r.stdevs_final = 0.0;
     return r;
+}
+
+// phases C (sliding extension past L, GROM.c:19476-19545) and D (trimming
+// the call's end, GROM.c:19550-19600) of a call found at `pos` with phase
+// A/B state r.  `a` serves the leading edge and the trim, `t` the trailing
+// edge of the slide.  Gives up (returns false) after max_steps steps.
+template <int KIND, class Acc>
+__device__ bool phase_cd(Acc &a, Acc &t, const WalkIn &W, int64_t pos, const PreAB &r, int64_t max_steps,
+                         int64_t &ce_out, double &stdevs_out) {
+    const int64_t L = W.L, ML = W.min_len, cs = pos;
+    const double *wsd = W.wsd;
+    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    auto cls = [](uint32_t b, int m) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : m; };
+    int64_t ce = r.ce, last_good = r.last_good, pa, pb, cnt = 0, steps = 0;
+    double stdevs = r.stdevs, tot = 0.0;
+    int mqi = r.mqi;
+    if (r.stop == 0) {
+        pa = pos + L;
+        int mqb = mqi;
+        while (pa < W.len && (pa - last_good) <= MAX_DIST_LAST_GOOD) {
+            if (++steps > max_steps) return false;
+            if (pa == pos + L) {
+                for (pb = pa - L + 1; pb < pa + 1; pb++) {
+                    const uint32_t b = t.bits(pb);
+                    mqb = cls(b, mqb);
+                    if (!(b & B_LOW) && (b & (B_W0 << mqb))) {
+                        if (KIND == 0) tot += t.z(pb); else tot -= t.z(pb);
+                        cnt += 1;
+                    }
+                }
+                steps += L;
+            } else {
+                pb = pa - L;
+                const uint32_t bb = t.bits(pb);
+                mqb = cls(bb, mqb);
+                if (!(bb & B_LOW) && (bb & (B_W0 << mqb))) {
+                    if (KIND == 0) tot -= t.z(pb); else tot += t.z(pb);
+                    cnt -= 1;
+                }
+                const uint32_t ba = a.bits(pa);
+                mqi = cls(ba, mqi);
+                if (!(ba & B_LOW) && (ba & (B_W0 << mqi))) {
+                    if (KIND == 0) tot += a.z(pa); else tot -= a.z(pa);
+                    cnt += 1;
+                }
+            }
+            if (cnt > 0 && wsd[L] > 0 && (tot / (cnt * wsd[L])) >= MIN_RD_LOW_STDEV &&
+                ((L - cnt) / ((double)L)) <= MAX_LOW_ACGT) {
+                last_good = pa;
+                ce = pa;
+                double ts = tot / (cnt * wsd[L]);
+                if (ts > stdevs) stdevs = ts;
+            }
+            pa += 1;
+        }
+    }
+    int64_t p = ce;
+    while (p > cs + ML) {
+        if (++steps > max_steps) return false;
+        const uint32_t b = a.bits(p);
+        mqi = cls(b, mqi);
+        if (!(b & (pb0 << mqi))) {
+            p -= 1;
+            ce = p;
+        } else {
+            int64_t c2 = 0, c3 = 0;
+            pa = ce;
+            int stop_while = 0, mqa = mqi;
+            while (pa > cs + ML && stop_while == 0) {
+                if (++steps > max_steps) return false;
+                const uint32_t ba = a.bits(pa);
+                if (!(ba & B_LOW)) {
+                    mqa = cls(ba, mqa);
+                    c3 += 1;
+                    if (ba & (pb0 << mqa)) c2 += 1;
+                }
+                if (c3 == 0 || (c3 > 0 && (c2 / ((double)c3)) < 0.5) ||
+                    ((ce - pa + 1 - c3) / ((double)ce - (double)pa + 1.0)) > MAX_LOW_ACGT) {
+                    ce = pa - 1;
+                    stop_while = 1;
+                }
+                pa -= 1;
+            }
+            p = pa;
+        }
+    }
+    ce_out = ce;
+    stdevs_out = stdevs;
+    return true;
 }
 
 struct GAcc {  // direct loads (one lane per base)
@@ -745,34 +861,92 @@ struct GAcc {  // direct loads (one lane per base)
     __device__ __forceinline__ double z(int64_t p) const { return sd[p]; }
 };
 
-// a base's first two phases, for every base and class the walk can meet it in:
-// nxt[m][p] = the position the walk continues from (before its +1), or
-// -(k+2) for a call whose record pre[k] the walk completes (phases C, D)
+// The bases (and classes) the walk can meet that pass the threshold,
+// compacted (wave-aggregated append); nxt[m][p] = p (no-op) everywhere else.
 template <int KIND>
-__global__ void k_cnv_pre(WalkIn W, int32_t *__restrict__ nxt, PreAB *__restrict__ pre, uint32_t *n_pre, uint32_t cap,
-                          int64_t *__restrict__ pre_pos) {
+__global__ __launch_bounds__(256) void k_cnv_cand(WalkIn W, int32_t *__restrict__ nxt, int64_t *__restrict__ cand,
+                                                  uint32_t *n_cand, uint32_t cap) {
+    __shared__ uint32_t wcnt[8], wbase[8], gbase;
     const int64_t p = W.start + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W.end) return;
-    GAcc c{W.wb, W.sd};
-    const uint32_t b = c.bits(p);
+    const bool in = p < W.end;
+    const uint32_t b = in ? (uint32_t)W.wb[p] : 0u;
     const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    bool want[2];
     for (int m = 0; m < 2; m++) {
-        int32_t out = (int32_t)p;
         const bool reach = (b & B_HI) ? m == 0 : (b & B_RTP) ? m == 1 : true;  // classes the walk can be in here
-        if (reach && (b & (pb0 << m))) {
-            PreAB r = phase_ab<KIND>(c, W, p, m);
-            if (r.begin == 1) {
-                uint32_t k = atomicAdd(n_pre, 1u);
-                if (k < cap) {
-                    pre[k] = r;
-                    pre_pos[k] = p;
-                    out = -(int32_t)k - 2;
-                }  // else: overflow, the host re-runs with a larger buffer
-            } else if (r.stop == 1) {
-                out = (int32_t)r.temp_pos;
-            }
-        }
-        nxt[m * W.len + p] = out;
+        want[m] = in && reach && (b & (pb0 << m));
+        if (in) nxt[m * W.len + p] = (int32_t)p;
+    }
+    // one global atomic per block: wave ballots, then the block's 8 (wave, m) counts
+    const unsigned long long m0 = __ballot(want[0]), m1 = __ballot(want[1]);
+    if (lane == 0) {
+        wcnt[wv * 2] = (uint32_t)__popcll(m0);
+        wcnt[wv * 2 + 1] = (uint32_t)__popcll(m1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < 8; i++) { wbase[i] = t; t += wcnt[i]; }
+        gbase = t ? atomicAdd(n_cand, t) : 0;
+    }
+    __syncthreads();
+    const unsigned long long below = (1ull << lane) - 1;
+    if (want[0]) {
+        const uint32_t k = gbase + wbase[wv * 2] + (uint32_t)__popcll(m0 & below);
+        if (k < cap) cand[k] = (p << 1);
+    }
+    if (want[1]) {
+        const uint32_t k = gbase + wbase[wv * 2 + 1] + (uint32_t)__popcll(m1 & below);
+        if (k < cap) cand[k] = (p << 1) | 1;
+    }
+}
+
+// a candidate's first two phases: nxt[m][p] = the position the walk continues
+// from (before its +1), or -(k+2) for a call whose record pre[k] the walk
+// completes (phases C, D)
+template <int KIND>
+__global__ void k_cnv_pre(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand, int32_t *__restrict__ nxt,
+                          PreAB *__restrict__ pre, uint32_t *n_pre, uint32_t cap, int64_t *__restrict__ pre_pos) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_cand) return;
+    const int64_t p = cand[i] >> 1;
+    const int m = (int)(cand[i] & 1);
+    GAcc c{W.wb, W.sd};
+    PreAB r = phase_ab<KIND>(c, W, p, m);
+    int32_t out = (int32_t)p;
+    if (r.begin == 1) {
+        uint32_t k = atomicAdd(n_pre, 1u);
+        if (k < cap) {
+            r.done = 0;
+            pre[k] = r;
+            pre_pos[k] = p;
+            out = -(int32_t)k - 2;
+        }  // else: overflow, the host re-runs with a larger buffer
+    } else if (r.stop == 1) {
+        out = (int32_t)r.temp_pos;
+    }
+    nxt[m * W.len + p] = out;
+}
+
+// phases C and D for every call start found by k_cnv_pre, one lane each,
+// capped so that long copy-number regions leave their few visited calls to
+// the walk
+template <int KIND>
+__global__ void k_cnv_post(WalkIn W, PreAB *__restrict__ pre, const uint32_t *n_pre, uint32_t cap,
+                           const int64_t *__restrict__ pre_pos, int64_t max_steps, uint32_t *n_left) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= min(*n_pre, cap)) return;
+    GAcc a{W.wb, W.sd}, t{W.wb, W.sd};
+    PreAB r = pre[i];
+    int64_t ce;
+    double sdv;
+    if (phase_cd<KIND>(a, t, W, pre_pos[i], r, max_steps, ce, sdv)) {
+        pre[i].ce_final = ce;
+        pre[i].stdevs_final = sdv;
+        pre[i].done = 1;
+    } else {
+        atomicAdd(n_left, 1u);
     }
 }
 
@@ -780,6 +954,7 @@ template <int KIND>
 struct Walk {
     WalkIn W;
     Win c;
+    Win t;  // second window: the trailing edge (pa - L) of the phase-C slide
     const int32_t *nxt;
     const PreAB *pre;
     __device__ Walk(const WalkIn &w, const uint8_t *vis, const int32_t *nx, const PreAB *pr) : W(w), nxt(nx), pre(pr) {
@@ -789,6 +964,9 @@ struct Walk {
         c.nxt = nx;
         c.len = w.len;
         c.base = INT64_MIN / 4;
+        t = c;
+        t.vis = nullptr;
+        t.nxt = nullptr;
     }
     __device__ __forceinline__ bool pass(uint32_t b, int m) const {
         return (b & ((KIND == 0 ? B_DEL0 : B_DUP0) << m)) != 0;
@@ -807,74 +985,21 @@ struct Walk {
     // extension past L, phase D: trimming the end).  Returns the position the
     // walk continues from (before its `pos += 1`).
     __device__ int64_t block(int64_t pos, int mqi, int32_t n, CallRec &call, bool &is_call) {
+        (void)mqi;
         is_call = n < -1;
         if (!is_call) return n;
         const PreAB r = pre[-n - 2];
-        const int64_t L = W.L, ML = W.min_len, cs = pos;
-        const double *wsd = W.wsd;
-        int64_t ce = r.ce, last_good = r.last_good, pa, pb, cnt = 0;
-        double stdevs = r.stdevs, tot = 0.0;
-        mqi = r.mqi;
-        if (r.stop == 0) {
-            pa = pos + L;
-            int mqb = mqi;
-            while (pa < W.len && (pa - last_good) <= MAX_DIST_LAST_GOOD) {
-                if (pa == pos + L) {
-                    for (pb = pa - L + 1; pb < pa + 1; pb++) {
-                        const uint32_t b = c.bits(pb);
-                        mqb = cls(b, mqb);
-                        if (!(b & B_LOW) && (b & (B_W0 << mqb))) { add(tot, c.z(pb)); cnt += 1; }
-                    }
-                } else {
-                    pb = pa - L;
-                    const uint32_t bb = c.bits(pb);
-                    mqb = cls(bb, mqb);
-                    if (!(bb & B_LOW) && (bb & (B_W0 << mqb))) { sub(tot, c.z(pb)); cnt -= 1; }
-                    const uint32_t ba = c.bits(pa);
-                    mqi = cls(ba, mqi);
-                    if (!(ba & B_LOW) && (ba & (B_W0 << mqi))) { add(tot, c.z(pa)); cnt += 1; }
-                }
-                if (cnt > 0 && wsd[L] > 0 && (tot / (cnt * wsd[L])) >= MIN_RD_LOW_STDEV &&
-                    ((L - cnt) / ((double)L)) <= MAX_LOW_ACGT) {
-                    last_good = pa;
-                    ce = pa;
-                    double ts = tot / (cnt * wsd[L]);
-                    if (ts > stdevs) stdevs = ts;
-                }
-                pa += 1;
-            }
+        int64_t ce;
+        double sdv;
+        if (r.done) {
+            ce = r.ce_final;
+            sdv = r.stdevs_final;
+        } else {
+            phase_cd<KIND>(c, t, W, pos, r, INT64_MAX, ce, sdv);
         }
-        int64_t p = ce;
-        while (p > cs + ML) {
-            const uint32_t b = c.bits(p);
-            mqi = cls(b, mqi);
-            if (!pass(b, mqi)) {
-                p -= 1;
-                ce = p;
-            } else {
-                int64_t c2 = 0, c3 = 0;
-                pa = ce;
-                int stop_while = 0, mqa = mqi;
-                while (pa > cs + ML && stop_while == 0) {
-                    const uint32_t ba = c.bits(pa);
-                    if (!(ba & B_LOW)) {
-                        mqa = cls(ba, mqa);
-                        c3 += 1;
-                        if (pass(ba, mqa)) c2 += 1;
-                    }
-                    if (c3 == 0 || (c3 > 0 && (c2 / ((double)c3)) < 0.5) ||
-                        ((ce - pa + 1 - c3) / ((double)ce - (double)pa + 1.0)) > MAX_LOW_ACGT) {
-                        ce = pa - 1;
-                        stop_while = 1;
-                    }
-                    pa -= 1;
-                }
-                p = pa;
-            }
-        }
-        call.p = cs;
+        call.p = pos;
         call.ce = ce;
-        call.stdevs = stdevs;
+        call.stdevs = sdv;
         return ce + 1;
     }
 };
@@ -914,11 +1039,14 @@ __device__ int64_t walk_run(Walk<KIND> &w, int64_t pos, int &last, int64_t lim, 
         const int64_t base = w.c.base;
         const int limi = (int)min<int64_t>(64, lim - base);
         const bool in = lane >= i0 && lane < limi;
-        const uint32_t b = w.c.b_l;
+        const uint32_t b = w.c.r.b;
         const int e = in ? ((b & B_HI) ? 0 : (b & B_RTP) ? 1 : -1) : -1;
         const int mi = wave_last_incl(e, last);
-        const bool ps = in && w.pass(b, mi);
-        const bool mg = merge_check && in && w.c.v_l == (uint32_t)(1 + mi);
+        // a base that passes but whose window search neither jumps nor calls
+        // (nxt == p) continues the walk exactly like one that does not pass
+        const int32_t nmi = mi == 0 ? w.c.r.n0 : w.c.r.n1;
+        const bool ps = in && w.pass(b, mi) && (int64_t)nmi != base + lane;
+        const bool mg = merge_check && in && w.c.r.v == (uint32_t)(1 + mi);
         const unsigned long long stop_m = __ballot(ps || mg);
         const unsigned long long mg_m = __ballot(mg);
         const int j = stop_m ? __ffsll((long long)stop_m) - 1 : limi - 1;
@@ -934,7 +1062,7 @@ __device__ int64_t walk_run(Walk<KIND> &w, int64_t pos, int &last, int64_t lim, 
             *merge = pos;
             return pos;
         }
-        const int32_t n = __builtin_amdgcn_readlane(last == 0 ? w.c.n0 : w.c.n1, j);
+        const int32_t n = __builtin_amdgcn_readlane(last == 0 ? w.c.r.n0 : w.c.r.n1, j);
         CallRec c;
         bool is_call = false;
         pos = w.block(pos, last, n, c, is_call);
@@ -1048,7 +1176,7 @@ struct Buf {
 }  // namespace
 
 struct CnvScratch {
-    Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
+    Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
 };
@@ -1136,6 +1264,23 @@ static void msort_lo(double *b, size_t n, double *t) {
     memcpy(b, t, (n - n2) * sizeof(double));
 }
 
+// sort of small non-negative ints (read depths): counting sort, same result
+// as the reference's qsort with cmpfunc on these values
+static void sort_depths(std::vector<int> &v) {
+    if (v.size() < 2) return;
+    int mx = 0;
+    for (int x : v) {
+        if (x < 0) { std::sort(v.begin(), v.end()); return; }
+        mx = std::max(mx, x);
+    }
+    if (mx > (1 << 20)) { std::sort(v.begin(), v.end()); return; }
+    std::vector<uint32_t> h((size_t)mx + 1, 0);
+    for (int x : v) h[x]++;
+    size_t k = 0;
+    for (int x = 0; x <= mx; x++)
+        for (uint32_t c = 0; c < h[x]; c++) v[k++] = x;
+}
+
 struct Gathered {
     std::vector<uint8_t> gc, ac, flag;
     std::vector<int32_t> mq, rt, rd, low;
@@ -1182,7 +1327,7 @@ CnvScratch *cnv_scratch_new() { return new CnvScratch(); }
 void cnv_scratch_free(CnvScratch *S) {
     if (!S) return;
     Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre,
-                  &S->prepos, &S->rep, &S->misc, &S->blk, &S->hist,
+                  &S->prepos, &S->ppos, &S->rep, &S->misc, &S->blk, &S->hist,
                   &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
                   &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok};
     for (Buf *b : all)
@@ -1214,6 +1359,19 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CK(hipEventCreate(&S->e1));
     }
     GlibcRand rng(seed);
+    // GROM_TIMING: per-phase wall clock (syncs the stream at each mark)
+    const bool tmg = getenv("GROM_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    std::string tlog;
+    auto mark = [&](const char *what) {
+        if (!tmg) return;
+        (void)hipStreamSynchronize(st);
+        auto now = std::chrono::steady_clock::now();
+        char b[96];
+        snprintf(b, sizeof(b), " %s %.2f", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        tlog += b;
+        t_last = now;
+    };
     Args A{};
     A.len = len;
     A.lo = m - 1;
@@ -1238,6 +1396,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     char *misc = (char *)S->misc.p;
     unsigned long long *acc = (unsigned long long *)misc;  // [0..3] block/chromosome sums
     uint32_t *n_rep = (uint32_t *)(misc + 64), *n_calls = (uint32_t *)(misc + 72), *n_pre = (uint32_t *)(misc + 76);
+    // misc + 80: candidate count of the window search (n_pre + 1)
     CK(hipEventRecord(S->e0, st));
     CK(hipMemsetAsync(misc, 0, 128, st));
     CK(hipMemsetAsync(S->hist.p, 0, 4 * (HIST_MAX + 1), st));
@@ -1355,6 +1514,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     for (size_t k = 0; k < ls.size(); k++)
         if (!(le[k] - ls[k] < P.min_rd_window_len)) { ss.push_back(ls[k]); se.push_back(le[k]); }
 
+    mark("pre+stats");
     // ---- A16: GC-bin samples every insert_mean/2 bases, GROM.c:18373-18456 ----
     const long half = m / 2;
     Tables T{};
@@ -1426,7 +1586,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             else { push(1, bin, v); last_low = 1; }
         }
         for (int k = 0; k < 2; k++)
-            for (int b = 0; b < NBINS; b++) std::sort(smp[k][b].begin(), smp[k][b].end());
+            for (int b = 0; b < NBINS; b++) sort_depths(smp[k][b]);
         // thin bins borrow their +-2 neighbours' samples, GROM.c:18480-18548
         for (int k = 0; k < 2; k++) {
             std::vector<std::vector<int>> add(NBINS);
@@ -1444,7 +1604,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 if (thin[b]) {
                     smp[k][b].insert(smp[k][b].end(), add[b].begin(), add[b].end());
                     idx[k][b] = (long)smp[k][b].size();
-                    std::sort(smp[k][b].begin(), smp[k][b].end());
+                    sort_depths(smp[k][b]);
                 }
         }
         // repeat-segment statistics, GROM.c:18336-18367 (only with a biased repeat)
@@ -1475,8 +1635,13 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     double a = 0.0;
                     for (long j = 0; j < n; j++) a += l[j];
                     a = a / n;
+                    // the same sequential sum; pow() evaluated once per run of equal depths
                     double s = 0.0;
-                    for (long j = 0; j < n; j++) s += pow((l[j] - a), 2);
+                    for (long j = 0; j < n;) {
+                        const int v = l[j];
+                        const double term = pow((v - a), 2);
+                        for (; j < n && l[j] == v; j++) s += term;
+                    }
                     if (n > 1) s = sqrt(s / (n - 1));
                     T.ave[k][b] = a;
                     T.sdv[k][b] = s;
@@ -1507,6 +1672,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CK(hipMemcpyAsync(S->tabs.p, &T, sizeof(Tables), hipMemcpyHostToDevice, st));
         const Tables *dT = (const Tables *)S->tabs.p;
 
+        mark("sampling");
         // ---- flags, z scores ----
         int8_t *tl = (int8_t *)S->tiles.p, *cr = (int8_t *)S->carry.p;
         const unsigned sblk = (unsigned)((n_seg + 3) / 4);  // 4 waves per block
@@ -1522,6 +1688,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                            (const int32_t *)S->samples.p, (const int16_t *)S->ztab.p, sd);
         CK(hipGetLastError());
 
+        mark("flags+z");
         // ---- window means by length, GROM.c:18967-19018 ----
         const int64_t L = P.max_rd_window_len, F = P.windows_sampling_factor, ML = P.min_rd_window_len;
         std::vector<WinDesc> wds;
@@ -1587,6 +1754,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         }
         for (int64_t l = ML; l <= L; l++) wsd[l] = wcnt[l] > 1 ? sqrt(wtot[l] / (wcnt[l] - 1)) : 0.0;  // GROM.c:19162
 
+        mark("windows");
         // ---- most-biased repeat z override, GROM.c:19022-19150 ----
         if (biased != -1 && !rrg.empty()) {
             Gathered rg2;
@@ -1662,12 +1830,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         const int64_t n_ch = (span + WALK_CHUNK - 1) / WALK_CHUNK;
         uint32_t call_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, len / 1000), 1 << 24);
         uint32_t pre_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, len / 64), 1 << 26);
+        uint32_t cand_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, len / 4), (int64_t)1 << 30);
         std::vector<CallRec> found[2];
         for (int kind = 0; kind < 2 && n_ch > 0; kind++) {
-            for (int attempt = 0; attempt < 2; attempt++) {
+            bool done = false;
+            for (int attempt = 0; attempt < 8 && !done; attempt++) {
                 if ((rc = grow(S->nxt, 8 * (size_t)len, err, errlen)) ||
                     (rc = grow(S->pre, sizeof(PreAB) * pre_cap, err, errlen)) ||
-                    (rc = grow(S->prepos, 8 * (size_t)pre_cap, err, errlen)) ||
+                    (rc = grow(S->prepos, 8 * (size_t)cand_cap, err, errlen)) ||
+                    (rc = grow(S->ppos, 8 * (size_t)pre_cap, err, errlen)) ||
                     (rc = grow(S->calls, sizeof(CallRec) * call_cap, err, errlen)) ||
                     (rc = grow(S->ok, call_cap, err, errlen)) ||
                     (rc = grow(S->tiles, sizeof(ChunkState) * n_ch, err, errlen)))
@@ -1680,11 +1851,37 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 int32_t *nxt = (int32_t *)S->nxt.p;
                 PreAB *pre = (PreAB *)S->pre.p;
                 const unsigned gpre = (unsigned)((span + 255) / 256);
+                uint32_t *n_cand = n_pre + 1;
+                CK(hipMemsetAsync(n_cand, 0, 8, st));  // candidates, capped call starts
+                int64_t *cand = (int64_t *)S->prepos.p;
                 if (kind == 0)
-                    hipLaunchKernelGGL(k_cnv_pre<0>, dim3(gpre), dim3(256), 0, st, WI, nxt, pre, n_pre, pre_cap, (int64_t *)S->prepos.p);
+                    hipLaunchKernelGGL(k_cnv_cand<0>, dim3(gpre), dim3(256), 0, st, WI, nxt, cand, n_cand, cand_cap);
                 else
-                    hipLaunchKernelGGL(k_cnv_pre<1>, dim3(gpre), dim3(256), 0, st, WI, nxt, pre, n_pre, pre_cap, (int64_t *)S->prepos.p);
+                    hipLaunchKernelGGL(k_cnv_cand<1>, dim3(gpre), dim3(256), 0, st, WI, nxt, cand, n_cand, cand_cap);
                 CK(hipGetLastError());
+                uint32_t ncand = 0;
+                CK(hipMemcpyAsync(&ncand, n_cand, 4, hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+                if (ncand > cand_cap) {
+                    cand_cap = ncand + ncand / 4 + 1024;
+                    found[kind].clear();
+                    continue;
+                }
+                if (ncand) {
+                    if (kind == 0)
+                        hipLaunchKernelGGL(k_cnv_pre<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)S->ppos.p);
+                    else
+                        hipLaunchKernelGGL(k_cnv_pre<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)S->ppos.p);
+                    CK(hipGetLastError());
+                    // phases C/D for every call start, capped (the walk finishes the rest)
+                    const int64_t cd_cap = 4 * L + 4 * MAX_DIST_LAST_GOOD;
+                    const unsigned gpost = (unsigned)((std::min<int64_t>(ncand, pre_cap) + 255) / 256);
+                    if (kind == 0)
+                        hipLaunchKernelGGL(k_cnv_post<0>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)S->ppos.p, cd_cap, n_pre + 2);
+                    else
+                        hipLaunchKernelGGL(k_cnv_post<1>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)S->ppos.p, cd_cap, n_pre + 2);
+                    CK(hipGetLastError());
+                }
                 const unsigned gch = (unsigned)n_ch;  // one wave per chunk
                 if (kind == 0) {
                     hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
@@ -1724,9 +1921,12 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     if (one.status == ST_MERGED && hcs[k].status != ST_PASSTHRU) { tx = ex; tl_ = el; }
                     else { tx = one.x2; tl_ = one.l2; }
                 }
-                if (getenv("GROM_TIMING"))
-                    fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired\n", kind == 0 ? "DEL" : "DUP",
-                            (long long)n_ch, (long long)n_fix);
+                if (tmg) {
+                    uint32_t np_[3] = {0, 0, 0};
+                    (void)hipMemcpy(np_, n_pre, 12, hipMemcpyDeviceToHost);
+                    fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired, %u candidates, %u call starts (%u left to the walk)\n",
+                            kind == 0 ? "DEL" : "DUP", (long long)n_ch, (long long)n_fix, ncand, np_[0], np_[2]);
+                }
                 uint32_t nc = 0;
                 CK(hipMemcpyAsync(&nc, n_calls, 4, hipMemcpyDeviceToHost, st));
                 CK(hipStreamSynchronize(st));
@@ -1755,10 +1955,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 found[kind].erase(std::unique(found[kind].begin(), found[kind].end(),
                                               [](const CallRec &a, const CallRec &b) { return a.p == b.p; }),
                                   found[kind].end());
-                break;
+                done = true;
+            }
+            if (!done) {
+                snprintf(err, errlen, "CNV window-search buffers could not be sized");
+                return GROM_E_NOMEM;
             }
         }
         CK(hipEventRecord(S->e1, st));
+        mark("walks");
 
         // ---- p value (Q8), filter, copy number, rows: GROM.c:17139-17300, 20024-20228 ----
         const double pp = 0.3275911, a1 = 0.254829592, a2 = -0.284496736, a3 = 1.421413741, a4 = -1.453152027,
@@ -1817,6 +2022,8 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 n_rows++;
             }
         }
+        mark("rows");
+        if (tmg) fprintf(stderr, "cnv phases ms:%s\n", tlog.c_str());
         if (timing) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, S->e0, S->e1);
