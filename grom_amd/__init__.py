@@ -62,6 +62,7 @@ class Stats(C.Structure):
 _SIGS = {
     "grom_abi_version": (C.c_int, []),
     "grom_abi_struct_size": (C.c_size_t, [C.c_int]),
+    "grom_device_count": (C.c_int, []),
     "grom_last_error": (C.c_char_p, []),
     "grom_dev_init": (C.c_int, [C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
     "grom_dev_fini": (None, [C.c_int]),

@@ -11,6 +11,7 @@
  * (tab-separated output).  Options that steer parts of the reference outside
  * the implemented scan rows are accepted and recorded.
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -142,7 +143,11 @@ typedef struct {
 
 static int g_plan_only = 0; /* GROM_PLAN_ONLY: report the record plan, no GPU */
 
-static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_params *P, FILE *vcf, int verbose) {
+/* Scan one chromosome's batch on `device`; its VCF rows go to *text (malloc'd). */
+static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_params *P, char **text, size_t *text_len,
+                      int verbose) {
+    *text = NULL;
+    *text_len = 0;
     grom_batch_finish(b, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size);
     if (g_plan_only) {
         printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d\n", cp->name, cp->tid, (long long)b->n, b->n_skip,
@@ -172,7 +177,10 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
         grom_out_free(&out);
         return rc;
     }
-    if (out.vcf_len) fwrite(out.vcf, 1, out.vcf_len, vcf);
+    *text = out.vcf;
+    *text_len = out.vcf_len;
+    out.vcf = NULL;
+    out.vcf_len = out.vcf_cap = 0;
     const char *dump = getenv("GROM_DUMP");
     if (dump) {
         /* test hook: per-base counters and caf depth, same files as the oracle's */
@@ -204,6 +212,65 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
     return GROM_OK;
 }
 
+/* ---- multi-GPU: chromosomes shard across devices ----
+ * The reference's -P forks one process per chromosome (GROM.c:328-624).  Here
+ * -P n (or GROM_DEVICES) runs one host thread per GPU; the main thread keeps
+ * reading the BAM once, in order, and hands each finished chromosome batch to
+ * the next free GPU.  Rows are written in chromosome order, so the VCF is the
+ * same bytes as a one-GPU run.  No data crosses devices. */
+typedef struct {
+    chrom_plan *cp;
+    grom_batch batch;
+    char *text;
+    size_t text_len;
+    int rc, ready, done;
+} grom_job;
+
+typedef struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    grom_job *jobs;
+    int n_jobs, next_run, closing;
+    const grom_params *P;
+    int verbose;
+} grom_pool;
+
+typedef struct {
+    grom_pool *pool;
+    int device;
+} grom_worker;
+
+/* one scan at a time per device (workers may share one: GROM_WORKER_DEVICES) */
+static pthread_mutex_t g_dev_mu[64] = {PTHREAD_MUTEX_INITIALIZER};
+
+static void *grom_worker_main(void *arg) {
+    grom_worker *w = (grom_worker *)arg;
+    grom_pool *pl = w->pool;
+    for (;;) {
+        pthread_mutex_lock(&pl->mu);
+        while (!(pl->next_run < pl->n_jobs && pl->jobs[pl->next_run].ready) && !pl->closing)
+            pthread_cond_wait(&pl->cv, &pl->mu);
+        if (!(pl->next_run < pl->n_jobs && pl->jobs[pl->next_run].ready)) {
+            pthread_mutex_unlock(&pl->mu);
+            break;
+        }
+        grom_job *j = &pl->jobs[pl->next_run++];
+        pthread_mutex_unlock(&pl->mu);
+        pthread_mutex_lock(&g_dev_mu[w->device & 63]);
+        int rc = scan_batch(w->device, j->cp, &j->batch, pl->P, &j->text, &j->text_len, pl->verbose);
+        pthread_mutex_unlock(&g_dev_mu[w->device & 63]);
+        free(j->cp->ref);
+        j->cp->ref = NULL;
+        grom_batch_free(&j->batch);
+        pthread_mutex_lock(&pl->mu);
+        j->rc = rc;
+        j->done = 1;
+        pthread_cond_broadcast(&pl->cv);
+        pthread_mutex_unlock(&pl->mu);
+    }
+    return NULL;
+}
+
 int grom_cli_main(int argc, char **argv) {
     optind = 0; /* GNU getopt: 0 fully re-initialises, so this is callable again */
     setlinebuf(stdout);
@@ -212,7 +279,7 @@ int grom_cli_main(int argc, char **argv) {
     const char *bam_name = NULL, *fasta_name = NULL, *out_name = NULL;
     long max_chr_len = 300000000; /* g_max_chr_fasta_len, GROM.c:946 */
     double num_sd = 3;
-    int device = 0, verbose = getenv("GROM_VERBOSE") != NULL;
+    int device = 0, verbose = getenv("GROM_VERBOSE") != NULL, n_dev = 1;
     if (getenv("GROM_DEVICE")) device = atoi(getenv("GROM_DEVICE"));
     int opt;
     /* getopt string of GROM.c:21908 */
@@ -236,6 +303,7 @@ int grom_cli_main(int argc, char **argv) {
         case 'a': P.min_snv_ratio = atof(optarg); break;
         case 'f': P.vcf = 0; break;
         case 'x': P.min_ave_bq = atof(optarg); break;
+        case 'P': n_dev = atoi(optarg); break; /* -P threads -> GPUs, GROM.c:21930 */
         case 'Z': P.block_min = atol(optarg); break;
         case 'W': P.min_rd_window_len = atol(optarg); break;
         case 'X': P.max_rd_window_len = atol(optarg); break;
@@ -306,7 +374,30 @@ int grom_cli_main(int argc, char **argv) {
     printf("median read length: %d\n", lseq);
 
     g_plan_only = getenv("GROM_PLAN_ONLY") != NULL;
-    int rc = g_plan_only ? GROM_OK : grom_dev_init(device, &P, hez, mq);
+    if (getenv("GROM_DEVICES")) n_dev = atoi(getenv("GROM_DEVICES"));
+    if (n_dev < 1) n_dev = 1;
+    if (!g_plan_only && n_dev > 1) {
+        int avail = grom_device_count();
+        if (avail < 1) { fprintf(stderr, "grom: no GPU\n"); return 1; }
+        if (n_dev > avail - device) n_dev = avail - device;
+        if (n_dev < 1) n_dev = 1;
+    }
+    /* test hook: GROM_WORKER_DEVICES=0,0,0 runs three workers on device 0 */
+    int wdev[64], n_work = n_dev;
+    for (int d = 0; d < 64; d++) wdev[d] = device + d;
+    if (getenv("GROM_WORKER_DEVICES")) {
+        char *sdup = strdup(getenv("GROM_WORKER_DEVICES")), *tok = strtok(sdup, ",");
+        n_work = 0;
+        while (tok && n_work < 64) { wdev[n_work++] = atoi(tok); tok = strtok(NULL, ","); }
+        free(sdup);
+        if (n_work < 1) { wdev[0] = device; n_work = 1; }
+    }
+    int rc = GROM_OK;
+    for (int d = 0; d < n_work && !g_plan_only && rc == GROM_OK; d++) {
+        int seen = 0;
+        for (int e = 0; e < d; e++) seen |= wdev[e] == wdev[d];
+        if (!seen) rc = grom_dev_init(wdev[d], &P, hez, mq);
+    }
     if (rc != GROM_OK) { fprintf(stderr, "grom: %s\n", grom_last_error()); return 1; }
 
     /* chromosome selection in BAM header order (GROM.c:20826-21050) */
@@ -347,7 +438,8 @@ int grom_cli_main(int argc, char **argv) {
     else
         snprintf(ctx_name, sizeof(ctx_name), "%s.ctx", out_name);
 
-    /* one serial pass over the records, split per chromosome (stream.h) */
+    /* one serial pass over the records, split per chromosome (stream.h);
+     * finished chromosomes go to the GPU workers, rows are written in order */
     bam_free_header(&hdr);
     if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) return 1;
     grom_planner pl;
@@ -358,30 +450,79 @@ int grom_cli_main(int argc, char **argv) {
     bam_rec rec;
     memset(&rec, 0, sizeof(rec));
     int status = 0;
+    grom_pool pool;
+    memset(&pool, 0, sizeof(pool));
+    pthread_mutex_init(&pool.mu, NULL);
+    pthread_cond_init(&pool.cv, NULL);
+    pool.jobs = calloc(n_plan > 0 ? n_plan : 1, sizeof(grom_job));
+    pool.n_jobs = n_plan;
+    pool.P = &P;
+    pool.verbose = verbose;
+    grom_worker *workers = calloc(n_work, sizeof(grom_worker));
+    pthread_t *tids = calloc(n_work, sizeof(pthread_t));
+    for (int d = 0; d < n_work; d++) {
+        workers[d].pool = &pool;
+        workers[d].device = wdev[d];
+        pthread_create(&tids[d], NULL, grom_worker_main, &workers[d]);
+    }
+    int next_write = 0;
+    /* hand chromosome `cur` (its batch complete) to the workers; keep at most
+     * 2 x n_dev chromosomes in host memory, writing finished rows in order */
+    #define SUBMIT_CUR()                                                                           \
+        do {                                                                                       \
+            plan[cur].ref = malloc(plan[cur].len + 1);                                             \
+            grom_fasta_load(&fa, plan[cur].fasta_idx, plan[cur].ref, plan[cur].len);               \
+            pthread_mutex_lock(&pool.mu);                                                          \
+            pool.jobs[cur].cp = &plan[cur];                                                        \
+            pool.jobs[cur].batch = batch;                                                          \
+            pool.jobs[cur].ready = 1;                                                              \
+            pthread_cond_broadcast(&pool.cv);                                                      \
+            for (;;) {                                                                             \
+                while (next_write <= cur && pool.jobs[next_write].done) {                          \
+                    grom_job *j = &pool.jobs[next_write++];                                        \
+                    pthread_mutex_unlock(&pool.mu);                                                \
+                    if (j->rc != GROM_OK) status = 1;                                              \
+                    if (j->text_len) fwrite(j->text, 1, j->text_len, vcf);                         \
+                    free(j->text);                                                                 \
+                    j->text = NULL;                                                                \
+                    pthread_mutex_lock(&pool.mu);                                                  \
+                }                                                                                  \
+                if (cur + 1 - next_write < 2 * n_work) break;                                       \
+                pthread_cond_wait(&pool.cv, &pool.mu);                                             \
+            }                                                                                      \
+            pthread_mutex_unlock(&pool.mu);                                                        \
+            cur++;                                                                                 \
+            if (cur < n_plan) grom_batch_init(&batch, order[cur], P.read_name_len);                \
+        } while (0)
     while (cur < n_plan && bam_read_rec(&br, &rec) > 0) {
         int k = grom_planner_feed(&pl, rec.tid);
-        while (cur < n_plan && pl.k > cur) {
-            /* chromosome `cur` is complete */
-            plan[cur].ref = malloc(plan[cur].len + 1);
-            grom_fasta_load(&fa, plan[cur].fasta_idx, plan[cur].ref, plan[cur].len);
-            if (scan_batch(device, &plan[cur], &batch, &P, vcf, verbose) != GROM_OK) status = 1;
-            free(plan[cur].ref);
-            grom_batch_free(&batch);
-            cur++;
-            if (cur < n_plan) grom_batch_init(&batch, order[cur], P.read_name_len);
-        }
+        while (cur < n_plan && pl.k > cur) SUBMIT_CUR(); /* chromosome `cur` is complete */
         if (k >= 0 && k == cur) grom_batch_add(&batch, &rec, s0);
     }
     /* end of file: the chromosome being read and every later one */
-    while (cur < n_plan) {
-        plan[cur].ref = malloc(plan[cur].len + 1);
-        grom_fasta_load(&fa, plan[cur].fasta_idx, plan[cur].ref, plan[cur].len);
-        if (scan_batch(device, &plan[cur], &batch, &P, vcf, verbose) != GROM_OK) status = 1;
-        free(plan[cur].ref);
-        grom_batch_free(&batch);
-        cur++;
-        if (cur < n_plan) grom_batch_init(&batch, order[cur], P.read_name_len);
+    while (cur < n_plan) SUBMIT_CUR();
+    #undef SUBMIT_CUR
+    pthread_mutex_lock(&pool.mu);
+    pool.closing = 1;
+    pthread_cond_broadcast(&pool.cv);
+    while (next_write < n_plan) {
+        if (pool.jobs[next_write].done) {
+            grom_job *j = &pool.jobs[next_write++];
+            if (j->rc != GROM_OK) status = 1;
+            if (j->text_len) fwrite(j->text, 1, j->text_len, vcf);
+            free(j->text);
+            j->text = NULL;
+        } else {
+            pthread_cond_wait(&pool.cv, &pool.mu);
+        }
     }
+    pthread_mutex_unlock(&pool.mu);
+    for (int d = 0; d < n_work; d++) pthread_join(tids[d], NULL);
+    free(tids);
+    free(workers);
+    free(pool.jobs);
+    pthread_mutex_destroy(&pool.mu);
+    pthread_cond_destroy(&pool.cv);
     bam_free_rec(&rec);
     bgzf_close_read(&br);
     fclose(vcf);
@@ -392,7 +533,7 @@ int grom_cli_main(int argc, char **argv) {
         if (P.vcf == 1) header(ctx, fasta_name, 1);
         fclose(ctx);
     }
-    grom_dev_fini(device);
+    for (int d = 0; d < n_work; d++) grom_dev_fini(wdev[d]);
     grom_fasta_close(&fa);
     bam_free_header(&hdr);
     free(plan);

@@ -550,6 +550,11 @@ static int upload(Ctx &C, const grom_chrom *ch, const grom_reads *h, grom_chrom 
 extern "C" {
 
 int grom_abi_version(void) { return GROM_AMD_ABI_VERSION; }
+int grom_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
 size_t grom_abi_struct_size(int which) {
     switch (which) {
     case 0: return sizeof(grom_params);

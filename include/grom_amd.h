@@ -156,6 +156,8 @@ typedef struct grom_stats {
 } grom_stats;
 
 int grom_abi_version(void);
+/* number of visible GPUs (hipGetDeviceCount); 0 if none */
+int grom_device_count(void);
 /* sizeof of the ABI structs, for bindings to check their layout:
  * 0 grom_params, 1 grom_chrom, 2 grom_reads, 3 grom_out, 4 grom_stats */
 size_t grom_abi_struct_size(int which);

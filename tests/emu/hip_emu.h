@@ -145,6 +145,7 @@ enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDevi
 inline const char *hipGetErrorString(hipError_t) { return "emulated error"; }
 inline hipError_t hipGetLastError() { return hipSuccess; }
 inline hipError_t hipSetDevice(int) { return hipSuccess; }
+inline hipError_t hipGetDeviceCount(int *n) { *n = 1; return hipSuccess; }
 inline hipError_t hipMalloc(void **p, size_t n) {
     *p = std::malloc(n);
     return *p ? hipSuccess : hipErrorInvalidValue;

@@ -93,3 +93,20 @@ def test_device_resident_path_matches_host_path():
     finally:
         dev.close()
         b.close()
+
+
+@pytest.mark.parametrize("workers,extra", [("0,0,0", []), ("0,0", ["-V", "1"])], ids=["w3", "w2_cnv"])
+def test_sharded_cli_matches_one_gpu(datadir, workers, extra):
+    """Chromosomes scanned by several device workers (GROM_WORKER_DEVICES maps
+    workers onto this box's one GPU; on an 8-GPU node -P 8 gives one per GPU)
+    give the byte-identical VCF, rows in chromosome order."""
+    import grom_amd
+    from _util import FILEDATE, SEED
+    case = "three_chr" if not extra else "cnv_multi"
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"shard_{workers.replace(',', '')}"
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    env = {"GROM_FILEDATE": FILEDATE, "GROM_SEED": SEED, "GROM_WORKER_DEVICES": workers}
+    rc = grom_amd.cli_main(["-i", bam, "-r", fa, "-o", f"g_{tag}.vcf", "-P", "8"] + extra, env=env, cwd=str(datadir))
+    assert rc == 0, grom_amd.last_error()
+    assert open(datadir / f"o_{tag}.vcf").read() == open(datadir / f"g_{tag}.vcf").read()
