@@ -1,7 +1,9 @@
 """bench.py -- GROM per-chromosome scan on MI355X.
 
-One step = one pass of the scan (grom_scan_chrom_device: the HIP kernels plus
-the host SNV-list flush and VCF formatting) over one synthetic 100 Mb, 30x,
+One step = one pass of the scan (grom_scan_chrom_device: the pileup/SNV HIP
+kernels, the host SNV-list flush and VCF formatting, and the read-depth CNV
+path -- GC windows, depth blocks, detect_del_dup and its rows) over one
+synthetic 100 Mb, 30x,
 2x150 bp paired-end chromosome whose reads are already resident in HBM
 (BASELINE.json configs[1]).  With --gpus N (torch.distributed.run, one rank per
 GPU) every rank scans its own chromosome: chromosomes shard with no data-path
@@ -97,6 +99,7 @@ def main():
 
     pile_ms = []
     tot_ms = []
+    cnv_ms = []
     out = grom_amd.Out()  # the VCF text buffer, reused across steps (grom_out)
     last = [0]
 
@@ -104,6 +107,7 @@ def main():
         vcf_len, st = dev.scan(dchrom, dreads, device_resident=True, out=out)
         pile_ms.append(st.ms_pileup)
         tot_ms.append(st.ms_total)
+        cnv_ms.append(st.ms_cnv)
         last[0] = vcf_len
 
     dt = timed_steps(step, args.steps, barrier)
@@ -145,10 +149,12 @@ def main():
             "data": "synthetic (seeded generator, grom_amd/csrc/synth.c)",
             "config": {
                 "workload": "BASELINE configs[1]: 1 chromosome of 100 Mb per GPU, 30x 2x150 bp paired-end, "
-                            "SNV/indel, reads resident in HBM; step = scan + SNV flush + VCF text",
+                            "SNV/indel, reads resident in HBM; step = pileup/SNV scan + SNV flush + VCF text + read-depth "
+                            "CNV path (GC windows, depth blocks, detect_del_dup, CNV rows)",
                 "chrom_len": args.chrom_len, "coverage": COVERAGE, "read_len": READ_LEN,
                 "reads_per_gpu": batch.n_reads, "vcf_rows_per_step": rows,
                 "device_ms_per_step": round(sum(tot_ms) / len(tot_ms), 3),
+                "cnv_ms_per_step": round(sum(cnv_ms) / len(cnv_ms), 3),
                 "host_generate_s": round(t_gen, 1),
             },
             "roofline": {
