@@ -1214,12 +1214,12 @@ struct GlibcRand {
     explicit GlibcRand(uint32_t seed) {
         if (seed == 0) seed = 1;
         st[0] = (int32_t)seed;
-        long word = seed;
+        int32_t word = (int32_t)seed;  // int32_t in glibc's __srandom_r
         for (int i = 1; i < 31; i++) {
             long hi = word / 127773, lo = word % 127773;
-            word = 16807 * lo - 2836 * hi;
+            word = (int32_t)(16807 * lo - 2836 * hi);
             if (word < 0) word += 2147483647;
-            st[i] = (int32_t)word;
+            st[i] = word;
         }
         for (int i = 0; i < 310; i++) next();
     }

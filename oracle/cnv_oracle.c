@@ -56,12 +56,12 @@ static glibc_rng g_rng;
 static void glibc_srand(glibc_rng *g, unsigned int seed) {
     if (seed == 0) seed = 1;
     g->st[0] = (int32_t)seed;
-    long word = seed;
+    int32_t word = (int32_t)seed; /* int32_t in glibc's __srandom_r: seeds >= 2^31 start negative */
     for (int i = 1; i < 31; i++) {
         long hi = word / 127773, lo = word % 127773;
-        word = 16807 * lo - 2836 * hi;
+        word = (int32_t)(16807 * lo - 2836 * hi);
         if (word < 0) word += 2147483647;
-        g->st[i] = (int32_t)word;
+        g->st[i] = word;
     }
     g->f = 3;
     g->r = 0;

@@ -1163,3 +1163,18 @@ int main(int argc, char **argv) {
     return grom_oracle_main(argc, argv, dump);
 }
 #endif
+
+/* ---- test hooks for the library restatements of the CNV path ---- */
+/* n outputs of glibc's rand() after srand(seed) (restated TYPE_3 generator) */
+void grom_oracle_rand_seq(unsigned int seed, int n, int *out) {
+    glibc_rng g;
+    glibc_srand(&g, seed);
+    for (int i = 0; i < n; i++) out[i] = glibc_rand(&g);
+}
+/* glibc 2.12 qsort (merge sort) of doubles with the reference's int comparator */
+void grom_oracle_msort_lo(double *a, long n) { qsort_dbl_intcmp(a, n); }
+/* grom_rand(max) n times after srand(seed), GROM.c:1185 */
+void grom_oracle_grom_rand(unsigned int seed, long mx, int n, long *out) {
+    glibc_srand(&g_rng, seed);
+    for (int i = 0; i < n; i++) out[i] = grom_rand(mx);
+}

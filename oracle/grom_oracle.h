@@ -40,6 +40,11 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix);
  * run with `-q min_mapq` uses them, i.e. after the "%e" text round trip. */
 void grom_oracle_tables(int min_mapq, double *mq_out, double *hez_out);
 
+/* test hooks of the CNV path's library restatements (cnv_oracle.c) */
+void grom_oracle_rand_seq(unsigned int seed, int n, int *out);
+void grom_oracle_msort_lo(double *a, long n);
+void grom_oracle_grom_rand(unsigned int seed, long mx, int n, long *out);
+
 #ifdef __cplusplus
 }
 #endif
