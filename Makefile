@@ -13,7 +13,7 @@ HOST_SRC = grom_amd/csrc/bamio.c grom_amd/csrc/stream.c grom_amd/csrc/tables.c g
 HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC)) build/snvfmt.o
 DEV_OBJ = build/scan.o build/cnv.o
 HDRS = include/grom_amd.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h
-KHDRS = grom_amd/csrc/k_scan_tile.h grom_amd/csrc/device_common.h grom_amd/csrc/snvfmt.h
+KHDRS = grom_amd/csrc/k_scan_tile.h grom_amd/csrc/device_common.h grom_amd/csrc/snvfmt.h grom_amd/csrc/k_scan_scatter.h
 
 all: $(LIBDIR)/libgrom_amd.so $(BINDIR)/grom $(BINDIR)/grom_synth oracle
 
@@ -50,11 +50,11 @@ oracle:
 	$(MAKE) -C oracle
 
 # kernel tuning variants, loaded with GROM_AMD_LIB=...:
-#   make variant V=w4 VFLAGS=-DGROM_WAVES_PER_EU=4  ->  build/variants/libgrom_amd_w4.so
+#   make variant V=w4 VFLAGS=-DGROM_WAVES_PER_EU=4  ->  grom_amd/lib/variants/libgrom_amd_w4.so
 variant: $(HOST_OBJ) build/cnv.o
-	@mkdir -p build/variants
+	@mkdir -p build/variants $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c grom_amd/csrc/scan.hip -o build/variants/scan_$(V).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o build/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/cnv.o $(HOST_OBJ) -lz -lm
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(LIBDIR)/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/cnv.o $(HOST_OBJ) -lz -lm
 
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR)

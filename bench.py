@@ -10,7 +10,9 @@ GPU) every rank scans its own chromosome: chromosomes shard with no data-path
 collective, so scaling is weak and `value` is all bases scanned / max-rank time.
 
 The JSON line also carries
-  roofline      k_scan_tile's algorithmic bytes per launch / its mean duration
+  roofline      the pileup kernel's (k_scan_tile; k_scan_scatter with
+                GROM_PILEUP=scatter) algorithmic bytes per launch / its mean
+                duration
                 (HIP events on the library's stream) against 8 TB/s HBM,
                 with PMC-measured traffic when profiles/pmc_<tag>.json exists;
   cpu_baseline  the CPU restatement of the reference (oracle/, "port"), one
@@ -33,10 +35,11 @@ COVERAGE = 30.0
 READ_LEN = 150
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 CPU_SAMPLE_LEN = 6_000_000
+PILEUP_KERNEL = "k_scan_scatter" if os.environ.get("GROM_PILEUP") == "scatter" else "k_scan_tile"
 
 
 def algorithmic_bytes(batch) -> int:
-    """Bytes k_scan_tile must move once per launch: every read record it ingests
+    """Bytes the pileup kernel must move once per launch: every read record it ingests
     (SoA metadata, CIGAR, packed bases, qualities), the reference, and the three
     whole-chromosome read-depth arrays it writes ('Roofline')."""
     r = batch.reads
@@ -125,7 +128,7 @@ def main():
     pmc = os.path.join(REPO, "profiles", f"pmc_{tag}.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("k_scan_tile_hbm_bytes_per_launch")
+            traffic = json.load(open(pmc)).get(f"{PILEUP_KERNEL}_hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -158,7 +161,7 @@ def main():
                 "host_generate_s": round(t_gen, 1),
             },
             "roofline": {
-                "bound": "hbm", "kernel": "k_scan_tile",
+                "bound": "hbm", "kernel": PILEUP_KERNEL,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "bytes_per_launch": abytes, "launch_ms": round(pile_s * 1e3, 3),

@@ -44,7 +44,7 @@ struct PileOut {
     uint32_t *n_cands;
     uint32_t cand_cap;
     uint32_t *run_base, *run_cnt;  // per tile: first candidate slot, candidates
-    unsigned long long *flush_acc;  // [0] sum of caf rd, [1] non-N bases
+    unsigned long long *flush_part;  // per tile: [0] sum of caf rd, [1] non-N bases (k_flush_reduce)
     int32_t *dbg;                   // nullable: GC_COUNT int32 per evaluated base
     uint32_t *status;               // reserved
     uint32_t *n_events;             // reserved

@@ -72,15 +72,20 @@ __global__ void k_prep(int64_t n, ReadArrays R, ReadMeta *__restrict__ meta, int
     if ((threadIdx.x & 63) == 0) atomicMax(halo, best);
 }
 
+// per-tile reductions of the output step (pile_emit)
+struct TileTail {
+    unsigned long long red[TG / 64][2];
+    uint32_t wcnt[TG / 64];  // candidates per wave
+    uint32_t cbase;          // the tile's first candidate slot
+};
+
 struct __align__(16) ScanLds {
     ReadMeta meta[RCHUNK];
     uint4 qual[QV];
     uint4 seq[SV];
     uint32_t cig[CIGCAP];
     char ref[TG];
-    unsigned long long red[TG / 64][2];
-    uint32_t wcnt[TG / 64];  // candidates per wave
-    uint32_t cbase;          // the tile's first candidate slot
+    TileTail tail;
     int32_t m2;  // reads of the chunk that fit the staging budgets
 };
 
@@ -206,6 +211,147 @@ __device__ __forceinline__ void staged_base(const uint8_t *lq8, const uint8_t *l
     sbyte = ls8[soff + (rel >> 1)];
 }
 
+// The outputs of position x (one lane per position; every lane of the
+// workgroup calls this, it has barriers): caf arrays, flush depth sums, the
+// debug counters, the SNV test (GROM.c:11096-11199) and the tile's candidate
+// run.  Shared by the gather and the scatter tile kernels.
+__device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *__restrict__ ref, const PileOut &O,
+                                          const double *__restrict__ mq_tab, const double *__restrict__ hez_tab,
+                                          TileTail &T_, int64_t tile, int32_t x, char rb, bool evals,
+                                          const LaneCounts &c, int32_t rd, int32_t caf_mq, int32_t caf_rd,
+                                          int32_t caf_low, const int32_t (&sch)[6], const int32_t (&scn)[6]) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int32_t clen = (int32_t)a.chr_len;
+    // soft-clip counters in the reference's order (GC_SC_LEFT..GC_INDEL_SC+4)
+    int32_t sc[15];
+    sc[0] = 6 * sch[0]; sc[1] = 6 * sch[1]; sc[2] = scn[0]; sc[3] = scn[1]; sc[4] = scn[0] + scn[1];
+    sc[5] = 6 * sch[2]; sc[6] = 6 * sch[3]; sc[7] = scn[2]; sc[8] = scn[3]; sc[9] = scn[2] + scn[3];
+    sc[10] = 6 * sch[4]; sc[11] = 6 * sch[5]; sc[12] = scn[4]; sc[13] = scn[5]; sc[14] = scn[4] + scn[5];
+
+    // ---- outputs of this position ----
+    unsigned long long fsum = 0, fcnt = 0;
+    if (x < clen) {
+        O.caf_mq[x] = caf_mq;
+        O.caf_rd[x] = caf_rd;
+        O.caf_low[x] = caf_low;
+        if (x < a.flush_end && rb != 'N') {  // SNV flush depth sums, GROM.c:15066-15073
+            fsum = (unsigned long long)((int64_t)caf_rd + caf_low);
+            fcnt = 1;
+        }
+    }
+    int best = -1;  // candidate base of this position, if any
+    float best_ratio = 0.f;
+    if (evals) {
+        const int32_t total = c.snv0 + c.snv1 + c.snv2 + c.snv3;
+        const int32_t rc_all = total + c.low0 + c.low1 + c.low2 + c.low3;
+        const int32_t bq_all = c.bq_hi + c.bq_lo, mq_all = c.mq_hi + c.mq_lo;
+        if (O.dbg) {
+            int32_t *d = O.dbg + (size_t)(x - a.eval_lo) * GC_COUNT;
+            d[GC_POS] = x;
+            d[GC_SNV + 0] = c.snv0; d[GC_SNV + 1] = c.snv1; d[GC_SNV + 2] = c.snv2; d[GC_SNV + 3] = c.snv3;
+            d[GC_SNV_LOWMQ + 0] = c.low0; d[GC_SNV_LOWMQ + 1] = c.low1;
+            d[GC_SNV_LOWMQ + 2] = c.low2; d[GC_SNV_LOWMQ + 3] = c.low3;
+            d[GC_PIR + 0] = c.pir0; d[GC_PIR + 1] = c.pir1; d[GC_PIR + 2] = c.pir2; d[GC_PIR + 3] = c.pir3;
+            d[GC_FS + 0] = c.fs0; d[GC_FS + 1] = c.fs1; d[GC_FS + 2] = c.fs2; d[GC_FS + 3] = c.fs3;
+            d[GC_BQ] = c.bq_hi;
+            d[GC_BQ_ALL] = bq_all;
+            d[GC_MQ] = c.mq_hi;
+            d[GC_MQ_ALL] = mq_all;
+            d[GC_BQ_RC] = total;
+            d[GC_MQ_RC] = total;
+            d[GC_RC_ALL] = rc_all;
+            d[GC_RD] = rd;
+#pragma unroll
+            for (int k = 0; k < 15; k++) d[GC_SC_LEFT + k] = sc[k];
+        }
+        // SNV test, GROM.c:11096-11199
+        // (the divisions only where some non-reference base reaches -n: the
+        // tests are pure, so skipping them elsewhere changes no result)
+        const int32_t snv[4] = {c.snv0, c.snv1, c.snv2, c.snv3};
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) any = any || (rb != c_acgt[k] && snv[k] >= a.min_snv);
+        if (any && rd + sc[14] > 0 && rb != 'N') {
+            const bool bq_ok = (double)bq_all / (double)rc_all >= a.min_ave_bq;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float ratio = (float)snv[k] / (float)total;
+                if (rb != c_acgt[k] && (double)ratio >= a.min_snv_ratio && snv[k] >= a.min_snv && bq_ok) {
+                    if (best < 0 || ratio > best_ratio) {
+                        best = k;
+                        best_ratio = ratio;
+                    }
+                }
+            }
+        }
+    }
+    // ---- block totals: flush depth sums and the tile's candidate run ----
+    // Candidates of a tile are written contiguously in position order at a
+    // base taken with one atomic per tile; k_run_* put the runs in tile order.
+    const uint64_t cmask = __ballot(best >= 0);
+    for (int o = 32; o > 0; o >>= 1) {
+        fsum += __shfl_xor(fsum, o, 64);
+        fcnt += __shfl_xor(fcnt, o, 64);
+    }
+    if (lane == 0) {
+        T_.red[wave][0] = fsum;
+        T_.red[wave][1] = fcnt;
+        T_.wcnt[wave] = (uint32_t)__popcll(cmask);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long s = 0, cc = 0;
+        uint32_t nc = 0;
+        for (int w = 0; w < TG / 64; w++) {
+            s += T_.red[w][0];
+            cc += T_.red[w][1];
+            nc += T_.wcnt[w];
+        }
+        // per-tile flush sums, reduced by k_flush_reduce (one global atomic
+        // per tile on a single address serialises the whole grid)
+        O.flush_part[2 * tile] = s;
+        O.flush_part[2 * tile + 1] = cc;
+        const uint32_t base = nc ? atomicAdd(O.n_cands, nc) : 0u;
+        T_.cbase = base;
+        O.run_base[tile] = base;
+        O.run_cnt[tile] = nc;
+    }
+    __syncthreads();
+    if (best >= 0) {
+        uint32_t ci = T_.cbase + (uint32_t)__popcll(cmask & ((1ull << lane) - 1));
+        for (int w = 0; w < wave; w++) ci += T_.wcnt[w];
+        if (ci < O.cand_cap) {  // else the host sees n_cands > cap and re-runs with room
+            const int32_t total = c.snv0 + c.snv1 + c.snv2 + c.snv3;
+            grom_snv_cand cd;
+            cd.pos = x;
+            cd.base = best;
+            cd.ratio = best_ratio;
+            cd.ref_base = (int32_t)(unsigned char)ref[x];
+            const int32_t sk = best == 0 ? c.snv0 : best == 1 ? c.snv1 : best == 2 ? c.snv2 : c.snv3;
+            const size_t ti = (total > GROM_MAX_TRIALS)
+                                  ? (size_t)GROM_MAX_TRIALS * (GROM_MAX_TRIALS + 1) + sk * GROM_MAX_TRIALS / total
+                                  : (size_t)total * (GROM_MAX_TRIALS + 1) + sk;
+            cd.binom = mq_tab[ti];
+            cd.hez = hez_tab[ti];
+            cd.snv[0] = c.snv0; cd.snv[1] = c.snv1; cd.snv[2] = c.snv2; cd.snv[3] = c.snv3;
+            cd.lowmq[0] = c.low0; cd.lowmq[1] = c.low1; cd.lowmq[2] = c.low2; cd.lowmq[3] = c.low3;
+            cd.pir[0] = c.pir0; cd.pir[1] = c.pir1; cd.pir[2] = c.pir2; cd.pir[3] = c.pir3;
+            cd.fs[0] = c.fs0; cd.fs[1] = c.fs1; cd.fs[2] = c.fs2; cd.fs[3] = c.fs3;
+            cd.bq = c.bq_hi;
+            cd.bq_all = c.bq_hi + c.bq_lo;
+            cd.mq = c.mq_hi;
+            cd.mq_all = c.mq_hi + c.mq_lo;
+            cd.bq_rc = total;
+            cd.mq_rc = total;
+            cd.rc_all = total + c.low0 + c.low1 + c.low2 + c.low3;
+            cd.pad1 = 0;
+            O.cands[ci] = cd;
+        }
+    }
+}
+
 // occupancy target: 5 waves per SIMD (a 96-register budget) measured faster
 // than the unconstrained 4 despite a few spills; GROM_WAVES_PER_EU overrides
 #ifndef GROM_WAVES_PER_EU
@@ -213,17 +359,11 @@ __device__ __forceinline__ void staged_base(const uint8_t *lq8, const uint8_t *l
 #endif
 #define GROM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GROM_WAVES_PER_EU)))
 
-__global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
-                                                  const ReadMeta *__restrict__ meta,
-                                                  const int32_t *__restrict__ tile_lo,
-                                                  const int32_t *__restrict__ tile_hi, PileOut O,
-                                                  const double *__restrict__ mq_tab,
-                                                  const double *__restrict__ hez_tab, int64_t n_tiles) {
-    __shared__ ScanLds L;
-    // XCD-contiguous tile order (speed only; any mapping is correct)
-    const int64_t per_xcd = (n_tiles + 7) / 8;
-    const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-    if (tile >= n_tiles) return;  // whole workgroup leaves together
+__device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const grom_scan_args &a,
+                                                 const char *__restrict__ ref, const ReadArrays &R,
+                                                 const ReadMeta *__restrict__ meta, const int32_t *__restrict__ tile_lo,
+                                                 const int32_t *__restrict__ tile_hi, const PileOut &O,
+                                                 const double *__restrict__ mq_tab, const double *__restrict__ hez_tab) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -475,126 +615,38 @@ __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args 
     GROM_ADD4(c, pir, rcode, mc.pir);
     GROM_ADD4(c, low, rcode, mc.low);
 
-    // soft-clip counters in the reference's order (GC_SC_LEFT..GC_INDEL_SC+4)
-    int32_t sc[15];
-    sc[0] = 6 * sch[0]; sc[1] = 6 * sch[1]; sc[2] = scn[0]; sc[3] = scn[1]; sc[4] = scn[0] + scn[1];
-    sc[5] = 6 * sch[2]; sc[6] = 6 * sch[3]; sc[7] = scn[2]; sc[8] = scn[3]; sc[9] = scn[2] + scn[3];
-    sc[10] = 6 * sch[4]; sc[11] = 6 * sch[5]; sc[12] = scn[4]; sc[13] = scn[5]; sc[14] = scn[4] + scn[5];
+    pile_emit(a, ref, O, mq_tab, hez_tab, L.tail, tile, x, rb, evals, c, rd, caf_mq, caf_rd, caf_low, sch, scn);
+}
 
-    // ---- outputs of this position ----
-    unsigned long long fsum = 0, fcnt = 0;
-    if (x < clen) {
-        O.caf_mq[x] = caf_mq;
-        O.caf_rd[x] = caf_rd;
-        O.caf_low[x] = caf_low;
-        if (x < a.flush_end && rb != 'N') {  // SNV flush depth sums, GROM.c:15066-15073
-            fsum = (unsigned long long)((int64_t)caf_rd + caf_low);
-            fcnt = 1;
-        }
-    }
-    int best = -1;  // candidate base of this position, if any
-    float best_ratio = 0.f;
-    if (evals) {
-        const int32_t total = c.snv0 + c.snv1 + c.snv2 + c.snv3;
-        const int32_t rc_all = total + c.low0 + c.low1 + c.low2 + c.low3;
-        const int32_t bq_all = c.bq_hi + c.bq_lo, mq_all = c.mq_hi + c.mq_lo;
-        if (O.dbg) {
-            int32_t *d = O.dbg + (size_t)(x - a.eval_lo) * GC_COUNT;
-            d[GC_POS] = x;
-            d[GC_SNV + 0] = c.snv0; d[GC_SNV + 1] = c.snv1; d[GC_SNV + 2] = c.snv2; d[GC_SNV + 3] = c.snv3;
-            d[GC_SNV_LOWMQ + 0] = c.low0; d[GC_SNV_LOWMQ + 1] = c.low1;
-            d[GC_SNV_LOWMQ + 2] = c.low2; d[GC_SNV_LOWMQ + 3] = c.low3;
-            d[GC_PIR + 0] = c.pir0; d[GC_PIR + 1] = c.pir1; d[GC_PIR + 2] = c.pir2; d[GC_PIR + 3] = c.pir3;
-            d[GC_FS + 0] = c.fs0; d[GC_FS + 1] = c.fs1; d[GC_FS + 2] = c.fs2; d[GC_FS + 3] = c.fs3;
-            d[GC_BQ] = c.bq_hi;
-            d[GC_BQ_ALL] = bq_all;
-            d[GC_MQ] = c.mq_hi;
-            d[GC_MQ_ALL] = mq_all;
-            d[GC_BQ_RC] = total;
-            d[GC_MQ_RC] = total;
-            d[GC_RC_ALL] = rc_all;
-            d[GC_RD] = rd;
-#pragma unroll
-            for (int k = 0; k < 15; k++) d[GC_SC_LEFT + k] = sc[k];
-        }
-        // SNV test, GROM.c:11096-11199
-        if (rd + sc[14] > 0 && rb != 'N') {
-            const int32_t snv[4] = {c.snv0, c.snv1, c.snv2, c.snv3};
-            const bool bq_ok = (double)bq_all / (double)rc_all >= a.min_ave_bq;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const float ratio = (float)snv[k] / (float)total;
-                if (rb != c_acgt[k] && (double)ratio >= a.min_snv_ratio && snv[k] >= a.min_snv && bq_ok) {
-                    if (best < 0 || ratio > best_ratio) {
-                        best = k;
-                        best_ratio = ratio;
-                    }
-                }
-            }
-        }
-    }
-    // ---- block totals: flush depth sums and the tile's candidate run ----
-    // Candidates of a tile are written contiguously in position order at a
-    // base taken with one atomic per tile; k_run_* put the runs in tile order.
-    const uint64_t cmask = __ballot(best >= 0);
-    for (int o = 32; o > 0; o >>= 1) {
-        fsum += __shfl_xor(fsum, o, 64);
-        fcnt += __shfl_xor(fcnt, o, 64);
-    }
-    if (lane == 0) {
-        L.red[wave][0] = fsum;
-        L.red[wave][1] = fcnt;
-        L.wcnt[wave] = (uint32_t)__popcll(cmask);
-    }
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long s = 0, cc = 0;
-        uint32_t nc = 0;
-        for (int w = 0; w < TG / 64; w++) {
-            s += L.red[w][0];
-            cc += L.red[w][1];
-            nc += L.wcnt[w];
-        }
-        if (cc) {
-            atomicAdd(&O.flush_acc[0], s);
-            atomicAdd(&O.flush_acc[1], cc);
-        }
-        const uint32_t base = nc ? atomicAdd(O.n_cands, nc) : 0u;
-        L.cbase = base;
-        O.run_base[tile] = base;
-        O.run_cnt[tile] = nc;
-    }
-    __syncthreads();
-    if (best >= 0) {
-        uint32_t ci = L.cbase + (uint32_t)__popcll(cmask & ((1ull << lane) - 1));
-        for (int w = 0; w < wave; w++) ci += L.wcnt[w];
-        if (ci < O.cand_cap) {  // else the host sees n_cands > cap and re-runs with room
-            const int32_t total = c.snv0 + c.snv1 + c.snv2 + c.snv3;
-            grom_snv_cand cd;
-            cd.pos = x;
-            cd.base = best;
-            cd.ratio = best_ratio;
-            cd.ref_base = (int32_t)(unsigned char)ref[x];
-            const int32_t sk = best == 0 ? c.snv0 : best == 1 ? c.snv1 : best == 2 ? c.snv2 : c.snv3;
-            const size_t ti = (total > GROM_MAX_TRIALS)
-                                  ? (size_t)GROM_MAX_TRIALS * (GROM_MAX_TRIALS + 1) + sk * GROM_MAX_TRIALS / total
-                                  : (size_t)total * (GROM_MAX_TRIALS + 1) + sk;
-            cd.binom = mq_tab[ti];
-            cd.hez = hez_tab[ti];
-            cd.snv[0] = c.snv0; cd.snv[1] = c.snv1; cd.snv[2] = c.snv2; cd.snv[3] = c.snv3;
-            cd.lowmq[0] = c.low0; cd.lowmq[1] = c.low1; cd.lowmq[2] = c.low2; cd.lowmq[3] = c.low3;
-            cd.pir[0] = c.pir0; cd.pir[1] = c.pir1; cd.pir[2] = c.pir2; cd.pir[3] = c.pir3;
-            cd.fs[0] = c.fs0; cd.fs[1] = c.fs1; cd.fs[2] = c.fs2; cd.fs[3] = c.fs3;
-            cd.bq = c.bq_hi;
-            cd.bq_all = c.bq_hi + c.bq_lo;
-            cd.mq = c.mq_hi;
-            cd.mq_all = c.mq_hi + c.mq_lo;
-            cd.bq_rc = total;
-            cd.mq_rc = total;
-            cd.rc_all = total + c.low0 + c.low1 + c.low2 + c.low3;
-            cd.pad1 = 0;
-            O.cands[ci] = cd;
-        }
+// every tile of the chromosome (GROM_PILEUP=gather)
+__global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
+                                                  const ReadMeta *__restrict__ meta,
+                                                  const int32_t *__restrict__ tile_lo,
+                                                  const int32_t *__restrict__ tile_hi, PileOut O,
+                                                  const double *__restrict__ mq_tab,
+                                                  const double *__restrict__ hez_tab, int64_t n_tiles) {
+    __shared__ ScanLds L;
+    // XCD-contiguous tile order (speed only; any mapping is correct)
+    const int64_t per_xcd = (n_tiles + 7) / 8;
+    const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    if (tile >= n_tiles) return;  // whole workgroup leaves together
+    scan_tile_gather(L, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+}
+
+// the tiles listed by the scatter kernel as over its LDS event budget; the
+// grid is fixed and the count is read on the device, so no host round trip
+__global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile_list(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
+                                                       const ReadMeta *__restrict__ meta,
+                                                       const int32_t *__restrict__ tile_lo,
+                                                       const int32_t *__restrict__ tile_hi, PileOut O,
+                                                       const double *__restrict__ mq_tab,
+                                                       const double *__restrict__ hez_tab,
+                                                       const uint32_t *__restrict__ list, const uint32_t *__restrict__ n_list) {
+    __shared__ ScanLds L;
+    const uint32_t n = *n_list;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        __syncthreads();  // the previous tile's LDS is no longer read
+        scan_tile_gather(L, (int64_t)list[i], a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
     }
 }
 
@@ -668,4 +720,3 @@ __global__ __launch_bounds__(256) void k_run_gather(int64_t n_tiles, const uint3
     }
 }
 
-#undef GROM_ADD4

@@ -149,6 +149,25 @@ __global__ void k_rmdup(int64_t n, int32_t tid, const int32_t *__restrict__ pos,
 // k_scan_tile: the tile kernel (k_scan_tile.h)
 // ---------------------------------------------------------------------------
 #include "k_scan_tile.h"
+#include "k_scan_scatter.h"
+
+// the per-tile flush sums of the pileup kernels into acc[0..1]
+__global__ __launch_bounds__(256) void k_flush_reduce(int64_t n_tiles, const unsigned long long *__restrict__ part,
+                                                      unsigned long long *__restrict__ acc) {
+    unsigned long long s = 0, c = 0;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n_tiles; t += (int64_t)gridDim.x * blockDim.x) {
+        s += part[2 * t];
+        c += part[2 * t + 1];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        c += __shfl_xor(c, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && (s | c)) {
+        atomicAdd(&acc[0], s);
+        atomicAdd(&acc[1], c);
+    }
+}
 
 // sums of caf_rd + caf_low over non-N bases of [0, e) for mid-scan flushes
 __global__ void k_flush_sum(int64_t e, const char *__restrict__ ref, const int32_t *__restrict__ rd,
@@ -205,7 +224,7 @@ struct Ctx {
     // reads (used when the caller passes host memory)
     DevBuf r_pos, r_flag, r_mapq, r_mtid, r_mpos, r_isize, r_lq, r_coff, r_cig, r_boff, r_seq, r_qual, r_nid, ref;
     // scan scratch
-    DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg;
+    DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, ovf, fpart;
     grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
     size_t h_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, ep0 = nullptr, ep1 = nullptr;
@@ -286,6 +305,17 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     }
     hipStream_t st = C.st;
     const bool timing = getenv("GROM_TIMING") != nullptr;  // per-phase host clock on stderr
+    // The pileup runs the gather kernel (k_scan_tile) on every tile.
+    // GROM_PILEUP=scatter selects the scatter formulation (k_scan_scatter,
+    // with the gather kernel redoing tiles over its LDS event budget); it is
+    // bit-exact but measured slower on MI355X.  GROM_EVCAP
+    // lowers the scatter kernel's per-tile event budget (tests use it to
+    // exercise the fallback).
+    const char *pk = getenv("GROM_PILEUP");
+    const bool gather_only = !(pk && strcmp(pk, "scatter") == 0);
+    uint32_t evcap = GROM_EVENT_CAP;
+    if (const char *ec = getenv("GROM_EVCAP")) evcap = (uint32_t)std::min<long>(std::max<long>(atol(ec), 0), GROM_EVENT_CAP);
+    uint32_t n_ovf_tiles = 0;
     const auto t_start = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -330,6 +360,8 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         (rc = ensure(C.keep, (size_t)std::max<int64_t>(n, 1))) ||
         (rc = ensure(C.meta, sizeof(ReadMeta) * (size_t)std::max<int64_t>(n, 1))) ||
         (rc = ensure(C.runb, sizeof(uint32_t) * n_tiles)) || (rc = ensure(C.runc, sizeof(uint32_t) * n_tiles)) ||
+        (rc = ensure(C.ovf, sizeof(uint32_t) * n_tiles)) ||
+        (rc = ensure(C.fpart, 2 * sizeof(unsigned long long) * n_tiles)) ||
         (rc = ensure(C.segs, sizeof(uint32_t) * (size_t)((n_tiles + RUN_SEG - 1) / RUN_SEG + 1))))
         return rc;
     if (want_dbg && (rc = ensure(C.dbg, sizeof(int32_t) * GC_COUNT * std::max<int64_t>(n_eval, 1)))) return rc;
@@ -337,7 +369,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     if (C.cands.cap >= sizeof(grom_snv_cand) * 2)
         cand_cap = std::max<uint32_t>(cand_cap, (uint32_t)(C.cands.cap / sizeof(grom_snv_cand)));
 
-    // misc layout: [0] halo (int32), [4..] n_cands, status[2], n_events ; [32..] flush_acc[2] ; [64..] mid acc[2]
+    // misc layout: [0] halo (int32), [4..] n_cands, n_ovf, n_events ; [32..] flush_acc[2] ; [64..] mid acc[2]
     char *misc = (char *)C.misc.p;
     int32_t *d_halo = (int32_t *)misc;
     uint32_t *d_ncand = (uint32_t *)(misc + 4);
@@ -372,23 +404,35 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                                (int32_t *)C.tlo.p, (int32_t *)C.thi.p);
         }
         PileOut po{(int32_t *)C.caf_mq.p, (int32_t *)C.caf_rd.p, (int32_t *)C.caf_low.p,
-                   (grom_snv_cand *)C.cands.p, d_ncand, cand_cap, (uint32_t *)C.runb.p, (uint32_t *)C.runc.p, d_facc,
+                   (grom_snv_cand *)C.cands.p, d_ncand, cand_cap, (uint32_t *)C.runb.p, (uint32_t *)C.runc.p,
+                   (unsigned long long *)C.fpart.p,
                    want_dbg ? (int32_t *)C.dbg.p : nullptr, d_status, d_nev};
         HIPCHK(hipEventRecord(C.ep0, st));
-        hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)(((n_tiles + 7) / 8) * 8)), dim3(GROM_TILE), 0, st, a,
-                           ch->ref, ra, (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez,
-                           n_tiles);
+        const unsigned grid = (unsigned)(((n_tiles + 7) / 8) * 8);
+        if (gather_only) {
+            hipLaunchKernelGGL(k_scan_tile, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
+                               (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
+                               C.d_mq, C.d_hez, n_tiles);
+        } else {
+            // scatter tiles; the few over the LDS event budget are redone by
+            // the gather kernel, whose grid reads their count on the device
+            hipLaunchKernelGGL(k_scan_scatter, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
+                               (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
+                               C.d_mq, C.d_hez, n_tiles, evcap, (uint32_t *)C.ovf.p, d_status);
+            hipLaunchKernelGGL(k_scan_tile_list, dim3((unsigned)std::min<int64_t>(n_tiles, 1024)), dim3(GROM_TILE), 0, st,
+                               a, ch->ref, ra, (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p,
+                               (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, (const uint32_t *)C.ovf.p,
+                               (const uint32_t *)d_status);
+        }
+        hipLaunchKernelGGL(k_flush_reduce, dim3(256), dim3(256), 0, st, n_tiles,
+                           (const unsigned long long *)C.fpart.p, d_facc);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(C.ep1, st));
         uint32_t hdr[4];
         HIPCHK(hipMemcpyAsync(hdr, misc + 4, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         const double t_kernels = ms_since(t_start);
-        if (hdr[1] != 0) {
-            set_err("per-tile event buffer overflow in %u tile(s), first tile %u (position %lld)", hdr[1], hdr[2],
-                    (long long)hdr[2] * T);
-            return GROM_E_OVERFLOW;
-        }
+        n_ovf_tiles = hdr[1];
         if (hdr[0] > cand_cap) {
             cand_cap = hdr[0] + hdr[0] / 4 + 1024;
             continue;
@@ -477,10 +521,10 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         if (timing)
             fprintf(stderr,
                     "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms, rows %.3f ms (%u candidates), "
-                    "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows)\n",
+                    "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows), %u of %lld tiles to the gather kernel\n",
                     ch->name ? ch->name : "?", t_kernels, t_copied - t_kernels, t_snv - t_copied, ncand,
                     ms_since(t_start) - t_snv, ct.ms_device, (long long)ct.del_calls, (long long)ct.dup_calls,
-                    (long long)ct.rows);
+                    (long long)ct.rows, gather_only ? (unsigned)n_tiles : n_ovf_tiles, (long long)n_tiles);
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
         if (stats) {
@@ -598,7 +642,7 @@ void grom_dev_fini(int device) {
     (void)hipStreamSynchronize(C.st);
     DevBuf *all[] = {&C.r_pos, &C.r_flag, &C.r_mapq, &C.r_mtid, &C.r_mpos, &C.r_isize, &C.r_lq, &C.r_coff,
                      &C.r_cig, &C.r_boff, &C.r_seq, &C.r_qual, &C.r_nid, &C.ref, &C.keep, &C.meta, &C.cands2,
-                     &C.runb, &C.runc, &C.segs, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
+                     &C.runb, &C.runc, &C.segs, &C.ovf, &C.fpart, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
                      &C.misc, &C.dbg};
     for (DevBuf *b : all)
         if (b->p) (void)hipFree(b->p);

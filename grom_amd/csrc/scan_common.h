@@ -7,10 +7,12 @@
 #include <stdint.h>
 
 /* positions per tile of the pileup kernel and threads per tile */
+#ifndef GROM_TILE
 #define GROM_TILE 256
-#define GROM_TILE_THREADS 256
-/* per-tile LDS event capacity (mismatches needing read-name de-duplication
- * plus soft-clip evidence); overflow is reported, never silently dropped */
+#endif
+#define GROM_TILE_THREADS GROM_TILE
+/* per-tile LDS event capacity of the scatter kernel (mismatches, soft-clip
+ * evidence); a tile over it is redone by the gather kernel */
 #define GROM_EVENT_CAP 1024
 /* read-name slots per position supported by the kernel (g_min_snv, -n) */
 #define GROM_MAX_NAME_SLOTS 8

@@ -53,13 +53,15 @@ def run_oracle(datadir, bam, fa, out, extra=(), dump=None):
     return run(ORACLE_BIN, ["-i", bam, "-r", fa, "-o", out] + list(extra), str(datadir), env)
 
 
-def run_grom(datadir, bam, fa, out, extra=(), dump=None):
+def run_grom(datadir, bam, fa, out, extra=(), dump=None, env_extra=None):
     """The product CLI, called in this process through the C ABI so the HIP
     library is loaded (and checked) by the test process itself."""
     import grom_amd
     env = {"GROM_FILEDATE": FILEDATE, "GROM_SEED": SEED}
     if dump:
         env["GROM_DUMP"] = dump
+    if env_extra:
+        env.update(env_extra)
     rc = grom_amd.cli_main(["-i", bam, "-r", fa, "-o", out] + list(extra), env=env, cwd=str(datadir))
     assert rc == 0, f"grom_cli_main returned {rc}: {grom_amd.last_error()}"
     return rc

@@ -42,13 +42,23 @@ def _names(datadir, tag):
     return sorted(f.split(".")[-2] for f in os.listdir(datadir) if f.startswith(tag + ".") and f.endswith(".cnt"))
 
 
-@pytest.mark.parametrize("case,extra", RUNS, ids=[f"{c}{''.join(e)}" for c, e in RUNS])
-def test_counters_and_vcf_bit_exact(datadir, case, extra):
+# the pileup has two kernels: gather (default) and scatter (GROM_PILEUP=
+# scatter), whose tiles over the LDS event budget the gather kernel redoes.
+# GROM_EVCAP shrinks that budget so most tiles take the fallback.
+KERNEL_RUNS = [
+    ("lowmapq_clip", [], {"GROM_PILEUP": "scatter"}),
+    ("lowmapq_clip", [], {"GROM_PILEUP": "scatter", "GROM_EVCAP": "4"}),
+    ("dups", ["-M"], {"GROM_PILEUP": "scatter", "GROM_EVCAP": "24"}),
+    ("three_chr", [], {"GROM_PILEUP": "scatter"}),
+    ("one_chr", ["-G", "40"], {"GROM_PILEUP": "scatter"}),
+]
+
+
+def _check_counters(datadir, case, extra, tag, env_extra=None):
     bam, fa = synth(datadir, case, CASES[case])
-    tag = f"{case}{''.join(extra).replace('-', '_')}"
     o_dump, g_dump = f"o_{tag}", f"g_{tag}"
     run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra, dump=str(datadir / o_dump))
-    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, dump=str(datadir / g_dump))
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, dump=str(datadir / g_dump), env_extra=env_extra)
     chroms = _names(datadir, o_dump)
     assert chroms
     for ch in chroms:
@@ -66,6 +76,18 @@ def test_counters_and_vcf_bit_exact(datadir, case, extra):
     assert ov.count("\n") > 46
     assert ov == gv
     assert filecmp.cmp(datadir / f"o_{tag}.ctx.vcf", datadir / f"g_{tag}.ctx.vcf", shallow=False)
+
+
+@pytest.mark.parametrize("case,extra", RUNS, ids=[f"{c}{''.join(e)}" for c, e in RUNS])
+def test_counters_and_vcf_bit_exact(datadir, case, extra):
+    _check_counters(datadir, case, extra, f"{case}{''.join(extra).replace('-', '_')}")
+
+
+@pytest.mark.parametrize("case,extra,env", KERNEL_RUNS,
+                         ids=[f"{c}{''.join(e)}_{'_'.join(f'{k}{v}' for k, v in n.items())}" for c, e, n in KERNEL_RUNS])
+def test_pileup_kernel_paths_bit_exact(datadir, case, extra, env):
+    tag = f"{case}{''.join(extra).replace('-', '_')}_{'_'.join(v for v in env.values())}"
+    _check_counters(datadir, case, extra, tag, env_extra=env)
 
 
 @pytest.mark.parametrize("case,extra", CNV_RUNS, ids=[f"{c}{''.join(e)}" for c, e in CNV_RUNS])
