@@ -122,6 +122,8 @@ inline unsigned long long __ballot(int p) {
     return m;
 }
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
+inline long long __double_as_longlong(double d) { long long r; std::memcpy(&r, &d, 8); return r; }
+inline double __longlong_as_double(long long v) { double r; std::memcpy(&r, &v, 8); return r; }
 
 // ---- atomics ----
 template <typename T, typename U>
