@@ -364,7 +364,7 @@ __device__ __forceinline__ void scat_scan(ScatLds &L, int32_t (&v)[NSCAN]) {
 }
 
 #ifndef GROM_SCAT_WAVES_PER_EU
-#define GROM_SCAT_WAVES_PER_EU 6
+#define GROM_SCAT_WAVES_PER_EU 4
 #endif
 
 __global__ __launch_bounds__(TG) __attribute__((amdgpu_waves_per_eu(GROM_SCAT_WAVES_PER_EU))) void k_scan_scatter(

@@ -120,7 +120,8 @@ __device__ __forceinline__ int acgt_code(int s4) {
 // character (bam_nt16_rev_table) equals the reference base, or 16 if none, so
 // `s4 == rb4` is the reference's `ref != read base` test negated; mv says the
 // reference base is one of ACGT.
-__device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, uint32_t (&slot)[GROM_MAX_NAME_SLOTS],
+template <int NS>
+__device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, uint32_t (&slot)[NS],
                                            int min_snv, bool hq, bool mv, int q, int s4, int rb4, bool fwd, int qi,
                                            int lseq_mod, int mq, uint32_t nid) {
     if (s4 == rb4) {
@@ -143,7 +144,7 @@ __device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, uint32
         // with selects so the slots stay in registers.
         bool done = false, found = false;
 #pragma unroll
-        for (int s = 0; s < GROM_MAX_NAME_SLOTS; s++) {
+        for (int s = 0; s < NS; s++) {
             const bool active = !done && s < min_snv;
             const bool empty = active && slot[s] == 0;
             const bool match = active && !empty && slot[s] == nid;
@@ -359,6 +360,8 @@ __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *_
 #endif
 #define GROM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GROM_WAVES_PER_EU)))
 
+// NS: read-name slots kept per position (>= -n; fewer slots, fewer VGPRs)
+template <int NS>
 __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const grom_scan_args &a,
                                                  const char *__restrict__ ref, const ReadArrays &R,
                                                  const ReadMeta *__restrict__ meta, const int32_t *__restrict__ tile_lo,
@@ -388,9 +391,9 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
     // soft-clip evidence per category (plain, ctx, indel) x side (L, R):
     // reads with mapq >= -q (each adds 6, GROM.c:5829-5836) and all reads
     int32_t sch[6] = {0, 0, 0, 0, 0, 0}, scn[6] = {0, 0, 0, 0, 0, 0};
-    uint32_t slot[GROM_MAX_NAME_SLOTS];
+    uint32_t slot[NS];
 #pragma unroll
-    for (int k = 0; k < GROM_MAX_NAME_SLOTS; k++) slot[k] = 0;
+    for (int k = 0; k < NS; k++) slot[k] = 0;
 
     const uint4 *gq4 = reinterpret_cast<const uint4 *>(R.qual);
     const uint4 *gs4 = reinterpret_cast<const uint4 *>(R.seq);
@@ -619,6 +622,7 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
 }
 
 // every tile of the chromosome (GROM_PILEUP=gather)
+template <int NS>
 __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
                                                   const ReadMeta *__restrict__ meta,
                                                   const int32_t *__restrict__ tile_lo,
@@ -630,11 +634,12 @@ __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args 
     const int64_t per_xcd = (n_tiles + 7) / 8;
     const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (tile >= n_tiles) return;  // whole workgroup leaves together
-    scan_tile_gather(L, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+    scan_tile_gather<NS>(L, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
 }
 
 // the tiles listed by the scatter kernel as over its LDS event budget; the
 // grid is fixed and the count is read on the device, so no host round trip
+template <int NS>
 __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile_list(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
                                                        const ReadMeta *__restrict__ meta,
                                                        const int32_t *__restrict__ tile_lo,
@@ -646,7 +651,7 @@ __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile_list(grom_scan_
     const uint32_t n = *n_list;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();  // the previous tile's LDS is no longer read
-        scan_tile_gather(L, (int64_t)list[i], a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+        scan_tile_gather<NS>(L, (int64_t)list[i], a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
     }
 }
 

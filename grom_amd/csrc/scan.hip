@@ -409,17 +409,23 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                    want_dbg ? (int32_t *)C.dbg.p : nullptr, d_status, d_nev};
         HIPCHK(hipEventRecord(C.ep0, st));
         const unsigned grid = (unsigned)(((n_tiles + 7) / 8) * 8);
+        const bool few = P.min_snv <= GROM_FEW_NAME_SLOTS;
         if (gather_only) {
-            hipLaunchKernelGGL(k_scan_tile, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
-                               (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                               C.d_mq, C.d_hez, n_tiles);
+            if (few)
+                hipLaunchKernelGGL(k_scan_tile<GROM_FEW_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
+                                   (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
+                                   C.d_mq, C.d_hez, n_tiles);
+            else
+                hipLaunchKernelGGL(k_scan_tile<GROM_MAX_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
+                                   (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
+                                   C.d_mq, C.d_hez, n_tiles);
         } else {
             // scatter tiles; the few over the LDS event budget are redone by
             // the gather kernel, whose grid reads their count on the device
             hipLaunchKernelGGL(k_scan_scatter, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
                                (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
                                C.d_mq, C.d_hez, n_tiles, evcap, (uint32_t *)C.ovf.p, d_status);
-            hipLaunchKernelGGL(k_scan_tile_list, dim3((unsigned)std::min<int64_t>(n_tiles, 1024)), dim3(GROM_TILE), 0, st,
+            hipLaunchKernelGGL(k_scan_tile_list<GROM_MAX_NAME_SLOTS>, dim3((unsigned)std::min<int64_t>(n_tiles, 1024)), dim3(GROM_TILE), 0, st,
                                a, ch->ref, ra, (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p,
                                (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, (const uint32_t *)C.ovf.p,
                                (const uint32_t *)d_status);

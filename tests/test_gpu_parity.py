@@ -24,6 +24,7 @@ RUNS = [
     ("empty_middle", []),
     ("one_chr", ["-p", "4", "-x", "28"]),
     ("one_chr", ["-G", "40"]),  # forces mid-scan SNV list flushes (GROM.c:11201)
+    ("dups", ["-n", "6", "-a", "0.1"]),  # -n above 4: the 8-slot build of the gather kernel
 ]
 
 # read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call
