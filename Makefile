@@ -51,10 +51,11 @@ oracle:
 
 # kernel tuning variants, loaded with GROM_AMD_LIB=...:
 #   make variant V=w4 VFLAGS=-DGROM_WAVES_PER_EU=4  ->  grom_amd/lib/variants/libgrom_amd_w4.so
-variant: $(HOST_OBJ) build/cnv.o
+variant: $(HOST_OBJ)
 	@mkdir -p build/variants $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c grom_amd/csrc/scan.hip -o build/variants/scan_$(V).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(LIBDIR)/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/cnv.o $(HOST_OBJ) -lz -lm
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -ffp-contract=off -c grom_amd/csrc/cnv.hip -o build/variants/cnv_$(V).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(LIBDIR)/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/variants/cnv_$(V).o $(HOST_OBJ) -lz -lm
 
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR)

@@ -353,6 +353,10 @@ __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *_
     }
 }
 
+#ifndef GROM_PAIR
+#define GROM_PAIR 2  // single-op reads folded per step of the gather kernel
+#endif
+
 // occupancy target: 5 waves per SIMD (a 96-register budget) measured faster
 // than the unconstrained 4 despite a few spills; GROM_WAVES_PER_EU overrides
 #ifndef GROM_WAVES_PER_EU
@@ -374,7 +378,11 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
     const int32_t t0 = (int32_t)(tile * TG);
     const int32_t x = t0 + tid;         // this lane's reference position
     const int32_t x0 = t0 + wave * 64;  // first position of this wave
+#ifdef GROM_PROF_NOREADS  // timing probe only: the tile's fixed work
+    const int32_t r0 = tile_lo[tile], r1 = r0;
+#else
     const int32_t r0 = tile_lo[tile], r1 = tile_hi[tile];
+#endif
     L.ref[tid] = (x < clen) ? upcase(ref[x]) : 'N';
     const char rb = L.ref[tid];
     int rb4 = 16;  // the 4-bit code printed as rb (GROM compares characters)
@@ -476,6 +484,57 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
             uint64_t mask = __ballot(rel);
             if (!mask) continue;
             while (mask) {
+                // GROM_PAIR single-op reads at once: their staged bases are
+                // read from LDS together, then tallied in read order
+                if (staged && __popcll(mask) >= GROM_PAIR) {
+                    ReadView uk[GROM_PAIR];
+                    uint64_t mk = mask;
+                    bool all_fast = true;
+#pragma unroll
+                    for (int k = 0; k < GROM_PAIR; k++) {
+                        uk[k] = view_of(G, __builtin_ctzll(mk));
+                        mk &= mk - 1;
+                        all_fast = all_fast && fast_read(uk[k]);
+                    }
+                    if (all_fast) {
+                        mask = mk;
+                        int32_t hk[GROM_PAIR];
+                        uint32_t qk[GROM_PAIR], sk[GROM_PAIR];
+#pragma unroll
+                        for (int k = 0; k < GROM_PAIR; k++) {
+                            const ReadView &u = uk[k];
+                            const int32_t p0 = u.p0, len = (int32_t)(u.cw0 >> 4);
+                            const int mq = (int)u.mq;
+                            const uint32_t dx = (uint32_t)(x - p0);
+                            if (p0 >= 0 && len < clen - p0 && dx < (uint32_t)len) {
+                                caf_mq += mq;
+                                caf_rd += (mq >= a.rd_min_mapq) ? 1 : 0;
+                                caf_low += (mq >= a.rd_min_mapq) ? 0 : 1;
+                            }
+                            const bool pos_ok = p0 >= 0 && p0 < clen;
+                            hk[k] = (pos_ok && evals && dx < (uint32_t)min(len, clen - p0)) ? (int32_t)dx : -1;
+                            rd += (dx < (uint32_t)u.lq) ? 1 : 0;  // E = pos + l_qseq
+                            qk[k] = 0;
+                            sk[k] = 0;
+                            if (hk[k] >= 0 && hk[k] < u.lq) staged_base(lq8, ls8, soff, u.bo + hk[k], qk[k], sk[k]);
+                        }
+#pragma unroll
+                        for (int k = 0; k < GROM_PAIR; k++) {
+                            const ReadView &u = uk[k];
+                            if (hk[k] >= 0) {
+                                int q = 0, s4 = 15;
+                                if (hk[k] < u.lq) {
+                                    q = (int)qk[k];
+                                    s4 = (int)((sk[k] >> ((((u.bo + hk[k]) & 1) ^ 1) << 2)) & 15u);
+                                }
+                                const int mq = (int)u.mq;
+                                tally_base(c, mc, slot, a.min_snv, mq >= a.min_mapq && q >= a.min_base_qual, mv, q,
+                                           s4, rb4, !(u.fl & 0x10), hk[k], u.lq, mq, u.nid);
+                            }
+                        }
+                        continue;
+                    }
+                }
                 const ReadView u = view_of(G, __builtin_ctzll(mask));
                 mask &= mask - 1;
                 const int32_t p0 = u.p0;
