@@ -1,7 +1,8 @@
 """bench.py -- GROM per-chromosome scan on MI355X.
 
 One step = one pass of the scan (grom_scan_chrom_device: the pileup/SNV HIP
-kernels, the host SNV-list flush and VCF formatting, and the read-depth CNV
+kernels, the host SNV-list flush and VCF formatting, the CIGAR indel-evidence
+pass, and the read-depth CNV
 path -- GC windows, depth blocks, detect_del_dup and its rows) over one
 synthetic 100 Mb, 30x,
 2x150 bp paired-end chromosome whose reads are already resident in HBM

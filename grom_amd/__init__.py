@@ -58,6 +58,12 @@ class Stats(C.Structure):
                 ("snv_candidates", C.c_int64), ("mismatch_events", C.c_int64)]
 
 
+class IndelRec(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("pos", "ins", "ins_len", "del_f", "del_f_len", "del_f_rd", "del_r",
+                                         "del_r_len", "del_r_rd", "other_len")] + \
+        [("ins_seq", C.c_char * 52), ("pad", C.c_int32)]
+
+
 # every function declared in include/grom_amd.h, with its ctypes signature
 _SIGS = {
     "grom_abi_version": (C.c_int, []),
@@ -71,6 +77,7 @@ _SIGS = {
                                          C.POINTER(Stats)]),
     "grom_debug_counts": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(C.c_int32), C.c_void_p,
                                     C.c_int64, C.c_void_p]),
+    "grom_debug_indels": (C.c_int64, [C.c_int, C.c_void_p, C.c_int64]),
     "grom_build_tables": (None, [C.c_int32, C.c_void_p, C.c_void_p]),
     "grom_default_params": (None, [C.POINTER(Params)]),
     "grom_params_set_insert": (None, [C.POINTER(Params), C.c_int32, C.c_int32, C.c_int32, C.c_int32]),

@@ -199,6 +199,17 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
             snprintf(path, sizeof(path), "%s.%s.caf", dump, cp->name);
             f = fopen(path, "wb");
             if (f) { fwrite(caf, sizeof(int32_t), 3 * cp->len, f); fclose(f); }
+            /* indel evidence of the same scan (row A7) */
+            int64_t n_ind = grom_debug_indels(device, NULL, 0);
+            grom_indel_rec *ind = n_ind > 0 ? malloc(sizeof(grom_indel_rec) * n_ind) : NULL;
+            if (n_ind >= 0 && (n_ind == 0 || (ind && grom_debug_indels(device, ind, n_ind) == n_ind))) {
+                snprintf(path, sizeof(path), "%s.%s.ind", dump, cp->name);
+                f = fopen(path, "wb");
+                if (f) { if (n_ind) fwrite(ind, sizeof(grom_indel_rec), n_ind, f); fclose(f); }
+            } else {
+                fprintf(stderr, "grom: indel dump of %s failed: %s\n", cp->name, grom_last_error());
+            }
+            free(ind);
         } else {
             fprintf(stderr, "grom: counter dump of %s failed: %s\n", cp->name, grom_last_error());
         }

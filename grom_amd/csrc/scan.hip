@@ -35,6 +35,7 @@
 
 #include "../../include/grom_amd.h"
 #include "cnv.h"
+#include "indel.h"
 #include "scan_common.h"
 #include "snvfmt.h"
 
@@ -229,6 +230,7 @@ struct Ctx {
     size_t h_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, ep0 = nullptr, ep1 = nullptr;
     CnvScratch *cnv = nullptr;  // read-depth CNV path (cnv.hip)
+    IndelScratch *indel = nullptr;  // CIGAR indel evidence (indel.hip)
 };
 
 static Ctx g_ctx[64];
@@ -508,6 +510,22 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         snv_rows(P, ch, cands + done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1], vt);
         const double t_snv = ms_since(t_start);
 
+        // CIGAR indel evidence of the evaluated bases (row A7, GROM.c:7187-7423);
+        // its records feed the indel evaluation (not built yet)
+        double ms_indel = 0;
+        int64_t n_indel = 0;
+        {
+            if (!C.indel) C.indel = indel_scratch_new();
+            char ierr[512] = {0};
+            rc = indel_chrom(C.indel, st, n, R->pos, R->mapq, keep, R->cigar_off, R->cigar, R->base_off, R->l_qseq,
+                             R->seq, P.min_mapq, a.eval_lo, a.eval_hi, &n_indel, &ms_indel, ierr, sizeof(ierr));
+            if (rc != GROM_OK) {
+                set_err("%s", ierr);
+                return rc;
+            }
+        }
+        const double t_indel = ms_since(t_start);
+
         // read-depth CNV path after the SV rows (GROM.c:16633-17300); the
         // reference runs it only when the FASTA name matched a BAM target
         CnvTiming ct{};
@@ -527,9 +545,10 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         if (timing)
             fprintf(stderr,
                     "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms, rows %.3f ms (%u candidates), "
+                    "indel evidence %.3f ms (device %.3f ms, %lld bases), "
                     "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows), %u of %lld tiles to the gather kernel\n",
                     ch->name ? ch->name : "?", t_kernels, t_copied - t_kernels, t_snv - t_copied, ncand,
-                    ms_since(t_start) - t_snv, ct.ms_device, (long long)ct.del_calls, (long long)ct.dup_calls,
+                    t_indel - t_snv, ms_indel, (long long)n_indel, ms_since(t_start) - t_indel, ct.ms_device, (long long)ct.del_calls, (long long)ct.dup_calls,
                     (long long)ct.rows, gather_only ? (unsigned)n_tiles : n_ovf_tiles, (long long)n_tiles);
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
@@ -612,6 +631,7 @@ size_t grom_abi_struct_size(int which) {
     case 2: return sizeof(grom_reads);
     case 3: return sizeof(grom_out);
     case 4: return sizeof(grom_stats);
+    case 5: return sizeof(grom_indel_rec);
     default: return 0;
     }
 }
@@ -654,6 +674,7 @@ void grom_dev_fini(int device) {
         if (b->p) (void)hipFree(b->p);
     if (C.h_cands) (void)hipHostFree(C.h_cands);
     cnv_scratch_free(C.cnv);
+    indel_scratch_free(C.indel);
     (void)hipFree(C.d_mq);
     (void)hipFree(C.d_hez);
     (void)hipEventDestroy(C.e0);
@@ -714,6 +735,19 @@ int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *rea
     rc = scan_device(*C, &dch, &dr, &tmp, nullptr, first_pos, counts, counts_cap, caf3);
     grom_out_free(&tmp);
     return rc;
+}
+
+int64_t grom_debug_indels(int device, grom_indel_rec *out, int64_t cap) {
+    Ctx *C = ctx_of(device);
+    if (!C) return GROM_E_NODEV;
+    if (!C->indel) return 0;
+    const int64_t n = indel_count(C->indel);
+    const int64_t m = std::min<int64_t>(n, std::max<int64_t>(cap, 0));
+    if (m > 0 && out) {
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipMemcpy(out, indel_records(C->indel), sizeof(grom_indel_rec) * (size_t)m, hipMemcpyDeviceToHost));
+    }
+    return n;
 }
 
 }  // extern "C"

@@ -74,6 +74,7 @@ void synth_default_cfg(synth_cfg *c) {
     c->repeat_rate = 2e-5;
     c->fasta_line = 60;
     c->cnv_rate = 0.0;
+    c->multi_indel = 0.0;
     c->cnv_min = 10000;
     c->cnv_max = 300000;
     c->seed = 2;
@@ -156,31 +157,37 @@ static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo h[2]
             } else {
                 int len = 1 + (int)xint(&r, c->max_indel);
                 int ins = xunif(&r) < 0.5;
+                /* multi-allelic: both haplotypes carry an indel, of two lengths */
+                int lens[2] = {len, len};
+                if (c->multi_indel > 0 && xunif(&r) < c->multi_indel) {
+                    gt = 2;
+                    lens[1] = 1 + (int)xint(&r, c->max_indel);
+                }
                 if (ins) {
                     for (int k = 0; k < 2; k++) {
                         int has = (gt == 2) || (gt == k);
                         h[k].seq[h[k].len] = ub;
                         h[k].map[h[k].len++] = (int32_t)i;
                         if (has)
-                            for (int q = 0; q < len; q++) {
+                            for (int q = 0; q < lens[k]; q++) {
                                 h[k].seq[h[k].len] = ACGT[xint(&r, 4)];
                                 h[k].map[h[k].len++] = -1;
                             }
                     }
                 } else {
-                    /* deletion of ref[i+1 .. i+len] */
+                    /* deletion of ref[i+1 .. i+lens[k]] on the haplotypes that carry it */
+                    int span = lens[0] > lens[1] ? lens[0] : lens[1];
                     for (int k = 0; k < 2; k++) {
                         int has = (gt == 2) || (gt == k);
                         h[k].seq[h[k].len] = ub;
                         h[k].map[h[k].len++] = (int32_t)i;
-                        if (!has)
-                            for (int q = 1; q <= len; q++) {
-                                char b = ref[i + q];
-                                h[k].seq[h[k].len] = (b >= 'a' && b <= 'z') ? (char)(b - 32) : b;
-                                h[k].map[h[k].len++] = (int32_t)(i + q);
-                            }
+                        for (int q = has ? lens[k] + 1 : 1; q <= span; q++) {
+                            char b = ref[i + q];
+                            h[k].seq[h[k].len] = (b >= 'a' && b <= 'z') ? (char)(b - 32) : b;
+                            h[k].map[h[k].len++] = (int32_t)(i + q);
+                        }
                     }
-                    consumed = 1 + len;
+                    consumed = 1 + span;
                 }
             }
             i += consumed;

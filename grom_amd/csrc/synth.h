@@ -44,6 +44,9 @@ typedef struct synth_cfg {
     double repeat_rate;   /* dinucleotide repeat runs per base */
     int fasta_line;       /* FASTA line width */
     double cnv_rate;      /* copy-number regions per base (0 = none) */
+    double multi_indel;   /* fraction of indels whose second haplotype carries
+                             a different length (exercises the evidence
+                             "other" slots); 0 keeps the random stream as is */
     long cnv_min, cnv_max;/* copy-number region length range */
     uint64_t seed;
 } synth_cfg;

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GROM_AMD_ABI_VERSION 2
+#define GROM_AMD_ABI_VERSION 3
 #define GROM_MAX_TRIALS 1000 /* max_trials, GROM.c:631 */
 
 enum {
@@ -159,7 +159,8 @@ int grom_abi_version(void);
 /* number of visible GPUs (hipGetDeviceCount); 0 if none */
 int grom_device_count(void);
 /* sizeof of the ABI structs, for bindings to check their layout:
- * 0 grom_params, 1 grom_chrom, 2 grom_reads, 3 grom_out, 4 grom_stats */
+ * 0 grom_params, 1 grom_chrom, 2 grom_reads, 3 grom_out, 4 grom_stats,
+ * 5 grom_indel_rec */
 size_t grom_abi_struct_size(int which);
 const char *grom_last_error(void);
 
@@ -189,6 +190,29 @@ int grom_scan_chrom_device(int device, const grom_chrom *chrom, const grom_reads
 #define GROM_NCOUNT 40
 int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *reads, int32_t *first_pos,
                       int32_t *counts, int64_t counts_cap, int32_t *caf3);
+
+/* CIGAR indel evidence of one evaluated base (row A7; replaces the reference's
+ * cdp_one_base_indel_* ring arrays, GROM.c:7187-7423): primary insertion,
+ * forward-deletion and reverse-deletion counters (+6 per MAPQ >= -q read, 0
+ * otherwise) with their lengths, the deletion read depths, the number of
+ * occupied "other" slots as the evaluation counts them (GROM.c:11415-11425;
+ * indel-typed slots only in this build) and the 50-byte inserted-sequence
+ * buffer (zero-filled when the base enters the window). */
+typedef struct grom_indel_rec {
+    int32_t pos;
+    int32_t ins, ins_len;
+    int32_t del_f, del_f_len, del_f_rd;
+    int32_t del_r, del_r_len, del_r_rd;
+    int32_t other_len;
+    char ins_seq[52];
+    int32_t pad;
+} grom_indel_rec;
+
+/* Test hook: the indel evidence records of the last scan on `device` (one per
+ * evaluated base that a CIGAR I/D op reached, in position order).  Copies at
+ * most `cap` records to `out` (may be NULL with cap 0) and returns how many
+ * the scan produced, or a negative GROM_E_* code. */
+int64_t grom_debug_indels(int device, grom_indel_rec *out, int64_t cap);
 
 /* Host helpers shared by the CLI and the tests (grom_amd/csrc/tables.c):
  * the tables exactly as a run with -q min_mapq uses them. */

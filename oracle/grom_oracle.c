@@ -333,7 +333,16 @@ typedef struct {
     int W;          /* window length = g_half_one_base_rd_len */
     orc_counts *c;  /* counters (pos field unused here) */
     int32_t *names; /* g_min_snv name ids per position */
+    orc_indel *ind; /* CIGAR indel evidence per position (row A7) */
+    uint8_t *ind_touched;            /* some I/D op reached the base */
+    uint8_t (*ot_type)[50];          /* cdp_one_base_other_type (indel types only) */
+    int32_t (*ot_cnt)[50];           /* cdp_one_base_other */
+    double (*ot_dist)[50];           /* cdp_one_base_other_dist */
 } win_t;
+
+#define ORC_OTHER_LEN 50 /* g_other_len, GROM.c:837 */
+#define ORC_INDEL_SEQ 50 /* g_indel_i_seq_len, GROM.c:904 */
+enum { OT_EMPTY = 0, OT_INDEL_I = 11, OT_INDEL_D_F = 12, OT_INDEL_D_R = 13 }; /* GROM.c:668-681 */
 
 static inline long wslot(const win_t *w, long x) { return ((x % w->W) + w->W) % w->W; }
 
@@ -554,6 +563,64 @@ static int rmdup_svtype(const cur_t *c) {
 }
 
 /* one record through the ingest body (GROM.c:6418-7185) */
+/* One CIGAR indel event folded into its base (GROM.c:7209-7283 for I,
+ * 7289-7420 for the two deletion ends): the primary counter takes the first
+ * length seen while its count is 0, a same-length event adds, and a different
+ * length goes to the "other" slots, where an entry that overtakes the primary
+ * swaps with it. */
+static void indel_fold(win_t *w, long x, int type, int add, long len, const char *seq) {
+    long sl = wslot(w, x);
+    orc_indel *k = &w->ind[sl];
+    w->ind_touched[sl] = 1;
+    int32_t *cnt, *dist;
+    if (type == OT_INDEL_I) { cnt = &k->ins; dist = &k->ins_len; }
+    else if (type == OT_INDEL_D_F) { cnt = &k->del_f; dist = &k->del_f_len; k->del_f_rd += 1; }
+    else { cnt = &k->del_r; dist = &k->del_r_len; k->del_r_rd += 1; }
+    if (*cnt == 0) {
+        *cnt = add;
+        *dist = (int32_t)len;
+        if (type == OT_INDEL_I && len <= ORC_INDEL_SEQ)
+            for (long q = 0; q < len; q++) k->ins_seq[q] = seq[q];
+    } else if ((uint32_t)len == (uint32_t)*dist) {
+        *cnt += add;
+    } else {
+        int found = 0;
+        for (int o = 0; o < ORC_OTHER_LEN; o++) {
+            if (w->ot_type[sl][o] == type) {
+                if ((uint32_t)len == (uint32_t)(w->ot_dist[sl][o] + 0.5)) {
+                    found = 1;
+                    w->ot_cnt[sl][o] += add;
+                    if (w->ot_cnt[sl][o] > *cnt) {
+                        int32_t tc = w->ot_cnt[sl][o];
+                        double td = w->ot_dist[sl][o];
+                        w->ot_cnt[sl][o] = *cnt;
+                        w->ot_dist[sl][o] = *dist;
+                        *cnt = tc;
+                        *dist = (int32_t)(uint32_t)(td + 0.5);
+                    }
+                    break;
+                }
+            } else if (w->ot_type[sl][o] == OT_EMPTY) {
+                found = 1;
+                w->ot_cnt[sl][o] = add;
+                w->ot_type[sl][o] = (uint8_t)type;
+                w->ot_dist[sl][o] = (double)len;
+                break;
+            }
+        }
+        if (!found) {
+            for (int o = 0; o < ORC_OTHER_LEN; o++) {
+                if (w->ot_cnt[sl][o] <= add) {
+                    w->ot_cnt[sl][o] = add;
+                    w->ot_type[sl][o] = (uint8_t)type;
+                    w->ot_dist[sl][o] = (double)len;
+                    break;
+                }
+            }
+        }
+    }
+}
+
 static void ingest(scan_t *s, cur_t *c) {
     const char *fasta = s->fasta;
     long chr_len = s->chr_len;
@@ -750,10 +817,38 @@ static void ingest(scan_t *s, cur_t *c) {
     }
     /* physical read depth over [pos, E), GROM.c:7173-7181 */
     for (long x = c->pos; x < E; x++) s->w.c[wslot(&s->w, x)].rd += 1;
+
+    /* CIGAR indel evidence, GROM.c:7187-7423: every ingested read; I at the
+     * base after the preceding aligned block, D at its first and last base */
+    {
+        long tp = c->pos;
+        int sb = 0;
+        char iseq[ORC_INDEL_SEQ];
+        for (int a = 0; a < cigar_len; a++) {
+            int op = c_type[a];
+            if (op == GC_SOFT_CLIP) {
+                sb += (int)c_len[a];
+            } else if (op == GC_MATCH || op == GC_REF_SKIP || op == GC_EQUAL || op == GC_DIFF) {
+                tp += c_len[a];
+                if (op != GC_REF_SKIP) sb += (int)c_len[a];
+            } else if (op == GC_INS) {
+                if (c_len[a] <= ORC_INDEL_SEQ)
+                    for (long q = 0; q < c_len[a]; q++)
+                        iseq[q] = (sb + q < lseq_q) ? grom_nt16_rev[bam_seqi(seq4, sb + q)] : 0;
+                indel_fold(&s->w, tp, OT_INDEL_I, c->add, c_len[a], iseq);
+                sb += (int)c_len[a];
+            } else if (op == GC_DEL) {
+                indel_fold(&s->w, tp, OT_INDEL_D_F, c->add, c_len[a], NULL);
+                indel_fold(&s->w, tp + c_len[a] - 1, OT_INDEL_D_R, c->add, c_len[a], NULL);
+                tp += c_len[a];
+            }
+        }
+    }
 }
 
 static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_match, int chr_match,
-                            const char *fasta, long chr_len, const char *chr_name, FILE *vcf, FILE *dump_cnt) {
+                            const char *fasta, long chr_len, const char *chr_name, FILE *vcf, FILE *dump_cnt,
+                            FILE *dump_ind) {
     (void)target_name_of_match;
     scan_t s;
     memset(&s, 0, sizeof(s));
@@ -769,6 +864,11 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     s.w.W = g_half_one_base_rd_len;
     s.w.c = (orc_counts *)calloc(s.w.W, sizeof(orc_counts));
     s.w.names = (int32_t *)calloc((size_t)s.w.W * g_min_snv, sizeof(int32_t));
+    s.w.ind = (orc_indel *)calloc(s.w.W, sizeof(orc_indel));
+    s.w.ind_touched = (uint8_t *)calloc(s.w.W, 1);
+    s.w.ot_type = calloc(s.w.W, sizeof(*s.w.ot_type));
+    s.w.ot_cnt = calloc(s.w.W, sizeof(*s.w.ot_cnt));
+    s.w.ot_dist = calloc(s.w.W, sizeof(*s.w.ot_dist));
     s.caf_mq = (int32_t *)calloc(chr_len, sizeof(int32_t));
     s.caf_rd = (int32_t *)calloc(chr_len, sizeof(int32_t));
     s.caf_low = (int32_t *)calloc(chr_len, sizeof(int32_t));
@@ -817,6 +917,15 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                                 orc_counts o = *k;
                                 o.pos = p;
                                 fwrite(&o, sizeof(o), 1, dump_cnt);
+                                long sl_ = wslot(&s.w, p);
+                                if (dump_ind && s.w.ind_touched[sl_]) {
+                                    orc_indel r = s.w.ind[sl_];
+                                    r.pos = p;
+                                    r.other_len = ORC_OTHER_LEN; /* GROM.c:11415-11425 */
+                                    for (int o = 0; o < ORC_OTHER_LEN; o++)
+                                        if (s.w.ot_type[sl_][o] == OT_EMPTY) { r.other_len = o; break; }
+                                    fwrite(&r, sizeof(r), 1, dump_ind);
+                                }
                             }
                             /* SNV test, GROM.c:11096-11199 */
                             if (k->rd + k->indel_sc_rd > 0 && fasta[p] != 'N' && fasta[p] != 'n') {
@@ -874,6 +983,11 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                             long sl_ = wslot(&s.w, x);
                             memset(&s.w.c[sl_], 0, sizeof(orc_counts));
                             memset(&s.w.names[sl_ * g_min_snv], 0, sizeof(int32_t) * g_min_snv);
+                            memset(&s.w.ind[sl_], 0, sizeof(orc_indel));
+                            s.w.ind_touched[sl_] = 0;
+                            memset(s.w.ot_type[sl_], 0, sizeof(s.w.ot_type[0]));
+                            memset(s.w.ot_cnt[sl_], 0, sizeof(s.w.ot_cnt[0]));
+                            memset(s.w.ot_dist[sl_], 0, sizeof(s.w.ot_dist[0]));
                         }
                     } else {
                         n_skipped++;
@@ -918,6 +1032,7 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     snv_list_free(&sl);
     nametab_free(&s.names);
     free(s.w.c); free(s.w.names);
+    free(s.w.ind); free(s.w.ind_touched); free(s.w.ot_type); free(s.w.ot_cnt); free(s.w.ot_dist);
     free(s.caf_mq); free(s.caf_rd); free(s.caf_low);
     free(s.rm_mchr); free(s.rm_mpos); free(s.rm_lseq); free(s.rm_tlen); free(s.rm_svtype);
 }
@@ -1123,16 +1238,19 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
             target_name = st.hdr.ref_name[a];
             if (names_match(lc, l2, g_chr_names[fmatch], g_chr_names_len[fmatch])) { chr_match = a; break; }
         }
-        FILE *dump_cnt = NULL;
+        FILE *dump_cnt = NULL, *dump_ind = NULL;
         char cname[MAX_CHR_NAME_LEN + 1];
         snprintf(cname, sizeof(cname), "%.*s", g_chr_names_len[fmatch], g_chr_names[fmatch]);
         if (g_dump_prefix) {
             char path[4096];
             snprintf(path, sizeof(path), "%s.%s.cnt", g_dump_prefix, cname);
             dump_cnt = fopen(path, "wb");
+            snprintf(path, sizeof(path), "%s.%s.ind", g_dump_prefix, cname);
+            dump_ind = fopen(path, "wb");
         }
-        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, dump_cnt);
+        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, dump_cnt, dump_ind);
         if (dump_cnt) fclose(dump_cnt);
+        if (dump_ind) fclose(dump_ind);
     }
     bam_free_rec(&cur.b);
     stream_close(&st);

@@ -28,11 +28,31 @@ typedef struct orc_counts {
     int32_t indel_sc_left, indel_sc_right, indel_sc_left_rd, indel_sc_right_rd, indel_sc_rd;
 } orc_counts;
 
+/* CIGAR indel evidence of one base (row A7, GROM.c:7187-7423): the primary
+ * insertion / forward-deletion / reverse-deletion counters with their lengths,
+ * the deletion read depths, how many of the base's "other" slots are occupied
+ * (the first OTHER_EMPTY index, as GROM.c:11415-11425 computes it) and the
+ * 50-byte inserted-sequence buffer (zero-filled when the base enters the
+ * window, GROM.c:5634-5636, 6030-6040).  Only indel-typed "other" slots exist
+ * here: the discordant-pair and split-read types that share them (A8/A9) are
+ * not restated.  Same layout as grom_indel_rec (include/grom_amd.h). */
+typedef struct orc_indel {
+    int32_t pos;
+    int32_t ins, ins_len;
+    int32_t del_f, del_f_len, del_f_rd;
+    int32_t del_r, del_r_len, del_r_rd;
+    int32_t other_len;
+    char ins_seq[52];
+    int32_t pad;
+} orc_indel;
+
 /* Run the reference CLI semantics: argv as for GROM (-i -r -o ...).
  * If dump_prefix is non-NULL, for every processed chromosome the counters of
  * every evaluated base (p > 2*insert_max, GROM.c:11086) are written to
  * <dump_prefix>.<chrname>.cnt as packed orc_counts records, and the caf read
- * depth arrays to <dump_prefix>.<chrname>.caf (3 x int32 x chr_len).
+ * depth arrays to <dump_prefix>.<chrname>.caf (3 x int32 x chr_len), and
+ * the indel evidence of every evaluated base that any CIGAR I/D op touched
+ * to <dump_prefix>.<chrname>.ind as packed orc_indel records.
  * Returns the process exit code the reference would return. */
 int grom_oracle_main(int argc, char **argv, const char *dump_prefix);
 

@@ -22,6 +22,10 @@ CASES = {
     "lowmapq_clip": ["-L", "300000", "-s", "13", "-Q", "0.2", "-C", "0.08", "-q", "0.1", "-U", "0.01"],
     "dups": ["-L", "300000", "-s", "14", "-D", "0.15"],
     "empty_middle": ["-L", "200000,200000,200000", "-s", "15", "-c", "30,0,30"],
+    # CIGAR indels at 10x the default rate, half of them multi-allelic (two
+    # lengths at one base: the evidence "other" slots and their swaps), with
+    # low-MAPQ reads (zero-weight evidence) and PCR duplicates for -M
+    "indels": ["-L", "400000", "-s", "21", "-I", "0.001", "-J", "0.5", "-Q", "0.1", "-D", "0.1"],
     # copy-number regions (0x, 0.5x, 1.5x, 2x depth) for the read-depth CNV path
     "cnv": ["-L", "1500000", "-s", "16", "-V", "0.000004", "-W", "20000,150000", "-Q", "0.05"],
     "cnv_multi": ["-L", "700000,900000", "-s", "17", "-V", "0.000005", "-W", "15000,80000", "-Q", "0.08"],
@@ -65,6 +69,16 @@ def run_grom(datadir, bam, fa, out, extra=(), dump=None, env_extra=None):
     rc = grom_amd.cli_main(["-i", bam, "-r", fa, "-o", out] + list(extra), env=env, cwd=str(datadir))
     assert rc == 0, f"grom_cli_main returned {rc}: {grom_amd.last_error()}"
     return rc
+
+
+INDEL_DTYPE = np.dtype([(n, "<i4") for n in ("pos", "ins", "ins_len", "del_f", "del_f_len", "del_f_rd", "del_r",
+                                             "del_r_len", "del_r_rd", "other_len")] +
+                       [("ins_seq", "S52"), ("pad", "<i4")])
+
+
+def load_indels(path):
+    """grom_indel_rec / orc_indel records (include/grom_amd.h)."""
+    return np.fromfile(path, dtype=INDEL_DTYPE)
 
 
 def load_counts(path):

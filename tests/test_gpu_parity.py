@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from _util import CASES, load_counts, run_grom, run_oracle, synth
+from _util import CASES, load_counts, load_indels, run_grom, run_oracle, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -25,6 +25,9 @@ RUNS = [
     ("one_chr", ["-p", "4", "-x", "28"]),
     ("one_chr", ["-G", "40"]),  # forces mid-scan SNV list flushes (GROM.c:11201)
     ("dups", ["-n", "6", "-a", "0.1"]),  # -n above 4: the 8-slot build of the gather kernel
+    ("indels", []),
+    ("indels", ["-M"]),
+    ("indels", ["-q", "10"]),
 ]
 
 # read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call
@@ -73,6 +76,14 @@ def _check_counters(datadir, case, extra, tag, env_extra=None):
         ocaf = np.fromfile(datadir / f"{o_dump}.{ch}.caf", np.int32)
         gcaf = np.fromfile(datadir / f"{g_dump}.{ch}.caf", np.int32)
         assert np.array_equal(ocaf, gcaf), ch
+        # CIGAR indel evidence (row A7): one record per evaluated base an I/D op reached
+        oi = load_indels(datadir / f"{o_dump}.{ch}.ind")
+        gi = load_indels(datadir / f"{g_dump}.{ch}.ind")
+        assert oi.shape == gi.shape, (ch, oi.shape, gi.shape)
+        bad = np.nonzero(oi != gi)[0]
+        assert bad.size == 0, (ch, "first differing indel record", oi[bad[0]], gi[bad[0]])
+        if case == "indels":
+            assert (oi["other_len"] > 0).sum() > 10 and (oi["ins"] > 0).sum() > 10
     ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"g_{tag}.vcf").read()
     assert ov.count("\n") > 46
     assert ov == gv

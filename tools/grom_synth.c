@@ -19,7 +19,7 @@ int main(int argc, char **argv) {
     const char *prefix = NULL;
     const char *names = NULL;
     int opt;
-    while ((opt = getopt(argc, argv, "o:L:c:l:m:d:s:e:Q:C:U:D:S:I:T:n:q:M:V:W:")) != -1) {
+    while ((opt = getopt(argc, argv, "o:L:c:l:m:d:s:e:Q:C:U:D:S:I:T:n:q:M:V:W:J:")) != -1) {
         switch (opt) {
         case 'o': prefix = optarg; break;
         case 'L': {
@@ -54,6 +54,7 @@ int main(int argc, char **argv) {
         case 'n': names = optarg; break;
         case 'q': c.lowq_frac = atof(optarg); break;
         case 'M': c.lower_frac = atof(optarg); break;
+        case 'J': c.multi_indel = atof(optarg); break;              /* multi-allelic indel fraction */
         case 'V': c.cnv_rate = atof(optarg); break;                 /* CNV regions per base */
         case 'W': sscanf(optarg, "%ld,%ld", &c.cnv_min, &c.cnv_max); break; /* CNV length range */
         default:
