@@ -153,8 +153,8 @@ def main():
             "data": "synthetic (seeded generator, grom_amd/csrc/synth.c)",
             "config": {
                 "workload": "BASELINE configs[1]: 1 chromosome of 100 Mb per GPU, 30x 2x150 bp paired-end, "
-                            "SNV/indel, reads resident in HBM; step = pileup/SNV scan + SNV flush + VCF text + read-depth "
-                            "CNV path (GC windows, depth blocks, detect_del_dup, CNV rows)",
+                            "SNV/indel, reads resident in HBM; step = pileup/SNV scan + SNV flush + VCF text + CIGAR "
+                            "indel evidence + read-depth CNV path (GC windows, depth blocks, detect_del_dup, CNV rows)",
                 "chrom_len": args.chrom_len, "coverage": COVERAGE, "read_len": READ_LEN,
                 "reads_per_gpu": batch.n_reads, "vcf_rows_per_step": rows,
                 "device_ms_per_step": round(sum(tot_ms) / len(tot_ms), 3),
