@@ -38,6 +38,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <thread>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -1175,7 +1177,17 @@ struct Buf {
 
 }  // namespace
 
+// per-class (DEL, DUP) window-search buffers and stream: the two classes are
+// independent (GROM.c:19359-20020 runs them one after the other over the same
+// inputs), so they run concurrently, each driven by its own host thread
+struct KindBufs {
+    Buf nxt, pre, prepos, ppos, calls, ok, tiles, vis, cnt;
+    hipStream_t st = nullptr;
+};
+
 struct CnvScratch {
+    KindBufs kb[2];
+    hipEvent_t walk_in = nullptr;
     Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1332,6 +1344,13 @@ void cnv_scratch_free(CnvScratch *S) {
                   &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok};
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
+    for (KindBufs &K : S->kb) {
+        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt};
+        for (Buf *b : kall)
+            if (b->p) (void)hipFree(b->p);
+        if (K.st) (void)hipStreamDestroy(K.st);
+    }
+    if (S->walk_in) (void)hipEventDestroy(S->walk_in);
     if (S->e0) (void)hipEventDestroy(S->e0);
     if (S->e1) (void)hipEventDestroy(S->e1);
     delete S;
@@ -1357,6 +1376,8 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     if (!S->e0) {
         CK(hipEventCreate(&S->e0));
         CK(hipEventCreate(&S->e1));
+        CK(hipEventCreateWithFlags(&S->walk_in, hipEventDisableTiming));
+        for (KindBufs &K : S->kb) CK(hipStreamCreateWithFlags(&K.st, hipStreamNonBlocking));
     }
     GlibcRand rng(seed);
     // GROM_TIMING: per-phase wall clock (syncs the stream at each mark)
@@ -1395,7 +1416,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     double *sd = (double *)S->sd.p;
     char *misc = (char *)S->misc.p;
     unsigned long long *acc = (unsigned long long *)misc;  // [0..3] block/chromosome sums
-    uint32_t *n_rep = (uint32_t *)(misc + 64), *n_calls = (uint32_t *)(misc + 72), *n_pre = (uint32_t *)(misc + 76);
+    uint32_t *n_rep = (uint32_t *)(misc + 64);
     // misc + 80: candidate count of the window search (n_pre + 1)
     CK(hipEventRecord(S->e0, st));
     CK(hipMemsetAsync(misc, 0, 128, st));
@@ -1832,28 +1853,37 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         uint32_t pre_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, len / 64), 1 << 26);
         uint32_t cand_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, len / 4), (int64_t)1 << 30);
         std::vector<CallRec> found[2];
-        for (int kind = 0; kind < 2 && n_ch > 0; kind++) {
+        // both threads call this one lambda: the buffer caps are per-call locals
+        auto run_kind = [&, call_cap0 = call_cap, pre_cap0 = pre_cap, cand_cap0 = cand_cap](int kind, char *err,
+                                                                                          size_t errlen) -> int {
+            uint32_t call_cap = call_cap0, pre_cap = pre_cap0, cand_cap = cand_cap0;
+            KindBufs &K = S->kb[kind];
+            hipStream_t st = K.st;
+            int rc = GROM_OK;
+            if ((rc = grow(K.cnt, 16, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
+            uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;  // n_calls, n_pre, n_cand, capped
+            CK(hipStreamWaitEvent(st, S->walk_in, 0));
             bool done = false;
             for (int attempt = 0; attempt < 8 && !done; attempt++) {
-                if ((rc = grow(S->nxt, 8 * (size_t)len, err, errlen)) ||
-                    (rc = grow(S->pre, sizeof(PreAB) * pre_cap, err, errlen)) ||
-                    (rc = grow(S->prepos, 8 * (size_t)cand_cap, err, errlen)) ||
-                    (rc = grow(S->ppos, 8 * (size_t)pre_cap, err, errlen)) ||
-                    (rc = grow(S->calls, sizeof(CallRec) * call_cap, err, errlen)) ||
-                    (rc = grow(S->ok, call_cap, err, errlen)) ||
-                    (rc = grow(S->tiles, sizeof(ChunkState) * n_ch, err, errlen)))
+                if ((rc = grow(K.nxt, 8 * (size_t)len, err, errlen)) ||
+                    (rc = grow(K.pre, sizeof(PreAB) * pre_cap, err, errlen)) ||
+                    (rc = grow(K.prepos, 8 * (size_t)cand_cap, err, errlen)) ||
+                    (rc = grow(K.ppos, 8 * (size_t)pre_cap, err, errlen)) ||
+                    (rc = grow(K.calls, sizeof(CallRec) * call_cap, err, errlen)) ||
+                    (rc = grow(K.ok, call_cap, err, errlen)) ||
+                    (rc = grow(K.tiles, sizeof(ChunkState) * n_ch, err, errlen)))
                     return rc;
-                ChunkState *dcs = (ChunkState *)S->tiles.p;
-                CallRec *dcalls = (CallRec *)S->calls.p;
-                uint8_t *vis = (uint8_t *)S->vis.p;
+                ChunkState *dcs = (ChunkState *)K.tiles.p;
+                CallRec *dcalls = (CallRec *)K.calls.p;
+                uint8_t *vis = (uint8_t *)K.vis.p;
                 CK(hipMemsetAsync(n_calls, 0, 8, st));  // n_calls, n_pre
                 CK(hipMemsetAsync(vis, 0, len, st));
-                int32_t *nxt = (int32_t *)S->nxt.p;
-                PreAB *pre = (PreAB *)S->pre.p;
+                int32_t *nxt = (int32_t *)K.nxt.p;
+                PreAB *pre = (PreAB *)K.pre.p;
                 const unsigned gpre = (unsigned)((span + 255) / 256);
                 uint32_t *n_cand = n_pre + 1;
                 CK(hipMemsetAsync(n_cand, 0, 8, st));  // candidates, capped call starts
-                int64_t *cand = (int64_t *)S->prepos.p;
+                int64_t *cand = (int64_t *)K.prepos.p;
                 if (kind == 0)
                     hipLaunchKernelGGL(k_cnv_cand<0>, dim3(gpre), dim3(256), 0, st, WI, nxt, cand, n_cand, cand_cap);
                 else
@@ -1869,17 +1899,17 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 }
                 if (ncand) {
                     if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_pre<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)S->ppos.p);
+                        hipLaunchKernelGGL(k_cnv_pre<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p);
                     else
-                        hipLaunchKernelGGL(k_cnv_pre<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)S->ppos.p);
+                        hipLaunchKernelGGL(k_cnv_pre<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p);
                     CK(hipGetLastError());
                     // phases C/D for every call start, capped (the walk finishes the rest)
                     const int64_t cd_cap = 4 * L + 4 * MAX_DIST_LAST_GOOD;
                     const unsigned gpost = (unsigned)((std::min<int64_t>(ncand, pre_cap) + 255) / 256);
                     if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_post<0>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)S->ppos.p, cd_cap, n_pre + 2);
+                        hipLaunchKernelGGL(k_cnv_post<0>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
                     else
-                        hipLaunchKernelGGL(k_cnv_post<1>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)S->ppos.p, cd_cap, n_pre + 2);
+                        hipLaunchKernelGGL(k_cnv_post<1>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
                     CK(hipGetLastError());
                 }
                 const unsigned gch = (unsigned)n_ch;  // one wave per chunk
@@ -1943,9 +1973,9 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 std::vector<uint8_t> ok(nc);
                 if (nc) {
                     hipLaunchKernelGGL(k_cnv_calls_valid, dim3((nc + 255) / 256), dim3(256), 0, st, dcalls, nc, vis,
-                                       (uint8_t *)S->ok.p);
+                                       (uint8_t *)K.ok.p);
                     CK(hipMemcpyAsync(hc.data(), dcalls, sizeof(CallRec) * nc, hipMemcpyDeviceToHost, st));
-                    CK(hipMemcpyAsync(ok.data(), S->ok.p, nc, hipMemcpyDeviceToHost, st));
+                    CK(hipMemcpyAsync(ok.data(), K.ok.p, nc, hipMemcpyDeviceToHost, st));
                     CK(hipStreamSynchronize(st));
                 }
                 for (uint32_t i = 0; i < nc; i++)
@@ -1961,6 +1991,29 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 snprintf(err, errlen, "CNV window-search buffers could not be sized");
                 return GROM_E_NOMEM;
             }
+            return GROM_OK;
+        };
+        if (n_ch > 0) {
+            CK(hipEventRecord(S->walk_in, st));
+            char kerr[2][512] = {{0}, {0}};
+            int krc[2] = {GROM_OK, GROM_OK};
+            int dev = 0;
+            CK(hipGetDevice(&dev));
+            std::thread dup_thread([&] {  // a new host thread starts on device 0: select ours
+                if (hipSetDevice(dev) != hipSuccess) {
+                    snprintf(kerr[1], sizeof(kerr[1]), "hipSetDevice(%d) failed in the CNV DUP thread", dev);
+                    krc[1] = GROM_E_HIP;
+                    return;
+                }
+                krc[1] = run_kind(1, kerr[1], sizeof(kerr[1]));
+            });
+            krc[0] = run_kind(0, kerr[0], sizeof(kerr[0]));
+            dup_thread.join();
+            for (int kind = 0; kind < 2; kind++)
+                if (krc[kind] != GROM_OK) {
+                    snprintf(err, errlen, "%s", kerr[kind]);
+                    return krc[kind];
+                }
         }
         CK(hipEventRecord(S->e1, st));
         mark("walks");

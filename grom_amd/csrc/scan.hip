@@ -266,14 +266,6 @@ struct Text {
     }
 };
 
-// rows of one SNV list flush (snvfmt.cpp), appended in order
-static void snv_rows(const grom_params &P, const grom_chrom *ch, const grom_snv_cand *c, size_t n, double ave_rd,
-                     Text &out) {
-    std::vector<std::string> parts;
-    snv_rows_format(P, ch->name, c, n, round(P.snv_rd_min_factor * ave_rd), parts);
-    for (auto &s : parts) out.add(s.data(), s.size());
-}
-
 static int check_params(const grom_params &p) {
     if (p.min_snv > GROM_MAX_NAME_SLOTS) {
         set_err("-n %d exceeds the %d read-name slots the kernel keeps per base", p.min_snv, GROM_MAX_NAME_SLOTS);
@@ -485,10 +477,14 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             if (dbg_first) *dbg_first = a.eval_lo;
         }
         HIPCHK(hipStreamSynchronize(st));
-        const double t_copied = ms_since(t_start);
 
-        // SNV list with its flushes (GROM.c:11201-11326, 15063-15160)
+        // SNV list with its flushes (GROM.c:11201-11326, 15063-15160).  The flush
+        // spans and their depth averages are settled here (a mid-scan flush
+        // needs a device sum); the rows are formatted on a host thread while
+        // the indel and CNV passes below keep the GPU busy.
         Text vt{&out->vcf, &out->vcf_len, &out->vcf_cap};
+        struct FlushSeg { size_t off, n; double ave_rd; };
+        std::vector<FlushSeg> fsegs;
         const int64_t thr = std::max<int64_t>((int64_t)P.sv_list_len - 10, 1);
         size_t done = 0;
         while ((int64_t)(ncand - done) >= thr) {
@@ -504,10 +500,22 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                 HIPCHK(hipMemcpyAsync(m, d_macc, 16, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
             }
-            snv_rows(P, ch, cands + done, (size_t)thr, (double)(int64_t)m[0] / (double)(int64_t)m[1], vt);
+            fsegs.push_back({done, (size_t)thr, (double)(int64_t)m[0] / (double)(int64_t)m[1]});
             done += (size_t)thr;
         }
-        snv_rows(P, ch, cands + done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1], vt);
+        fsegs.push_back({done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1]});
+        std::string snv_text;
+        std::thread fmt([&P, ch, cands, &fsegs, &snv_text] {
+            for (const FlushSeg &f : fsegs) {
+                std::vector<std::string> parts;
+                snv_rows_format(P, ch->name, cands + f.off, f.n, round(P.snv_rd_min_factor * f.ave_rd), parts);
+                for (auto &part : parts) snv_text += part;
+            }
+        });
+        struct Joiner {
+            std::thread &t;
+            ~Joiner() { if (t.joinable()) t.join(); }
+        } fmt_join{fmt};
         const double t_snv = ms_since(t_start);
 
         // CIGAR indel evidence of the evaluated bases (row A7, GROM.c:7187-7423);
@@ -529,6 +537,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         // read-depth CNV path after the SV rows (GROM.c:16633-17300); the
         // reference runs it only when the FASTA name matched a BAM target
         CnvTiming ct{};
+        std::string cnv_text;
         if (ch->cnv && !want_dbg) {
             if (!C.cnv) C.cnv = cnv_scratch_new();
             std::string crow;
@@ -539,17 +548,24 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                 set_err("%s", cerr);
                 return rc;
             }
-            vt.add(crow.data(), crow.size());
+            cnv_text.swap(crow);
         }
+        const double t_cnv = ms_since(t_start);
+        fmt.join();
+        const double t_rows = ms_since(t_start);
+        vt.add(snv_text.data(), snv_text.size());  // SNV rows, then the CNV rows (GROM.c:16633)
+        vt.add(cnv_text.data(), cnv_text.size());
 
         if (timing)
             fprintf(stderr,
-                    "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms, rows %.3f ms (%u candidates), "
+                    "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms (%u candidates), "
                     "indel evidence %.3f ms (device %.3f ms, %lld bases), "
-                    "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows), %u of %lld tiles to the gather kernel\n",
-                    ch->name ? ch->name : "?", t_kernels, t_copied - t_kernels, t_snv - t_copied, ncand,
-                    t_indel - t_snv, ms_indel, (long long)n_indel, ms_since(t_start) - t_indel, ct.ms_device, (long long)ct.del_calls, (long long)ct.dup_calls,
-                    (long long)ct.rows, gather_only ? (unsigned)n_tiles : n_ovf_tiles, (long long)n_tiles);
+                    "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows), SNV rows (overlapped) "
+                    "joined after %.3f ms more, %u of %lld tiles to the gather kernel\n",
+                    ch->name ? ch->name : "?", t_kernels, t_snv - t_kernels, ncand, t_indel - t_snv, ms_indel,
+                    (long long)n_indel, t_cnv - t_indel, ct.ms_device, (long long)ct.del_calls,
+                    (long long)ct.dup_calls, (long long)ct.rows, t_rows - t_cnv,
+                    gather_only ? (unsigned)n_tiles : n_ovf_tiles, (long long)n_tiles);
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
         if (stats) {
