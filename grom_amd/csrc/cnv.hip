@@ -514,70 +514,128 @@ struct WinDesc {
     int64_t p0, n0, p1, n1, p2, n2;
     int64_t row;
 };
-__global__ void k_cnv_windows(const WinDesc *__restrict__ wd, int64_t n_win, const uint8_t *__restrict__ flag,
-                              const double *__restrict__ sd, int64_t L, int64_t min_len, double *__restrict__ out) {
-    int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= n_win) return;
-    const WinDesc d = wd[w];
-    double *row = out + d.row;  // out[l * n_win + row]: lanes of a wave store adjacent words
+// Window means for every length (GROM.c:18967-19018).  Each window's running
+// sums are one sequential chain in the reference's order, so one lane owns a
+// window; what made the one-lane form slow was everything else per base (two
+// f64 divisions and a store) on a grid of only ~n_win/64 waves.  Here a
+// 256-thread block owns 64 windows: wave 0 runs the 64 chains over chunks of
+// WCH bases and leaves (tot, cnt, ftot) per base in LDS; waves 1-3 turn the
+// previous chunk into means (the divisions spread over three waves) and store
+// them length-major, so each store of a wave covers 64 adjacent windows.
+constexpr int WCH = 32;
+__global__ __launch_bounds__(256) void k_cnv_windows(const WinDesc *__restrict__ wd, int64_t n_win,
+                                                     const uint8_t *__restrict__ flag, const double *__restrict__ sd,
+                                                     int64_t L, int64_t min_len, double *__restrict__ out) {
+    __shared__ double s_tot[2][WCH][64];
+    __shared__ int32_t s_cnt[2][WCH][64], s_ft[2][WCH][64];
+    __shared__ int64_t s_nmax;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t w = (int64_t)blockIdx.x * 64 + lane;
+    WinDesc d{};
+    int64_t ntot = 0;
+    if (w < n_win) {
+        d = wd[w];
+        ntot = d.n0 + d.n1 + d.n2;
+    }
+    if (threadIdx.x == 0) s_nmax = 0;
+    __syncthreads();
+    if (wave == 0) {
+        int64_t mx = ntot;
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (int64_t)__shfl_xor(mx, o, 64));
+        if (lane == 0) s_nmax = mx;
+    }
+    __syncthreads();
+    const int64_t nch = (s_nmax + WCH - 1) / WCH;
     double tot = 0.0;
-    long cnt = 0, ftot = 0, wl = 0;
-    const int64_t ps[3] = {d.p0, d.p1, d.p2}, ns[3] = {d.n0, d.n1, d.n2};
-    for (int s = 0; s < 3; s++) {
-        const int64_t pb = ps[s], n = ns[s];
-        for (int64_t k0 = 0; k0 < n; k0 += 32) {
-            // 32 loads in flight, then the sequential sum in reference order
-            uint8_t f[32];
-            double v[32];
+    int32_t cnt = 0, ftot = 0;
+    for (int64_t c = 0; c <= nch; c++) {
+        if (wave == 0 && c < nch) {
+            // the chain over bases [c*WCH, c*WCH + WCH) of this lane's window
+            uint8_t f[WCH];
+            double v[WCH];
 #pragma unroll
-            for (int j = 0; j < 32; j++) {
-                const bool ok = k0 + j < n;
-                f[j] = ok ? flag[pb + k0 + j] : (uint8_t)0xff;
-                v[j] = ok ? sd[pb + k0 + j] : 0.0;
+            for (int j = 0; j < WCH; j++) {
+                const int64_t g = c * WCH + j;
+                int64_t a = -1;
+                if (g < d.n0) a = d.p0 + g;
+                else if (g < d.n0 + d.n1) a = d.p1 + (g - d.n0);
+                else if (g < ntot) a = d.p2 + (g - d.n0 - d.n1);
+                f[j] = a >= 0 ? flag[a] : (uint8_t)0;
+                v[j] = a >= 0 ? sd[a] : 0.0;
             }
+            const int b = (int)(c & 1);
 #pragma unroll
-            for (int j = 0; j < 32; j++) {
-                if (f[j] != 0xff) {
-                    if (f[j] & F_GUARD) { tot += v[j]; cnt += 1; }
-                    ftot += (f[j] & F_LOW);
-                    wl += 1;
-                    if (wl >= min_len) {
-                        double x = __builtin_nan("");
-                        if ((ftot / (double)wl) < MAX_LOW_ACGT && cnt > 0) x = tot / (double)cnt;
-                        row[wl * n_win] = x;
-                    }
+            for (int j = 0; j < WCH; j++) {
+                if (f[j] & F_GUARD) { tot += v[j]; cnt += 1; }
+                ftot += (f[j] & F_LOW);
+                s_tot[b][j][lane] = tot;
+                s_cnt[b][j][lane] = cnt;
+                s_ft[b][j][lane] = ftot;
+            }
+        } else if (wave > 0 && c > 0) {
+            const int b = (int)((c - 1) & 1);
+            for (int j = wave - 1; j < WCH; j += 3) {
+                const int64_t g = (c - 1) * WCH + j, wl = g + 1;
+                if (g < ntot && wl >= min_len) {
+                    const int32_t cn = s_cnt[b][j][lane];
+                    double x = __builtin_nan("");
+                    if (((int64_t)s_ft[b][j][lane] / (double)wl) < MAX_LOW_ACGT && cn > 0)
+                        x = s_tot[b][j][lane] / (double)cn;
+                    out[wl * n_win + d.row] = x;
                 }
             }
         }
+        __syncthreads();
     }
 }
 
 // per window length: the sum of squared window means in window order
-// (GROM.c:19162-19170), one lane per length
-__global__ void k_cnv_window_sq(const double *__restrict__ rows, int64_t n_rows, const int64_t *__restrict__ row_len,
-                                int64_t L, int64_t min_len, double *__restrict__ tot, int64_t *__restrict__ cnt) {
-    int64_t l = min_len + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (l > L) return;
-    const double *row = rows + l * n_rows;  // this length's means, in window order
+// (GROM.c:19162-19170).  A block owns 64 lengths: all four waves stage a
+// 64-length x 64-window tile (each row segment a coalesced 512-byte load, the
+// next tile in flight while the current one is summed), and wave 0 sums its
+// lane's length over the tile in window order.
+__global__ __launch_bounds__(256) void k_cnv_window_sq(const double *__restrict__ rows, int64_t n_rows,
+                                                       const int64_t *__restrict__ row_len, int64_t L,
+                                                       int64_t min_len, double *__restrict__ tot,
+                                                       int64_t *__restrict__ cnt) {
+    __shared__ double tile[64][65];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t l0 = min_len + (int64_t)blockIdx.x * 64;
+    const int64_t n_t = (n_rows + 63) / 64;
+    double reg[16];
+    auto load = [&](int64_t t) {
+        const int64_t r = t * 64 + lane;
+        const int64_t rl = r < n_rows ? row_len[r] : -1;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int64_t l = l0 + wave * 16 + i;
+            reg[i] = (l <= L && rl >= l) ? rows[l * n_rows + r] : __builtin_nan("");
+        }
+    };
     double s = 0.0;
     int64_t c = 0;
-    for (int64_t r0 = 0; r0 < n_rows; r0 += 48) {
-        double v[48];
+    if (n_t > 0) load(0);
+    for (int64_t t = 0; t < n_t; t++) {
 #pragma unroll
-        for (int j = 0; j < 48; j++) {
-            const int64_t r = r0 + j;
-            v[j] = (r < n_rows && row_len[r] >= l) ? row[r] : __builtin_nan("");
-        }
-#pragma unroll
-        for (int j = 0; j < 48; j++) {
-            if (v[j] == v[j]) {
-                s += v[j] * v[j];
-                c += 1;
+        for (int i = 0; i < 16; i++) tile[wave * 16 + i][lane] = reg[i];
+        __syncthreads();
+        if (t + 1 < n_t) load(t + 1);
+        if (wave == 0) {
+            for (int j = 0; j < 64; j++) {
+                const double v = tile[lane][j];
+                if (v == v) {
+                    s += v * v;
+                    c += 1;
+                }
             }
         }
+        __syncthreads();
     }
-    tot[l] = s;
-    cnt[l] = c;
+    const int64_t l = l0 + lane;
+    if (wave == 0 && l <= L) {
+        tot[l] = s;
+        cnt[l] = c;
+    }
 }
 
 // ---------------- DEL / DUP window search (GROM.c:19359-20020) ----------------
@@ -1763,9 +1821,9 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         if (n_win > 0) {
             CK(hipMemcpyAsync(S->wd.p, wds.data(), sizeof(WinDesc) * n_win, hipMemcpyHostToDevice, st));
             CK(hipMemcpyAsync(S->rowlen.p, rlen.data(), 8 * n_win, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_cnv_windows, dim3((unsigned)((n_win + 63) / 64)), dim3(64), 0, st,
+            hipLaunchKernelGGL(k_cnv_windows, dim3((unsigned)((n_win + 63) / 64)), dim3(256), 0, st,
                                (const WinDesc *)S->wd.p, n_win, flag, sd, L, ML, (double *)S->rows.p);
-            hipLaunchKernelGGL(k_cnv_window_sq, dim3((unsigned)((L - ML + 1 + 63) / 64)), dim3(64), 0, st,
+            hipLaunchKernelGGL(k_cnv_window_sq, dim3((unsigned)((L - ML + 1 + 63) / 64)), dim3(256), 0, st,
                                (const double *)S->rows.p, n_win, (const int64_t *)S->rowlen.p, L, ML,
                                (double *)S->wtot.p, (int64_t *)S->wcnt.p);
             CK(hipGetLastError());
