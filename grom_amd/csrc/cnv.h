@@ -13,6 +13,13 @@ struct CnvScratch;
 CnvScratch *cnv_scratch_new();
 void cnv_scratch_free(CnvScratch *s);
 
+// Start the reference-only GC/ACGT window kernel of a chromosome on the CNV
+// path's own stream (to overlap the pileup); the next cnv_chrom with the same
+// d_ref and len waits for it instead of launching it.  The kernel starts after
+// the work already queued on `after` (the reference upload).
+int cnv_prelaunch(CnvScratch *S, hipStream_t after, const grom_params &P, const char *d_ref, int64_t len, char *err,
+                  size_t errlen);
+
 struct CnvTiming {
     double ms_device;  // device time of the CNV kernels (HIP events)
     double ms_host;    // host wall time of the whole CNV step

@@ -1246,6 +1246,10 @@ struct KindBufs {
 struct CnvScratch {
     KindBufs kb[2];
     hipEvent_t walk_in = nullptr;
+    // k_cnv_gc launched early on kb[0].st by cnv_prelaunch (overlaps the pileup)
+    hipEvent_t gc_done = nullptr;
+    const char *gc_ref = nullptr;
+    int64_t gc_len = -1, gc_m = -1;
     Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1394,6 +1398,46 @@ static int gather(CnvScratch *S, hipStream_t st, const std::vector<GatherRange> 
 
 CnvScratch *cnv_scratch_new() { return new CnvScratch(); }
 
+static int cnv_init(CnvScratch *S, char *err, size_t errlen) {
+    if (S->e0) return GROM_OK;
+    CK(hipEventCreate(&S->e0));
+    CK(hipEventCreate(&S->e1));
+    CK(hipEventCreateWithFlags(&S->walk_in, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&S->gc_done, hipEventDisableTiming));
+    for (KindBufs &K : S->kb) CK(hipStreamCreateWithFlags(&K.st, hipStreamNonBlocking));
+    return GROM_OK;
+}
+
+// GC/ACGT weights and dinucleotide classes depend on the reference alone
+// (GROM.c:1586-1881), so the scan driver starts them before the pileup on a
+// stream of their own; cnv_chrom then only waits for them.
+int cnv_prelaunch(CnvScratch *S, hipStream_t after, const grom_params &P, const char *d_ref, int64_t len, char *err,
+                  size_t errlen) {
+    int rc;
+    S->gc_ref = nullptr;
+    const int64_t m = P.insert_mean;
+    if (m < 1 || m > GC_MMAX || len <= 0) return GROM_OK;  // cnv_chrom reports it
+    if ((rc = cnv_init(S, err, errlen))) return rc;
+    if ((rc = grow(S->gcw, len, err, errlen)) || (rc = grow(S->acw, len, err, errlen)) ||
+        (rc = grow(S->rtype, len, err, errlen)))
+        return rc;
+    Args A{};  // the fields k_cnv_gc reads, as cnv_chrom sets them
+    A.len = len;
+    A.lo = m - 1;
+    A.hi = std::max<int64_t>(A.lo, len - (2 * m - 1));
+    const hipStream_t side = S->kb[0].st;
+    CK(hipEventRecord(S->gc_done, after));  // the reference may still be uploading on `after`
+    CK(hipStreamWaitEvent(side, S->gc_done, 0));
+    hipLaunchKernelGGL(k_cnv_gc, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, side, d_ref, A, (int)m,
+                       (int64_t)m * m, (uint8_t *)S->gcw.p, (uint8_t *)S->acw.p, (uint8_t *)S->rtype.p);
+    CK(hipGetLastError());
+    CK(hipEventRecord(S->gc_done, side));
+    S->gc_ref = d_ref;
+    S->gc_len = len;
+    S->gc_m = m;
+    return GROM_OK;
+}
+
 void cnv_scratch_free(CnvScratch *S) {
     if (!S) return;
     Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre,
@@ -1409,6 +1453,7 @@ void cnv_scratch_free(CnvScratch *S) {
         if (K.st) (void)hipStreamDestroy(K.st);
     }
     if (S->walk_in) (void)hipEventDestroy(S->walk_in);
+    if (S->gc_done) (void)hipEventDestroy(S->gc_done);
     if (S->e0) (void)hipEventDestroy(S->e0);
     if (S->e1) (void)hipEventDestroy(S->e1);
     delete S;
@@ -1431,12 +1476,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                  (long long)P.min_rd_window_len, (long long)P.max_rd_window_len, (long long)P.windows_sampling_factor);
         return GROM_E_ARG;
     }
-    if (!S->e0) {
-        CK(hipEventCreate(&S->e0));
-        CK(hipEventCreate(&S->e1));
-        CK(hipEventCreateWithFlags(&S->walk_in, hipEventDisableTiming));
-        for (KindBufs &K : S->kb) CK(hipStreamCreateWithFlags(&K.st, hipStreamNonBlocking));
-    }
+    if ((rc = cnv_init(S, err, errlen))) return rc;
     GlibcRand rng(seed);
     // GROM_TIMING: per-phase wall clock (syncs the stream at each mark)
     const bool tmg = getenv("GROM_TIMING") != nullptr;
@@ -1480,10 +1520,16 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     CK(hipMemsetAsync(misc, 0, 128, st));
     CK(hipMemsetAsync(S->hist.p, 0, 4 * (HIST_MAX + 1), st));
 
-    // ---- A14: weighted GC / ACGT and repeat classes ----
-    hipLaunchKernelGGL(k_cnv_gc, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, st, d_ref, A, (int)m,
-                       total_w, gcw, acw, rtype);
-    CK(hipGetLastError());
+    // ---- A14: weighted GC / ACGT and repeat classes (already running if the
+    // driver prelaunched them for this reference) ----
+    if (S->gc_ref == d_ref && S->gc_len == len && S->gc_m == m) {
+        CK(hipStreamWaitEvent(st, S->gc_done, 0));
+    } else {
+        hipLaunchKernelGGL(k_cnv_gc, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, st, d_ref, A, (int)m,
+                           total_w, gcw, acw, rtype);
+        CK(hipGetLastError());
+    }
+    S->gc_ref = nullptr;
     // ---- A15: mapq division, blocks, chromosome depth ----
     hipLaunchKernelGGL(k_cnv_blocks, dim3((unsigned)(n_blk + 1)), dim3(256), 0, st, d_ref, A, d_mq, d_rd, d_low, acw,
                        (int64_t *)S->blk.p, acc, (unsigned int *)S->hist.p);

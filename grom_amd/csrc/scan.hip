@@ -372,6 +372,15 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     unsigned long long *d_facc = (unsigned long long *)(misc + 32);
     unsigned long long *d_macc = (unsigned long long *)(misc + 64);
 
+    // the reference-only part of the CNV path runs beside the pileup
+    if (ch->cnv && !want_dbg) {
+        if (!C.cnv) C.cnv = cnv_scratch_new();
+        char cerr[512] = {0};
+        if ((rc = cnv_prelaunch(C.cnv, st, P, ch->ref, ch->len, cerr, sizeof(cerr)))) {
+            set_err("%s", cerr);
+            return rc;
+        }
+    }
     for (int attempt = 0; attempt < 2; attempt++) {
         if ((rc = ensure(C.cands, sizeof(grom_snv_cand) * (size_t)cand_cap)) ||
             (rc = ensure(C.cands2, sizeof(grom_snv_cand) * (size_t)cand_cap)))
