@@ -10,6 +10,13 @@ synthetic 100 Mb, 30x,
 GPU) every rank scans its own chromosome: chromosomes shard with no data-path
 collective, so scaling is weak and `value` is all bases scanned / max-rank time.
 
+With --inflight F (default 2) each GPU runs F scans at once: F library
+contexts on the device (grom_ctx_init), one host thread each, steps dealt
+round-robin, all K finished inside the timed region.  The pileup kernel then
+shares the GPU, so its launch time over the timed region (roofline.launch_ms)
+is longer than alone; roofline.launch_ms_alone / frac_alone give the kernel
+measured one scan at a time during warmup.
+
 The JSON line also carries
   roofline      the pileup kernel's (k_scan_tile; k_scan_scatter with
                 GROM_PILEUP=scatter) algorithmic bytes per launch / its mean
@@ -73,6 +80,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chrom-len", type=int, default=CHROM_LEN)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="chromosome scans in flight per GPU: library context slots on the same device, one host "
+                         "thread each (a genome's chromosomes are independent scans)")
     args = ap.parse_args()
 
     import torch
@@ -86,15 +96,21 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import grom_amd
-    from grom_amd.shard import max_over_ranks, timed_steps
+    from grom_amd.shard import max_over_ranks, timed_concurrent
 
     t_gen = time.perf_counter()
     batch = grom_amd.SynthBatch(args.chrom_len, COVERAGE, READ_LEN, 500.0, 50.0, seed=1000 + rank)
     t_gen = time.perf_counter() - t_gen
+    F = max(1, min(args.inflight, 8))
     dev = grom_amd.Device(local, batch.params)
+    # more contexts on the same GPU (slots local + 8k); they scan the reads uploaded once by the first
+    devs = [dev] + [grom_amd.Device(local, batch.params, slot=local + 8 * k) for k in range(1, F)]
     dchrom, dreads = dev.upload(batch.chrom, batch.reads)
+    alone_ms = []  # the pileup kernel with nothing else on the GPU (warmup, one scan at a time)
     for _ in range(args.warmup):
-        dev.scan(dchrom, dreads, device_resident=True)
+        for d in devs:
+            _, st = d.scan(dchrom, dreads, device_resident=True)
+            alone_ms.append(st.ms_pileup)
 
     def barrier():
         if world > 1:
@@ -104,19 +120,25 @@ def main():
     pile_ms = []
     tot_ms = []
     cnv_ms = []
-    out = grom_amd.Out()  # the VCF text buffer, reused across steps (grom_out)
-    last = [0]
+    outs = [grom_amd.Out() for _ in devs]  # VCF text buffers, reused across steps (grom_out)
+    last = [0] * F
 
-    def step():
-        vcf_len, st = dev.scan(dchrom, dreads, device_resident=True, out=out)
-        pile_ms.append(st.ms_pileup)
-        tot_ms.append(st.ms_total)
-        cnv_ms.append(st.ms_cnv)
-        last[0] = vcf_len
+    def step_on(k):
+        def step(i):
+            vcf_len, st = devs[k].scan(dchrom, dreads, device_resident=True, out=outs[k])
+            pile_ms.append(st.ms_pileup)
+            tot_ms.append(st.ms_total)
+            cnv_ms.append(st.ms_cnv)
+            last[k] = vcf_len
+        return step
 
-    dt = timed_steps(step, args.steps, barrier)
-    rows = ctypes.string_at(out.vcf, last[0]).count(b"\n") if last[0] else 0
-    grom_amd.lib().grom_out_free(ctypes.byref(out))
+    dt = timed_concurrent([step_on(k) for k in range(F)], args.steps, barrier)
+    texts = [ctypes.string_at(outs[k].vcf, last[k]) for k in range(F) if last[k]]
+    rows = texts[0].count(b"\n") if texts else 0
+    if any(t != texts[0] for t in texts):
+        raise RuntimeError("contexts produced different VCF text for the same chromosome")
+    for o in outs:
+        grom_amd.lib().grom_out_free(ctypes.byref(o))
     dt = max_over_ranks(dt, device="cuda")
 
     bases = args.chrom_len * world * args.steps
@@ -160,17 +182,22 @@ def main():
                 "device_ms_per_step": round(sum(tot_ms) / len(tot_ms), 3),
                 "cnv_ms_per_step": round(sum(cnv_ms) / len(cnv_ms), 3),
                 "host_generate_s": round(t_gen, 1),
+                "scans_in_flight_per_gpu": F,
             },
             "roofline": {
                 "bound": "hbm", "kernel": PILEUP_KERNEL,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "bytes_per_launch": abytes, "launch_ms": round(pile_s * 1e3, 3),
+                "launch_ms_alone": round(sum(alone_ms) / len(alone_ms), 3) if alone_ms else None,
+                "frac_alone": (round(abytes / (sum(alone_ms) / len(alone_ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                               if alone_ms else None),
             },
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    dev.close()
+    for d in reversed(devs):
+        d.close()
     batch.close()
     if world > 1:
         dist.destroy_process_group()

@@ -72,6 +72,7 @@ _SIGS = {
     "grom_last_error": (C.c_char_p, []),
     "grom_dev_init": (C.c_int, [C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
     "grom_dev_fini": (None, [C.c_int]),
+    "grom_ctx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
     "grom_scan_chrom": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Out), C.POINTER(Stats)]),
     "grom_scan_chrom_device": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Out),
                                          C.POINTER(Stats)]),
@@ -136,12 +137,15 @@ def build_tables(min_mapq: int = 20):
 class Device:
     """One initialised GPU (grom_dev_init / grom_dev_fini)."""
 
-    def __init__(self, device: int, params: Params):
-        self.device = device
+    def __init__(self, device: int, params: Params, slot: "int | None" = None):
+        """slot: the library context to use (default: the device number); a
+        second slot on the same device scans concurrently with the first."""
+        self.device = device if slot is None else slot  # the slot every call names
+        self.gpu = device
         self.params = params
         self.hez, self.mq = build_tables(params.min_mapq)
-        check(lib().grom_dev_init(device, C.byref(params), self.hez.ctypes.data, self.mq.ctypes.data),
-              "grom_dev_init")
+        check(lib().grom_ctx_init(self.device, device, C.byref(params), self.hez.ctypes.data, self.mq.ctypes.data),
+              "grom_ctx_init")
 
     def close(self):
         lib().grom_dev_fini(self.device)

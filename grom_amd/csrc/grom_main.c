@@ -248,11 +248,8 @@ typedef struct {
 
 typedef struct {
     grom_pool *pool;
-    int device;
+    int slot; /* the worker's own library context (grom_ctx_init), on some GPU */
 } grom_worker;
-
-/* one scan at a time per device (workers may share one: GROM_WORKER_DEVICES) */
-static pthread_mutex_t g_dev_mu[64] = {PTHREAD_MUTEX_INITIALIZER};
 
 static void *grom_worker_main(void *arg) {
     grom_worker *w = (grom_worker *)arg;
@@ -267,9 +264,8 @@ static void *grom_worker_main(void *arg) {
         }
         grom_job *j = &pl->jobs[pl->next_run++];
         pthread_mutex_unlock(&pl->mu);
-        pthread_mutex_lock(&g_dev_mu[w->device & 63]);
-        int rc = scan_batch(w->device, j->cp, &j->batch, pl->P, &j->text, &j->text_len, pl->verbose);
-        pthread_mutex_unlock(&g_dev_mu[w->device & 63]);
+        /* contexts are independent: workers sharing a GPU scan concurrently */
+        int rc = scan_batch(w->slot, j->cp, &j->batch, pl->P, &j->text, &j->text_len, pl->verbose);
         free(j->cp->ref);
         j->cp->ref = NULL;
         grom_batch_free(&j->batch);
@@ -393,9 +389,14 @@ int grom_cli_main(int argc, char **argv) {
         if (n_dev > avail - device) n_dev = avail - device;
         if (n_dev < 1) n_dev = 1;
     }
-    /* test hook: GROM_WORKER_DEVICES=0,0,0 runs three workers on device 0 */
-    int wdev[64], n_work = n_dev;
-    for (int d = 0; d < 64; d++) wdev[d] = device + d;
+    /* GROM_SCANS_PER_GPU (default 2) workers per GPU, each with its own
+     * context, so two chromosomes are in flight on every GPU;
+     * test hook: GROM_WORKER_DEVICES=0,0,0 runs three workers on device 0 */
+    int per_gpu = getenv("GROM_SCANS_PER_GPU") ? atoi(getenv("GROM_SCANS_PER_GPU")) : 2;
+    if (per_gpu < 1) per_gpu = 1;
+    if (per_gpu * n_dev > 64) per_gpu = 64 / n_dev;
+    int wdev[64], n_work = n_dev * per_gpu;
+    for (int d = 0; d < 64; d++) wdev[d] = device + d % n_dev;
     if (getenv("GROM_WORKER_DEVICES")) {
         char *sdup = strdup(getenv("GROM_WORKER_DEVICES")), *tok = strtok(sdup, ",");
         n_work = 0;
@@ -404,11 +405,7 @@ int grom_cli_main(int argc, char **argv) {
         if (n_work < 1) { wdev[0] = device; n_work = 1; }
     }
     int rc = GROM_OK;
-    for (int d = 0; d < n_work && !g_plan_only && rc == GROM_OK; d++) {
-        int seen = 0;
-        for (int e = 0; e < d; e++) seen |= wdev[e] == wdev[d];
-        if (!seen) rc = grom_dev_init(wdev[d], &P, hez, mq);
-    }
+    for (int d = 0; d < n_work && !g_plan_only && rc == GROM_OK; d++) rc = grom_ctx_init(d, wdev[d], &P, hez, mq);
     if (rc != GROM_OK) { fprintf(stderr, "grom: %s\n", grom_last_error()); return 1; }
 
     /* chromosome selection in BAM header order (GROM.c:20826-21050) */
@@ -473,7 +470,7 @@ int grom_cli_main(int argc, char **argv) {
     pthread_t *tids = calloc(n_work, sizeof(pthread_t));
     for (int d = 0; d < n_work; d++) {
         workers[d].pool = &pool;
-        workers[d].device = wdev[d];
+        workers[d].slot = d;
         pthread_create(&tids[d], NULL, grom_worker_main, &workers[d]);
     }
     int next_write = 0;
@@ -544,7 +541,7 @@ int grom_cli_main(int argc, char **argv) {
         if (P.vcf == 1) header(ctx, fasta_name, 1);
         fclose(ctx);
     }
-    for (int d = 0; d < n_work; d++) grom_dev_fini(wdev[d]);
+    for (int d = 0; d < n_work; d++) grom_dev_fini(d);
     grom_fasta_close(&fa);
     bam_free_header(&hdr);
     free(plan);

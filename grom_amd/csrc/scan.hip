@@ -43,7 +43,7 @@
 #define NTHR GROM_TILE_THREADS
 #define NWAVES (NTHR / 64)
 
-static char g_err[512];
+static thread_local char g_err[512];  // per host thread: contexts may run concurrently
 static void set_err(const char *fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
@@ -662,13 +662,13 @@ size_t grom_abi_struct_size(int which) {
 }
 const char *grom_last_error(void) { return g_err; }
 
-int grom_dev_init(int device, const grom_params *params, const double *hez, const double *mq) {
-    if (device < 0 || device >= 64 || !params || !hez || !mq) {
-        set_err("grom_dev_init: bad argument");
+int grom_ctx_init(int slot, int device, const grom_params *params, const double *hez, const double *mq) {
+    if (slot < 0 || slot >= 64 || device < 0 || !params || !hez || !mq) {
+        set_err("grom_ctx_init: bad argument");
         return GROM_E_ARG;
     }
-    Ctx &C = g_ctx[device];
-    if (C.init) grom_dev_fini(device);
+    Ctx &C = g_ctx[slot];
+    if (C.init) grom_dev_fini(slot);
     HIPCHK(hipSetDevice(device));
     C.device = device;
     C.prm = *params;
@@ -686,10 +686,14 @@ int grom_dev_init(int device, const grom_params *params, const double *hez, cons
     return GROM_OK;
 }
 
+int grom_dev_init(int device, const grom_params *params, const double *hez, const double *mq) {
+    return grom_ctx_init(device, device, params, hez, mq);
+}
+
 void grom_dev_fini(int device) {
     if (device < 0 || device >= 64 || !g_ctx[device].init) return;
     Ctx &C = g_ctx[device];
-    (void)hipSetDevice(device);
+    (void)hipSetDevice(C.device);
     (void)hipStreamSynchronize(C.st);
     DevBuf *all[] = {&C.r_pos, &C.r_flag, &C.r_mapq, &C.r_mtid, &C.r_mpos, &C.r_isize, &C.r_lq, &C.r_coff,
                      &C.r_cig, &C.r_boff, &C.r_seq, &C.r_qual, &C.r_nid, &C.ref, &C.keep, &C.meta, &C.cands2,
@@ -710,11 +714,12 @@ void grom_dev_fini(int device) {
     g_ctx[device] = Ctx();
 }
 
+
 int grom_scan_chrom(int device, const grom_chrom *chrom, const grom_reads *reads, grom_out *out, grom_stats *stats) {
     Ctx *C = ctx_of(device);
     if (!C) return GROM_E_NODEV;
     if (!chrom || !reads || !out || !chrom->ref) { set_err("grom_scan_chrom: null argument"); return GROM_E_ARG; }
-    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipSetDevice(C->device));
     grom_chrom dch;
     grom_reads dr;
     int rc = upload(*C, chrom, reads, &dch, &dr);
@@ -731,7 +736,7 @@ int grom_scan_chrom_device(int device, const grom_chrom *chrom, const grom_reads
         set_err("grom_scan_chrom_device: qual and seq must be 16-byte aligned");
         return GROM_E_ARG;
     }
-    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipSetDevice(C->device));
     return scan_device(*C, chrom, dev_reads, out, stats, nullptr, nullptr, 0, nullptr);
 }
 
@@ -740,7 +745,7 @@ int grom_upload(int device, const grom_chrom *chrom, const grom_reads *reads, gr
     Ctx *C = ctx_of(device);
     if (!C) return GROM_E_NODEV;
     if (!chrom || !reads || !dev_chrom || !dev_reads) { set_err("grom_upload: null argument"); return GROM_E_ARG; }
-    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipSetDevice(C->device));
     int rc = upload(*C, chrom, reads, dev_chrom, dev_reads);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(C->st));
@@ -751,7 +756,7 @@ int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *rea
                       int32_t *counts, int64_t counts_cap, int32_t *caf3) {
     Ctx *C = ctx_of(device);
     if (!C) return GROM_E_NODEV;
-    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipSetDevice(C->device));
     grom_chrom dch;
     grom_reads dr;
     int rc = upload(*C, chrom, reads, &dch, &dr);
@@ -769,7 +774,7 @@ int64_t grom_debug_indels(int device, grom_indel_rec *out, int64_t cap) {
     const int64_t n = indel_count(C->indel);
     const int64_t m = std::min<int64_t>(n, std::max<int64_t>(cap, 0));
     if (m > 0 && out) {
-        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipSetDevice(C->device));
         HIPCHK(hipMemcpy(out, indel_records(C->indel), sizeof(grom_indel_rec) * (size_t)m, hipMemcpyDeviceToHost));
     }
     return n;

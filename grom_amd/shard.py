@@ -40,6 +40,35 @@ def timed_steps(step: Callable[[], None], steps: int, barrier: Callable[[], None
     return time.perf_counter() - t0
 
 
+def timed_concurrent(steps_of: "list[Callable[[int], None]]", steps: int, barrier: Callable[[], None]) -> float:
+    """Seconds for exactly `steps` steps dealt round-robin over len(steps_of)
+    host threads (thread k runs steps k, k+F, ...; one library context each),
+    bracketed by barrier().  Any step's exception is re-raised."""
+    import threading
+    F = len(steps_of)
+    errs = []
+
+    def worker(k):
+        try:
+            for i in range(k, steps, F):
+                steps_of[k](i)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errs.append(e)
+
+    barrier()
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(F)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    barrier()
+    dt = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    return dt
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """Max of `value` over all ranks (identity without a process group)."""
     import torch

@@ -168,6 +168,13 @@ const char *grom_last_error(void);
  * (GROM_MAX_TRIALS+1)^2 doubles, row-major: g_hez_prob_binom_cdf_table and
  * g_mq_prob_binom_cdf_table, GROM.c:780-783) and the parameters. */
 int grom_dev_init(int device, const grom_params *params, const double *hez_table, const double *mq_table);
+/* A scan context in `slot` (0..63) on physical `device`.  Every entry point
+ * below takes a slot: grom_dev_init(d, ...) is grom_ctx_init(d, d, ...).
+ * Several slots may share one GPU; each has its own stream and scratch, so
+ * scans in different slots run concurrently when called from different host
+ * threads (two chromosomes in flight per GPU).  Device-resident reads from
+ * grom_upload in one slot may be scanned from another slot on the same GPU. */
+int grom_ctx_init(int slot, int device, const grom_params *params, const double *hez_table, const double *mq_table);
 void grom_dev_fini(int device);
 
 /* Scan one chromosome whose reads are in host memory; appends its VCF rows to

@@ -68,3 +68,13 @@ def test_gloo_world2_timing_is_max_over_ranks():
     # both ranks report the same max, and it covers the slow rank's 3 x 0.1 s
     assert m0 == m1 == max(dt0, dt1)
     assert m0 >= 0.3
+
+
+def test_timed_concurrent_runs_every_step_once():
+    from grom_amd.shard import timed_concurrent
+    seen = []
+    fns = [lambda i, k=k: seen.append((k, i)) for k in range(3)]
+    dt = timed_concurrent(fns, 8, lambda: None)
+    assert dt >= 0
+    assert sorted(i for _, i in seen) == list(range(8))
+    assert all(i % 3 == k for k, i in seen)
