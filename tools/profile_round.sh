@@ -11,6 +11,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $out/bench_trace.log 2>&1 || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $c -d $out/pmc_$c -o run -- \
-        python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $out/pmc_$c.log 2>&1 || exit $?
+        python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --inflight 1 > $out/pmc_$c.log 2>&1 || exit $?
 done
 find $out -name "*.csv" | head -50
