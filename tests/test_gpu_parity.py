@@ -144,3 +144,35 @@ def test_sharded_cli_matches_one_gpu(datadir, workers, extra):
     rc = grom_amd.cli_main(["-i", bam, "-r", fa, "-o", f"g_{tag}.vcf", "-P", "8"] + extra, env=env, cwd=str(datadir))
     assert rc == 0, grom_amd.last_error()
     assert open(datadir / f"o_{tag}.vcf").read() == open(datadir / f"g_{tag}.vcf").read()
+
+
+def test_two_contexts_scan_concurrently():
+    """Two library contexts on one GPU (grom_ctx_init; bench's --inflight 2)
+    scanning the same device-resident chromosome from two host threads give
+    the text of a lone scan."""
+    import threading
+
+    import grom_amd
+    b = grom_amd.SynthBatch(400_000, seed=23)
+    d0 = grom_amd.Device(0, b.params)
+    d1 = grom_amd.Device(0, b.params, slot=8)
+    try:
+        dc, dr = d0.upload(b.chrom, b.reads)
+        want, _ = d0.scan(dc, dr, device_resident=True)
+        assert want.count("\n") > 50
+        got = {0: [], 1: []}
+
+        def run(k, dev):
+            for _ in range(3):
+                got[k].append(dev.scan(dc, dr, device_resident=True)[0])
+
+        ts = [threading.Thread(target=run, args=(k, d)) for k, d in ((0, d0), (1, d1))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert got[0] == [want] * 3 and got[1] == [want] * 3
+    finally:
+        d1.close()
+        d0.close()
+        b.close()
