@@ -70,6 +70,8 @@ _SIGS = {
     "grom_abi_struct_size": (C.c_size_t, [C.c_int]),
     "grom_device_count": (C.c_int, []),
     "grom_last_error": (C.c_char_p, []),
+    "grom_set_last_error": (None, [C.c_char_p]),
+    "grom_device_mem_free": (C.c_int64, [C.c_int]),
     "grom_dev_init": (C.c_int, [C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
     "grom_dev_fini": (None, [C.c_int]),
     "grom_ctx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),

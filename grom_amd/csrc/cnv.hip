@@ -31,10 +31,10 @@
 //
 // Exactness: every double the VCF depends on is produced with the reference's
 // operation order (sequential sums stay sequential, one lane each; this file
-// is compiled with -ffp-contract=off so no multiply-add is fused).  The one
-// order-dependent sum computed differently is the chromosome depth variance
-// of GROM.c:16664-16677; it only feeds the repeat-bias comparison
-// (GROM.c:16765) and is summed from an exact depth histogram.
+// is compiled with -ffp-contract=off so no multiply-add is fused).  The
+// chromosome depth variance of GROM.c:16664-16677 only feeds the repeat-bias
+// comparison (GROM.c:16765): it is bounded from an exact depth histogram, and
+// redone in base order on the host when the bound cannot decide.
 
 #include <hip/hip_runtime.h>
 
@@ -1557,21 +1557,11 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     if (hnrep) CK(hipMemcpy(reps.data(), S->rep.p, sizeof(RepeatRec) * hnrep, hipMemcpyDeviceToHost));
     std::sort(reps.begin(), reps.end(), [](const RepeatRec &a, const RepeatRec &b) { return a.start < b.start; });
 
-    // chromosome depth mean / stdev over ACGT-rich bases, GROM.c:16645-16684
-    double chr_ave = 0, chr_sd = 0;
+    // chromosome depth mean over ACGT-rich bases, GROM.c:16645-16660: a double
+    // sum of integers below 2^53, so the exact integer total is the same value
+    double chr_ave = 0;
     const long chr_cnt = (long)hacc[3];
     if (chr_cnt > 0) chr_ave = (double)hacc[2] / chr_cnt;
-    if (hist[HIST_MAX] != 0 && 2 * chr_ave > HIST_MAX) {
-        snprintf(err, errlen, "read depth above %d: outside the CNV histogram", HIST_MAX);
-        return GROM_E_ARG;
-    }
-    for (int v = 0; v < HIST_MAX; v++) {
-        if (!hist[v]) continue;
-        double term = (v < 2 * chr_ave) ? (v - chr_ave) * (v - chr_ave) : chr_ave * chr_ave;
-        chr_sd += term * hist[v];
-    }
-    chr_sd += (double)hist[HIST_MAX] * chr_ave * chr_ave;
-    chr_sd = chr_cnt > 1 ? sqrt(chr_sd / ((double)chr_cnt - 1.0)) : 0;
     // repeat-type depth and the most biased repeat, GROM.c:16686-16775
     double rave[10] = {0}, rsd[10] = {0};
     long rcnt[10] = {0};
@@ -1588,14 +1578,66 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         rsd[t] += (v - rave[t]) * (v - rave[t]);
     }
     for (int t = 0; t < 10; t++) rsd[t] = rcnt[t] > 1 ? sqrt(rsd[t] / ((double)rcnt[t] - 1.0)) : 0;
+    // The chromosome depth stdev (GROM.c:16664-16685) is a sequential double
+    // sum in base order, and it only feeds the comparison below.  The terms
+    // are the reference's own doubles; only their summation order differs, so
+    // the reference's sum lies within gamma(n) = n*u/(1-n*u) (relative) of the
+    // exact sum of the histogram's terms.  When every comparison comes out the
+    // same at both ends of that interval it is decided; otherwise (or when the
+    // depth histogram cannot hold twice the mean) the sum is redone on the host
+    // in base order.
+    auto biased_for = [&](double sd) {
+        int b = -1;
+        long bc = 0;
+        for (int t = 0; t < 10; t++)
+            if (rcnt[t] > NO_COMBINE && (rave[t] + (P.min_repeat_stdev * rsd[t])) < chr_ave &&
+                (chr_ave - (P.min_repeat_stdev * sd)) > rave[t] && rcnt[t] > bc) {
+                b = t;
+                bc = rcnt[t];
+            }
+        return b;
+    };
     int biased = -1;
-    long biased_cnt = 0;
-    for (int t = 0; t < 10; t++)
-        if (rcnt[t] > NO_COMBINE && (rave[t] + (P.min_repeat_stdev * rsd[t])) < chr_ave &&
-            (chr_ave - (P.min_repeat_stdev * chr_sd)) > rave[t] && rcnt[t] > biased_cnt) {
-            biased = t;
-            biased_cnt = rcnt[t];
+    bool decided = false;
+    if (chr_cnt <= 1) {
+        biased = biased_for(0.0);
+        decided = true;
+    } else if (!(2 * chr_ave >= HIST_MAX) && !getenv("GROM_CNV_SERIAL_SD")) {
+        long double s = 0;
+        for (int v = 0; v < HIST_MAX; v++) {
+            if (!hist[v]) continue;
+            double term = (v < 2 * chr_ave) ? (v - chr_ave) * (v - chr_ave) : chr_ave * chr_ave;
+            s += (long double)term * hist[v];
         }
+        s += (long double)hist[HIST_MAX] * (long double)(chr_ave * chr_ave);
+        const long double nu = (long double)chr_cnt * 0x1p-53L;
+        const long double g = nu / (1.0L - nu) + 1e-15L;  // + histogram rounding and sqrt/div ulps
+        const double sd_lo = (double)sqrtl(s * (1.0L - g) / ((long double)chr_cnt - 1.0L));
+        const double sd_hi = (double)sqrtl(s * (1.0L + g) / ((long double)chr_cnt - 1.0L));
+        const int b_lo = biased_for(nextafter(sd_lo, 0.0)), b_hi = biased_for(nextafter(sd_hi, INFINITY));
+        if (b_lo == b_hi) {
+            biased = b_lo;
+            decided = true;
+        }
+    }
+    if (!decided) {
+        const int64_t n = A.hi - A.lo;
+        std::vector<int32_t> hrd(n), hlow(n);
+        std::vector<uint8_t> hacw(n);
+        CK(hipMemcpyAsync(hrd.data(), d_rd + A.lo, 4 * n, hipMemcpyDeviceToHost, st));
+        CK(hipMemcpyAsync(hlow.data(), d_low + A.lo, 4 * n, hipMemcpyDeviceToHost, st));
+        CK(hipMemcpyAsync(hacw.data(), acw + A.lo, n, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        double sd = 0;
+        for (int64_t i = 0; i < n; i++) {
+            if (hacw[i] < MIN_ACGT) continue;
+            const int r = hrd[i] + hlow[i];
+            if (r < 2 * chr_ave) sd += (r - chr_ave) * (r - chr_ave);
+            else sd += chr_ave * chr_ave;
+        }
+        sd = sqrt(sd / ((double)chr_cnt - 1.0));
+        biased = biased_for(sd);
+    }
     // 10 kb blocks over twice the mean depth -> low-variance sample blocks, GROM.c:16784-16993
     const double chr_rd_ave = (double)hacc[0] / (double)hacc[1];
     const double chr_rd_thr = P.chr_rd_threshold_factor * chr_rd_ave;

@@ -235,6 +235,7 @@ typedef struct {
     char *text;
     size_t text_len;
     int rc, ready, done;
+    char err[512]; /* the worker's grom_last_error() when rc != GROM_OK */
 } grom_job;
 
 typedef struct {
@@ -266,6 +267,7 @@ static void *grom_worker_main(void *arg) {
         pthread_mutex_unlock(&pl->mu);
         /* contexts are independent: workers sharing a GPU scan concurrently */
         int rc = scan_batch(w->slot, j->cp, &j->batch, pl->P, &j->text, &j->text_len, pl->verbose);
+        if (rc != GROM_OK) snprintf(j->err, sizeof(j->err), "%s: %s", j->cp->name, grom_last_error());
         free(j->cp->ref);
         j->cp->ref = NULL;
         grom_batch_free(&j->batch);
@@ -393,8 +395,26 @@ int grom_cli_main(int argc, char **argv) {
      * context, so two chromosomes are in flight on every GPU;
      * test hook: GROM_WORKER_DEVICES=0,0,0 runs three workers on device 0 */
     int per_gpu = getenv("GROM_SCANS_PER_GPU") ? atoi(getenv("GROM_SCANS_PER_GPU")) : 2;
+    if (n_dev > 64) n_dev = 64;
     if (per_gpu < 1) per_gpu = 1;
     if (per_gpu * n_dev > 64) per_gpu = 64 / n_dev;
+    if (per_gpu < 1) per_gpu = 1;
+    /* a second context per GPU doubles the scan's device buffers: keep it
+     * only when the free HBM holds per_gpu scans of the longest chromosome
+     * (about 64 B per base at 30x) */
+    if (per_gpu > 1 && !g_plan_only) {
+        long longest = 0;
+        for (int i = 0; i < fa.n; i++)
+            if (fa.len[i] > longest) longest = fa.len[i];
+        const double need = 64.0 * (double)longest;
+        for (int d = 0; d < n_dev; d++) {
+            int64_t fr = grom_device_mem_free(device + d);
+            if (fr >= 0 && (double)fr < need * per_gpu) {
+                int fit = (int)((double)fr / need);
+                per_gpu = fit < 1 ? 1 : (fit < per_gpu ? fit : per_gpu);
+            }
+        }
+    }
     int wdev[64], n_work = n_dev * per_gpu;
     for (int d = 0; d < 64; d++) wdev[d] = device + d % n_dev;
     if (getenv("GROM_WORKER_DEVICES")) {
@@ -404,9 +424,17 @@ int grom_cli_main(int argc, char **argv) {
         free(sdup);
         if (n_work < 1) { wdev[0] = device; n_work = 1; }
     }
-    int rc = GROM_OK;
-    for (int d = 0; d < n_work && !g_plan_only && rc == GROM_OK; d++) rc = grom_ctx_init(d, wdev[d], &P, hez, mq);
-    if (rc != GROM_OK) { fprintf(stderr, "grom: %s\n", grom_last_error()); return 1; }
+    int rc = GROM_OK, n_init = 0;
+    for (int d = 0; d < n_work && !g_plan_only && rc == GROM_OK; d++) {
+        rc = grom_ctx_init(d, wdev[d], &P, hez, mq);
+        if (rc == GROM_OK) n_init = d + 1;
+    }
+    #define CLI_FAIL()                                                                             \
+        do {                                                                                       \
+            for (int d_ = 0; d_ < n_init; d_++) grom_dev_fini(d_);                                 \
+            return 1;                                                                              \
+        } while (0)
+    if (rc != GROM_OK) { fprintf(stderr, "grom: %s\n", grom_last_error()); CLI_FAIL(); }
 
     /* chromosome selection in BAM header order (GROM.c:20826-21050) */
     const int32_t s0 = P.one_base_rd_len / 4 + 1;
@@ -437,7 +465,7 @@ int grom_cli_main(int argc, char **argv) {
     }
 
     FILE *vcf = fopen(out_name, "w");
-    if (!vcf) { printf("Error opening file %s\n", out_name); return 1; }
+    if (!vcf) { printf("Error opening file %s\n", out_name); CLI_FAIL(); }
     if (P.vcf == 1) header(vcf, fasta_name, 0);
     char ctx_name[4096];
     size_t ol = strlen(out_name);
@@ -449,7 +477,7 @@ int grom_cli_main(int argc, char **argv) {
     /* one serial pass over the records, split per chromosome (stream.h);
      * finished chromosomes go to the GPU workers, rows are written in order */
     bam_free_header(&hdr);
-    if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) return 1;
+    if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) { fclose(vcf); CLI_FAIL(); }
     grom_planner pl;
     grom_planner_init(&pl, order, n_plan);
     grom_batch batch;
@@ -474,8 +502,9 @@ int grom_cli_main(int argc, char **argv) {
         pthread_create(&tids[d], NULL, grom_worker_main, &workers[d]);
     }
     int next_write = 0;
-    /* hand chromosome `cur` (its batch complete) to the workers; keep at most
-     * 2 x n_dev chromosomes in host memory, writing finished rows in order */
+    /* hand chromosome `cur` (its batch complete) to the workers; at most one
+     * decoded chromosome waits beyond those being scanned (n_work + 1 batches
+     * in host memory), finished rows are written in order */
     #define SUBMIT_CUR()                                                                           \
         do {                                                                                       \
             plan[cur].ref = malloc(plan[cur].len + 1);                                             \
@@ -495,7 +524,7 @@ int grom_cli_main(int argc, char **argv) {
                     j->text = NULL;                                                                \
                     pthread_mutex_lock(&pool.mu);                                                  \
                 }                                                                                  \
-                if (cur + 1 - next_write < 2 * n_work) break;                                       \
+                if (cur + 1 - next_write < n_work + 1) break;                                      \
                 pthread_cond_wait(&pool.cv, &pool.mu);                                             \
             }                                                                                      \
             pthread_mutex_unlock(&pool.mu);                                                        \
@@ -526,6 +555,8 @@ int grom_cli_main(int argc, char **argv) {
     }
     pthread_mutex_unlock(&pool.mu);
     for (int d = 0; d < n_work; d++) pthread_join(tids[d], NULL);
+    for (int j = 0; j < n_plan; j++)
+        if (pool.jobs[j].rc != GROM_OK) { grom_set_last_error(pool.jobs[j].err); break; }
     free(tids);
     free(workers);
     free(pool.jobs);
@@ -541,7 +572,8 @@ int grom_cli_main(int argc, char **argv) {
         if (P.vcf == 1) header(ctx, fasta_name, 1);
         fclose(ctx);
     }
-    for (int d = 0; d < n_work; d++) grom_dev_fini(d);
+    for (int d = 0; d < n_init; d++) grom_dev_fini(d);
+    #undef CLI_FAIL
     grom_fasta_close(&fa);
     bam_free_header(&hdr);
     free(plan);

@@ -661,6 +661,12 @@ size_t grom_abi_struct_size(int which) {
     }
 }
 const char *grom_last_error(void) { return g_err; }
+void grom_set_last_error(const char *msg) { set_err("%s", msg ? msg : ""); }
+int64_t grom_device_mem_free(int device) {
+    size_t fr = 0, tot = 0;
+    if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&fr, &tot) != hipSuccess) return -1;
+    return (int64_t)fr;
+}
 
 int grom_ctx_init(int slot, int device, const grom_params *params, const double *hez, const double *mq) {
     if (slot < 0 || slot >= 64 || device < 0 || !params || !hez || !mq) {

@@ -162,7 +162,16 @@ int grom_device_count(void);
  * 0 grom_params, 1 grom_chrom, 2 grom_reads, 3 grom_out, 4 grom_stats,
  * 5 grom_indel_rec */
 size_t grom_abi_struct_size(int which);
+/* The message of the last failing call made FROM THE CALLING HOST THREAD
+ * (errors are kept per thread, since contexts run concurrently).
+ * grom_cli_main copies the first failing worker's message into the caller's
+ * thread before it returns. */
 const char *grom_last_error(void);
+/* Set the calling thread's error text (used by the CLI to hand a worker's
+ * failure to its caller). */
+void grom_set_last_error(const char *msg);
+/* Free device memory in bytes (hipMemGetInfo), or -1. */
+int64_t grom_device_mem_free(int device);
 
 /* Initialise `device`: upload the two binomial tables (each
  * (GROM_MAX_TRIALS+1)^2 doubles, row-major: g_hez_prob_binom_cdf_table and

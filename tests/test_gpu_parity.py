@@ -114,6 +114,22 @@ def test_cnv_rows_bit_exact(datadir, case, extra):
     assert ov == gv
 
 
+@pytest.mark.parametrize("case,extra", [("cnv", ["-V", "1"]), ("cnv_multi", ["-V", "1", "-p", "3"])],
+                         ids=["cnv_V1", "cnv_multi_V1_p3"])
+def test_cnv_serial_stdev_path(datadir, case, extra):
+    """The chromosome depth stdev (GROM.c:16664-16685) decided from the
+    histogram bound and redone in base order on the host (GROM_CNV_SERIAL_SD
+    forces the host path; it also runs whenever the bound cannot decide or the
+    depth exceeds the histogram) give the oracle's rows."""
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"serialsd_{case}"
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, env_extra={"GROM_CNV_SERIAL_SD": "1"})
+    ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"g_{tag}.vcf").read()
+    assert ov.count("<DEL>") + ov.count("<DUP>") > 0
+    assert ov == gv
+
+
 def test_device_resident_path_matches_host_path():
     import grom_amd
     b = grom_amd.SynthBatch(300_000, seed=21)
