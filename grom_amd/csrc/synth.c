@@ -77,6 +77,8 @@ void synth_default_cfg(synth_cfg *c) {
     c->multi_indel = 0.0;
     c->cnv_min = 10000;
     c->cnv_max = 300000;
+    c->sv_per_mb = 0.0;
+    c->sv_evidence = 0.5;
     c->seed = 2;
 }
 
@@ -383,6 +385,323 @@ static int synth_cnv_regions(const synth_cfg *c, int ci, cnv_reg **out) {
     return m;
 }
 
+/* ---------------- breakpoint SVs (alignment-level model) ----------------
+ * Each SV is simulated as the alignments an aligner would report around its
+ * breakpoints, on top of the normal reference-like coverage: discordant
+ * pairs (orientation and insert size of the rearranged donor), split reads
+ * with SA:Z tags, soft-clipped reads and unmapped mates.  Read sequence is
+ * the reference at the mapped bases (no mismatches), quality hi_q.  Events
+ * are drawn genome-wide from their own stream, so both sides of a
+ * translocation are generated consistently by the two chromosomes' passes. */
+enum { SV_DEL, SV_DUP, SV_INV, SV_INS, SV_CTX, SV_NTYPES };
+typedef struct { int type, chr, chr2; long s, e, y; uint64_t id; } sv_event;
+
+static int synth_sv_events(const synth_cfg *c, sv_event **out) {
+    *out = NULL;
+    if (c->sv_per_mb <= 0) return 0;
+    int cap = 64, n = 0;
+    sv_event *ev = (sv_event *)malloc(sizeof(sv_event) * cap);
+    for (int ci = 0; ci < c->n_chr; ci++) {
+        long len = c->chr_len[ci];
+        int k = (int)(c->sv_per_mb * (double)len / 1e6 + 0.5);
+        if (k <= 0) continue;
+        xrng g;
+        xseed(&g, c->seed, (uint64_t)ci + 1, 11);
+        long span = len / k;
+        for (int i = 0; i < k; i++) {
+            long lo = (long)i * span + c->telomere_n + 4000, hi = (long)(i + 1) * span - c->telomere_n - 4000;
+            int type = (int)xint(&g, SV_NTYPES);
+            if (type == SV_CTX && c->n_chr < 2) type = SV_DEL;
+            long L;
+            switch (type) {
+            case SV_DEL: L = xunif(&g) < 0.5 ? 40 + xint(&g, 120) : 300 + xint(&g, 3000); break;
+            case SV_DUP: L = 200 + xint(&g, 3000); break;
+            case SV_INV: L = 600 + xint(&g, 4000); break;
+            case SV_INS: L = 150 + xint(&g, 300); break; /* inserted length (novel sequence) */
+            default: L = 1;
+            }
+            if (hi - lo <= L + 2) continue;
+            long st = lo + xint(&g, hi - lo - (type == SV_INS || type == SV_CTX ? 1 : L));
+            if (n == cap) { cap *= 2; ev = (sv_event *)realloc(ev, sizeof(sv_event) * cap); }
+            sv_event *e = &ev[n++];
+            e->type = type;
+            e->chr = ci;
+            e->s = st;
+            e->e = (type == SV_INS || type == SV_CTX) ? st : st + L;
+            e->chr2 = -1;
+            e->y = L; /* INS: inserted length */
+            if (type == SV_CTX) {
+                e->chr2 = (ci + 1) % c->n_chr;
+                long l2 = c->chr_len[e->chr2];
+                e->y = c->telomere_n + 4000 + xint(&g, l2 - 2 * (c->telomere_n + 4000));
+            }
+            e->id = ((uint64_t)ci << 32) | (uint64_t)i;
+        }
+    }
+    *out = ev;
+    return n;
+}
+
+typedef struct {
+    const synth_cfg *c;
+    int ci;
+    const char *ref;
+    long len;
+    rheap *heap;
+    uint64_t *order;
+    long n;
+} sv_out;
+
+/* one alignment: ops (op,len) pairs; SEQ is the reference under M ops */
+static void sv_emit(sv_out *o, const char *name, long pos, const int *ops, int n_ops, int flag, int mapq, int mtid,
+                    long mpos, long isize, const char *sa) {
+    const synth_cfg *c = o->c;
+    int L = c->read_len;
+    if (pos < 0 || pos + L >= o->len) return;
+    aln a;
+    a.n_cigar = 0;
+    a.len = L;
+    long rp = pos;
+    int q = 0;
+    for (int k = 0; k < n_ops; k++) {
+        int op = ops[2 * k], ln = ops[2 * k + 1];
+        push_op(&a, op, ln);
+        for (int j = 0; j < ln && q < L; j++) {
+            char b;
+            if (op == GC_MATCH) b = o->ref[rp++];
+            else b = o->ref[(pos + L + 7 * q) % o->len]; /* clipped bases: some other sequence */
+            if (b >= 'a' && b <= 'z') b = (char)(b - 32);
+            a.seq[q] = b;
+            a.qual[q] = (uint8_t)c->hi_q;
+            q++;
+        }
+    }
+    a.pos = (int32_t)pos;
+    a.ref_end = (int32_t)rp;
+    hent e;
+    memset(&e, 0, sizeof(e));
+    fill_rec(&e.rec, name, o->ci, &a, 1, flag, mapq, mtid, (int)mpos, (int)isize, 0);
+    if (sa) {
+        /* append SA:Z:<sa> (GROM parses it when the record's aux is 1..99 bytes) */
+        int sl = (int)strlen(sa) + 1;
+        e.rec.data = (uint8_t *)realloc(e.rec.data, e.rec.data_len + 3 + sl);
+        uint8_t *p = e.rec.data + e.rec.data_len;
+        p[0] = 'S'; p[1] = 'A'; p[2] = 'Z';
+        memcpy(p + 3, sa, sl);
+        e.rec.data_len += 3 + sl;
+        e.rec.m_data = e.rec.data_len;
+    }
+    e.pos = e.rec.pos;
+    e.order = (*o->order)++;
+    hpush(o->heap, e);
+    o->n++;
+}
+
+/* a read-pair: (pos1, flag1) on this chromosome, its mate at mpos; isize
+ * from the reference span (positive for the leftmost read) */
+static long sv_isize(long p1, long p2, int L, int first) {
+    long lo = p1 < p2 ? p1 : p2, hi = (p1 > p2 ? p1 : p2) + L;
+    long v = hi - lo;
+    return first ? v : -v;
+}
+
+static int sv_mapq(const synth_cfg *c, xrng *r) { return xunif(r) < c->lowmapq_frac ? (int)xint(r, 20) : 60; }
+
+static void sv_pair(sv_out *o, xrng *r, const char *name, long p1, int rev1, long p2, int rev2) {
+    int L = o->c->read_len;
+    int f1 = GF_PAIRED | GF_READ1 | (rev1 ? GF_REVERSE : 0) | (rev2 ? GF_MREVERSE : 0);
+    int f2 = GF_PAIRED | GF_READ2 | (rev2 ? GF_REVERSE : 0) | (rev1 ? GF_MREVERSE : 0);
+    int m = GC_MATCH;
+    int ops[2] = {m, L};
+    int q1 = sv_mapq(o->c, r), q2 = sv_mapq(o->c, r);
+    sv_emit(o, name, p1, ops, 1, f1, q1, o->ci, p2, sv_isize(p1, p2, L, p1 <= p2), NULL);
+    sv_emit(o, name, p2, ops, 1, f2, q2, o->ci, p1, sv_isize(p1, p2, L, p2 < p1), NULL);
+}
+
+/* a split read: k bases at ref a (then clipped), the other L-k at ref b
+ * (after a clip); the longer part is the primary alignment, the other one
+ * its SA:Z entry; `rev` strand for both parts (sa_rev flips the SA strand). */
+static void sv_split(sv_out *o, xrng *r, const char *name, long a, long b, int k, int rev, int sa_rev, long mpos,
+                     int mrev, int flag_mate_unmapped) {
+    int L = o->c->read_len;
+    char sa[96];
+    int ops[4];
+    long pos;
+    const char *cn = o->c->chr_name[o->ci];
+    if (k >= L - k) {
+        pos = a;
+        ops[0] = GC_MATCH; ops[1] = k; ops[2] = GC_SOFT_CLIP; ops[3] = L - k;
+        snprintf(sa, sizeof(sa), "%s,%ld,%c,%dS%dM,60,0;", cn, b + 1, (rev ^ sa_rev) ? '-' : '+', k, L - k);
+    } else {
+        pos = b;
+        ops[0] = GC_SOFT_CLIP; ops[1] = k; ops[2] = GC_MATCH; ops[3] = L - k;
+        snprintf(sa, sizeof(sa), "%s,%ld,%c,%dM%dS,60,0;", cn, a + 1, (rev ^ sa_rev) ? '-' : '+', k, L - k);
+    }
+    int flag = GF_PAIRED | GF_READ1 | (rev ? GF_REVERSE : 0);
+    if (flag_mate_unmapped) flag |= GF_MUNMAP;
+    else if (mrev) flag |= GF_MREVERSE;
+    long isz = flag_mate_unmapped ? 0 : sv_isize(pos, mpos, L, pos <= mpos);
+    sv_emit(o, name, pos, ops, 2, flag, sv_mapq(o->c, r), o->ci, flag_mate_unmapped ? pos : mpos, isz, sa);
+    if (!flag_mate_unmapped) {
+        int m_ops[2] = {GC_MATCH, L};
+        int mf = GF_PAIRED | GF_READ2 | (mrev ? GF_REVERSE : 0) | (rev ? GF_MREVERSE : 0);
+        sv_emit(o, name, mpos, m_ops, 1, mf, sv_mapq(o->c, r), o->ci, pos, sv_isize(pos, mpos, L, mpos < pos), NULL);
+    }
+}
+
+/* every record chromosome ci contributes to the SV events */
+static long synth_sv_records(const synth_cfg *c, int ci, const char *ref, rheap *heap, uint64_t *order) {
+    sv_event *ev;
+    int n_ev = synth_sv_events(c, &ev);
+    sv_out o = {c, ci, ref, c->chr_len[ci], heap, order, 0};
+    const int L = c->read_len;
+    const double cov = c->chr_cov[ci] >= 0 ? c->chr_cov[ci] : c->coverage;
+    const int ins = (int)c->insert_mean;
+    /* spanning fragments over one breakpoint: depth x insert / (2 L), scaled */
+    int npair = (int)(cov * (double)(ins - L) / (2.0 * L) * c->sv_evidence + 0.5);
+    int nsplit = (int)(cov * 0.5 * c->sv_evidence + 0.5);
+    if (npair < 1) npair = 1;
+    char name[64];
+    for (int k = 0; k < n_ev; k++) {
+        const sv_event *e = &ev[k];
+        if (e->chr != ci && e->chr2 != ci) continue;
+        xrng r;
+        xseed(&r, c->seed, e->id + 1000003ULL, 13);
+        const long s = e->s, en = e->e;
+        int f = 0;
+#define NAME() snprintf(name, sizeof(name), "SV%02d:%06d:%04d", e->chr, k, f++)
+        switch (e->type) {
+        case SV_DEL:
+            for (int j = 0; j < npair; j++) {
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                long a = s - L - xint(&r, fi > 2 * L ? fi - 2 * L : 1);
+                long b = en + (fi - (s - a)) - L;
+                if (b < en) b = en;
+                NAME();
+                sv_pair(&o, &r, name, a, 0, b, 1);
+            }
+            for (int j = 0; j < nsplit; j++) {
+                int kk = 30 + (int)xint(&r, L - 60);
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                NAME();
+                if (j & 1) {
+                    /* F read over the junction, its R mate downstream in the donor */
+                    long mp = en + (fi - kk) - L;
+                    sv_split(&o, &r, name, s - kk, en, kk, 0, 0, mp, 1, 0);
+                } else {
+                    /* R read over the junction, its F mate upstream */
+                    long mp = s - kk - (fi - L);
+                    sv_split(&o, &r, name, s - kk, en, kk, 1, 0, mp, 0, 0);
+                }
+            }
+            break;
+        case SV_DUP:
+            for (int j = 0; j < npair; j++) {
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                long a = en - L - xint(&r, fi > 2 * L ? fi - 2 * L : 1);
+                long b = s + (fi - (en - a)) - L;
+                if (b < s) b = s;
+                NAME();
+                sv_pair(&o, &r, name, a, 0, b, 1); /* F at the dup end, R mate near its start */
+            }
+            for (int j = 0; j < nsplit; j++) {
+                int kk = 30 + (int)xint(&r, L - 60);
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                NAME();
+                if (j & 1) {
+                    /* F read: k bases before the dup end, then its start; R mate downstream of the start */
+                    long mp = s + (fi - kk) - L;
+                    sv_split(&o, &r, name, en - kk, s, kk, 0, 0, mp, 1, 0);
+                } else {
+                    /* R read over the junction, its F mate upstream (before the dup end) */
+                    long mp = en - kk - (fi - L);
+                    sv_split(&o, &r, name, en - kk, s, kk, 1, 0, mp, 0, 0);
+                }
+            }
+            break;
+        case SV_INV:
+            for (int j = 0; j < npair; j++) {
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                /* junction at s: F outside, the mate reads the inverted segment forward */
+                long a = s - L - xint(&r, fi > 2 * L ? fi - 2 * L : 1);
+                long t = fi - L - (s - a);
+                if (t < 0) t = 0;
+                NAME();
+                sv_pair(&o, &r, name, a, 0, en - t - L, 0);
+                /* junction at e: both reverse */
+                fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                long u = (en - s) - L - xint(&r, fi > 2 * L ? fi - 2 * L : 1);
+                if (u < 0) u = 0;
+                long p1 = en - u - L, p2 = s + u + fi - L;
+                if (p2 < en) p2 = en;
+                NAME();
+                sv_pair(&o, &r, name, p1, 1, p2, 1);
+            }
+            for (int j = 0; j < nsplit; j++) {
+                int kk = 30 + (int)xint(&r, L - 60);
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                NAME();
+                /* the inverted part aligns on the other strand */
+                sv_split(&o, &r, name, s - kk, en - (L - kk), kk, 0, 1, s - kk + fi - L, 1, 0);
+            }
+            break;
+        case SV_INS: {
+            const long I = e->y;
+            for (int j = 0; j < npair; j++) {
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                long a = s - L - xint(&r, 40);
+                long b = s + (fi - I - (s - a)) - L + L / 2;
+                if (b < s + 1) b = s + 1;
+                NAME();
+                if (j % 3 == 2) {
+                    /* the mate lies inside the insertion: unmapped */
+                    int ops[2] = {GC_MATCH, L};
+                    sv_emit(&o, name, a, ops, 1, GF_PAIRED | GF_READ1 | GF_MUNMAP, sv_mapq(c, &r), ci, a, 0, NULL);
+                } else {
+                    sv_pair(&o, &r, name, a, 0, b, 1);
+                }
+                /* reads clipped at the insertion point */
+                int kk = 10 + (int)xint(&r, 60);
+                int ops1[4] = {GC_MATCH, L - kk, GC_SOFT_CLIP, kk};
+                NAME();
+                sv_emit(&o, name, s + 1 - (L - kk), ops1, 2, 0, sv_mapq(c, &r), -1, -1, 0, NULL);
+                int ops2[4] = {GC_SOFT_CLIP, kk, GC_MATCH, L - kk};
+                NAME();
+                sv_emit(&o, name, s + 1, ops2, 2, GF_REVERSE, sv_mapq(c, &r), -1, -1, 0, NULL);
+            }
+            break;
+        }
+        case SV_CTX: {
+            /* fragments joining (chr, s) to (chr2, y); both sides from the same stream */
+            for (int j = 0; j < npair; j++) {
+                int fi = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
+                long a = s - L - xint(&r, fi > 2 * L ? fi - 2 * L : 1);
+                long t = fi - (s - a) - L;
+                if (t < 0) t = 0;
+                int orient = (int)xint(&r, 2); /* partner read reverse (0) or forward (1) */
+                long b = orient == 0 ? e->y + t : e->y - t - L;
+                int q1 = sv_mapq(c, &r), q2 = sv_mapq(c, &r);
+                snprintf(name, sizeof(name), "SX%02d:%06d:%04d", e->chr, k, f++);
+                int ops[2] = {GC_MATCH, L};
+                int rev2 = orient == 0;
+                if (ci == e->chr) {
+                    int fl = GF_PAIRED | GF_READ1 | (rev2 ? GF_MREVERSE : 0);
+                    sv_emit(&o, name, a, ops, 1, fl, q1, e->chr2, b, 0, NULL);
+                }
+                if (ci == e->chr2) {
+                    int fl = GF_PAIRED | GF_READ2 | (rev2 ? GF_REVERSE : 0);
+                    sv_emit(&o, name, b, ops, 1, fl, q2, e->chr, a, 0, NULL);
+                }
+            }
+            break;
+        }
+        }
+#undef NAME
+    }
+    free(ev);
+    return o.n;
+}
+
 long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit, void *ctx) {
     long n = c->chr_len[ci];
     int L = c->read_len;
@@ -406,6 +725,8 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
     uint64_t frag_id = 0;
     cnv_reg *creg;
     int n_creg = synth_cnv_regions(c, ci, &creg), ic = 0;
+    /* the SV evidence records wait in the heap until their position comes up */
+    synth_sv_records(c, ci, ref, &heap, &order);
     aln a1, a2;
     char name[64];
     while (start_f < (double)n) {

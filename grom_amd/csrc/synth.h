@@ -48,6 +48,12 @@ typedef struct synth_cfg {
                              a different length (exercises the evidence
                              "other" slots); 0 keeps the random stream as is */
     long cnv_min, cnv_max;/* copy-number region length range */
+    double sv_per_mb;     /* breakpoint SVs per Mb (DEL, DUP, INV, INS, and
+                             CTX with the next chromosome), each with its
+                             discordant pairs, split reads (SA:Z tags), soft
+                             clips and unmapped mates; 0 = none */
+    double sv_evidence;   /* evidence depth: pairs per breakpoint as a
+                             fraction of the spanning-fragment depth */
     uint64_t seed;
 } synth_cfg;
 

@@ -62,6 +62,23 @@ static int g_read_name_len = 50;
 static int g_sc_min = 1;
 static int g_insert_max_mult = 5;
 static int insert_sample_size = 10000000;
+/* breakpoint-path parameters (GROM.c:807-974) */
+static int g_min_disc = 3;              /* -d */
+static int g_sc_range = 35;
+static int g_max_split_loss = 20;       /* -y */
+static int g_min_sr_len = 30;           /* -z */
+static double g_pval_threshold = 0.001; /* -v; g_pval_threshold1 is set from it, GROM.c:22101 */
+static double g_pval_threshold1 = 0.01;
+static double g_pval_insertion1 = 0.01;
+static double g_pval_insertion = 0.0000000001; /* -e */
+static double g_min_sv_ratio = 0.05;    /* -j */
+static int g_max_homopolymer = 10;      /* -k */
+static double g_min_indel_ratio = 0.125; /* -m */
+static double g_max_evidence_ratio = 0.25; /* -u */
+static int g_max_ins_range = 10;        /* -w */
+static double g_range_mult = 0.75;
+static double g_max_inv_rd_diff = 1.75;
+static double g_min_overlap_ratio = 0.5;
 
 static double g_prob2, g_mq_prob;
 static int g_insert_mean, g_insert_min_size, g_insert_max_size, g_lseq;
@@ -315,6 +332,7 @@ static int bam_name_lc(const char *target, char *out, int cap) {
 }
 
 #include "cnv_oracle.c"
+#include "sv_oracle.c"
 
 /* ---------------- per-chromosome scan state ---------------- */
 typedef struct {
@@ -335,9 +353,7 @@ typedef struct {
     int32_t *names; /* g_min_snv name ids per position */
     orc_indel *ind; /* CIGAR indel evidence per position (row A7) */
     uint8_t *ind_touched;            /* some I/D op reached the base */
-    uint8_t (*ot_type)[50];          /* cdp_one_base_other_type (indel types only) */
-    int32_t (*ot_cnt)[50];           /* cdp_one_base_other */
-    double (*ot_dist)[50];           /* cdp_one_base_other_dist */
+    int32_t *conc, *ins;             /* cdp_one_base_conc / cdp_one_base_ins (row A9) */
 } win_t;
 
 #define ORC_OTHER_LEN 50 /* g_other_len, GROM.c:837 */
@@ -540,6 +556,9 @@ typedef struct {
     int *rm_mchr, *rm_mpos, *rm_lseq, *rm_tlen, *rm_svtype;
     int rm_index, old_pos;
     int p, one_base_index;
+    sv_ring ring;      /* cluster arrays with the reference's ring semantics (sv_oracle.c) */
+    sv_lists lists;    /* candidate lists of the per-base tests */
+    const char *target_name; /* cdp_target_name: the split-read chromosome test, GROM.c:7431 */
 } scan_t;
 
 enum { SV_DEL = 0, SV_DUP = 1, SV_INV_F = 8, SV_INV_R = 9, SV_CTX_FF = 11, SV_CTX_FR = 12, SV_CTX_RF = 13, SV_CTX_RR = 14 };
@@ -568,7 +587,8 @@ static int rmdup_svtype(const cur_t *c) {
  * length seen while its count is 0, a same-length event adds, and a different
  * length goes to the "other" slots, where an entry that overtakes the primary
  * swaps with it. */
-static void indel_fold(win_t *w, long x, int type, int add, long len, const char *seq) {
+static void indel_fold(scan_t *s, long x, int type, int add, long len, const char *seq) {
+    win_t *w = &s->w;
     long sl = wslot(w, x);
     orc_indel *k = &w->ind[sl];
     w->ind_touched[sl] = 1;
@@ -584,42 +604,16 @@ static void indel_fold(win_t *w, long x, int type, int add, long len, const char
     } else if ((uint32_t)len == (uint32_t)*dist) {
         *cnt += add;
     } else {
-        int found = 0;
-        for (int o = 0; o < ORC_OTHER_LEN; o++) {
-            if (w->ot_type[sl][o] == type) {
-                if ((uint32_t)len == (uint32_t)(w->ot_dist[sl][o] + 0.5)) {
-                    found = 1;
-                    w->ot_cnt[sl][o] += add;
-                    if (w->ot_cnt[sl][o] > *cnt) {
-                        int32_t tc = w->ot_cnt[sl][o];
-                        double td = w->ot_dist[sl][o];
-                        w->ot_cnt[sl][o] = *cnt;
-                        w->ot_dist[sl][o] = *dist;
-                        *cnt = tc;
-                        *dist = (int32_t)(uint32_t)(td + 0.5);
-                    }
-                    break;
-                }
-            } else if (w->ot_type[sl][o] == OT_EMPTY) {
-                found = 1;
-                w->ot_cnt[sl][o] = add;
-                w->ot_type[sl][o] = (uint8_t)type;
-                w->ot_dist[sl][o] = (double)len;
-                break;
-            }
-        }
-        if (!found) {
-            for (int o = 0; o < ORC_OTHER_LEN; o++) {
-                if (w->ot_cnt[sl][o] <= add) {
-                    w->ot_cnt[sl][o] = add;
-                    w->ot_type[sl][o] = (uint8_t)type;
-                    w->ot_dist[sl][o] = (double)len;
-                    break;
-                }
-            }
-        }
+        /* the "other" slots are shared with the breakpoint clusters (ring) */
+        sv_indel_other(&s->ring, s->one_base_index + (int)(x - s->p), type, add, len, cnt, dist);
     }
 }
+
+/* window accessors for the breakpoint restatement (sv_oracle.c) */
+static int32_t *acc_rd(void *u, long x) { scan_t *s = (scan_t *)u; return &s->w.c[wslot(&s->w, x)].rd; }
+static int32_t *acc_conc(void *u, long x) { scan_t *s = (scan_t *)u; return &s->w.conc[wslot(&s->w, x)]; }
+static int32_t *acc_ins(void *u, long x) { scan_t *s = (scan_t *)u; return &s->w.ins[wslot(&s->w, x)]; }
+static void acc_indel(void *u, long x, int type, int add, long len) { indel_fold((scan_t *)u, x, type, add, len, NULL); }
 
 static void ingest(scan_t *s, cur_t *c) {
     const char *fasta = s->fasta;
@@ -835,21 +829,36 @@ static void ingest(scan_t *s, cur_t *c) {
                 if (c_len[a] <= ORC_INDEL_SEQ)
                     for (long q = 0; q < c_len[a]; q++)
                         iseq[q] = (sb + q < lseq_q) ? grom_nt16_rev[bam_seqi(seq4, sb + q)] : 0;
-                indel_fold(&s->w, tp, OT_INDEL_I, c->add, c_len[a], iseq);
+                indel_fold(s, tp, OT_INDEL_I, c->add, c_len[a], iseq);
                 sb += (int)c_len[a];
             } else if (op == GC_DEL) {
-                indel_fold(&s->w, tp, OT_INDEL_D_F, c->add, c_len[a], NULL);
-                indel_fold(&s->w, tp + c_len[a] - 1, OT_INDEL_D_R, c->add, c_len[a], NULL);
+                indel_fold(s, tp, OT_INDEL_D_F, c->add, c_len[a], NULL);
+                indel_fold(s, tp + c_len[a] - 1, OT_INDEL_D_R, c->add, c_len[a], NULL);
                 tp += c_len[a];
             }
         }
     }
+
+    /* split-read and read-pair breakpoint evidence (rows A8/A9, sv_oracle.c) */
+    sv_read r;
+    memset(&r, 0, sizeof(r));
+    r.pos = c->pos; r.mpos = c->mpos; r.tlen = c->tlen; r.lseq = c->lseq; r.chr = c->chr; r.mchr = c->mchr;
+    r.mq = c->mq; r.flag = c->flag; r.add = c->add;
+    r.start_adj = start_adj; r.end_adj = end_adj; r.end_adj_indel = end_adj_indel;
+    r.aux_pos = c->aux_pos; r.aux_mq = c->aux_mq; r.aux_strand = c->aux_strand;
+    if (c->aux_pos >= 0) {
+        r.aux_same_chr = strncmp(s->target_name, c->aux_chr, strlen(s->target_name)) == 0;
+        sv_aux_cigar(c->aux_cigar, &r.aux_start_adj, &r.aux_end_adj, &r.aux_end_adj_indel); /* GROM.c:6683-6733 */
+    }
+    sv_ctx X = {&s->ring, s->one_base_index, s->p, acc_rd, acc_conc, acc_ins, acc_indel, s,
+                g_insert_max_size, g_insert_min_size, g_insert_mean, g_sc_min, g_min_mapq, g_max_split_loss,
+                g_min_sr_len, g_lseq};
+    sv_ingest(&X, &r);
 }
 
 static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_match, int chr_match,
-                            const char *fasta, long chr_len, const char *chr_name, FILE *vcf, FILE *dump_cnt,
-                            FILE *dump_ind) {
-    (void)target_name_of_match;
+                            const char *fasta, long chr_len, const char *chr_name, FILE *vcf, FILE *ctx_raw,
+                            FILE *dump_cnt, FILE *dump_ind) {
     scan_t s;
     memset(&s, 0, sizeof(s));
     /* srand(time()) per chromosome, GROM.c:1584; GROM_SEED pins it */
@@ -866,9 +875,11 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     s.w.names = (int32_t *)calloc((size_t)s.w.W * g_min_snv, sizeof(int32_t));
     s.w.ind = (orc_indel *)calloc(s.w.W, sizeof(orc_indel));
     s.w.ind_touched = (uint8_t *)calloc(s.w.W, 1);
-    s.w.ot_type = calloc(s.w.W, sizeof(*s.w.ot_type));
-    s.w.ot_cnt = calloc(s.w.W, sizeof(*s.w.ot_cnt));
-    s.w.ot_dist = calloc(s.w.W, sizeof(*s.w.ot_dist));
+    s.w.conc = (int32_t *)calloc(s.w.W, sizeof(int32_t));
+    s.w.ins = (int32_t *)calloc(s.w.W, sizeof(int32_t));
+    sv_ring_init(&s.ring, g_one_base_rd_len);
+    sv_lists_init(&s.lists, g_sv_list_len);
+    s.target_name = target_name_of_match ? target_name_of_match : "";
     s.caf_mq = (int32_t *)calloc(chr_len, sizeof(int32_t));
     s.caf_rd = (int32_t *)calloc(chr_len, sizeof(int32_t));
     s.caf_low = (int32_t *)calloc(chr_len, sizeof(int32_t));
@@ -897,10 +908,15 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                 begin = 1;
                 while (begin < 2) {
                     idx += 1;
-                    if (idx == g_34_one_base_rd_len) idx = g_14_one_base_rd_len; /* ring shift */
+                    if (idx == g_34_one_base_rd_len) { /* ring shift, GROM.c:5847-6401 */
+                        idx = g_14_one_base_rd_len;
+                        sv_ring_shift(&s.ring);
+                    }
                     if (begin < 2 && c->pos >= idx_start) {
                         if (c->pos - g_overlap_mult * g_insert_max_size <= p) {
                             while (c->pos - g_overlap_mult * g_insert_max_size <= p && begin < 2) {
+                                s.p = p;
+                                s.one_base_index = idx;
                                 ingest(&s, c);
                                 n_ingested++;
                                 if (my_samread(st, &c->b) > 0) {
@@ -921,9 +937,7 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                                 if (dump_ind && s.w.ind_touched[sl_]) {
                                     orc_indel r = s.w.ind[sl_];
                                     r.pos = p;
-                                    r.other_len = ORC_OTHER_LEN; /* GROM.c:11415-11425 */
-                                    for (int o = 0; o < ORC_OTHER_LEN; o++)
-                                        if (s.w.ot_type[sl_][o] == OT_EMPTY) { r.other_len = o; break; }
+                                    r.other_len = sv_other_len(&s.ring, idx); /* GROM.c:11415-11425 */
                                     fwrite(&r, sizeof(r), 1, dump_ind);
                                 }
                             }
@@ -975,6 +989,29 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                                     snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx,
                                               &rc_total, &base_total, chr_name, vcf, c->lseq);
                             }
+                            /* indel, insertion and breakpoint tests, GROM.c:11338-13553 */
+                            {
+                                const orc_counts *k1 = &s.w.c[wslot(&s.w, (long)p + 1)];
+                                const orc_indel *in = &s.w.ind[wslot(&s.w, p)];
+                                sv_base B;
+                                B.rd = k->rd; B.sc_rd = k->sc_rd; B.indel_sc_rd = k->indel_sc_rd;
+                                B.sc_left = k->sc_left; B.sc_right = k->sc_right;
+                                B.sc_left_rd = k->sc_left_rd; B.sc_right_rd = k->sc_right_rd;
+                                B.indel_sc_left = k->indel_sc_left; B.indel_sc_right = k->indel_sc_right;
+                                B.sc_left_next = k1->sc_left; B.sc_left_rd_next = k1->sc_left_rd;
+                                B.snv_all = 0;
+                                for (int a = 0; a < 4; a++) B.snv_all += k->snv[a] + k->snv_lowmq[a];
+                                B.conc = s.w.conc[wslot(&s.w, p)];
+                                B.ins = s.w.ins[wslot(&s.w, p)];
+                                B.indel_i = in->ins; B.indel_idist = in->ins_len;
+                                B.indel_d_f = in->del_f; B.indel_d_f_rd = in->del_f_rd;
+                                B.indel_d_r = in->del_r; B.indel_d_rdist = in->del_r_len; B.indel_d_r_rd = in->del_r_rd;
+                                B.ins_seq = in->ins_seq;
+                                sv_eval_prm E = {&g_mq_table[0][0], &g_hez_table[0][0], g_min_disc, g_insert_max_size,
+                                                 g_insert_min_size, g_insert_mean, g_lseq, g_sc_range, g_pval_threshold1,
+                                                 g_pval_insertion1, g_max_evidence_ratio, g_range_mult};
+                                sv_eval(&E, &s.lists, &s.ring, idx, p, &B, c->lseq);
+                            }
                         }
                         p += 1;
                         /* slide the modular window: the slot of p-H/2-1 now holds p+H/2-1 */
@@ -985,9 +1022,8 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                             memset(&s.w.names[sl_ * g_min_snv], 0, sizeof(int32_t) * g_min_snv);
                             memset(&s.w.ind[sl_], 0, sizeof(orc_indel));
                             s.w.ind_touched[sl_] = 0;
-                            memset(s.w.ot_type[sl_], 0, sizeof(s.w.ot_type[0]));
-                            memset(s.w.ot_cnt[sl_], 0, sizeof(s.w.ot_cnt[0]));
-                            memset(s.w.ot_dist[sl_], 0, sizeof(s.w.ot_dist[0]));
+                            s.w.conc[sl_] = 0;
+                            s.w.ins[sl_] = 0;
                         }
                     } else {
                         n_skipped++;
@@ -1007,6 +1043,12 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     /* final SNV flush, GROM.c:15063-15160 */
     snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx, &rc_total, &base_total,
               chr_name, vcf, c->lseq);
+    /* SV assembly and rows, GROM.c:15163-16580 */
+    if (g_vcf == 1) {
+        sv_out_prm O = {g_insert_max_size, g_lseq, g_vcf, 0, g_pval_threshold, g_pval_insertion, g_min_sv_ratio,
+                        g_min_indel_ratio, g_max_inv_rd_diff, g_min_overlap_ratio, g_max_homopolymer, g_max_ins_range};
+        sv_write_rows(&O, &s.lists, chr_name, fasta, chr_len, s.caf_rd, s.caf_low, vcf, ctx_raw);
+    }
 
     if (g_dump_prefix) {
         char path[4096];
@@ -1032,7 +1074,9 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     snv_list_free(&sl);
     nametab_free(&s.names);
     free(s.w.c); free(s.w.names);
-    free(s.w.ind); free(s.w.ind_touched); free(s.w.ot_type); free(s.w.ot_cnt); free(s.w.ot_dist);
+    free(s.w.ind); free(s.w.ind_touched); free(s.w.conc); free(s.w.ins);
+    sv_ring_free(&s.ring);
+    sv_lists_free(&s.lists);
     free(s.caf_mq); free(s.caf_rd); free(s.caf_low);
     free(s.rm_mchr); free(s.rm_mpos); free(s.rm_lseq); free(s.rm_tlen); free(s.rm_svtype);
 }
@@ -1040,6 +1084,9 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
 /* VCF header, GROM.c:20517-20565; the .ctx.vcf variant (GROM.c:22612-22651)
  * omits the GT and the four CNV FORMAT lines.  fileDate may be pinned by
  * GROM_FILEDATE for reproducible comparisons. */
+static void write_header(FILE *f, const char *fasta_file_name, int ctx);
+static const char *g_hdr_fasta = "";
+static void write_ctx_header(FILE *f) { write_header(f, g_hdr_fasta, 1); }
 static void write_header(FILE *f, const char *fasta_file_name, int ctx) {
     const char *pin = getenv("GROM_FILEDATE");
     fprintf(f, "##fileformat=VCFv4.2\n");
@@ -1125,6 +1172,16 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
         case 'a': g_min_snv_ratio = atof(optarg); break;
         case 'f': g_vcf = 0; break;
         case 'x': g_min_ave_bq = atof(optarg); break;
+        case 'v': g_pval_threshold = atof(optarg); break;
+        case 'd': g_min_disc = atoi(optarg); break;
+        case 'y': g_max_split_loss = atoi(optarg); break;
+        case 'z': g_min_sr_len = atoi(optarg); break;
+        case 'e': g_pval_insertion = atof(optarg); break;
+        case 'j': g_min_sv_ratio = atof(optarg); break;
+        case 'k': g_max_homopolymer = atoi(optarg); break;
+        case 'm': g_min_indel_ratio = atof(optarg); break;
+        case 'u': g_max_evidence_ratio = atof(optarg); break;
+        case 'w': g_max_ins_range = atoi(optarg); break;
         case 'Z': g_block_min = atol(optarg); break;
         case 'W': g_min_rd_window_len = atol(optarg); break;
         case 'X': g_max_rd_window_len = atol(optarg); break;
@@ -1142,6 +1199,7 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
         default: break; /* options outside this restatement's scope */
         }
     }
+    g_pval_threshold1 = g_pval_threshold; /* GROM.c:22101 */
     g_rd_min_mapq = g_min_mapq; /* GROM.c:22102 */
     if (!bam_file_name) { printf("ERROR: No bam file specified.\n"); return 1; }
     stream_t st;
@@ -1248,20 +1306,31 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
             snprintf(path, sizeof(path), "%s.%s.ind", g_dump_prefix, cname);
             dump_ind = fopen(path, "wb");
         }
-        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, dump_cnt, dump_ind);
+        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, ctx, dump_cnt, dump_ind);
         if (dump_cnt) fclose(dump_cnt);
         if (dump_ind) fclose(dump_ind);
+    }
+    /* BAM target names, lower-cased, for main's CTX post-pass (GROM.c:22408-22430) */
+    int n_targets = st.hdr.n_ref;
+    char **names_lc = (char **)calloc(n_targets > 0 ? n_targets : 1, sizeof(char *));
+    for (int a = 0; a < n_targets; a++) {
+        size_t L = strlen(st.hdr.ref_name[a]);
+        names_lc[a] = (char *)malloc(L + 1);
+        for (size_t b = 0; b <= L; b++) names_lc[a][b] = (char)tolower((unsigned char)st.hdr.ref_name[a][b]);
     }
     bam_free_rec(&cur.b);
     stream_close(&st);
     free(chr_fasta);
     fclose(vcf);
     if (ctx) {
-        /* CTX post-pass of main (GROM.c:22400-22770) rewrites the file with the
-         * header; with no CTX rows that is the header alone. */
-        if (g_vcf == 1) write_header(ctx, fasta_file_name, 1);
+        /* CTX post-pass of main (GROM.c:22400-22770): pair the raw CTX rows
+         * and rewrite the file with its header */
         fclose(ctx);
+        g_hdr_fasta = fasta_file_name;
+        if (g_vcf == 1) sv_ctx_postpass(ctx_name, names_lc, n_targets, g_insert_max_size, g_lseq, write_ctx_header);
     }
+    for (int a = 0; a < n_targets; a++) free(names_lc[a]);
+    free(names_lc);
     fclose(fasta);
     return 0;
 }

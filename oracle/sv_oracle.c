@@ -1,0 +1,1478 @@
+/*
+ * sv_oracle.c -- TEST INFRASTRUCTURE ONLY (included by grom_oracle.c).
+ *
+ * CPU restatement of GROM's breakpoint path: split-read evidence (row A8,
+ * GROM.c:6683-6733, 7431-7945 and the split-read DUP branches of
+ * 7978-8340 / 9363-9729), discordant/concordant pair binning (row A9,
+ * GROM.c:7954-10953), the per-base indel / insertion / breakpoint tests and
+ * their candidate lists (row A10, GROM.c:11340-13553), the SV assembly and
+ * row writer (row A13, GROM.c:15163-16580) and main's CTX mate pairing
+ * (GROM.c:22400-22770).  It is the checker for the HIP path; nothing in
+ * grom_amd/ links it.
+ *
+ * State layout.  Arrays the reference copies unconditionally at a ring shift
+ * (rd, conc, ins, soft clips, indel primaries) live in the oracle's modular
+ * window (grom_oracle.c).  The cluster arrays (del/dup/inv/ctx, munmapped and
+ * the 50 "other" slots) are copied only when their group's "set" flags say so
+ * (GROM.c:5868-6392), and one write site (the split-read DUP start of
+ * GROM.c:8020-8045) sets the DEL flags instead of the DUP flags; so they are
+ * kept in a restated ring of g_one_base_rd_len entries indexed exactly as the
+ * reference's (cdp_one_base_index + pos - p) with the reference's flag logic.
+ */
+
+#define SV_OTHER 50 /* g_other_len, GROM.c:837 */
+
+/* cluster types, in the order of the OTHER_* codes minus one (GROM.c:668-681) */
+enum { CL_DEL_F, CL_DEL_R, CL_DUP_F, CL_DUP_R, CL_INV_F1, CL_INV_R1, CL_INV_F2, CL_INV_R2, CL_CTX_F, CL_CTX_R, CL_N };
+/* ring "set" flag groups (GROM.c:5868-6020) */
+enum { G_DEL, G_DUP, G_INV_F, G_INV_R, G_CTX_F, G_CTX_R, G_N };
+static const int cl_group[CL_N] = {G_DEL, G_DEL, G_DUP, G_DUP, G_INV_F, G_INV_R, G_INV_F, G_INV_R, G_CTX_F, G_CTX_R};
+
+typedef struct {
+    int32_t cnt;
+    double dist; /* running mean; the mate position for ctx (negative: mate reverse) */
+    int32_t rs, re;
+} clus_t;
+
+typedef struct {
+    int R, H;                     /* g_one_base_rd_len, g_half_one_base_rd_len */
+    clus_t *cl[CL_N];             /* [R] */
+    int32_t *ctx_mchr[2];         /* cdp_one_base_ctx_f_mchr / _r_mchr */
+    int32_t *mun[2];              /* cdp_one_base_munmapped_f / _r */
+    int32_t *ocnt, *omchr, *ors, *ore; /* [SV_OTHER * R] */
+    double *odist;
+    uint8_t *otype;
+    int gset[G_N][2], mset[2][2], oset[SV_OTHER][2];
+} sv_ring;
+
+static void sv_ring_init(sv_ring *r, int R) {
+    memset(r, 0, sizeof(*r));
+    r->R = R;
+    r->H = R / 2;
+    for (int t = 0; t < CL_N; t++) r->cl[t] = (clus_t *)calloc(R, sizeof(clus_t));
+    for (int k = 0; k < 2; k++) {
+        r->ctx_mchr[k] = (int32_t *)calloc(R, sizeof(int32_t));
+        r->mun[k] = (int32_t *)calloc(R, sizeof(int32_t));
+    }
+    r->ocnt = (int32_t *)calloc((size_t)SV_OTHER * R, sizeof(int32_t));
+    r->omchr = (int32_t *)calloc((size_t)SV_OTHER * R, sizeof(int32_t));
+    r->ors = (int32_t *)calloc((size_t)SV_OTHER * R, sizeof(int32_t));
+    r->ore = (int32_t *)calloc((size_t)SV_OTHER * R, sizeof(int32_t));
+    r->odist = (double *)calloc((size_t)SV_OTHER * R, sizeof(double));
+    r->otype = (uint8_t *)calloc((size_t)SV_OTHER * R, 1);
+}
+
+static void sv_ring_free(sv_ring *r) {
+    for (int t = 0; t < CL_N; t++) free(r->cl[t]);
+    for (int k = 0; k < 2; k++) { free(r->ctx_mchr[k]); free(r->mun[k]); }
+    free(r->ocnt); free(r->omchr); free(r->ors); free(r->ore); free(r->odist); free(r->otype);
+}
+
+/* lower half := upper half (copy) or zero, then the upper half is cleared,
+ * as the set flags allow (GROM.c:5868-6020 and 6157-6300) */
+#define SV_SHIFT_ARR(arr, T, set)                                                                     \
+    do {                                                                                           \
+        if ((set)[0] != 0 || (set)[1] != 0) {                                                       \
+            if ((set)[1] == 0) memset((arr), 0, (size_t)r->H * sizeof(T));                          \
+            else memcpy((arr), (arr) + r->H, (size_t)r->H * sizeof(T));                             \
+        }                                                                                          \
+        if ((set)[1] != 0) memset((arr) + r->H, 0, (size_t)r->H * sizeof(T));                       \
+    } while (0)
+
+static void sv_ring_shift(sv_ring *r) {
+    for (int t = 0; t < CL_N; t++) SV_SHIFT_ARR(r->cl[t], clus_t, r->gset[cl_group[t]]);
+    SV_SHIFT_ARR(r->ctx_mchr[0], int32_t, r->gset[G_CTX_F]);
+    SV_SHIFT_ARR(r->ctx_mchr[1], int32_t, r->gset[G_CTX_R]);
+    for (int k = 0; k < 2; k++) SV_SHIFT_ARR(r->mun[k], int32_t, r->mset[k]);
+    for (int o = 0; o < SV_OTHER; o++) {
+        size_t b = (size_t)o * r->R;
+        SV_SHIFT_ARR(r->ocnt + b, int32_t, r->oset[o]);
+        SV_SHIFT_ARR(r->otype + b, uint8_t, r->oset[o]);
+        SV_SHIFT_ARR(r->omchr + b, int32_t, r->oset[o]);
+        SV_SHIFT_ARR(r->odist + b, double, r->oset[o]);
+        SV_SHIFT_ARR(r->ors + b, int32_t, r->oset[o]);
+        SV_SHIFT_ARR(r->ore + b, int32_t, r->oset[o]);
+    }
+    /* GROM.c:6381-6400 */
+    for (int g = 0; g < G_N; g++) { r->gset[g][0] = r->gset[g][1]; r->gset[g][1] = 0; }
+    for (int k = 0; k < 2; k++) { r->mset[k][0] = r->mset[k][1]; r->mset[k][1] = 0; }
+    for (int o = 0; o < SV_OTHER; o++) { r->oset[o][0] = r->oset[o][1]; r->oset[o][1] = 0; }
+}
+
+/* abs() of a double in the reference converts to int first (cvttsd2si:
+ * NaN or out of range gives INT_MIN), SURVEY Q4 */
+static inline int abs_trunc(double x) {
+    int i = (x != x || x >= 2147483648.0 || x < -2147483648.0) ? (int)0x80000000u : (int)x;
+    return abs(i);
+}
+
+/* read-position bookkeeping of a cluster (the four forms the 22 blocks use) */
+enum {
+    RM_SET,    /* re = rp on a compatible read (range blocks, GROM.c:8421) */
+    RM_MAX,    /* re = max(re, rp) (split-read DEL start, GROM.c:7681-7694) */
+    RM_MINMAX, /* rs = min, re = max (GROM.c:8712-8719, 7818-7840) */
+};
+
+typedef struct {
+    int t;          /* CL_* */
+    int w;          /* count increment (add, or add/2 away from the clipped edge) */
+    double wd;      /* running-mean weight (add, or add/2.0) */
+    int add;        /* full weight: the "overwrite a slot <= add" test */
+    double v;       /* value the cluster averages */
+    double tol;     /* (Mx - Mn [+ insert_temp]) */
+    int rp;         /* read position kept in rs/re */
+    int rmode;
+    int ctx;        /* 0: distance cluster; 1: ctx, mate forward; 2: ctx, mate reverse */
+    int mchr;
+    int init_quirk; /* split-read DUP_F start: 1 = GROM.c:8020-8045 (DEL flags only),
+                       2 = GROM.c:9405-9422 (DEL and DUP flags); both write
+                       del_f_read_end instead of dup_f_read_end */
+} sv_ev;
+
+static inline void rs_re_update(int32_t *rs, int32_t *re, int rp, int mode) {
+    if (mode == RM_SET) *re = rp;
+    else if (mode == RM_MAX) { if (rp > *re) *re = rp; }
+    else { if (rp < *rs) *rs = rp; if (rp > *re) *re = rp; }
+}
+
+/* compatibility of value e->v with a cluster holding (dist, cnt) */
+static inline int sv_compat(const sv_ev *e, double dist, int32_t cnt, int32_t mchr) {
+    const double lim = e->tol * (1.0 + (1.0 / (double)cnt));
+    if (e->ctx == 0) return (double)abs_trunc(dist - e->v) <= lim;
+    if (e->ctx == 1) return mchr == e->mchr && (double)abs_trunc(dist - e->v) <= lim && dist > 0;
+    /* mate reverse: the stored value is -mpos; abs() of the stored mean
+     * truncates before the second abs() (GROM.c:10494) */
+    return mchr == e->mchr && (double)abs_trunc((double)abs_trunc(dist) - (-e->v)) <= lim && dist < 0;
+}
+
+/* One event folded into ring index i: the block of GROM.c:8403-8523 and its
+ * siblings (primary cluster, then the "other" slots with swap-to-primary). */
+static void sv_fold(sv_ring *r, int i, const sv_ev *e) {
+    clus_t *c = &r->cl[e->t][i];
+    int32_t *pm = (e->t == CL_CTX_F) ? &r->ctx_mchr[0][i] : (e->t == CL_CTX_R) ? &r->ctx_mchr[1][i] : NULL;
+    const int g = cl_group[e->t];
+    if (c->cnt == 0) {
+        if (e->init_quirk == 1) { r->gset[G_DEL][0] = r->gset[G_DEL][1] = 1; }
+        else if (e->init_quirk == 2) {
+            r->gset[G_DEL][0] = r->gset[G_DEL][1] = 1;
+            r->gset[G_DUP][0] = r->gset[G_DUP][1] = 1;
+        } else { r->gset[g][0] = r->gset[g][1] = 1; }
+        c->cnt = e->w;
+        c->dist = e->v;
+        if (pm) *pm = e->mchr;
+        c->rs = e->rp;
+        if (e->init_quirk) r->cl[CL_DEL_F][i].re = e->rp;
+        else c->re = e->rp;
+        return;
+    }
+    if (sv_compat(e, c->dist, c->cnt, pm ? *pm : 0)) {
+        r->gset[g][0] = r->gset[g][1] = 1;
+        c->cnt += e->w;
+        c->dist += e->wd * (e->v - c->dist) / (double)c->cnt;
+        rs_re_update(&c->rs, &c->re, e->rp, e->rmode);
+        return;
+    }
+    const int otype = e->t + 1;
+    int found = 0;
+    for (int o = 0; o < SV_OTHER; o++) {
+        size_t k = (size_t)o * r->R + i;
+        if (r->otype[k] == otype) {
+            if (sv_compat(e, r->odist[k], r->ocnt[k], r->omchr[k])) {
+                found = 1;
+                r->ocnt[k] += e->w;
+                r->odist[k] += e->wd * (e->v - r->odist[k]) / (double)r->ocnt[k];
+                rs_re_update(&r->ors[k], &r->ore[k], e->rp, e->rmode);
+                if (r->ocnt[k] > c->cnt) {
+                    clus_t tmp = {r->ocnt[k], r->odist[k], r->ors[k], r->ore[k]};
+                    r->ocnt[k] = c->cnt;
+                    r->odist[k] = c->dist;
+                    r->ors[k] = c->rs;
+                    r->ore[k] = c->re;
+                    *c = tmp;
+                    if (pm) { int32_t tm = r->omchr[k]; r->omchr[k] = *pm; *pm = tm; }
+                }
+                break;
+            }
+        } else if (r->otype[k] == 0) {
+            found = 1;
+            r->oset[o][0] = r->oset[o][1] = 1;
+            r->ocnt[k] = e->w;
+            r->otype[k] = (uint8_t)otype;
+            r->odist[k] = e->v;
+            if (pm) r->omchr[k] = e->mchr;
+            r->ors[k] = r->ore[k] = e->rp;
+            break;
+        }
+    }
+    if (!found) {
+        for (int o = 0; o < SV_OTHER; o++) {
+            size_t k = (size_t)o * r->R + i;
+            if (r->ocnt[k] <= e->add) {
+                r->ocnt[k] = e->w;
+                r->otype[k] = (uint8_t)otype;
+                r->odist[k] = e->v;
+                if (pm) r->omchr[k] = e->mchr;
+                r->ors[k] = r->ore[k] = e->rp;
+                break;
+            }
+        }
+    }
+}
+
+/* An indel event's "other" slots (GROM.c:7230-7280 for I, 7303-7350 for the
+ * deletion ends): same-length compatibility with the slot length rounded
+ * (uint32_t)(dist + 0.5); a swap moves only (count, length).  Returns via
+ * cnt/dist the primary after a possible swap. */
+static void sv_indel_other(sv_ring *r, int i, int type, int add, long len, int32_t *cnt, int32_t *dist) {
+    int found = 0;
+    for (int o = 0; o < SV_OTHER; o++) {
+        size_t k = (size_t)o * r->R + i;
+        if (r->otype[k] == type) {
+            if ((uint32_t)len == (uint32_t)(r->odist[k] + 0.5)) {
+                found = 1;
+                r->ocnt[k] += add;
+                if (r->ocnt[k] > *cnt) {
+                    int32_t tc = r->ocnt[k];
+                    double td = r->odist[k];
+                    r->ocnt[k] = *cnt;
+                    r->odist[k] = *dist;
+                    *cnt = tc;
+                    *dist = (int32_t)(uint32_t)(td + 0.5);
+                }
+                break;
+            }
+        } else if (r->otype[k] == 0) {
+            found = 1;
+            r->oset[o][0] = r->oset[o][1] = 1;
+            r->ocnt[k] = add;
+            r->otype[k] = (uint8_t)type;
+            r->odist[k] = (double)len;
+            break;
+        }
+    }
+    if (!found) {
+        for (int o = 0; o < SV_OTHER; o++) {
+            size_t k = (size_t)o * r->R + i;
+            if (r->ocnt[k] <= add) {
+                r->ocnt[k] = add;
+                r->otype[k] = (uint8_t)type;
+                r->odist[k] = (double)len;
+                r->ors[k] = 0;
+                r->ore[k] = 0;
+                break;
+            }
+        }
+    }
+}
+
+/* number of occupied "other" slots at ring index i (GROM.c:11415-11425) */
+static int sv_other_len(const sv_ring *r, int i) {
+    for (int o = 0; o < SV_OTHER; o++)
+        if (r->otype[(size_t)o * r->R + i] == 0) return o;
+    return SV_OTHER;
+}
+
+/* ------------------------------------------------------------------------
+ * Candidate lists (GROM.c:3690-5000; start/end positions start at -1,
+ * GROM.c:5524-5560; everything else is read as the zero of a fresh mapping)
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    int32_t start, end, conc_s, conc_e, dist, other_s, other_e, i, rd, sc;
+    double binom, hez;
+    char seq[SV_OTHER + 1];
+} ii_ent; /* indel_i_list */
+
+typedef struct {
+    int32_t start, end, conc_s, conc_e, other_s, other_e, f, r, rd_s, rd_e, sc_s, sc_e;
+    double binom_s, binom_e, hez_s, hez_e;
+} id_ent; /* indel_d_list */
+
+typedef struct {
+    int32_t start, end, ins_s, ins_e, rd_s, rd_e, conc_s, conc_e, other_s, other_e;
+    double binom_s, binom_e;
+} ins_ent; /* ins_list / ins_list2 */
+
+typedef struct {
+    int32_t start, end, cnt_s, cnt_e, rd_s, rd_e, conc_s, conc_e, other_s, other_e, rs_s, re_s, rs_e, re_e;
+    double dist, binom_s, binom_e, hez_s, hez_e;
+} pr_ent; /* dup / del / inv_f / inv_r lists and their list2 */
+
+typedef struct {
+    int32_t pos, cnt, rd, conc, mchr, mpos, other, rs, re;
+    double binom, hez;
+} ctx_ent; /* ctx_f_list / ctx_r_list */
+
+typedef struct {
+    int cap, cap2;
+    ii_ent *ii;
+    int n_ii;
+    id_ent *id;
+    int n_id; /* cdp_indel_d_list_index (starts at -1) */
+    ins_ent *ins;
+    int n_ins; /* cdp_ins_list_index (starts at -1) */
+    pr_ent *pr[4]; /* 0 dup, 1 del, 2 inv_f, 3 inv_r */
+    int n_pr[4];
+    ctx_ent *cx[2];
+    int n_cx[2];
+} sv_lists;
+
+enum { PR_DUP, PR_DEL, PR_INVF, PR_INVR };
+
+static void sv_lists_init(sv_lists *L, int cap) {
+    memset(L, 0, sizeof(*L));
+    L->cap = cap;
+    L->cap2 = cap / 10; /* g_sv_list2_len: 100000 by default, -G sets G/10 (GROM.c:21925) */
+    if (L->cap2 < 1) L->cap2 = 1;
+    L->ii = (ii_ent *)calloc(cap + 1, sizeof(ii_ent));
+    L->id = (id_ent *)calloc(cap + 1, sizeof(id_ent));
+    L->ins = (ins_ent *)calloc(cap + 1, sizeof(ins_ent));
+    for (int k = 0; k < 4; k++) L->pr[k] = (pr_ent *)calloc(cap + 1, sizeof(pr_ent));
+    for (int k = 0; k < 2; k++) L->cx[k] = (ctx_ent *)calloc(cap + 1, sizeof(ctx_ent));
+    for (int a = 0; a <= cap; a++) {
+        L->ii[a].start = L->ii[a].end = -1;
+        L->id[a].start = L->id[a].end = -1;
+        L->ins[a].start = L->ins[a].end = -1;
+        for (int k = 0; k < 4; k++) L->pr[k][a].start = L->pr[k][a].end = -1;
+        for (int k = 0; k < 2; k++) L->cx[k][a].pos = -1;
+    }
+    L->n_id = -1;
+    L->n_ins = -1;
+}
+
+static void sv_lists_free(sv_lists *L) {
+    free(L->ii); free(L->id); free(L->ins);
+    for (int k = 0; k < 4; k++) free(L->pr[k]);
+    for (int k = 0; k < 2; k++) free(L->cx[k]);
+}
+
+/* ------------------------------------------------------------------------
+ * Per-read evidence (rows A8/A9).  `sv_read` carries the fields of the read
+ * being ingested as GROM's locals hold them at GROM.c:7431 (cdp_lseq already
+ * includes hard clips, GROM.c:6997-7000).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    int32_t pos, mpos, tlen, lseq, chr, mchr, mq;
+    uint16_t flag;
+    int add;
+    int start_adj, end_adj, end_adj_indel;
+    int aux_pos, aux_mq, aux_strand, aux_same_chr; /* aux_same_chr: the prefix strncmp of GROM.c:7431 */
+    int aux_start_adj, aux_end_adj, aux_end_adj_indel;
+} sv_read;
+
+/* The SA/XP CIGAR's clip and indel lengths (GROM.c:6683-6733): digits
+ * accumulate, a letter closes an op; only 'S' counts as a clip here. */
+static void sv_aux_cigar(const char *cig, int *sa, int *ea, int *eai) {
+    char tstr[1001];
+    char ctype[1000];
+    int clen[1000];
+    int n = 0, sl = 0;
+    *sa = *ea = *eai = 0;
+    if (!cig) return;
+    int L = (int)strlen(cig);
+    for (int a = 0; a < L; a++) {
+        if (isdigit((unsigned char)cig[a]) && sl < 1000) {
+            tstr[sl++] = cig[a];
+        } else if (isalpha((unsigned char)cig[a])) {
+            if (n >= 1000) break;
+            ctype[n] = cig[a];
+            tstr[sl] = cig[a];
+            tstr[sl + 1] = 0;
+            clen[n] = (int)strtol(tstr, NULL, 10);
+            n += 1;
+            sl = 0;
+        }
+    }
+    if (n == 0) return; /* the reference reads c_type[-1] here; synthetic data never has an empty CIGAR */
+    if (ctype[0] == 'S') *sa = clen[0];
+    if (ctype[n - 1] == 'S') *ea = clen[n - 1];
+    for (int a = 0; a < n; a++) {
+        if (ctype[a] == 'I') *eai += clen[a];
+        else if (ctype[a] == 'D') *eai -= clen[a];
+    }
+}
+
+typedef struct {
+    sv_ring *ring;
+    int idx, p; /* cdp_one_base_index and cdp_pos_in_contig_start at the ingest */
+    int32_t *(*rd)(void *u, long x);   /* window cdp_one_base_rd at absolute x */
+    int32_t *(*conc)(void *u, long x); /* cdp_one_base_conc */
+    int32_t *(*ins)(void *u, long x);  /* cdp_one_base_ins */
+    void (*indel)(void *u, long x, int type, int add, long len); /* CIGAR-style D_F/D_R event */
+    void *u;
+    int Mx, Mn, mean, sc_min, min_mapq, max_split_loss, min_sr_len, glseq;
+} sv_ctx;
+
+#define RI(x) (X->idx + (x) - X->p)             /* ring index of absolute position x */
+#define AX(a) ((long)(a) - X->idx + X->p)       /* absolute position of ring index a */
+
+/* an event at ring index a */
+static void sv_ev_at(sv_ctx *X, int a, sv_ev *e) { sv_fold(X->ring, a, e); }
+
+/* Range block: rd += 1 then the cluster event at every a in [lps, lpe)
+ * (e.g. GROM.c:8388-8525).  half: 0 none, 1 end-clipped F reads (full weight
+ * only at lps, GROM.c:8396), 2 start-clipped R reads (full weight only at
+ * lpe-1, GROM.c:8690). */
+static void sv_range(sv_ctx *X, const sv_read *r, int lps, int lpe, int t, double v, double tol, int ctx, int half) {
+    for (int a = lps; a < lpe; a++) {
+        *X->rd(X->u, AX(a)) += 1;
+        int full = (half == 1) ? (r->end_adj < X->sc_min || a == lps) : (r->start_adj < X->sc_min || a == lpe - 1);
+        sv_ev e = {t, full ? r->add : r->add / 2, full ? (double)r->add : (double)r->add / 2.0, r->add, v, tol,
+                   r->pos, RM_SET, ctx, r->mchr, 0};
+        sv_ev_at(X, a, &e);
+    }
+}
+
+static void sv_ingest(sv_ctx *X, const sv_read *r) {
+    const int rev = (r->flag & GF_REVERSE) != 0, mrev = (r->flag & GF_MREVERSE) != 0;
+    const int paired = (r->flag & GF_PAIRED) != 0, munmap = (r->flag & GF_MUNMAP) != 0;
+    const int pos = r->pos, mpos = r->mpos, tlen = r->tlen, lseq = r->lseq;
+    const int sa = r->start_adj, ea = r->end_adj, eai = r->end_adj_indel;
+    const int asa = r->aux_start_adj, aea = r->aux_end_adj, aeai = r->aux_end_adj_indel;
+    const int Mx = X->Mx, Mn = X->Mn, R = X->ring->R;
+    const int E = pos - sa + lseq - ea - eai; /* reference end of the aligned part */
+    const double tol = (double)(Mx - Mn);
+    int lps, lpe;
+
+    /* ---- split-read deletion, GROM.c:7431-7945 ---- */
+    if (r->aux_pos >= 0 && r->aux_same_chr) {
+        int sr_del = 0;
+        if (r->aux_mq >= X->min_mapq && r->mq >= X->min_mapq) {
+            if ((!rev && r->aux_strand == 0) || (rev && r->aux_strand == 1)) {
+                if (paired && !munmap && r->chr == r->mchr) {
+                    if (!rev && r->aux_strand == 0) {
+                        if (pos < r->aux_pos && tlen <= Mx && r->aux_pos < mpos) {
+                            if (r->aux_pos - E < Mx && r->aux_pos - E > 0) {
+                                if (abs(lseq - ea - asa) <= X->max_split_loss && lseq - sa - ea - eai >= X->min_sr_len &&
+                                    lseq - asa - aea - aeai >= X->min_sr_len) {
+                                    sr_del = 1;
+                                    lps = RI(E);
+                                    lpe = RI(r->aux_pos);
+                                }
+                            }
+                        }
+                    } else if (rev && r->aux_strand == 1) {
+                        if (r->aux_pos < pos && abs(tlen) < Mx && mpos < r->aux_pos) {
+                            if (abs(lseq - sa - aea) <= X->max_split_loss && lseq - sa - ea - eai >= X->min_sr_len &&
+                                lseq - asa - aea - aeai >= X->min_sr_len) {
+                                lps = RI(r->aux_pos - asa + lseq - aea - aeai);
+                                lpe = RI(pos);
+                                if (lps < lpe) sr_del = 1;
+                            }
+                        }
+                    }
+                } else {
+                    if (!rev && r->aux_strand == 0) {
+                        if (pos < r->aux_pos) {
+                            if (r->aux_pos - E < Mx && r->aux_pos - E > 0) {
+                                sr_del = 1;
+                                lps = RI(E);
+                                lpe = RI(r->aux_pos);
+                            }
+                        }
+                    } else if (rev && r->aux_strand == 1) {
+                        if (r->aux_pos < pos && pos - (r->aux_pos - asa + lseq - aea - aeai) < Mx) {
+                            lps = RI(r->aux_pos - asa + lseq - aea - aeai);
+                            lpe = RI(pos);
+                            if (lps < lpe) sr_del = 1;
+                        }
+                    }
+                }
+            }
+            if (sr_del == 1) {
+                /* a short split-read deletion is also CIGAR-style indel evidence, GROM.c:7514-7640 */
+                if (lpe - lps < X->glseq && lpe - lps < Mx - X->mean) {
+                    X->indel(X->u, AX(lps), 12 /* OTHER_INDEL_D_F */, r->add, lpe - lps);
+                    X->indel(X->u, AX(lpe - 1), 13 /* OTHER_INDEL_D_R */, r->add, lpe - lps);
+                }
+                const double v = (double)(lpe - lps + X->mean);
+                *X->rd(X->u, AX(lps)) += 1;
+                sv_ev e1 = {CL_DEL_F, r->add, (double)r->add, r->add, v, tol, pos < r->aux_pos ? pos : r->aux_pos,
+                            RM_MAX, 0, 0, 0};
+                sv_ev_at(X, lps, &e1);
+                *X->rd(X->u, AX(lpe - 1)) += 1;
+                sv_ev e2 = {CL_DEL_R, r->add, (double)r->add, r->add, v, tol, pos < r->aux_pos ? r->aux_pos : pos,
+                            RM_MINMAX, 0, 0, 0};
+                sv_ev_at(X, lpe - 1, &e2);
+            }
+        }
+    }
+
+    const int insert_temp = (X->mean - 2 * lseq > 0) ? X->mean - 2 * lseq : 0; /* GROM.c:7954-7958 */
+    const double tol_inv = (double)(Mx - Mn + insert_temp);
+
+    /* ---- pair classification, GROM.c:7960-10953 ---- */
+    if (paired && !munmap) {
+        if (r->chr == r->mchr) {
+            if (mpos > pos) {
+                if (!rev && mrev) {
+                    if (tlen >= Mn && tlen <= Mx) {
+                        /* concordant; split read over a tandem duplication (GROM.c:7974-8003) */
+                        int sr_dup = 0;
+                        if (r->aux_pos >= 0 && r->aux_same_chr && r->aux_mq >= X->min_mapq && r->mq >= X->min_mapq &&
+                            !rev && r->aux_strand == 0 && pos < r->aux_pos && r->aux_pos < mpos) {
+                            int eai_t = eai > 0 ? eai : 0;
+                            int aeai_t = aeai > 0 ? eai : 0; /* sic: cdp_end_adj_indel, GROM.c:7995 */
+                            if (abs(lseq - sa - aea) <= X->max_split_loss && lseq - sa - ea - eai_t >= X->min_sr_len &&
+                                lseq - asa - aea - aeai_t >= X->min_sr_len) {
+                                sr_dup = 1;
+                                lps = RI(pos);
+                                lpe = RI(r->aux_pos - asa + lseq - aea - aeai);
+                            }
+                        }
+                        if (sr_dup == 1) {
+                            const double v = (double)(lpe - lps - X->mean);
+                            *X->rd(X->u, AX(lpe)) += 1;
+                            sv_ev e1 = {CL_DUP_F, r->add, (double)r->add, r->add, v, tol,
+                                        pos < r->aux_pos ? r->aux_pos : pos, RM_MINMAX, 0, 0, 1};
+                            sv_ev_at(X, lpe, &e1);
+                            *X->rd(X->u, AX(lps - 1)) += 1;
+                            sv_ev e2 = {CL_DUP_R, r->add, (double)r->add, r->add, v, tol,
+                                        pos < r->aux_pos ? pos : r->aux_pos, RM_MINMAX, 0, 0, 0};
+                            sv_ev_at(X, lps - 1, &e2);
+                        }
+                        if (sr_dup == 0) {
+                            /* concordant gap: physical depth and concordant pairs, GROM.c:8342-8365 */
+                            lps = RI(E);
+                            lpe = RI(mpos);
+                            if (R < lpe) lpe = R;
+                            for (int a = lps; a < lpe; a++) *X->rd(X->u, AX(a)) += 1;
+                            for (int a = lps; a < lpe; a++) *X->conc(X->u, AX(a)) += 1;
+                        }
+                    } else if (tlen > 2 * Mx) {
+                        /* GROM.c:8370-8526 */
+                        lps = RI(E);
+                        lpe = RI(pos - sa - eai + Mx - lseq);
+                        if (R < lpe) lpe = R;
+                        if (RI(mpos) < lpe) lpe = RI(mpos);
+                        sv_range(X, r, lps, lpe, CL_DEL_F, (double)tlen, tol, 0, 1);
+                    } else if (tlen > Mx) {
+                        /* GROM.c:8531-8825 */
+                        lps = RI(E);
+                        lpe = RI(mpos);
+                        if (R < lpe) lpe = R;
+                        for (int a = lps; a < lpe; a++) {
+                            *X->rd(X->u, AX(a)) += 1;
+                            if (AX(a) < pos - sa - eai + Mx - lseq) {
+                                int full = (ea < X->sc_min || a == lps);
+                                sv_ev e = {CL_DEL_F, full ? r->add : r->add / 2,
+                                           full ? (double)r->add : (double)r->add / 2.0, r->add, (double)tlen, tol, pos,
+                                           RM_SET, 0, 0, 0};
+                                sv_ev_at(X, a, &e);
+                            }
+                            if (abs(tlen) <= 2 * Mx && AX(a) > pos - sa + tlen - Mx + lseq) {
+                                int full = (sa < X->sc_min || a == lpe - 1);
+                                sv_ev e = {CL_DEL_R, full ? r->add : r->add / 2,
+                                           full ? (double)r->add : (double)r->add / 2.0, r->add, (double)tlen, tol, mpos,
+                                           RM_MINMAX, 0, 0, 0};
+                                sv_ev_at(X, a, &e);
+                            }
+                        }
+                    } else if (tlen < Mn) {
+                        /* GROM.c:8826-8873; the reverse-strand veto is nested unreachably */
+                        int no_ins = 0;
+                        if (r->aux_pos >= 0 && r->aux_same_chr &&
+                            ((!rev && r->aux_strand == 0) || (rev && r->aux_strand == 1)) && !rev &&
+                            r->aux_strand == 0 && r->aux_pos < pos && pos < mpos)
+                            no_ins = 1;
+                        lps = RI(E);
+                        lpe = RI(mpos);
+                        if (no_ins == 0) {
+                            if (R < lpe) lpe = R;
+                            for (int a = lps; a < lpe; a++) {
+                                *X->rd(X->u, AX(a)) += 1;
+                                *X->ins(X->u, AX(a)) += r->add;
+                            }
+                        }
+                    }
+                } else if (!rev && !mrev) {
+                    /* GROM.c:8875-9044 */
+                    if (mpos - pos >= 10) {
+                        lps = RI(E);
+                        lpe = RI(pos - sa + Mx - lseq - eai);
+                        if (R < lpe) lpe = R;
+                        if (RI(mpos) < lpe) lpe = RI(mpos);
+                        sv_range(X, r, lps, lpe, CL_INV_F1, (double)tlen, tol_inv, 0, 1);
+                    }
+                } else if (rev) {
+                    /* GROM.c:9045-9351 */
+                    if (mpos - pos >= 10) {
+                        lps = RI(pos - sa - Mx + 2 * lseq);
+                        if (lps < 0) lps = 0;
+                        lpe = RI(pos);
+                        if (mrev) sv_range(X, r, lps, lpe, CL_INV_R1, (double)tlen, tol_inv, 0, 2);
+                        else sv_range(X, r, lps, lpe, CL_DUP_R, (double)tlen, tol, 0, 2);
+                    }
+                }
+            } else {
+                if (rev && !mrev) {
+                    if (abs(tlen) >= Mn && abs(tlen) <= Mx) {
+                        /* split read over a tandem duplication, GROM.c:9359-9727 */
+                        int sr_dup = 0;
+                        if (r->aux_pos >= 0 && r->aux_same_chr && r->aux_mq >= X->min_mapq && r->mq >= X->min_mapq &&
+                            rev && r->aux_strand == 1 && r->aux_pos < pos && mpos < r->aux_pos) {
+                            int eai_t = eai > 0 ? eai : 0;
+                            int aeai_t = aeai > 0 ? eai : 0; /* sic, GROM.c:9381 */
+                            if (abs(lseq - asa - ea) <= X->max_split_loss && lseq - sa - ea - eai_t >= X->min_sr_len &&
+                                lseq - asa - aea - aeai_t >= X->min_sr_len) {
+                                lps = RI(r->aux_pos);
+                                lpe = RI(E);
+                                if (lps < lpe) sr_dup = 1;
+                            }
+                        }
+                        if (sr_dup == 1) {
+                            const double v = (double)(lpe - lps - X->mean);
+                            *X->rd(X->u, AX(lpe)) += 1;
+                            sv_ev e1 = {CL_DUP_F, r->add, (double)r->add, r->add, v, tol,
+                                        pos < r->aux_pos ? r->aux_pos : pos, RM_MINMAX, 0, 0, 2};
+                            sv_ev_at(X, lpe, &e1);
+                            *X->rd(X->u, AX(lps - 1)) += 1;
+                            sv_ev e2 = {CL_DUP_R, r->add, (double)r->add, r->add, v, tol,
+                                        pos < r->aux_pos ? pos : r->aux_pos, RM_MINMAX, 0, 0, 0};
+                            sv_ev_at(X, lps - 1, &e2);
+                        }
+                    } else if (abs(tlen) > 2 * Mx) {
+                        /* GROM.c:9730-9867 */
+                        lps = RI(pos - sa - Mx + 2 * lseq);
+                        if (lps < 0) lps = 0;
+                        lpe = RI(pos);
+                        sv_range(X, r, lps, lpe, CL_DEL_R, (double)abs(tlen), tol, 0, 2);
+                    }
+                } else if (!rev && !mrev) {
+                    /* GROM.c:9876-10019 */
+                    if (pos - mpos >= 10) {
+                        lps = RI(E);
+                        lpe = RI(pos - sa - eai + Mx - lseq);
+                        if (R < lpe) lpe = R;
+                        sv_range(X, r, lps, lpe, CL_INV_F2, (double)abs(tlen), tol_inv, 0, 1);
+                    }
+                } else if (mrev) {
+                    /* GROM.c:10023-10312 */
+                    if (pos - mpos >= 10) {
+                        if (!rev) {
+                            lps = RI(E);
+                            lpe = RI(pos - sa - eai + Mx - lseq);
+                            if (R < lpe) lpe = R;
+                            sv_range(X, r, lps, lpe, CL_DUP_F, (double)abs(tlen), tol, 0, 1);
+                        } else {
+                            lps = RI(pos - sa - Mx + 2 * lseq);
+                            if (lps < RI(mpos + lseq)) lps = RI(mpos + lseq);
+                            lpe = RI(pos);
+                            sv_range(X, r, lps, lpe, CL_INV_R2, (double)abs(tlen), tol_inv, 0, 2);
+                        }
+                    }
+                }
+            }
+        } else {
+            /* mate on another chromosome, GROM.c:10321-10903 */
+            if (!rev) {
+                lps = RI(E);
+                lpe = RI(pos - sa - eai + Mx - lseq);
+                if (R < lpe) lpe = R;
+                if (!mrev) sv_range(X, r, lps, lpe, CL_CTX_F, (double)mpos, tol, 1, 1);
+                else sv_range(X, r, lps, lpe, CL_CTX_F, (double)(-mpos), tol, 2, 1);
+            } else {
+                lps = RI(pos - sa + lseq - Mx + lseq);
+                if (lps < 0) lps = 0;
+                lpe = RI(pos);
+                if (!mrev) sv_range(X, r, lps, lpe, CL_CTX_R, (double)mpos, tol, 1, 2);
+                else sv_range(X, r, lps, lpe, CL_CTX_R, (double)(-mpos), tol, 2, 2);
+            }
+        }
+    } else if (paired && munmap) {
+        /* mate unmapped, GROM.c:10908-10952 */
+        const int k = rev ? 1 : 0;
+        if (!rev) {
+            lps = RI(E);
+            lpe = RI(pos - sa - eai + Mx - lseq);
+            if (R < lpe) lpe = R;
+        } else {
+            lps = RI(pos - sa + lseq + eai - Mx + lseq);
+            if (lps < 0) lps = 0;
+            lpe = RI(pos);
+        }
+        X->ring->mset[k][0] = X->ring->mset[k][1] = 1;
+        for (int a = lps; a < lpe; a++) {
+            *X->rd(X->u, AX(a)) += 1;
+            X->ring->mun[k][a] += r->add;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * Per-base tests (row A10, GROM.c:11340-13553).  `sv_base` holds the window
+ * values the tests read at p (and the two read at p+1).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    int32_t rd, sc_rd, indel_sc_rd;
+    int32_t sc_left, sc_right, sc_left_rd, sc_right_rd, indel_sc_left, indel_sc_right;
+    int32_t sc_left_next, sc_left_rd_next; /* at p + 1 */
+    int32_t snv_all;                       /* sum of snv[4] + snv_lowmq[4] */
+    int32_t conc, ins;
+    int32_t indel_i, indel_idist, indel_d_f, indel_d_f_rd, indel_d_r, indel_d_rdist, indel_d_r_rd;
+    const char *ins_seq;
+} sv_base;
+
+typedef struct {
+    const double *mq, *hez; /* (MAX_TRIALS+1)^2, row-major: the reference indexes past a row as the flat array does */
+    int min_disc, Mx, Mn, mean, glseq, sc_range;
+    double pval1, pval_ins1, max_evidence_ratio, range_mult;
+} sv_eval_prm;
+
+#define SV_AF 6    /* cdp_add_factor, GROM.c:1548 */
+#define SV_MT 1000 /* g_max_trials */
+#define TMQ(n, k) (E->mq[(long)(n) * (SV_MT + 1) + (k)])
+#define THZ(n, k) (E->hez[(long)(n) * (SV_MT + 1) + (k)])
+
+/* binomial test of a breakpoint count (GROM.c:11968-12006 and nine copies).
+ * The evidence-ratio check reads (rn_hi, rden_hi) above g_max_trials and
+ * (rn_lo, rden_lo) otherwise: they differ only for CTX_R. */
+static void sv_test(const sv_eval_prm *E, int cnt, int rd, int scmu, int rn_hi, int rden_hi, int rn_lo, int rden_lo,
+                    double *binom, double *hez) {
+    *hez = 2.0;
+    if (rd > SV_MT) {
+        *binom = TMQ(SV_MT, cnt * SV_MT / (SV_AF * rd));
+        if ((float)rn_hi / (float)rden_hi <= E->max_evidence_ratio) {
+            if ((cnt + scmu) / SV_AF < rd) *hez = THZ(SV_MT, (cnt + scmu) * SV_MT / (SV_AF * rd));
+            else *hez = THZ(SV_MT, SV_MT);
+        }
+    } else {
+        *binom = TMQ(rd, cnt / SV_AF);
+        if ((float)rn_lo / (float)rden_lo <= E->max_evidence_ratio) {
+            if ((cnt + scmu) / SV_AF < rd) *hez = THZ(rd, (cnt + scmu) / SV_AF);
+            else *hez = THZ(rd, rd);
+        }
+    }
+}
+
+/* The reference's inlined bisect over a start list (GROM.c:12270-12345):
+ * an interpolated first guess from list[end] (one past the last entry, -1),
+ * then a bisection; type 0 rounds up, type 1 down. */
+static int sv_bisect(const int32_t *(*at)(const void *, int), const void *lst, int pos, int start, int end, int type) {
+    int range = end / 64;
+    if (range < 4) range = 4;
+    else if (range > 64) range = 64;
+    const double guess = round((double)pos * (double)end / (double)*at(lst, end));
+    /* (int) of an out-of-range double is INT_MIN (cvttsd2si) */
+    double glo = guess - range, ghi = guess + range;
+    int lo = (glo != glo || glo >= 2147483648.0 || glo < -2147483648.0) ? (int)0x80000000u : (int)glo;
+    int hi = (ghi != ghi || ghi >= 2147483648.0 || ghi < -2147483648.0) ? (int)0x80000000u : (int)ghi;
+    if (lo < start || lo >= end) lo = start;
+    else if (*at(lst, lo) > pos) { hi = lo; lo = start; }
+    if (hi > end || hi < start) hi = end;
+    else if (*at(lst, hi) < pos) { lo = hi; hi = end; }
+    int idx = lo + (hi - lo) / 2;
+    for (;;) {
+        if (pos < *at(lst, idx)) {
+            hi = idx;
+            idx = lo + (idx - lo) / 2;
+            if (hi == idx) break;
+        } else if (pos > *at(lst, idx)) {
+            lo = idx;
+            idx = idx + (hi - idx) / 2;
+            if (lo == idx) break;
+        } else break;
+    }
+    if (type == 0 && pos > *at(lst, idx) && idx < end) idx += 1;
+    else if (type == 1 && pos < *at(lst, idx) && idx > start) idx -= 1;
+    return idx;
+}
+static const int32_t *pr_start_at(const void *l, int i) { return &((const pr_ent *)l)[i].start; }
+
+/* end breakpoint matched against the start list (DUP_F GROM.c:12247-12470,
+ * DEL_R 12595-12844, INV_F2 12969-13193, INV_R2 13316-13541) */
+static void sv_match_end(const sv_eval_prm *E, pr_ent *lst, int n, int p, double base, int off, int cnt, double binom,
+                         double hez, int tie_ge, int32_t conc, int32_t rd, int32_t rs, int32_t re, int other) {
+    const int mn = (int)((base - E->range_mult * (double)(E->Mx - E->Mn)) + (double)0.5);
+    const int mx = (int)((base + E->range_mult * (double)(E->Mx - E->Mn)) + (double)0.5);
+    int lps = sv_bisect(pr_start_at, lst, p + off - mn, 0, n, 0);
+    int lpe = sv_bisect(pr_start_at, lst, p + off - mx, 0, n, 1);
+    if (lpe < lps) { int t = lpe; lpe = lps; lps = t; }
+    const int sp = p + off - mx, ep = p + off - mn;
+    for (int a = lps; a < lpe; a++) {
+        pr_ent *q = &lst[a];
+        if (q->dist >= mn && q->dist <= mx && q->start >= sp && q->start <= ep) {
+            if ((q->binom_e > binom && cnt >= q->cnt_e) || q->end == -1 ||
+                (q->binom_e == binom && (tie_ge ? cnt >= q->cnt_e : cnt > q->cnt_e))) {
+                q->end = p;
+                q->binom_e = binom;
+                q->hez_e = hez;
+                q->conc_e = conc;
+                q->rd_e = rd;
+                q->cnt_e = cnt;
+                q->rs_e = rs;
+                q->re_e = re;
+                q->other_e = other;
+            }
+        }
+    }
+}
+
+static void sv_append_start(sv_lists *L, int k, int p, double dist, double binom, double hez, int32_t conc, int32_t rd,
+                            int cnt, int32_t rs, int32_t re, int other) {
+    if (L->n_pr[k] < L->cap - 1) {
+        pr_ent *q = &L->pr[k][L->n_pr[k]];
+        q->start = p;
+        q->dist = dist;
+        q->binom_s = binom;
+        q->hez_s = hez;
+        q->conc_s = conc;
+        q->rd_s = rd;
+        q->cnt_s = cnt;
+        q->rs_s = rs;
+        q->re_s = re;
+        q->other_s = other;
+        L->n_pr[k] += 1;
+    }
+}
+
+static void sv_eval(const sv_eval_prm *E, sv_lists *L, const sv_ring *ring, int i, int p, const sv_base *B,
+                    int cur_lseq) {
+    const int AF = SV_AF;
+    double binom, hez;
+    const int other = sv_other_len(ring, i);
+    if (B->rd + B->indel_sc_rd > 0) {
+        /* (the SNV test runs here, in grom_oracle.c) */
+        /* insertion from CIGAR I ops, GROM.c:11338-11453 */
+        int irt = B->snv_all;
+        int it = B->indel_i;
+        if (it / AF > irt) it = irt * AF;
+        if (it / AF >= E->min_disc && irt <= SV_MT) {
+            binom = TMQ(irt, it / AF);
+            if ((it + B->indel_sc_left) / AF < irt) {
+                hez = THZ(irt, (it + B->indel_sc_left) / AF);
+                if ((it + B->indel_sc_right) / AF < irt) {
+                    if (THZ(irt, (it + B->indel_sc_right) / AF) > hez) hez = THZ(irt, (it + B->indel_sc_right) / AF);
+                } else {
+                    hez = THZ(irt, irt);
+                }
+            } else {
+                hez = THZ(irt, irt);
+            }
+            if (binom <= E->pval1) {
+                if (L->n_ii < L->cap - 1) {
+                    ii_ent *q = &L->ii[L->n_ii];
+                    q->start = p;
+                    q->binom = binom;
+                    q->hez = hez;
+                    q->dist = B->indel_idist;
+                    q->conc_s = B->conc;
+                    q->i = it;
+                    q->sc = B->sc_left_next + B->sc_right;
+                    q->rd = irt;
+                    if (q->dist <= SV_OTHER)
+                        for (int k = 0; k < q->dist; k++) q->seq[k] = B->ins_seq[k];
+                    q->other_s = other;
+                    L->n_ii += 1;
+                }
+            }
+        }
+        /* deletion start, GROM.c:11460-11629 */
+        irt = B->indel_d_f / AF + B->snv_all;
+        int dft = B->indel_d_f;
+        if (dft / AF >= E->min_disc && irt <= SV_MT) {
+            binom = TMQ(irt, dft / AF);
+            hez = ((dft + B->indel_sc_right) / AF < irt) ? THZ(irt, (dft + B->indel_sc_right) / AF) : THZ(irt, irt);
+            if (binom <= E->pval1) {
+                int set = 0;
+                if (L->n_id == -1) { L->n_id = 0; set = 1; }
+                else if (L->id[L->n_id].start != -1 && L->id[L->n_id].end != -1) {
+                    if (L->n_id < L->cap - 1) { L->n_id += 1; set = 1; }
+                } else if ((p - L->id[L->n_id].start > E->glseq && L->id[L->n_id].end == -1) ||
+                           binom < L->id[L->n_id].binom_s) {
+                    set = 2;
+                }
+                if (set) {
+                    id_ent *q = &L->id[L->n_id];
+                    q->start = p;
+                    q->binom_s = binom;
+                    q->hez_s = hez;
+                    q->conc_s = B->conc;
+                    if (set == 2 && q->end < q->start) q->end = -1;
+                    q->f = dft;
+                    q->sc_s = B->sc_right;
+                    q->rd_s = irt;
+                    q->other_s = other;
+                }
+            }
+        }
+        /* deletion end, GROM.c:11631-11745 */
+        irt = B->indel_d_r / AF + B->snv_all;
+        int drt = B->indel_d_r;
+        if (L->n_id >= 0 && drt / AF >= E->min_disc && irt <= SV_MT) {
+            binom = TMQ(irt, drt / AF);
+            hez = ((drt + B->indel_sc_left) / AF < irt) ? THZ(irt, (drt + B->indel_sc_left) / AF) : THZ(irt, irt);
+            if (binom <= E->pval1) {
+                id_ent *q = &L->id[L->n_id];
+                /* float arithmetic, GROM.c:11670 */
+                volatile float fp = (float)p, fs = (float)q->start;
+                volatile float d = fp - fs;
+                d = d - (float)B->indel_d_rdist;
+                if ((d < 5.0f && q->start != -1 && q->end != -1) ||
+                    (d < 5.0f && (q->end == -1 || binom < q->binom_e))) {
+                    q->end = p;
+                    q->binom_e = binom;
+                    q->hez_e = hez;
+                    q->conc_e = B->conc;
+                    q->r = drt;
+                    q->sc_e = B->sc_left;
+                    q->rd_e = irt;
+                    q->other_e = other;
+                }
+            }
+        }
+    }
+    if (B->rd + B->sc_rd > 0) {
+        /* soft-clip insertion start/end, GROM.c:11750-11960 */
+        for (int side = 0; side < 2; side++) {
+            const int sc = side == 0 ? B->sc_left : B->sc_right;
+            const int mu = side == 0 ? ring->mun[1][i] : ring->mun[0][i];
+            const int rdt = B->rd + (side == 0 ? B->sc_left_rd : B->sc_right_rd);
+            if ((sc + B->ins) / AF >= E->min_disc && rdt <= SV_MT) {
+                if ((mu + sc + B->ins) / AF < rdt) binom = TMQ(rdt, (mu + sc + B->ins) / AF);
+                else binom = TMQ(rdt, rdt);
+                if (binom <= E->pval_ins1) {
+                    int set = 0;
+                    if (L->n_ins == -1) { L->n_ins = 0; set = 1; }
+                    else {
+                        ins_ent *c = &L->ins[L->n_ins];
+                        if ((p - c->start > E->sc_range && c->start != -1) || (p - c->end > E->sc_range && c->end != -1)) {
+                            if (L->n_ins < L->cap - 1) { L->n_ins += 1; set = 1; }
+                        } else if (side == 0 ? (c->start == -1 || binom < c->binom_s) : (c->end == -1 || binom < c->binom_e)) {
+                            set = 1;
+                        }
+                    }
+                    if (set) {
+                        ins_ent *q = &L->ins[L->n_ins];
+                        if (side == 0) {
+                            q->start = p; q->binom_s = binom; q->ins_s = B->ins; q->rd_s = B->rd; q->conc_s = B->conc; q->other_s = other;
+                        } else {
+                            q->end = p; q->binom_e = binom; q->ins_e = B->ins; q->rd_e = B->rd; q->conc_e = B->conc; q->other_e = other;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (B->rd > 0) {
+        const clus_t *cf = &ring->cl[CL_CTX_F][i], *cr = &ring->cl[CL_CTX_R][i];
+        const int scr_muf = B->sc_right + ring->mun[0][i], scl_mur = B->sc_left + ring->mun[1][i];
+        /* CTX_F, GROM.c:11966-12045 */
+        if (cf->cnt / AF >= E->min_disc && p - cf->re < E->mean) {
+            sv_test(E, cf->cnt, B->rd, scr_muf, scr_muf, cf->cnt, scr_muf, cf->cnt, &binom, &hez);
+            if (binom <= E->pval1 && L->n_cx[0] < L->cap - 1) {
+                ctx_ent *q = &L->cx[0][L->n_cx[0]++];
+                q->pos = p; q->binom = binom; q->hez = hez; q->mchr = ring->ctx_mchr[0][i];
+                q->mpos = (int32_t)cf->dist; q->conc = B->conc; q->rd = B->rd; q->cnt = cf->cnt;
+                q->rs = cf->rs; q->re = cf->re; q->other = other;
+            }
+        }
+        /* CTX_R, GROM.c:12047-12126 (its low-depth ratio check reads CTX_F, Q7) */
+        if (cr->cnt / AF >= E->min_disc && cr->rs + cur_lseq - p < E->mean) {
+            sv_test(E, cr->cnt, B->rd, scl_mur, scl_mur, cr->cnt, scr_muf, cf->cnt, &binom, &hez);
+            if (binom <= E->pval1 && L->n_cx[1] < L->cap - 1) {
+                ctx_ent *q = &L->cx[1][L->n_cx[1]++];
+                q->pos = p; q->binom = binom; q->hez = hez; q->mchr = ring->ctx_mchr[1][i];
+                q->mpos = (int32_t)cr->dist; q->conc = B->conc; q->rd = B->rd; q->cnt = cr->cnt;
+                q->rs = cr->rs; q->re = cr->re; q->other = other;
+            }
+        }
+        /* DUP_R start, GROM.c:12128-12205 */
+        const clus_t *c = &ring->cl[CL_DUP_R][i];
+        if (c->cnt / AF >= E->min_disc && c->rs + cur_lseq - p < E->mean) {
+            sv_test(E, c->cnt, B->rd, scl_mur, scl_mur, c->cnt, scl_mur, c->cnt, &binom, &hez);
+            if (binom <= E->pval1) sv_append_start(L, PR_DUP, p, c->dist, binom, hez, B->conc, B->rd, c->cnt, c->rs, c->re, other);
+        }
+        /* DUP_F end, GROM.c:12207-12472 */
+        c = &ring->cl[CL_DUP_F][i];
+        if (c->cnt / AF >= E->min_disc && p - c->re < E->mean) {
+            sv_test(E, c->cnt, B->rd, scr_muf, scr_muf, c->cnt, scr_muf, c->cnt, &binom, &hez);
+            if (binom <= E->pval1)
+                sv_match_end(E, L->pr[PR_DUP], L->n_pr[PR_DUP], p, c->dist + 2 * E->glseq, -E->mean + 2 * E->glseq, c->cnt,
+                             binom, hez, 0, B->conc, B->rd, c->rs, c->re, other);
+        }
+        /* DEL_F start, GROM.c:12474-12553 */
+        c = &ring->cl[CL_DEL_F][i];
+        if (c->cnt / AF >= E->min_disc && p - c->re < E->mean) {
+            sv_test(E, c->cnt, B->rd, scr_muf, scr_muf, c->cnt, scr_muf, c->cnt, &binom, &hez);
+            if (binom <= E->pval1) sv_append_start(L, PR_DEL, p, c->dist, binom, hez, B->conc, B->rd, c->cnt, c->rs, c->re, other);
+        }
+        /* DEL_R end, GROM.c:12555-12846 */
+        c = &ring->cl[CL_DEL_R][i];
+        if (c->cnt / AF >= E->min_disc && c->rs + cur_lseq - p < E->mean) {
+            sv_test(E, c->cnt, B->rd, scl_mur, scl_mur, c->cnt, scl_mur, c->cnt, &binom, &hez);
+            if (binom <= E->pval1)
+                sv_match_end(E, L->pr[PR_DEL], L->n_pr[PR_DEL], p, c->dist, E->mean, c->cnt, binom, hez, 1, B->conc, B->rd,
+                             c->rs, c->re, other);
+        }
+        /* INV_F1 start, GROM.c:12848-12927 */
+        c = &ring->cl[CL_INV_F1][i];
+        if (c->cnt / AF >= E->min_disc && p - c->re < E->mean) {
+            sv_test(E, c->cnt, B->rd, scr_muf, scr_muf, c->cnt, scr_muf, c->cnt, &binom, &hez);
+            if (binom <= E->pval1) sv_append_start(L, PR_INVF, p, c->dist, binom, hez, B->conc, B->rd, c->cnt, c->rs, c->re, other);
+        }
+        /* INV_F2 end, GROM.c:12929-13195 */
+        c = &ring->cl[CL_INV_F2][i];
+        if (c->cnt / AF >= E->min_disc && p - c->re < E->mean) {
+            sv_test(E, c->cnt, B->rd, scr_muf, scr_muf, c->cnt, scr_muf, c->cnt, &binom, &hez);
+            if (binom <= E->pval1)
+                sv_match_end(E, L->pr[PR_INVF], L->n_pr[PR_INVF], p, c->dist + E->glseq, E->glseq, c->cnt, binom, hez, 0,
+                             B->conc, B->rd, c->rs, c->re, other);
+        }
+        /* INV_R1 start, GROM.c:13197-13274 */
+        c = &ring->cl[CL_INV_R1][i];
+        if (c->cnt / AF >= E->min_disc && c->rs + cur_lseq - p < E->mean) {
+            sv_test(E, c->cnt, B->rd, scl_mur, scl_mur, c->cnt, scl_mur, c->cnt, &binom, &hez);
+            if (binom <= E->pval1) sv_append_start(L, PR_INVR, p, c->dist, binom, hez, B->conc, B->rd, c->cnt, c->rs, c->re, other);
+        }
+        /* INV_R2 end, GROM.c:13276-13543 */
+        c = &ring->cl[CL_INV_R2][i];
+        if (c->cnt / AF >= E->min_disc && c->rs + cur_lseq - p < E->mean) {
+            sv_test(E, c->cnt, B->rd, scl_mur, scl_mur, c->cnt, scl_mur, c->cnt, &binom, &hez);
+            if (binom <= E->pval1)
+                sv_match_end(E, L->pr[PR_INVR], L->n_pr[PR_INVR], p, c->dist + E->glseq, E->glseq, c->cnt, binom, hez, 0,
+                             B->conc, B->rd, c->rs, c->re, other);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * SV assembly and rows (row A13, GROM.c:15163-16580)
+ * ------------------------------------------------------------------------ */
+
+/* list -> list2 merge of a start/end pair list (DUP GROM.c:15163-15318; DEL,
+ * INV_F and INV_R are the same code over their lists) */
+static int sv_merge_pairs(const pr_ent *lst, int n, pr_ent *l2, int cap2, int Mx, int glseq) {
+    int n2 = 0, begin = 0;
+    int first_start = 0, last_start = 0, first_end = 0, last_end = 0;
+    double first_dist = 0, last_dist = 0;
+    for (int a = 0; a < n; a++) {
+        const pr_ent *q = &lst[a];
+        if (begin == 1) {
+            if (q->start > last_start + Mx - 2 * glseq) {
+                begin = 0;
+                first_start = last_start = first_end = last_end = 0;
+                first_dist = last_dist = 0;
+            } else {
+                pr_ent *t = &l2[n2 - 1];
+                double mb = q->binom_s;
+                if (q->binom_e > mb) mb = q->binom_e;
+                double mb2 = t->binom_s;
+                if (t->binom_e > mb2) mb2 = t->binom_e;
+                if (mb <= mb2 && q->start >= 0 && q->end >= 0 && t->cnt_s <= q->cnt_s && t->cnt_e <= q->cnt_e) {
+                    int replace = 0;
+                    if (q->binom_s == t->binom_s && q->binom_e == t->binom_e) {
+                        if ((t->cnt_s < q->cnt_s && t->cnt_e <= q->cnt_e) || (t->cnt_s <= q->cnt_s && t->cnt_e < q->cnt_e)) {
+                            replace = 1;
+                        } else if (t->cnt_s == q->cnt_s && t->cnt_e == q->cnt_e) {
+                            last_start = q->start;
+                            last_end = q->end;
+                            last_dist = q->dist;
+                            int32_t cs = t->cnt_s, ce = t->cnt_e;
+                            *t = *q;
+                            t->cnt_s = cs;
+                            t->cnt_e = ce;
+                            t->start = (first_start + last_start) / 2;
+                            t->end = (first_end + last_end) / 2;
+                            t->dist = (first_dist + last_dist) / (double)(2.0);
+                        }
+                    } else {
+                        replace = 1;
+                    }
+                    if (replace) {
+                        first_start = last_start = q->start;
+                        first_end = last_end = q->end;
+                        first_dist = last_dist = q->dist;
+                        *t = *q;
+                    }
+                }
+            }
+        }
+        if (begin == 0) {
+            if (q->start >= 0 && q->end >= 0) {
+                if (n2 < cap2 - 1) {
+                    begin = 1;
+                    first_start = last_start = q->start;
+                    first_end = last_end = q->end;
+                    first_dist = last_dist = q->dist;
+                    l2[n2++] = *q;
+                }
+            }
+        }
+    }
+    return n2;
+}
+
+/* reference bases over [lo, hi) of the whole-chromosome depth arrays */
+static double sv_caf_sum(const int32_t *rd, const int32_t *low, long len, long lo, long hi) {
+    double s = 0;
+    for (long b = lo; b < hi; b++)
+        if (b >= 0 && b < len) s += rd[b] + low[b];
+    return s;
+}
+
+typedef struct {
+    int Mx, glseq, vcf, ploidy_unused;
+    double pval, pval_ins, min_sv_ratio, min_indel_ratio, max_inv_rd_diff, min_overlap_ratio;
+    int max_homopolymer, max_ins_range;
+} sv_out_prm;
+
+static void pr_row(FILE *f, const char *chr, const char *alt, const pr_ent *q) {
+    fprintf(f,
+            "%s\t%d\t.\t.\t%s\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT:SFR:SLR:EFR:ELR\t%e:%e:%.1f:%.1f:%d:%d:%d:%d:%d:"
+            "%d:%d:%d:%d:%d\n",
+            chr, q->start + 1, alt, q->end + 1, q->binom_s, q->binom_e, (double)q->cnt_s / (double)SV_AF,
+            (double)q->cnt_e / (double)SV_AF, q->rd_s, q->rd_e, q->conc_s, q->conc_e, q->other_s, q->other_e,
+            q->rs_s + 1, q->re_s + 1, q->rs_e + 1, q->re_e + 1);
+}
+
+static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, const char *fasta, long chr_len,
+                          const int32_t *caf_rd, const int32_t *caf_low, FILE *vcf, FILE *ctx) {
+    const int AF = SV_AF;
+    const int span = O->Mx - 2 * O->glseq;
+    pr_ent *l2[4];
+    int n2[4];
+    for (int k = 0; k < 4; k++) {
+        l2[k] = (pr_ent *)calloc(L->cap2 + 1, sizeof(pr_ent));
+        n2[k] = sv_merge_pairs(L->pr[k], L->n_pr[k], l2[k], L->cap2, O->Mx, O->glseq);
+    }
+    /* DUP rows, GROM.c:15320-15334 */
+    for (int a = 0; a < n2[PR_DUP]; a++) {
+        const pr_ent *q = &l2[PR_DUP][a];
+        if ((q->binom_s <= O->pval || q->hez_s <= O->pval) && (q->binom_e <= O->pval || q->hez_e <= O->pval) &&
+            (double)q->cnt_s / (double)q->rd_s >= O->min_sv_ratio * (double)AF &&
+            (double)q->cnt_e / (double)q->rd_e >= O->min_sv_ratio * (double)AF)
+            pr_row(vcf, chr, "<DUP>", q);
+    }
+    /* INV rows: each orientation is dropped when the other one overlaps it
+     * with a smaller p-value product, or when the depth at the two ends
+     * differs (GROM.c:15795-15890) */
+    for (int side = 0; side < 2; side++) {
+        const pr_ent *A = l2[side == 0 ? PR_INVF : PR_INVR], *Bl = l2[side == 0 ? PR_INVR : PR_INVF];
+        const int na = n2[side == 0 ? PR_INVF : PR_INVR], nb = n2[side == 0 ? PR_INVR : PR_INVF];
+        for (int a = 0; a < na; a++) {
+            const pr_ent *q = &A[a];
+            int overlap = 0;
+            if (q->binom_s <= O->pval && q->binom_e <= O->pval && (double)q->cnt_s / (double)q->rd_s >= O->min_sv_ratio * (double)AF &&
+                (double)q->cnt_e / (double)q->rd_e >= O->min_sv_ratio * (double)AF) {
+                for (int b = 0; b < nb; b++) {
+                    const pr_ent *o = &Bl[b];
+                    if (abs(q->start - o->start) < span && abs(q->end - o->end) < span) {
+                        if ((q->start >= o->start && q->start <= o->end) || (o->start >= q->start && o->start <= q->end)) {
+                            int better = side == 0 ? (o->binom_s * o->binom_e < q->binom_s * q->binom_e)
+                                                   : (o->binom_s * o->binom_e <= q->binom_s * q->binom_e);
+                            if (better) { overlap = 1; break; }
+                        }
+                    }
+                }
+                double r1 = sv_caf_sum(caf_rd, caf_low, chr_len, q->rs_s, (long)q->re_s + O->glseq);
+                r1 = r1 / (q->re_s + O->glseq - q->rs_s);
+                double r2 = sv_caf_sum(caf_rd, caf_low, chr_len, q->rs_e, (long)q->re_e + O->glseq);
+                r2 = r2 / (q->re_e + O->glseq - q->rs_e);
+                if (overlap == 0 && r1 / r2 <= O->max_inv_rd_diff && r2 / r1 <= O->max_inv_rd_diff) pr_row(vcf, chr, "<INV>", q);
+            }
+        }
+    }
+    /* INS: start/end merge and rows, GROM.c:15897-15968 */
+    {
+        ins_ent *i2 = (ins_ent *)calloc(L->cap2 + 1, sizeof(ins_ent));
+        int n = 0, begin = 0;
+        for (int a = 0; a < L->n_ins; a++) {
+            const ins_ent *q = &L->ins[a];
+            if (begin == 1) {
+                const ins_ent *t = &i2[n - 1];
+                if (q->start > t->start + span || q->start > t->end + span || q->end > t->start + span || q->end > t->end + span) {
+                    begin = 0;
+                } else if (q->binom_s <= t->binom_s && q->start >= 0 && q->binom_e <= t->binom_e && q->end >= 0) {
+                    i2[n - 1] = *q;
+                }
+            }
+            if (begin == 0 && q->start >= 0 && q->end >= 0) {
+                if (L->n_ins < L->cap2 - 1) { /* sic: the guard reads ins_list_index, GROM.c:15935 */
+                    begin = 1;
+                    i2[n++] = *q;
+                }
+            }
+        }
+        for (int a = 0; a < n; a++) {
+            const ins_ent *q = &i2[a];
+            if (q->binom_s <= O->pval_ins && q->binom_e <= O->pval_ins && abs(q->end - q->start) <= O->max_ins_range)
+                fprintf(vcf, "%s\t%d\t.\t.\t<INS>\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT\t%e:%e:%.1f:%.1f:%d:%d:%d:%d:%d:%d\n",
+                        chr, q->start + 1, q->start + 1, q->binom_s, q->binom_e, (double)q->ins_s / (double)AF,
+                        (double)q->ins_e / (double)AF, q->rd_s, q->rd_e, q->conc_s, q->conc_e, q->other_s, q->other_e);
+        }
+        free(i2);
+    }
+    /* CTX_F / CTX_R: merge and raw rows for main's post-pass, GROM.c:15970-16248 */
+    for (int k = 0; k < 2; k++) {
+        ctx_ent *c2 = (ctx_ent *)calloc(L->cap2 + 1, sizeof(ctx_ent));
+        int n = 0, begin = 0;
+        for (int a = 0; a < L->n_cx[k]; a++) {
+            const ctx_ent *q = &L->cx[k][a];
+            if (begin == 1) {
+                ctx_ent *t = &c2[n - 1];
+                if (q->pos > t->pos + span) begin = 0;
+                else if (((q->binom < t->binom && t->cnt <= q->cnt) || (q->binom == t->binom && t->cnt < q->cnt)) && q->pos >= 0)
+                    *t = *q;
+            }
+            if (begin == 0 && q->pos >= 0 && n < L->cap2 - 1) {
+                begin = 1;
+                c2[n++] = *q;
+            }
+        }
+        for (int a = 0; a < n; a++) {
+            const ctx_ent *q = &c2[a];
+            if ((q->binom <= O->pval || q->hez <= O->pval) && (double)q->cnt / (double)q->rd >= O->min_sv_ratio * (double)AF)
+                fprintf(ctx, "%s\t%s\t%d\t%e\t%.1f\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%e\n", k == 0 ? "CTX_F" : "CTX_R", chr, q->pos,
+                        q->binom, (double)q->cnt / (double)AF, q->rd, q->conc, q->other, q->mchr, q->mpos, q->rs, q->re,
+                        q->hez);
+        }
+        free(c2);
+    }
+    /* INDEL_INS rows, GROM.c:16250-16330 */
+    char gts[101];
+    for (int a = 0; a < L->n_ii; a++) {
+        const ii_ent *q = &L->ii[a];
+        if (!(q->binom <= O->pval && (double)q->i / (double)q->rd > O->min_indel_ratio * (double)AF)) continue;
+        int hp = 1;
+        char hc = fasta[q->start];
+        for (int b = 1; b < 20; b++) {
+            if (q->start - b >= 0) {
+                if (hc == fasta[q->start - b]) hp += 1;
+                else break;
+            } else break;
+        }
+        int hp2 = 1;
+        if (fasta[q->start] + 1 < chr_len) { /* sic: a base letter plus one, GROM.c:16282 */
+            hc = (char)(fasta[q->start] + 1);
+            for (int b = 1; b < 20; b++) {
+                if (q->start + b + 1 < chr_len) {
+                    if (hc == fasta[q->start + b + 1]) hp2 += 1;
+                    else break;
+                } else break;
+            }
+        }
+        if (hp2 > hp) hp = hp2;
+        if (hp > O->max_homopolymer) continue;
+        if (q->dist <= SV_OTHER) {
+            for (int b = 0; b < q->dist; b++) gts[b] = q->seq[b];
+            gts[q->dist] = 0;
+        } else {
+            strcpy(gts, "<INS>");
+        }
+        fprintf(vcf, "%s\t%d\t.\t.\t%s\t.\t.\tEND=%d\tSPR:SEV:SRD:SCO:ECO:SOT:EOT:SSC:HP\t%e:%.1f:%d:%d:%d:%d:%d:%d:%d\n", chr,
+                q->start + 1, gts, q->end + 1, q->binom, (double)q->i / (double)AF, q->rd, q->conc_s, q->conc_e, q->other_s,
+                q->other_e, q->sc, hp);
+    }
+    /* INDEL_DEL rows, dropped when a <DEL> call overlaps with a smaller p-value
+     * product, GROM.c:16336-16470 */
+    const pr_ent *d2 = l2[PR_DEL];
+    const int nd2 = n2[PR_DEL];
+    /* the loops stop before the open last entry (index, not count: GROM.c:16336) */
+    for (int a = 0; a < L->n_id; a++) {
+        const id_ent *q = &L->id[a];
+        if (!(q->binom_s <= O->pval && q->binom_e <= O->pval && (double)q->f / (double)q->rd_s > O->min_indel_ratio * (double)AF &&
+              (double)q->r / (double)q->rd_e > O->min_indel_ratio * (double)AF))
+            continue;
+        int overlap = 0;
+        for (int b = 0; b < nd2; b++) {
+            const pr_ent *o = &d2[b];
+            if (abs(o->start - q->start) < span && abs(o->end - q->end) < span) {
+                double r1 = 0, r2 = 0;
+                if (o->start >= q->start && o->start <= q->end) {
+                    if (o->end >= q->end) {
+                        r1 = (double)(q->end - o->start) / (double)(q->end - q->start);
+                        r2 = (double)(q->end - o->start) / (double)(o->end - o->start);
+                    } else {
+                        r1 = (double)(o->end - o->start) / (double)(q->end - q->start);
+                        /* sic: del_list2_end[a_loop] with the indel's index, GROM.c:16366 */
+                        r2 = (double)(d2[a].end - o->start) / (double)(o->end - o->start);
+                    }
+                } else if (q->start >= o->start && q->start <= o->end) {
+                    if (o->end >= q->end) {
+                        r1 = (double)(q->end - q->start) / (double)(q->end - q->start);
+                        r2 = (double)(q->end - q->start) / (double)(o->end - o->start);
+                    } else {
+                        r1 = (double)(o->end - q->start) / (double)(q->end - q->start);
+                        r2 = (double)(o->end - q->start) / (double)(o->end - o->start);
+                    }
+                }
+                if (r1 >= O->min_overlap_ratio && r2 >= O->min_overlap_ratio && o->binom_s * o->binom_e < q->binom_s * q->binom_e) {
+                    overlap = 1;
+                    break;
+                }
+            }
+        }
+        if (overlap) continue;
+        int hp = 1;
+        if (fasta[q->start] - 1 >= 0) {
+            char hc = fasta[q->start - 1];
+            for (int b = 1; b < 20; b++) {
+                if (q->start - b - 1 >= 0) {
+                    if (hc == fasta[q->start - b - 1]) hp += 1;
+                    else break;
+                } else break;
+            }
+        }
+        int hp2 = 1;
+        if (fasta[q->end] + 1 < chr_len) {
+            char hc = (char)(fasta[q->end] + 1);
+            for (int b = 1; b < 20; b++) {
+                if (q->end + b + 1 < chr_len) {
+                    if (hc == fasta[q->end + b + 1]) hp2 += 1;
+                    else break;
+                } else break;
+            }
+        }
+        if (hp2 > hp) hp = hp2;
+        if (hp > O->max_homopolymer) continue;
+        int cn = q->end - q->start + 1;
+        if (cn > 0 && cn < 100 - 1) {
+            for (int b = 0; b < cn; b++) gts[b] = fasta[q->start + b];
+            gts[cn] = 0;
+            fprintf(vcf, "%s\t%d\t.\t%s\t.\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT:SSC:ESC:HP\t%e:%e:%.1f:%.1f:%d:%d:%d:%d:%d:%d:%d:%d:%d\n",
+                    chr, q->start + 1, gts, q->end + 1, q->binom_s, q->binom_e, (double)q->f / (double)AF, (double)q->r / (double)AF,
+                    q->conc_s, q->conc_e, q->other_s, q->other_e, q->rd_s, q->rd_e, q->sc_s, q->sc_e, hp);
+        } else {
+            fprintf(vcf, "%s\t%d\t.\t.\t<DEL>\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT:SSC:ESC:HP\t%e:%e:%.1f:%.1f:%d:%d:%d:%d:%d:%d:%d:%d:%d\n",
+                    chr, q->start + 1, q->end + 1, q->binom_s, q->binom_e, (double)q->f / (double)AF, (double)q->r / (double)AF,
+                    q->conc_s, q->conc_e, q->other_s, q->other_e, q->rd_s, q->rd_e, q->sc_s, q->sc_e, hp);
+        }
+    }
+    /* DEL rows, dropped when an indel deletion overlaps with a smaller or
+     * equal p-value product, GROM.c:16474-16580 */
+    for (int a = 0; a < nd2; a++) {
+        const pr_ent *q = &d2[a];
+        if (!((q->binom_s <= O->pval || q->hez_s <= O->pval) && (q->binom_e <= O->pval || q->hez_e <= O->pval) &&
+              (double)q->cnt_s / (double)q->rd_s >= O->min_sv_ratio * (double)AF &&
+              (double)q->cnt_e / (double)q->rd_e >= O->min_sv_ratio * (double)AF))
+            continue;
+        int overlap = 0;
+        for (int b = 0; b < L->n_id; b++) {
+            const id_ent *o = &L->id[b];
+            if (o->binom_s <= O->pval && o->binom_e <= O->pval && (double)o->f / (double)o->rd_s > O->min_indel_ratio * (double)AF &&
+                (double)o->r / (double)o->rd_e > O->min_indel_ratio * (double)AF && abs(q->start - o->start) < span &&
+                abs(q->end - o->end) < span) {
+                double r1 = 0, r2 = 0;
+                if (q->start >= o->start && q->start <= o->end) {
+                    if (q->end >= o->end) {
+                        r1 = (double)(o->end - q->start) / (double)(o->end - o->start);
+                        r2 = (double)(o->end - q->start) / (double)(q->end - q->start);
+                    } else {
+                        r1 = (double)(q->end - q->start) / (double)(o->end - o->start);
+                        r2 = (double)(q->end - q->start) / (double)(q->end - q->start);
+                    }
+                } else if (o->start >= q->start && o->start <= q->end) {
+                    if (q->end >= o->end) {
+                        r1 = (double)(o->end - o->start) / (double)(o->end - o->start);
+                        r2 = (double)(o->end - o->start) / (double)(q->end - q->start);
+                    } else {
+                        r1 = (double)(q->end - o->start) / (double)(o->end - o->start);
+                        r2 = (double)(q->end - o->start) / (double)(q->end - q->start);
+                    }
+                }
+                if (r1 >= O->min_overlap_ratio && r2 >= O->min_overlap_ratio && o->binom_s * o->binom_e <= q->binom_s * q->binom_e) {
+                    overlap = 1;
+                    break;
+                }
+            }
+        }
+        if (overlap == 0) pr_row(vcf, chr, "<DEL>", q);
+    }
+    for (int k = 0; k < 4; k++) free(l2[k]);
+}
+
+/* ------------------------------------------------------------------------
+ * main's CTX post-pass (GROM.c:22400-22770): read the raw CTX rows back,
+ * pair each breakpoint with its mate, keep the better of near-duplicates and
+ * rewrite the file as VCF BND rows.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    int type, chr, pos, rd, conc, other, mchr, mpos, rs, re, mateid, keep;
+    double binom, ev, hez;
+} ctx_row;
+
+static void sv_ctx_postpass(const char *ctx_path, char **bam_names_lc, int n_targets, int Mx, int glseq,
+                            void (*header)(FILE *)) {
+    FILE *f = fopen(ctx_path, "r");
+    if (!f) return;
+    int cap = 1024, n = 0;
+    ctx_row *rw = (ctx_row *)calloc(cap, sizeof(ctx_row));
+    char line[100000];
+    while (fgets(line, sizeof(line), f)) {
+        if (n == cap) { cap *= 2; rw = (ctx_row *)realloc(rw, cap * sizeof(ctx_row)); }
+        ctx_row *q = &rw[n];
+        memset(q, 0, sizeof(*q));
+        char *save = NULL, *t = strtok_r(line, "\t", &save);
+        q->type = -1;
+        if (t) q->type = strcmp(t, "CTX_F") == 0 ? 6 : strcmp(t, "CTX_R") == 0 ? 7 : -1; /* g_sv_types index */
+        t = strtok_r(NULL, "\t", &save);
+        q->chr = -1;
+        if (t) {
+            char lc[1024];
+            size_t L = strlen(t);
+            for (size_t b = 0; b < L && b < sizeof(lc) - 1; b++) lc[b] = (char)tolower((unsigned char)t[b]);
+            lc[L < sizeof(lc) - 1 ? L : sizeof(lc) - 1] = 0;
+            for (int a = 0; a < n_targets; a++)
+                if (strcmp(bam_names_lc[a], lc) == 0) { q->chr = a; break; }
+        }
+#define NEXT_I(fld) do { t = strtok_r(NULL, "\t", &save); q->fld = t ? atoi(t) : 0; } while (0)
+#define NEXT_D(fld) do { t = strtok_r(NULL, "\t", &save); q->fld = t ? atof(t) : 0; } while (0)
+        NEXT_I(pos); NEXT_D(binom); NEXT_D(ev); NEXT_I(rd); NEXT_I(conc); NEXT_I(other);
+        NEXT_I(mchr); NEXT_I(mpos); NEXT_I(rs); NEXT_I(re); NEXT_D(hez);
+#undef NEXT_I
+#undef NEXT_D
+        n++;
+    }
+    fclose(f);
+    const int span = Mx - 2 * glseq;
+    for (int b = 0; b < n; b++) { rw[b].keep = 0; rw[b].mateid = -1; }
+    for (int b = 0; b < n; b++) {
+        for (int c = 0; c < n; c++) {
+            if (rw[b].chr == rw[c].mchr && rw[c].chr == rw[b].mchr) {
+                if (abs(rw[b].pos - abs(rw[c].mpos)) < span && abs(rw[c].pos - abs(rw[b].mpos)) < span) {
+                    if (((rw[b].type == 6 && rw[c].mpos >= 0) || (rw[b].type == 7 && rw[c].mpos < 0)) &&
+                        ((rw[c].type == 6 && rw[b].mpos >= 0) || (rw[c].type == 7 && rw[b].mpos < 0))) {
+                        rw[b].keep = 1;
+                        rw[b].mateid = c;
+                        rw[b].mpos = rw[b].mpos < 0 ? -rw[c].pos : rw[c].pos;
+                    }
+                }
+            }
+        }
+    }
+    for (int b = 0; b < n; b++) {
+        for (int c = 0; c < n; c++) {
+            if (b != c && rw[b].chr == rw[c].chr && rw[b].mchr == rw[c].mchr) {
+                if (abs(rw[b].pos - rw[c].pos) < span && abs(abs(rw[b].mpos) - abs(rw[c].mpos)) < span) {
+                    if (rw[b].keep == 1 && rw[c].keep == 1 &&
+                        (rw[b].binom > rw[c].binom || (rw[b].binom == rw[c].binom && b > c))) {
+                        rw[b].keep = 0;
+                        if (rw[b].mateid >= 0) rw[rw[b].mateid].keep = 0;
+                    }
+                }
+            }
+        }
+    }
+    printf("Translocations before filter: %d\n", n);
+    f = fopen(ctx_path, "w");
+    if (!f) { free(rw); return; }
+    header(f);
+    int n2 = 0;
+    for (int b = 0; b < n; b++) {
+        const ctx_row *q = &rw[b];
+        if (q->keep != 1) continue;
+        n2++;
+        char bnd[64];
+        const char *mn = (q->mchr >= 0 && q->mchr < n_targets) ? bam_names_lc[q->mchr] : "";
+        if (q->type == 6 && q->mpos < 0) snprintf(bnd, sizeof(bnd), "N[%s:%d[", mn, abs(q->mpos));
+        else if (q->type == 6 && q->mpos >= 0) snprintf(bnd, sizeof(bnd), "N]%s:%d]", mn, abs(q->mpos));
+        else if (q->type == 7 && q->mpos < 0) snprintf(bnd, sizeof(bnd), "[%s:%d[N", mn, abs(q->mpos));
+        else snprintf(bnd, sizeof(bnd), "]%s:%d]N", mn, abs(q->mpos));
+        fprintf(f, "%s\t%d\t%d\tN\t%s\t.\t.\tSVTYPE=BND;MATEID=%d\tSPR:SEV:SRD:SCO:SOT:SFR:SLR:SHPR\t%e:%.1f:%d:%d:%d:%d:%d:%e\n",
+                (q->chr >= 0 && q->chr < n_targets) ? bam_names_lc[q->chr] : "", q->pos + 1, b, bnd, q->mateid, q->binom,
+                q->ev, q->rd, q->conc, q->other, q->rs + 1, q->re + 1, q->hez);
+    }
+    printf("Translocations after filter: %d\n", n2);
+    fclose(f);
+    free(rw);
+}

@@ -94,7 +94,8 @@ def test_oracle_snv_row_layout_matches_golden(datadir):
     run_oracle(datadir, bam, fa, "lay.vcf")
     pat = re.compile(r"^[^\t]+\t\d+\t\t[A-Za-z]\t[ACGT]\t\.\t\.\t\.\tGT:PR:AF:A:C:G:T:AL:CL:GL:TL:BQ:MQ:PIR:FS\t"
                      r"[01](/[01])*:\d\.\d{6}e[+-]\d\d:\d\.\d{6}e[+-]\d\d(:\d+){8}(:-?\d+\.\d\d){4}$")
-    rows = [l.rstrip("\n") for l in open(datadir / "lay.vcf") if not l.startswith("#")]
+    rows = [l.rstrip("\n") for l in open(datadir / "lay.vcf")
+            if not l.startswith("#") and l.split("\t")[8].startswith("GT:PR:AF")]
     assert rows, "no SNV rows on the synthetic case"
     for r in rows:
         assert pat.match(r), r
