@@ -10,8 +10,8 @@ LIBDIR  = grom_amd/lib
 BINDIR  = grom_amd/bin
 
 HOST_SRC = grom_amd/csrc/bamio.c grom_amd/csrc/stream.c grom_amd/csrc/tables.c grom_amd/csrc/synth.c grom_amd/csrc/hostapi.c grom_amd/csrc/grom_main.c
-HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC)) build/snvfmt.o
-DEV_OBJ = build/scan.o build/cnv.o build/indel.o
+HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC)) build/snvfmt.o build/svcall.o
+DEV_OBJ = build/scan.o build/cnv.o build/sv.o
 HDRS = include/grom_amd.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h
 KHDRS = grom_amd/csrc/k_scan_tile.h grom_amd/csrc/device_common.h grom_amd/csrc/snvfmt.h grom_amd/csrc/k_scan_scatter.h
 
@@ -25,7 +25,7 @@ build/snvfmt.o: grom_amd/csrc/snvfmt.cpp grom_amd/csrc/snvfmt.h $(HDRS)
 	@mkdir -p build
 	$(CXX) -O2 -g -Wall -fPIC -std=c++17 -pthread -c $< -o $@
 
-build/scan.o: grom_amd/csrc/scan.hip $(HDRS) $(KHDRS) grom_amd/csrc/cnv.h grom_amd/csrc/indel.h
+build/scan.o: grom_amd/csrc/scan.hip $(HDRS) $(KHDRS) grom_amd/csrc/cnv.h grom_amd/csrc/sv.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -34,9 +34,15 @@ build/cnv.o: grom_amd/csrc/cnv.hip grom_amd/csrc/cnv.h $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -ffp-contract=off -c $< -o $@
 
-build/indel.o: grom_amd/csrc/indel.hip grom_amd/csrc/indel.h $(HDRS)
+# the breakpoint clusters keep the reference's running-mean arithmetic: no fused multiply-add
+build/sv.o: grom_amd/csrc/sv.hip grom_amd/csrc/sv.h $(HDRS)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -ffp-contract=off -c $< -o $@
+
+# host list logic and SV rows (needs only the HIP runtime headers)
+build/svcall.o: grom_amd/csrc/svcall.cpp grom_amd/csrc/sv.h $(HDRS)
+	@mkdir -p build
+	$(HIPCC) -O2 -g -Wall -fPIC -std=c++17 -ffp-contract=off -c $< -o $@
 
 $(LIBDIR)/libgrom_amd.so: $(DEV_OBJ) $(HOST_OBJ)
 	@mkdir -p $(LIBDIR)
@@ -55,11 +61,11 @@ oracle:
 
 # kernel tuning variants, loaded with GROM_AMD_LIB=...:
 #   make variant V=w4 VFLAGS=-DGROM_WAVES_PER_EU=4  ->  grom_amd/lib/variants/libgrom_amd_w4.so
-variant: $(HOST_OBJ) build/indel.o
+variant: $(HOST_OBJ) build/sv.o
 	@mkdir -p build/variants $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c grom_amd/csrc/scan.hip -o build/variants/scan_$(V).o
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -ffp-contract=off -c grom_amd/csrc/cnv.hip -o build/variants/cnv_$(V).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(LIBDIR)/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/variants/cnv_$(V).o build/indel.o $(HOST_OBJ) -lz -lm
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(LIBDIR)/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/variants/cnv_$(V).o build/sv.o $(HOST_OBJ) -lz -lm
 
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR)

@@ -33,18 +33,31 @@ class Params(C.Structure):
                                   "ranks_stdev", "chr_rd_threshold_factor")] + \
         [(n, C.c_int64) for n in ("min_repeat", "min_blocks", "block_min", "min_rd_window_len", "max_rd_window_len",
                                   "windows_sampling_factor", "dup_threshold_factor")] + \
-        [(n, C.c_double) for n in ("min_repeat_stdev", "rd_pval_threshold", "mapq_factor")]
+        [(n, C.c_double) for n in ("min_repeat_stdev", "rd_pval_threshold", "mapq_factor")] + \
+        [(n, C.c_int32) for n in ("min_disc", "sc_range", "max_split_loss", "min_sr_len", "max_homopolymer",
+                                  "max_ins_range", "sv_list2_len", "pad_sv")] + \
+        [(n, C.c_double) for n in ("pval_threshold", "pval_threshold1", "pval_insertion1", "pval_insertion",
+                                   "min_sv_ratio", "min_indel_ratio", "max_evidence_ratio", "range_mult",
+                                   "max_inv_rd_diff", "min_overlap_ratio")]
 
 
 class Chrom(C.Structure):
     _fields_ = [("ref", C.c_void_p), ("len", C.c_int64), ("name", C.c_char_p), ("tid", C.c_int32),
-                ("n_skip", C.c_int32), ("p_last", C.c_int32), ("cnv", C.c_int32), ("seed", C.c_uint32)]
+                ("n_skip", C.c_int32), ("p_last", C.c_int32), ("cnv", C.c_int32), ("seed", C.c_uint32),
+                ("lseq_tail", C.c_int32), ("pad", C.c_int32)]
 
 
 class Reads(C.Structure):
     _fields_ = [("n", C.c_int64), ("n_cigar_ops", C.c_int64), ("n_bases", C.c_int64)] + \
         [(n, C.c_void_p) for n in ("pos", "flag", "mapq", "mtid", "mpos", "isize", "l_qseq", "cigar_off", "cigar",
-                                   "base_off", "seq", "qual", "name_id")]
+                                   "base_off", "seq", "qual", "name_id")] + \
+        [("n_aux", C.c_int64), ("aux_idx", C.c_void_p), ("aux", C.c_void_p),
+         ("n_drop", C.c_int64), ("drop_pos", C.c_void_p), ("drop_lq", C.c_void_p), ("drop_before", C.c_void_p)]
+
+
+class Aux(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("pos", "start_adj", "end_adj", "end_adj_indel")] + \
+        [("mq", C.c_int16), ("strand", C.c_uint8), ("same_chr", C.c_uint8), ("pad", C.c_int32)]
 
 
 class Out(C.Structure):
@@ -64,6 +77,18 @@ class IndelRec(C.Structure):
         [("ins_seq", C.c_char * 52), ("pad", C.c_int32)]
 
 
+class SvRec(C.Structure):
+    _fields_ = [("pos", C.c_int32), ("other_len", C.c_int32), ("cnt", C.c_int32 * 10), ("rs", C.c_int32 * 10),
+                ("re", C.c_int32 * 10), ("dist", C.c_double * 10), ("ctx_mchr", C.c_int32 * 2)] + \
+        [(n, C.c_int32) for n in ("rd_add", "conc", "ins", "mun_f", "mun_r", "pad")]
+
+
+# numpy view of the breakpoint test-hook records (grom_sv_rec)
+SV_DTYPE = np.dtype([("pos", "<i4"), ("other_len", "<i4"), ("cnt", "<i4", 10), ("rs", "<i4", 10), ("re", "<i4", 10),
+                     ("dist", "<f8", 10), ("ctx_mchr", "<i4", 2), ("rd_add", "<i4"), ("conc", "<i4"), ("ins", "<i4"),
+                     ("mun_f", "<i4"), ("mun_r", "<i4"), ("pad", "<i4")])
+
+
 # every function declared in include/grom_amd.h, with its ctypes signature
 _SIGS = {
     "grom_abi_version": (C.c_int, []),
@@ -81,6 +106,7 @@ _SIGS = {
     "grom_debug_counts": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(C.c_int32), C.c_void_p,
                                     C.c_int64, C.c_void_p]),
     "grom_debug_indels": (C.c_int64, [C.c_int, C.c_void_p, C.c_int64]),
+    "grom_debug_sv": (C.c_int64, [C.c_int, C.c_void_p, C.c_int64]),
     "grom_build_tables": (None, [C.c_int32, C.c_void_p, C.c_void_p]),
     "grom_default_params": (None, [C.POINTER(Params)]),
     "grom_params_set_insert": (None, [C.POINTER(Params), C.c_int32, C.c_int32, C.c_int32, C.c_int32]),

@@ -48,6 +48,13 @@ struct PileOut {
     int32_t *dbg;                   // nullable: GC_COUNT int32 per evaluated base
     uint32_t *status;               // reserved
     uint32_t *n_events;             // reserved
+    // breakpoint-test context (sv.hip): positions marked in sv_bits or with
+    // soft-clip evidence get a grom_sv_ctx record (unordered; sorted later)
+    const uint32_t *sv_bits;
+    grom_sv_ctx *sv_ctx;
+    uint32_t *n_sv_ctx;
+    uint32_t sv_ctx_cap;
+    const int32_t *rd_add;          // nullable: breakpoint depth adds, for the debug counters
 };
 
 #endif

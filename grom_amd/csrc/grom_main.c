@@ -11,6 +11,7 @@
  * (tab-separated output).  Options that steer parts of the reference outside
  * the implemented scan rows are accepted and recorded.
  */
+#include <ctype.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -139,15 +140,132 @@ typedef struct {
     char *ref;
     long len;
     char name[GROM_MAX_CHR_NAME_LEN + 1];
+    char *target; /* BAM name the SA/XP chromosome test compares with (GROM.c:1894-1961, 7431) */
 } chrom_plan;
 
 static int g_plan_only = 0; /* GROM_PLAN_ONLY: report the record plan, no GPU */
 
+typedef struct {
+    char *p;
+    size_t len, cap;
+} textbuf;
+
+static void textbuf_add(textbuf *t, const char *s, size_t n) {
+    if (t->len + n + 1 > t->cap) {
+        size_t nc = t->cap ? 2 * t->cap : 1 << 16;
+        while (nc < t->len + n + 1) nc *= 2;
+        t->p = realloc(t->p, nc);
+        t->cap = nc;
+    }
+    memcpy(t->p + t->len, s, n);
+    t->len += n;
+    t->p[t->len] = 0;
+}
+
+/* main's translocation post-pass (GROM.c:22400-22770): the raw CTX rows of
+ * every chromosome are read back, each breakpoint is paired with a mate row
+ * (its chromosome and mate chromosome swapped, positions within
+ * insert_max - 2*lseq, orientations consistent), the weaker of two nearby
+ * paired rows is dropped with its mate, and the rest are written as BND rows. */
+typedef struct {
+    int type, chr, pos, rd, conc, other, mchr, mpos, rs, re, mateid, keep;
+    double binom, ev, hez;
+} ctx_row_t;
+
+static void ctx_postpass(const char *raw, size_t raw_len, const bam_hdr *hdr, int Mx, int glseq, FILE *out) {
+    int n_t = hdr->n_ref;
+    char **lc = calloc(n_t > 0 ? n_t : 1, sizeof(char *));
+    for (int a = 0; a < n_t; a++) {
+        size_t L = strlen(hdr->ref_name[a]);
+        lc[a] = malloc(L + 1);
+        for (size_t b = 0; b <= L; b++) lc[a][b] = (char)tolower((unsigned char)hdr->ref_name[a][b]);
+    }
+    int n = 0, cap = 1024;
+    ctx_row_t *rw = calloc(cap, sizeof(ctx_row_t));
+    size_t off = 0;
+    while (raw && off < raw_len) {
+        const char *e = memchr(raw + off, '\n', raw_len - off);
+        size_t ll = e ? (size_t)(e - (raw + off)) : raw_len - off;
+        char *line = malloc(ll + 1);
+        memcpy(line, raw + off, ll);
+        line[ll] = 0;
+        off += ll + (e ? 1 : 0);
+        if (n == cap) { cap *= 2; rw = realloc(rw, cap * sizeof(ctx_row_t)); }
+        ctx_row_t *q = &rw[n++];
+        memset(q, 0, sizeof(*q));
+        char *save = NULL, *t = strtok_r(line, "\t", &save);
+        q->type = t ? (strcmp(t, "CTX_F") == 0 ? 6 : strcmp(t, "CTX_R") == 0 ? 7 : -1) : -1; /* g_sv_types */
+        t = strtok_r(NULL, "\t", &save);
+        q->chr = -1;
+        if (t) {
+            char tl[1024];
+            size_t L = strlen(t);
+            if (L > sizeof(tl) - 1) L = sizeof(tl) - 1;
+            for (size_t b = 0; b < L; b++) tl[b] = (char)tolower((unsigned char)t[b]);
+            tl[L] = 0;
+            for (int a = 0; a < n_t; a++)
+                if (strcmp(lc[a], tl) == 0) { q->chr = a; break; }
+        }
+        int *ifld[] = {&q->pos, NULL, NULL, &q->rd, &q->conc, &q->other, &q->mchr, &q->mpos, &q->rs, &q->re, NULL};
+        double *dfld[] = {NULL, &q->binom, &q->ev, NULL, NULL, NULL, NULL, NULL, NULL, NULL, &q->hez};
+        for (int k = 0; k < 11; k++) {
+            t = strtok_r(NULL, "\t", &save);
+            if (ifld[k]) *ifld[k] = t ? atoi(t) : 0;
+            else *dfld[k] = t ? atof(t) : 0;
+        }
+        free(line);
+    }
+    const int span = Mx - 2 * glseq;
+    for (int b = 0; b < n; b++) { rw[b].keep = 0; rw[b].mateid = -1; }
+    for (int b = 0; b < n; b++)
+        for (int c = 0; c < n; c++) {
+            if (!(rw[b].chr == rw[c].mchr && rw[c].chr == rw[b].mchr)) continue;
+            if (!(abs(rw[b].pos - abs(rw[c].mpos)) < span && abs(rw[c].pos - abs(rw[b].mpos)) < span)) continue;
+            const int bo = (rw[b].type == 6 && rw[c].mpos >= 0) || (rw[b].type == 7 && rw[c].mpos < 0);
+            const int co = (rw[c].type == 6 && rw[b].mpos >= 0) || (rw[c].type == 7 && rw[b].mpos < 0);
+            if (bo && co) {
+                rw[b].keep = 1;
+                rw[b].mateid = c;
+                rw[b].mpos = rw[b].mpos < 0 ? -rw[c].pos : rw[c].pos;
+            }
+        }
+    for (int b = 0; b < n; b++)
+        for (int c = 0; c < n; c++) {
+            if (b == c || rw[b].chr != rw[c].chr || rw[b].mchr != rw[c].mchr) continue;
+            if (!(abs(rw[b].pos - rw[c].pos) < span && abs(abs(rw[b].mpos) - abs(rw[c].mpos)) < span)) continue;
+            if (rw[b].keep == 1 && rw[c].keep == 1 && (rw[b].binom > rw[c].binom || (rw[b].binom == rw[c].binom && b > c))) {
+                rw[b].keep = 0;
+                if (rw[b].mateid >= 0) rw[rw[b].mateid].keep = 0;
+            }
+        }
+    printf("Translocations before filter: %d\n", n);
+    int n2 = 0;
+    for (int b = 0; b < n; b++) {
+        const ctx_row_t *q = &rw[b];
+        if (q->keep != 1) continue;
+        n2++;
+        char bnd[64];
+        const char *mn = (q->mchr >= 0 && q->mchr < n_t) ? lc[q->mchr] : "";
+        const int am = abs(q->mpos);
+        if (q->type == 6) snprintf(bnd, sizeof(bnd), q->mpos < 0 ? "N[%s:%d[" : "N]%s:%d]", mn, am);
+        else snprintf(bnd, sizeof(bnd), q->mpos < 0 ? "[%s:%d[N" : "]%s:%d]N", mn, am);
+        fprintf(out, "%s\t%d\t%d\tN\t%s\t.\t.\tSVTYPE=BND;MATEID=%d\tSPR:SEV:SRD:SCO:SOT:SFR:SLR:SHPR\t%e:%.1f:%d:%d:%d:%d:%d:%e\n",
+                (q->chr >= 0 && q->chr < n_t) ? lc[q->chr] : "", q->pos + 1, b, bnd, q->mateid, q->binom, q->ev, q->rd,
+                q->conc, q->other, q->rs + 1, q->re + 1, q->hez);
+    }
+    printf("Translocations after filter: %d\n", n2);
+    for (int a = 0; a < n_t; a++) free(lc[a]);
+    free(lc);
+    free(rw);
+}
+
 /* Scan one chromosome's batch on `device`; its VCF rows go to *text (malloc'd). */
 static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_params *P, char **text, size_t *text_len,
-                      int verbose) {
+                      char **ctx_text, size_t *ctx_len, int verbose) {
     *text = NULL;
     *text_len = 0;
+    *ctx_text = NULL;
+    *ctx_len = 0;
     grom_batch_finish(b, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size);
     if (g_plan_only) {
         printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d\n", cp->name, cp->tid, (long long)b->n, b->n_skip,
@@ -155,6 +273,8 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
         return GROM_OK;
     }
     grom_chrom ch;
+    memset(&ch, 0, sizeof(ch));
+    ch.lseq_tail = b->lseq_tail;
     ch.ref = cp->ref;
     ch.len = cp->len;
     ch.name = cp->name;
@@ -181,6 +301,10 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
     *text_len = out.vcf_len;
     out.vcf = NULL;
     out.vcf_len = out.vcf_cap = 0;
+    *ctx_text = out.ctx; /* raw CTX rows for the translocation post-pass */
+    *ctx_len = out.ctx_len;
+    out.ctx = NULL;
+    out.ctx_len = out.ctx_cap = 0;
     const char *dump = getenv("GROM_DUMP");
     if (dump) {
         /* test hook: per-base counters and caf depth, same files as the oracle's */
@@ -210,6 +334,16 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
                 fprintf(stderr, "grom: indel dump of %s failed: %s\n", cp->name, grom_last_error());
             }
             free(ind);
+            /* breakpoint cluster records (rows A8/A9; the scan keeps them when
+             * GROM_SV_DEBUG is set) */
+            int64_t n_sv = grom_debug_sv(device, NULL, 0);
+            grom_sv_rec *svr = n_sv > 0 ? malloc(sizeof(grom_sv_rec) * n_sv) : NULL;
+            if (n_sv >= 0 && (n_sv == 0 || (svr && grom_debug_sv(device, svr, n_sv) == n_sv))) {
+                snprintf(path, sizeof(path), "%s.%s.sv", dump, cp->name);
+                f = fopen(path, "wb");
+                if (f) { if (n_sv) fwrite(svr, sizeof(grom_sv_rec), n_sv, f); fclose(f); }
+            }
+            free(svr);
         } else {
             fprintf(stderr, "grom: counter dump of %s failed: %s\n", cp->name, grom_last_error());
         }
@@ -232,11 +366,21 @@ static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_para
 typedef struct {
     chrom_plan *cp;
     grom_batch batch;
-    char *text;
-    size_t text_len;
+    char *text, *ctx_text;
+    size_t text_len, ctx_len;
     int rc, ready, done;
     char err[512]; /* the worker's grom_last_error() when rc != GROM_OK */
 } grom_job;
+
+/* a finished chromosome: its VCF rows go out, its raw CTX rows are kept */
+static void take_rows(grom_job *j, FILE *vcf, textbuf *ctx_all) {
+    if (j->text_len) fwrite(j->text, 1, j->text_len, vcf);
+    free(j->text);
+    j->text = NULL;
+    if (j->ctx_len) textbuf_add(ctx_all, j->ctx_text, j->ctx_len);
+    free(j->ctx_text);
+    j->ctx_text = NULL;
+}
 
 typedef struct {
     pthread_mutex_t mu;
@@ -266,7 +410,8 @@ static void *grom_worker_main(void *arg) {
         grom_job *j = &pl->jobs[pl->next_run++];
         pthread_mutex_unlock(&pl->mu);
         /* contexts are independent: workers sharing a GPU scan concurrently */
-        int rc = scan_batch(w->slot, j->cp, &j->batch, pl->P, &j->text, &j->text_len, pl->verbose);
+        int rc = scan_batch(w->slot, j->cp, &j->batch, pl->P, &j->text, &j->text_len, &j->ctx_text, &j->ctx_len,
+                            pl->verbose);
         if (rc != GROM_OK) snprintf(j->err, sizeof(j->err), "%s: %s", j->cp->name, grom_last_error());
         free(j->cp->ref);
         j->cp->ref = NULL;
@@ -325,6 +470,16 @@ int grom_cli_main(int argc, char **argv) {
         case 'U': P.chr_rd_threshold_factor = atoi(optarg); break;
         case 'L': P.dup_threshold_factor = atol(optarg); break;
         case 'F': P.mapq_factor = atof(optarg); break;
+        case 'v': P.pval_threshold = atof(optarg); break;
+        case 'd': P.min_disc = atoi(optarg); break;
+        case 'y': P.max_split_loss = atoi(optarg); break;
+        case 'z': P.min_sr_len = atoi(optarg); break;
+        case 'e': P.pval_insertion = atof(optarg); break;
+        case 'j': P.min_sv_ratio = atof(optarg); break;
+        case 'k': P.max_homopolymer = atoi(optarg); break;
+        case 'm': P.min_indel_ratio = atof(optarg); break;
+        case 'u': P.max_evidence_ratio = atof(optarg); break;
+        case 'w': P.max_ins_range = atoi(optarg); break;
         case 'N':
             if (atol(optarg) > 0) {
                 printf("ERROR: -N (.1000gen side file) is not supported by this build\n");
@@ -336,7 +491,9 @@ int grom_cli_main(int argc, char **argv) {
         default: break; /* accepted; steers rows outside the implemented scan */
         }
     }
-    P.rd_min_mapq = P.min_mapq; /* GROM.c:22102 */
+    P.rd_min_mapq = P.min_mapq;         /* GROM.c:22102 */
+    P.pval_threshold1 = P.pval_threshold; /* GROM.c:22101 */
+    P.sv_list2_len = P.sv_list_len / 10;  /* GROM.c:21925 */
     printf("bam %s\n", bam_name ? bam_name : "(null)");
     printf("ref %s\n", fasta_name ? fasta_name : "(null)");
     printf("results %s\n", out_name ? out_name : "(null)");
@@ -459,6 +616,8 @@ int grom_cli_main(int argc, char **argv) {
         plan[n_plan].fasta_idx = fi;
         plan[n_plan].tid = tid2;
         plan[n_plan].len = len;
+        /* the name loop leaves the last target's name when nothing matches */
+        plan[n_plan].target = strdup(hdr.n_ref > 0 ? hdr.ref_name[tid2 >= 0 ? tid2 : hdr.n_ref - 1] : "");
         snprintf(plan[n_plan].name, sizeof(plan[n_plan].name), "%.*s", fa.name_len[fi], fa.names[fi]);
         order[n_plan] = tid2;
         n_plan++;
@@ -482,7 +641,11 @@ int grom_cli_main(int argc, char **argv) {
     grom_planner_init(&pl, order, n_plan);
     grom_batch batch;
     int cur = 0;
-    if (n_plan > 0) grom_batch_init(&batch, order[0], P.read_name_len);
+    int batch_ended = 0; /* the record after the chromosome's last one was seen */
+    if (n_plan > 0) {
+        grom_batch_init(&batch, order[0], P.read_name_len);
+        grom_batch_set_sv(&batch, plan[0].target, P.splitread);
+    }
     bam_rec rec;
     memset(&rec, 0, sizeof(rec));
     int status = 0;
@@ -502,6 +665,7 @@ int grom_cli_main(int argc, char **argv) {
         pthread_create(&tids[d], NULL, grom_worker_main, &workers[d]);
     }
     int next_write = 0;
+    textbuf ctx_all = {0};
     /* hand chromosome `cur` (its batch complete) to the workers; at most one
      * decoded chromosome waits beyond those being scanned (n_work + 1 batches
      * in host memory), finished rows are written in order */
@@ -519,9 +683,7 @@ int grom_cli_main(int argc, char **argv) {
                     grom_job *j = &pool.jobs[next_write++];                                        \
                     pthread_mutex_unlock(&pool.mu);                                                \
                     if (j->rc != GROM_OK) status = 1;                                              \
-                    if (j->text_len) fwrite(j->text, 1, j->text_len, vcf);                         \
-                    free(j->text);                                                                 \
-                    j->text = NULL;                                                                \
+                    take_rows(j, vcf, &ctx_all);                                                   \
                     pthread_mutex_lock(&pool.mu);                                                  \
                 }                                                                                  \
                 if (cur + 1 - next_write < n_work + 1) break;                                      \
@@ -529,9 +691,19 @@ int grom_cli_main(int argc, char **argv) {
             }                                                                                      \
             pthread_mutex_unlock(&pool.mu);                                                        \
             cur++;                                                                                 \
-            if (cur < n_plan) grom_batch_init(&batch, order[cur], P.read_name_len);                \
+            if (cur < n_plan) {                                                                    \
+                grom_batch_init(&batch, order[cur], P.read_name_len);                              \
+                grom_batch_set_sv(&batch, plan[cur].target, P.splitread);                          \
+                batch_ended = 0;                                                                   \
+            }                                                                                      \
         } while (0)
     while (cur < n_plan && bam_read_rec(&br, &rec) > 0) {
+        /* cdp_lseq after the chromosome: the l_qseq of the record that ended
+         * it (the R-side edge tests of its last bases read it, GROM.c:12047) */
+        if (!batch_ended && batch.n_seen > 0 && rec.tid != order[cur]) {
+            grom_batch_end_record(&batch, &rec);
+            batch_ended = 1;
+        }
         int k = grom_planner_feed(&pl, rec.tid);
         while (cur < n_plan && pl.k > cur) SUBMIT_CUR(); /* chromosome `cur` is complete */
         if (k >= 0 && k == cur) grom_batch_add(&batch, &rec, s0);
@@ -546,9 +718,7 @@ int grom_cli_main(int argc, char **argv) {
         if (pool.jobs[next_write].done) {
             grom_job *j = &pool.jobs[next_write++];
             if (j->rc != GROM_OK) status = 1;
-            if (j->text_len) fwrite(j->text, 1, j->text_len, vcf);
-            free(j->text);
-            j->text = NULL;
+            take_rows(j, vcf, &ctx_all);
         } else {
             pthread_cond_wait(&pool.cv, &pool.mu);
         }
@@ -565,13 +735,18 @@ int grom_cli_main(int argc, char **argv) {
     bam_free_rec(&rec);
     bgzf_close_read(&br);
     fclose(vcf);
-    /* CTX post-pass (GROM.c:22400-22770): with no translocation rows the
-     * rewritten file is the header alone */
+    /* CTX post-pass (GROM.c:22400-22770): pair the translocation rows of all
+     * chromosomes with their mates and write them under the header */
     FILE *ctx = fopen(ctx_name, "w");
     if (ctx) {
-        if (P.vcf == 1) header(ctx, fasta_name, 1);
+        if (P.vcf == 1) {
+            header(ctx, fasta_name, 1);
+            ctx_postpass(ctx_all.p, ctx_all.len, &hdr, P.insert_max_size, P.lseq, ctx);
+        }
         fclose(ctx);
     }
+    free(ctx_all.p);
+    for (int i = 0; i < n_plan; i++) free(plan[i].target);
     for (int d = 0; d < n_init; d++) grom_dev_fini(d);
     #undef CLI_FAIL
     grom_fasta_close(&fa);

@@ -60,6 +60,17 @@ static void trim_prefix(grom_batch *b, int32_t s0, int64_t *n_dropped_mapped) {
     memmove(b->isize, b->isize + k, sizeof(int32_t) * n);
     memmove(b->l_qseq, b->l_qseq + k, sizeof(int32_t) * n);
     memmove(b->name_id, b->name_id + k, sizeof(uint32_t) * n);
+    memmove(b->aux_idx, b->aux_idx + k, sizeof(int32_t) * n);
+    /* dropped (unmapped / duplicate) records of the prefix go with it */
+    int64_t nd = 0;
+    for (int64_t d = 0; d < b->n_drop; d++) {
+        if (b->drop_pos[d] < s0) continue;
+        b->drop_pos[nd] = b->drop_pos[d];
+        b->drop_lq[nd] = b->drop_lq[d];
+        b->drop_before[nd] = b->drop_before[d] > k ? b->drop_before[d] - k : 0;
+        nd++;
+    }
+    b->n_drop = nd;
     for (int64_t i = 0; i <= n; i++) b->cigar_off[i] = b->cigar_off[i + k] - (uint32_t)c0;
     memmove(b->cigar, b->cigar + c0, sizeof(uint32_t) * (b->n_cig - c0));
     b->n_cig -= c0;
@@ -123,6 +134,8 @@ int grom_batch_get(grom_batch_handle *h, grom_chrom *ch, grom_reads *rd) {
     ch->p_last = h->b.p_last;
     ch->cnv = 1;
     ch->seed = 1;
+    ch->lseq_tail = h->b.lseq_tail;
+    ch->pad = 0;
     grom_batch_view(&h->b, rd);
     return GROM_OK;
 }

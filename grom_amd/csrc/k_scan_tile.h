@@ -263,7 +263,7 @@ __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *_
             d[GC_BQ_RC] = total;
             d[GC_MQ_RC] = total;
             d[GC_RC_ALL] = rc_all;
-            d[GC_RD] = rd;
+            d[GC_RD] = rd + (O.rd_add ? O.rd_add[x] : 0);  // + the breakpoint ranges (row A9)
 #pragma unroll
             for (int k = 0; k < 15; k++) d[GC_SC_LEFT + k] = sc[k];
         }
@@ -284,6 +284,37 @@ __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *_
                         best = k;
                         best_ratio = ratio;
                     }
+                }
+            }
+        }
+    }
+    // ---- breakpoint-test context (row A10, sv.hip): positions the SV fold
+    // marked, and every position with soft-clip evidence (whose absence then
+    // means zero counters) ----
+    if (O.sv_ctx) {
+        const bool want = evals && (((O.sv_bits[x >> 5] >> (x & 31)) & 1u) || sc[0] || sc[1] || sc[2] || sc[3]);
+        const uint64_t wm = __ballot(want);
+        if (wm) {
+            uint32_t wb = 0;
+            if (lane == 0) wb = atomicAdd(O.n_sv_ctx, (uint32_t)__popcll(wm));
+            wb = __shfl(wb, 0, 64);
+            if (want) {
+                const uint32_t k = wb + (uint32_t)__popcll(wm & ((1ull << lane) - 1));
+                if (k < O.sv_ctx_cap) {
+                    grom_sv_ctx r;
+                    r.pos = x;
+                    r.rd = rd;
+                    r.sc_rd = sc[4];
+                    r.indel_sc_rd = sc[14];
+                    r.sc_left = sc[0];
+                    r.sc_right = sc[1];
+                    r.sc_left_rd = sc[2];
+                    r.sc_right_rd = sc[3];
+                    r.indel_sc_left = sc[10];
+                    r.indel_sc_right = sc[11];
+                    r.snv_all = c.snv0 + c.snv1 + c.snv2 + c.snv3 + c.low0 + c.low1 + c.low2 + c.low3;
+                    r.pad = 0;
+                    O.sv_ctx[k] = r;
                 }
             }
         }

@@ -35,7 +35,7 @@
 
 #include "../../include/grom_amd.h"
 #include "cnv.h"
-#include "indel.h"
+#include "sv.h"
 #include "scan_common.h"
 #include "snvfmt.h"
 
@@ -224,13 +224,15 @@ struct Ctx {
     double *d_mq = nullptr, *d_hez = nullptr;
     // reads (used when the caller passes host memory)
     DevBuf r_pos, r_flag, r_mapq, r_mtid, r_mpos, r_isize, r_lq, r_coff, r_cig, r_boff, r_seq, r_qual, r_nid, ref;
+    DevBuf r_aidx, r_aux, r_dpos, r_dlq, r_dbef;
     // scan scratch
     DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, ovf, fpart;
     grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
+    const char *host_ref = nullptr;    // the caller's host reference during grom_scan_chrom
     size_t h_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, ep0 = nullptr, ep1 = nullptr;
     CnvScratch *cnv = nullptr;  // read-depth CNV path (cnv.hip)
-    IndelScratch *indel = nullptr;  // CIGAR indel evidence (indel.hip)
+    SvScratch *sv = nullptr;        // breakpoint evidence and tests (sv.hip)
 };
 
 static Ctx g_ctx[64];
@@ -242,6 +244,31 @@ static Ctx *ctx_of(int device) {
     }
     return &g_ctx[device];
 }
+
+// sum of caf_rd + caf_low over [lo, hi) of the device arrays, as the INV
+// depth check reads them (GROM.c:15816-15826): int per base, double total
+struct CafSum {
+    hipStream_t st;
+    const int32_t *rd, *low;
+    int64_t len;
+    int rc;
+    static double call(void *u, int64_t lo, int64_t hi) {
+        CafSum &c = *(CafSum *)u;
+        const int64_t a = std::max<int64_t>(lo, 0), b = std::min<int64_t>(hi, c.len);
+        if (a >= b || c.rc != GROM_OK) return 0.0;
+        std::vector<int32_t> r((size_t)(b - a)), l((size_t)(b - a));
+        if (hipMemcpyAsync(r.data(), c.rd + a, sizeof(int32_t) * r.size(), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+            hipMemcpyAsync(l.data(), c.low + a, sizeof(int32_t) * l.size(), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
+            hipStreamSynchronize(c.st) != hipSuccess) {
+            set_err("INV depth check: device copy failed");
+            c.rc = GROM_E_HIP;
+            return 0.0;
+        }
+        double s = 0;
+        for (size_t k = 0; k < r.size(); k++) s += r[k] + l[k];
+        return s;
+    }
+};
 
 // ring index of the reference walk after k iterations (GROM.c:5845-5847,
 // 6392): starts at index_start = r14 + 1 and wraps r34 -> r14.
@@ -347,6 +374,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
 
     // scratch
     const bool want_dbg = dbg_counts != nullptr;
+    const bool sv_debug = getenv("GROM_SV_DEBUG") != nullptr;  // keep the breakpoint records for grom_debug_sv
     int64_t n_eval = (a.eval_hi >= a.eval_lo) ? (int64_t)a.eval_hi - a.eval_lo + 1 : 0;
     if ((rc = ensure(C.tlo, sizeof(int32_t) * n_tiles)) || (rc = ensure(C.thi, sizeof(int32_t) * n_tiles)) ||
         (rc = ensure(C.caf_mq, sizeof(int32_t) * ch->len)) || (rc = ensure(C.caf_rd, sizeof(int32_t) * ch->len)) ||
@@ -397,6 +425,28 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         }
         ReadArrays ra{R->pos, R->flag, R->mapq, R->mtid, R->mpos, R->isize, R->l_qseq, R->cigar_off, R->cigar,
                       R->base_off, R->seq, R->qual, R->name_id, keep};
+        // breakpoint evidence of every read (rows A7-A9): range sums, the
+        // ordered cluster fold, and the bases the pileup must describe
+        SvInput svin{n, R->pos, R->flag, R->mapq, R->mtid, R->mpos, R->isize, R->l_qseq, R->cigar_off, R->cigar,
+                     R->base_off, R->seq, keep, nullptr, nullptr, 0, nullptr, nullptr, nullptr};
+        if (R->n_aux > 0 && R->aux_idx && R->aux) {
+            svin.aux_idx = R->aux_idx;
+            svin.aux = R->aux;
+        }
+        if (R->n_drop > 0 && R->drop_pos && R->drop_lq && R->drop_before) {
+            svin.n_drop = R->n_drop;
+            svin.drop_pos = R->drop_pos;
+            svin.drop_lq = R->drop_lq;
+            svin.drop_before = R->drop_before;
+        }
+        {
+            if (!C.sv) C.sv = sv_scratch_new();
+            char serr[512] = {0};
+            if ((rc = sv_prepare(C.sv, st, P, svin, *ch, a.eval_lo, a.eval_hi, sv_debug, serr, sizeof(serr)))) {
+                set_err("%s", serr);
+                return rc;
+            }
+        }
         if (n > 0) {
             int g = (int)std::min<int64_t>((n + 255) / 256, 8192);
             hipLaunchKernelGGL(k_prep, dim3(g), dim3(256), 0, st, n, ra, (ReadMeta *)C.meta.p, d_halo);
@@ -409,7 +459,8 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         PileOut po{(int32_t *)C.caf_mq.p, (int32_t *)C.caf_rd.p, (int32_t *)C.caf_low.p,
                    (grom_snv_cand *)C.cands.p, d_ncand, cand_cap, (uint32_t *)C.runb.p, (uint32_t *)C.runc.p,
                    (unsigned long long *)C.fpart.p,
-                   want_dbg ? (int32_t *)C.dbg.p : nullptr, d_status, d_nev};
+                   want_dbg ? (int32_t *)C.dbg.p : nullptr, d_status, d_nev, sv_bits(C.sv), sv_ctx_buf(C.sv),
+                   sv_ctx_count(C.sv), sv_ctx_cap(C.sv), want_dbg ? sv_rd_add(C.sv) : nullptr};
         HIPCHK(hipEventRecord(C.ep0, st));
         const unsigned grid = (unsigned)(((n_tiles + 7) / 8) * 8);
         const bool few = P.min_snv <= GROM_FEW_NAME_SLOTS;
@@ -527,21 +578,39 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         } fmt_join{fmt};
         const double t_snv = ms_since(t_start);
 
-        // CIGAR indel evidence of the evaluated bases (row A7, GROM.c:7187-7423);
-        // its records feed the indel evaluation (not built yet)
-        double ms_indel = 0;
-        int64_t n_indel = 0;
+        // per-base indel / insertion / breakpoint tests (row A10) on the device,
+        // then the candidate lists, SV assembly and rows on the host (A13)
+        double ms_sv = 0;
+        std::string sv_text, ctx_text;
+        size_t n_hits = 0;
         {
-            if (!C.indel) C.indel = indel_scratch_new();
-            char ierr[512] = {0};
-            rc = indel_chrom(C.indel, st, n, R->pos, R->mapq, keep, R->cigar_off, R->cigar, R->base_off, R->l_qseq,
-                             R->seq, P.min_mapq, a.eval_lo, a.eval_hi, &n_indel, &ms_indel, ierr, sizeof(ierr));
+            std::vector<SvHit> hits;
+            char serr[512] = {0};
+            rc = sv_evaluate(C.sv, st, P, svin, *ch, a.eval_lo, a.eval_hi, C.d_mq, C.d_hez, hits, &ms_sv, serr,
+                             sizeof(serr));
             if (rc != GROM_OK) {
-                set_err("%s", ierr);
+                set_err("%s", serr);
                 return rc;
             }
+            n_hits = hits.size();
+            if (P.vcf == 1 && !hits.empty()) {
+                // the rows read reference bases (REF text, homopolymer runs):
+                // the caller's host copy when there is one, else one download
+                const char *href = C.host_ref;
+                std::vector<char> ref_copy;
+                if (!href) {
+                    ref_copy.resize((size_t)ch->len);
+                    HIPCHK(hipMemcpyAsync(ref_copy.data(), ch->ref, (size_t)ch->len, hipMemcpyDeviceToHost, st));
+                    HIPCHK(hipStreamSynchronize(st));
+                    href = ref_copy.data();
+                }
+                CafSum cs{st, (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, ch->len, GROM_OK};
+                SvRowsInput ri{&P, ch->name, href, ch->len, &CafSum::call, &cs};
+                sv_rows(ri, hits, sv_text, ctx_text);
+                if (cs.rc != GROM_OK) return cs.rc;
+            }
         }
-        const double t_indel = ms_since(t_start);
+        const double t_sv = ms_since(t_start);
 
         // read-depth CNV path after the SV rows (GROM.c:16633-17300); the
         // reference runs it only when the FASTA name matched a BAM target
@@ -562,17 +631,21 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         const double t_cnv = ms_since(t_start);
         fmt.join();
         const double t_rows = ms_since(t_start);
-        vt.add(snv_text.data(), snv_text.size());  // SNV rows, then the CNV rows (GROM.c:16633)
+        // SNV rows, the breakpoint rows (GROM.c:15163-16580), then the CNV rows (16633)
+        vt.add(snv_text.data(), snv_text.size());
+        vt.add(sv_text.data(), sv_text.size());
         vt.add(cnv_text.data(), cnv_text.size());
+        Text ctt{&out->ctx, &out->ctx_len, &out->ctx_cap};
+        if (!ctx_text.empty()) ctt.add(ctx_text.data(), ctx_text.size());
 
         if (timing)
             fprintf(stderr,
                     "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms (%u candidates), "
-                    "indel evidence %.3f ms (device %.3f ms, %lld bases), "
+                    "breakpoint tests %.3f ms (device %.3f ms, %zu hit bases), "
                     "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows), SNV rows (overlapped) "
                     "joined after %.3f ms more, %u of %lld tiles to the gather kernel\n",
-                    ch->name ? ch->name : "?", t_kernels, t_snv - t_kernels, ncand, t_indel - t_snv, ms_indel,
-                    (long long)n_indel, t_cnv - t_indel, ct.ms_device, (long long)ct.del_calls,
+                    ch->name ? ch->name : "?", t_kernels, t_snv - t_kernels, ncand, t_sv - t_snv, ms_sv,
+                    n_hits, t_cnv - t_sv, ct.ms_device, (long long)ct.del_calls,
                     (long long)ct.dup_calls, (long long)ct.rows, t_rows - t_cnv,
                     gather_only ? (unsigned)n_tiles : n_ovf_tiles, (long long)n_tiles);
         HIPCHK(hipEventRecord(C.e1, st));
@@ -620,6 +693,12 @@ static int upload(Ctx &C, const grom_chrom *ch, const grom_reads *h, grom_chrom 
         (rc = up(C.r_seq, h->seq, (h->n_bases + 1) / 2, st)) || (rc = up(C.r_qual, h->qual, h->n_bases, st)) ||
         (rc = up(C.r_nid, h->name_id, n, st)) || (rc = up(C.ref, ch->ref, ch->len, st)))
         return rc;
+    const bool has_aux = h->n_aux > 0 && h->aux_idx && h->aux;
+    if (has_aux && ((rc = up(C.r_aidx, h->aux_idx, n, st)) || (rc = up(C.r_aux, h->aux, h->n_aux, st)))) return rc;
+    const bool has_drop = h->n_drop > 0 && h->drop_pos && h->drop_lq && h->drop_before;
+    if (has_drop && ((rc = up(C.r_dpos, h->drop_pos, h->n_drop, st)) || (rc = up(C.r_dlq, h->drop_lq, h->n_drop, st)) ||
+                     (rc = up(C.r_dbef, h->drop_before, h->n_drop, st))))
+        return rc;
     *dch = *ch;
     dch->ref = (const char *)C.ref.p;
     *d = *h;
@@ -636,6 +715,13 @@ static int upload(Ctx &C, const grom_chrom *ch, const grom_reads *h, grom_chrom 
     d->seq = (const uint8_t *)C.r_seq.p;
     d->qual = (const uint8_t *)C.r_qual.p;
     d->name_id = (const uint32_t *)C.r_nid.p;
+    d->n_aux = has_aux ? h->n_aux : 0;
+    d->aux_idx = has_aux ? (const int32_t *)C.r_aidx.p : nullptr;
+    d->aux = has_aux ? (const grom_aux *)C.r_aux.p : nullptr;
+    d->n_drop = has_drop ? h->n_drop : 0;
+    d->drop_pos = has_drop ? (const int32_t *)C.r_dpos.p : nullptr;
+    d->drop_lq = has_drop ? (const int32_t *)C.r_dlq.p : nullptr;
+    d->drop_before = has_drop ? (const int64_t *)C.r_dbef.p : nullptr;
     return GROM_OK;
 }
 
@@ -657,6 +743,8 @@ size_t grom_abi_struct_size(int which) {
     case 3: return sizeof(grom_out);
     case 4: return sizeof(grom_stats);
     case 5: return sizeof(grom_indel_rec);
+    case 6: return sizeof(grom_aux);
+    case 7: return sizeof(grom_sv_rec);
     default: return 0;
     }
 }
@@ -704,12 +792,12 @@ void grom_dev_fini(int device) {
     DevBuf *all[] = {&C.r_pos, &C.r_flag, &C.r_mapq, &C.r_mtid, &C.r_mpos, &C.r_isize, &C.r_lq, &C.r_coff,
                      &C.r_cig, &C.r_boff, &C.r_seq, &C.r_qual, &C.r_nid, &C.ref, &C.keep, &C.meta, &C.cands2,
                      &C.runb, &C.runc, &C.segs, &C.ovf, &C.fpart, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
-                     &C.misc, &C.dbg};
+                     &C.misc, &C.dbg, &C.r_aidx, &C.r_aux, &C.r_dpos, &C.r_dlq, &C.r_dbef};
     for (DevBuf *b : all)
         if (b->p) (void)hipFree(b->p);
     if (C.h_cands) (void)hipHostFree(C.h_cands);
     cnv_scratch_free(C.cnv);
-    indel_scratch_free(C.indel);
+    sv_scratch_free(C.sv);
     (void)hipFree(C.d_mq);
     (void)hipFree(C.d_hez);
     (void)hipEventDestroy(C.e0);
@@ -730,7 +818,10 @@ int grom_scan_chrom(int device, const grom_chrom *chrom, const grom_reads *reads
     grom_reads dr;
     int rc = upload(*C, chrom, reads, &dch, &dr);
     if (rc) return rc;
-    return scan_device(*C, &dch, &dr, out, stats, nullptr, nullptr, 0, nullptr);
+    C->host_ref = chrom->ref;
+    rc = scan_device(*C, &dch, &dr, out, stats, nullptr, nullptr, 0, nullptr);
+    C->host_ref = nullptr;
+    return rc;
 }
 
 int grom_scan_chrom_device(int device, const grom_chrom *chrom, const grom_reads *dev_reads, grom_out *out,
@@ -776,12 +867,25 @@ int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *rea
 int64_t grom_debug_indels(int device, grom_indel_rec *out, int64_t cap) {
     Ctx *C = ctx_of(device);
     if (!C) return GROM_E_NODEV;
-    if (!C->indel) return 0;
-    const int64_t n = indel_count(C->indel);
+    if (!C->sv) return 0;
+    const int64_t n = sv_indel_count(C->sv);
     const int64_t m = std::min<int64_t>(n, std::max<int64_t>(cap, 0));
     if (m > 0 && out) {
         HIPCHK(hipSetDevice(C->device));
-        HIPCHK(hipMemcpy(out, indel_records(C->indel), sizeof(grom_indel_rec) * (size_t)m, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(out, sv_indel_records(C->sv), sizeof(grom_indel_rec) * (size_t)m, hipMemcpyDeviceToHost));
+    }
+    return n;
+}
+
+int64_t grom_debug_sv(int device, grom_sv_rec *out, int64_t cap) {
+    Ctx *C = ctx_of(device);
+    if (!C) return GROM_E_NODEV;
+    if (!C->sv) return 0;
+    const int64_t n = sv_debug_count(C->sv);
+    const int64_t m = std::min<int64_t>(n, std::max<int64_t>(cap, 0));
+    if (m > 0 && out) {
+        HIPCHK(hipSetDevice(C->device));
+        HIPCHK(hipMemcpy(out, sv_debug_records(C->sv), sizeof(grom_sv_rec) * (size_t)m, hipMemcpyDeviceToHost));
     }
     return n;
 }

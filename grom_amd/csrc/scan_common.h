@@ -49,6 +49,19 @@ typedef struct grom_snv_cand {
     int32_t pad1;
 } grom_snv_cand;
 
+/* The pileup's counters at a position the breakpoint tests may use (row
+ * A10): every position with soft-clip evidence, and the positions the SV
+ * fold or the insertion ranges mark (sv.hip). */
+typedef struct grom_sv_ctx {
+    int32_t pos;
+    int32_t rd;            /* physical depth over the read spans (GROM.c:7173-7181) */
+    int32_t sc_rd, indel_sc_rd;
+    int32_t sc_left, sc_right, sc_left_rd, sc_right_rd;
+    int32_t indel_sc_left, indel_sc_right;
+    int32_t snv_all;       /* sum of snv[4] + snv_lowmq[4] (GROM.c:11341-11344) */
+    int32_t pad;
+} grom_sv_ctx;
+
 /* scan-wide scalars handed to the kernels */
 typedef struct grom_scan_args {
     int64_t chr_len;

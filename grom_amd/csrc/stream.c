@@ -178,9 +178,86 @@ void grom_batch_init(grom_batch *b, int32_t tid, int read_name_len) {
     b->tid = tid;
     b->p_last = -1;
     b->read_name_len = read_name_len;
+    b->splitread = 1;
+    b->target_name = "";
+}
+
+void grom_batch_set_sv(grom_batch *b, const char *target_name, int splitread) {
+    b->target_name = target_name ? target_name : "";
+    b->splitread = splitread;
+}
+
+void grom_batch_end_record(grom_batch *b, const bam_rec *r) { b->lseq_tail = r->l_qseq; }
+
+/* The SA CIGAR's leading/trailing 'S' and I-D balance (GROM.c:6683-6733):
+ * digits accumulate until a letter closes an op. */
+static void aux_cigar(const char *cig, grom_aux *o) {
+    char num[1001];
+    int nl = 0, n = 0;
+    char first = 0, last = 0;
+    int first_len = 0, last_len = 0;
+    o->start_adj = o->end_adj = o->end_adj_indel = 0;
+    for (const char *c = cig; *c; c++) {
+        if (*c >= '0' && *c <= '9') {
+            if (nl < 1000) num[nl++] = *c;
+        } else if ((*c >= 'A' && *c <= 'Z') || (*c >= 'a' && *c <= 'z')) {
+            num[nl] = 0;
+            int len = (int)strtol(num, NULL, 10);
+            if (n == 0) { first = *c; first_len = len; }
+            last = *c;
+            last_len = len;
+            if (*c == 'I') o->end_adj_indel += len;
+            else if (*c == 'D') o->end_adj_indel -= len;
+            n++;
+            nl = 0;
+            if (n >= 1000) break;
+        }
+    }
+    if (n == 0) return;
+    if (first == 'S') o->start_adj = first_len;
+    if (last == 'S') o->end_adj = last_len;
+}
+
+int grom_parse_aux(const bam_rec *r, const char *target_name, grom_aux *out) {
+    const int l_aux = bam_l_aux(r);
+    if (!(l_aux > 0 && l_aux < 100)) return 0; /* aux_str_len, GROM.c:643, 5763 */
+    int is_xp = 1;
+    const uint8_t *a = bam_aux_find(r, "XP");
+    if (!a) { is_xp = 0; a = bam_aux_find(r, "SA"); }
+    if (!a) return 0;
+    char buf[128];
+    const uint8_t *src = (a[0] == 'Z') ? a + 1 : a, *end = r->data + r->data_len;
+    int k = 0;
+    while (src + k < end && src[k] && k < (int)sizeof(buf) - 1) { buf[k] = (char)src[k]; k++; }
+    buf[k] = 0;
+    char *save = NULL;
+    char *chr = strtok_r(buf, ",", &save);
+    char *t1 = strtok_r(NULL, ",", &save);
+    memset(out, 0, sizeof(*out));
+    char *cig, *mq;
+    if (is_xp) { /* XP:Z:chr,+pos,CIGAR,mapq (GROM.c:5776-5790) */
+        if (!t1) return 0;
+        out->strand = (t1[0] == '+') ? 0 : 1;
+        out->pos = atoi(t1 + 1);
+        cig = strtok_r(NULL, ",", &save);
+        mq = strtok_r(NULL, ",", &save);
+    } else { /* SA:Z:chr,pos,strand,CIGAR,mapq,NM; (GROM.c:5806-5820) */
+        char *t2 = strtok_r(NULL, ",", &save);
+        if (!t1 || !t2) return 0;
+        out->pos = atoi(t1);
+        out->strand = (t2[0] == '+') ? 0 : 1;
+        cig = strtok_r(NULL, ",", &save);
+        mq = strtok_r(NULL, ",", &save);
+    }
+    if (!chr || !cig) return 0;
+    out->mq = (int16_t)(mq ? atoi(mq) : 0);
+    out->same_chr = strncmp(target_name, chr, strlen(target_name)) == 0;
+    aux_cigar(cig, out);
+    return 1;
 }
 
 void grom_batch_free(grom_batch *b) {
+    free(b->aux_idx); free(b->aux); free(b->drop_pos); free(b->drop_lq); free(b->drop_before);
     free(b->pos); free(b->flag); free(b->mapq); free(b->mtid); free(b->mpos); free(b->isize); free(b->l_qseq);
     free(b->cigar_off); free(b->cigar); free(b->base_off); free(b->seq); free(b->qual); free(b->name_id);
     for (int64_t i = 0; i < b->ncap; i++) free(b->nkeys[i]);
@@ -226,13 +303,34 @@ static uint32_t intern(grom_batch *b, const char *s) {
 }
 
 void grom_batch_add(grom_batch *b, const bam_rec *r, int32_t index_start) {
+    /* which fetch site loaded this record: the scan start (GROM.c:5743) and
+     * the skip branch (14861) parse SA/XP always, the ingest loop (10968)
+     * only without -S */
+    const int parse_aux = (b->n_seen == 0) || b->prev_skipped || b->splitread;
+    b->n_seen++;
     if (r->pos < index_start && !b->any_ingested) { /* skip branch, GROM.c:14859-14969 */
         b->n_skip++;
+        b->prev_skipped = 1;
         return;
     }
+    b->prev_skipped = 0;
     b->any_ingested = 1;
     b->last_pos = r->pos;
-    if ((r->flag & GF_UNMAP) || (r->flag & GF_DUP)) return; /* GROM.c:6418 */
+    b->lseq_tail = r->l_qseq; /* at end of file the last record's length (plus hard clips, below) */
+    if ((r->flag & GF_UNMAP) || (r->flag & GF_DUP)) { /* GROM.c:6418 */
+        if (b->n_drop + 1 > b->cap_drop) {
+            int64_t nc = b->cap_drop ? 2 * b->cap_drop : 1024;
+            b->drop_pos = realloc(b->drop_pos, sizeof(int32_t) * nc);
+            b->drop_lq = realloc(b->drop_lq, sizeof(int32_t) * nc);
+            b->drop_before = realloc(b->drop_before, sizeof(int64_t) * nc);
+            b->cap_drop = nc;
+        }
+        b->drop_pos[b->n_drop] = r->pos;
+        b->drop_lq[b->n_drop] = r->l_qseq;
+        b->drop_before[b->n_drop] = b->n;
+        b->n_drop++;
+        return;
+    }
     int64_t i = b->n;
     if (i + 1 > b->cap) {
         int64_t nc = b->cap ? b->cap * 2 : 1024;
@@ -246,7 +344,21 @@ void grom_batch_add(grom_batch *b, const bam_rec *r, int32_t index_start) {
         b->cigar_off = realloc(b->cigar_off, sizeof(uint32_t) * (nc + 1));
         b->base_off = realloc(b->base_off, sizeof(int64_t) * nc);
         b->name_id = realloc(b->name_id, sizeof(uint32_t) * nc);
+        b->aux_idx = realloc(b->aux_idx, sizeof(int32_t) * nc);
         b->cap = nc;
+    }
+    {
+        grom_aux ax;
+        b->aux_idx[i] = -1;
+        if (parse_aux && grom_parse_aux(r, b->target_name, &ax)) {
+            if (b->n_aux + 1 > b->cap_aux) {
+                int64_t nc = b->cap_aux ? 2 * b->cap_aux : 1024;
+                b->aux = realloc(b->aux, sizeof(grom_aux) * nc);
+                b->cap_aux = nc;
+            }
+            b->aux_idx[i] = (int32_t)b->n_aux;
+            b->aux[b->n_aux++] = ax;
+        }
     }
     b->pos[i] = r->pos;
     b->flag[i] = r->flag;
@@ -270,6 +382,8 @@ void grom_batch_add(grom_batch *b, const bam_rec *r, int32_t index_start) {
         if (op == GC_MATCH || op == GC_DEL || op == GC_REF_SKIP || op == GC_EQUAL || op == GC_DIFF) span += (int32_t)(cg[k] >> 4);
     }
     if (span > b->max_ref_span) b->max_ref_span = span;
+    for (int k = 0; k < r->n_cigar; k++) /* the ingest adds hard clips to cdp_lseq, GROM.c:6997-7000 */
+        if ((cg[k] & 0xf) == GC_HARD_CLIP) b->lseq_tail += (int32_t)(cg[k] >> 4);
     b->n_cig += r->n_cigar;
     b->cigar_off[i + 1] = (uint32_t)b->n_cig;
     int64_t L = r->l_qseq, Lp = (L + 1) & ~1LL; /* keep every read's first base on a byte */
@@ -314,6 +428,13 @@ void grom_batch_view(const grom_batch *b, grom_reads *o) {
     o->seq = b->seq;
     o->qual = b->qual;
     o->name_id = b->name_id;
+    o->n_aux = b->n_aux;
+    o->aux_idx = b->aux_idx;
+    o->aux = b->aux;
+    o->n_drop = b->n_drop;
+    o->drop_pos = b->drop_pos;
+    o->drop_lq = b->drop_lq;
+    o->drop_before = b->drop_before;
 }
 
 /* ---------------- serial stream planner ---------------- */

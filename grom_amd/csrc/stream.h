@@ -80,9 +80,29 @@ typedef struct grom_batch {
     int32_t max_ref_span;  /* max over reads of the M/D/N/=/X extent */
     int read_name_len;
     int any_ingested;
+    /* split-read alignments (SA:Z / XP:Z) of the kept reads */
+    int32_t *aux_idx;
+    grom_aux *aux;
+    int64_t n_aux, cap_aux;
+    /* records dropped by the flag filter (unmapped / duplicate) */
+    int32_t *drop_pos, *drop_lq;
+    int64_t *drop_before;
+    int64_t n_drop, cap_drop;
+    int32_t lseq_tail;     /* grom_chrom.lseq_tail */
+    const char *target_name; /* BAM name of the chromosome (the SA chromosome test) */
+    int splitread;         /* g_splitread: -S gates the ingest-loop fetch only */
+    int n_seen, prev_skipped;
 } grom_batch;
 
 void grom_batch_init(grom_batch *b, int32_t tid, int read_name_len);
+/* the chromosome's BAM target name and -S (before the first add) */
+void grom_batch_set_sv(grom_batch *b, const char *target_name, int splitread);
+/* the record of another chromosome that ends this one's stream (its length
+ * is what the walk's last evaluated base sees) */
+void grom_batch_end_record(grom_batch *b, const bam_rec *r);
+/* GROM's SA/XP parse of one record (GROM.c:5763-5826, 6683-6733); returns 1
+ * and fills *out when the record carries one it would read */
+int grom_parse_aux(const bam_rec *r, const char *target_name, grom_aux *out);
 void grom_batch_free(grom_batch *b);
 /* feed one record of this chromosome's stream (in stream order) */
 void grom_batch_add(grom_batch *b, const bam_rec *r, int32_t index_start);

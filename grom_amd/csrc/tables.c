@@ -133,6 +133,24 @@ void grom_default_params(grom_params *p) {
     p->min_repeat_stdev = 1.5;
     p->rd_pval_threshold = 0.000000001;
     p->mapq_factor = 0.5;
+    /* breakpoint path (GROM.c:810-969) */
+    p->min_disc = 3;
+    p->sc_range = 35;
+    p->max_split_loss = 20;
+    p->min_sr_len = 30;
+    p->max_homopolymer = 10;
+    p->max_ins_range = 10;
+    p->sv_list2_len = p->sv_list_len / 10;
+    p->pval_threshold = 0.001;
+    p->pval_threshold1 = 0.001; /* = g_pval_threshold, GROM.c:22101 */
+    p->pval_insertion1 = 0.01;
+    p->pval_insertion = 0.0000000001;
+    p->min_sv_ratio = 0.05;
+    p->min_indel_ratio = 0.125;
+    p->max_evidence_ratio = 0.25;
+    p->range_mult = 0.75;
+    p->max_inv_rd_diff = 1.75;
+    p->min_overlap_ratio = 0.5;
 }
 
 void grom_params_set_insert(grom_params *p, int32_t mean, int32_t imin, int32_t imax, int32_t lseq) {

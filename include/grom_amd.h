@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GROM_AMD_ABI_VERSION 3
+#define GROM_AMD_ABI_VERSION 4
 #define GROM_MAX_TRIALS 1000 /* max_trials, GROM.c:631 */
 
 enum {
@@ -91,6 +91,25 @@ typedef struct grom_params {
     double min_repeat_stdev;      /* g_min_repeat_stdev (-E), GROM.c:734 */
     double rd_pval_threshold;     /* g_rd_pval_threshold (-V), GROM.c:722 */
     double mapq_factor;           /* g_mapq_factor (-F), GROM.c:719 */
+    /* breakpoint path (rows A8-A13), ABI 4 */
+    int32_t min_disc;             /* g_min_disc (-d), GROM.c:810 */
+    int32_t sc_range;             /* g_sc_range, GROM.c:812 */
+    int32_t max_split_loss;       /* g_max_split_loss (-y), GROM.c:967 */
+    int32_t min_sr_len;           /* g_min_sr_len (-z), GROM.c:969 */
+    int32_t max_homopolymer;      /* g_max_homopolymer (-k), GROM.c:898 */
+    int32_t max_ins_range;        /* g_max_ins_range (-w), GROM.c:899 */
+    int32_t sv_list2_len;         /* g_sv_list2_len (-G sets it to G/10), GROM.c:831 */
+    int32_t pad_sv;
+    double pval_threshold;        /* g_pval_threshold (-v), GROM.c:942 */
+    double pval_threshold1;       /* g_pval_threshold1 = g_pval_threshold, GROM.c:22101 */
+    double pval_insertion1;       /* g_pval_insertion1, GROM.c:943 */
+    double pval_insertion;        /* g_pval_insertion (-e), GROM.c:944 */
+    double min_sv_ratio;          /* g_min_sv_ratio (-j), GROM.c:901 */
+    double min_indel_ratio;       /* g_min_indel_ratio (-m), GROM.c:902 */
+    double max_evidence_ratio;    /* g_max_evidence_ratio (-u), GROM.c:900 */
+    double range_mult;            /* g_range_mult, GROM.c:828 */
+    double max_inv_rd_diff;       /* g_max_inv_rd_diff, GROM.c:907 */
+    double min_overlap_ratio;     /* g_min_overlap_ratio, GROM.c:817 */
 } grom_params;
 
 /* One chromosome.  `ref` holds exactly what find_disc_svs loaded
@@ -109,7 +128,27 @@ typedef struct grom_chrom {
                            when the FASTA name matched a BAM target) */
     uint32_t seed;      /* CNV sampling seed: replaces srand(time()) at
                            GROM.c:1584 */
+    int32_t lseq_tail;  /* cdp_lseq when the walk evaluates p_last: l_qseq of
+                           the record that ended the chromosome's stream, or
+                           at end of file the last record's (plus its hard
+                           clips when it was ingested).  The breakpoint tests
+                           read the pending record's length (GROM.c:12047) */
+    int32_t pad;
 } grom_chrom;
+
+/* The SA:Z / XP:Z alignment of a read as GROM parses it (GROM.c:5763-5826,
+ * 6683-6733): only when the record's aux block is 1..99 bytes, and under -S
+ * only for records not fetched inside the ingest loop. */
+typedef struct grom_aux {
+    int32_t pos;            /* as written in the tag (1-based, kept as is) */
+    int32_t start_adj;      /* leading 'S' of its CIGAR */
+    int32_t end_adj;        /* trailing 'S' */
+    int32_t end_adj_indel;  /* sum I - sum D */
+    int16_t mq;             /* atoi of the mapq field */
+    uint8_t strand;         /* 0 '+', 1 otherwise */
+    uint8_t same_chr;       /* strncmp(target_name, tag_chr, strlen(target_name)) == 0 */
+    int32_t pad;
+} grom_aux;
 
 /* The records the chromosome's scan ingests (stream order, after the serial
  * stream's boundary drops and the n_skip prefix), minus records flagged
@@ -134,6 +173,18 @@ typedef struct grom_reads {
     const uint8_t *qual;
     const uint32_t *name_id;    /* equal ids <=> equal read names; 0 = a
                                    name that is never stored (len >= 50) */
+    /* ABI 4: split-read alignments: aux_idx[i] indexes aux[] or is -1 */
+    int64_t n_aux;
+    const int32_t *aux_idx;
+    const grom_aux *aux;
+    /* ABI 4: the records of the stream dropped from the arrays above
+     * (unmapped / duplicate flag): position, l_qseq, and how many kept
+     * reads precede each in stream order.  The breakpoint tests read the
+     * length of the next record in the stream (GROM.c:12047). */
+    int64_t n_drop;
+    const int32_t *drop_pos;
+    const int32_t *drop_lq;
+    const int64_t *drop_before;
 } grom_reads;
 
 /* Growable output text (the two FILE*s of count_discordant_pairs). */
@@ -160,7 +211,7 @@ int grom_abi_version(void);
 int grom_device_count(void);
 /* sizeof of the ABI structs, for bindings to check their layout:
  * 0 grom_params, 1 grom_chrom, 2 grom_reads, 3 grom_out, 4 grom_stats,
- * 5 grom_indel_rec */
+ * 5 grom_indel_rec, 6 grom_aux, 7 grom_sv_rec */
 size_t grom_abi_struct_size(int which);
 /* The message of the last failing call made FROM THE CALLING HOST THREAD
  * (errors are kept per thread, since contexts run concurrently).
@@ -212,7 +263,7 @@ int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *rea
  * forward-deletion and reverse-deletion counters (+6 per MAPQ >= -q read, 0
  * otherwise) with their lengths, the deletion read depths, the number of
  * occupied "other" slots as the evaluation counts them (GROM.c:11415-11425;
- * indel-typed slots only in this build) and the 50-byte inserted-sequence
+ * the slots are shared with the breakpoint clusters) and the 50-byte inserted-sequence
  * buffer (zero-filled when the base enters the window). */
 typedef struct grom_indel_rec {
     int32_t pos;
@@ -225,10 +276,33 @@ typedef struct grom_indel_rec {
 } grom_indel_rec;
 
 /* Test hook: the indel evidence records of the last scan on `device` (one per
- * evaluated base that a CIGAR I/D op reached, in position order).  Copies at
+ * evaluated base that a CIGAR I/D op or a split-read deletion reached, in
+ * position order).  Copies at
  * most `cap` records to `out` (may be NULL with cap 0) and returns how many
  * the scan produced, or a negative GROM_E_* code. */
 int64_t grom_debug_indels(int device, grom_indel_rec *out, int64_t cap);
+
+/* Breakpoint cluster state of one evaluated base (rows A8/A9; replaces the
+ * reference's cdp_one_base_{del,dup,inv,ctx}_* ring arrays and the "other"
+ * slots, GROM.c:7431-10953) as the per-base tests see it: per cluster type
+ * (DEL_F, DEL_R, DUP_F, DUP_R, INV_F1, INV_R1, INV_F2, INV_R2, CTX_F, CTX_R)
+ * the weighted count, running-mean distance (the mate position for CTX) and
+ * first/last read positions; the CTX mate chromosomes; the number of
+ * occupied "other" slots; and the order-free range sums at the base: depth
+ * adds, concordant pairs, short-insert pairs and unmapped-mate reads. */
+typedef struct grom_sv_rec {
+    int32_t pos, other_len;
+    int32_t cnt[10], rs[10], re[10];
+    double dist[10];
+    int32_t ctx_mchr[2];
+    int32_t rd_add, conc, ins, mun_f, mun_r, pad;
+} grom_sv_rec;
+
+/* Test hook: the breakpoint records of the last scan on `device`: one per
+ * evaluated base with a nonzero cluster count or an occupied "other" slot,
+ * in position order; same calling convention as grom_debug_indels.  Needs the
+ * scan to run with GROM_SV_DEBUG set in the environment. */
+int64_t grom_debug_sv(int device, grom_sv_rec *out, int64_t cap);
 
 /* Host helpers shared by the CLI and the tests (grom_amd/csrc/tables.c):
  * the tables exactly as a run with -q min_mapq uses them. */

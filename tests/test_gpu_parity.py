@@ -28,6 +28,12 @@ RUNS = [
     ("indels", []),
     ("indels", ["-M"]),
     ("indels", ["-q", "10"]),
+    # breakpoint path (rows A8-A10, A13): split reads, pair classes, the
+    # per-base tests, the candidate lists, SV rows and the CTX post-pass
+    ("sv", []),
+    ("sv", ["-S"]),
+    ("sv", ["-d", "2", "-u", "0.5", "-j", "0.02"]),
+    ("sv", ["-l", "2"]),
 ]
 
 # read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call

@@ -25,11 +25,12 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 15
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.grom_abi_version() == 3
+    assert lib.grom_abi_version() == 4
     # the ctypes mirror has the C layout of every ABI struct
     for i, st in enumerate((grom_amd.Params, grom_amd.Chrom, grom_amd.Reads, grom_amd.Out, grom_amd.Stats,
-                              grom_amd.IndelRec)):
+                              grom_amd.IndelRec, grom_amd.Aux, grom_amd.SvRec)):
         assert lib.grom_abi_struct_size(i) == ctypes.sizeof(st), st.__name__
+    assert grom_amd.SV_DTYPE.itemsize == ctypes.sizeof(grom_amd.SvRec)
     # and the python binding declares a signature for each
     assert set(names) <= set(grom_amd._SIGS), set(names) - set(grom_amd._SIGS)
 

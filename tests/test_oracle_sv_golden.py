@@ -23,14 +23,14 @@ import re
 import numpy as np
 import pytest
 
-from _util import GOLDEN_VCF, synth, run_oracle
+from _util import CASES, GOLDEN_VCF, synth, run_oracle
 from test_oracle_golden import oracle_tables
 
 AF = 6  # cdp_add_factor
 PVAL = 0.001  # g_pval_threshold (also g_pval_threshold1, GROM.c:22101)
 
 # SV parity case: one 600 kb chromosome + a 300 kb partner for translocations
-SV_CASE = ["-L", "600000,300000", "-s", "31", "-X", "30", "-I", "0.0003", "-J", "0.3", "-Q", "0.05"]
+SV_CASE = CASES["sv"]
 
 
 def _rows():
