@@ -94,6 +94,13 @@ def _check_counters(datadir, case, extra, tag, env_extra=None):
     assert ov.count("\n") > 46
     assert ov == gv
     assert filecmp.cmp(datadir / f"o_{tag}.ctx.vcf", datadir / f"g_{tag}.ctx.vcf", shallow=False)
+    if case == "sv":
+        # the comparison covered every breakpoint row class
+        alts = {l.split("\t")[4] for l in gv.splitlines() if not l.startswith("#")}
+        assert {"<DEL>", "<DUP>", "<INV>"} <= alts, alts
+        assert any(l.startswith("SPR:SEV:SRD:SCO:ECO") or "SPR:SEV:SRD:SCO:ECO" in l for l in gv.splitlines())
+        bnd = [l for l in open(datadir / f"g_{tag}.ctx.vcf") if not l.startswith("#")]
+        assert bnd and all("SVTYPE=BND" in l for l in bnd)
 
 
 @pytest.mark.parametrize("case,extra", RUNS, ids=[f"{c}{''.join(e)}" for c, e in RUNS])
