@@ -60,6 +60,16 @@ class Aux(C.Structure):
         [("mq", C.c_int16), ("strand", C.c_uint8), ("same_chr", C.c_uint8), ("pad", C.c_int32)]
 
 
+class SynthSpec(C.Structure):
+    """grom_synth_spec: one chromosome of a multi-chromosome synthetic genome."""
+    _fields_ = [("n_chr", C.c_int32), ("chrom", C.c_int32), ("chr_len", C.POINTER(C.c_int64)),
+                ("names", C.c_char_p), ("coverage", C.c_double), ("read_len", C.c_int32), ("ploidy", C.c_int32),
+                ("insert_mean", C.c_double), ("insert_sd", C.c_double), ("dup_frac", C.c_double),
+                ("sv_per_mb", C.c_double), ("cnv_rate", C.c_double), ("cnv_min", C.c_int64),
+                ("cnv_max", C.c_int64), ("chr_cov", C.POINTER(C.c_double)), ("munmap_frac", C.c_double),
+                ("seed", C.c_uint64)]
+
+
 class Out(C.Structure):
     _fields_ = [("vcf", C.c_void_p), ("vcf_len", C.c_size_t), ("vcf_cap", C.c_size_t),
                 ("ctx", C.c_void_p), ("ctx_len", C.c_size_t), ("ctx_cap", C.c_size_t)]
@@ -115,6 +125,11 @@ _SIGS = {
     "grom_upload": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Chrom), C.POINTER(Reads)]),
     "grom_synth_batch": (C.c_void_p, [C.c_int64, C.c_double, C.c_int32, C.c_double, C.c_double, C.c_uint64,
                                       C.POINTER(Params)]),
+    "grom_synth_chrom": (C.c_void_p, [C.POINTER(SynthSpec), C.POINTER(Params)]),
+    "grom_resident_new": (C.c_void_p, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Chrom),
+                                       C.POINTER(Reads)]),
+    "grom_resident_bytes": (C.c_int64, [C.c_void_p]),
+    "grom_resident_free": (None, [C.c_void_p]),
     "grom_batch_get": (C.c_int, [C.c_void_p, C.POINTER(Chrom), C.POINTER(Reads)]),
     "grom_batch_release": (None, [C.c_void_p]),
     "grom_cli_main": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
@@ -213,18 +228,55 @@ class Device:
         return cnt[:n_eval], caf
 
 
+class Resident:
+    """A chromosome's inputs kept in HBM (grom_resident_new); scan them from any
+    context on the same device with Device.scan(..., device_resident=True)."""
+
+    def __init__(self, device: int, chrom: Chrom, reads: Reads):
+        self.chrom, self.reads = Chrom(), Reads()
+        self.h = lib().grom_resident_new(device, C.byref(chrom), C.byref(reads), C.byref(self.chrom),
+                                         C.byref(self.reads))
+        if not self.h:
+            raise RuntimeError(f"grom_resident_new failed: {last_error()}")
+        self.bytes = lib().grom_resident_bytes(self.h)
+        # the name is host text owned by the source batch: keep a copy here
+        self.chrom.name = bytes(chrom.name or b"")
+
+    def close(self):
+        if self.h:
+            lib().grom_resident_free(self.h)
+            self.h = None
+
+
 class SynthBatch:
     """A synthetic chromosome and the read batch its scan ingests (host memory)."""
 
     def __init__(self, length: int, coverage: float = 30.0, read_len: int = 150, insert_mean: float = 500.0,
-                 insert_sd: float = 50.0, seed: int = 2, params: Params | None = None):
+                 insert_sd: float = 50.0, seed: int = 2, params: Params | None = None, _handle=None):
         self.params = params if params is not None else default_params()
-        self.h = lib().grom_synth_batch(length, coverage, read_len, insert_mean, insert_sd, seed,
-                                        C.byref(self.params))
+        self.h = _handle if _handle is not None else lib().grom_synth_batch(
+            length, coverage, read_len, insert_mean, insert_sd, seed, C.byref(self.params))
         if not self.h:
             raise RuntimeError("grom_synth_batch failed")
         self.chrom, self.reads = Chrom(), Reads()
         check(lib().grom_batch_get(self.h, C.byref(self.chrom), C.byref(self.reads)), "grom_batch_get")
+
+    @classmethod
+    def genome_chrom(cls, lengths, chrom: int, params: Params, names=None, coverage: float = 30.0,
+                     read_len: int = 150, ploidy: int = 2, insert_mean: float = 500.0, insert_sd: float = 50.0,
+                     dup_frac: float = 0.0, sv_per_mb: float = 0.0, cnv_rate: float = 0.0,
+                     cnv_range=(0, 0), chr_cov=None, munmap_frac: float = 0.002, seed: int = 2) -> "SynthBatch":
+        """Chromosome `chrom` of a multi-chromosome synthetic genome (grom_synth_chrom).
+        `params` keeps genome-wide insert statistics once set (see include/grom_amd.h)."""
+        arr = (C.c_int64 * len(lengths))(*lengths)
+        cov = (C.c_double * len(lengths))(*chr_cov) if chr_cov is not None else None
+        sp = SynthSpec(len(lengths), chrom, arr, ",".join(names).encode() if names else None, coverage, read_len,
+                       ploidy, insert_mean, insert_sd, dup_frac, sv_per_mb, cnv_rate, cnv_range[0], cnv_range[1],
+                       cov, munmap_frac, seed)
+        h = lib().grom_synth_chrom(C.byref(sp), C.byref(params))
+        if not h:
+            raise RuntimeError(f"grom_synth_chrom failed for chromosome {chrom}")
+        return cls(lengths[chrom], params=params, _handle=h)
 
     def close(self):
         if self.h:

@@ -1220,6 +1220,14 @@ __global__ __launch_bounds__(64) void k_cnv_walk_fix(WalkIn W, const int32_t *nx
     }
 }
 
+// repeat z overrides (GROM.c:19022-19150): positions are unique here (the
+// host keeps the last write of each), so a plain scatter
+__global__ void k_cnv_zscatter(const int64_t *__restrict__ pos, const double *__restrict__ z, int64_t n,
+                               double *__restrict__ sd) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sd[pos[i]] = z[i];
+}
+
 // a call is on the true walk iff its start was visited in its class
 __global__ void k_cnv_calls_valid(const CallRec *calls, uint32_t n, const uint8_t *vis, uint8_t *ok) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1250,6 +1258,7 @@ struct CnvScratch {
     hipEvent_t gc_done = nullptr;
     const char *gc_ref = nullptr;
     int64_t gc_len = -1, gc_m = -1;
+    Buf zover;  // repeat z overrides: positions then values
     Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1443,7 +1452,7 @@ void cnv_scratch_free(CnvScratch *S) {
     Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre,
                   &S->prepos, &S->ppos, &S->rep, &S->misc, &S->blk, &S->hist,
                   &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
-                  &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok};
+                  &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover};
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
     for (KindBufs &K : S->kb) {
@@ -1982,9 +1991,32 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     nz++;
                 }
             }
-            // later writes win, as in the reference's loop order
-            for (int64_t i = 0; i < nz; i++) CK(hipMemcpyAsync(sd + zp[i], &zv[i], 8, hipMemcpyHostToDevice, st));
-            CK(hipStreamSynchronize(st));
+            // later writes win, as in the reference's loop order: keep each
+            // position's last value, then one upload and a scatter
+            std::vector<int64_t> ord(nz);
+            for (int64_t i = 0; i < nz; i++) ord[i] = i;
+            std::stable_sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) { return zp[x] < zp[y]; });
+            std::vector<int64_t> up_p;
+            std::vector<double> up_z;
+            up_p.reserve(nz);
+            up_z.reserve(nz);
+            for (int64_t k = 0; k < nz; k++) {
+                const int64_t i = ord[k];
+                if (k + 1 < nz && zp[ord[k + 1]] == zp[i]) continue;  // a later write to the same base wins
+                up_p.push_back(zp[i]);
+                up_z.push_back(zv[i]);
+            }
+            const int64_t nu = (int64_t)up_p.size();
+            if (nu > 0) {
+                if ((rc = grow(S->zover, 16 * (size_t)nu, err, errlen))) return rc;
+                int64_t *dp = (int64_t *)S->zover.p;
+                double *dz = (double *)(dp + nu);
+                CK(hipMemcpyAsync(dp, up_p.data(), 8 * nu, hipMemcpyHostToDevice, st));
+                CK(hipMemcpyAsync(dz, up_z.data(), 8 * nu, hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_cnv_zscatter, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0, st, dp, dz, nu, sd);
+                CK(hipGetLastError());
+                CK(hipStreamSynchronize(st));  // the host vectors are released on return
+            }
         }
         CK(hipMemcpyAsync(S->wsd.p, wsd.data(), 8 * (L + 1), hipMemcpyHostToDevice, st));
 

@@ -14,6 +14,7 @@ struct grom_batch_handle {
     grom_batch b;
     char *ref;
     int64_t len;
+    int32_t tid;
     char name[48];
     /* insert statistics sample (find_insert_mean's rule) */
     int *ins, *lq;
@@ -43,6 +44,22 @@ static void on_record(void *ctx, const bam_rec *r) {
 }
 
 static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
+
+/* find_insert_mean's statistics (GROM.c:1276-1310) from the sampled pairs */
+static void insert_stats(struct grom_batch_handle *h, grom_params *P) {
+    qsort(h->ins, h->n_ins, sizeof(int), icmp);
+    int64_t n = h->n_ins;
+    int mean = h->ins[n / 2], lim = mean * 5;
+    int64_t end = 0;
+    for (int64_t a = n - 1; a >= 0; a--)
+        if (h->ins[a] <= lim) { end = a; break; }
+    end += 1;
+    mean = h->ins[end / 2];
+    int lo = (int)(grom_prob2(3.0) * end / 2);
+    int imin = h->ins[lo], imax = h->ins[end - lo < n ? end - lo : n - 1];
+    qsort(h->lq, n, sizeof(int), icmp);
+    grom_params_set_insert(P, mean, imin, imax, h->lq[n / 2]);
+}
 
 /* drop the leading records with pos < s0 (the walk's skip branch) */
 static void trim_prefix(grom_batch *b, int32_t s0, int64_t *n_dropped_mapped) {
@@ -101,19 +118,7 @@ grom_batch_handle *grom_synth_batch(int64_t chr_len, double coverage, int32_t re
     grom_batch_init(&h->b, 0, P->read_name_len);
     synth_reads(&c, 0, h->ref, on_record, h);
     if (h->n_ins == 0) { grom_batch_release(h); return NULL; }
-    /* find_insert_mean, GROM.c:1276-1310 */
-    qsort(h->ins, h->n_ins, sizeof(int), icmp);
-    int64_t n = h->n_ins;
-    int mean = h->ins[n / 2], lim = mean * 5;
-    int64_t end = 0;
-    for (int64_t a = n - 1; a >= 0; a--)
-        if (h->ins[a] <= lim) { end = a; break; }
-    end += 1;
-    mean = h->ins[end / 2];
-    int lo = (int)(grom_prob2(3.0) * end / 2);
-    int imin = h->ins[lo], imax = h->ins[end - lo < n ? end - lo : n - 1];
-    qsort(h->lq, n, sizeof(int), icmp);
-    grom_params_set_insert(P, mean, imin, imax, h->lq[n / 2]);
+    insert_stats(h, P);
     int32_t s0 = P->one_base_rd_len / 4 + 1;
     int64_t dropped = 0;
     trim_prefix(&h->b, s0, &dropped);
@@ -124,12 +129,86 @@ grom_batch_handle *grom_synth_batch(int64_t chr_len, double coverage, int32_t re
     return h;
 }
 
+/* records straight into the batch with the walk's skip rule applied
+ * (index_start known up front: the insert statistics are already set) */
+struct direct_ctx { grom_batch *b; int32_t s0; };
+static void on_record_direct(void *ctx, const bam_rec *r) {
+    struct direct_ctx *d = (struct direct_ctx *)ctx;
+    grom_batch_add(d->b, r, d->s0);
+}
+
+grom_batch_handle *grom_synth_chrom(const grom_synth_spec *sp, grom_params *P) {
+    if (!sp || !P || sp->n_chr < 1 || sp->n_chr > SYNTH_MAX_CHR || sp->chrom < 0 || sp->chrom >= sp->n_chr ||
+        !sp->chr_len)
+        return NULL;
+    synth_cfg c;
+    synth_default_cfg(&c);
+    c.n_chr = sp->n_chr;
+    for (int i = 0; i < c.n_chr; i++) {
+        c.chr_len[i] = sp->chr_len[i];
+        snprintf(c.chr_name[i], sizeof(c.chr_name[i]), "chr%d", i + 1);
+    }
+    if (sp->names) { /* comma-separated, as grom_synth -n */
+        const char *q = sp->names;
+        for (int i = 0; i < c.n_chr && *q; i++) {
+            const char *e = strchr(q, ',');
+            size_t l = e ? (size_t)(e - q) : strlen(q);
+            if (l >= sizeof(c.chr_name[i])) l = sizeof(c.chr_name[i]) - 1;
+            memcpy(c.chr_name[i], q, l);
+            c.chr_name[i][l] = 0;
+            if (!e) break;
+            q = e + 1;
+        }
+    }
+    if (sp->coverage > 0) c.coverage = sp->coverage;
+    if (sp->read_len > 0) c.read_len = sp->read_len;
+    if (sp->ploidy > 0) c.ploidy = sp->ploidy;
+    if (sp->insert_mean > 0) c.insert_mean = sp->insert_mean;
+    if (sp->insert_sd > 0) c.insert_sd = sp->insert_sd;
+    c.dup_frac = sp->dup_frac;
+    c.sv_per_mb = sp->sv_per_mb;
+    c.cnv_rate = sp->cnv_rate;
+    if (sp->cnv_min > 0) c.cnv_min = sp->cnv_min;
+    if (sp->cnv_max > 0) c.cnv_max = sp->cnv_max;
+    if (sp->chr_cov)
+        for (int i = 0; i < c.n_chr; i++) c.chr_cov[i] = sp->chr_cov[i];
+    c.munmap_frac = sp->munmap_frac;
+    c.seed = sp->seed;
+    const int ci = sp->chrom;
+    struct grom_batch_handle *h = calloc(1, sizeof(*h));
+    if (!h) return NULL;
+    h->len = c.chr_len[ci];
+    h->tid = ci;
+    snprintf(h->name, sizeof(h->name), "%s", c.chr_name[ci]);
+    /* the scan takes the lower-cased FASTA name (GROM.c:20893-20906) */
+    for (char *q = h->name; *q; q++)
+        if (*q >= 'A' && *q <= 'Z') *q = (char)(*q + 32);
+    h->ref = synth_reference(&c, ci);
+    grom_batch_init(&h->b, ci, P->read_name_len);
+    grom_batch_set_sv(&h->b, c.chr_name[ci], P->splitread);
+    if (P->half_one_base_rd_len > 0) {
+        struct direct_ctx d = {&h->b, P->one_base_rd_len / 4 + 1};
+        synth_reads(&c, ci, h->ref, on_record_direct, &d);
+    } else {
+        synth_reads(&c, ci, h->ref, on_record, h);
+        if (h->n_ins == 0) { grom_batch_release(h); return NULL; }
+        insert_stats(h, P);
+        int64_t dropped = 0;
+        trim_prefix(&h->b, P->one_base_rd_len / 4 + 1, &dropped);
+        h->b.n_skip = (int32_t)dropped;
+        h->b.any_ingested = h->b.n > 0;
+        if (h->b.n > 0) h->b.last_pos = h->b.pos[h->b.n - 1];
+    }
+    grom_batch_finish(&h->b, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size);
+    return h;
+}
+
 int grom_batch_get(grom_batch_handle *h, grom_chrom *ch, grom_reads *rd) {
     if (!h) return GROM_E_ARG;
     ch->ref = h->ref;
     ch->len = h->len;
     ch->name = h->name;
-    ch->tid = 0;
+    ch->tid = h->tid;
     ch->n_skip = h->b.n_skip;
     ch->p_last = h->b.p_last;
     ch->cnv = 1;

@@ -229,6 +229,13 @@ struct Ctx {
     DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, ovf, fpart;
     grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
     const char *host_ref = nullptr;    // the caller's host reference during grom_scan_chrom
+    // device-resident scans: the breakpoint rows read reference bases on the
+    // host, so the reference is copied into this pinned buffer on a side
+    // stream while the pileup runs (ref_ev marks the copy done)
+    char *h_ref = nullptr;
+    size_t h_ref_cap = 0;
+    hipStream_t st_copy = nullptr;
+    hipEvent_t ref_ev = nullptr;
     size_t h_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, ep0 = nullptr, ep1 = nullptr;
     CnvScratch *cnv = nullptr;  // read-depth CNV path (cnv.hip)
@@ -400,6 +407,21 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     unsigned long long *d_facc = (unsigned long long *)(misc + 32);
     unsigned long long *d_macc = (unsigned long long *)(misc + 64);
 
+    // device-resident reference: its host copy for the breakpoint rows,
+    // overlapped with the pileup on the copy stream
+    bool ref_copy_pending = false;
+    if (!C.host_ref && P.vcf == 1) {
+        if ((size_t)ch->len > C.h_ref_cap) {
+            if (C.h_ref) (void)hipHostFree(C.h_ref);
+            C.h_ref = nullptr;
+            C.h_ref_cap = 0;
+            HIPCHK(hipHostMalloc((void **)&C.h_ref, (size_t)ch->len, 0));
+            C.h_ref_cap = (size_t)ch->len;
+        }
+        HIPCHK(hipMemcpyAsync(C.h_ref, ch->ref, (size_t)ch->len, hipMemcpyDeviceToHost, C.st_copy));
+        HIPCHK(hipEventRecord(C.ref_ev, C.st_copy));
+        ref_copy_pending = true;
+    }
     // the reference-only part of the CNV path runs beside the pileup
     if (ch->cnv && !want_dbg) {
         if (!C.cnv) C.cnv = cnv_scratch_new();
@@ -580,11 +602,18 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
 
         // per-base indel / insertion / breakpoint tests (row A10) on the device,
         // then the candidate lists, SV assembly and rows on the host (A13)
-        double ms_sv = 0;
+        double ms_sv = 0, t_sv_eval = 0, t_sv_ref = 0;
         std::string sv_text, ctx_text;
         size_t n_hits = 0;
+        std::vector<SvHit> hits;
+        // the rows' INV depth sums read caf_rd/caf_low on the copy stream, so
+        // the row thread never waits behind the CNV kernels on `st` (the CNV
+        // path only rewrites caf_mq)
+        CafSum cs{C.st_copy, (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, ch->len, GROM_OK};
+        const char *href = nullptr;
+        std::thread svt;
+        Joiner sv_join{svt};
         {
-            std::vector<SvHit> hits;
             char serr[512] = {0};
             rc = sv_evaluate(C.sv, st, P, svin, *ch, a.eval_lo, a.eval_hi, C.d_mq, C.d_hez, hits, &ms_sv, serr,
                              sizeof(serr));
@@ -593,21 +622,24 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                 return rc;
             }
             n_hits = hits.size();
+            t_sv_eval = ms_since(t_start);
             if (P.vcf == 1 && !hits.empty()) {
                 // the rows read reference bases (REF text, homopolymer runs):
-                // the caller's host copy when there is one, else one download
-                const char *href = C.host_ref;
-                std::vector<char> ref_copy;
+                // the caller's host copy when there is one, else the pinned
+                // copy made beside the pileup
+                href = C.host_ref;
                 if (!href) {
-                    ref_copy.resize((size_t)ch->len);
-                    HIPCHK(hipMemcpyAsync(ref_copy.data(), ch->ref, (size_t)ch->len, hipMemcpyDeviceToHost, st));
-                    HIPCHK(hipStreamSynchronize(st));
-                    href = ref_copy.data();
+                    HIPCHK(hipEventSynchronize(C.ref_ev));
+                    ref_copy_pending = false;
+                    href = C.h_ref;
                 }
-                CafSum cs{st, (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, ch->len, GROM_OK};
-                SvRowsInput ri{&P, ch->name, href, ch->len, &CafSum::call, &cs};
-                sv_rows(ri, hits, sv_text, ctx_text);
-                if (cs.rc != GROM_OK) return cs.rc;
+                t_sv_ref = ms_since(t_start);
+                // candidate lists, SV assembly and rows on a host thread while
+                // the CNV path runs on the GPU
+                svt = std::thread([&P, ch, href, &cs, &hits, &sv_text, &ctx_text] {
+                    SvRowsInput ri{&P, ch->name, href, ch->len, &CafSum::call, &cs};
+                    sv_rows(ri, hits, sv_text, ctx_text);
+                });
             }
         }
         const double t_sv = ms_since(t_start);
@@ -629,6 +661,11 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             cnv_text.swap(crow);
         }
         const double t_cnv = ms_since(t_start);
+        if (svt.joinable()) svt.join();
+        if (cs.rc != GROM_OK) {
+            set_err("INV depth check: device copy failed");  // raised on the row thread
+            return cs.rc;
+        }
         fmt.join();
         const double t_rows = ms_since(t_start);
         // SNV rows, the breakpoint rows (GROM.c:15163-16580), then the CNV rows (16633)
@@ -641,15 +678,17 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         if (timing)
             fprintf(stderr,
                     "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms (%u candidates), "
-                    "breakpoint tests %.3f ms (device %.3f ms, %zu hit bases), "
+                    "breakpoint tests %.3f ms (device %.3f ms, %zu hit bases; eval %.3f, ref copy %.3f, rows %.3f), "
                     "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows), SNV rows (overlapped) "
                     "joined after %.3f ms more, %u of %lld tiles to the gather kernel\n",
                     ch->name ? ch->name : "?", t_kernels, t_snv - t_kernels, ncand, t_sv - t_snv, ms_sv,
-                    n_hits, t_cnv - t_sv, ct.ms_device, (long long)ct.del_calls,
+                    n_hits, t_sv_eval - t_snv, t_sv_ref > 0 ? t_sv_ref - t_sv_eval : 0.0,
+                    t_sv - (t_sv_ref > 0 ? t_sv_ref : t_sv_eval), t_cnv - t_sv, ct.ms_device, (long long)ct.del_calls,
                     (long long)ct.dup_calls, (long long)ct.rows, t_rows - t_cnv,
                     gather_only ? (unsigned)n_tiles : n_ovf_tiles, (long long)n_tiles);
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
+        if (ref_copy_pending) HIPCHK(hipEventSynchronize(C.ref_ev));
         if (stats) {
             float ms = 0, msp = 0;
             (void)hipEventElapsedTime(&ms, C.e0, C.e1);
@@ -767,6 +806,8 @@ int grom_ctx_init(int slot, int device, const grom_params *params, const double 
     C.device = device;
     C.prm = *params;
     HIPCHK(hipStreamCreateWithFlags(&C.st, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&C.st_copy, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&C.ref_ev, hipEventDisableTiming));
     const size_t tb = sizeof(double) * (GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);
     HIPCHK(hipMalloc(&C.d_mq, tb));
     HIPCHK(hipMalloc(&C.d_hez, tb));
@@ -796,6 +837,10 @@ void grom_dev_fini(int device) {
     for (DevBuf *b : all)
         if (b->p) (void)hipFree(b->p);
     if (C.h_cands) (void)hipHostFree(C.h_cands);
+    if (C.st_copy) (void)hipStreamSynchronize(C.st_copy);
+    if (C.h_ref) (void)hipHostFree(C.h_ref);
+    if (C.ref_ev) (void)hipEventDestroy(C.ref_ev);
+    if (C.st_copy) (void)hipStreamDestroy(C.st_copy);
     cnv_scratch_free(C.cnv);
     sv_scratch_free(C.sv);
     (void)hipFree(C.d_mq);
@@ -847,6 +892,90 @@ int grom_upload(int device, const grom_chrom *chrom, const grom_reads *reads, gr
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(C->st));
     return GROM_OK;
+}
+
+struct grom_resident {
+    int device;
+    void *base;
+    int64_t bytes;
+};
+
+grom_resident *grom_resident_new(int device, const grom_chrom *ch, const grom_reads *h, grom_chrom *dch,
+                                 grom_reads *d) {
+    if (!ch || !h || !dch || !d || !ch->ref || ch->len <= 0) {
+        set_err("grom_resident_new: bad argument");
+        return nullptr;
+    }
+    const int64_t n = h->n;
+    const bool has_aux = h->n_aux > 0 && h->aux_idx && h->aux;
+    const bool has_drop = h->n_drop > 0 && h->drop_pos && h->drop_lq && h->drop_before;
+    static const uint32_t zero_off[1] = {0};
+    struct Part { const void *src; size_t bytes; size_t off; };
+    // every array 256-byte aligned; qual/seq padded past their end (16-byte reads)
+    Part parts[] = {
+        {h->pos, 4 * (size_t)n}, {h->flag, 2 * (size_t)n}, {h->mapq, (size_t)n}, {h->mtid, 4 * (size_t)n},
+        {h->mpos, 4 * (size_t)n}, {h->isize, 4 * (size_t)n}, {h->l_qseq, 4 * (size_t)n},
+        {n > 0 && h->cigar_off ? h->cigar_off : zero_off, 4 * (size_t)(n + 1)},
+        {h->cigar, 4 * (size_t)h->n_cigar_ops}, {h->base_off, 8 * (size_t)n}, {h->seq, (size_t)(h->n_bases + 1) / 2},
+        {h->qual, (size_t)h->n_bases}, {h->name_id, 4 * (size_t)n}, {ch->ref, (size_t)ch->len},
+        {has_aux ? h->aux_idx : nullptr, has_aux ? 4 * (size_t)n : 0},
+        {has_aux ? h->aux : nullptr, has_aux ? sizeof(grom_aux) * (size_t)h->n_aux : 0},
+        {has_drop ? h->drop_pos : nullptr, has_drop ? 4 * (size_t)h->n_drop : 0},
+        {has_drop ? h->drop_lq : nullptr, has_drop ? 4 * (size_t)h->n_drop : 0},
+        {has_drop ? h->drop_before : nullptr, has_drop ? 8 * (size_t)h->n_drop : 0},
+    };
+    size_t off = 0;
+    for (Part &q : parts) {
+        q.off = off;
+        off += (q.bytes + 64 + 255) & ~(size_t)255;
+    }
+    grom_resident *r = new grom_resident{device, nullptr, (int64_t)off};
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&r->base, off) != hipSuccess) {
+        set_err("grom_resident_new: hipMalloc(%zu) on device %d failed", off, device);
+        delete r;
+        return nullptr;
+    }
+    for (const Part &q : parts)
+        if (q.bytes && hipMemcpy((char *)r->base + q.off, q.src, q.bytes, hipMemcpyHostToDevice) != hipSuccess) {
+            set_err("grom_resident_new: copy to device failed");
+            (void)hipFree(r->base);
+            delete r;
+            return nullptr;
+        }
+    auto at = [&](int k) { return (const void *)((const char *)r->base + parts[k].off); };
+    *dch = *ch;
+    dch->ref = (const char *)at(13);
+    *d = *h;
+    d->pos = (const int32_t *)at(0);
+    d->flag = (const uint16_t *)at(1);
+    d->mapq = (const uint8_t *)at(2);
+    d->mtid = (const int32_t *)at(3);
+    d->mpos = (const int32_t *)at(4);
+    d->isize = (const int32_t *)at(5);
+    d->l_qseq = (const int32_t *)at(6);
+    d->cigar_off = (const uint32_t *)at(7);
+    d->cigar = (const uint32_t *)at(8);
+    d->base_off = (const int64_t *)at(9);
+    d->seq = (const uint8_t *)at(10);
+    d->qual = (const uint8_t *)at(11);
+    d->name_id = (const uint32_t *)at(12);
+    d->n_aux = has_aux ? h->n_aux : 0;
+    d->aux_idx = has_aux ? (const int32_t *)at(14) : nullptr;
+    d->aux = has_aux ? (const grom_aux *)at(15) : nullptr;
+    d->n_drop = has_drop ? h->n_drop : 0;
+    d->drop_pos = has_drop ? (const int32_t *)at(16) : nullptr;
+    d->drop_lq = has_drop ? (const int32_t *)at(17) : nullptr;
+    d->drop_before = has_drop ? (const int64_t *)at(18) : nullptr;
+    return r;
+}
+
+int64_t grom_resident_bytes(const grom_resident *r) { return r ? r->bytes : 0; }
+
+void grom_resident_free(grom_resident *r) {
+    if (!r) return;
+    (void)hipSetDevice(r->device);
+    (void)hipFree(r->base);
+    delete r;
 }
 
 int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *reads, int32_t *first_pos,

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -453,9 +454,17 @@ static bool del_dropped(const grom_params &P, const PairEnt &q, Lists &L, int sp
 
 void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string &vcf, std::string &ctx) {
     const grom_params &P = *in.P;
+    const bool timing = getenv("GROM_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    double tm[8] = {0};
+    int ti = 0;
+    auto mark = [&]() {
+        if (timing) tm[ti++] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    };
     Lists L;
     L.cap = P.sv_list_len;
     for (const SvHit &h : hits) apply_hit(P, L, h);
+    mark();
 
     const char *chr = in.chr_name ? in.chr_name : "";
     const char *fasta = in.ref;
@@ -467,6 +476,7 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
     Out o{vcf};
     std::vector<PairEnt> l2[4];
     for (int k = 0; k < 4; k++) l2[k] = merge_pairs(L.pr[k], L.n_pr[k], cap2, Mx, glseq);
+    mark();
 
     // DUP rows, GROM.c:15320-15334
     for (const PairEnt &q : l2[PR_DUP])
@@ -502,6 +512,7 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
         }
     }
 
+    mark();
     // INS: start/end merge and rows, GROM.c:15897-15968
     {
         std::vector<InsEnt> i2;
@@ -557,6 +568,7 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
         }
     }
 
+    mark();
     // INDEL_INS rows, GROM.c:16250-16330
     const double iratio = P.min_indel_ratio * (double)AF;
     for (int64_t a = 0; a < L.n_ii; a++) {
@@ -590,6 +602,7 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
             q.other_e, q.sc, hp);
     }
 
+    mark();
     // INDEL_DEL rows, dropped when a <DEL> call overlaps with a smaller
     // p-value product; the loop stops before the open last entry (the list
     // index, not a count: GROM.c:16336-16470)
@@ -632,6 +645,7 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
         }
     }
 
+    mark();
     // DEL rows, dropped when an indel deletion overlaps with a smaller or
     // equal p-value product (GROM.c:16474-16580)
     for (const PairEnt &q : l2[PR_DEL]) {
@@ -640,4 +654,13 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
             continue;
         if (!del_dropped(P, q, L, span)) pair_row(o, chr, "<DEL>", q);
     }
+    mark();
+    if (timing)
+        fprintf(stderr,
+                "sv rows ms: lists %.3f merge %.3f dup+inv %.3f ins+ctx %.3f indel_ins %.3f indel_del %.3f del %.3f "
+                "(%zu hits; list sizes ii %lld id %lld ins %lld dup %lld del %lld invf %lld invr %lld; "
+                "list2 del %zu)\n",
+                tm[0], tm[1] - tm[0], tm[2] - tm[1], tm[3] - tm[2], tm[4] - tm[3], tm[5] - tm[4], tm[6] - tm[5],
+                hits.size(), (long long)L.n_ii, (long long)L.n_id, (long long)L.n_ins, (long long)L.n_pr[0],
+                (long long)L.n_pr[1], (long long)L.n_pr[2], (long long)L.n_pr[3], l2[PR_DEL].size());
 }

@@ -79,6 +79,7 @@ void synth_default_cfg(synth_cfg *c) {
     c->cnv_max = 300000;
     c->sv_per_mb = 0.0;
     c->sv_evidence = 0.5;
+    c->ploidy = 2;
     c->seed = 2;
 }
 
@@ -128,11 +129,21 @@ typedef struct {
     long len;
 } haplo;
 
-static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo h[2]) {
+static int synth_ploidy(const synth_cfg *c) {
+    return c->ploidy >= 1 && c->ploidy <= SYNTH_MAX_PLOIDY ? c->ploidy : 2;
+}
+
+/* Donor haplotypes of chromosome ci: `ploidy` copies (synth_cfg.ploidy, 2 by
+ * default).  A diploid variant is on haplotype 0, 1 or both (gt 0/1/2); with
+ * another ploidy it is on a random non-empty subset (carrier mask), so allele
+ * fractions take every value k/ploidy.  The diploid random stream is the one
+ * the generator has always drawn. */
+static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo *h) {
     long n = c->chr_len[ci];
+    const int P = synth_ploidy(c);
     xrng r;
     xseed(&r, c->seed, (uint64_t)ci + 1, 2);
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < P; k++) {
         long cap = n + n / 50 + 1024;
         h[k].seq = (char *)malloc(cap);
         h[k].map = (int32_t *)malloc(cap * sizeof(int32_t));
@@ -145,29 +156,37 @@ static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo h[2]
         char rb = ref[i];
         char ub = (rb >= 'a' && rb <= 'z') ? (char)(rb - 32) : rb;
         if (i == next_var && ub != 'N' && i > 0 && i + c->max_indel + 2 < n) {
-            int gt = (int)xint(&r, 3); /* 0: hap0 only, 1: hap1 only, 2: both */
+            unsigned carriers;
+            if (P == 2) {
+                int gt = (int)xint(&r, 3); /* 0: hap0 only, 1: hap1 only, 2: both */
+                carriers = gt == 2 ? 3u : (1u << gt);
+            } else {
+                do { carriers = (unsigned)xint(&r, 1L << P); } while (carriers == 0);
+            }
             double u = xunif(&r) * vrate;
             int consumed = 1;
             if (u < c->snv_rate) {
                 char alt;
                 do { alt = ACGT[xint(&r, 4)]; } while (alt == ub);
-                for (int k = 0; k < 2; k++) {
-                    int has = (gt == 2) || (gt == k);
+                for (int k = 0; k < P; k++) {
+                    int has = (carriers >> k) & 1;
                     h[k].seq[h[k].len] = has ? alt : ub;
                     h[k].map[h[k].len++] = (int32_t)i;
                 }
             } else {
                 int len = 1 + (int)xint(&r, c->max_indel);
                 int ins = xunif(&r) < 0.5;
-                /* multi-allelic: both haplotypes carry an indel, of two lengths */
-                int lens[2] = {len, len};
+                /* multi-allelic: the carriers after the first carry a second length */
+                int lens[SYNTH_MAX_PLOIDY];
+                for (int k = 0; k < P; k++) lens[k] = len;
                 if (c->multi_indel > 0 && xunif(&r) < c->multi_indel) {
-                    gt = 2;
-                    lens[1] = 1 + (int)xint(&r, c->max_indel);
+                    carriers = (1u << P) - 1;
+                    int len2 = 1 + (int)xint(&r, c->max_indel);
+                    for (int k = 1; k < P; k++) lens[k] = len2;
                 }
                 if (ins) {
-                    for (int k = 0; k < 2; k++) {
-                        int has = (gt == 2) || (gt == k);
+                    for (int k = 0; k < P; k++) {
+                        int has = (carriers >> k) & 1;
                         h[k].seq[h[k].len] = ub;
                         h[k].map[h[k].len++] = (int32_t)i;
                         if (has)
@@ -178,9 +197,10 @@ static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo h[2]
                     }
                 } else {
                     /* deletion of ref[i+1 .. i+lens[k]] on the haplotypes that carry it */
-                    int span = lens[0] > lens[1] ? lens[0] : lens[1];
-                    for (int k = 0; k < 2; k++) {
-                        int has = (gt == 2) || (gt == k);
+                    int span = 0;
+                    for (int k = 0; k < P; k++) span = lens[k] > span ? lens[k] : span;
+                    for (int k = 0; k < P; k++) {
+                        int has = (carriers >> k) & 1;
                         h[k].seq[h[k].len] = ub;
                         h[k].map[h[k].len++] = (int32_t)i;
                         for (int q = has ? lens[k] + 1 : 1; q <= span; q++) {
@@ -197,13 +217,13 @@ static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo h[2]
             continue;
         }
         if (i == next_var) next_var++;
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < P; k++) {
             h[k].seq[h[k].len] = ub;
             h[k].map[h[k].len++] = (int32_t)i;
         }
         i++;
     }
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < P; k++) {
         h[k].inv = (int32_t *)malloc((size_t)(n + 1) * sizeof(int32_t));
         long ri = 0;
         for (long d = 0; d < h[k].len; d++) {
@@ -215,8 +235,8 @@ static void build_haplos(const synth_cfg *c, int ci, const char *ref, haplo h[2]
     }
 }
 
-static void free_haplos(haplo h[2]) {
-    for (int k = 0; k < 2; k++) { free(h[k].seq); free(h[k].map); free(h[k].inv); }
+static void free_haplos(haplo *h, int P) {
+    for (int k = 0; k < P; k++) { free(h[k].seq); free(h[k].map); free(h[k].inv); }
 }
 
 /* ---------------- record heap (sorted emission) ---------------- */
@@ -705,7 +725,8 @@ static long synth_sv_records(const synth_cfg *c, int ci, const char *ref, rheap 
 long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit, void *ctx) {
     long n = c->chr_len[ci];
     int L = c->read_len;
-    haplo h[2];
+    haplo h[SYNTH_MAX_PLOIDY];
+    const int ploidy = synth_ploidy(c);
     build_haplos(c, ci, ref, h);
     /* prefix count of N bases so fragments never touch an N block */
     int32_t *ncount = (int32_t *)malloc((size_t)(n + 1) * sizeof(int32_t));
@@ -739,7 +760,7 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
             continue;
         }
         start_f += (f == 1.0) ? xexp(&r, gap) : xexp(&r, gap / f);
-        int hk = (int)xint(&r, 2);
+        int hk = (int)xint(&r, ploidy);
         const haplo *hp = &h[hk];
         int ins = (int)lround(c->insert_mean + c->insert_sd * xnorm(&r));
         if (ins < L) ins = L;
@@ -804,7 +825,7 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
     free(heap.a);
     free(creg);
     free(ncount);
-    free_haplos(h);
+    free_haplos(h, ploidy);
     return emitted;
 }
 

@@ -20,6 +20,7 @@ extern "C" {
 #endif
 
 #define SYNTH_MAX_CHR 64
+#define SYNTH_MAX_PLOIDY 8
 
 typedef struct synth_cfg {
     int n_chr;
@@ -54,6 +55,9 @@ typedef struct synth_cfg {
                              clips and unmapped mates; 0 = none */
     double sv_evidence;   /* evidence depth: pairs per breakpoint as a
                              fraction of the spanning-fragment depth */
+    int ploidy;           /* donor haplotypes (2; 4 for the -p 4 configuration):
+                             variants sit on a random non-empty subset, so
+                             allele fractions are k/ploidy */
     uint64_t seed;
 } synth_cfg;
 

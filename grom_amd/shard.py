@@ -69,6 +69,38 @@ def timed_concurrent(steps_of: "list[Callable[[int], None]]", steps: int, barrie
     return dt
 
 
+def run_queue(workers: "list[Callable[[int], None]]", items: Sequence[int]) -> None:
+    """One pass over `items`: len(workers) host threads (one library context
+    each) take the next item in the given order -- longest chromosome first --
+    until none is left (greedy list scheduling).  Any exception is re-raised
+    after every thread has stopped."""
+    import threading
+    lock = threading.Lock()
+    nxt = [0]
+    errs = []
+
+    def loop(k):
+        try:
+            while True:
+                with lock:
+                    if errs or nxt[0] >= len(items):
+                        return
+                    i = items[nxt[0]]
+                    nxt[0] += 1
+                workers[k](i)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            with lock:
+                errs.append(e)
+
+    ths = [threading.Thread(target=loop, args=(k,)) for k in range(len(workers))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """Max of `value` over all ranks (identity without a process group)."""
     import torch

@@ -325,6 +325,17 @@ int64_t grom_fmt_selftest(int64_t n, uint64_t seed);
 int grom_upload(int device, const grom_chrom *chrom, const grom_reads *reads, grom_chrom *dev_chrom,
                 grom_reads *dev_reads);
 
+/* A device-resident copy of one chromosome's inputs in a single allocation
+ * the library makes on physical `device` (not owned by any context), so a
+ * caller can keep a whole genome in HBM and scan any chromosome from any slot
+ * on that device.  Fills *dev_chrom / *dev_reads with device views (valid
+ * until grom_resident_free).  NULL on failure (grom_last_error). */
+typedef struct grom_resident grom_resident;
+grom_resident *grom_resident_new(int device, const grom_chrom *chrom, const grom_reads *reads, grom_chrom *dev_chrom,
+                                 grom_reads *dev_reads);
+int64_t grom_resident_bytes(const grom_resident *r);
+void grom_resident_free(grom_resident *r);
+
 /* The drop-in command line (GROM's main, GROM.c:21865) as a library call:
  * argv as for `GROM -i BAM -r FASTA -o OUT [options]`; returns the exit code.
  * The `grom` executable is a wrapper around it. */
@@ -339,6 +350,34 @@ typedef struct grom_batch_handle grom_batch_handle;
  * *params (with grom_params_set_insert); *params must hold the other options. */
 grom_batch_handle *grom_synth_batch(int64_t chr_len, double coverage, int32_t read_len, double insert_mean,
                                     double insert_sd, uint64_t seed, grom_params *params);
+/* One chromosome of a multi-chromosome synthetic genome (the BASELINE
+ * configs[2]-[4] shapes: human-like contig lengths and names, breakpoint SVs
+ * with split reads and discordant pairs, copy-number regions, PCR duplicates,
+ * a ploidy other than 2).  Chromosome `chrom` is generated exactly as the
+ * genome's BAM would hold it (grom_synth), and turned into the batch its scan
+ * ingests with tid = chrom and the chromosome's own name.  When
+ * params->half_one_base_rd_len is already set, the insert statistics are kept
+ * (one genome-wide find_insert_mean, as the reference runs it once per BAM);
+ * otherwise they are measured on this chromosome's pairs first. */
+typedef struct grom_synth_spec {
+    int32_t n_chr;
+    int32_t chrom;             /* the chromosome to generate, 0..n_chr-1 */
+    const int64_t *chr_len;    /* n_chr lengths */
+    const char *names;         /* comma-separated names, NULL: chr1..chrN */
+    double coverage;
+    int32_t read_len;
+    int32_t ploidy;            /* donor haplotypes (0 = 2) */
+    double insert_mean, insert_sd;
+    double dup_frac;           /* fragments emitted twice (the -M filter's work) */
+    double sv_per_mb;          /* breakpoint SVs per Mb (DEL/DUP/INV/INS/CTX) */
+    double cnv_rate;           /* copy-number regions per base */
+    int64_t cnv_min, cnv_max;  /* their length range (0: 10 kb - 300 kb) */
+    const double *chr_cov;     /* per-chromosome depth (n_chr), NULL: coverage
+                                  everywhere (a male genome halves chrX/chrY) */
+    double munmap_frac;        /* pairs with an unmapped mate */
+    uint64_t seed;
+} grom_synth_spec;
+grom_batch_handle *grom_synth_chrom(const grom_synth_spec *spec, grom_params *params);
 /* views into the handle (valid until grom_batch_release) */
 int grom_batch_get(grom_batch_handle *h, grom_chrom *chrom, grom_reads *reads);
 void grom_batch_release(grom_batch_handle *h);

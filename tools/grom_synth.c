@@ -5,7 +5,7 @@
  *   grom_synth -o prefix [-L len[,len...]] [-c cov] [-l readlen] [-m mean] [-d sd]
  *              [-s seed] [-e err] [-Q lowmapq_frac] [-C clip_frac] [-U munmap_frac]
  *              [-D dup_frac] [-S snv_rate] [-I indel_rate] [-T telomere_n] [-n names]
- *              [-X sv_per_mb] [-E sv_evidence]
+ *              [-X sv_per_mb] [-E sv_evidence] [-P ploidy]
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,7 +20,7 @@ int main(int argc, char **argv) {
     const char *prefix = NULL;
     const char *names = NULL;
     int opt;
-    while ((opt = getopt(argc, argv, "o:L:c:l:m:d:s:e:Q:C:U:D:S:I:T:n:q:M:V:W:J:X:E:")) != -1) {
+    while ((opt = getopt(argc, argv, "o:L:c:l:m:d:s:e:Q:C:U:D:S:I:T:n:q:M:V:W:J:X:E:P:")) != -1) {
         switch (opt) {
         case 'o': prefix = optarg; break;
         case 'L': {
@@ -55,6 +55,7 @@ int main(int argc, char **argv) {
         case 'n': names = optarg; break;
         case 'q': c.lowq_frac = atof(optarg); break;
         case 'M': c.lower_frac = atof(optarg); break;
+        case 'P': c.ploidy = atoi(optarg); break;                   /* donor haplotypes (allele fractions k/P) */
         case 'J': c.multi_indel = atof(optarg); break;              /* multi-allelic indel fraction */
         case 'X': c.sv_per_mb = atof(optarg); break;                /* breakpoint SVs per Mb */
         case 'E': c.sv_evidence = atof(optarg); break;              /* SV evidence depth factor */
