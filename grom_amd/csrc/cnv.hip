@@ -669,6 +669,7 @@ struct WalkIn {
     const uint16_t *wb;
     const double *sd, *wsd;
     int64_t len, start, end, L, min_len;
+    unsigned long long *stats;  // GROM_TIMING: walk counters (ab/cd wave calls and rounds), else null
 };
 
 __device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) {
@@ -677,6 +678,25 @@ __device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) {
     __builtin_memcpy(&d, &u, 8);
     return d;
 }
+
+// RN(tot / d) >= MIN_RD_LOW_STDEV for d > 0, as the reference's division and
+// compare decide it, without the division on the common path.  RN(x) >= 3
+// iff x >= 3 - 2^-52 (the midpoint below 3 rounds to 3, whose significand is
+// even), i.e. iff tot - 3d >= -2^-52 d.  e = fma(-3, d, tot) is that
+// difference rounded once, and rounding is monotonic, so e != t decides it;
+// e == t is settled by the division itself.
+static_assert(MIN_RD_LOW_STDEV == 3, "ratio_ge_min assumes the threshold 3");
+__device__ __forceinline__ bool ratio_ge_min(double tot, double d) {
+    const double t = -0x1p-52 * d;
+    const double e = __builtin_fma(-3.0, d, tot);
+    if (e != t) return e > t;
+    return tot / d >= (double)MIN_RD_LOW_STDEV;
+}
+// The low-base fraction tests compare a sub-count over its window (a ratio
+// in [0, 1]) with MAX_LOW_ACGT = 2: they never decide anything, so they are
+// kept only as this compile-time constant.
+static_assert(MAX_LOW_ACGT >= 1.0, "the low-fraction tests are dropped only while MAX_LOW_ACGT >= 1");
+constexpr bool LOW_FRAC_OK = true;
 
 // The walk is one serial computation.  A wave runs it with every lane
 // executing the same uniform statements; per-position inputs come from a
@@ -750,7 +770,8 @@ struct PreAB {
 // a base that passes the threshold (GROM.c:19370-19470 DEL, 19685-19785 DUP);
 // Acc provides bits(p) and z(p)
 template <int KIND, class Acc>
-__device__ PreAB phase_ab(Acc &c, const WalkIn &W, int64_t pos, int mqi) {
+__device__ PreAB phase_ab(Acc &c, const WalkIn &W, int64_t pos, int mqi, int64_t max_steps = INT64_MAX,
+                          bool *capped = nullptr) {
     const int64_t L = W.L, ML = W.min_len, end = W.end;
     const double *wsd = W.wsd;
     int begin = 0, stop = 0;
@@ -775,8 +796,7 @@ __device__ PreAB phase_ab(Acc &c, const WalkIn &W, int64_t pos, int mqi) {
             if (KIND == 0) tot += c.z(a); else tot -= c.z(a);
         }
     }
-    if (stop == 0 && cnt > 0 && wsd[ML] > 0 && (tot / (cnt * wsd[ML])) >= MIN_RD_LOW_STDEV &&
-        ((ML - cnt) / ((double)ML)) <= MAX_LOW_ACGT) {
+    if (stop == 0 && cnt > 0 && wsd[ML] > 0 && ratio_ge_min(tot, cnt * wsd[ML]) && LOW_FRAC_OK) {
         begin = 1;
         last_good = pos + ML;
         ce = pos + ML;
@@ -784,6 +804,7 @@ __device__ PreAB phase_ab(Acc &c, const WalkIn &W, int64_t pos, int mqi) {
     }
     if (stop == 0) {
         for (pa = pos + ML; pa < pos + L; pa++) {
+            if (capped && pa - pos >= max_steps) { *capped = true; break; }  // the walk decides this base
             wl += 1;
             if (pa < end) {
                 const uint32_t b = c.bits(pa);
@@ -793,8 +814,7 @@ __device__ PreAB phase_ab(Acc &c, const WalkIn &W, int64_t pos, int mqi) {
                     cnt += 1;
                     if (b & (pb0 << mqi)) {
                         cnt2 += 1;
-                        if (wsd[wl] > 0 && (tot / (cnt * wsd[wl])) >= MIN_RD_LOW_STDEV &&
-                            ((wl - cnt) / ((double)wl)) <= MAX_LOW_ACGT) {
+                        if (wsd[wl] > 0 && ratio_ge_min(tot, cnt * wsd[wl]) && LOW_FRAC_OK) {
                             last_good = pa;
                             if (begin == 0) {
                                 begin = 1;
@@ -869,8 +889,7 @@ __device__ bool phase_cd(Acc &a, Acc &t, const WalkIn &W, int64_t pos, const Pre
                     cnt += 1;
                 }
             }
-            if (cnt > 0 && wsd[L] > 0 && (tot / (cnt * wsd[L])) >= MIN_RD_LOW_STDEV &&
-                ((L - cnt) / ((double)L)) <= MAX_LOW_ACGT) {
+            if (cnt > 0 && wsd[L] > 0 && ratio_ge_min(tot, cnt * wsd[L]) && LOW_FRAC_OK) {
                 last_good = pa;
                 ce = pa;
                 double ts = tot / (cnt * wsd[L]);
@@ -899,8 +918,7 @@ __device__ bool phase_cd(Acc &a, Acc &t, const WalkIn &W, int64_t pos, const Pre
                     c3 += 1;
                     if (ba & (pb0 << mqa)) c2 += 1;
                 }
-                if (c3 == 0 || (c3 > 0 && (c2 / ((double)c3)) < 0.5) ||
-                    ((ce - pa + 1 - c3) / ((double)ce - (double)pa + 1.0)) > MAX_LOW_ACGT) {
+                if (c3 == 0 || (c3 > 0 && 2 * c2 < c3) || !LOW_FRAC_OK) {  // c2/(double)c3 < 0.5 exactly, for counts < 2^26
                     ce = pa - 1;
                     stop_while = 1;
                 }
@@ -912,6 +930,321 @@ __device__ bool phase_cd(Acc &a, Acc &t, const WalkIn &W, int64_t pos, const Pre
     ce_out = ce;
     stdevs_out = stdevs;
     return true;
+}
+
+// ---- wave-cooperative window search (the walk's long calls) ----
+//
+// A call inside a long copy-number region slides its window across the whole
+// region (phase C) and trims it back (phase D), and phase B extends every
+// candidate up to L bases: serial loops that one lane runs at ~0.5 us per
+// step.  The versions below keep the serial parts serial -- the running
+// double sum `tot` is added in the reference's order, one IEEE operation per
+// step -- and spread everything else over the 64 lanes, 64 steps at a time:
+// coalesced loads, the class state as a last-value scan, integer counts as
+// prefix sums, each step's window test on its own lane, the first stopping
+// step by ballot.  The results are those of phase_ab / phase_cd exactly.
+
+__device__ __forceinline__ int cdef(uint32_t b) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : -1; }
+
+__device__ __forceinline__ int wave_incl_sum(int v) {
+    const int lane = threadIdx.x & 63;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ double rl_d(double v, int k) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    return dbl_of((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k),
+                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k));
+}
+
+__device__ __forceinline__ int64_t rl_i64(int64_t v, int k) {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, k)) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), k) << 32));
+}
+
+__device__ __forceinline__ double wave_max_d(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// `tot` advanced over the lanes in order: at lane k, tot + a then (two-op
+// form) + b, where a lane without an operation contributes 0.0.  Adding 0.0
+// is exact here: tot starts at +0.0 and a sum of doubles is -0.0 only when
+// both terms are, so tot is never -0.0 and x + (+-0.0) == x.  Every lane
+// computes the same chain (the addends are broadcast from LDS, so the reads
+// run ahead of the dependent adds) and keeps the value after its own step.
+// The callers run in one-wave blocks (the walk kernels), so the block
+// barrier is the wave's.
+__device__ __forceinline__ double wave_chain1(double &tot, double a) {
+    __shared__ double buf[64];
+    const int lane = threadIdx.x & 63;
+    buf[lane] = a;
+    __syncthreads();
+    double t = tot, mine = t;
+#pragma unroll 16
+    for (int k = 0; k < 64; k++) {
+        t = t + buf[k];
+        mine = lane == k ? t : mine;
+    }
+    __syncthreads();
+    tot = t;
+    return mine;
+}
+
+__device__ __forceinline__ double wave_chain2(double &tot, double a, double b) {
+    __shared__ double buf2[2][64];
+    const int lane = threadIdx.x & 63;
+    buf2[0][lane] = a;
+    buf2[1][lane] = b;
+    __syncthreads();
+    double t = tot, mine = t;
+#pragma unroll 16
+    for (int k = 0; k < 64; k++) {
+        t = t + buf2[0][k];
+        t = t + buf2[1][k];
+        mine = lane == k ? t : mine;
+    }
+    __syncthreads();
+    tot = t;
+    return mine;
+}
+
+// phases A and B (phase_ab) for the wave; every lane returns the same record
+template <int KIND>
+__device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
+    const int lane = threadIdx.x & 63;
+    const int64_t L = W.L, ML = W.min_len, end = W.end;
+    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    const double sgn = KIND == 0 ? 1.0 : -1.0;  // tot -= z is tot + (-z), exactly
+    int begin = 0, stop = 0;
+    int64_t ce = 0, last_good = 0, temp_pos = pos, wl = 0, cnt = 0, cnt2 = 0;
+    double stdevs = 0.0, tot = 0.0;
+    // phase A: the first ML bases (GROM.c:19370-19400)
+    for (int64_t p0 = pos; p0 < pos + ML && !stop; p0 += 64) {
+        const int64_t p = p0 + lane;
+        const bool in = p < pos + ML;
+        const uint32_t b = in ? W.wb[p] : 0u;
+        const bool nl = in && !(b & B_LOW);
+        const int m = wave_last_incl(nl ? cdef(b) : -1, mqi);
+        const bool ps = nl && (b & (pb0 << m));
+        const int64_t c2 = cnt2 + wave_incl_sum(ps ? 1 : 0);
+        const int64_t w = wl + lane + 1;
+        const bool st = in && !ps && (2 * c2) < w;
+        const unsigned long long sm = __ballot(st);
+        const int n_in = (int)min<int64_t>(64, pos + ML - p0);
+        const int last = sm ? __ffsll((long long)sm) - 1 : n_in - 1;
+        mqi = __builtin_amdgcn_readlane(m, last);
+        cnt2 = rl_i64(c2, last);
+        wl += last + 1;
+        if (sm) {
+            stop = 1;
+            temp_pos = p0 + last;
+        }
+    }
+    if (stop == 0) {
+        cnt = ML;
+        for (int64_t p0 = pos; p0 < pos + ML; p0 += 64) {
+            const int64_t p = p0 + lane;
+            const bool in = p < pos + ML;
+            const uint32_t b = in ? W.wb[p] : 0u;
+            cnt -= __popcll(__ballot(in && (b & B_LOW)));
+            const double v = in ? sgn * W.sd[p] : 0.0;
+            wave_chain1(tot, v);
+        }
+    }
+    if (stop == 0 && cnt > 0 && W.wsd[ML] > 0 && ratio_ge_min(tot, cnt * W.wsd[ML]) && LOW_FRAC_OK) {
+        begin = 1;
+        last_good = pos + ML;
+        ce = pos + ML;
+        stdevs = tot / (cnt * W.wsd[ML]);
+    }
+    // phase B: extension to L (GROM.c:19405-19470)
+    for (int64_t p0 = pos + ML; p0 < pos + L && !stop; p0 += 64) {
+        const int64_t p = p0 + lane;
+        const bool in = p < pos + L;
+        const bool inend = in && p < end;
+        const uint32_t b = inend ? W.wb[p] : 0u;
+        const bool nl = inend && !(b & B_LOW);
+        const int m = wave_last_incl(nl ? cdef(b) : -1, mqi);
+        const bool ps = nl && (b & (pb0 << m));
+        const int64_t c = cnt + wave_incl_sum(nl ? 1 : 0);
+        const int64_t c2 = cnt2 + wave_incl_sum(ps ? 1 : 0);
+        const int64_t w = wl + lane + 1;
+        const double v = nl ? sgn * W.sd[p] : 0.0;
+        const double tj = wave_chain1(tot, v);
+        const double wsdw = in ? W.wsd[w] : 0.0;
+        const bool good = ps && wsdw > 0 && ratio_ge_min(tj, c * wsdw) && LOW_FRAC_OK;
+        const double ts = good ? tj / (c * wsdw) : 0.0;
+        const bool st = in && (!inend || (!ps && (2 * c2) < w));
+        const unsigned long long sm = __ballot(st);
+        const int n_in = (int)min<int64_t>(64, pos + L - p0);
+        const int js = sm ? __ffsll((long long)sm) - 1 : n_in;  // steps before the stopping one
+        const bool eg = good && lane < js;
+        const unsigned long long gm = __ballot(eg);
+        if (gm) {
+            const int jl = 63 - __clzll(gm);
+            last_good = ce = p0 + jl;
+            const double mx = wave_max_d(eg ? ts : 0.0);
+            if (begin == 0) { begin = 1; stdevs = mx; }
+            else if (mx > stdevs) stdevs = mx;
+        }
+        const int last = sm ? js : n_in - 1;  // the stopping step still updates the state
+        mqi = __builtin_amdgcn_readlane(m, last);
+        cnt = rl_i64(c, last);
+        cnt2 = rl_i64(c2, last);
+        tot = rl_d(tj, last);
+        wl += last + 1;
+        if (sm) stop = 1;
+    }
+    PreAB r;
+    r.temp_pos = temp_pos;
+    r.ce = ce;
+    r.last_good = last_good;
+    r.stdevs = stdevs;
+    r.stop = stop;
+    r.begin = begin;
+    r.mqi = mqi;
+    r.done = 0;
+    r.ce_final = 0;
+    r.stdevs_final = 0.0;
+    return r;
+}
+
+// phases C and D (phase_cd) for the wave
+template <int KIND>
+__device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int64_t &ce_out, double &stdevs_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t L = W.L, ML = W.min_len, cs = pos;
+    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    const double sgn = KIND == 0 ? 1.0 : -1.0;
+    const double wsdL = W.wsd[L];
+    int64_t ce = r.ce, last_good = r.last_good, cnt = 0;
+    double stdevs = r.stdevs, tot = 0.0;
+    int mqi = r.mqi;
+    if (r.stop == 0) {
+        int64_t pa = pos + L;
+        int mqb = mqi;
+        if (pa < W.len && (pa - last_good) <= MAX_DIST_LAST_GOOD) {
+            // the first window [pos+1, pos+L] (GROM.c:19480-19490)
+            for (int64_t p0 = pos + 1; p0 <= pos + L; p0 += 64) {
+                const int64_t p = p0 + lane;
+                const bool in = p <= pos + L;
+                const uint32_t b = in ? W.wb[p] : 0u;
+                const int m = wave_last_incl(in ? cdef(b) : -1, mqb);
+                const bool q = in && !(b & B_LOW) && (b & (B_W0 << m));
+                const double v = q ? sgn * W.sd[p] : 0.0;
+                const unsigned long long qm = __ballot(q);
+                cnt += __popcll(qm);
+                wave_chain1(tot, v);
+                mqb = __builtin_amdgcn_readlane(m, (int)min<int64_t>(63, pos + L - p0));
+            }
+            if (cnt > 0 && wsdL > 0 && ratio_ge_min(tot, cnt * wsdL) && LOW_FRAC_OK) {
+                last_good = pa;
+                ce = pa;
+                const double ts = tot / (cnt * wsdL);
+                if (ts > stdevs) stdevs = ts;
+            }
+            pa += 1;
+            // the slide (GROM.c:19492-19545), 64 steps per round
+            for (;;) {
+                const int64_t p = pa + lane;
+                const bool inl = p < W.len;
+                const uint32_t ba = inl ? W.wb[p] : 0u, bb = inl ? W.wb[p - L] : 0u;
+                const int mt = wave_last_incl(inl ? cdef(bb) : -1, mqb);
+                const int ml = wave_last_incl(inl ? cdef(ba) : -1, mqi);
+                const bool qt = inl && !(bb & B_LOW) && (bb & (B_W0 << mt));
+                const bool ql = inl && !(ba & B_LOW) && (ba & (B_W0 << ml));
+                const double vt = qt ? -sgn * W.sd[p - L] : 0.0;
+                const double vl = ql ? sgn * W.sd[p] : 0.0;
+                const int64_t cj = cnt + wave_incl_sum((ql ? 1 : 0) - (qt ? 1 : 0));
+                double t = tot;
+                const double tj = wave_chain2(t, vt, vl);
+                const bool good = inl && cj > 0 && wsdL > 0 && ratio_ge_min(tj, cj * wsdL) && LOW_FRAC_OK;
+                const double ts = good ? tj / (cj * wsdL) : 0.0;
+                // the loop test of step j sees the last good step before it
+                int gi = wave_last_incl(good ? lane : -1, -1);
+                int ge = __shfl_up(gi, 1);
+                if (lane == 0) ge = -1;
+                const int64_t lgb = ge >= 0 ? pa + ge : last_good;
+                const bool cont = inl && (p - lgb) <= MAX_DIST_LAST_GOOD;
+                const unsigned long long sm = __ballot(!cont);
+                const int js = sm ? __ffsll((long long)sm) - 1 : 64;
+                const bool eg = good && lane < js;
+                const unsigned long long gm = __ballot(eg);
+                if (gm) {
+                    last_good = ce = pa + (63 - __clzll(gm));
+                    const double mx = wave_max_d(eg ? ts : 0.0);
+                    if (mx > stdevs) stdevs = mx;
+                }
+                if (js > 0) {
+                    tot = rl_d(tj, js - 1);
+                    cnt = rl_i64(cj, js - 1);
+                    mqi = __builtin_amdgcn_readlane(ml, js - 1);
+                    mqb = __builtin_amdgcn_readlane(mt, js - 1);
+                }
+                pa += js;
+                if (W.stats && lane == 0) atomicAdd(W.stats + 2, 1ull);
+                if (js < 64) break;
+            }
+        }
+    }
+    // phase D: trim the end back (GROM.c:19550-19600)
+    int64_t p = ce;
+    while (p > cs + ML) {
+        const int64_t q = p - lane;
+        const bool in = q > cs + ML;
+        const uint32_t b = in ? W.wb[q] : 0u;
+        const int m = wave_last_incl(in ? cdef(b) : -1, mqi);
+        const unsigned long long pm = __ballot(in && (b & (pb0 << m)));
+        if (!pm) {
+            const int n_in = __popcll(__ballot(in));
+            mqi = __builtin_amdgcn_readlane(m, n_in - 1);
+            p -= n_in;
+            ce = p;
+            continue;
+        }
+        const int j = __ffsll((long long)pm) - 1;
+        mqi = __builtin_amdgcn_readlane(m, j);
+        if (j > 0) {
+            p -= j;
+            ce = p;
+        }
+        int64_t c2 = 0, c3 = 0, pa = ce;
+        int mqa = mqi;
+        bool stopped = false;
+        while (pa > cs + ML && !stopped) {
+            const int64_t x = pa - lane;
+            const bool in2 = x > cs + ML;
+            const uint32_t bx = in2 ? W.wb[x] : 0u;
+            const bool nl = in2 && !(bx & B_LOW);
+            const int mx = wave_last_incl(nl ? cdef(bx) : -1, mqa);
+            const bool px = nl && (bx & (pb0 << mx));
+            const int64_t c3j = c3 + wave_incl_sum(nl ? 1 : 0), c2j = c2 + wave_incl_sum(px ? 1 : 0);
+            const bool st = in2 && (c3j == 0 || (c3j > 0 && 2 * c2j < c3j) || !LOW_FRAC_OK);
+            const unsigned long long sm = __ballot(st);
+            if (sm) {
+                const int k = __ffsll((long long)sm) - 1;
+                ce = pa - k - 1;
+                pa = ce;
+                stopped = true;
+            } else {
+                const int n_in = __popcll(__ballot(in2));
+                c3 = rl_i64(c3j, n_in - 1);
+                c2 = rl_i64(c2j, n_in - 1);
+                mqa = __builtin_amdgcn_readlane(mx, n_in - 1);
+                pa -= n_in;
+            }
+        }
+        p = pa;
+        if (W.stats && lane == 0) atomicAdd(W.stats + 3, 1ull);
+    }
+    ce_out = ce;
+    stdevs_out = stdevs;
 }
 
 struct GAcc {  // direct loads (one lane per base)
@@ -965,17 +1298,25 @@ __global__ __launch_bounds__(256) void k_cnv_cand(WalkIn W, int32_t *__restrict_
 // a candidate's first two phases: nxt[m][p] = the position the walk continues
 // from (before its +1), or -(k+2) for a call whose record pre[k] the walk
 // completes (phases C, D)
+// nxt value of a candidate whose phase B ran past the precompute budget: the
+// walk computes it (phase_ab_wave) if it gets there
+constexpr int32_t NXT_UNDECIDED = INT32_MIN;
+
 template <int KIND>
 __global__ void k_cnv_pre(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand, int32_t *__restrict__ nxt,
-                          PreAB *__restrict__ pre, uint32_t *n_pre, uint32_t cap, int64_t *__restrict__ pre_pos) {
+                          PreAB *__restrict__ pre, uint32_t *n_pre, uint32_t cap, int64_t *__restrict__ pre_pos,
+                          int64_t max_steps) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_cand) return;
     const int64_t p = cand[i] >> 1;
     const int m = (int)(cand[i] & 1);
     GAcc c{W.wb, W.sd};
-    PreAB r = phase_ab<KIND>(c, W, p, m);
+    bool capped = false;
+    PreAB r = phase_ab<KIND>(c, W, p, m, max_steps, &capped);
     int32_t out = (int32_t)p;
-    if (r.begin == 1) {
+    if (capped) {
+        out = NXT_UNDECIDED;
+    } else if (r.begin == 1) {
         uint32_t k = atomicAdd(n_pre, 1u);
         if (k < cap) {
             r.done = 0;
@@ -1045,17 +1386,25 @@ struct Walk {
     // extension past L, phase D: trimming the end).  Returns the position the
     // walk continues from (before its `pos += 1`).
     __device__ int64_t block(int64_t pos, int mqi, int32_t n, CallRec &call, bool &is_call) {
-        (void)mqi;
-        is_call = n < -1;
-        if (!is_call) return n;
-        const PreAB r = pre[-n - 2];
+        PreAB r;
+        if (n == NXT_UNDECIDED) {  // phases A/B were not precomputed (long region): the wave runs them
+            if (W.stats && (threadIdx.x & 63) == 0) atomicAdd(W.stats + 0, 1ull);
+            r = phase_ab_wave<KIND>(W, pos, mqi);
+            is_call = r.begin == 1;
+            if (!is_call) return r.stop == 1 ? r.temp_pos : pos;
+        } else {
+            is_call = n < -1;
+            if (!is_call) return n;
+            r = pre[-n - 2];
+        }
         int64_t ce;
         double sdv;
-        if (r.done) {
+        if (r.done == 1) {
             ce = r.ce_final;
             sdv = r.stdevs_final;
         } else {
-            phase_cd<KIND>(c, t, W, pos, r, INT64_MAX, ce, sdv);
+            if (W.stats && (threadIdx.x & 63) == 0) atomicAdd(W.stats + 1, 1ull);
+            phase_cd_wave<KIND>(W, pos, r, ce, sdv);
         }
         call.p = pos;
         call.ce = ce;
@@ -1123,6 +1472,7 @@ __device__ int64_t walk_run(Walk<KIND> &w, int64_t pos, int &last, int64_t lim, 
             return pos;
         }
         const int32_t n = __builtin_amdgcn_readlane(last == 0 ? w.c.r.n0 : w.c.r.n1, j);
+        if (w.W.stats && lane == 0) atomicAdd(w.W.stats + 4, 1ull);
         CallRec c;
         bool is_call = false;
         pos = w.block(pos, last, n, c, is_call);
@@ -2024,7 +2374,8 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         hipLaunchKernelGGL(k_cnv_wbits, dim3((unsigned)std::min<int64_t>((len + 255) / 256, 65536)), dim3(256), 0, st,
                            A, gcw, d_mq, d_rd, d_low, flag, dT, (uint16_t *)S->wbits.p);
         CK(hipGetLastError());
-        WalkIn WI{(const uint16_t *)S->wbits.p, sd, (const double *)S->wsd.p, len, m - 1, (len - W) - ML, L, ML};
+        WalkIn WI{(const uint16_t *)S->wbits.p, sd, (const double *)S->wsd.p, len, m - 1, (len - W) - ML, L, ML,
+                  nullptr};
         const int64_t span = std::max<int64_t>(0, WI.end - WI.start);
         const int64_t n_ch = (span + WALK_CHUNK - 1) / WALK_CHUNK;
         uint32_t call_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, len / 1000), 1 << 24);
@@ -2038,9 +2389,12 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             KindBufs &K = S->kb[kind];
             hipStream_t st = K.st;
             int rc = GROM_OK;
-            if ((rc = grow(K.cnt, 16, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
+            if ((rc = grow(K.cnt, 64, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
             uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;  // n_calls, n_pre, n_cand, capped
+            WalkIn WK = WI;
+            WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 16) : nullptr;
             CK(hipStreamWaitEvent(st, S->walk_in, 0));
+            if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 48, st));
             bool done = false;
             for (int attempt = 0; attempt < 8 && !done; attempt++) {
                 if ((rc = grow(K.nxt, 8 * (size_t)len, err, errlen)) ||
@@ -2063,9 +2417,9 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 CK(hipMemsetAsync(n_cand, 0, 8, st));  // candidates, capped call starts
                 int64_t *cand = (int64_t *)K.prepos.p;
                 if (kind == 0)
-                    hipLaunchKernelGGL(k_cnv_cand<0>, dim3(gpre), dim3(256), 0, st, WI, nxt, cand, n_cand, cand_cap);
+                    hipLaunchKernelGGL(k_cnv_cand<0>, dim3(gpre), dim3(256), 0, st, WK, nxt, cand, n_cand, cand_cap);
                 else
-                    hipLaunchKernelGGL(k_cnv_cand<1>, dim3(gpre), dim3(256), 0, st, WI, nxt, cand, n_cand, cand_cap);
+                    hipLaunchKernelGGL(k_cnv_cand<1>, dim3(gpre), dim3(256), 0, st, WK, nxt, cand, n_cand, cand_cap);
                 CK(hipGetLastError());
                 uint32_t ncand = 0;
                 CK(hipMemcpyAsync(&ncand, n_cand, 4, hipMemcpyDeviceToHost, st));
@@ -2075,28 +2429,50 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     found[kind].clear();
                     continue;
                 }
+                if (ncand > pre_cap) {  // every candidate may start a call (a long region): no re-run
+                    pre_cap = ncand;
+                    if ((rc = grow(K.pre, sizeof(PreAB) * pre_cap, err, errlen)) ||
+                        (rc = grow(K.ppos, 8 * (size_t)pre_cap, err, errlen)))
+                        return rc;
+                    pre = (PreAB *)K.pre.p;
+                }
                 if (ncand) {
+                    // one lane per candidate is the fast way through the noise, whose
+                    // searches stop early; inside a long copy-number region every base
+                    // is a candidate that extends to L, and the walk visits only the
+                    // first: past a budget of lane steps, the walk decides (the wave
+                    // routines, phase_ab_wave / phase_cd_wave)
+                    // GROM_CNV_BUDGET (tests) shrinks the budget so the wave routines take every long search
+                    const char *bud = getenv("GROM_CNV_BUDGET");
+                    const int64_t budget = bud ? std::max<int64_t>(atoll(bud), 1) : (int64_t)1 << 27;
+                    // phases A/B: every candidate the walk can meet inside a region
+                    // is a visited no-op there (the reference runs each to L), so by
+                    // default all of them are precomputed, one lane each
+                    const int64_t ab_cap = bud ? std::max<int64_t>(std::min<int64_t>(L, budget / ncand), ML + 256) : L;
                     if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_pre<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p);
+                        hipLaunchKernelGGL(k_cnv_pre<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p, ab_cap);
                     else
-                        hipLaunchKernelGGL(k_cnv_pre<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WI, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p);
+                        hipLaunchKernelGGL(k_cnv_pre<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p, ab_cap);
                     CK(hipGetLastError());
-                    // phases C/D for every call start, capped (the walk finishes the rest)
-                    const int64_t cd_cap = 4 * L + 4 * MAX_DIST_LAST_GOOD;
+                    // phases C/D for every call start, within the same kind of budget
+                    // (the walk finishes the rest)
+                    const int64_t cd_cap = std::max<int64_t>(
+                        std::min<int64_t>(4 * L + 4 * MAX_DIST_LAST_GOOD, budget / std::max<uint32_t>(ncand / 4, 1)),
+                        (int64_t)1024);
                     const unsigned gpost = (unsigned)((std::min<int64_t>(ncand, pre_cap) + 255) / 256);
                     if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_post<0>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
+                        hipLaunchKernelGGL(k_cnv_post<0>, dim3(gpost), dim3(256), 0, st, WK, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
                     else
-                        hipLaunchKernelGGL(k_cnv_post<1>, dim3(gpost), dim3(256), 0, st, WI, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
+                        hipLaunchKernelGGL(k_cnv_post<1>, dim3(gpost), dim3(256), 0, st, WK, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
                     CK(hipGetLastError());
                 }
                 const unsigned gch = (unsigned)n_ch;  // one wave per chunk
                 if (kind == 0) {
-                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
                 } else {
-                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WI, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
                 }
                 CK(hipGetLastError());
                 std::vector<ChunkState> hcs(n_ch);
@@ -2108,7 +2484,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 int64_t n_fix = 0;
                 for (int64_t k = 1; k < n_ch; k++) {
                     const bool entry_ok = tx == hcs[k - 1].x1 && tl_ == hcs[k - 1].l1;
-                    const int64_t c0 = WI.start + k * WALK_CHUNK, c1 = std::min<int64_t>(WI.end, c0 + WALK_CHUNK);
+                    const int64_t c0 = WK.start + k * WALK_CHUNK, c1 = std::min<int64_t>(WK.end, c0 + WALK_CHUNK);
                     // the exit of the walk whose marks this chunk holds after its mode-1 pass
                     const int64_t ex = hcs[k].status == ST_NOMERGE ? hcs[k].x2 : hcs[k].x1;
                     const int el = hcs[k].status == ST_NOMERGE ? hcs[k].l2 : hcs[k].l1;
@@ -2118,9 +2494,9 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         continue;
                     }
                     if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_walk_fix<0>, dim3(1), dim3(64), 0, st, WI, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
+                        hipLaunchKernelGGL(k_cnv_walk_fix<0>, dim3(1), dim3(64), 0, st, WK, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
                     else
-                        hipLaunchKernelGGL(k_cnv_walk_fix<1>, dim3(1), dim3(64), 0, st, WI, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
+                        hipLaunchKernelGGL(k_cnv_walk_fix<1>, dim3(1), dim3(64), 0, st, WK, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
                     CK(hipGetLastError());
                     ChunkState one;
                     CK(hipMemcpyAsync(&one, dcs + k, sizeof(ChunkState), hipMemcpyDeviceToHost, st));
@@ -2132,8 +2508,12 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 if (tmg) {
                     uint32_t np_[3] = {0, 0, 0};
                     (void)hipMemcpy(np_, n_pre, 12, hipMemcpyDeviceToHost);
-                    fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired, %u candidates, %u call starts (%u left to the walk)\n",
-                            kind == 0 ? "DEL" : "DUP", (long long)n_ch, (long long)n_fix, ncand, np_[0], np_[2]);
+                    unsigned long long ws[5] = {0, 0, 0, 0, 0};
+                    (void)hipMemcpy(ws, WK.stats, sizeof(ws), hipMemcpyDeviceToHost);
+                    fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired, %u candidates, %u call starts (%u left to the walk); "
+                            "walk stops %llu, wave A/B %llu, wave C/D %llu (%llu slide rounds, %llu trim rounds)\n",
+                            kind == 0 ? "DEL" : "DUP", (long long)n_ch, (long long)n_fix, ncand, np_[0], np_[2], ws[4],
+                            ws[0], ws[1], ws[2], ws[3]);
                 }
                 uint32_t nc = 0;
                 CK(hipMemcpyAsync(&nc, n_calls, 4, hipMemcpyDeviceToHost, st));

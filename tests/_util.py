@@ -29,6 +29,9 @@ CASES = {
     # copy-number regions (0x, 0.5x, 1.5x, 2x depth) for the read-depth CNV path
     "cnv": ["-L", "1500000", "-s", "16", "-V", "0.000004", "-W", "20000,150000", "-Q", "0.05"],
     "cnv_multi": ["-L", "700000,900000", "-s", "17", "-V", "0.000005", "-W", "15000,80000", "-Q", "0.08"],
+    # long copy-number regions (0.3-1 Mb, as in BASELINE configs[2]): calls whose
+    # window search spans the region (the walk's wave-cooperative phases)
+    "cnv_long": ["-L", "4000000", "-s", "18", "-V", "0.0000008", "-W", "300000,1000000", "-Q", "0.05", "-D", "0.05"],
     # breakpoint evidence: deletions, duplications, inversions, insertions and
     # translocations with split reads (SA tags), a 300 kb partner chromosome
     "sv": ["-L", "600000,300000", "-s", "31", "-X", "30", "-I", "0.0003", "-J", "0.3", "-Q", "0.05"],

@@ -45,6 +45,8 @@ CNV_RUNS = [
     ("cnv", ["-V", "1", "-A", "3", "-X", "4000", "-W", "60", "-L", "3", "-F", "0.3"]),
     ("cnv_multi", ["-V", "1", "-p", "3"]),
     ("cnv_multi", ["-V", "1", "-M", "-U", "1", "-Y", "2", "-Z", "20000"]),
+    ("cnv_long", ["-V", "1", "-M"]),
+    ("cnv_long", []),
 ]
 
 
@@ -115,15 +117,38 @@ def test_pileup_kernel_paths_bit_exact(datadir, case, extra, env):
     _check_counters(datadir, case, extra, tag, env_extra=env)
 
 
-@pytest.mark.parametrize("case,extra", CNV_RUNS, ids=[f"{c}{''.join(e)}" for c, e in CNV_RUNS])
-def test_cnv_rows_bit_exact(datadir, case, extra):
+def _oracle_once(datadir, case, extra):
+    """The oracle's VCF for (case, flags), run once per session (the long-region
+    cases take the oracle about a minute)."""
     bam, fa = synth(datadir, case, CASES[case])
     tag = f"{case}{''.join(extra).replace('-', '_').replace('.', 'p')}"
-    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    if not os.path.exists(datadir / f"o_{tag}.vcf"):
+        run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    return bam, fa, tag
+
+
+@pytest.mark.parametrize("case,extra", CNV_RUNS, ids=[f"{c}{''.join(e)}" for c, e in CNV_RUNS])
+def test_cnv_rows_bit_exact(datadir, case, extra):
+    bam, fa, tag = _oracle_once(datadir, case, extra)
     run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra)
     ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"g_{tag}.vcf").read()
     if "-V" in extra:
         assert ov.count("<DEL>") + ov.count("<DUP>") > 0
+    assert ov == gv
+
+
+@pytest.mark.parametrize("case,extra", [("cnv", ["-V", "1"]), ("cnv_long", ["-V", "1", "-M"]),
+                                        ("cnv_multi", ["-V", "1", "-p", "3"])],
+                         ids=["cnv_V1", "cnv_long_V1_M", "cnv_multi_V1_p3"])
+def test_cnv_wave_window_search(datadir, case, extra):
+    """GROM_CNV_BUDGET=1 leaves every DEL/DUP window search past its first
+    ML+256 bases (phase B) and every call's slide and trim (phases C/D) to
+    the walk's wave-cooperative routines (phase_ab_wave, phase_cd_wave): the
+    rows must still be the oracle's."""
+    bam, fa, tag = _oracle_once(datadir, case, extra)
+    run_grom(datadir, bam, fa, f"gw_{tag}.vcf", extra, env_extra={"GROM_CNV_BUDGET": "1"})
+    ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"gw_{tag}.vcf").read()
+    assert ov.count("<DEL>") + ov.count("<DUP>") > 0
     assert ov == gv
 
 
