@@ -32,6 +32,14 @@ CASES = {
     # long copy-number regions (0.3-1 Mb, as in BASELINE configs[2]): calls whose
     # window search spans the region (the walk's wave-cooperative phases)
     "cnv_long": ["-L", "4000000", "-s", "18", "-V", "0.0000008", "-W", "300000,1000000", "-Q", "0.05", "-D", "0.05"],
+    # BASELINE configs[4] shape: 60x tetraploid donor (allele fractions k/4),
+    # a male genome (chrX and chrY at half depth), run with -p 4 -g 1
+    "c5_tetra_male": ["-L", "500000,400000,300000", "-n", "chr1,chrX,chrY", "-c", "60,30,30", "-P", "4", "-s", "5",
+                      "-X", "4", "-D", "0.02"],
+    # BASELINE configs[2] shape: six contigs with SNVs/indels, breakpoint SVs,
+    # copy-number regions and 5% PCR duplicates, run with -M
+    "c3_genome": ["-L", "500000,420000,380000,300000,260000,220000", "-s", "3", "-D", "0.05", "-X", "6",
+                  "-V", "0.000002", "-W", "20000,120000"],
     # breakpoint evidence: deletions, duplications, inversions, insertions and
     # translocations with split reads (SA tags), a 300 kb partner chromosome
     "sv": ["-L", "600000,300000", "-s", "31", "-X", "30", "-I", "0.0003", "-J", "0.3", "-Q", "0.05"],

@@ -34,6 +34,11 @@ RUNS = [
     ("sv", ["-S"]),
     ("sv", ["-d", "2", "-u", "0.5", "-j", "0.02"]),
     ("sv", ["-l", "2"]),
+    # BASELINE configs[4] and configs[2] shapes
+    ("c5_tetra_male", ["-p", "4", "-g", "1"]),
+    ("c5_tetra_male", ["-p", "4", "-g", "1", "-M", "-V", "1"]),
+    ("c3_genome", ["-M"]),
+    ("c3_genome", ["-M", "-V", "1"]),
 ]
 
 # read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call
@@ -230,3 +235,15 @@ def test_two_contexts_scan_concurrently():
         d1.close()
         d0.close()
         b.close()
+
+
+def test_configs1_full_chromosome_vcf(datadir):
+    """BASELINE configs[1] at full size: one 100 Mb chromosome at 30x through
+    the GPU CLI and through the oracle; VCF and .ctx.vcf byte-identical."""
+    bam, fa = synth(datadir, "c2_100mb", ["-L", "100000000", "-s", "2"])
+    run_oracle(datadir, bam, fa, "o_c2.vcf")
+    run_grom(datadir, bam, fa, "g_c2.vcf")
+    for ext in (".vcf", ".ctx.vcf"):
+        assert filecmp.cmp(datadir / f"o_c2{ext}", datadir / f"g_c2{ext}", shallow=False), ext
+    rows = sum(1 for ln in open(datadir / "g_c2.vcf") if not ln.startswith("#"))
+    assert rows > 50000
