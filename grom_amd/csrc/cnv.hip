@@ -981,36 +981,62 @@ __device__ __forceinline__ double wave_max_d(double v) {
 // The callers run in one-wave blocks (the walk kernels), so the block
 // barrier is the wave's.
 __device__ __forceinline__ double wave_chain1(double &tot, double a) {
-    __shared__ double buf[64];
+    __shared__ double buf[64], outb[64];
     const int lane = threadIdx.x & 63;
     buf[lane] = a;
     __syncthreads();
-    double t = tot, mine = t;
-#pragma unroll 16
-    for (int k = 0; k < 64; k++) {
-        t = t + buf[k];
-        mine = lane == k ? t : mine;
+    if (lane == 0) {  // one lane runs the dependent adds; the others wait at the barrier
+        double t = tot;
+        for (int k = 0; k < 64; k += 16) {
+            double v[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = buf[k + j];
+            double o[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                t = t + v[j];
+                o[j] = t;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; j++) outb[k + j] = o[j];
+        }
     }
     __syncthreads();
-    tot = t;
+    const double mine = outb[lane];
+    tot = outb[63];
+    __syncthreads();
     return mine;
 }
 
 __device__ __forceinline__ double wave_chain2(double &tot, double a, double b) {
-    __shared__ double buf2[2][64];
+    // interleaved (a_k, b_k) pairs, read 4 steps at a time into registers
+    // ahead of the dependent adds
+    __shared__ double2 ab[64];
+    __shared__ double outb2[64];
     const int lane = threadIdx.x & 63;
-    buf2[0][lane] = a;
-    buf2[1][lane] = b;
+    ab[lane] = make_double2(a, b);
     __syncthreads();
-    double t = tot, mine = t;
-#pragma unroll 16
-    for (int k = 0; k < 64; k++) {
-        t = t + buf2[0][k];
-        t = t + buf2[1][k];
-        mine = lane == k ? t : mine;
+    if (lane == 0) {
+        double t = tot;
+        for (int k = 0; k < 64; k += 8) {
+            double2 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = ab[k + j];
+            double o[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                t = t + v[j].x;
+                t = t + v[j].y;
+                o[j] = t;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) outb2[k + j] = o[j];
+        }
     }
     __syncthreads();
-    tot = t;
+    const double mine = outb2[lane];
+    tot = outb2[63];
+    __syncthreads();
     return mine;
 }
 
@@ -1150,17 +1176,32 @@ __device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int6
                 if (ts > stdevs) stdevs = ts;
             }
             pa += 1;
-            // the slide (GROM.c:19492-19545), 64 steps per round
+            // the slide (GROM.c:19492-19545), 64 steps per round; the next
+            // round's inputs are loaded while this one runs (the rounds are a
+            // serial chain, so load latency would otherwise add up)
+            uint32_t nba, nbb;
+            double nza, nzb;
+            auto load = [&](int64_t at) {
+                const int64_t q = at + lane;
+                const bool ok = q < W.len;
+                nba = ok ? W.wb[q] : 0u;
+                nbb = ok ? W.wb[q - L] : 0u;
+                nza = ok ? W.sd[q] : 0.0;
+                nzb = ok ? W.sd[q - L] : 0.0;
+            };
+            load(pa);
             for (;;) {
                 const int64_t p = pa + lane;
                 const bool inl = p < W.len;
-                const uint32_t ba = inl ? W.wb[p] : 0u, bb = inl ? W.wb[p - L] : 0u;
+                const uint32_t ba = nba, bb = nbb;
+                const double za = nza, zb = nzb;
+                load(pa + 64);
                 const int mt = wave_last_incl(inl ? cdef(bb) : -1, mqb);
                 const int ml = wave_last_incl(inl ? cdef(ba) : -1, mqi);
                 const bool qt = inl && !(bb & B_LOW) && (bb & (B_W0 << mt));
                 const bool ql = inl && !(ba & B_LOW) && (ba & (B_W0 << ml));
-                const double vt = qt ? -sgn * W.sd[p - L] : 0.0;
-                const double vl = ql ? sgn * W.sd[p] : 0.0;
+                const double vt = qt ? -sgn * zb : 0.0;
+                const double vl = ql ? sgn * za : 0.0;
                 const int64_t cj = cnt + wave_incl_sum((ql ? 1 : 0) - (qt ? 1 : 0));
                 double t = tot;
                 const double tj = wave_chain2(t, vt, vl);
@@ -1578,6 +1619,207 @@ __global__ void k_cnv_zscatter(const int64_t *__restrict__ pos, const double *__
     if (i < n) sd[pos[i]] = z[i];
 }
 
+// ---- candidate classification: phases A and B without the serial sum ----
+//
+// Inside a long copy-number region every base is a candidate whose phase B
+// runs to L = 10,000 bases.  The walk needs, per candidate, only: does phase A
+// stop (a jump), does any window pass the z test (a call -- rare, and the
+// walk then leaves the region), or neither (a no-op, the walk steps on).
+// The integer parts (class state, pass counts, the 2*cnt2 < wl stop) are
+// exact from per-64-base bit words and popcounts; the z test needs the
+// reference's sequential double sum only near its threshold: with the sum
+// approximated from per-block sums (error far below 1e-9 of sum |z|), a
+// window whose bound stays below 3 * cnt * wsd by that margin is certainly
+// not a pass, and a whole 64-base block is skipped when no step in it can
+// stop or pass.  Everything else -- phase A's own exact sum decides the first
+// window -- is UNDECIDED and computed exactly (k_cnv_pre, or the walk).
+constexpr int CW_SEG = 64;  // words per wave segment in the word kernels
+
+struct CandWords {
+    uint64_t *nl, *def;  // nonlow; nonlow and class-defining (HI or depth > 0)
+    uint64_t *pm;        // [kind][class][word]: nonlow and passing with the class fixed
+    uint64_t *pk;        // [kind][word]: nonlow and passing under the last defining base's class
+    double *bsum, *bmax, *bmin, *babs;  // per word: sum z (nonlow), max/min running sum, sum |z|
+    int8_t *kend;        // per word: the last defining class at its end
+    int64_t n_words;
+};
+
+// last defining class per segment of CW_SEG words (for the carry scan)
+__global__ __launch_bounds__(256) void k_cnv_cls_seg(const uint16_t *__restrict__ wb, int64_t len, int64_t n_seg,
+                                                     int8_t *__restrict__ seg_last) {
+    const int64_t sg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sg >= n_seg) return;
+    int c = -1;
+    for (int w = 0; w < CW_SEG; w++) {
+        const int64_t p = (sg * CW_SEG + w) * 64 + lane;
+        const uint32_t b = p < len ? (uint32_t)wb[p] : (uint32_t)B_LOW;
+        const int e = !(b & B_LOW) ? cdef(b) : -1;
+        c = __builtin_amdgcn_readlane(wave_last_incl(e, c), 63);
+    }
+    if (lane == 0) seg_last[sg] = (int8_t)c;
+}
+
+__global__ __launch_bounds__(256) void k_cnv_words(const uint16_t *__restrict__ wb, const double *__restrict__ sd,
+                                                   int64_t len, int64_t n_seg, const int8_t *__restrict__ carry,
+                                                   CandWords C) {
+    const int64_t sg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sg >= n_seg) return;
+    int c = carry[sg];
+    for (int w = 0; w < CW_SEG; w++) {
+        const int64_t wi = sg * CW_SEG + w;
+        if (wi >= C.n_words) return;
+        const int64_t p = wi * 64 + lane;
+        const bool in = p < len;
+        const uint32_t b = in ? (uint32_t)wb[p] : 0u;
+        const bool nl = in && !(b & B_LOW);
+        const int e = nl ? cdef(b) : -1;
+        const int K = wave_last_incl(e, c);
+        c = __builtin_amdgcn_readlane(K, 63);
+        const unsigned long long wnl = __ballot(nl), wdef = __ballot(e >= 0);
+        unsigned long long wpm[2][2], wpk[2];
+        for (int k = 0; k < 2; k++) {
+            const uint32_t pb0 = k == 0 ? B_DEL0 : B_DUP0;
+            wpm[k][0] = __ballot(nl && (b & pb0));
+            wpm[k][1] = __ballot(nl && (b & (pb0 << 1)));
+            wpk[k] = __ballot(nl && K >= 0 && (b & (pb0 << K)));
+        }
+        // running sum of z over the word's nonlow bases (any association: a bound input)
+        double z = nl ? sd[p] : 0.0, ps = z;
+        for (int d = 1; d < 64; d <<= 1) {
+            const double t = __shfl_up(ps, d);
+            if (lane >= d) ps += t;
+        }
+        double mx = ps, mn = ps, ab = fabs(z);
+        for (int o = 32; o > 0; o >>= 1) {
+            mx = fmax(mx, __shfl_xor(mx, o));
+            mn = fmin(mn, __shfl_xor(mn, o));
+            ab += __shfl_xor(ab, o);
+        }
+        const double tot = __shfl(ps, 63);
+        if (lane == 0) {
+            C.nl[wi] = wnl;
+            C.def[wi] = wdef;
+            for (int k = 0; k < 2; k++) {
+                C.pm[(k * 2 + 0) * C.n_words + wi] = wpm[k][0];
+                C.pm[(k * 2 + 1) * C.n_words + wi] = wpm[k][1];
+                C.pk[k * C.n_words + wi] = wpk[k];
+            }
+            C.kend[wi] = (int8_t)c;
+            C.bsum[wi] = tot;
+            C.bmax[wi] = mx;
+            C.bmin[wi] = mn;
+            C.babs[wi] = ab;
+        }
+    }
+}
+
+// One lane per candidate.  nxt[m][p] gets the no-op (p) or phase A's jump;
+// the rest are listed in und[] (and get NXT_UNDECIDED).
+template <int KIND>
+__global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand,
+                                                      CandWords C, const double *__restrict__ wsdmin,
+                                                      int32_t *__restrict__ nxt, int64_t *__restrict__ und,
+                                                      uint32_t *n_und, uint32_t und_cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_cand) return;
+    const int64_t p = cand[i] >> 1;
+    const int m = (int)(cand[i] & 1);
+    const int64_t L = W.L, ML = W.min_len, end = W.end;
+    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    const double sgn = KIND == 0 ? 1.0 : -1.0;
+    const double *wsd = W.wsd;
+    auto cls = [](uint32_t b, int c) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : c; };
+    int32_t out = (int32_t)p;
+    bool undecided = false;
+    // phase A, exactly (GROM.c:19370-19400)
+    int mqi = m;
+    bool defined = false;
+    int64_t wl = 0, cnt2 = 0;
+    for (int64_t pa = p; pa < p + ML; pa++) {
+        wl += 1;
+        const uint32_t b = W.wb[pa];
+        if (!(b & B_LOW)) {
+            if (cdef(b) >= 0) defined = true;
+            mqi = cls(b, mqi);
+            if (b & (pb0 << mqi)) cnt2 += 1;
+            else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
+        } else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
+    }
+    {
+        // the first window's sum is the reference's own (same order)
+        int64_t cnt = ML;
+        double R = 0.0, A = 0.0;
+        for (int64_t a = p; a < p + ML; a++) {
+            const uint32_t b = W.wb[a];
+            cnt -= (b & B_LOW);
+            const double z = W.sd[a];
+            if (KIND == 0) R += z; else R -= z;
+            A += fabs(z);
+        }
+        if (cnt > 0 && wsd[ML] > 0 && ratio_ge_min(R, cnt * wsd[ML])) { undecided = true; goto done; }
+        // phase B (GROM.c:19405-19470)
+        int64_t x = p + ML;
+        const int64_t xend = p + L;
+        while (x < xend) {
+            if ((x & 63) == 0 && x + 64 <= xend && x + 64 <= end && 2 * cnt2 - wl >= 64) {
+                const int64_t wi = x >> 6;
+                const uint64_t dw = C.def[wi];
+                if (defined || dw == 0) {
+                    const uint64_t pw = defined ? C.pk[KIND * C.n_words + wi] : C.pm[(KIND * 2 + mqi) * C.n_words + wi];
+                    bool skip = pw == 0;
+                    if (!skip) {
+                        const double ub = R + (KIND == 0 ? C.bmax[wi] : -C.bmin[wi]);
+                        const double slack = 1e-9 * (A + C.babs[wi] + fabs(ub)) + 1e-300;
+                        const double dlo = (double)(cnt + 1) * wsdmin[wl + 1];
+                        skip = dlo > 0 && ub + slack < 3.0 * dlo * (1.0 - 1e-15);
+                    }
+                    if (skip) {
+                        if (defined) mqi = C.kend[wi];
+                        cnt += __popcll(C.nl[wi]);
+                        cnt2 += __popcll(pw);
+                        R += sgn * C.bsum[wi];
+                        A += C.babs[wi];
+                        wl += 64;
+                        x += 64;
+                        continue;
+                    }
+                }
+            }
+            // step by step to the next word boundary
+            const int64_t xb = min(xend, (x | 63) + 1);
+            for (; x < xb; x++) {
+                wl += 1;
+                if (x >= end) goto done;  // a stop: no-op
+                const uint32_t b = W.wb[x];
+                if (!(b & B_LOW)) {
+                    if (cdef(b) >= 0) defined = true;
+                    mqi = cls(b, mqi);
+                    const double z = W.sd[x];
+                    R += sgn * z;
+                    A += fabs(z);
+                    cnt += 1;
+                    if (b & (pb0 << mqi)) {
+                        cnt2 += 1;
+                        if (wsd[wl] > 0) {
+                            const double d = cnt * wsd[wl];
+                            if (!(R + 1e-9 * (A + fabs(R)) < 3.0 * d * (1.0 - 1e-15))) { undecided = true; goto done; }
+                        }
+                    } else if ((2 * cnt2) < wl) goto done;
+                } else if ((2 * cnt2) < wl) goto done;
+            }
+        }
+    }
+done:
+    if (undecided) {
+        out = NXT_UNDECIDED;
+        const uint32_t k = atomicAdd(n_und, 1u);
+        if (k < und_cap) und[k] = cand[i];
+    }
+    nxt[m * W.len + p] = out;
+}
+
 // a call is on the true walk iff its start was visited in its class
 __global__ void k_cnv_calls_valid(const CallRec *calls, uint32_t n, const uint8_t *vis, uint8_t *ok) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1597,7 +1839,7 @@ struct Buf {
 // independent (GROM.c:19359-20020 runs them one after the other over the same
 // inputs), so they run concurrently, each driven by its own host thread
 struct KindBufs {
-    Buf nxt, pre, prepos, ppos, calls, ok, tiles, vis, cnt;
+    Buf nxt, pre, prepos, ppos, calls, ok, tiles, vis, cnt, und;
     hipStream_t st = nullptr;
 };
 
@@ -1609,6 +1851,7 @@ struct CnvScratch {
     const char *gc_ref = nullptr;
     int64_t gc_len = -1, gc_m = -1;
     Buf zover;  // repeat z overrides: positions then values
+    Buf cwords, cw_seg, cw_carry, wsdmin;  // candidate classification: bit words, their class carry, min wsd per 64
     Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1802,11 +2045,12 @@ void cnv_scratch_free(CnvScratch *S) {
     Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre,
                   &S->prepos, &S->ppos, &S->rep, &S->misc, &S->blk, &S->hist,
                   &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
-                  &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover};
+                  &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover, &S->cwords, &S->cw_seg,
+                  &S->cw_carry, &S->wsdmin};
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
     for (KindBufs &K : S->kb) {
-        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt};
+        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und};
         for (Buf *b : kall)
             if (b->p) (void)hipFree(b->p);
         if (K.st) (void)hipStreamDestroy(K.st);
@@ -2376,6 +2620,44 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CK(hipGetLastError());
         WalkIn WI{(const uint16_t *)S->wbits.p, sd, (const double *)S->wsd.p, len, m - 1, (len - W) - ML, L, ML,
                   nullptr};
+        // bit words and block sums for the candidate classification (both kinds)
+        CandWords CW{};
+        {
+            const int64_t n_words = (len + 63) / 64 + 1, n_seg = (n_words + CW_SEG - 1) / CW_SEG;
+            const size_t wbytes = (size_t)n_words * (8 * 8 + 4 * 8 + 1) + 256;
+            if ((rc = grow(S->cwords, wbytes, err, errlen)) || (rc = grow(S->cw_seg, (size_t)n_seg, err, errlen)) ||
+                (rc = grow(S->cw_carry, (size_t)n_seg, err, errlen)) || (rc = grow(S->wsdmin, 8 * (size_t)(L + 2), err, errlen)))
+                return rc;
+            uint64_t *u = (uint64_t *)S->cwords.p;
+            CW.n_words = n_words;
+            CW.nl = u;
+            CW.def = u + n_words;
+            CW.pm = u + 2 * n_words;   // 4 words
+            CW.pk = u + 6 * n_words;   // 2 words
+            double *dd = (double *)(u + 8 * n_words);
+            CW.bsum = dd;
+            CW.bmax = dd + n_words;
+            CW.bmin = dd + 2 * n_words;
+            CW.babs = dd + 3 * n_words;
+            CW.kend = (int8_t *)(dd + 4 * n_words);
+            const unsigned gs = (unsigned)((n_seg * 64 + 255) / 256);
+            hipLaunchKernelGGL(k_cnv_cls_seg, dim3(gs), dim3(256), 0, st, (const uint16_t *)S->wbits.p, len, n_seg,
+                               (int8_t *)S->cw_seg.p);
+            hipLaunchKernelGGL(k_cnv_carry, dim3(1), dim3(1024), 0, st, (const int8_t *)S->cw_seg.p, n_seg,
+                               (int8_t *)S->cw_carry.p);
+            hipLaunchKernelGGL(k_cnv_words, dim3(gs), dim3(256), 0, st, (const uint16_t *)S->wbits.p, (const double *)sd,
+                               len, n_seg, (const int8_t *)S->cw_carry.p, CW);
+            CK(hipGetLastError());
+            std::vector<double> wmin((size_t)L + 2, 0.0);
+            for (int64_t a = 0; a <= L; a++) {
+                double v = wsd[a];
+                for (int64_t b2 = a + 1; b2 <= std::min<int64_t>(a + 63, L); b2++) v = std::min(v, wsd[b2]);
+                wmin[a] = v;
+            }
+            wmin[L + 1] = 0.0;
+            CK(hipMemcpyAsync(S->wsdmin.p, wmin.data(), 8 * (L + 2), hipMemcpyHostToDevice, st));
+            CK(hipStreamSynchronize(st));  // wmin is released on scope exit
+        }
         const int64_t span = std::max<int64_t>(0, WI.end - WI.start);
         const int64_t n_ch = (span + WALK_CHUNK - 1) / WALK_CHUNK;
         uint32_t call_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, len / 1000), 1 << 24);
@@ -2389,10 +2671,11 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             KindBufs &K = S->kb[kind];
             hipStream_t st = K.st;
             int rc = GROM_OK;
-            if ((rc = grow(K.cnt, 64, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
-            uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;  // n_calls, n_pre, n_cand, capped
+            if ((rc = grow(K.cnt, 128, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
+            // n_calls, n_pre, n_cand, capped, n_und; walk counters from byte 64
+            uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;
             WalkIn WK = WI;
-            WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 16) : nullptr;
+            WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 64) : nullptr;
             CK(hipStreamWaitEvent(st, S->walk_in, 0));
             if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 48, st));
             bool done = false;
@@ -2437,34 +2720,57 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     pre = (PreAB *)K.pre.p;
                 }
                 if (ncand) {
-                    // one lane per candidate is the fast way through the noise, whose
-                    // searches stop early; inside a long copy-number region every base
-                    // is a candidate that extends to L, and the walk visits only the
-                    // first: past a budget of lane steps, the walk decides (the wave
-                    // routines, phase_ab_wave / phase_cd_wave)
-                    // GROM_CNV_BUDGET (tests) shrinks the budget so the wave routines take every long search
+                    // GROM_CNV_BUDGET (tests) shrinks the precompute budgets so the
+                    // walk's wave routines take the long searches; GROM_CNV_CLASSIFY=0
+                    // sends every candidate through the exact per-lane phases A/B
                     const char *bud = getenv("GROM_CNV_BUDGET");
                     const int64_t budget = bud ? std::max<int64_t>(atoll(bud), 1) : (int64_t)1 << 27;
-                    // phases A/B: every candidate the walk can meet inside a region
-                    // is a visited no-op there (the reference runs each to L), so by
-                    // default all of them are precomputed, one lane each
-                    const int64_t ab_cap = bud ? std::max<int64_t>(std::min<int64_t>(L, budget / ncand), ML + 256) : L;
-                    if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_pre<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p, ab_cap);
-                    else
-                        hipLaunchKernelGGL(k_cnv_pre<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p, ab_cap);
-                    CK(hipGetLastError());
-                    // phases C/D for every call start, within the same kind of budget
-                    // (the walk finishes the rest)
-                    const int64_t cd_cap = std::max<int64_t>(
-                        std::min<int64_t>(4 * L + 4 * MAX_DIST_LAST_GOOD, budget / std::max<uint32_t>(ncand / 4, 1)),
-                        (int64_t)1024);
-                    const unsigned gpost = (unsigned)((std::min<int64_t>(ncand, pre_cap) + 255) / 256);
-                    if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_post<0>, dim3(gpost), dim3(256), 0, st, WK, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
-                    else
-                        hipLaunchKernelGGL(k_cnv_post<1>, dim3(gpost), dim3(256), 0, st, WK, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
-                    CK(hipGetLastError());
+                    const char *cl = getenv("GROM_CNV_CLASSIFY");
+                    const bool classify = !(cl && strcmp(cl, "0") == 0);
+                    // candidates whose phases A/B are computed exactly, one lane each
+                    const int64_t *pcand = cand;
+                    uint32_t npc = ncand;
+                    if (classify) {
+                        // no-ops and phase-A jumps settled here; the undecided rest listed
+                        if ((rc = grow(K.und, 8 * (size_t)ncand, err, errlen))) return rc;
+                        int64_t *und = (int64_t *)K.und.p;
+                        uint32_t *n_und = n_pre + 3;
+                        CK(hipMemsetAsync(n_und, 0, 4, st));
+                        if (kind == 0)
+                            hipLaunchKernelGGL(k_cnv_classify<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand);
+                        else
+                            hipLaunchKernelGGL(k_cnv_classify<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand);
+                        CK(hipGetLastError());
+                        uint32_t nu = 0;
+                        CK(hipMemcpyAsync(&nu, n_und, 4, hipMemcpyDeviceToHost, st));
+                        CK(hipStreamSynchronize(st));
+                        // few undecided (calls in the noise): exact per-lane precompute;
+                        // many (calls inside long regions, of which the walk visits the
+                        // first): the walk decides them
+                        npc = (int64_t)nu * L <= budget ? nu : 0;
+                        pcand = und;
+                        if (tmg) fprintf(stderr, "cnv classify %s: %u candidates, %u undecided (%s)\n", kind == 0 ? "DEL" : "DUP",
+                                         ncand, nu, npc ? "precomputed" : "left to the walk");
+                    }
+                    if (npc) {
+                        const int64_t ab_cap = bud ? std::max<int64_t>(std::min<int64_t>(L, budget / npc), ML + 256) : L;
+                        if (kind == 0)
+                            hipLaunchKernelGGL(k_cnv_pre<0>, dim3((npc + 255) / 256), dim3(256), 0, st, WK, pcand, npc, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p, ab_cap);
+                        else
+                            hipLaunchKernelGGL(k_cnv_pre<1>, dim3((npc + 255) / 256), dim3(256), 0, st, WK, pcand, npc, nxt, pre, n_pre, pre_cap, (int64_t *)K.ppos.p, ab_cap);
+                        CK(hipGetLastError());
+                        // phases C/D for every call start, within the same kind of budget
+                        // (the walk finishes the rest)
+                        const int64_t cd_cap = std::max<int64_t>(
+                            std::min<int64_t>(4 * L + 4 * MAX_DIST_LAST_GOOD, budget / std::max<uint32_t>(npc / 4, 1)),
+                            (int64_t)1024);
+                        const unsigned gpost = (unsigned)((std::min<int64_t>(npc, pre_cap) + 255) / 256);
+                        if (kind == 0)
+                            hipLaunchKernelGGL(k_cnv_post<0>, dim3(gpost), dim3(256), 0, st, WK, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
+                        else
+                            hipLaunchKernelGGL(k_cnv_post<1>, dim3(gpost), dim3(256), 0, st, WK, pre, n_pre, pre_cap, (const int64_t *)K.ppos.p, cd_cap, n_pre + 2);
+                        CK(hipGetLastError());
+                    }
                 }
                 const unsigned gch = (unsigned)n_ch;  // one wave per chunk
                 if (kind == 0) {
