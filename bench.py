@@ -129,6 +129,7 @@ def main():
                          "thread each")
     ap.add_argument("--gen-workers", type=int, default=0, help="host generator threads (0: auto)")
     ap.add_argument("--cnv-rate", type=float, default=None, help="override the copy-number region rate (tests)")
+    ap.add_argument("--sweep-inflight", default="", help="e.g. 1,2,3,4: time one pass per value first (stderr)")
     args = ap.parse_args()
 
     import torch
@@ -194,6 +195,24 @@ def main():
     run_queue([make] * workers, order)
     t_gen = time.perf_counter() - t_gen
 
+    if args.sweep_inflight:
+        for f in [int(v) for v in args.sweep_inflight.split(",")]:
+            dv = [grom_amd.Device(local, params, slot=local + 8 * k) for k in range(f)]
+            ot = [grom_amd.Out() for _ in dv]
+
+            def sw(k):
+                return lambda i: dv[k].scan(res[i].chrom, res[i].reads, device_resident=True, out=ot[k])
+            run_queue([sw(k) for k in range(f)], order)  # warm
+            t1 = time.perf_counter()
+            run_queue([sw(k) for k in range(f)], order)
+            t1 = time.perf_counter() - t1
+            print(f"[bench] inflight {f}: {t1 * 1e3:.0f} ms per pass, {sum(lengths[i] for i in mine) / t1 / 1e6:.1f} "
+                  f"Mbases/s, {grom_amd.lib().grom_device_mem_free(local) / 2**30:.0f} GiB HBM free", file=sys.stderr,
+                  flush=True)
+            for o in ot:
+                grom_amd.lib().grom_out_free(ctypes.byref(o))
+            for d in reversed(dv):
+                d.close()
     F = max(1, min(args.inflight, 8))
     devs = [grom_amd.Device(local, params, slot=local + 8 * k) for k in range(F)]
     outs = [grom_amd.Out() for _ in devs]

@@ -41,6 +41,7 @@
 #include <thread>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -1821,10 +1822,13 @@ done:
 }
 
 // a call is on the true walk iff its start was visited in its class
-__global__ void k_cnv_calls_valid(const CallRec *calls, uint32_t n, const uint8_t *vis, uint8_t *ok) {
+// (chunks the true walk jumps over entirely are flagged in `skipped`)
+__global__ void k_cnv_calls_valid(const CallRec *calls, uint32_t n, const uint8_t *vis, const uint8_t *skipped,
+                                  int64_t start, int64_t chunk, uint8_t *ok) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    ok[i] = vis[calls[i].p] == 1 + calls[i].m;
+    const int64_t p = calls[i].p;
+    ok[i] = vis[p] == 1 + calls[i].m && !skipped[(p - start) / chunk];
 }
 
 // ---------------- host side ----------------
@@ -1839,7 +1843,7 @@ struct Buf {
 // independent (GROM.c:19359-20020 runs them one after the other over the same
 // inputs), so they run concurrently, each driven by its own host thread
 struct KindBufs {
-    Buf nxt, pre, prepos, ppos, calls, ok, tiles, vis, cnt, und;
+    Buf nxt, pre, prepos, ppos, calls, ok, tiles, vis, cnt, und, skip;
     hipStream_t st = nullptr;
 };
 
@@ -2050,7 +2054,7 @@ void cnv_scratch_free(CnvScratch *S) {
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
     for (KindBufs &K : S->kb) {
-        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und};
+        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und, &K.skip};
         for (Buf *b : kall)
             if (b->p) (void)hipFree(b->p);
         if (K.st) (void)hipStreamDestroy(K.st);
@@ -2784,6 +2788,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 std::vector<ChunkState> hcs(n_ch);
                 CK(hipMemcpyAsync(hcs.data(), dcs, sizeof(ChunkState) * n_ch, hipMemcpyDeviceToHost, st));
                 CK(hipStreamSynchronize(st));
+                std::vector<uint8_t> skipped((size_t)n_ch, 0);
                 // reconcile: the true exit of each chunk, in order (GROM.c's walk is one pass)
                 int64_t tx = hcs[0].x1;
                 int tl_ = hcs[0].l1;
@@ -2796,7 +2801,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     const int el = hcs[k].status == ST_NOMERGE ? hcs[k].l2 : hcs[k].l1;
                     if (entry_ok && hcs[k].status != ST_PASSTHRU) { tx = ex; tl_ = el; continue; }
                     if (tx >= c1) {  // the true walk jumps over this chunk
-                        CK(hipMemsetAsync(vis + c0, 0, c1 - c0, st));
+                        skipped[k] = 1;
                         continue;
                     }
                     if (kind == 0)
@@ -2836,8 +2841,10 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 std::vector<CallRec> hc(nc);
                 std::vector<uint8_t> ok(nc);
                 if (nc) {
+                    if ((rc = grow(K.skip, (size_t)n_ch, err, errlen))) return rc;
+                    CK(hipMemcpyAsync(K.skip.p, skipped.data(), (size_t)n_ch, hipMemcpyHostToDevice, st));
                     hipLaunchKernelGGL(k_cnv_calls_valid, dim3((nc + 255) / 256), dim3(256), 0, st, dcalls, nc, vis,
-                                       (uint8_t *)K.ok.p);
+                                       (const uint8_t *)K.skip.p, WK.start, WALK_CHUNK, (uint8_t *)K.ok.p);
                     CK(hipMemcpyAsync(hc.data(), dcalls, sizeof(CallRec) * nc, hipMemcpyDeviceToHost, st));
                     CK(hipMemcpyAsync(ok.data(), K.ok.p, nc, hipMemcpyDeviceToHost, st));
                     CK(hipStreamSynchronize(st));
@@ -2906,9 +2913,10 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             }
             Gathered g;
             if ((rc = gather(S, st, rg, tot, gcw, acw, d_mq, d_rd, d_low, flag, g, err, errlen))) return rc;
-            std::vector<double> pl, tmp;
-            for (size_t j = 0; j < keep.size(); j++) {
-                const CallRec &c = found[kind][keep[j].first];
+            // copy number of every kept call (GROM.c:20100-20160): independent per
+            // call, so host threads share them; the rows are then written in order
+            std::vector<double> cnv_cn(keep.size(), -1.0), cnv_cs(keep.size(), 0.0);
+            auto cn_of = [&](size_t j, std::vector<double> &pl, std::vector<double> &tmp) {
                 pl.clear();
                 for (int64_t i = 0; i < rg[j].count; i++) {
                     const int64_t o = rg[j].out + i;
@@ -2931,10 +2939,29 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         cns = sqrt(cns / pc);
                     }
                 }
+                cnv_cn[j] = cn;
+                cnv_cs[j] = cns;
+            };
+            {
+                int64_t work = 0;
+                for (size_t j = 0; j < keep.size(); j++) work += rg[j].count;
+                const unsigned nt = (unsigned)std::min<int64_t>({(int64_t)8, (int64_t)keep.size(), 1 + work / 200000});
+                std::atomic<size_t> next{0};
+                auto worker = [&] {
+                    std::vector<double> pl, tmp;
+                    for (size_t j; (j = next.fetch_add(1)) < keep.size();) cn_of(j, pl, tmp);
+                };
+                std::vector<std::thread> th;
+                for (unsigned t = 1; t < nt; t++) th.emplace_back(worker);
+                worker();
+                for (auto &t : th) t.join();
+            }
+            for (size_t j = 0; j < keep.size(); j++) {
+                const CallRec &c = found[kind][keep[j].first];
                 char line[512];
                 int nl = snprintf(line, sizeof(line), "%s\t%lld\t.\t.\t%s\t.\t.\tEND=%lld\tSD:Z:CN:CS\t%e:%e:%.2f:%e\n",
                                   chr_name, (long long)c.p + 1, kind == 0 ? "<DEL>" : "<DUP>", (long long)c.ce + 1,
-                                  c.stdevs, keep[j].second, cn, cns);
+                                  c.stdevs, keep[j].second, cnv_cn[j], cnv_cs[j]);
                 rows.append(line, (size_t)nl);
                 n_rows++;
             }
