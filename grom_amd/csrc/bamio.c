@@ -3,6 +3,7 @@
  */
 #include "bamio.h"
 
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include <zlib.h>
@@ -37,25 +38,55 @@ int bgzf_open_read(bgzf_reader *r, const char *path) {
     return 0;
 }
 
-void bgzf_close_read(bgzf_reader *r) {
-    if (r->fp) fclose(r->fp);
-    free(r->blk);
-    free(r->cbuf);
-    memset(r, 0, sizeof(*r));
+/* ---- multi-threaded inflate: the caller reads compressed blocks in file
+ * order into a ring of slots, workers inflate them, the caller consumes the
+ * slots in order (so the byte stream is the same as the serial reader's) ---- */
+enum { SLOT_FREE = 0, SLOT_QUEUED, SLOT_BUSY, SLOT_DONE };
+typedef struct {
+    unsigned char *cbuf, *blk;
+    int clen, len, rc, state;
+    uint32_t isize;
+} bgzf_slot;
+
+struct bgzf_mt {
+    int n_thr, n_slot;
+    bgzf_slot *slot;
+    long head, tail; /* next slot to consume / to fill */
+    int file_eof, file_err;
+    int stop;
+    pthread_t *thr;
+    pthread_mutex_t mu;
+    pthread_cond_t work, done;
+};
+
+static int inflate_block(const unsigned char *cbuf, int clen, uint32_t isize, unsigned char *out) {
+    if (isize == 0) return 0;
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    if (inflateInit2(&zs, -15) != Z_OK) return -1;
+    zs.next_in = (unsigned char *)cbuf;
+    zs.avail_in = clen - 8;
+    zs.next_out = out;
+    zs.avail_out = BGZF_MAX_BLOCK;
+    int rc = inflate(&zs, Z_FINISH);
+    inflateEnd(&zs);
+    if (rc != Z_STREAM_END || zs.total_out != isize) return -1;
+    return (int)isize;
 }
 
-/* inflate the next block into r->blk; returns block length, 0 at EOF, -1 error */
-static int bgzf_next_block(bgzf_reader *r) {
+/* one compressed block: header parsed, deflate data + trailer into cbuf;
+ * returns 1, 0 at EOF, -1 on error */
+static int read_cblock(FILE *fp, unsigned char *cbuf, int *clen_out, uint32_t *isize_out) {
     unsigned char hdr[18];
-    size_t got = fread(hdr, 1, 18, r->fp);
-    if (got == 0) { r->eof = 1; return 0; }
+    size_t got = fread(hdr, 1, 18, fp);
+    if (got == 0) return 0;
     if (got != 18 || hdr[0] != 0x1f || hdr[1] != 0x8b || hdr[3] != 0x04) return -1;
     uint16_t xlen = rd16(hdr + 10);
     /* locate the BC subfield; hdr holds the first 6 bytes of the extra field */
     unsigned char extra[1024];
     if (xlen > sizeof(extra) || xlen < 6) return -1;
     memcpy(extra, hdr + 12, 6);
-    if (xlen > 6 && fread(extra + 6, 1, xlen - 6, r->fp) != (size_t)(xlen - 6)) return -1;
+    if (xlen > 6 && fread(extra + 6, 1, xlen - 6, fp) != (size_t)(xlen - 6)) return -1;
     int bsize = -1;
     for (int o = 0; o + 4 <= xlen;) {
         int sl = rd16(extra + o + 2);
@@ -65,21 +96,141 @@ static int bgzf_next_block(bgzf_reader *r) {
     if (bsize < 0) return -1;
     int clen = bsize + 1 - 12 - xlen; /* deflate data + 8-byte trailer */
     if (clen < 8 || clen > BGZF_MAX_BLOCK) return -1;
-    if (fread(r->cbuf, 1, clen, r->fp) != (size_t)clen) return -1;
-    uint32_t isize = rd32(r->cbuf + clen - 4);
+    if (fread(cbuf, 1, clen, fp) != (size_t)clen) return -1;
+    uint32_t isize = rd32(cbuf + clen - 4);
     if (isize > BGZF_MAX_BLOCK) return -1;
-    if (isize == 0) { r->blk_len = 0; r->blk_off = 0; return 1; /* empty block (e.g. EOF marker) */ }
-    z_stream zs;
-    memset(&zs, 0, sizeof(zs));
-    if (inflateInit2(&zs, -15) != Z_OK) return -1;
-    zs.next_in = r->cbuf;
-    zs.avail_in = clen - 8;
-    zs.next_out = r->blk;
-    zs.avail_out = BGZF_MAX_BLOCK;
-    int rc = inflate(&zs, Z_FINISH);
-    inflateEnd(&zs);
-    if (rc != Z_STREAM_END || zs.total_out != isize) return -1;
-    r->blk_len = (int)isize;
+    *clen_out = clen;
+    *isize_out = isize;
+    return 1;
+}
+
+static void *bgzf_worker(void *arg) {
+    struct bgzf_mt *m = (struct bgzf_mt *)arg;
+    pthread_mutex_lock(&m->mu);
+    for (;;) {
+        bgzf_slot *s = NULL;
+        while (!m->stop) {
+            for (long k = m->head; k < m->tail; k++)
+                if (m->slot[k % m->n_slot].state == SLOT_QUEUED) { s = &m->slot[k % m->n_slot]; break; }
+            if (s) break;
+            pthread_cond_wait(&m->work, &m->mu);
+        }
+        if (m->stop) break;
+        s->state = SLOT_BUSY;
+        pthread_mutex_unlock(&m->mu);
+        const int rc = inflate_block(s->cbuf, s->clen, s->isize, s->blk);
+        pthread_mutex_lock(&m->mu);
+        s->rc = rc;
+        s->len = rc;
+        s->state = SLOT_DONE;
+        pthread_cond_broadcast(&m->done);
+    }
+    pthread_mutex_unlock(&m->mu);
+    return NULL;
+}
+
+int bgzf_set_threads(bgzf_reader *r, int n) {
+    if (n <= 1 || r->mt) return 0;
+    struct bgzf_mt *m = (struct bgzf_mt *)calloc(1, sizeof(*m));
+    if (!m) return -1;
+    m->n_thr = n;
+    m->n_slot = 4 * n;
+    m->slot = (bgzf_slot *)calloc(m->n_slot, sizeof(bgzf_slot));
+    m->thr = (pthread_t *)calloc(n, sizeof(pthread_t));
+    if (!m->slot || !m->thr) { free(m->slot); free(m->thr); free(m); return -1; }
+    for (int k = 0; k < m->n_slot; k++) {
+        m->slot[k].cbuf = (unsigned char *)malloc(BGZF_MAX_BLOCK);
+        m->slot[k].blk = (unsigned char *)malloc(BGZF_MAX_BLOCK);
+        if (!m->slot[k].cbuf || !m->slot[k].blk) return -1;
+    }
+    pthread_mutex_init(&m->mu, NULL);
+    pthread_cond_init(&m->work, NULL);
+    pthread_cond_init(&m->done, NULL);
+    for (int t = 0; t < n; t++) pthread_create(&m->thr[t], NULL, bgzf_worker, m);
+    r->mt = m;
+    return 0;
+}
+
+static void bgzf_mt_free(struct bgzf_mt *m) {
+    if (!m) return;
+    pthread_mutex_lock(&m->mu);
+    m->stop = 1;
+    pthread_cond_broadcast(&m->work);
+    pthread_mutex_unlock(&m->mu);
+    for (int t = 0; t < m->n_thr; t++) pthread_join(m->thr[t], NULL);
+    for (int k = 0; k < m->n_slot; k++) {
+        free(m->slot[k].cbuf);
+        free(m->slot[k].blk);
+    }
+    pthread_mutex_destroy(&m->mu);
+    pthread_cond_destroy(&m->work);
+    pthread_cond_destroy(&m->done);
+    free(m->slot);
+    free(m->thr);
+    free(m);
+}
+
+/* the next block in file order through the pipeline: 1, 0 at EOF, -1 error */
+static int bgzf_mt_next(bgzf_reader *r) {
+    struct bgzf_mt *m = r->mt;
+    pthread_mutex_lock(&m->mu);
+    /* top up the read-ahead: compressed blocks are read here, in file order,
+     * into slots that are free (consumed) */
+    while (!m->file_eof && !m->file_err && m->tail - m->head < m->n_slot) {
+        bgzf_slot *s = &m->slot[m->tail % m->n_slot];
+        pthread_mutex_unlock(&m->mu);
+        const int rc = read_cblock(r->fp, s->cbuf, &s->clen, &s->isize);
+        pthread_mutex_lock(&m->mu);
+        if (rc <= 0) {
+            if (rc < 0) m->file_err = 1;
+            else m->file_eof = 1;
+            break;
+        }
+        s->state = SLOT_QUEUED;
+        m->tail++;
+        pthread_cond_signal(&m->work);
+    }
+    if (m->head == m->tail) {
+        const int err = m->file_err;
+        pthread_mutex_unlock(&m->mu);
+        if (err) return -1;
+        r->eof = 1;
+        return 0;
+    }
+    bgzf_slot *s = &m->slot[m->head % m->n_slot];
+    while (s->state != SLOT_DONE) pthread_cond_wait(&m->done, &m->mu);
+    m->head++;
+    pthread_mutex_unlock(&m->mu);
+    if (s->rc < 0) return -1;
+    /* hand the block over by swapping buffers (the slot is refilled later) */
+    unsigned char *t = r->blk;
+    r->blk = s->blk;
+    s->blk = t;
+    s->state = SLOT_FREE;
+    r->blk_len = s->len;
+    r->blk_off = 0;
+    return 1;
+}
+
+void bgzf_close_read(bgzf_reader *r) {
+    bgzf_mt_free(r->mt);
+    if (r->fp) fclose(r->fp);
+    free(r->blk);
+    free(r->cbuf);
+    memset(r, 0, sizeof(*r));
+}
+
+/* the next block into r->blk; returns 1, 0 at EOF, -1 error */
+static int bgzf_next_block(bgzf_reader *r) {
+    if (r->mt) return bgzf_mt_next(r);
+    int clen = 0;
+    uint32_t isize = 0;
+    const int rc = read_cblock(r->fp, r->cbuf, &clen, &isize);
+    if (rc == 0) { r->eof = 1; return 0; }
+    if (rc < 0) return -1;
+    const int n = inflate_block(r->cbuf, clen, isize, r->blk);
+    if (n < 0) return -1;
+    r->blk_len = n;
     r->blk_off = 0;
     return 1;
 }

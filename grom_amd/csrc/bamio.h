@@ -45,12 +45,14 @@ extern "C" {
 #define GC_EQUAL 7
 #define GC_DIFF 8
 
+struct bgzf_mt;
 typedef struct bgzf_reader {
     FILE *fp;
     unsigned char *blk;     /* decompressed block */
     int blk_len, blk_off;
     unsigned char *cbuf;    /* compressed block */
     int eof;
+    struct bgzf_mt *mt;     /* multi-threaded inflate (bgzf_set_threads), or NULL */
 } bgzf_reader;
 
 typedef struct bgzf_writer {
@@ -95,6 +97,9 @@ int bgzf_open_read(bgzf_reader *r, const char *path);
 void bgzf_close_read(bgzf_reader *r);
 /* read exactly n bytes; returns n, 0 at clean EOF, -1 on error/truncation */
 int bgzf_read(bgzf_reader *r, void *dst, int n);
+/* inflate blocks on n worker threads (n <= 1: in the caller), read ahead in
+ * file order and consumed in order; call before the first read.  0 on success. */
+int bgzf_set_threads(bgzf_reader *r, int n);
 
 int bgzf_open_write(bgzf_writer *w, const char *path, int level);
 int bgzf_write(bgzf_writer *w, const void *src, int n);

@@ -636,7 +636,15 @@ int grom_cli_main(int argc, char **argv) {
     /* one serial pass over the records, split per chromosome (stream.h);
      * finished chromosomes go to the GPU workers, rows are written in order */
     bam_free_header(&hdr);
-    if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) { fclose(vcf); CLI_FAIL(); }
+    if (bgzf_open_read(&br, bam_name) != 0) { fclose(vcf); CLI_FAIL(); }
+    {
+        /* BGZF blocks inflate on GROM_DECODE_THREADS threads (default 4) while
+         * this thread parses records in order (htslib's bgzf_mt) */
+        const char *dt = getenv("GROM_DECODE_THREADS");
+        const int n_dec = dt ? atoi(dt) : 4;
+        if (bgzf_set_threads(&br, n_dec) != 0) { fclose(vcf); CLI_FAIL(); }
+    }
+    if (bam_read_header(&br, &hdr) != 0) { fclose(vcf); CLI_FAIL(); }
     grom_planner pl;
     grom_planner_init(&pl, order, n_plan);
     grom_batch batch;

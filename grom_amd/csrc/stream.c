@@ -260,44 +260,64 @@ void grom_batch_free(grom_batch *b) {
     free(b->aux_idx); free(b->aux); free(b->drop_pos); free(b->drop_lq); free(b->drop_before);
     free(b->pos); free(b->flag); free(b->mapq); free(b->mtid); free(b->mpos); free(b->isize); free(b->l_qseq);
     free(b->cigar_off); free(b->cigar); free(b->base_off); free(b->seq); free(b->qual); free(b->name_id);
-    for (int64_t i = 0; i < b->ncap; i++) free(b->nkeys[i]);
     free(b->nkeys);
+    free(b->nhash);
     free(b->nids);
+    free(b->narena);
     memset(b, 0, sizeof(*b));
 }
 
-static uint64_t hash_name(const char *s) {
+static uint64_t hash_name(const char *s, size_t *len) {
     uint64_t h = 0xcbf29ce484222325ULL;
-    for (; *s; s++) h = (h ^ (unsigned char)*s) * 0x100000001b3ULL;
+    const char *p = s;
+    for (; *p; p++) h = (h ^ (unsigned char)*p) * 0x100000001b3ULL;
+    *len = (size_t)(p - s);
     return h;
 }
 
+/* read name -> 32-bit id, equal names <=> equal ids (names of read_name_len
+ * or more characters are never stored: id 0, GROM.c:6813).  Names live in one
+ * growing arena, so interning a new name is a copy, not an allocation. */
 static uint32_t intern(grom_batch *b, const char *s) {
-    size_t L = strlen(s);
-    if (L == 0 || L >= (size_t)b->read_name_len) return 0; /* never stored, GROM.c:6813 */
+    size_t L;
+    const uint64_t h = hash_name(s, &L);
+    if (L == 0 || L >= (size_t)b->read_name_len) return 0;
     if (2 * (b->nn + 1) > b->ncap) {
         int64_t nc = b->ncap ? 2 * b->ncap : 65536;
-        char **nk = calloc(nc, sizeof(char *));
-        uint32_t *ni = calloc(nc, sizeof(uint32_t));
+        int64_t *nk = calloc(nc, sizeof(int64_t));
+        uint64_t *nh = malloc(sizeof(uint64_t) * nc);
+        uint32_t *ni = malloc(sizeof(uint32_t) * nc);
         for (int64_t i = 0; i < b->ncap; i++)
             if (b->nkeys[i]) {
-                int64_t j = (int64_t)(hash_name(b->nkeys[i]) & (uint64_t)(nc - 1));
+                int64_t j = (int64_t)(b->nhash[i] & (uint64_t)(nc - 1));
                 while (nk[j]) j = (j + 1) & (nc - 1);
                 nk[j] = b->nkeys[i];
+                nh[j] = b->nhash[i];
                 ni[j] = b->nids[i];
             }
         free(b->nkeys);
+        free(b->nhash);
         free(b->nids);
         b->nkeys = nk;
+        b->nhash = nh;
         b->nids = ni;
         b->ncap = nc;
     }
-    int64_t j = (int64_t)(hash_name(s) & (uint64_t)(b->ncap - 1));
+    int64_t j = (int64_t)(h & (uint64_t)(b->ncap - 1));
     while (b->nkeys[j]) {
-        if (strcmp(b->nkeys[j], s) == 0) return b->nids[j];
+        if (b->nhash[j] == h && strcmp(b->narena + b->nkeys[j] - 1, s) == 0) return b->nids[j];
         j = (j + 1) & (b->ncap - 1);
     }
-    b->nkeys[j] = strdup(s);
+    if (b->narena_len + (int64_t)L + 1 > b->narena_cap) {
+        int64_t nc = b->narena_cap ? 2 * b->narena_cap : (1 << 22);
+        while (nc < b->narena_len + (int64_t)L + 1) nc *= 2;
+        b->narena = realloc(b->narena, nc);
+        b->narena_cap = nc;
+    }
+    memcpy(b->narena + b->narena_len, s, L + 1);
+    b->nkeys[j] = b->narena_len + 1;
+    b->narena_len += (int64_t)L + 1;
+    b->nhash[j] = h;
     b->nids[j] = (uint32_t)(++b->nn);
     return b->nids[j];
 }

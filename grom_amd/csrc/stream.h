@@ -74,9 +74,14 @@ typedef struct grom_batch {
     uint8_t *seq, *qual;
     uint32_t *name_id;
     /* read-name interning */
-    char **nkeys;
+    /* open-addressing table: name offset into the arena (+1, 0 = empty),
+     * its 64-bit hash and id */
+    int64_t *nkeys;
+    uint64_t *nhash;
     uint32_t *nids;
     int64_t ncap, nn;
+    char *narena;          /* NUL-terminated names, appended */
+    int64_t narena_len, narena_cap;
     int32_t max_ref_span;  /* max over reads of the M/D/N/=/X extent */
     int read_name_len;
     int any_ingested;
