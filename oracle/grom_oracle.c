@@ -33,7 +33,7 @@
 #include <time.h>
 #include <unistd.h>
 
-#include "../grom_amd/csrc/bamio.h"
+#include "orc_bam.h" /* the oracle's own BAM reader: nothing from grom_amd/ */
 
 #define MAX_TRIALS 1000
 #define MAX_CHR_NAMES 30000
