@@ -101,6 +101,40 @@ def run_queue(workers: "list[Callable[[int], None]]", items: Sequence[int]) -> N
         raise errs[0]
 
 
+def sharded_genome_text(scan_chrom: "Callable[[int], str]", lengths: Sequence[int], world: int, rank: int,
+                        gather: "Callable[[dict], list] | None" = None) -> "str | None":
+    """The genome's output text with its chromosomes scanned across ranks:
+    rank r scans its longest-processing-time share (assign_chromosomes), the
+    per-chromosome texts are gathered on rank 0 (the only exchange, off the
+    scan path) and joined in chromosome order -- the order a one-rank run, and
+    GROM's serial loop over the FASTA, writes them.  Returns the text on rank
+    0, None elsewhere.  `gather(obj)` returns every rank's obj on rank 0
+    (torch.distributed.gather_object); None means a single rank."""
+    mine = assign_chromosomes(lengths, world)[rank] if world > 1 else list(range(len(lengths)))
+    texts = {i: scan_chrom(i) for i in mine}
+    parts = [texts] if gather is None else gather(texts)
+    if rank != 0:
+        return None
+    merged = {}
+    for d in parts:
+        for i, t in d.items():
+            if i in merged:
+                raise RuntimeError(f"chromosome {i} scanned by two ranks")
+            merged[i] = t
+    missing = [i for i in range(len(lengths)) if i not in merged]
+    if missing:
+        raise RuntimeError(f"chromosomes {missing} scanned by no rank")
+    return "".join(merged[i] for i in range(len(lengths)))
+
+
+def gather_to_rank0(obj):
+    """torch.distributed.gather_object onto rank 0 (gloo or RCCL)."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
+    dist.gather_object(obj, out, dst=0)
+    return out
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """Max of `value` over all ranks (identity without a process group)."""
     import torch

@@ -247,3 +247,68 @@ def test_configs1_full_chromosome_vcf(datadir):
         assert filecmp.cmp(datadir / f"o_c2{ext}", datadir / f"g_c2{ext}", shallow=False), ext
     rows = sum(1 for ln in open(datadir / "g_c2.vcf") if not ln.startswith("#"))
     assert rows > 50000
+
+
+# ---- multi-GPU path: chromosomes sharded over two ranks (both on this GPU) ----
+GENOME_LENGTHS = [700_000, 600_000, 500_000, 400_000]
+GENOME_NAMES = ["chr1", "chr2", "chrX", "chrY"]
+
+
+def _gpu_scan_factory(slot):
+    import grom_amd
+    p = grom_amd.default_params()
+    p.rmdup = 1
+    probe = grom_amd.SynthBatch.genome_chrom([2_000_000], 0, p, seed=6)
+    probe.close()
+    dev = grom_amd.Device(0, p, slot=slot)
+
+    def scan(i):
+        b = grom_amd.SynthBatch.genome_chrom(GENOME_LENGTHS, i, p, names=GENOME_NAMES, sv_per_mb=4.0,
+                                             dup_frac=0.05, cnv_rate=2e-6, cnv_range=(20_000, 80_000), seed=6)
+        try:
+            text, _ = dev.scan(b.chrom, b.reads)
+            return text
+        finally:
+            b.close()
+    return dev, scan
+
+
+def _gpu_shard_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from grom_amd.shard import gather_to_rank0, sharded_genome_text
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev, scan = _gpu_scan_factory(rank)
+        q.put((rank, sharded_genome_text(scan, GENOME_LENGTHS, world, rank, gather_to_rank0)))
+        dev.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_sharded_genome_matches_one_rank():
+    """configs[3]'s sharding on one GPU: two processes (gloo for the gather),
+    each scanning its longest-processing-time share of a 4-contig genome; the
+    merged VCF rows equal a one-process scan of every chromosome."""
+    import socket
+    import torch.multiprocessing as mp
+    from grom_amd.shard import sharded_genome_text
+    dev, scan = _gpu_scan_factory(40)
+    one = sharded_genome_text(scan, GENOME_LENGTHS, 1, 0)
+    dev.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == one
+    assert one.count("\n") > 100 and "chrx" in one

@@ -78,3 +78,68 @@ def test_timed_concurrent_runs_every_step_once():
     assert dt >= 0
     assert sorted(i for _, i in seen) == list(range(8))
     assert all(i % 3 == k for k, i in seen)
+
+
+# ---- a genome sharded over two ranks: the merged output equals one rank's ----
+SHARD_LENGTHS = [1_300_000, 1_000_000, 900_000, 700_000, 600_000]
+SHARD_NAMES = ["chr1", "chr2", "chr3", "chrX", "chrY"]
+
+
+def _stub_scan(i):
+    """A CPU stand-in for the GPU scan: the chromosome's synthetic reads
+    (generated in this process) summarised into one deterministic line."""
+    import zlib
+    import numpy as np
+    import grom_amd
+    p = grom_amd.default_params()
+    probe = grom_amd.SynthBatch.genome_chrom([2_000_000], 0, p, coverage=8.0, seed=4)
+    probe.close()
+    b = grom_amd.SynthBatch.genome_chrom(SHARD_LENGTHS, i, p, names=SHARD_NAMES, coverage=8.0, sv_per_mb=3.0,
+                                         dup_frac=0.02, seed=4)
+    try:
+        pos = np.ctypeslib.as_array(grom_amd.C.cast(b.reads.pos, grom_amd.C.POINTER(grom_amd.C.c_int32)),
+                                    shape=(b.reads.n,))
+        crc = zlib.crc32(pos.tobytes())
+        return f"{b.chrom.name.decode()}\t{b.reads.n}\t{b.reads.n_aux}\t{b.chrom.p_last}\t{crc:08x}\n"
+    finally:
+        b.close()
+
+
+def _shard_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from grom_amd.shard import gather_to_rank0, sharded_genome_text
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        text = sharded_genome_text(_stub_scan, SHARD_LENGTHS, world, rank, gather_to_rank0)
+        q.put((rank, text))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_genome_matches_one_rank():
+    import torch.multiprocessing as mp
+    from grom_amd.shard import sharded_genome_text
+    one = sharded_genome_text(_stub_scan, SHARD_LENGTHS, 1, 0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None
+    assert res[0] == one
+    assert one.count("\n") == len(SHARD_LENGTHS) and "chrx" in one and "chry" in one
+
+
+def test_sharded_text_rejects_gaps_and_overlaps():
+    from grom_amd.shard import sharded_genome_text
+    with pytest.raises(RuntimeError):
+        sharded_genome_text(lambda i: "x", [5, 4], 2, 0, gather=lambda d: [d, d])  # same chromosome twice
+    with pytest.raises(RuntimeError):
+        sharded_genome_text(lambda i: "x", [5, 4], 2, 0, gather=lambda d: [d])  # rank 1's share missing
