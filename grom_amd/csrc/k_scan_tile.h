@@ -87,7 +87,18 @@ struct __align__(16) ScanLds {
     char ref[TG];
     TileTail tail;
     int32_t m2;  // reads of the chunk that fit the staging budgets
+    // interval sums of the single-op reads (DIFFED below): the caf MAPQ sum
+    // and, packed, the caf counts (MAPQ >= -q in the low half, the rest in
+    // the high half; their sum is also the read's physical depth), as
+    // difference arrays over the tile, prefix-summed once at the end
+    int32_t dmq[TG + 1];
+    uint32_t dcnt[TG + 1];
 };
+// G.mk bit: the read's caf and depth intervals went to the difference arrays
+#define DIFFED (1u << 16)
+// tiles with more reads than this keep the per-lane interval updates (the
+// packed 16-bit caf counts could overflow)
+#define DIFF_MAX_READS 30000
 
 // per-lane counters of one position (cdp_one_base_*)
 struct LaneCounts {
@@ -179,7 +190,7 @@ struct GroupRegs {
 // the scalar view of read g + i
 struct ReadView {
     int32_t p0, lq, bo;  // bo: base offset relative to the staged window
-    uint32_t cw0, ncig, fl, mq, nid, cb;
+    uint32_t cw0, ncig, fl, mq, mkf, nid, cb;
     int i;
 };
 
@@ -193,7 +204,8 @@ __device__ __forceinline__ ReadView view_of(const GroupRegs &G, int i) {
     const uint32_t nf = lane_get(G.nf, i);
     v.ncig = nf & 0xffffu;
     v.fl = nf >> 16;
-    v.mq = lane_get(G.mk, i) & 255u;
+    v.mkf = lane_get(G.mk, i);
+    v.mq = v.mkf & 255u;
     v.nid = lane_get(G.nid, i);
     v.cb = lane_get(G.cb, i);
     return v;
@@ -437,6 +449,11 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
     const uint4 *gq4 = reinterpret_cast<const uint4 *>(R.qual);
     const uint4 *gs4 = reinterpret_cast<const uint4 *>(R.seq);
 
+    const bool use_diff = r1 - r0 <= DIFF_MAX_READS;  // workgroup-uniform
+    L.dmq[tid] = 0;
+    L.dcnt[tid] = 0;
+    if (tid == 0) { L.dmq[TG] = 0; L.dcnt[TG] = 0; }
+
     int32_t c0 = r0;
     while (c0 < r1) {
         const int32_t m = min(RCHUNK, r1 - c0);
@@ -485,6 +502,29 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
             for (int k = 0; k < SLOADS; k++) {
                 const int64_t w = sv0 + tid + k * TG;
                 if (w < sv1) L.seq[w - sv0] = vs[k];
+            }
+        }
+        // single-op staged reads: their caf and physical-depth intervals go
+        // to the tile's difference arrays (one lane per read), so the fold
+        // below skips those per-lane updates (GROM.c:6605-6671, 7173-7181)
+        if (use_diff && staged && tid < m2) {
+            const ReadMeta &rm = L.meta[tid];
+            // (the first CIGAR word from global memory: L.cig is still being written)
+            const uint32_t nc = rm.b.y & 0xffffu, cw = nc == 1 ? R.cigar[rm.b.x] : 0u;
+            const uint32_t op = cw & 15u;
+            const int32_t p0 = (int32_t)rm.a.x, len = (int32_t)(cw >> 4), lq = (int32_t)rm.a.z;
+            const uint32_t mq = rm.b.z & 255u;
+            const bool keep = ((rm.b.z >> 8) & 255u) != 0;
+            if (nc == 1 && (op == 0 || op == 7 || op == 8) && keep && len == lq && p0 >= 0 && len < clen - p0) {
+                const int32_t lo = max(p0, t0) - t0, hi = min(p0 + len, t0 + TG) - t0;
+                if (lo < hi) {
+                    const uint32_t inc = (mq >= (uint32_t)a.rd_min_mapq) ? 1u : 65536u;
+                    atomicAdd(&L.dmq[lo], (int32_t)mq);
+                    atomicSub(&L.dmq[hi], (int32_t)mq);
+                    atomicAdd(&L.dcnt[lo], inc);
+                    atomicSub(&L.dcnt[hi], inc);
+                }
+                L.meta[tid].b.z = rm.b.z | DIFFED;  // read by the fold, written only here
             }
         }
         __syncthreads();
@@ -537,14 +577,16 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
                             const int32_t p0 = u.p0, len = (int32_t)(u.cw0 >> 4);
                             const int mq = (int)u.mq;
                             const uint32_t dx = (uint32_t)(x - p0);
-                            if (p0 >= 0 && len < clen - p0 && dx < (uint32_t)len) {
-                                caf_mq += mq;
-                                caf_rd += (mq >= a.rd_min_mapq) ? 1 : 0;
-                                caf_low += (mq >= a.rd_min_mapq) ? 0 : 1;
+                            if (!(u.mkf & DIFFED)) {  // wave-uniform
+                                if (p0 >= 0 && len < clen - p0 && dx < (uint32_t)len) {
+                                    caf_mq += mq;
+                                    caf_rd += (mq >= a.rd_min_mapq) ? 1 : 0;
+                                    caf_low += (mq >= a.rd_min_mapq) ? 0 : 1;
+                                }
+                                rd += (dx < (uint32_t)u.lq) ? 1 : 0;  // E = pos + l_qseq
                             }
                             const bool pos_ok = p0 >= 0 && p0 < clen;
                             hk[k] = (pos_ok && evals && dx < (uint32_t)min(len, clen - p0)) ? (int32_t)dx : -1;
-                            rd += (dx < (uint32_t)u.lq) ? 1 : 0;  // E = pos + l_qseq
                             qk[k] = 0;
                             sk[k] = 0;
                             if (hk[k] >= 0 && hk[k] < u.lq) staged_base(lq8, ls8, soff, u.bo + hk[k], qk[k], sk[k]);
@@ -581,13 +623,15 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
                     // ---- fast path: a single M/=/X op ----
                     const int32_t len = (int32_t)(u.cw0 >> 4);
                     const uint32_t dx = (uint32_t)(x - p0);
-                    if (p0 >= 0 && len < clen - p0 && dx < (uint32_t)len) {
-                        caf_mq += mq;
-                        caf_rd += (mq >= a.rd_min_mapq) ? 1 : 0;
-                        caf_low += (mq >= a.rd_min_mapq) ? 0 : 1;
+                    if (!(u.mkf & DIFFED)) {  // wave-uniform
+                        if (p0 >= 0 && len < clen - p0 && dx < (uint32_t)len) {
+                            caf_mq += mq;
+                            caf_rd += (mq >= a.rd_min_mapq) ? 1 : 0;
+                            caf_low += (mq >= a.rd_min_mapq) ? 0 : 1;
+                        }
+                        rd += (dx < (uint32_t)u.lq) ? 1 : 0;  // E = pos + l_qseq
                     }
                     if (pos_ok && evals && dx < (uint32_t)min(len, clen - p0)) hit_qi = (int32_t)dx;
-                    rd += (dx < (uint32_t)u.lq) ? 1 : 0;  // E = pos + l_qseq
                 } else {
                     // ---- general CIGAR walk (rare: int64 arithmetic) ----
                     const uint32_t cb = u.cb, ce = u.cb + u.ncig;
@@ -700,6 +744,27 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
             }
         }
         c0 += m2;
+    }
+
+    // the difference arrays: an inclusive scan over the tile (wave scans,
+    // then the earlier waves' totals)
+    if (use_diff) {
+        __syncthreads();
+        int32_t vm = L.dmq[tid];
+        uint32_t vc = L.dcnt[tid];
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t tm = __shfl_up(vm, d, 64);
+            const uint32_t tc = __shfl_up(vc, d, 64);
+            if (lane >= d) { vm += tm; vc += tc; }
+        }
+        __syncthreads();  // every lane has read its entry
+        if (lane == 63) { L.dmq[wave] = vm; L.dcnt[wave] = vc; }
+        __syncthreads();
+        for (int w = 0; w < wave; w++) { vm += L.dmq[w]; vc += L.dcnt[w]; }
+        caf_mq += vm;
+        caf_rd += (int32_t)(vc & 0xffffu);
+        caf_low += (int32_t)(vc >> 16);
+        rd += (int32_t)(vc & 0xffffu) + (int32_t)(vc >> 16);
     }
 
     // matched bases go to the reference base's counters
