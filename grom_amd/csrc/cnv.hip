@@ -947,13 +947,58 @@ __device__ bool phase_cd(Acc &a, Acc &t, const WalkIn &W, int64_t pos, const Pre
 
 __device__ __forceinline__ int cdef(uint32_t b) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : -1; }
 
-__device__ __forceinline__ int wave_incl_sum(int v) {
-    const int lane = threadIdx.x & 63;
-    for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(v, d);
-        if (lane >= d) v += t;
-    }
+// Inclusive max-scan over the wave with DPP row shifts and row broadcasts
+// (no LDS round trip): rows of 16 by Hillis-Steele (row_shr 1, 2, 4, 8), then
+// row 0 -> 1 and 2 -> 3 (row_bcast:15), then rows 0-1 -> 2, 3 (row_bcast:31).
+// Values are >= 0; lanes without a valid source keep their own value.
+__device__ __forceinline__ int dpp_max_scan(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
+}
+
+// wave_last_incl for classes e in {-1, 0, 1}: the max-scan of (lane+1)*4 + e
+// picks the latest defined lane at or below this one
+__device__ __forceinline__ int dpp_last_incl(int e, int c) {
+    const int lane = threadIdx.x & 63;
+    const int v = dpp_max_scan(e >= 0 ? ((lane + 1) << 2) | e : 0);
+    return v ? (v & 3) : c;
+}
+
+// max of non-negative doubles over the wave (their bit patterns order as
+// unsigned integers), returned to every lane
+template <int CTL, int RM>
+__device__ __forceinline__ void dpp_max_step_u64(int &hi, int &lo) {
+    const int h2 = __builtin_amdgcn_update_dpp(hi, hi, CTL, RM, 0xf, false);
+    const int l2 = __builtin_amdgcn_update_dpp(lo, lo, CTL, RM, 0xf, false);
+    const bool gt = (uint32_t)h2 > (uint32_t)hi || ((uint32_t)h2 == (uint32_t)hi && (uint32_t)l2 > (uint32_t)lo);
+    hi = gt ? h2 : hi;
+    lo = gt ? l2 : lo;
+}
+
+__device__ __forceinline__ double dpp_max_pos(double d) {
+    uint64_t u;
+    __builtin_memcpy(&u, &d, 8);
+    int hi = (int)(uint32_t)(u >> 32), lo = (int)(uint32_t)u;
+    dpp_max_step_u64<0x111, 0xf>(hi, lo);
+    dpp_max_step_u64<0x112, 0xf>(hi, lo);
+    dpp_max_step_u64<0x114, 0xf>(hi, lo);
+    dpp_max_step_u64<0x118, 0xf>(hi, lo);
+    dpp_max_step_u64<0x142, 0xa>(hi, lo);
+    dpp_max_step_u64<0x143, 0xc>(hi, lo);
+    return dbl_of((uint32_t)__builtin_amdgcn_readlane(lo, 63), (uint32_t)__builtin_amdgcn_readlane(hi, 63));
+}
+
+// inclusive count of the lanes at or below this one whose flag is set
+// (mbcnt over the ballot: no cross-lane data movement)
+__device__ __forceinline__ int wave_incl_count(bool f) {
+    const unsigned long long m = __ballot(f);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    return below + (f ? 1 : 0);
 }
 
 __device__ __forceinline__ double rl_d(double v, int k) {
@@ -968,7 +1013,7 @@ __device__ __forceinline__ int64_t rl_i64(int64_t v, int k) {
                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), k) << 32));
 }
 
-__device__ __forceinline__ double wave_max_d(double v) {
+[[maybe_unused]] __device__ __forceinline__ double wave_max_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
     return v;
 }
@@ -1057,9 +1102,9 @@ __device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
         const bool in = p < pos + ML;
         const uint32_t b = in ? W.wb[p] : 0u;
         const bool nl = in && !(b & B_LOW);
-        const int m = wave_last_incl(nl ? cdef(b) : -1, mqi);
+        const int m = dpp_last_incl(nl ? cdef(b) : -1, mqi);
         const bool ps = nl && (b & (pb0 << m));
-        const int64_t c2 = cnt2 + wave_incl_sum(ps ? 1 : 0);
+        const int64_t c2 = cnt2 + wave_incl_count(ps);
         const int64_t w = wl + lane + 1;
         const bool st = in && !ps && (2 * c2) < w;
         const unsigned long long sm = __ballot(st);
@@ -1097,10 +1142,10 @@ __device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
         const bool inend = in && p < end;
         const uint32_t b = inend ? W.wb[p] : 0u;
         const bool nl = inend && !(b & B_LOW);
-        const int m = wave_last_incl(nl ? cdef(b) : -1, mqi);
+        const int m = dpp_last_incl(nl ? cdef(b) : -1, mqi);
         const bool ps = nl && (b & (pb0 << m));
-        const int64_t c = cnt + wave_incl_sum(nl ? 1 : 0);
-        const int64_t c2 = cnt2 + wave_incl_sum(ps ? 1 : 0);
+        const int64_t c = cnt + wave_incl_count(nl);
+        const int64_t c2 = cnt2 + wave_incl_count(ps);
         const int64_t w = wl + lane + 1;
         const double v = nl ? sgn * W.sd[p] : 0.0;
         const double tj = wave_chain1(tot, v);
@@ -1116,7 +1161,7 @@ __device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
         if (gm) {
             const int jl = 63 - __clzll(gm);
             last_good = ce = p0 + jl;
-            const double mx = wave_max_d(eg ? ts : 0.0);
+            const double mx = dpp_max_pos(eg ? ts : 0.0);
             if (begin == 0) { begin = 1; stdevs = mx; }
             else if (mx > stdevs) stdevs = mx;
         }
@@ -1162,7 +1207,7 @@ __device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int6
                 const int64_t p = p0 + lane;
                 const bool in = p <= pos + L;
                 const uint32_t b = in ? W.wb[p] : 0u;
-                const int m = wave_last_incl(in ? cdef(b) : -1, mqb);
+                const int m = dpp_last_incl(in ? cdef(b) : -1, mqb);
                 const bool q = in && !(b & B_LOW) && (b & (B_W0 << m));
                 const double v = q ? sgn * W.sd[p] : 0.0;
                 const unsigned long long qm = __ballot(q);
@@ -1197,30 +1242,35 @@ __device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int6
                 const uint32_t ba = nba, bb = nbb;
                 const double za = nza, zb = nzb;
                 load(pa + 64);
-                const int mt = wave_last_incl(inl ? cdef(bb) : -1, mqb);
-                const int ml = wave_last_incl(inl ? cdef(ba) : -1, mqi);
+                const int mt = dpp_last_incl(inl ? cdef(bb) : -1, mqb);
+                const int ml = dpp_last_incl(inl ? cdef(ba) : -1, mqi);
                 const bool qt = inl && !(bb & B_LOW) && (bb & (B_W0 << mt));
                 const bool ql = inl && !(ba & B_LOW) && (ba & (B_W0 << ml));
                 const double vt = qt ? -sgn * zb : 0.0;
                 const double vl = ql ? sgn * za : 0.0;
-                const int64_t cj = cnt + wave_incl_sum((ql ? 1 : 0) - (qt ? 1 : 0));
+                const int64_t cj = cnt + wave_incl_count(ql) - wave_incl_count(qt);
                 double t = tot;
                 const double tj = wave_chain2(t, vt, vl);
                 const bool good = inl && cj > 0 && wsdL > 0 && ratio_ge_min(tj, cj * wsdL) && LOW_FRAC_OK;
                 const double ts = good ? tj / (cj * wsdL) : 0.0;
-                // the loop test of step j sees the last good step before it
-                int gi = wave_last_incl(good ? lane : -1, -1);
-                int ge = __shfl_up(gi, 1);
-                if (lane == 0) ge = -1;
-                const int64_t lgb = ge >= 0 ? pa + ge : last_good;
-                const bool cont = inl && (p - lgb) <= MAX_DIST_LAST_GOOD;
+                // the loop test of step j sees the last good step before it;
+                // no step of the round can fail it while pa + 63 is within
+                // MAX_DIST of last_good (the common case: skip the scan)
+                bool cont = inl;
+                if (pa + 63 - last_good > MAX_DIST_LAST_GOOD) {
+                    int gi = wave_last_incl(good ? lane : -1, -1);
+                    int ge = __shfl_up(gi, 1);
+                    if (lane == 0) ge = -1;
+                    const int64_t lgb = ge >= 0 ? pa + ge : last_good;
+                    cont = inl && (p - lgb) <= MAX_DIST_LAST_GOOD;
+                }
                 const unsigned long long sm = __ballot(!cont);
                 const int js = sm ? __ffsll((long long)sm) - 1 : 64;
                 const bool eg = good && lane < js;
                 const unsigned long long gm = __ballot(eg);
                 if (gm) {
                     last_good = ce = pa + (63 - __clzll(gm));
-                    const double mx = wave_max_d(eg ? ts : 0.0);
+                    const double mx = dpp_max_pos(eg ? ts : 0.0);
                     if (mx > stdevs) stdevs = mx;
                 }
                 if (js > 0) {
@@ -1241,7 +1291,7 @@ __device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int6
         const int64_t q = p - lane;
         const bool in = q > cs + ML;
         const uint32_t b = in ? W.wb[q] : 0u;
-        const int m = wave_last_incl(in ? cdef(b) : -1, mqi);
+        const int m = dpp_last_incl(in ? cdef(b) : -1, mqi);
         const unsigned long long pm = __ballot(in && (b & (pb0 << m)));
         if (!pm) {
             const int n_in = __popcll(__ballot(in));
@@ -1264,9 +1314,9 @@ __device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int6
             const bool in2 = x > cs + ML;
             const uint32_t bx = in2 ? W.wb[x] : 0u;
             const bool nl = in2 && !(bx & B_LOW);
-            const int mx = wave_last_incl(nl ? cdef(bx) : -1, mqa);
+            const int mx = dpp_last_incl(nl ? cdef(bx) : -1, mqa);
             const bool px = nl && (bx & (pb0 << mx));
-            const int64_t c3j = c3 + wave_incl_sum(nl ? 1 : 0), c2j = c2 + wave_incl_sum(px ? 1 : 0);
+            const int64_t c3j = c3 + wave_incl_count(nl), c2j = c2 + wave_incl_count(px);
             const bool st = in2 && (c3j == 0 || (c3j > 0 && 2 * c2j < c3j) || !LOW_FRAC_OK);
             const unsigned long long sm = __ballot(st);
             if (sm) {
@@ -1536,6 +1586,7 @@ __global__ __launch_bounds__(64) void k_cnv_walk(WalkIn W, const int32_t *nxt, c
                                                  uint32_t cap) {
     const int64_t k = blockIdx.x;
     if (k >= n_chunks) return;
+    if (mode == 1 && W.stats) W.stats += 5;  // counters per mode (GROM_TIMING)
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
     int64_t merge;
     if (mode == 0) {
@@ -1591,6 +1642,7 @@ __global__ __launch_bounds__(64) void k_cnv_walk_fix(WalkIn W, const int32_t *nx
                                                      int64_t chunk, int64_t x, int l, uint8_t *__restrict__ vis,
                                                      ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
                                                      uint32_t cap) {
+    if (W.stats) W.stats += 10;  // the repair walks' own counters (GROM_TIMING)
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
     int64_t merge;
     {
@@ -2675,13 +2727,13 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             KindBufs &K = S->kb[kind];
             hipStream_t st = K.st;
             int rc = GROM_OK;
-            if ((rc = grow(K.cnt, 128, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
+            if ((rc = grow(K.cnt, 256, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
             // n_calls, n_pre, n_cand, capped, n_und; walk counters from byte 64
             uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;
             WalkIn WK = WI;
             WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 64) : nullptr;
             CK(hipStreamWaitEvent(st, S->walk_in, 0));
-            if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 48, st));
+            if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 128, st));
             bool done = false;
             for (int attempt = 0; attempt < 8 && !done; attempt++) {
                 if ((rc = grow(K.nxt, 8 * (size_t)len, err, errlen)) ||
@@ -2819,8 +2871,14 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 if (tmg) {
                     uint32_t np_[3] = {0, 0, 0};
                     (void)hipMemcpy(np_, n_pre, 12, hipMemcpyDeviceToHost);
-                    unsigned long long ws[5] = {0, 0, 0, 0, 0};
-                    (void)hipMemcpy(ws, WK.stats, sizeof(ws), hipMemcpyDeviceToHost);
+                    unsigned long long wsa[15] = {0};
+                    (void)hipMemcpy(wsa, WK.stats, sizeof(wsa), hipMemcpyDeviceToHost);
+                    for (int mo = 0; mo < 3; mo++)
+                        fprintf(stderr, "cnv walk %s %s: stops %llu, wave A/B %llu, wave C/D %llu, slide rounds %llu, trim rounds %llu\n",
+                                kind == 0 ? "DEL" : "DUP", mo == 0 ? "mode 0" : mo == 1 ? "mode 1" : "repairs",
+                                wsa[5 * mo + 4], wsa[5 * mo], wsa[5 * mo + 1], wsa[5 * mo + 2], wsa[5 * mo + 3]);
+                    unsigned long long ws[5];
+                    for (int q = 0; q < 5; q++) ws[q] = wsa[q] + wsa[5 + q] + wsa[10 + q];
                     fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired, %u candidates, %u call starts (%u left to the walk); "
                             "walk stops %llu, wave A/B %llu, wave C/D %llu (%llu slide rounds, %llu trim rounds)\n",
                             kind == 0 ? "DEL" : "DUP", (long long)n_ch, (long long)n_fix, ncand, np_[0], np_[2], ws[4],
