@@ -227,7 +227,7 @@ __device__ __forceinline__ void staged_base(const uint8_t *lq8, const uint8_t *l
 // The outputs of position x (one lane per position; every lane of the
 // workgroup calls this, it has barriers): caf arrays, flush depth sums, the
 // debug counters, the SNV test (GROM.c:11096-11199) and the tile's candidate
-// run.  Shared by the gather and the scatter tile kernels.
+// run.
 __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *__restrict__ ref, const PileOut &O,
                                           const double *__restrict__ mq_tab, const double *__restrict__ hez_tab,
                                           TileTail &T_, int64_t tile, int32_t x, char rb, bool evals,
@@ -790,24 +790,6 @@ __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args 
     const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (tile >= n_tiles) return;  // whole workgroup leaves together
     scan_tile_gather<NS>(L, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
-}
-
-// the tiles listed by the scatter kernel as over its LDS event budget; the
-// grid is fixed and the count is read on the device, so no host round trip
-template <int NS>
-__global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile_list(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
-                                                       const ReadMeta *__restrict__ meta,
-                                                       const int32_t *__restrict__ tile_lo,
-                                                       const int32_t *__restrict__ tile_hi, PileOut O,
-                                                       const double *__restrict__ mq_tab,
-                                                       const double *__restrict__ hez_tab,
-                                                       const uint32_t *__restrict__ list, const uint32_t *__restrict__ n_list) {
-    __shared__ ScanLds L;
-    const uint32_t n = *n_list;
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        __syncthreads();  // the previous tile's LDS is no longer read
-        scan_tile_gather<NS>(L, (int64_t)list[i], a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
-    }
 }
 
 // ---- candidate runs in tile order: exclusive scan of run_cnt, then gather ----

@@ -150,7 +150,6 @@ __global__ void k_rmdup(int64_t n, int32_t tid, const int32_t *__restrict__ pos,
 // k_scan_tile: the tile kernel (k_scan_tile.h)
 // ---------------------------------------------------------------------------
 #include "k_scan_tile.h"
-#include "k_scan_scatter.h"
 
 // the per-tile flush sums of the pileup kernels into acc[0..1]
 __global__ __launch_bounds__(256) void k_flush_reduce(int64_t n_tiles, const unsigned long long *__restrict__ part,
@@ -226,7 +225,7 @@ struct Ctx {
     DevBuf r_pos, r_flag, r_mapq, r_mtid, r_mpos, r_isize, r_lq, r_coff, r_cig, r_boff, r_seq, r_qual, r_nid, ref;
     DevBuf r_aidx, r_aux, r_dpos, r_dlq, r_dbef;
     // scan scratch
-    DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, ovf, fpart;
+    DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, fpart;
     grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
     const char *host_ref = nullptr;    // the caller's host reference during grom_scan_chrom
     // device-resident scans: the breakpoint rows read reference bases on the
@@ -333,17 +332,6 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     }
     hipStream_t st = C.st;
     const bool timing = getenv("GROM_TIMING") != nullptr;  // per-phase host clock on stderr
-    // The pileup runs the gather kernel (k_scan_tile) on every tile.
-    // GROM_PILEUP=scatter selects the scatter formulation (k_scan_scatter,
-    // with the gather kernel redoing tiles over its LDS event budget); it is
-    // bit-exact but measured slower on MI355X.  GROM_EVCAP
-    // lowers the scatter kernel's per-tile event budget (tests use it to
-    // exercise the fallback).
-    const char *pk = getenv("GROM_PILEUP");
-    const bool gather_only = !(pk && strcmp(pk, "scatter") == 0);
-    uint32_t evcap = GROM_EVENT_CAP;
-    if (const char *ec = getenv("GROM_EVCAP")) evcap = (uint32_t)std::min<long>(std::max<long>(atol(ec), 0), GROM_EVENT_CAP);
-    uint32_t n_ovf_tiles = 0;
     const auto t_start = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -389,7 +377,6 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         (rc = ensure(C.keep, (size_t)std::max<int64_t>(n, 1))) ||
         (rc = ensure(C.meta, sizeof(ReadMeta) * (size_t)std::max<int64_t>(n, 1))) ||
         (rc = ensure(C.runb, sizeof(uint32_t) * n_tiles)) || (rc = ensure(C.runc, sizeof(uint32_t) * n_tiles)) ||
-        (rc = ensure(C.ovf, sizeof(uint32_t) * n_tiles)) ||
         (rc = ensure(C.fpart, 2 * sizeof(unsigned long long) * n_tiles)) ||
         (rc = ensure(C.segs, sizeof(uint32_t) * (size_t)((n_tiles + RUN_SEG - 1) / RUN_SEG + 1))))
         return rc;
@@ -398,7 +385,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     if (C.cands.cap >= sizeof(grom_snv_cand) * 2)
         cand_cap = std::max<uint32_t>(cand_cap, (uint32_t)(C.cands.cap / sizeof(grom_snv_cand)));
 
-    // misc layout: [0] halo (int32), [4..] n_cands, n_ovf, n_events ; [32..] flush_acc[2] ; [64..] mid acc[2]
+    // misc layout: [0] halo (int32), [4..] n_cands, status, n_events ; [32..] flush_acc[2] ; [64..] mid acc[2]
     char *misc = (char *)C.misc.p;
     int32_t *d_halo = (int32_t *)misc;
     uint32_t *d_ncand = (uint32_t *)(misc + 4);
@@ -486,26 +473,14 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         HIPCHK(hipEventRecord(C.ep0, st));
         const unsigned grid = (unsigned)(((n_tiles + 7) / 8) * 8);
         const bool few = P.min_snv <= GROM_FEW_NAME_SLOTS;
-        if (gather_only) {
-            if (few)
-                hipLaunchKernelGGL(k_scan_tile<GROM_FEW_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
-                                   (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                                   C.d_mq, C.d_hez, n_tiles);
-            else
-                hipLaunchKernelGGL(k_scan_tile<GROM_MAX_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
-                                   (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                                   C.d_mq, C.d_hez, n_tiles);
-        } else {
-            // scatter tiles; the few over the LDS event budget are redone by
-            // the gather kernel, whose grid reads their count on the device
-            hipLaunchKernelGGL(k_scan_scatter, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
+        if (few)
+            hipLaunchKernelGGL(k_scan_tile<GROM_FEW_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
                                (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                               C.d_mq, C.d_hez, n_tiles, evcap, (uint32_t *)C.ovf.p, d_status);
-            hipLaunchKernelGGL(k_scan_tile_list<GROM_MAX_NAME_SLOTS>, dim3((unsigned)std::min<int64_t>(n_tiles, 1024)), dim3(GROM_TILE), 0, st,
-                               a, ch->ref, ra, (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p,
-                               (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, (const uint32_t *)C.ovf.p,
-                               (const uint32_t *)d_status);
-        }
+                               C.d_mq, C.d_hez, n_tiles);
+        else
+            hipLaunchKernelGGL(k_scan_tile<GROM_MAX_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
+                               (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
+                               C.d_mq, C.d_hez, n_tiles);
         hipLaunchKernelGGL(k_flush_reduce, dim3(256), dim3(256), 0, st, n_tiles,
                            (const unsigned long long *)C.fpart.p, d_facc);
         HIPCHK(hipGetLastError());
@@ -514,7 +489,6 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         HIPCHK(hipMemcpyAsync(hdr, misc + 4, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         const double t_kernels = ms_since(t_start);
-        n_ovf_tiles = hdr[1];
         if (hdr[0] > cand_cap) {
             cand_cap = hdr[0] + hdr[0] / 4 + 1024;
             continue;
@@ -680,12 +654,11 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                     "grom timing %s: kernels %.3f ms, candidates ordered+copied %.3f ms (%u candidates), "
                     "breakpoint tests %.3f ms (device %.3f ms, %zu hit bases; eval %.3f, ref copy %.3f, rows %.3f), "
                     "cnv %.3f ms (device %.3f ms, %lld/%lld DEL/DUP calls, %lld rows), SNV rows (overlapped) "
-                    "joined after %.3f ms more, %u of %lld tiles to the gather kernel\n",
+                    "joined after %.3f ms more, %lld tiles\n",
                     ch->name ? ch->name : "?", t_kernels, t_snv - t_kernels, ncand, t_sv - t_snv, ms_sv,
                     n_hits, t_sv_eval - t_snv, t_sv_ref > 0 ? t_sv_ref - t_sv_eval : 0.0,
                     t_sv - (t_sv_ref > 0 ? t_sv_ref : t_sv_eval), t_cnv - t_sv, ct.ms_device, (long long)ct.del_calls,
-                    (long long)ct.dup_calls, (long long)ct.rows, t_rows - t_cnv,
-                    gather_only ? (unsigned)n_tiles : n_ovf_tiles, (long long)n_tiles);
+                    (long long)ct.dup_calls, (long long)ct.rows, t_rows - t_cnv, (long long)n_tiles);
         HIPCHK(hipEventRecord(C.e1, st));
         HIPCHK(hipEventSynchronize(C.e1));
         if (ref_copy_pending) HIPCHK(hipEventSynchronize(C.ref_ev));
@@ -832,7 +805,7 @@ void grom_dev_fini(int device) {
     (void)hipStreamSynchronize(C.st);
     DevBuf *all[] = {&C.r_pos, &C.r_flag, &C.r_mapq, &C.r_mtid, &C.r_mpos, &C.r_isize, &C.r_lq, &C.r_coff,
                      &C.r_cig, &C.r_boff, &C.r_seq, &C.r_qual, &C.r_nid, &C.ref, &C.keep, &C.meta, &C.cands2,
-                     &C.runb, &C.runc, &C.segs, &C.ovf, &C.fpart, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
+                     &C.runb, &C.runc, &C.segs, &C.fpart, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
                      &C.misc, &C.dbg, &C.r_aidx, &C.r_aux, &C.r_dpos, &C.r_dlq, &C.r_dbef};
     for (DevBuf *b : all)
         if (b->p) (void)hipFree(b->p);

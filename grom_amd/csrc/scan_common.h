@@ -11,9 +11,6 @@
 #define GROM_TILE 256
 #endif
 #define GROM_TILE_THREADS GROM_TILE
-/* per-tile LDS event capacity of the scatter kernel (mismatches, soft-clip
- * evidence); a tile over it is redone by the gather kernel */
-#define GROM_EVENT_CAP 1024
 /* read-name slots per position supported by the kernel (g_min_snv, -n);
  * the gather kernel is also built with GROM_FEW_NAME_SLOTS for -n up to that */
 #define GROM_MAX_NAME_SLOTS 8

@@ -59,16 +59,6 @@ def _names(datadir, tag):
     return sorted(f.split(".")[-2] for f in os.listdir(datadir) if f.startswith(tag + ".") and f.endswith(".cnt"))
 
 
-# the pileup has two kernels: gather (default) and scatter (GROM_PILEUP=
-# scatter), whose tiles over the LDS event budget the gather kernel redoes.
-# GROM_EVCAP shrinks that budget so most tiles take the fallback.
-KERNEL_RUNS = [
-    ("lowmapq_clip", [], {"GROM_PILEUP": "scatter"}),
-    ("lowmapq_clip", [], {"GROM_PILEUP": "scatter", "GROM_EVCAP": "4"}),
-    ("dups", ["-M"], {"GROM_PILEUP": "scatter", "GROM_EVCAP": "24"}),
-    ("three_chr", [], {"GROM_PILEUP": "scatter"}),
-    ("one_chr", ["-G", "40"], {"GROM_PILEUP": "scatter"}),
-]
 
 
 def _check_counters(datadir, case, extra, tag, env_extra=None):
@@ -113,13 +103,6 @@ def _check_counters(datadir, case, extra, tag, env_extra=None):
 @pytest.mark.parametrize("case,extra", RUNS, ids=[f"{c}{''.join(e)}" for c, e in RUNS])
 def test_counters_and_vcf_bit_exact(datadir, case, extra):
     _check_counters(datadir, case, extra, f"{case}{''.join(extra).replace('-', '_')}")
-
-
-@pytest.mark.parametrize("case,extra,env", KERNEL_RUNS,
-                         ids=[f"{c}{''.join(e)}_{'_'.join(f'{k}{v}' for k, v in n.items())}" for c, e, n in KERNEL_RUNS])
-def test_pileup_kernel_paths_bit_exact(datadir, case, extra, env):
-    tag = f"{case}{''.join(extra).replace('-', '_')}_{'_'.join(v for v in env.values())}"
-    _check_counters(datadir, case, extra, tag, env_extra=env)
 
 
 def _oracle_once(datadir, case, extra):
