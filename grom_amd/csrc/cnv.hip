@@ -2768,13 +2768,6 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     found[kind].clear();
                     continue;
                 }
-                if (ncand > pre_cap) {  // every candidate may start a call (a long region): no re-run
-                    pre_cap = ncand;
-                    if ((rc = grow(K.pre, sizeof(PreAB) * pre_cap, err, errlen)) ||
-                        (rc = grow(K.ppos, 8 * (size_t)pre_cap, err, errlen)))
-                        return rc;
-                    pre = (PreAB *)K.pre.p;
-                }
                 if (ncand) {
                     // GROM_CNV_BUDGET (tests) shrinks the precompute budgets so the
                     // walk's wave routines take the long searches; GROM_CNV_CLASSIFY=0
@@ -2807,6 +2800,13 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         pcand = und;
                         if (tmg) fprintf(stderr, "cnv classify %s: %u candidates, %u undecided (%s)\n", kind == 0 ? "DEL" : "DUP",
                                          ncand, nu, npc ? "precomputed" : "left to the walk");
+                    }
+                    if (npc > pre_cap) {  // every precomputed candidate may start a call: no re-run
+                        pre_cap = npc;
+                        if ((rc = grow(K.pre, sizeof(PreAB) * pre_cap, err, errlen)) ||
+                            (rc = grow(K.ppos, 8 * (size_t)pre_cap, err, errlen)))
+                            return rc;
+                        pre = (PreAB *)K.pre.p;
                     }
                     if (npc) {
                         const int64_t ab_cap = bud ? std::max<int64_t>(std::min<int64_t>(L, budget / npc), ML + 256) : L;

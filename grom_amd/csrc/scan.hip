@@ -579,7 +579,8 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         double ms_sv = 0, t_sv_eval = 0, t_sv_ref = 0;
         std::string sv_text, ctx_text;
         size_t n_hits = 0;
-        std::vector<SvHit> hits;
+        const SvHit *hits = nullptr;  // pinned, in base order (the SV scratch owns it)
+        size_t nh = 0;
         // the rows' INV depth sums read caf_rd/caf_low on the copy stream, so
         // the row thread never waits behind the CNV kernels on `st` (the CNV
         // path only rewrites caf_mq)
@@ -589,15 +590,15 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         Joiner sv_join{svt};
         {
             char serr[512] = {0};
-            rc = sv_evaluate(C.sv, st, P, svin, *ch, a.eval_lo, a.eval_hi, C.d_mq, C.d_hez, hits, &ms_sv, serr,
+            rc = sv_evaluate(C.sv, st, P, svin, *ch, a.eval_lo, a.eval_hi, C.d_mq, C.d_hez, &hits, &nh, &ms_sv, serr,
                              sizeof(serr));
             if (rc != GROM_OK) {
                 set_err("%s", serr);
                 return rc;
             }
-            n_hits = hits.size();
+            n_hits = nh;
             t_sv_eval = ms_since(t_start);
-            if (P.vcf == 1 && !hits.empty()) {
+            if (P.vcf == 1 && nh > 0) {
                 // the rows read reference bases (REF text, homopolymer runs):
                 // the caller's host copy when there is one, else the pinned
                 // copy made beside the pileup
@@ -610,9 +611,9 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                 t_sv_ref = ms_since(t_start);
                 // candidate lists, SV assembly and rows on a host thread while
                 // the CNV path runs on the GPU
-                svt = std::thread([&P, ch, href, &cs, &hits, &sv_text, &ctx_text] {
+                svt = std::thread([&P, ch, href, &cs, hits, nh, &sv_text, &ctx_text] {
                     SvRowsInput ri{&P, ch->name, href, ch->len, &CafSum::call, &cs};
-                    sv_rows(ri, hits, sv_text, ctx_text);
+                    sv_rows(ri, hits, nh, sv_text, ctx_text);
                 });
             }
         }

@@ -86,9 +86,11 @@ uint32_t *sv_ctx_count(const SvScratch *S);
 
 // Phase 2, after the pileup: the per-base tests at every context record;
 // the bases where one passed come back in position order.
+// the hits come back in base order in a pinned host buffer owned by S
+// (valid until the next call on S)
 int sv_evaluate(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput &in, const grom_chrom &ch,
-                int32_t eval_lo, int32_t eval_hi, const double *d_mq, const double *d_hez, std::vector<SvHit> &hits,
-                double *ms_device, char *err, size_t errlen);
+                int32_t eval_lo, int32_t eval_hi, const double *d_mq, const double *d_hez, const SvHit **hits,
+                size_t *n_hits, double *ms_device, char *err, size_t errlen);
 
 // test hooks: records of the last scan
 const grom_indel_rec *sv_indel_records(const SvScratch *S);
@@ -107,4 +109,4 @@ struct SvRowsInput {
     double (*caf_sum)(void *u, int64_t lo, int64_t hi);
     void *u;
 };
-void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string &vcf, std::string &ctx);
+void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::string &vcf, std::string &ctx);

@@ -927,7 +927,9 @@ struct Buf {
 struct SvScratch {
     Buf cnt, off, keys, vals, keys2, vals2, ev, run_pos, run_len, run_off, n_runs, tmp, sums, bits, epochs;
     Buf f_cand, f_ind, f_dbg, o_cand, o_ind, o_dbg, rec, irec_c, irec, drec;
-    Buf ctx, ctx2, ckeys, ckeys2, cvals, cvals2, n_ctx, hits, n_hits;
+    Buf ctx, ctx2, ckeys, ckeys2, cvals, cvals2, n_ctx, hits, n_hits, hits2;
+    SvHit *h_hits = nullptr;  // pinned: the hits of the last evaluation, in base order
+    size_t h_hits_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int64_t len = 0;
     uint32_t n_rec = 0, n_irec = 0, n_drec = 0, ctx_cap = 0;
@@ -955,9 +957,10 @@ void sv_scratch_free(SvScratch *s) {
     Buf *all[] = {&s->cnt, &s->off, &s->keys, &s->vals, &s->keys2, &s->vals2, &s->ev, &s->run_pos, &s->run_len,
                   &s->run_off, &s->n_runs, &s->tmp, &s->sums, &s->bits, &s->epochs, &s->f_cand, &s->f_ind, &s->f_dbg,
                   &s->o_cand, &s->o_ind, &s->o_dbg, &s->rec, &s->irec_c, &s->irec, &s->drec, &s->ctx, &s->ctx2,
-                  &s->ckeys, &s->ckeys2, &s->cvals, &s->cvals2, &s->n_ctx, &s->hits, &s->n_hits};
+                  &s->ckeys, &s->ckeys2, &s->cvals, &s->cvals2, &s->n_ctx, &s->hits, &s->n_hits, &s->hits2};
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
+    if (s->h_hits) (void)hipHostFree(s->h_hits);
     if (s->e0) (void)hipEventDestroy(s->e0);
     if (s->e1) (void)hipEventDestroy(s->e1);
     delete s;
@@ -1183,11 +1186,27 @@ int sv_prepare(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput
     return GROM_OK;
 }
 
+// (pos, slot) of each hit, and the hits gathered into base order
+__global__ void k_hit_keys(const SvHit *__restrict__ h, uint32_t n, uint32_t *__restrict__ keys,
+                           uint32_t *__restrict__ vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        keys[i] = (uint32_t)h[i].pos;
+        vals[i] = i;
+    }
+}
+__global__ void k_hit_gather(const SvHit *__restrict__ h, const uint32_t *__restrict__ idx, uint32_t n,
+                             SvHit *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = h[idx[i]];
+}
+
 int sv_evaluate(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput &in, const grom_chrom &ch,
-                int32_t eval_lo, int32_t eval_hi, const double *d_mq, const double *d_hez, std::vector<SvHit> &hits,
-                double *ms_device, char *err, size_t errlen) {
+                int32_t eval_lo, int32_t eval_hi, const double *d_mq, const double *d_hez, const SvHit **hits_out,
+                size_t *n_hits_out, double *ms_device, char *err, size_t errlen) {
     int rc;
-    hits.clear();
+    *hits_out = S->h_hits;
+    *n_hits_out = 0;
     uint32_t n_ctx = 0;
     SCHK(hipMemcpyAsync(&n_ctx, S->n_ctx.p, 4, hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
@@ -1255,11 +1274,36 @@ int sv_evaluate(SvScratch *S, hipStream_t st, const grom_params &P, const SvInpu
                 hit_cap = nh + nh / 4 + 64;
                 continue;
             }
-            hits.resize(nh);
-            if (nh) SCHK(hipMemcpy(hits.data(), S->hits.p, sizeof(SvHit) * nh, hipMemcpyDeviceToHost));
+            if (nh) {
+                // base order on the device (the lanes append in any order):
+                // sort (pos, slot) and gather, then one copy to pinned memory
+                if ((rc = sbuf(S->hits2, sizeof(SvHit) * nh, err, errlen))) return rc;
+                uint32_t *hk = (uint32_t *)S->ckeys.p, *hv = (uint32_t *)S->cvals.p;
+                uint32_t *hk2 = (uint32_t *)S->ckeys2.p, *hv2 = (uint32_t *)S->cvals2.p;  // n_ctx >= nh entries
+                hipLaunchKernelGGL(k_hit_keys, dim3((nh + 255) / 256), dim3(256), 0, st, (const SvHit *)S->hits.p, nh, hk,
+                                   hv);
+                size_t tb = 0;
+                SCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, hk, hk2, hv, hv2, (int)nh, 0, bit_hi, st));
+                if ((rc = sbuf(S->tmp, tb, err, errlen))) return rc;
+                SCHK(hipcub::DeviceRadixSort::SortPairs(S->tmp.p, tb, hk, hk2, hv, hv2, (int)nh, 0, bit_hi, st));
+                hipLaunchKernelGGL(k_hit_gather, dim3((nh + 255) / 256), dim3(256), 0, st, (const SvHit *)S->hits.p, hv2,
+                                   nh, (SvHit *)S->hits2.p);
+                SCHK(hipGetLastError());
+                if (nh > S->h_hits_cap) {
+                    if (S->h_hits) (void)hipHostFree(S->h_hits);
+                    S->h_hits = nullptr;
+                    S->h_hits_cap = 0;
+                    const size_t want = nh + nh / 4 + 1024;
+                    SCHK(hipHostMalloc((void **)&S->h_hits, sizeof(SvHit) * want, 0));
+                    S->h_hits_cap = want;
+                }
+                SCHK(hipMemcpyAsync(S->h_hits, S->hits2.p, sizeof(SvHit) * nh, hipMemcpyDeviceToHost, st));
+                SCHK(hipStreamSynchronize(st));
+            }
+            *hits_out = S->h_hits;
+            *n_hits_out = nh;
             break;
         }
-        std::sort(hits.begin(), hits.end(), [](const SvHit &a, const SvHit &b) { return a.pos < b.pos; });
     }
     SCHK(hipEventRecord(S->e1, st));
     SCHK(hipEventSynchronize(S->e1));

@@ -452,7 +452,7 @@ static bool del_dropped(const grom_params &P, const PairEnt &q, Lists &L, int sp
 
 }  // namespace
 
-void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string &vcf, std::string &ctx) {
+void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::string &vcf, std::string &ctx) {
     const grom_params &P = *in.P;
     const bool timing = getenv("GROM_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
@@ -463,7 +463,7 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
     };
     Lists L;
     L.cap = P.sv_list_len;
-    for (const SvHit &h : hits) apply_hit(P, L, h);
+    for (size_t k = 0; k < n_hits; k++) apply_hit(P, L, hits[k]);
     mark();
 
     const char *chr = in.chr_name ? in.chr_name : "";
@@ -661,6 +661,6 @@ void sv_rows(const SvRowsInput &in, const std::vector<SvHit> &hits, std::string 
                 "(%zu hits; list sizes ii %lld id %lld ins %lld dup %lld del %lld invf %lld invr %lld; "
                 "list2 del %zu)\n",
                 tm[0], tm[1] - tm[0], tm[2] - tm[1], tm[3] - tm[2], tm[4] - tm[3], tm[5] - tm[4], tm[6] - tm[5],
-                hits.size(), (long long)L.n_ii, (long long)L.n_id, (long long)L.n_ins, (long long)L.n_pr[0],
+                n_hits, (long long)L.n_ii, (long long)L.n_id, (long long)L.n_ins, (long long)L.n_pr[0],
                 (long long)L.n_pr[1], (long long)L.n_pr[2], (long long)L.n_pr[3], l2[PR_DEL].size());
 }
