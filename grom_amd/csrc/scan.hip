@@ -472,15 +472,16 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                    sv_ctx_count(C.sv), sv_ctx_cap(C.sv), want_dbg ? sv_rd_add(C.sv) : nullptr};
         HIPCHK(hipEventRecord(C.ep0, st));
         const unsigned grid = (unsigned)(((n_tiles + 7) / 8) * 8);
-        const bool few = P.min_snv <= GROM_FEW_NAME_SLOTS;
-        if (few)
-            hipLaunchKernelGGL(k_scan_tile<GROM_FEW_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
-                               (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                               C.d_mq, C.d_hez, n_tiles);
-        else
-            hipLaunchKernelGGL(k_scan_tile<GROM_MAX_NAME_SLOTS>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
-                               (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                               C.d_mq, C.d_hez, n_tiles);
+        // the build with the fewest read-name slots that holds -n (fewer
+        // slots, fewer registers: GROM.c keeps -n names per base)
+#define GROM_LAUNCH_TILE(NSL)                                                                                    \
+    hipLaunchKernelGGL(k_scan_tile<NSL>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra, (const ReadMeta *)C.meta.p, \
+                       (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, n_tiles)
+        if (P.min_snv <= GROM_FEW_NAME_SLOTS) GROM_LAUNCH_TILE(GROM_FEW_NAME_SLOTS);
+        else if (P.min_snv <= 8) GROM_LAUNCH_TILE(8);
+        else if (P.min_snv <= 16) GROM_LAUNCH_TILE(16);
+        else GROM_LAUNCH_TILE(32);
+#undef GROM_LAUNCH_TILE
         hipLaunchKernelGGL(k_flush_reduce, dim3(256), dim3(256), 0, st, n_tiles,
                            (const unsigned long long *)C.fpart.p, d_facc);
         HIPCHK(hipGetLastError());

@@ -25,6 +25,8 @@ RUNS = [
     ("one_chr", ["-p", "4", "-x", "28"]),
     ("one_chr", ["-G", "40"]),  # forces mid-scan SNV list flushes (GROM.c:11201)
     ("dups", ["-n", "6", "-a", "0.1"]),  # -n above 4: the 8-slot build of the gather kernel
+    ("dups", ["-n", "12", "-a", "0.05"]),  # the 16-slot build
+    ("c5_tetra_male", ["-n", "20", "-a", "0.05", "-p", "4"]),  # the 32-slot build at 60x
     ("indels", []),
     ("indels", ["-M"]),
     ("indels", ["-q", "10"]),
