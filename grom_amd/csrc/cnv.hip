@@ -716,18 +716,24 @@ struct Win {
     int64_t len;
     int64_t base;
     WinRegs r, nx;  // the window [base, base+64) and, already in flight, [base+64, base+128)
+    // unconditional loads from a clamped index (vis and nxt are never null):
+    // a load under a branch would be waited for at the join, so the
+    // prefetched window would not be in flight while the walk works
     __device__ void load(int64_t b, WinRegs &o) const {
-        const int64_t q = b + (int64_t)(threadIdx.x & 63);
-        const bool ok = q >= 0 && q < len;
-        o.b = ok ? wb[q] : 0u;
-        double v = ok ? sd[q] : 0.0;
+        const int64_t q0 = b + (int64_t)(threadIdx.x & 63);
+        const bool ok = q0 >= 0 && q0 < len;
+        const int64_t q = q0 < 0 ? 0 : q0 >= len ? len - 1 : q0;
+        const uint32_t bb = wb[q], vv = vis[q];
+        const double v = sd[q];
+        const int32_t n0 = nxt[q], n1 = nxt[len + q];
         uint64_t u;
         __builtin_memcpy(&u, &v, 8);
-        o.s_lo = (uint32_t)u;
-        o.s_hi = (uint32_t)(u >> 32);
-        o.v = (ok && vis) ? vis[q] : 0u;
-        o.n0 = (ok && nxt) ? nxt[q] : 0;
-        o.n1 = (ok && nxt) ? nxt[len + q] : 0;
+        o.b = ok ? bb : 0u;
+        o.s_lo = ok ? (uint32_t)u : 0u;
+        o.s_hi = ok ? (uint32_t)(u >> 32) : 0u;
+        o.v = ok ? vv : 0u;
+        o.n0 = ok ? n0 : 0;
+        o.n1 = ok ? n1 : 0;
     }
     __device__ void fill(int64_t b) {
         base = b;
@@ -947,26 +953,15 @@ __device__ bool phase_cd(Acc &a, Acc &t, const WalkIn &W, int64_t pos, const Pre
 
 __device__ __forceinline__ int cdef(uint32_t b) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : -1; }
 
-// Inclusive max-scan over the wave with DPP row shifts and row broadcasts
-// (no LDS round trip): rows of 16 by Hillis-Steele (row_shr 1, 2, 4, 8), then
-// row 0 -> 1 and 2 -> 3 (row_bcast:15), then rows 0-1 -> 2, 3 (row_bcast:31).
-// Values are >= 0; lanes without a valid source keep their own value.
-__device__ __forceinline__ int dpp_max_scan(int v) {
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return v;
-}
-
-// wave_last_incl for classes e in {-1, 0, 1}: the max-scan of (lane+1)*4 + e
-// picks the latest defined lane at or below this one
+// wave_last_incl for classes e in {-1, 0, 1}: the latest defined lane at or
+// below this one, found from two ballots (highest set bit of the defined
+// lanes up to this one) -- no cross-lane chain
 __device__ __forceinline__ int dpp_last_incl(int e, int c) {
     const int lane = threadIdx.x & 63;
-    const int v = dpp_max_scan(e >= 0 ? ((lane + 1) << 2) | e : 0);
-    return v ? (v & 3) : c;
+    const unsigned long long d = __ballot(e >= 0) & (~0ull >> (63 - lane));
+    const unsigned long long c1 = __ballot(e == 1);
+    const int j = 63 - __clzll(d);
+    return d ? (int)((c1 >> j) & 1ull) : c;
 }
 
 // max of non-negative doubles over the wave (their bit patterns order as
@@ -1021,70 +1016,46 @@ __device__ __forceinline__ int64_t rl_i64(int64_t v, int k) {
 // `tot` advanced over the lanes in order: at lane k, tot + a then (two-op
 // form) + b, where a lane without an operation contributes 0.0.  Adding 0.0
 // is exact here: tot starts at +0.0 and a sum of doubles is -0.0 only when
-// both terms are, so tot is never -0.0 and x + (+-0.0) == x.  Every lane
-// computes the same chain (the addends are broadcast from LDS, so the reads
-// run ahead of the dependent adds) and keeps the value after its own step.
-// The callers run in one-wave blocks (the walk kernels), so the block
-// barrier is the wave's.
+// both terms are, so tot is never -0.0 and x + (+-0.0) == x.
+//
+// The chain stays one IEEE operation per step in the reference's order, and
+// runs in registers: each of 63 rounds shifts the partial sums one lane up
+// (DPP wave_shr:1, lane 0 refilled with the incoming tot) and adds the lane's
+// own addend, so after round k lanes 0..k hold their exact prefix
+// ((tot + a_0) + a_1) + ... + a_lane.  No LDS, no barrier.
+// Lane 0 reads +0.0 from the shift (bound_ctrl) and its first addend is
+// tot + a_0, the chain's own first operation: +0.0 + x == x for x != -0.0,
+// and tot + a_0 is -0.0 only if tot is.
+__device__ __forceinline__ double dpp_wave_shr1(double v) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, 0x138, 0xf, 0xf, true);  // wave_shr:1
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), 0x138, 0xf, 0xf, true);
+    return dbl_of((uint32_t)lo, (uint32_t)hi);
+}
+
 __device__ __forceinline__ double wave_chain1(double &tot, double a) {
-    __shared__ double buf[64], outb[64];
-    const int lane = threadIdx.x & 63;
-    buf[lane] = a;
-    __syncthreads();
-    if (lane == 0) {  // one lane runs the dependent adds; the others wait at the barrier
-        double t = tot;
-        for (int k = 0; k < 64; k += 16) {
-            double v[16];
+    const double a0 = (threadIdx.x & 63) == 0 ? tot + a : a;
+    double t = a0;
 #pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = buf[k + j];
-            double o[16];
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                t = t + v[j];
-                o[j] = t;
-            }
-#pragma unroll
-            for (int j = 0; j < 16; j++) outb[k + j] = o[j];
-        }
-    }
-    __syncthreads();
-    const double mine = outb[lane];
-    tot = outb[63];
-    __syncthreads();
-    return mine;
+    for (int k = 1; k < 64; k++) t = dpp_wave_shr1(t) + a0;
+    tot = rl_d(t, 63);
+    return t;
 }
 
 __device__ __forceinline__ double wave_chain2(double &tot, double a, double b) {
-    // interleaved (a_k, b_k) pairs, read 4 steps at a time into registers
-    // ahead of the dependent adds
-    __shared__ double2 ab[64];
-    __shared__ double outb2[64];
-    const int lane = threadIdx.x & 63;
-    ab[lane] = make_double2(a, b);
-    __syncthreads();
-    if (lane == 0) {
-        double t = tot;
-        for (int k = 0; k < 64; k += 8) {
-            double2 v[8];
+    const double a0 = (threadIdx.x & 63) == 0 ? tot + a : a;
+    double t = a0 + b;
 #pragma unroll
-            for (int j = 0; j < 8; j++) v[j] = ab[k + j];
-            double o[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                t = t + v[j].x;
-                t = t + v[j].y;
-                o[j] = t;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) outb2[k + j] = o[j];
-        }
-    }
-    __syncthreads();
-    const double mine = outb2[lane];
-    tot = outb2[63];
-    __syncthreads();
-    return mine;
+    for (int k = 1; k < 64; k++) t = (dpp_wave_shr1(t) + a0) + b;
+    tot = rl_d(t, 63);
+    return t;
 }
+
+// the round-by-round loops below read the next round's inputs before the
+// current round's serial work: unconditional loads from a clamped index (a
+// load under a branch would be waited for at the join)
+__device__ __forceinline__ int64_t clamp_pos(const WalkIn &W, int64_t q) { return q < 0 ? 0 : q >= W.len ? W.len - 1 : q; }
 
 // phases A and B (phase_ab) for the wave; every lane returns the same record
 template <int KIND>
@@ -1097,10 +1068,12 @@ __device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
     int64_t ce = 0, last_good = 0, temp_pos = pos, wl = 0, cnt = 0, cnt2 = 0;
     double stdevs = 0.0, tot = 0.0;
     // phase A: the first ML bases (GROM.c:19370-19400)
+    uint32_t nb = W.wb[clamp_pos(W, pos + lane)];
     for (int64_t p0 = pos; p0 < pos + ML && !stop; p0 += 64) {
         const int64_t p = p0 + lane;
         const bool in = p < pos + ML;
-        const uint32_t b = in ? W.wb[p] : 0u;
+        const uint32_t b = in ? nb : 0u;
+        nb = W.wb[clamp_pos(W, p + 64)];
         const bool nl = in && !(b & B_LOW);
         const int m = dpp_last_incl(nl ? cdef(b) : -1, mqi);
         const bool ps = nl && (b & (pb0 << m));
@@ -1120,12 +1093,17 @@ __device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
     }
     if (stop == 0) {
         cnt = ML;
+        uint32_t nb2 = W.wb[clamp_pos(W, pos + lane)];
+        double nz2 = W.sd[clamp_pos(W, pos + lane)];
         for (int64_t p0 = pos; p0 < pos + ML; p0 += 64) {
             const int64_t p = p0 + lane;
             const bool in = p < pos + ML;
-            const uint32_t b = in ? W.wb[p] : 0u;
+            const uint32_t b = in ? nb2 : 0u;
+            const double z = nz2;
+            nb2 = W.wb[clamp_pos(W, p + 64)];
+            nz2 = W.sd[clamp_pos(W, p + 64)];
             cnt -= __popcll(__ballot(in && (b & B_LOW)));
-            const double v = in ? sgn * W.sd[p] : 0.0;
+            const double v = in ? sgn * z : 0.0;
             wave_chain1(tot, v);
         }
     }
@@ -1135,21 +1113,29 @@ __device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
         ce = pos + ML;
         stdevs = tot / (cnt * W.wsd[ML]);
     }
-    // phase B: extension to L (GROM.c:19405-19470)
+    // phase B: extension to L (GROM.c:19405-19470); the next round's wsd
+    // index assumes this round does not stop (if it does, the loop ends)
+    uint32_t nb3 = W.wb[clamp_pos(W, pos + ML + lane)];
+    double nz3 = W.sd[clamp_pos(W, pos + ML + lane)];
+    double nw3 = W.wsd[min<int64_t>(wl + lane + 1, L)];
     for (int64_t p0 = pos + ML; p0 < pos + L && !stop; p0 += 64) {
         const int64_t p = p0 + lane;
         const bool in = p < pos + L;
         const bool inend = in && p < end;
-        const uint32_t b = inend ? W.wb[p] : 0u;
+        const uint32_t b = inend ? nb3 : 0u;
+        const double z = nz3, wsdn = nw3;
+        nb3 = W.wb[clamp_pos(W, p + 64)];
+        nz3 = W.sd[clamp_pos(W, p + 64)];
+        nw3 = W.wsd[min<int64_t>(wl + 64 + lane + 1, L)];
         const bool nl = inend && !(b & B_LOW);
         const int m = dpp_last_incl(nl ? cdef(b) : -1, mqi);
         const bool ps = nl && (b & (pb0 << m));
         const int64_t c = cnt + wave_incl_count(nl);
         const int64_t c2 = cnt2 + wave_incl_count(ps);
         const int64_t w = wl + lane + 1;
-        const double v = nl ? sgn * W.sd[p] : 0.0;
+        const double v = nl ? sgn * z : 0.0;
         const double tj = wave_chain1(tot, v);
-        const double wsdw = in ? W.wsd[w] : 0.0;
+        const double wsdw = in ? wsdn : 0.0;
         const bool good = ps && wsdw > 0 && ratio_ge_min(tj, c * wsdw) && LOW_FRAC_OK;
         const double ts = good ? tj / (c * wsdw) : 0.0;
         const bool st = in && (!inend || (!ps && (2 * c2) < w));
@@ -1187,105 +1173,163 @@ __device__ PreAB phase_ab_wave(const WalkIn &W, int64_t pos, int mqi) {
     return r;
 }
 
-// phases C and D (phase_cd) for the wave
+// phases C and D (phase_cd) for the wave, in three parts so that the walk can
+// pause a long slide (SlideState holds everything the slide carries) and
+// resume it later, possibly from another kernel
+struct SlideState {
+    int64_t pos, pa, cnt, last_good, ce;
+    double tot, stdevs;
+    int32_t mqi, mqb, m, sliding;  // m: the walk's class at the call base; sliding: phase C not finished
+};
+
+// phase C's first window [pos+1, pos+L] (GROM.c:19480-19490)
 template <int KIND>
-__device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int64_t &ce_out, double &stdevs_out) {
+__device__ SlideState slide_begin(const WalkIn &W, int64_t pos, const PreAB &r, int m) {
     const int lane = threadIdx.x & 63;
-    const int64_t L = W.L, ML = W.min_len, cs = pos;
-    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    const int64_t L = W.L;
     const double sgn = KIND == 0 ? 1.0 : -1.0;
     const double wsdL = W.wsd[L];
-    int64_t ce = r.ce, last_good = r.last_good, cnt = 0;
-    double stdevs = r.stdevs, tot = 0.0;
-    int mqi = r.mqi;
-    if (r.stop == 0) {
-        int64_t pa = pos + L;
-        int mqb = mqi;
-        if (pa < W.len && (pa - last_good) <= MAX_DIST_LAST_GOOD) {
-            // the first window [pos+1, pos+L] (GROM.c:19480-19490)
-            for (int64_t p0 = pos + 1; p0 <= pos + L; p0 += 64) {
-                const int64_t p = p0 + lane;
-                const bool in = p <= pos + L;
-                const uint32_t b = in ? W.wb[p] : 0u;
-                const int m = dpp_last_incl(in ? cdef(b) : -1, mqb);
-                const bool q = in && !(b & B_LOW) && (b & (B_W0 << m));
-                const double v = q ? sgn * W.sd[p] : 0.0;
-                const unsigned long long qm = __ballot(q);
-                cnt += __popcll(qm);
-                wave_chain1(tot, v);
-                mqb = __builtin_amdgcn_readlane(m, (int)min<int64_t>(63, pos + L - p0));
-            }
-            if (cnt > 0 && wsdL > 0 && ratio_ge_min(tot, cnt * wsdL) && LOW_FRAC_OK) {
-                last_good = pa;
-                ce = pa;
-                const double ts = tot / (cnt * wsdL);
-                if (ts > stdevs) stdevs = ts;
-            }
-            pa += 1;
-            // the slide (GROM.c:19492-19545), 64 steps per round; the next
-            // round's inputs are loaded while this one runs (the rounds are a
-            // serial chain, so load latency would otherwise add up)
-            uint32_t nba, nbb;
-            double nza, nzb;
-            auto load = [&](int64_t at) {
-                const int64_t q = at + lane;
-                const bool ok = q < W.len;
-                nba = ok ? W.wb[q] : 0u;
-                nbb = ok ? W.wb[q - L] : 0u;
-                nza = ok ? W.sd[q] : 0.0;
-                nzb = ok ? W.sd[q - L] : 0.0;
-            };
-            load(pa);
-            for (;;) {
-                const int64_t p = pa + lane;
-                const bool inl = p < W.len;
-                const uint32_t ba = nba, bb = nbb;
-                const double za = nza, zb = nzb;
-                load(pa + 64);
-                const int mt = dpp_last_incl(inl ? cdef(bb) : -1, mqb);
-                const int ml = dpp_last_incl(inl ? cdef(ba) : -1, mqi);
-                const bool qt = inl && !(bb & B_LOW) && (bb & (B_W0 << mt));
-                const bool ql = inl && !(ba & B_LOW) && (ba & (B_W0 << ml));
-                const double vt = qt ? -sgn * zb : 0.0;
-                const double vl = ql ? sgn * za : 0.0;
-                const int64_t cj = cnt + wave_incl_count(ql) - wave_incl_count(qt);
-                double t = tot;
-                const double tj = wave_chain2(t, vt, vl);
-                const bool good = inl && cj > 0 && wsdL > 0 && ratio_ge_min(tj, cj * wsdL) && LOW_FRAC_OK;
-                const double ts = good ? tj / (cj * wsdL) : 0.0;
-                // the loop test of step j sees the last good step before it;
-                // no step of the round can fail it while pa + 63 is within
-                // MAX_DIST of last_good (the common case: skip the scan)
-                bool cont = inl;
-                if (pa + 63 - last_good > MAX_DIST_LAST_GOOD) {
-                    int gi = wave_last_incl(good ? lane : -1, -1);
-                    int ge = __shfl_up(gi, 1);
-                    if (lane == 0) ge = -1;
-                    const int64_t lgb = ge >= 0 ? pa + ge : last_good;
-                    cont = inl && (p - lgb) <= MAX_DIST_LAST_GOOD;
-                }
-                const unsigned long long sm = __ballot(!cont);
-                const int js = sm ? __ffsll((long long)sm) - 1 : 64;
-                const bool eg = good && lane < js;
-                const unsigned long long gm = __ballot(eg);
-                if (gm) {
-                    last_good = ce = pa + (63 - __clzll(gm));
-                    const double mx = dpp_max_pos(eg ? ts : 0.0);
-                    if (mx > stdevs) stdevs = mx;
-                }
-                if (js > 0) {
-                    tot = rl_d(tj, js - 1);
-                    cnt = rl_i64(cj, js - 1);
-                    mqi = __builtin_amdgcn_readlane(ml, js - 1);
-                    mqb = __builtin_amdgcn_readlane(mt, js - 1);
-                }
-                pa += js;
-                if (W.stats && lane == 0) atomicAdd(W.stats + 2, 1ull);
-                if (js < 64) break;
-            }
-        }
+    SlideState s;
+    s.pos = pos;
+    s.ce = r.ce;
+    s.last_good = r.last_good;
+    s.cnt = 0;
+    s.stdevs = r.stdevs;
+    s.tot = 0.0;
+    s.mqi = r.mqi;
+    s.mqb = r.mqi;
+    s.m = m;
+    s.sliding = 0;
+    s.pa = pos + L;
+    if (r.stop != 0 || !(s.pa < W.len && (s.pa - s.last_good) <= MAX_DIST_LAST_GOOD)) return s;
+    uint32_t nb = W.wb[clamp_pos(W, pos + 1 + lane)];
+    double nz = W.sd[clamp_pos(W, pos + 1 + lane)];
+    for (int64_t p0 = pos + 1; p0 <= pos + L; p0 += 64) {
+        const int64_t p = p0 + lane;
+        const bool in = p <= pos + L;
+        const uint32_t b = in ? nb : 0u;
+        const double z = nz;
+        nb = W.wb[clamp_pos(W, p + 64)];
+        nz = W.sd[clamp_pos(W, p + 64)];
+        const int mm = dpp_last_incl(in ? cdef(b) : -1, s.mqb);
+        const bool q = in && !(b & B_LOW) && (b & (B_W0 << mm));
+        const double v = q ? sgn * z : 0.0;
+        s.cnt += __popcll(__ballot(q));
+        wave_chain1(s.tot, v);
+        s.mqb = __builtin_amdgcn_readlane(mm, (int)min<int64_t>(63, pos + L - p0));
     }
-    // phase D: trim the end back (GROM.c:19550-19600)
+    if (s.cnt > 0 && wsdL > 0 && ratio_ge_min(s.tot, s.cnt * wsdL) && LOW_FRAC_OK) {
+        s.last_good = s.pa;
+        s.ce = s.pa;
+        const double ts = s.tot / (s.cnt * wsdL);
+        if (ts > s.stdevs) s.stdevs = ts;
+    }
+    s.pa += 1;
+    s.sliding = 1;
+    return s;
+}
+
+// the slide (GROM.c:19492-19545), 64 steps per round; the next round's
+// inputs are loaded while this one runs (the rounds are a serial chain, so
+// load latency would otherwise add up).  Stops before a round that would
+// start at or past `cap` and returns false (s then resumes exactly there).
+template <int KIND>
+__device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
+    if (!s.sliding) return true;
+    const int lane = threadIdx.x & 63;
+    const int64_t L = W.L;
+    const double sgn = KIND == 0 ? 1.0 : -1.0;
+    const double wsdL = W.wsd[L];
+    int64_t pa = s.pa, cnt = s.cnt, last_good = s.last_good, ce = s.ce;
+    double tot = s.tot;
+    // the largest good ratio per lane; max is exact and order-free, so the
+    // wave's maximum is taken once, when the slide ends or pauses
+    double lmax = 0.0;
+    int mqi = s.mqi, mqb = s.mqb;
+    uint32_t nba, nbb;
+    double nza, nzb;
+    // unconditional loads from a clamped index (q - L >= 0 here): a load
+    // under a branch makes the compiler wait for it at the join, which
+    // would put a memory latency into every round
+    auto load = [&](int64_t at) {
+        const int64_t q0 = at + lane;
+        const bool ok = q0 < W.len;
+        const int64_t q = ok ? q0 : W.len - 1;
+        const uint32_t a = W.wb[q], b = W.wb[q - L];
+        const double za = W.sd[q], zb = W.sd[q - L];
+        nba = ok ? a : 0u;
+        nbb = ok ? b : 0u;
+        nza = ok ? za : 0.0;
+        nzb = ok ? zb : 0.0;
+    };
+    load(pa);
+    bool finished = true;
+    for (;;) {
+        if (pa >= cap) { finished = false; break; }
+        const int64_t p = pa + lane;
+        const bool inl = p < W.len;
+        const uint32_t ba = nba, bb = nbb;
+        const double za = nza, zb = nzb;
+        load(pa + 64);
+        const int mt = dpp_last_incl(inl ? cdef(bb) : -1, mqb);
+        const int ml = dpp_last_incl(inl ? cdef(ba) : -1, mqi);
+        const bool qt = inl && !(bb & B_LOW) && (bb & (B_W0 << mt));
+        const bool ql = inl && !(ba & B_LOW) && (ba & (B_W0 << ml));
+        const double vt = qt ? -sgn * zb : 0.0;
+        const double vl = ql ? sgn * za : 0.0;
+        const int64_t cj = cnt + wave_incl_count(ql) - wave_incl_count(qt);
+        double t = tot;
+        const double tj = wave_chain2(t, vt, vl);
+        const bool good = inl && cj > 0 && wsdL > 0 && ratio_ge_min(tj, cj * wsdL) && LOW_FRAC_OK;
+        const double ts = good ? tj / (cj * wsdL) : 0.0;
+        // the loop test of step j sees the last good step before it; no
+        // step of the round can fail it while pa + 63 is within MAX_DIST of
+        // last_good (the common case: skip the scan)
+        bool cont = inl;
+        if (pa + 63 - last_good > MAX_DIST_LAST_GOOD) {
+            int gi = wave_last_incl(good ? lane : -1, -1);
+            int ge = __shfl_up(gi, 1);
+            if (lane == 0) ge = -1;
+            const int64_t lgb = ge >= 0 ? pa + ge : last_good;
+            cont = inl && (p - lgb) <= MAX_DIST_LAST_GOOD;
+        }
+        const unsigned long long sm = __ballot(!cont);
+        const int js = sm ? __ffsll((long long)sm) - 1 : 64;
+        const bool eg = good && lane < js;
+        const unsigned long long gm = __ballot(eg);
+        if (gm) last_good = ce = pa + (63 - __clzll(gm));
+        lmax = (eg && ts > lmax) ? ts : lmax;
+        if (js > 0) {
+            tot = rl_d(tj, js - 1);
+            cnt = rl_i64(cj, js - 1);
+            mqi = __builtin_amdgcn_readlane(ml, js - 1);
+            mqb = __builtin_amdgcn_readlane(mt, js - 1);
+        }
+        pa += js;
+        if (W.stats && lane == 0) atomicAdd(W.stats + 2, 1ull);
+        if (js < 64) break;
+    }
+    s.pa = pa;
+    s.cnt = cnt;
+    s.last_good = last_good;
+    s.ce = ce;
+    s.tot = tot;
+    const double mx = dpp_max_pos(lmax);  // ratios are >= 3 > 0; lanes without one hold 0
+    if (mx > s.stdevs) s.stdevs = mx;
+    s.mqi = mqi;
+    s.mqb = mqb;
+    s.sliding = finished ? 0 : 1;
+    return finished;
+}
+
+// phase D: trim the end back (GROM.c:19550-19600)
+template <int KIND>
+__device__ void trim_end(const WalkIn &W, const SlideState &s, int64_t &ce_out, double &stdevs_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ML = W.min_len, cs = s.pos;
+    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
+    int64_t ce = s.ce;
+    int mqi = s.mqi;
     int64_t p = ce;
     while (p > cs + ML) {
         const int64_t q = p - lane;
@@ -1336,7 +1380,14 @@ __device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int6
         if (W.stats && lane == 0) atomicAdd(W.stats + 3, 1ull);
     }
     ce_out = ce;
-    stdevs_out = stdevs;
+    stdevs_out = s.stdevs;
+}
+
+template <int KIND>
+__device__ void phase_cd_wave(const WalkIn &W, int64_t pos, const PreAB &r, int64_t &ce_out, double &stdevs_out) {
+    SlideState s = slide_begin<KIND>(W, pos, r, 0);
+    slide_run<KIND>(W, s, INT64_MAX);
+    trim_end<KIND>(W, s, ce_out, stdevs_out);
 }
 
 struct GAcc {  // direct loads (one lane per base)
@@ -1447,19 +1498,18 @@ template <int KIND>
 struct Walk {
     WalkIn W;
     Win c;
-    Win t;  // second window: the trailing edge (pa - L) of the phase-C slide
     const int32_t *nxt;
     const PreAB *pre;
+    // vis: the marks an earlier walk left (merge checks), or null; the window
+    // then reads the bit words in its place (any readable bytes: the marks
+    // are only looked at with merge checks on)
     __device__ Walk(const WalkIn &w, const uint8_t *vis, const int32_t *nx, const PreAB *pr) : W(w), nxt(nx), pre(pr) {
         c.wb = w.wb;
         c.sd = w.sd;
-        c.vis = vis;
+        c.vis = vis ? vis : (const uint8_t *)w.wb;
         c.nxt = nx;
         c.len = w.len;
         c.base = INT64_MIN / 4;
-        t = c;
-        t.vis = nullptr;
-        t.nxt = nullptr;
     }
     __device__ __forceinline__ bool pass(uint32_t b, int m) const {
         return (b & ((KIND == 0 ? B_DEL0 : B_DUP0) << m)) != 0;
@@ -1476,8 +1526,10 @@ struct Walk {
     // the reference's `if` body at a base that passes the threshold: phases A
     // and B come precomputed; a call is completed here (phase C: the sliding
     // extension past L, phase D: trimming the end).  Returns the position the
-    // walk continues from (before its `pos += 1`).
-    __device__ int64_t block(int64_t pos, int mqi, int32_t n, CallRec &call, bool &is_call) {
+    // walk continues from (before its `pos += 1`), or -1 when the slide
+    // reached `cap` and paused (its state in *ps).
+    __device__ int64_t block(int64_t pos, int mqi, int32_t n, CallRec &call, bool &is_call, int64_t cap,
+                             SlideState *ps) {
         PreAB r;
         if (n == NXT_UNDECIDED) {  // phases A/B were not precomputed (long region): the wave runs them
             if (W.stats && (threadIdx.x & 63) == 0) atomicAdd(W.stats + 0, 1ull);
@@ -1496,7 +1548,13 @@ struct Walk {
             sdv = r.stdevs_final;
         } else {
             if (W.stats && (threadIdx.x & 63) == 0) atomicAdd(W.stats + 1, 1ull);
-            phase_cd_wave<KIND>(W, pos, r, ce, sdv);
+            SlideState s = slide_begin<KIND>(W, pos, r, mqi);
+            if (!slide_run<KIND>(W, s, cap)) {
+                *ps = s;
+                is_call = false;
+                return -1;
+            }
+            trim_end<KIND>(W, s, ce, sdv);
         }
         call.p = pos;
         call.ce = ce;
@@ -1510,7 +1568,7 @@ struct ChunkState {
     int64_t x2;  // W2/W3 exit position (NOMERGE / redone chunks)
     int32_t l1, l2, status, pad;
 };
-enum { ST_MERGED = 0, ST_NOMERGE = 1, ST_PASSTHRU = 2, ST_FIRST = 3 };
+enum { ST_MERGED = 0, ST_NOMERGE = 1, ST_PASSTHRU = 2, ST_FIRST = 3, ST_PENDING = 4 };
 
 __device__ __forceinline__ void emit_call(const CallRec &c, int m, CallRec *calls, uint32_t *n_calls, uint32_t cap) {
     if ((threadIdx.x & 63) == 0) {
@@ -1529,10 +1587,13 @@ __device__ __forceinline__ void emit_call(const CallRec &c, int m, CallRec *call
 // passes (or, with merge_check, whose mark from an earlier walk equals its
 // class -- from there both walks are identical).  Marks are stored
 // coalesced; calls are completed serially (Walk::block).  Returns the exit
-// position; *merge = the merge base or -1.
+// position; *merge = the merge base or -1.  With a `pend` record, a call
+// whose slide reaches `slide_cap` pauses the walk: the slide state goes to
+// *pend, *paused is set and the call base is returned.
 template <int KIND>
 __device__ int64_t walk_run(Walk<KIND> &w, int64_t pos, int &last, int64_t lim, uint8_t *vis_out, bool merge_check,
-                            int64_t *merge, CallRec *calls, uint32_t *n_calls, uint32_t cap, bool emit) {
+                            int64_t *merge, CallRec *calls, uint32_t *n_calls, uint32_t cap, bool emit,
+                            int64_t slide_cap = INT64_MAX, SlideState *pend = nullptr, bool *paused = nullptr) {
     const int lane = threadIdx.x & 63;
     *merge = -1;
     while (pos < lim) {
@@ -1567,7 +1628,14 @@ __device__ int64_t walk_run(Walk<KIND> &w, int64_t pos, int &last, int64_t lim, 
         if (w.W.stats && lane == 0) atomicAdd(w.W.stats + 4, 1ull);
         CallRec c;
         bool is_call = false;
-        pos = w.block(pos, last, n, c, is_call);
+        SlideState sst;
+        const int64_t nx = w.block(pos, last, n, c, is_call, pend ? slide_cap : INT64_MAX, &sst);
+        if (nx < 0) {
+            if (lane == 0) *pend = sst;
+            *paused = true;
+            return pos;
+        }
+        pos = nx;
         if (is_call && emit) emit_call(c, last, calls, n_calls, cap);
         pos += 1;
     }
@@ -1582,8 +1650,8 @@ __device__ int64_t walk_run(Walk<KIND> &w, int64_t pos, int &last, int64_t lim, 
 template <int KIND>
 __global__ __launch_bounds__(64) void k_cnv_walk(WalkIn W, const int32_t *nxt, const PreAB *pre, int mode,
                                                  int64_t n_chunks, int64_t chunk, uint8_t *__restrict__ vis,
-                                                 ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
-                                                 uint32_t cap) {
+                                                 ChunkState *__restrict__ cs, SlideState *pend, CallRec *calls,
+                                                 uint32_t *n_calls, uint32_t cap) {
     const int64_t k = blockIdx.x;
     if (k >= n_chunks) return;
     if (mode == 1 && W.stats) W.stats += 5;  // counters per mode (GROM_TIMING)
@@ -1592,11 +1660,13 @@ __global__ __launch_bounds__(64) void k_cnv_walk(WalkIn W, const int32_t *nxt, c
     if (mode == 0) {
         Walk<KIND> w(W, nullptr, nxt, pre);
         int last = 0;  // exact for chunk 0 (GROM.c:19366-19367), a guess elsewhere
-        const int64_t pos = walk_run<KIND>(w, c0, last, c1, vis, false, &merge, calls, n_calls, cap, true);
+        bool paused = false;
+        const int64_t pos = walk_run<KIND>(w, c0, last, c1, vis, false, &merge, calls, n_calls, cap, true,
+                                           c1 + chunk, pend + k, &paused);
         if ((threadIdx.x & 63) == 0) {
             cs[k].x1 = pos;
             cs[k].l1 = last;
-            cs[k].status = k == 0 ? ST_FIRST : ST_MERGED;
+            cs[k].status = paused ? ST_PENDING : k == 0 ? ST_FIRST : ST_MERGED;
         }
         return;
     }
@@ -1629,6 +1699,54 @@ __global__ __launch_bounds__(64) void k_cnv_walk(WalkIn W, const int32_t *nxt, c
             cs[k].x2 = pos;
             cs[k].l2 = last;
         }
+    }
+}
+
+// Paused slides.  A speculative chunk that starts inside a long copy-number
+// region finds a call there whose slide runs to the region's end; every chunk
+// of the region would slide to the same end, of which only the first one's
+// walk is on the true path.  So mode 0 pauses a slide that passes the next
+// chunk (ST_PENDING, state in pend[k]), and the host resumes, round by round,
+// only the pending chunks whose predecessor has a known exit that does not
+// jump over them (the others take that exit: the true walk passes them).
+// The resumed walk finishes the call, emits it and walks on to the chunk's
+// end as mode 0 would (it may pause again at a later call).
+template <int KIND>
+__global__ __launch_bounds__(64) void k_cnv_walk_resume(WalkIn W, const int32_t *nxt, const PreAB *pre,
+                                                        const int32_t *__restrict__ list, int64_t chunk,
+                                                        uint8_t *__restrict__ vis, ChunkState *__restrict__ cs,
+                                                        SlideState *pend, CallRec *calls, uint32_t *n_calls,
+                                                        uint32_t cap) {
+    const int64_t k = list[blockIdx.x];
+    const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
+    if (W.stats) W.stats += 15;  // the resumed walks' own counters (GROM_TIMING)
+    SlideState s = pend[k];
+    __syncthreads();  // every lane has read the record before lane 0 may write a new one
+    const int64_t pa0 = s.pa;
+    const uint64_t t0 = W.stats ? wall_clock64() : 0;
+    slide_run<KIND>(W, s, INT64_MAX);
+    if (W.stats && (threadIdx.x & 63) == 0) {  // the longest resumed slide: steps, wall-clock ticks
+        atomicMax(W.stats + 5, (unsigned long long)(s.pa - pa0));  // slots 20, 21 of the counters
+        atomicMax(W.stats + 6, (unsigned long long)(wall_clock64() - t0));
+    }
+    int64_t ce;
+    double sdv;
+    trim_end<KIND>(W, s, ce, sdv);
+    CallRec c;
+    c.p = s.pos;
+    c.ce = ce;
+    c.stdevs = sdv;
+    emit_call(c, s.m, calls, n_calls, cap);
+    Walk<KIND> w(W, nullptr, nxt, pre);
+    int last = s.m;
+    int64_t merge;
+    bool paused = false;
+    const int64_t pos = walk_run<KIND>(w, ce + 1, last, c1, vis, false, &merge, calls, n_calls, cap, true,
+                                       c1 + chunk, pend + k, &paused);
+    if ((threadIdx.x & 63) == 0) {
+        cs[k].x1 = pos;
+        cs[k].l1 = last;
+        cs[k].status = paused ? ST_PENDING : k == 0 ? ST_FIRST : ST_MERGED;
     }
 }
 
@@ -1895,7 +2013,7 @@ struct Buf {
 // independent (GROM.c:19359-20020 runs them one after the other over the same
 // inputs), so they run concurrently, each driven by its own host thread
 struct KindBufs {
-    Buf nxt, pre, prepos, ppos, calls, ok, tiles, vis, cnt, und, skip;
+    Buf nxt, pre, prepos, ppos, calls, ok, tiles, vis, cnt, und, skip, pend, plist;
     hipStream_t st = nullptr;
 };
 
@@ -2106,7 +2224,7 @@ void cnv_scratch_free(CnvScratch *S) {
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
     for (KindBufs &K : S->kb) {
-        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und, &K.skip};
+        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und, &K.skip, &K.pend, &K.plist};
         for (Buf *b : kall)
             if (b->p) (void)hipFree(b->p);
         if (K.st) (void)hipStreamDestroy(K.st);
@@ -2213,7 +2331,10 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         return GROM_E_OVERFLOW;
     }
     std::vector<RepeatRec> reps(hnrep);
-    if (hnrep) CK(hipMemcpy(reps.data(), S->rep.p, sizeof(RepeatRec) * hnrep, hipMemcpyDeviceToHost));
+    if (hnrep) {
+        CK(hipMemcpyAsync(reps.data(), S->rep.p, sizeof(RepeatRec) * hnrep, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+    }
     std::sort(reps.begin(), reps.end(), [](const RepeatRec &a, const RepeatRec &b) { return a.start < b.start; });
 
     // chromosome depth mean over ACGT-rich bases, GROM.c:16645-16660: a double
@@ -2733,7 +2854,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             WalkIn WK = WI;
             WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 64) : nullptr;
             CK(hipStreamWaitEvent(st, S->walk_in, 0));
-            if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 128, st));
+            if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 176, st));
             bool done = false;
             for (int attempt = 0; attempt < 8 && !done; attempt++) {
                 if ((rc = grow(K.nxt, 8 * (size_t)len, err, errlen)) ||
@@ -2742,7 +2863,9 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     (rc = grow(K.ppos, 8 * (size_t)pre_cap, err, errlen)) ||
                     (rc = grow(K.calls, sizeof(CallRec) * call_cap, err, errlen)) ||
                     (rc = grow(K.ok, call_cap, err, errlen)) ||
-                    (rc = grow(K.tiles, sizeof(ChunkState) * n_ch, err, errlen)))
+                    (rc = grow(K.tiles, sizeof(ChunkState) * n_ch, err, errlen)) ||
+                    (rc = grow(K.pend, sizeof(SlideState) * n_ch, err, errlen)) ||
+                    (rc = grow(K.plist, 4 * (size_t)n_ch, err, errlen)))
                     return rc;
                 ChunkState *dcs = (ChunkState *)K.tiles.p;
                 CallRec *dcalls = (CallRec *)K.calls.p;
@@ -2829,15 +2952,53 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                     }
                 }
                 const unsigned gch = (unsigned)n_ch;  // one wave per chunk
-                if (kind == 0) {
-                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                } else {
-                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, dcalls, n_calls, call_cap);
-                }
+                SlideState *pend = (SlideState *)K.pend.p;
+                if (kind == 0)
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, pend, dcalls, n_calls, call_cap);
+                else
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 0, n_ch, WALK_CHUNK, vis, dcs, pend, dcalls, n_calls, call_cap);
                 CK(hipGetLastError());
                 std::vector<ChunkState> hcs(n_ch);
+                // paused slides (k_cnv_walk_resume): resume, round by round, the
+                // pending chunks whose predecessor's exit is known and lands in
+                // them; a pending chunk that exit jumps over takes that exit
+                std::vector<int32_t> plist;
+                int n_rounds = 0;
+                for (;;) {
+                    CK(hipMemcpyAsync(hcs.data(), dcs, sizeof(ChunkState) * n_ch, hipMemcpyDeviceToHost, st));
+                    CK(hipStreamSynchronize(st));
+                    plist.clear();
+                    bool covered = false;
+                    for (int64_t k = 0; k < n_ch; k++) {
+                        if (hcs[k].status != ST_PENDING) continue;
+                        if (k > 0 && hcs[k - 1].status == ST_PENDING) continue;
+                        const int64_t c1 = std::min<int64_t>(WK.end, WK.start + (k + 1) * WALK_CHUNK);
+                        if (k > 0 && hcs[k - 1].x1 >= c1) {
+                            hcs[k].x1 = hcs[k - 1].x1;
+                            hcs[k].l1 = hcs[k - 1].l1;
+                            hcs[k].status = ST_MERGED;
+                            covered = true;
+                        } else {
+                            plist.push_back((int32_t)k);
+                        }
+                    }
+                    if (covered) CK(hipMemcpyAsync(dcs, hcs.data(), sizeof(ChunkState) * n_ch, hipMemcpyHostToDevice, st));
+                    if (plist.empty()) break;
+                    n_rounds++;
+                    CK(hipMemcpyAsync(K.plist.p, plist.data(), 4 * plist.size(), hipMemcpyHostToDevice, st));
+                    const int32_t *dl = (const int32_t *)K.plist.p;
+                    if (kind == 0)
+                        hipLaunchKernelGGL(k_cnv_walk_resume<0>, dim3((unsigned)plist.size()), dim3(64), 0, st, WK, nxt, pre, dl, WALK_CHUNK, vis, dcs, pend, dcalls, n_calls, call_cap);
+                    else
+                        hipLaunchKernelGGL(k_cnv_walk_resume<1>, dim3((unsigned)plist.size()), dim3(64), 0, st, WK, nxt, pre, dl, WALK_CHUNK, vis, dcs, pend, dcalls, n_calls, call_cap);
+                    CK(hipGetLastError());
+                }
+                if (tmg) fprintf(stderr, "cnv walk %s: %d resume rounds\n", kind == 0 ? "DEL" : "DUP", n_rounds);
+                if (kind == 0)
+                    hipLaunchKernelGGL(k_cnv_walk<0>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, pend, dcalls, n_calls, call_cap);
+                else
+                    hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, pend, dcalls, n_calls, call_cap);
+                CK(hipGetLastError());
                 CK(hipMemcpyAsync(hcs.data(), dcs, sizeof(ChunkState) * n_ch, hipMemcpyDeviceToHost, st));
                 CK(hipStreamSynchronize(st));
                 std::vector<uint8_t> skipped((size_t)n_ch, 0);
@@ -2871,14 +3032,16 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 if (tmg) {
                     uint32_t np_[3] = {0, 0, 0};
                     (void)hipMemcpy(np_, n_pre, 12, hipMemcpyDeviceToHost);
-                    unsigned long long wsa[15] = {0};
+                    unsigned long long wsa[22] = {0};
                     (void)hipMemcpy(wsa, WK.stats, sizeof(wsa), hipMemcpyDeviceToHost);
-                    for (int mo = 0; mo < 3; mo++)
+                    for (int mo = 0; mo < 4; mo++)
                         fprintf(stderr, "cnv walk %s %s: stops %llu, wave A/B %llu, wave C/D %llu, slide rounds %llu, trim rounds %llu\n",
-                                kind == 0 ? "DEL" : "DUP", mo == 0 ? "mode 0" : mo == 1 ? "mode 1" : "repairs",
+                                kind == 0 ? "DEL" : "DUP", mo == 0 ? "mode 0" : mo == 1 ? "mode 1" : mo == 2 ? "repairs" : "resumed",
                                 wsa[5 * mo + 4], wsa[5 * mo], wsa[5 * mo + 1], wsa[5 * mo + 2], wsa[5 * mo + 3]);
+                    fprintf(stderr, "cnv walk %s: longest resumed slide %llu steps in %llu wall-clock ticks\n",
+                            kind == 0 ? "DEL" : "DUP", wsa[20], wsa[21]);
                     unsigned long long ws[5];
-                    for (int q = 0; q < 5; q++) ws[q] = wsa[q] + wsa[5 + q] + wsa[10 + q];
+                    for (int q = 0; q < 5; q++) ws[q] = wsa[q] + wsa[5 + q] + wsa[10 + q] + wsa[15 + q];
                     fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired, %u candidates, %u call starts (%u left to the walk); "
                             "walk stops %llu, wave A/B %llu, wave C/D %llu (%llu slide rounds, %llu trim rounds)\n",
                             kind == 0 ? "DEL" : "DUP", (long long)n_ch, (long long)n_fix, ncand, np_[0], np_[2], ws[4],
