@@ -122,6 +122,9 @@ _SIGS = {
     "grom_params_set_insert": (None, [C.POINTER(Params), C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "grom_out_free": (None, [C.POINTER(Out)]),
     "grom_fmt_selftest": (C.c_int64, [C.c_int64, C.c_uint64]),
+    "grom_bai_build": (C.c_int, [C.c_char_p]),
+    "grom_bai_summary": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
+    "grom_bai_selftest": (C.c_int64, [C.c_char_p, C.c_int64, C.c_uint64, C.POINTER(C.c_int64)]),
     "grom_upload": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Chrom), C.POINTER(Reads)]),
     "grom_synth_batch": (C.c_void_p, [C.c_int64, C.c_double, C.c_int32, C.c_double, C.c_double, C.c_uint64,
                                       C.POINTER(Params)]),

@@ -225,7 +225,9 @@ static int bgzf_next_block(bgzf_reader *r) {
     if (r->mt) return bgzf_mt_next(r);
     int clen = 0;
     uint32_t isize = 0;
+    r->blk_coff = r->next_coff;
     const int rc = read_cblock(r->fp, r->cbuf, &clen, &isize);
+    r->next_coff = (int64_t)ftell(r->fp);
     if (rc == 0) { r->eof = 1; return 0; }
     if (rc < 0) return -1;
     const int n = inflate_block(r->cbuf, clen, isize, r->blk);
@@ -482,6 +484,20 @@ int bai_write_minimal(const char *bam_path, int32_t n_ref) {
     return fclose(f);
 }
 
+int bai_loads(const char *bam_path) {
+    char path[4096];
+    bai_index idx;
+    snprintf(path, sizeof(path), "%s.bai", bam_path);
+    if (access(path, R_OK) != 0) {
+        size_t n = strlen(bam_path);
+        if (n <= 4 || strcmp(bam_path + n - 4, ".bam") != 0) return 0;
+        snprintf(path, sizeof(path), "%.*s.bai", (int)(n - 4), bam_path);
+    }
+    if (bai_load(path, &idx) != 0) return 0;
+    bai_free(&idx);
+    return 1;
+}
+
 int bai_exists(const char *bam_path) {
     char path[4096];
     snprintf(path, sizeof(path), "%s.bai", bam_path);
@@ -492,4 +508,343 @@ int bai_exists(const char *bam_path) {
         if (access(path, R_OK) == 0) return 1;
     }
     return 0;
+}
+
+/* ---------------- virtual offsets and the BAI index ---------------- */
+
+int64_t bgzf_tell(const bgzf_reader *r) {
+    if (r->mt) return -1;
+    if (r->blk_off >= r->blk_len) return r->next_coff << 16;
+    return (r->blk_coff << 16) | r->blk_off;
+}
+
+int bgzf_seek(bgzf_reader *r, int64_t voff) {
+    if (r->mt) return -1;
+    const int64_t coff = voff >> 16;
+    const int uoff = (int)(voff & 0xffff);
+    if (fseek(r->fp, (long)coff, SEEK_SET) != 0) return -1;
+    r->next_coff = coff;
+    r->blk_len = r->blk_off = 0;
+    r->eof = 0;
+    if (uoff == 0) return 0;  /* the block is read on demand */
+    if (bgzf_next_block(r) != 1 || uoff > r->blk_len) return -1;
+    r->blk_off = uoff;
+    return 0;
+}
+
+int32_t bam_end_pos(const bam_rec *b) {
+    int32_t len = 0;
+    if (!(b->flag & 4)) {
+        const uint32_t *c = bam_cigar(b);
+        for (int i = 0; i < b->n_cigar; i++) {
+            const int op = c[i] & 15;
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) len += (int32_t)(c[i] >> 4);
+        }
+    }
+    return b->pos + (len > 0 ? len : 1);
+}
+
+/* growable per-reference index under construction */
+typedef struct {
+    uint32_t bin;
+    int32_t n, cap;
+    bai_chunk *c;
+} bin_acc;
+typedef struct {
+    bin_acc *bins;
+    int32_t n_bins, cap_bins;
+    uint64_t *lin;
+    int32_t n_lin;
+    uint64_t off_beg, off_end, n_mapped, n_unmapped;
+    int any;
+} ref_acc;
+
+static bin_acc *acc_bin(ref_acc *R, uint32_t bin) {
+    for (int i = R->n_bins - 1; i >= 0; i--)  /* bins recur close together in sorted input */
+        if (R->bins[i].bin == bin) return &R->bins[i];
+    if (R->n_bins == R->cap_bins) {
+        R->cap_bins = R->cap_bins ? 2 * R->cap_bins : 64;
+        R->bins = (bin_acc *)realloc(R->bins, sizeof(bin_acc) * R->cap_bins);
+    }
+    bin_acc *b = &R->bins[R->n_bins++];
+    memset(b, 0, sizeof(*b));
+    b->bin = bin;
+    return b;
+}
+
+static void acc_chunk(ref_acc *R, uint32_t bin, uint64_t beg, uint64_t end) {
+    bin_acc *b = acc_bin(R, bin);
+    if (b->n > 0 && b->c[b->n - 1].end >> 16 == beg >> 16) {  /* adjacent within a block: extend */
+        if (end > b->c[b->n - 1].end) b->c[b->n - 1].end = end;
+        return;
+    }
+    if (b->n == b->cap) {
+        b->cap = b->cap ? 2 * b->cap : 4;
+        b->c = (bai_chunk *)realloc(b->c, sizeof(bai_chunk) * b->cap);
+    }
+    b->c[b->n].beg = beg;
+    b->c[b->n].end = end;
+    b->n++;
+}
+
+static int cmp_bin_acc(const void *a, const void *b) {
+    const uint32_t x = ((const bin_acc *)a)->bin, y = ((const bin_acc *)b)->bin;
+    return x < y ? -1 : x > y;
+}
+
+static void put32(FILE *f, uint32_t v) {
+    unsigned char b[4];
+    wr32(b, v);
+    fwrite(b, 1, 4, f);
+}
+static void put64(FILE *f, uint64_t v) {
+    put32(f, (uint32_t)v);
+    put32(f, (uint32_t)(v >> 32));
+}
+
+int bai_build(const char *bam_path) {
+    bgzf_reader r;
+    bam_hdr h;
+    if (bgzf_open_read(&r, bam_path) != 0 || bam_read_header(&r, &h) != 0) return -1;
+    ref_acc *R = (ref_acc *)calloc(h.n_ref > 0 ? h.n_ref : 1, sizeof(ref_acc));
+    bam_rec b;
+    memset(&b, 0, sizeof(b));
+    uint64_t n_no_coor = 0;
+    int rc = 0, last_tid = -1;
+    int32_t last_pos = -1;
+    int64_t off = bgzf_tell(&r);
+    /* the current run of records with one bin (a chunk is flushed when it ends) */
+    int run_tid = -1;
+    uint32_t run_bin = 0;
+    uint64_t run_beg = 0;
+    for (;;) {
+        const int k = bam_read_rec(&r, &b);
+        if (k < 0) { rc = -1; break; }
+        const int64_t end_off = bgzf_tell(&r);
+        if (k == 0) break;
+        if (b.tid < 0) {  /* unplaced reads sort last */
+            n_no_coor++;
+            off = end_off;
+            continue;
+        }
+        if (b.tid >= h.n_ref || b.tid < last_tid || (b.tid == last_tid && b.pos < last_pos)) { rc = -1; break; }
+        if (b.tid != last_tid) last_pos = -1;
+        last_tid = b.tid;
+        last_pos = b.pos;
+        ref_acc *A = &R[b.tid];
+        const int32_t beg = b.pos < 0 ? 0 : b.pos, end = bam_end_pos(&b);
+        const uint32_t bin = (uint32_t)bam_reg2bin(beg, end);
+        if (run_tid >= 0 && (run_tid != b.tid || run_bin != bin)) acc_chunk(&R[run_tid], run_bin, run_beg, (uint64_t)off);
+        if (run_tid != b.tid || run_bin != bin) {
+            run_tid = b.tid;
+            run_bin = bin;
+            run_beg = (uint64_t)off;
+        }
+        /* linear index: the first record overlapping each 16 kb window */
+        const int w0 = beg >> 14, w1 = (end - 1) >> 14;
+        if (w1 >= A->n_lin) {
+            A->lin = (uint64_t *)realloc(A->lin, sizeof(uint64_t) * (w1 + 1));
+            for (int w = A->n_lin; w <= w1; w++) A->lin[w] = UINT64_MAX;
+            A->n_lin = w1 + 1;
+        }
+        for (int w = w0; w <= w1; w++)
+            if (A->lin[w] == UINT64_MAX) A->lin[w] = (uint64_t)off;
+        if (!A->any) A->off_beg = (uint64_t)off;
+        A->any = 1;
+        A->off_end = (uint64_t)end_off;
+        if (b.flag & 4) A->n_unmapped++;
+        else A->n_mapped++;
+        off = end_off;
+    }
+    if (rc == 0 && run_tid >= 0) acc_chunk(&R[run_tid], run_bin, run_beg, (uint64_t)off);
+    bam_free_rec(&b);
+    bgzf_close_read(&r);
+    if (rc == 0) {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s.bai", bam_path);
+        FILE *f = fopen(path, "wb");
+        if (!f) rc = -1;
+        else {
+            fwrite("BAI\1", 1, 4, f);
+            put32(f, (uint32_t)h.n_ref);
+            for (int t = 0; t < h.n_ref; t++) {
+                ref_acc *A = &R[t];
+                qsort(A->bins, A->n_bins, sizeof(bin_acc), cmp_bin_acc);
+                put32(f, (uint32_t)(A->n_bins + (A->any ? 1 : 0)));
+                for (int i = 0; i < A->n_bins; i++) {
+                    put32(f, A->bins[i].bin);
+                    put32(f, (uint32_t)A->bins[i].n);
+                    for (int c = 0; c < A->bins[i].n; c++) {
+                        put64(f, A->bins[i].c[c].beg);
+                        put64(f, A->bins[i].c[c].end);
+                    }
+                }
+                if (A->any) {  /* pseudo-bin 37450: offset span, mapped/unmapped counts */
+                    put32(f, 37450u);
+                    put32(f, 2u);
+                    put64(f, A->off_beg);
+                    put64(f, A->off_end);
+                    put64(f, A->n_mapped);
+                    put64(f, A->n_unmapped);
+                }
+                /* empty windows take the offset of the window before them
+                 * (a smaller offset only makes a query read more) */
+                uint64_t prev = A->n_lin > 0 && A->lin[0] != UINT64_MAX ? A->lin[0] : 0;
+                for (int w = 0; w < A->n_lin; w++) {
+                    if (A->lin[w] == UINT64_MAX) A->lin[w] = prev;
+                    prev = A->lin[w];
+                }
+                put32(f, (uint32_t)A->n_lin);
+                for (int w = 0; w < A->n_lin; w++) put64(f, A->lin[w]);
+            }
+            put64(f, n_no_coor);
+            if (fclose(f) != 0) rc = -1;
+        }
+    }
+    for (int t = 0; t < h.n_ref; t++) {
+        for (int i = 0; i < R[t].n_bins; i++) free(R[t].bins[i].c);
+        free(R[t].bins);
+        free(R[t].lin);
+    }
+    free(R);
+    bam_free_header(&h);
+    return rc;
+}
+
+static int get32(FILE *f, uint32_t *v) {
+    unsigned char b[4];
+    if (fread(b, 1, 4, f) != 4) return -1;
+    *v = rd32(b);
+    return 0;
+}
+static int get64(FILE *f, uint64_t *v) {
+    uint32_t lo, hi;
+    if (get32(f, &lo) || get32(f, &hi)) return -1;
+    *v = ((uint64_t)hi << 32) | lo;
+    return 0;
+}
+
+void bai_free(bai_index *idx) {
+    for (int t = 0; t < idx->n_ref; t++) {
+        for (int i = 0; i < idx->ref[t].n_bin; i++) free(idx->ref[t].bin[i].chunk);
+        free(idx->ref[t].bin);
+        free(idx->ref[t].ioff);
+    }
+    free(idx->ref);
+    memset(idx, 0, sizeof(*idx));
+}
+
+int bai_load(const char *bai_path, bai_index *idx) {
+    memset(idx, 0, sizeof(*idx));
+    FILE *f = fopen(bai_path, "rb");
+    if (!f) return -1;
+    char magic[4];
+    uint32_t u;
+    int rc = -1;
+    if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "BAI\1", 4) != 0 || get32(f, &u) || u > (1u << 24)) goto out;
+    idx->n_ref = (int32_t)u;
+    idx->ref = (bai_ref *)calloc(idx->n_ref ? idx->n_ref : 1, sizeof(bai_ref));
+    for (int t = 0; t < idx->n_ref; t++) {
+        bai_ref *R = &idx->ref[t];
+        if (get32(f, &u) || u > (1u << 20)) goto out;
+        R->bin = (bai_bin *)calloc(u ? u : 1, sizeof(bai_bin));
+        R->n_bin = (int32_t)u;
+        for (int i = 0; i < R->n_bin; i++) {
+            uint32_t nc;
+            if (get32(f, &R->bin[i].bin) || get32(f, &nc) || nc > (1u << 26)) goto out;
+            R->bin[i].chunk = (bai_chunk *)malloc(sizeof(bai_chunk) * (nc ? nc : 1));
+            R->bin[i].n_chunk = (int32_t)nc;
+            for (uint32_t c = 0; c < nc; c++)
+                if (get64(f, &R->bin[i].chunk[c].beg) || get64(f, &R->bin[i].chunk[c].end)) goto out;
+        }
+        if (get32(f, &u) || u > (1u << 20)) goto out;
+        R->ioff = (uint64_t *)malloc(sizeof(uint64_t) * (u ? u : 1));
+        R->n_intv = (int32_t)u;
+        for (int w = 0; w < R->n_intv; w++)
+            if (get64(f, &R->ioff[w])) goto out;
+    }
+    idx->has_no_coor = get64(f, &idx->n_no_coor) == 0;
+    rc = 0;
+out:
+    fclose(f);
+    if (rc) bai_free(idx);
+    return rc;
+}
+
+static int cmp_chunk(const void *a, const void *b) {
+    const uint64_t x = ((const bai_chunk *)a)->beg, y = ((const bai_chunk *)b)->beg;
+    return x < y ? -1 : x > y;
+}
+
+int bai_query(const bai_index *idx, int tid, int beg, int end, bai_chunk **out) {
+    *out = NULL;
+    if (tid < 0 || tid >= idx->n_ref || end <= beg) return 0;
+    if (beg < 0) beg = 0;
+    const bai_ref *R = &idx->ref[tid];
+    /* reg2bins (SAM v1 section 5.3): the bins of every level overlapping [beg, end) */
+    uint32_t want[4682 + 8];
+    int nw = 0;
+    const int e = end - 1;
+    want[nw++] = 0;
+    for (int k = 1 + (beg >> 26); k <= 1 + (e >> 26); k++) want[nw++] = (uint32_t)k;
+    for (int k = 9 + (beg >> 23); k <= 9 + (e >> 23); k++) want[nw++] = (uint32_t)k;
+    for (int k = 73 + (beg >> 20); k <= 73 + (e >> 20); k++) want[nw++] = (uint32_t)k;
+    for (int k = 585 + (beg >> 17); k <= 585 + (e >> 17); k++) want[nw++] = (uint32_t)k;
+    for (int k = 4681 + (beg >> 14); k <= 4681 + (e >> 14) && nw < (int)(sizeof(want) / sizeof(want[0])); k++)
+        want[nw++] = (uint32_t)k;
+    const uint64_t min_off = R->n_intv > 0 ? R->ioff[(beg >> 14) < R->n_intv ? (beg >> 14) : R->n_intv - 1] : 0;
+    int n = 0, cap = 16;
+    bai_chunk *c = (bai_chunk *)malloc(sizeof(bai_chunk) * cap);
+    for (int i = 0; i < R->n_bin; i++) {
+        const uint32_t bn = R->bin[i].bin;
+        if (bn == 37450u) continue;
+        int hit = 0;
+        for (int w = 0; w < nw && !hit; w++) hit = want[w] == bn;
+        if (!hit) continue;
+        for (int k = 0; k < R->bin[i].n_chunk; k++) {
+            if (R->bin[i].chunk[k].end <= min_off) continue;
+            if (n == cap) {
+                cap *= 2;
+                c = (bai_chunk *)realloc(c, sizeof(bai_chunk) * cap);
+            }
+            c[n++] = R->bin[i].chunk[k];
+        }
+    }
+    qsort(c, n, sizeof(bai_chunk), cmp_chunk);
+    int m = 0;
+    for (int i = 0; i < n; i++) {
+        if (m > 0 && c[i].beg <= c[m - 1].end) {
+            if (c[i].end > c[m - 1].end) c[m - 1].end = c[i].end;
+        } else {
+            c[m++] = c[i];
+        }
+    }
+    *out = c;
+    return m;
+}
+
+long bam_fetch(bgzf_reader *r, const bai_index *idx, int tid, int beg, int end,
+               void (*visit)(void *ctx, const bam_rec *b), void *ctx) {
+    bai_chunk *c = NULL;
+    const int n = bai_query(idx, tid, beg, end, &c);
+    if (n < 0) return -1;
+    bam_rec b;
+    memset(&b, 0, sizeof(b));
+    long seen = 0;
+    int rc = 0;
+    for (int i = 0; i < n && rc == 0; i++) {
+        if (bgzf_seek(r, (int64_t)c[i].beg) != 0) { rc = -1; break; }
+        while ((uint64_t)bgzf_tell(r) < c[i].end) {
+            const int k = bam_read_rec(r, &b);
+            if (k <= 0) { rc = k; break; }
+            if (b.tid != tid || b.pos >= end) { i = n; break; }  /* sorted: nothing later overlaps */
+            if (bam_end_pos(&b) > beg) {
+                visit(ctx, &b);
+                seen++;
+            }
+        }
+    }
+    free(c);
+    bam_free_rec(&b);
+    return rc < 0 ? -1 : seen;
 }

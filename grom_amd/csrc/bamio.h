@@ -53,6 +53,8 @@ typedef struct bgzf_reader {
     unsigned char *cbuf;    /* compressed block */
     int eof;
     struct bgzf_mt *mt;     /* multi-threaded inflate (bgzf_set_threads), or NULL */
+    int64_t blk_coff;       /* file offset of the current block (serial mode) */
+    int64_t next_coff;      /* file offset of the block after it */
 } bgzf_reader;
 
 typedef struct bgzf_writer {
@@ -118,10 +120,57 @@ int bam_write_rec(bgzf_writer *w, const bam_rec *b);
 /* htslib bam_aux_get: pointer to the type byte of tag, or NULL */
 uint8_t *bam_aux_find(const bam_rec *b, const char tag[2]);
 
+/* virtual offset (compressed block offset << 16 | offset in the block) of
+ * the next byte, canonical at block ends as htslib's bgzf_tell; -1 with
+ * threaded inflate */
+int64_t bgzf_tell(const bgzf_reader *r);
+/* position the (serial) reader at a virtual offset: 0, or -1 */
+int bgzf_seek(bgzf_reader *r, int64_t voff);
+
 /* writes <bam>.bai with n_ref empty references (enough for GROM's serial mode) */
 int bai_write_minimal(const char *bam_path, int32_t n_ref);
+
+/* ---- BAI (SAM v1 section 5.2): the binning index with 16 kb linear index ---- */
+typedef struct { uint64_t beg, end; } bai_chunk;
+typedef struct {
+    uint32_t bin;
+    int32_t n_chunk;
+    bai_chunk *chunk;
+} bai_bin;
+typedef struct {
+    int32_t n_bin;
+    bai_bin *bin;
+    int32_t n_intv;
+    uint64_t *ioff;
+} bai_ref;
+typedef struct {
+    int32_t n_ref;
+    bai_ref *ref;
+    int has_no_coor;
+    uint64_t n_no_coor;
+} bai_index;
+
+/* index a coordinate-sorted BAM as samtools index does: per reference the
+ * bins with their chunks (adjacent chunks merged), the pseudo-bin 37450
+ * (offset span, mapped/unmapped counts), the linear index, then the count of
+ * unplaced reads; writes <bam>.bai.  0, or -1 (unsorted input, I/O error). */
+int bai_build(const char *bam_path);
+/* parse an index file; 0, or -1 */
+int bai_load(const char *bai_path, bai_index *idx);
+void bai_free(bai_index *idx);
+/* the chunks that can hold records of tid overlapping [beg, end) (0-based),
+ * sorted and merged; *out is malloc'd.  Returns the count, or -1. */
+int bai_query(const bai_index *idx, int tid, int beg, int end, bai_chunk **out);
+/* visit every record of tid overlapping [beg, end) through the index, in
+ * file order; returns the number visited, or -1 */
+long bam_fetch(bgzf_reader *r, const bai_index *idx, int tid, int beg, int end,
+               void (*visit)(void *ctx, const bam_rec *b), void *ctx);
+/* reference span of a record from its CIGAR (M/D/N/=/X), bam_endpos */
+int32_t bam_end_pos(const bam_rec *b);
 /* 1 if an index file for bam_path exists (<bam>.bai or <stem>.bai) */
 int bai_exists(const char *bam_path);
+/* 1 if that index file parses (bam_index_load's test, GROM.c:22128-22138) */
+int bai_loads(const char *bam_path);
 
 /* reg2bin from the SAM spec (0-based, end exclusive) */
 int bam_reg2bin(int beg, int end);

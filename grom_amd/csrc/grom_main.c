@@ -504,14 +504,14 @@ int grom_cli_main(int argc, char **argv) {
         printf("\nCould not open %s\n", bam_name);
         return 1;
     }
-    if (!bai_exists(bam_name)) { printf("Could not open BAM indexing file\n"); return 1; }
+    if (!bai_loads(bam_name)) { printf("Could not open BAM indexing file\n"); return 1; }
     if (!out_name) { printf("ERROR: No output file specified.\n"); return 1; }
     FILE *probe = fopen(out_name, "w");
     if (!probe) { printf("\nCould not open %s\n", out_name); return 1; }
     fclose(probe);
     if (!fasta_name) { printf("ERROR: No reference file specified.\n"); return 1; }
     grom_fasta fa;
-    if (grom_fasta_open(&fa, fasta_name) != 0) { printf("\nCould not open %s\n", fasta_name); return 1; }
+    if (grom_fasta_open_cached(&fa, fasta_name) != 0) { printf("\nCould not open %s\n", fasta_name); return 1; }
 
     /* tables (read_binom_tables, GROM.c:22234) */
     size_t tn = (size_t)(GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);

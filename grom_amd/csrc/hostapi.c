@@ -227,3 +227,103 @@ void grom_batch_release(grom_batch_handle *h) {
     free(h->lq);
     free(h);
 }
+
+/* ---------------- BAM index entry points ---------------- */
+int grom_bai_build(const char *bam_path) { return bai_build(bam_path) == 0 ? 0 : GROM_E_ARG; }
+
+int grom_bai_summary(const char *bai_path, int64_t out[5]) {
+    bai_index idx;
+    if (bai_load(bai_path, &idx) != 0) return GROM_E_ARG;
+    int64_t bins = 0, chunks = 0, intv = 0;
+    for (int t = 0; t < idx.n_ref; t++) {
+        bins += idx.ref[t].n_bin;
+        intv += idx.ref[t].n_intv;
+        for (int i = 0; i < idx.ref[t].n_bin; i++) chunks += idx.ref[t].bin[i].n_chunk;
+    }
+    out[0] = idx.n_ref;
+    out[1] = bins;
+    out[2] = chunks;
+    out[3] = intv;
+    out[4] = idx.has_no_coor ? (int64_t)idx.n_no_coor : -1;
+    bai_free(&idx);
+    return 0;
+}
+
+typedef struct {
+    uint64_t hash;
+    int64_t n;
+} fetch_acc;
+
+/* an order-free digest of a record set: sum of per-record hashes */
+static uint64_t rec_hash(const bam_rec *b) {
+    uint64_t h = 1469598103934665603ull ^ ((uint64_t)(uint32_t)b->tid << 32 | (uint32_t)b->pos);
+    for (int i = 0; i < b->data_len; i++) h = (h ^ b->data[i]) * 1099511628211ull;
+    return h ^ ((uint64_t)b->flag << 48);
+}
+
+static void fetch_visit(void *ctx, const bam_rec *b) {
+    fetch_acc *a = (fetch_acc *)ctx;
+    a->hash += rec_hash(b);
+    a->n++;
+}
+
+int64_t grom_bai_selftest(const char *bam_path, int64_t n_queries, uint64_t seed, int64_t *visited) {
+    char bai[4096];
+    snprintf(bai, sizeof(bai), "%s.bai", bam_path);
+    bai_index idx;
+    if (bai_load(bai, &idx) != 0) return GROM_E_ARG;
+    bgzf_reader r;
+    bam_hdr h;
+    if (bgzf_open_read(&r, bam_path) != 0 || bam_read_header(&r, &h) != 0) {
+        bai_free(&idx);
+        return GROM_E_ARG;
+    }
+    /* every placed record once: tid, pos, end, hash */
+    int64_t n = 0, cap = 1 << 16;
+    int32_t *tp = (int32_t *)malloc(sizeof(int32_t) * 3 * cap);
+    uint64_t *hs = (uint64_t *)malloc(sizeof(uint64_t) * cap);
+    bam_rec b;
+    memset(&b, 0, sizeof(b));
+    while (bam_read_rec(&r, &b) == 1) {
+        if (b.tid < 0) continue;
+        if (n == cap) {
+            cap *= 2;
+            tp = (int32_t *)realloc(tp, sizeof(int32_t) * 3 * cap);
+            hs = (uint64_t *)realloc(hs, sizeof(uint64_t) * cap);
+        }
+        tp[3 * n] = b.tid;
+        tp[3 * n + 1] = b.pos;
+        tp[3 * n + 2] = bam_end_pos(&b);
+        hs[n] = rec_hash(&b);
+        n++;
+    }
+    uint64_t s = seed ? seed : 1;
+    int64_t bad = 0, seen = 0;
+    for (int64_t q = 0; q < n_queries && h.n_ref > 0; q++) {
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        const int tid = (int)(s % (uint64_t)h.n_ref);
+        const int32_t L = h.ref_len[tid] > 0 ? h.ref_len[tid] : 1;
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        const int32_t beg = (int32_t)(s % (uint64_t)L);
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        const int32_t span = (q % 4 == 0) ? 1 : (int32_t)(1 + s % (q % 4 == 1 ? 200u : q % 4 == 2 ? 40000u : 3000000u));
+        const int32_t end = beg + span;
+        fetch_acc want = {0, 0}, got = {0, 0};
+        for (int64_t i = 0; i < n; i++)
+            if (tp[3 * i] == tid && tp[3 * i + 1] < end && tp[3 * i + 2] > beg) {
+                want.hash += hs[i];
+                want.n++;
+            }
+        if (bam_fetch(&r, &idx, tid, beg, end, fetch_visit, &got) < 0) { bad = GROM_E_ARG; break; }
+        seen += got.n;
+        if (got.n != want.n || got.hash != want.hash) bad++;
+    }
+    if (visited) *visited = seen;
+    bam_free_rec(&b);
+    free(tp);
+    free(hs);
+    bam_free_header(&h);
+    bgzf_close_read(&r);
+    bai_free(&idx);
+    return bad;
+}

@@ -10,6 +10,86 @@
 
 /* ---------------- FASTA ---------------- */
 
+static int fasta_grow(grom_fasta *f, int want, int *cap) {
+    if (want <= *cap) return 0;
+    int c = *cap ? *cap : 64;
+    while (c < want) c *= 2;
+    void *a = realloc(f->names, sizeof(*f->names) * c), *b = realloc(f->name_len, sizeof(int) * c),
+         *d = realloc(f->file_pos, sizeof(long) * c), *e = realloc(f->len, sizeof(long) * c);
+    if (a) f->names = a;
+    if (b) f->name_len = b;
+    if (d) f->file_pos = d;
+    if (e) f->len = e;
+    if (!a || !b || !d || !e) return -1;
+    *cap = c;
+    return 0;
+}
+
+/* load_genome_info (GROM.c:1047-1081): "<n> <mappable>" then per chromosome
+ * "<i> <name_len> <file_pos> <len> <name>"; a line that does not parse or is
+ * out of order drops the whole table (n = 0) but, as in the reference, keeps
+ * the mappable length already read from the first line. */
+static void fasta_load_info(grom_fasta *f, const char *path, int *cap) {
+    char name[4096];
+    snprintf(name, sizeof(name), "%s.info", path);
+    FILE *fp = fopen(name, "r");
+    if (!fp) return;
+    int n = 0;
+    long mappable = 0;
+    if (fscanf(fp, "%d %ld\n", &n, &mappable) == 2) {
+        f->mappable = mappable;
+        if (n < 0 || n > GROM_MAX_CHR_NAMES || fasta_grow(f, n, cap) != 0) n = 0;
+        for (int i = 0; i < n; i++) {
+            int idx = -1, nl = 0;
+            long pos = 0, len = 0;
+            char nm[GROM_MAX_CHR_NAME_LEN];
+            if (fscanf(fp, "%d %d %ld %ld %49s\n", &idx, &nl, &pos, &len, nm) != 5 || idx != i) {
+                n = 0;
+                break;
+            }
+            memset(f->names[i], 0, GROM_MAX_CHR_NAME_LEN);
+            memcpy(f->names[i], nm, strlen(nm));
+            f->name_len[i] = nl;
+            f->file_pos[i] = pos;
+            f->len[i] = len;
+        }
+        f->n = n;
+    }
+    fclose(fp);
+}
+
+/* save_genome_info (GROM.c:1028-1045) */
+static void fasta_save_info(const grom_fasta *f, const char *path) {
+    char name[4096];
+    snprintf(name, sizeof(name), "%s.info", path);
+    FILE *fp = fopen(name, "w");
+    if (!fp) return;
+    fprintf(fp, "%d %ld\n", f->n, f->mappable);
+    for (int i = 0; i < f->n; i++) fprintf(fp, "%d %d %ld %ld %s\n", i, f->name_len[i], f->file_pos[i], f->len[i], f->names[i]);
+    fclose(fp);
+}
+
+int grom_fasta_open_cached(grom_fasta *f, const char *path) {
+    memset(f, 0, sizeof(*f));
+    f->fh = fopen(path, "r");
+    if (!f->fh) return -1;
+    int cap = 0;
+    fasta_load_info(f, path, &cap);
+    if (f->n > 0) return 0;
+    /* GROM.c:22308-22311: no usable cache -> index the FASTA and save it
+     * (find_genome_length adds to a mappable length a failed load kept) */
+    const long kept = f->mappable;
+    fclose(f->fh);
+    free(f->names);
+    free(f->name_len);
+    free(f->file_pos);
+    free(f->len);
+    if (grom_fasta_open(f, path) != 0) return -1;
+    f->mappable += kept;
+    fasta_save_info(f, path);
+    return 0;
+}
+
 int grom_fasta_open(grom_fasta *f, const char *path) {
     memset(f, 0, sizeof(*f));
     f->fh = fopen(path, "r");

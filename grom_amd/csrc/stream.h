@@ -39,6 +39,9 @@ typedef struct grom_fasta {
 } grom_fasta;
 
 int grom_fasta_open(grom_fasta *f, const char *path); /* find_genome_length */
+/* the CLI's open: the <fasta>.info cache when it loads (load_genome_info),
+ * else grom_fasta_open + save_genome_info (GROM.c:22308-22311) */
+int grom_fasta_open_cached(grom_fasta *f, const char *path);
 void grom_fasta_close(grom_fasta *f);
 /* load chromosome `i` into buf (capacity cap); returns its length */
 long grom_fasta_load(grom_fasta *f, int i, char *buf, long cap);

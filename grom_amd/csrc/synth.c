@@ -834,6 +834,12 @@ static void emit_to_bam(void *ctx, const bam_rec *b) { bam_write_rec((bgzf_write
 int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *bam_path) {
     FILE *fa = fopen(fasta_path, "w");
     if (!fa) return -1;
+    {  /* a new FASTA under an old name: drop its <fasta>.info cache, which the
+        * CLI (like GROM.c:22308) would otherwise trust */
+        char info[4096];
+        snprintf(info, sizeof(info), "%s.info", fasta_path);
+        remove(info);
+    }
     char **refs = (char **)calloc(c->n_chr, sizeof(char *));
     for (int i = 0; i < c->n_chr; i++) {
         refs[i] = synth_reference(c, i);
@@ -873,6 +879,6 @@ int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *ba
     free(h.ref_name);
     free(h.ref_len);
     free(refs);
-    if (rc == 0) rc = bai_write_minimal(bam_path, c->n_chr);
+    if (rc == 0) rc = bai_build(bam_path);  /* a real index, as samtools index writes */
     return rc;
 }

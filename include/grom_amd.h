@@ -382,6 +382,18 @@ grom_batch_handle *grom_synth_chrom(const grom_synth_spec *spec, grom_params *pa
 int grom_batch_get(grom_batch_handle *h, grom_chrom *chrom, grom_reads *reads);
 void grom_batch_release(grom_batch_handle *h);
 
+/* ---- BAM index (replaces htslib's bam_index_build / bam_index_load /
+ * bam_fetch, GROM.c:216-261 and 22128-22138; SAM v1 section 5.2) ---- */
+/* index <bam> into <bam>.bai: 0, or negative */
+int grom_bai_build(const char *bam_path);
+/* parse an index file; out = {n_ref, bins, chunks, linear intervals,
+ * unplaced-read count or -1 when absent}.  0, or negative */
+int grom_bai_summary(const char *bai_path, int64_t out[5]);
+/* n_queries seeded random regions of <bam> fetched through <bam>.bai and by a
+ * full scan: the number of regions whose record sets differ (0 = all equal),
+ * negative on error.  *visited gets the records the fetches returned. */
+int64_t grom_bai_selftest(const char *bam_path, int64_t n_queries, uint64_t seed, int64_t *visited);
+
 #ifdef __cplusplus
 }
 #endif

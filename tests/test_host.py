@@ -100,3 +100,60 @@ def test_fmt_2f_matches_printf():
     integer ratios, exact binary ties and edge cases (inf, nan, -0.0)."""
     import grom_amd
     assert grom_amd.lib().grom_fmt_selftest(200000, 12345) == 0
+
+
+def _find_genome_length(fa):
+    """find_genome_length (GROM.c:1321-1428) in Python: fgets(1000) lines,
+    names cut at the first non-graph byte, lower-cased, file offsets after the
+    header line."""
+    recs, mappable, cur = [], 0, 0
+    with open(fa, "rb") as f:
+        while True:
+            line = f.readline(999)
+            if not line:
+                break
+            if line[:1] != b">":
+                for c in line:
+                    if chr(c).isalpha():
+                        mappable += c not in b"Nn"
+                        cur += 1
+                continue
+            if recs:
+                recs[-1][3] = cur
+            cur = 0
+            end = len(line)
+            for w in range(len(line) - 1, 0, -1):
+                if not (0x21 <= line[w] <= 0x7e):
+                    end = w
+            end = min(end, 50)
+            recs.append([len(recs), end - 1, f.tell(), 0, line[1:end].decode().lower()])
+    if recs:
+        recs[-1][3] = cur
+    return mappable, recs
+
+
+def test_fasta_info_cache_written_and_trusted(datadir, tmp_path):
+    """The CLI writes <fasta>.info in save_genome_info's format (GROM.c:1028-1045)
+    and, like GROM.c:22308, trusts it when it loads: a renamed chromosome in the
+    cache makes that BAM target unmatched."""
+    import shutil
+    bam0, fa0 = synth(datadir, "three_chr", CASES["three_chr"])
+    bam, fa = str(tmp_path / "g.bam"), str(tmp_path / "g.fa")
+    shutil.copy(bam0, bam)
+    shutil.copy(fa0, fa)
+    shutil.copy(bam0 + ".bai", bam + ".bai")
+    r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "a.vcf"], str(tmp_path), {"GROM_PLAN_ONLY": "1"})
+    assert {"chr1", "chr2", "chr3"} <= set(parse_plan(r.stdout)), r.stdout
+    mappable, recs = _find_genome_length(fa)
+    want = f"{len(recs)} {mappable}\n" + "".join(f"{i} {nl} {pos} {ln} {nm}\n" for i, nl, pos, ln, nm in recs)
+    assert open(fa + ".info").read() == want
+    lines = want.splitlines(True)
+    lines[2] = lines[2].replace("chr2", "chrz")
+    open(fa + ".info", "w").writelines(lines)
+    r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "b.vcf"], str(tmp_path), {"GROM_PLAN_ONLY": "1"})
+    plan = parse_plan(r.stdout)
+    assert "chr1" in plan and "chr3" in plan and "chr2" not in plan, r.stdout
+    # a cache that does not parse is rebuilt from the FASTA
+    open(fa + ".info", "w").write("3 1\n0 x\n")
+    run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "c.vcf"], str(tmp_path), {"GROM_PLAN_ONLY": "1"})
+    assert open(fa + ".info").read().splitlines()[1:] == want.splitlines()[1:]
