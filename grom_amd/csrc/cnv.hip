@@ -72,9 +72,9 @@ constexpr double STDEV_STEP = 0.01;        // g_stdev_step, GROM.c:940
 constexpr long MAX_DIST_LAST_GOOD = 10500; // default -X + 500, set before getopt (GROM.c:21898)
 constexpr int MAX_BLOCK_LIST = 10000;      // max_block_list_len, GROM.c:633
 
-constexpr int GC_TP = 4096;                // positions per k_cnv_gc tile
-constexpr int GC_MMAX = 1536;              // largest insert mean the LDS tile holds
-constexpr int GC_LEN = GC_TP + 2 * GC_MMAX + 2;
+constexpr int GC_TP = 16384;               // positions per k_cnv_gc tile
+constexpr int GC_MMAX = 1536;              // largest insert mean the kernels accept
+constexpr int GC_NW = (GC_TP + 2 * GC_MMAX + 1 + 63) / 64;  // 64-bit class words per tile (with halo)
 constexpr int SEG_W = 4096;                // positions per wave in the state scans
 constexpr int ZT_MAX = 1024;               // depths with a precomputed z rank index
 constexpr int HIST_MAX = 4096;             // exact depth histogram for the chromosome variance
@@ -122,72 +122,89 @@ __device__ __forceinline__ int pair_type(char x, char y) {
     return base[a] + (b - a);
 }
 
-// exclusive prefix sum of a[0..n) in place, one 256-thread block
-__device__ void block_excl_scan(int *a, int n, int *tmp) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, per = (n + 255) / 256;
-    const int lo = min(n, tid * per), hi = min(n, lo + per);
-    int s = 0;
-    for (int i = lo; i < hi; i++) s += a[i];
-    int x = s;  // inclusive scan within the wave
-    for (int d = 1; d < 64; d <<= 1) {
-        int y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) tmp[wv] = x;
-    __syncthreads();
-    int acc = x - s;
-    for (int w = 0; w < wv; w++) acc += tmp[w];
-    for (int i = lo; i < hi; i++) {
-        int v = a[i];
-        a[i] = acc;
-        acc += v;
-    }
-    __syncthreads();
+// sum of the bit indices set in w: bit b of each index, weighted 2^b
+__device__ __forceinline__ int bit_index_sum(uint64_t w) {
+    return __popcll(w & 0xAAAAAAAAAAAAAAAAull) + 2 * __popcll(w & 0xCCCCCCCCCCCCCCCCull) +
+           4 * __popcll(w & 0xF0F0F0F0F0F0F0F0ull) + 8 * __popcll(w & 0xFF00FF00FF00FF00ull) +
+           16 * __popcll(w & 0xFFFF0000FFFF0000ull) + 32 * __popcll(w & 0xFFFFFFFF00000000ull);
 }
 
 // Weighted GC / ACGT percent and dinucleotide class per base (GROM.c:1684-1861).
 // The reference's rolling sums equal, for p in [m-1, len-2m+1),
 //   T(p) = sum_{|q-p|<m} g(q) (m - |q-p|) = Q[p+m+1] - 2 Q[p+1] + Q[p-m+1]
-// with P the prefix count of g and Q the prefix sum of P (exact integers).
+// with P[x] = #{q < x : g(q)} and Q[x] = sum_{y<x} P[y] = (x-1) P[x] - R[x],
+// R[x] = sum_{q<x} q g(q) (exact integers; tile-local coordinates, so linear
+// offsets cancel in the second difference). The tile's classes are two bit
+// planes built by wave ballots; P and R at any x are a per-word prefix plus
+// popcounts of the masked word, so the kernel reads each reference byte once
+// (plus the 2m halo) and writes 3 bytes per base.
 __global__ __launch_bounds__(256) void k_cnv_gc(const char *__restrict__ ref, Args A, int m, int64_t total,
                                                 uint8_t *__restrict__ gcw, uint8_t *__restrict__ acw,
                                                 uint8_t *__restrict__ rtype) {
-    __shared__ int P[GC_LEN + 1];
-    __shared__ int Q[GC_LEN + 1];
-    __shared__ uint8_t cls[GC_LEN];
-    __shared__ int tmp[256];
+    __shared__ uint64_t bits[2][GC_NW];  // plane 0: GC, plane 1: ACGT
+    __shared__ int pw[2][GC_NW];         // exclusive prefix of the set-bit counts
+    __shared__ int rw[2][GC_NW];         // exclusive prefix of the set-bit local indices
     const int64_t t0 = (int64_t)blockIdx.x * GC_TP;
     const int64_t base = t0 - m;
     const int L = GC_TP + 2 * m + 1;
-    for (int i = threadIdx.x; i < L; i += 256) {
-        int64_t q = base + i;
-        cls[i] = (q >= 0 && q < A.len) ? (uint8_t)gc_class(ref[q]) : 0;
+    const int nw = (L + 63) >> 6;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int wi = wv; wi < nw; wi += 4) {
+        const int k = wi * 64 + lane;
+        const int64_t q = base + k;
+        const int c = (k < L && q >= 0 && q < A.len) ? gc_class(ref[q]) : 0;
+        const uint64_t g = __ballot(c & 1), a = __ballot(c & 2);
+        if (lane == 0) {
+            bits[0][wi] = g;
+            bits[1][wi] = a;
+        }
     }
     __syncthreads();
-    for (int pass = 0; pass < 2; pass++) {
-        for (int i = threadIdx.x; i <= L; i += 256) P[i] = (i < L) ? ((cls[i] >> pass) & 1) : 0;
-        __syncthreads();
-        block_excl_scan(P, L + 1, tmp);
-        for (int i = threadIdx.x; i <= L; i += 256) Q[i] = P[i];
-        __syncthreads();
-        block_excl_scan(Q, L + 1, tmp);
-        uint8_t *out = pass == 0 ? gcw : acw;
-        for (int j = threadIdx.x; j < GC_TP; j += 256) {
-            int64_t p = t0 + j;
-            if (p >= A.len) break;
-            uint8_t w = 0;
-            if (p >= A.lo && p < A.hi) {
-                int lp = j + m;
-                int64_t Tv = (int64_t)Q[lp + m + 1] - 2 * (int64_t)Q[lp + 1] + (int64_t)Q[lp - m + 1];
-                w = (uint8_t)(100 * Tv / total);
+    {  // wave w scans array w: counts / index sums of plane w & 1
+        const int pl = wv & 1, isr = wv >> 1;
+        int carry = 0;
+        for (int c0 = 0; c0 < nw; c0 += 64) {
+            const int wi = c0 + lane;
+            int v = 0;
+            if (wi < nw) {
+                const uint64_t w = bits[pl][wi];
+                v = isr ? wi * 64 * __popcll(w) + bit_index_sum(w) : __popcll(w);
             }
-            out[p] = w;
+            int x = v;
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            if (wi < nw) (isr ? rw : pw)[pl][wi] = carry + x - v;
+            carry += __shfl(x, 63);
         }
-        __syncthreads();
     }
+    __syncthreads();
+    const uint32_t tot = (uint32_t)total;  // m*m <= GC_MMAX^2
     for (int j = threadIdx.x; j < GC_TP; j += 256) {
-        int64_t p = t0 + j;
+        const int64_t p = t0 + j;
         if (p >= A.len) break;
+        uint8_t w2[2] = {0, 0};
+        if (p >= A.lo && p < A.hi) {
+            const int xs[3] = {j + 2 * m + 1, j + m + 1, j + 1};
+#pragma unroll
+            for (int pl = 0; pl < 2; pl++) {
+                int Qv[3];
+#pragma unroll
+                for (int t = 0; t < 3; t++) {
+                    const int x = xs[t], wi = x >> 6, b = x & 63;
+                    const uint64_t wd = bits[pl][wi] & ((1ull << b) - 1ull);
+                    const int c = __popcll(wd);
+                    const int Pv = pw[pl][wi] + c;
+                    const int Rv = rw[pl][wi] + wi * 64 * c + bit_index_sum(wd);
+                    Qv[t] = (x - 1) * Pv - Rv;
+                }
+                const uint32_t Tv = (uint32_t)(Qv[0] - 2 * Qv[1] + Qv[2]);
+                w2[pl] = (uint8_t)(100u * Tv / tot);
+            }
+        }
+        gcw[p] = w2[0];
+        acw[p] = w2[1];
         rtype[p] = (p >= A.lo && p < A.hi) ? (uint8_t)pair_type(ref[p], ref[p + 1]) : (uint8_t)10;
     }
 }
