@@ -1903,6 +1903,8 @@ __global__ __launch_bounds__(256) void k_cnv_words(const uint16_t *__restrict__ 
     }
 }
 
+constexpr int CLS_B = 8;  // k_cnv_classify: per-base loads issued together
+
 // One lane per candidate.  nxt[m][p] gets the no-op (p) or phase A's jump;
 // the rest are listed in und[] (and get NXT_UNDECIDED).
 template <int KIND>
@@ -1925,26 +1927,47 @@ __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *_
     int mqi = m;
     bool defined = false;
     int64_t wl = 0, cnt2 = 0;
-    for (int64_t pa = p; pa < p + ML; pa++) {
-        wl += 1;
-        const uint32_t b = W.wb[pa];
-        if (!(b & B_LOW)) {
-            if (cdef(b) >= 0) defined = true;
-            mqi = cls(b, mqi);
-            if (b & (pb0 << mqi)) cnt2 += 1;
-            else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
-        } else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
+    // (loads in batches of CLS_B, clamped to the window, so several are in
+    // flight; the bases are still consumed one at a time, in order)
+    for (int64_t pb = p; pb < p + ML; pb += CLS_B) {
+        uint32_t bb[CLS_B];
+#pragma unroll
+        for (int k = 0; k < CLS_B; k++) bb[k] = W.wb[min(pb + k, p + ML - 1)];
+#pragma unroll
+        for (int k = 0; k < CLS_B; k++) {
+            const int64_t pa = pb + k;
+            if (pa >= p + ML) break;
+            wl += 1;
+            const uint32_t b = bb[k];
+            if (!(b & B_LOW)) {
+                if (cdef(b) >= 0) defined = true;
+                mqi = cls(b, mqi);
+                if (b & (pb0 << mqi)) cnt2 += 1;
+                else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
+            } else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
+        }
     }
     {
         // the first window's sum is the reference's own (same order)
         int64_t cnt = ML;
         double R = 0.0, A = 0.0;
-        for (int64_t a = p; a < p + ML; a++) {
-            const uint32_t b = W.wb[a];
-            cnt -= (b & B_LOW);
-            const double z = W.sd[a];
-            if (KIND == 0) R += z; else R -= z;
-            A += fabs(z);
+        for (int64_t ab = p; ab < p + ML; ab += CLS_B) {
+            uint32_t bb[CLS_B];
+            double zz[CLS_B];
+#pragma unroll
+            for (int k = 0; k < CLS_B; k++) {
+                const int64_t a = min(ab + k, p + ML - 1);
+                bb[k] = W.wb[a];
+                zz[k] = W.sd[a];
+            }
+#pragma unroll
+            for (int k = 0; k < CLS_B; k++) {
+                if (ab + k >= p + ML) break;
+                cnt -= (bb[k] & B_LOW);
+                const double z = zz[k];
+                if (KIND == 0) R += z; else R -= z;
+                A += fabs(z);
+            }
         }
         if (cnt > 0 && wsd[ML] > 0 && ratio_ge_min(R, cnt * wsd[ML])) { undecided = true; goto done; }
         // phase B (GROM.c:19405-19470)
@@ -1977,25 +2000,38 @@ __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *_
             }
             // step by step to the next word boundary
             const int64_t xb = min(xend, (x | 63) + 1);
-            for (; x < xb; x++) {
-                wl += 1;
-                if (x >= end) goto done;  // a stop: no-op
-                const uint32_t b = W.wb[x];
-                if (!(b & B_LOW)) {
-                    if (cdef(b) >= 0) defined = true;
-                    mqi = cls(b, mqi);
-                    const double z = W.sd[x];
-                    R += sgn * z;
-                    A += fabs(z);
-                    cnt += 1;
-                    if (b & (pb0 << mqi)) {
-                        cnt2 += 1;
-                        if (wsd[wl] > 0) {
-                            const double d = cnt * wsd[wl];
-                            if (!(R + 1e-9 * (A + fabs(R)) < 3.0 * d * (1.0 - 1e-15))) { undecided = true; goto done; }
-                        }
+            const int64_t xl = max<int64_t>(0, min(xb, end) - 1);  // last base a load may touch
+            while (x < xb) {
+                uint32_t bb[CLS_B];  // the next CLS_B bases' words and z, loaded together
+                double zz[CLS_B];
+#pragma unroll
+                for (int t = 0; t < CLS_B; t++) {
+                    const int64_t xi = min(x + t, xl);
+                    bb[t] = W.wb[xi];
+                    zz[t] = W.sd[xi];
+                }
+#pragma unroll
+                for (int k = 0; k < CLS_B; k++, x++) {
+                    if (x >= xb) break;
+                    wl += 1;
+                    if (x >= end) goto done;  // a stop: no-op
+                    const uint32_t b = bb[k];
+                    if (!(b & B_LOW)) {
+                        if (cdef(b) >= 0) defined = true;
+                        mqi = cls(b, mqi);
+                        const double z = zz[k];
+                        R += sgn * z;
+                        A += fabs(z);
+                        cnt += 1;
+                        if (b & (pb0 << mqi)) {
+                            cnt2 += 1;
+                            if (wsd[wl] > 0) {
+                                const double d = cnt * wsd[wl];
+                                if (!(R + 1e-9 * (A + fabs(R)) < 3.0 * d * (1.0 - 1e-15))) { undecided = true; goto done; }
+                            }
+                        } else if ((2 * cnt2) < wl) goto done;
                     } else if ((2 * cnt2) < wl) goto done;
-                } else if ((2 * cnt2) < wl) goto done;
+                }
             }
         }
     }
