@@ -181,31 +181,51 @@ __global__ __launch_bounds__(256) void k_cnv_gc(const char *__restrict__ ref, Ar
     }
     __syncthreads();
     const uint32_t tot = (uint32_t)total;  // m*m <= GC_MMAX^2
-    for (int j = threadIdx.x; j < GC_TP; j += 256) {
-        const int64_t p = t0 + j;
-        if (p >= A.len) break;
-        uint8_t w2[2] = {0, 0};
-        if (p >= A.lo && p < A.hi) {
-            const int xs[3] = {j + 2 * m + 1, j + m + 1, j + 1};
+    // four consecutive positions per thread, stored as one 32-bit word per
+    // output (t0 is a multiple of GC_TP, so the words are aligned)
+    for (int j0 = 4 * threadIdx.x; j0 < GC_TP; j0 += 4 * 256) {
+        const int64_t p0 = t0 + j0;
+        if (p0 >= A.len) break;
+        uint32_t o[3] = {0, 0, 0};  // gcw, acw, rtype
 #pragma unroll
-            for (int pl = 0; pl < 2; pl++) {
-                int Qv[3];
+        for (int u = 0; u < 4; u++) {
+            const int j = j0 + u;
+            const int64_t p = p0 + u;
+            uint32_t w2[2] = {0, 0}, rt = 10;
+            if (p >= A.lo && p < A.hi) {
+                const int xs[3] = {j + 2 * m + 1, j + m + 1, j + 1};
 #pragma unroll
-                for (int t = 0; t < 3; t++) {
-                    const int x = xs[t], wi = x >> 6, b = x & 63;
-                    const uint64_t wd = bits[pl][wi] & ((1ull << b) - 1ull);
-                    const int c = __popcll(wd);
-                    const int Pv = pw[pl][wi] + c;
-                    const int Rv = rw[pl][wi] + wi * 64 * c + bit_index_sum(wd);
-                    Qv[t] = (x - 1) * Pv - Rv;
+                for (int pl = 0; pl < 2; pl++) {
+                    int Qv[3];
+#pragma unroll
+                    for (int t = 0; t < 3; t++) {
+                        const int x = xs[t], wi = x >> 6, b = x & 63;
+                        const uint64_t wd = bits[pl][wi] & ((1ull << b) - 1ull);
+                        const int c = __popcll(wd);
+                        const int Pv = pw[pl][wi] + c;
+                        const int Rv = rw[pl][wi] + wi * 64 * c + bit_index_sum(wd);
+                        Qv[t] = (x - 1) * Pv - Rv;
+                    }
+                    const uint32_t Tv = (uint32_t)(Qv[0] - 2 * Qv[1] + Qv[2]);
+                    w2[pl] = (100u * Tv / tot) & 255u;
                 }
-                const uint32_t Tv = (uint32_t)(Qv[0] - 2 * Qv[1] + Qv[2]);
-                w2[pl] = (uint8_t)(100u * Tv / tot);
+                rt = (uint32_t)pair_type(ref[p], ref[p + 1]);
+            }
+            o[0] |= w2[0] << (8 * u);
+            o[1] |= w2[1] << (8 * u);
+            o[2] |= rt << (8 * u);
+        }
+        if (p0 + 4 <= A.len) {
+            *reinterpret_cast<uint32_t *>(gcw + p0) = o[0];
+            *reinterpret_cast<uint32_t *>(acw + p0) = o[1];
+            *reinterpret_cast<uint32_t *>(rtype + p0) = o[2];
+        } else {  // the chromosome's last partial word
+            for (int u = 0; p0 + u < A.len; u++) {
+                gcw[p0 + u] = (uint8_t)(o[0] >> (8 * u));
+                acw[p0 + u] = (uint8_t)(o[1] >> (8 * u));
+                rtype[p0 + u] = (uint8_t)(o[2] >> (8 * u));
             }
         }
-        gcw[p] = w2[0];
-        acw[p] = w2[1];
-        rtype[p] = (p >= A.lo && p < A.hi) ? (uint8_t)pair_type(ref[p], ref[p + 1]) : (uint8_t)10;
     }
 }
 
