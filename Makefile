@@ -9,10 +9,10 @@ HIPFLAGS ?= -O3 -g --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -pthread
 LIBDIR  = grom_amd/lib
 BINDIR  = grom_amd/bin
 
-HOST_SRC = grom_amd/csrc/bamio.c grom_amd/csrc/stream.c grom_amd/csrc/tables.c grom_amd/csrc/synth.c grom_amd/csrc/hostapi.c grom_amd/csrc/grom_main.c
+HOST_SRC = grom_amd/csrc/bamio.c grom_amd/csrc/stream.c grom_amd/csrc/tables.c grom_amd/csrc/synth.c grom_amd/csrc/hostapi.c grom_amd/csrc/grom_main.c grom_amd/csrc/pdecode.c
 HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC)) build/snvfmt.o build/svcall.o
 DEV_OBJ = build/scan.o build/cnv.o build/sv.o
-HDRS = include/grom_amd.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h
+HDRS = include/grom_amd.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h grom_amd/csrc/pdecode.h
 KHDRS = grom_amd/csrc/k_scan_tile.h grom_amd/csrc/device_common.h grom_amd/csrc/snvfmt.h
 
 all: $(LIBDIR)/libgrom_amd.so $(BINDIR)/grom $(BINDIR)/grom_synth oracle
@@ -46,7 +46,7 @@ build/svcall.o: grom_amd/csrc/svcall.cpp grom_amd/csrc/sv.h $(HDRS)
 
 $(LIBDIR)/libgrom_amd.so: $(DEV_OBJ) $(HOST_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lz -lm
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lz -lm -ldl -lpthread
 
 $(BINDIR)/grom: grom_amd/csrc/grom_cli.c $(LIBDIR)/libgrom_amd.so $(HDRS)
 	@mkdir -p $(BINDIR)
@@ -54,7 +54,7 @@ $(BINDIR)/grom: grom_amd/csrc/grom_cli.c $(LIBDIR)/libgrom_amd.so $(HDRS)
 
 $(BINDIR)/grom_synth: tools/grom_synth.c build/synth.o build/bamio.o
 	@mkdir -p $(BINDIR)
-	$(CC) $(CFLAGS) -o $@ $^ -lz -lm
+	$(CC) $(CFLAGS) -o $@ $^ -lz -lm -ldl -lpthread
 
 oracle:
 	$(MAKE) -C oracle

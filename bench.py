@@ -32,7 +32,14 @@ The JSON line also carries
                 generator and flags (rank 0, N=1);
   concordance   the GPU CLI on that same sample's BAM/FASTA against the
                 oracle's VCF and .ctx.vcf, byte for byte, with the CLI's
-                end-to-end time (BAM decode and upload included).
+                end-to-end time (BAM decode and upload included);
+  cli_whole_run the drop-in CLI (grom_amd/bin/grom, a fresh process) on a
+                >=100 Mb 24-contig 30x BAM of the same generator (the GRCh38
+                contigs scaled by --cli-scale): SURVEY 8(d)'s metric as
+                defined, bases / wall time of the whole run (BAM decode on
+                the host's cores, pinned pieces streamed to HBM, scans, VCF),
+                with its VCF and .ctx.vcf compared byte for byte against the
+                oracle run on the same files (rank 0, N=1).
 """
 import argparse
 import ctypes
@@ -126,6 +133,70 @@ def cpu_baseline_and_concordance(work_dir, knobs, flags):
     return cpu, conc
 
 
+def cli_whole_run_start(work_dir, knobs, flags, scale):
+    """Write the >=100 Mb BAM, start the oracle on it in the background (its
+    VCF is compared at the end), then time the GPU CLI twice as a fresh process."""
+    from grom_amd import GROM_BIN, run_synth
+    names = [n for n, _ in GRCH38]
+    lengths = [max(int(L * scale), 1_000_000) for _, L in GRCH38]
+    total = sum(lengths)
+    src = os.path.join(work_dir, "src")
+    os.makedirs(src, exist_ok=True)
+    t0 = time.perf_counter()
+    bam, fa = run_synth(os.path.join(src, "cli"), *synth_args(knobs, lengths), "-n", ",".join(names), timeout=1200)
+    t_synth = time.perf_counter() - t0
+    env = dict(os.environ, GROM_FILEDATE="20260101", GROM_SEED="7")
+    dirs = {}
+    for side in ("gpu", "cpu"):  # own copies of the side files (.mean, .info); same paths in the VCF header
+        d = os.path.join(work_dir, side)
+        os.makedirs(d, exist_ok=True)
+        for f, t in (("cli.bam", bam), ("cli.bam.bai", bam + ".bai"), ("cli.fa", fa)):
+            os.symlink(t, os.path.join(d, f))
+        dirs[side] = d
+    args = ["-i", "cli.bam", "-r", "cli.fa", "-o", "out.vcf"] + flags
+    runs = []
+    for _ in range(2):
+        t1 = time.perf_counter()
+        r = subprocess.run([GROM_BIN] + args, cwd=dirs["gpu"], env=dict(env, GROM_VERBOSE="1"), capture_output=True,
+                           text=True, timeout=1200)
+        runs.append(time.perf_counter() - t1)
+        if r.returncode != 0:
+            raise RuntimeError("GPU CLI failed on the whole-run BAM: " + r.stdout[-2000:] + r.stderr[-2000:])
+    dec = [ln for ln in r.stdout.splitlines() if ln.startswith("streamed decode:")]
+    oracle = os.path.join(REPO, "oracle", "grom_oracle")
+    t2 = time.perf_counter()
+    proc = subprocess.Popen([oracle] + args, cwd=dirs["cpu"], env=env, stdout=subprocess.DEVNULL,
+                            stderr=subprocess.PIPE, text=True)
+    info = {"bam": f"{len(lengths)} GRCh38 contigs x {scale:g} ({total / 1e6:.1f} Mb), same generator and flags "
+                   f"as the workload (grom_synth {' '.join(synth_args(knobs, ['...']))})",
+            "bam_bytes": os.path.getsize(bam), "genome_bases": total, "synth_s": round(t_synth, 1),
+            "cli_wall_s": [round(x, 3) for x in runs],
+            "value": round(total / min(runs) / 1e6, 2), "unit": "Mbases/s",
+            "value_first_run": round(total / runs[0] / 1e6, 2),
+            "decode": dec[-1] if dec else None,
+            "note": "grom_amd/bin/grom as a fresh process (process start, HIP init, BAM index + parallel decode on "
+                    "the host, pinned pieces -> HBM, scans, VCF + .ctx.vcf); best of two runs, the BAM in the page "
+                    "cache"}
+    return {"info": info, "proc": proc, "t_oracle": t2, "dirs": dirs, "total": total}
+
+
+def cli_whole_run_finish(st):
+    info = st["info"]
+    err = st["proc"].communicate(timeout=3600)[1]
+    dt = time.perf_counter() - st["t_oracle"]
+    if st["proc"].returncode != 0:
+        info["identical_to_oracle"] = None
+        info["oracle_error"] = (err or "")[-500:]
+        return info
+    same = all(open(os.path.join(st["dirs"]["gpu"], "out" + ext), "rb").read() ==
+               open(os.path.join(st["dirs"]["cpu"], "out" + ext), "rb").read() for ext in (".vcf", ".ctx.vcf"))
+    info["identical_to_oracle"] = same
+    info["vcf_rows"] = sum(1 for ln in open(os.path.join(st["dirs"]["gpu"], "out.vcf")) if not ln.startswith("#"))
+    info["oracle_s"] = round(dt, 1)
+    info["oracle_mbases_per_s"] = round(st["total"] / dt / 1e6, 3)
+    return info
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -141,6 +212,8 @@ def main():
     ap.add_argument("--gen-workers", type=int, default=0, help="host generator threads (0: auto)")
     ap.add_argument("--cnv-rate", type=float, default=None, help="override the copy-number region rate (tests)")
     ap.add_argument("--sweep-inflight", default="", help="e.g. 1,2,3,4: time one pass per value first (stderr)")
+    ap.add_argument("--cli-scale", type=float, default=0.04,
+                    help="contig scale of the whole-run CLI leg's BAM (0.04: 24 contigs, 124 Mb); 0 skips it")
     args = ap.parse_args()
 
     import torch
@@ -174,6 +247,13 @@ def main():
     gen = dict(coverage=knobs["coverage"], read_len=READ_LEN, dup_frac=knobs["dup_frac"],
                sv_per_mb=knobs["sv_per_mb"], cnv_rate=knobs["cnv_rate"], cnv_range=knobs["cnv_range"],
                seed=knobs["seed"] + (rank if not genome else 0))
+    # the whole-run CLI leg first, while HBM is empty (its oracle runs meanwhile)
+    cli_state, cli_dir = None, None
+    if genome and rank == 0 and world == 1 and args.cli_scale > 0 and not args.no_cpu_baseline:
+        cli_dir = tempfile.TemporaryDirectory()
+        cli_state = cli_whole_run_start(cli_dir.name, knobs, flags, args.cli_scale)
+        print(f"[bench] CLI whole run: {cli_state['info']['cli_wall_s']} s, {cli_state['info']['value']} Mbases/s",
+              file=sys.stderr, flush=True)
     # genome-wide insert statistics (find_insert_mean runs once per BAM): the
     # same generator on a 2 Mb probe, identical on every rank
     probe = grom_amd.SynthBatch.genome_chrom([2_000_000], 0, params, **dict(gen, sv_per_mb=0.0, cnv_rate=0.0))
@@ -284,6 +364,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             with tempfile.TemporaryDirectory() as d:
                 cpu, conc = cpu_baseline_and_concordance(d, knobs, flags)
+        cli_info = cli_whole_run_finish(cli_state) if cli_state else None
+        if cli_dir:
+            cli_dir.cleanup()
         wl = ("BASELINE configs[2]: synthetic 30x 2x150 bp human-shape genome, 24 GRCh38 contigs "
               f"({sum(lengths) / 1e9:.3f} Gb), SNV/indel, {knobs['sv_per_mb']:.2f} breakpoint SVs/Mb "
               "(DEL/DUP/INV/INS/CTX with split reads + discordant pairs), 500 CNVs/3.1 Gb, 5% PCR duplicates, -M"
@@ -334,6 +417,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "concordance": conc,
+            "cli_whole_run": cli_info,
         }
         print(json.dumps(line), flush=True)
     for d in reversed(devs):

@@ -136,6 +136,23 @@ _SIGS = {
     "grom_batch_get": (C.c_int, [C.c_void_p, C.POINTER(Chrom), C.POINTER(Reads)]),
     "grom_batch_release": (None, [C.c_void_p]),
     "grom_cli_main": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
+    # streamed input (ABI 5)
+    "grom_pinned_alloc": (C.c_void_p, [C.c_size_t]),
+    "grom_pinned_free": (None, [C.c_void_p]),
+    "grom_stage_new": (C.c_void_p, [C.c_int]),
+    "grom_stage_free": (None, [C.c_void_p]),
+    "grom_stage_begin": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "grom_stage_set_ref": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "grom_stage_append": (C.c_int64, [C.c_void_p, C.POINTER(Reads)]),
+    "grom_stage_ticket_done": (C.c_int, [C.c_void_p, C.c_int64]),
+    "grom_stage_ticket_wait": (C.c_int, [C.c_void_p, C.c_int64]),
+    "grom_stage_trim": (C.c_int, [C.c_void_p, C.c_int64]),
+    "grom_stage_patch_aux": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(Aux)]),
+    "grom_stage_bytes": (C.c_int64, [C.c_void_p]),
+    "grom_stage_view": (C.c_int, [C.c_void_p, C.POINTER(Chrom), C.POINTER(Chrom), C.POINTER(Reads)]),
+    "grom_scan_chrom_staged": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(Chrom), C.POINTER(Out), C.POINTER(Stats)]),
+    "grom_debug_counts_staged": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(Chrom), C.POINTER(C.c_int32), C.c_void_p,
+                                           C.c_int64, C.c_void_p]),
 }
 
 _lib = None

@@ -3,6 +3,7 @@
  */
 #include "bamio.h"
 
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -265,32 +266,76 @@ int bgzf_open_write(bgzf_writer *w, const char *path, int level) {
     return w->buf ? 0 : -1;
 }
 
-int bgzf_flush_block(bgzf_writer *w) {
-    if (w->len == 0) return 0;
-    unsigned char out[BGZF_MAX_BLOCK + 64];
-    z_stream zs;
-    memset(&zs, 0, sizeof(zs));
-    if (deflateInit2(&zs, w->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return -1;
-    zs.next_in = w->buf;
-    zs.avail_in = w->len;
-    zs.next_out = out + 18;
-    zs.avail_out = BGZF_MAX_BLOCK - 18 - 8;
-    int rc = deflate(&zs, Z_FINISH);
-    int clen = (int)zs.total_out;
-    deflateEnd(&zs);
-    if (rc != Z_STREAM_END) return -1;
+/* ---- block compression: libdeflate when the image has it, else zlib ---- */
+typedef void *(*ldc_alloc_fn)(int);
+typedef size_t (*ldc_comp_fn)(void *, const void *, size_t, void *, size_t);
+typedef void (*ldc_free_fn)(void *);
+static ldc_alloc_fn ldc_alloc;
+static ldc_comp_fn ldc_comp;
+static ldc_free_fn ldc_free;
+static pthread_once_t ldc_once = PTHREAD_ONCE_INIT;
+static void ldc_init(void) {
+    if (getenv("GROM_NO_LIBDEFLATE")) return;
+    void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    ldc_alloc_fn a = (ldc_alloc_fn)dlsym(h, "libdeflate_alloc_compressor");
+    ldc_comp_fn c = (ldc_comp_fn)dlsym(h, "libdeflate_deflate_compress");
+    ldc_free_fn f = (ldc_free_fn)dlsym(h, "libdeflate_free_compressor");
+    if (a && c && f) { ldc_alloc = a; ldc_comp = c; ldc_free = f; }
+}
+
+int bgzf_block_compress(const unsigned char *in, int len, unsigned char *out, int level) {
+    pthread_once(&ldc_once, ldc_init);
+    int clen = -1;
+    const int room = BGZF_MAX_BLOCK - 18 - 8;
+    if (ldc_alloc) {
+        static __thread void *cmp = NULL;
+        static __thread int cmp_level = -1;
+        if (!cmp || cmp_level != level) {
+            if (cmp) ldc_free(cmp);
+            cmp = ldc_alloc(level < 1 ? 1 : level);
+            cmp_level = level;
+        }
+        if (cmp) {
+            const size_t k = ldc_comp(cmp, in, (size_t)len, out + 18, (size_t)room);
+            if (k > 0) clen = (int)k;
+        }
+    }
+    if (clen < 0) {
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return -1;
+        zs.next_in = (unsigned char *)in;
+        zs.avail_in = (uInt)len;
+        zs.next_out = out + 18;
+        zs.avail_out = (uInt)room;
+        int rc = deflate(&zs, Z_FINISH);
+        clen = (int)zs.total_out;
+        deflateEnd(&zs);
+        if (rc != Z_STREAM_END) return -1;
+    }
     static const unsigned char h[12] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0, 0xff, 0x06, 0x00};
     memcpy(out, h, 12);
     out[12] = 'B'; out[13] = 'C';
     wr16(out + 14, 2);
     wr16(out + 16, (uint16_t)(18 + clen + 8 - 1));
-    uint32_t crc = crc32(0L, w->buf, w->len);
+    uint32_t crc = crc32(0L, in, (uInt)len);
     wr32(out + 18 + clen, crc);
-    wr32(out + 18 + clen + 4, (uint32_t)w->len);
-    if (fwrite(out, 1, 18 + clen + 8, w->fp) != (size_t)(18 + clen + 8)) return -1;
+    wr32(out + 18 + clen + 4, (uint32_t)len);
+    return 18 + clen + 8;
+}
+
+int bgzf_flush_block(bgzf_writer *w) {
+    if (w->len == 0) return 0;
+    unsigned char out[BGZF_MAX_BLOCK + 64];
+    const int n = bgzf_block_compress(w->buf, w->len, out, w->level);
+    if (n < 0) return -1;
+    if (fwrite(out, 1, n, w->fp) != (size_t)n) return -1;
     w->len = 0;
     return 0;
 }
+
+const unsigned char *bgzf_eof_block(void) { return BGZF_EOF_BLOCK; }
 
 int bgzf_write(bgzf_writer *w, const void *src, int n) {
     const unsigned char *s = (const unsigned char *)src;
@@ -550,16 +595,20 @@ typedef struct {
     int32_t n, cap;
     bai_chunk *c;
 } bin_acc;
-typedef struct {
+struct bai_racc {
     bin_acc *bins;
     int32_t n_bins, cap_bins;
     uint64_t *lin;
     int32_t n_lin;
     uint64_t off_beg, off_end, n_mapped, n_unmapped;
     int any;
-} ref_acc;
+    /* the current run of records with one bin (a chunk is flushed when it ends) */
+    int in_run;
+    uint32_t run_bin;
+    uint64_t run_beg, run_end;
+};
 
-static bin_acc *acc_bin(ref_acc *R, uint32_t bin) {
+static bin_acc *acc_bin(bai_racc *R, uint32_t bin) {
     for (int i = R->n_bins - 1; i >= 0; i--)  /* bins recur close together in sorted input */
         if (R->bins[i].bin == bin) return &R->bins[i];
     if (R->n_bins == R->cap_bins) {
@@ -572,7 +621,7 @@ static bin_acc *acc_bin(ref_acc *R, uint32_t bin) {
     return b;
 }
 
-static void acc_chunk(ref_acc *R, uint32_t bin, uint64_t beg, uint64_t end) {
+static void acc_chunk(bai_racc *R, uint32_t bin, uint64_t beg, uint64_t end) {
     bin_acc *b = acc_bin(R, bin);
     if (b->n > 0 && b->c[b->n - 1].end >> 16 == beg >> 16) {  /* adjacent within a block: extend */
         if (end > b->c[b->n - 1].end) b->c[b->n - 1].end = end;
@@ -585,6 +634,47 @@ static void acc_chunk(ref_acc *R, uint32_t bin, uint64_t beg, uint64_t end) {
     b->c[b->n].beg = beg;
     b->c[b->n].end = end;
     b->n++;
+}
+
+bai_racc *bai_racc_new(void) { return (bai_racc *)calloc(1, sizeof(bai_racc)); }
+
+void bai_racc_free(bai_racc *R) {
+    if (!R) return;
+    for (int i = 0; i < R->n_bins; i++) free(R->bins[i].c);
+    free(R->bins);
+    free(R->lin);
+    free(R);
+}
+
+void bai_racc_push(bai_racc *A, int32_t beg, int32_t end, uint64_t voff_beg, uint64_t voff_end, int unmapped) {
+    if (beg < 0) beg = 0;
+    const uint32_t bin = (uint32_t)bam_reg2bin(beg, end);
+    if (A->in_run && A->run_bin != bin) acc_chunk(A, A->run_bin, A->run_beg, A->run_end);
+    if (!A->in_run || A->run_bin != bin) {
+        A->in_run = 1;
+        A->run_bin = bin;
+        A->run_beg = voff_beg;
+    }
+    A->run_end = voff_end;
+    /* linear index: the first record overlapping each 16 kb window */
+    const int w0 = beg >> 14, w1 = (end - 1) >> 14;
+    if (w1 >= A->n_lin) {
+        A->lin = (uint64_t *)realloc(A->lin, sizeof(uint64_t) * (w1 + 1));
+        for (int w = A->n_lin; w <= w1; w++) A->lin[w] = UINT64_MAX;
+        A->n_lin = w1 + 1;
+    }
+    for (int w = w0; w <= w1; w++)
+        if (A->lin[w] == UINT64_MAX) A->lin[w] = voff_beg;
+    if (!A->any) A->off_beg = voff_beg;
+    A->any = 1;
+    A->off_end = voff_end;
+    if (unmapped) A->n_unmapped++;
+    else A->n_mapped++;
+}
+
+void bai_racc_flush(bai_racc *A) {
+    if (A->in_run) acc_chunk(A, A->run_bin, A->run_beg, A->run_end);
+    A->in_run = 0;
 }
 
 static int cmp_bin_acc(const void *a, const void *b) {
@@ -602,21 +692,64 @@ static void put64(FILE *f, uint64_t v) {
     put32(f, (uint32_t)(v >> 32));
 }
 
+static uint64_t map_id(void *ctx, int ref, uint64_t v) { (void)ctx; (void)ref; return v; }
+
+int bai_write_racc(const char *path, bai_racc **R, int n_ref, uint64_t n_no_coor,
+                   uint64_t (*map)(void *ctx, int ref, uint64_t voff), void *ctx) {
+    if (!map) map = map_id;
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    fwrite("BAI\1", 1, 4, f);
+    put32(f, (uint32_t)n_ref);
+    for (int t = 0; t < n_ref; t++) {
+        bai_racc *A = R[t];
+        if (!A) { put32(f, 0); put32(f, 0); continue; }
+        bai_racc_flush(A);
+        qsort(A->bins, A->n_bins, sizeof(bin_acc), cmp_bin_acc);
+        put32(f, (uint32_t)(A->n_bins + (A->any ? 1 : 0)));
+        for (int i = 0; i < A->n_bins; i++) {
+            put32(f, A->bins[i].bin);
+            put32(f, (uint32_t)A->bins[i].n);
+            for (int c = 0; c < A->bins[i].n; c++) {
+                put64(f, map(ctx, t, A->bins[i].c[c].beg));
+                put64(f, map(ctx, t, A->bins[i].c[c].end));
+            }
+        }
+        if (A->any) {  /* pseudo-bin 37450: offset span, mapped/unmapped counts */
+            put32(f, 37450u);
+            put32(f, 2u);
+            put64(f, map(ctx, t, A->off_beg));
+            put64(f, map(ctx, t, A->off_end));
+            put64(f, A->n_mapped);
+            put64(f, A->n_unmapped);
+        }
+        /* empty windows take the offset of the window before them
+         * (a smaller offset only makes a query read more) */
+        uint64_t prev = A->n_lin > 0 && A->lin[0] != UINT64_MAX ? A->lin[0] : 0;
+        for (int w = 0; w < A->n_lin; w++) {
+            if (A->lin[w] == UINT64_MAX) A->lin[w] = prev;
+            prev = A->lin[w];
+        }
+        put32(f, (uint32_t)A->n_lin);
+        for (int w = 0; w < A->n_lin; w++) put64(f, map(ctx, t, A->lin[w]));
+    }
+    put64(f, n_no_coor);
+    return fclose(f) != 0 ? -1 : 0;
+}
+
 int bai_build(const char *bam_path) {
     bgzf_reader r;
     bam_hdr h;
-    if (bgzf_open_read(&r, bam_path) != 0 || bam_read_header(&r, &h) != 0) return -1;
-    ref_acc *R = (ref_acc *)calloc(h.n_ref > 0 ? h.n_ref : 1, sizeof(ref_acc));
+    if (bgzf_open_read(&r, bam_path) != 0) return -1;
+    if (bam_read_header(&r, &h) != 0) { bgzf_close_read(&r); return -1; }
+    bai_racc **R = (bai_racc **)calloc(h.n_ref > 0 ? h.n_ref : 1, sizeof(bai_racc *));
+    for (int t = 0; t < h.n_ref; t++) R[t] = bai_racc_new();
     bam_rec b;
     memset(&b, 0, sizeof(b));
     uint64_t n_no_coor = 0;
-    int rc = 0, last_tid = -1;
+    int rc = 0, last_tid = -1, seen_unplaced = 0;
     int32_t last_pos = -1;
     int64_t off = bgzf_tell(&r);
-    /* the current run of records with one bin (a chunk is flushed when it ends) */
-    int run_tid = -1;
-    uint32_t run_bin = 0;
-    uint64_t run_beg = 0;
     for (;;) {
         const int k = bam_read_rec(&r, &b);
         if (k < 0) { rc = -1; break; }
@@ -624,88 +757,30 @@ int bai_build(const char *bam_path) {
         if (k == 0) break;
         if (b.tid < 0) {  /* unplaced reads sort last */
             n_no_coor++;
+            seen_unplaced = 1;
             off = end_off;
             continue;
         }
-        if (b.tid >= h.n_ref || b.tid < last_tid || (b.tid == last_tid && b.pos < last_pos)) { rc = -1; break; }
-        if (b.tid != last_tid) last_pos = -1;
+        /* a placed record after an unplaced one, or out of order: unsorted */
+        if (seen_unplaced || b.tid >= h.n_ref || b.tid < last_tid || (b.tid == last_tid && b.pos < last_pos)) {
+            rc = -1;
+            break;
+        }
+        if (b.tid != last_tid && last_tid >= 0) bai_racc_flush(R[last_tid]);
         last_tid = b.tid;
         last_pos = b.pos;
-        ref_acc *A = &R[b.tid];
-        const int32_t beg = b.pos < 0 ? 0 : b.pos, end = bam_end_pos(&b);
-        const uint32_t bin = (uint32_t)bam_reg2bin(beg, end);
-        if (run_tid >= 0 && (run_tid != b.tid || run_bin != bin)) acc_chunk(&R[run_tid], run_bin, run_beg, (uint64_t)off);
-        if (run_tid != b.tid || run_bin != bin) {
-            run_tid = b.tid;
-            run_bin = bin;
-            run_beg = (uint64_t)off;
-        }
-        /* linear index: the first record overlapping each 16 kb window */
-        const int w0 = beg >> 14, w1 = (end - 1) >> 14;
-        if (w1 >= A->n_lin) {
-            A->lin = (uint64_t *)realloc(A->lin, sizeof(uint64_t) * (w1 + 1));
-            for (int w = A->n_lin; w <= w1; w++) A->lin[w] = UINT64_MAX;
-            A->n_lin = w1 + 1;
-        }
-        for (int w = w0; w <= w1; w++)
-            if (A->lin[w] == UINT64_MAX) A->lin[w] = (uint64_t)off;
-        if (!A->any) A->off_beg = (uint64_t)off;
-        A->any = 1;
-        A->off_end = (uint64_t)end_off;
-        if (b.flag & 4) A->n_unmapped++;
-        else A->n_mapped++;
+        bai_racc_push(R[b.tid], b.pos < 0 ? 0 : b.pos, bam_end_pos(&b), (uint64_t)off, (uint64_t)end_off,
+                      (b.flag & 4) != 0);
         off = end_off;
     }
-    if (rc == 0 && run_tid >= 0) acc_chunk(&R[run_tid], run_bin, run_beg, (uint64_t)off);
     bam_free_rec(&b);
     bgzf_close_read(&r);
     if (rc == 0) {
         char path[4096];
         snprintf(path, sizeof(path), "%s.bai", bam_path);
-        FILE *f = fopen(path, "wb");
-        if (!f) rc = -1;
-        else {
-            fwrite("BAI\1", 1, 4, f);
-            put32(f, (uint32_t)h.n_ref);
-            for (int t = 0; t < h.n_ref; t++) {
-                ref_acc *A = &R[t];
-                qsort(A->bins, A->n_bins, sizeof(bin_acc), cmp_bin_acc);
-                put32(f, (uint32_t)(A->n_bins + (A->any ? 1 : 0)));
-                for (int i = 0; i < A->n_bins; i++) {
-                    put32(f, A->bins[i].bin);
-                    put32(f, (uint32_t)A->bins[i].n);
-                    for (int c = 0; c < A->bins[i].n; c++) {
-                        put64(f, A->bins[i].c[c].beg);
-                        put64(f, A->bins[i].c[c].end);
-                    }
-                }
-                if (A->any) {  /* pseudo-bin 37450: offset span, mapped/unmapped counts */
-                    put32(f, 37450u);
-                    put32(f, 2u);
-                    put64(f, A->off_beg);
-                    put64(f, A->off_end);
-                    put64(f, A->n_mapped);
-                    put64(f, A->n_unmapped);
-                }
-                /* empty windows take the offset of the window before them
-                 * (a smaller offset only makes a query read more) */
-                uint64_t prev = A->n_lin > 0 && A->lin[0] != UINT64_MAX ? A->lin[0] : 0;
-                for (int w = 0; w < A->n_lin; w++) {
-                    if (A->lin[w] == UINT64_MAX) A->lin[w] = prev;
-                    prev = A->lin[w];
-                }
-                put32(f, (uint32_t)A->n_lin);
-                for (int w = 0; w < A->n_lin; w++) put64(f, A->lin[w]);
-            }
-            put64(f, n_no_coor);
-            if (fclose(f) != 0) rc = -1;
-        }
+        rc = bai_write_racc(path, R, h.n_ref, n_no_coor, NULL, NULL);
     }
-    for (int t = 0; t < h.n_ref; t++) {
-        for (int i = 0; i < R[t].n_bins; i++) free(R[t].bins[i].c);
-        free(R[t].bins);
-        free(R[t].lin);
-    }
+    for (int t = 0; t < h.n_ref; t++) bai_racc_free(R[t]);
     free(R);
     bam_free_header(&h);
     return rc;

@@ -107,6 +107,12 @@ int bgzf_open_write(bgzf_writer *w, const char *path, int level);
 int bgzf_write(bgzf_writer *w, const void *src, int n);
 int bgzf_flush_block(bgzf_writer *w);
 int bgzf_close_write(bgzf_writer *w); /* writes the EOF marker block */
+/* one BGZF block of `len` (<= 0xff00) payload bytes into out (room for
+ * 65536 bytes); returns its size or -1.  Thread-safe. */
+int bgzf_block_compress(const unsigned char *in, int len, unsigned char *out, int level);
+/* the 28-byte BGZF end-of-file marker */
+const unsigned char *bgzf_eof_block(void);
+#define BGZF_PAYLOAD 0xff00
 
 int bam_read_header(bgzf_reader *r, bam_hdr *h);
 void bam_free_header(bam_hdr *h);
@@ -155,6 +161,19 @@ typedef struct {
  * (offset span, mapped/unmapped counts), the linear index, then the count of
  * unplaced reads; writes <bam>.bai.  0, or -1 (unsorted input, I/O error). */
 int bai_build(const char *bam_path);
+/* the same index built incrementally: one accumulator per reference fed
+ * its records in file order (start/end virtual offsets of each record),
+ * written with an optional offset map (the parallel writer records offsets
+ * as block index << 16 | offset in block and maps them once the compressed
+ * block sizes are known) */
+typedef struct bai_racc bai_racc;
+bai_racc *bai_racc_new(void);
+void bai_racc_push(bai_racc *A, int32_t beg, int32_t end, uint64_t voff_beg, uint64_t voff_end, int unmapped);
+void bai_racc_flush(bai_racc *A);
+void bai_racc_free(bai_racc *A);
+/* R[t] may be NULL (no records); 0 or -1 */
+int bai_write_racc(const char *path, bai_racc **R, int n_ref, uint64_t n_no_coor,
+                   uint64_t (*map)(void *ctx, int ref, uint64_t voff), void *ctx);
 /* parse an index file; 0, or -1 */
 int bai_load(const char *bai_path, bai_index *idx);
 void bai_free(bai_index *idx);

@@ -22,6 +22,7 @@
 #include "../../include/grom_amd.h"
 #include "bamio.h"
 #include "stream.h"
+#include "pdecode.h"
 
 static const char *VERSION = "GROM, Version 1.0.1\n"; /* g_version_name, GROM.c:690 */
 
@@ -145,6 +146,12 @@ typedef struct {
 
 static int g_plan_only = 0; /* GROM_PLAN_ONLY: report the record plan, no GPU */
 
+static double clock_gettime_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
 typedef struct {
     char *p;
     size_t len, cap;
@@ -259,118 +266,141 @@ static void ctx_postpass(const char *raw, size_t raw_len, const bam_hdr *hdr, in
     free(rw);
 }
 
-/* Scan one chromosome's batch on `device`; its VCF rows go to *text (malloc'd). */
-static int scan_batch(int device, chrom_plan *cp, grom_batch *b, const grom_params *P, char **text, size_t *text_len,
-                      char **ctx_text, size_t *ctx_len, int verbose) {
-    *text = NULL;
-    *text_len = 0;
-    *ctx_text = NULL;
-    *ctx_len = 0;
-    grom_batch_finish(b, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size);
-    if (g_plan_only) {
-        printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d\n", cp->name, cp->tid, (long long)b->n, b->n_skip,
-               b->p_last);
-        return GROM_OK;
+/* ---- one chromosome's scan, from either input path ----
+ * serial path: `batch` holds the chromosome's records in host memory;
+ * streamed path: `stage` holds them in HBM (pdecode.c) and `facts` the
+ * serial stream's facts about them. */
+typedef struct {
+    chrom_plan *cp;
+    grom_batch batch;
+    int has_batch;
+    grom_stage *stage;
+    pd_chrom_facts facts;
+    pd_session *pd;        /* releases the stage after the scan */
+    int device;            /* the GPU the stage lives on, -1: any */
+    char *text, *ctx_text;
+    size_t text_len, ctx_len;
+    int rc, ready, done, taken;
+    char err[512];
+} grom_job;
+
+static void write_dumps(int slot, const chrom_plan *cp, const grom_chrom *ch, const grom_reads *host_rd,
+                        grom_stage *stage, const grom_params *P) {
+    /* test hook: per-base counters and caf depth, same files as the oracle's */
+    const char *dump = getenv("GROM_DUMP");
+    int32_t first = 0;
+    int32_t lo = P->one_base_rd_len / 4 + 1;
+    if (lo < 2 * P->insert_max_size + 1) lo = 2 * P->insert_max_size + 1;
+    int64_t n_eval = (ch->p_last >= lo) ? (int64_t)ch->p_last - lo + 1 : 0;
+    int32_t *cnt = malloc(sizeof(int32_t) * GROM_NCOUNT * (n_eval > 0 ? n_eval : 1));
+    int32_t *caf = malloc(sizeof(int32_t) * 3 * cp->len);
+    int rc = stage ? grom_debug_counts_staged(slot, stage, ch, &first, cnt, GROM_NCOUNT * n_eval, caf)
+                   : grom_debug_counts(slot, ch, host_rd, &first, cnt, GROM_NCOUNT * n_eval, caf);
+    if (rc == GROM_OK) {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s.%s.cnt", dump, cp->name);
+        FILE *f = fopen(path, "wb");
+        if (f) { fwrite(cnt, sizeof(int32_t) * GROM_NCOUNT, n_eval, f); fclose(f); }
+        snprintf(path, sizeof(path), "%s.%s.caf", dump, cp->name);
+        f = fopen(path, "wb");
+        if (f) { fwrite(caf, sizeof(int32_t), 3 * cp->len, f); fclose(f); }
+        /* indel evidence of the same scan (row A7) */
+        int64_t n_ind = grom_debug_indels(slot, NULL, 0);
+        grom_indel_rec *ind = n_ind > 0 ? malloc(sizeof(grom_indel_rec) * n_ind) : NULL;
+        if (n_ind >= 0 && (n_ind == 0 || (ind && grom_debug_indels(slot, ind, n_ind) == n_ind))) {
+            snprintf(path, sizeof(path), "%s.%s.ind", dump, cp->name);
+            f = fopen(path, "wb");
+            if (f) { if (n_ind) fwrite(ind, sizeof(grom_indel_rec), n_ind, f); fclose(f); }
+        } else {
+            fprintf(stderr, "grom: indel dump of %s failed: %s\n", cp->name, grom_last_error());
+        }
+        free(ind);
+        /* breakpoint cluster records (rows A8/A9; the scan keeps them when
+         * GROM_SV_DEBUG is set) */
+        int64_t n_sv = grom_debug_sv(slot, NULL, 0);
+        grom_sv_rec *svr = n_sv > 0 ? malloc(sizeof(grom_sv_rec) * n_sv) : NULL;
+        if (n_sv >= 0 && (n_sv == 0 || (svr && grom_debug_sv(slot, svr, n_sv) == n_sv))) {
+            snprintf(path, sizeof(path), "%s.%s.sv", dump, cp->name);
+            f = fopen(path, "wb");
+            if (f) { if (n_sv) fwrite(svr, sizeof(grom_sv_rec), n_sv, f); fclose(f); }
+        }
+        free(svr);
+    } else {
+        fprintf(stderr, "grom: counter dump of %s failed: %s\n", cp->name, grom_last_error());
     }
+    free(cnt);
+    free(caf);
+}
+
+static uint32_t chrom_seed(void) {
+    /* srand(time()) per chromosome, GROM.c:1584; GROM_SEED pins it */
+    const char *e = getenv("GROM_SEED");
+    return e ? (uint32_t)strtoul(e, NULL, 10) : (uint32_t)time(NULL);
+}
+
+/* Scan one chromosome on context `slot`; its VCF rows go to j->text (malloc'd). */
+static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
+    chrom_plan *cp = j->cp;
+    j->text = j->ctx_text = NULL;
+    j->text_len = j->ctx_len = 0;
     grom_chrom ch;
     memset(&ch, 0, sizeof(ch));
-    ch.lseq_tail = b->lseq_tail;
+    grom_reads rd;
+    memset(&rd, 0, sizeof(rd));
+    int64_t n_reads;
+    if (j->has_batch) {
+        grom_batch *b = &j->batch;
+        grom_batch_finish(b, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size);
+        if (g_plan_only) {
+            grom_batch_view(b, &rd);
+            printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d lseq_tail=%d digest=%016llx\n", cp->name, cp->tid,
+                   (long long)b->n, b->n_skip, b->p_last, b->lseq_tail, (unsigned long long)pd_digest(&rd));
+            return GROM_OK;
+        }
+        ch.lseq_tail = b->lseq_tail;
+        ch.n_skip = b->n_skip;
+        ch.p_last = b->p_last;
+        grom_batch_view(b, &rd);
+        n_reads = b->n;
+    } else {
+        ch.lseq_tail = j->facts.lseq_tail;
+        ch.n_skip = j->facts.n_skip;
+        ch.p_last = j->facts.p_last;
+        n_reads = j->facts.n_reads;
+    }
     ch.ref = cp->ref;
     ch.len = cp->len;
     ch.name = cp->name;
     ch.tid = cp->tid;
-    ch.n_skip = b->n_skip;
-    ch.p_last = b->p_last;
     ch.cnv = cp->tid >= 0; /* detect_del_dup runs for a matched target, GROM.c:16633 */
-    {
-        /* srand(time()) per chromosome, GROM.c:1584; GROM_SEED pins it */
-        const char *e = getenv("GROM_SEED");
-        ch.seed = e ? (uint32_t)strtoul(e, NULL, 10) : (uint32_t)time(NULL);
-    }
-    grom_reads rd;
-    grom_batch_view(b, &rd);
+    ch.seed = chrom_seed();
     grom_out out = {0};
     grom_stats st = {0};
-    int rc = grom_scan_chrom(device, &ch, &rd, &out, &st);
+    int rc = j->has_batch ? grom_scan_chrom(slot, &ch, &rd, &out, &st)
+                          : grom_scan_chrom_staged(slot, j->stage, &ch, &out, &st);
     if (rc != GROM_OK) {
         fprintf(stderr, "grom: scan of %s failed: %s\n", cp->name, grom_last_error());
         grom_out_free(&out);
         return rc;
     }
-    *text = out.vcf;
-    *text_len = out.vcf_len;
-    out.vcf = NULL;
-    out.vcf_len = out.vcf_cap = 0;
-    *ctx_text = out.ctx; /* raw CTX rows for the translocation post-pass */
-    *ctx_len = out.ctx_len;
-    out.ctx = NULL;
-    out.ctx_len = out.ctx_cap = 0;
-    const char *dump = getenv("GROM_DUMP");
-    if (dump) {
-        /* test hook: per-base counters and caf depth, same files as the oracle's */
-        int32_t first = 0;
-        int32_t lo = P->one_base_rd_len / 4 + 1;
-        if (lo < 2 * P->insert_max_size + 1) lo = 2 * P->insert_max_size + 1;
-        int64_t n_eval = (ch.p_last >= lo) ? (int64_t)ch.p_last - lo + 1 : 0;
-        int32_t *cnt = malloc(sizeof(int32_t) * GROM_NCOUNT * (n_eval > 0 ? n_eval : 1));
-        int32_t *caf = malloc(sizeof(int32_t) * 3 * cp->len);
-        rc = grom_debug_counts(device, &ch, &rd, &first, cnt, GROM_NCOUNT * n_eval, caf);
-        if (rc == GROM_OK) {
-            char path[4096];
-            snprintf(path, sizeof(path), "%s.%s.cnt", dump, cp->name);
-            FILE *f = fopen(path, "wb");
-            if (f) { fwrite(cnt, sizeof(int32_t) * GROM_NCOUNT, n_eval, f); fclose(f); }
-            snprintf(path, sizeof(path), "%s.%s.caf", dump, cp->name);
-            f = fopen(path, "wb");
-            if (f) { fwrite(caf, sizeof(int32_t), 3 * cp->len, f); fclose(f); }
-            /* indel evidence of the same scan (row A7) */
-            int64_t n_ind = grom_debug_indels(device, NULL, 0);
-            grom_indel_rec *ind = n_ind > 0 ? malloc(sizeof(grom_indel_rec) * n_ind) : NULL;
-            if (n_ind >= 0 && (n_ind == 0 || (ind && grom_debug_indels(device, ind, n_ind) == n_ind))) {
-                snprintf(path, sizeof(path), "%s.%s.ind", dump, cp->name);
-                f = fopen(path, "wb");
-                if (f) { if (n_ind) fwrite(ind, sizeof(grom_indel_rec), n_ind, f); fclose(f); }
-            } else {
-                fprintf(stderr, "grom: indel dump of %s failed: %s\n", cp->name, grom_last_error());
-            }
-            free(ind);
-            /* breakpoint cluster records (rows A8/A9; the scan keeps them when
-             * GROM_SV_DEBUG is set) */
-            int64_t n_sv = grom_debug_sv(device, NULL, 0);
-            grom_sv_rec *svr = n_sv > 0 ? malloc(sizeof(grom_sv_rec) * n_sv) : NULL;
-            if (n_sv >= 0 && (n_sv == 0 || (svr && grom_debug_sv(device, svr, n_sv) == n_sv))) {
-                snprintf(path, sizeof(path), "%s.%s.sv", dump, cp->name);
-                f = fopen(path, "wb");
-                if (f) { if (n_sv) fwrite(svr, sizeof(grom_sv_rec), n_sv, f); fclose(f); }
-            }
-            free(svr);
-        } else {
-            fprintf(stderr, "grom: counter dump of %s failed: %s\n", cp->name, grom_last_error());
-        }
-        free(cnt);
-        free(caf);
-    }
+    j->text = out.vcf;
+    j->text_len = out.vcf_len;
+    j->ctx_text = out.ctx; /* raw CTX rows for the translocation post-pass */
+    j->ctx_len = out.ctx_len;
+    if (getenv("GROM_DUMP")) write_dumps(slot, cp, &ch, &rd, j->has_batch ? NULL : j->stage, P);
     if (verbose)
-        printf("%s: %lld reads, %.3f ms on GPU (%.2f Mbases/s)\n", cp->name, (long long)b->n, st.ms_total,
+        printf("%s: %lld reads, %.3f ms on GPU (%.2f Mbases/s)\n", cp->name, (long long)n_reads, st.ms_total,
                st.ms_total > 0 ? cp->len / (st.ms_total * 1e3) : 0.0);
-    grom_out_free(&out);
     return GROM_OK;
 }
 
 /* ---- multi-GPU: chromosomes shard across devices ----
  * The reference's -P forks one process per chromosome (GROM.c:328-624).  Here
- * -P n (or GROM_DEVICES) runs one host thread per GPU; the main thread keeps
- * reading the BAM once, in order, and hands each finished chromosome batch to
- * the next free GPU.  Rows are written in chromosome order, so the VCF is the
- * same bytes as a one-GPU run.  No data crosses devices. */
-typedef struct {
-    chrom_plan *cp;
-    grom_batch batch;
-    char *text, *ctx_text;
-    size_t text_len, ctx_len;
-    int rc, ready, done;
-    char err[512]; /* the worker's grom_last_error() when rc != GROM_OK */
-} grom_job;
+ * -P n (or GROM_DEVICES) runs GROM_SCANS_PER_GPU worker threads per GPU, each
+ * with its own library context.  Streamed input: every chromosome is staged
+ * on the GPU chosen for it (longest-processing-time over the index's record
+ * counts) and scanned by one of that GPU's workers.  Rows are written in
+ * chromosome order, so the VCF is the same bytes as a one-GPU run. */
 
 /* a finished chromosome: its VCF rows go out, its raw CTX rows are kept */
 static void take_rows(grom_job *j, FILE *vcf, textbuf *ctx_all) {
@@ -386,36 +416,46 @@ typedef struct {
     pthread_mutex_t mu;
     pthread_cond_t cv;
     grom_job *jobs;
-    int n_jobs, next_run, closing;
+    int n_jobs, closing;
     const grom_params *P;
     int verbose;
 } grom_pool;
 
 typedef struct {
     grom_pool *pool;
-    int slot; /* the worker's own library context (grom_ctx_init), on some GPU */
+    int slot;   /* the worker's own library context (grom_ctx_init) */
+    int device; /* its GPU */
 } grom_worker;
 
 static void *grom_worker_main(void *arg) {
     grom_worker *w = (grom_worker *)arg;
     grom_pool *pl = w->pool;
+    int cur = 0; /* jobs before `cur` are taken or belong to other GPUs */
     for (;;) {
         pthread_mutex_lock(&pl->mu);
-        while (!(pl->next_run < pl->n_jobs && pl->jobs[pl->next_run].ready) && !pl->closing)
+        grom_job *j = NULL;
+        for (;;) {
+            while (cur < pl->n_jobs && pl->jobs[cur].ready &&
+                   (pl->jobs[cur].taken || (pl->jobs[cur].device >= 0 && pl->jobs[cur].device != w->device)))
+                cur++;
+            if (cur < pl->n_jobs && pl->jobs[cur].ready) { j = &pl->jobs[cur]; break; }
+            if (pl->closing) break;
             pthread_cond_wait(&pl->cv, &pl->mu);
-        if (!(pl->next_run < pl->n_jobs && pl->jobs[pl->next_run].ready)) {
+        }
+        if (!j) {
             pthread_mutex_unlock(&pl->mu);
             break;
         }
-        grom_job *j = &pl->jobs[pl->next_run++];
+        j->taken = 1;
         pthread_mutex_unlock(&pl->mu);
         /* contexts are independent: workers sharing a GPU scan concurrently */
-        int rc = scan_batch(w->slot, j->cp, &j->batch, pl->P, &j->text, &j->text_len, &j->ctx_text, &j->ctx_len,
-                            pl->verbose);
+        int rc = scan_job(w->slot, j, pl->P, pl->verbose);
         if (rc != GROM_OK) snprintf(j->err, sizeof(j->err), "%s: %s", j->cp->name, grom_last_error());
         free(j->cp->ref);
         j->cp->ref = NULL;
-        grom_batch_free(&j->batch);
+        if (j->has_batch) grom_batch_free(&j->batch);
+        if (j->stage && j->pd) pd_release_stage(j->pd, j->stage);
+        j->stage = NULL;
         pthread_mutex_lock(&pl->mu);
         j->rc = rc;
         j->done = 1;
@@ -425,283 +465,268 @@ static void *grom_worker_main(void *arg) {
     return NULL;
 }
 
-int grom_cli_main(int argc, char **argv) {
-    optind = 0; /* GNU getopt: 0 fully re-initialises, so this is callable again */
-    setlinebuf(stdout);
+/* everything the two input paths share */
+typedef struct {
     grom_params P;
-    grom_default_params(&P);
-    const char *bam_name = NULL, *fasta_name = NULL, *out_name = NULL;
-    long max_chr_len = 300000000; /* g_max_chr_fasta_len, GROM.c:946 */
-    double num_sd = 3;
-    int device = 0, verbose = getenv("GROM_VERBOSE") != NULL, n_dev = 1;
-    if (getenv("GROM_DEVICE")) device = atoi(getenv("GROM_DEVICE"));
-    int opt;
-    /* getopt string of GROM.c:21908 */
-    while ((opt = getopt(argc, argv,
-                         "Z:W:X:Q:A:Y:B:D:E:K:N:V:U:L:F:SP:c:R:MG:i:r:o:p:q:s:v:g:l:d:b:n:a:y:z:e:fj:k:m:u:w:x:h")) != -1) {
-        switch (opt) {
-        case 'S': P.splitread = 0; break;
-        case 'G': P.sv_list_len = atoi(optarg); break;
-        case 'M': P.rmdup = 1; break;
-        case 'i': bam_name = optarg; break;
-        case 'r': fasta_name = optarg; break;
-        case 'o': out_name = optarg; break;
-        case 'B': max_chr_len = atol(optarg); break;
-        case 'p': P.ploidy = atoi(optarg); break;
-        case 'q': P.min_mapq = atoi(optarg); break;
-        case 's': num_sd = atof(optarg); break;
-        case 'g': P.gender = atoi(optarg); break;
-        case 'l': P.overlap_mult = atoi(optarg); break;
-        case 'b': P.min_base_qual = atoi(optarg); break;
-        case 'n': P.min_snv = atoi(optarg); break;
-        case 'a': P.min_snv_ratio = atof(optarg); break;
-        case 'f': P.vcf = 0; break;
-        case 'x': P.min_ave_bq = atof(optarg); break;
-        case 'P': n_dev = atoi(optarg); break; /* -P threads -> GPUs, GROM.c:21930 */
-        case 'Z': P.block_min = atol(optarg); break;
-        case 'W': P.min_rd_window_len = atol(optarg); break;
-        case 'X': P.max_rd_window_len = atol(optarg); break;
-        case 'A': P.windows_sampling_factor = atol(optarg); break;
-        case 'Y': P.min_blocks = atol(optarg); break;
-        case 'D': P.min_repeat = atol(optarg); break;
-        case 'E': P.min_repeat_stdev = atof(optarg); break;
-        case 'K': P.ranks_stdev = atoi(optarg); break;
-        case 'V': P.rd_pval_threshold = atof(optarg); break;
-        case 'U': P.chr_rd_threshold_factor = atoi(optarg); break;
-        case 'L': P.dup_threshold_factor = atol(optarg); break;
-        case 'F': P.mapq_factor = atof(optarg); break;
-        case 'v': P.pval_threshold = atof(optarg); break;
-        case 'd': P.min_disc = atoi(optarg); break;
-        case 'y': P.max_split_loss = atoi(optarg); break;
-        case 'z': P.min_sr_len = atoi(optarg); break;
-        case 'e': P.pval_insertion = atof(optarg); break;
-        case 'j': P.min_sv_ratio = atof(optarg); break;
-        case 'k': P.max_homopolymer = atoi(optarg); break;
-        case 'm': P.min_indel_ratio = atof(optarg); break;
-        case 'u': P.max_evidence_ratio = atof(optarg); break;
-        case 'w': P.max_ins_range = atoi(optarg); break;
-        case 'N':
-            if (atol(optarg) > 0) {
-                printf("ERROR: -N (.1000gen side file) is not supported by this build\n");
-                return 1;
-            }
-            break;
-        case 'h': print_help(); return 0;
-        case '?': return 1;
-        default: break; /* accepted; steers rows outside the implemented scan */
-        }
-    }
-    P.rd_min_mapq = P.min_mapq;         /* GROM.c:22102 */
-    P.pval_threshold1 = P.pval_threshold; /* GROM.c:22101 */
-    P.sv_list2_len = P.sv_list_len / 10;  /* GROM.c:21925 */
-    printf("bam %s\n", bam_name ? bam_name : "(null)");
-    printf("ref %s\n", fasta_name ? fasta_name : "(null)");
-    printf("results %s\n", out_name ? out_name : "(null)");
-    if (!bam_name) { printf("ERROR: No bam file specified.\n"); return 1; }
-    bgzf_reader br;
+    const char *bam_name, *fasta_name, *out_name;
+    long max_chr_len;
+    double num_sd;
+    int device, verbose, n_dev;
     bam_hdr hdr;
-    if (bgzf_open_read(&br, bam_name) != 0 || bam_read_header(&br, &hdr) != 0) {
-        printf("\nCould not open %s\n", bam_name);
-        return 1;
-    }
-    if (!bai_loads(bam_name)) { printf("Could not open BAM indexing file\n"); return 1; }
-    if (!out_name) { printf("ERROR: No output file specified.\n"); return 1; }
-    FILE *probe = fopen(out_name, "w");
-    if (!probe) { printf("\nCould not open %s\n", out_name); return 1; }
-    fclose(probe);
-    if (!fasta_name) { printf("ERROR: No reference file specified.\n"); return 1; }
     grom_fasta fa;
-    if (grom_fasta_open_cached(&fa, fasta_name) != 0) { printf("\nCould not open %s\n", fasta_name); return 1; }
+    double *hez, *mq;
+    pthread_t tables_thr;
+    int tables_started;
+    chrom_plan *plan; /* candidates in BAM order (preliminary: before the length test) */
+    int n_cand;
+    char ctx_name[4096];
+    int wdev[64], n_work, n_init;
+} cli_state;
 
-    /* tables (read_binom_tables, GROM.c:22234) */
-    size_t tn = (size_t)(GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);
-    double *hez = malloc(sizeof(double) * tn), *mq = malloc(sizeof(double) * tn);
-    grom_build_tables(P.min_mapq, hez, mq);
+#define CLI_FALLBACK 99 /* the streamed path could not be used: read serially */
 
-    /* insert-size pre-pass on the first records (GROM.c:22255) */
-    int lseq = 0, imin = 0, imax = 0;
-    long mapped = 0;
-    int imean = grom_insert_stats(&br, grom_prob2(num_sd), &lseq, &imin, &imax, &mapped, P.min_mapq);
-    bgzf_close_read(&br);
-    if (imean < 0) { printf("ERROR: no reads to estimate the insert size from\n"); return 1; }
-    printf("insert_min_size, insert_max_size %d %d\n", imin, imax);
-    {
-        char mean_name[4096];
-        snprintf(mean_name, sizeof(mean_name), "%s.mean", bam_name);
-        FILE *mf = fopen(mean_name, "w"); /* save_insert_mean, GROM.c:994-1008 */
-        if (mf) {
-            printf("Saving insert_mean et al to %s\n", mean_name);
-            fprintf(mf, "%d %d %d %d %ld\n", imean, lseq, imin, imax, mapped);
-            fclose(mf);
-        }
-    }
-    grom_params_set_insert(&P, imean, imin, imax, lseq);
-    printf("insert mean, insert minimum, insert maximum: %d %d %d\n", P.insert_mean, imin, imax);
-    printf("median read length: %d\n", lseq);
+static void *tables_main(void *arg) {
+    cli_state *S = (cli_state *)arg;
+    grom_build_tables(S->P.min_mapq, S->hez, S->mq); /* read_binom_tables, GROM.c:22234 */
+    return NULL;
+}
 
-    g_plan_only = getenv("GROM_PLAN_ONLY") != NULL;
-    if (getenv("GROM_DEVICES")) n_dev = atoi(getenv("GROM_DEVICES"));
-    if (n_dev < 1) n_dev = 1;
-    if (!g_plan_only && n_dev > 1) {
+static void tables_join(cli_state *S) {
+    if (S->tables_started) pthread_join(S->tables_thr, NULL);
+    S->tables_started = 0;
+}
+
+/* worker contexts: GROM_SCANS_PER_GPU (default 2) per GPU, so two
+ * chromosomes are in flight on every GPU; GROM_WORKER_DEVICES=0,0,0 runs
+ * three workers on device 0 (test hook) */
+static int setup_workers(cli_state *S) {
+    grom_params *P = &S->P;
+    if (getenv("GROM_DEVICES")) S->n_dev = atoi(getenv("GROM_DEVICES"));
+    if (S->n_dev < 1) S->n_dev = 1;
+    if (!g_plan_only && S->n_dev > 1) {
         int avail = grom_device_count();
-        if (avail < 1) { fprintf(stderr, "grom: no GPU\n"); return 1; }
-        if (n_dev > avail - device) n_dev = avail - device;
-        if (n_dev < 1) n_dev = 1;
+        if (avail < 1) { fprintf(stderr, "grom: no GPU\n"); return -1; }
+        if (S->n_dev > avail - S->device) S->n_dev = avail - S->device;
+        if (S->n_dev < 1) S->n_dev = 1;
     }
-    /* GROM_SCANS_PER_GPU (default 2) workers per GPU, each with its own
-     * context, so two chromosomes are in flight on every GPU;
-     * test hook: GROM_WORKER_DEVICES=0,0,0 runs three workers on device 0 */
     int per_gpu = getenv("GROM_SCANS_PER_GPU") ? atoi(getenv("GROM_SCANS_PER_GPU")) : 2;
-    if (n_dev > 64) n_dev = 64;
+    if (S->n_dev > 64) S->n_dev = 64;
     if (per_gpu < 1) per_gpu = 1;
-    if (per_gpu * n_dev > 64) per_gpu = 64 / n_dev;
+    if (per_gpu * S->n_dev > 64) per_gpu = 64 / S->n_dev;
     if (per_gpu < 1) per_gpu = 1;
     /* a second context per GPU doubles the scan's device buffers: keep it
      * only when the free HBM holds per_gpu scans of the longest chromosome
      * (about 64 B per base at 30x) */
     if (per_gpu > 1 && !g_plan_only) {
         long longest = 0;
-        for (int i = 0; i < fa.n; i++)
-            if (fa.len[i] > longest) longest = fa.len[i];
+        for (int i = 0; i < S->fa.n; i++)
+            if (S->fa.len[i] > longest) longest = S->fa.len[i];
         const double need = 64.0 * (double)longest;
-        for (int d = 0; d < n_dev; d++) {
-            int64_t fr = grom_device_mem_free(device + d);
+        for (int d = 0; d < S->n_dev; d++) {
+            int64_t fr = grom_device_mem_free(S->device + d);
             if (fr >= 0 && (double)fr < need * per_gpu) {
                 int fit = (int)((double)fr / need);
                 per_gpu = fit < 1 ? 1 : (fit < per_gpu ? fit : per_gpu);
             }
         }
     }
-    int wdev[64], n_work = n_dev * per_gpu;
-    for (int d = 0; d < 64; d++) wdev[d] = device + d % n_dev;
+    S->n_work = S->n_dev * per_gpu;
+    for (int d = 0; d < 64; d++) S->wdev[d] = S->device + d % S->n_dev;
     if (getenv("GROM_WORKER_DEVICES")) {
         char *sdup = strdup(getenv("GROM_WORKER_DEVICES")), *tok = strtok(sdup, ",");
-        n_work = 0;
-        while (tok && n_work < 64) { wdev[n_work++] = atoi(tok); tok = strtok(NULL, ","); }
+        S->n_work = 0;
+        while (tok && S->n_work < 64) { S->wdev[S->n_work++] = atoi(tok); tok = strtok(NULL, ","); }
         free(sdup);
-        if (n_work < 1) { wdev[0] = device; n_work = 1; }
+        if (S->n_work < 1) { S->wdev[0] = S->device; S->n_work = 1; }
     }
-    int rc = GROM_OK, n_init = 0;
-    for (int d = 0; d < n_work && !g_plan_only && rc == GROM_OK; d++) {
-        rc = grom_ctx_init(d, wdev[d], &P, hez, mq);
-        if (rc == GROM_OK) n_init = d + 1;
+    tables_join(S);
+    int rc = GROM_OK;
+    for (int d = 0; d < S->n_work && !g_plan_only && rc == GROM_OK; d++) {
+        rc = grom_ctx_init(d, S->wdev[d], P, S->hez, S->mq);
+        if (rc == GROM_OK) S->n_init = d + 1;
     }
-    #define CLI_FAIL()                                                                             \
-        do {                                                                                       \
-            for (int d_ = 0; d_ < n_init; d_++) grom_dev_fini(d_);                                 \
-            return 1;                                                                              \
-        } while (0)
-    if (rc != GROM_OK) { fprintf(stderr, "grom: %s\n", grom_last_error()); CLI_FAIL(); }
+    if (rc != GROM_OK) { fprintf(stderr, "grom: %s\n", grom_last_error()); return -1; }
+    return 0;
+}
 
-    /* chromosome selection in BAM header order (GROM.c:20826-21050) */
-    const int32_t s0 = P.one_base_rd_len / 4 + 1;
-    chrom_plan *plan = calloc(hdr.n_ref > 0 ? hdr.n_ref : 1, sizeof(chrom_plan));
-    int32_t *order = calloc(hdr.n_ref > 0 ? hdr.n_ref : 1, sizeof(int32_t));
+static void print_insert(cli_state *S, int imean, int lseq, int imin, int imax, long mapped) {
+    printf("insert_min_size, insert_max_size %d %d\n", imin, imax);
+    char mean_name[4096];
+    snprintf(mean_name, sizeof(mean_name), "%s.mean", S->bam_name);
+    FILE *mf = fopen(mean_name, "w"); /* save_insert_mean, GROM.c:994-1008 */
+    if (mf) {
+        printf("Saving insert_mean et al to %s\n", mean_name);
+        fprintf(mf, "%d %d %d %d %ld\n", imean, lseq, imin, imax, mapped);
+        fclose(mf);
+    }
+    grom_params_set_insert(&S->P, imean, imin, imax, lseq);
+    printf("insert mean, insert minimum, insert maximum: %d %d %d\n", S->P.insert_mean, imin, imax);
+    printf("median read length: %d\n", lseq);
+}
+
+/* find_disc_svs' length test (GROM.c:20826-21050), needs the insert size */
+static int passes_length(const cli_state *S, const chrom_plan *c) {
+    const int32_t s0 = S->P.one_base_rd_len / 4 + 1;
+    if (c->len > S->max_chr_len)
+        printf("ERROR: Reference chromosome length exceeds maximum allowed chromosome size (%ld)\n", S->max_chr_len);
+    if (!(c->len > s0 + (long)S->P.overlap_mult * S->P.insert_max_size)) return 0;
+    if (!(c->len > 0 && c->len <= S->max_chr_len)) return 0;
+    return 1;
+}
+
+static void finish_outputs(cli_state *S, textbuf *ctx_all) {
+    /* CTX post-pass (GROM.c:22400-22770): pair the translocation rows of all
+     * chromosomes with their mates and write them under the header */
+    FILE *ctx = fopen(S->ctx_name, "w");
+    if (ctx) {
+        if (S->P.vcf == 1) {
+            header(ctx, S->fasta_name, 1);
+            ctx_postpass(ctx_all->p, ctx_all->len, &S->hdr, S->P.insert_max_size, S->P.lseq, ctx);
+        }
+        fclose(ctx);
+    }
+}
+
+/* rows of finished jobs, in chromosome order (caller holds pool.mu) */
+static void drain_rows(grom_pool *pool, int *next_write, int upto, FILE *vcf, textbuf *ctx_all, int *status) {
+    while (*next_write < upto && pool->jobs[*next_write].done) {
+        grom_job *j = &pool->jobs[(*next_write)++];
+        pthread_mutex_unlock(&pool->mu);
+        if (j->rc != GROM_OK) *status = 1;
+        take_rows(j, vcf, ctx_all);
+        pthread_mutex_lock(&pool->mu);
+    }
+}
+
+static void pool_start(grom_pool *pool, cli_state *S, int n_jobs, grom_worker **workers, pthread_t **tids) {
+    memset(pool, 0, sizeof(*pool));
+    pthread_mutex_init(&pool->mu, NULL);
+    pthread_cond_init(&pool->cv, NULL);
+    pool->jobs = calloc(n_jobs > 0 ? n_jobs : 1, sizeof(grom_job));
+    pool->n_jobs = n_jobs;
+    pool->P = &S->P;
+    pool->verbose = S->verbose;
+    *workers = calloc(S->n_work, sizeof(grom_worker));
+    *tids = calloc(S->n_work, sizeof(pthread_t));
+    for (int d = 0; d < S->n_work; d++) {
+        (*workers)[d].pool = pool;
+        (*workers)[d].slot = d;
+        (*workers)[d].device = S->wdev[d];
+        pthread_create(&(*tids)[d], NULL, grom_worker_main, &(*workers)[d]);
+    }
+}
+
+/* close the pool: wait for every job, write the remaining rows */
+static void pool_finish(grom_pool *pool, cli_state *S, grom_worker *workers, pthread_t *tids, int *next_write,
+                        FILE *vcf, textbuf *ctx_all, int *status) {
+    pthread_mutex_lock(&pool->mu);
+    pool->closing = 1;
+    pthread_cond_broadcast(&pool->cv);
+    for (;;) {
+        drain_rows(pool, next_write, pool->n_jobs, vcf, ctx_all, status);
+        int busy = 0;
+        for (int j = *next_write; j < pool->n_jobs; j++)
+            if (pool->jobs[j].ready && !pool->jobs[j].done) busy = 1;
+        if (!busy) break;
+        pthread_cond_wait(&pool->cv, &pool->mu);
+    }
+    pthread_mutex_unlock(&pool->mu);
+    for (int d = 0; d < S->n_work; d++) pthread_join(tids[d], NULL);
+    for (int j = 0; j < pool->n_jobs; j++)
+        if (pool->jobs[j].ready && pool->jobs[j].rc != GROM_OK) { grom_set_last_error(pool->jobs[j].err); *status = 1; break; }
+    free(tids);
+    free(workers);
+    free(pool->jobs);
+    pthread_mutex_destroy(&pool->mu);
+    pthread_cond_destroy(&pool->cv);
+}
+
+/* ---------------- serial input: one pass over the record stream ---------------- */
+static int run_serial(cli_state *S) {
+    grom_params *P = &S->P;
+    bgzf_reader br;
+    if (bgzf_open_read(&br, S->bam_name) != 0) return 1;
+    {
+        bam_hdr h2;
+        if (bam_read_header(&br, &h2) != 0) { bgzf_close_read(&br); return 1; }
+        bam_free_header(&h2);
+    }
+    /* insert-size pre-pass on the first records (GROM.c:22255) */
+    int lseq = 0, imin = 0, imax = 0;
+    long mapped = 0;
+    int imean = grom_insert_stats(&br, grom_prob2(S->num_sd), &lseq, &imin, &imax, &mapped, P->min_mapq);
+    bgzf_close_read(&br);
+    if (imean < 0) { printf("ERROR: no reads to estimate the insert size from\n"); return 1; }
+    print_insert(S, imean, lseq, imin, imax, mapped);
+    if (setup_workers(S)) return 1;
+    /* the final plan: candidates that pass the length test */
+    const int32_t s0 = P->one_base_rd_len / 4 + 1;
+    chrom_plan **plan = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(chrom_plan *));
+    int32_t *order = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int32_t));
     int n_plan = 0;
-    for (int t = 0; t < hdr.n_ref; t++) {
-        int fi = grom_match_target(&fa, hdr.ref_name[t]);
-        char lc[GROM_MAX_CHR_NAMES];
-        int bl = grom_target_name_lc(hdr.ref_name[t], lc, (int)sizeof(lc));
-        if (P.gender == 0 && ((bl == 4 && strncmp(lc, "chry", 4) == 0) || (bl == 1 && lc[0] == 'y'))) fi = -1;
-        if (fi < 0) continue;
-        long len = grom_fasta_load(&fa, fi, NULL, 0);
-        if (len > max_chr_len) printf("ERROR: Reference chromosome length exceeds maximum allowed chromosome size (%ld)\n", max_chr_len);
-        if (!(len > s0 + (long)P.overlap_mult * P.insert_max_size)) continue;
-        if (!(len > 0 && len <= max_chr_len)) continue;
-        /* count_discordant_pairs re-derives the BAM target from the FASTA name
-         * (GROM.c:1894-1961): the first target matching it */
-        int32_t tid2 = -1;
-        for (int a = 0; a < hdr.n_ref; a++)
-            if (grom_match_target(&fa, hdr.ref_name[a]) == fi) { tid2 = a; break; }
-        plan[n_plan].fasta_idx = fi;
-        plan[n_plan].tid = tid2;
-        plan[n_plan].len = len;
-        /* the name loop leaves the last target's name when nothing matches */
-        plan[n_plan].target = strdup(hdr.n_ref > 0 ? hdr.ref_name[tid2 >= 0 ? tid2 : hdr.n_ref - 1] : "");
-        snprintf(plan[n_plan].name, sizeof(plan[n_plan].name), "%.*s", fa.name_len[fi], fa.names[fi]);
-        order[n_plan] = tid2;
-        n_plan++;
-    }
-
-    FILE *vcf = fopen(out_name, "w");
-    if (!vcf) { printf("Error opening file %s\n", out_name); CLI_FAIL(); }
-    if (P.vcf == 1) header(vcf, fasta_name, 0);
-    char ctx_name[4096];
-    size_t ol = strlen(out_name);
-    if (ol > 4 && strcmp(out_name + ol - 4, ".vcf") == 0)
-        snprintf(ctx_name, sizeof(ctx_name), "%.*s.ctx.vcf", (int)(ol - 4), out_name);
-    else
-        snprintf(ctx_name, sizeof(ctx_name), "%s.ctx", out_name);
-
+    for (int c = 0; c < S->n_cand; c++)
+        if (passes_length(S, &S->plan[c])) {
+            order[n_plan] = S->plan[c].tid;
+            plan[n_plan++] = &S->plan[c];
+        }
+    FILE *vcf = fopen(S->out_name, "w");
+    if (!vcf) { printf("Error opening file %s\n", S->out_name); free(plan); free(order); return 1; }
+    if (P->vcf == 1) header(vcf, S->fasta_name, 0);
     /* one serial pass over the records, split per chromosome (stream.h);
      * finished chromosomes go to the GPU workers, rows are written in order */
-    bam_free_header(&hdr);
-    if (bgzf_open_read(&br, bam_name) != 0) { fclose(vcf); CLI_FAIL(); }
+    if (bgzf_open_read(&br, S->bam_name) != 0) { fclose(vcf); free(plan); free(order); return 1; }
     {
         /* BGZF blocks inflate on GROM_DECODE_THREADS threads (default 4) while
          * this thread parses records in order (htslib's bgzf_mt) */
         const char *dt = getenv("GROM_DECODE_THREADS");
         const int n_dec = dt ? atoi(dt) : 4;
-        if (bgzf_set_threads(&br, n_dec) != 0) { fclose(vcf); CLI_FAIL(); }
+        if (bgzf_set_threads(&br, n_dec) != 0) { bgzf_close_read(&br); fclose(vcf); free(plan); free(order); return 1; }
     }
-    if (bam_read_header(&br, &hdr) != 0) { fclose(vcf); CLI_FAIL(); }
+    {
+        bam_hdr h2;
+        if (bam_read_header(&br, &h2) != 0) { bgzf_close_read(&br); fclose(vcf); free(plan); free(order); return 1; }
+        bam_free_header(&h2);
+    }
     grom_planner pl;
     grom_planner_init(&pl, order, n_plan);
     grom_batch batch;
     int cur = 0;
     int batch_ended = 0; /* the record after the chromosome's last one was seen */
     if (n_plan > 0) {
-        grom_batch_init(&batch, order[0], P.read_name_len);
-        grom_batch_set_sv(&batch, plan[0].target, P.splitread);
+        grom_batch_init(&batch, order[0], P->read_name_len);
+        grom_batch_set_sv(&batch, plan[0]->target, P->splitread);
     }
     bam_rec rec;
     memset(&rec, 0, sizeof(rec));
-    int status = 0;
+    int status = 0, next_write = 0;
     grom_pool pool;
-    memset(&pool, 0, sizeof(pool));
-    pthread_mutex_init(&pool.mu, NULL);
-    pthread_cond_init(&pool.cv, NULL);
-    pool.jobs = calloc(n_plan > 0 ? n_plan : 1, sizeof(grom_job));
-    pool.n_jobs = n_plan;
-    pool.P = &P;
-    pool.verbose = verbose;
-    grom_worker *workers = calloc(n_work, sizeof(grom_worker));
-    pthread_t *tids = calloc(n_work, sizeof(pthread_t));
-    for (int d = 0; d < n_work; d++) {
-        workers[d].pool = &pool;
-        workers[d].slot = d;
-        pthread_create(&tids[d], NULL, grom_worker_main, &workers[d]);
-    }
-    int next_write = 0;
+    grom_worker *workers;
+    pthread_t *tids;
+    pool_start(&pool, S, n_plan, &workers, &tids);
     textbuf ctx_all = {0};
     /* hand chromosome `cur` (its batch complete) to the workers; at most one
-     * decoded chromosome waits beyond those being scanned (n_work + 1 batches
-     * in host memory), finished rows are written in order */
+     * decoded chromosome waits beyond those being scanned */
     #define SUBMIT_CUR()                                                                           \
         do {                                                                                       \
-            plan[cur].ref = malloc(plan[cur].len + 1);                                             \
-            grom_fasta_load(&fa, plan[cur].fasta_idx, plan[cur].ref, plan[cur].len);               \
+            plan[cur]->ref = malloc(plan[cur]->len + 1);                                           \
+            grom_fasta_load(&S->fa, plan[cur]->fasta_idx, plan[cur]->ref, plan[cur]->len);         \
             pthread_mutex_lock(&pool.mu);                                                          \
-            pool.jobs[cur].cp = &plan[cur];                                                        \
+            pool.jobs[cur].cp = plan[cur];                                                         \
             pool.jobs[cur].batch = batch;                                                          \
+            pool.jobs[cur].has_batch = 1;                                                          \
+            pool.jobs[cur].device = -1;                                                            \
             pool.jobs[cur].ready = 1;                                                              \
             pthread_cond_broadcast(&pool.cv);                                                      \
             for (;;) {                                                                             \
-                while (next_write <= cur && pool.jobs[next_write].done) {                          \
-                    grom_job *j = &pool.jobs[next_write++];                                        \
-                    pthread_mutex_unlock(&pool.mu);                                                \
-                    if (j->rc != GROM_OK) status = 1;                                              \
-                    take_rows(j, vcf, &ctx_all);                                                   \
-                    pthread_mutex_lock(&pool.mu);                                                  \
-                }                                                                                  \
-                if (cur + 1 - next_write < n_work + 1) break;                                      \
+                drain_rows(&pool, &next_write, cur + 1, vcf, &ctx_all, &status);                   \
+                if (cur + 1 - next_write < S->n_work + 1) break;                                   \
                 pthread_cond_wait(&pool.cv, &pool.mu);                                             \
             }                                                                                      \
             pthread_mutex_unlock(&pool.mu);                                                        \
             cur++;                                                                                 \
             if (cur < n_plan) {                                                                    \
-                grom_batch_init(&batch, order[cur], P.read_name_len);                              \
-                grom_batch_set_sv(&batch, plan[cur].target, P.splitread);                          \
+                grom_batch_init(&batch, order[cur], P->read_name_len);                             \
+                grom_batch_set_sv(&batch, plan[cur]->target, P->splitread);                        \
                 batch_ended = 0;                                                                   \
             }                                                                                      \
         } while (0)
@@ -719,49 +744,423 @@ int grom_cli_main(int argc, char **argv) {
     /* end of file: the chromosome being read and every later one */
     while (cur < n_plan) SUBMIT_CUR();
     #undef SUBMIT_CUR
-    pthread_mutex_lock(&pool.mu);
-    pool.closing = 1;
-    pthread_cond_broadcast(&pool.cv);
-    while (next_write < n_plan) {
-        if (pool.jobs[next_write].done) {
-            grom_job *j = &pool.jobs[next_write++];
-            if (j->rc != GROM_OK) status = 1;
-            take_rows(j, vcf, &ctx_all);
-        } else {
-            pthread_cond_wait(&pool.cv, &pool.mu);
-        }
-    }
-    pthread_mutex_unlock(&pool.mu);
-    for (int d = 0; d < n_work; d++) pthread_join(tids[d], NULL);
-    for (int j = 0; j < n_plan; j++)
-        if (pool.jobs[j].rc != GROM_OK) { grom_set_last_error(pool.jobs[j].err); break; }
-    free(tids);
-    free(workers);
-    free(pool.jobs);
-    pthread_mutex_destroy(&pool.mu);
-    pthread_cond_destroy(&pool.cv);
+    pool_finish(&pool, S, workers, tids, &next_write, vcf, &ctx_all, &status);
     bam_free_rec(&rec);
     bgzf_close_read(&br);
     fclose(vcf);
-    /* CTX post-pass (GROM.c:22400-22770): pair the translocation rows of all
-     * chromosomes with their mates and write them under the header */
-    FILE *ctx = fopen(ctx_name, "w");
-    if (ctx) {
-        if (P.vcf == 1) {
-            header(ctx, fasta_name, 1);
-            ctx_postpass(ctx_all.p, ctx_all.len, &hdr, P.insert_max_size, P.lseq, ctx);
-        }
-        fclose(ctx);
-    }
+    finish_outputs(S, &ctx_all);
     free(ctx_all.p);
-    for (int i = 0; i < n_plan; i++) free(plan[i].target);
-    for (int d = 0; d < n_init; d++) grom_dev_fini(d);
-    #undef CLI_FAIL
-    grom_fasta_close(&fa);
-    bam_free_header(&hdr);
     free(plan);
     free(order);
-    free(hez);
-    free(mq);
     return status;
+}
+
+/* ---------------- streamed input: parallel decode -> pinned pieces -> HBM ---------------- */
+typedef struct {
+    cli_state *S;
+    chrom_plan **plan;
+    int n_plan;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int loaded, consumed, stop; /* refs loaded ahead of the consumer, at most `ahead` */
+    int ahead;
+} fasta_feed;
+
+/* find_disc_svs loads each chromosome in order (GROM.c:21009-21045); here a
+ * thread does it ahead of the scans */
+static void *fasta_main(void *arg) {
+    fasta_feed *F = (fasta_feed *)arg;
+    for (int k = 0; k < F->n_plan; k++) {
+        pthread_mutex_lock(&F->mu);
+        while (!F->stop && k >= F->consumed + F->ahead) pthread_cond_wait(&F->cv, &F->mu);
+        const int stop = F->stop;
+        pthread_mutex_unlock(&F->mu);
+        if (stop) break;
+        chrom_plan *c = F->plan[k];
+        c->ref = malloc(c->len + 1);
+        if (c->ref) grom_fasta_load(&F->S->fa, c->fasta_idx, c->ref, c->len);
+        pthread_mutex_lock(&F->mu);
+        F->loaded = k + 1;
+        pthread_cond_broadcast(&F->cv);
+        pthread_mutex_unlock(&F->mu);
+    }
+    return NULL;
+}
+
+static int run_streamed(cli_state *S) {
+    grom_params *P = &S->P;
+    const double t_start = clock_gettime_s();
+    /* the preliminary plan: every candidate (the length test needs the
+     * insert size, which the same decode measures) */
+    pd_chrom_in *cin = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(pd_chrom_in));
+    for (int c = 0; c < S->n_cand; c++) {
+        cin[c].tid = S->plan[c].tid;
+        cin[c].target_name = S->plan[c].target;
+    }
+    const char *dt = getenv("GROM_DECODE_THREADS");
+    long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    int n_thr = dt ? atoi(dt) : (int)(ncpu < 16 ? ncpu : 16);
+    if (n_thr < 1) n_thr = 1;
+    char why[256] = "";
+    pd_session *pd = pd_open(S->bam_name, &S->hdr, cin, S->n_cand, P->splitread, P->read_name_len, n_thr, why,
+                             (int)sizeof(why));
+    free(cin);
+    if (!pd) {
+        if (S->verbose) printf("streamed decode not used: %s\n", why);
+        return CLI_FALLBACK;
+    }
+    /* GPUs: contexts need the insert statistics, stages do not */
+    if (getenv("GROM_DEVICES")) S->n_dev = atoi(getenv("GROM_DEVICES"));
+    if (S->n_dev < 1) S->n_dev = 1;
+    if (!g_plan_only && S->n_dev > 1) {
+        int avail = grom_device_count();
+        if (avail < 1) { fprintf(stderr, "grom: no GPU\n"); pd_close(pd); return 1; }
+        if (S->n_dev > avail - S->device) S->n_dev = avail - S->device;
+        if (S->n_dev < 1) S->n_dev = 1;
+    }
+    int *dev_of = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
+    {
+        /* longest processing time first over the chromosome lengths */
+        double load[64] = {0};
+        int *idx = malloc(sizeof(int) * (S->n_cand > 0 ? S->n_cand : 1));
+        for (int c = 0; c < S->n_cand; c++) idx[c] = c;
+        for (int a = 1; a < S->n_cand; a++) /* insertion sort, longest first, stable */
+            for (int b = a; b > 0 && S->plan[idx[b]].len > S->plan[idx[b - 1]].len; b--) {
+                int t = idx[b]; idx[b] = idx[b - 1]; idx[b - 1] = t;
+            }
+        for (int a = 0; a < S->n_cand; a++) {
+            int best = 0;
+            for (int d = 1; d < S->n_dev; d++)
+                if (load[d] < load[best]) best = d;
+            dev_of[idx[a]] = S->device + best;
+            load[best] += (double)S->plan[idx[a]].len;
+        }
+        free(idx);
+    }
+    const char *wd = getenv("GROM_WORKER_DEVICES");
+    if (wd) { /* test hook: every stage on the first listed device */
+        for (int c = 0; c < S->n_cand; c++) dev_of[c] = atoi(wd);
+    }
+    grom_stage *stages[256];
+    int n_stages = 0;
+    if (!g_plan_only) {
+        int per_gpu = getenv("GROM_SCANS_PER_GPU") ? atoi(getenv("GROM_SCANS_PER_GPU")) : 2;
+        if (per_gpu < 1) per_gpu = 1;
+        for (int d = 0; d < S->n_dev && !wd; d++)
+            for (int k = 0; k < per_gpu + 2 && n_stages < 256; k++) {
+                grom_stage *st = grom_stage_new(S->device + d);
+                if (!st) break;
+                stages[n_stages++] = st;
+                pd_add_stage(pd, st, S->device + d);
+            }
+        for (int k = 0; wd && k < 4; k++) {
+            grom_stage *st = grom_stage_new(atoi(wd));
+            if (!st) break;
+            stages[n_stages++] = st;
+            pd_add_stage(pd, st, atoi(wd));
+        }
+    }
+    if (pd_start(pd, P->min_mapq, S->n_dev, dev_of, g_plan_only)) {
+        fprintf(stderr, "grom: %s\n", pd_error(pd));
+        pd_close(pd);
+        for (int i = 0; i < n_stages; i++) grom_stage_free(stages[i]);
+        free(dev_of);
+        return 1;
+    }
+    int status = 0;
+    int lseq = 0, imin = 0, imax = 0;
+    long mapped = 0;
+    const int imean = pd_insert_stats(pd, grom_prob2(S->num_sd), P->min_mapq, &lseq, &imin, &imax, &mapped);
+    if (imean < 0) {
+        const int fallback = imean == -2;
+        if (!fallback) printf("ERROR: no reads to estimate the insert size from\n");
+        else if (S->verbose) printf("streamed decode stopped: %s\n", pd_error(pd));
+        pd_close(pd);
+        for (int i = 0; i < n_stages; i++) grom_stage_free(stages[i]);
+        free(dev_of);
+        return fallback ? CLI_FALLBACK : 1;
+    }
+    print_insert(S, imean, lseq, imin, imax, mapped);
+    int *keep = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
+    chrom_plan **plan = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(chrom_plan *));
+    int *pidx = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
+    int n_plan = 0;
+    for (int c = 0; c < S->n_cand; c++)
+        if ((keep[c] = passes_length(S, &S->plan[c]))) {
+            pidx[n_plan] = c;
+            plan[n_plan++] = &S->plan[c];
+        }
+    pd_set_walk(pd, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size, keep);
+    FILE *vcf = NULL;
+    grom_pool pool;
+    grom_worker *workers = NULL;
+    pthread_t *tids = NULL;
+    textbuf ctx_all = {0};
+    int next_write = 0, started = 0, fallback = 0;
+    fasta_feed F;
+    memset(&F, 0, sizeof(F));
+    pthread_t fthr;
+    int fasta_started = 0;
+    if (setup_workers(S)) { status = 1; goto done; }
+    vcf = fopen(S->out_name, "w");
+    if (!vcf) { printf("Error opening file %s\n", S->out_name); status = 1; goto done; }
+    if (P->vcf == 1) header(vcf, S->fasta_name, 0);
+    F.S = S;
+    F.plan = plan;
+    F.n_plan = g_plan_only ? 0 : n_plan;
+    F.ahead = 3;
+    pthread_mutex_init(&F.mu, NULL);
+    pthread_cond_init(&F.cv, NULL);
+    pthread_create(&fthr, NULL, fasta_main, &F);
+    fasta_started = 1;
+    if (!g_plan_only) {
+        pool_start(&pool, S, n_plan, &workers, &tids);
+        started = 1;
+    }
+    for (int k = 0; k < n_plan; k++) {
+        grom_stage *st = NULL;
+        pd_chrom_facts facts;
+        const int rc = pd_wait_chrom(pd, pidx[k], &st, &facts);
+        if (rc == 1) { fallback = 1; break; }
+        if (rc != 0) {
+            fprintf(stderr, "grom: streamed decode failed: %s\n", pd_error(pd));
+            grom_set_last_error(pd_error(pd));
+            status = 1;
+            break;
+        }
+        if (g_plan_only) {
+            grom_reads rd;
+            pd_mirror_view(pd, pidx[k], &rd);
+            printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d lseq_tail=%d digest=%016llx\n", plan[k]->name,
+                   plan[k]->tid, (long long)facts.n_reads, facts.n_skip, facts.p_last, facts.lseq_tail,
+                   (unsigned long long)pd_digest(&rd));
+            continue;
+        }
+        pthread_mutex_lock(&F.mu);
+        while (F.loaded <= k) pthread_cond_wait(&F.cv, &F.mu);
+        F.consumed = k + 1;
+        pthread_cond_broadcast(&F.cv);
+        pthread_mutex_unlock(&F.mu);
+        if (!plan[k]->ref || grom_stage_set_ref(st, plan[k]->ref, plan[k]->len) != GROM_OK) {
+            fprintf(stderr, "grom: staging the reference of %s failed: %s\n", plan[k]->name, grom_last_error());
+            status = 1;
+            pd_release_stage(pd, st);
+            break;
+        }
+        pthread_mutex_lock(&pool.mu);
+        grom_job *j = &pool.jobs[k];
+        j->cp = plan[k];
+        j->stage = st;
+        j->facts = facts;
+        j->pd = pd;
+        j->device = dev_of[pidx[k]];
+        j->ready = 1;
+        pthread_cond_broadcast(&pool.cv);
+        drain_rows(&pool, &next_write, k + 1, vcf, &ctx_all, &status);
+        pthread_mutex_unlock(&pool.mu);
+    }
+done:
+    if (fasta_started) {
+        pthread_mutex_lock(&F.mu);
+        F.stop = 1;
+        pthread_cond_broadcast(&F.cv);
+        pthread_mutex_unlock(&F.mu);
+        pthread_join(fthr, NULL);
+        for (int k = 0; k < n_plan; k++)
+            if (plan[k]->ref && (fallback || status)) { free(plan[k]->ref); plan[k]->ref = NULL; }
+        pthread_mutex_destroy(&F.mu);
+        pthread_cond_destroy(&F.cv);
+    }
+    if (started) pool_finish(&pool, S, workers, tids, &next_write, vcf, &ctx_all, &status);
+    if (!fallback && status == 0 && S->verbose) {
+        pd_counters pc;
+        pd_get_counters(pd, &pc);
+        printf("streamed decode: %lld records in %lld pieces, %d threads (%s), %.2f GB inflated, %.2f GB to HBM, "
+               "decoder busy %.2f s (inflate %.2f s), uploader %.2f s (waiting %.2f s), wall %.2f s\n",
+               (long long)pc.records, (long long)pc.pieces, pc.threads, pc.libdeflate ? "libdeflate" : "zlib",
+               pc.inflated_bytes / 1e9, pc.h2d_bytes / 1e9, pc.decode_thread_s, pc.inflate_s, pc.upload_s, pc.wait_s,
+               clock_gettime_s() - t_start);
+    }
+    pd_close(pd);
+    for (int i = 0; i < n_stages; i++) grom_stage_free(stages[i]);
+    if (vcf) fclose(vcf);
+    if (!fallback && status == 0) finish_outputs(S, &ctx_all);
+    free(ctx_all.p);
+    free(plan);
+    free(pidx);
+    free(keep);
+    free(dev_of);
+    if (fallback) {
+        for (int d = 0; d < S->n_init; d++) grom_dev_fini(d);
+        S->n_init = 0;
+        return CLI_FALLBACK;
+    }
+    return status;
+}
+
+static int cli_run(int argc, char **argv, int force_serial) {
+    optind = 0; /* GNU getopt: 0 fully re-initialises, so this is callable again */
+    setlinebuf(stdout);
+    cli_state *S = calloc(1, sizeof(cli_state));
+    grom_params *P = &S->P;
+    grom_default_params(P);
+    S->max_chr_len = 300000000; /* g_max_chr_fasta_len, GROM.c:946 */
+    S->num_sd = 3;
+    S->verbose = getenv("GROM_VERBOSE") != NULL;
+    S->n_dev = 1;
+    if (getenv("GROM_DEVICE")) S->device = atoi(getenv("GROM_DEVICE"));
+    int opt, ret = 1;
+    /* getopt string of GROM.c:21908 */
+    while ((opt = getopt(argc, argv,
+                         "Z:W:X:Q:A:Y:B:D:E:K:N:V:U:L:F:SP:c:R:MG:i:r:o:p:q:s:v:g:l:d:b:n:a:y:z:e:fj:k:m:u:w:x:h")) != -1) {
+        switch (opt) {
+        case 'S': P->splitread = 0; break;
+        case 'G': P->sv_list_len = atoi(optarg); break;
+        case 'M': P->rmdup = 1; break;
+        case 'i': S->bam_name = optarg; break;
+        case 'r': S->fasta_name = optarg; break;
+        case 'o': S->out_name = optarg; break;
+        case 'B': S->max_chr_len = atol(optarg); break;
+        case 'p': P->ploidy = atoi(optarg); break;
+        case 'q': P->min_mapq = atoi(optarg); break;
+        case 's': S->num_sd = atof(optarg); break;
+        case 'g': P->gender = atoi(optarg); break;
+        case 'l': P->overlap_mult = atoi(optarg); break;
+        case 'b': P->min_base_qual = atoi(optarg); break;
+        case 'n': P->min_snv = atoi(optarg); break;
+        case 'a': P->min_snv_ratio = atof(optarg); break;
+        case 'f': P->vcf = 0; break;
+        case 'x': P->min_ave_bq = atof(optarg); break;
+        case 'P': S->n_dev = atoi(optarg); break; /* -P threads -> GPUs, GROM.c:21930 */
+        case 'Z': P->block_min = atol(optarg); break;
+        case 'W': P->min_rd_window_len = atol(optarg); break;
+        case 'X': P->max_rd_window_len = atol(optarg); break;
+        case 'A': P->windows_sampling_factor = atol(optarg); break;
+        case 'Y': P->min_blocks = atol(optarg); break;
+        case 'D': P->min_repeat = atol(optarg); break;
+        case 'E': P->min_repeat_stdev = atof(optarg); break;
+        case 'K': P->ranks_stdev = atoi(optarg); break;
+        case 'V': P->rd_pval_threshold = atof(optarg); break;
+        case 'U': P->chr_rd_threshold_factor = atoi(optarg); break;
+        case 'L': P->dup_threshold_factor = atol(optarg); break;
+        case 'F': P->mapq_factor = atof(optarg); break;
+        case 'v': P->pval_threshold = atof(optarg); break;
+        case 'd': P->min_disc = atoi(optarg); break;
+        case 'y': P->max_split_loss = atoi(optarg); break;
+        case 'z': P->min_sr_len = atoi(optarg); break;
+        case 'e': P->pval_insertion = atof(optarg); break;
+        case 'j': P->min_sv_ratio = atof(optarg); break;
+        case 'k': P->max_homopolymer = atoi(optarg); break;
+        case 'm': P->min_indel_ratio = atof(optarg); break;
+        case 'u': P->max_evidence_ratio = atof(optarg); break;
+        case 'w': P->max_ins_range = atoi(optarg); break;
+        case 'N':
+            if (atol(optarg) > 0) {
+                printf("ERROR: -N (.1000gen side file) is not supported by this build\n");
+                free(S);
+                return 1;
+            }
+            break;
+        case 'h': print_help(); free(S); return 0;
+        case '?': free(S); return 1;
+        default: break; /* accepted; steers rows outside the implemented scan */
+        }
+    }
+    P->rd_min_mapq = P->min_mapq;         /* GROM.c:22102 */
+    P->pval_threshold1 = P->pval_threshold; /* GROM.c:22101 */
+    P->sv_list2_len = P->sv_list_len / 10;  /* GROM.c:21925 */
+    if (!force_serial) {
+        printf("bam %s\n", S->bam_name ? S->bam_name : "(null)");
+        printf("ref %s\n", S->fasta_name ? S->fasta_name : "(null)");
+        printf("results %s\n", S->out_name ? S->out_name : "(null)");
+    }
+    if (!S->bam_name) { printf("ERROR: No bam file specified.\n"); free(S); return 1; }
+    {
+        bgzf_reader br;
+        if (bgzf_open_read(&br, S->bam_name) != 0 || bam_read_header(&br, &S->hdr) != 0) {
+            printf("\nCould not open %s\n", S->bam_name);
+            bgzf_close_read(&br);
+            free(S);
+            return 1;
+        }
+        bgzf_close_read(&br);
+    }
+    if (!bai_loads(S->bam_name)) { printf("Could not open BAM indexing file\n"); goto out_hdr; }
+    if (!S->out_name) { printf("ERROR: No output file specified.\n"); goto out_hdr; }
+    {
+        FILE *probe = fopen(S->out_name, "w");
+        if (!probe) { printf("\nCould not open %s\n", S->out_name); goto out_hdr; }
+        fclose(probe);
+    }
+    if (!S->fasta_name) { printf("ERROR: No reference file specified.\n"); goto out_hdr; }
+    if (grom_fasta_open_cached(&S->fa, S->fasta_name) != 0) {
+        printf("\nCould not open %s\n", S->fasta_name);
+        goto out_hdr;
+    }
+    g_plan_only = getenv("GROM_PLAN_ONLY") != NULL;
+    /* tables (read_binom_tables, GROM.c:22234) on a thread beside the decode */
+    {
+        size_t tn = (size_t)(GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);
+        S->hez = malloc(sizeof(double) * tn);
+        S->mq = malloc(sizeof(double) * tn);
+        S->tables_started = pthread_create(&S->tables_thr, NULL, tables_main, S) == 0;
+        if (!S->tables_started) grom_build_tables(P->min_mapq, S->hez, S->mq);
+    }
+    /* candidate chromosomes in BAM header order (GROM.c:20826-21050); the
+     * length test that needs the insert size comes later */
+    S->plan = calloc(S->hdr.n_ref > 0 ? S->hdr.n_ref : 1, sizeof(chrom_plan));
+    for (int t = 0; t < S->hdr.n_ref; t++) {
+        int fi = grom_match_target(&S->fa, S->hdr.ref_name[t]);
+        char lc[GROM_MAX_CHR_NAMES];
+        int bl = grom_target_name_lc(S->hdr.ref_name[t], lc, (int)sizeof(lc));
+        if (P->gender == 0 && ((bl == 4 && strncmp(lc, "chry", 4) == 0) || (bl == 1 && lc[0] == 'y'))) fi = -1;
+        if (fi < 0) continue;
+        long len = grom_fasta_load(&S->fa, fi, NULL, 0);
+        /* count_discordant_pairs re-derives the BAM target from the FASTA name
+         * (GROM.c:1894-1961): the first target matching it */
+        int32_t tid2 = -1;
+        for (int a = 0; a < S->hdr.n_ref; a++)
+            if (grom_match_target(&S->fa, S->hdr.ref_name[a]) == fi) { tid2 = a; break; }
+        chrom_plan *c = &S->plan[S->n_cand++];
+        c->fasta_idx = fi;
+        c->tid = tid2;
+        c->len = len;
+        /* the name loop leaves the last target's name when nothing matches */
+        c->target = strdup(S->hdr.n_ref > 0 ? S->hdr.ref_name[tid2 >= 0 ? tid2 : S->hdr.n_ref - 1] : "");
+        snprintf(c->name, sizeof(c->name), "%.*s", S->fa.name_len[fi], S->fa.names[fi]);
+    }
+    {
+        size_t ol = strlen(S->out_name);
+        if (ol > 4 && strcmp(S->out_name + ol - 4, ".vcf") == 0)
+            snprintf(S->ctx_name, sizeof(S->ctx_name), "%.*s.ctx.vcf", (int)(ol - 4), S->out_name);
+        else
+            snprintf(S->ctx_name, sizeof(S->ctx_name), "%s.ctx", S->out_name);
+    }
+    const char *ser = getenv("GROM_SERIAL_DECODE");
+    if (force_serial || (ser && atoi(ser) > 0)) ret = run_serial(S);
+    else ret = run_streamed(S);
+    tables_join(S);
+    for (int d = 0; d < S->n_init; d++) grom_dev_fini(d);
+    for (int i = 0; i < S->n_cand; i++) {
+        free(S->plan[i].target);
+        free(S->plan[i].ref);
+    }
+    free(S->plan);
+    free(S->hez);
+    free(S->mq);
+    grom_fasta_close(&S->fa);
+out_hdr:
+    tables_join(S);
+    bam_free_header(&S->hdr);
+    free(S);
+    return ret;
+}
+
+int grom_cli_main(int argc, char **argv) {
+    int rc = cli_run(argc, argv, 0);
+    if (rc == CLI_FALLBACK) {
+        if (getenv("GROM_VERBOSE")) printf("reading the BAM serially\n");
+        rc = cli_run(argc, argv, 1);
+    }
+    return rc;
 }

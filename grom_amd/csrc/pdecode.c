@@ -1,0 +1,2099 @@
+/*
+ * pdecode.c -- parallel BAM decode into pinned pieces, streamed to device
+ * stages in file order (see pdecode.h).
+ *
+ * Threads: n decoder threads take pieces in file order (at most `window`
+ * pieces ahead of the uploader) and inflate + parse each into a pinned
+ * buffer; one uploader thread takes finished pieces in file order,
+ * accumulates find_insert_mean's sample, applies the order-dependent fix-ups
+ * and appends the piece to its chromosome's stage (async copies); chromosomes
+ * are finalised in plan order once the walk parameters are known and handed
+ * to the caller through pd_stream_chrom.
+ */
+#define _GNU_SOURCE
+#include "pdecode.h"
+
+#include <dlfcn.h>
+#include <stddef.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include "stream.h"
+
+#define PD_INSERT_CAP 10000000 /* insert_sample_size, GROM.c:913 */
+#define PD_PIECE_RECS 65536    /* target records per piece */
+#define PD_LOWPOS_LIMIT (1 << 22) /* the skip prefix is resolved below this position */
+#define PD_MAX_REC (256 << 20)    /* a record larger than this is taken as a bad offset */
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static uint16_t ld16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+static uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static int32_t ldi32(const uint8_t *p) { int32_t v; memcpy(&v, p, 4); return v; }
+
+/* ---------------- inflate: libdeflate when the image has it, else zlib ---------------- */
+typedef void *(*ld_alloc_fn)(void);
+typedef int (*ld_dec_fn)(void *, const void *, size_t, void *, size_t, size_t *);
+typedef void (*ld_free_fn)(void *);
+static ld_alloc_fn ld_alloc;
+static ld_dec_fn ld_dec;
+static ld_free_fn ld_free;
+static pthread_once_t ld_once = PTHREAD_ONCE_INIT;
+
+static void ld_init(void) {
+    if (getenv("GROM_NO_LIBDEFLATE")) return;
+    void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    ld_alloc_fn a = (ld_alloc_fn)dlsym(h, "libdeflate_alloc_decompressor");
+    ld_dec_fn d = (ld_dec_fn)dlsym(h, "libdeflate_deflate_decompress");
+    ld_free_fn f = (ld_free_fn)dlsym(h, "libdeflate_free_decompressor");
+    if (a && d && f) { ld_alloc = a; ld_dec = d; ld_free = f; }
+}
+
+typedef struct {
+    void *ld;
+    z_stream zs;
+    int zinit;
+} pd_inflater;
+
+static void inf_init(pd_inflater *f) {
+    memset(f, 0, sizeof(*f));
+    pthread_once(&ld_once, ld_init);
+    if (ld_alloc) f->ld = ld_alloc();
+}
+
+static void inf_free(pd_inflater *f) {
+    if (f->ld) ld_free(f->ld);
+    if (f->zinit) inflateEnd(&f->zs);
+    memset(f, 0, sizeof(*f));
+}
+
+/* raw deflate data -> exactly isize bytes; 0 or -1 */
+static int inf_block(pd_inflater *f, const uint8_t *c, size_t clen, uint8_t *out, uint32_t isize) {
+    if (isize == 0) return 0;
+    if (f->ld) {
+        size_t got = 0;
+        if (ld_dec(f->ld, c, clen, out, isize, &got) != 0 || got != isize) return -1;
+        return 0;
+    }
+    if (!f->zinit) {
+        if (inflateInit2(&f->zs, -15) != Z_OK) return -1;
+        f->zinit = 1;
+    } else if (inflateReset(&f->zs) != Z_OK) {
+        return -1;
+    }
+    f->zs.next_in = (uint8_t *)c;
+    f->zs.avail_in = (uInt)clen;
+    f->zs.next_out = out;
+    f->zs.avail_out = isize;
+    int rc = inflate(&f->zs, Z_FINISH);
+    return (rc == Z_STREAM_END && f->zs.total_out == isize) ? 0 : -1;
+}
+
+/* ---------------- a reader over [vbeg, vend) of the decompressed stream ---------------- */
+typedef struct {
+    int fd;
+    int64_t file_size;
+    uint8_t *cbuf;
+    int64_t cbuf_cap, cbuf_off, cbuf_len; /* cbuf holds file bytes [cbuf_off, cbuf_off + cbuf_len) */
+    int64_t next_coff;                     /* the next block to inflate */
+    uint8_t *ub;
+    int64_t ub_cap, ub_len, ub_pos;
+    int64_t stop_at;                       /* ub offset where parsing stops, -1 unknown */
+    int64_t stop_coff;                     /* -1: read to end of file */
+    int stop_uoff, no_more;
+    pd_inflater inf;
+    int64_t inflated, compressed;
+    double t_inflate, t_io;
+} pd_reader;
+
+static int rd_fetch(pd_reader *r, int64_t off, int64_t need) {
+    if (off >= r->cbuf_off && off + need <= r->cbuf_off + r->cbuf_len) return 0;
+    int64_t want = need > (4 << 20) ? need : (4 << 20);
+    if (want > r->cbuf_cap) {
+        uint8_t *nb = (uint8_t *)realloc(r->cbuf, (size_t)want);
+        if (!nb) return -1;
+        r->cbuf = nb;
+        r->cbuf_cap = want;
+    }
+    if (off + want > r->file_size) want = r->file_size - off;
+    if (want < need) return -1;
+    int64_t got = 0;
+    while (got < want) {
+        ssize_t k = pread(r->fd, r->cbuf + got, (size_t)(want - got), (off_t)(off + got));
+        if (k <= 0) break;
+        got += k;
+    }
+    if (got < need) return -1;
+    r->t_io += 0;
+    r->cbuf_off = off;
+    r->cbuf_len = got;
+    return 0;
+}
+
+static int rd_reserve(pd_reader *r, int64_t cap) {
+    if (cap <= r->ub_cap) return 0;
+    int64_t nc = r->ub_cap ? r->ub_cap : (1 << 20);
+    while (nc < cap) nc *= 2;
+    uint8_t *nb = (uint8_t *)realloc(r->ub, (size_t)nc);
+    if (!nb) return -1;
+    r->ub = nb;
+    r->ub_cap = nc;
+    return 0;
+}
+
+/* inflate the next block onto ub: 1, 0 when there is nothing more, -1 error */
+static int rd_next_block(pd_reader *r) {
+    for (;;) {
+        if (r->no_more) return 0;
+        if (r->stop_coff >= 0 && r->next_coff > r->stop_coff) return -1; /* the stop offset is not a block start */
+        if (r->next_coff == r->stop_coff && r->stop_uoff == 0) {
+            r->stop_at = r->ub_len;
+            r->no_more = 1;
+            return 0;
+        }
+        if (r->next_coff >= r->file_size) {
+            if (r->stop_coff >= 0) return -1;
+            r->no_more = 1;
+            return 0;
+        }
+        if (rd_fetch(r, r->next_coff, 18)) return -1;
+        const uint8_t *h = r->cbuf + (r->next_coff - r->cbuf_off);
+        if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return -1;
+        const int xlen = ld16(h + 10);
+        if (rd_fetch(r, r->next_coff, 12 + xlen)) return -1;
+        h = r->cbuf + (r->next_coff - r->cbuf_off);
+        int bsize = -1;
+        for (int o = 0; o + 4 <= xlen;) {
+            const int sl = ld16(h + 12 + o + 2);
+            if (h[12 + o] == 'B' && h[12 + o + 1] == 'C' && sl == 2) { bsize = ld16(h + 12 + o + 4); break; }
+            o += 4 + sl;
+        }
+        if (bsize < 0) return -1;
+        const int64_t blen = (int64_t)bsize + 1;
+        if (blen < 12 + xlen + 8 || rd_fetch(r, r->next_coff, blen)) return -1;
+        h = r->cbuf + (r->next_coff - r->cbuf_off);
+        const uint32_t isize = ld32(h + blen - 4);
+        if (isize > 65536) return -1;
+        if (rd_reserve(r, r->ub_len + isize + 64)) return -1;
+        const double t0 = now_s();
+        if (inf_block(&r->inf, h + 12 + xlen, (size_t)(blen - 12 - xlen - 8), r->ub + r->ub_len, isize)) return -1;
+        r->t_inflate += now_s() - t0;
+        if (r->next_coff == r->stop_coff) {
+            r->stop_at = r->ub_len + r->stop_uoff;
+            r->no_more = 1;
+        }
+        r->ub_len += isize;
+        r->next_coff += blen;
+        r->inflated += isize;
+        r->compressed += blen;
+        if (isize > 0 || r->no_more) return 1;
+    }
+}
+
+static int rd_open(pd_reader *r, int fd, int64_t file_size, uint64_t vbeg, uint64_t vend) {
+    r->fd = fd;
+    r->file_size = file_size;
+    r->cbuf_off = r->cbuf_len = 0;
+    r->ub_len = r->ub_pos = 0;
+    r->stop_at = -1;
+    r->no_more = 0;
+    r->stop_coff = vend == UINT64_MAX ? -1 : (int64_t)(vend >> 16);
+    r->stop_uoff = vend == UINT64_MAX ? 0 : (int)(vend & 0xffff);
+    r->next_coff = (int64_t)(vbeg >> 16);
+    const int uoff = (int)(vbeg & 0xffff);
+    if (uoff > 0 || r->next_coff != r->stop_coff) {
+        int k = rd_next_block(r);
+        if (k < 0) return -1;
+        if (uoff > r->ub_len) return -1;
+    }
+    r->ub_pos = uoff;
+    return 0;
+}
+
+/* make at least `need` bytes available at ub_pos: 1, 0 if the range/file
+ * ended first, -1 on error */
+static int rd_avail(pd_reader *r, int64_t need) {
+    while (r->ub_len - r->ub_pos < need) {
+        if (r->ub_pos > 0) {
+            memmove(r->ub, r->ub + r->ub_pos, (size_t)(r->ub_len - r->ub_pos));
+            r->ub_len -= r->ub_pos;
+            if (r->stop_at >= 0) r->stop_at -= r->ub_pos;
+            r->ub_pos = 0;
+        }
+        int k = rd_next_block(r);
+        if (k < 0) return -1;
+        if (k == 0) return 0;
+    }
+    return 1;
+}
+
+static void rd_free(pd_reader *r) {
+    free(r->cbuf);
+    free(r->ub);
+    inf_free(&r->inf);
+    memset(r, 0, sizeof(*r));
+}
+
+/* ---------------- piece buffers ---------------- */
+typedef struct pd_buf {
+    /* pinned, appended to the stage */
+    int64_t cap;
+    void *rec_mem;
+    int32_t *pos, *mtid, *mpos, *isize, *lq, *aidx;
+    uint16_t *flag;
+    uint8_t *mapq;
+    uint32_t *coff, *nid;
+    int64_t *boff;
+    int64_t cap_cig;
+    uint32_t *cig;
+    int64_t cap_b;
+    uint8_t *qual, *seq;
+    int64_t cap_aux;
+    grom_aux *aux;
+    /* pageable */
+    int32_t *end, *hclip;
+    int64_t cap_drop;
+    int32_t *dpos, *dlq;
+    int64_t *dbef;
+    /* read names: open-addressing table of local ids, arena offsets per id */
+    uint32_t *nt_id;
+    uint64_t *nt_hash;
+    int64_t nt_cap;
+    uint32_t *id_off;
+    int64_t cap_ids;
+    char *arena;
+    int64_t arena_len, arena_cap;
+    /* counts */
+    int64_t n, n_cig, n_b, n_aux, n_drop, n_names;
+    /* after the append: which copy must finish before reuse */
+    grom_stage *stage;
+    int64_t ticket;
+    struct pd_buf *next;
+} pd_buf;
+
+typedef struct {
+    int run;
+    uint64_t vbeg, vend;
+    int full;             /* decode into a buffer (a processed chromosome's run) */
+    volatile int state;   /* 0 pending, 1 busy, 2 done, 3 skipped, 4 error */
+    pd_buf *buf;
+    int stats;            /* the sample arrays below were collected */
+    int32_t *st_ins, *st_lq;
+    int64_t *st_m;
+    int64_t st_n, st_cap, m_total;
+    int64_t n_rec;
+    int sorted;           /* positions non-decreasing inside the piece */
+    int32_t first_pos;    /* first record's position */
+    int32_t last_pos, last_lq, last_hclip, last_kept;
+    double secs;
+    char err[200];
+} pd_piece;
+
+typedef struct {
+    int32_t tid;
+    int64_t count;        /* -1: unknown (unplaced reads without the index's count) */
+    uint64_t vbeg, vend;
+    int chrom;            /* plan index taking this run, -1 none */
+    int64_t j0;           /* leading records consumed by the previous chromosome (Q1) */
+    int first_piece, n_pieces;
+    int has_next;         /* a record follows this run in the file */
+    int32_t next_lq;      /* its l_qseq (grom_batch_end_record) */
+} pd_run;
+
+/* T: reads of earlier pieces of the chromosome that can still overlap a read */
+typedef struct {
+    uint32_t gid;
+    int32_t end;
+    int64_t name_off;
+} tail_ent;
+
+typedef struct {
+    tail_ent *e;
+    int64_t n, cap;
+    char *arena;
+    int64_t arena_len, arena_cap;
+    int64_t *ht; /* index+1 into e, 0 empty */
+    uint64_t *hh;
+    int64_t ht_cap;
+    int32_t max_end;
+} tail_set;
+
+typedef struct {
+    int32_t pos;
+    int32_t lq;
+    int64_t before;
+} drop_rec;
+
+typedef struct {
+    int64_t idx;
+    grom_aux a;
+} saux_rec;
+
+/* per processed chromosome: upload progress and its stream facts */
+typedef struct {
+    int run;              /* -1: no records */
+    int device;
+    grom_stage *stage;
+    int begun, uploaded, final, handed;
+    int64_t j_left;
+    int64_t n_kept, n_cig, n_bases, n_aux, n_names;
+    int64_t n_seen;       /* stream records after the Q1 drops */
+    int32_t last_pos, last_lq, last_hclip, last_kept;
+    int32_t prev_pos;     /* sortedness check across pieces */
+    drop_rec *drops;
+    int64_t n_drops, cap_drops;
+    int32_t *lowpos;      /* kept positions < PD_LOWPOS_LIMIT, stream order */
+    int64_t n_low, cap_low;
+    saux_rec *saux;       /* -S: every kept read's split alignment, resolved at the end */
+    int64_t n_saux, cap_saux;
+    int kept;             /* in the final plan */
+    pd_chrom_facts facts;
+    int rc;
+    /* host mirror (plan-only) */
+    grom_batch mirror;
+    int mirror_used;
+} pd_chrom;
+
+struct pd_session {
+    int fd;
+    int64_t file_size;
+    int n_plan;
+    pd_chrom_in *plan;
+    pd_chrom *ch;
+    pd_run *runs;
+    int n_runs;
+    pd_piece *pieces;
+    int n_pieces;
+    int splitread, read_name_len, min_mapq_stats;
+    /* threads */
+    int n_threads, window;
+    pthread_t *thr;
+    pthread_t upl;
+    int upl_started;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;     /* pieces, buffers, window, chromosomes, stats */
+    int next_piece, head, abort, stop;
+    char abort_msg[300];
+    int abort_soft;        /* the index plan was contradicted: read serially */
+    /* buffers */
+    pd_buf *free_bufs, *inflight_head, *inflight_tail;
+    int n_bufs, max_bufs, buf_waiters;
+    void **old_pinned;     /* replaced pinned blocks, freed at close */
+    int n_old, cap_old;
+    /* stats */
+    int stats_done, stats_collect;
+    int32_t *s_ins, *s_lq;
+    int64_t s_n, s_m;
+    int walk_set, final_pending, final_applied;
+    int *keep;             /* final plan (per preliminary chromosome) */
+    int32_t index_start, overlap_mult, insert_max;
+    /* devices and stages (pd_stream_chrom's caller owns the stages) */
+    int plan_only, no_mirror;
+    int n_dev;
+    int *dev_of;           /* plan index -> device */
+    grom_stage **stages;   /* pool: n_stage, each with its device and busy flag */
+    int *stage_dev, *stage_busy;
+    int n_stage, cap_stage;
+    /* counters */
+    int64_t c_records, c_inflated, c_compressed, c_h2d;
+    double c_dec_s, c_upl_s, c_wait_s, c_inflate_s;
+    /* uploader scratch */
+    uint32_t *remap;
+    int64_t remap_cap;
+    tail_set T;
+};
+
+static void sess_abort(pd_session *s, int soft, const char *msg) {
+    pthread_mutex_lock(&s->mu);
+    if (!s->abort) {
+        s->abort = 1;
+        s->abort_soft = soft;
+        snprintf(s->abort_msg, sizeof(s->abort_msg), "%s", msg);
+    }
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+}
+
+/* ---- pinned buffer growth ---- */
+static void *pin_alloc(pd_session *s, size_t bytes, int pinned) {
+    (void)s;
+    return pinned ? grom_pinned_alloc(bytes) : malloc(bytes ? bytes : 16);
+}
+
+static void pin_retire(pd_session *s, void *p, int pinned) {
+    if (!p) return;
+    if (!pinned) { free(p); return; }
+    pthread_mutex_lock(&s->mu);
+    if (s->n_old == s->cap_old) {
+        s->cap_old = s->cap_old ? 2 * s->cap_old : 64;
+        s->old_pinned = (void **)realloc(s->old_pinned, sizeof(void *) * s->cap_old);
+    }
+    s->old_pinned[s->n_old++] = p;
+    pthread_mutex_unlock(&s->mu);
+}
+
+/* the per-read arrays as one block: grow to hold `need` reads */
+static int buf_grow_recs(pd_session *s, pd_buf *b, int64_t need) {
+    if (need <= b->cap) return 0;
+    int64_t nc = b->cap ? b->cap : PD_PIECE_RECS + PD_PIECE_RECS / 2;
+    while (nc < need) nc *= 2;
+    /* pos mtid mpos isize lq aidx (6 x 4) + flag 2 + mapq 1 + coff (n+1)x4 + nid 4 + boff 8 */
+    const size_t per = 6 * 4 + 2 + 1 + 4 + 4 + 8;
+    const size_t bytes = per * (size_t)nc + 4 + 8 * 64;
+    char *m = (char *)pin_alloc(s, bytes, !s->plan_only);
+    int32_t *end = (int32_t *)malloc(sizeof(int32_t) * (size_t)nc), *hc = (int32_t *)malloc(sizeof(int32_t) * (size_t)nc);
+    if (!m || !end || !hc) { free(end); free(hc); return -1; }
+    size_t o = 0;
+#define CARVE(field, type, count)                                                                 \
+    do {                                                                                           \
+        type *p_ = (type *)(m + o);                                                                \
+        if (b->n) memcpy(p_, b->field, sizeof(type) * (size_t)(b->n + ((count) > nc ? 1 : 0)));    \
+        b->field = p_;                                                                             \
+        o += ((sizeof(type) * (size_t)(count)) + 63) & ~(size_t)63;                                \
+    } while (0)
+    CARVE(boff, int64_t, nc);
+    CARVE(pos, int32_t, nc);
+    CARVE(mtid, int32_t, nc);
+    CARVE(mpos, int32_t, nc);
+    CARVE(isize, int32_t, nc);
+    CARVE(lq, int32_t, nc);
+    CARVE(aidx, int32_t, nc);
+    CARVE(coff, uint32_t, nc + 1);
+    CARVE(nid, uint32_t, nc);
+    CARVE(flag, uint16_t, nc);
+    CARVE(mapq, uint8_t, nc);
+#undef CARVE
+    if (b->n) {
+        memcpy(end, b->end, sizeof(int32_t) * (size_t)b->n);
+        memcpy(hc, b->hclip, sizeof(int32_t) * (size_t)b->n);
+    }
+    free(b->end);
+    free(b->hclip);
+    b->end = end;
+    b->hclip = hc;
+    pin_retire(s, b->rec_mem, !s->plan_only);
+    b->rec_mem = m;
+    b->cap = nc;
+    return 0;
+}
+
+static int buf_grow_cig(pd_session *s, pd_buf *b, int64_t need) {
+    if (need <= b->cap_cig) return 0;
+    int64_t nc = b->cap_cig ? b->cap_cig : 4 * PD_PIECE_RECS;
+    while (nc < need) nc *= 2;
+    uint32_t *p = (uint32_t *)pin_alloc(s, sizeof(uint32_t) * (size_t)nc, !s->plan_only);
+    if (!p) return -1;
+    if (b->n_cig) memcpy(p, b->cig, sizeof(uint32_t) * (size_t)b->n_cig);
+    pin_retire(s, b->cig, !s->plan_only);
+    b->cig = p;
+    b->cap_cig = nc;
+    return 0;
+}
+
+static int buf_grow_bases(pd_session *s, pd_buf *b, int64_t need) {
+    if (need <= b->cap_b) return 0;
+    int64_t nc = b->cap_b ? b->cap_b : (int64_t)200 * PD_PIECE_RECS;
+    while (nc < need) nc *= 2;
+    /* qual then seq (nc/2) in one block, seq 16-byte aligned */
+    uint8_t *p = (uint8_t *)pin_alloc(s, (size_t)nc + (size_t)nc / 2 + 64, !s->plan_only);
+    if (!p) return -1;
+    uint8_t *q = p, *sq = p + ((nc + 15) & ~(int64_t)15);
+    if (b->n_b) {
+        memcpy(q, b->qual, (size_t)b->n_b);
+        memcpy(sq, b->seq, (size_t)b->n_b / 2);
+    }
+    pin_retire(s, b->qual, !s->plan_only);
+    b->qual = q;
+    b->seq = sq;
+    b->cap_b = nc;
+    return 0;
+}
+
+static int buf_grow_aux(pd_session *s, pd_buf *b, int64_t need) {
+    if (need <= b->cap_aux) return 0;
+    int64_t nc = b->cap_aux ? 2 * b->cap_aux : 1024;
+    while (nc < need) nc *= 2;
+    grom_aux *p = (grom_aux *)pin_alloc(s, sizeof(grom_aux) * (size_t)nc, !s->plan_only);
+    if (!p) return -1;
+    if (b->n_aux) memcpy(p, b->aux, sizeof(grom_aux) * (size_t)b->n_aux);
+    pin_retire(s, b->aux, !s->plan_only);
+    b->aux = p;
+    b->cap_aux = nc;
+    return 0;
+}
+
+static int buf_grow_drop(pd_buf *b, int64_t need) {
+    if (need <= b->cap_drop) return 0;
+    int64_t nc = b->cap_drop ? 2 * b->cap_drop : 4096;
+    while (nc < need) nc *= 2;
+    int32_t *a = (int32_t *)realloc(b->dpos, sizeof(int32_t) * (size_t)nc);
+    if (!a) return -1;
+    b->dpos = a;
+    a = (int32_t *)realloc(b->dlq, sizeof(int32_t) * (size_t)nc);
+    if (!a) return -1;
+    b->dlq = a;
+    int64_t *c = (int64_t *)realloc(b->dbef, sizeof(int64_t) * (size_t)nc);
+    if (!c) return -1;
+    b->dbef = c;
+    b->cap_drop = nc;
+    return 0;
+}
+
+static void buf_reset(pd_buf *b) {
+    b->n = b->n_cig = b->n_b = b->n_aux = b->n_drop = b->n_names = 0;
+    b->arena_len = 0;
+    b->stage = NULL;
+    b->ticket = -1;
+    if (b->nt_cap) memset(b->nt_id, 0, sizeof(uint32_t) * (size_t)b->nt_cap);
+}
+
+static void buf_destroy(pd_buf *b, int pinned) {
+    if (pinned) {
+        grom_pinned_free(b->rec_mem);
+        grom_pinned_free(b->cig);
+        grom_pinned_free(b->qual);
+        grom_pinned_free(b->aux);
+    } else {
+        free(b->rec_mem);
+        free(b->cig);
+        free(b->qual);
+        free(b->aux);
+    }
+    free(b->end);
+    free(b->hclip);
+    free(b->dpos);
+    free(b->dlq);
+    free(b->dbef);
+    free(b->nt_id);
+    free(b->nt_hash);
+    free(b->id_off);
+    free(b->arena);
+    free(b);
+}
+
+static uint64_t fnv(const char *p, size_t *len) {
+    uint64_t h = 0xcbf29ce484222325ULL;
+    const char *q = p;
+    for (; *q; q++) h = (h ^ (unsigned char)*q) * 0x100000001b3ULL;
+    *len = (size_t)(q - p);
+    return h;
+}
+
+/* local read-name id (1..), 0 for names the reference never stores
+ * (empty or >= read_name_len characters, GROM.c:6813) */
+static int64_t buf_intern(pd_buf *b, const char *name, int read_name_len) {
+    size_t L;
+    const uint64_t h = fnv(name, &L);
+    if (L == 0 || L >= (size_t)read_name_len) return 0;
+    if (2 * (b->n_names + 1) > b->nt_cap) {
+        int64_t nc = b->nt_cap ? 2 * b->nt_cap : 2 * PD_PIECE_RECS;
+        uint32_t *ni = (uint32_t *)calloc((size_t)nc, sizeof(uint32_t));
+        uint64_t *nh = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nc);
+        if (!ni || !nh) { free(ni); free(nh); return -1; }
+        for (int64_t i = 0; i < b->nt_cap; i++)
+            if (b->nt_id[i]) {
+                int64_t j = (int64_t)(b->nt_hash[i] & (uint64_t)(nc - 1));
+                while (ni[j]) j = (j + 1) & (nc - 1);
+                ni[j] = b->nt_id[i];
+                nh[j] = b->nt_hash[i];
+            }
+        free(b->nt_id);
+        free(b->nt_hash);
+        b->nt_id = ni;
+        b->nt_hash = nh;
+        b->nt_cap = nc;
+    }
+    int64_t j = (int64_t)(h & (uint64_t)(b->nt_cap - 1));
+    while (b->nt_id[j]) {
+        if (b->nt_hash[j] == h && strcmp(b->arena + b->id_off[b->nt_id[j]], name) == 0) return b->nt_id[j];
+        j = (j + 1) & (b->nt_cap - 1);
+    }
+    if (b->arena_len + (int64_t)L + 1 > b->arena_cap) {
+        int64_t nc = b->arena_cap ? 2 * b->arena_cap : (1 << 22);
+        while (nc < b->arena_len + (int64_t)L + 1) nc *= 2;
+        char *na = (char *)realloc(b->arena, (size_t)nc);
+        if (!na) return -1;
+        b->arena = na;
+        b->arena_cap = nc;
+    }
+    if (b->n_names + 2 > b->cap_ids) {
+        int64_t nc = b->cap_ids ? 2 * b->cap_ids : PD_PIECE_RECS;
+        uint32_t *no = (uint32_t *)realloc(b->id_off, sizeof(uint32_t) * (size_t)nc);
+        if (!no) return -1;
+        b->id_off = no;
+        b->cap_ids = nc;
+    }
+    memcpy(b->arena + b->arena_len, name, L + 1);
+    const uint32_t id = (uint32_t)(++b->n_names);
+    b->id_off[id] = (uint32_t)b->arena_len;
+    b->arena_len += (int64_t)L + 1;
+    b->nt_id[j] = id;
+    b->nt_hash[j] = h;
+    return id;
+}
+
+/* ---------------- decoding one piece ---------------- */
+static int stat_push(pd_piece *p, int32_t ins, int32_t lq, int64_t m) {
+    if (p->st_n == p->st_cap) {
+        int64_t nc = p->st_cap ? 2 * p->st_cap : 16384;
+        int32_t *a = (int32_t *)realloc(p->st_ins, sizeof(int32_t) * (size_t)nc);
+        if (!a) return -1;
+        p->st_ins = a;
+        a = (int32_t *)realloc(p->st_lq, sizeof(int32_t) * (size_t)nc);
+        if (!a) return -1;
+        p->st_lq = a;
+        int64_t *c = (int64_t *)realloc(p->st_m, sizeof(int64_t) * (size_t)nc);
+        if (!c) return -1;
+        p->st_m = c;
+        p->st_cap = nc;
+    }
+    p->st_ins[p->st_n] = ins;
+    p->st_lq[p->st_n] = lq;
+    p->st_m[p->st_n] = m;
+    p->st_n++;
+    return 0;
+}
+
+static int decode_piece(pd_session *s, pd_reader *r, pd_piece *p, pd_buf *b) {
+    const pd_run *run = &s->runs[p->run];
+    const char *target = (run->chrom >= 0 && s->plan[run->chrom].target_name) ? s->plan[run->chrom].target_name : "";
+    if (rd_open(r, s->fd, s->file_size, p->vbeg, p->vend)) {
+        snprintf(p->err, sizeof(p->err), "piece at voffset %llu: bad block", (unsigned long long)p->vbeg);
+        return -1;
+    }
+    const int collect = p->stats;
+    int64_t m = 0;
+    int32_t prev = INT32_MIN;
+    p->sorted = 1;
+    p->n_rec = 0;
+    p->last_kept = -1;
+    for (;;) {
+        if (r->stop_at >= 0 && r->ub_pos >= r->stop_at) break;
+        int k = rd_avail(r, 4);
+        if (k < 0) goto bad;
+        if (k == 0) {
+            if (r->ub_len - r->ub_pos == 0) break;
+            goto bad;
+        }
+        if (r->stop_at >= 0 && r->ub_pos >= r->stop_at) break;
+        const uint32_t bs = ld32(r->ub + r->ub_pos);
+        if (bs < 32 || bs > PD_MAX_REC) goto bad;
+        if ((k = rd_avail(r, 4 + (int64_t)bs)) <= 0) goto bad;
+        const uint8_t *q = r->ub + r->ub_pos + 4;
+        const int32_t tid = ldi32(q), pos = ldi32(q + 4);
+        const int l_qname = q[8], mapq = q[9];
+        const int n_cigar = ld16(q + 12), flag = ld16(q + 14);
+        const int32_t lq = ldi32(q + 16), mtid = ldi32(q + 20), mpos = ldi32(q + 24), isz = ldi32(q + 28);
+        if (lq < 0 || l_qname < 1 || 32 + (int64_t)l_qname + 4 * (int64_t)n_cigar + (lq + 1) / 2 + lq > (int64_t)bs ||
+            tid != run->tid)
+            goto bad;
+        if (p->n_rec == 0) p->first_pos = pos;
+        if (pos < prev) p->sorted = 0;
+        prev = pos;
+        p->n_rec++;
+        const int dropped = (flag & GF_UNMAP) || (flag & GF_DUP);
+        if (collect && !dropped) { /* find_insert_mean, GROM.c:1226-1317 */
+            int take = 0;
+            int32_t v = 0;
+            if (!(flag & GF_PAIRED)) { take = 1; v = lq; }
+            else if (!(flag & GF_MUNMAP) && tid == mtid && pos < mpos && (flag & GF_PROPER) && isz > 0) { take = 1; v = isz; }
+            if (mapq >= s->min_mapq_stats) m += lq;
+            if (take && stat_push(p, v, lq, m)) goto oom;
+        }
+        p->last_pos = pos;
+        p->last_lq = lq;
+        p->last_hclip = 0;
+        if (!b) { /* stats only */
+            p->last_kept = !dropped;
+            r->ub_pos += 4 + (int64_t)bs;
+            continue;
+        }
+        if (dropped) { /* GROM.c:6418: skipped by the ingest, kept for the breakpoint tests */
+            if (buf_grow_drop(b, b->n_drop + 1)) goto oom;
+            b->dpos[b->n_drop] = pos;
+            b->dlq[b->n_drop] = lq;
+            b->dbef[b->n_drop] = b->n;
+            b->n_drop++;
+            p->last_kept = 0;
+            r->ub_pos += 4 + (int64_t)bs;
+            continue;
+        }
+        const int64_t i = b->n;
+        if (buf_grow_recs(s, b, i + 1) || buf_grow_cig(s, b, b->n_cig + n_cigar) ||
+            buf_grow_bases(s, b, b->n_b + lq + 2))
+            goto oom;
+        const uint8_t *data = q + 32;
+        b->pos[i] = pos;
+        b->flag[i] = (uint16_t)flag;
+        b->mapq[i] = (uint8_t)mapq;
+        b->mtid[i] = mtid;
+        b->mpos[i] = mpos;
+        b->isize[i] = isz;
+        b->lq[i] = lq;
+        if (i == 0) b->coff[0] = (uint32_t)b->n_cig;
+        const uint8_t *cg = data + l_qname;
+        memcpy(b->cig + b->n_cig, cg, 4 * (size_t)n_cigar);
+        int32_t span = 0, hc = 0;
+        for (int c = 0; c < n_cigar; c++) {
+            const uint32_t op = ld32(cg + 4 * c);
+            const int o = op & 0xf;
+            if (o == GC_MATCH || o == GC_DEL || o == GC_REF_SKIP || o == GC_EQUAL || o == GC_DIFF) span += (int32_t)(op >> 4);
+            else if (o == GC_HARD_CLIP) hc += (int32_t)(op >> 4);
+        }
+        b->n_cig += n_cigar;
+        b->coff[i + 1] = (uint32_t)b->n_cig;
+        const int64_t Lp = ((int64_t)lq + 1) & ~1LL;
+        b->boff[i] = b->n_b;
+        const uint8_t *sq = cg + 4 * n_cigar;
+        memcpy(b->seq + b->n_b / 2, sq, (size_t)(lq + 1) / 2);
+        memcpy(b->qual + b->n_b, sq + (lq + 1) / 2, (size_t)lq);
+        if (Lp > lq) b->qual[b->n_b + lq] = 0;
+        b->n_b += Lp;
+        b->end[i] = pos + span + lq + hc + 1; /* covers every base the read can touch */
+        b->hclip[i] = hc;
+        p->last_hclip = hc;
+        p->last_kept = 1;
+        int64_t id = buf_intern(b, (const char *)data, s->read_name_len);
+        if (id < 0) goto oom;
+        b->nid[i] = (uint32_t)id;
+        {
+            bam_rec rv;
+            memset(&rv, 0, sizeof(rv));
+            rv.tid = tid;
+            rv.pos = pos;
+            rv.l_qname = (uint8_t)l_qname;
+            rv.n_cigar = (uint16_t)n_cigar;
+            rv.l_qseq = lq;
+            rv.data = (uint8_t *)data;
+            rv.data_len = (int32_t)bs - 32;
+            grom_aux ax;
+            b->aidx[i] = -1;
+            if (grom_parse_aux(&rv, target, &ax)) {
+                if (buf_grow_aux(s, b, b->n_aux + 1)) goto oom;
+                b->aidx[i] = (int32_t)b->n_aux;
+                b->aux[b->n_aux++] = ax;
+            }
+        }
+        b->n = i + 1;
+        r->ub_pos += 4 + (int64_t)bs;
+    }
+    p->m_total = m;
+    return 0;
+bad:
+    snprintf(p->err, sizeof(p->err), "piece [%llu, %llu) of target %d does not decode as records of that target",
+             (unsigned long long)p->vbeg, (unsigned long long)p->vend, run->tid);
+    return -2;
+oom:
+    snprintf(p->err, sizeof(p->err), "out of host memory decoding a piece");
+    return -1;
+}
+
+/* ---------------- buffer pool ---------------- */
+static pd_buf *pool_get(pd_session *s) {
+    pthread_mutex_lock(&s->mu);
+    for (;;) {
+        if (s->abort) { pthread_mutex_unlock(&s->mu); return NULL; }
+        if (s->free_bufs) {
+            pd_buf *b = s->free_bufs;
+            s->free_bufs = b->next;
+            pthread_mutex_unlock(&s->mu);
+            buf_reset(b);
+            return b;
+        }
+        if (s->n_bufs < s->max_bufs) {
+            s->n_bufs++;
+            pthread_mutex_unlock(&s->mu);
+            pd_buf *b = (pd_buf *)calloc(1, sizeof(pd_buf));
+            if (b) buf_reset(b);
+            return b;
+        }
+        s->buf_waiters++;
+        pthread_cond_broadcast(&s->cv);
+        pthread_cond_wait(&s->cv, &s->mu);
+        s->buf_waiters--;
+    }
+}
+
+/* uploader: buffers whose copies finished go back to the free list (force:
+ * wait for the oldest one if decoders are starved) */
+static void pool_reclaim(pd_session *s, int force) {
+    for (;;) {
+        pd_buf *b = s->inflight_head;
+        if (!b) return;
+        if (!grom_stage_ticket_done(b->stage, b->ticket)) {
+            if (!force) return;
+            (void)grom_stage_ticket_wait(b->stage, b->ticket);
+        }
+        force = 0;
+        s->inflight_head = b->next;
+        if (!s->inflight_head) s->inflight_tail = NULL;
+        pthread_mutex_lock(&s->mu);
+        b->next = s->free_bufs;
+        s->free_bufs = b;
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+    }
+}
+
+static void pool_put_now(pd_session *s, pd_buf *b) {
+    pthread_mutex_lock(&s->mu);
+    b->next = s->free_bufs;
+    s->free_bufs = b;
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+}
+
+static void pool_put_inflight(pd_session *s, pd_buf *b) {
+    b->next = NULL;
+    if (s->inflight_tail) s->inflight_tail->next = b;
+    else s->inflight_head = b;
+    s->inflight_tail = b;
+}
+
+/* ---------------- decoder threads ---------------- */
+static void *decoder_main(void *arg) {
+    pd_session *s = (pd_session *)arg;
+    pd_reader r;
+    memset(&r, 0, sizeof(r));
+    inf_init(&r.inf);
+    int64_t recs = 0;
+    double secs = 0;
+    for (;;) {
+        pthread_mutex_lock(&s->mu);
+        while (!s->abort && !s->stop && s->next_piece < s->n_pieces && s->next_piece >= s->head + s->window)
+            pthread_cond_wait(&s->cv, &s->mu);
+        if (s->abort || s->stop || s->next_piece >= s->n_pieces) {
+            pthread_mutex_unlock(&s->mu);
+            break;
+        }
+        const int idx = s->next_piece++;
+        pd_piece *p = &s->pieces[idx];
+        const int need_stats = !s->stats_done;
+        const int full = p->full;
+        p->state = 1;
+        pthread_mutex_unlock(&s->mu);
+        const double t0 = now_s();
+        int rc = 0;
+        if (!full && !need_stats) {
+            pthread_mutex_lock(&s->mu);
+            p->state = 3;
+            pthread_cond_broadcast(&s->cv);
+            pthread_mutex_unlock(&s->mu);
+            continue;
+        }
+        p->stats = need_stats;
+        pd_buf *b = NULL;
+        if (full) {
+            b = pool_get(s);
+            if (!b) { rc = -1; snprintf(p->err, sizeof(p->err), "no piece buffer"); }
+        }
+        if (rc == 0) rc = decode_piece(s, &r, p, b);
+        p->buf = b;
+        p->secs = now_s() - t0;
+        secs += p->secs;
+        recs += p->n_rec;
+        pthread_mutex_lock(&s->mu);
+        p->state = rc == 0 ? 2 : 4;
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+        if (rc != 0) sess_abort(s, rc == -2, p->err);
+    }
+    pthread_mutex_lock(&s->mu);
+    s->c_dec_s += secs;
+    s->c_inflated += r.inflated;
+    s->c_inflate_s += r.t_inflate;
+    s->c_compressed += r.compressed;
+    pthread_mutex_unlock(&s->mu);
+    rd_free(&r);
+    return NULL;
+}
+
+/* ---------------- the tail set of read names ---------------- */
+static void tail_reset(tail_set *T) {
+    T->n = 0;
+    T->arena_len = 0;
+    T->max_end = INT32_MIN;
+    if (T->ht_cap) memset(T->ht, 0, sizeof(int64_t) * (size_t)T->ht_cap);
+}
+
+static void tail_rehash(tail_set *T, int64_t want) {
+    int64_t nc = 64;
+    while (nc < 4 * want) nc *= 2;
+    if (nc != T->ht_cap) {
+        free(T->ht);
+        free(T->hh);
+        T->ht = (int64_t *)calloc((size_t)nc, sizeof(int64_t));
+        T->hh = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nc);
+        T->ht_cap = nc;
+    } else {
+        memset(T->ht, 0, sizeof(int64_t) * (size_t)nc);
+    }
+    for (int64_t i = 0; i < T->n; i++) {
+        size_t L;
+        const uint64_t h = fnv(T->arena + T->e[i].name_off, &L);
+        int64_t j = (int64_t)(h & (uint64_t)(T->ht_cap - 1));
+        while (T->ht[j]) j = (j + 1) & (T->ht_cap - 1);
+        T->ht[j] = i + 1;
+        T->hh[j] = h;
+    }
+}
+
+/* keep the entries that can still overlap a read at or after p0 */
+static void tail_filter(tail_set *T, int32_t p0) {
+    int64_t k = 0, al = 0;
+    int32_t mx = INT32_MIN;
+    for (int64_t i = 0; i < T->n; i++) {
+        if (T->e[i].end <= p0) continue;
+        const char *nm = T->arena + T->e[i].name_off;
+        const size_t L = strlen(nm);
+        memmove(T->arena + al, nm, L + 1);
+        T->e[k] = T->e[i];
+        T->e[k].name_off = al;
+        al += (int64_t)L + 1;
+        if (T->e[k].end > mx) mx = T->e[k].end;
+        k++;
+    }
+    T->n = k;
+    T->arena_len = al;
+    T->max_end = mx;
+    tail_rehash(T, k + 64);
+}
+
+static int64_t tail_find(const tail_set *T, const char *name) {
+    if (!T->n) return -1;
+    size_t L;
+    const uint64_t h = fnv(name, &L);
+    int64_t j = (int64_t)(h & (uint64_t)(T->ht_cap - 1));
+    while (T->ht[j]) {
+        const int64_t i = T->ht[j] - 1;
+        if (T->hh[j] == h && strcmp(T->arena + T->e[i].name_off, name) == 0) return i;
+        j = (j + 1) & (T->ht_cap - 1);
+    }
+    return -1;
+}
+
+static void tail_add(tail_set *T, const char *name, uint32_t gid, int32_t end) {
+    const int64_t f = tail_find(T, name);
+    if (f >= 0) {
+        if (end > T->e[f].end) T->e[f].end = end;
+        if (end > T->max_end) T->max_end = end;
+        return;
+    }
+    const size_t L = strlen(name);
+    if (T->n == T->cap) {
+        T->cap = T->cap ? 2 * T->cap : 256;
+        T->e = (tail_ent *)realloc(T->e, sizeof(tail_ent) * (size_t)T->cap);
+    }
+    if (T->arena_len + (int64_t)L + 1 > T->arena_cap) {
+        T->arena_cap = T->arena_cap ? 2 * T->arena_cap : 16384;
+        while (T->arena_len + (int64_t)L + 1 > T->arena_cap) T->arena_cap *= 2;
+        T->arena = (char *)realloc(T->arena, (size_t)T->arena_cap);
+    }
+    memcpy(T->arena + T->arena_len, name, L + 1);
+    T->e[T->n].gid = gid;
+    T->e[T->n].end = end;
+    T->e[T->n].name_off = T->arena_len;
+    T->arena_len += (int64_t)L + 1;
+    T->n++;
+    if (end > T->max_end) T->max_end = end;
+    if (4 * T->n > T->ht_cap) tail_rehash(T, T->n);
+    else {
+        uint64_t h;
+        size_t LL;
+        h = fnv(name, &LL);
+        int64_t j = (int64_t)(h & (uint64_t)(T->ht_cap - 1));
+        while (T->ht[j]) j = (j + 1) & (T->ht_cap - 1);
+        T->ht[j] = T->n;
+        T->hh[j] = h;
+    }
+}
+
+/* ---------------- host mirror (plan-only / tests) ---------------- */
+static int mirror_append(grom_batch *m, const grom_reads *p) {
+    const int64_t n = m->n + p->n;
+    if (n + 1 > m->cap) {
+        int64_t nc = m->cap ? 2 * m->cap : 4096;
+        while (nc < n + 1) nc *= 2;
+#define RA(f, t) m->f = (t *)realloc(m->f, sizeof(t) * (size_t)nc)
+        RA(pos, int32_t); RA(flag, uint16_t); RA(mapq, uint8_t); RA(mtid, int32_t); RA(mpos, int32_t);
+        RA(isize, int32_t); RA(l_qseq, int32_t); RA(base_off, int64_t); RA(name_id, uint32_t); RA(aux_idx, int32_t);
+#undef RA
+        m->cigar_off = (uint32_t *)realloc(m->cigar_off, sizeof(uint32_t) * (size_t)(nc + 1));
+        m->cap = nc;
+    }
+    if (m->n_cig + p->n_cigar_ops > m->cap_cig) {
+        int64_t nc = m->cap_cig ? m->cap_cig : 4096;
+        while (nc < m->n_cig + p->n_cigar_ops) nc *= 2;
+        m->cigar = (uint32_t *)realloc(m->cigar, sizeof(uint32_t) * (size_t)nc);
+        m->cap_cig = nc;
+    }
+    if (m->n_bases + p->n_bases > m->cap_bases) {
+        int64_t nc = m->cap_bases ? m->cap_bases : 1 << 20;
+        while (nc < m->n_bases + p->n_bases) nc *= 2;
+        m->qual = (uint8_t *)realloc(m->qual, (size_t)nc);
+        m->seq = (uint8_t *)realloc(m->seq, (size_t)nc / 2);
+        m->cap_bases = nc;
+    }
+    if (m->n_aux + p->n_aux > m->cap_aux) {
+        int64_t nc = m->cap_aux ? 2 * m->cap_aux : 1024;
+        while (nc < m->n_aux + p->n_aux) nc *= 2;
+        m->aux = (grom_aux *)realloc(m->aux, sizeof(grom_aux) * (size_t)nc);
+        m->cap_aux = nc;
+    }
+    if (m->n_drop + p->n_drop > m->cap_drop) {
+        int64_t nc = m->cap_drop ? 2 * m->cap_drop : 1024;
+        while (nc < m->n_drop + p->n_drop) nc *= 2;
+        m->drop_pos = (int32_t *)realloc(m->drop_pos, sizeof(int32_t) * (size_t)nc);
+        m->drop_lq = (int32_t *)realloc(m->drop_lq, sizeof(int32_t) * (size_t)nc);
+        m->drop_before = (int64_t *)realloc(m->drop_before, sizeof(int64_t) * (size_t)nc);
+        m->cap_drop = nc;
+    }
+    const int64_t k = p->n, o = m->n;
+    if (k > 0) {
+        memcpy(m->pos + o, p->pos, 4 * (size_t)k);
+        memcpy(m->flag + o, p->flag, 2 * (size_t)k);
+        memcpy(m->mapq + o, p->mapq, (size_t)k);
+        memcpy(m->mtid + o, p->mtid, 4 * (size_t)k);
+        memcpy(m->mpos + o, p->mpos, 4 * (size_t)k);
+        memcpy(m->isize + o, p->isize, 4 * (size_t)k);
+        memcpy(m->l_qseq + o, p->l_qseq, 4 * (size_t)k);
+        memcpy(m->cigar_off + o, p->cigar_off, 4 * (size_t)(k + 1));
+        memcpy(m->base_off + o, p->base_off, 8 * (size_t)k);
+        memcpy(m->name_id + o, p->name_id, 4 * (size_t)k);
+        if (p->aux_idx) memcpy(m->aux_idx + o, p->aux_idx, 4 * (size_t)k);
+        else memset(m->aux_idx + o, 0xff, 4 * (size_t)k);
+        memcpy(m->cigar + m->n_cig, p->cigar, 4 * (size_t)p->n_cigar_ops);
+        memcpy(m->qual + m->n_bases, p->qual, (size_t)p->n_bases);
+        memcpy(m->seq + m->n_bases / 2, p->seq, (size_t)p->n_bases / 2);
+    }
+    if (p->n_aux > 0) memcpy(m->aux + m->n_aux, p->aux, sizeof(grom_aux) * (size_t)p->n_aux);
+    if (p->n_drop > 0) {
+        memcpy(m->drop_pos + m->n_drop, p->drop_pos, 4 * (size_t)p->n_drop);
+        memcpy(m->drop_lq + m->n_drop, p->drop_lq, 4 * (size_t)p->n_drop);
+        memcpy(m->drop_before + m->n_drop, p->drop_before, 8 * (size_t)p->n_drop);
+    }
+    m->n = n;
+    m->n_cig += p->n_cigar_ops;
+    m->n_bases += p->n_bases;
+    m->n_aux += p->n_aux;
+    m->n_drop += p->n_drop;
+    if (m->n == 0) {
+        if (!m->cigar_off) m->cigar_off = (uint32_t *)calloc(1, sizeof(uint32_t));
+    }
+    return 0;
+}
+
+/* ---------------- the uploader ---------------- */
+static void apply_final(pd_session *s, int idx);
+
+static int stage_acquire(pd_session *s, int dev, grom_stage **out) {
+    pthread_mutex_lock(&s->mu);
+    for (;;) {
+        if (s->abort) { pthread_mutex_unlock(&s->mu); return -1; }
+        for (int i = 0; i < s->n_stage; i++)
+            if (!s->stage_busy[i] && s->stage_dev[i] == dev) {
+                s->stage_busy[i] = 1;
+                *out = s->stages[i];
+                pthread_mutex_unlock(&s->mu);
+                return 0;
+            }
+        /* while the insert statistics are incomplete no chromosome can be
+         * finalised, so every busy stage waits on this thread: add one */
+        if (!s->stats_done || s->n_stage < 1) {
+            pthread_mutex_unlock(&s->mu);
+            grom_stage *st = grom_stage_new(dev);
+            if (!st) return -1;
+            pthread_mutex_lock(&s->mu);
+            if (s->n_stage == s->cap_stage) {
+                s->cap_stage = s->cap_stage ? 2 * s->cap_stage : 16;
+                s->stages = (grom_stage **)realloc(s->stages, sizeof(grom_stage *) * s->cap_stage);
+                s->stage_dev = (int *)realloc(s->stage_dev, sizeof(int) * s->cap_stage);
+                s->stage_busy = (int *)realloc(s->stage_busy, sizeof(int) * s->cap_stage);
+            }
+            s->stages[s->n_stage] = st;
+            s->stage_dev[s->n_stage] = dev;
+            s->stage_busy[s->n_stage] = 1;
+            s->n_stage++;
+            *out = st;
+            pthread_mutex_unlock(&s->mu);
+            return 0;
+        }
+        pthread_cond_wait(&s->cv, &s->mu);
+    }
+}
+
+static void stats_take(pd_session *s, pd_piece *p) {
+    if (s->stats_done || !p->stats) return;
+    for (int64_t i = 0; i < p->st_n && s->s_n < PD_INSERT_CAP; i++) {
+        s->s_ins[s->s_n] = p->st_ins[i];
+        s->s_lq[s->s_n] = p->st_lq[i];
+        s->s_n++;
+        if (s->s_n == PD_INSERT_CAP) s->s_m += p->st_m[i];
+    }
+    if (s->s_n < PD_INSERT_CAP) s->s_m += p->m_total;
+}
+
+static void piece_free_stats(pd_piece *p) {
+    free(p->st_ins);
+    free(p->st_lq);
+    free(p->st_m);
+    p->st_ins = p->st_lq = NULL;
+    p->st_m = NULL;
+    p->st_n = p->st_cap = 0;
+}
+
+static void mark_stats_done(pd_session *s) {
+    pthread_mutex_lock(&s->mu);
+    s->stats_done = 1;
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+}
+
+static int chrom_begin(pd_session *s, int k, const pd_buf *first) {
+    pd_chrom *c = &s->ch[k];
+    c->begun = 1;
+    if (s->plan_only) return 0;
+    if (stage_acquire(s, c->device, &c->stage)) return -1;
+    grom_stage_sizes est;
+    memset(&est, 0, sizeof(est));
+    if (c->run >= 0) {
+        const pd_run *r = &s->runs[c->run];
+        const int64_t cnt = r->count > 0 ? r->count : 1;
+        est.n = cnt;
+        est.n_drop = first && first->n_drop ? (int64_t)((double)first->n_drop / (first->n + first->n_drop + 1) * cnt * 1.5) + 1024 : 1024;
+        if (first && first->n > 0) {
+            est.n_cigar_ops = (int64_t)((double)first->n_cig / first->n * cnt * 1.15) + 4096;
+            est.n_bases = ((int64_t)((double)first->n_b / first->n * cnt * 1.15) + 65536) & ~1LL;
+            est.n_aux = (int64_t)((double)first->n_aux / first->n * cnt * 1.5) + 1024;
+        }
+    }
+    return grom_stage_begin(c->stage, &est) == GROM_OK ? 0 : -1;
+}
+
+static int upload_piece(pd_session *s, pd_piece *p) {
+    const pd_run *run = &s->runs[p->run];
+    pd_chrom *c = &s->ch[run->chrom];
+    pd_buf *b = p->buf;
+    if (!c->begun && chrom_begin(s, run->chrom, b)) return -1;
+    const int64_t n = b->n, nd = b->n_drop;
+    /* the records the previous chromosome's walk consumed (Q1): the stream's
+     * first j0 records, in stream order (a dropped record with before == k
+     * precedes kept read k) */
+    int64_t k0 = 0, d0 = 0;
+    while (c->j_left > 0 && (k0 < n || d0 < nd)) {
+        if (d0 < nd && b->dbef[d0] == k0) d0++;
+        else k0++;
+        c->j_left--;
+    }
+    const int64_t seen = (n - k0) + (nd - d0);
+    if (seen > 0) {
+        if (!p->sorted) { sess_abort(s, 1, "records are not sorted by position"); return -1; }
+        const int32_t first_pos = (k0 < n && (d0 >= nd || b->dbef[d0] > k0)) ? b->pos[k0] : b->dpos[d0];
+        if (c->n_seen > 0 && first_pos < c->prev_pos) { sess_abort(s, 1, "records are not sorted by position"); return -1; }
+        c->prev_pos = p->last_pos;
+        c->n_seen += seen;
+        c->last_pos = p->last_pos;
+        c->last_lq = p->last_lq;
+        c->last_hclip = p->last_hclip;
+        c->last_kept = p->last_kept;
+    }
+    /* drops: to the chromosome's host list (uploaded when it is finalised) */
+    for (int64_t d = d0; d < nd; d++) {
+        if (c->n_drops == c->cap_drops) {
+            c->cap_drops = c->cap_drops ? 2 * c->cap_drops : 4096;
+            c->drops = (drop_rec *)realloc(c->drops, sizeof(drop_rec) * (size_t)c->cap_drops);
+            if (!c->drops) return -1;
+        }
+        drop_rec *q = &c->drops[c->n_drops++];
+        q->pos = b->dpos[d];
+        q->lq = b->dlq[d];
+        q->before = c->n_kept + (b->dbef[d] - k0);
+    }
+    const int64_t m = n - k0;
+    if (m > 0) {
+        /* read-name ids: piece-local -> chromosome ids, equal for equal names
+         * of reads that can share a base (T holds the earlier pieces' reads
+         * that reach this far) */
+        if (s->remap_cap < b->n_names + 1) {
+            s->remap_cap = b->n_names + 1 + 1024;
+            s->remap = (uint32_t *)realloc(s->remap, sizeof(uint32_t) * (size_t)s->remap_cap);
+            if (!s->remap) return -1;
+        }
+        s->remap[0] = 0;
+        for (int64_t l = 1; l <= b->n_names; l++) s->remap[l] = (uint32_t)(c->n_names + l);
+        tail_filter(&s->T, b->pos[k0]);
+        for (int64_t i = k0; i < n && b->pos[i] < s->T.max_end; i++) {
+            const uint32_t l = b->nid[i];
+            if (!l) continue;
+            const int64_t f = tail_find(&s->T, b->arena + b->id_off[l]);
+            if (f >= 0) s->remap[l] = s->T.e[f].gid;
+        }
+        c->n_names += b->n_names;
+        for (int64_t i = k0; i < n; i++) {
+            const uint32_t l = b->nid[i];
+            if (l && b->end[i] > p->last_pos) tail_add(&s->T, b->arena + b->id_off[l], s->remap[l], b->end[i]);
+        }
+        for (int64_t i = k0; i < n; i++) b->nid[i] = s->remap[b->nid[i]];
+        /* kept positions that may lie in the walk's skip prefix */
+        for (int64_t i = k0; i < n && b->pos[i] < PD_LOWPOS_LIMIT; i++) {
+            if (c->n_low == c->cap_low) {
+                c->cap_low = c->cap_low ? 2 * c->cap_low : 65536;
+                c->lowpos = (int32_t *)realloc(c->lowpos, sizeof(int32_t) * (size_t)c->cap_low);
+                if (!c->lowpos) return -1;
+            }
+            c->lowpos[c->n_low++] = b->pos[i];
+        }
+        /* global offsets */
+        const uint32_t c0 = b->coff[k0];
+        const int64_t b0 = b->boff[k0];
+        for (int64_t i = k0; i <= n; i++) b->coff[i] = b->coff[i] - c0 + (uint32_t)c->n_cig;
+        for (int64_t i = k0; i < n; i++) b->boff[i] = b->boff[i] - b0 + c->n_bases;
+        int64_t a0 = b->n_aux;
+        for (int64_t i = k0; i < n; i++)
+            if (b->aidx[i] >= 0) { a0 = b->aidx[i]; break; }
+        grom_reads v;
+        memset(&v, 0, sizeof(v));
+        v.n = m;
+        v.pos = b->pos + k0;
+        v.flag = b->flag + k0;
+        v.mapq = b->mapq + k0;
+        v.mtid = b->mtid + k0;
+        v.mpos = b->mpos + k0;
+        v.isize = b->isize + k0;
+        v.l_qseq = b->lq + k0;
+        v.cigar_off = b->coff + k0;
+        v.cigar = b->cig + c0 - 0; /* c0 was the piece-local offset of read k0 */
+        v.n_cigar_ops = (int64_t)b->n_cig - (int64_t)c0;
+        v.base_off = b->boff + k0;
+        v.seq = b->seq + b0 / 2;
+        v.qual = b->qual + b0;
+        v.n_bases = b->n_b - b0;
+        v.name_id = b->nid + k0;
+        if (s->splitread) {
+            for (int64_t i = k0; i < n; i++)
+                if (b->aidx[i] >= 0) b->aidx[i] = (int32_t)(b->aidx[i] - a0 + c->n_aux);
+            v.aux_idx = b->aidx + k0;
+            v.aux = b->aux + a0;
+            v.n_aux = b->n_aux - a0;
+        } else {
+            /* -S: only the walk's first ingested read keeps its SA/XP (Q13),
+             * known when the chromosome is finalised */
+            for (int64_t i = k0; i < n; i++)
+                if (b->aidx[i] >= 0) {
+                    if (c->n_saux == c->cap_saux) {
+                        c->cap_saux = c->cap_saux ? 2 * c->cap_saux : 1024;
+                        c->saux = (saux_rec *)realloc(c->saux, sizeof(saux_rec) * (size_t)c->cap_saux);
+                        if (!c->saux) return -1;
+                    }
+                    c->saux[c->n_saux].idx = c->n_kept + (i - k0);
+                    c->saux[c->n_saux].a = b->aux[b->aidx[i]];
+                    c->n_saux++;
+                }
+            v.aux_idx = NULL;
+            v.n_aux = 0;
+        }
+        if (s->plan_only) {
+            if (!s->no_mirror) mirror_append(&c->mirror, &v);
+            c->mirror_used = 1;
+        } else {
+            const int64_t t = grom_stage_append(c->stage, &v);
+            if (t < 0) return -1;
+            b->stage = c->stage;
+            b->ticket = t;
+        }
+        c->n_kept += m;
+        c->n_cig += v.n_cigar_ops;
+        c->n_bases += v.n_bases;
+        c->n_aux += v.n_aux;
+    }
+    return 0;
+}
+
+/* the walk's facts and the trims that need the insert statistics
+ * (grom_batch_add's skip branch and grom_batch_finish, GROM.c:14859-14969,
+ * 5842, 6406-6412) */
+static int chrom_finalize(pd_session *s, int k) {
+    pd_chrom *c = &s->ch[k];
+    if (!c->begun && chrom_begin(s, k, NULL)) return -1;
+    const int32_t s0 = s->index_start;
+    if (s0 > PD_LOWPOS_LIMIT) { sess_abort(s, 1, "walk index start beyond the streamed prefix limit"); return -1; }
+    int64_t sk = 0, sd = 0;
+    for (int64_t i = 0; i < c->n_low; i++) sk += c->lowpos[i] < s0;
+    while (sd < c->n_drops && c->drops[sd].pos < s0) sd++;
+    const int any = (c->n_kept + c->n_drops) > (sk + sd);
+    pd_chrom_facts *f = &c->facts;
+    memset(f, 0, sizeof(*f));
+    f->n_skip = (int32_t)(sk + sd);
+    f->n_reads = c->n_kept - sk;
+    f->n_drop = c->n_drops - sd;
+    if (any) {
+        const int32_t p = c->last_pos - s->overlap_mult * s->insert_max;
+        f->p_last = p > s0 ? p : s0;
+    } else {
+        f->p_last = -1;
+    }
+    if (c->n_seen > 0 && c->run >= 0 && s->runs[c->run].has_next) f->lseq_tail = s->runs[c->run].next_lq;
+    else if (any) f->lseq_tail = c->last_lq + (c->last_kept == 1 ? c->last_hclip : 0);
+    else f->lseq_tail = 0;
+    /* drops after the prefix, counting kept reads after the trim */
+    grom_reads dv;
+    memset(&dv, 0, sizeof(dv));
+    const int64_t ndr = c->n_drops - sd;
+    int32_t *dp = NULL, *dl = NULL;
+    int64_t *db = NULL;
+    if (ndr > 0) {
+        dp = s->plan_only ? (int32_t *)malloc(4 * (size_t)ndr) : (int32_t *)grom_pinned_alloc(4 * (size_t)ndr);
+        dl = s->plan_only ? (int32_t *)malloc(4 * (size_t)ndr) : (int32_t *)grom_pinned_alloc(4 * (size_t)ndr);
+        db = s->plan_only ? (int64_t *)malloc(8 * (size_t)ndr) : (int64_t *)grom_pinned_alloc(8 * (size_t)ndr);
+        if (!dp || !dl || !db) return -1;
+        for (int64_t d = 0; d < ndr; d++) {
+            const drop_rec *q = &c->drops[sd + d];
+            dp[d] = q->pos;
+            dl[d] = q->lq;
+            db[d] = q->before >= sk ? q->before - sk : 0;
+        }
+        dv.n_drop = ndr;
+        dv.drop_pos = dp;
+        dv.drop_lq = dl;
+        dv.drop_before = db;
+    }
+    /* -S: the first ingested record, if it is a kept read, keeps its SA/XP */
+    int64_t patch = -1;
+    grom_aux pa;
+    memset(&pa, 0, sizeof(pa));
+    if (!s->splitread && any) {
+        const int first_is_drop = sd < c->n_drops && c->drops[sd].before == sk;
+        if (!first_is_drop)
+            for (int64_t i = 0; i < c->n_saux; i++)
+                if (c->saux[i].idx == sk) { patch = sk; pa = c->saux[i].a; break; }
+    }
+    int rc = 0;
+    if (s->plan_only) {
+        grom_batch *m = &c->mirror;
+        if (patch >= 0) {
+            grom_reads one;
+            memset(&one, 0, sizeof(one));
+            one.n_aux = 1;
+            one.aux = &pa;
+            mirror_append(m, &one);
+            m->aux_idx[patch] = (int32_t)(m->n_aux - 1);
+        }
+        if (ndr > 0) mirror_append(m, &dv);
+        if (sk > 0) { /* drop the prefix from the front (the device uses a trimmed view) */
+            const int64_t r = m->n - sk;
+            memmove(m->pos, m->pos + sk, 4 * (size_t)r);
+            memmove(m->flag, m->flag + sk, 2 * (size_t)r);
+            memmove(m->mapq, m->mapq + sk, (size_t)r);
+            memmove(m->mtid, m->mtid + sk, 4 * (size_t)r);
+            memmove(m->mpos, m->mpos + sk, 4 * (size_t)r);
+            memmove(m->isize, m->isize + sk, 4 * (size_t)r);
+            memmove(m->l_qseq, m->l_qseq + sk, 4 * (size_t)r);
+            memmove(m->cigar_off, m->cigar_off + sk, 4 * (size_t)(r + 1));
+            memmove(m->base_off, m->base_off + sk, 8 * (size_t)r);
+            memmove(m->name_id, m->name_id + sk, 4 * (size_t)r);
+            memmove(m->aux_idx, m->aux_idx + sk, 4 * (size_t)r);
+            m->n = r;
+        }
+        if (!m->cigar_off) m->cigar_off = (uint32_t *)calloc(1, sizeof(uint32_t));
+        free(dp);
+        free(dl);
+        free(db);
+    } else {
+        if (patch >= 0 && grom_stage_patch_aux(c->stage, patch, &pa) != GROM_OK) rc = -1;
+        if (rc == 0 && ndr > 0) {
+            const int64_t t = grom_stage_append(c->stage, &dv);
+            /* the copies read these arrays: wait for them before they go */
+            if (t < 0 || grom_stage_ticket_wait(c->stage, t) != GROM_OK) rc = -1;
+        }
+        if (rc == 0 && grom_stage_trim(c->stage, sk) != GROM_OK) rc = -1;
+        s->c_h2d += grom_stage_bytes(c->stage);
+        grom_pinned_free(dp);
+        grom_pinned_free(dl);
+        grom_pinned_free(db);
+    }
+    free(c->drops);
+    c->drops = NULL;
+    free(c->lowpos);
+    c->lowpos = NULL;
+    free(c->saux);
+    c->saux = NULL;
+    return rc;
+}
+
+static void *uploader_main(void *arg) {
+    pd_session *s = (pd_session *)arg;
+    int next_final = 0;
+    int cur_chrom = -1;
+    for (int idx = 0; idx <= s->n_pieces; idx++) {
+        pthread_mutex_lock(&s->mu);
+        const int pend = s->final_pending && !s->final_applied;
+        pthread_mutex_unlock(&s->mu);
+        if (pend) apply_final(s, idx < s->n_pieces ? idx : s->n_pieces);
+        /* finalise every chromosome whose records are all staged */
+        for (;;) {
+            pthread_mutex_lock(&s->mu);
+            while (next_final < s->n_plan && s->final_applied && !s->ch[next_final].kept) next_final++;
+            const int ok = !s->abort && next_final < s->n_plan && s->stats_done && s->final_applied &&
+                           (s->ch[next_final].run < 0 || s->ch[next_final].uploaded);
+            pthread_mutex_unlock(&s->mu);
+            if (!ok) break;
+            const double t0 = now_s();
+            const int rc = chrom_finalize(s, next_final);
+            s->c_upl_s += now_s() - t0;
+            pthread_mutex_lock(&s->mu);
+            s->ch[next_final].rc = rc;
+            s->ch[next_final].final = 1;
+            pthread_cond_broadcast(&s->cv);
+            pthread_mutex_unlock(&s->mu);
+            if (rc) { sess_abort(s, 0, "finalising a chromosome failed"); break; }
+            next_final++;
+        }
+        if (idx == s->n_pieces) {
+            if (!s->stats_done) mark_stats_done(s);
+            /* the walk parameters may still be on their way */
+            pthread_mutex_lock(&s->mu);
+            while (!s->abort && next_final < s->n_plan && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
+            while (next_final < s->n_plan && s->final_applied && !s->ch[next_final].kept) next_final++;
+            const int more = !s->abort && next_final < s->n_plan;
+            pthread_mutex_unlock(&s->mu);
+            if (more) { idx--; continue; } /* loop back to finalise */
+            break;
+        }
+        pd_piece *p = &s->pieces[idx];
+        const double tw = now_s();
+        pthread_mutex_lock(&s->mu);
+        while (!s->abort && (p->state == 0 || p->state == 1)) {
+            if (s->buf_waiters > 0 && s->inflight_head) {
+                pthread_mutex_unlock(&s->mu);
+                pool_reclaim(s, 1);
+                pthread_mutex_lock(&s->mu);
+                continue;
+            }
+            struct timespec ts;
+            clock_gettime(CLOCK_REALTIME, &ts);
+            ts.tv_nsec += 2000000;
+            if (ts.tv_nsec >= 1000000000) { ts.tv_sec++; ts.tv_nsec -= 1000000000; }
+            pthread_cond_timedwait(&s->cv, &s->mu, &ts);
+            if (s->inflight_head) {
+                pthread_mutex_unlock(&s->mu);
+                pool_reclaim(s, 0);
+                pthread_mutex_lock(&s->mu);
+            }
+        }
+        const int aborted = s->abort;
+        pthread_mutex_unlock(&s->mu);
+        s->c_wait_s += now_s() - tw;
+        if (aborted) break;
+        const double t0 = now_s();
+        if (p->state == 2) {
+            s->c_records += p->n_rec;
+            stats_take(s, p);
+            piece_free_stats(p);
+            if (!s->stats_done && s->s_n >= PD_INSERT_CAP) mark_stats_done(s);
+        }
+        const pd_run *run = &s->runs[p->run];
+        if (p->buf && run->chrom < 0) { /* decoded for a chromosome the final plan dropped */
+            pool_put_now(s, p->buf);
+            p->buf = NULL;
+        }
+        if (p->buf && p->state == 2) {
+            if (run->chrom != cur_chrom) {
+                cur_chrom = run->chrom;
+                tail_reset(&s->T);
+            }
+            if (upload_piece(s, p)) {
+                sess_abort(s, 0, grom_last_error());
+                break;
+            }
+            if (s->plan_only || p->buf->ticket < 0) pool_put_now(s, p->buf);
+            else pool_put_inflight(s, p->buf);
+            p->buf = NULL;
+        }
+        /* a run's records all decoded: check them against the index's count */
+        if (idx == run->first_piece + run->n_pieces - 1) {
+            int64_t got = 0;
+            int all = 1;
+            for (int q = run->first_piece; q <= idx; q++) {
+                if (s->pieces[q].state != 2) all = 0;
+                got += s->pieces[q].n_rec;
+            }
+            if (all && run->count >= 0 && got != run->count) {
+                char msg[200];
+                snprintf(msg, sizeof(msg), "target %d: %lld records decoded, the index counts %lld", run->tid,
+                         (long long)got, (long long)run->count);
+                sess_abort(s, 1, msg);
+                break;
+            }
+            if (run->chrom >= 0) {
+                pthread_mutex_lock(&s->mu);
+                s->ch[run->chrom].uploaded = 1;
+                pthread_mutex_unlock(&s->mu);
+            }
+        }
+        s->c_upl_s += now_s() - t0;
+        pthread_mutex_lock(&s->mu);
+        s->head = idx + 1;
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+        pool_reclaim(s, 0);
+    }
+    /* wake everyone: the plan is done (or aborted) */
+    pthread_mutex_lock(&s->mu);
+    s->stop = 1;
+    if (!s->stats_done) s->stats_done = 1;
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+    return NULL;
+}
+
+/* ---------------- session ---------------- */
+/* The serial record stream over the runs (grom_planner_feed's state machine,
+ * GROM.c:5740, 11075-11083, 14960-14976): which run each kept plan
+ * chromosome consumes, after how many of its records (the two records the
+ * previous chromosome's loop reads past its end, Q1); a chromosome whose
+ * target has no records left starves every later one (Q21). */
+static void plan_runs(const pd_session *s, const int *keep, int *rc, int64_t *rj, int *chr) {
+    for (int i = 0; i < s->n_runs; i++) {
+        rc[i] = -1;
+        rj[i] = 0;
+    }
+    int cr = 0, stuck = 0;
+    int64_t co = 0;
+    for (int k = 0; k < s->n_plan; k++) {
+        chr[k] = -1;
+        if ((keep && !keep[k]) || stuck) continue;
+        int R = -1;
+        for (int i = 0; i < s->n_runs && s->plan[k].tid >= 0; i++)
+            if (s->runs[i].tid == s->plan[k].tid) { R = i; break; }
+        if (R < 0 || R < cr || rc[R] >= 0 || (R == cr && s->runs[R].count >= 0 && co >= s->runs[R].count)) {
+            stuck = 1;
+            continue;
+        }
+        const int64_t j0 = (R == cr) ? co : 0;
+        rc[R] = k;
+        rj[R] = j0;
+        chr[k] = R;
+        /* the foreign record and one more are consumed (Q1) */
+        int r = R + 1;
+        int64_t off = 0, drop = 2;
+        while (drop > 0 && r < s->n_runs) {
+            const int64_t cnt = s->runs[r].count >= 0 ? s->runs[r].count : INT64_MAX;
+            const int64_t take = drop < cnt - off ? drop : cnt - off;
+            off += take;
+            drop -= take;
+            if (off == cnt) { r++; off = 0; }
+        }
+        cr = r;
+        co = off;
+    }
+}
+
+/* the final plan (uploader thread, before piece `idx`): runs already being
+ * uploaded must keep their assignment, runs a decoder already took must keep
+ * whether they are decoded into buffers */
+static void apply_final(pd_session *s, int idx) {
+    int *rc = (int *)malloc(sizeof(int) * (size_t)(s->n_runs + 1));
+    int64_t *rj = (int64_t *)malloc(sizeof(int64_t) * (size_t)(s->n_runs + 1));
+    int *chr = (int *)malloc(sizeof(int) * (size_t)(s->n_plan + 1));
+    plan_runs(s, s->keep, rc, rj, chr);
+    pthread_mutex_lock(&s->mu);
+    int bad = 0;
+    for (int i = 0; i < s->n_runs && !bad; i++) {
+        const pd_run *r = &s->runs[i];
+        if (r->first_piece < idx && (rc[i] != r->chrom || rj[i] != r->j0)) bad = 1;
+        if (r->first_piece < s->next_piece && ((rc[i] >= 0) != (r->chrom >= 0))) bad = 1;
+    }
+    for (int k = 0; k < s->n_plan && !bad; k++)
+        if (!s->keep[k] && s->ch[k].begun) bad = 1;
+    if (!bad) {
+        for (int i = 0; i < s->n_runs; i++) {
+            pd_run *r = &s->runs[i];
+            r->chrom = rc[i];
+            r->j0 = rj[i];
+            for (int q = r->first_piece; q < r->first_piece + r->n_pieces; q++)
+                if (q >= s->next_piece) s->pieces[q].full = rc[i] >= 0;
+        }
+        for (int k = 0; k < s->n_plan; k++) {
+            pd_chrom *c = &s->ch[k];
+            c->kept = s->keep[k];
+            if (!c->begun) {
+                c->run = chr[k];
+                c->j_left = chr[k] >= 0 ? rj[chr[k]] : 0;
+            }
+        }
+        s->final_applied = 1;
+        pthread_cond_broadcast(&s->cv);
+    }
+    pthread_mutex_unlock(&s->mu);
+    free(rc);
+    free(rj);
+    free(chr);
+    if (bad) sess_abort(s, 1, "the final chromosome plan differs where decoding already began");
+}
+
+static int read_first_lq(int fd, int64_t fsize, uint64_t voff, int32_t *lq) {
+    pd_reader r;
+    memset(&r, 0, sizeof(r));
+    inf_init(&r.inf);
+    int rc = -1;
+    if (rd_open(&r, fd, fsize, voff, UINT64_MAX) == 0 && rd_avail(&r, 36) == 1) {
+        *lq = ldi32(r.ub + r.ub_pos + 4 + 16);
+        rc = 0;
+    }
+    rd_free(&r);
+    return rc;
+}
+
+static int cmp_run(const void *a, const void *b) {
+    const pd_run *x = (const pd_run *)a, *y = (const pd_run *)b;
+    return x->vbeg < y->vbeg ? -1 : x->vbeg > y->vbeg;
+}
+
+pd_session *pd_open(const char *bam_path, const bam_hdr *hdr, const pd_chrom_in *plan, int n_plan, int splitread,
+                    int read_name_len, int n_threads, char *why, int why_len) {
+#define FAIL(...)                                                   \
+    do {                                                            \
+        if (why) snprintf(why, (size_t)why_len, __VA_ARGS__);       \
+        goto fail;                                                  \
+    } while (0)
+    pd_session *s = (pd_session *)calloc(1, sizeof(pd_session));
+    bai_index idx;
+    memset(&idx, 0, sizeof(idx));
+    int have_idx = 0;
+    if (!s) return NULL;
+    s->fd = -1;
+    {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s.bai", bam_path);
+        if (access(path, R_OK) != 0) {
+            size_t L = strlen(bam_path);
+            if (L > 4 && strcmp(bam_path + L - 4, ".bam") == 0) snprintf(path, sizeof(path), "%.*s.bai", (int)(L - 4), bam_path);
+        }
+        if (bai_load(path, &idx) != 0) FAIL("index does not load");
+        have_idx = 1;
+    }
+    if (idx.n_ref != hdr->n_ref) FAIL("index has %d references, BAM header %d", idx.n_ref, hdr->n_ref);
+    s->fd = open(bam_path, O_RDONLY);
+    if (s->fd < 0) FAIL("cannot open BAM");
+    {
+        struct stat st;
+        if (fstat(s->fd, &st) != 0) FAIL("cannot stat BAM");
+        s->file_size = (int64_t)st.st_size;
+    }
+    /* runs of records per reference from the pseudo-bins */
+    s->runs = (pd_run *)calloc((size_t)hdr->n_ref + 1, sizeof(pd_run));
+    uint64_t max_end = 0;
+    int any_bins = 0;
+    for (int t = 0; t < idx.n_ref; t++) {
+        const bai_ref *R = &idx.ref[t];
+        const bai_bin *meta = NULL;
+        int n_real = 0;
+        for (int i = 0; i < R->n_bin; i++) {
+            if (R->bin[i].bin == 37450u) meta = &R->bin[i];
+            else if (R->bin[i].n_chunk > 0) n_real++;
+        }
+        if (!meta) {
+            if (n_real > 0) FAIL("index has no pseudo-bin for target %d", t);
+            continue;
+        }
+        if (meta->n_chunk != 2) FAIL("malformed pseudo-bin for target %d", t);
+        any_bins = 1;
+        const int64_t cnt = (int64_t)(meta->chunk[1].beg + meta->chunk[1].end);
+        if (cnt <= 0) continue;
+        pd_run *r = &s->runs[s->n_runs++];
+        r->tid = t;
+        r->count = cnt;
+        r->vbeg = meta->chunk[0].beg;
+        r->vend = meta->chunk[0].end;
+        r->chrom = -1;
+        if (r->vend > max_end) max_end = r->vend;
+    }
+    if (!any_bins && idx.n_ref > 0) FAIL("index has no pseudo-bins");
+    qsort(s->runs, (size_t)s->n_runs, sizeof(pd_run), cmp_run);
+    for (int i = 0; i < s->n_runs; i++) {
+        if (i > 0 && (s->runs[i].tid <= s->runs[i - 1].tid || s->runs[i].vbeg < s->runs[i - 1].vend))
+            FAIL("index runs are not in target order");
+        if (s->runs[i].vend <= s->runs[i].vbeg) FAIL("empty run in the index");
+    }
+    /* unplaced reads after the placed ones (their count when the index has it) */
+    if (!(idx.has_no_coor && idx.n_no_coor == 0)) {
+        pd_run *r = &s->runs[s->n_runs];
+        r->tid = -1;
+        r->count = idx.has_no_coor ? (int64_t)idx.n_no_coor : -1;
+        if (max_end == 0) {
+            bgzf_reader br;
+            bam_hdr h2;
+            if (bgzf_open_read(&br, bam_path) != 0 || bam_read_header(&br, &h2) != 0) FAIL("cannot read header");
+            max_end = (uint64_t)bgzf_tell(&br);
+            bam_free_header(&h2);
+            bgzf_close_read(&br);
+        }
+        r->vbeg = max_end;
+        r->vend = UINT64_MAX;
+        r->chrom = -1;
+        s->n_runs++;
+    }
+    /* the record after each run (the one that ends a chromosome's stream) */
+    for (int i = 0; i + 1 < s->n_runs; i++) {
+        s->runs[i].has_next = 1;
+        if (read_first_lq(s->fd, s->file_size, s->runs[i + 1].vbeg, &s->runs[i].next_lq) != 0) {
+            if (s->runs[i + 1].tid < 0 && s->runs[i + 1].count < 0) s->runs[i].has_next = 0; /* no unplaced reads */
+            else FAIL("cannot read the record after target %d", s->runs[i].tid);
+        }
+    }
+    s->n_plan = n_plan;
+    s->plan = (pd_chrom_in *)calloc((size_t)(n_plan > 0 ? n_plan : 1), sizeof(pd_chrom_in));
+    s->ch = (pd_chrom *)calloc((size_t)(n_plan > 0 ? n_plan : 1), sizeof(pd_chrom));
+    s->keep = (int *)calloc((size_t)(n_plan > 0 ? n_plan : 1), sizeof(int));
+    memcpy(s->plan, plan, sizeof(pd_chrom_in) * (size_t)n_plan);
+    {
+        int *rc = (int *)malloc(sizeof(int) * (size_t)(s->n_runs + 1));
+        int64_t *rj = (int64_t *)malloc(sizeof(int64_t) * (size_t)(s->n_runs + 1));
+        int *chr = (int *)malloc(sizeof(int) * (size_t)(n_plan + 1));
+        plan_runs(s, NULL, rc, rj, chr);
+        for (int i = 0; i < s->n_runs; i++) {
+            s->runs[i].chrom = rc[i];
+            s->runs[i].j0 = rj[i];
+        }
+        for (int k = 0; k < n_plan; k++) {
+            pd_chrom *c = &s->ch[k];
+            grom_batch_init(&c->mirror, plan[k].tid, read_name_len);
+            c->run = chr[k];
+            c->j_left = chr[k] >= 0 ? rj[chr[k]] : 0;
+            c->kept = 1;
+            s->keep[k] = 1;
+        }
+        free(rc);
+        free(rj);
+        free(chr);
+    }
+    /* pieces: each run cut at linear-index offsets into ~PD_PIECE_RECS records */
+    {
+        int cap = 1024;
+        s->pieces = (pd_piece *)calloc((size_t)cap, sizeof(pd_piece));
+        for (int i = 0; i < s->n_runs; i++) {
+            pd_run *r = &s->runs[i];
+            r->first_piece = s->n_pieces;
+            uint64_t cut[4096 + 2];
+            int nc = 0;
+            cut[nc++] = r->vbeg;
+            if (r->tid >= 0) {
+                const bai_ref *R = &idx.ref[r->tid];
+                const int64_t nw = R->n_intv > 0 ? R->n_intv : 1;
+                const double per_w = (double)r->count / (double)nw;
+                const char *pr = getenv("GROM_PIECE_RECS"); /* test hook: smaller pieces, more borders */
+                const double target = pr && atof(pr) > 0 ? atof(pr) : (double)PD_PIECE_RECS;
+                int64_t wpp = per_w > 0 ? (int64_t)(target / per_w) : nw;
+                if (wpp < 1) wpp = 1;
+                while (nw / wpp > 4096) wpp *= 2;
+                for (int64_t w = wpp; w < R->n_intv; w += wpp) {
+                    const uint64_t v = R->ioff[w];
+                    if (v > cut[nc - 1] && v < r->vend) cut[nc++] = v;
+                }
+            }
+            cut[nc] = r->vend;
+            for (int j = 0; j < nc; j++) {
+                if (s->n_pieces == cap) {
+                    cap *= 2;
+                    s->pieces = (pd_piece *)realloc(s->pieces, sizeof(pd_piece) * (size_t)cap);
+                    memset(s->pieces + cap / 2, 0, sizeof(pd_piece) * (size_t)(cap / 2));
+                }
+                pd_piece *p = &s->pieces[s->n_pieces++];
+                p->run = i;
+                p->vbeg = cut[j];
+                p->vend = cut[j + 1];
+                p->full = r->chrom >= 0;
+            }
+            r->n_pieces = s->n_pieces - r->first_piece;
+        }
+    }
+    bai_free(&idx);
+    have_idx = 0;
+    s->splitread = splitread;
+    s->read_name_len = read_name_len;
+    s->n_threads = n_threads < 1 ? 1 : n_threads;
+    s->window = 4 * s->n_threads + 8;
+    s->max_bufs = s->window + s->n_threads + 16;
+    s->s_ins = (int32_t *)malloc(sizeof(int32_t) * PD_INSERT_CAP);
+    s->s_lq = (int32_t *)malloc(sizeof(int32_t) * PD_INSERT_CAP);
+    if (!s->s_ins || !s->s_lq) FAIL("out of memory");
+    pthread_mutex_init(&s->mu, NULL);
+    pthread_cond_init(&s->cv, NULL);
+    return s;
+fail:
+    if (have_idx) bai_free(&idx);
+    if (s->fd >= 0) close(s->fd);
+    if (s->ch)
+        for (int k = 0; k < n_plan; k++) grom_batch_free(&s->ch[k].mirror);
+    free(s->ch);
+    free(s->plan);
+    free(s->keep);
+    free(s->runs);
+    free(s->pieces);
+    free(s->s_ins);
+    free(s->s_lq);
+    free(s);
+    return NULL;
+#undef FAIL
+}
+
+int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan_only) {
+    s->min_mapq_stats = min_mapq;
+    s->plan_only = plan_only;
+    s->no_mirror = plan_only && getenv("GROM_DECODE_ONLY") != NULL; /* time the decode alone */
+    s->n_dev = n_dev < 1 ? 1 : n_dev;
+    for (int k = 0; k < s->n_plan; k++) s->ch[k].device = dev_of ? dev_of[k] : 0;
+    s->thr = (pthread_t *)calloc((size_t)s->n_threads, sizeof(pthread_t));
+    for (int t = 0; t < s->n_threads; t++)
+        if (pthread_create(&s->thr[t], NULL, decoder_main, s) != 0) {
+            s->n_threads = t;
+            break;
+        }
+    if (s->n_threads == 0 || pthread_create(&s->upl, NULL, uploader_main, s) != 0) {
+        sess_abort(s, 0, "cannot start decoder threads");
+        return -1;
+    }
+    s->upl_started = 1;
+    return 0;
+}
+
+static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
+
+int pd_insert_stats(pd_session *s, double prob2, int min_mapq, int *lseq, int *imin, int *imax, long *mapped) {
+    (void)min_mapq;
+    pthread_mutex_lock(&s->mu);
+    while (!s->stats_done && !s->abort) pthread_cond_wait(&s->cv, &s->mu);
+    const int ab = s->abort;
+    pthread_mutex_unlock(&s->mu);
+    if (ab) return -2;
+    const int64_t n = s->s_n;
+    if (n == 0) return -1;
+    /* find_insert_mean's arithmetic, as grom_insert_stats */
+    qsort(s->s_ins, (size_t)n, sizeof(int), icmp);
+    int mean = s->s_ins[n / 2], lim = mean * 5, end = 0;
+    for (int64_t a = n - 1; a >= 0; a--)
+        if (s->s_ins[a] <= lim) { end = (int)a; break; }
+    end += 1;
+    mean = s->s_ins[end / 2];
+    int lo = (int)(prob2 * end / 2);
+    *imin = s->s_ins[lo];
+    *imax = s->s_ins[end - lo < n ? end - lo : n - 1];
+    qsort(s->s_lq, (size_t)n, sizeof(int), icmp);
+    *lseq = s->s_lq[n / 2];
+    if (mapped) *mapped = (long)s->s_m;
+    return mean;
+}
+
+void pd_set_walk(pd_session *s, int32_t index_start, int32_t overlap_mult, int32_t insert_max, const int *keep) {
+    pthread_mutex_lock(&s->mu);
+    for (int k = 0; k < s->n_plan; k++) s->keep[k] = keep ? (keep[k] != 0) : 1;
+    s->final_pending = 1;
+    s->index_start = index_start;
+    s->overlap_mult = overlap_mult;
+    s->insert_max = insert_max;
+    s->walk_set = 1;
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+}
+
+int pd_wait_chrom(pd_session *s, int k, grom_stage **stage, pd_chrom_facts *facts) {
+    pthread_mutex_lock(&s->mu);
+    while (!s->abort && !s->ch[k].final) pthread_cond_wait(&s->cv, &s->mu);
+    const int ab = s->abort, soft = s->abort_soft;
+    pthread_mutex_unlock(&s->mu);
+    if (ab) return soft ? 1 : GROM_E_ARG;
+    if (s->ch[k].rc) return GROM_E_ARG;
+    if (stage) *stage = s->ch[k].stage;
+    if (facts) *facts = s->ch[k].facts;
+    s->ch[k].handed = 1;
+    return 0;
+}
+
+void pd_release_stage(pd_session *s, grom_stage *st) {
+    pthread_mutex_lock(&s->mu);
+    for (int i = 0; i < s->n_stage; i++)
+        if (s->stages[i] == st) s->stage_busy[i] = 0;
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+}
+
+int pd_add_stage(pd_session *s, grom_stage *st, int device) {
+    pthread_mutex_lock(&s->mu);
+    if (s->n_stage == s->cap_stage) {
+        s->cap_stage = s->cap_stage ? 2 * s->cap_stage : 16;
+        s->stages = (grom_stage **)realloc(s->stages, sizeof(grom_stage *) * s->cap_stage);
+        s->stage_dev = (int *)realloc(s->stage_dev, sizeof(int) * s->cap_stage);
+        s->stage_busy = (int *)realloc(s->stage_busy, sizeof(int) * s->cap_stage);
+    }
+    s->stages[s->n_stage] = st;
+    s->stage_dev[s->n_stage] = device;
+    s->stage_busy[s->n_stage] = 0;
+    s->n_stage++;
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+    return 0;
+}
+
+const char *pd_error(pd_session *s) { return s->abort_msg; }
+
+int pd_mirror_view(pd_session *s, int k, grom_reads *out) {
+    if (k < 0 || k >= s->n_plan) return -1;
+    grom_batch_view(&s->ch[k].mirror, out);
+    return 0;
+}
+
+void pd_get_counters(pd_session *s, pd_counters *c) {
+    memset(c, 0, sizeof(*c));
+    pthread_mutex_lock(&s->mu);
+    c->records = s->c_records;
+    c->pieces = s->n_pieces;
+    c->inflated_bytes = s->c_inflated;
+    c->compressed_bytes = s->c_compressed;
+    c->decode_thread_s = s->c_dec_s;
+    c->inflate_s = s->c_inflate_s;
+    c->upload_s = s->c_upl_s;
+    c->wait_s = s->c_wait_s;
+    c->threads = s->n_threads;
+    pthread_mutex_unlock(&s->mu);
+    pthread_once(&ld_once, ld_init);
+    c->libdeflate = ld_alloc != NULL;
+}
+
+void pd_close(pd_session *s) {
+    if (!s) return;
+    pthread_mutex_lock(&s->mu);
+    s->stop = 1;
+    if (!s->abort) s->abort = 1; /* wake and stop everyone */
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+    for (int t = 0; t < s->n_threads && s->thr; t++) pthread_join(s->thr[t], NULL);
+    if (s->upl_started) pthread_join(s->upl, NULL);
+    /* buffers: wait for their copies, then free */
+    while (s->inflight_head) {
+        pd_buf *b = s->inflight_head;
+        (void)grom_stage_ticket_wait(b->stage, b->ticket);
+        s->inflight_head = b->next;
+        buf_destroy(b, !s->plan_only);
+    }
+    while (s->free_bufs) {
+        pd_buf *b = s->free_bufs;
+        s->free_bufs = b->next;
+        buf_destroy(b, !s->plan_only);
+    }
+    for (int i = 0; i < s->n_pieces; i++) {
+        if (s->pieces[i].buf) buf_destroy(s->pieces[i].buf, !s->plan_only);
+        piece_free_stats(&s->pieces[i]);
+    }
+    for (int i = 0; i < s->n_old; i++) grom_pinned_free(s->old_pinned[i]);
+    free(s->old_pinned);
+    for (int k = 0; k < s->n_plan; k++) {
+        grom_batch_free(&s->ch[k].mirror);
+        free(s->ch[k].drops);
+        free(s->ch[k].lowpos);
+        free(s->ch[k].saux);
+    }
+    free(s->T.e);
+    free(s->T.arena);
+    free(s->T.ht);
+    free(s->T.hh);
+    free(s->remap);
+    free(s->stages);
+    free(s->stage_dev);
+    free(s->stage_busy);
+    free(s->thr);
+    free(s->ch);
+    free(s->plan);
+    free(s->keep);
+    free(s->runs);
+    free(s->pieces);
+    free(s->s_ins);
+    free(s->s_lq);
+    if (s->fd >= 0) close(s->fd);
+    pthread_mutex_destroy(&s->mu);
+    pthread_cond_destroy(&s->cv);
+    free(s);
+}
+
+/* ---------------- digest of a read batch (tests) ---------------- */
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+static uint64_t hbytes(uint64_t h, const void *p, size_t n) {
+    const uint8_t *q = (const uint8_t *)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ q[i]) * 0x100000001b3ULL;
+    return h;
+}
+
+static int32_t ref_span(const grom_reads *r, int64_t i) {
+    int32_t span = 0;
+    for (uint32_t c = r->cigar_off[i]; c < r->cigar_off[i + 1]; c++) {
+        const int o = r->cigar[c] & 0xf;
+        if (o == GC_MATCH || o == GC_DEL || o == GC_REF_SKIP || o == GC_EQUAL || o == GC_DIFF) span += (int32_t)(r->cigar[c] >> 4);
+    }
+    return span;
+}
+
+uint64_t pd_digest(const grom_reads *r) {
+    uint64_t h = mix64((uint64_t)r->n * 31 + (uint64_t)r->n_drop);
+    int32_t max_span = 0;
+    for (int64_t i = 0; i < r->n; i++) {
+        const int32_t sp = ref_span(r, i);
+        if (sp > max_span) max_span = sp;
+    }
+    for (int64_t i = 0; i < r->n; i++) {
+        uint64_t x = 0xcbf29ce484222325ULL;
+        x = hbytes(x, &r->pos[i], 4);
+        x = hbytes(x, &r->flag[i], 2);
+        x = hbytes(x, &r->mapq[i], 1);
+        x = hbytes(x, &r->mtid[i], 4);
+        x = hbytes(x, &r->mpos[i], 4);
+        x = hbytes(x, &r->isize[i], 4);
+        x = hbytes(x, &r->l_qseq[i], 4);
+        const uint32_t c0 = r->cigar_off[i], c1 = r->cigar_off[i + 1];
+        x = hbytes(x, r->cigar + c0, 4 * (size_t)(c1 - c0));
+        const int64_t L = r->l_qseq[i];
+        x = hbytes(x, r->qual + r->base_off[i], (size_t)L);
+        x = hbytes(x, r->seq + r->base_off[i] / 2, (size_t)(L + 1) / 2);
+        if (r->aux_idx && r->aux_idx[i] >= 0 && r->aux) {
+            const grom_aux *a = &r->aux[r->aux_idx[i]];
+            x = hbytes(x, a, offsetof(grom_aux, pad));
+        } else {
+            x = hbytes(x, "-", 1);
+        }
+        h += mix64(x + (uint64_t)i * 0x9e3779b97f4a7c15ULL);
+        /* earlier reads sharing a base with this one, with the same name id
+         * (the relation the pileup's read-name de-duplication reads) */
+        if (r->name_id[i]) {
+            for (int64_t j = i - 1; j >= 0 && (int64_t)r->pos[j] + max_span > r->pos[i]; j--) {
+                if (r->name_id[j] == r->name_id[i] && r->pos[j] + ref_span(r, j) > r->pos[i])
+                    h += mix64(((uint64_t)i << 32) ^ (uint64_t)j ^ 0x5bd1e995ULL);
+            }
+        }
+    }
+    for (int64_t d = 0; d < r->n_drop; d++) {
+        uint64_t x = 0x84222325cbf29ce4ULL;
+        x = hbytes(x, &r->drop_pos[d], 4);
+        x = hbytes(x, &r->drop_lq[d], 4);
+        x = hbytes(x, &r->drop_before[d], 8);
+        h += mix64(x + (uint64_t)d * 0x632be59bd9b4e019ULL);
+    }
+    return h;
+}

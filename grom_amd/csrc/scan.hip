@@ -953,6 +953,343 @@ void grom_resident_free(grom_resident *r) {
     delete r;
 }
 
+// ---------------------------------------------------------------------------
+// Streamed input (include/grom_amd.h, "streamed input"): a chromosome's reads
+// arrive as pieces in pinned host memory; each piece is appended with async
+// copies on the stage's own stream, so the copies of chromosome k+1 overlap
+// the scan of chromosome k on the contexts' streams.
+// ---------------------------------------------------------------------------
+void *grom_pinned_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocPortable) != hipSuccess) {
+        set_err("hipHostMalloc(%zu) failed", bytes);
+        return nullptr;
+    }
+    return p;
+}
+
+void grom_pinned_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+#define GROM_STAGE_EVENTS 256
+
+struct grom_stage {
+    int device = -1;
+    hipStream_t st = nullptr;
+    // growable device arrays (slack: kernels read whole 16-byte words)
+    DevBuf pos, flag, mapq, mtid, mpos, isize, lq, coff, cig, boff, seq, qual, nid, aidx, aux, dpos, dlq, dbef, ref;
+    int64_t n = 0, n_cig = 0, n_bases = 0, n_aux = 0, n_drop = 0, ref_len = 0;
+    int64_t front = 0;  // reads trimmed from the front of the views (grom_stage_trim)
+    int32_t patch_idx = -1;
+    grom_aux patch_aux{};
+    hipEvent_t ev[GROM_STAGE_EVENTS] = {};
+    hipEvent_t all_ev = nullptr;  // every copy issued so far (the scans wait on it)
+    int64_t tickets = 0;  // appends issued (ticket t uses ev[t % GROM_STAGE_EVENTS])
+    int64_t done_upto = 0; // every ticket below this is known complete
+    int64_t bytes_h2d = 0;
+};
+
+// grow a device array keeping its first `keep` bytes (copied on the stage
+// stream, which also orders it before later appends)
+static int stage_grow(grom_stage *s, DevBuf &b, size_t need, size_t keep) {
+    if (b.cap >= need + 64) return GROM_OK;
+    size_t want = need + need / 4 + 4096;
+    void *p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) {
+        set_err("grom_stage: hipMalloc(%zu) failed", want);
+        return GROM_E_NOMEM;
+    }
+    if (b.p) {
+        if (keep) HIPCHK(hipMemcpyAsync(p, b.p, keep, hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipStreamSynchronize(s->st));
+        (void)hipFree(b.p);
+    }
+    b.p = p;
+    b.cap = want;
+    return GROM_OK;
+}
+
+grom_stage *grom_stage_new(int device) {
+    if (hipSetDevice(device) != hipSuccess) {
+        set_err("grom_stage_new: no device %d", device);
+        return nullptr;
+    }
+    grom_stage *s = new grom_stage();
+    s->device = device;
+    if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
+        set_err("grom_stage_new: stream creation failed");
+        delete s;
+        return nullptr;
+    }
+    for (int k = 0; k <= GROM_STAGE_EVENTS; k++)
+        if (hipEventCreateWithFlags(k < GROM_STAGE_EVENTS ? &s->ev[k] : &s->all_ev, hipEventDisableTiming) !=
+            hipSuccess) {
+            set_err("grom_stage_new: event creation failed");
+            grom_stage_free(s);
+            return nullptr;
+        }
+    return s;
+}
+
+void grom_stage_free(grom_stage *s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->st) (void)hipStreamSynchronize(s->st);
+    DevBuf *all[] = {&s->pos, &s->flag, &s->mapq, &s->mtid, &s->mpos, &s->isize, &s->lq, &s->coff, &s->cig, &s->boff,
+                     &s->seq, &s->qual, &s->nid, &s->aidx, &s->aux, &s->dpos, &s->dlq, &s->dbef, &s->ref};
+    for (DevBuf *b : all)
+        if (b->p) (void)hipFree(b->p);
+    for (int k = 0; k < GROM_STAGE_EVENTS; k++)
+        if (s->ev[k]) (void)hipEventDestroy(s->ev[k]);
+    if (s->all_ev) (void)hipEventDestroy(s->all_ev);
+    if (s->st) (void)hipStreamDestroy(s->st);
+    delete s;
+}
+
+int grom_stage_begin(grom_stage *s, const grom_stage_sizes *est) {
+    if (!s) { set_err("grom_stage_begin: null stage"); return GROM_E_ARG; }
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipStreamSynchronize(s->st));  // the previous chromosome's copies are done
+    s->n = s->n_cig = s->n_bases = s->n_aux = s->n_drop = s->ref_len = 0;
+    s->front = 0;
+    s->done_upto = s->tickets;
+    s->bytes_h2d = 0;
+    if (est) {
+        int rc;
+        const int64_t n = std::max<int64_t>(est->n, 1);
+        if ((rc = stage_grow(s, s->pos, 4 * n, 0)) || (rc = stage_grow(s, s->flag, 2 * n, 0)) ||
+            (rc = stage_grow(s, s->mapq, n, 0)) || (rc = stage_grow(s, s->mtid, 4 * n, 0)) ||
+            (rc = stage_grow(s, s->mpos, 4 * n, 0)) || (rc = stage_grow(s, s->isize, 4 * n, 0)) ||
+            (rc = stage_grow(s, s->lq, 4 * n, 0)) || (rc = stage_grow(s, s->coff, 4 * (n + 1), 0)) ||
+            (rc = stage_grow(s, s->boff, 8 * n, 0)) || (rc = stage_grow(s, s->nid, 4 * n, 0)) ||
+            (rc = stage_grow(s, s->aidx, 4 * n, 0)) ||
+            (rc = stage_grow(s, s->cig, 4 * (size_t)std::max<int64_t>(est->n_cigar_ops, 1), 0)) ||
+            (rc = stage_grow(s, s->qual, (size_t)std::max<int64_t>(est->n_bases, 16), 0)) ||
+            (rc = stage_grow(s, s->seq, (size_t)std::max<int64_t>(est->n_bases, 16) / 2, 0)) ||
+            (rc = stage_grow(s, s->aux, sizeof(grom_aux) * (size_t)std::max<int64_t>(est->n_aux, 1), 0)) ||
+            (rc = stage_grow(s, s->dpos, 4 * (size_t)std::max<int64_t>(est->n_drop, 1), 0)) ||
+            (rc = stage_grow(s, s->dlq, 4 * (size_t)std::max<int64_t>(est->n_drop, 1), 0)) ||
+            (rc = stage_grow(s, s->dbef, 8 * (size_t)std::max<int64_t>(est->n_drop, 1), 0)) ||
+            (rc = stage_grow(s, s->ref, (size_t)std::max<int64_t>(est->ref_len, 16), 0)))
+            return rc;
+    }
+    return GROM_OK;
+}
+
+int grom_stage_set_ref(grom_stage *s, const char *ref, int64_t len) {
+    if (!s || (!ref && len > 0) || len < 0) { set_err("grom_stage_set_ref: bad argument"); return GROM_E_ARG; }
+    HIPCHK(hipSetDevice(s->device));
+    int rc = stage_grow(s, s->ref, (size_t)std::max<int64_t>(len, 16), 0);
+    if (rc) return rc;
+    if (len > 0) HIPCHK(hipMemcpyAsync(s->ref.p, ref, (size_t)len, hipMemcpyHostToDevice, s->st));
+    s->ref_len = len;
+    s->bytes_h2d += len;
+    return GROM_OK;
+}
+
+static int stage_ticket_wait(grom_stage *s, int64_t t) {
+    if (t < s->done_upto) return GROM_OK;
+    HIPCHK(hipEventSynchronize(s->ev[t % GROM_STAGE_EVENTS]));
+    s->done_upto = t + 1;
+    return GROM_OK;
+}
+
+int64_t grom_stage_append(grom_stage *s, const grom_reads *p) {
+    if (!s || !p || p->n < 0 || (p->n > 0 && (!p->pos || !p->cigar_off || !p->base_off))) {
+        set_err("grom_stage_append: bad argument");
+        return GROM_E_ARG;
+    }
+    if (p->n_bases & 1) { set_err("grom_stage_append: n_bases must be even"); return GROM_E_ARG; }
+    HIPCHK(hipSetDevice(s->device));
+    // the event of this ticket's slot must be free (the append 256 back is done)
+    if (s->tickets >= GROM_STAGE_EVENTS) {
+        int rc = stage_ticket_wait(s, s->tickets - GROM_STAGE_EVENTS);
+        if (rc) return rc;
+    }
+    const int64_t n = s->n + p->n, nc = s->n_cig + p->n_cigar_ops, nb = s->n_bases + p->n_bases;
+    const bool has_aux = p->n_aux > 0 && p->aux;
+    const bool has_drop = p->n_drop > 0 && p->drop_pos && p->drop_lq && p->drop_before;
+    const int64_t na = s->n_aux + (has_aux ? p->n_aux : 0), nd = s->n_drop + (has_drop ? p->n_drop : 0);
+    int rc;
+    if ((rc = stage_grow(s, s->pos, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->flag, 2 * n, 2 * s->n)) ||
+        (rc = stage_grow(s, s->mapq, n, s->n)) || (rc = stage_grow(s, s->mtid, 4 * n, 4 * s->n)) ||
+        (rc = stage_grow(s, s->mpos, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->isize, 4 * n, 4 * s->n)) ||
+        (rc = stage_grow(s, s->lq, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->coff, 4 * (n + 1), 4 * (s->n + 1))) ||
+        (rc = stage_grow(s, s->boff, 8 * n, 8 * s->n)) || (rc = stage_grow(s, s->nid, 4 * n, 4 * s->n)) ||
+        (rc = stage_grow(s, s->aidx, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->cig, 4 * nc, 4 * s->n_cig)) ||
+        (rc = stage_grow(s, s->qual, nb, s->n_bases)) || (rc = stage_grow(s, s->seq, nb / 2, s->n_bases / 2)) ||
+        (rc = stage_grow(s, s->aux, sizeof(grom_aux) * na, sizeof(grom_aux) * s->n_aux)) ||
+        (rc = stage_grow(s, s->dpos, 4 * nd, 4 * s->n_drop)) || (rc = stage_grow(s, s->dlq, 4 * nd, 4 * s->n_drop)) ||
+        (rc = stage_grow(s, s->dbef, 8 * nd, 8 * s->n_drop)))
+        return rc;
+    int64_t bytes = 0;
+    auto cp = [&](DevBuf &b, int64_t off_bytes, const void *src, int64_t nbytes) -> int {
+        if (nbytes <= 0) return GROM_OK;
+        HIPCHK(hipMemcpyAsync((char *)b.p + off_bytes, src, (size_t)nbytes, hipMemcpyHostToDevice, s->st));
+        bytes += nbytes;
+        return GROM_OK;
+    };
+    const int64_t k = p->n;
+    if (k > 0) {
+        if ((rc = cp(s->pos, 4 * s->n, p->pos, 4 * k)) || (rc = cp(s->flag, 2 * s->n, p->flag, 2 * k)) ||
+            (rc = cp(s->mapq, s->n, p->mapq, k)) || (rc = cp(s->mtid, 4 * s->n, p->mtid, 4 * k)) ||
+            (rc = cp(s->mpos, 4 * s->n, p->mpos, 4 * k)) || (rc = cp(s->isize, 4 * s->n, p->isize, 4 * k)) ||
+            (rc = cp(s->lq, 4 * s->n, p->l_qseq, 4 * k)) || (rc = cp(s->coff, 4 * s->n, p->cigar_off, 4 * (k + 1))) ||
+            (rc = cp(s->boff, 8 * s->n, p->base_off, 8 * k)) ||
+            (rc = cp(s->nid, 4 * s->n, p->name_id, 4 * k)) ||
+            (rc = cp(s->cig, 4 * s->n_cig, p->cigar, 4 * p->n_cigar_ops)) ||
+            (rc = cp(s->qual, s->n_bases, p->qual, p->n_bases)) ||
+            (rc = cp(s->seq, s->n_bases / 2, p->seq, p->n_bases / 2)))
+            return rc;
+        if (p->aux_idx) {
+            if ((rc = cp(s->aidx, 4 * s->n, p->aux_idx, 4 * k))) return rc;
+        } else {
+            HIPCHK(hipMemsetAsync((char *)s->aidx.p + 4 * s->n, 0xff, 4 * (size_t)k, s->st));
+        }
+    }
+    if (has_aux && (rc = cp(s->aux, sizeof(grom_aux) * s->n_aux, p->aux, sizeof(grom_aux) * p->n_aux))) return rc;
+    if (has_drop && ((rc = cp(s->dpos, 4 * s->n_drop, p->drop_pos, 4 * p->n_drop)) ||
+                     (rc = cp(s->dlq, 4 * s->n_drop, p->drop_lq, 4 * p->n_drop)) ||
+                     (rc = cp(s->dbef, 8 * s->n_drop, p->drop_before, 8 * p->n_drop))))
+        return rc;
+    const int64_t t = s->tickets++;
+    HIPCHK(hipEventRecord(s->ev[t % GROM_STAGE_EVENTS], s->st));
+    s->n = n;
+    s->n_cig = nc;
+    s->n_bases = nb;
+    s->n_aux = na;
+    s->n_drop = nd;
+    s->bytes_h2d += bytes;
+    return t;
+}
+
+int grom_stage_ticket_done(grom_stage *s, int64_t ticket) {
+    if (!s || ticket < 0 || ticket >= s->tickets) return 1;
+    if (ticket < s->done_upto) return 1;
+    if (s->tickets - ticket > GROM_STAGE_EVENTS) return 1;  // its slot was reused after it completed
+    if (hipSetDevice(s->device) != hipSuccess) return 0;
+    hipError_t e = hipEventQuery(s->ev[ticket % GROM_STAGE_EVENTS]);
+    return e == hipSuccess ? 1 : 0;
+}
+
+int grom_stage_ticket_wait(grom_stage *s, int64_t ticket) {
+    if (!s || ticket < 0 || ticket >= s->tickets || s->tickets - ticket > GROM_STAGE_EVENTS) return GROM_OK;
+    HIPCHK(hipSetDevice(s->device));
+    return stage_ticket_wait(s, ticket);
+}
+
+int grom_stage_view(grom_stage *s, const grom_chrom *chrom, grom_chrom *dch, grom_reads *d) {
+    if (!s || !chrom || !dch || !d) { set_err("grom_stage_view: null argument"); return GROM_E_ARG; }
+    if (s->ref_len != chrom->len) {
+        set_err("grom_stage_view: reference of %lld bases staged, chromosome has %lld", (long long)s->ref_len,
+                (long long)chrom->len);
+        return GROM_E_ARG;
+    }
+    HIPCHK(hipSetDevice(s->device));
+    if (s->n == 0) {  // an empty chromosome still needs cigar_off[0] = 0
+        int rc = stage_grow(s, s->coff, 4, 0);
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(s->coff.p, 0, 4, s->st));
+    }
+    *dch = *chrom;
+    dch->ref = (const char *)s->ref.p;
+    memset(d, 0, sizeof(*d));
+    const int64_t f = s->front;
+    d->n = s->n - f;
+    d->n_cigar_ops = s->n_cig;
+    d->n_bases = s->n_bases;
+    d->pos = (const int32_t *)s->pos.p + f;
+    d->flag = (const uint16_t *)s->flag.p + f;
+    d->mapq = (const uint8_t *)s->mapq.p + f;
+    d->mtid = (const int32_t *)s->mtid.p + f;
+    d->mpos = (const int32_t *)s->mpos.p + f;
+    d->isize = (const int32_t *)s->isize.p + f;
+    d->l_qseq = (const int32_t *)s->lq.p + f;
+    d->cigar_off = (const uint32_t *)s->coff.p + f;  // absolute offsets into cigar
+    d->cigar = (const uint32_t *)s->cig.p;
+    d->base_off = (const int64_t *)s->boff.p + f;    // absolute offsets into seq/qual
+    d->seq = (const uint8_t *)s->seq.p;
+    d->qual = (const uint8_t *)s->qual.p;
+    d->name_id = (const uint32_t *)s->nid.p + f;
+    d->n_aux = s->n_aux;
+    d->aux_idx = s->n_aux > 0 ? (const int32_t *)s->aidx.p + f : nullptr;
+    d->aux = s->n_aux > 0 ? (const grom_aux *)s->aux.p : nullptr;
+    d->n_drop = s->n_drop;
+    d->drop_pos = s->n_drop > 0 ? (const int32_t *)s->dpos.p : nullptr;
+    d->drop_lq = s->n_drop > 0 ? (const int32_t *)s->dlq.p : nullptr;
+    d->drop_before = s->n_drop > 0 ? (const int64_t *)s->dbef.p : nullptr;
+    return GROM_OK;
+}
+
+int64_t grom_stage_bytes(const grom_stage *s) { return s ? s->bytes_h2d : 0; }
+
+int grom_stage_trim(grom_stage *s, int64_t n_front) {
+    if (!s || n_front < 0 || n_front > s->n) { set_err("grom_stage_trim: bad argument"); return GROM_E_ARG; }
+    s->front = n_front;
+    return GROM_OK;
+}
+
+int grom_stage_patch_aux(grom_stage *s, int64_t read_index, const grom_aux *aux) {
+    if (!s || !aux || read_index < 0 || read_index >= s->n || read_index > INT32_MAX) {
+        set_err("grom_stage_patch_aux: bad argument");
+        return GROM_E_ARG;
+    }
+    HIPCHK(hipSetDevice(s->device));
+    int rc = stage_grow(s, s->aux, sizeof(grom_aux) * (s->n_aux + 1), sizeof(grom_aux) * s->n_aux);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(s->st));  // the values below are copied from the stage itself
+    s->patch_idx = (int32_t)s->n_aux;
+    s->patch_aux = *aux;
+    HIPCHK(hipMemcpyAsync((char *)s->aux.p + sizeof(grom_aux) * s->n_aux, &s->patch_aux, sizeof(grom_aux),
+                          hipMemcpyHostToDevice, s->st));
+    HIPCHK(hipMemcpyAsync((char *)s->aidx.p + 4 * read_index, &s->patch_idx, 4, hipMemcpyHostToDevice, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));
+    s->n_aux++;
+    return GROM_OK;
+}
+
+int grom_scan_chrom_staged(int slot, grom_stage *s, const grom_chrom *chrom, grom_out *out, grom_stats *stats) {
+    Ctx *C = ctx_of(slot);
+    if (!C) return GROM_E_NODEV;
+    if (!s || !chrom || !out || !chrom->ref) { set_err("grom_scan_chrom_staged: null argument"); return GROM_E_ARG; }
+    if (s->device != C->device) {
+        set_err("grom_scan_chrom_staged: stage on device %d, context %d on device %d", s->device, slot, C->device);
+        return GROM_E_ARG;
+    }
+    HIPCHK(hipSetDevice(C->device));
+    grom_chrom dch;
+    grom_reads dr;
+    int rc = grom_stage_view(s, chrom, &dch, &dr);
+    if (rc) return rc;
+    // the scan's stream waits for every copy of the stage (device-side order)
+    HIPCHK(hipEventRecord(s->all_ev, s->st));
+    HIPCHK(hipStreamWaitEvent(C->st, s->all_ev, 0));
+    C->host_ref = chrom->ref;
+    rc = scan_device(*C, &dch, &dr, out, stats, nullptr, nullptr, 0, nullptr);
+    C->host_ref = nullptr;
+    return rc;
+}
+
+int grom_debug_counts_staged(int slot, grom_stage *s, const grom_chrom *chrom, int32_t *first_pos, int32_t *counts,
+                             int64_t counts_cap, int32_t *caf3) {
+    Ctx *C = ctx_of(slot);
+    if (!C) return GROM_E_NODEV;
+    if (!s || !chrom || !chrom->ref) { set_err("grom_debug_counts_staged: null argument"); return GROM_E_ARG; }
+    HIPCHK(hipSetDevice(C->device));
+    grom_chrom dch;
+    grom_reads dr;
+    int rc = grom_stage_view(s, chrom, &dch, &dr);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(s->st));
+    grom_out tmp{};
+    C->host_ref = chrom->ref;
+    rc = scan_device(*C, &dch, &dr, &tmp, nullptr, first_pos, counts, counts_cap, caf3);
+    C->host_ref = nullptr;
+    grom_out_free(&tmp);
+    return rc;
+}
+
 int grom_debug_counts(int device, const grom_chrom *chrom, const grom_reads *reads, int32_t *first_pos,
                       int32_t *counts, int64_t counts_cap, int32_t *caf3) {
     Ctx *C = ctx_of(device);

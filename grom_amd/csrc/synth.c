@@ -829,30 +829,223 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
     return emitted;
 }
 
-static void emit_to_bam(void *ctx, const bam_rec *b) { bam_write_rec((bgzf_writer *)ctx, b); }
+/* ---------------- the files: FASTA, BAM and its index ----------------
+ * Chromosomes are generated on parallel threads; each fills 0xff00-byte BGZF
+ * payloads (records kept inside one block when they fit, as htslib does) and
+ * queues them for a pool of compressor threads.  The index is accumulated
+ * while the records are written, with offsets as (block number << 16 | offset
+ * in the block), and mapped to file offsets once the compressed block sizes
+ * are known. */
+#include <pthread.h>
+#include <unistd.h>
+
+typedef struct {
+    unsigned char *raw, *comp;
+    int len, clen;
+} sblock;
+
+typedef struct {
+    sblock **blk;
+    int n_blk, cap_blk;
+    unsigned char *cur;
+    int cur_len;
+    bai_racc *acc;
+    char *ref;
+    int done;
+    struct swriter *w;
+} schrom;
+
+typedef struct swriter {
+    const synth_cfg *c;
+    schrom *ch;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    sblock **q;       /* blocks waiting for compression */
+    int q_head, q_tail, q_cap;
+    int next_chr, gens_left, err;
+    int order[SYNTH_MAX_CHR];
+} swriter;
+
+static void q_push(swriter *w, sblock *b) {
+    pthread_mutex_lock(&w->mu);
+    if (w->q_tail - w->q_head == w->q_cap) {
+        int nc = w->q_cap ? 2 * w->q_cap : 1024;
+        sblock **nq = (sblock **)malloc(sizeof(sblock *) * (size_t)nc);
+        for (int i = 0; i < w->q_tail - w->q_head; i++) nq[i] = w->q[(w->q_head + i) % (w->q_cap ? w->q_cap : 1)];
+        free(w->q);
+        w->q = nq;
+        w->q_tail -= w->q_head;
+        w->q_head = 0;
+        w->q_cap = nc;
+    }
+    w->q[w->q_tail % w->q_cap] = b;
+    w->q_tail++;
+    pthread_cond_signal(&w->cv);
+    pthread_mutex_unlock(&w->mu);
+}
+
+static int compress_one(sblock *b) {
+    unsigned char out[65536 + 64];
+    const int n = bgzf_block_compress(b->raw, b->len, out, 6);
+    if (n < 0) return -1;
+    b->comp = (unsigned char *)malloc((size_t)n);
+    if (!b->comp) return -1;
+    memcpy(b->comp, out, (size_t)n);
+    b->clen = n;
+    free(b->raw);
+    b->raw = NULL;
+    return 0;
+}
+
+static void sc_flush(schrom *c) {
+    if (c->cur_len == 0) return;
+    sblock *b = (sblock *)calloc(1, sizeof(sblock));
+    b->raw = c->cur;
+    b->len = c->cur_len;
+    if (c->n_blk == c->cap_blk) {
+        c->cap_blk = c->cap_blk ? 2 * c->cap_blk : 1024;
+        c->blk = (sblock **)realloc(c->blk, sizeof(sblock *) * (size_t)c->cap_blk);
+    }
+    c->blk[c->n_blk++] = b;
+    c->cur = (unsigned char *)malloc(BGZF_PAYLOAD);
+    c->cur_len = 0;
+    q_push(c->w, b);
+}
+
+static void sc_write(schrom *c, const void *src, int n) {
+    const unsigned char *p = (const unsigned char *)src;
+    while (n > 0) {
+        int take = BGZF_PAYLOAD - c->cur_len;
+        if (take > n) take = n;
+        memcpy(c->cur + c->cur_len, p, (size_t)take);
+        c->cur_len += take;
+        p += take;
+        n -= take;
+        if (c->cur_len >= BGZF_PAYLOAD) sc_flush(c);
+    }
+}
+
+static void le32(unsigned char *p, uint32_t v) { p[0] = v & 0xff; p[1] = (v >> 8) & 0xff; p[2] = (v >> 16) & 0xff; p[3] = v >> 24; }
+static void le16(unsigned char *p, uint16_t v) { p[0] = v & 0xff; p[1] = v >> 8; }
+
+static void emit_par(void *ctx, const bam_rec *b) {
+    schrom *c = (schrom *)ctx;
+    unsigned char h[36];
+    le32(h, (uint32_t)(32 + b->data_len));
+    le32(h + 4, (uint32_t)b->tid);
+    le32(h + 8, (uint32_t)b->pos);
+    h[12] = b->l_qname;
+    h[13] = b->mapq;
+    le16(h + 14, b->bin);
+    le16(h + 16, b->n_cigar);
+    le16(h + 18, b->flag);
+    le32(h + 20, (uint32_t)b->l_qseq);
+    le32(h + 24, (uint32_t)b->mtid);
+    le32(h + 28, (uint32_t)b->mpos);
+    le32(h + 32, (uint32_t)b->isize);
+    if (c->cur_len + 36 + b->data_len > BGZF_PAYLOAD && c->cur_len > 0) sc_flush(c);
+    const uint64_t vb = ((uint64_t)c->n_blk << 16) | (uint64_t)c->cur_len;
+    sc_write(c, h, 36);
+    sc_write(c, b->data, b->data_len);
+    const uint64_t ve = ((uint64_t)c->n_blk << 16) | (uint64_t)c->cur_len;
+    bai_racc_push(c->acc, b->pos < 0 ? 0 : b->pos, bam_end_pos(b), vb, ve, (b->flag & 4) != 0);
+}
+
+static void *gen_main(void *arg) {
+    swriter *w = (swriter *)arg;
+    for (;;) {
+        pthread_mutex_lock(&w->mu);
+        const int k = w->next_chr < w->c->n_chr ? w->order[w->next_chr++] : -1;
+        pthread_mutex_unlock(&w->mu);
+        if (k < 0) break;
+        schrom *c = &w->ch[k];
+        c->w = w;
+        c->acc = bai_racc_new();
+        c->cur = (unsigned char *)malloc(BGZF_PAYLOAD);
+        c->ref = synth_reference(w->c, k);
+        synth_reads(w->c, k, c->ref, emit_par, c);
+        sc_flush(c);
+        free(c->cur);
+        c->cur = NULL;
+        bai_racc_flush(c->acc);
+    }
+    pthread_mutex_lock(&w->mu);
+    w->gens_left--;
+    pthread_cond_broadcast(&w->cv);
+    pthread_mutex_unlock(&w->mu);
+    /* then help compress */
+    for (;;) {
+        pthread_mutex_lock(&w->mu);
+        while (w->q_head == w->q_tail && w->gens_left > 0) pthread_cond_wait(&w->cv, &w->mu);
+        if (w->q_head == w->q_tail) {
+            pthread_mutex_unlock(&w->mu);
+            break;
+        }
+        sblock *b = w->q[w->q_head % w->q_cap];
+        w->q_head++;
+        pthread_mutex_unlock(&w->mu);
+        if (compress_one(b)) w->err = 1;
+    }
+    return NULL;
+}
+
+typedef struct {
+    const schrom *ch;
+    int64_t *base; /* file offset of each chromosome's first block */
+    int64_t **coff; /* per chromosome: file offset of block b (n_blk + 1 entries) */
+} voff_map;
+
+static uint64_t map_voff(void *ctx, int ref, uint64_t v) {
+    const voff_map *m = (const voff_map *)ctx;
+    const int64_t b = (int64_t)(v >> 16);
+    /* the end of a block is written as the start of the next one, as
+     * bgzf_tell (and htslib) report it */
+    if (b < m->ch[ref].n_blk && (int)(v & 0xffff) == m->ch[ref].blk[b]->len) return (uint64_t)m->coff[ref][b + 1] << 16;
+    return ((uint64_t)m->coff[ref][b] << 16) | (v & 0xffff);
+}
 
 int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *bam_path) {
-    FILE *fa = fopen(fasta_path, "w");
-    if (!fa) return -1;
     {  /* a new FASTA under an old name: drop its <fasta>.info cache, which the
         * CLI (like GROM.c:22308) would otherwise trust */
         char info[4096];
         snprintf(info, sizeof(info), "%s.info", fasta_path);
         remove(info);
     }
-    char **refs = (char **)calloc(c->n_chr, sizeof(char *));
-    for (int i = 0; i < c->n_chr; i++) {
-        refs[i] = synth_reference(c, i);
+    swriter w;
+    memset(&w, 0, sizeof(w));
+    w.c = c;
+    w.ch = (schrom *)calloc((size_t)c->n_chr, sizeof(schrom));
+    pthread_mutex_init(&w.mu, NULL);
+    pthread_cond_init(&w.cv, NULL);
+    for (int i = 0; i < c->n_chr; i++) w.order[i] = i;
+    for (int a = 1; a < c->n_chr; a++) /* longest first */
+        for (int b = a; b > 0 && c->chr_len[w.order[b]] > c->chr_len[w.order[b - 1]]; b--) {
+            int t = w.order[b]; w.order[b] = w.order[b - 1]; w.order[b - 1] = t;
+        }
+    long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    int n_thr = getenv("GROM_SYNTH_THREADS") ? atoi(getenv("GROM_SYNTH_THREADS")) : (int)(ncpu < 16 ? ncpu : 16);
+    if (n_thr < 1) n_thr = 1;
+    w.gens_left = n_thr;
+    pthread_t thr[64];
+    if (n_thr > 64) n_thr = 64;
+    for (int t = 0; t < n_thr; t++) pthread_create(&thr[t], NULL, gen_main, &w);
+    for (int t = 0; t < n_thr; t++) pthread_join(thr[t], NULL);
+    int rc = w.err ? -1 : 0;
+
+    FILE *fa = fopen(fasta_path, "w");
+    if (!fa) rc = -1;
+    for (int i = 0; i < c->n_chr && fa; i++) {
         fprintf(fa, ">%s synthetic\n", c->chr_name[i]);
         for (long k = 0; k < c->chr_len[i]; k += c->fasta_line) {
             long m = c->chr_len[i] - k;
             if (m > c->fasta_line) m = c->fasta_line;
-            fwrite(refs[i] + k, 1, m, fa);
+            fwrite(w.ch[i].ref + k, 1, m, fa);
             fputc('\n', fa);
         }
     }
-    if (fclose(fa) != 0) return -1;
+    if (fa && fclose(fa) != 0) rc = -1;
 
+    /* header blocks, then each chromosome's blocks in order, then EOF */
     bam_hdr h;
     memset(&h, 0, sizeof(h));
     char text[64 * 96 + 64];
@@ -868,17 +1061,55 @@ int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *ba
         h.ref_name[i] = (char *)c->chr_name[i];
         h.ref_len[i] = (int32_t)c->chr_len[i];
     }
-    bgzf_writer w;
-    if (bgzf_open_write(&w, bam_path, 6) != 0) return -1;
-    int rc = bam_write_header(&w, &h);
-    for (int i = 0; i < c->n_chr && rc == 0; i++) {
-        synth_reads(c, i, refs[i], emit_to_bam, &w);
-        free(refs[i]);
+    voff_map vm;
+    vm.ch = w.ch;
+    vm.base = (int64_t *)calloc((size_t)c->n_chr + 1, sizeof(int64_t));
+    vm.coff = (int64_t **)calloc((size_t)c->n_chr, sizeof(int64_t *));
+    bgzf_writer bw;
+    if (rc == 0 && bgzf_open_write(&bw, bam_path, 6) != 0) rc = -1;
+    if (rc == 0) {
+        rc = bam_write_header(&bw, &h);
+        if (rc == 0 && bgzf_flush_block(&bw) != 0) rc = -1;
+        int64_t off = ftell(bw.fp);
+        for (int i = 0; i < c->n_chr && rc == 0; i++) {
+            schrom *s = &w.ch[i];
+            vm.coff[i] = (int64_t *)malloc(sizeof(int64_t) * ((size_t)s->n_blk + 1));
+            for (int b = 0; b < s->n_blk; b++) {
+                vm.coff[i][b] = off;
+                if (fwrite(s->blk[b]->comp, 1, (size_t)s->blk[b]->clen, bw.fp) != (size_t)s->blk[b]->clen) rc = -1;
+                off += s->blk[b]->clen;
+            }
+            vm.coff[i][s->n_blk] = off;
+        }
+        if (bgzf_close_write(&bw) != 0) rc = -1;
     }
-    if (bgzf_close_write(&w) != 0) rc = -1;
+    if (rc == 0) {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s.bai", bam_path);
+        bai_racc **R = (bai_racc **)calloc((size_t)c->n_chr, sizeof(bai_racc *));
+        for (int i = 0; i < c->n_chr; i++) R[i] = w.ch[i].acc;
+        rc = bai_write_racc(path, R, c->n_chr, 0, map_voff, &vm);  /* a real index, as samtools index writes */
+        free(R);
+    }
+    for (int i = 0; i < c->n_chr; i++) {
+        schrom *s = &w.ch[i];
+        for (int b = 0; b < s->n_blk; b++) {
+            free(s->blk[b]->raw);
+            free(s->blk[b]->comp);
+            free(s->blk[b]);
+        }
+        free(s->blk);
+        free(s->ref);
+        bai_racc_free(s->acc);
+        free(vm.coff[i]);
+    }
+    free(vm.coff);
+    free(vm.base);
+    free(w.ch);
+    free(w.q);
     free(h.ref_name);
     free(h.ref_len);
-    free(refs);
-    if (rc == 0) rc = bai_build(bam_path);  /* a real index, as samtools index writes */
+    pthread_mutex_destroy(&w.mu);
+    pthread_cond_destroy(&w.cv);
     return rc;
 }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GROM_AMD_ABI_VERSION 4
+#define GROM_AMD_ABI_VERSION 5
 #define GROM_MAX_TRIALS 1000 /* max_trials, GROM.c:631 */
 
 enum {
@@ -335,6 +335,58 @@ grom_resident *grom_resident_new(int device, const grom_chrom *chrom, const grom
                                  grom_reads *dev_reads);
 int64_t grom_resident_bytes(const grom_resident *r);
 void grom_resident_free(grom_resident *r);
+
+/* ---- streamed input (ABI 5) ----
+ * The reference pulls records one at a time from htslib into its ring
+ * (my_samread, GROM.c:981-992; the reader thread GROM.c:82-324).  Here a
+ * caller decodes pieces of a chromosome (runs of consecutive records) into
+ * PINNED host memory (grom_pinned_alloc) in grom_reads form and appends them
+ * to a stage: every append is a set of async host->device copies on the
+ * stage's own stream, so a decoder refills one piece while the previous one
+ * is in flight and a chromosome's copies overlap the scan of the one before
+ * it (which runs on a context's stream).  A piece's offsets must already be
+ * global for the chromosome: cigar_off (n+1 entries) and base_off count from
+ * the start of the chromosome's arrays, aux_idx indexes its aux array,
+ * drop_before counts every kept read appended before (the stage concatenates
+ * pieces as given).  n_bases must be even (every read starts on a byte). */
+typedef struct grom_stage grom_stage;
+typedef struct grom_stage_sizes {
+    int64_t n, n_cigar_ops, n_bases, n_aux, n_drop, ref_len; /* capacity hints */
+} grom_stage_sizes;
+void *grom_pinned_alloc(size_t bytes); /* page-locked host memory, NULL on failure */
+void grom_pinned_free(void *p);
+grom_stage *grom_stage_new(int device);
+void grom_stage_free(grom_stage *s);
+/* start a new chromosome (waits for the stage's previous copies; the caller
+ * must not reuse a stage whose scan is still running); est may be NULL */
+int grom_stage_begin(grom_stage *s, const grom_stage_sizes *est);
+/* async upload of the chromosome's reference bases (host memory) */
+int grom_stage_set_ref(grom_stage *s, const char *ref, int64_t len);
+/* append one piece; returns a ticket >= 0 (or a negative GROM_E_* code).
+ * The piece's host memory may be reused once grom_stage_ticket_done returns 1
+ * or grom_stage_ticket_wait returns. */
+int64_t grom_stage_append(grom_stage *s, const grom_reads *piece);
+int grom_stage_ticket_done(grom_stage *s, int64_t ticket);
+int grom_stage_ticket_wait(grom_stage *s, int64_t ticket);
+/* views start after the first n_front appended reads (the walk's skip prefix,
+ * known once the insert statistics are): cigar_off/base_off/aux_idx stay
+ * absolute, drop_before must count kept reads after the trim */
+int grom_stage_trim(grom_stage *s, int64_t n_front);
+/* give appended read `read_index` (counted before any trim) the split-read
+ * alignment *aux (the one record -S still parses) */
+int grom_stage_patch_aux(grom_stage *s, int64_t read_index, const grom_aux *aux);
+/* host->device bytes issued for the current chromosome */
+int64_t grom_stage_bytes(const grom_stage *s);
+/* device views of the staged chromosome (chrom->len must equal the staged
+ * reference); the arrays stay valid until the next grom_stage_begin */
+int grom_stage_view(grom_stage *s, const grom_chrom *chrom, grom_chrom *dev_chrom, grom_reads *dev_reads);
+/* scan the staged chromosome from context `slot` (same device): the scan's
+ * stream waits for the stage's copies; chrom->ref is the HOST copy of the
+ * reference (the breakpoint rows read it) */
+int grom_scan_chrom_staged(int slot, grom_stage *s, const grom_chrom *chrom, grom_out *out, grom_stats *stats);
+/* grom_debug_counts on a staged chromosome */
+int grom_debug_counts_staged(int slot, grom_stage *s, const grom_chrom *chrom, int32_t *first_pos, int32_t *counts,
+                             int64_t counts_cap, int32_t *caf3);
 
 /* The drop-in command line (GROM's main, GROM.c:21865) as a library call:
  * argv as for `GROM -i BAM -r FASTA -o OUT [options]`; returns the exit code.

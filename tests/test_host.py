@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 15
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.grom_abi_version() == 4
+    assert lib.grom_abi_version() == 5
     # the ctypes mirror has the C layout of every ABI struct
     for i, st in enumerate((grom_amd.Params, grom_amd.Chrom, grom_amd.Reads, grom_amd.Out, grom_amd.Stats,
                               grom_amd.IndelRec, grom_amd.Aux, grom_amd.SvRec)):
@@ -55,7 +55,7 @@ def parse_plan(stdout):
         if line.startswith("plan "):
             f = line.split()
             kv = dict(x.split("=") for x in f[2:])
-            out[f[1]] = {k: int(v) for k, v in kv.items()}
+            out[f[1]] = {k: int(v, 16 if k == "digest" else 10) for k, v in kv.items()}
     return out
 
 
@@ -85,6 +85,33 @@ def test_stream_plan_matches_oracle_walk(datadir, case):
             assert p["p_last"] + 1 == meta["p_end"], (name, p, meta)
         else:
             assert meta["n_ingested"] == 0
+
+
+@pytest.mark.parametrize("case,extra", [(c, []) for c in CASES] + [("sv", ["-S"]), ("dups", ["-M"]),
+                                                                    ("sv", ["-l", "2"])],
+                         ids=[c for c in CASES] + ["sv_S", "dups_M", "sv_l2"])
+def test_streamed_decode_matches_serial_reader(datadir, case, extra):
+    """The parallel, index-driven decoder (pdecode.c: pieces cut at BAI
+    offsets, decoded by several threads, fixed up in file order) hands every
+    chromosome's scan exactly the input of the serial reader (stream.c, the
+    restated my_samread loop): same stream facts (skip prefix, last base,
+    pending record length, Q1/Q21) and the same digest of every array, CIGAR,
+    base, quality and SA/XP record, dropped record, and of which overlapping
+    reads share a read name.  Small pieces (GROM_PIECE_RECS) force many piece
+    borders inside each chromosome."""
+    bam, fa = synth(datadir, case, CASES[case])
+    base = ["-i", bam, "-r", fa, "-o", f"pd_{case}.vcf"] + extra
+    ser = run(GROM_BIN, base, str(datadir), {"GROM_PLAN_ONLY": "1", "GROM_SERIAL_DECODE": "1"})
+    out = {}
+    for thr, recs in (("1", "1000"), ("4", "777"), ("3", "65536")):
+        r = run(GROM_BIN, base, str(datadir), {"GROM_PLAN_ONLY": "1", "GROM_DECODE_THREADS": thr,
+                                               "GROM_PIECE_RECS": recs, "GROM_VERBOSE": "1"})
+        assert "streamed decode:" in r.stdout, r.stdout[-2000:]
+        out[thr] = sorted(l for l in r.stdout.splitlines() if l.startswith("plan "))
+    want = sorted(l for l in ser.stdout.splitlines() if l.startswith("plan "))
+    assert want
+    for thr, got in out.items():
+        assert got == want, (thr, got, want)
 
 
 def test_q21_empty_chromosome_starves_later_ones(datadir):
