@@ -57,7 +57,18 @@ namespace {
 // ---- fixed parameters of the reference (not on its command line) ----
 constexpr int NBINS = 101;                 // g_num_gc_bins, GROM.c:947
 constexpr int REP_SEGS = 10;               // g_repeat_segments, GROM.c:732
-constexpr long SAMPLE_LEN = 100000;        // g_sample_lists_len, GROM.c:725
+// g_sample_lists_len, GROM.c:725; GROM_SAMPLE_LISTS_LEN lowers it (test hook:
+// the reservoir draws of GROM.c:18292/18393 then fire on small inputs, and
+// the oracle reads the same variable)
+static long sample_len() {
+    static const long v = [] {
+        const char *e = getenv("GROM_SAMPLE_LISTS_LEN");
+        const long x = e ? atol(e) : 0;
+        return (x > 0 && x < 100000) ? x : 100000L;
+    }();
+    return v;
+}
+#define SAMPLE_LEN sample_len()
 constexpr long REDUCTION = 1;              // g_genome_reduction_factor, GROM.c:726
 constexpr long BLOCK_FACTOR = 4;           // g_block_factor, GROM.c:738
 constexpr long BLOCK_UNIT = 10000;         // g_block_unit_size, GROM.c:740
@@ -2554,13 +2565,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         Gathered g;
         if ((rc = gather(S, st, rg, tot, gcw, acw, d_mq, d_rd, d_low, nullptr, g, err, errlen))) return rc;
         int last_low = 0;
+        long res_over = 0, res_repl = 0;  // reservoir draws past a full list (GROM_CNV_STATS)
         auto push = [&](int k, int bin, int v) {
             if (idx[k][bin] < SAMPLE_LEN) {
                 smp[k][bin].push_back(v);
                 idx[k][bin] += 1;
                 all[k][bin] += 1;
             } else {
-                if (rng.grom_rand(all[k][bin]) == 0) smp[k][bin][rng.grom_rand(idx[k][bin])] = v;
+                res_over++;
+                if (rng.grom_rand(all[k][bin]) == 0) { smp[k][bin][rng.grom_rand(idx[k][bin])] = v; res_repl++; }
                 all[k][bin] += 1;
             }
         };
@@ -2592,7 +2605,8 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         mb_idx[seg]++;
                         mb_all[seg]++;
                     } else {
-                        if (rng.grom_rand(mb_all[seg]) == 0) rsmp[seg][rng.grom_rand(mb_idx[seg])] = rgth.rt[o];
+                        res_over++;
+                        if (rng.grom_rand(mb_all[seg]) == 0) { rsmp[seg][rng.grom_rand(mb_idx[seg])] = rgth.rt[o]; res_repl++; }
                         mb_all[seg]++;
                     }
                 }
@@ -2607,6 +2621,10 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         }
         for (int k = 0; k < 2; k++)
             for (int b = 0; b < NBINS; b++) sort_depths(smp[k][b]);
+        if (const char *sp = getenv("GROM_CNV_STATS")) {
+            FILE *sf = fopen(sp, "a");
+            if (sf) { fprintf(sf, "%s over=%ld repl=%ld\n", chr_name, res_over, res_repl); fclose(sf); }
+        }
         // thin bins borrow their +-2 neighbours' samples, GROM.c:18480-18548
         for (int k = 0; k < 2; k++) {
             std::vector<std::vector<int>> add(NBINS);

@@ -83,17 +83,79 @@ void synth_default_cfg(synth_cfg *c) {
     c->seed = 2;
 }
 
+/* record i of a FASTA: its letters (case kept), NUL-terminated */
+static char *fasta_record(const char *path, int want, long *len_out) {
+    FILE *f = fopen(path, "r");
+    if (!f) return NULL;
+    char line[1 << 16];
+    int rec = -1;
+    long n = 0, cap = 1 << 20;
+    char *s = NULL;
+    while (fgets(line, sizeof(line), f)) {
+        if (line[0] == '>') {
+            if (rec == want) break;
+            rec++;
+            if (rec == want) s = (char *)malloc((size_t)cap);
+            continue;
+        }
+        if (rec != want) continue;
+        for (const char *q = line; *q; q++) {
+            if (!((*q >= 'A' && *q <= 'Z') || (*q >= 'a' && *q <= 'z'))) continue;
+            if (n + 1 >= cap) { cap *= 2; s = (char *)realloc(s, (size_t)cap); }
+            s[n++] = *q;
+        }
+    }
+    fclose(f);
+    if (s) s[n] = 0;
+    if (len_out) *len_out = n;
+    return s;
+}
+
+int synth_cfg_from_fasta(synth_cfg *c, const char *path) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    char line[1 << 16];
+    c->n_chr = 0;
+    while (fgets(line, sizeof(line), f)) {
+        if (line[0] == '>') {
+            if (c->n_chr == SYNTH_MAX_CHR) break;
+            int k = 0;
+            while (line[1 + k] && line[1 + k] > ' ' && k < 47) { c->chr_name[c->n_chr][k] = line[1 + k]; k++; }
+            c->chr_name[c->n_chr][k] = 0;
+            c->chr_len[c->n_chr++] = 0;
+            continue;
+        }
+        if (c->n_chr == 0) continue;
+        for (const char *q = line; *q; q++)
+            if ((*q >= 'A' && *q <= 'Z') || (*q >= 'a' && *q <= 'z')) c->chr_len[c->n_chr - 1]++;
+    }
+    fclose(f);
+    c->ref_fasta = path;
+    return c->n_chr > 0 ? 0 : -1;
+}
+
 char *synth_reference(const synth_cfg *c, int ci) {
+    if (c->ref_fasta) return fasta_record(c->ref_fasta, ci, NULL);
     long n = c->chr_len[ci];
     char *s = (char *)malloc((size_t)n + 1);
     xrng r;
     xseed(&r, c->seed, (uint64_t)ci + 1, 1);
     double gc = 0.41;
-    for (long i = 0; i < n; i++) {
-        if (i % 100000 == 0) gc = c->gc_lo + (c->gc_hi - c->gc_lo) * xunif(&r);
-        double u = xunif(&r);
-        if (u < gc) s[i] = (u < gc * 0.5) ? 'G' : 'C';
-        else s[i] = (u < gc + (1.0 - gc) * 0.5) ? 'A' : 'T';
+    if (c->ref_period > 0) { /* one pattern, repeated */
+        const long P = c->ref_period < n ? c->ref_period : n;
+        for (long i = 0; i < P; i++) {
+            double u = xunif(&r);
+            if (u < gc) s[i] = (u < gc * 0.5) ? 'G' : 'C';
+            else s[i] = (u < gc + (1.0 - gc) * 0.5) ? 'A' : 'T';
+        }
+        for (long i = P; i < n; i++) s[i] = s[i - P];
+    } else {
+        for (long i = 0; i < n; i++) {
+            if (i % 100000 == 0) gc = c->gc_lo + (c->gc_hi - c->gc_lo) * xunif(&r);
+            double u = xunif(&r);
+            if (u < gc) s[i] = (u < gc * 0.5) ? 'G' : 'C';
+            else s[i] = (u < gc + (1.0 - gc) * 0.5) ? 'A' : 'T';
+        }
     }
     /* dinucleotide repeat runs */
     if (c->repeat_rate > 0) {
@@ -439,6 +501,12 @@ static int synth_sv_events(const synth_cfg *c, sv_event **out) {
             case SV_INV: L = 600 + xint(&g, 4000); break;
             case SV_INS: L = 150 + xint(&g, 300); break; /* inserted length (novel sequence) */
             default: L = 1;
+            }
+            if (hi - lo <= L + 2) { /* dense SVs: a slot narrower than two telomere margins */
+                lo = (long)i * span + 1500;
+                hi = (long)(i + 1) * span - 1500;
+                if (lo < c->telomere_n + 4000) lo = c->telomere_n + 4000;
+                if (hi > len - c->telomere_n - 4000) hi = len - c->telomere_n - 4000;
             }
             if (hi - lo <= L + 2) continue;
             long st = lo + xint(&g, hi - lo - (type == SV_INS || type == SV_CTX ? 1 : L));
@@ -1034,7 +1102,15 @@ int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *ba
 
     FILE *fa = fopen(fasta_path, "w");
     if (!fa) rc = -1;
-    for (int i = 0; i < c->n_chr && fa; i++) {
+    if (fa && c->ref_fasta) { /* the given FASTA, byte for byte */
+        FILE *in = fopen(c->ref_fasta, "rb");
+        char buf[1 << 16];
+        size_t k;
+        if (!in) rc = -1;
+        while (in && (k = fread(buf, 1, sizeof(buf), in)) > 0) fwrite(buf, 1, k, fa);
+        if (in) fclose(in);
+    }
+    for (int i = 0; i < c->n_chr && fa && !c->ref_fasta; i++) {
         fprintf(fa, ">%s synthetic\n", c->chr_name[i]);
         for (long k = 0; k < c->chr_len[i]; k += c->fasta_line) {
             long m = c->chr_len[i] - k;

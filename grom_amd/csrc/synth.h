@@ -55,6 +55,12 @@ typedef struct synth_cfg {
                              clips and unmapped mates; 0 = none */
     double sv_evidence;   /* evidence depth: pairs per breakpoint as a
                              fraction of the spanning-fragment depth */
+    const char *ref_fasta; /* non-NULL: the chromosomes are this FASTA's records
+                             (names, lengths and bases, case kept; written out
+                             byte for byte), reads simulated from them */
+    int ref_period;       /* > 0: the reference repeats one random pattern of
+                             this length (every window has the same GC: one
+                             GC bin takes every CNV depth sample) */
     int ploidy;           /* donor haplotypes (2; 4 for the -p 4 configuration):
                              variants sit on a random non-empty subset, so
                              allele fractions are k/ploidy */
@@ -62,6 +68,8 @@ typedef struct synth_cfg {
 } synth_cfg;
 
 void synth_default_cfg(synth_cfg *c);
+/* names and lengths of an existing FASTA's records into c (-F); 0 or -1 */
+int synth_cfg_from_fasta(synth_cfg *c, const char *path);
 
 /* Generate chromosome i's reference sequence (chr_len bytes, not NUL-terminated,
  * returned buffer has one extra NUL). Deterministic in (seed, i). */

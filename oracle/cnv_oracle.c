@@ -321,6 +321,10 @@ static void cnv_list_free(cnv_list *l) { free(l->start); free(l->end); free(l->s
 
 /* detect_del_dup, GROM.c:18228-20358 (g_normal == 0 branch; the CN loop and
  * the 1000gen side file excluded as noted in the header) */
+/* test hook: samples that met a full list (the reservoir draws of
+ * GROM.c:18292, 18393-18451) and how many replaced a kept sample */
+static long g_res_over, g_res_repl;
+
 static void detect_del_dup(long len, const int *gc_w, const int *acgt_w, const int *mql, const int *rd, const int *low,
                            const cnv_pre *pre, int ploidy, cnv_list *del, cnv_list *dup) {
     long pos;
@@ -348,7 +352,8 @@ static void detect_del_dup(long len, const int *gc_w, const int *acgt_w, const i
                         mb_idx[seg] += 1;
                         mb_all[seg] += 1;
                     } else {
-                        if (grom_rand(mb_all[seg]) == 0) g_sample_rep[seg][grom_rand(mb_idx[seg])] = RDT(pos);
+                        g_res_over++;
+                        if (grom_rand(mb_all[seg]) == 0) { g_sample_rep[seg][grom_rand(mb_idx[seg])] = RDT(pos); g_res_repl++; }
                         mb_all[seg] += 1;
                     }
                 }
@@ -381,7 +386,11 @@ static void detect_del_dup(long len, const int *gc_w, const int *acgt_w, const i
             IDX[BIN] += 1;                                                        \
             ALL[BIN] += 1;                                                        \
         } else {                                                                  \
-            if (grom_rand(ALL[BIN]) == 0) LIST[BIN][grom_rand(IDX[BIN])] = (VAL); \
+            g_res_over++;                                                         \
+            if (grom_rand(ALL[BIN]) == 0) {                                       \
+                LIST[BIN][grom_rand(IDX[BIN])] = (VAL);                           \
+                g_res_repl++;                                                     \
+            }                                                                     \
             ALL[BIN] += 1;                                                        \
         }                                                                         \
     } while (0)
@@ -1013,7 +1022,12 @@ static void cnv_chromosome(long len, const char *fa, const cnv_pre *pre, int *mq
     g_lowvar_block_start_list[0] = g_insert_mean - 1;
     g_lowvar_block_end_list[0] = len - W;
     g_lowvar_block_index = 1;
+    g_res_over = g_res_repl = 0;
     detect_del_dup(len, pre->gc_w, pre->acgt_w, mql, rd, low, pre, ploidy, &del, &dup);
+    if (getenv("GROM_CNV_STATS")) {
+        FILE *sf = fopen(getenv("GROM_CNV_STATS"), "a");
+        if (sf) { fprintf(sf, "%s over=%ld repl=%ld\n", chr_name, g_res_over, g_res_repl); fclose(sf); }
+    }
     /* p value (Q8: t = 1/(1+p+x)) and filter, GROM.c:17139-17236 */
     double p = 0.3275911, a1 = 0.254829592, a2 = -0.284496736, a3 = 1.421413741, a4 = -1.453152027,
            a5 = 1.061405429;

@@ -354,6 +354,7 @@ typedef struct {
     orc_indel *ind; /* CIGAR indel evidence per position (row A7) */
     uint8_t *ind_touched;            /* some I/D op reached the base */
     int32_t *conc, *ins;             /* cdp_one_base_conc / cdp_one_base_ins (row A9) */
+    int32_t *rd_add;                 /* the A9 part of cdp_one_base_rd (dump only) */
 } win_t;
 
 #define ORC_OTHER_LEN 50 /* g_other_len, GROM.c:837 */
@@ -610,7 +611,14 @@ static void indel_fold(scan_t *s, long x, int type, int add, long len, const cha
 }
 
 /* window accessors for the breakpoint restatement (sv_oracle.c) */
-static int32_t *acc_rd(void *u, long x) { scan_t *s = (scan_t *)u; return &s->w.c[wslot(&s->w, x)].rd; }
+/* the pair binning's depth adds go into cdp_one_base_rd; rd_add keeps them
+ * apart for the breakpoint-record dump (grom_sv_rec.rd_add) */
+static void acc_rd_inc(void *u, long x) {
+    scan_t *s = (scan_t *)u;
+    const long sl = wslot(&s->w, x);
+    s->w.c[sl].rd += 1;
+    s->w.rd_add[sl] += 1;
+}
 static int32_t *acc_conc(void *u, long x) { scan_t *s = (scan_t *)u; return &s->w.conc[wslot(&s->w, x)]; }
 static int32_t *acc_ins(void *u, long x) { scan_t *s = (scan_t *)u; return &s->w.ins[wslot(&s->w, x)]; }
 static void acc_indel(void *u, long x, int type, int add, long len) { indel_fold((scan_t *)u, x, type, add, len, NULL); }
@@ -850,7 +858,7 @@ static void ingest(scan_t *s, cur_t *c) {
         r.aux_same_chr = strncmp(s->target_name, c->aux_chr, strlen(s->target_name)) == 0;
         sv_aux_cigar(c->aux_cigar, &r.aux_start_adj, &r.aux_end_adj, &r.aux_end_adj_indel); /* GROM.c:6683-6733 */
     }
-    sv_ctx X = {&s->ring, s->one_base_index, s->p, acc_rd, acc_conc, acc_ins, acc_indel, s,
+    sv_ctx X = {&s->ring, s->one_base_index, s->p, acc_rd_inc, acc_conc, acc_ins, acc_indel, s,
                 g_insert_max_size, g_insert_min_size, g_insert_mean, g_sc_min, g_min_mapq, g_max_split_loss,
                 g_min_sr_len, g_lseq};
     sv_ingest(&X, &r);
@@ -858,7 +866,7 @@ static void ingest(scan_t *s, cur_t *c) {
 
 static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_match, int chr_match,
                             const char *fasta, long chr_len, const char *chr_name, FILE *vcf, FILE *ctx_raw,
-                            FILE *dump_cnt, FILE *dump_ind) {
+                            FILE *dump_cnt, FILE *dump_ind, FILE *dump_sv) {
     scan_t s;
     memset(&s, 0, sizeof(s));
     /* srand(time()) per chromosome, GROM.c:1584; GROM_SEED pins it */
@@ -876,6 +884,7 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     s.w.ind = (orc_indel *)calloc(s.w.W, sizeof(orc_indel));
     s.w.ind_touched = (uint8_t *)calloc(s.w.W, 1);
     s.w.conc = (int32_t *)calloc(s.w.W, sizeof(int32_t));
+    s.w.rd_add = (int32_t *)calloc(s.w.W, sizeof(int32_t));
     s.w.ins = (int32_t *)calloc(s.w.W, sizeof(int32_t));
     sv_ring_init(&s.ring, g_one_base_rd_len);
     sv_lists_init(&s.lists, g_sv_list_len);
@@ -940,13 +949,44 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                                     r.other_len = sv_other_len(&s.ring, idx); /* GROM.c:11415-11425 */
                                     fwrite(&r, sizeof(r), 1, dump_ind);
                                 }
+                                /* breakpoint cluster state of the base (rows A8/A9), the
+                                 * records grom_debug_sv returns: every base with a cluster
+                                 * count or an occupied "other" slot */
+                                if (dump_sv) {
+                                    orc_sv_rec v;
+                                    memset(&v, 0, sizeof(v));
+                                    v.pos = p;
+                                    v.other_len = sv_other_len(&s.ring, idx);
+                                    int any = v.other_len > 0;
+                                    for (int t = 0; t < CL_N; t++) {
+                                        const clus_t *q = &s.ring.cl[t][idx];
+                                        v.cnt[t] = q->cnt;
+                                        v.rs[t] = q->rs;
+                                        v.re[t] = q->re;
+                                        v.dist[t] = q->dist;
+                                        any = any || q->cnt != 0;
+                                    }
+                                    v.ctx_mchr[0] = s.ring.ctx_mchr[0][idx];
+                                    v.ctx_mchr[1] = s.ring.ctx_mchr[1][idx];
+                                    v.rd_add = s.w.rd_add[sl_];
+                                    v.conc = s.w.conc[sl_];
+                                    v.ins = s.w.ins[sl_];
+                                    v.mun_f = s.ring.mun[0][idx];
+                                    v.mun_r = s.ring.mun[1][idx];
+                                    if (any) fwrite(&v, sizeof(v), 1, dump_sv);
+                                }
                             }
                             /* SNV test, GROM.c:11096-11199 */
                             if (k->rd + k->indel_sc_rd > 0 && fasta[p] != 'N' && fasta[p] != 'n') {
                                 int total = 0;
                                 for (int a = 0; a < 4; a++) total += k->snv[a];
-                                for (int a = 0; a < 4; a++) {
-                                    float ratio = (float)k->snv[a] / (float)total;
+                                /* the alt kept at this base: the first passing base with the
+                                 * largest ratio (a later base replaces it only when strictly
+                                 * larger, GROM.c:11150-11156) */
+                                const int a = grom_oracle_snv_pick(k->snv, fasta[p], k->bq_all, k->rc_all, g_min_snv,
+                                                                   g_min_snv_ratio, g_min_ave_bq);
+                                if (a >= 0) {
+                                    const float ratio = (float)k->snv[a] / (float)total;
                                     double binom, hez;
                                     if (total > MAX_TRIALS) {
                                         binom = g_mq_table[MAX_TRIALS][k->snv[a] * MAX_TRIALS / total];
@@ -955,35 +995,23 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                                         binom = g_mq_table[total][k->snv[a]];
                                         hez = g_hez_table[total][k->snv[a]];
                                     }
-                                    if (toupper((unsigned char)fasta[p]) != g_dna[a] && ratio >= g_min_snv_ratio &&
-                                        k->snv[a] >= g_min_snv && (double)k->bq_all / (double)k->rc_all >= g_min_ave_bq) {
-                                        if (sl.n > 0 && sl.pos[sl.n - 1] == p) {
-                                            if (ratio > sl.ratio[sl.n - 1]) {
-                                                sl.ratio[sl.n - 1] = ratio;
-                                                sl.base[sl.n - 1] = a;
-                                                sl.binom[sl.n - 1] = binom;
-                                                sl.hez[sl.n - 1] = hez;
-                                            }
-                                        } else {
-                                            int n = sl.n;
-                                            sl.pos[n] = p;
-                                            for (int bb = 0; bb < 4; bb++) {
-                                                sl.snv[n][bb] = k->snv[bb];
-                                                sl.lowmq[n][bb] = k->snv_lowmq[bb];
-                                                sl.pir[n][bb] = k->pir[bb];
-                                                sl.fs[n][bb] = k->fs[bb];
-                                            }
-                                            sl.ratio[n] = ratio;
-                                            sl.base[n] = a;
-                                            sl.binom[n] = binom;
-                                            sl.hez[n] = hez;
-                                            sl.bq[n] = k->bq; sl.bq_all[n] = k->bq_all;
-                                            sl.mq[n] = k->mq; sl.mq_all[n] = k->mq_all;
-                                            sl.bq_rc[n] = k->bq_rc; sl.mq_rc[n] = k->mq_rc;
-                                            sl.rc_all[n] = k->rc_all;
-                                            sl.n += 1;
-                                        }
+                                    int n = sl.n;
+                                    sl.pos[n] = p;
+                                    for (int bb = 0; bb < 4; bb++) {
+                                        sl.snv[n][bb] = k->snv[bb];
+                                        sl.lowmq[n][bb] = k->snv_lowmq[bb];
+                                        sl.pir[n][bb] = k->pir[bb];
+                                        sl.fs[n][bb] = k->fs[bb];
                                     }
+                                    sl.ratio[n] = ratio;
+                                    sl.base[n] = a;
+                                    sl.binom[n] = binom;
+                                    sl.hez[n] = hez;
+                                    sl.bq[n] = k->bq; sl.bq_all[n] = k->bq_all;
+                                    sl.mq[n] = k->mq; sl.mq_all[n] = k->mq_all;
+                                    sl.bq_rc[n] = k->bq_rc; sl.mq_rc[n] = k->mq_rc;
+                                    sl.rc_all[n] = k->rc_all;
+                                    sl.n += 1;
                                 }
                                 if (sl.n >= g_sv_list_len - 10)
                                     snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx,
@@ -1024,6 +1052,7 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
                             s.w.ind_touched[sl_] = 0;
                             s.w.conc[sl_] = 0;
                             s.w.ins[sl_] = 0;
+                            s.w.rd_add[sl_] = 0;
                         }
                     } else {
                         n_skipped++;
@@ -1074,7 +1103,7 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     snv_list_free(&sl);
     nametab_free(&s.names);
     free(s.w.c); free(s.w.names);
-    free(s.w.ind); free(s.w.ind_touched); free(s.w.conc); free(s.w.ins);
+    free(s.w.ind); free(s.w.ind_touched); free(s.w.conc); free(s.w.ins); free(s.w.rd_add);
     sv_ring_free(&s.ring);
     sv_lists_free(&s.lists);
     free(s.caf_mq); free(s.caf_rd); free(s.caf_low);
@@ -1244,6 +1273,11 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
     }
 
     build_pval2sd(); /* GROM.c:20705-20748 */
+    /* test hook: a smaller sample-list cap makes the reservoir draws of
+     * GROM.c:18292/18393 fire on small inputs (the product reads the same) */
+    if (getenv("GROM_SAMPLE_LISTS_LEN") && atol(getenv("GROM_SAMPLE_LISTS_LEN")) > 0 &&
+        atol(getenv("GROM_SAMPLE_LISTS_LEN")) < g_sample_lists_len)
+        g_sample_lists_len = atol(getenv("GROM_SAMPLE_LISTS_LEN"));
     for (int g = 0; g < G_NUM_GC_BINS; g++) {
         if (!g_sample_hi[g]) g_sample_hi[g] = (int *)malloc(g_sample_lists_len * sizeof(int));
         if (!g_sample_lo[g]) g_sample_lo[g] = (int *)malloc(g_sample_lists_len * sizeof(int));
@@ -1296,7 +1330,7 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
             target_name = st.hdr.ref_name[a];
             if (names_match(lc, l2, g_chr_names[fmatch], g_chr_names_len[fmatch])) { chr_match = a; break; }
         }
-        FILE *dump_cnt = NULL, *dump_ind = NULL;
+        FILE *dump_cnt = NULL, *dump_ind = NULL, *dump_sv = NULL;
         char cname[MAX_CHR_NAME_LEN + 1];
         snprintf(cname, sizeof(cname), "%.*s", g_chr_names_len[fmatch], g_chr_names[fmatch]);
         if (g_dump_prefix) {
@@ -1305,10 +1339,14 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
             dump_cnt = fopen(path, "wb");
             snprintf(path, sizeof(path), "%s.%s.ind", g_dump_prefix, cname);
             dump_ind = fopen(path, "wb");
+            snprintf(path, sizeof(path), "%s.%s.sv", g_dump_prefix, cname);
+            dump_sv = fopen(path, "wb");
         }
-        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, ctx, dump_cnt, dump_ind);
+        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, ctx, dump_cnt, dump_ind,
+                        dump_sv);
         if (dump_cnt) fclose(dump_cnt);
         if (dump_ind) fclose(dump_ind);
+        if (dump_sv) fclose(dump_sv);
     }
     /* BAM target names, lower-cased, for main's CTX post-pass (GROM.c:22408-22430) */
     int n_targets = st.hdr.n_ref;
@@ -1336,6 +1374,29 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
 }
 
 /* test hook: the two binomial tables exactly as a run with -q min_mapq uses them */
+/* The SNV acceptance test of one base (GROM.c:11126-11156): a base other
+ * than the (upper-cased) reference with float ratio >= -a, at least -n reads
+ * and average base quality (all reads) >= -x; of several, the first with the
+ * largest ratio.  Returns the base index (ACGT) or -1. */
+int grom_oracle_snv_pick(const int snv[4], int ref, long bq_all, long rc_all, int min_snv, double min_ratio,
+                         double min_ave_bq) {
+    int total = 0;
+    for (int a = 0; a < 4; a++) total += snv[a];
+    int best = -1;
+    float best_ratio = 0;
+    for (int a = 0; a < 4; a++) {
+        const float ratio = (float)snv[a] / (float)total;
+        if (toupper((unsigned char)ref) != g_dna[a] && ratio >= min_ratio && snv[a] >= min_snv &&
+            (double)bq_all / (double)rc_all >= min_ave_bq) {
+            if (best < 0 || ratio > best_ratio) {
+                best = a;
+                best_ratio = ratio;
+            }
+        }
+    }
+    return best;
+}
+
 void grom_oracle_tables(int min_mapq, double *mq_out, double *hez_out) {
     g_min_mapq = min_mapq;
     calculate_normal_binom_constants();

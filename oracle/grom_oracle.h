@@ -46,19 +46,37 @@ typedef struct orc_indel {
     int32_t pad;
 } orc_indel;
 
+/* Breakpoint cluster state of one evaluated base (rows A8/A9), same layout
+ * as grom_sv_rec (include/grom_amd.h): per cluster type (DEL_F, DEL_R,
+ * DUP_F, DUP_R, INV_F1, INV_R1, INV_F2, INV_R2, CTX_F, CTX_R) the weighted
+ * count, first/last read position and running-mean distance; the CTX mate
+ * chromosomes; the occupied "other" slots; the pair binning's depth adds,
+ * concordant pairs, short-insert pairs and unmapped-mate reads. */
+typedef struct orc_sv_rec {
+    int32_t pos, other_len;
+    int32_t cnt[10], rs[10], re[10];
+    double dist[10];
+    int32_t ctx_mchr[2];
+    int32_t rd_add, conc, ins, mun_f, mun_r, pad;
+} orc_sv_rec;
+
 /* Run the reference CLI semantics: argv as for GROM (-i -r -o ...).
  * If dump_prefix is non-NULL, for every processed chromosome the counters of
  * every evaluated base (p > 2*insert_max, GROM.c:11086) are written to
  * <dump_prefix>.<chrname>.cnt as packed orc_counts records, and the caf read
  * depth arrays to <dump_prefix>.<chrname>.caf (3 x int32 x chr_len), and
  * the indel evidence of every evaluated base that any CIGAR I/D op touched
- * to <dump_prefix>.<chrname>.ind as packed orc_indel records.
+ * to <dump_prefix>.<chrname>.ind as packed orc_indel records, and the
+ * breakpoint state of every evaluated base with any to <dump>.<chr>.sv.
  * Returns the process exit code the reference would return. */
 int grom_oracle_main(int argc, char **argv, const char *dump_prefix);
 
 /* The mq and hez binomial tables (1001 x 1001 doubles each, row-major) as a
  * run with `-q min_mapq` uses them, i.e. after the "%e" text round trip. */
 void grom_oracle_tables(int min_mapq, double *mq_out, double *hez_out);
+/* the SNV acceptance test of one base (GROM.c:11126-11156): the picked alt or -1 */
+int grom_oracle_snv_pick(const int snv[4], int ref, long bq_all, long rc_all, int min_snv, double min_ratio,
+                         double min_ave_bq);
 
 /* test hooks of the CNV path's library restatements (cnv_oracle.c) */
 void grom_oracle_rand_seq(unsigned int seed, int n, int *out);

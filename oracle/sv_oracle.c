@@ -394,7 +394,7 @@ static void sv_aux_cigar(const char *cig, int *sa, int *ea, int *eai) {
 typedef struct {
     sv_ring *ring;
     int idx, p; /* cdp_one_base_index and cdp_pos_in_contig_start at the ingest */
-    int32_t *(*rd)(void *u, long x);   /* window cdp_one_base_rd at absolute x */
+    void (*rd_inc)(void *u, long x);   /* window cdp_one_base_rd at absolute x, += 1 */
     int32_t *(*conc)(void *u, long x); /* cdp_one_base_conc */
     int32_t *(*ins)(void *u, long x);  /* cdp_one_base_ins */
     void (*indel)(void *u, long x, int type, int add, long len); /* CIGAR-style D_F/D_R event */
@@ -414,7 +414,7 @@ static void sv_ev_at(sv_ctx *X, int a, sv_ev *e) { sv_fold(X->ring, a, e); }
  * lpe-1, GROM.c:8690). */
 static void sv_range(sv_ctx *X, const sv_read *r, int lps, int lpe, int t, double v, double tol, int ctx, int half) {
     for (int a = lps; a < lpe; a++) {
-        *X->rd(X->u, AX(a)) += 1;
+        X->rd_inc(X->u, AX(a));
         int full = (half == 1) ? (r->end_adj < X->sc_min || a == lps) : (r->start_adj < X->sc_min || a == lpe - 1);
         sv_ev e = {t, full ? r->add : r->add / 2, full ? (double)r->add : (double)r->add / 2.0, r->add, v, tol,
                    r->pos, RM_SET, ctx, r->mchr, 0};
@@ -485,11 +485,11 @@ static void sv_ingest(sv_ctx *X, const sv_read *r) {
                     X->indel(X->u, AX(lpe - 1), 13 /* OTHER_INDEL_D_R */, r->add, lpe - lps);
                 }
                 const double v = (double)(lpe - lps + X->mean);
-                *X->rd(X->u, AX(lps)) += 1;
+                X->rd_inc(X->u, AX(lps));
                 sv_ev e1 = {CL_DEL_F, r->add, (double)r->add, r->add, v, tol, pos < r->aux_pos ? pos : r->aux_pos,
                             RM_MAX, 0, 0, 0};
                 sv_ev_at(X, lps, &e1);
-                *X->rd(X->u, AX(lpe - 1)) += 1;
+                X->rd_inc(X->u, AX(lpe - 1));
                 sv_ev e2 = {CL_DEL_R, r->add, (double)r->add, r->add, v, tol, pos < r->aux_pos ? r->aux_pos : pos,
                             RM_MINMAX, 0, 0, 0};
                 sv_ev_at(X, lpe - 1, &e2);
@@ -521,11 +521,11 @@ static void sv_ingest(sv_ctx *X, const sv_read *r) {
                         }
                         if (sr_dup == 1) {
                             const double v = (double)(lpe - lps - X->mean);
-                            *X->rd(X->u, AX(lpe)) += 1;
+                            X->rd_inc(X->u, AX(lpe));
                             sv_ev e1 = {CL_DUP_F, r->add, (double)r->add, r->add, v, tol,
                                         pos < r->aux_pos ? r->aux_pos : pos, RM_MINMAX, 0, 0, 1};
                             sv_ev_at(X, lpe, &e1);
-                            *X->rd(X->u, AX(lps - 1)) += 1;
+                            X->rd_inc(X->u, AX(lps - 1));
                             sv_ev e2 = {CL_DUP_R, r->add, (double)r->add, r->add, v, tol,
                                         pos < r->aux_pos ? pos : r->aux_pos, RM_MINMAX, 0, 0, 0};
                             sv_ev_at(X, lps - 1, &e2);
@@ -535,7 +535,7 @@ static void sv_ingest(sv_ctx *X, const sv_read *r) {
                             lps = RI(E);
                             lpe = RI(mpos);
                             if (R < lpe) lpe = R;
-                            for (int a = lps; a < lpe; a++) *X->rd(X->u, AX(a)) += 1;
+                            for (int a = lps; a < lpe; a++) X->rd_inc(X->u, AX(a));
                             for (int a = lps; a < lpe; a++) *X->conc(X->u, AX(a)) += 1;
                         }
                     } else if (tlen > 2 * Mx) {
@@ -551,7 +551,7 @@ static void sv_ingest(sv_ctx *X, const sv_read *r) {
                         lpe = RI(mpos);
                         if (R < lpe) lpe = R;
                         for (int a = lps; a < lpe; a++) {
-                            *X->rd(X->u, AX(a)) += 1;
+                            X->rd_inc(X->u, AX(a));
                             if (AX(a) < pos - sa - eai + Mx - lseq) {
                                 int full = (ea < X->sc_min || a == lps);
                                 sv_ev e = {CL_DEL_F, full ? r->add : r->add / 2,
@@ -579,7 +579,7 @@ static void sv_ingest(sv_ctx *X, const sv_read *r) {
                         if (no_ins == 0) {
                             if (R < lpe) lpe = R;
                             for (int a = lps; a < lpe; a++) {
-                                *X->rd(X->u, AX(a)) += 1;
+                                X->rd_inc(X->u, AX(a));
                                 *X->ins(X->u, AX(a)) += r->add;
                             }
                         }
@@ -621,11 +621,11 @@ static void sv_ingest(sv_ctx *X, const sv_read *r) {
                         }
                         if (sr_dup == 1) {
                             const double v = (double)(lpe - lps - X->mean);
-                            *X->rd(X->u, AX(lpe)) += 1;
+                            X->rd_inc(X->u, AX(lpe));
                             sv_ev e1 = {CL_DUP_F, r->add, (double)r->add, r->add, v, tol,
                                         pos < r->aux_pos ? r->aux_pos : pos, RM_MINMAX, 0, 0, 2};
                             sv_ev_at(X, lpe, &e1);
-                            *X->rd(X->u, AX(lps - 1)) += 1;
+                            X->rd_inc(X->u, AX(lps - 1));
                             sv_ev e2 = {CL_DUP_R, r->add, (double)r->add, r->add, v, tol,
                                         pos < r->aux_pos ? pos : r->aux_pos, RM_MINMAX, 0, 0, 0};
                             sv_ev_at(X, lps - 1, &e2);
@@ -692,7 +692,7 @@ static void sv_ingest(sv_ctx *X, const sv_read *r) {
         }
         X->ring->mset[k][0] = X->ring->mset[k][1] = 1;
         for (int a = lps; a < lpe; a++) {
-            *X->rd(X->u, AX(a)) += 1;
+            X->rd_inc(X->u, AX(a));
             X->ring->mun[k][a] += r->add;
         }
     }

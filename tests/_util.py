@@ -11,6 +11,10 @@ GROM_BIN = os.path.join(REPO, "grom_amd", "bin", "grom")
 SYNTH_BIN = os.path.join(REPO, "grom_amd", "bin", "grom_synth")
 GOLDEN_VCF = os.path.join(REPO, "tests", "golden", "tilapia_v1.0.0.vcf")
 GOLDEN_CTX = os.path.join(REPO, "tests", "golden", "tilapia_v1.0.0.ctx.vcf")
+# the reference's own test FASTA (test_data/oreNil2_GL831235-1.fa, 2.65 Mb,
+# soft-masked, N runs), copied as a data fixture: SURVEY 8(d)'s C1s stand-in
+# for the bundled tilapia BAM (a missing blob) simulates reads from it
+TILAPIA_FA = os.path.join(REPO, "tests", "fixtures", "oreNil2_GL831235-1.fa")
 NCOUNT = 40
 FILEDATE = "20260101"
 SEED = "7"  # GROM_SEED: pins the CNV sampling generator (srand(time()) at GROM.c:1584)
@@ -43,6 +47,16 @@ CASES = {
     # breakpoint evidence: deletions, duplications, inversions, insertions and
     # translocations with split reads (SA tags), a 300 kb partner chromosome
     "sv": ["-L", "600000,300000", "-s", "31", "-X", "30", "-I", "0.0003", "-J", "0.3", "-Q", "0.05"],
+    # dense breakpoint SVs: >= 50 rows of every <DEL>/<DUP>/<INV>/<INS> class and
+    # translocation (BND) pairs in .ctx.vcf
+    "sv_many": ["-L", "3000000,1500000", "-s", "33", "-X", "80", "-I", "0.0003", "-J", "0.3", "-Q", "0.05"],
+    # reads simulated from the reference's tilapia FASTA at
+    # 5x, 2x100 bp, seed 1 (the bundled test's contig, names and case kept)
+    "c1s": ["-F", TILAPIA_FA, "-c", "5", "-l", "100", "-s", "1"],
+    # a 30 Mb contig whose every window has one GC content: one GC bin gets
+    # more than g_sample_lists_len (100,000) depth samples, so the reservoir
+    # draws of GROM.c:18385-18451 run at the reference's own cap
+    "cnv_reservoir": ["-L", "30000000", "-R", "50", "-s", "41", "-V", "0.0000002", "-W", "50000,300000", "-Q", "0.05"],
 }
 
 

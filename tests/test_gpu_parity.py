@@ -10,6 +10,7 @@ import os
 import numpy as np
 import pytest
 
+import grom_amd
 from _util import CASES, load_counts, load_indels, run_grom, run_oracle, synth
 
 pytestmark = pytest.mark.gpu
@@ -41,6 +42,10 @@ RUNS = [
     ("c5_tetra_male", ["-p", "4", "-g", "1", "-M", "-V", "1"]),
     ("c3_genome", ["-M"]),
     ("c3_genome", ["-M", "-V", "1"]),
+    # dense breakpoint SVs (>= 50 rows of each class) and SURVEY 8(d)'s C1s
+    ("sv_many", []),
+    ("c1s", []),
+    ("c1s", ["-V", "1", "-n", "2"]),
 ]
 
 # read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call
@@ -63,11 +68,28 @@ def _names(datadir, tag):
 
 
 
+def _check_sv_records(datadir, o_dump, g_dump, ch):
+    """Per-base breakpoint cluster state (rows A8/A9: every evaluated base with
+    a DEL/DUP/INV/CTX cluster count or an occupied "other" slot -- counts,
+    running-mean distances bit for bit, first/last read positions, CTX mate
+    chromosomes, the pair binning's depth adds, concordant, short-insert and
+    unmapped-mate sums) against the oracle's ring at the same base."""
+    o = np.fromfile(datadir / f"{o_dump}.{ch}.sv", dtype=grom_amd.SV_DTYPE)
+    g = np.fromfile(datadir / f"{g_dump}.{ch}.sv", dtype=grom_amd.SV_DTYPE)
+    assert o.shape == g.shape, (ch, o.shape, g.shape, o["pos"][:5], g["pos"][:5])
+    if o.tobytes() != g.tobytes():
+        ob, gb = o.view(np.uint8).reshape(len(o), -1), g.view(np.uint8).reshape(len(g), -1)
+        i = int(np.nonzero((ob != gb).any(axis=1))[0][0])
+        raise AssertionError((ch, "first differing breakpoint record", o[i], g[i]))
+    return len(o)
+
+
 def _check_counters(datadir, case, extra, tag, env_extra=None):
     bam, fa = synth(datadir, case, CASES[case])
     o_dump, g_dump = f"o_{tag}", f"g_{tag}"
     run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra, dump=str(datadir / o_dump))
-    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, dump=str(datadir / g_dump), env_extra=env_extra)
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, dump=str(datadir / g_dump),
+             env_extra=dict(env_extra or {}, GROM_SV_DEBUG="1"))
     chroms = _names(datadir, o_dump)
     assert chroms
     for ch in chroms:
@@ -89,17 +111,30 @@ def _check_counters(datadir, case, extra, tag, env_extra=None):
         assert bad.size == 0, (ch, "first differing indel record", oi[bad[0]], gi[bad[0]])
         if case == "indels":
             assert (oi["other_len"] > 0).sum() > 10 and (oi["ins"] > 0).sum() > 10
+        n_sv = _check_sv_records(datadir, o_dump, g_dump, ch)
+        if case in ("sv", "sv_many", "c3_genome"):
+            assert n_sv > 1000, (ch, n_sv)
     ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"g_{tag}.vcf").read()
     assert ov.count("\n") > 46
     assert ov == gv
     assert filecmp.cmp(datadir / f"o_{tag}.ctx.vcf", datadir / f"g_{tag}.ctx.vcf", shallow=False)
-    if case == "sv":
+    if case in ("sv", "sv_many"):
         # the comparison covered every breakpoint row class
-        alts = {l.split("\t")[4] for l in gv.splitlines() if not l.startswith("#")}
-        assert {"<DEL>", "<DUP>", "<INV>"} <= alts, alts
+        alts = [l.split("\t")[4] for l in gv.splitlines() if not l.startswith("#")]
+        assert {"<DEL>", "<DUP>", "<INV>"} <= set(alts), set(alts)
+        if case == "sv_many":
+            for cls in ("<DEL>", "<DUP>", "<INV>", "<INS>"):
+                assert alts.count(cls) >= 50, (cls, alts.count(cls))
         assert any(l.startswith("SPR:SEV:SRD:SCO:ECO") or "SPR:SEV:SRD:SCO:ECO" in l for l in gv.splitlines())
         bnd = [l for l in open(datadir / f"g_{tag}.ctx.vcf") if not l.startswith("#")]
         assert bnd and all("SVTYPE=BND" in l for l in bnd)
+        if case == "sv_many":
+            assert len(bnd) >= 50, len(bnd)
+    if case == "c1s":
+        # the tilapia contig, its soft-masked (lower-case) REF bases printed as loaded
+        rows = [l for l in gv.splitlines() if not l.startswith("#")]
+        assert rows and all(l.startswith("gl831235-1\t") for l in rows)
+        assert any(l.split("\t")[3].islower() for l in rows)
 
 
 @pytest.mark.parametrize("case,extra", RUNS, ids=[f"{c}{''.join(e)}" for c, e in RUNS])
@@ -156,6 +191,73 @@ def test_cnv_serial_stdev_path(datadir, case, extra):
     ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"g_{tag}.vcf").read()
     assert ov.count("<DEL>") + ov.count("<DUP>") > 0
     assert ov == gv
+
+
+def _stats(path):
+    out = {}
+    if os.path.exists(path):
+        for line in open(path):
+            name, over, repl = line.split()
+            out[name] = (int(over.split("=")[1]), int(repl.split("=")[1]))
+    return out
+
+
+@pytest.mark.parametrize("case,extra,cap", [("cnv", ["-V", "1"], "100"), ("cnv_multi", ["-V", "1", "-p", "3"], "150"),
+                                            ("c3_genome", ["-M", "-V", "1"], "60")],
+                         ids=["cnv_cap100", "cnv_multi_cap150", "c3_genome_cap60"])
+def test_cnv_reservoir_draws_forced(datadir, case, extra, cap):
+    """once a GC bin holds g_sample_lists_len depth samples, each
+    new one draws grom_rand (glibc random()) to replace a kept sample
+    (GROM.c:18385-18451).  GROM_SAMPLE_LISTS_LEN lowers the cap in the oracle
+    and in the product alike, so the draws run thousands of times on a small
+    input: the number of draws past the cap and of replacements, and the rows,
+    must be the oracle's."""
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"res{cap}_{case}"
+    env = {"GROM_SAMPLE_LISTS_LEN": cap}
+    so, sg = str(datadir / f"o_{tag}.stats"), str(datadir / f"g_{tag}.stats")
+    run_oracle_env = dict(env, GROM_CNV_STATS=so)
+    from _util import run, ORACLE_BIN
+    run(ORACLE_BIN, ["-i", bam, "-r", fa, "-o", f"o_{tag}.vcf"] + extra, str(datadir), run_oracle_env)
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, env_extra=dict(env, GROM_CNV_STATS=sg))
+    o, g = _stats(so), _stats(sg)
+    assert o == g, (o, g)
+    assert sum(v[0] for v in o.values()) > 1000 and sum(v[1] for v in o.values()) > 0, o
+    assert open(datadir / f"o_{tag}.vcf").read() == open(datadir / f"g_{tag}.vcf").read()
+
+
+def test_cnv_reservoir_draws_at_the_reference_cap(datadir):
+    """The same draws at the reference's own cap of 100,000 samples: a 30 Mb
+    contig whose windows all have one GC content (grom_synth -R) puts every
+    depth sample in one bin, as the longest configs[2] chromosomes do with
+    their dominant bins.  Draw counts and rows equal the oracle's."""
+    case = "cnv_reservoir"
+    bam, fa = synth(datadir, case, CASES[case])
+    so, sg = str(datadir / "o_resfull.stats"), str(datadir / "g_resfull.stats")
+    from _util import run, ORACLE_BIN
+    run(ORACLE_BIN, ["-i", bam, "-r", fa, "-o", "o_resfull.vcf", "-V", "1"], str(datadir), {"GROM_CNV_STATS": so})
+    run_grom(datadir, bam, fa, "g_resfull.vcf", ["-V", "1"], env_extra={"GROM_CNV_STATS": sg})
+    o, g = _stats(so), _stats(sg)
+    assert o == g, (o, g)
+    assert o["chr1"][0] > 10000, o
+    ov, gv = open(datadir / "o_resfull.vcf").read(), open(datadir / "g_resfull.vcf").read()
+    assert ov.count("<DEL>") + ov.count("<DUP>") > 0
+    assert ov == gv
+
+
+@pytest.mark.parametrize("case,extra", [("three_chr", []), ("sv", ["-S"]), ("c3_genome", ["-M", "-V", "1"]),
+                                        ("empty_middle", [])],
+                         ids=["three_chr", "sv_S", "c3_genome_M_V1", "empty_middle"])
+def test_serial_reader_path(datadir, case, extra):
+    """The serial reader (GROM_SERIAL_DECODE=1: one pass over the record
+    stream, host batches uploaded per chromosome) -- the CLI's fallback when an
+    index lacks what the streamed decoder needs -- gives the oracle's VCF."""
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"ser_{case}{''.join(extra).replace('-', '_')}"
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, env_extra={"GROM_SERIAL_DECODE": "1"})
+    for ext in (".vcf", ".ctx.vcf"):
+        assert open(datadir / f"o_{tag}{ext}").read() == open(datadir / f"g_{tag}{ext}").read(), ext
 
 
 def test_device_resident_path_matches_host_path():

@@ -101,3 +101,40 @@ def test_oracle_snv_row_layout_matches_golden(datadir):
         assert pat.match(r), r
     for f in golden_snv_rows()[:2000]:
         assert pat.match("\t".join(f)), f
+
+
+def test_oracle_snv_acceptance_on_every_golden_row():
+    """The oracle's SNV acceptance test (grom_oracle_snv_pick, the function its
+    walk calls; GROM.c:11126-11156) accepts every one of the 18,099 golden SNV
+    rows with the defaults (-n 3, -a 0.2, -x 15) and picks the printed ALT from
+    the printed A:C:G:T counts.  BQ is printed as %.2f of bq_all/rc_all, so the
+    test feeds bq_all = 100*BQ over rc_all = 100; a row printed at exactly the
+    -x bound would be ambiguous (none is)."""
+    lib = ctypes.CDLL(ORACLE_LIB)
+    fn = lib.grom_oracle_snv_pick
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_long, ctypes.c_long, ctypes.c_int,
+                   ctypes.c_double, ctypes.c_double]
+    bad, ambiguous, multi = [], 0, 0
+    for f in golden_snv_rows():
+        v = f[9].split(":")
+        cnt = (ctypes.c_int * 4)(*map(int, v[3:7]))
+        bq = float(v[11])
+        if abs(bq - 15.0) < 0.006:
+            ambiguous += 1
+            continue
+        alts = [a for a in range(4) if "ACGT"[a] != f[3].upper() and cnt[a] >= 3]
+        multi += len(alts) > 1
+        got = fn(cnt, ord(f[3]), int(round(bq * 100)), 100, 3, 0.2, 15.0)
+        if got < 0 or "ACGT"[got] != f[4]:
+            bad.append((f[1], f[3], f[4], list(cnt), bq, got))
+    assert ambiguous == 0
+    assert not bad, bad[:10]
+    # and the predicate rejects what it must: a reference-base "alt", too few
+    # reads, too low a ratio, too low an average base quality
+    c = (ctypes.c_int * 4)(0, 0, 10, 0)
+    assert fn(c, ord("g"), 3000, 100, 3, 0.2, 15.0) == -1
+    assert fn((ctypes.c_int * 4)(20, 0, 2, 0), ord("A"), 3000, 100, 3, 0.05, 15.0) == -1
+    assert fn((ctypes.c_int * 4)(90, 0, 10, 0), ord("A"), 3000, 100, 3, 0.2, 15.0) == -1
+    assert fn((ctypes.c_int * 4)(0, 0, 10, 0), ord("A"), 1400, 100, 3, 0.2, 15.0) == -1
+    assert fn((ctypes.c_int * 4)(0, 5, 5, 0), ord("A"), 3000, 100, 3, 0.2, 15.0) == 1  # tie: the first

@@ -5,7 +5,7 @@
  *   grom_synth -o prefix [-L len[,len...]] [-c cov] [-l readlen] [-m mean] [-d sd]
  *              [-s seed] [-e err] [-Q lowmapq_frac] [-C clip_frac] [-U munmap_frac]
  *              [-D dup_frac] [-S snv_rate] [-I indel_rate] [-T telomere_n] [-n names]
- *              [-X sv_per_mb] [-E sv_evidence] [-P ploidy]
+ *              [-X sv_per_mb] [-E sv_evidence] [-P ploidy] [-R ref_period] [-F ref.fa]
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -18,9 +18,9 @@ int main(int argc, char **argv) {
     synth_cfg c;
     synth_default_cfg(&c);
     const char *prefix = NULL;
-    const char *names = NULL;
+    const char *names = NULL, *ref_fasta = NULL;
     int opt;
-    while ((opt = getopt(argc, argv, "o:L:c:l:m:d:s:e:Q:C:U:D:S:I:T:n:q:M:V:W:J:X:E:P:")) != -1) {
+    while ((opt = getopt(argc, argv, "o:L:c:l:m:d:s:e:Q:C:U:D:S:I:T:n:q:M:V:W:J:X:E:P:R:F:")) != -1) {
         switch (opt) {
         case 'o': prefix = optarg; break;
         case 'L': {
@@ -55,7 +55,9 @@ int main(int argc, char **argv) {
         case 'n': names = optarg; break;
         case 'q': c.lowq_frac = atof(optarg); break;
         case 'M': c.lower_frac = atof(optarg); break;
-        case 'P': c.ploidy = atoi(optarg); break;                   /* donor haplotypes (allele fractions k/P) */
+        case 'P': c.ploidy = atoi(optarg); break;
+        case 'R': c.ref_period = atoi(optarg); break;               /* periodic reference (one GC bin) */
+        case 'F': ref_fasta = optarg; break;                        /* reads from an existing FASTA */                   /* donor haplotypes (allele fractions k/P) */
         case 'J': c.multi_indel = atof(optarg); break;              /* multi-allelic indel fraction */
         case 'X': c.sv_per_mb = atof(optarg); break;                /* breakpoint SVs per Mb */
         case 'E': c.sv_evidence = atof(optarg); break;              /* SV evidence depth factor */
@@ -68,6 +70,10 @@ int main(int argc, char **argv) {
     }
     if (!prefix) { fprintf(stderr, "grom_synth: -o prefix required\n"); return 2; }
     for (int i = 0; i < c.n_chr; i++) snprintf(c.chr_name[i], sizeof(c.chr_name[i]), "chr%d", i + 1);
+    if (ref_fasta && synth_cfg_from_fasta(&c, ref_fasta) != 0) {
+        fprintf(stderr, "grom_synth: cannot read %s\n", ref_fasta);
+        return 1;
+    }
     if (names) {
         char *s = strdup(names), *tok = strtok(s, ",");
         for (int i = 0; tok && i < c.n_chr; i++) {
