@@ -136,6 +136,8 @@ _SIGS = {
     "grom_batch_get": (C.c_int, [C.c_void_p, C.POINTER(Chrom), C.POINTER(Reads)]),
     "grom_batch_release": (None, [C.c_void_p]),
     "grom_cli_main": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
+    "grom_ctx_postpass": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_char_p), C.c_int32, C.c_int32, C.c_int32,
+                                    C.POINTER(Out)]),
     # streamed input (ABI 5)
     "grom_pinned_alloc": (C.c_void_p, [C.c_size_t]),
     "grom_pinned_free": (None, [C.c_void_p]),
@@ -232,6 +234,17 @@ class Device:
         lib().grom_out_free(C.byref(out))
         return text, st
 
+    def scan_rows(self, chrom: Chrom, reads: Reads, device_resident: bool = False):
+        """Scan one chromosome; returns (VCF text, raw CTX rows, Stats).  The raw
+        CTX rows of every chromosome feed ctx_postpass."""
+        out, st = Out(), Stats()
+        fn = lib().grom_scan_chrom_device if device_resident else lib().grom_scan_chrom
+        check(fn(self.device, C.byref(chrom), C.byref(reads), C.byref(out), C.byref(st)), "scan")
+        vcf = C.string_at(out.vcf, out.vcf_len).decode() if out.vcf_len else ""
+        ctx = C.string_at(out.ctx, out.ctx_len).decode() if out.ctx_len else ""
+        lib().grom_out_free(C.byref(out))
+        return vcf, ctx, st
+
     def upload(self, chrom: Chrom, reads: Reads):
         dc, dr = Chrom(), Reads()
         check(lib().grom_upload(self.device, C.byref(chrom), C.byref(reads), C.byref(dc), C.byref(dr)), "upload")
@@ -310,6 +323,19 @@ class SynthBatch:
     @property
     def n_bases(self) -> int:
         return self.reads.n_bases
+
+
+def ctx_postpass(raw: str, target_names, insert_max: int, lseq: int) -> str:
+    """main's translocation post-pass (grom_ctx_postpass) over the raw CTX rows
+    of every chromosome in chromosome order: the BND rows of .ctx.vcf."""
+    names = (C.c_char_p * max(len(target_names), 1))(*[n.encode() for n in target_names])
+    out = Out()
+    data = raw.encode()
+    check(lib().grom_ctx_postpass(data, len(data), names, len(target_names), insert_max, lseq, C.byref(out)),
+          "grom_ctx_postpass")
+    text = C.string_at(out.ctx, out.ctx_len).decode() if out.ctx_len else ""
+    lib().grom_out_free(C.byref(out))
+    return text
 
 
 def cli_main(args, env=None, cwd=None) -> int:

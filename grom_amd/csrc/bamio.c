@@ -130,24 +130,40 @@ static void *bgzf_worker(void *arg) {
     return NULL;
 }
 
+static void bgzf_mt_free(struct bgzf_mt *m);
+
 int bgzf_set_threads(bgzf_reader *r, int n) {
     if (n <= 1 || r->mt) return 0;
     struct bgzf_mt *m = (struct bgzf_mt *)calloc(1, sizeof(*m));
     if (!m) return -1;
-    m->n_thr = n;
+    m->n_thr = 0; /* threads actually started (the only ones joined) */
     m->n_slot = 4 * n;
     m->slot = (bgzf_slot *)calloc(m->n_slot, sizeof(bgzf_slot));
     m->thr = (pthread_t *)calloc(n, sizeof(pthread_t));
-    if (!m->slot || !m->thr) { free(m->slot); free(m->thr); free(m); return -1; }
-    for (int k = 0; k < m->n_slot; k++) {
+    int ok = m->slot && m->thr;
+    for (int k = 0; ok && k < m->n_slot; k++) {
         m->slot[k].cbuf = (unsigned char *)malloc(BGZF_MAX_BLOCK);
         m->slot[k].blk = (unsigned char *)malloc(BGZF_MAX_BLOCK);
-        if (!m->slot[k].cbuf || !m->slot[k].blk) return -1;
+        if (!m->slot[k].cbuf || !m->slot[k].blk) ok = 0;
+    }
+    if (!ok) {
+        for (int k = 0; m->slot && k < m->n_slot; k++) { free(m->slot[k].cbuf); free(m->slot[k].blk); }
+        free(m->slot);
+        free(m->thr);
+        free(m);
+        return -1;
     }
     pthread_mutex_init(&m->mu, NULL);
     pthread_cond_init(&m->work, NULL);
     pthread_cond_init(&m->done, NULL);
-    for (int t = 0; t < n; t++) pthread_create(&m->thr[t], NULL, bgzf_worker, m);
+    for (int t = 0; t < n; t++) {
+        if (pthread_create(&m->thr[t], NULL, bgzf_worker, m) != 0) break;
+        m->n_thr++;
+    }
+    if (m->n_thr == 0) { /* no worker: the serial reader */
+        bgzf_mt_free(m);
+        return 0;
+    }
     r->mt = m;
     return 0;
 }
@@ -856,33 +872,30 @@ int bai_query(const bai_index *idx, int tid, int beg, int end, bai_chunk **out) 
     if (tid < 0 || tid >= idx->n_ref || end <= beg) return 0;
     if (beg < 0) beg = 0;
     const bai_ref *R = &idx->ref[tid];
-    /* reg2bins (SAM v1 section 5.3): the bins of every level overlapping [beg, end) */
-    uint32_t want[4682 + 8];
-    int nw = 0;
+    /* reg2bins (SAM v1 section 5.3): a bin of level l (first bin number
+     * off[l], 2^shift[l] bases each) overlaps [beg, end) iff its index lies
+     * between beg >> shift and (end - 1) >> shift -- tested per bin, so no
+     * span is too long */
+    static const uint32_t lv_off[6] = {0, 1, 9, 73, 585, 4681};
+    static const int lv_shift[6] = {29, 26, 23, 20, 17, 14};
     const int e = end - 1;
-    want[nw++] = 0;
-    for (int k = 1 + (beg >> 26); k <= 1 + (e >> 26); k++) want[nw++] = (uint32_t)k;
-    for (int k = 9 + (beg >> 23); k <= 9 + (e >> 23); k++) want[nw++] = (uint32_t)k;
-    for (int k = 73 + (beg >> 20); k <= 73 + (e >> 20); k++) want[nw++] = (uint32_t)k;
-    for (int k = 585 + (beg >> 17); k <= 585 + (e >> 17); k++) want[nw++] = (uint32_t)k;
-    for (int k = 4681 + (beg >> 14); k <= 4681 + (e >> 14) && nw < (int)(sizeof(want) / sizeof(want[0])); k++)
-        want[nw++] = (uint32_t)k;
     const uint64_t min_off = R->n_intv > 0 ? R->ioff[(beg >> 14) < R->n_intv ? (beg >> 14) : R->n_intv - 1] : 0;
     int n = 0, cap = 16;
     bai_chunk *c = (bai_chunk *)malloc(sizeof(bai_chunk) * cap);
     for (int i = 0; i < R->n_bin; i++) {
         const uint32_t bn = R->bin[i].bin;
-        if (bn == 37450u) continue;
-        int hit = 0;
-        for (int w = 0; w < nw && !hit; w++) hit = want[w] == bn;
-        if (!hit) continue;
-        for (int k = 0; k < R->bin[i].n_chunk; k++) {
-            if (R->bin[i].chunk[k].end <= min_off) continue;
+        if (bn >= 37450u) continue;
+        int l = 5;
+        while (l > 0 && bn < lv_off[l]) l--;
+        const uint32_t k = bn - lv_off[l];
+        if (!(k >= (uint32_t)(beg >> lv_shift[l]) && k <= (uint32_t)(e >> lv_shift[l]))) continue;
+        for (int q = 0; q < R->bin[i].n_chunk; q++) {
+            if (R->bin[i].chunk[q].end <= min_off) continue;
             if (n == cap) {
                 cap *= 2;
                 c = (bai_chunk *)realloc(c, sizeof(bai_chunk) * cap);
             }
-            c[n++] = R->bin[i].chunk[k];
+            c[n++] = R->bin[i].chunk[q];
         }
     }
     qsort(c, n, sizeof(bai_chunk), cmp_chunk);

@@ -61,14 +61,10 @@ constexpr int REP_SEGS = 10;               // g_repeat_segments, GROM.c:732
 // the reservoir draws of GROM.c:18292/18393 then fire on small inputs, and
 // the oracle reads the same variable)
 static long sample_len() {
-    static const long v = [] {
-        const char *e = getenv("GROM_SAMPLE_LISTS_LEN");
-        const long x = e ? atol(e) : 0;
-        return (x > 0 && x < 100000) ? x : 100000L;
-    }();
-    return v;
+    const char *e = getenv("GROM_SAMPLE_LISTS_LEN");
+    const long x = e ? atol(e) : 0;
+    return (x > 0 && x < 100000) ? x : 100000L;
 }
-#define SAMPLE_LEN sample_len()
 constexpr long REDUCTION = 1;              // g_genome_reduction_factor, GROM.c:726
 constexpr long BLOCK_FACTOR = 4;           // g_block_factor, GROM.c:738
 constexpr long BLOCK_UNIT = 10000;         // g_block_unit_size, GROM.c:740
@@ -2548,6 +2544,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     mark("pre+stats");
     // ---- A16: GC-bin samples every insert_mean/2 bases, GROM.c:18373-18456 ----
     const long half = m / 2;
+    const long SAMPLE_LEN = sample_len();  // read per chromosome
     Tables T{};
     std::vector<std::vector<int>> smp[2];
     smp[0].assign(NBINS, {});

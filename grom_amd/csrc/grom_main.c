@@ -266,6 +266,37 @@ static void ctx_postpass(const char *raw, size_t raw_len, const bam_hdr *hdr, in
     free(rw);
 }
 
+int grom_ctx_postpass(const char *raw, size_t raw_len, const char *const *target_names, int32_t n_targets,
+                      int32_t insert_max, int32_t lseq, grom_out *out) {
+    if (!out || n_targets < 0 || (n_targets > 0 && !target_names)) {
+        grom_set_last_error("grom_ctx_postpass: bad argument");
+        return GROM_E_ARG;
+    }
+    bam_hdr h;
+    memset(&h, 0, sizeof(h));
+    h.n_ref = n_targets;
+    h.ref_name = (char **)target_names;
+    char *buf = NULL;
+    size_t len = 0;
+    FILE *f = open_memstream(&buf, &len);
+    if (!f) { grom_set_last_error("grom_ctx_postpass: no memory"); return GROM_E_NOMEM; }
+    ctx_postpass(raw, raw_len, &h, insert_max, lseq, f);
+    fclose(f);
+    if (out->ctx_len + len + 1 > out->ctx_cap) {
+        size_t nc = out->ctx_cap ? out->ctx_cap : 4096;
+        while (nc < out->ctx_len + len + 1) nc *= 2;
+        char *p = realloc(out->ctx, nc);
+        if (!p) { free(buf); grom_set_last_error("grom_ctx_postpass: no memory"); return GROM_E_NOMEM; }
+        out->ctx = p;
+        out->ctx_cap = nc;
+    }
+    memcpy(out->ctx + out->ctx_len, buf, len);
+    out->ctx_len += len;
+    out->ctx[out->ctx_len] = 0;
+    free(buf);
+    return GROM_OK;
+}
+
 /* ---- one chromosome's scan, from either input path ----
  * serial path: `batch` holds the chromosome's records in host memory;
  * streamed path: `stage` holds them in HBM (pdecode.c) and `facts` the

@@ -3,6 +3,7 @@
  * chromosome turned straight into the read batch its scan ingests, without a
  * BAM round trip (the SoA the BAM decoder would have produced).
  */
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -306,15 +307,19 @@ int64_t grom_bai_selftest(const char *bam_path, int64_t n_queries, uint64_t seed
         s ^= s << 13; s ^= s >> 7; s ^= s << 17;
         const int32_t beg = (int32_t)(s % (uint64_t)L);
         s ^= s << 13; s ^= s >> 7; s ^= s << 17;
-        const int32_t span = (q % 4 == 0) ? 1 : (int32_t)(1 + s % (q % 4 == 1 ? 200u : q % 4 == 2 ? 40000u : 3000000u));
-        const int32_t end = beg + span;
+        /* point, short, medium and long regions; every fifth query a whole
+         * chromosome or more (100 Mb: more bins than any fixed list holds) */
+        const int32_t span = (q % 5 == 4) ? (q % 2 ? L : 100000000)
+                             : (q % 4 == 0) ? 1 : (int32_t)(1 + s % (q % 4 == 1 ? 200u : q % 4 == 2 ? 40000u : 3000000u));
+        const int32_t b0 = (q % 5 == 4) ? 0 : beg;
+        const int32_t end = (int32_t)((int64_t)b0 + span > INT32_MAX ? INT32_MAX : b0 + span);
         fetch_acc want = {0, 0}, got = {0, 0};
         for (int64_t i = 0; i < n; i++)
-            if (tp[3 * i] == tid && tp[3 * i + 1] < end && tp[3 * i + 2] > beg) {
+            if (tp[3 * i] == tid && tp[3 * i + 1] < end && tp[3 * i + 2] > b0) {
                 want.hash += hs[i];
                 want.n++;
             }
-        if (bam_fetch(&r, &idx, tid, beg, end, fetch_visit, &got) < 0) { bad = GROM_E_ARG; break; }
+        if (bam_fetch(&r, &idx, tid, b0, end, fetch_visit, &got) < 0) { bad = GROM_E_ARG; break; }
         seen += got.n;
         if (got.n != want.n || got.hash != want.hash) bad++;
     }

@@ -418,7 +418,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             return rc;
         }
     }
-    for (int attempt = 0; attempt < 2; attempt++) {
+    for (int attempt = 0; attempt < 4; attempt++) {
         if ((rc = ensure(C.cands, sizeof(grom_snv_cand) * (size_t)cand_cap)) ||
             (rc = ensure(C.cands2, sizeof(grom_snv_cand) * (size_t)cand_cap)))
             return rc;
@@ -490,9 +490,15 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         HIPCHK(hipMemcpyAsync(hdr, misc + 4, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         const double t_kernels = ms_since(t_start);
-        if (hdr[0] > cand_cap) {
-            cand_cap = hdr[0] + hdr[0] / 4 + 1024;
-            continue;
+        {
+            // the breakpoint context records (every clipped or marked base) have
+            // a guessed buffer: a pass that wanted more runs again with room
+            uint32_t used = 0;
+            if ((rc = sv_ctx_used(C.sv, st, &used))) { set_err("reading the context record count failed"); return rc; }
+            const bool ctx_over = used > sv_ctx_cap(C.sv), cand_over = hdr[0] > cand_cap;
+            if (ctx_over) sv_ctx_reserve(C.sv, used + used / 4 + 65536);
+            if (cand_over) cand_cap = hdr[0] + hdr[0] / 4 + 1024;
+            if (ctx_over || cand_over) continue;
         }
         uint32_t ncand = hdr[0];
         if (ncand > C.h_cap) {

@@ -82,6 +82,10 @@ const int32_t *sv_rd_add(const SvScratch *S);
 // the buffer the pileup fills with grom_sv_ctx records (grown by sv_prepare)
 grom_sv_ctx *sv_ctx_buf(const SvScratch *S);
 uint32_t sv_ctx_cap(const SvScratch *S);
+// the pileup's context records written (or wanted) in the last pass; a pass
+// that wanted more than sv_ctx_cap is run again after sv_ctx_reserve
+int sv_ctx_used(SvScratch *S, hipStream_t st, uint32_t *used);
+void sv_ctx_reserve(SvScratch *S, uint32_t cap);
 uint32_t *sv_ctx_count(const SvScratch *S);
 
 // Phase 2, after the pileup: the per-base tests at every context record;

@@ -933,6 +933,7 @@ struct SvScratch {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int64_t len = 0;
     uint32_t n_rec = 0, n_irec = 0, n_drec = 0, ctx_cap = 0;
+    uint32_t ctx_min = 0;  // a retry's capacity for the pileup's context records
 };
 
 static int sbuf(Buf &b, size_t bytes, char *err, size_t errlen) {
@@ -970,6 +971,17 @@ const uint32_t *sv_bits(const SvScratch *S) { return (const uint32_t *)S->bits.p
 const int32_t *sv_rd_add(const SvScratch *S) { return (const int32_t *)S->sums.p; }
 grom_sv_ctx *sv_ctx_buf(const SvScratch *S) { return (grom_sv_ctx *)S->ctx.p; }
 uint32_t sv_ctx_cap(const SvScratch *S) { return S->ctx_cap; }
+int sv_ctx_used(SvScratch *S, hipStream_t st, uint32_t *used) {
+    *used = 0;
+    if (!S || !S->n_ctx.p) return GROM_OK;
+    if (hipMemcpyAsync(used, S->n_ctx.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return GROM_E_HIP;
+    return GROM_OK;
+}
+void sv_ctx_reserve(SvScratch *S, uint32_t cap) {
+    if (S) S->ctx_min = std::max(S->ctx_min, cap);
+}
 uint32_t *sv_ctx_count(const SvScratch *S) { return (uint32_t *)S->n_ctx.p; }
 const grom_indel_rec *sv_indel_records(const SvScratch *S) { return (const grom_indel_rec *)S->irec.p; }
 int64_t sv_indel_count(const SvScratch *S) { return S->n_irec; }
@@ -1042,6 +1054,10 @@ int sv_prepare(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput
     SCHK(hipMemsetAsync(S->n_ctx.p, 0, 16, st));
     // room for the pileup's context records: every clipped base and every marked one
     S->ctx_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, len / 64 + 2 * n / 16), (int64_t)1 << 28);
+    if (const char *e = getenv("GROM_SV_CTX_CAP")) {  // test hook: a small first guess forces the retry
+        if (atol(e) > 0) S->ctx_cap = (uint32_t)atol(e);
+    }
+    if (S->ctx_min > S->ctx_cap) S->ctx_cap = S->ctx_min;
     if ((rc = sbuf(S->ctx, sizeof(grom_sv_ctx) * S->ctx_cap, err, errlen))) return rc;
     if (eval_hi < eval_lo || n <= 0) return GROM_OK;
 

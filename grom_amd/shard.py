@@ -1,10 +1,14 @@
 """Chromosome sharding and multi-rank timing (one process per GPU).
 
-The scan has no cross-chromosome state (every array of
-count_discordant_pairs is local to one call, GROM.c:1432), so ranks split the
-chromosomes and never exchange data on the scan path.  torch.distributed (RCCL
-on the GPU box, gloo in the CPU tests) carries only the barrier around the
-timed region and the max-over-ranks of its duration.
+The per-chromosome scan has no cross-chromosome state (every
+array of count_discordant_pairs is local to one call, GROM.c:1432), so ranks
+split the chromosomes and never exchange data on the scan path.  The one
+genome-wide step after the scans is main's translocation post-pass
+(GROM.c:22400-22770), which pairs CTX rows across chromosomes: ranks hand
+their raw CTX rows to rank 0 with the VCF text and rank 0 runs it
+(grom_amd.ctx_postpass).  torch.distributed (RCCL on the GPU box, gloo in the
+CPU tests) carries that gather, the barrier around the timed region and the
+max-over-ranks of its duration.
 """
 import time
 from typing import Callable, List, Sequence
@@ -101,15 +105,19 @@ def run_queue(workers: "list[Callable[[int], None]]", items: Sequence[int]) -> N
         raise errs[0]
 
 
-def sharded_genome_text(scan_chrom: "Callable[[int], str]", lengths: Sequence[int], world: int, rank: int,
-                        gather: "Callable[[dict], list] | None" = None) -> "str | None":
+def sharded_genome_text(scan_chrom: "Callable[[int], object]", lengths: Sequence[int], world: int, rank: int,
+                        gather: "Callable[[dict], list] | None" = None, ctx_post: "Callable[[str], str] | None" = None):
     """The genome's output text with its chromosomes scanned across ranks:
     rank r scans its longest-processing-time share (assign_chromosomes), the
     per-chromosome texts are gathered on rank 0 (the only exchange, off the
     scan path) and joined in chromosome order -- the order a one-rank run, and
     GROM's serial loop over the FASTA, writes them.  Returns the text on rank
     0, None elsewhere.  `gather(obj)` returns every rank's obj on rank 0
-    (torch.distributed.gather_object); None means a single rank."""
+    (torch.distributed.gather_object); None means a single rank.
+
+    When scan_chrom returns (vcf, raw_ctx) pairs, rank 0 also joins the raw
+    CTX rows in chromosome order and returns (vcf, ctx_post(raw)) -- the
+    translocation post-pass over the whole genome's CTX rows."""
     mine = assign_chromosomes(lengths, world)[rank] if world > 1 else list(range(len(lengths)))
     texts = {i: scan_chrom(i) for i in mine}
     parts = [texts] if gather is None else gather(texts)
@@ -124,7 +132,12 @@ def sharded_genome_text(scan_chrom: "Callable[[int], str]", lengths: Sequence[in
     missing = [i for i in range(len(lengths)) if i not in merged]
     if missing:
         raise RuntimeError(f"chromosomes {missing} scanned by no rank")
-    return "".join(merged[i] for i in range(len(lengths)))
+    vals = [merged[i] for i in range(len(lengths))]
+    if vals and isinstance(vals[0], tuple):
+        vcf = "".join(v[0] for v in vals)
+        raw = "".join(v[1] for v in vals)
+        return vcf, (ctx_post(raw) if ctx_post else raw)
+    return "".join(vals)
 
 
 def gather_to_rank0(obj):

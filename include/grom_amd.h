@@ -388,6 +388,15 @@ int grom_scan_chrom_staged(int slot, grom_stage *s, const grom_chrom *chrom, gro
 int grom_debug_counts_staged(int slot, grom_stage *s, const grom_chrom *chrom, int32_t *first_pos, int32_t *counts,
                              int64_t counts_cap, int32_t *caf3);
 
+/* main's translocation post-pass (GROM.c:22400-22770) over the raw CTX rows
+ * of every chromosome (grom_out.ctx of each scan, concatenated in chromosome
+ * order): pairs each breakpoint with its mate row, drops the weaker of two
+ * nearby pairs and appends the BND rows of .ctx.vcf (no header) to out->ctx.
+ * target_names: the BAM header's target names (the mate chromosome ids index
+ * them).  Used by the CLI and by a multi-rank caller on rank 0. */
+int grom_ctx_postpass(const char *raw, size_t raw_len, const char *const *target_names, int32_t n_targets,
+                      int32_t insert_max, int32_t lseq, grom_out *out);
+
 /* The drop-in command line (GROM's main, GROM.c:21865) as a library call:
  * argv as for `GROM -i BAM -r FASTA -o OUT [options]`; returns the exit code.
  * The `grom` executable is a wrapper around it. */

@@ -142,6 +142,14 @@ def test_counters_and_vcf_bit_exact(datadir, case, extra):
     _check_counters(datadir, case, extra, f"{case}{''.join(extra).replace('-', '_')}")
 
 
+def test_breakpoint_context_buffer_retry(datadir):
+    """The pileup's breakpoint context records (one per clipped or marked base)
+    go to a buffer sized by a guess; a scan that wants more runs again with
+    room (scan.hip).  GROM_SV_CTX_CAP=2000 makes the first pass overflow on the
+    sv case: counters, breakpoint records and rows must still be the oracle's."""
+    _check_counters(datadir, "sv", [], "svctxcap", env_extra={"GROM_SV_CTX_CAP": "2000"})
+
+
 def _oracle_once(datadir, case, extra):
     """The oracle's VCF for (case, flags), run once per session (the long-region
     cases take the oracle about a minute)."""
@@ -353,11 +361,14 @@ def _gpu_scan_factory(slot):
         b = grom_amd.SynthBatch.genome_chrom(GENOME_LENGTHS, i, p, names=GENOME_NAMES, sv_per_mb=4.0,
                                              dup_frac=0.05, cnv_rate=2e-6, cnv_range=(20_000, 80_000), seed=6)
         try:
-            text, _ = dev.scan(b.chrom, b.reads)
-            return text
+            vcf, ctx, _ = dev.scan_rows(b.chrom, b.reads)
+            return vcf, ctx
         finally:
             b.close()
-    return dev, scan
+
+    def post(raw):
+        return grom_amd.ctx_postpass(raw, GENOME_NAMES, p.insert_max_size, p.lseq)
+    return dev, scan, post
 
 
 def _gpu_shard_worker(rank, world, port, q):
@@ -367,8 +378,8 @@ def _gpu_shard_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        dev, scan = _gpu_scan_factory(rank)
-        q.put((rank, sharded_genome_text(scan, GENOME_LENGTHS, world, rank, gather_to_rank0)))
+        dev, scan, post = _gpu_scan_factory(rank)
+        q.put((rank, sharded_genome_text(scan, GENOME_LENGTHS, world, rank, gather_to_rank0, ctx_post=post)))
         dev.close()
     finally:
         dist.destroy_process_group()
@@ -381,8 +392,8 @@ def test_two_ranks_sharded_genome_matches_one_rank():
     import socket
     import torch.multiprocessing as mp
     from grom_amd.shard import sharded_genome_text
-    dev, scan = _gpu_scan_factory(40)
-    one = sharded_genome_text(scan, GENOME_LENGTHS, 1, 0)
+    dev, scan, post = _gpu_scan_factory(40)
+    one = sharded_genome_text(scan, GENOME_LENGTHS, 1, 0, ctx_post=post)
     dev.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -398,4 +409,7 @@ def test_two_ranks_sharded_genome_matches_one_rank():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0] == one
-    assert one.count("\n") > 100 and "chrx" in one
+    vcf, bnd = one
+    assert vcf.count("\n") > 100 and "chrx" in vcf
+    # the translocation rows of the whole genome, paired across the ranks' chromosomes
+    assert bnd.count("SVTYPE=BND") >= 2, bnd

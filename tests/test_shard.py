@@ -143,3 +143,26 @@ def test_sharded_text_rejects_gaps_and_overlaps():
         sharded_genome_text(lambda i: "x", [5, 4], 2, 0, gather=lambda d: [d, d])  # same chromosome twice
     with pytest.raises(RuntimeError):
         sharded_genome_text(lambda i: "x", [5, 4], 2, 0, gather=lambda d: [d])  # rank 1's share missing
+
+
+def test_sharded_text_carries_ctx_rows_to_the_postpass():
+    """With (vcf, raw CTX) per chromosome, rank 0 joins both in chromosome order
+    and runs the translocation post-pass over the whole genome's CTX rows."""
+    from grom_amd.shard import sharded_genome_text
+    parts = {0: {0: ("v0\n", "c0\n"), 2: ("v2\n", "c2\n")}, 1: {1: ("v1\n", "c1\n")}}
+    out = sharded_genome_text(lambda i: None, [5, 4, 3], 2, 0, gather=lambda d: [parts[0], parts[1]],
+                              ctx_post=lambda raw: raw.upper())
+    assert out == ("v0\nv1\nv2\n", "C0\nC1\nC2\n")
+
+
+def test_ctx_postpass_pairs_translocations():
+    """grom_ctx_postpass (main's post-pass, GROM.c:22400-22770) on two raw CTX
+    rows that are each other's mates: both kept, as BND rows naming the mate."""
+    import grom_amd
+    # raw row: type chr pos binom ev rd conc other mchr mpos rs re hez
+    raw = ("CTX_F\tchr1\t1000\t1e-10\t5.0\t30\t10\t0\t1\t-5000\t900\t990\t1e-5\n"
+           "CTX_R\tchr2\t5000\t1e-10\t5.0\t30\t10\t0\t0\t1000\t5010\t5100\t1e-5\n")
+    text = grom_amd.ctx_postpass(raw, ["chr1", "chr2"], 600, 150)
+    rows = text.splitlines()
+    assert len(rows) == 2 and all("SVTYPE=BND" in r for r in rows), text
+    assert rows[0].startswith("chr1\t1001\t") and "chr2:5000" in rows[0]
