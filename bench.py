@@ -145,6 +145,8 @@ def cli_whole_run_start(work_dir, knobs, flags, scale):
     t0 = time.perf_counter()
     bam, fa = run_synth(os.path.join(src, "cli"), *synth_args(knobs, lengths), "-n", ",".join(names), timeout=1200)
     t_synth = time.perf_counter() - t0
+    print(f"[bench] whole-run BAM written: {total / 1e6:.1f} Mb, {os.path.getsize(bam) / 1e9:.2f} GB in {t_synth:.1f} s",
+          file=sys.stderr, flush=True)
     env = dict(os.environ, GROM_FILEDATE="20260101", GROM_SEED="7")
     dirs = {}
     for side in ("gpu", "cpu"):  # own copies of the side files (.mean, .info); same paths in the VCF header
@@ -158,8 +160,9 @@ def cli_whole_run_start(work_dir, knobs, flags, scale):
     for _ in range(2):
         t1 = time.perf_counter()
         r = subprocess.run([GROM_BIN] + args, cwd=dirs["gpu"], env=dict(env, GROM_VERBOSE="1"), capture_output=True,
-                           text=True, timeout=1200)
+                           text=True, timeout=600)
         runs.append(time.perf_counter() - t1)
+        print(f"[bench] CLI whole run {len(runs)}: {runs[-1]:.2f} s", file=sys.stderr, flush=True)
         if r.returncode != 0:
             raise RuntimeError("GPU CLI failed on the whole-run BAM: " + r.stdout[-2000:] + r.stderr[-2000:])
     dec = [ln for ln in r.stdout.splitlines() if ln.startswith("streamed decode:")]

@@ -404,8 +404,9 @@ struct pd_session {
     int n_dev;
     int *dev_of;           /* plan index -> device */
     grom_stage **stages;   /* pool: n_stage, each with its device and busy flag */
-    int *stage_dev, *stage_busy;
-    int n_stage, cap_stage;
+    int *stage_dev, *stage_busy, *stage_owner; /* owner: the chromosome using it */
+    int *stage_mine;       /* made here (freed by pd_close), not by the caller */
+    int n_stage, cap_stage, extra_stages;
     /* counters */
     int64_t c_records, c_inflated, c_compressed, c_h2d;
     double c_dec_s, c_upl_s, c_wait_s, c_inflate_s;
@@ -1098,20 +1099,27 @@ static int mirror_append(grom_batch *m, const grom_reads *p) {
 /* ---------------- the uploader ---------------- */
 static void apply_final(pd_session *s, int idx);
 
-static int stage_acquire(pd_session *s, int dev, grom_stage **out) {
+/* A stage for chromosome k on GPU `dev`.  Waiting for a busy one is safe
+ * only when every busy stage belongs to a chromosome already finalised (the
+ * scans release those); a stage held by a chromosome still waiting for its
+ * finalisation -- which this same thread does -- would never come back, so
+ * then one more stage is made instead. */
+static int stage_acquire(pd_session *s, int dev, int k, grom_stage **out) {
     pthread_mutex_lock(&s->mu);
     for (;;) {
         if (s->abort) { pthread_mutex_unlock(&s->mu); return -1; }
         for (int i = 0; i < s->n_stage; i++)
             if (!s->stage_busy[i] && s->stage_dev[i] == dev) {
                 s->stage_busy[i] = 1;
+                s->stage_owner[i] = k;
                 *out = s->stages[i];
                 pthread_mutex_unlock(&s->mu);
                 return 0;
             }
-        /* while the insert statistics are incomplete no chromosome can be
-         * finalised, so every busy stage waits on this thread: add one */
-        if (!s->stats_done || s->n_stage < 1) {
+        int unsafe = s->n_stage < 1;
+        for (int i = 0; i < s->n_stage && !unsafe; i++)
+            if (s->stage_busy[i] && (s->stage_owner[i] < 0 || !s->ch[s->stage_owner[i]].final)) unsafe = 1;
+        if (unsafe) {
             pthread_mutex_unlock(&s->mu);
             grom_stage *st = grom_stage_new(dev);
             if (!st) return -1;
@@ -1121,11 +1129,16 @@ static int stage_acquire(pd_session *s, int dev, grom_stage **out) {
                 s->stages = (grom_stage **)realloc(s->stages, sizeof(grom_stage *) * s->cap_stage);
                 s->stage_dev = (int *)realloc(s->stage_dev, sizeof(int) * s->cap_stage);
                 s->stage_busy = (int *)realloc(s->stage_busy, sizeof(int) * s->cap_stage);
+                s->stage_owner = (int *)realloc(s->stage_owner, sizeof(int) * s->cap_stage);
+                s->stage_mine = (int *)realloc(s->stage_mine, sizeof(int) * s->cap_stage);
             }
             s->stages[s->n_stage] = st;
             s->stage_dev[s->n_stage] = dev;
             s->stage_busy[s->n_stage] = 1;
+            s->stage_owner[s->n_stage] = k;
+            s->stage_mine[s->n_stage] = 1;
             s->n_stage++;
+            s->extra_stages++;
             *out = st;
             pthread_mutex_unlock(&s->mu);
             return 0;
@@ -1165,7 +1178,7 @@ static int chrom_begin(pd_session *s, int k, const pd_buf *first) {
     pd_chrom *c = &s->ch[k];
     c->begun = 1;
     if (s->plan_only) return 0;
-    if (stage_acquire(s, c->device, &c->stage)) return -1;
+    if (stage_acquire(s, c->device, k, &c->stage)) return -1;
     grom_stage_sizes est;
     memset(&est, 0, sizeof(est));
     if (c->run >= 0) {
@@ -1924,7 +1937,7 @@ int pd_wait_chrom(pd_session *s, int k, grom_stage **stage, pd_chrom_facts *fact
 void pd_release_stage(pd_session *s, grom_stage *st) {
     pthread_mutex_lock(&s->mu);
     for (int i = 0; i < s->n_stage; i++)
-        if (s->stages[i] == st) s->stage_busy[i] = 0;
+        if (s->stages[i] == st) { s->stage_busy[i] = 0; s->stage_owner[i] = -1; }
     pthread_cond_broadcast(&s->cv);
     pthread_mutex_unlock(&s->mu);
 }
@@ -1936,10 +1949,14 @@ int pd_add_stage(pd_session *s, grom_stage *st, int device) {
         s->stages = (grom_stage **)realloc(s->stages, sizeof(grom_stage *) * s->cap_stage);
         s->stage_dev = (int *)realloc(s->stage_dev, sizeof(int) * s->cap_stage);
         s->stage_busy = (int *)realloc(s->stage_busy, sizeof(int) * s->cap_stage);
+        s->stage_owner = (int *)realloc(s->stage_owner, sizeof(int) * s->cap_stage);
+        s->stage_mine = (int *)realloc(s->stage_mine, sizeof(int) * s->cap_stage);
     }
     s->stages[s->n_stage] = st;
     s->stage_dev[s->n_stage] = device;
     s->stage_busy[s->n_stage] = 0;
+    s->stage_owner[s->n_stage] = -1;
+    s->stage_mine[s->n_stage] = 0;
     s->n_stage++;
     pthread_cond_broadcast(&s->cv);
     pthread_mutex_unlock(&s->mu);
@@ -2011,7 +2028,11 @@ void pd_close(pd_session *s) {
     free(s->remap);
     free(s->stages);
     free(s->stage_dev);
+    for (int i = 0; i < s->n_stage; i++)
+        if (s->stage_mine[i]) grom_stage_free(s->stages[i]);
     free(s->stage_busy);
+    free(s->stage_owner);
+    free(s->stage_mine);
     free(s->thr);
     free(s->ch);
     free(s->plan);
