@@ -185,7 +185,13 @@ def cli_whole_run_start(work_dir, knobs, flags, scale):
 
 def cli_whole_run_finish(st):
     info = st["info"]
-    err = st["proc"].communicate(timeout=3600)[1]
+    while True:  # a line every 30 s while the oracle runs (long silent runs look hung)
+        try:
+            err = st["proc"].communicate(timeout=30)[1]
+            break
+        except subprocess.TimeoutExpired:
+            print(f"[bench] oracle on the whole-run BAM: {time.perf_counter() - st['t_oracle']:.0f} s", file=sys.stderr,
+                  flush=True)
     dt = time.perf_counter() - st["t_oracle"]
     if st["proc"].returncode != 0:
         info["identical_to_oracle"] = None

@@ -1,4 +1,29 @@
-/* grom_cli.c -- the `grom` executable: a thin wrapper over grom_cli_main. */
+/* grom_cli.c -- the `grom` executable: a thin wrapper over grom_cli_main.
+ * A fatal signal prints the host stack (addresses resolve with addr2line
+ * against grom_amd/lib/libgrom_amd.so) before the process ends. */
+#include <execinfo.h>
+#include <signal.h>
+#include <string.h>
+#include <unistd.h>
+
 #include "../../include/grom_amd.h"
 
-int main(int argc, char **argv) { return grom_cli_main(argc, argv); }
+static void on_fatal(int sig) {
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    static const char msg[] = "grom: fatal signal, host stack:\n";
+    if (write(2, msg, sizeof(msg) - 1) < 0) { /* nothing more to do */ }
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+int main(int argc, char **argv) {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_handler = on_fatal;
+    sigaction(SIGBUS, &sa, NULL);
+    sigaction(SIGSEGV, &sa, NULL);
+    sigaction(SIGABRT, &sa, NULL);
+    return grom_cli_main(argc, argv);
+}

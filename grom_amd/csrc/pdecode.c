@@ -397,6 +397,7 @@ struct pd_session {
     int32_t *s_ins, *s_lq;
     int64_t s_n, s_m;
     int walk_set, final_pending, final_applied;
+    int next_final, finalizing; /* the uploader's finalisation cursor */
     int *keep;             /* final plan (per preliminary chromosome) */
     int32_t index_start, overlap_mult, insert_max;
     /* devices and stages (pd_stream_chrom's caller owns the stages) */
@@ -1174,10 +1175,14 @@ static void mark_stats_done(pd_session *s) {
     pthread_mutex_unlock(&s->mu);
 }
 
+static int finalize_ready(pd_session *s);
+
 static int chrom_begin(pd_session *s, int k, const pd_buf *first) {
     pd_chrom *c = &s->ch[k];
     c->begun = 1;
     if (s->plan_only) return 0;
+    /* earlier chromosomes first: their stages can then go back to the pool */
+    if (finalize_ready(s)) return -1;
     if (stage_acquire(s, c->device, k, &c->stage)) return -1;
     grom_stage_sizes est;
     memset(&est, 0, sizeof(est));
@@ -1445,41 +1450,55 @@ static int chrom_finalize(pd_session *s, int k) {
     return rc;
 }
 
+/* finalise, in plan order, every chromosome whose records are all staged
+ * (uploader thread only); 0, or -1 after an abort */
+static int finalize_ready(pd_session *s) {
+    if (s->finalizing) return 0;
+    s->finalizing = 1;
+    int rc = 0;
+    for (;;) {
+        pthread_mutex_lock(&s->mu);
+        while (s->next_final < s->n_plan && s->final_applied && !s->ch[s->next_final].kept) s->next_final++;
+        const int k = s->next_final;
+        const int ok = !s->abort && k < s->n_plan && s->stats_done && s->final_applied &&
+                       (s->ch[k].run < 0 || s->ch[k].uploaded);
+        pthread_mutex_unlock(&s->mu);
+        if (!ok) break;
+        const double t0 = now_s();
+        const int r = chrom_finalize(s, k);
+        s->c_upl_s += now_s() - t0;
+        pthread_mutex_lock(&s->mu);
+        s->ch[k].rc = r;
+        s->ch[k].final = 1;
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+        if (r) {
+            sess_abort(s, 0, "finalising a chromosome failed");
+            rc = -1;
+            break;
+        }
+        s->next_final++;
+    }
+    s->finalizing = 0;
+    return rc;
+}
+
 static void *uploader_main(void *arg) {
     pd_session *s = (pd_session *)arg;
-    int next_final = 0;
     int cur_chrom = -1;
     for (int idx = 0; idx <= s->n_pieces; idx++) {
         pthread_mutex_lock(&s->mu);
         const int pend = s->final_pending && !s->final_applied;
         pthread_mutex_unlock(&s->mu);
         if (pend) apply_final(s, idx < s->n_pieces ? idx : s->n_pieces);
-        /* finalise every chromosome whose records are all staged */
-        for (;;) {
-            pthread_mutex_lock(&s->mu);
-            while (next_final < s->n_plan && s->final_applied && !s->ch[next_final].kept) next_final++;
-            const int ok = !s->abort && next_final < s->n_plan && s->stats_done && s->final_applied &&
-                           (s->ch[next_final].run < 0 || s->ch[next_final].uploaded);
-            pthread_mutex_unlock(&s->mu);
-            if (!ok) break;
-            const double t0 = now_s();
-            const int rc = chrom_finalize(s, next_final);
-            s->c_upl_s += now_s() - t0;
-            pthread_mutex_lock(&s->mu);
-            s->ch[next_final].rc = rc;
-            s->ch[next_final].final = 1;
-            pthread_cond_broadcast(&s->cv);
-            pthread_mutex_unlock(&s->mu);
-            if (rc) { sess_abort(s, 0, "finalising a chromosome failed"); break; }
-            next_final++;
-        }
+        if (finalize_ready(s)) break;
         if (idx == s->n_pieces) {
             if (!s->stats_done) mark_stats_done(s);
             /* the walk parameters may still be on their way */
             pthread_mutex_lock(&s->mu);
-            while (!s->abort && next_final < s->n_plan && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
-            while (next_final < s->n_plan && s->final_applied && !s->ch[next_final].kept) next_final++;
-            const int more = !s->abort && next_final < s->n_plan;
+            while (!s->abort && s->next_final < s->n_plan && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
+            while (s->next_final < s->n_plan && s->final_applied && !s->ch[s->next_final].kept) s->next_final++;
+            const int more = !s->abort && s->next_final < s->n_plan;
             pthread_mutex_unlock(&s->mu);
             if (more) { idx--; continue; } /* loop back to finalise */
             break;
@@ -2026,10 +2045,10 @@ void pd_close(pd_session *s) {
     free(s->T.ht);
     free(s->T.hh);
     free(s->remap);
-    free(s->stages);
-    free(s->stage_dev);
     for (int i = 0; i < s->n_stage; i++)
         if (s->stage_mine[i]) grom_stage_free(s->stages[i]);
+    free(s->stages);
+    free(s->stage_dev);
     free(s->stage_busy);
     free(s->stage_owner);
     free(s->stage_mine);
