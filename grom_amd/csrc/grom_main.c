@@ -308,6 +308,7 @@ typedef struct {
     grom_stage *stage;
     pd_chrom_facts facts;
     pd_session *pd;        /* releases the stage after the scan */
+    int k;                 /* plan index (trace) */
     int device;            /* the GPU the stage lives on, -1: any */
     char *text, *ctx_text;
     size_t text_len, ctx_len;
@@ -407,8 +408,10 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     ch.seed = chrom_seed();
     grom_out out = {0};
     grom_stats st = {0};
+    if (j->pd) pd_trace(j->pd, PD_EV_SCAN, j->k, 0);
     int rc = j->has_batch ? grom_scan_chrom(slot, &ch, &rd, &out, &st)
                           : grom_scan_chrom_staged(slot, j->stage, &ch, &out, &st);
+    if (j->pd) pd_trace(j->pd, PD_EV_SCAN, j->k, 1);
     if (rc != GROM_OK) {
         fprintf(stderr, "grom: scan of %s failed: %s\n", cp->name, grom_last_error());
         grom_out_free(&out);
@@ -512,7 +515,22 @@ typedef struct {
     int n_cand;
     char ctx_name[4096];
     int wdev[64], n_work, n_init;
+    double t_cli0, t_cand; /* CLI start, candidates (FASTA lengths) done */
+    double t_scans, t_pdclose, t_outputs; /* scans done, decoder closed, outputs written */
+    pthread_t hip_thr;     /* HIP runtime start-up, beside the header/FASTA/index work */
+    int hip_started;
 } cli_state;
+
+static void *hip_init_main(void *arg) {
+    (void)arg;
+    (void)grom_device_count();
+    return NULL;
+}
+
+static void hip_ready(cli_state *S) {
+    if (S->hip_started) pthread_join(S->hip_thr, NULL);
+    S->hip_started = 0;
+}
 
 #define CLI_FALLBACK 99 /* the streamed path could not be used: read serially */
 
@@ -571,6 +589,7 @@ static int setup_workers(cli_state *S) {
         if (S->n_work < 1) { S->wdev[0] = S->device; S->n_work = 1; }
     }
     tables_join(S);
+    hip_ready(S);
     int rc = GROM_OK;
     for (int d = 0; d < S->n_work && !g_plan_only && rc == GROM_OK; d++) {
         rc = grom_ctx_init(d, S->wdev[d], P, S->hez, S->mq);
@@ -841,6 +860,7 @@ static int run_streamed(cli_state *S) {
         return CLI_FALLBACK;
     }
     /* GPUs: contexts need the insert statistics, stages do not */
+    hip_ready(S);
     if (getenv("GROM_DEVICES")) S->n_dev = atoi(getenv("GROM_DEVICES"));
     if (S->n_dev < 1) S->n_dev = 1;
     if (!g_plan_only && S->n_dev > 1) {
@@ -901,6 +921,7 @@ static int run_streamed(cli_state *S) {
     int status = 0;
     int lseq = 0, imin = 0, imax = 0;
     long mapped = 0;
+    const double t_started = clock_gettime_s();
     const int imean = pd_insert_stats(pd, grom_prob2(S->num_sd), P->min_mapq, &lseq, &imin, &imax, &mapped);
     if (imean < 0) {
         const int fallback = imean == -2;
@@ -912,6 +933,7 @@ static int run_streamed(cli_state *S) {
         return fallback ? CLI_FALLBACK : 1;
     }
     print_insert(S, imean, lseq, imin, imax, mapped);
+    const double t_stats = clock_gettime_s();
     int *keep = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
     chrom_plan **plan = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(chrom_plan *));
     int *pidx = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
@@ -933,6 +955,7 @@ static int run_streamed(cli_state *S) {
     pthread_t fthr;
     int fasta_started = 0;
     if (setup_workers(S)) { status = 1; goto done; }
+    const double t_ctx = clock_gettime_s();
     vcf = fopen(S->out_name, "w");
     if (!vcf) { printf("Error opening file %s\n", S->out_name); status = 1; goto done; }
     if (P->vcf == 1) header(vcf, S->fasta_name, 0);
@@ -984,7 +1007,9 @@ static int run_streamed(cli_state *S) {
         j->stage = st;
         j->facts = facts;
         j->pd = pd;
+        j->k = pidx[k];
         j->device = dev_of[pidx[k]];
+        pd_trace(pd, PD_EV_HANDED, pidx[k], 0);
         j->ready = 1;
         pthread_cond_broadcast(&pool.cv);
         drain_rows(&pool, &next_write, k + 1, vcf, &ctx_all, &status);
@@ -1002,8 +1027,13 @@ done:
         pthread_mutex_destroy(&F.mu);
         pthread_cond_destroy(&F.cv);
     }
+    const double t_loop = clock_gettime_s();
     if (started) pool_finish(&pool, S, workers, tids, &next_write, vcf, &ctx_all, &status);
     if (!fallback && status == 0 && S->verbose) {
+        const double t_end = clock_gettime_s();
+        printf("cli phases (s from start): candidates/FASTA lengths %.3f, decoder open %.3f, insert statistics %.3f, "
+               "contexts %.3f, last chromosome handed %.3f, scans done %.3f\n", S->t_cand - S->t_cli0,
+               t_started - S->t_cli0, t_stats - S->t_cli0, t_ctx - S->t_cli0, t_loop - S->t_cli0, t_end - S->t_cli0);
         pd_counters pc;
         pd_get_counters(pd, &pc);
         printf("streamed decode: %lld records in %lld pieces, %d threads (%s), %.2f GB inflated, %.2f GB to HBM, "
@@ -1012,10 +1042,13 @@ done:
                pc.inflated_bytes / 1e9, pc.h2d_bytes / 1e9, pc.decode_thread_s, pc.inflate_s, pc.upload_s, pc.wait_s,
                clock_gettime_s() - t_start);
     }
+    S->t_scans = clock_gettime_s();
     pd_close(pd);
     for (int i = 0; i < n_stages; i++) grom_stage_free(stages[i]);
+    S->t_pdclose = clock_gettime_s();
     if (vcf) fclose(vcf);
     if (!fallback && status == 0) finish_outputs(S, &ctx_all);
+    S->t_outputs = clock_gettime_s();
     free(ctx_all.p);
     free(plan);
     free(pidx);
@@ -1033,6 +1066,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
     optind = 0; /* GNU getopt: 0 fully re-initialises, so this is callable again */
     setlinebuf(stdout);
     cli_state *S = calloc(1, sizeof(cli_state));
+    S->t_cli0 = clock_gettime_s();
     grom_params *P = &S->P;
     grom_default_params(P);
     S->max_chr_len = 300000000; /* g_max_chr_fasta_len, GROM.c:946 */
@@ -1129,6 +1163,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
         goto out_hdr;
     }
     g_plan_only = getenv("GROM_PLAN_ONLY") != NULL;
+    if (!g_plan_only) S->hip_started = pthread_create(&S->hip_thr, NULL, hip_init_main, NULL) == 0;
     /* tables (read_binom_tables, GROM.c:22234) on a thread beside the decode */
     {
         size_t tn = (size_t)(GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);
@@ -1160,6 +1195,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
         c->target = strdup(S->hdr.n_ref > 0 ? S->hdr.ref_name[tid2 >= 0 ? tid2 : S->hdr.n_ref - 1] : "");
         snprintf(c->name, sizeof(c->name), "%.*s", S->fa.name_len[fi], S->fa.names[fi]);
     }
+    S->t_cand = clock_gettime_s();
     {
         size_t ol = strlen(S->out_name);
         if (ol > 4 && strcmp(S->out_name + ol - 4, ".vcf") == 0)
@@ -1172,6 +1208,10 @@ static int cli_run(int argc, char **argv, int force_serial) {
     else ret = run_streamed(S);
     tables_join(S);
     for (int d = 0; d < S->n_init; d++) grom_dev_fini(d);
+    if (S->verbose && S->t_outputs > 0)
+        printf("cli teardown (s from start): scans done %.3f, decoder + stages freed %.3f, outputs %.3f, contexts "
+               "freed %.3f\n", S->t_scans - S->t_cli0, S->t_pdclose - S->t_cli0, S->t_outputs - S->t_cli0,
+               clock_gettime_s() - S->t_cli0);
     for (int i = 0; i < S->n_cand; i++) {
         free(S->plan[i].target);
         free(S->plan[i].ref);
@@ -1182,6 +1222,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
     grom_fasta_close(&S->fa);
 out_hdr:
     tables_join(S);
+    hip_ready(S);
     bam_free_header(&S->hdr);
     free(S);
     return ret;

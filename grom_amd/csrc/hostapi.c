@@ -44,11 +44,10 @@ static void on_record(void *ctx, const bam_rec *r) {
     grom_batch_add(&h->b, r, 0); /* the skip prefix is trimmed once index_start is known */
 }
 
-static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
 
 /* find_insert_mean's statistics (GROM.c:1276-1310) from the sampled pairs */
 static void insert_stats(struct grom_batch_handle *h, grom_params *P) {
-    qsort(h->ins, h->n_ins, sizeof(int), icmp);
+    grom_sort_ints(h->ins, h->n_ins);
     int64_t n = h->n_ins;
     int mean = h->ins[n / 2], lim = mean * 5;
     int64_t end = 0;
@@ -58,7 +57,7 @@ static void insert_stats(struct grom_batch_handle *h, grom_params *P) {
     mean = h->ins[end / 2];
     int lo = (int)(grom_prob2(3.0) * end / 2);
     int imin = h->ins[lo], imax = h->ins[end - lo < n ? end - lo : n - 1];
-    qsort(h->lq, n, sizeof(int), icmp);
+    grom_sort_ints(h->lq, n);
     grom_params_set_insert(P, mean, imin, imax, h->lq[n / 2]);
 }
 

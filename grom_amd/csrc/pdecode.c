@@ -248,7 +248,10 @@ static void rd_free(pd_reader *r) {
 
 /* ---------------- piece buffers ---------------- */
 typedef struct pd_buf {
-    /* pinned, appended to the stage */
+    /* pinned, appended to the stage: one block holds every part at its first
+     * capacity (a part that outgrows it gets a block of its own) */
+    char *base;
+    size_t base_len;
     int64_t cap;
     void *rec_mem;
     int32_t *pos, *mtid, *mpos, *isize, *lq, *aidx;
@@ -411,11 +414,31 @@ struct pd_session {
     /* counters */
     int64_t c_records, c_inflated, c_compressed, c_h2d;
     double c_dec_s, c_upl_s, c_wait_s, c_inflate_s;
+    /* GROM_TRACE */
+    char *trace_path;
+    double t0;
+    struct { double t; int64_t a, b; int ev, thr; } *tr;
+    int64_t tr_n, tr_cap;
     /* uploader scratch */
     uint32_t *remap;
     int64_t remap_cap;
     tail_set T;
 };
+
+static __thread int tls_thread_id = -1;
+static int g_thread_ids;
+
+void pd_trace(pd_session *s, int ev, int64_t a, int64_t b) {
+    if (!s || !s->tr) return;
+    if (tls_thread_id < 0) tls_thread_id = __sync_fetch_and_add(&g_thread_ids, 1);
+    const int64_t i = __sync_fetch_and_add(&s->tr_n, 1);
+    if (i >= s->tr_cap) return;
+    s->tr[i].t = now_s() - s->t0;
+    s->tr[i].ev = ev;
+    s->tr[i].a = a;
+    s->tr[i].b = b;
+    s->tr[i].thr = tls_thread_id;
+}
 
 static void sess_abort(pd_session *s, int soft, const char *msg) {
     pthread_mutex_lock(&s->mu);
@@ -434,8 +457,9 @@ static void *pin_alloc(pd_session *s, size_t bytes, int pinned) {
     return pinned ? grom_pinned_alloc(bytes) : malloc(bytes ? bytes : 16);
 }
 
-static void pin_retire(pd_session *s, void *p, int pinned) {
+static void pin_retire(pd_session *s, const pd_buf *b, void *p, int pinned) {
     if (!p) return;
+    if (b->base && (char *)p >= b->base && (char *)p < b->base + b->base_len) return; /* part of the block */
     if (!pinned) { free(p); return; }
     pthread_mutex_lock(&s->mu);
     if (s->n_old == s->cap_old) {
@@ -485,7 +509,7 @@ static int buf_grow_recs(pd_session *s, pd_buf *b, int64_t need) {
     free(b->hclip);
     b->end = end;
     b->hclip = hc;
-    pin_retire(s, b->rec_mem, !s->plan_only);
+    pin_retire(s, b, b->rec_mem, !s->plan_only);
     b->rec_mem = m;
     b->cap = nc;
     return 0;
@@ -498,7 +522,7 @@ static int buf_grow_cig(pd_session *s, pd_buf *b, int64_t need) {
     uint32_t *p = (uint32_t *)pin_alloc(s, sizeof(uint32_t) * (size_t)nc, !s->plan_only);
     if (!p) return -1;
     if (b->n_cig) memcpy(p, b->cig, sizeof(uint32_t) * (size_t)b->n_cig);
-    pin_retire(s, b->cig, !s->plan_only);
+    pin_retire(s, b, b->cig, !s->plan_only);
     b->cig = p;
     b->cap_cig = nc;
     return 0;
@@ -516,7 +540,7 @@ static int buf_grow_bases(pd_session *s, pd_buf *b, int64_t need) {
         memcpy(q, b->qual, (size_t)b->n_b);
         memcpy(sq, b->seq, (size_t)b->n_b / 2);
     }
-    pin_retire(s, b->qual, !s->plan_only);
+    pin_retire(s, b, b->qual, !s->plan_only);
     b->qual = q;
     b->seq = sq;
     b->cap_b = nc;
@@ -530,7 +554,7 @@ static int buf_grow_aux(pd_session *s, pd_buf *b, int64_t need) {
     grom_aux *p = (grom_aux *)pin_alloc(s, sizeof(grom_aux) * (size_t)nc, !s->plan_only);
     if (!p) return -1;
     if (b->n_aux) memcpy(p, b->aux, sizeof(grom_aux) * (size_t)b->n_aux);
-    pin_retire(s, b->aux, !s->plan_only);
+    pin_retire(s, b, b->aux, !s->plan_only);
     b->aux = p;
     b->cap_aux = nc;
     return 0;
@@ -562,16 +586,12 @@ static void buf_reset(pd_buf *b) {
 }
 
 static void buf_destroy(pd_buf *b, int pinned) {
-    if (pinned) {
-        grom_pinned_free(b->rec_mem);
-        grom_pinned_free(b->cig);
-        grom_pinned_free(b->qual);
-        grom_pinned_free(b->aux);
-    } else {
-        free(b->rec_mem);
-        free(b->cig);
-        free(b->qual);
-        free(b->aux);
+    void *parts[5] = {b->rec_mem, b->cig, b->qual, b->aux, b->base};
+    for (int i = 0; i < 5; i++) {
+        void *q = parts[i];
+        if (!q || (i < 4 && b->base && (char *)q >= b->base && (char *)q < b->base + b->base_len)) continue;
+        if (pinned) grom_pinned_free(q);
+        else free(q);
     }
     free(b->end);
     free(b->hclip);
@@ -803,6 +823,56 @@ oom:
 }
 
 /* ---------------- buffer pool ---------------- */
+/* a new buffer: every part carved from one block at its first capacity */
+static int buf_block(pd_session *s, pd_buf *b) {
+    const int64_t nr = PD_PIECE_RECS + PD_PIECE_RECS / 2, ncig = 4 * PD_PIECE_RECS, nb = (int64_t)160 * PD_PIECE_RECS,
+                  naux = 1024;
+    const size_t rec = (6 * 4 + 2 + 1 + 4 + 4 + 8) * (size_t)nr + 4 + 8 * 64;
+    const size_t sz[4] = {rec, 4 * (size_t)ncig, (size_t)nb + (size_t)nb / 2 + 64, sizeof(grom_aux) * (size_t)naux};
+    size_t off[4], tot = 0;
+    for (int i = 0; i < 4; i++) {
+        off[i] = tot;
+        tot += (sz[i] + 255) & ~(size_t)255;
+    }
+    b->base = (char *)pin_alloc(s, tot, !s->plan_only);
+    if (!b->base) return -1;
+    b->base_len = tot;
+    /* the growth functions carve from a part pointer that they then retire:
+     * point them at the block and let them "grow" from zero */
+    char *m = b->base + off[0];
+    size_t o = 0;
+#define CARVE0(field, type, count)                                                                \
+    do {                                                                                          \
+        b->field = (type *)(m + o);                                                               \
+        o += ((sizeof(type) * (size_t)(count)) + 63) & ~(size_t)63;                               \
+    } while (0)
+    CARVE0(boff, int64_t, nr);
+    CARVE0(pos, int32_t, nr);
+    CARVE0(mtid, int32_t, nr);
+    CARVE0(mpos, int32_t, nr);
+    CARVE0(isize, int32_t, nr);
+    CARVE0(lq, int32_t, nr);
+    CARVE0(aidx, int32_t, nr);
+    CARVE0(coff, uint32_t, nr + 1);
+    CARVE0(nid, uint32_t, nr);
+    CARVE0(flag, uint16_t, nr);
+    CARVE0(mapq, uint8_t, nr);
+#undef CARVE0
+    b->rec_mem = m;
+    b->cap = nr;
+    b->end = (int32_t *)malloc(sizeof(int32_t) * (size_t)nr);
+    b->hclip = (int32_t *)malloc(sizeof(int32_t) * (size_t)nr);
+    if (!b->end || !b->hclip) return -1;
+    b->cig = (uint32_t *)(b->base + off[1]);
+    b->cap_cig = ncig;
+    b->qual = (uint8_t *)(b->base + off[2]);
+    b->seq = b->qual + ((nb + 15) & ~(int64_t)15);
+    b->cap_b = nb;
+    b->aux = (grom_aux *)(b->base + off[3]);
+    b->cap_aux = naux;
+    return 0;
+}
+
 static pd_buf *pool_get(pd_session *s) {
     pthread_mutex_lock(&s->mu);
     for (;;) {
@@ -818,6 +888,7 @@ static pd_buf *pool_get(pd_session *s) {
             s->n_bufs++;
             pthread_mutex_unlock(&s->mu);
             pd_buf *b = (pd_buf *)calloc(1, sizeof(pd_buf));
+            if (b && buf_block(s, b)) { buf_destroy(b, !s->plan_only); b = NULL; }
             if (b) buf_reset(b);
             return b;
         }
@@ -888,6 +959,7 @@ static void *decoder_main(void *arg) {
         pthread_mutex_unlock(&s->mu);
         const double t0 = now_s();
         int rc = 0;
+        pd_trace(s, PD_EV_DECODE, idx, 0);
         if (!full && !need_stats) {
             pthread_mutex_lock(&s->mu);
             p->state = 3;
@@ -903,6 +975,7 @@ static void *decoder_main(void *arg) {
         }
         if (rc == 0) rc = decode_piece(s, &r, p, b);
         p->buf = b;
+        pd_trace(s, PD_EV_DECODE, idx, 1);
         p->secs = now_s() - t0;
         secs += p->secs;
         recs += p->n_rec;
@@ -1106,6 +1179,7 @@ static void apply_final(pd_session *s, int idx);
  * finalisation -- which this same thread does -- would never come back, so
  * then one more stage is made instead. */
 static int stage_acquire(pd_session *s, int dev, int k, grom_stage **out) {
+    pd_trace(s, PD_EV_STAGE, k, 0);
     pthread_mutex_lock(&s->mu);
     for (;;) {
         if (s->abort) { pthread_mutex_unlock(&s->mu); return -1; }
@@ -1115,6 +1189,7 @@ static int stage_acquire(pd_session *s, int dev, int k, grom_stage **out) {
                 s->stage_owner[i] = k;
                 *out = s->stages[i];
                 pthread_mutex_unlock(&s->mu);
+                pd_trace(s, PD_EV_STAGE, k, 1);
                 return 0;
             }
         int unsafe = s->n_stage < 1;
@@ -1142,6 +1217,7 @@ static int stage_acquire(pd_session *s, int dev, int k, grom_stage **out) {
             s->extra_stages++;
             *out = st;
             pthread_mutex_unlock(&s->mu);
+            pd_trace(s, PD_EV_STAGE, k, 2);
             return 0;
         }
         pthread_cond_wait(&s->cv, &s->mu);
@@ -1169,6 +1245,7 @@ static void piece_free_stats(pd_piece *p) {
 }
 
 static void mark_stats_done(pd_session *s) {
+    pd_trace(s, PD_EV_STATS, 0, 0);
     pthread_mutex_lock(&s->mu);
     s->stats_done = 1;
     pthread_cond_broadcast(&s->cv);
@@ -1470,6 +1547,7 @@ static int finalize_ready(pd_session *s) {
         pthread_mutex_lock(&s->mu);
         s->ch[k].rc = r;
         s->ch[k].final = 1;
+        pd_trace(s, PD_EV_FINAL, k, 0);
         pthread_cond_broadcast(&s->cv);
         pthread_mutex_unlock(&s->mu);
         if (r) {
@@ -1545,7 +1623,10 @@ static void *uploader_main(void *arg) {
                 cur_chrom = run->chrom;
                 tail_reset(&s->T);
             }
-            if (upload_piece(s, p)) {
+            pd_trace(s, PD_EV_UPLOAD, idx, 0);
+            const int urc = upload_piece(s, p);
+            pd_trace(s, PD_EV_UPLOAD, idx, 1);
+            if (urc) {
                 sess_abort(s, 0, grom_last_error());
                 break;
             }
@@ -1856,13 +1937,19 @@ pd_session *pd_open(const char *bam_path, const bam_hdr *hdr, const pd_chrom_in 
     s->splitread = splitread;
     s->read_name_len = read_name_len;
     s->n_threads = n_threads < 1 ? 1 : n_threads;
-    s->window = 4 * s->n_threads + 8;
-    s->max_bufs = s->window + s->n_threads + 16;
+    s->window = 2 * s->n_threads + 4;
+    s->max_bufs = s->window + s->n_threads / 2 + 8;
     s->s_ins = (int32_t *)malloc(sizeof(int32_t) * PD_INSERT_CAP);
     s->s_lq = (int32_t *)malloc(sizeof(int32_t) * PD_INSERT_CAP);
     if (!s->s_ins || !s->s_lq) FAIL("out of memory");
     pthread_mutex_init(&s->mu, NULL);
     pthread_cond_init(&s->cv, NULL);
+    s->t0 = now_s();
+    if (getenv("GROM_TRACE")) {
+        s->trace_path = strdup(getenv("GROM_TRACE"));
+        s->tr_cap = 8 * (int64_t)s->n_pieces + 16 * (int64_t)n_plan + 4096;
+        s->tr = calloc((size_t)s->tr_cap, sizeof(*s->tr));
+    }
     return s;
 fail:
     if (have_idx) bai_free(&idx);
@@ -1901,8 +1988,6 @@ int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan
     return 0;
 }
 
-static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
-
 int pd_insert_stats(pd_session *s, double prob2, int min_mapq, int *lseq, int *imin, int *imax, long *mapped) {
     (void)min_mapq;
     pthread_mutex_lock(&s->mu);
@@ -1913,7 +1998,7 @@ int pd_insert_stats(pd_session *s, double prob2, int min_mapq, int *lseq, int *i
     const int64_t n = s->s_n;
     if (n == 0) return -1;
     /* find_insert_mean's arithmetic, as grom_insert_stats */
-    qsort(s->s_ins, (size_t)n, sizeof(int), icmp);
+    grom_sort_ints(s->s_ins, n);
     int mean = s->s_ins[n / 2], lim = mean * 5, end = 0;
     for (int64_t a = n - 1; a >= 0; a--)
         if (s->s_ins[a] <= lim) { end = (int)a; break; }
@@ -1922,7 +2007,7 @@ int pd_insert_stats(pd_session *s, double prob2, int min_mapq, int *lseq, int *i
     int lo = (int)(prob2 * end / 2);
     *imin = s->s_ins[lo];
     *imax = s->s_ins[end - lo < n ? end - lo : n - 1];
-    qsort(s->s_lq, (size_t)n, sizeof(int), icmp);
+    grom_sort_ints(s->s_lq, n);
     *lseq = s->s_lq[n / 2];
     if (mapped) *mapped = (long)s->s_m;
     return mean;
@@ -1998,6 +2083,7 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
     c->inflated_bytes = s->c_inflated;
     c->compressed_bytes = s->c_compressed;
     c->decode_thread_s = s->c_dec_s;
+    c->h2d_bytes = s->c_h2d;
     c->inflate_s = s->c_inflate_s;
     c->upload_s = s->c_upl_s;
     c->wait_s = s->c_wait_s;
@@ -2009,6 +2095,22 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
 
 void pd_close(pd_session *s) {
     if (!s) return;
+    if (s->tr && s->trace_path) {
+        FILE *f = fopen(s->trace_path, "w");
+        if (f) {
+            static const char *names[] = {"", "decode", "upload", "final", "stats", "stage", "scan", "handed", "phase"};
+            fprintf(f, "t,thread,event,a,b\n");
+            const int64_t n = s->tr_n < s->tr_cap ? s->tr_n : s->tr_cap;
+            for (int64_t i = 0; i < n; i++)
+                fprintf(f, "%.6f,%d,%s,%lld,%lld\n", s->tr[i].t, s->tr[i].thr,
+                        s->tr[i].ev >= 1 && s->tr[i].ev <= 8 ? names[s->tr[i].ev] : "?", (long long)s->tr[i].a,
+                        (long long)s->tr[i].b);
+            fclose(f);
+        }
+    }
+    free(s->tr);
+    s->tr = NULL;
+    free(s->trace_path);
     pthread_mutex_lock(&s->mu);
     s->stop = 1;
     if (!s->abort) s->abort = 1; /* wake and stop everyone */

@@ -92,6 +92,21 @@ typedef struct pd_counters {
 void pd_get_counters(pd_session *s, pd_counters *c);
 void pd_close(pd_session *s);
 
+/* GROM_TRACE=<path>: a host timeline of the streamed run (CSV: seconds since
+ * the session opened, thread, event, two arguments), written by pd_close.
+ * The CLI adds its own events (scan start/end per chromosome). */
+enum {
+    PD_EV_DECODE = 1,   /* a: piece, b: 0 start / 1 end */
+    PD_EV_UPLOAD = 2,   /* a: piece, b: 0 start / 1 end */
+    PD_EV_FINAL = 3,    /* a: chromosome */
+    PD_EV_STATS = 4,    /* insert statistics complete */
+    PD_EV_STAGE = 5,    /* a: chromosome, b: 0 wait start / 1 got / 2 made */
+    PD_EV_SCAN = 6,     /* a: chromosome, b: 0 start / 1 end (CLI workers) */
+    PD_EV_HANDED = 7,   /* a: chromosome handed to the scans (CLI) */
+    PD_EV_PHASE = 8,    /* a: CLI phase id, b: 0 start / 1 end */
+};
+void pd_trace(pd_session *s, int ev, int64_t a, int64_t b);
+
 /* a digest of one chromosome's read batch as the scan receives it (every
  * array, CIGAR/base/aux contents per read, the dropped records, and which
  * overlapping reads share a read name); used by the CPU tests to show the

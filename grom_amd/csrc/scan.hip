@@ -978,13 +978,20 @@ void grom_pinned_free(void *p) {
     if (p) (void)hipHostFree(p);
 }
 
-#define GROM_STAGE_EVENTS 256
+#define GROM_STAGE_EVENTS 64
+
+// the arrays of a staged chromosome, all in one device block
+enum { SA_POS, SA_FLAG, SA_MAPQ, SA_MTID, SA_MPOS, SA_ISIZE, SA_LQ, SA_COFF, SA_BOFF, SA_NID, SA_AIDX, SA_CIG, SA_QUAL,
+       SA_SEQ, SA_AUX, SA_DPOS, SA_DLQ, SA_DBEF, SA_REF, SA_N };
 
 struct grom_stage {
     int device = -1;
     hipStream_t st = nullptr;
-    // growable device arrays (slack: kernels read whole 16-byte words)
-    DevBuf pos, flag, mapq, mtid, mpos, isize, lq, coff, cig, boff, seq, qual, nid, aidx, aux, dpos, dlq, dbef, ref;
+    // one device block; array a at off[a] with cap[a] bytes (slack: kernels
+    // read whole 16-byte words past an array's end)
+    char *blk = nullptr;
+    size_t blk_cap = 0;
+    size_t off[SA_N] = {}, cap[SA_N] = {};
     int64_t n = 0, n_cig = 0, n_bases = 0, n_aux = 0, n_drop = 0, ref_len = 0;
     int64_t front = 0;  // reads trimmed from the front of the views (grom_stage_trim)
     int32_t patch_idx = -1;
@@ -994,25 +1001,46 @@ struct grom_stage {
     int64_t tickets = 0;  // appends issued (ticket t uses ev[t % GROM_STAGE_EVENTS])
     int64_t done_upto = 0; // every ticket below this is known complete
     int64_t bytes_h2d = 0;
+    char *a(int k) const { return blk + off[k]; }
 };
 
-// grow a device array keeping its first `keep` bytes (copied on the stage
-// stream, which also orders it before later appends)
-static int stage_grow(grom_stage *s, DevBuf &b, size_t need, size_t keep) {
-    if (b.cap >= need + 64) return GROM_OK;
-    size_t want = need + need / 4 + 4096;
-    void *p = nullptr;
-    if (hipMalloc(&p, want) != hipSuccess) {
-        set_err("grom_stage: hipMalloc(%zu) failed", want);
+// bytes each array holds now (kept when the block grows)
+static void stage_used(const grom_stage *s, size_t u[SA_N]) {
+    u[SA_POS] = 4 * s->n; u[SA_FLAG] = 2 * s->n; u[SA_MAPQ] = s->n; u[SA_MTID] = 4 * s->n; u[SA_MPOS] = 4 * s->n;
+    u[SA_ISIZE] = 4 * s->n; u[SA_LQ] = 4 * s->n; u[SA_COFF] = 4 * (s->n + 1); u[SA_BOFF] = 8 * s->n;
+    u[SA_NID] = 4 * s->n; u[SA_AIDX] = 4 * s->n; u[SA_CIG] = 4 * s->n_cig; u[SA_QUAL] = s->n_bases;
+    u[SA_SEQ] = s->n_bases / 2; u[SA_AUX] = sizeof(grom_aux) * s->n_aux; u[SA_DPOS] = 4 * s->n_drop;
+    u[SA_DLQ] = 4 * s->n_drop; u[SA_DBEF] = 8 * s->n_drop; u[SA_REF] = s->ref_len;
+}
+
+// make every array hold need[a] bytes (+64 slack), keeping keep[a] bytes of
+// its contents: one new block when anything is short (copies on the stage
+// stream), else nothing
+static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t keep[SA_N]) {
+    bool ok = s->blk != nullptr;
+    for (int k = 0; k < SA_N && ok; k++) ok = s->cap[k] >= need[k] + 64;
+    if (ok) return GROM_OK;
+    size_t cap[SA_N], off[SA_N], tot = 0;
+    for (int k = 0; k < SA_N; k++) {
+        cap[k] = s->cap[k] >= need[k] + 64 ? s->cap[k] : need[k] + need[k] / 4 + 4096;
+        off[k] = tot;
+        tot += (cap[k] + 255) & ~(size_t)255;
+    }
+    char *nb = nullptr;
+    if (hipMalloc((void **)&nb, tot) != hipSuccess) {
+        set_err("grom_stage: hipMalloc(%zu) failed", tot);
         return GROM_E_NOMEM;
     }
-    if (b.p) {
-        if (keep) HIPCHK(hipMemcpyAsync(p, b.p, keep, hipMemcpyDeviceToDevice, s->st));
+    if (s->blk) {
+        for (int k = 0; k < SA_N; k++)
+            if (keep[k]) HIPCHK(hipMemcpyAsync(nb + off[k], s->a(k), keep[k], hipMemcpyDeviceToDevice, s->st));
         HIPCHK(hipStreamSynchronize(s->st));
-        (void)hipFree(b.p);
+        (void)hipFree(s->blk);
     }
-    b.p = p;
-    b.cap = want;
+    s->blk = nb;
+    s->blk_cap = tot;
+    memcpy(s->off, off, sizeof(off));
+    memcpy(s->cap, cap, sizeof(cap));
     return GROM_OK;
 }
 
@@ -1042,10 +1070,7 @@ void grom_stage_free(grom_stage *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
-    DevBuf *all[] = {&s->pos, &s->flag, &s->mapq, &s->mtid, &s->mpos, &s->isize, &s->lq, &s->coff, &s->cig, &s->boff,
-                     &s->seq, &s->qual, &s->nid, &s->aidx, &s->aux, &s->dpos, &s->dlq, &s->dbef, &s->ref};
-    for (DevBuf *b : all)
-        if (b->p) (void)hipFree(b->p);
+    if (s->blk) (void)hipFree(s->blk);
     for (int k = 0; k < GROM_STAGE_EVENTS; k++)
         if (s->ev[k]) (void)hipEventDestroy(s->ev[k]);
     if (s->all_ev) (void)hipEventDestroy(s->all_ev);
@@ -1062,23 +1087,14 @@ int grom_stage_begin(grom_stage *s, const grom_stage_sizes *est) {
     s->done_upto = s->tickets;
     s->bytes_h2d = 0;
     if (est) {
-        int rc;
-        const int64_t n = std::max<int64_t>(est->n, 1);
-        if ((rc = stage_grow(s, s->pos, 4 * n, 0)) || (rc = stage_grow(s, s->flag, 2 * n, 0)) ||
-            (rc = stage_grow(s, s->mapq, n, 0)) || (rc = stage_grow(s, s->mtid, 4 * n, 0)) ||
-            (rc = stage_grow(s, s->mpos, 4 * n, 0)) || (rc = stage_grow(s, s->isize, 4 * n, 0)) ||
-            (rc = stage_grow(s, s->lq, 4 * n, 0)) || (rc = stage_grow(s, s->coff, 4 * (n + 1), 0)) ||
-            (rc = stage_grow(s, s->boff, 8 * n, 0)) || (rc = stage_grow(s, s->nid, 4 * n, 0)) ||
-            (rc = stage_grow(s, s->aidx, 4 * n, 0)) ||
-            (rc = stage_grow(s, s->cig, 4 * (size_t)std::max<int64_t>(est->n_cigar_ops, 1), 0)) ||
-            (rc = stage_grow(s, s->qual, (size_t)std::max<int64_t>(est->n_bases, 16), 0)) ||
-            (rc = stage_grow(s, s->seq, (size_t)std::max<int64_t>(est->n_bases, 16) / 2, 0)) ||
-            (rc = stage_grow(s, s->aux, sizeof(grom_aux) * (size_t)std::max<int64_t>(est->n_aux, 1), 0)) ||
-            (rc = stage_grow(s, s->dpos, 4 * (size_t)std::max<int64_t>(est->n_drop, 1), 0)) ||
-            (rc = stage_grow(s, s->dlq, 4 * (size_t)std::max<int64_t>(est->n_drop, 1), 0)) ||
-            (rc = stage_grow(s, s->dbef, 8 * (size_t)std::max<int64_t>(est->n_drop, 1), 0)) ||
-            (rc = stage_grow(s, s->ref, (size_t)std::max<int64_t>(est->ref_len, 16), 0)))
-            return rc;
+        const size_t n = (size_t)std::max<int64_t>(est->n, 1), nd = (size_t)std::max<int64_t>(est->n_drop, 1);
+        const size_t nb = (size_t)std::max<int64_t>(est->n_bases, 16);
+        size_t need[SA_N] = {4 * n, 2 * n, n, 4 * n, 4 * n, 4 * n, 4 * n, 4 * (n + 1), 8 * n, 4 * n, 4 * n,
+                             4 * (size_t)std::max<int64_t>(est->n_cigar_ops, 1), nb, nb / 2,
+                             sizeof(grom_aux) * (size_t)std::max<int64_t>(est->n_aux, 1), 4 * nd, 4 * nd, 8 * nd,
+                             (size_t)std::max<int64_t>(est->ref_len, 16)};
+        const size_t keep[SA_N] = {};
+        return stage_reserve(s, need, keep);
     }
     return GROM_OK;
 }
@@ -1086,9 +1102,14 @@ int grom_stage_begin(grom_stage *s, const grom_stage_sizes *est) {
 int grom_stage_set_ref(grom_stage *s, const char *ref, int64_t len) {
     if (!s || (!ref && len > 0) || len < 0) { set_err("grom_stage_set_ref: bad argument"); return GROM_E_ARG; }
     HIPCHK(hipSetDevice(s->device));
-    int rc = stage_grow(s, s->ref, (size_t)std::max<int64_t>(len, 16), 0);
+    size_t need[SA_N], keep[SA_N];
+    stage_used(s, need);
+    stage_used(s, keep);
+    need[SA_REF] = (size_t)std::max<int64_t>(len, 16);
+    keep[SA_REF] = 0;
+    int rc = stage_reserve(s, need, keep);
     if (rc) return rc;
-    if (len > 0) HIPCHK(hipMemcpyAsync(s->ref.p, ref, (size_t)len, hipMemcpyHostToDevice, s->st));
+    if (len > 0) HIPCHK(hipMemcpyAsync(s->a(SA_REF), ref, (size_t)len, hipMemcpyHostToDevice, s->st));
     s->ref_len = len;
     s->bytes_h2d += len;
     return GROM_OK;
@@ -1108,64 +1129,61 @@ int64_t grom_stage_append(grom_stage *s, const grom_reads *p) {
     }
     if (p->n_bases & 1) { set_err("grom_stage_append: n_bases must be even"); return GROM_E_ARG; }
     HIPCHK(hipSetDevice(s->device));
-    // the event of this ticket's slot must be free (the append 256 back is done)
+    // the event of this ticket's slot must be free (the append GROM_STAGE_EVENTS back is done)
     if (s->tickets >= GROM_STAGE_EVENTS) {
         int rc = stage_ticket_wait(s, s->tickets - GROM_STAGE_EVENTS);
         if (rc) return rc;
     }
-    const int64_t n = s->n + p->n, nc = s->n_cig + p->n_cigar_ops, nb = s->n_bases + p->n_bases;
     const bool has_aux = p->n_aux > 0 && p->aux;
     const bool has_drop = p->n_drop > 0 && p->drop_pos && p->drop_lq && p->drop_before;
-    const int64_t na = s->n_aux + (has_aux ? p->n_aux : 0), nd = s->n_drop + (has_drop ? p->n_drop : 0);
-    int rc;
-    if ((rc = stage_grow(s, s->pos, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->flag, 2 * n, 2 * s->n)) ||
-        (rc = stage_grow(s, s->mapq, n, s->n)) || (rc = stage_grow(s, s->mtid, 4 * n, 4 * s->n)) ||
-        (rc = stage_grow(s, s->mpos, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->isize, 4 * n, 4 * s->n)) ||
-        (rc = stage_grow(s, s->lq, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->coff, 4 * (n + 1), 4 * (s->n + 1))) ||
-        (rc = stage_grow(s, s->boff, 8 * n, 8 * s->n)) || (rc = stage_grow(s, s->nid, 4 * n, 4 * s->n)) ||
-        (rc = stage_grow(s, s->aidx, 4 * n, 4 * s->n)) || (rc = stage_grow(s, s->cig, 4 * nc, 4 * s->n_cig)) ||
-        (rc = stage_grow(s, s->qual, nb, s->n_bases)) || (rc = stage_grow(s, s->seq, nb / 2, s->n_bases / 2)) ||
-        (rc = stage_grow(s, s->aux, sizeof(grom_aux) * na, sizeof(grom_aux) * s->n_aux)) ||
-        (rc = stage_grow(s, s->dpos, 4 * nd, 4 * s->n_drop)) || (rc = stage_grow(s, s->dlq, 4 * nd, 4 * s->n_drop)) ||
-        (rc = stage_grow(s, s->dbef, 8 * nd, 8 * s->n_drop)))
-        return rc;
+    grom_stage after = {};  // the counts after this piece (for the sizes only)
+    after.n = s->n + p->n;
+    after.n_cig = s->n_cig + p->n_cigar_ops;
+    after.n_bases = s->n_bases + p->n_bases;
+    after.n_aux = s->n_aux + (has_aux ? p->n_aux : 0);
+    after.n_drop = s->n_drop + (has_drop ? p->n_drop : 0);
+    after.ref_len = s->ref_len;
+    size_t need[SA_N], keep[SA_N];
+    stage_used(&after, need);
+    stage_used(s, keep);
+    int rc = stage_reserve(s, need, keep);
+    if (rc) return rc;
     int64_t bytes = 0;
-    auto cp = [&](DevBuf &b, int64_t off_bytes, const void *src, int64_t nbytes) -> int {
+    auto cp = [&](int arr, int64_t off_bytes, const void *src, int64_t nbytes) -> int {
         if (nbytes <= 0) return GROM_OK;
-        HIPCHK(hipMemcpyAsync((char *)b.p + off_bytes, src, (size_t)nbytes, hipMemcpyHostToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(s->a(arr) + off_bytes, src, (size_t)nbytes, hipMemcpyHostToDevice, s->st));
         bytes += nbytes;
         return GROM_OK;
     };
     const int64_t k = p->n;
     if (k > 0) {
-        if ((rc = cp(s->pos, 4 * s->n, p->pos, 4 * k)) || (rc = cp(s->flag, 2 * s->n, p->flag, 2 * k)) ||
-            (rc = cp(s->mapq, s->n, p->mapq, k)) || (rc = cp(s->mtid, 4 * s->n, p->mtid, 4 * k)) ||
-            (rc = cp(s->mpos, 4 * s->n, p->mpos, 4 * k)) || (rc = cp(s->isize, 4 * s->n, p->isize, 4 * k)) ||
-            (rc = cp(s->lq, 4 * s->n, p->l_qseq, 4 * k)) || (rc = cp(s->coff, 4 * s->n, p->cigar_off, 4 * (k + 1))) ||
-            (rc = cp(s->boff, 8 * s->n, p->base_off, 8 * k)) ||
-            (rc = cp(s->nid, 4 * s->n, p->name_id, 4 * k)) ||
-            (rc = cp(s->cig, 4 * s->n_cig, p->cigar, 4 * p->n_cigar_ops)) ||
-            (rc = cp(s->qual, s->n_bases, p->qual, p->n_bases)) ||
-            (rc = cp(s->seq, s->n_bases / 2, p->seq, p->n_bases / 2)))
+        if ((rc = cp(SA_POS, 4 * s->n, p->pos, 4 * k)) || (rc = cp(SA_FLAG, 2 * s->n, p->flag, 2 * k)) ||
+            (rc = cp(SA_MAPQ, s->n, p->mapq, k)) || (rc = cp(SA_MTID, 4 * s->n, p->mtid, 4 * k)) ||
+            (rc = cp(SA_MPOS, 4 * s->n, p->mpos, 4 * k)) || (rc = cp(SA_ISIZE, 4 * s->n, p->isize, 4 * k)) ||
+            (rc = cp(SA_LQ, 4 * s->n, p->l_qseq, 4 * k)) || (rc = cp(SA_COFF, 4 * s->n, p->cigar_off, 4 * (k + 1))) ||
+            (rc = cp(SA_BOFF, 8 * s->n, p->base_off, 8 * k)) || (rc = cp(SA_NID, 4 * s->n, p->name_id, 4 * k)) ||
+            (rc = cp(SA_CIG, 4 * s->n_cig, p->cigar, 4 * p->n_cigar_ops)) ||
+            (rc = cp(SA_QUAL, s->n_bases, p->qual, p->n_bases)) ||
+            (rc = cp(SA_SEQ, s->n_bases / 2, p->seq, p->n_bases / 2)))
             return rc;
         if (p->aux_idx) {
-            if ((rc = cp(s->aidx, 4 * s->n, p->aux_idx, 4 * k))) return rc;
+            if ((rc = cp(SA_AIDX, 4 * s->n, p->aux_idx, 4 * k))) return rc;
         } else {
-            HIPCHK(hipMemsetAsync((char *)s->aidx.p + 4 * s->n, 0xff, 4 * (size_t)k, s->st));
+            HIPCHK(hipMemsetAsync(s->a(SA_AIDX) + 4 * s->n, 0xff, 4 * (size_t)k, s->st));
         }
     }
-    if (has_aux && (rc = cp(s->aux, sizeof(grom_aux) * s->n_aux, p->aux, sizeof(grom_aux) * p->n_aux))) return rc;
-    if (has_drop && ((rc = cp(s->dpos, 4 * s->n_drop, p->drop_pos, 4 * p->n_drop)) ||
-                     (rc = cp(s->dlq, 4 * s->n_drop, p->drop_lq, 4 * p->n_drop)) ||
-                     (rc = cp(s->dbef, 8 * s->n_drop, p->drop_before, 8 * p->n_drop))))
+    if (has_aux && (rc = cp(SA_AUX, sizeof(grom_aux) * s->n_aux, p->aux, sizeof(grom_aux) * p->n_aux))) return rc;
+    if (has_drop && ((rc = cp(SA_DPOS, 4 * s->n_drop, p->drop_pos, 4 * p->n_drop)) ||
+                     (rc = cp(SA_DLQ, 4 * s->n_drop, p->drop_lq, 4 * p->n_drop)) ||
+                     (rc = cp(SA_DBEF, 8 * s->n_drop, p->drop_before, 8 * p->n_drop))))
         return rc;
     const int64_t t = s->tickets++;
     HIPCHK(hipEventRecord(s->ev[t % GROM_STAGE_EVENTS], s->st));
-    s->n = n;
-    s->n_cig = nc;
-    s->n_bases = nb;
-    s->n_aux = na;
-    s->n_drop = nd;
+    s->n = after.n;
+    s->n_cig = after.n_cig;
+    s->n_bases = after.n_bases;
+    s->n_aux = after.n_aux;
+    s->n_drop = after.n_drop;
     s->bytes_h2d += bytes;
     return t;
 }
@@ -1194,37 +1212,40 @@ int grom_stage_view(grom_stage *s, const grom_chrom *chrom, grom_chrom *dch, gro
     }
     HIPCHK(hipSetDevice(s->device));
     if (s->n == 0) {  // an empty chromosome still needs cigar_off[0] = 0
-        int rc = stage_grow(s, s->coff, 4, 0);
+        size_t need[SA_N], keep[SA_N];
+        stage_used(s, need);
+        stage_used(s, keep);
+        int rc = stage_reserve(s, need, keep);
         if (rc) return rc;
-        HIPCHK(hipMemsetAsync(s->coff.p, 0, 4, s->st));
+        HIPCHK(hipMemsetAsync(s->a(SA_COFF), 0, 4, s->st));
     }
     *dch = *chrom;
-    dch->ref = (const char *)s->ref.p;
+    dch->ref = (const char *)s->a(SA_REF);
     memset(d, 0, sizeof(*d));
     const int64_t f = s->front;
     d->n = s->n - f;
     d->n_cigar_ops = s->n_cig;
     d->n_bases = s->n_bases;
-    d->pos = (const int32_t *)s->pos.p + f;
-    d->flag = (const uint16_t *)s->flag.p + f;
-    d->mapq = (const uint8_t *)s->mapq.p + f;
-    d->mtid = (const int32_t *)s->mtid.p + f;
-    d->mpos = (const int32_t *)s->mpos.p + f;
-    d->isize = (const int32_t *)s->isize.p + f;
-    d->l_qseq = (const int32_t *)s->lq.p + f;
-    d->cigar_off = (const uint32_t *)s->coff.p + f;  // absolute offsets into cigar
-    d->cigar = (const uint32_t *)s->cig.p;
-    d->base_off = (const int64_t *)s->boff.p + f;    // absolute offsets into seq/qual
-    d->seq = (const uint8_t *)s->seq.p;
-    d->qual = (const uint8_t *)s->qual.p;
-    d->name_id = (const uint32_t *)s->nid.p + f;
+    d->pos = (const int32_t *)s->a(SA_POS) + f;
+    d->flag = (const uint16_t *)s->a(SA_FLAG) + f;
+    d->mapq = (const uint8_t *)s->a(SA_MAPQ) + f;
+    d->mtid = (const int32_t *)s->a(SA_MTID) + f;
+    d->mpos = (const int32_t *)s->a(SA_MPOS) + f;
+    d->isize = (const int32_t *)s->a(SA_ISIZE) + f;
+    d->l_qseq = (const int32_t *)s->a(SA_LQ) + f;
+    d->cigar_off = (const uint32_t *)s->a(SA_COFF) + f;  // absolute offsets into cigar
+    d->cigar = (const uint32_t *)s->a(SA_CIG);
+    d->base_off = (const int64_t *)s->a(SA_BOFF) + f;    // absolute offsets into seq/qual
+    d->seq = (const uint8_t *)s->a(SA_SEQ);
+    d->qual = (const uint8_t *)s->a(SA_QUAL);
+    d->name_id = (const uint32_t *)s->a(SA_NID) + f;
     d->n_aux = s->n_aux;
-    d->aux_idx = s->n_aux > 0 ? (const int32_t *)s->aidx.p + f : nullptr;
-    d->aux = s->n_aux > 0 ? (const grom_aux *)s->aux.p : nullptr;
+    d->aux_idx = s->n_aux > 0 ? (const int32_t *)s->a(SA_AIDX) + f : nullptr;
+    d->aux = s->n_aux > 0 ? (const grom_aux *)s->a(SA_AUX) : nullptr;
     d->n_drop = s->n_drop;
-    d->drop_pos = s->n_drop > 0 ? (const int32_t *)s->dpos.p : nullptr;
-    d->drop_lq = s->n_drop > 0 ? (const int32_t *)s->dlq.p : nullptr;
-    d->drop_before = s->n_drop > 0 ? (const int64_t *)s->dbef.p : nullptr;
+    d->drop_pos = s->n_drop > 0 ? (const int32_t *)s->a(SA_DPOS) : nullptr;
+    d->drop_lq = s->n_drop > 0 ? (const int32_t *)s->a(SA_DLQ) : nullptr;
+    d->drop_before = s->n_drop > 0 ? (const int64_t *)s->a(SA_DBEF) : nullptr;
     return GROM_OK;
 }
 
@@ -1242,14 +1263,18 @@ int grom_stage_patch_aux(grom_stage *s, int64_t read_index, const grom_aux *aux)
         return GROM_E_ARG;
     }
     HIPCHK(hipSetDevice(s->device));
-    int rc = stage_grow(s, s->aux, sizeof(grom_aux) * (s->n_aux + 1), sizeof(grom_aux) * s->n_aux);
+    size_t need[SA_N], keep[SA_N];
+    stage_used(s, keep);
+    stage_used(s, need);
+    need[SA_AUX] += sizeof(grom_aux);
+    int rc = stage_reserve(s, need, keep);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s->st));  // the values below are copied from the stage itself
     s->patch_idx = (int32_t)s->n_aux;
     s->patch_aux = *aux;
-    HIPCHK(hipMemcpyAsync((char *)s->aux.p + sizeof(grom_aux) * s->n_aux, &s->patch_aux, sizeof(grom_aux),
+    HIPCHK(hipMemcpyAsync(s->a(SA_AUX) + sizeof(grom_aux) * s->n_aux, &s->patch_aux, sizeof(grom_aux),
                           hipMemcpyHostToDevice, s->st));
-    HIPCHK(hipMemcpyAsync((char *)s->aidx.p + 4 * read_index, &s->patch_idx, 4, hipMemcpyHostToDevice, s->st));
+    HIPCHK(hipMemcpyAsync(s->a(SA_AIDX) + 4 * read_index, &s->patch_idx, 4, hipMemcpyHostToDevice, s->st));
     HIPCHK(hipStreamSynchronize(s->st));
     s->n_aux++;
     return GROM_OK;

@@ -211,7 +211,38 @@ double grom_prob2(double num_sd) {
     return (1.0 - e) / 2.0;
 }
 
-static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
+static int icmp_slow(const void *a, const void *b) {
+    const int x = *(const int *)a, y = *(const int *)b;
+    return (x > y) - (x < y);
+}
+
+/* ascending sort of ints in O(n): LSD radix, 3 passes of 11 bits over the
+ * value with its sign bit flipped (the order qsort with an int comparator
+ * gives, GROM.c:1276-1310, is the plain numeric order: the result is the
+ * same array) */
+void grom_sort_ints(int *a, int64_t n) {
+    if (n < 2) return;
+    uint32_t *x = (uint32_t *)a, *t = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)n);
+    if (!t) { /* no scratch: an insertion-free fallback keeps the result */
+        qsort(a, (size_t)n, sizeof(int), icmp_slow);
+        return;
+    }
+    for (int64_t i = 0; i < n; i++) x[i] ^= 0x80000000u;
+    uint32_t *src = x, *dst = t;
+    for (int pass = 0; pass < 3; pass++) {
+        const int sh = 11 * pass;
+        int64_t cnt[2049] = {0};
+        for (int64_t i = 0; i < n; i++) cnt[((src[i] >> sh) & 2047) + 1]++;
+        for (int b = 0; b < 2048; b++) cnt[b + 1] += cnt[b];
+        for (int64_t i = 0; i < n; i++) dst[cnt[(src[i] >> sh) & 2047]++] = src[i];
+        uint32_t *sw = src;
+        src = dst;
+        dst = sw;
+    }
+    /* three passes: the sorted data is in t */
+    for (int64_t i = 0; i < n; i++) x[i] = src[i] ^ 0x80000000u;
+    free(t);
+}
 
 int grom_insert_stats(bgzf_reader *r, double prob2, int *lseq, int *imin, int *imax, long *mapped, int min_mapq) {
     const int cap = 10000000; /* insert_sample_size, GROM.c:913 */
@@ -233,7 +264,7 @@ int grom_insert_stats(bgzf_reader *r, double prob2, int *lseq, int *imin, int *i
     }
     bam_free_rec(&b);
     if (n == 0) { free(ins); free(lq); return -1; }
-    qsort(ins, n, sizeof(int), icmp);
+    grom_sort_ints(ins, n);
     int mean = ins[n / 2], lim = mean * 5, end = 0; /* g_insert_max_mult = 5 */
     for (int a = n - 1; a >= 0; a--)
         if (ins[a] <= lim) { end = a; break; }
@@ -242,7 +273,7 @@ int grom_insert_stats(bgzf_reader *r, double prob2, int *lseq, int *imin, int *i
     int lo = (int)(prob2 * end / 2);
     *imin = ins[lo];
     *imax = ins[end - lo < n ? end - lo : n - 1];
-    qsort(lq, n, sizeof(int), icmp);
+    grom_sort_ints(lq, n);
     *lseq = lq[n / 2];
     if (mapped) *mapped = m;
     free(ins);

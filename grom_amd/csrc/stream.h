@@ -56,6 +56,8 @@ int grom_target_name_lc(const char *target, char *out, int cap);
  * after the header; returns the insert mean, fills lseq/min/max. */
 int grom_insert_stats(bgzf_reader *r, double prob2, int *lseq, int *imin, int *imax, long *mapped_reads,
                       int min_mapq);
+/* ascending sort of n ints (O(n) radix; same result as qsort) */
+void grom_sort_ints(int *a, int64_t n);
 /* g_prob2 of calculate_normal_binom_constants for `-s num_sd` */
 double grom_prob2(double num_sd);
 
