@@ -715,6 +715,7 @@ struct WalkIn {
     const double *sd, *wsd;
     int64_t len, start, end, L, min_len;
     unsigned long long *stats;  // GROM_TIMING: walk counters (ab/cd wave calls and rounds), else null
+    unsigned long long *prof;   // GROM_TIMING: slide clock counters (not moved per walk mode), else null
 };
 
 __device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) {
@@ -1078,7 +1079,72 @@ __device__ __forceinline__ double dpp_wave_shr1(double v) {
     return dbl_of((uint32_t)lo, (uint32_t)hi);
 }
 
-__device__ __forceinline__ double wave_chain1(double &tot, double a) {
+// The same chain through LDS, for the walk kernels (one wave per block): the
+// lanes store their addends, then every lane runs the whole chain on the
+// broadcast values -- two dependent f64 adds per step, with no cross-lane move
+// on the dependency path -- and lane 0 stores each step's sum for its lane to
+// pick up.  Bit-identical to the DPP form (same operations, same order).
+struct ChainLds {
+    double2 ad[64];
+    double to[64];
+};
+
+[[maybe_unused]] __device__ __forceinline__ ChainLds &chain_lds() {
+    __shared__ ChainLds c;
+    return c;
+}
+
+// LDS ordering inside the one wave: the wave's LDS instructions execute in
+// order, so only the compiler has to be kept from moving them; unlike
+// __syncthreads this does not wait for the wave's global loads in flight
+// (the next round's inputs)
+[[maybe_unused]] __device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only (vmcnt, expcnt at their maximum)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <bool TWO>
+[[maybe_unused]] __device__ __forceinline__ double lds_chain(double &tot, double a, double b) {
+    ChainLds &c = chain_lds();
+    const int lane = threadIdx.x & 63;
+    c.ad[lane] = make_double2(a, b);
+    wave_lds_sync();
+    double t = tot;
+    // software pipeline: group g+1's addends are read while group g's eight
+    // steps run, so the LDS latency stays off the chain
+    double2 cur[8], nxt[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) cur[k] = c.ad[k];
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+        if (g < 7) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) nxt[k] = c.ad[(g + 1) * 8 + k];
+        }
+        double tt[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            t = t + cur[k].x;
+            if (TWO) t = t + cur[k].y;
+            tt[k] = t;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) c.to[g * 8 + k] = tt[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) cur[k] = nxt[k];
+    }
+    wave_lds_sync();
+    const double r = c.to[lane];
+    wave_lds_sync();  // every lane has read `to` before a next call's lane 0 rewrites it
+    tot = t;
+    return r;
+}
+
+// the register-only form: each round shifts the partial sums one lane up
+[[maybe_unused]] __device__ __forceinline__ double dpp_chain1(double &tot, double a) {
     const double a0 = (threadIdx.x & 63) == 0 ? tot + a : a;
     double t = a0;
 #pragma unroll
@@ -1087,7 +1153,7 @@ __device__ __forceinline__ double wave_chain1(double &tot, double a) {
     return t;
 }
 
-__device__ __forceinline__ double wave_chain2(double &tot, double a, double b) {
+[[maybe_unused]] __device__ __forceinline__ double dpp_chain2(double &tot, double a, double b) {
     const double a0 = (threadIdx.x & 63) == 0 ? tot + a : a;
     double t = a0 + b;
 #pragma unroll
@@ -1095,6 +1161,17 @@ __device__ __forceinline__ double wave_chain2(double &tot, double a, double b) {
     tot = rl_d(t, 63);
     return t;
 }
+
+// measured (tools/chain_bench.hip, and the walk's slide clocks): the DPP form
+// 24.7 cycles per step with every lane's sum in place, the LDS form 20.8 for
+// the chain alone but 31-35 once the sums are handed back to the lanes
+#ifdef GROM_CHAIN_LDS
+__device__ __forceinline__ double wave_chain1(double &tot, double a) { return lds_chain<false>(tot, a, 0.0); }
+__device__ __forceinline__ double wave_chain2(double &tot, double a, double b) { return lds_chain<true>(tot, a, b); }
+#else
+__device__ __forceinline__ double wave_chain1(double &tot, double a) { return dpp_chain1(tot, a); }
+__device__ __forceinline__ double wave_chain2(double &tot, double a, double b) { return dpp_chain2(tot, a, b); }
+#endif
 
 // the round-by-round loops below read the next round's inputs before the
 // current round's serial work: unconditional loads from a clamped index (a
@@ -1290,31 +1367,38 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
     // wave's maximum is taken once, when the slide ends or pauses
     double lmax = 0.0;
     int mqi = s.mqi, mqb = s.mqb;
-    uint32_t nba, nbb;
-    double nza, nzb;
+    // the inputs of one round: lane j holds the leading and trailing bases of step j
+    struct In {
+        uint32_t ba, bb;
+        double za, zb;
+    };
     // unconditional loads from a clamped index (q - L >= 0 here): a load
     // under a branch makes the compiler wait for it at the join, which
     // would put a memory latency into every round
-    auto load = [&](int64_t at) {
+    // (no select on the loaded values here: that would wait for them; the
+    // round masks lanes past the end itself, inl below)
+    auto load = [&](int64_t at, In &o) {
         const int64_t q0 = at + lane;
-        const bool ok = q0 < W.len;
-        const int64_t q = ok ? q0 : W.len - 1;
-        const uint32_t a = W.wb[q], b = W.wb[q - L];
-        const double za = W.sd[q], zb = W.sd[q - L];
-        nba = ok ? a : 0u;
-        nbb = ok ? b : 0u;
-        nza = ok ? za : 0.0;
-        nzb = ok ? zb : 0.0;
+        const int64_t q = q0 < W.len ? q0 : W.len - 1;
+        o.ba = W.wb[q];
+        o.bb = W.wb[q - L];
+        o.za = W.sd[q];
+        o.zb = W.sd[q - L];
     };
-    load(pa);
     bool finished = true;
-    for (;;) {
-        if (pa >= cap) { finished = false; break; }
+    const long long ck_start = W.stats ? clock64() : 0;
+    // GROM_TIMING counters, kept in registers (an atomic per round would put
+    // its round trip into the next round's load wait)
+    long long pc_chain = 0, pc_before = 0, pc_after = 0, pc_rounds = 0;
+    // one round (64 steps) from pa with its inputs; false when the slide
+    // stops or pauses in it
+    auto round = [&](const In &in) -> bool {
+        if (pa >= cap) { finished = false; return false; }
+        const long long ckt = W.stats ? clock64() : 0;
         const int64_t p = pa + lane;
         const bool inl = p < W.len;
-        const uint32_t ba = nba, bb = nbb;
-        const double za = nza, zb = nzb;
-        load(pa + 64);
+        const uint32_t ba = in.ba, bb = in.bb;
+        const double za = in.za, zb = in.zb;
         const int mt = dpp_last_incl(inl ? cdef(bb) : -1, mqb);
         const int ml = dpp_last_incl(inl ? cdef(ba) : -1, mqi);
         const bool qt = inl && !(bb & B_LOW) && (bb & (B_W0 << mt));
@@ -1323,7 +1407,11 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
         const double vl = ql ? sgn * za : 0.0;
         const int64_t cj = cnt + wave_incl_count(ql) - wave_incl_count(qt);
         double t = tot;
+        const long long ck0 = W.stats ? clock64() : 0;
         const double tj = wave_chain2(t, vt, vl);
+        const long long ck1 = W.stats ? clock64() : 0;
+        pc_chain += ck1 - ck0;
+        pc_before += ck0 - ckt;
         const bool good = inl && cj > 0 && wsdL > 0 && ratio_ge_min(tj, cj * wsdL) && LOW_FRAC_OK;
         const double ts = good ? tj / (cj * wsdL) : 0.0;
         // the loop test of step j sees the last good step before it; no
@@ -1343,15 +1431,45 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
         const unsigned long long gm = __ballot(eg);
         if (gm) last_good = ce = pa + (63 - __clzll(gm));
         lmax = (eg && ts > lmax) ? ts : lmax;
-        if (js > 0) {
+        if (js == 64) {
+            tot = t;  // the chain's last sum (== tj of lane 63), without a cross-lane read
+            cnt = rl_i64(cj, 63);
+            mqi = __builtin_amdgcn_readlane(ml, 63);
+            mqb = __builtin_amdgcn_readlane(mt, 63);
+        } else if (js > 0) {
             tot = rl_d(tj, js - 1);
             cnt = rl_i64(cj, js - 1);
             mqi = __builtin_amdgcn_readlane(ml, js - 1);
             mqb = __builtin_amdgcn_readlane(mt, js - 1);
         }
         pa += js;
-        if (W.stats && lane == 0) atomicAdd(W.stats + 2, 1ull);
-        if (js < 64) break;
+        pc_rounds++;
+        if (W.stats) pc_after += clock64() - ck1;
+        return js == 64;
+    };
+    // four rounds of inputs in flight: a round's loads are issued three
+    // rounds before it runs (one round's work does not cover an HBM miss)
+    In b0, b1, b2, b3;
+    load(pa, b0);
+    load(pa + 64, b1);
+    load(pa + 128, b2);
+    load(pa + 192, b3);
+    for (;;) {
+        if (!round(b0)) break;
+        load(pa + 192, b0);
+        if (!round(b1)) break;
+        load(pa + 192, b1);
+        if (!round(b2)) break;
+        load(pa + 192, b2);
+        if (!round(b3)) break;
+        load(pa + 192, b3);
+    }
+    if (W.stats && lane == 0) {
+        atomicAdd(W.prof + 1, (unsigned long long)(clock64() - ck_start));
+        atomicAdd(W.prof + 0, (unsigned long long)pc_chain);
+        atomicAdd(W.prof + 2, (unsigned long long)pc_before);
+        atomicAdd(W.prof + 3, (unsigned long long)pc_after);
+        atomicAdd(W.stats + 2, (unsigned long long)pc_rounds);
     }
     s.pa = pa;
     s.cnt = cnt;
@@ -1768,10 +1886,12 @@ __global__ __launch_bounds__(64) void k_cnv_walk_resume(WalkIn W, const int32_t 
     __syncthreads();  // every lane has read the record before lane 0 may write a new one
     const int64_t pa0 = s.pa;
     const uint64_t t0 = W.stats ? wall_clock64() : 0;
+    const long long k0 = W.stats ? clock64() : 0;
     slide_run<KIND>(W, s, INT64_MAX);
-    if (W.stats && (threadIdx.x & 63) == 0) {  // the longest resumed slide: steps, wall-clock ticks
+    if (W.stats && (threadIdx.x & 63) == 0) {  // the longest resumed slide: steps, wall-clock ticks, clocks
         atomicMax(W.stats + 5, (unsigned long long)(s.pa - pa0));  // slots 20, 21 of the counters
         atomicMax(W.stats + 6, (unsigned long long)(wall_clock64() - t0));
+        atomicMax(W.prof + 4, (unsigned long long)(clock64() - k0));
     }
     int64_t ce;
     double sdv;
@@ -1856,6 +1976,7 @@ struct CandWords {
     uint64_t *pk;        // [kind][word]: nonlow and passing under the last defining base's class
     double *bsum, *bmax, *bmin, *babs;  // per word: sum z (nonlow), max/min running sum, sum |z|
     int8_t *kend;        // per word: the last defining class at its end
+    double *rsn, *rsa;   // per base: running sum of z inside its word, nonlow bases / all bases
     int64_t n_words;
 };
 
@@ -1906,13 +2027,24 @@ __global__ __launch_bounds__(256) void k_cnv_words(const uint16_t *__restrict__ 
             const double t = __shfl_up(ps, d);
             if (lane >= d) ps += t;
         }
-        double mx = ps, mn = ps, ab = fabs(z);
+        double mx = ps, mn = ps, ab = fabs(in ? sd[p] : 0.0);  // |z| of every base: a slack bound for both phases
         for (int o = 32; o > 0; o >>= 1) {
             mx = fmax(mx, __shfl_xor(mx, o));
             mn = fmin(mn, __shfl_xor(mn, o));
             ab += __shfl_xor(ab, o);
         }
         const double tot = __shfl(ps, 63);
+        // the same running sums per base, and over all bases (phase A's first
+        // window adds every base's z)
+        double pa = in ? sd[p] : 0.0;
+        for (int d = 1; d < 64; d <<= 1) {
+            const double t = __shfl_up(pa, d);
+            if (lane >= d) pa += t;
+        }
+        if (in) {
+            C.rsn[p] = ps;
+            C.rsa[p] = pa;
+        }
         if (lane == 0) {
             C.nl[wi] = wnl;
             C.def[wi] = wdef;
@@ -1930,145 +2062,186 @@ __global__ __launch_bounds__(256) void k_cnv_words(const uint16_t *__restrict__ 
     }
 }
 
-constexpr int CLS_B = 8;  // k_cnv_classify: per-base loads issued together
+// First-passage tables for the 2*cnt2 - wl walk (+1 at a passing base, -1 at
+// any other): per byte of pass bits, the lowest prefix level and, for a
+// starting level e in 0..7, the first step that reaches -1 (8: none).
+struct ClsTabs {
+    int8_t minp[256];
+    uint8_t first[256][8];
+};
 
-// One lane per candidate.  nxt[m][p] gets the no-op (p) or phase A's jump;
-// the rest are listed in und[] (and get NXT_UNDECIDED).
+__device__ __forceinline__ void cls_tabs_build(ClsTabs &T) {
+    for (int by = threadIdx.x; by < 256; by += blockDim.x) {
+        int lvl = 0, mn = 8;
+        uint8_t f[8] = {8, 8, 8, 8, 8, 8, 8, 8};
+        for (int j = 0; j < 8; j++) {
+            lvl += ((by >> j) & 1) ? 1 : -1;
+            mn = min(mn, lvl);
+            if (lvl < 0 && f[-lvl - 1] == 8) f[-lvl - 1] = (uint8_t)j;
+        }
+        T.minp[by] = (int8_t)mn;
+        for (int e = 0; e < 8; e++) T.first[by][e] = f[e];
+    }
+}
+
+__device__ __forceinline__ uint64_t low_bits(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
+
+// the first step j in [0, n) at which the walk from level e >= 0 (+1 on a set
+// bit of P, -1 otherwise) reaches -1, or n
+__device__ __forceinline__ int first_passage(uint64_t P, int n, int e, const ClsTabs &T) {
+    // (__popcll is unsigned: keep the arithmetic signed)
+    const int nonpass = n - (int)__popcll(P & low_bits(n));
+    if (nonpass <= e) return n;  // even every non-passing base cannot get there
+    for (int b = 0; b < n; b += 8) {
+        uint32_t by = (uint32_t)(P >> b) & 0xffu;
+        if (n - b < 8) by |= (0xffu << (n - b)) & 0xffu;  // steps past the end count as +1 (never a new low)
+        if (e + T.minp[by] <= -1) return b + T.first[by][e];  // e <= 7 here
+        e += 2 * (int)__popc(by) - 8;
+    }
+    return n;
+}
+
+// One lane per candidate, a 64-base word at a time.  nxt[m][p] gets the
+// no-op (p) or phase A's jump; the rest are listed in und[] (and get
+// NXT_UNDECIDED).  Per word segment the pass bits follow the class rule
+// (the candidate's class until the first class-defining base, the running
+// class from there), the stop is the first passage of 2*cnt2 - wl to -1
+// (exact, from the bits), and the z test is bounded from the word's running
+// sums: only a segment whose bound reaches the threshold tests its passing
+// bases one by one (from the in-word running sums).  The sums here are not
+// the reference's order; any base whose window could pass within a margin
+// far above that difference is UNDECIDED and computed exactly (k_cnv_pre or
+// the walk), so the jumps and no-ops written are exact.
 template <int KIND>
 __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand,
                                                       CandWords C, const double *__restrict__ wsdmin,
                                                       int32_t *__restrict__ nxt, int64_t *__restrict__ und,
                                                       uint32_t *n_und, uint32_t und_cap) {
+    __shared__ ClsTabs T;
+    // GROM_TIMING counters (W.stats + 24): candidates, phase-A jumps, first
+    // window undecided, passing bases tested one by one, segments settled by
+    // the bound, phase-B undecided, no-ops, segments tested base by base
+    __shared__ unsigned long long cst[8];
+    cls_tabs_build(T);
+    if (W.stats && threadIdx.x < 8) cst[threadIdx.x] = 0;
+    __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_cand) return;
-    const int64_t p = cand[i] >> 1;
-    const int m = (int)(cand[i] & 1);
-    const int64_t L = W.L, ML = W.min_len, end = W.end;
-    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
-    const double sgn = KIND == 0 ? 1.0 : -1.0;
-    const double *wsd = W.wsd;
-    auto cls = [](uint32_t b, int c) { return (b & B_HI) ? 0 : (b & B_RTP) ? 1 : c; };
-    int32_t out = (int32_t)p;
-    bool undecided = false;
-    // phase A, exactly (GROM.c:19370-19400)
-    int mqi = m;
-    bool defined = false;
-    int64_t wl = 0, cnt2 = 0;
-    // (loads in batches of CLS_B, clamped to the window, so several are in
-    // flight; the bases are still consumed one at a time, in order)
-    for (int64_t pb = p; pb < p + ML; pb += CLS_B) {
-        uint32_t bb[CLS_B];
-#pragma unroll
-        for (int k = 0; k < CLS_B; k++) bb[k] = W.wb[min(pb + k, p + ML - 1)];
-#pragma unroll
-        for (int k = 0; k < CLS_B; k++) {
-            const int64_t pa = pb + k;
-            if (pa >= p + ML) break;
-            wl += 1;
-            const uint32_t b = bb[k];
-            if (!(b & B_LOW)) {
-                if (cdef(b) >= 0) defined = true;
-                mqi = cls(b, mqi);
-                if (b & (pb0 << mqi)) cnt2 += 1;
-                else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
-            } else if ((2 * cnt2) < wl) { out = (int32_t)pa; goto done; }
-        }
-    }
-    {
-        // the first window's sum is the reference's own (same order)
-        int64_t cnt = ML;
+    unsigned long long c_steps = 0, c_skip = 0, c_wstep = 0;
+    int c_out = -1;  // 0 jump, 1 first-window undecided, 2 B undecided, -1 no-op
+    if (i < n_cand) {
+        const int64_t p = cand[i] >> 1;
+        const int m = (int)(cand[i] & 1);
+        const int64_t L = W.L, ML = W.min_len, end = W.end, nw = C.n_words;
+        const double sgn = KIND == 0 ? 1.0 : -1.0;
+        const uint64_t *pmw = C.pm + (KIND * 2 + m) * nw, *pkw = C.pk + KIND * nw;
+        bool defined = false;
+        // the pass bits of a segment (mask M of word w) under the class rule
+        auto pass_bits = [&](int64_t w, uint64_t M) -> uint64_t {
+            if (defined) return pkw[w] & M;
+            const uint64_t dw = C.def[w] & M;
+            if (!dw) return pmw[w] & M;
+            const uint64_t below = (dw & (0 - dw)) - 1;
+            defined = true;
+            return ((pmw[w] & below) | (pkw[w] & ~below)) & M;
+        };
+        int32_t out = (int32_t)p;
+        bool undecided = false;
+        int E = 0;  // 2*cnt2 - wl
+        int64_t wl = 0, cnt = 0;
         double R = 0.0, A = 0.0;
-        for (int64_t ab = p; ab < p + ML; ab += CLS_B) {
-            uint32_t bb[CLS_B];
-            double zz[CLS_B];
-#pragma unroll
-            for (int k = 0; k < CLS_B; k++) {
-                const int64_t a = min(ab + k, p + ML - 1);
-                bb[k] = W.wb[a];
-                zz[k] = W.sd[a];
+        // phase A: the first ML bases (GROM.c:19370-19400)
+        for (int64_t lo = p; lo < p + ML;) {
+            const int64_t w = lo >> 6, hi = min(p + ML, (w + 1) << 6);
+            const int s0 = (int)(lo & 63), n = (int)(hi - lo);
+            const uint64_t M = low_bits(n) << s0;
+            const uint64_t P = pass_bits(w, M);
+            const int j = first_passage(P >> s0, n, E, T);
+            if (j < n) {  // the stop: the walk jumps here
+                out = (int32_t)(lo + j);
+                c_out = 0;
+                goto done;
             }
-#pragma unroll
-            for (int k = 0; k < CLS_B; k++) {
-                if (ab + k >= p + ML) break;
-                cnt -= (bb[k] & B_LOW);
-                const double z = zz[k];
-                if (KIND == 0) R += z; else R -= z;
-                A += fabs(z);
+            E += 2 * (int)__popcll(P) - n;
+            wl += n;
+            cnt += __popcll(C.nl[w] & M);
+            R += sgn * (C.rsa[hi - 1] - (s0 ? C.rsa[lo - 1] : 0.0));
+            A += C.babs[w];
+            lo = hi;
+        }
+        // the first window's z test (every base's z, nonlow count)
+        if (cnt > 0 && W.wsd[ML] > 0) {
+            const double d = (double)cnt * W.wsd[ML];
+            if (!(R + 1e-9 * (A + fabs(R)) + 1e-300 < 3.0 * d * (1.0 - 1e-15))) {
+                undecided = true;
+                c_out = 1;
+                goto done;
             }
         }
-        if (cnt > 0 && wsd[ML] > 0 && ratio_ge_min(R, cnt * wsd[ML])) { undecided = true; goto done; }
-        // phase B (GROM.c:19405-19470)
-        int64_t x = p + ML;
-        const int64_t xend = p + L;
-        while (x < xend) {
-            if ((x & 63) == 0 && x + 64 <= xend && x + 64 <= end && 2 * cnt2 - wl >= 64) {
-                const int64_t wi = x >> 6;
-                const uint64_t dw = C.def[wi];
-                if (defined || dw == 0) {
-                    const uint64_t pw = defined ? C.pk[KIND * C.n_words + wi] : C.pm[(KIND * 2 + mqi) * C.n_words + wi];
-                    bool skip = pw == 0;
-                    if (!skip) {
-                        const double ub = R + (KIND == 0 ? C.bmax[wi] : -C.bmin[wi]);
-                        const double slack = 1e-9 * (A + C.babs[wi] + fabs(ub)) + 1e-300;
-                        const double dlo = (double)(cnt + 1) * wsdmin[wl + 1];
-                        skip = dlo > 0 && ub + slack < 3.0 * dlo * (1.0 - 1e-15);
-                    }
-                    if (skip) {
-                        if (defined) mqi = C.kend[wi];
-                        cnt += __popcll(C.nl[wi]);
-                        cnt2 += __popcll(pw);
-                        R += sgn * C.bsum[wi];
-                        A += C.babs[wi];
-                        wl += 64;
-                        x += 64;
-                        continue;
-                    }
-                }
-            }
-            // step by step to the next word boundary
-            const int64_t xb = min(xend, (x | 63) + 1);
-            const int64_t xl = max<int64_t>(0, min(xb, end) - 1);  // last base a load may touch
-            while (x < xb) {
-                uint32_t bb[CLS_B];  // the next CLS_B bases' words and z, loaded together
-                double zz[CLS_B];
-#pragma unroll
-                for (int t = 0; t < CLS_B; t++) {
-                    const int64_t xi = min(x + t, xl);
-                    bb[t] = W.wb[xi];
-                    zz[t] = W.sd[xi];
-                }
-#pragma unroll
-                for (int k = 0; k < CLS_B; k++, x++) {
-                    if (x >= xb) break;
-                    wl += 1;
-                    if (x >= end) goto done;  // a stop: no-op
-                    const uint32_t b = bb[k];
-                    if (!(b & B_LOW)) {
-                        if (cdef(b) >= 0) defined = true;
-                        mqi = cls(b, mqi);
-                        const double z = zz[k];
-                        R += sgn * z;
-                        A += fabs(z);
-                        cnt += 1;
-                        if (b & (pb0 << mqi)) {
-                            cnt2 += 1;
-                            if (wsd[wl] > 0) {
-                                const double d = cnt * wsd[wl];
-                                if (!(R + 1e-9 * (A + fabs(R)) < 3.0 * d * (1.0 - 1e-15))) { undecided = true; goto done; }
+        // phase B: extension to L (GROM.c:19405-19470); reaching `end` stops it
+        {
+            const int64_t xlim = min(p + L, end);
+            for (int64_t lo = p + ML; lo < xlim;) {
+                const int64_t w = lo >> 6, hi = min(xlim, (w + 1) << 6);
+                const int s0 = (int)(lo & 63), n = (int)(hi - lo);
+                const uint64_t M = low_bits(n) << s0;
+                const uint64_t P = pass_bits(w, M);
+                const int j = first_passage(P >> s0, n, E, T);
+                const uint64_t Pr = (P >> s0) & low_bits(j);  // passing bases before the stop
+                const double base = s0 ? C.rsn[lo - 1] : 0.0;
+                if (Pr) {
+                    const double ub = KIND == 0 ? R + (C.bmax[w] - base) : R - (C.bmin[w] - base);
+                    const double dlo = (double)(cnt + 1) * wsdmin[wl + 1];
+                    const double slack = 1e-9 * (A + C.babs[w] + fabs(ub)) + 1e-300;
+                    if (dlo > 0 && ub + slack < 3.0 * dlo * (1.0 - 1e-15)) {
+                        c_skip++;
+                    } else {
+                        c_wstep++;
+                        const uint64_t nlr = C.nl[w] >> s0;
+                        for (uint64_t q = Pr; q; q &= q - 1) {
+                            const int k = __ffsll((long long)q) - 1;
+                            const double Rk = R + sgn * (C.rsn[lo + k] - base);
+                            const int64_t ck = cnt + __popcll(nlr & low_bits(k + 1));
+                            const double ws = W.wsd[wl + k + 1];
+                            c_steps++;
+                            if (ws > 0) {
+                                const double d = (double)ck * ws;
+                                if (!(Rk + 1e-9 * (A + C.babs[w] + fabs(Rk)) + 1e-300 < 3.0 * d * (1.0 - 1e-15))) {
+                                    undecided = true;
+                                    c_out = 2;
+                                    goto done;
+                                }
                             }
-                        } else if ((2 * cnt2) < wl) goto done;
-                    } else if ((2 * cnt2) < wl) goto done;
+                        }
+                    }
                 }
+                if (j < n) goto done;  // phase B stops without a call: no-op
+                E += 2 * (int)__popcll(P) - n;
+                wl += n;
+                cnt += __popcll(C.nl[w] & M);
+                R += sgn * (C.rsn[hi - 1] - base);
+                A += C.babs[w];
+                lo = hi;
             }
         }
+    done:
+        if (undecided) {
+            out = NXT_UNDECIDED;
+            const uint32_t k = atomicAdd(n_und, 1u);
+            if (k < und_cap) und[k] = cand[i];
+        }
+        nxt[m * W.len + p] = out;
     }
-done:
-    if (undecided) {
-        out = NXT_UNDECIDED;
-        const uint32_t k = atomicAdd(n_und, 1u);
-        if (k < und_cap) und[k] = cand[i];
+    if (W.stats) {
+        if (i < n_cand) {
+            atomicAdd(&cst[0], 1ull);
+            atomicAdd(&cst[c_out < 0 ? 6 : c_out == 0 ? 1 : c_out == 1 ? 2 : 5], 1ull);
+            atomicAdd(&cst[3], c_steps);
+            atomicAdd(&cst[4], c_skip);
+            atomicAdd(&cst[7], c_wstep);
+        }
+        __syncthreads();
+        if (threadIdx.x < 8) atomicAdd(W.stats + 24 + threadIdx.x, cst[threadIdx.x]);
     }
-    nxt[m * W.len + p] = out;
 }
 
 // a call is on the true walk iff its start was visited in its class
@@ -2889,7 +3062,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CandWords CW{};
         {
             const int64_t n_words = (len + 63) / 64 + 1, n_seg = (n_words + CW_SEG - 1) / CW_SEG;
-            const size_t wbytes = (size_t)n_words * (8 * 8 + 4 * 8 + 1) + 256;
+            const size_t wbytes = (size_t)n_words * (8 * 8 + 4 * 8 + 1) + 256 + 2 * 8 * (size_t)n_words * 64;
             if ((rc = grow(S->cwords, wbytes, err, errlen)) || (rc = grow(S->cw_seg, (size_t)n_seg, err, errlen)) ||
                 (rc = grow(S->cw_carry, (size_t)n_seg, err, errlen)) || (rc = grow(S->wsdmin, 8 * (size_t)(L + 2), err, errlen)))
                 return rc;
@@ -2904,7 +3077,9 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             CW.bmax = dd + n_words;
             CW.bmin = dd + 2 * n_words;
             CW.babs = dd + 3 * n_words;
-            CW.kend = (int8_t *)(dd + 4 * n_words);
+            CW.rsn = dd + 4 * n_words;
+            CW.rsa = CW.rsn + n_words * 64;
+            CW.kend = (int8_t *)(CW.rsa + n_words * 64);
             const unsigned gs = (unsigned)((n_seg * 64 + 255) / 256);
             hipLaunchKernelGGL(k_cnv_cls_seg, dim3(gs), dim3(256), 0, st, (const uint16_t *)S->wbits.p, len, n_seg,
                                (int8_t *)S->cw_seg.p);
@@ -2936,13 +3111,14 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             KindBufs &K = S->kb[kind];
             hipStream_t st = K.st;
             int rc = GROM_OK;
-            if ((rc = grow(K.cnt, 256, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
+            if ((rc = grow(K.cnt, 512, err, errlen)) || (rc = grow(K.vis, (size_t)len, err, errlen))) return rc;
             // n_calls, n_pre, n_cand, capped, n_und; walk counters from byte 64
             uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;
             WalkIn WK = WI;
             WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 64) : nullptr;
+            WK.prof = tmg ? WK.stats + 40 : nullptr;  // slots 40..44 (the mode offsets reach slot 21)
             CK(hipStreamWaitEvent(st, S->walk_in, 0));
-            if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 176, st));
+            if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 448, st));
             bool done = false;
             for (int attempt = 0; attempt < 8 && !done; attempt++) {
                 if ((rc = grow(K.nxt, 8 * (size_t)len, err, errlen)) ||
@@ -3009,8 +3185,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         // first): the walk decides them
                         npc = (int64_t)nu * L <= budget ? nu : 0;
                         pcand = und;
-                        if (tmg) fprintf(stderr, "cnv classify %s: %u candidates, %u undecided (%s)\n", kind == 0 ? "DEL" : "DUP",
-                                         ncand, nu, npc ? "precomputed" : "left to the walk");
+                        if (tmg) {
+                            unsigned long long cs8[8];
+                            (void)hipMemcpy(cs8, WK.stats + 24, sizeof(cs8), hipMemcpyDeviceToHost);
+                            fprintf(stderr, "cnv classify %s: %u candidates, %u undecided (%s); jumps %llu, first-window "
+                                    "undecided %llu, B undecided %llu, no-ops %llu, bases tested %llu, segments settled by the bound %llu, "
+                                    "segments tested %llu\n", kind == 0 ? "DEL" : "DUP", ncand, nu,
+                                    npc ? "precomputed" : "left to the walk", cs8[1], cs8[2], cs8[5], cs8[6], cs8[3],
+                                    cs8[4], cs8[7]);
+                        }
                     }
                     if (npc > pre_cap) {  // every precomputed candidate may start a call: no re-run
                         pre_cap = npc;
@@ -3128,6 +3311,11 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                                 wsa[5 * mo + 4], wsa[5 * mo], wsa[5 * mo + 1], wsa[5 * mo + 2], wsa[5 * mo + 3]);
                     fprintf(stderr, "cnv walk %s: longest resumed slide %llu steps in %llu wall-clock ticks\n",
                             kind == 0 ? "DEL" : "DUP", wsa[20], wsa[21]);
+                    unsigned long long ck2[5];
+                    (void)hipMemcpy(ck2, WK.stats + 40, sizeof(ck2), hipMemcpyDeviceToHost);
+                    fprintf(stderr, "cnv walk %s: slide cycles %llu: before the sum chain %llu, chain %llu, after %llu; "
+                            "longest resumed slide %llu clocks\n",
+                            kind == 0 ? "DEL" : "DUP", ck2[1], ck2[2], ck2[0], ck2[3], ck2[4]);
                     unsigned long long ws[5];
                     for (int q = 0; q < 5; q++) ws[q] = wsa[q] + wsa[5 + q] + wsa[10 + q] + wsa[15 + q];
                     fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired, %u candidates, %u call starts (%u left to the walk); "
