@@ -72,3 +72,34 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle variant
+
+# host code under sanitizers (tests/test_sanitize.py): SAN=asan (AddressSanitizer
+# + UBSan) or SAN=tsan (ThreadSanitizer).  The device objects are linked
+# uninstrumented and never called (tools/san_driver.c runs host paths only).
+SAN ?= asan
+SANDIR = build/san-$(SAN)
+ifeq ($(SAN),tsan)
+SANFLAGS = -fsanitize=thread
+else
+SANFLAGS = -fsanitize=address,undefined -fno-sanitize-recover=undefined
+endif
+SAN_OBJ = $(patsubst grom_amd/csrc/%.c,$(SANDIR)/%.o,$(HOST_SRC)) $(SANDIR)/snvfmt.o
+
+$(SANDIR)/%.o: grom_amd/csrc/%.c $(HDRS)
+	@mkdir -p $(SANDIR)
+	$(CC) -O1 -g -fno-omit-frame-pointer -Wall -Wno-alloc-size-larger-than -fPIC $(SANFLAGS) -c $< -o $@
+
+$(SANDIR)/snvfmt.o: grom_amd/csrc/snvfmt.cpp grom_amd/csrc/snvfmt.h $(HDRS)
+	@mkdir -p $(SANDIR)
+	$(CXX) -O1 -g -fno-omit-frame-pointer -Wall -fPIC -std=c++17 -pthread $(SANFLAGS) -c $< -o $@
+
+$(SANDIR)/san_driver: tools/san_driver.c $(SAN_OBJ) build/svcall.o $(DEV_OBJ)
+	$(CXX) -O1 -g -fno-omit-frame-pointer $(SANFLAGS) -x c tools/san_driver.c -x none $(SAN_OBJ) build/svcall.o $(DEV_OBJ) \
+	    -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -lz -lm -ldl -lpthread -o $@
+
+$(SANDIR)/grom_synth: tools/grom_synth.c $(SANDIR)/synth.o $(SANDIR)/bamio.o
+	$(CC) -O1 -g -fno-omit-frame-pointer $(SANFLAGS) -o $@ $^ -lz -lm -ldl -lpthread
+
+sanitize: $(SANDIR)/san_driver $(SANDIR)/grom_synth
+
+.PHONY: sanitize

@@ -290,8 +290,22 @@ static ldc_alloc_fn ldc_alloc;
 static ldc_comp_fn ldc_comp;
 static ldc_free_fn ldc_free;
 static pthread_once_t ldc_once = PTHREAD_ONCE_INIT;
+/* one compressor per thread, freed when the thread exits */
+typedef struct {
+    void *cmp;
+    int level;
+} ldc_tls;
+static pthread_key_t ldc_key;
+static int ldc_key_ok;
+static void ldc_tls_free(void *p) {
+    ldc_tls *t = (ldc_tls *)p;
+    if (t && t->cmp) ldc_free(t->cmp);
+    free(t);
+}
 static void ldc_init(void) {
     if (getenv("GROM_NO_LIBDEFLATE")) return;
+    ldc_key_ok = pthread_key_create(&ldc_key, ldc_tls_free) == 0;
+    if (!ldc_key_ok) return;
     void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
     if (!h) return;
     ldc_alloc_fn a = (ldc_alloc_fn)dlsym(h, "libdeflate_alloc_compressor");
@@ -305,15 +319,21 @@ int bgzf_block_compress(const unsigned char *in, int len, unsigned char *out, in
     int clen = -1;
     const int room = BGZF_MAX_BLOCK - 18 - 8;
     if (ldc_alloc) {
-        static __thread void *cmp = NULL;
-        static __thread int cmp_level = -1;
-        if (!cmp || cmp_level != level) {
-            if (cmp) ldc_free(cmp);
-            cmp = ldc_alloc(level < 1 ? 1 : level);
-            cmp_level = level;
+        ldc_tls *t = (ldc_tls *)pthread_getspecific(ldc_key);
+        if (!t && (t = (ldc_tls *)calloc(1, sizeof(ldc_tls))) != NULL) {
+            t->level = -1;
+            if (pthread_setspecific(ldc_key, t) != 0) {
+                free(t);
+                t = NULL;
+            }
         }
-        if (cmp) {
-            const size_t k = ldc_comp(cmp, in, (size_t)len, out + 18, (size_t)room);
+        if (t && (!t->cmp || t->level != level)) {
+            if (t->cmp) ldc_free(t->cmp);
+            t->cmp = ldc_alloc(level < 1 ? 1 : level);
+            t->level = level;
+        }
+        if (t && t->cmp) {
+            const size_t k = ldc_comp(t->cmp, in, (size_t)len, out + 18, (size_t)room);
             if (k > 0) clen = (int)k;
         }
     }
@@ -596,10 +616,10 @@ int bgzf_seek(bgzf_reader *r, int64_t voff) {
 int32_t bam_end_pos(const bam_rec *b) {
     int32_t len = 0;
     if (!(b->flag & 4)) {
-        const uint32_t *c = bam_cigar(b);
         for (int i = 0; i < b->n_cigar; i++) {
-            const int op = c[i] & 15;
-            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) len += (int32_t)(c[i] >> 4);
+            const uint32_t c = bam_cigar_op(b, i);
+            const int op = c & 15;
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) len += (int32_t)(c >> 4);
         }
     }
     return b->pos + (len > 0 ? len : 1);

@@ -13,6 +13,7 @@
 #define GROM_AMD_BAMIO_H
 
 #include <stdint.h>
+#include <string.h>
 #include <stdio.h>
 #include <stddef.h>
 
@@ -84,7 +85,14 @@ typedef struct bam_rec {
 } bam_rec;
 
 static inline char *bam_qname(const bam_rec *b) { return (char *)b->data; }
-static inline uint32_t *bam_cigar(const bam_rec *b) { return (uint32_t *)(b->data + b->l_qname); }
+/* the CIGAR starts right after the read name, at any byte offset: read its
+ * operations through bam_cigar_op (an unaligned uint32_t load is undefined) */
+static inline const uint8_t *bam_cigar(const bam_rec *b) { return b->data + b->l_qname; }
+static inline uint32_t bam_cigar_op(const bam_rec *b, int i) {
+    uint32_t v;
+    memcpy(&v, b->data + b->l_qname + 4 * (size_t)i, 4);
+    return v;
+}
 static inline uint8_t *bam_seq(const bam_rec *b) { return b->data + b->l_qname + 4 * b->n_cigar; }
 static inline uint8_t *bam_qual(const bam_rec *b) { return bam_seq(b) + ((b->l_qseq + 1) >> 1); }
 static inline uint8_t *bam_aux(const bam_rec *b) { return bam_qual(b) + b->l_qseq; }

@@ -954,8 +954,9 @@ static int run_streamed(cli_state *S) {
     memset(&F, 0, sizeof(F));
     pthread_t fthr;
     int fasta_started = 0;
+    double t_ctx = 0.0;
     if (setup_workers(S)) { status = 1; goto done; }
-    const double t_ctx = clock_gettime_s();
+    t_ctx = clock_gettime_s();
     vcf = fopen(S->out_name, "w");
     if (!vcf) { printf("Error opening file %s\n", S->out_name); status = 1; goto done; }
     if (P->vcf == 1) header(vcf, S->fasta_name, 0);

@@ -499,14 +499,14 @@ void grom_batch_add(grom_batch *b, const bam_rec *r, int32_t index_start) {
     b->isize[i] = r->isize;
     b->l_qseq[i] = r->l_qseq;
     if (i == 0) b->cigar_off[0] = 0;
-    const uint32_t *cg = bam_cigar(r);
     if (b->n_cig + r->n_cigar > b->cap_cig) {
         int64_t nc = b->cap_cig ? b->cap_cig : 4096;
         while (nc < b->n_cig + r->n_cigar) nc *= 2;
         b->cigar = realloc(b->cigar, sizeof(uint32_t) * nc);
         b->cap_cig = nc;
     }
-    memcpy(b->cigar + b->n_cig, cg, sizeof(uint32_t) * r->n_cigar);
+    memcpy(b->cigar + b->n_cig, bam_cigar(r), sizeof(uint32_t) * r->n_cigar);
+    const uint32_t *cg = b->cigar + b->n_cig;  /* the aligned copy */
     int32_t span = 0;
     for (int k = 0; k < r->n_cigar; k++) {
         int op = cg[k] & 0xf;

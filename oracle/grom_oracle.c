@@ -655,8 +655,10 @@ static void ingest(scan_t *s, cur_t *c) {
         }
     }
     if (add_to_list != 1) return;
-    const uint32_t *cig = bam_cigar(b);
     int n_cigar = b->n_cigar;
+    /* an aligned copy of the CIGAR (it sits at any byte offset in the record) */
+    uint32_t cig_buf[512], *cig = n_cigar <= 512 ? cig_buf : (uint32_t *)malloc(4 * (size_t)n_cigar);
+    memcpy(cig, bam_cigar(b), 4 * (size_t)n_cigar);
 
     /* whole-chromosome read depth, GROM.c:6605-6671 */
     long caf_pos = c->pos;
@@ -682,6 +684,7 @@ static void ingest(scan_t *s, cur_t *c) {
     int c_type[1000];
     long c_len[1000];
     for (int a = 0; a < cigar_len; a++) { c_type[a] = cig[a] & 0xf; c_len[a] = cig[a] >> 4; }
+    if (cig != cig_buf) free(cig);
 
     const char *rname = bam_qname(b);
     int name_storable = strlen(rname) < (size_t)g_read_name_len && rname[0] != 0;
