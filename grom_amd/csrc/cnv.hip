@@ -1167,10 +1167,10 @@ template <bool TWO>
 // the chain alone but 31-35 once the sums are handed back to the lanes
 #ifdef GROM_CHAIN_LDS
 __device__ __forceinline__ double wave_chain1(double &tot, double a) { return lds_chain<false>(tot, a, 0.0); }
-__device__ __forceinline__ double wave_chain2(double &tot, double a, double b) { return lds_chain<true>(tot, a, b); }
+[[maybe_unused]] __device__ __forceinline__ double wave_chain2(double &tot, double a, double b) { return lds_chain<true>(tot, a, b); }
 #else
 __device__ __forceinline__ double wave_chain1(double &tot, double a) { return dpp_chain1(tot, a); }
-__device__ __forceinline__ double wave_chain2(double &tot, double a, double b) { return dpp_chain2(tot, a, b); }
+[[maybe_unused]] __device__ __forceinline__ double wave_chain2(double &tot, double a, double b) { return dpp_chain2(tot, a, b); }
 #endif
 
 // the round-by-round loops below read the next round's inputs before the
@@ -1355,7 +1355,7 @@ __device__ SlideState slide_begin(const WalkIn &W, int64_t pos, const PreAB &r, 
 // load latency would otherwise add up).  Stops before a round that would
 // start at or past `cap` and returns false (s then resumes exactly there).
 template <int KIND>
-__device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
+[[maybe_unused]] __device__ bool slide_run64(const WalkIn &W, SlideState &s, int64_t cap) {
     if (!s.sliding) return true;
     const int lane = threadIdx.x & 63;
     const int64_t L = W.L;
@@ -1469,6 +1469,307 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
         atomicAdd(W.prof + 0, (unsigned long long)pc_chain);
         atomicAdd(W.prof + 2, (unsigned long long)pc_before);
         atomicAdd(W.prof + 3, (unsigned long long)pc_after);
+        atomicAdd(W.stats + 2, (unsigned long long)pc_rounds);
+    }
+    s.pa = pa;
+    s.cnt = cnt;
+    s.last_good = last_good;
+    s.ce = ce;
+    s.tot = tot;
+    const double mx = dpp_max_pos(lmax);  // ratios are >= 3 > 0; lanes without one hold 0
+    if (mx > s.stdevs) s.stdevs = mx;
+    s.mqi = mqi;
+    s.mqb = mqb;
+    s.sliding = finished ? 0 : 1;
+    return finished;
+}
+
+// ---- the slide, 256 steps per round (4 per lane) ----
+//
+// The window sum `tot` is one chain of f64 adds in the reference's order.
+// Instead of running it across the lanes (one DPP hop per step, ~25 cycles),
+// every lane runs its own four steps from a GUESSED start value, and the
+// guesses are then checked: lane l's start must equal lane l-1's end, bit for
+// bit.  Lane 0 starts from the exact `tot`, so if every check holds, every
+// start -- and so every step's sum -- is the reference's exact value (by
+// induction over the lanes); the first lane that fails restarts the guessing
+// from the exact end of the lane before it.
+//
+// The guess: while a sum stays in one binade [2^e, 2^(e+1)), every value is an
+// integer multiple of u = 2^(e-52), and fl(t + x) = t + RN(x / u) u with the
+// rounding independent of t except for exact ties.  So per lane the integer
+// increment D = sum of RN(x / u) over its eight adds is computed in parallel,
+// a prefix sum over the lanes gives each lane's start, and only a tie or a
+// binade change can make a guess wrong -- which the check catches.
+__device__ __forceinline__ double dpp_sum_step(double v, int ctl_sel) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
+    switch (ctl_sel) {  // (constant after unrolling)
+    case 0: lo = __builtin_amdgcn_update_dpp(0, lo, 0x111, 0xf, 0xf, true); hi = __builtin_amdgcn_update_dpp(0, hi, 0x111, 0xf, 0xf, true); break;
+    case 1: lo = __builtin_amdgcn_update_dpp(0, lo, 0x112, 0xf, 0xf, true); hi = __builtin_amdgcn_update_dpp(0, hi, 0x112, 0xf, 0xf, true); break;
+    case 2: lo = __builtin_amdgcn_update_dpp(0, lo, 0x114, 0xf, 0xf, true); hi = __builtin_amdgcn_update_dpp(0, hi, 0x114, 0xf, 0xf, true); break;
+    case 3: lo = __builtin_amdgcn_update_dpp(0, lo, 0x118, 0xf, 0xf, true); hi = __builtin_amdgcn_update_dpp(0, hi, 0x118, 0xf, 0xf, true); break;
+    case 4: lo = __builtin_amdgcn_update_dpp(0, lo, 0x142, 0xa, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x142, 0xa, 0xf, false); break;
+    default: lo = __builtin_amdgcn_update_dpp(0, lo, 0x143, 0xc, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x143, 0xc, 0xf, false); break;
+    }
+    return dbl_of((uint32_t)lo, (uint32_t)hi);
+}
+
+// inclusive prefix sum over the lanes (exact for integer-valued doubles
+// whose partial sums stay below 2^53, which is all the guess needs)
+__device__ __forceinline__ double wave_incl_sum(double v) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) v += dpp_sum_step(v, k);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t dbits(double v) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    return u;
+}
+
+// the class at the start of each lane: the last class-defining step (e: the
+// lane's own last, -1 none) among the lanes below, else the carry c
+__device__ __forceinline__ int lane_last_excl(int e, int c) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long d = __ballot(e >= 0) & ((1ull << lane) - 1);
+    const unsigned long long c1 = __ballot(e == 1);
+    return d ? (int)((c1 >> (63 - __clzll(d))) & 1ull) : c;
+}
+
+// exclusive prefix over the lanes of small counts n in [0, 7], and the total
+__device__ __forceinline__ int excl_small(int n, int &total) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
+    const unsigned long long below = (1ull << lane) - 1;
+    total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    return (int)(__popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below));
+}
+
+// the chain over the round: tj[i] = the sum after step 4*lane + i, exact
+// (see above); `tot` is the sum before the round
+__device__ __forceinline__ void chain_round4(double tot, const double (&vt)[4], const double (&vl)[4], double (&tj)[4],
+                                             unsigned long long &n_fix) {
+    const int lane = threadIdx.x & 63;
+    int b = 0;         // lanes below b are checked
+    double T = tot;    // the exact start of lane b
+    double tin = 0.0;  // this lane's start
+    bool ok = false;
+    for (int it = 0; it < 4; it++) {
+        int E;
+        (void)frexp(T, &E);  // |T| in [2^(E-1), 2^E)
+        const double inv_u = ldexp(1.0, 53 - E), u = ldexp(1.0, E - 53);
+        const double sT = T < 0.0 ? -1.0 : 1.0, scale = sT * inv_u;
+        double D = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const double ya = vt[i] * scale, qa = floor(ya);
+            const double yb = vl[i] * scale, qb = floor(yb);
+            D += (qa + (ya - qa > 0.5 ? 1.0 : 0.0)) + (qb + (yb - qb > 0.5 ? 1.0 : 0.0));
+        }
+        if (lane < b) D = 0.0;
+        const double ex = wave_incl_sum(D) - D;
+        if (lane >= b) tin = lane == b ? T : sT * ((fabs(T) * inv_u + ex) * u);
+        double t = tin;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            t = t + vt[i];
+            t = t + vl[i];
+            tj[i] = t;
+        }
+        const double prev = dpp_wave_shr1(t);
+        const unsigned long long bm = __ballot(lane > b && dbits(tin) != dbits(prev));
+        if (!bm) {
+            ok = true;
+            break;
+        }
+        n_fix++;
+        b = __ffsll((long long)bm) - 1;
+        T = rl_d(t, b - 1);
+    }
+    if (!ok) {  // lane by lane from lane b (rare: repeated ties or binade changes)
+        for (int l = b; l < 64; l++) {
+            if (lane == l) {
+                double t = T;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    t = t + vt[i];
+                    t = t + vl[i];
+                    tj[i] = t;
+                }
+            }
+            T = rl_d(tj[3], l);
+        }
+    }
+}
+
+__device__ __forceinline__ double pick4(const double (&v)[4], int k) {
+    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+}
+__device__ __forceinline__ int64_t pick4(const int64_t (&v)[4], int k) {
+    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+}
+__device__ __forceinline__ int pick4(const int (&v)[4], int k) {
+    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+}
+
+// the slide (GROM.c:19492-19545), 256 steps per round (lane l: steps 4l..4l+3);
+// the inputs are loaded three rounds ahead.  Stops before a round that would
+// start at or past `cap` and returns false (s then resumes exactly there).
+template <int KIND>
+__device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
+    if (!s.sliding) return true;
+    const int lane = threadIdx.x & 63;
+    const int64_t L = W.L;
+    const double sgn = KIND == 0 ? 1.0 : -1.0;
+    const double wsdL = W.wsd[L];
+    int64_t pa = s.pa, cnt = s.cnt, last_good = s.last_good, ce = s.ce;
+    double tot = s.tot;
+    // the largest good ratio per lane; max is exact and order-free, so the
+    // wave's maximum is taken once, when the slide ends or pauses
+    double lmax = 0.0;
+    int mqi = s.mqi, mqb = s.mqb;
+    bool finished = true;
+    const long long ck_start = W.stats ? clock64() : 0;
+    long long pc_chain = 0, pc_before = 0, pc_after = 0, pc_rounds = 0;
+    unsigned long long n_fix = 0;
+    struct In {
+        uint32_t ba[4], bb[4];
+        double za[4], zb[4];
+    };
+    // unconditional loads from a clamped index (q - L >= 0 here); no select
+    // on the loaded values (that would wait for them): the round masks steps
+    // past the end itself
+    auto load = [&](int64_t at, In &o) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int64_t q0 = at + 4 * lane + i;
+            const int64_t q = q0 < W.len ? q0 : W.len - 1;
+            o.ba[i] = W.wb[q];
+            o.bb[i] = W.wb[q - L];
+            o.za[i] = W.sd[q];
+            o.zb[i] = W.sd[q - L];
+        }
+    };
+    auto round = [&](const In &in) -> bool {
+        if (pa >= cap) { finished = false; return false; }
+        const long long ckt = W.stats ? clock64() : 0;
+        const int64_t p0 = pa + 4 * lane;
+        bool inl[4];
+        int ct[4], cl[4], lt = -1, ll = -1;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            inl[i] = p0 + i < W.len;
+            ct[i] = inl[i] ? cdef(in.bb[i]) : -1;
+            cl[i] = inl[i] ? cdef(in.ba[i]) : -1;
+            lt = ct[i] >= 0 ? ct[i] : lt;
+            ll = cl[i] >= 0 ? cl[i] : ll;
+        }
+        int mt_c = lane_last_excl(lt, mqb), ml_c = lane_last_excl(ll, mqi);
+        int mt[4], ml[4], nqt = 0, nql = 0;
+        bool qt[4], ql[4];
+        double vt[4], vl[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            mt_c = ct[i] >= 0 ? ct[i] : mt_c;
+            ml_c = cl[i] >= 0 ? cl[i] : ml_c;
+            mt[i] = mt_c;
+            ml[i] = ml_c;
+            qt[i] = inl[i] && !(in.bb[i] & B_LOW) && (in.bb[i] & (B_W0 << mt_c));
+            ql[i] = inl[i] && !(in.ba[i] & B_LOW) && (in.ba[i] & (B_W0 << ml_c));
+            vt[i] = qt[i] ? -sgn * in.zb[i] : 0.0;
+            vl[i] = ql[i] ? sgn * in.za[i] : 0.0;
+            nqt += qt[i];
+            nql += ql[i];
+        }
+        int tot_l, tot_t;
+        int64_t run = cnt + excl_small(nql, tot_l) - excl_small(nqt, tot_t);
+        int64_t cj[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            run += (int)ql[i] - (int)qt[i];
+            cj[i] = run;
+        }
+        const long long ck0 = W.stats ? clock64() : 0;
+        double tj[4];
+        chain_round4(tot, vt, vl, tj, n_fix);
+        const long long ck1 = W.stats ? clock64() : 0;
+        pc_chain += ck1 - ck0;
+        pc_before += ck0 - ckt;
+        bool good[4];
+        double ts[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            good[i] = inl[i] && cj[i] > 0 && wsdL > 0 && ratio_ge_min(tj[i], cj[i] * wsdL) && LOW_FRAC_OK;
+            ts[i] = good[i] ? tj[i] / (cj[i] * wsdL) : 0.0;
+        }
+        // the loop test of step j (GROM.c:19492) sees the last good step
+        // before it; no step of the round can fail it while pa + 255 is
+        // within MAX_DIST of last_good (the common case: skip the scan)
+        int fi = 4;  // this lane's first step that fails the loop test
+        if (pa + 255 - last_good > MAX_DIST_LAST_GOOD) {
+            int lg = -1;
+#pragma unroll
+            for (int i = 0; i < 4; i++) lg = good[i] ? 4 * lane + i : lg;
+            const unsigned long long d = __ballot(lg >= 0) & ((1ull << lane) - 1);
+            const int src = d ? 63 - __clzll(d) : 0;
+            const int lgv = __shfl(lg, src);
+            int64_t lgb = d ? pa + lgv : last_good;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (fi == 4 && !(inl[i] && (p0 + i - lgb) <= MAX_DIST_LAST_GOOD)) fi = i;
+                if (good[i]) lgb = p0 + i;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (fi == 4 && !inl[i]) fi = i;
+        }
+        const unsigned long long sm = __ballot(fi < 4);
+        const int fl_ = sm ? __ffsll((long long)sm) - 1 : 64;
+        const int js = sm ? 4 * fl_ + __builtin_amdgcn_readlane(fi, fl_) : 256;
+        int eg_last = -1;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const bool eg = good[i] && 4 * lane + i < js;
+            eg_last = eg ? 4 * lane + i : eg_last;
+            lmax = (eg && ts[i] > lmax) ? ts[i] : lmax;
+        }
+        const unsigned long long gm = __ballot(eg_last >= 0);
+        if (gm) last_good = ce = pa + __builtin_amdgcn_readlane(eg_last, 63 - __clzll(gm));
+        if (js > 0) {
+            const int l = (js - 1) >> 2, k = (js - 1) & 3;
+            tot = rl_d(pick4(tj, k), l);
+            cnt = rl_i64(pick4(cj, k), l);
+            mqi = __builtin_amdgcn_readlane(pick4(ml, k), l);
+            mqb = __builtin_amdgcn_readlane(pick4(mt, k), l);
+        }
+        pa += js;
+        pc_rounds++;
+        if (W.stats) pc_after += clock64() - ck1;
+        return js == 256;
+    };
+    // three rounds of inputs in flight
+    In b0, b1, b2;
+    load(pa, b0);
+    load(pa + 256, b1);
+    load(pa + 512, b2);
+    for (;;) {
+        if (!round(b0)) break;
+        load(pa + 512, b0);
+        if (!round(b1)) break;
+        load(pa + 512, b1);
+        if (!round(b2)) break;
+        load(pa + 512, b2);
+    }
+    if (W.stats && lane == 0) {
+        atomicAdd(W.prof + 1, (unsigned long long)(clock64() - ck_start));
+        atomicAdd(W.prof + 0, (unsigned long long)pc_chain);
+        atomicAdd(W.prof + 2, (unsigned long long)pc_before);
+        atomicAdd(W.prof + 3, (unsigned long long)pc_after);
+        atomicAdd(W.prof + 5, n_fix);
         atomicAdd(W.stats + 2, (unsigned long long)pc_rounds);
     }
     s.pa = pa;
@@ -1882,6 +2183,7 @@ __global__ __launch_bounds__(64) void k_cnv_walk_resume(WalkIn W, const int32_t 
     const int64_t k = list[blockIdx.x];
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
     if (W.stats) W.stats += 15;  // the resumed walks' own counters (GROM_TIMING)
+    const long long kk0 = W.stats ? clock64() : 0;
     SlideState s = pend[k];
     __syncthreads();  // every lane has read the record before lane 0 may write a new one
     const int64_t pa0 = s.pa;
@@ -1895,6 +2197,7 @@ __global__ __launch_bounds__(64) void k_cnv_walk_resume(WalkIn W, const int32_t 
     }
     int64_t ce;
     double sdv;
+    const long long kk1 = W.stats ? clock64() : 0;
     trim_end<KIND>(W, s, ce, sdv);
     CallRec c;
     c.p = s.pos;
@@ -1905,8 +2208,15 @@ __global__ __launch_bounds__(64) void k_cnv_walk_resume(WalkIn W, const int32_t 
     int last = s.m;
     int64_t merge;
     bool paused = false;
+    const long long kk2 = W.stats ? clock64() : 0;
     const int64_t pos = walk_run<KIND>(w, ce + 1, last, c1, vis, false, &merge, calls, n_calls, cap, true,
                                        c1 + chunk, pend + k, &paused);
+    if (W.stats && (threadIdx.x & 63) == 0) {  // the longest resumed wave: whole, trim, walk on
+        const long long kk3 = clock64();
+        atomicMax(W.prof + 6, (unsigned long long)(kk3 - kk0));
+        atomicMax(W.prof + 7, (unsigned long long)(kk2 - kk1));
+        atomicMax(W.prof + 8, (unsigned long long)(kk3 - kk2));
+    }
     if ((threadIdx.x & 63) == 0) {
         cs[k].x1 = pos;
         cs[k].l1 = last;
@@ -3116,7 +3426,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;
             WalkIn WK = WI;
             WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 64) : nullptr;
-            WK.prof = tmg ? WK.stats + 40 : nullptr;  // slots 40..44 (the mode offsets reach slot 21)
+            WK.prof = tmg ? WK.stats + 40 : nullptr;  // slots 40..48 (the mode offsets reach slot 21)
             CK(hipStreamWaitEvent(st, S->walk_in, 0));
             if (WK.stats) CK(hipMemsetAsync(WK.stats, 0, 448, st));
             bool done = false;
@@ -3311,11 +3621,13 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                                 wsa[5 * mo + 4], wsa[5 * mo], wsa[5 * mo + 1], wsa[5 * mo + 2], wsa[5 * mo + 3]);
                     fprintf(stderr, "cnv walk %s: longest resumed slide %llu steps in %llu wall-clock ticks\n",
                             kind == 0 ? "DEL" : "DUP", wsa[20], wsa[21]);
-                    unsigned long long ck2[5];
+                    unsigned long long ck2[9];
                     (void)hipMemcpy(ck2, WK.stats + 40, sizeof(ck2), hipMemcpyDeviceToHost);
                     fprintf(stderr, "cnv walk %s: slide cycles %llu: before the sum chain %llu, chain %llu, after %llu; "
-                            "longest resumed slide %llu clocks\n",
-                            kind == 0 ? "DEL" : "DUP", ck2[1], ck2[2], ck2[0], ck2[3], ck2[4]);
+                            "longest resumed slide %llu clocks; chain guesses repaired %llu; longest resumed wave %llu "
+                            "clocks (trim %llu, walk on %llu)\n",
+                            kind == 0 ? "DEL" : "DUP", ck2[1], ck2[2], ck2[0], ck2[3], ck2[4], ck2[5], ck2[6], ck2[7],
+                            ck2[8]);
                     unsigned long long ws[5];
                     for (int q = 0; q < 5; q++) ws[q] = wsa[q] + wsa[5 + q] + wsa[10 + q] + wsa[15 + q];
                     fprintf(stderr, "cnv walk %s: %lld chunks, %lld repaired, %u candidates, %u call starts (%u left to the walk); "
