@@ -716,7 +716,14 @@ struct WalkIn {
     int64_t len, start, end, L, min_len;
     unsigned long long *stats;  // GROM_TIMING: walk counters (ab/cd wave calls and rounds), else null
     unsigned long long *prof;   // GROM_TIMING: slide clock counters (not moved per walk mode), else null
+    // per 64-base word bit masks for the trim (phase D), this kind: defining
+    // bases and their class-1 bits over every base (the outer scan) and over
+    // nonlow bases (the inner scan), nonlow bases, and the pass bits under
+    // class 0 / 1 over every base and over nonlow bases
+    const uint64_t *t_defa, *t_c1a, *t_defn, *t_c1n, *t_nl, *t_pa0, *t_pa1, *t_pn0, *t_pn1;
 };
+
+__device__ __forceinline__ uint64_t low_bits(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
 __device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) {
     uint64_t u = ((uint64_t)hi << 32) | lo;
@@ -1785,63 +1792,160 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
     return finished;
 }
 
-// phase D: trim the end back (GROM.c:19550-19600)
+// phase D: trim the end back (GROM.c:19550-19600), 64 words (4096 bases) per
+// round, one word per lane (lane i: the i-th word below the top).  Its two
+// scans are searches over bit masks:
+//  - the outer one steps down from the end while a base does not pass; the
+//    class it tests with is carried down over EVERY base (low ones included)
+//    and a low base may pass;
+//  - the inner one, from a passing base q, counts nonlow bases (c3) and
+//    passing ones (c2) downward -- the class carried over nonlow bases only --
+//    and stops at the first base where c3 == 0 or 2*c2 < c3: the first passage
+//    of the walk +1 (pass) / -1 (nonlow, not passing) to -1, or q itself when
+//    q is low.  The outer class carry does not follow the inner scan: after a
+//    stop the outer scan resumes with the class it had at q (as the
+//    reference's separate mqi/mqa variables do).
+__device__ __forceinline__ uint64_t word_range_mask(int64_t w, int64_t lo, int64_t hi) {
+    const int64_t a = max(lo, w * 64), b = min(hi, w * 64 + 63);
+    if (a > b) return 0;
+    return low_bits((int)(b - a + 1)) << (a - w * 64);
+}
+
+// class-1 mask of a word: each base takes the class of the nearest defining
+// base at or above it (def/c1: defining bases and their class-1 bits, within
+// the valid mask), else the carry from above
+__device__ __forceinline__ uint64_t class1_fill_down(uint64_t def, uint64_t c1, int carry) {
+    uint64_t have = def, val = c1 & def;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        val |= (val >> d) & ~have;
+        have |= have >> d;
+    }
+    return val | (carry == 1 ? ~have : 0ull);
+}
+
+// the class each lane's word starts from (the carry from the words above it
+// in this round) and the carry below the round; e: the class of the lane's
+// lowest defining base, -1 none
+__device__ __forceinline__ int round_carry(int e, int carry_in, int &carry_out) {
+    const unsigned long long d = __ballot(e >= 0), c1 = __ballot(e == 1);
+    carry_out = d ? (int)((c1 >> (63 - __clzll(d))) & 1ull) : carry_in;
+    return lane_last_excl(e, carry_in);
+}
+
 template <int KIND>
 __device__ void trim_end(const WalkIn &W, const SlideState &s, int64_t &ce_out, double &stdevs_out) {
     const int lane = threadIdx.x & 63;
-    const int64_t ML = W.min_len, cs = s.pos;
-    const uint32_t pb0 = KIND == 0 ? B_DEL0 : B_DUP0;
-    int64_t ce = s.ce;
-    int mqi = s.mqi;
-    int64_t p = ce;
-    while (p > cs + ML) {
-        const int64_t q = p - lane;
-        const bool in = q > cs + ML;
-        const uint32_t b = in ? W.wb[q] : 0u;
-        const int m = dpp_last_incl(in ? cdef(b) : -1, mqi);
-        const unsigned long long pm = __ballot(in && (b & (pb0 << m)));
-        if (!pm) {
-            const int n_in = __popcll(__ballot(in));
-            mqi = __builtin_amdgcn_readlane(m, n_in - 1);
-            p -= n_in;
-            ce = p;
-            continue;
-        }
-        const int j = __ffsll((long long)pm) - 1;
-        mqi = __builtin_amdgcn_readlane(m, j);
-        if (j > 0) {
-            p -= j;
-            ce = p;
-        }
-        int64_t c2 = 0, c3 = 0, pa = ce;
-        int mqa = mqi;
-        bool stopped = false;
-        while (pa > cs + ML && !stopped) {
-            const int64_t x = pa - lane;
-            const bool in2 = x > cs + ML;
-            const uint32_t bx = in2 ? W.wb[x] : 0u;
-            const bool nl = in2 && !(bx & B_LOW);
-            const int mx = dpp_last_incl(nl ? cdef(bx) : -1, mqa);
-            const bool px = nl && (bx & (pb0 << mx));
-            const int64_t c3j = c3 + wave_incl_count(nl), c2j = c2 + wave_incl_count(px);
-            const bool st = in2 && (c3j == 0 || (c3j > 0 && 2 * c2j < c3j) || !LOW_FRAC_OK);
-            const unsigned long long sm = __ballot(st);
-            if (sm) {
-                const int k = __ffsll((long long)sm) - 1;
-                ce = pa - k - 1;
-                pa = ce;
-                stopped = true;
-            } else {
-                const int n_in = __popcll(__ballot(in2));
-                c3 = rl_i64(c3j, n_in - 1);
-                c2 = rl_i64(c2j, n_in - 1);
-                mqa = __builtin_amdgcn_readlane(mx, n_in - 1);
-                pa -= n_in;
+    const int64_t lim = s.pos + W.min_len;  // both scans run while the position is > lim
+    int64_t ce = s.ce, p = ce;
+    int mq = s.mqi;
+    int64_t rounds = 0;
+    while (p > lim) {
+        // outer scan: the first base q <= p (q > lim) that passes
+        int64_t q = lim;
+        int cq = mq;
+        {
+            int64_t top = p;
+            int carry = mq;
+            while (top > lim) {
+                rounds++;
+                const int64_t w = (top >> 6) - lane;
+                const uint64_t vm = w >= 0 ? word_range_mask(w, lim + 1, top) : 0ull;
+                const uint64_t dfa = vm ? W.t_defa[w] & vm : 0ull, c1a = vm ? W.t_c1a[w] : 0ull;
+                const int e = dfa ? (int)((c1a >> (__ffsll((long long)dfa) - 1)) & 1ull) : -1;
+                int cout;
+                const int cl = round_carry(e, carry, cout);
+                const uint64_t cm = class1_fill_down(dfa, c1a, cl);
+                const uint64_t pass = vm ? ((W.t_pa0[w] & ~cm) | (W.t_pa1[w] & cm)) & vm : 0ull;
+                const unsigned long long fm = __ballot(pass != 0);
+                if (fm) {
+                    const int f = __ffsll((long long)fm) - 1;
+                    const int bit = 63 - __clzll(pass);
+                    const int64_t qq = w * 64 + bit;
+                    q = __builtin_amdgcn_readlane((int)(uint32_t)qq, f) |
+                        ((int64_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)qq >> 32), f) << 32);
+                    cq = __builtin_amdgcn_readlane((int)((cm >> bit) & 1ull), f);
+                    break;
+                }
+                carry = cout;
+                top = ((top >> 6) - 63) * 64 - 1;
             }
         }
-        p = pa;
-        if (W.stats && lane == 0) atomicAdd(W.stats + 3, 1ull);
+        if (q <= lim) {  // nothing passes down to the limit: the end steps all the way down
+            ce = lim;
+            break;
+        }
+        ce = q;
+        mq = cq;
+        // inner scan from q
+        int64_t x = lim;  // the stop base, lim: none
+        if (!(W.t_nl[q >> 6] >> (q & 63) & 1ull)) {
+            x = q;  // q is low: c3 == 0 at once
+        } else {
+            int64_t top = q;
+            int carry = cq, level = 0;
+            while (top > lim) {
+                rounds++;
+                const int64_t w = (top >> 6) - lane;
+                const uint64_t vm = w >= 0 ? word_range_mask(w, lim + 1, top) : 0ull;
+                const uint64_t dfn = vm ? W.t_defn[w] & vm : 0ull, c1n = vm ? W.t_c1n[w] : 0ull;
+                const int e = dfn ? (int)((c1n >> (__ffsll((long long)dfn) - 1)) & 1ull) : -1;
+                int cout;
+                const int cl = round_carry(e, carry, cout);
+                const uint64_t cm = class1_fill_down(dfn, c1n, cl);
+                const uint64_t nl = vm ? W.t_nl[w] & vm : 0ull;
+                const uint64_t up = vm ? ((W.t_pn0[w] & ~cm) | (W.t_pn1[w] & cm)) & vm : 0ull;
+                const uint64_t down = nl & ~up;
+                // this word's walk from its top bit down: net change and lowest prefix
+                int rel = 0, mn = 0;
+                for (uint64_t m = up | down; m; ) {
+                    const int bit = 63 - __clzll(m);
+                    m &= ~(1ull << bit);
+                    rel += (up >> bit) & 1ull ? 1 : -1;
+                    mn = min(mn, rel);
+                }
+                // each lane's starting level: the levels of the words above it
+                int ex = rel;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int t = __shfl_up(ex, d);
+                    if (lane >= d) ex += t;
+                }
+                ex -= rel;
+                const int start = level + ex;
+                const unsigned long long hit = __ballot(vm != 0 && start + mn <= -1);
+                if (hit) {
+                    const int f = __ffsll((long long)hit) - 1;
+                    int64_t xx = 0;
+                    if (lane == f) {  // the first base of this word where the level reaches -1
+                        int lv = start;
+                        for (uint64_t m = up | down; m; ) {
+                            const int bit = 63 - __clzll(m);
+                            m &= ~(1ull << bit);
+                            lv += (up >> bit) & 1ull ? 1 : -1;
+                            if (lv <= -1) { xx = w * 64 + bit; break; }
+                        }
+                    }
+                    x = __builtin_amdgcn_readlane((int)(uint32_t)xx, f) |
+                        ((int64_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)xx >> 32), f) << 32);
+                    break;
+                }
+                int tot_rel = rel;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) tot_rel += __shfl_xor(tot_rel, o);
+                level += tot_rel;
+                carry = cout;
+                top = ((top >> 6) - 63) * 64 - 1;
+            }
+        }
+        if (x > lim) {
+            ce = x - 1;
+            p = x - 1;
+        } else {
+            p = lim;
+        }
     }
+    if (W.stats && lane == 0) atomicAdd(W.stats + 3, (unsigned long long)rounds);
     ce_out = ce;
     stdevs_out = s.stdevs;
 }
@@ -2287,6 +2391,8 @@ struct CandWords {
     double *bsum, *bmax, *bmin, *babs;  // per word: sum z (nonlow), max/min running sum, sum |z|
     int8_t *kend;        // per word: the last defining class at its end
     double *rsn, *rsa;   // per base: running sum of z inside its word, nonlow bases / all bases
+    uint64_t *defa, *c1a, *c1n;  // class-defining bases (any / their class-1 bits), class-1 bits of `def`
+    uint64_t *pa;        // [kind][class][word]: passing with the class fixed, low bases included
     int64_t n_words;
 };
 
@@ -2323,13 +2429,17 @@ __global__ __launch_bounds__(256) void k_cnv_words(const uint16_t *__restrict__ 
         const int e = nl ? cdef(b) : -1;
         const int K = wave_last_incl(e, c);
         c = __builtin_amdgcn_readlane(K, 63);
-        const unsigned long long wnl = __ballot(nl), wdef = __ballot(e >= 0);
-        unsigned long long wpm[2][2], wpk[2];
+        const unsigned long long wnl = __ballot(nl), wdef = __ballot(e >= 0), wc1n = __ballot(e == 1);
+        const int ea = in ? cdef(b) : -1;
+        const unsigned long long wdefa = __ballot(ea >= 0), wc1a = __ballot(ea == 1);
+        unsigned long long wpm[2][2], wpk[2], wpa[2][2];
         for (int k = 0; k < 2; k++) {
             const uint32_t pb0 = k == 0 ? B_DEL0 : B_DUP0;
             wpm[k][0] = __ballot(nl && (b & pb0));
             wpm[k][1] = __ballot(nl && (b & (pb0 << 1)));
             wpk[k] = __ballot(nl && K >= 0 && (b & (pb0 << K)));
+            wpa[k][0] = __ballot(in && (b & pb0));
+            wpa[k][1] = __ballot(in && (b & (pb0 << 1)));
         }
         // running sum of z over the word's nonlow bases (any association: a bound input)
         double z = nl ? sd[p] : 0.0, ps = z;
@@ -2358,6 +2468,13 @@ __global__ __launch_bounds__(256) void k_cnv_words(const uint16_t *__restrict__ 
         if (lane == 0) {
             C.nl[wi] = wnl;
             C.def[wi] = wdef;
+            C.defa[wi] = wdefa;
+            C.c1a[wi] = wc1a;
+            C.c1n[wi] = wc1n;
+            for (int k = 0; k < 2; k++) {
+                C.pa[(k * 2 + 0) * C.n_words + wi] = wpa[k][0];
+                C.pa[(k * 2 + 1) * C.n_words + wi] = wpa[k][1];
+            }
             for (int k = 0; k < 2; k++) {
                 C.pm[(k * 2 + 0) * C.n_words + wi] = wpm[k][0];
                 C.pm[(k * 2 + 1) * C.n_words + wi] = wpm[k][1];
@@ -2393,8 +2510,6 @@ __device__ __forceinline__ void cls_tabs_build(ClsTabs &T) {
         for (int e = 0; e < 8; e++) T.first[by][e] = f[e];
     }
 }
-
-__device__ __forceinline__ uint64_t low_bits(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
 // the first step j in [0, n) at which the walk from level e >= 0 (+1 on a set
 // bit of P, -1 otherwise) reaches -1, or n
@@ -3372,7 +3487,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CandWords CW{};
         {
             const int64_t n_words = (len + 63) / 64 + 1, n_seg = (n_words + CW_SEG - 1) / CW_SEG;
-            const size_t wbytes = (size_t)n_words * (8 * 8 + 4 * 8 + 1) + 256 + 2 * 8 * (size_t)n_words * 64;
+            const size_t wbytes = (size_t)n_words * (15 * 8 + 4 * 8 + 1) + 256 + 2 * 8 * (size_t)n_words * 64;
             if ((rc = grow(S->cwords, wbytes, err, errlen)) || (rc = grow(S->cw_seg, (size_t)n_seg, err, errlen)) ||
                 (rc = grow(S->cw_carry, (size_t)n_seg, err, errlen)) || (rc = grow(S->wsdmin, 8 * (size_t)(L + 2), err, errlen)))
                 return rc;
@@ -3382,7 +3497,11 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             CW.def = u + n_words;
             CW.pm = u + 2 * n_words;   // 4 words
             CW.pk = u + 6 * n_words;   // 2 words
-            double *dd = (double *)(u + 8 * n_words);
+            CW.defa = u + 8 * n_words;
+            CW.c1a = u + 9 * n_words;
+            CW.c1n = u + 10 * n_words;
+            CW.pa = u + 11 * n_words;  // 4 words
+            double *dd = (double *)(u + 15 * n_words);
             CW.bsum = dd;
             CW.bmax = dd + n_words;
             CW.bmin = dd + 2 * n_words;
@@ -3425,6 +3544,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             // n_calls, n_pre, n_cand, capped, n_und; walk counters from byte 64
             uint32_t *n_calls = (uint32_t *)K.cnt.p, *n_pre = n_calls + 1;
             WalkIn WK = WI;
+            WK.t_defa = CW.defa;
+            WK.t_c1a = CW.c1a;
+            WK.t_defn = CW.def;
+            WK.t_c1n = CW.c1n;
+            WK.t_nl = CW.nl;
+            WK.t_pa0 = CW.pa + (kind * 2 + 0) * CW.n_words;
+            WK.t_pa1 = CW.pa + (kind * 2 + 1) * CW.n_words;
+            WK.t_pn0 = CW.pm + (kind * 2 + 0) * CW.n_words;
+            WK.t_pn1 = CW.pm + (kind * 2 + 1) * CW.n_words;
             WK.stats = tmg ? (unsigned long long *)((char *)K.cnt.p + 64) : nullptr;
             WK.prof = tmg ? WK.stats + 40 : nullptr;  // slots 40..48 (the mode offsets reach slot 21)
             CK(hipStreamWaitEvent(st, S->walk_in, 0));
