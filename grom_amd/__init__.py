@@ -38,7 +38,8 @@ class Params(C.Structure):
                                   "max_ins_range", "sv_list2_len", "pad_sv")] + \
         [(n, C.c_double) for n in ("pval_threshold", "pval_threshold1", "pval_insertion1", "pval_insertion",
                                    "min_sv_ratio", "min_indel_ratio", "max_evidence_ratio", "range_mult",
-                                   "max_inv_rd_diff", "min_overlap_ratio")]
+                                   "max_inv_rd_diff", "min_overlap_ratio")] + \
+        [("gen1000_window", C.c_int64)]
 
 
 class Chrom(C.Structure):
@@ -72,7 +73,9 @@ class SynthSpec(C.Structure):
 
 class Out(C.Structure):
     _fields_ = [("vcf", C.c_void_p), ("vcf_len", C.c_size_t), ("vcf_cap", C.c_size_t),
-                ("ctx", C.c_void_p), ("ctx_len", C.c_size_t), ("ctx_cap", C.c_size_t)]
+                ("ctx", C.c_void_p), ("ctx_len", C.c_size_t), ("ctx_cap", C.c_size_t),
+                ("side", C.c_void_p), ("side_len", C.c_size_t), ("side_cap", C.c_size_t),
+                ("side_written", C.c_int32), ("side_pad", C.c_int32)]
 
 
 class Stats(C.Structure):

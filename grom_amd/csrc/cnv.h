@@ -37,4 +37,4 @@ struct CnvTiming {
 // appended to `rows`.  `seed` replaces the srand(time()) of GROM.c:1584.
 int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed, const char *chr_name,
               const char *d_ref, int64_t len, int32_t *d_mq, const int32_t *d_rd, const int32_t *d_low,
-              std::string &rows, CnvTiming *timing, char *err, size_t errlen);
+              std::string &rows, CnvTiming *timing, char *err, size_t errlen, std::string *side = nullptr);

@@ -80,8 +80,10 @@ constexpr long MAX_DIST_LAST_GOOD = 10500; // default -X + 500, set before getop
 constexpr int MAX_BLOCK_LIST = 10000;      // max_block_list_len, GROM.c:633
 
 constexpr int GC_TP = 16384;               // positions per k_cnv_gc tile
-constexpr int GC_MMAX = 1536;              // largest insert mean the kernels accept
-constexpr int GC_NW = (GC_TP + 2 * GC_MMAX + 1 + 63) / 64;  // 64-bit class words per tile (with halo)
+constexpr int GC_MMAX_S = 1536;            // k_cnv_gc<GC_MMAX_S>: 32-bit window arithmetic
+constexpr int GC_MMAX = 16384;             // largest insert mean: k_cnv_gc<GC_MMAX>, 64-bit (a 25 KB LDS halo)
+template <int MMAX>
+constexpr int gc_nw() { return (GC_TP + 2 * MMAX + 1 + 63) / 64; }  // 64-bit class words per tile (with halo)
 constexpr int SEG_W = 4096;                // positions per wave in the state scans
 constexpr int ZT_MAX = 1024;               // depths with a precomputed z rank index
 constexpr int HIST_MAX = 4096;             // exact depth histogram for the chromosome variance
@@ -145,12 +147,19 @@ __device__ __forceinline__ int bit_index_sum(uint64_t w) {
 // planes built by wave ballots; P and R at any x are a per-word prefix plus
 // popcounts of the masked word, so the kernel reads each reference byte once
 // (plus the 2m halo) and writes 3 bytes per base.
+// MMAX: the largest insert mean m the instance takes; above GC_MMAX_S the
+// window sums (up to m^2 * 100) need 64-bit arithmetic, as the reference's
+// longs give them (GROM.c:1602, 1860)
+template <int MMAX>
 __global__ __launch_bounds__(256) void k_cnv_gc(const char *__restrict__ ref, Args A, int m, int64_t total,
                                                 uint8_t *__restrict__ gcw, uint8_t *__restrict__ acw,
                                                 uint8_t *__restrict__ rtype) {
+    constexpr int GC_NW = gc_nw<MMAX>();
+    using acc_t = typename std::conditional<(MMAX > GC_MMAX_S), int64_t, int>::type;
+    using uacc_t = typename std::conditional<(MMAX > GC_MMAX_S), uint64_t, uint32_t>::type;
     __shared__ uint64_t bits[2][GC_NW];  // plane 0: GC, plane 1: ACGT
-    __shared__ int pw[2][GC_NW];         // exclusive prefix of the set-bit counts
-    __shared__ int rw[2][GC_NW];         // exclusive prefix of the set-bit local indices
+    __shared__ acc_t pw[2][GC_NW];       // exclusive prefix of the set-bit counts
+    __shared__ acc_t rw[2][GC_NW];       // exclusive prefix of the set-bit local indices
     const int64_t t0 = (int64_t)blockIdx.x * GC_TP;
     const int64_t base = t0 - m;
     const int L = GC_TP + 2 * m + 1;
@@ -169,17 +178,17 @@ __global__ __launch_bounds__(256) void k_cnv_gc(const char *__restrict__ ref, Ar
     __syncthreads();
     {  // wave w scans array w: counts / index sums of plane w & 1
         const int pl = wv & 1, isr = wv >> 1;
-        int carry = 0;
+        acc_t carry = 0;
         for (int c0 = 0; c0 < nw; c0 += 64) {
             const int wi = c0 + lane;
-            int v = 0;
+            acc_t v = 0;
             if (wi < nw) {
                 const uint64_t w = bits[pl][wi];
-                v = isr ? wi * 64 * __popcll(w) + bit_index_sum(w) : __popcll(w);
+                v = isr ? (acc_t)wi * 64 * (acc_t)__popcll(w) + (acc_t)bit_index_sum(w) : (acc_t)__popcll(w);
             }
-            int x = v;
+            acc_t x = v;
             for (int d = 1; d < 64; d <<= 1) {
-                const int y = __shfl_up(x, d);
+                const acc_t y = __shfl_up(x, d);
                 if (lane >= d) x += y;
             }
             if (wi < nw) (isr ? rw : pw)[pl][wi] = carry + x - v;
@@ -187,7 +196,7 @@ __global__ __launch_bounds__(256) void k_cnv_gc(const char *__restrict__ ref, Ar
         }
     }
     __syncthreads();
-    const uint32_t tot = (uint32_t)total;  // m*m <= GC_MMAX^2
+    const uacc_t tot = (uacc_t)total;  // m*m
     // four consecutive positions per thread, stored as one 32-bit word per
     // output (t0 is a multiple of GC_TP, so the words are aligned)
     for (int j0 = 4 * threadIdx.x; j0 < GC_TP; j0 += 4 * 256) {
@@ -203,18 +212,18 @@ __global__ __launch_bounds__(256) void k_cnv_gc(const char *__restrict__ ref, Ar
                 const int xs[3] = {j + 2 * m + 1, j + m + 1, j + 1};
 #pragma unroll
                 for (int pl = 0; pl < 2; pl++) {
-                    int Qv[3];
+                    acc_t Qv[3];
 #pragma unroll
                     for (int t = 0; t < 3; t++) {
                         const int x = xs[t], wi = x >> 6, b = x & 63;
                         const uint64_t wd = bits[pl][wi] & ((1ull << b) - 1ull);
-                        const int c = __popcll(wd);
-                        const int Pv = pw[pl][wi] + c;
-                        const int Rv = rw[pl][wi] + wi * 64 * c + bit_index_sum(wd);
-                        Qv[t] = (x - 1) * Pv - Rv;
+                        const acc_t c = (acc_t)__popcll(wd);
+                        const acc_t Pv = pw[pl][wi] + c;
+                        const acc_t Rv = rw[pl][wi] + (acc_t)wi * 64 * c + (acc_t)bit_index_sum(wd);
+                        Qv[t] = (acc_t)(x - 1) * Pv - Rv;
                     }
-                    const uint32_t Tv = (uint32_t)(Qv[0] - 2 * Qv[1] + Qv[2]);
-                    w2[pl] = (100u * Tv / tot) & 255u;
+                    const uacc_t Tv = (uacc_t)(Qv[0] - 2 * Qv[1] + Qv[2]);
+                    w2[pl] = (uint32_t)((100u * Tv / tot) & 255u);
                 }
                 rt = (uint32_t)pair_type(ref[p], ref[p + 1]);
             }
@@ -553,10 +562,14 @@ __global__ __launch_bounds__(256) void k_cnv_z(Args A, const uint8_t *__restrict
 
 // Window means for every length of one sampled window (GROM.c:18967-19018):
 // one lane per window, its sum accumulated in the reference's order.  A
-// window is up to 3 pieces of consecutive bases (it can straddle the
-// sampling passes of a block).  out row: [min_len..len] means, NaN = none.
+// window is a run of pieces of consecutive bases (it straddles the sampling
+// passes of a block: as many as -A when a block is short for -X).  out row:
+// [min_len..len] means, NaN = none.
+struct WinPiece {
+    int64_t start, count;
+};
 struct WinDesc {
-    int64_t p0, n0, p1, n1, p2, n2;
+    int64_t piece0, n_pieces, ntot;  // pieces [piece0, piece0 + n_pieces) of the piece list, ntot bases
     int64_t row;
 };
 // Window means for every length (GROM.c:18967-19018).  Each window's running
@@ -568,9 +581,10 @@ struct WinDesc {
 // previous chunk into means (the divisions spread over three waves) and store
 // them length-major, so each store of a wave covers 64 adjacent windows.
 constexpr int WCH = 32;
-__global__ __launch_bounds__(256) void k_cnv_windows(const WinDesc *__restrict__ wd, int64_t n_win,
-                                                     const uint8_t *__restrict__ flag, const double *__restrict__ sd,
-                                                     int64_t L, int64_t min_len, double *__restrict__ out) {
+__global__ __launch_bounds__(256) void k_cnv_windows(const WinDesc *__restrict__ wd, const WinPiece *__restrict__ pcs,
+                                                     int64_t n_win, const uint8_t *__restrict__ flag,
+                                                     const double *__restrict__ sd, int64_t L, int64_t min_len,
+                                                     double *__restrict__ out) {
     __shared__ double s_tot[2][WCH][64];
     __shared__ int32_t s_cnt[2][WCH][64], s_ft[2][WCH][64];
     __shared__ int64_t s_nmax;
@@ -580,8 +594,10 @@ __global__ __launch_bounds__(256) void k_cnv_windows(const WinDesc *__restrict__
     int64_t ntot = 0;
     if (w < n_win) {
         d = wd[w];
-        ntot = d.n0 + d.n1 + d.n2;
+        ntot = d.ntot;
     }
+    // the lane's cursor in its window's pieces (the bases are taken in order)
+    int64_t pi = d.piece0, po = 0;
     if (threadIdx.x == 0) s_nmax = 0;
     __syncthreads();
     if (wave == 0) {
@@ -602,9 +618,11 @@ __global__ __launch_bounds__(256) void k_cnv_windows(const WinDesc *__restrict__
             for (int j = 0; j < WCH; j++) {
                 const int64_t g = c * WCH + j;
                 int64_t a = -1;
-                if (g < d.n0) a = d.p0 + g;
-                else if (g < d.n0 + d.n1) a = d.p1 + (g - d.n0);
-                else if (g < ntot) a = d.p2 + (g - d.n0 - d.n1);
+                if (g < ntot) {
+                    while (po >= pcs[pi].count) { pi++; po = 0; }
+                    a = pcs[pi].start + po;
+                    po++;
+                }
                 f[j] = a >= 0 ? flag[a] : (uint8_t)0;
                 v[j] = a >= 0 ? sd[a] : 0.0;
             }
@@ -681,6 +699,47 @@ __global__ __launch_bounds__(256) void k_cnv_window_sq(const double *__restrict_
         tot[l] = s;
         cnt[l] = c;
     }
+}
+
+// ---- the -N side file (GROM.c:20234-20345): per g_1000gen_window bases, the
+// copy number of the ratios depth / GC-bin average over the window's
+// qualifying bases.  One lane per window; each lane adds its window's terms in
+// the reference's order (sum, then the squared deviations), so cn and the
+// deviation sum are the reference's doubles; the host takes the sqrt.
+__global__ __launch_bounds__(256) void k_cnv_gen1000(const uint8_t *__restrict__ flag, const int32_t *__restrict__ mq,
+                                                     const int32_t *__restrict__ rd, const int32_t *__restrict__ low,
+                                                     const uint8_t *__restrict__ gcw, const Tables *__restrict__ T,
+                                                     int64_t win, int64_t n_win, int min_mapq, int ploidy,
+                                                     double *__restrict__ out_cn, double *__restrict__ out_s2,
+                                                     int64_t *__restrict__ out_n) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= n_win) return;
+    const int64_t b0 = w * win;
+    double sum = 0.0;
+    int64_t n = 0;
+    for (int64_t a = b0; a < b0 + win; a++) {
+        if (flag[a] & F_LOW) continue;
+        const double ave = T->ave[mq[a] >= min_mapq ? 0 : 1][gcw[a]];
+        if (ave > 0) {
+            sum += (double)(rd[a] + low[a]) / ave;
+            n += 1;
+        }
+    }
+    double cn = -1.0, s2 = 0.0;
+    if (n > 0) {
+        cn = (sum / (double)n) * (double)ploidy;
+        for (int64_t a = b0; a < b0 + win; a++) {
+            if (flag[a] & F_LOW) continue;
+            const double ave = T->ave[mq[a] >= min_mapq ? 0 : 1][gcw[a]];
+            if (ave > 0) {
+                const double t = (double)ploidy * ((double)(rd[a] + low[a]) / ave) - cn;
+                s2 += t * t;  // pow(t, 2): both correctly rounded
+            }
+        }
+    }
+    out_cn[w] = cn;
+    out_s2[w] = s2;
+    out_n[w] = n;
 }
 
 // ---------------- DEL / DUP window search (GROM.c:19359-20020) ----------------
@@ -2704,6 +2763,7 @@ struct CnvScratch {
     int64_t gc_len = -1, gc_m = -1;
     Buf zover;  // repeat z overrides: positions then values
     Buf cwords, cw_seg, cw_carry, wsdmin;  // candidate classification: bit words, their class carry, min wsd per 64
+    Buf gen1000;                           // the -N side file's per-window results
     Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -2882,7 +2942,7 @@ int cnv_prelaunch(CnvScratch *S, hipStream_t after, const grom_params &P, const 
     const hipStream_t side = S->kb[0].st;
     CK(hipEventRecord(S->gc_done, after));  // the reference may still be uploading on `after`
     CK(hipStreamWaitEvent(side, S->gc_done, 0));
-    hipLaunchKernelGGL(k_cnv_gc, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, side, d_ref, A, (int)m,
+    hipLaunchKernelGGL(m <= GC_MMAX_S ? k_cnv_gc<GC_MMAX_S> : k_cnv_gc<GC_MMAX>, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, side, d_ref, A, (int)m,
                        (int64_t)m * m, (uint8_t *)S->gcw.p, (uint8_t *)S->acw.p, (uint8_t *)S->rtype.p);
     CK(hipGetLastError());
     CK(hipEventRecord(S->gc_done, side));
@@ -2898,7 +2958,7 @@ void cnv_scratch_free(CnvScratch *S) {
                   &S->prepos, &S->ppos, &S->rep, &S->misc, &S->blk, &S->hist,
                   &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
                   &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover, &S->cwords, &S->cw_seg,
-                  &S->cw_carry, &S->wsdmin};
+                  &S->cw_carry, &S->wsdmin, &S->gen1000};
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
     for (KindBufs &K : S->kb) {
@@ -2916,7 +2976,7 @@ void cnv_scratch_free(CnvScratch *S) {
 
 int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed, const char *chr_name,
               const char *d_ref, int64_t len, int32_t *d_mq, const int32_t *d_rd, const int32_t *d_low,
-              std::string &rows, CnvTiming *timing, char *err, size_t errlen) {
+              std::string &rows, CnvTiming *timing, char *err, size_t errlen, std::string *side) {
     const auto t_host0 = std::chrono::steady_clock::now();
     int rc;
     const int64_t m = P.insert_mean, W = 2 * (int64_t)m - 1;
@@ -2925,8 +2985,10 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         snprintf(err, errlen, "insert mean %lld outside the CNV kernels' range 1..%d", (long long)m, GC_MMAX);
         return GROM_E_ARG;
     }
+    // (window lengths index int32 positions in the walk; -X past a chromosome
+    // only makes every window search stop at the end)
     if (P.max_rd_window_len < P.min_rd_window_len || P.min_rd_window_len < 1 || P.windows_sampling_factor < 1 ||
-        P.max_rd_window_len > 1000000) {
+        P.max_rd_window_len > ((int64_t)1 << 30)) {
         snprintf(err, errlen, "unsupported CNV window parameters (-W %lld -X %lld -A %lld)",
                  (long long)P.min_rd_window_len, (long long)P.max_rd_window_len, (long long)P.windows_sampling_factor);
         return GROM_E_ARG;
@@ -2980,7 +3042,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     if (S->gc_ref == d_ref && S->gc_len == len && S->gc_m == m) {
         CK(hipStreamWaitEvent(st, S->gc_done, 0));
     } else {
-        hipLaunchKernelGGL(k_cnv_gc, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, st, d_ref, A, (int)m,
+        hipLaunchKernelGGL(m <= GC_MMAX_S ? k_cnv_gc<GC_MMAX_S> : k_cnv_gc<GC_MMAX>, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, st, d_ref, A, (int)m,
                            total_w, gcw, acw, rtype);
         CK(hipGetLastError());
     }
@@ -3322,9 +3384,36 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CK(hipGetLastError());
 
         mark("flags+z");
+        // ---- the -N side file (its flags are final here; GROM.c:20234-20345) ----
+        if (side && P.gen1000_window > 0) {
+            const int64_t win = P.gen1000_window, n_win = len / win;
+            side->clear();
+            if (n_win > 0) {
+                if ((rc = grow(S->gen1000, (size_t)n_win * 24, err, errlen))) return rc;
+                double *d_cn = (double *)S->gen1000.p, *d_s2 = d_cn + n_win;
+                int64_t *d_n = (int64_t *)(d_s2 + n_win);
+                hipLaunchKernelGGL(k_cnv_gen1000, dim3((unsigned)((n_win + 255) / 256)), dim3(256), 0, st, flag, d_mq,
+                                   d_rd, d_low, gcw, dT, win, n_win, (int)P.rd_min_mapq, (int)P.ploidy, d_cn, d_s2, d_n);
+                CK(hipGetLastError());
+                std::vector<double> hcn((size_t)n_win), hs2((size_t)n_win);
+                std::vector<int64_t> hn((size_t)n_win);
+                CK(hipMemcpyAsync(hcn.data(), d_cn, 8 * n_win, hipMemcpyDeviceToHost, st));
+                CK(hipMemcpyAsync(hs2.data(), d_s2, 8 * n_win, hipMemcpyDeviceToHost, st));
+                CK(hipMemcpyAsync(hn.data(), d_n, 8 * n_win, hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+                side->reserve((size_t)n_win * 40);
+                for (int64_t w = 0; w < n_win; w++) {
+                    const double sd_w = hn[w] > 0 ? sqrt(hs2[w] / (double)hn[w]) : 0.0;
+                    char line[128];
+                    const int nl = snprintf(line, sizeof(line), "%ld\t%e\t%e\n", (long)(w * win), hcn[w], sd_w);
+                    side->append(line, (size_t)nl);
+                }
+            }
+        }
         // ---- window means by length, GROM.c:18967-19018 ----
         const int64_t L = P.max_rd_window_len, F = P.windows_sampling_factor, ML = P.min_rd_window_len;
         std::vector<WinDesc> wds;
+        std::vector<WinPiece> wps;
         std::vector<int64_t> rlen;
         long twc = 0;  // ddd_temp_win_count carries across blocks
         for (size_t b = 0; b < ss.size(); b++) {
@@ -3339,33 +3428,29 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             while (si < segs.size()) {
                 WinDesc d{};
                 int64_t need = L, got = 0;
-                int np = 0;
-                int64_t *pp[3] = {&d.p0, &d.p1, &d.p2}, *nn[3] = {&d.n0, &d.n1, &d.n2};
+                d.piece0 = (int64_t)wps.size();
                 while (need > 0 && si < segs.size()) {
                     int64_t take = std::min(need, segs[si].second - so);
-                    if (np == 3) break;
-                    *pp[np] = segs[si].first + so;
-                    *nn[np] = take;
-                    np++;
+                    wps.push_back(WinPiece{segs[si].first + so, take});
                     so += take;
                     need -= take;
                     got += take;
                     if (so == segs[si].second) { si++; so = 0; }
                 }
-                if (np == 3 && need > 0 && si < segs.size()) {
-                    snprintf(err, errlen, "CNV window spans more than 3 sampling pieces (block too short for -A)");
-                    return GROM_E_ARG;
-                }
+                d.n_pieces = (int64_t)wps.size() - d.piece0;
+                d.ntot = got;
                 if (twc == 0 && got >= ML) {
                     d.row = (int64_t)wds.size();
                     wds.push_back(d);
                     rlen.push_back(got);
+                } else {
+                    wps.resize((size_t)d.piece0);  // not sampled: its pieces are not needed
                 }
                 if (got == L) { twc += 1; if (twc == REDUCTION) twc = 0; }
             }
         }
         const int64_t n_win = (int64_t)wds.size();
-        if ((rc = grow(S->wd, sizeof(WinDesc) * (n_win + 1), err, errlen)) ||
+        if ((rc = grow(S->wd, sizeof(WinDesc) * (n_win + 1) + sizeof(WinPiece) * (wps.size() + 1), err, errlen)) ||
             (rc = grow(S->rows, 8 * (size_t)std::max<int64_t>(n_win, 1) * (L + 1), err, errlen)) ||
             (rc = grow(S->rowlen, 8 * (n_win + 1), err, errlen)) || (rc = grow(S->wtot, 8 * (L + 1), err, errlen)) ||
             (rc = grow(S->wcnt, 8 * (L + 1), err, errlen)) || (rc = grow(S->wsd, 8 * (L + 1), err, errlen)))
@@ -3373,10 +3458,13 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         std::vector<double> wtot(L + 1, 0.0), wsd(L + 1, 0.0);
         std::vector<int64_t> wcnt(L + 1, 0);
         if (n_win > 0) {
+            WinPiece *d_pcs = (WinPiece *)((WinDesc *)S->wd.p + n_win);
             CK(hipMemcpyAsync(S->wd.p, wds.data(), sizeof(WinDesc) * n_win, hipMemcpyHostToDevice, st));
+            CK(hipMemcpyAsync(d_pcs, wps.data(), sizeof(WinPiece) * wps.size(), hipMemcpyHostToDevice, st));
             CK(hipMemcpyAsync(S->rowlen.p, rlen.data(), 8 * n_win, hipMemcpyHostToDevice, st));
             hipLaunchKernelGGL(k_cnv_windows, dim3((unsigned)((n_win + 63) / 64)), dim3(256), 0, st,
-                               (const WinDesc *)S->wd.p, n_win, flag, sd, L, ML, (double *)S->rows.p);
+                               (const WinDesc *)S->wd.p, (const WinPiece *)d_pcs, n_win, flag, sd, L, ML,
+                               (double *)S->rows.p);
             hipLaunchKernelGGL(k_cnv_window_sq, dim3((unsigned)((L - ML + 1 + 63) / 64)), dim3(256), 0, st,
                                (const double *)S->rows.p, n_win, (const int64_t *)S->rowlen.p, L, ML,
                                (double *)S->wtot.p, (int64_t *)S->wcnt.p);

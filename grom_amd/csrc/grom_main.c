@@ -145,6 +145,7 @@ typedef struct {
 } chrom_plan;
 
 static int g_plan_only = 0; /* GROM_PLAN_ONLY: report the record plan, no GPU */
+static const char *g_side_base; /* -o name: the -N side files are named after it */
 
 static double clock_gettime_s(void) {
     struct timespec t;
@@ -421,6 +422,21 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     j->text_len = out.vcf_len;
     j->ctx_text = out.ctx; /* raw CTX rows for the translocation post-pass */
     j->ctx_len = out.ctx_len;
+    if (out.side_written && g_side_base) { /* -N: <results>.1000gen.<chr>, GROM.c:20246-20267 */
+        char *fn = malloc(strlen(g_side_base) + strlen(cp->name) + 16);
+        sprintf(fn, "%s.1000gen.%s", g_side_base, cp->name);
+        FILE *f = fopen(fn, "w");
+        if (!f) {
+            printf("\nCould not open %s\n", fn);
+            free(fn);
+            free(out.side);
+            return GROM_E_ARG;
+        }
+        if (out.side_len) fwrite(out.side, 1, out.side_len, f);
+        fclose(f);
+        free(fn);
+    }
+    free(out.side);
     if (getenv("GROM_DUMP")) write_dumps(slot, cp, &ch, &rd, j->has_batch ? NULL : j->stage, P);
     if (verbose)
         printf("%s: %lld reads, %.3f ms on GPU (%.2f Mbases/s)\n", cp->name, (long long)n_reads, st.ms_total,
@@ -1085,7 +1101,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
         case 'M': P->rmdup = 1; break;
         case 'i': S->bam_name = optarg; break;
         case 'r': S->fasta_name = optarg; break;
-        case 'o': S->out_name = optarg; break;
+        case 'o': S->out_name = optarg; g_side_base = optarg; break;
         case 'B': S->max_chr_len = atol(optarg); break;
         case 'p': P->ploidy = atoi(optarg); break;
         case 'q': P->min_mapq = atoi(optarg); break;
@@ -1120,13 +1136,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
         case 'm': P->min_indel_ratio = atof(optarg); break;
         case 'u': P->max_evidence_ratio = atof(optarg); break;
         case 'w': P->max_ins_range = atoi(optarg); break;
-        case 'N':
-            if (atol(optarg) > 0) {
-                printf("ERROR: -N (.1000gen side file) is not supported by this build\n");
-                free(S);
-                return 1;
-            }
-            break;
+        case 'N': P->gen1000_window = atol(optarg); break;
         case 'h': print_help(); free(S); return 0;
         case '?': free(S); return 1;
         default: break; /* accepted; steers rows outside the implemented scan */

@@ -632,15 +632,21 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         std::string cnv_text;
         if (ch->cnv && !want_dbg) {
             if (!C.cnv) C.cnv = cnv_scratch_new();
-            std::string crow;
+            std::string crow, side;
             char cerr[512] = {0};
             rc = cnv_chrom(C.cnv, st, P, ch->seed, ch->name, ch->ref, ch->len, (int32_t *)C.caf_mq.p,
-                           (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, crow, &ct, cerr, sizeof(cerr));
+                           (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, crow, &ct, cerr, sizeof(cerr),
+                           P.gen1000_window > 0 ? &side : nullptr);
             if (rc != GROM_OK) {
                 set_err("%s", cerr);
                 return rc;
             }
             cnv_text.swap(crow);
+            if (P.gen1000_window > 0) {
+                Text sdt{&out->side, &out->side_len, &out->side_cap};
+                if (!side.empty()) sdt.add(side.data(), side.size());
+                out->side_written = 1;
+            }
         }
         const double t_cnv = ms_since(t_start);
         if (svt.joinable()) svt.join();

@@ -151,6 +151,7 @@ void grom_default_params(grom_params *p) {
     p->range_mult = 0.75;
     p->max_inv_rd_diff = 1.75;
     p->min_overlap_ratio = 0.5;
+    p->gen1000_window = 0;
 }
 
 void grom_params_set_insert(grom_params *p, int32_t mean, int32_t imin, int32_t imax, int32_t lseq) {
@@ -170,5 +171,6 @@ void grom_params_set_insert(grom_params *p, int32_t mean, int32_t imin, int32_t 
 void grom_out_free(grom_out *o) {
     free(o->vcf);
     free(o->ctx);
+    free(o->side);
     memset(o, 0, sizeof(*o));
 }

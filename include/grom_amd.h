@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GROM_AMD_ABI_VERSION 5
+#define GROM_AMD_ABI_VERSION 6
 #define GROM_MAX_TRIALS 1000 /* max_trials, GROM.c:631 */
 
 enum {
@@ -110,6 +110,8 @@ typedef struct grom_params {
     double range_mult;            /* g_range_mult, GROM.c:828 */
     double max_inv_rd_diff;       /* g_max_inv_rd_diff, GROM.c:907 */
     double min_overlap_ratio;     /* g_min_overlap_ratio, GROM.c:817 */
+    /* ABI 6 */
+    int64_t gen1000_window;       /* g_1000gen_window (-N), GROM.c:746: the .1000gen side file when > 0 */
 } grom_params;
 
 /* One chromosome.  `ref` holds exactly what find_disc_svs loaded
@@ -193,6 +195,11 @@ typedef struct grom_out {
     size_t vcf_len, vcf_cap;
     char *ctx;
     size_t ctx_len, ctx_cap;
+    /* ABI 6: the chromosome's <results>.1000gen.<chr> side file (-N,
+     * GROM.c:20234-20345), written whenever its CNV pass ran and -N > 0 */
+    char *side;
+    size_t side_len, side_cap;
+    int32_t side_written, side_pad;
 } grom_out;
 
 /* Per-chromosome run statistics (for benchmarks / logs). */

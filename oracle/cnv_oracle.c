@@ -14,7 +14,7 @@
  *
  * Not restated: the N-block list (GROM.c:1626-1722; it is built but never
  * read, only freed at GROM.c:18100-18101), tumor/normal mode (g_normal is
- * never set from argv, SURVEY.md §2 #18b) and the -N ".1000gen" side file.
+ * never set from argv, SURVEY.md §2 #18b).
  */
 
 /* ---- parameters (GROM.c:710-979; CLI letters GROM.c:21907-22102) ---- */
@@ -32,6 +32,9 @@ static long g_max_rd_window_len = 10000;        /* -X, GROM.c:933 */
 /* set from the DEFAULT -X before getopt runs (GROM.c:21898) */
 static long g_max_distance_since_last_del_good = 10000 + 500;
 static double g_rd_pval_threshold = 0.000000001; /* -V, GROM.c:722 */
+static long g_1000gen_window = 0;               /* -N, GROM.c:746 */
+static const char *g_1000gen_base;              /* the results file name (-o), GROM.c:21057 */
+static const char *g_1000gen_chr;               /* ddd_chr_name */
 static int g_rd_max_mapq = 60;                  /* GROM.c:718 */
 static double g_mapq_factor = 0.5;              /* -F, GROM.c:719 */
 static long g_sample_lists_len = 100000;        /* GROM.c:725 */
@@ -871,6 +874,47 @@ static void detect_del_dup(long len, const int *gc_w, const int *acgt_w, const i
         }
         free(pl);
     }
+    /* the -N side file <results>.1000gen.<chr>, GROM.c:20234-20345: per
+     * complete window of g_1000gen_window bases, the copy number of the
+     * window's qualifying bases and its deviation */
+    if (g_1000gen_window > 0 && g_1000gen_base && g_1000gen_chr) {
+        char *fn = (char *)malloc(strlen(g_1000gen_base) + strlen(g_1000gen_chr) + 16);
+        sprintf(fn, "%s.1000gen.%s", g_1000gen_base, g_1000gen_chr);
+        FILE *gf = fopen(fn, "w");
+        if (gf == NULL) {
+            printf("\nCould not open %s\n", fn);
+            exit(1);
+        }
+        double *gl = (double *)malloc((g_1000gen_window + 1) * sizeof(double));
+        double g_sum = 0.0, g_cn, g_sd;
+        long g_n = 0, g_nw = 0;
+        for (a = 0; a < len; a++) {
+            if (flag[a] == 0) {
+                int k = (mql[a] >= g_rd_min_mapq) ? 0 : 1;
+                if (ave[k][gc_w[a]] > 0) { gl[g_n] = (double)RDT(a) / ave[k][gc_w[a]]; g_n += 1; }
+            }
+            g_nw += 1;
+            if (g_nw == g_1000gen_window) {
+                if (g_n > 0) {
+                    for (long c = 0; c < g_n; c++) g_sum += gl[c];
+                    g_cn = (g_sum / g_n) * ploidy;
+                    g_sd = 0;
+                    for (long c = 0; c < g_n; c++) g_sd += pow((ploidy * gl[c] - g_cn), 2);
+                    g_sd = sqrt(g_sd / g_n);
+                } else {
+                    g_cn = -1;
+                    g_sd = 0;
+                }
+                fprintf(gf, "%ld\t%e\t%e\n", a - g_1000gen_window + 1, g_cn, g_sd);
+                g_n = 0;
+                g_nw = 0;
+                g_sum = 0;
+            }
+        }
+        fclose(gf);
+        free(gl);
+        free(fn);
+    }
 #undef GUARD
 #undef MQF
     free(wsd);
@@ -1023,6 +1067,7 @@ static void cnv_chromosome(long len, const char *fa, const cnv_pre *pre, int *mq
     g_lowvar_block_end_list[0] = len - W;
     g_lowvar_block_index = 1;
     g_res_over = g_res_repl = 0;
+    g_1000gen_chr = chr_name;
     detect_del_dup(len, pre->gc_w, pre->acgt_w, mql, rd, low, pre, ploidy, &del, &dup);
     if (getenv("GROM_CNV_STATS")) {
         FILE *sf = fopen(getenv("GROM_CNV_STATS"), "a");

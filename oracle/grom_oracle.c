@@ -1183,6 +1183,7 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
     const char *bam_file_name = NULL, *fasta_file_name = NULL, *results_file_name = NULL;
     optind = 0; /* GNU getopt: full re-initialisation */
     int opt;
+    g_1000gen_window = 0;
     /* getopt string of GROM.c:21908 */
     while ((opt = getopt(argc, argv,
                          "Z:W:X:Q:A:Y:B:D:E:K:N:V:U:L:F:SP:c:R:MG:i:r:o:p:q:s:v:g:l:d:b:n:a:y:z:e:fj:k:m:u:w:x:h")) != -1) {
@@ -1223,6 +1224,7 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
         case 'E': g_min_repeat_stdev = atof(optarg); break;
         case 'K': g_ranks_stdev = atoi(optarg); break;
         case 'V': g_rd_pval_threshold = atof(optarg); break;
+        case 'N': g_1000gen_window = atol(optarg); break;
         case 'U': g_chr_rd_threshold_factor = atoi(optarg); break;
         case 'L': g_dup_threshold_factor = atol(optarg); break;
         case 'F': g_mapq_factor = atof(optarg); break;
@@ -1232,6 +1234,7 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
         }
     }
     g_pval_threshold1 = g_pval_threshold; /* GROM.c:22101 */
+    g_1000gen_base = results_file_name;
     g_rd_min_mapq = g_min_mapq; /* GROM.c:22102 */
     if (!bam_file_name) { printf("ERROR: No bam file specified.\n"); return 1; }
     stream_t st;

@@ -57,6 +57,10 @@ CASES = {
     # more than g_sample_lists_len (100,000) depth samples, so the reservoir
     # draws of GROM.c:18385-18451 run at the reference's own cap
     "cnv_reservoir": ["-L", "30000000", "-R", "50", "-s", "41", "-V", "0.0000002", "-W", "50000,300000", "-Q", "0.05"],
+    # a 2.2 kb insert library (mean above the 1536 of the 32-bit GC-window
+    # kernel: k_cnv_gc's 64-bit instance), with copy-number regions and SVs
+    "wide_insert": ["-L", "1500000", "-s", "19", "-m", "2200", "-d", "200", "-V", "0.000004", "-W", "20000,150000",
+                    "-Q", "0.05", "-X", "5"],
 }
 
 

@@ -59,6 +59,12 @@ CNV_RUNS = [
     ("cnv_multi", ["-V", "1", "-M", "-U", "1", "-Y", "2", "-Z", "20000"]),
     ("cnv_long", ["-V", "1", "-M"]),
     ("cnv_long", []),
+    ("wide_insert", []),
+    ("wide_insert", ["-V", "1"]),
+    # -X past the chromosome lengths and beyond 1e6 with -A 20: every sampled
+    # window straddles up to six sampling passes of its block (GROM.c:18967-19018)
+    ("cnv_multi", ["-V", "1", "-X", "2500000", "-A", "20", "-W", "100"]),
+    ("cnv", ["-V", "1", "-X", "40000", "-A", "9"]),
 ]
 
 
@@ -266,6 +272,29 @@ def test_serial_reader_path(datadir, case, extra):
     run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra, env_extra={"GROM_SERIAL_DECODE": "1"})
     for ext in (".vcf", ".ctx.vcf"):
         assert open(datadir / f"o_{tag}{ext}").read() == open(datadir / f"g_{tag}{ext}").read(), ext
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,extra", [("cnv", ["-N", "1000"]), ("cnv_multi", ["-V", "1", "-N", "777"]),
+                                        ("three_chr", ["-N", "5000"])])
+def test_gen1000_side_file(datadir, case, extra):
+    """-N: the per-chromosome <results>.1000gen.<chr> side file (GROM.c:20234-
+    20345) -- per window of -N bases the copy number of its qualifying bases
+    and their deviation, in the reference's summation order -- is the
+    oracle's, byte for byte, for every chromosome; the VCF is unchanged."""
+    import glob
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"g1k_{case}{''.join(extra).replace('-', '_')}"
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra)
+    of = sorted(glob.glob(str(datadir / f"o_{tag}.vcf.1000gen.*")))
+    gf = sorted(glob.glob(str(datadir / f"g_{tag}.vcf.1000gen.*")))
+    assert of and [os.path.basename(f)[2:] for f in of] == [os.path.basename(f)[2:] for f in gf], (of, gf)
+    for a, b in zip(of, gf):
+        ta, tb = open(a).read(), open(b).read()
+        assert ta == tb, a
+    assert any(open(f).read() for f in of)  # at least one chromosome has complete windows
+    assert open(datadir / f"o_{tag}.vcf").read() == open(datadir / f"g_{tag}.vcf").read()
 
 
 def test_device_resident_path_matches_host_path():

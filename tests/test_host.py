@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 15
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.grom_abi_version() == 5
+    assert lib.grom_abi_version() == 6
     # the ctypes mirror has the C layout of every ABI struct
     for i, st in enumerate((grom_amd.Params, grom_amd.Chrom, grom_amd.Reads, grom_amd.Out, grom_amd.Stats,
                               grom_amd.IndelRec, grom_amd.Aux, grom_amd.SvRec)):
