@@ -569,7 +569,8 @@ struct WinPiece {
     int64_t start, count;
 };
 struct WinDesc {
-    int64_t piece0, n_pieces, ntot;  // pieces [piece0, piece0 + n_pieces) of the piece list, ntot bases
+    int64_t p0, n0, p1, n1, p2, n2;  // the first three pieces inline (the common case)
+    int64_t piece0, n_pieces, ntot;  // all pieces: [piece0, piece0 + n_pieces) of the piece list, ntot bases
     int64_t row;
 };
 // Window means for every length (GROM.c:18967-19018).  Each window's running
@@ -618,7 +619,11 @@ __global__ __launch_bounds__(256) void k_cnv_windows(const WinDesc *__restrict__
             for (int j = 0; j < WCH; j++) {
                 const int64_t g = c * WCH + j;
                 int64_t a = -1;
-                if (g < ntot) {
+                if (d.n_pieces <= 3) {
+                    if (g < d.n0) a = d.p0 + g;
+                    else if (g < d.n0 + d.n1) a = d.p1 + (g - d.n0);
+                    else if (g < ntot) a = d.p2 + (g - d.n0 - d.n1);
+                } else if (g < ntot) {  // more pieces (a block short for -X and -A): walk the list
                     while (po >= pcs[pi].count) { pi++; po = 0; }
                     a = pcs[pi].start + po;
                     po++;
@@ -3439,6 +3444,13 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 }
                 d.n_pieces = (int64_t)wps.size() - d.piece0;
                 d.ntot = got;
+                {
+                    int64_t *pp[3] = {&d.p0, &d.p1, &d.p2}, *nn[3] = {&d.n0, &d.n1, &d.n2};
+                    for (int64_t q = 0; q < 3 && q < d.n_pieces; q++) {
+                        *pp[q] = wps[(size_t)(d.piece0 + q)].start;
+                        *nn[q] = wps[(size_t)(d.piece0 + q)].count;
+                    }
+                }
                 if (twc == 0 && got >= ML) {
                     d.row = (int64_t)wds.size();
                     wds.push_back(d);
