@@ -2857,6 +2857,30 @@ static void msort_lo(double *b, size_t n, double *t) {
     memcpy(b, t, (n - n2) * sizeof(double));
 }
 
+// the same merge sort with the two halves of the top `depth` levels sorted on
+// their own threads (each with its own half of the scratch): the same
+// operations on the same data, so the same order -- which matters, since the
+// reference's comparator (low 32 bits, wrapping difference) is not a total
+// order and only this exact merge sequence reproduces its result
+static void msort_lo_par(double *b, size_t n, double *t, int depth) {
+    if (depth <= 0 || n < (1u << 16)) {
+        msort_lo(b, n, t);
+        return;
+    }
+    size_t n1 = n / 2, n2 = n - n1;
+    double *b1 = b, *b2 = b + n1;
+    std::thread th([=] { msort_lo_par(b1, n1, t, depth - 1); });
+    msort_lo_par(b2, n2, t + n1, depth - 1);
+    th.join();
+    double *o = t;
+    while (n1 > 0 && n2 > 0) {
+        if (dcmp_lo(*b1, *b2) <= 0) { *o++ = *b1++; --n1; }
+        else { *o++ = *b2++; --n2; }
+    }
+    if (n1 > 0) memcpy(o, b1, n1 * sizeof(double));
+    memcpy(b, t, (n - n2) * sizeof(double));
+}
+
 // sort of small non-negative ints (read depths): counting sort, same result
 // as the reference's qsort with cmpfunc on these values
 static void sort_depths(std::vector<int> &v) {
@@ -3965,7 +3989,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 const long pc = (long)pl.size();
                 if (pc > 0) {
                     tmp.resize(pc);
-                    msort_lo(pl.data(), pl.size(), tmp.data());
+                    msort_lo_par(pl.data(), pl.size(), tmp.data(), 3);
                     long s0 = 0.1 * pc, e0 = pc - s0;
                     double sum = 0.0;
                     for (long i = s0; i < e0; i++) sum += pl[i];
