@@ -33,10 +33,10 @@
 // (g_one_base_rd_len, GROM.c:8350-8353).  The running means use the
 // reference's operation order; this file is built with -ffp-contract=off.
 // The reference's ring keeps cluster groups only under "set" flags
-// (GROM.c:5868-6392); one write site sets the wrong group's flags
-// (GROM.c:8020-8045), which can displace DUP evidence when a ring half-turn
-// sees no other DUP write.  The fold records per half-turn whether that
-// happened, and the scan refuses such input.
+// (GROM.c:5868-6392); every write of a group's primary arrays sets that
+// group's flags (the split-read DUP_F starts set the DEL and DUP flags,
+// GROM.c:8027-8043, 9408-9411), so no evidence is left behind by a shift and
+// the ring is exactly the absolute-coordinate state folded here.
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -58,22 +58,20 @@ constexpr int MT = GROM_MAX_TRIALS;
 enum : uint8_t { OT_EMPTY = 0, OT_I = 11, OT_DF = 12, OT_DR = 13 };  // GROM.c:668-681
 enum { RM_SET = 0, RM_MAX = 1, RM_MINMAX = 2 };
 enum { SUM_RD = 0, SUM_CONC, SUM_INS, SUM_MUNF, SUM_MUNR, SUM_N };
-// groups of the ring's "set" flags (GROM.c:5868-6020)
-__constant__ int8_t c_group[CL_N] = {0, 0, 1, 1, 2, 3, 2, 3, 4, 5};
 
 __constant__ char c_nt16_sv[16] = {'=', 'A', 'C', 'M', 'G', 'R', 'S', 'V', 'T', 'W', 'Y', 'H', 'K', 'D', 'B', 'N'};
 
 // one ordered evidence event (32 bytes)
 struct SvEv {
     double v;      // cluster: the value its running mean averages
-    int64_t aux;   // indel I: nibble offset of the inserted bases; cluster: ring half-turn of the write
+    int64_t aux;   // indel I: nibble offset of the inserted bases
     int32_t rp;    // cluster: read position kept in rs/re; indel I: read bases left from aux
     int32_t mchr;  // ctx: mate chromosome
     int32_t len;   // indel: op length; cluster: tolerance (Mx - Mn [+ insert_temp])
     uint8_t type;  // 1..10 cluster (CL_* + 1), 11..13 indel
     uint8_t w;     // count increment (add, or add/2 away from a clipped edge)
     uint8_t add;   // full weight (6 or 0)
-    uint8_t fl;    // bits 0-1 rs/re rule, 2-3 ctx kind, 4-5 split DUP_F start quirk
+    uint8_t fl;    // bits 0-1 rs/re rule, 2-3 ctx kind, 4-5 split DUP_F start (re -> del_f_read_end)
 };
 
 struct Geo {
@@ -104,11 +102,10 @@ __device__ void sv_walk(const View &V, int64_t i, EV &&ev, RG &&rg) {
     const int32_t pos = in.pos[i], mpos = in.mpos[i], tlen = in.isize[i], mtid = in.mtid[i];
     const int32_t mq = in.mapq[i];
     const int add = mq >= g.min_mapq ? AF : 0;
-    // the iteration that ingests this read, and the ring index / half-turn then
+    // the iteration that ingests this read, and the ring index then
     const int64_t p_ing = max((int64_t)g.s0, (int64_t)pos - (int64_t)g.overlap * g.Mx);
     const int64_t k_ing = (int64_t)g.n_skip + (p_ing - g.s0) + 1;
     const int64_t idx = ring_idx(g, k_ing);
-    const int64_t epoch = (k_ing + 1) / g.H;
     const int64_t ring_lo = p_ing - idx, ring_hi = p_ing - idx + g.R;  // positions of ring index 0 and R
     const int64_t vis_lo = max(p_ing, (int64_t)g.eval_lo), vis_hi = g.eval_hi;  // inclusive
     auto event = [&](int64_t x, SvEv e) {
@@ -177,7 +174,6 @@ __device__ void sv_walk(const View &V, int64_t i, EV &&ev, RG &&rg) {
     auto clus = [&](int64_t x, int t, int w, double v, int32_t tl, int32_t rp, int rmode, int ctx, int quirk) {
         SvEv e{};
         e.v = v;
-        e.aux = epoch;
         e.rp = rp;
         e.mchr = mtid;
         e.len = tl;
@@ -451,8 +447,6 @@ struct FoldOut {
     grom_indel_rec *irec;     // every base an indel event reached (test hook)
     grom_sv_rec *drec;        // debug: every base with cluster state
     uint32_t *bits;
-    uint32_t *epochs;         // per ring half-turn: bit 0 DUP write under DUP flags, bit 1 DUP write without
-    int64_t n_epochs;
     int32_t min_disc;
     const uint8_t *seq;
 };
@@ -565,21 +559,20 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
         const bool is_ctx = t >= CL_CTX_F;
         Clus &c = cl[t];
         int32_t *pm = is_ctx ? &mchr[t - CL_CTX_F] : nullptr;
-        const bool dup_group = c_group[t] == 1;
-        uint32_t epoch_bit = 0;  // 1: a DUP write under DUP flags, 2: a DUP write without
         if (c.cnt == 0) {
             c.cnt = E.w;
             c.dist = E.v;
             if (pm) *pm = E.mchr;
             c.rs = E.rp;
-            if (quirk) cl[CL_DEL_F].re = E.rp;  // sic: del_f_read_end (GROM.c:8035, 9416)
+            // sic: del_f_read_end (GROM.c:8036, 9419); both starts set the DEL
+            // and DUP ring flags (GROM.c:8027-8036, 9408-9411), so the ring
+            // shifts this evidence like any other
+            if (quirk) cl[CL_DEL_F].re = E.rp;
             else c.re = E.rp;
-            epoch_bit = quirk == 1 ? 2u : 1u;
         } else if (compat(E, c.dist, c.cnt, pm ? *pm : 0)) {
             c.cnt += E.w;
             c.dist += (double)E.w * (E.v - c.dist) / (double)c.cnt;
             rsre(c.rs, c.re, E.rp, rmode);
-            epoch_bit = 1u;
         } else {
             // an "other" slot write leaves the group's flags alone but moves no
             // primary data, so it cannot strand DUP evidence
@@ -625,8 +618,6 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
                 }
             }
         }
-        if (!WRITE && dup_group && epoch_bit && E.aux >= 0 && E.aux < O.n_epochs)
-            atomicOr(&O.epochs[E.aux], epoch_bit);
     }
     int other_len = OTHER_LEN;  // GROM.c:11415-11425
     for (int o = 0; o < OTHER_LEN; o++)
@@ -925,7 +916,7 @@ struct Buf {
 }  // namespace
 
 struct SvScratch {
-    Buf cnt, off, keys, vals, keys2, vals2, ev, run_pos, run_len, run_off, n_runs, tmp, sums, bits, epochs;
+    Buf cnt, off, keys, vals, keys2, vals2, ev, run_pos, run_len, run_off, n_runs, tmp, sums, bits;
     Buf f_cand, f_ind, f_dbg, o_cand, o_ind, o_dbg, rec, irec_c, irec, drec;
     Buf ctx, ctx2, ckeys, ckeys2, cvals, cvals2, n_ctx, hits, n_hits, hits2;
     SvHit *h_hits = nullptr;  // pinned: the hits of the last evaluation, in base order
@@ -956,7 +947,7 @@ SvScratch *sv_scratch_new() { return new SvScratch(); }
 void sv_scratch_free(SvScratch *s) {
     if (!s) return;
     Buf *all[] = {&s->cnt, &s->off, &s->keys, &s->vals, &s->keys2, &s->vals2, &s->ev, &s->run_pos, &s->run_len,
-                  &s->run_off, &s->n_runs, &s->tmp, &s->sums, &s->bits, &s->epochs, &s->f_cand, &s->f_ind, &s->f_dbg,
+                  &s->run_off, &s->n_runs, &s->tmp, &s->sums, &s->bits, &s->f_cand, &s->f_ind, &s->f_dbg,
                   &s->o_cand, &s->o_ind, &s->o_dbg, &s->rec, &s->irec_c, &s->irec, &s->drec, &s->ctx, &s->ctx2,
                   &s->ckeys, &s->ckeys2, &s->cvals, &s->cvals2, &s->n_ctx, &s->hits, &s->n_hits, &s->hits2};
     for (Buf *b : all)
@@ -1038,11 +1029,8 @@ int sv_prepare(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput
     SCHK(hipEventRecord(S->e0, st));
     const size_t L = (size_t)(len + 1);
     const int64_t n_words = (len + 64) / 32 + 1;
-    const int64_t half = std::max<int64_t>(P.half_one_base_rd_len, 1);
-    const int64_t n_epochs = ((int64_t)ch.n_skip + len + 2) / half + 2;
     if ((rc = sbuf(S->sums, sizeof(int32_t) * SUM_N * L, err, errlen)) ||
         (rc = sbuf(S->bits, sizeof(uint32_t) * n_words, err, errlen)) ||
-        (rc = sbuf(S->epochs, sizeof(uint32_t) * n_epochs, err, errlen)) ||
         (rc = sbuf(S->cnt, sizeof(uint32_t) * (n + 1), err, errlen)) ||
         (rc = sbuf(S->off, sizeof(uint32_t) * (n + 1), err, errlen)) ||
         (rc = sbuf(S->n_ctx, 16, err, errlen)))
@@ -1050,7 +1038,6 @@ int sv_prepare(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput
     int32_t *sums = (int32_t *)S->sums.p;
     SCHK(hipMemsetAsync(sums, 0, sizeof(int32_t) * SUM_N * L, st));
     SCHK(hipMemsetAsync(S->bits.p, 0, sizeof(uint32_t) * n_words, st));
-    SCHK(hipMemsetAsync(S->epochs.p, 0, sizeof(uint32_t) * n_epochs, st));
     SCHK(hipMemsetAsync(S->n_ctx.p, 0, 16, st));
     // room for the pileup's context records: every clipped base and every marked one
     S->ctx_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1 << 16, len / 64 + 2 * n / 16), (int64_t)1 << 28);
@@ -1125,7 +1112,7 @@ int sv_prepare(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput
     }
     SCHK(hipcub::DeviceScan::ExclusiveSum(S->tmp.p, t_scan, (uint32_t *)S->run_len.p, (uint32_t *)S->run_off.p,
                                           (int)n_runs, st));
-    // the fold, pass 1: flags, candidate bits, DUP-flag half-turns
+    // the fold, pass 1: flags and candidate bits
     if ((rc = sbuf(S->f_cand, sizeof(uint32_t) * (n_runs + 1), err, errlen)) ||
         (rc = sbuf(S->f_ind, sizeof(uint32_t) * (n_runs + 1), err, errlen)) ||
         (rc = sbuf(S->f_dbg, sizeof(uint32_t) * (n_runs + 1), err, errlen)) ||
@@ -1141,8 +1128,6 @@ int sv_prepare(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput
     O.o_ind = (const uint32_t *)S->o_ind.p;
     O.o_dbg = (const uint32_t *)S->o_dbg.p;
     O.bits = (uint32_t *)S->bits.p;
-    O.epochs = (uint32_t *)S->epochs.p;
-    O.n_epochs = n_epochs;
     O.min_disc = P.min_disc;
     O.seq = in.seq;
     SCHK(hipMemsetAsync(O.f_cand + n_runs, 0, 4, st));
@@ -1165,19 +1150,7 @@ int sv_prepare(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput
     SCHK(hipMemcpyAsync(&cnts[0], (uint32_t *)S->o_cand.p + n_runs, 4, hipMemcpyDeviceToHost, st));
     SCHK(hipMemcpyAsync(&cnts[1], (uint32_t *)S->o_ind.p + n_runs, 4, hipMemcpyDeviceToHost, st));
     SCHK(hipMemcpyAsync(&cnts[2], (uint32_t *)S->o_dbg.p + n_runs, 4, hipMemcpyDeviceToHost, st));
-    std::vector<uint32_t> ep((size_t)n_epochs);
-    SCHK(hipMemcpyAsync(ep.data(), S->epochs.p, sizeof(uint32_t) * n_epochs, hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
-    for (int64_t k = 0; k < n_epochs; k++)
-        if ((ep[k] & 2u) && !(ep[k] & 1u)) {
-            // a ring half-turn in which DUP evidence was written only without the
-            // DUP flags: the reference's shift would move it (GROM.c:5893-5916)
-            snprintf(err, errlen,
-                     "breakpoint pass: DUP evidence written without its ring flags in half-turn %lld "
-                     "(GROM.c:8020-8045); this input needs the ring-exact fallback, which is not built",
-                     (long long)k);
-            return GROM_E_ARG;
-        }
     S->n_rec = cnts[0];
     S->n_irec = cnts[1];
     S->n_drec = debug ? cnts[2] : 0;

@@ -124,8 +124,8 @@ typedef struct {
     int rmode;
     int ctx;        /* 0: distance cluster; 1: ctx, mate forward; 2: ctx, mate reverse */
     int mchr;
-    int init_quirk; /* split-read DUP_F start: 1 = GROM.c:8020-8045 (DEL flags only),
-                       2 = GROM.c:9405-9422 (DEL and DUP flags); both write
+    int init_quirk; /* split-read DUP_F start: 1 = GROM.c:8020-8045, 2 = GROM.c:9405-9422;
+                       both set the DEL and DUP flags and write
                        del_f_read_end instead of dup_f_read_end */
 } sv_ev;
 
@@ -152,8 +152,10 @@ static void sv_fold(sv_ring *r, int i, const sv_ev *e) {
     int32_t *pm = (e->t == CL_CTX_F) ? &r->ctx_mchr[0][i] : (e->t == CL_CTX_R) ? &r->ctx_mchr[1][i] : NULL;
     const int g = cl_group[e->t];
     if (c->cnt == 0) {
-        if (e->init_quirk == 1) { r->gset[G_DEL][0] = r->gset[G_DEL][1] = 1; }
-        else if (e->init_quirk == 2) {
+        if (e->init_quirk) {
+            /* both split-read DUP_F starts set the DUP flags (GROM.c:8027-8028,
+             * 9410-9411) and, for the del_f_read_end write, the DEL flags
+             * (GROM.c:8035-8036 / 8042-8043, 9408-9409) */
             r->gset[G_DEL][0] = r->gset[G_DEL][1] = 1;
             r->gset[G_DUP][0] = r->gset[G_DUP][1] = 1;
         } else { r->gset[g][0] = r->gset[g][1] = 1; }
