@@ -4017,10 +4017,18 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 worker();
                 for (auto &t : th) t.join();
             }
+            // -f: a column header before each kind's rows (GROM.c:17242-17245,
+            // 17378), rows named by caf_del_text / caf_dup_text (GROM.c:1575)
+            if (P.vcf != 1) rows += "SV Type\tChromosome\tStart\tEnd\tStdev from mean\tP Value\tCopy Number\n";
             for (size_t j = 0; j < keep.size(); j++) {
                 const CallRec &c = found[kind][keep[j].first];
                 char line[512];
-                int nl = snprintf(line, sizeof(line), "%s\t%lld\t.\t.\t%s\t.\t.\tEND=%lld\tSD:Z:CN:CS\t%e:%e:%.2f:%e\n",
+                int nl;
+                if (P.vcf != 1)  // GROM.c:17340-17343
+                    nl = snprintf(line, sizeof(line), "%s\t%s\t%lld\t%lld\t%e\t%e\t%e\t%e\n", kind == 0 ? "DEL RD" : "DUP RD",
+                                  chr_name, (long long)c.p, (long long)c.ce, c.stdevs, keep[j].second, cnv_cn[j], cnv_cs[j]);
+                else
+                    nl = snprintf(line, sizeof(line), "%s\t%lld\t.\t.\t%s\t.\t.\tEND=%lld\tSD:Z:CN:CS\t%e:%e:%.2f:%e\n",
                                   chr_name, (long long)c.p + 1, kind == 0 ? "<DEL>" : "<DUP>", (long long)c.ce + 1,
                                   c.stdevs, keep[j].second, cnv_cn[j], cnv_cs[j]);
                 rows.append(line, (size_t)nl);

@@ -135,6 +135,46 @@ static void header(FILE *f, const char *fasta_name, int ctx) {
     fprintf(f, "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\n");
 }
 
+/* -f: the insert statistics and the column header instead of the VCF header
+ * (GROM.c:20566-20671) */
+static const char TAB_COLUMNS[] =
+    "SV\tChromosome\tStart (Tumor)\tEnd (Tumor)\tLength (Tumor)\tP-val (Start, Tumor)\t"
+    "P-val (End, Tumor)\tConcordant Pairs (Start, Tumor)\tConcordant Pairs (End, Tumor)\t"
+    "Start or End?\tRead Depth (High MapQ, Normal)\tRead Depth (Low MapQ, Normal)\t"
+    "Concordant Pairs (Normal)\tINS (Normal)\tDEL (For, Normal)\tDEL (Rev, Normal)\t"
+    "DEL (For, Length, Normal)\tDEL (Rev, Length, Normal)\tDUP (Rev, Normal)\tDUP (For, Normal)\t"
+    "DUP (Rev, Length, Normal)\tDUP (For, Length, Normal)\tINV (For, Start, Normal)\t"
+    "INV (Rev, Start, Normal)\tINV (For, End, Normal)\tINV (Rev, End, Normal)\t"
+    "INV (For, Start, Length, Normal)\tINV (Rev, Start, Length, Normal)\t"
+    "INV (For, End, Length, Normal)\tINV (Rev, End, Length, Normal)\tUnmapped Mate (For, Normal)\t"
+    "Unmapped Mate (Rev, Normal)\tSoft-clipping (Left, Normal)\tSoft-clipping (Right, Normal)\t"
+    "Soft-clipping Read Depth (Left, Normal)\tSoft-clipping Read Depth (Right, Normal)\t"
+    "Soft-clipping Read Depth (Left+Right, Normal)\tINS Indel (Normal)\tDEL Indel (Start, Normal)\t"
+    "DEL Indel (End, Normal)\tDEL Indel (Start, Length, Normal)\tDEL Indel (End, Length, Normal)\t"
+    "CTX Soft-clipping (Left, Normal)\tCTX Soft-clipping (Right, Normal)\t"
+    "CTX Soft-clipping Read Depth (Left, Normal)\tCTX Soft-clipping Read Depth (Right, Normal)\t"
+    "CTX Soft-clipping Read Depth (Left+Right, Normal)\tIndel Soft-clipping (Left, Normal)\t"
+    "Indel Soft-clipping (Right, Normal)\tIndel Soft-clipping Read Depth (Left, Normal)\t"
+    "Indel Soft-clipping Read Depth (Right, Normal)\t"
+    "Indel Soft-clipping Read Depth (Left+Right, Normal)\t"
+    "Soft-clipping (Left Max including CTX, Normal)\t"
+    "Soft-clipping (Right Max including CTX, Normal)\tOther (Number of Non-Empty, Normal)\t"
+    "CTX (For, Normal)\tCTX (Rev, Normal)\tSV Overlap (Normal)\tOther (Number of Non-Empty, Tumor)\t"
+    "Read Start (Start, Tumor)\tRead End (Start, Tumor)\tRead Start (End, Tumor)\t"
+    "Read End (End, Tumor)\tDEL Read Start (For/Rev, Normal)\tDEL Read End (For/Rev, Normal)\t"
+    "DUP Read Start (Rev/For, Normal)\tDUP Read End (Rev/For, Normal)\tINV Read Start (For, Normal)\t"
+    "INV Read End (For, Normal)\tINV Read Start (Rev, Normal)\tINV Read End (Rev, Normal)\t"
+    "CTX Read Start (For, Normal)\tCTX Read End (For, Normal)\tCTX Read Start (Rev, Normal)\t"
+    "CTX Read End (Rev, Normal)\tMate Chr (CTX only, Tumor)\tMate Pos (CTX only, Tumor)\t"
+    "Mate Chr (For, Normal)\tMate Pos (For, Normal)\tMate Chr (Rev, Normal)\tMate Pos (Rev, Normal)\t"
+    "Reference Base\tSNV Base (Tumor)\tSNV Ratio (Tumor)\tSNV Count (A, Tumor)\t"
+    "SNV Count (C, Tumor)\tSNV Count (G, Tumor)\tSNV Count (T, Tumor)\tSNV Count (A, Normal)\t"
+    "SNV Count (C, Normal)\tSNV Count (G, Normal)\tSNV Count (T, Normal)\t\n";
+static void tab_header(FILE *f, const grom_params *P) {
+    fprintf(f, "%d\t%d\t%d\t%d\n", P->insert_mean, P->insert_min_size, P->insert_max_size, P->lseq);
+    fputs(TAB_COLUMNS, f);
+}
+
 typedef struct {
     int fasta_idx;
     int32_t tid;
@@ -180,7 +220,7 @@ typedef struct {
     double binom, ev, hez;
 } ctx_row_t;
 
-static void ctx_postpass(const char *raw, size_t raw_len, const bam_hdr *hdr, int Mx, int glseq, FILE *out) {
+static void ctx_postpass(const char *raw, size_t raw_len, const bam_hdr *hdr, int Mx, int glseq, int vcf, FILE *out) {
     int n_t = hdr->n_ref;
     char **lc = calloc(n_t > 0 ? n_t : 1, sizeof(char *));
     for (int a = 0; a < n_t; a++) {
@@ -254,6 +294,12 @@ static void ctx_postpass(const char *raw, size_t raw_len, const bam_hdr *hdr, in
         n2++;
         char bnd[64];
         const char *mn = (q->mchr >= 0 && q->mchr < n_t) ? lc[q->mchr] : "";
+        if (!vcf) { /* -f rows, GROM.c:22734 (g_sv_types[6] "CTX_F", [7] "CTX_R", GROM.c:867) */
+            fprintf(out, "%s\t%s\t%d\t%d\t%d\t%e\t%.1f\t%d\t%d\t%d\t%s\t%d\t%d\t%d\t%e\n", q->type == 6 ? "CTX_F" : "CTX_R",
+                    (q->chr >= 0 && q->chr < n_t) ? lc[q->chr] : "", q->pos, b, q->mateid, q->binom, q->ev, q->rd, q->conc,
+                    q->other, mn, q->mpos, q->rs, q->re, q->hez);
+            continue;
+        }
         const int am = abs(q->mpos);
         if (q->type == 6) snprintf(bnd, sizeof(bnd), q->mpos < 0 ? "N[%s:%d[" : "N]%s:%d]", mn, am);
         else snprintf(bnd, sizeof(bnd), q->mpos < 0 ? "[%s:%d[N" : "]%s:%d]N", mn, am);
@@ -281,7 +327,7 @@ int grom_ctx_postpass(const char *raw, size_t raw_len, const char *const *target
     size_t len = 0;
     FILE *f = open_memstream(&buf, &len);
     if (!f) { grom_set_last_error("grom_ctx_postpass: no memory"); return GROM_E_NOMEM; }
-    ctx_postpass(raw, raw_len, &h, insert_max, lseq, f);
+    ctx_postpass(raw, raw_len, &h, insert_max, lseq, 1, f);
     fclose(f);
     if (out->ctx_len + len + 1 > out->ctx_cap) {
         size_t nc = out->ctx_cap ? out->ctx_cap : 4096;
@@ -645,10 +691,12 @@ static void finish_outputs(cli_state *S, textbuf *ctx_all) {
      * chromosomes with their mates and write them under the header */
     FILE *ctx = fopen(S->ctx_name, "w");
     if (ctx) {
-        if (S->P.vcf == 1) {
-            header(ctx, S->fasta_name, 1);
-            ctx_postpass(ctx_all->p, ctx_all->len, &S->hdr, S->P.insert_max_size, S->P.lseq, ctx);
-        }
+        if (S->P.vcf == 1) header(ctx, S->fasta_name, 1);
+        else /* the trimmed file's column header, GROM.c:22652-22700 */
+            fputs("SV\tChromosome\tStart\tID\tMate ID\tBinom Prob (Start)\tCTX evidence\tRead Depth (High MapQ)\t"
+                  "Concordant Pairs\tOther (Number of Non-Empty)\tMate Chr\tMate Pos\tRead Start\tRead End\t"
+                  "Hez binom prob\n", ctx);
+        ctx_postpass(ctx_all->p, ctx_all->len, &S->hdr, S->P.insert_max_size, S->P.lseq, S->P.vcf == 1, ctx);
         fclose(ctx);
     }
 }
@@ -738,6 +786,7 @@ static int run_serial(cli_state *S) {
     FILE *vcf = fopen(S->out_name, "w");
     if (!vcf) { printf("Error opening file %s\n", S->out_name); free(plan); free(order); return 1; }
     if (P->vcf == 1) header(vcf, S->fasta_name, 0);
+    else tab_header(vcf, P);
     /* one serial pass over the records, split per chromosome (stream.h);
      * finished chromosomes go to the GPU workers, rows are written in order */
     if (bgzf_open_read(&br, S->bam_name) != 0) { fclose(vcf); free(plan); free(order); return 1; }
@@ -976,6 +1025,7 @@ static int run_streamed(cli_state *S) {
     vcf = fopen(S->out_name, "w");
     if (!vcf) { printf("Error opening file %s\n", S->out_name); status = 1; goto done; }
     if (P->vcf == 1) header(vcf, S->fasta_name, 0);
+    else tab_header(vcf, P);
     F.S = S;
     F.plan = plan;
     F.n_plan = g_plan_only ? 0 : n_plan;

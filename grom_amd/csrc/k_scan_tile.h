@@ -125,14 +125,64 @@ __device__ __forceinline__ int acgt_code(int s4) {
     return (s4 != 0 && (s4 & (s4 - 1)) == 0) ? __builtin_ctz((unsigned)s4) : 4;
 }
 
+// The read-name slots of one position (GROM.c:6805-6824): the first empty
+// slot takes the name (names >= 50 chars are never stored, id 0); a slot
+// holding the name marks the base as seen.  Slots fill from 0 and are never
+// emptied while the position is open, so "first empty" is the fill count.
+//
+// RegSlots: NS slots in registers (-n <= NS), written with selects so they
+// stay in registers; the kernel is built for NS = 4, 8, 16, 32.
+template <int NS>
+struct RegSlots {
+    uint32_t s[NS];
+    __device__ __forceinline__ void reset() {
+#pragma unroll
+        for (int k = 0; k < NS; k++) s[k] = 0;
+    }
+    __device__ __forceinline__ bool probe(uint32_t nid, int min_snv) {
+        bool done = false, found = false;
+#pragma unroll
+        for (int k = 0; k < NS; k++) {
+            const bool active = !done && k < min_snv;
+            const bool empty = active && s[k] == 0;
+            const bool match = active && !empty && s[k] == nid;
+            s[k] = (empty && nid != 0) ? nid : s[k];
+            found = found || match;
+            done = done || empty || match;
+        }
+        return found;
+    }
+};
+
+// MemSlots: any -n.  The slots live in global scratch, [slot][lane] per
+// workgroup (one column per position, stride GROM_TILE, so a wave's probes
+// are coalesced); the fill count is a register.  Only mismatching bases with
+// a high-quality read probe the slots (<1% of visits), so the L2 round trips
+// are off the common path.
+struct MemSlots {
+    uint32_t *col;
+    int nf;
+    __device__ __forceinline__ void reset() { nf = 0; }
+    __device__ __forceinline__ bool probe(uint32_t nid, int min_snv) {
+        const int lim = min(nf, min_snv);
+        for (int k = 0; k < lim; k++)
+            if (col[(size_t)k * TG] == nid) return true;  // stored ids are never 0
+        if (nf < min_snv && nid != 0) {
+            col[(size_t)nf * TG] = nid;
+            nf++;
+        }
+        return false;
+    }
+};
+
 // one aligned base of a read at this lane's position: the SNV tally body of
 // GROM.c:6800-6992 (high-quality branch with read-name slots) and
 // GROM.c:6995-7040 (low-quality branch).  rb4 is the 4-bit code whose
 // character (bam_nt16_rev_table) equals the reference base, or 16 if none, so
 // `s4 == rb4` is the reference's `ref != read base` test negated; mv says the
 // reference base is one of ACGT.
-template <int NS>
-__device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, uint32_t (&slot)[NS],
+template <class SLOTS>
+__device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, SLOTS &slot,
                                            int min_snv, bool hq, bool mv, int q, int s4, int rb4, bool fwd, int qi,
                                            int lseq_mod, int mq, uint32_t nid) {
     if (s4 == rb4) {
@@ -149,22 +199,7 @@ __device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, uint32
     }
     const int code = acgt_code(s4);
     bool count = hq && code < 4;
-    if (hq) {
-        // first empty slot takes the name (names >= 50 chars are never
-        // stored); a slot holding the name marks the base as seen.  Written
-        // with selects so the slots stay in registers.
-        bool done = false, found = false;
-#pragma unroll
-        for (int s = 0; s < NS; s++) {
-            const bool active = !done && s < min_snv;
-            const bool empty = active && slot[s] == 0;
-            const bool match = active && !empty && slot[s] == nid;
-            slot[s] = (empty && nid != 0) ? nid : slot[s];
-            found = found || match;
-            done = done || empty || match;
-        }
-        count = count && !found;
-    }
+    if (hq) count = count && !slot.probe(nid, min_snv);
     const bool low = !hq && code < 4;
     const int32_t ch = count ? 1 : 0, cl = low ? 1 : 0;
     GROM_ADD4(c, snv, code, ch);
@@ -407,9 +442,10 @@ __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *_
 #endif
 #define GROM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GROM_WAVES_PER_EU)))
 
-// NS: read-name slots kept per position (>= -n; fewer slots, fewer VGPRs)
-template <int NS>
-__device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const grom_scan_args &a,
+// SLOTS: the read-name slots of the lane's position (RegSlots<NS> with
+// NS >= -n: fewer slots, fewer VGPRs; MemSlots for any -n)
+template <class SLOTS>
+__device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_t tile, const grom_scan_args &a,
                                                  const char *__restrict__ ref, const ReadArrays &R,
                                                  const ReadMeta *__restrict__ meta, const int32_t *__restrict__ tile_lo,
                                                  const int32_t *__restrict__ tile_hi, const PileOut &O,
@@ -442,9 +478,7 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, int64_t tile, const
     // soft-clip evidence per category (plain, ctx, indel) x side (L, R):
     // reads with mapq >= -q (each adds 6, GROM.c:5829-5836) and all reads
     int32_t sch[6] = {0, 0, 0, 0, 0, 0}, scn[6] = {0, 0, 0, 0, 0, 0};
-    uint32_t slot[NS];
-#pragma unroll
-    for (int k = 0; k < NS; k++) slot[k] = 0;
+    slot.reset();
 
     const uint4 *gq4 = reinterpret_cast<const uint4 *>(R.qual);
     const uint4 *gs4 = reinterpret_cast<const uint4 *>(R.seq);
@@ -789,7 +823,27 @@ __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args 
     const int64_t per_xcd = (n_tiles + 7) / 8;
     const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (tile >= n_tiles) return;  // whole workgroup leaves together
-    scan_tile_gather<NS>(L, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+    RegSlots<NS> slot;
+    scan_tile_gather(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+}
+
+// -n above the register builds: a fixed grid of workgroups, each walking
+// tiles blockIdx.x, blockIdx.x + gridDim.x, ... with its own slot columns in
+// `slots` ([gridDim.x][min_snv][GROM_TILE] uint32, sized by the host)
+__global__ __launch_bounds__(TG) void k_scan_tile_mem(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
+                                                     const ReadMeta *__restrict__ meta,
+                                                     const int32_t *__restrict__ tile_lo,
+                                                     const int32_t *__restrict__ tile_hi, PileOut O,
+                                                     const double *__restrict__ mq_tab,
+                                                     const double *__restrict__ hez_tab, int64_t n_tiles,
+                                                     uint32_t *__restrict__ slots) {
+    __shared__ ScanLds L;
+    MemSlots slot;
+    slot.col = slots + (size_t)blockIdx.x * a.min_snv * TG + threadIdx.x;
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        __syncthreads();  // the previous tile's LDS is no longer read
+        scan_tile_gather(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+    }
 }
 
 // ---- candidate runs in tile order: exclusive scan of run_cnt, then gather ----

@@ -225,7 +225,7 @@ struct Ctx {
     DevBuf r_pos, r_flag, r_mapq, r_mtid, r_mpos, r_isize, r_lq, r_coff, r_cig, r_boff, r_seq, r_qual, r_nid, ref;
     DevBuf r_aidx, r_aux, r_dpos, r_dlq, r_dbef;
     // scan scratch
-    DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, fpart;
+    DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, fpart, slots;
     grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
     const char *host_ref = nullptr;    // the caller's host reference during grom_scan_chrom
     // device-resident scans: the breakpoint rows read reference bases on the
@@ -300,12 +300,8 @@ struct Text {
 };
 
 static int check_params(const grom_params &p) {
-    if (p.min_snv > GROM_MAX_NAME_SLOTS) {
-        set_err("-n %d exceeds the %d read-name slots the kernel keeps per base", p.min_snv, GROM_MAX_NAME_SLOTS);
-        return GROM_E_ARG;
-    }
-    if (p.vcf != 1) {
-        set_err("-f (tab-separated output) is not supported by this build");
+    if (p.min_snv < 0) {
+        set_err("-n %d is negative", p.min_snv);
         return GROM_E_ARG;
     }
     if (p.half_one_base_rd_len <= 0) {
@@ -397,7 +393,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     // device-resident reference: its host copy for the breakpoint rows,
     // overlapped with the pileup on the copy stream
     bool ref_copy_pending = false;
-    if (!C.host_ref && P.vcf == 1) {
+    if (!C.host_ref) {
         if ((size_t)ch->len > C.h_ref_cap) {
             if (C.h_ref) (void)hipHostFree(C.h_ref);
             C.h_ref = nullptr;
@@ -477,10 +473,21 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
 #define GROM_LAUNCH_TILE(NSL)                                                                                    \
     hipLaunchKernelGGL(k_scan_tile<NSL>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra, (const ReadMeta *)C.meta.p, \
                        (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, n_tiles)
-        if (P.min_snv <= GROM_FEW_NAME_SLOTS) GROM_LAUNCH_TILE(GROM_FEW_NAME_SLOTS);
+        // (GROM_MEM_SLOTS=1, a test hook: the global-slot kernel for any -n)
+        static const bool force_mem_slots = getenv("GROM_MEM_SLOTS") && atoi(getenv("GROM_MEM_SLOTS")) == 1;
+        if (P.min_snv > GROM_MAX_NAME_SLOTS || force_mem_slots) {
+            // more slots than registers hold: slot columns in global scratch,
+            // one set per workgroup of a fixed grid that walks the tiles
+            const unsigned mg = (unsigned)std::min<int64_t>(n_tiles, GROM_MEM_SLOT_BLOCKS);
+            const size_t ns = (size_t)std::max(P.min_snv, 1);
+            if ((rc = ensure(C.slots, sizeof(uint32_t) * (size_t)mg * ns * GROM_TILE))) return rc;
+            hipLaunchKernelGGL(k_scan_tile_mem, dim3(mg), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
+                               (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
+                               C.d_mq, C.d_hez, n_tiles, (uint32_t *)C.slots.p);
+        } else if (P.min_snv <= GROM_FEW_NAME_SLOTS) GROM_LAUNCH_TILE(GROM_FEW_NAME_SLOTS);
         else if (P.min_snv <= 8) GROM_LAUNCH_TILE(8);
         else if (P.min_snv <= 16) GROM_LAUNCH_TILE(16);
-        else GROM_LAUNCH_TILE(32);
+        else GROM_LAUNCH_TILE(GROM_MAX_NAME_SLOTS);
 #undef GROM_LAUNCH_TILE
         hipLaunchKernelGGL(k_flush_reduce, dim3(256), dim3(256), 0, st, n_tiles,
                            (const unsigned long long *)C.fpart.p, d_facc);
@@ -567,11 +574,37 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             done += (size_t)thr;
         }
         fsegs.push_back({done, ncand - done, (double)(int64_t)facc[0] / (double)(int64_t)facc[1]});
+        // -f rows print cdp_lseq bases of reference context: the pending
+        // record's length at each mid-scan flush, the tail record's at the end
+        std::vector<int32_t> flush_lseq(fsegs.size(), ch->lseq_tail);
+        const char *tab_ref = nullptr;
+        if (P.vcf != 1) {
+            std::vector<int32_t> fpos;
+            for (size_t k = 0; k + 1 < fsegs.size(); k++) fpos.push_back(cands[fsegs[k].off + fsegs[k].n - 1].pos);
+            char serr[512] = {0};
+            if ((rc = sv_pending_lseq(st, P, svin, *ch, fpos.data(), (int)fpos.size(), flush_lseq.data(), serr,
+                                      sizeof(serr)))) {
+                set_err("%s", serr);
+                return rc;
+            }
+            tab_ref = C.host_ref;
+            if (!tab_ref) {
+                HIPCHK(hipEventSynchronize(C.ref_ev));
+                ref_copy_pending = false;
+                tab_ref = C.h_ref;
+            }
+        }
         std::string snv_text;
-        std::thread fmt([&P, ch, cands, &fsegs, &snv_text] {
-            for (const FlushSeg &f : fsegs) {
+        std::thread fmt([&P, ch, cands, &fsegs, &snv_text, &flush_lseq, tab_ref] {
+            for (size_t k = 0; k < fsegs.size(); k++) {
+                const FlushSeg &f = fsegs[k];
+                const double lim = round(P.snv_rd_min_factor * f.ave_rd);
+                if (tab_ref) {
+                    snv_rows_format_tab(P, ch->name, cands + f.off, f.n, lim, tab_ref, ch->len, flush_lseq[k], snv_text);
+                    continue;
+                }
                 std::vector<std::string> parts;
-                snv_rows_format(P, ch->name, cands + f.off, f.n, round(P.snv_rd_min_factor * f.ave_rd), parts);
+                snv_rows_format(P, ch->name, cands + f.off, f.n, lim, parts);
                 for (auto &part : parts) snv_text += part;
             }
         });
@@ -605,7 +638,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             }
             n_hits = nh;
             t_sv_eval = ms_since(t_start);
-            if (P.vcf == 1 && nh > 0) {
+            if (nh > 0) {
                 // the rows read reference bases (REF text, homopolymer runs):
                 // the caller's host copy when there is one, else the pinned
                 // copy made beside the pileup
@@ -820,7 +853,7 @@ void grom_dev_fini(int device) {
     DevBuf *all[] = {&C.r_pos, &C.r_flag, &C.r_mapq, &C.r_mtid, &C.r_mpos, &C.r_isize, &C.r_lq, &C.r_coff,
                      &C.r_cig, &C.r_boff, &C.r_seq, &C.r_qual, &C.r_nid, &C.ref, &C.keep, &C.meta, &C.cands2,
                      &C.runb, &C.runc, &C.segs, &C.fpart, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
-                     &C.misc, &C.dbg, &C.r_aidx, &C.r_aux, &C.r_dpos, &C.r_dlq, &C.r_dbef};
+                     &C.misc, &C.dbg, &C.slots, &C.r_aidx, &C.r_aux, &C.r_dpos, &C.r_dlq, &C.r_dbef};
     for (DevBuf *b : all)
         if (b->p) (void)hipFree(b->p);
     if (C.h_cands) (void)hipHostFree(C.h_cands);

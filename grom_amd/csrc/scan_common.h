@@ -13,7 +13,8 @@
 #define GROM_TILE_THREADS GROM_TILE
 /* read-name slots per position supported by the kernel (g_min_snv, -n);
  * the gather kernel is also built with GROM_FEW_NAME_SLOTS for -n up to that */
-#define GROM_MAX_NAME_SLOTS 32 /* largest -n: builds for 4, 8, 16 and 32 slots */
+#define GROM_MAX_NAME_SLOTS 32 /* register builds for 4, 8, 16 and 32 slots */
+#define GROM_MEM_SLOT_BLOCKS 2048 /* -n above 32: workgroups of the global-slot kernel */
 #define GROM_FEW_NAME_SLOTS 4
 
 /* order of the GROM_NCOUNT int32 per-base counters exported by

@@ -194,3 +194,37 @@ extern "C" int64_t grom_fmt_selftest(int64_t n, uint64_t seed) {
     }
     return bad;
 }
+
+void snv_rows_format_tab(const grom_params &P, const char *chr_name, const grom_snv_cand *c, size_t n, double lim,
+                         const char *ref, int64_t len, int32_t lseq, std::string &out) {
+    static const char dna[4] = {'A', 'C', 'G', 'T'};
+    char b[512];
+    for (size_t i = 0; i < n; i++) {
+        const grom_snv_cand &s = c[i];
+        const double ratio = (double)s.ratio;
+        if (!(s.rc_all <= lim || ratio >= P.high_cov_min_snv_ratio)) continue;
+        const int k = s.base;
+        // the two depth lists of this row are never written by the reference
+        // (GROM.c:3771-3778, malloc'ed and printed only): fresh pages read 0
+        int w = snprintf(b, sizeof b, "SNV\t%s\t%d\t%c\t%e\t%d\t%d", chr_name, s.pos, dna[k], ratio, 0, 0);
+        out.append(b, (size_t)w);
+        for (int j = 0; j < 4; j++) out.append(b, (size_t)snprintf(b, sizeof b, "\t%d", s.snv[j]));
+        for (int j = 0; j < 4; j++) out.append(b, (size_t)snprintf(b, sizeof b, "\t%d", s.lowmq[j]));
+        w = snprintf(b, sizeof b, "\t%d\t%d\t%d\t%d\t%d\t%d\t%d", s.bq, s.bq_all, s.mq, s.mq_all, s.bq_rc, s.mq_rc, s.rc_all);
+        out.append(b, (size_t)w);
+        const double pir = (double)s.pir[k] / (double)s.snv[k], fs = (double)s.fs[k] / (double)s.snv[k];
+        const bool inner = s.pos > 0 && s.pos < len - 1;
+        w = snprintf(b, sizeof b, "\t%.2f\t%.2f\t%c%c%c\t", pir, fs, inner ? ref[s.pos - 1] : '.', inner ? ref[s.pos] : '.',
+                     inner ? ref[s.pos + 1] : '.');
+        out.append(b, (size_t)w);
+        for (int32_t j = 0; j < lseq; j++) {
+            const int64_t x = (int64_t)s.pos - lseq + 1 + j;
+            out.push_back(x < 0 ? 'N' : ref[x]);
+        }
+        for (int32_t j = 0; j < lseq - 1; j++) {
+            const int64_t x = (int64_t)s.pos + lseq - 1 - j;
+            out.push_back(x >= len - 1 ? 'N' : ref[x]);
+        }
+        out.append(b, (size_t)snprintf(b, sizeof b, "\t%e\t%e\n", s.binom, s.hez));
+    }
+}

@@ -96,6 +96,11 @@ int sv_evaluate(SvScratch *S, hipStream_t st, const grom_params &P, const SvInpu
                 int32_t eval_lo, int32_t eval_hi, const double *d_mq, const double *d_hez, const SvHit **hits,
                 size_t *n_hits, double *ms_device, char *err, size_t errlen);
 
+// cdp_lseq at the evaluation of each base h_pos[0..n) (host arrays): the
+// length of the stream's next record not yet ingested there
+int sv_pending_lseq(hipStream_t st, const grom_params &P, const SvInput &in, const grom_chrom &ch,
+                    const int32_t *h_pos, int n, int32_t *h_out, char *err, size_t errlen);
+
 // test hooks: records of the last scan
 const grom_indel_rec *sv_indel_records(const SvScratch *S);
 int64_t sv_indel_count(const SvScratch *S);

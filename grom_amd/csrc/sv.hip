@@ -747,6 +747,13 @@ __device__ int32_t pending_lseq(const EvalIn &I, int32_t p) {
     return I.lseq_tail;
 }
 
+// cdp_lseq at the evaluation of each base in pos[] (the -f SNV rows print
+// that many bases of context at a mid-scan flush, GROM.c:11296-11316)
+__global__ void k_pending_lseq(EvalIn I, const int32_t *__restrict__ pos, int n, int32_t *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = pending_lseq(I, pos[i]);
+}
+
 __global__ void k_sv_eval(EvalIn I) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= I.n_ctx) return;
@@ -1188,6 +1195,25 @@ __global__ void k_hit_gather(const SvHit *__restrict__ h, const uint32_t *__rest
                              SvHit *__restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = h[idx[i]];
+}
+
+int sv_pending_lseq(hipStream_t st, const grom_params &P, const SvInput &in, const grom_chrom &ch,
+                    const int32_t *h_pos, int n, int32_t *h_out, char *err, size_t errlen) {
+    if (n <= 0) return GROM_OK;
+    EvalIn I{};
+    I.in = in;
+    I.lseq_tail = ch.lseq_tail;
+    I.Mx = P.insert_max_size;
+    I.overlap = P.overlap_mult;
+    int32_t *d = nullptr;
+    SCHK(hipMallocAsync((void **)&d, sizeof(int32_t) * 2 * (size_t)n, st));
+    SCHK(hipMemcpyAsync(d, h_pos, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_pending_lseq, dim3((n + 63) / 64), dim3(64), 0, st, I, (const int32_t *)d, n, d + n);
+    SCHK(hipGetLastError());
+    SCHK(hipMemcpyAsync(h_out, d + n, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipFreeAsync(d, st));
+    SCHK(hipStreamSynchronize(st));
+    return GROM_OK;
 }
 
 int sv_evaluate(SvScratch *S, hipStream_t st, const grom_params &P, const SvInput &in, const grom_chrom &ch,

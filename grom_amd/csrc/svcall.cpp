@@ -376,6 +376,14 @@ struct Out {
     }
 };
 
+// -f rows of the paired classes: DUP (GROM.c:15347), INV_F/INV_R (15947,
+// 16003), DEL (16564) -- raw counts, 0-based positions, the hez p-values
+static void pair_row_tab(Out &o, const char *chr, const char *type, const PairEnt &q) {
+    o.f("%s\t%s\t%d\t%d\t%6.2f\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%e\t%e\n", type, chr, q.start,
+        q.end, q.dist, q.binom_s, q.binom_e, q.cnt_s, q.cnt_e, q.rd_s, q.rd_e, q.conc_s, q.conc_e, q.other_s, q.other_e,
+        q.rs_s, q.re_s, q.rs_e, q.re_e, q.hez_s, q.hez_e);
+}
+
 static void pair_row(Out &o, const char *chr, const char *alt, const PairEnt &q) {
     o.f("%s\t%d\t.\t.\t%s\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT:SFR:SLR:EFR:ELR\t"
         "%e:%e:%.1f:%.1f:%d:%d:%d:%d:%d:%d:%d:%d:%d:%d\n",
@@ -474,6 +482,7 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
     const int64_t cap2 = P.sv_list2_len > 0 ? P.sv_list2_len : std::max<int64_t>(P.sv_list_len / 10, 1);
     const double pv = P.pval_threshold, ratio = P.min_sv_ratio * (double)AF;
     Out o{vcf};
+    const bool tab = P.vcf != 1;  // -f: tab-separated rows (g_vcf == 0)
     std::vector<PairEnt> l2[4];
     for (int k = 0; k < 4; k++) l2[k] = merge_pairs(L.pr[k], L.n_pr[k], cap2, Mx, glseq);
     mark();
@@ -482,7 +491,7 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
     for (const PairEnt &q : l2[PR_DUP])
         if ((q.binom_s <= pv || q.hez_s <= pv) && (q.binom_e <= pv || q.hez_e <= pv) &&
             (double)q.cnt_s / (double)q.rd_s >= ratio && (double)q.cnt_e / (double)q.rd_e >= ratio)
-            pair_row(o, chr, "<DUP>", q);
+            tab ? pair_row_tab(o, chr, "DUP", q) : pair_row(o, chr, "<DUP>", q);
 
     // INV rows: dropped when the other orientation overlaps with a smaller
     // p-value product, or when the depth at the two ends differs (GROM.c:15795-15890)
@@ -508,7 +517,8 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
             r1 = r1 / (q.re_s + glseq - q.rs_s);
             double r2 = in.caf_sum(in.u, q.rs_e, (int64_t)q.re_e + glseq);
             r2 = r2 / (q.re_e + glseq - q.rs_e);
-            if (!overlap && r1 / r2 <= P.max_inv_rd_diff && r2 / r1 <= P.max_inv_rd_diff) pair_row(o, chr, "<INV>", q);
+            if (!overlap && r1 / r2 <= P.max_inv_rd_diff && r2 / r1 <= P.max_inv_rd_diff)
+                tab ? pair_row_tab(o, chr, side == 0 ? "INV_F" : "INV_R", q) : pair_row(o, chr, "<INV>", q);
         }
     }
 
@@ -532,13 +542,19 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
                 i2.push_back(q);
             }
         }
-        for (const InsEnt &q : i2)
-            if (q.binom_s <= P.pval_insertion && q.binom_e <= P.pval_insertion &&
-                std::abs(q.end - q.start) <= P.max_ins_range)
+        for (const InsEnt &q : i2) {
+            if (!(q.binom_s <= P.pval_insertion && q.binom_e <= P.pval_insertion &&
+                  std::abs(q.end - q.start) <= P.max_ins_range))
+                continue;
+            if (tab)  // GROM.c:16091
+                o.f("INS\t%s\t%d\t%d\t\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\n", chr, q.start, q.end, q.binom_s, q.binom_e,
+                    q.ins_s, q.ins_e, q.rd_s, q.rd_e, q.conc_s, q.conc_e, q.other_s, q.other_e);
+            else
                 o.f("%s\t%d\t.\t.\t<INS>\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT\t"
                     "%e:%e:%.1f:%.1f:%d:%d:%d:%d:%d:%d\n",
                     chr, q.start + 1, q.start + 1, q.binom_s, q.binom_e, (double)q.ins_s / (double)AF,
                     (double)q.ins_e / (double)AF, q.rd_s, q.rd_e, q.conc_s, q.conc_e, q.other_s, q.other_e);
+        }
     }
 
     // CTX_F / CTX_R: merged and written raw for the translocation post-pass
@@ -590,6 +606,11 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
         }
         if (hp2 > hp) hp = hp2;
         if (hp > P.max_homopolymer) continue;
+        if (tab) {  // GROM.c:16342
+            o.f("INDEL_INS\t%s\t%d\t%d\t%d\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\n", chr, q.start, q.end, q.dist, q.binom,
+                q.hez, q.conc_s, q.conc_e, q.other_s, q.other_e, q.i, q.rd, q.sc, hp);
+            continue;
+        }
         char gts[SEQ_MAX + 8];
         if (q.dist <= SEQ_MAX) {
             memcpy(gts, q.seq, (size_t)std::max(q.dist, 0));
@@ -631,6 +652,12 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
         if (hp2 > hp) hp = hp2;
         if (hp > P.max_homopolymer) continue;
         const int cn = q.end - q.start + 1;
+        if (tab) {  // GROM.c:16490
+            o.f("INDEL_DEL\t%s\t%d\t%d\t%d\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%e\t%e\t%d\n", chr, q.start,
+                q.end, cn, q.binom_s, q.binom_e, q.conc_s, q.conc_e, q.other_s, q.other_e, q.f, q.r, q.rd_s, q.rd_e, q.sc_s,
+                q.sc_e, q.hez_s, q.hez_e, hp);
+            continue;
+        }
         if (cn > 0 && cn < 100 - 1) {
             std::string ref(fasta + q.start, (size_t)cn);
             o.f("%s\t%d\t.\t%s\t.\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT:SSC:ESC:HP\t"
@@ -652,7 +679,7 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
         if (!((q.binom_s <= pv || q.hez_s <= pv) && (q.binom_e <= pv || q.hez_e <= pv) &&
               (double)q.cnt_s / (double)q.rd_s >= ratio && (double)q.cnt_e / (double)q.rd_e >= ratio))
             continue;
-        if (!del_dropped(P, q, L, span)) pair_row(o, chr, "<DEL>", q);
+        if (!del_dropped(P, q, L, span)) tab ? pair_row_tab(o, chr, "DEL", q) : pair_row(o, chr, "<DEL>", q);
     }
     mark();
     if (timing)

@@ -1086,12 +1086,17 @@ static void cnv_chromosome(long len, const char *fa, const cnv_pre *pre, int *mq
                                  exp(-pow(x, 2)));
             pv[a] = (1.0 - erf_) / 2.0;
         }
+        /* -f: a column header before each kind's rows, GROM.c:17242-17245, 17378 */
+        if (g_vcf == 0) fprintf(vcf, "SV Type\tChromosome\tStart\tEnd\tStdev from mean\tP Value\tCopy Number\n");
         /* caf_old_*_list_index stays 0, so every passing call is written */
         for (a = 0; a < l->n; a++) {
             if (!(pv[a] < g_rd_pval_threshold)) continue;
             if (g_vcf == 1)
                 fprintf(vcf, "%s\t%ld\t.\t.\t%s\t.\t.\tEND=%ld\tSD:Z:CN:CS\t%e:%e:%.2f:%e\n", chr_name, l->start[a] + 1,
                         kind == 0 ? "<DEL>" : "<DUP>", l->end[a] + 1, l->stdev[a], pv[a], l->cn[a], l->cn_stdev[a]);
+            else /* GROM.c:17340-17343 (caf_del_text / caf_dup_text, GROM.c:1575-1576) */
+                fprintf(vcf, "%s\t%s\t%ld\t%ld\t%e\t%e\t%e\t%e\n", kind == 0 ? "DEL RD" : "DUP RD", chr_name, l->start[a],
+                        l->end[a], l->stdev[a], pv[a], l->cn[a], l->cn_stdev[a]);
         }
         free(pv);
     }

@@ -1076,7 +1076,7 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
     snv_flush(&sl, fasta, chr_len, s.caf_rd, s.caf_low, &last_group_pos, (long)p - idx, &rc_total, &base_total,
               chr_name, vcf, c->lseq);
     /* SV assembly and rows, GROM.c:15163-16580 */
-    if (g_vcf == 1) {
+    {
         sv_out_prm O = {g_insert_max_size, g_lseq, g_vcf, 0, g_pval_threshold, g_pval_insertion, g_min_sv_ratio,
                         g_min_indel_ratio, g_max_inv_rd_diff, g_min_overlap_ratio, g_max_homopolymer, g_max_ins_range};
         sv_write_rows(&O, &s.lists, chr_name, fasta, chr_len, s.caf_rd, s.caf_low, vcf, ctx_raw);
@@ -1119,6 +1119,50 @@ static void scan_chromosome(stream_t *st, cur_t *c, const char *target_name_of_m
 static void write_header(FILE *f, const char *fasta_file_name, int ctx);
 static const char *g_hdr_fasta = "";
 static void write_ctx_header(FILE *f) { write_header(f, g_hdr_fasta, 1); }
+/* -f: the insert statistics and the column header instead of the VCF
+ * header, GROM.c:20566-20671 */
+static const char TAB_COLUMNS[] =
+    "SV\tChromosome\tStart (Tumor)\tEnd (Tumor)\tLength (Tumor)\tP-val (Start, Tumor)\t"
+    "P-val (End, Tumor)\tConcordant Pairs (Start, Tumor)\tConcordant Pairs (End, Tumor)\t"
+    "Start or End?\tRead Depth (High MapQ, Normal)\tRead Depth (Low MapQ, Normal)\t"
+    "Concordant Pairs (Normal)\tINS (Normal)\tDEL (For, Normal)\tDEL (Rev, Normal)\t"
+    "DEL (For, Length, Normal)\tDEL (Rev, Length, Normal)\tDUP (Rev, Normal)\tDUP (For, Normal)\t"
+    "DUP (Rev, Length, Normal)\tDUP (For, Length, Normal)\tINV (For, Start, Normal)\t"
+    "INV (Rev, Start, Normal)\tINV (For, End, Normal)\tINV (Rev, End, Normal)\t"
+    "INV (For, Start, Length, Normal)\tINV (Rev, Start, Length, Normal)\t"
+    "INV (For, End, Length, Normal)\tINV (Rev, End, Length, Normal)\tUnmapped Mate (For, Normal)\t"
+    "Unmapped Mate (Rev, Normal)\tSoft-clipping (Left, Normal)\tSoft-clipping (Right, Normal)\t"
+    "Soft-clipping Read Depth (Left, Normal)\tSoft-clipping Read Depth (Right, Normal)\t"
+    "Soft-clipping Read Depth (Left+Right, Normal)\tINS Indel (Normal)\tDEL Indel (Start, Normal)\t"
+    "DEL Indel (End, Normal)\tDEL Indel (Start, Length, Normal)\tDEL Indel (End, Length, Normal)\t"
+    "CTX Soft-clipping (Left, Normal)\tCTX Soft-clipping (Right, Normal)\t"
+    "CTX Soft-clipping Read Depth (Left, Normal)\tCTX Soft-clipping Read Depth (Right, Normal)\t"
+    "CTX Soft-clipping Read Depth (Left+Right, Normal)\tIndel Soft-clipping (Left, Normal)\t"
+    "Indel Soft-clipping (Right, Normal)\tIndel Soft-clipping Read Depth (Left, Normal)\t"
+    "Indel Soft-clipping Read Depth (Right, Normal)\t"
+    "Indel Soft-clipping Read Depth (Left+Right, Normal)\t"
+    "Soft-clipping (Left Max including CTX, Normal)\t"
+    "Soft-clipping (Right Max including CTX, Normal)\tOther (Number of Non-Empty, Normal)\t"
+    "CTX (For, Normal)\tCTX (Rev, Normal)\tSV Overlap (Normal)\tOther (Number of Non-Empty, Tumor)\t"
+    "Read Start (Start, Tumor)\tRead End (Start, Tumor)\tRead Start (End, Tumor)\t"
+    "Read End (End, Tumor)\tDEL Read Start (For/Rev, Normal)\tDEL Read End (For/Rev, Normal)\t"
+    "DUP Read Start (Rev/For, Normal)\tDUP Read End (Rev/For, Normal)\tINV Read Start (For, Normal)\t"
+    "INV Read End (For, Normal)\tINV Read Start (Rev, Normal)\tINV Read End (Rev, Normal)\t"
+    "CTX Read Start (For, Normal)\tCTX Read End (For, Normal)\tCTX Read Start (Rev, Normal)\t"
+    "CTX Read End (Rev, Normal)\tMate Chr (CTX only, Tumor)\tMate Pos (CTX only, Tumor)\t"
+    "Mate Chr (For, Normal)\tMate Pos (For, Normal)\tMate Chr (Rev, Normal)\tMate Pos (Rev, Normal)\t"
+    "Reference Base\tSNV Base (Tumor)\tSNV Ratio (Tumor)\tSNV Count (A, Tumor)\t"
+    "SNV Count (C, Tumor)\tSNV Count (G, Tumor)\tSNV Count (T, Tumor)\tSNV Count (A, Normal)\t"
+    "SNV Count (C, Normal)\tSNV Count (G, Normal)\tSNV Count (T, Normal)\t\n";
+static void write_tab_header(FILE *f) {
+    fprintf(f, "%d\t%d\t%d\t%d\n", g_insert_mean, g_insert_min_size, g_insert_max_size, g_lseq);
+    fputs(TAB_COLUMNS, f);
+}
+/* -f: the trimmed .ctx file's column header, GROM.c:22652-22700 */
+static void write_ctx_tab_header(FILE *f) {
+    fprintf(f, "SV\tChromosome\tStart\tID\tMate ID\tBinom Prob (Start)\tCTX evidence\tRead Depth (High MapQ)\t"
+               "Concordant Pairs\tOther (Number of Non-Empty)\tMate Chr\tMate Pos\tRead Start\tRead End\tHez binom prob\n");
+}
 static void write_header(FILE *f, const char *fasta_file_name, int ctx) {
     const char *pin = getenv("GROM_FILEDATE");
     fprintf(f, "##fileformat=VCFv4.2\n");
@@ -1274,9 +1318,8 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
     else
         snprintf(ctx_name, sizeof(ctx_name), "%s.ctx", results_file_name);
     FILE *ctx = fopen(ctx_name, "w");
-    if (g_vcf == 1) {
-        write_header(vcf, fasta_file_name, 0);
-    }
+    if (g_vcf == 1) write_header(vcf, fasta_file_name, 0);
+    else write_tab_header(vcf);
 
     build_pval2sd(); /* GROM.c:20705-20748 */
     /* test hook: a smaller sample-list cap makes the reservoir draws of
@@ -1371,7 +1414,8 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
          * and rewrite the file with its header */
         fclose(ctx);
         g_hdr_fasta = fasta_file_name;
-        if (g_vcf == 1) sv_ctx_postpass(ctx_name, names_lc, n_targets, g_insert_max_size, g_lseq, write_ctx_header);
+        sv_ctx_postpass(ctx_name, names_lc, n_targets, g_insert_max_size, g_lseq,
+                        g_vcf == 1 ? write_ctx_header : write_ctx_tab_header, g_vcf);
     }
     for (int a = 0; a < n_targets; a++) free(names_lc[a]);
     free(names_lc);

@@ -1127,6 +1127,14 @@ static void pr_row(FILE *f, const char *chr, const char *alt, const pr_ent *q) {
             q->rs_s + 1, q->re_s + 1, q->rs_e + 1, q->re_e + 1);
 }
 
+/* -f rows of the paired classes: DUP (GROM.c:15347), INV_F/INV_R
+ * (15947, 16003), DEL (16564) */
+static void pr_row_tab(FILE *f, const char *type, const char *chr, const pr_ent *q) {
+    fprintf(f, "%s\t%s\t%d\t%d\t%6.2f\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%e\t%e\n", type, chr,
+            q->start, q->end, q->dist, q->binom_s, q->binom_e, q->cnt_s, q->cnt_e, q->rd_s, q->rd_e, q->conc_s, q->conc_e,
+            q->other_s, q->other_e, q->rs_s, q->re_s, q->rs_e, q->re_e, q->hez_s, q->hez_e);
+}
+
 static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, const char *fasta, long chr_len,
                           const int32_t *caf_rd, const int32_t *caf_low, FILE *vcf, FILE *ctx) {
     const int AF = SV_AF;
@@ -1143,7 +1151,7 @@ static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, con
         if ((q->binom_s <= O->pval || q->hez_s <= O->pval) && (q->binom_e <= O->pval || q->hez_e <= O->pval) &&
             (double)q->cnt_s / (double)q->rd_s >= O->min_sv_ratio * (double)AF &&
             (double)q->cnt_e / (double)q->rd_e >= O->min_sv_ratio * (double)AF)
-            pr_row(vcf, chr, "<DUP>", q);
+            O->vcf ? pr_row(vcf, chr, "<DUP>", q) : pr_row_tab(vcf, "DUP", chr, q);
     }
     /* INV rows: each orientation is dropped when the other one overlaps it
      * with a smaller p-value product, or when the depth at the two ends
@@ -1170,7 +1178,8 @@ static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, con
                 r1 = r1 / (q->re_s + O->glseq - q->rs_s);
                 double r2 = sv_caf_sum(caf_rd, caf_low, chr_len, q->rs_e, (long)q->re_e + O->glseq);
                 r2 = r2 / (q->re_e + O->glseq - q->rs_e);
-                if (overlap == 0 && r1 / r2 <= O->max_inv_rd_diff && r2 / r1 <= O->max_inv_rd_diff) pr_row(vcf, chr, "<INV>", q);
+                if (overlap == 0 && r1 / r2 <= O->max_inv_rd_diff && r2 / r1 <= O->max_inv_rd_diff)
+                    O->vcf ? pr_row(vcf, chr, "<INV>", q) : pr_row_tab(vcf, side == 0 ? "INV_F" : "INV_R", chr, q);
             }
         }
     }
@@ -1197,7 +1206,11 @@ static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, con
         }
         for (int a = 0; a < n; a++) {
             const ins_ent *q = &i2[a];
-            if (q->binom_s <= O->pval_ins && q->binom_e <= O->pval_ins && abs(q->end - q->start) <= O->max_ins_range)
+            if (!(q->binom_s <= O->pval_ins && q->binom_e <= O->pval_ins && abs(q->end - q->start) <= O->max_ins_range)) continue;
+            if (!O->vcf) /* GROM.c:16091 */
+                fprintf(vcf, "INS\t%s\t%d\t%d\t\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\n", chr, q->start, q->end, q->binom_s,
+                        q->binom_e, q->ins_s, q->ins_e, q->rd_s, q->rd_e, q->conc_s, q->conc_e, q->other_s, q->other_e);
+            else
                 fprintf(vcf, "%s\t%d\t.\t.\t<INS>\t.\t.\tEND=%d\tSPR:EPR:SEV:EEV:SRD:ERD:SCO:ECO:SOT:EOT\t%e:%e:%.1f:%.1f:%d:%d:%d:%d:%d:%d\n",
                         chr, q->start + 1, q->start + 1, q->binom_s, q->binom_e, (double)q->ins_s / (double)AF,
                         (double)q->ins_e / (double)AF, q->rd_s, q->rd_e, q->conc_s, q->conc_e, q->other_s, q->other_e);
@@ -1255,6 +1268,11 @@ static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, con
         }
         if (hp2 > hp) hp = hp2;
         if (hp > O->max_homopolymer) continue;
+        if (!O->vcf) { /* GROM.c:16342 */
+            fprintf(vcf, "INDEL_INS\t%s\t%d\t%d\t%d\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\n", chr, q->start, q->end, q->dist,
+                    q->binom, q->hez, q->conc_s, q->conc_e, q->other_s, q->other_e, q->i, q->rd, q->sc, hp);
+            continue;
+        }
         if (q->dist <= SV_OTHER) {
             for (int b = 0; b < q->dist; b++) gts[b] = q->seq[b];
             gts[q->dist] = 0;
@@ -1328,6 +1346,12 @@ static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, con
         if (hp2 > hp) hp = hp2;
         if (hp > O->max_homopolymer) continue;
         int cn = q->end - q->start + 1;
+        if (!O->vcf) { /* GROM.c:16490 */
+            fprintf(vcf, "INDEL_DEL\t%s\t%d\t%d\t%d\t%e\t%e\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%d\t%e\t%e\t%d\n", chr,
+                    q->start, q->end, cn, q->binom_s, q->binom_e, q->conc_s, q->conc_e, q->other_s, q->other_e, q->f, q->r,
+                    q->rd_s, q->rd_e, q->sc_s, q->sc_e, q->hez_s, q->hez_e, hp);
+            continue;
+        }
         if (cn > 0 && cn < 100 - 1) {
             for (int b = 0; b < cn; b++) gts[b] = fasta[q->start + b];
             gts[cn] = 0;
@@ -1378,7 +1402,7 @@ static void sv_write_rows(const sv_out_prm *O, sv_lists *L, const char *chr, con
                 }
             }
         }
-        if (overlap == 0) pr_row(vcf, chr, "<DEL>", q);
+        if (overlap == 0) O->vcf ? pr_row(vcf, chr, "<DEL>", q) : pr_row_tab(vcf, "DEL", chr, q);
     }
     for (int k = 0; k < 4; k++) free(l2[k]);
 }
@@ -1394,7 +1418,7 @@ typedef struct {
 } ctx_row;
 
 static void sv_ctx_postpass(const char *ctx_path, char **bam_names_lc, int n_targets, int Mx, int glseq,
-                            void (*header)(FILE *)) {
+                            void (*header)(FILE *), int vcf) {
     FILE *f = fopen(ctx_path, "r");
     if (!f) return;
     int cap = 1024, n = 0;
@@ -1466,6 +1490,12 @@ static void sv_ctx_postpass(const char *ctx_path, char **bam_names_lc, int n_tar
         n2++;
         char bnd[64];
         const char *mn = (q->mchr >= 0 && q->mchr < n_targets) ? bam_names_lc[q->mchr] : "";
+        if (!vcf) { /* GROM.c:22734 (g_sv_types[6] = "CTX_F", [7] = "CTX_R", GROM.c:867) */
+            fprintf(f, "%s\t%s\t%d\t%d\t%d\t%e\t%.1f\t%d\t%d\t%d\t%s\t%d\t%d\t%d\t%e\n", q->type == 6 ? "CTX_F" : "CTX_R",
+                    (q->chr >= 0 && q->chr < n_targets) ? bam_names_lc[q->chr] : "", q->pos, b, q->mateid, q->binom, q->ev,
+                    q->rd, q->conc, q->other, mn, q->mpos, q->rs, q->re, q->hez);
+            continue;
+        }
         if (q->type == 6 && q->mpos < 0) snprintf(bnd, sizeof(bnd), "N[%s:%d[", mn, abs(q->mpos));
         else if (q->type == 6 && q->mpos >= 0) snprintf(bnd, sizeof(bnd), "N]%s:%d]", mn, abs(q->mpos));
         else if (q->type == 7 && q->mpos < 0) snprintf(bnd, sizeof(bnd), "[%s:%d[N", mn, abs(q->mpos));

@@ -28,6 +28,10 @@ RUNS = [
     ("dups", ["-n", "6", "-a", "0.1"]),  # -n above 4: the 8-slot build of the gather kernel
     ("dups", ["-n", "12", "-a", "0.05"]),  # the 16-slot build
     ("c5_tetra_male", ["-n", "20", "-a", "0.05", "-p", "4"]),  # the 32-slot build at 60x
+    # -n above 32: slot columns in global memory (k_scan_tile_mem); at 60x the
+    # homozygous sites fill all 40 slots
+    ("c5_tetra_male", ["-n", "40", "-a", "0.05", "-p", "4"]),
+    ("dups", ["-n", "100", "-a", "0.01"]),
     ("indels", []),
     ("indels", ["-M"]),
     ("indels", ["-q", "10"]),
@@ -46,6 +50,13 @@ RUNS = [
     ("sv_many", []),
     ("c1s", []),
     ("c1s", ["-V", "1", "-n", "2"]),
+    # -f tab-separated rows (g_vcf == 0): SNV rows with their reference
+    # context, every breakpoint class, CNV rows under their column headers,
+    # the CTX post-pass table; -G 40 adds mid-scan SNV flushes (cdp_lseq of
+    # the pending record)
+    ("sv", ["-f"]),
+    ("c3_genome", ["-M", "-V", "1", "-f"]),
+    ("one_chr", ["-G", "40", "-f"]),
 ]
 
 # read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call
@@ -124,6 +135,15 @@ def _check_counters(datadir, case, extra, tag, env_extra=None):
     assert ov.count("\n") > 46
     assert ov == gv
     assert filecmp.cmp(datadir / f"o_{tag}.ctx.vcf", datadir / f"g_{tag}.ctx.vcf", shallow=False)
+    if "-f" in extra:
+        # tab rows: every class named in its first column
+        kinds = {l.split("\t")[0] for l in gv.splitlines()[2:]}
+        assert "SNV" in kinds, kinds
+        if case == "sv":
+            assert {"DEL", "DUP", "INV_F", "INDEL_INS", "INDEL_DEL"} <= kinds, kinds
+        if "-V" in extra:
+            assert {"SV Type", "DEL RD", "DUP RD"} <= kinds, kinds
+        return
     if case in ("sv", "sv_many"):
         # the comparison covered every breakpoint row class
         alts = [l.split("\t")[4] for l in gv.splitlines() if not l.startswith("#")]
@@ -146,6 +166,31 @@ def _check_counters(datadir, case, extra, tag, env_extra=None):
 @pytest.mark.parametrize("case,extra", RUNS, ids=[f"{c}{''.join(e)}" for c, e in RUNS])
 def test_counters_and_vcf_bit_exact(datadir, case, extra):
     _check_counters(datadir, case, extra, f"{case}{''.join(extra).replace('-', '_')}")
+
+
+@pytest.mark.parametrize("case,extra", [("dups", ["-n", "3"]), ("c5_tetra_male", ["-n", "20", "-a", "0.05", "-p", "4"])],
+                         ids=["dups-n3", "tetra-n20"])
+def test_global_name_slots_forced(datadir, case, extra):
+    """The global-slot kernel (built for -n above 32) forced at small -n, where
+    the register builds also run: both must equal the oracle."""
+    _check_counters(datadir, case, extra, "memslots" + "".join(extra), env_extra={"GROM_MEM_SLOTS": "1"})
+
+
+def test_tab_output_names(datadir):
+    """-f with an output name without .vcf: rows in OUT, the translocation
+    table in OUT.ctx (GROM.c:20494-20505, 22446-22460)."""
+    bam, fa = synth(datadir, "sv", CASES["sv"])
+    run_oracle(datadir, bam, fa, "o_tabnames.txt", ["-f"])
+    run_grom(datadir, bam, fa, "g_tabnames.txt", ["-f"])
+    for suffix in ("", ".ctx"):
+        o = open(datadir / f"o_tabnames.txt{suffix}").read()
+        g = open(datadir / f"g_tabnames.txt{suffix}").read()
+        assert o == g, suffix
+        assert o.count("\n") > 1
+    rows = open(datadir / "g_tabnames.txt").read().splitlines()
+    assert rows[1].startswith("SV\tChromosome\t")
+    kinds = {l.split("\t")[0] for l in rows[2:]}
+    assert {"SNV", "DEL", "DUP", "INDEL_INS", "INDEL_DEL"} <= kinds, kinds
 
 
 def test_breakpoint_context_buffer_retry(datadir):
