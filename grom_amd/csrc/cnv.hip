@@ -37,6 +37,7 @@
 // redone in base order on the host when the bound cannot decide.
 
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <thread>
 
@@ -81,7 +82,7 @@ constexpr int MAX_BLOCK_LIST = 10000;      // max_block_list_len, GROM.c:633
 
 constexpr int GC_TP = 16384;               // positions per k_cnv_gc tile
 constexpr int GC_MMAX_S = 1536;            // k_cnv_gc<GC_MMAX_S>: 32-bit window arithmetic
-constexpr int GC_MMAX = 16384;             // largest insert mean: k_cnv_gc<GC_MMAX>, 64-bit (a 25 KB LDS halo)
+constexpr int GC_MMAX = 16384;             // k_cnv_gc<GC_MMAX>: 64-bit, a 25 KB LDS halo; above, k_cnv_gc_global
 template <int MMAX>
 constexpr int gc_nw() { return (GC_TP + 2 * MMAX + 1 + 63) / 64; }  // 64-bit class words per tile (with halo)
 constexpr int SEG_W = 4096;                // positions per wave in the state scans
@@ -2769,6 +2770,7 @@ struct CnvScratch {
     Buf zover;  // repeat z overrides: positions then values
     Buf cwords, cw_seg, cw_carry, wsdmin;  // candidate classification: bit words, their class carry, min wsd per 64
     Buf gen1000;                           // the -N side file's per-window results
+    Buf gpre, gtmp;                        // insert means above GC_MMAX: chromosome-wide GC/ACGT prefixes
     Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -2951,6 +2953,53 @@ static int cnv_init(CnvScratch *S, char *err, size_t errlen) {
     return GROM_OK;
 }
 
+// Insert means above GC_MMAX (the tile kernel's LDS halo): the same closed
+// form over chromosome-wide prefixes in global memory.  k_cnv_gc_marks writes
+// per base the GC and ACGT class bits and their positions (4 int64 arrays of
+// len+1, the last entry 0); exclusive scans turn them into P and R; then
+// T(p) = Q[p+m+1] - 2 Q[p+1] + Q[p-m+1], Q[x] = (x-1) P[x] - R[x], with
+// positions past either end holding no class bits, as in k_cnv_gc.
+__global__ void k_cnv_gc_marks(const char *__restrict__ ref, int64_t len, int64_t *__restrict__ pre) {
+    const int64_t n = len + 1;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int c = q < len ? gc_class(ref[q]) : 0;
+        pre[q] = c & 1;
+        pre[n + q] = (c & 1) ? q : 0;
+        pre[2 * n + q] = (c >> 1) & 1;
+        pre[3 * n + q] = (c & 2) ? q : 0;
+    }
+}
+
+__global__ void k_cnv_gc_global(const char *__restrict__ ref, Args A, int64_t m, int64_t total,
+                                const int64_t *__restrict__ pre, uint8_t *__restrict__ gcw,
+                                uint8_t *__restrict__ acw, uint8_t *__restrict__ rtype) {
+    const int64_t n = A.len + 1;
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < A.len; p += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t w2[2] = {0, 0}, rt = 10;
+        if (p >= A.lo && p < A.hi) {
+            const int64_t xs[3] = {p + m + 1, p + 1, p - m + 1};
+#pragma unroll
+            for (int pl = 0; pl < 2; pl++) {
+                const int64_t *P = pre + (2 * pl) * n, *R = pre + (2 * pl + 1) * n;
+                int64_t Qv[3];
+#pragma unroll
+                for (int t = 0; t < 3; t++) {
+                    const int64_t x = xs[t];
+                    const int64_t xc = x < 0 ? 0 : (x > A.len ? A.len : x);
+                    const int64_t Pv = x < 0 ? 0 : P[xc], Rv = x < 0 ? 0 : R[xc];
+                    Qv[t] = (x - 1) * Pv - Rv;
+                }
+                const uint64_t Tv = (uint64_t)(Qv[0] - 2 * Qv[1] + Qv[2]);
+                w2[pl] = (uint32_t)((100u * Tv / (uint64_t)total) & 255u);
+            }
+            rt = (uint32_t)pair_type(ref[p], ref[p + 1]);
+        }
+        gcw[p] = (uint8_t)w2[0];
+        acw[p] = (uint8_t)w2[1];
+        rtype[p] = (uint8_t)rt;
+    }
+}
+
 // GC/ACGT weights and dinucleotide classes depend on the reference alone
 // (GROM.c:1586-1881), so the scan driver starts them before the pileup on a
 // stream of their own; cnv_chrom then only waits for them.
@@ -2959,7 +3008,7 @@ int cnv_prelaunch(CnvScratch *S, hipStream_t after, const grom_params &P, const 
     int rc;
     S->gc_ref = nullptr;
     const int64_t m = P.insert_mean;
-    if (m < 1 || m > GC_MMAX || len <= 0) return GROM_OK;  // cnv_chrom reports it
+    if (m < 1 || m > GC_MMAX || len <= 0) return GROM_OK;  // cnv_chrom builds these itself
     if ((rc = cnv_init(S, err, errlen))) return rc;
     if ((rc = grow(S->gcw, len, err, errlen)) || (rc = grow(S->acw, len, err, errlen)) ||
         (rc = grow(S->rtype, len, err, errlen)))
@@ -2987,7 +3036,7 @@ void cnv_scratch_free(CnvScratch *S) {
                   &S->prepos, &S->ppos, &S->rep, &S->misc, &S->blk, &S->hist,
                   &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
                   &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover, &S->cwords, &S->cw_seg,
-                  &S->cw_carry, &S->wsdmin, &S->gen1000};
+                  &S->cw_carry, &S->wsdmin, &S->gen1000, &S->gpre, &S->gtmp};
     for (Buf *b : all)
         if (b->p) (void)hipFree(b->p);
     for (KindBufs &K : S->kb) {
@@ -3010,8 +3059,8 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     int rc;
     const int64_t m = P.insert_mean, W = 2 * (int64_t)m - 1;
     const int64_t total_w = (int64_t)m * m;  // g_one_base_window_size_total, GROM.c:22265-22269
-    if (m < 1 || m > GC_MMAX) {
-        snprintf(err, errlen, "insert mean %lld outside the CNV kernels' range 1..%d", (long long)m, GC_MMAX);
+    if (m < 1) {
+        snprintf(err, errlen, "insert mean %lld below 1", (long long)m);
         return GROM_E_ARG;
     }
     // (window lengths index int32 positions in the walk; -X past a chromosome
@@ -3070,6 +3119,20 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     // driver prelaunched them for this reference) ----
     if (S->gc_ref == d_ref && S->gc_len == len && S->gc_m == m) {
         CK(hipStreamWaitEvent(st, S->gc_done, 0));
+    } else if (m > GC_MMAX) {
+        const int64_t n = len + 1;
+        size_t tb = 0;
+        int64_t *pre = nullptr;
+        CK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, pre, pre, (int)n, st));
+        if ((rc = grow(S->gpre, sizeof(int64_t) * 4 * (size_t)n, err, errlen)) || (rc = grow(S->gtmp, tb, err, errlen)))
+            return rc;
+        pre = (int64_t *)S->gpre.p;
+        hipLaunchKernelGGL(k_cnv_gc_marks, dim3(8192), dim3(256), 0, st, d_ref, len, pre);
+        CK(hipGetLastError());
+        for (int k = 0; k < 4; k++) CK(hipcub::DeviceScan::ExclusiveSum(S->gtmp.p, tb, pre + k * n, pre + k * n, (int)n, st));
+        hipLaunchKernelGGL(k_cnv_gc_global, dim3(8192), dim3(256), 0, st, d_ref, A, m, total_w, (const int64_t *)pre, gcw,
+                           acw, rtype);
+        CK(hipGetLastError());
     } else {
         hipLaunchKernelGGL(m <= GC_MMAX_S ? k_cnv_gc<GC_MMAX_S> : k_cnv_gc<GC_MMAX>, dim3((unsigned)((len + GC_TP - 1) / GC_TP)), dim3(256), 0, st, d_ref, A, (int)m,
                            total_w, gcw, acw, rtype);

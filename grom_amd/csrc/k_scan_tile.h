@@ -40,8 +40,20 @@ struct ReadMeta {
     uint4 a, b, c;
 };
 
+// Bits of ReadMeta.b.z above mapq | keep << 8.  k_prep sets MK_FAST (one
+// M/=/X op of l_qseq bases inside the chromosome, kept), MK_REV (reverse
+// strand) and MK_HQ (mapq >= -m, the reference's high-quality read test);
+// the staging step sets DIFFED on the MK_FAST reads it staged: their caf and
+// depth intervals went to the difference arrays, and the fold takes them on
+// the fast path, which only tallies each one's base at the lane.
+#define DIFFED (1u << 16)
+#define MK_REV (1u << 17)
+#define MK_HQ (1u << 18)
+#define MK_FAST (1u << 19)
+
 // k_prep: one record per read, and the tile halo (max ext - pos)
-__global__ void k_prep(int64_t n, ReadArrays R, ReadMeta *__restrict__ meta, int32_t *__restrict__ halo) {
+__global__ void k_prep(int64_t n, ReadArrays R, ReadMeta *__restrict__ meta, int32_t *__restrict__ halo,
+                       int64_t clen, int32_t min_mapq) {
     int32_t best = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t cb = R.cig_off[i], ce = R.cig_off[i + 1];
@@ -60,9 +72,17 @@ __global__ void k_prep(int64_t n, ReadArrays R, ReadMeta *__restrict__ meta, int
         best = max(best, span);
         const int64_t bo = R.base_off[i];
         const uint32_t keep = R.keep ? R.keep[i] : 1u;
+        const uint32_t mq = R.mapq[i], fl = R.flag[i];
+        // the fast path's candidates: one M/=/X op of l_qseq bases inside the
+        // chromosome, kept (the staging step makes them DIFFED)
+        const uint32_t op0 = ce - cb == 1 ? (R.cigar[cb] & 15u) : 15u;
+        const bool fast = ce - cb == 1 && (op0 == 0 || op0 == 7 || op0 == 8) && keep && s == lq && p >= 0 &&
+                          (int64_t)s < clen - p;
         ReadMeta m;
         m.a = make_uint4((uint32_t)p, (uint32_t)(p + span), (uint32_t)lq, R.name_id[i]);
-        m.b = make_uint4(cb, (ce - cb) | ((uint32_t)R.flag[i] << 16), (uint32_t)R.mapq[i] | (keep << 8),
+        m.b = make_uint4(cb, (ce - cb) | (fl << 16),
+                         mq | (keep << 8) | (fast ? MK_FAST : 0u) | ((fl & 0x10u) ? MK_REV : 0u) |
+                             (mq >= (uint32_t)min_mapq ? MK_HQ : 0u),
                          (uint32_t)(bo & 0xffffffffu));
         m.c = make_uint4((uint32_t)((uint64_t)bo >> 32), (uint32_t)R.mtid[i], (uint32_t)R.mpos[i],
                          (uint32_t)R.isize[i]);
@@ -81,8 +101,8 @@ struct TileTail {
 
 struct __align__(16) ScanLds {
     ReadMeta meta[RCHUNK];
-    uint4 qual[QV];
-    uint4 seq[SV];
+    uint4 qual[QV + 1];  // + a slot the clamped loads past the window are stored to
+    uint4 seq[SV + 1];
     uint32_t cig[CIGCAP];
     char ref[TG];
     TileTail tail;
@@ -94,8 +114,7 @@ struct __align__(16) ScanLds {
     int32_t dmq[TG + 1];
     uint32_t dcnt[TG + 1];
 };
-// G.mk bit: the read's caf and depth intervals went to the difference arrays
-#define DIFFED (1u << 16)
+
 // tiles with more reads than this keep the per-lane interval updates (the
 // packed 16-bit caf counts could overflow)
 #define DIFF_MAX_READS 30000
@@ -113,6 +132,71 @@ struct LaneCounts {
         cnt.f##2 += ((code) == 2) ? (v) : 0; \
         cnt.f##3 += ((code) == 3) ? (v) : 0; \
     } while (0)
+
+// The same counters with the per-code counts (snv, fs, low) kept as 16-bit
+// pairs: fewer registers for the tile kernel.  Each count is bounded by the
+// position's depth, hence by the tile's read count; tiles with more than
+// PACK_MAX_READS reads go to the unpacked kernel (k_scan_tile_mem).
+#define PACK_MAX_READS 65535
+struct PackedCounts {
+    uint32_t snv01, snv23, fs01, fs23, low01, low23;
+    int32_t pir0, pir1, pir2, pir3;
+    int32_t bq_hi, mq_hi, bq_lo, mq_lo;
+};
+
+// per-code adds of one base (or of the matched-base totals): code 0..3, or 4
+// (not ACGT: nothing)
+__device__ __forceinline__ void add_codes(LaneCounts &c, int code, int32_t snv, int32_t fs, int32_t pir, int32_t low) {
+    GROM_ADD4(c, snv, code, snv);
+    GROM_ADD4(c, fs, code, fs);
+    GROM_ADD4(c, pir, code, pir);
+    GROM_ADD4(c, low, code, low);
+}
+__device__ __forceinline__ void add_codes(PackedCounts &c, int code, int32_t snv, int32_t fs, int32_t pir, int32_t low) {
+    const uint32_t sh = (code & 1) ? 16u : 0u;
+    const bool lo2 = code < 2, hi2 = code >= 2 && code < 4;
+    c.snv01 += lo2 ? ((uint32_t)snv << sh) : 0u;
+    c.snv23 += hi2 ? ((uint32_t)snv << sh) : 0u;
+    c.fs01 += lo2 ? ((uint32_t)fs << sh) : 0u;
+    c.fs23 += hi2 ? ((uint32_t)fs << sh) : 0u;
+    c.low01 += lo2 ? ((uint32_t)low << sh) : 0u;
+    c.low23 += hi2 ? ((uint32_t)low << sh) : 0u;
+    c.pir0 += (code == 0) ? pir : 0;
+    c.pir1 += (code == 1) ? pir : 0;
+    c.pir2 += (code == 2) ? pir : 0;
+    c.pir3 += (code == 3) ? pir : 0;
+}
+__device__ __forceinline__ LaneCounts unpack(const LaneCounts &c) { return c; }
+__device__ __forceinline__ LaneCounts unpack(const PackedCounts &c) {
+    LaneCounts u;
+    u.snv0 = (int32_t)(c.snv01 & 0xffffu); u.snv1 = (int32_t)(c.snv01 >> 16);
+    u.snv2 = (int32_t)(c.snv23 & 0xffffu); u.snv3 = (int32_t)(c.snv23 >> 16);
+    u.fs0 = (int32_t)(c.fs01 & 0xffffu); u.fs1 = (int32_t)(c.fs01 >> 16);
+    u.fs2 = (int32_t)(c.fs23 & 0xffffu); u.fs3 = (int32_t)(c.fs23 >> 16);
+    u.low0 = (int32_t)(c.low01 & 0xffffu); u.low1 = (int32_t)(c.low01 >> 16);
+    u.low2 = (int32_t)(c.low23 & 0xffffu); u.low3 = (int32_t)(c.low23 >> 16);
+    u.pir0 = c.pir0; u.pir1 = c.pir1; u.pir2 = c.pir2; u.pir3 = c.pir3;
+    u.bq_hi = c.bq_hi; u.mq_hi = c.mq_hi; u.bq_lo = c.bq_lo; u.mq_lo = c.mq_lo;
+    return u;
+}
+
+// soft-clip evidence per category (plain, ctx, indel) x side (L, R): reads
+// with mapq >= -q (h) and all reads (n); packed as h | n << 16 under the same
+// bound as PackedCounts
+template <bool PK>
+struct ClipCounts {
+    int32_t h[6], n[6];
+    __device__ __forceinline__ void add(int k, int hv) { h[k] += hv; n[k] += 1; }
+    __device__ __forceinline__ int32_t hi(int k) const { return h[k]; }
+    __device__ __forceinline__ int32_t all(int k) const { return n[k]; }
+};
+template <>
+struct ClipCounts<true> {
+    uint32_t v[6];
+    __device__ __forceinline__ void add(int k, int hv) { v[k] += (uint32_t)hv + 65536u; }
+    __device__ __forceinline__ int32_t hi(int k) const { return (int32_t)(v[k] & 0xffffu); }
+    __device__ __forceinline__ int32_t all(int k) const { return (int32_t)(v[k] >> 16); }
+};
 
 // bases matching the reference base of the lane (the common case), counted
 // without selecting a counter by base code; folded into LaneCounts at the end
@@ -139,8 +223,8 @@ struct RegSlots {
 #pragma unroll
         for (int k = 0; k < NS; k++) s[k] = 0;
     }
-    __device__ __forceinline__ bool probe(uint32_t nid, int min_snv) {
-        bool done = false, found = false;
+    __device__ __forceinline__ bool probe(uint32_t nid, int min_snv, bool on = true) {
+        bool done = !on, found = false;
 #pragma unroll
         for (int k = 0; k < NS; k++) {
             const bool active = !done && k < min_snv;
@@ -163,7 +247,8 @@ struct MemSlots {
     uint32_t *col;
     int nf;
     __device__ __forceinline__ void reset() { nf = 0; }
-    __device__ __forceinline__ bool probe(uint32_t nid, int min_snv) {
+    __device__ __forceinline__ bool probe(uint32_t nid, int min_snv, bool on = true) {
+        if (!on) return false;
         const int lim = min(nf, min_snv);
         for (int k = 0; k < lim; k++)
             if (col[(size_t)k * TG] == nid) return true;  // stored ids are never 0
@@ -181,8 +266,8 @@ struct MemSlots {
 // character (bam_nt16_rev_table) equals the reference base, or 16 if none, so
 // `s4 == rb4` is the reference's `ref != read base` test negated; mv says the
 // reference base is one of ACGT.
-template <class SLOTS>
-__device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, SLOTS &slot,
+template <class SLOTS, class CNT>
+__device__ __forceinline__ void tally_base(CNT &c, MatchCounts &m, SLOTS &slot,
                                            int min_snv, bool hq, bool mv, int q, int s4, int rb4, bool fwd, int qi,
                                            int lseq_mod, int mq, uint32_t nid) {
     if (s4 == rb4) {
@@ -202,10 +287,27 @@ __device__ __forceinline__ void tally_base(LaneCounts &c, MatchCounts &m, SLOTS 
     if (hq) count = count && !slot.probe(nid, min_snv);
     const bool low = !hq && code < 4;
     const int32_t ch = count ? 1 : 0, cl = low ? 1 : 0;
-    GROM_ADD4(c, snv, code, ch);
-    GROM_ADD4(c, fs, code, fwd ? ch : 0);
-    GROM_ADD4(c, pir, code, count ? qi : 0);  // mismatches add the offset on both strands (GROM.c:6896)
-    GROM_ADD4(c, low, code, cl);
+    // mismatches add the offset on both strands (GROM.c:6896)
+    add_codes(c, code, ch, fwd ? ch : 0, count ? qi : 0, cl);
+    c.bq_hi += count ? q : 0;
+    c.mq_hi += count ? mq : 0;
+    c.bq_lo += low ? q : 0;
+    c.mq_lo += low ? mq : 0;
+}
+
+// a mismatching base of the fast path (the second half of tally_base),
+// predicated by `on` instead of branched on, so a wave with any mismatching
+// lane runs it once for all lanes
+template <class SLOTS, class CNT>
+__device__ __forceinline__ void tally_mismatch(CNT &c, SLOTS &slot, bool on, int min_snv, bool hq, int q, int s4,
+                                               bool fwd, int qi, int mq, uint32_t nid) {
+    const int code = acgt_code(s4);
+    const bool probe_on = on && hq;
+    const bool found = slot.probe(nid, min_snv, probe_on);
+    const bool count = probe_on && code < 4 && !found;
+    const bool low = on && !hq && code < 4;
+    const int32_t ch = count ? 1 : 0, cl = low ? 1 : 0;
+    add_codes(c, code, ch, fwd ? ch : 0, count ? qi : 0, cl);  // GROM.c:6896
     c.bq_hi += count ? q : 0;
     c.mq_hi += count ? mq : 0;
     c.bq_lo += low ? q : 0;
@@ -431,9 +533,12 @@ __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *_
     }
 }
 
-#ifndef GROM_PAIR
-#define GROM_PAIR 2  // single-op reads folded per step of the gather kernel
+
+// DIFFED reads looked up per step of the fast path (their LDS reads in flight together)
+#ifndef GROM_FAST_READS
+#define GROM_FAST_READS 2
 #endif
+#define FR GROM_FAST_READS
 
 // occupancy target: 5 waves per SIMD (a 96-register budget) measured faster
 // than the unconstrained 4 despite a few spills; GROM_WAVES_PER_EU overrides
@@ -443,8 +548,9 @@ __device__ __forceinline__ void pile_emit(const grom_scan_args &a, const char *_
 #define GROM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GROM_WAVES_PER_EU)))
 
 // SLOTS: the read-name slots of the lane's position (RegSlots<NS> with
-// NS >= -n: fewer slots, fewer VGPRs; MemSlots for any -n)
-template <class SLOTS>
+// NS >= -n: fewer slots, fewer VGPRs; MemSlots for any -n).  PK: packed
+// 16-bit counters (tiles of at most PACK_MAX_READS reads).
+template <bool PK, class SLOTS>
 __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_t tile, const grom_scan_args &a,
                                                  const char *__restrict__ ref, const ReadArrays &R,
                                                  const ReadMeta *__restrict__ meta, const int32_t *__restrict__ tile_lo,
@@ -469,15 +575,18 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
     const int rcode = (rb4 < 16) ? acgt_code(rb4) : 4;
     const bool mv = rcode < 4;
     const bool evals = x >= a.eval_lo && x <= a.eval_hi;  // GROM.c:11086, 5842
+    // the fast path's lane position: outside the evaluated range no read's
+    // offset (x - pos, unsigned) falls inside it, so no base is tallied
+    const int32_t xe = evals ? x : (int32_t)(INT32_MIN / 2);
     const uint8_t *lq8 = reinterpret_cast<const uint8_t *>(L.qual);
     const uint8_t *ls8 = reinterpret_cast<const uint8_t *>(L.seq);
 
-    LaneCounts c = {};
+    typename std::conditional<PK, PackedCounts, LaneCounts>::type c = {};
     MatchCounts mc = {0, 0, 0, 0};
     int32_t rd = 0, caf_mq = 0, caf_rd = 0, caf_low = 0;
     // soft-clip evidence per category (plain, ctx, indel) x side (L, R):
     // reads with mapq >= -q (each adds 6, GROM.c:5829-5836) and all reads
-    int32_t sch[6] = {0, 0, 0, 0, 0, 0}, scn[6] = {0, 0, 0, 0, 0, 0};
+    ClipCounts<PK> sc = {};
     slot.reset();
 
     const uint4 *gq4 = reinterpret_cast<const uint4 *>(R.qual);
@@ -530,12 +639,12 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
 #pragma unroll
             for (int k = 0; k < QLOADS; k++) {
                 const int64_t w = qv0 + tid + k * TG;
-                if (w < qv1) L.qual[w - qv0] = vq[k];
+                L.qual[w < qv1 ? (int)(w - qv0) : QV] = vq[k];  // unconditional: the loads stay in flight together
             }
 #pragma unroll
             for (int k = 0; k < SLOADS; k++) {
                 const int64_t w = sv0 + tid + k * TG;
-                if (w < sv1) L.seq[w - sv0] = vs[k];
+                L.seq[w < sv1 ? (int)(w - sv0) : SV] = vs[k];
             }
         }
         // single-op staged reads: their caf and physical-depth intervals go
@@ -543,13 +652,9 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
         // below skips those per-lane updates (GROM.c:6605-6671, 7173-7181)
         if (use_diff && staged && tid < m2) {
             const ReadMeta &rm = L.meta[tid];
-            // (the first CIGAR word from global memory: L.cig is still being written)
-            const uint32_t nc = rm.b.y & 0xffffu, cw = nc == 1 ? R.cigar[rm.b.x] : 0u;
-            const uint32_t op = cw & 15u;
-            const int32_t p0 = (int32_t)rm.a.x, len = (int32_t)(cw >> 4), lq = (int32_t)rm.a.z;
+            const int32_t p0 = (int32_t)rm.a.x, len = (int32_t)rm.a.z;
             const uint32_t mq = rm.b.z & 255u;
-            const bool keep = ((rm.b.z >> 8) & 255u) != 0;
-            if (nc == 1 && (op == 0 || op == 7 || op == 8) && keep && len == lq && p0 >= 0 && len < clen - p0) {
+            if (rm.b.z & MK_FAST) {
                 const int32_t lo = max(p0, t0) - t0, hi = min(p0 + len, t0 + TG) - t0;
                 if (lo < hi) {
                     const uint32_t inc = (mq >= (uint32_t)a.rd_min_mapq) ? 1u : 65536u;
@@ -581,6 +686,9 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
                 G.nf = rm.b.y;
                 G.mk = rm.b.z;
                 G.bo = (uint32_t)((((int64_t)rm.c.x << 32) | rm.b.w) - qb0);
+                // DIFFED reads sit in the staged window (offset and length
+                // below QBYTES): both travel in one word to the fast path
+                if (rm.b.z & DIFFED) G.bo |= rm.a.z << 16;
                 G.cw0 = (staged && (rm.b.y & 0xffffu) != 0) ? L.cig[rm.b.x - cf] : 0u;
                 // touches [x0, x0+64)?  contributions span [pos-1 (left clip), ext)
                 rel = ((rm.b.z >> 8) & 255u) != 0 &&  // -M duplicate (GROM.c:6590)
@@ -588,60 +696,84 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
             }
             uint64_t mask = __ballot(rel);
             if (!mask) continue;
+            const uint64_t dmask = __ballot(j < m2 && (G.mk & DIFFED));
             while (mask) {
-                // GROM_PAIR single-op reads at once: their staged bases are
-                // read from LDS together, then tallied in read order
-                if (staged && __popcll(mask) >= GROM_PAIR) {
-                    ReadView uk[GROM_PAIR];
-                    uint64_t mk = mask;
-                    bool all_fast = true;
+                // ---- fast path: the next one or two reads in order are
+                // DIFFED (one aligned block of l_qseq bases): each lane only
+                // looks up the read's base at its position.  Both pairs of
+                // LDS reads are issued before either base is tallied; the
+                // order-free matched-base sums are added first, then the
+                // mismatching bases in read order (the read-name slots are
+                // order-dependent, GROM.c:6805-6824) ----
+                const uint64_t b0 = mask & (0ull - mask);
+                if (b0 & dmask) {
+                    // the run of up to FR consecutive DIFFED reads at the front
+                    // of the mask (wave-uniform); empty slots tally nothing
+                    int32_t fp[FR], fl[FR], fb[FR], fi[FR];
+                    uint32_t fm[FR];
+                    uint64_t mm = mask;
+                    bool run = true;
 #pragma unroll
-                    for (int k = 0; k < GROM_PAIR; k++) {
-                        uk[k] = view_of(G, __builtin_ctzll(mk));
-                        mk &= mk - 1;
-                        all_fast = all_fast && fast_read(uk[k]);
+                    for (int k = 0; k < FR; k++) {
+                        const uint64_t b = mm & (0ull - mm);
+                        run = run && (b & dmask) != 0;
+                        mm = run ? (mm ^ b) : mm;
+                        const int i = run ? __builtin_ctzll(b) : __builtin_ctzll(b0);
+                        fp[k] = (int32_t)lane_get(G.p0, i);
+                        const uint32_t bl = lane_get(G.bo, i);
+                        fl[k] = run ? (int32_t)(bl >> 16) : 0;
+                        fb[k] = (int32_t)(bl & 0xffffu);
+                        fi[k] = i;
+                        fm[k] = lane_get(G.mk, i);
                     }
-                    if (all_fast) {
-                        mask = mk;
-                        int32_t hk[GROM_PAIR];
-                        uint32_t qk[GROM_PAIR], sk[GROM_PAIR];
+                    mask = mm;
+#ifdef GROM_PROF_NOFAST  // timing probe only: the fast reads are skipped
+                    continue;
+#endif
+                    uint32_t fq[FR], fs4[FR], fdx[FR];
+                    bool fhit[FR];
 #pragma unroll
-                        for (int k = 0; k < GROM_PAIR; k++) {
-                            const ReadView &u = uk[k];
-                            const int32_t p0 = u.p0, len = (int32_t)(u.cw0 >> 4);
-                            const int mq = (int)u.mq;
-                            const uint32_t dx = (uint32_t)(x - p0);
-                            if (!(u.mkf & DIFFED)) {  // wave-uniform
-                                if (p0 >= 0 && len < clen - p0 && dx < (uint32_t)len) {
-                                    caf_mq += mq;
-                                    caf_rd += (mq >= a.rd_min_mapq) ? 1 : 0;
-                                    caf_low += (mq >= a.rd_min_mapq) ? 0 : 1;
-                                }
-                                rd += (dx < (uint32_t)u.lq) ? 1 : 0;  // E = pos + l_qseq
-                            }
-                            const bool pos_ok = p0 >= 0 && p0 < clen;
-                            hk[k] = (pos_ok && evals && dx < (uint32_t)min(len, clen - p0)) ? (int32_t)dx : -1;
-                            qk[k] = 0;
-                            sk[k] = 0;
-                            if (hk[k] >= 0 && hk[k] < u.lq) staged_base(lq8, ls8, soff, u.bo + hk[k], qk[k], sk[k]);
-                        }
-#pragma unroll
-                        for (int k = 0; k < GROM_PAIR; k++) {
-                            const ReadView &u = uk[k];
-                            if (hk[k] >= 0) {
-                                int q = 0, s4 = 15;
-                                if (hk[k] < u.lq) {
-                                    q = (int)qk[k];
-                                    s4 = (int)((sk[k] >> ((((u.bo + hk[k]) & 1) ^ 1) << 2)) & 15u);
-                                }
-                                const int mq = (int)u.mq;
-                                tally_base(c, mc, slot, a.min_snv, mq >= a.min_mapq && q >= a.min_base_qual, mv, q,
-                                           s4, rb4, !(u.fl & 0x10), hk[k], u.lq, mq, u.nid);
-                            }
-                        }
-                        continue;
+                    for (int k = 0; k < FR; k++) {
+                        fdx[k] = (uint32_t)(xe - fp[k]);
+                        fhit[k] = fdx[k] < (uint32_t)fl[k];
+                        const int32_t r = fhit[k] ? fb[k] + (int32_t)fdx[k] : 0;
+                        fq[k] = lq8[r];
+                        fs4[k] = (uint32_t)ls8[soff + (r >> 1)] >> ((((uint32_t)r & 1u) ^ 1u) << 2);
                     }
+#pragma unroll
+                    for (int k = 0; k < FR; k++) {
+                        const int s4 = (int)(fs4[k] & 15u), q = (int)fq[k], mq = (int)(fm[k] & 255u);
+                        const bool fwd = !(fm[k] & MK_REV);
+                        const bool hq = (fm[k] & MK_HQ) && q >= a.min_base_qual;
+                        const bool mt = fhit[k] && s4 == rb4 && mv;
+                        const bool h = mt && hq, l = mt && !hq;
+                        mc.cnt += h ? 1 : 0;
+                        mc.fs += (h && fwd) ? 1 : 0;
+                        mc.pir += h ? (fwd ? (int32_t)fdx[k] : fl[k] - (int32_t)fdx[k]) : 0;
+                        mc.low += l ? 1 : 0;
+                        c.bq_hi += h ? q : 0;
+                        c.mq_hi += h ? mq : 0;
+                        c.bq_lo += l ? q : 0;
+                        c.mq_lo += l ? mq : 0;
+                    }
+                    bool anymm = false;
+#pragma unroll
+                    for (int k = 0; k < FR; k++) anymm = anymm || (fhit[k] && (int)(fs4[k] & 15u) != rb4);
+                    if (__ballot(anymm)) {  // wave-uniform: predicated for every lane
+#pragma unroll
+                        for (int k = 0; k < FR; k++) {
+                            const int s4 = (int)(fs4[k] & 15u), q = (int)fq[k], mq = (int)(fm[k] & 255u);
+                            tally_mismatch(c, slot, fhit[k] && s4 != rb4, a.min_snv,
+                                           (fm[k] & MK_HQ) && q >= a.min_base_qual, q, s4, !(fm[k] & MK_REV),
+                                           (int)fdx[k], mq, lane_get(G.nid, fi[k]));
+                        }
+                    }
+                    continue;
                 }
+#ifdef GROM_PROF_NOGENERAL  // timing probe only: skip the reads off the fast path
+                mask &= mask - 1;
+                continue;
+#endif
                 const ReadView u = view_of(G, __builtin_ctzll(mask));
                 mask &= mask - 1;
                 const int32_t p0 = u.p0;
@@ -735,20 +867,20 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
                         // ctx (mate on another chromosome), indel (close mate)
                         if (at_l) {
                             if (!paired || (!rev && (munmap || (!munmap && same_chr && mp > p0)))) {
-                                sch[0] += h; scn[0] += 1;
+                                sc.add(0, h);
                             }
-                            if (paired && !munmap && !same_chr && rev) { sch[2] += h; scn[2] += 1; }
+                            if (paired && !munmap && !same_chr && rev) sc.add(2, h);
                             if (paired && !munmap && same_chr && rev && abs(tl) <= a.insert_max && mp < p0) {
-                                sch[4] += h; scn[4] += 1;
+                                sc.add(4, h);
                             }
                         }
                         if (at_r) {
                             if (!paired || (rev && (munmap || (!munmap && same_chr && mp < p0)))) {
-                                sch[1] += h; scn[1] += 1;
+                                sc.add(1, h);
                             }
-                            if (paired && !munmap && !same_chr && !rev) { sch[3] += h; scn[3] += 1; }
+                            if (paired && !munmap && !same_chr && !rev) sc.add(3, h);
                             if (paired && !munmap && same_chr && !rev && abs(tl) <= a.insert_max && mp > p0) {
-                                sch[5] += h; scn[5] += 1;
+                                sc.add(5, h);
                             }
                         }
                     }
@@ -802,12 +934,12 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
     }
 
     // matched bases go to the reference base's counters
-    GROM_ADD4(c, snv, rcode, mc.cnt);
-    GROM_ADD4(c, fs, rcode, mc.fs);
-    GROM_ADD4(c, pir, rcode, mc.pir);
-    GROM_ADD4(c, low, rcode, mc.low);
+    add_codes(c, rcode, mc.cnt, mc.fs, mc.pir, mc.low);
+    int32_t sch[6], scn[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) { sch[k] = sc.hi(k); scn[k] = sc.all(k); }
 
-    pile_emit(a, ref, O, mq_tab, hez_tab, L.tail, tile, x, rb, evals, c, rd, caf_mq, caf_rd, caf_low, sch, scn);
+    pile_emit(a, ref, O, mq_tab, hez_tab, L.tail, tile, x, rb, evals, unpack(c), rd, caf_mq, caf_rd, caf_low, sch, scn);
 }
 
 // every tile of the chromosome (GROM_PILEUP=gather)
@@ -823,26 +955,30 @@ __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args 
     const int64_t per_xcd = (n_tiles + 7) / 8;
     const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (tile >= n_tiles) return;  // whole workgroup leaves together
+    if (tile_hi[tile] - tile_lo[tile] > PACK_MAX_READS) return;  // k_scan_tile_mem takes it
     RegSlots<NS> slot;
-    scan_tile_gather(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+    scan_tile_gather<true>(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
 }
 
 // -n above the register builds: a fixed grid of workgroups, each walking
 // tiles blockIdx.x, blockIdx.x + gridDim.x, ... with its own slot columns in
-// `slots` ([gridDim.x][min_snv][GROM_TILE] uint32, sized by the host)
+// `slots` ([gridDim.x][min_snv][GROM_TILE] uint32, sized by the host), with
+// 32-bit counters.  heavy_only: only the tiles k_scan_tile leaves (more than
+// PACK_MAX_READS reads).
 __global__ __launch_bounds__(TG) void k_scan_tile_mem(grom_scan_args a, const char *__restrict__ ref, ReadArrays R,
                                                      const ReadMeta *__restrict__ meta,
                                                      const int32_t *__restrict__ tile_lo,
                                                      const int32_t *__restrict__ tile_hi, PileOut O,
                                                      const double *__restrict__ mq_tab,
                                                      const double *__restrict__ hez_tab, int64_t n_tiles,
-                                                     uint32_t *__restrict__ slots) {
+                                                     uint32_t *__restrict__ slots, int heavy_only) {
     __shared__ ScanLds L;
     MemSlots slot;
     slot.col = slots + (size_t)blockIdx.x * a.min_snv * TG + threadIdx.x;
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        if (heavy_only && tile_hi[tile] - tile_lo[tile] <= PACK_MAX_READS) continue;  // workgroup-uniform
         __syncthreads();  // the previous tile's LDS is no longer read
-        scan_tile_gather(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
+        scan_tile_gather<false>(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
     }
 }
 

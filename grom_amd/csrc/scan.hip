@@ -454,7 +454,8 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         }
         if (n > 0) {
             int g = (int)std::min<int64_t>((n + 255) / 256, 8192);
-            hipLaunchKernelGGL(k_prep, dim3(g), dim3(256), 0, st, n, ra, (ReadMeta *)C.meta.p, d_halo);
+            hipLaunchKernelGGL(k_prep, dim3(g), dim3(256), 0, st, n, ra, (ReadMeta *)C.meta.p, d_halo, (int64_t)ch->len,
+                               (int32_t)P.min_mapq);
         }
         {
             int g = (int)std::min<int64_t>((n + 1 + 255) / 256, 8192);
@@ -475,15 +476,20 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                        (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, n_tiles)
         // (GROM_MEM_SLOTS=1, a test hook: the global-slot kernel for any -n)
         static const bool force_mem_slots = getenv("GROM_MEM_SLOTS") && atoi(getenv("GROM_MEM_SLOTS")) == 1;
-        if (P.min_snv > GROM_MAX_NAME_SLOTS || force_mem_slots) {
-            // more slots than registers hold: slot columns in global scratch,
-            // one set per workgroup of a fixed grid that walks the tiles
+        // the global-slot kernel: every tile when -n exceeds the register
+        // builds, else only the tiles with too many reads for the register
+        // builds' 16-bit counters (a quick pass over the tile ranges when
+        // there are none)
+        const bool mem_all = P.min_snv > GROM_MAX_NAME_SLOTS || force_mem_slots;
+        {
             const unsigned mg = (unsigned)std::min<int64_t>(n_tiles, GROM_MEM_SLOT_BLOCKS);
             const size_t ns = (size_t)std::max(P.min_snv, 1);
             if ((rc = ensure(C.slots, sizeof(uint32_t) * (size_t)mg * ns * GROM_TILE))) return rc;
             hipLaunchKernelGGL(k_scan_tile_mem, dim3(mg), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
                                (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                               C.d_mq, C.d_hez, n_tiles, (uint32_t *)C.slots.p);
+                               C.d_mq, C.d_hez, n_tiles, (uint32_t *)C.slots.p, mem_all ? 0 : 1);
+        }
+        if (mem_all) {
         } else if (P.min_snv <= GROM_FEW_NAME_SLOTS) GROM_LAUNCH_TILE(GROM_FEW_NAME_SLOTS);
         else if (P.min_snv <= 8) GROM_LAUNCH_TILE(8);
         else if (P.min_snv <= 16) GROM_LAUNCH_TILE(16);

@@ -59,6 +59,10 @@ CASES = {
     "cnv_reservoir": ["-L", "30000000", "-R", "50", "-s", "41", "-V", "0.0000002", "-W", "50000,300000", "-Q", "0.05"],
     # a 2.2 kb insert library (mean above the 1536 of the 32-bit GC-window
     # kernel: k_cnv_gc's 64-bit instance), with copy-number regions and SVs
+    # a 20 kb insert library: above k_cnv_gc's 16,384 LDS halo, the GC windows
+    # come from chromosome-wide prefixes (k_cnv_gc_global)
+    "huge_insert": ["-L", "2500000", "-s", "23", "-m", "20000", "-d", "1500", "-V", "0.000003", "-W", "60000,300000",
+                    "-Q", "0.05"],
     "wide_insert": ["-L", "1500000", "-s", "19", "-m", "2200", "-d", "200", "-V", "0.000004", "-W", "20000,150000",
                     "-Q", "0.05", "-X", "5"],
 }

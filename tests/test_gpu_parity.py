@@ -72,6 +72,7 @@ CNV_RUNS = [
     ("cnv_long", []),
     ("wide_insert", []),
     ("wide_insert", ["-V", "1"]),
+    ("huge_insert", ["-V", "1"]),
     # -X past the chromosome lengths and beyond 1e6 with -A 20: every sampled
     # window straddles up to six sampling passes of its block (GROM.c:18967-19018)
     ("cnv_multi", ["-V", "1", "-X", "2500000", "-A", "20", "-W", "100"]),
