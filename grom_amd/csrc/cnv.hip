@@ -3000,6 +3000,12 @@ __global__ void k_cnv_gc_global(const char *__restrict__ ref, Args A, int64_t m,
     }
 }
 
+// test hook GROM_GC_GLOBAL=1: the prefix form at any insert mean
+static bool gc_global_forced() {
+    static const bool f = getenv("GROM_GC_GLOBAL") && atoi(getenv("GROM_GC_GLOBAL")) == 1;
+    return f;
+}
+
 // GC/ACGT weights and dinucleotide classes depend on the reference alone
 // (GROM.c:1586-1881), so the scan driver starts them before the pileup on a
 // stream of their own; cnv_chrom then only waits for them.
@@ -3008,7 +3014,7 @@ int cnv_prelaunch(CnvScratch *S, hipStream_t after, const grom_params &P, const 
     int rc;
     S->gc_ref = nullptr;
     const int64_t m = P.insert_mean;
-    if (m < 1 || m > GC_MMAX || len <= 0) return GROM_OK;  // cnv_chrom builds these itself
+    if (m < 1 || m > GC_MMAX || len <= 0 || gc_global_forced()) return GROM_OK;  // cnv_chrom builds these itself
     if ((rc = cnv_init(S, err, errlen))) return rc;
     if ((rc = grow(S->gcw, len, err, errlen)) || (rc = grow(S->acw, len, err, errlen)) ||
         (rc = grow(S->rtype, len, err, errlen)))
@@ -3119,7 +3125,7 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
     // driver prelaunched them for this reference) ----
     if (S->gc_ref == d_ref && S->gc_len == len && S->gc_m == m) {
         CK(hipStreamWaitEvent(st, S->gc_done, 0));
-    } else if (m > GC_MMAX) {
+    } else if (m > GC_MMAX || gc_global_forced()) {
         const int64_t n = len + 1;
         size_t tb = 0;
         int64_t *pre = nullptr;

@@ -72,7 +72,6 @@ CNV_RUNS = [
     ("cnv_long", []),
     ("wide_insert", []),
     ("wide_insert", ["-V", "1"]),
-    ("huge_insert", ["-V", "1"]),
     # -X past the chromosome lengths and beyond 1e6 with -A 20: every sampled
     # window straddles up to six sampling passes of its block (GROM.c:18967-19018)
     ("cnv_multi", ["-V", "1", "-X", "2500000", "-A", "20", "-W", "100"]),
@@ -175,6 +174,21 @@ def test_global_name_slots_forced(datadir, case, extra):
     """The global-slot kernel (built for -n above 32) forced at small -n, where
     the register builds also run: both must equal the oracle."""
     _check_counters(datadir, case, extra, "memslots" + "".join(extra), env_extra={"GROM_MEM_SLOTS": "1"})
+
+
+@pytest.mark.parametrize("case,extra", [("cnv", ["-V", "1"]), ("wide_insert", ["-V", "1"]), ("huge_insert", [])],
+                         ids=["cnv", "wide_insert", "huge_insert"])
+def test_gc_windows_prefix_form(datadir, case, extra):
+    """k_cnv_gc_global, the GC/ACGT window form for insert means above the
+    tile kernel's 16,384 halo: forced at insert means 500 and 2,200 (where
+    CNV calls exist to compare), and on its own at a 20 kb insert library."""
+    bam, fa, tag = _oracle_once(datadir, case, extra)
+    run_grom(datadir, bam, fa, f"g_gcglobal_{tag}.vcf", extra,
+             env_extra={"GROM_GC_GLOBAL": "1"} if case != "huge_insert" else None)
+    ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"g_gcglobal_{tag}.vcf").read()
+    if "-V" in extra:
+        assert ov.count("<DEL>") + ov.count("<DUP>") > 0
+    assert ov == gv
 
 
 def test_tab_output_names(datadir):
