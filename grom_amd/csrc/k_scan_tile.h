@@ -949,13 +949,17 @@ __global__ __launch_bounds__(TG) GROM_OCCUPANCY void k_scan_tile(grom_scan_args 
                                                   const int32_t *__restrict__ tile_lo,
                                                   const int32_t *__restrict__ tile_hi, PileOut O,
                                                   const double *__restrict__ mq_tab,
-                                                  const double *__restrict__ hez_tab, int64_t n_tiles) {
+                                                  const double *__restrict__ hez_tab, int64_t n_tiles,
+                                                  uint32_t *__restrict__ heavy, int32_t pack_max) {
     __shared__ ScanLds L;
     // XCD-contiguous tile order (speed only; any mapping is correct)
     const int64_t per_xcd = (n_tiles + 7) / 8;
     const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (tile >= n_tiles) return;  // whole workgroup leaves together
-    if (tile_hi[tile] - tile_lo[tile] > PACK_MAX_READS) return;  // k_scan_tile_mem takes it
+    if (tile_hi[tile] - tile_lo[tile] > pack_max) {  // k_scan_tile_mem takes it (pack_max <= PACK_MAX_READS)
+        if (threadIdx.x == 0) atomicOr(heavy, 1u);
+        return;
+    }
     RegSlots<NS> slot;
     scan_tile_gather<true>(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
 }
@@ -971,12 +975,14 @@ __global__ __launch_bounds__(TG) void k_scan_tile_mem(grom_scan_args a, const ch
                                                      const int32_t *__restrict__ tile_hi, PileOut O,
                                                      const double *__restrict__ mq_tab,
                                                      const double *__restrict__ hez_tab, int64_t n_tiles,
-                                                     uint32_t *__restrict__ slots, int heavy_only) {
+                                                     uint32_t *__restrict__ slots, int heavy_only,
+                                                     const uint32_t *__restrict__ heavy, int32_t pack_max) {
     __shared__ ScanLds L;
+    if (heavy_only && *heavy == 0) return;  // k_scan_tile left no tile (the usual case)
     MemSlots slot;
     slot.col = slots + (size_t)blockIdx.x * a.min_snv * TG + threadIdx.x;
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        if (heavy_only && tile_hi[tile] - tile_lo[tile] <= PACK_MAX_READS) continue;  // workgroup-uniform
+        if (heavy_only && tile_hi[tile] - tile_lo[tile] <= pack_max) continue;  // workgroup-uniform
         __syncthreads();  // the previous tile's LDS is no longer read
         scan_tile_gather<false>(L, slot, tile, a, ref, R, meta, tile_lo, tile_hi, O, mq_tab, hez_tab);
     }

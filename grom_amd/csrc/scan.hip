@@ -381,7 +381,8 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     if (C.cands.cap >= sizeof(grom_snv_cand) * 2)
         cand_cap = std::max<uint32_t>(cand_cap, (uint32_t)(C.cands.cap / sizeof(grom_snv_cand)));
 
-    // misc layout: [0] halo (int32), [4..] n_cands, status, n_events ; [32..] flush_acc[2] ; [64..] mid acc[2]
+    // misc layout: [0] halo (int32), [4..] n_cands, status, n_events ; [24] heavy-tile flag ;
+    // [32..] flush_acc[2] ; [64..] mid acc[2]
     char *misc = (char *)C.misc.p;
     int32_t *d_halo = (int32_t *)misc;
     uint32_t *d_ncand = (uint32_t *)(misc + 4);
@@ -473,27 +474,32 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         // slots, fewer registers: GROM.c keeps -n names per base)
 #define GROM_LAUNCH_TILE(NSL)                                                                                    \
     hipLaunchKernelGGL(k_scan_tile<NSL>, dim3(grid), dim3(GROM_TILE), 0, st, a, ch->ref, ra, (const ReadMeta *)C.meta.p, \
-                       (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, n_tiles)
+                       (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po, C.d_mq, C.d_hez, n_tiles, d_heavy, pack_max)
         // (GROM_MEM_SLOTS=1, a test hook: the global-slot kernel for any -n)
         static const bool force_mem_slots = getenv("GROM_MEM_SLOTS") && atoi(getenv("GROM_MEM_SLOTS")) == 1;
-        // the global-slot kernel: every tile when -n exceeds the register
-        // builds, else only the tiles with too many reads for the register
-        // builds' 16-bit counters (a quick pass over the tile ranges when
-        // there are none)
+        // the register builds first; then the global-slot kernel: every tile
+        // when -n exceeds the register builds, else only the tiles with too
+        // many reads for the register builds' 16-bit counters (it returns at
+        // once when k_scan_tile flagged none)
+        uint32_t *d_heavy = (uint32_t *)(misc + 24);
+        // (GROM_HEAVY_TILES=1, a test hook: every tile takes the heavy-tile route)
+        static const bool all_heavy = getenv("GROM_HEAVY_TILES") && atoi(getenv("GROM_HEAVY_TILES")) == 1;
+        const int32_t pack_max = all_heavy ? -1 : PACK_MAX_READS;
         const bool mem_all = P.min_snv > GROM_MAX_NAME_SLOTS || force_mem_slots;
+        if (mem_all) {
+        } else if (P.min_snv <= GROM_FEW_NAME_SLOTS) GROM_LAUNCH_TILE(GROM_FEW_NAME_SLOTS);
+        else if (P.min_snv <= 8) GROM_LAUNCH_TILE(8);
+        else if (P.min_snv <= 16) GROM_LAUNCH_TILE(16);
+        else GROM_LAUNCH_TILE(GROM_MAX_NAME_SLOTS);
         {
             const unsigned mg = (unsigned)std::min<int64_t>(n_tiles, GROM_MEM_SLOT_BLOCKS);
             const size_t ns = (size_t)std::max(P.min_snv, 1);
             if ((rc = ensure(C.slots, sizeof(uint32_t) * (size_t)mg * ns * GROM_TILE))) return rc;
             hipLaunchKernelGGL(k_scan_tile_mem, dim3(mg), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
                                (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
-                               C.d_mq, C.d_hez, n_tiles, (uint32_t *)C.slots.p, mem_all ? 0 : 1);
+                               C.d_mq, C.d_hez, n_tiles, (uint32_t *)C.slots.p, mem_all ? 0 : 1,
+                               (const uint32_t *)d_heavy, pack_max);
         }
-        if (mem_all) {
-        } else if (P.min_snv <= GROM_FEW_NAME_SLOTS) GROM_LAUNCH_TILE(GROM_FEW_NAME_SLOTS);
-        else if (P.min_snv <= 8) GROM_LAUNCH_TILE(8);
-        else if (P.min_snv <= 16) GROM_LAUNCH_TILE(16);
-        else GROM_LAUNCH_TILE(GROM_MAX_NAME_SLOTS);
 #undef GROM_LAUNCH_TILE
         hipLaunchKernelGGL(k_flush_reduce, dim3(256), dim3(256), 0, st, n_tiles,
                            (const unsigned long long *)C.fpart.p, d_facc);

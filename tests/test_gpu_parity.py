@@ -191,6 +191,14 @@ def test_gc_windows_prefix_form(datadir, case, extra):
     assert ov == gv
 
 
+@pytest.mark.parametrize("case,extra", [("dups", ["-M"]), ("c5_tetra_male", ["-p", "4", "-g", "1"])],
+                         ids=["dups-M", "tetra"])
+def test_heavy_tile_route(datadir, case, extra):
+    """Tiles with more reads than the register kernels' 16-bit counters hold
+    go to k_scan_tile_mem (32-bit counters): forced for every tile."""
+    _check_counters(datadir, case, extra, "heavy" + "".join(extra), env_extra={"GROM_HEAVY_TILES": "1"})
+
+
 def test_tab_output_names(datadir):
     """-f with an output name without .vcf: rows in OUT, the translocation
     table in OUT.ctx (GROM.c:20494-20505, 22446-22460)."""
