@@ -1,50 +1,58 @@
-"""bench.py -- GROM per-chromosome scan on MI355X, whole genome.
+"""bench.py -- GROM's per-chromosome scan on MI355X, whole genome, whole run.
+
+Metric (BASELINE.json): "Mbases/sec scanned (whole genome)" -- SURVEY 8(d):
+genome bases / wall time of the whole run, BAM in, VCF out.
 
 Default workload (BASELINE.json configs[2]): a synthetic 30x 2x150 bp
 paired-end human-shape genome -- the 24 GRCh38 contig lengths (3.09 Gb), SNVs
 and indels, breakpoint SVs (DEL/DUP/INV/INS and CTX, with split reads and
-discordant pairs), copy-number regions, 5% PCR duplicates -- scanned with
-`-M`.  Every chromosome's reads are generated on the host (grom_synth_chrom,
-the generator behind grom_synth) and kept resident in HBM (grom_resident_new);
-the timed region starts with all inputs in HBM.
+discordant pairs), copy-number regions, 5% PCR duplicates -- written once as
+a BAM + BAI + FASTA by grom_synth, and scanned with `-M -g 1` (the male
+genome: chrY is processed too, so all 24 contigs are scanned).
 
-One step = one whole-genome pass: every chromosome through
-grom_scan_chrom_device -- pileup/SNV kernels, duplicate filter, breakpoint
-evidence and tests, SV assembly and rows, CTX records, the read-depth CNV path
-and its rows -- with --inflight F chromosomes in flight per GPU (F library
-contexts, one host thread each, longest chromosome first).  value = genome
-bases / step time.
+One step = one whole run of the drop-in CLI (grom_amd/bin/grom) as a fresh
+process: BAM index, parallel BGZF decode on the host's CPU share into pinned
+pieces, host->HBM copies, every chromosome's scan (pileup/SNV, duplicate
+filter, breakpoint evidence and tests, SV/INDEL rows, CTX records, read-depth
+CNV path and rows), the VCF and the translocation post-pass (.ctx.vcf).  The
+BAM sits in the page cache (the first warmup run reads it from disk).
+value = genome bases * steps / (time of the steps).
 
 --gpus N (torch.distributed.run, one rank per GPU): the chromosomes are
-assigned longest-processing-time-first to ranks (configs[3]: the same genome
-sharded by chromosome, strong scaling); ranks never exchange data on the scan
-path -- RCCL carries only the barrier and the max-over-ranks of the step time.
---workload chrom is configs[1] (one 100 Mb chromosome per rank, weak scaling).
+assigned longest-processing-time-first to ranks (configs[3]); each rank runs
+its own CLI process on its GPU over its share (GROM_CHROMS: the serial
+stream's plan is kept, so each chromosome gets exactly a one-process run's
+input), with its own decoder threads (the CPU quota split over the ranks);
+after a barrier rank 0 joins the shares in chromosome order and runs the
+translocation post-pass over all raw CTX rows (grom_amd.shard.merge_rank_outputs)
+-- inside the timed step.  The step time is the max over ranks.  There is no
+data-path collective: chromosomes are independent.
 
-The JSON line also carries
-  roofline      the pileup kernel (k_scan_tile): algorithmic bytes of every
-                timed launch / their summed durations (HIP events on the
-                library's stream), against 8 TB/s HBM, for this build's byte
-                model (`bytes_model`) and for SURVEY.md 8(d)'s 158.8 B/base,
-                with PMC-measured traffic when profiles/pmc_<tag>.json exists;
-  cpu_baseline  the CPU restatement of the reference (oracle/, "port"), one
-                thread, on a bounded 3-contig 6 Mb sample of the same
-                generator and flags (rank 0, N=1);
-  concordance   the GPU CLI on that same sample's BAM/FASTA against the
-                oracle's VCF and .ctx.vcf, byte for byte, with the CLI's
-                end-to-end time (BAM decode and upload included);
-  cli_whole_run the drop-in CLI (grom_amd/bin/grom, a fresh process) on a
-                >=100 Mb 24-contig 30x BAM of the same generator (the GRCh38
-                contigs scaled by --cli-scale): SURVEY 8(d)'s metric as
-                defined, bases / wall time of the whole run (BAM decode on
-                the host's cores, pinned pieces streamed to HBM, scans, VCF),
-                with its VCF and .ctx.vcf compared byte for byte against the
-                oracle run on the same files (rank 0, N=1).
+The JSON line also carries (rank 0, N=1):
+  roofline        the pileup kernel (k_scan_tile) in the timed whole runs:
+                  algorithmic bytes of every launch (read records, CIGAR,
+                  packed bases + qualities, reference, caf arrays)
+                  / the launches' HIP-event durations, against 8 TB/s HBM;
+                  SURVEY 8(d)'s 158.8 B/base model beside it; PMC traffic from
+                  profiles/pmc_genome_30x.json;
+  device_resident the same genome generated on the host (grom_synth_chrom_stream:
+                  each chromosome as the BAM's serial stream hands it to its
+                  scan) and kept in HBM, scanned with two chromosomes in flight:
+                  the device-only throughput, and its rows compared with the
+                  whole run's VCF and .ctx.vcf (decode + staging checked at
+                  full scale); skipped when --budget-s would be exceeded;
+  cpu_baseline    the CPU restatement of the reference (oracle/, "port"), one
+                  thread, on a bounded 3-contig 6 Mb sample of the same
+                  generator and flags;
+  concordance     the GPU CLI on that sample against the oracle, byte for byte.
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
+import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -59,6 +67,7 @@ SURVEY_BYTES_PER_BASE = 158.8  # SURVEY.md 8(d), pileup kernel at 30x, 2x150
 READ_LEN = 150
 CPU_SAMPLE_LENS = (3_000_000, 2_000_000, 1_000_000)  # the bounded cpu_baseline / concordance sample: 3 contigs
 PILEUP_KERNEL = "k_scan_tile"
+FILEDATE, SEED = "20260101", "7"
 
 GRCH38 = [("chr1", 248956422), ("chr2", 242193529), ("chr3", 198295559), ("chr4", 190214555),
           ("chr5", 181538259), ("chr6", 170805979), ("chr7", 159345973), ("chr8", 145138636),
@@ -68,19 +77,38 @@ GRCH38 = [("chr1", 248956422), ("chr2", 242193529), ("chr3", 198295559), ("chr4"
           ("chr21", 46709983), ("chr22", 50818468), ("chrX", 156040895), ("chrY", 57227415)]
 
 # 2,000 DEL/DUP/INV/INS + 200 CTX, 500 CNVs of 10 kb-1 Mb,
-# 5% PCR duplicates, seed 3, run with -M
+# 5% PCR duplicates, seed 3, run with -M (and -g 1: every contig processed)
 C3 = dict(coverage=30.0, dup_frac=0.05, sv_per_mb=2200 / 3088.3, cnv_rate=500 / 3.0883e9,
           cnv_range=(10_000, 1_000_000), seed=3)
 C2 = dict(coverage=30.0, dup_frac=0.0, sv_per_mb=0.0, cnv_rate=0.0, cnv_range=(0, 0), seed=2)
+GENOME_FLAGS = ["-M", "-g", "1"]
+
+CHROM_LINE = re.compile(r"^(\S+): (\d+) reads, ([\d.]+) ms on GPU .*; pileup ([\d.]+) ms, cnv ([\d.]+) ms, "
+                        r"cigar_ops (\d+), bases (\d+), len (\d+)$")
 
 
-def algorithmic_bytes(reads, chrom_len) -> int:
-    """Bytes the pileup kernel must move once per launch: every read record it ingests
-    (SoA metadata, CIGAR, packed bases, qualities), the reference, and the three
-    whole-chromosome read-depth arrays it writes ('Roofline')."""
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_quota() -> int:
+    """CPUs this container may use: the cgroup quota (cpu.max) if any, else the online CPUs."""
+    n = os.cpu_count() or 1
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(period) > 0:
+            n = min(n, max(1, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def launch_bytes(reads, cigar_ops, bases, chrom_len) -> int:
+    """Bytes the pileup kernel must move once per launch: every read record it
+    ingests (SoA metadata, CIGAR, packed bases, qualities), the reference and
+    the three whole-chromosome read-depth arrays it writes."""
     per_read = 4 + 2 + 1 + 4 + 4 + 4 + 4 + 4 + 8 + 4  # pos flag mapq mtid mpos isize lqseq cig_off base_off name
-    return (reads.n * per_read + reads.n_cigar_ops * 4 + reads.n_bases // 2 + reads.n_bases
-            + chrom_len * (1 + 3 * 4))
+    return reads * per_read + cigar_ops * 4 + bases // 2 + bases + chrom_len * (1 + 3 * 4)
 
 
 def synth_args(knobs, lengths):
@@ -95,16 +123,110 @@ def synth_args(knobs, lengths):
     return a
 
 
+def run_heartbeat(cmd, what, timeout, **kw):
+    """Run a long child with a progress line every 30 s (silent runs look hung)."""
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, **kw)
+    while True:
+        try:
+            out, err = p.communicate(timeout=30)
+            break
+        except subprocess.TimeoutExpired:
+            if time.perf_counter() - t0 > timeout:
+                p.kill()
+                p.communicate()
+                raise RuntimeError(f"{what}: timed out after {timeout} s")
+            log(f"{what}: {time.perf_counter() - t0:.0f} s")
+    if p.returncode != 0:
+        raise RuntimeError(f"{what} failed ({p.returncode}): {out[-2000:]} {err[-2000:]}")
+    return out, time.perf_counter() - t0
+
+
+def write_genome(work, knobs, lengths, names):
+    from grom_amd import SYNTH_BIN
+    prefix = os.path.join(work, "genome")
+    _, dt = run_heartbeat([SYNTH_BIN, "-o", prefix] + synth_args(knobs, lengths) + ["-n", ",".join(names)],
+                          "grom_synth", 1500)
+    bam = prefix + ".bam"
+    log(f"genome BAM written: {sum(lengths) / 1e9:.3f} Gb, {os.path.getsize(bam) / 1e9:.2f} GB in {dt:.1f} s")
+    return bam, prefix + ".fa", dt
+
+
+def cli_env(extra=None):
+    e = dict(os.environ, GROM_FILEDATE=FILEDATE, GROM_SEED=SEED, GROM_VERBOSE="1")
+    e.update(extra or {})
+    return e
+
+
+def whole_run(work, bam, fa, out, flags, env_extra=None, timeout=900):
+    """The drop-in CLI as a fresh process; (seconds, stdout)."""
+    from grom_amd import GROM_BIN
+    t0 = time.perf_counter()
+    r = subprocess.run([GROM_BIN, "-i", bam, "-r", fa, "-o", out] + flags, cwd=work, env=cli_env(env_extra),
+                       capture_output=True, text=True, timeout=timeout)
+    dt = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"grom failed ({r.returncode}): {r.stdout[-3000:]} {r.stderr[-3000:]}")
+    return dt, r.stdout
+
+
+def chrom_stats(stdout):
+    out = {}
+    for line in stdout.splitlines():
+        m = CHROM_LINE.match(line)
+        if m:
+            out[m.group(1)] = dict(reads=int(m.group(2)), ms_total=float(m.group(3)), ms_pileup=float(m.group(4)),
+                                   ms_cnv=float(m.group(5)), cigar_ops=int(m.group(6)), bases=int(m.group(7)),
+                                   len=int(m.group(8)))
+    return out
+
+
+def rows_digest(path):
+    """(rows, sha256) of a VCF's non-header lines."""
+    h, n = hashlib.sha256(), 0
+    with open(path, "rb") as f:
+        for line in f:
+            if not line.startswith(b"#"):
+                h.update(line)
+                n += 1
+    return n, h.hexdigest()
+
+
+def roofline_of(per_launch, alone=None):
+    """per_launch: [(bytes, ms, chrom_len)] of the pileup kernel's launches."""
+    byt = sum(b for b, _, _ in per_launch)
+    sec = sum(ms for _, ms, _ in per_launch) / 1e3
+    bases = sum(L for _, _, L in per_launch)
+    achieved = byt / sec / 1e9
+    survey = SURVEY_BYTES_PER_BASE * bases / sec / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_genome_30x.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(f"{PILEUP_KERNEL}_hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    r = {"bound": "hbm", "kernel": PILEUP_KERNEL, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+         "bytes_model": "this build (DESIGN.md 7): read records + CIGAR + 1.5 B per read base + 13 B per reference "
+                        "base, summed over the timed launches (HIP events on the scan stream)",
+         "launches": len(per_launch), "launch_ms_mean": round(sec * 1e3 / max(len(per_launch), 1), 3),
+         "bytes_per_100mb": round(byt / bases * 1e8), "survey_bytes_per_base": SURVEY_BYTES_PER_BASE,
+         "survey_achieved": round(survey, 1), "survey_frac": round(survey / HBM_PEAK_GBS, 4)}
+    if alone:
+        r["alone"] = alone
+    return r
+
+
 def cpu_baseline_and_concordance(work_dir, knobs, flags):
     """The oracle (CPU port of GROM's scan, one thread) on a bounded 3-contig
     sample of the workload's generator, whole run (BAM decode + scan + VCF);
-    then the GPU CLI on the same files, timed end to end (BAM decode, host
-    batches, upload, scans, rows) and compared byte for byte."""
+    then the GPU CLI on the same files, compared byte for byte."""
     from grom_amd import cli_main, last_error, run_synth
     total = sum(CPU_SAMPLE_LENS)
     sample = f"{len(CPU_SAMPLE_LENS)} contigs, {total / 1e6:g} Mb"
     bam, fa = run_synth(os.path.join(work_dir, "sample"), *synth_args(knobs, CPU_SAMPLE_LENS))
-    env = dict(os.environ, GROM_FILEDATE="20260101", GROM_SEED="7")
+    env = dict(os.environ, GROM_FILEDATE=FILEDATE, GROM_SEED=SEED)
     oracle = os.path.join(REPO, "oracle", "grom_oracle")
     t0 = time.perf_counter()
     r = subprocess.run([oracle, "-i", bam, "-r", fa, "-o", "cpu.vcf"] + flags, cwd=work_dir, env=env,
@@ -117,7 +239,7 @@ def cpu_baseline_and_concordance(work_dir, knobs, flags):
                      f"(grom_synth {' '.join(synth_args(knobs, CPU_SAMPLE_LENS))}), flags {' '.join(flags) or '-'}; "
                      f"whole oracle run (BAM decode + scan + VCF) in {dt:.2f} s, 1 thread"}
     t0 = time.perf_counter()
-    rc = cli_main(["-i", bam, "-r", fa, "-o", "gpu.vcf"] + flags, env={"GROM_FILEDATE": "20260101", "GROM_SEED": "7"},
+    rc = cli_main(["-i", bam, "-r", fa, "-o", "gpu.vcf"] + flags, env={"GROM_FILEDATE": FILEDATE, "GROM_SEED": SEED},
                   cwd=work_dir)
     dt_gpu = time.perf_counter() - t0
     if rc != 0:
@@ -127,86 +249,92 @@ def cpu_baseline_and_concordance(work_dir, knobs, flags):
     rows = sum(1 for ln in open(os.path.join(work_dir, "gpu.vcf")) if not ln.startswith("#"))
     conc = {"sample": f"the cpu_baseline sample ({sample}) through the GPU CLI (grom_cli_main)",
             "vcf_rows": rows, "identical_to_oracle": same,
-            "cli_end_to_end_s": round(dt_gpu, 2), "cli_end_to_end_mbases_per_s": round(total / dt_gpu / 1e6, 2),
-            "cli_note": "whole CLI run: insert pre-pass, BAM decode (host), upload, scans, VCF; on a sample this "
-                        "small the fixed costs (binomial tables, contexts) dominate"}
+            "cli_end_to_end_s": round(dt_gpu, 2), "cli_end_to_end_mbases_per_s": round(total / dt_gpu / 1e6, 2)}
     return cpu, conc
 
 
-def cli_whole_run_start(work_dir, knobs, flags, scale):
-    """Write the >=100 Mb BAM, start the oracle on it in the background (its
-    VCF is compared at the end), then time the GPU CLI twice as a fresh process."""
-    from grom_amd import GROM_BIN, run_synth
-    names = [n for n, _ in GRCH38]
-    lengths = [max(int(L * scale), 1_000_000) for _, L in GRCH38]
-    total = sum(lengths)
-    src = os.path.join(work_dir, "src")
-    os.makedirs(src, exist_ok=True)
-    t0 = time.perf_counter()
-    bam, fa = run_synth(os.path.join(src, "cli"), *synth_args(knobs, lengths), "-n", ",".join(names), timeout=1200)
-    t_synth = time.perf_counter() - t0
-    print(f"[bench] whole-run BAM written: {total / 1e6:.1f} Mb, {os.path.getsize(bam) / 1e9:.2f} GB in {t_synth:.1f} s",
-          file=sys.stderr, flush=True)
-    env = dict(os.environ, GROM_FILEDATE="20260101", GROM_SEED="7")
-    dirs = {}
-    for side in ("gpu", "cpu"):  # own copies of the side files (.mean, .info); same paths in the VCF header
-        d = os.path.join(work_dir, side)
-        os.makedirs(d, exist_ok=True)
-        for f, t in (("cli.bam", bam), ("cli.bam.bai", bam + ".bai"), ("cli.fa", fa)):
-            os.symlink(t, os.path.join(d, f))
-        dirs[side] = d
-    args = ["-i", "cli.bam", "-r", "cli.fa", "-o", "out.vcf"] + flags
-    runs = []
-    for _ in range(2):
-        t1 = time.perf_counter()
-        r = subprocess.run([GROM_BIN] + args, cwd=dirs["gpu"], env=dict(env, GROM_VERBOSE="1"), capture_output=True,
-                           text=True, timeout=600)
-        runs.append(time.perf_counter() - t1)
-        print(f"[bench] CLI whole run {len(runs)}: {runs[-1]:.2f} s", file=sys.stderr, flush=True)
-        if r.returncode != 0:
-            raise RuntimeError("GPU CLI failed on the whole-run BAM: " + r.stdout[-2000:] + r.stderr[-2000:])
-    dec = [ln for ln in r.stdout.splitlines() if ln.startswith("streamed decode:")]
-    info = {"bam": f"{len(lengths)} GRCh38 contigs x {scale:g} ({total / 1e6:.1f} Mb), same generator and flags "
-                   f"as the workload (grom_synth {' '.join(synth_args(knobs, ['...']))})",
-            "bam_bytes": os.path.getsize(bam), "genome_bases": total, "synth_s": round(t_synth, 1),
-            "cli_wall_s": [round(x, 3) for x in runs],
-            "value": round(total / min(runs) / 1e6, 2), "unit": "Mbases/s",
-            "value_first_run": round(total / runs[0] / 1e6, 2),
-            "decode": dec[-1] if dec else None,
-            "note": "grom_amd/bin/grom as a fresh process (process start, HIP init, BAM index + parallel decode on "
-                    "the host, pinned pieces -> HBM, scans, VCF + .ctx.vcf); best of two runs, the BAM in the page "
-                    "cache"}
-    # the oracle runs after the timed region (cli_whole_run_finish): beside
-    # it, it took host cores from the scans' row threads (1,640 vs 1,458 ms
-    # per pass in round 3)
-    return {"info": info, "args": args, "env": env, "dirs": dirs, "total": total}
+def resident_leg(local, knobs, lengths, names, bam, whole_vcf, steps, inflight):
+    """The genome generated on the host as the BAM's serial stream hands each
+    chromosome to its scan (grom_synth_chrom_stream), kept in HBM, scanned
+    with `inflight` chromosomes in flight; device-only Mbases/s, the pileup
+    kernel alone on the largest chromosome, and the rows against the whole
+    run's VCF / .ctx.vcf."""
+    import grom_amd
+    from grom_amd.shard import run_queue
+    imean, lseq, imin, imax = (int(x) for x in open(bam + ".mean").read().split()[:4])
+    params = grom_amd.default_params()
+    params.rmdup, params.gender = 1, 1
+    grom_amd.lib().grom_params_set_insert(ctypes.byref(params), imean, imin, imax, lseq)
+    order = sorted(range(len(lengths)), key=lambda i: (-lengths[i], i))  # longest first, as GROM.c:22318-22336
+    res, info = {}, {}
+    lock = threading.Lock()
+    t_gen = time.perf_counter()
 
-
-def cli_whole_run_finish(st):
-    info = st["info"]
-    oracle = os.path.join(REPO, "oracle", "grom_oracle")
-    st["t_oracle"] = time.perf_counter()
-    st["proc"] = subprocess.Popen([oracle] + st["args"], cwd=st["dirs"]["cpu"], env=st["env"],
-                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
-    while True:  # a line every 30 s while the oracle runs (long silent runs look hung)
+    def make(i):
+        b = grom_amd.SynthBatch.genome_chrom(lengths, i, params, names=names, coverage=knobs["coverage"],
+                                             read_len=READ_LEN, dup_frac=knobs["dup_frac"],
+                                             sv_per_mb=knobs["sv_per_mb"], cnv_rate=knobs["cnv_rate"],
+                                             cnv_range=knobs["cnv_range"], seed=knobs["seed"], stream=True)
         try:
-            err = st["proc"].communicate(timeout=30)[1]
-            break
-        except subprocess.TimeoutExpired:
-            print(f"[bench] oracle on the whole-run BAM: {time.perf_counter() - st['t_oracle']:.0f} s", file=sys.stderr,
-                  flush=True)
-    dt = time.perf_counter() - st["t_oracle"]
-    if st["proc"].returncode != 0:
-        info["identical_to_oracle"] = None
-        info["oracle_error"] = (err or "")[-500:]
-        return info
-    same = all(open(os.path.join(st["dirs"]["gpu"], "out" + ext), "rb").read() ==
-               open(os.path.join(st["dirs"]["cpu"], "out" + ext), "rb").read() for ext in (".vcf", ".ctx.vcf"))
-    info["identical_to_oracle"] = same
-    info["vcf_rows"] = sum(1 for ln in open(os.path.join(st["dirs"]["gpu"], "out.vcf")) if not ln.startswith("#"))
-    info["oracle_s"] = round(dt, 1)
-    info["oracle_mbases_per_s"] = round(st["total"] / dt / 1e6, 3)
-    return info
+            r = grom_amd.Resident(local, b.chrom, b.reads)
+            r.chrom.seed = int(SEED)  # what the CLI's scans get (GROM_SEED)
+            with lock:
+                res[i] = r
+                info[i] = {"bytes": launch_bytes(b.reads.n, b.reads.n_cigar_ops, b.reads.n_bases, lengths[i]),
+                           "resident_bytes": r.bytes}
+        finally:
+            b.close()
+
+    run_queue([make] * max(1, min(cpu_quota(), 16, len(order))), order)
+    t_gen = time.perf_counter() - t_gen
+    log(f"resident genome generated in {t_gen:.1f} s ({sum(v['resident_bytes'] for v in info.values()) / 1e9:.1f} GB)")
+    devs = [grom_amd.Device(local, params, slot=local + 8 * k) for k in range(inflight)]
+    texts, rec = {}, []
+    try:
+        def scanner(k, record):
+            def scan(i):
+                vcf, ctx, st = devs[k].scan_rows(res[i].chrom, res[i].reads, device_resident=True)
+                with lock:
+                    if record is None:
+                        texts[i] = (vcf, ctx)
+                    else:
+                        record.append((i, st.ms_pileup))
+            return scan
+        run_queue([scanner(k, None) for k in range(inflight)], order)  # warm pass; keeps the rows
+        _, st_alone = devs[0].scan(res[order[0]].chrom, res[order[0]].reads, device_resident=True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run_queue([scanner(k, rec) for k in range(inflight)], order)
+        dt = time.perf_counter() - t0
+    finally:
+        for d in reversed(devs):
+            d.close()
+        for r in res.values():
+            r.close()
+    # rows: the resident pass against the whole run
+    vcf = "".join(texts[i][0] for i in range(len(lengths)))
+    bnd = grom_amd.ctx_postpass("".join(texts[i][1] for i in range(len(lengths))), names, params.insert_max_size,
+                                params.lseq)
+    n_whole, d_whole = rows_digest(whole_vcf)
+    n_ctx, d_ctx = rows_digest(whole_vcf[:-4] + ".ctx.vcf")
+    same_vcf = (vcf.count("\n"), hashlib.sha256(vcf.encode()).hexdigest()) == (n_whole, d_whole)
+    same_ctx = (bnd.count("\n"), hashlib.sha256(bnd.encode()).hexdigest()) == (n_ctx, d_ctx)
+    big = order[0]
+    alone_ach = info[big]["bytes"] / (st_alone.ms_pileup / 1e3) / 1e9
+    out = {"value": round(sum(lengths) * steps / dt / 1e6, 1), "unit": "Mbases/s", "passes": steps,
+           "ms_per_pass": round(dt / steps * 1e3, 1), "scans_in_flight": inflight,
+           "host_generate_s": round(t_gen, 1),
+           "hbm_resident_gb": round(sum(v["resident_bytes"] for v in info.values()) / 1e9, 1),
+           "rows_identical_to_whole_run": same_vcf, "ctx_identical_to_whole_run": same_ctx,
+           "vcf_rows": n_whole, "bnd_rows": n_ctx,
+           "note": "inputs already in HBM when the pass starts (no BAM decode, no host->device copies); the rows "
+                   "are compared with the timed whole run's VCF and .ctx.vcf (sha256 of the rows)"}
+    alone = {"chrom": names[big], "launch_ms": round(st_alone.ms_pileup, 3), "achieved": round(alone_ach, 1),
+             "frac": round(alone_ach / HBM_PEAK_GBS, 4),
+             "survey_frac": round(SURVEY_BYTES_PER_BASE * lengths[big] / (st_alone.ms_pileup / 1e3) / 1e9
+                                  / HBM_PEAK_GBS, 4)}
+    launches = [(info[i]["bytes"], ms, lengths[i]) for i, ms in rec]
+    return out, alone, launches
 
 
 def main():
@@ -218,15 +346,14 @@ def main():
                     help="genome: configs[2]/[3] human-shape 3.09 Gb genome; chrom: configs[1] 100 Mb chromosome")
     ap.add_argument("--scale", type=float, default=1.0, help="scale every contig length (tests / quick runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="chromosome scans in flight per GPU: library context slots on the same device, one host "
-                         "thread each")
-    ap.add_argument("--gen-workers", type=int, default=0, help="host generator threads (0: auto)")
-    ap.add_argument("--cnv-rate", type=float, default=None, help="override the copy-number region rate (tests)")
-    ap.add_argument("--sweep-inflight", default="", help="e.g. 1,2,3,4: time one pass per value first (stderr)")
-    ap.add_argument("--cli-scale", type=float, default=0.04,
-                    help="contig scale of the whole-run CLI leg's BAM (0.04: 24 contigs, 124 Mb); 0 skips it")
+    ap.add_argument("--no-resident", action="store_true", help="skip the device-resident leg")
+    ap.add_argument("--resident-steps", type=int, default=2)
+    ap.add_argument("--inflight", type=int, default=2, help="resident leg: chromosome scans in flight per GPU")
+    ap.add_argument("--budget-s", type=float, default=540.0,
+                    help="skip the resident leg when it would end the run after this many seconds")
+    ap.add_argument("--workdir", default="", help="keep the BAM here (default: a temporary directory)")
     args = ap.parse_args()
+    t_start = time.perf_counter()
 
     import torch
     import torch.distributed as dist
@@ -239,152 +366,112 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import grom_amd
-    from grom_amd.shard import assign_chromosomes, max_over_ranks, run_queue
-
-    genome = args.workload == "genome"
-    if genome:
-        knobs, flags = C3, ["-M"]
-        names = [n for n, _ in GRCH38]
-        lengths = [max(int(L * args.scale), 1_000_000) for _, L in GRCH38]
-        mine = assign_chromosomes(lengths, world)[rank] if world > 1 else list(range(len(lengths)))
-    else:
-        knobs, flags = C2, []
-        names = ["chr1"]
-        lengths = [max(int(100_000_000 * args.scale), 1_000_000)]
-        mine = [0]
-    if args.cnv_rate is not None:
-        knobs = dict(knobs, cnv_rate=args.cnv_rate)
-    params = grom_amd.default_params()
-    params.rmdup = 1 if "-M" in flags else 0
-    gen = dict(coverage=knobs["coverage"], read_len=READ_LEN, dup_frac=knobs["dup_frac"],
-               sv_per_mb=knobs["sv_per_mb"], cnv_rate=knobs["cnv_rate"], cnv_range=knobs["cnv_range"],
-               seed=knobs["seed"] + (rank if not genome else 0))
-    # the whole-run CLI leg first, while HBM is empty (its oracle runs meanwhile)
-    cli_state, cli_dir = None, None
-    if genome and rank == 0 and world == 1 and args.cli_scale > 0 and not args.no_cpu_baseline:
-        cli_dir = tempfile.TemporaryDirectory()
-        cli_state = cli_whole_run_start(cli_dir.name, knobs, flags, args.cli_scale)
-        print(f"[bench] CLI whole run: {cli_state['info']['cli_wall_s']} s, {cli_state['info']['value']} Mbases/s",
-              file=sys.stderr, flush=True)
-    # genome-wide insert statistics (find_insert_mean runs once per BAM): the
-    # same generator on a 2 Mb probe, identical on every rank
-    probe = grom_amd.SynthBatch.genome_chrom([2_000_000], 0, params, **dict(gen, sv_per_mb=0.0, cnv_rate=0.0))
-    probe.close()
-
-    # generate each chromosome on the host and keep its inputs in HBM
-    order = sorted(mine, key=lambda i: (-lengths[i], i))  # longest first, as GROM.c:22318-22336
-    workers = args.gen_workers or max(1, min(8, 16 // max(world, 1), len(order)))
-    res, info = {}, {}
-    lock = threading.Lock()
-    mem_reserve = 48 << 30  # scratch of the scan contexts on the largest chromosome
-
-    def make(i):
-        b = grom_amd.SynthBatch.genome_chrom(lengths, i, params, names=names, **gen)
-        try:
-            r = grom_amd.Resident(local, b.chrom, b.reads)
-            with lock:
-                res[i] = r
-                info[i] = {"reads": b.reads.n, "bytes": algorithmic_bytes(b.reads, lengths[i]),
-                           "resident_bytes": r.bytes}
-            free = grom_amd.lib().grom_device_mem_free(local)
-            print(f"[bench] {names[i]}: {b.reads.n} reads generated and resident ({r.bytes / 1e9:.1f} GB), "
-                  f"{free / 2**30:.0f} GiB HBM free, {time.perf_counter() - t_gen:.0f} s", file=sys.stderr, flush=True)
-            if 0 <= free < mem_reserve:
-                raise RuntimeError(f"HBM nearly full after uploading {names[i]} ({free / 2**30:.1f} GiB free)")
-        finally:
-            b.close()
-
-    t_gen = time.perf_counter()
-    run_queue([make] * workers, order)
-    t_gen = time.perf_counter() - t_gen
-
-    if args.sweep_inflight:
-        for f in [int(v) for v in args.sweep_inflight.split(",")]:
-            dv = [grom_amd.Device(local, params, slot=local + 8 * k) for k in range(f)]
-            ot = [grom_amd.Out() for _ in dv]
-
-            def sw(k):
-                return lambda i: dv[k].scan(res[i].chrom, res[i].reads, device_resident=True, out=ot[k])
-            run_queue([sw(k) for k in range(f)], order)  # warm
-            t1 = time.perf_counter()
-            run_queue([sw(k) for k in range(f)], order)
-            t1 = time.perf_counter() - t1
-            print(f"[bench] inflight {f}: {t1 * 1e3:.0f} ms per pass, {sum(lengths[i] for i in mine) / t1 / 1e6:.1f} "
-                  f"Mbases/s, {grom_amd.lib().grom_device_mem_free(local) / 2**30:.0f} GiB HBM free", file=sys.stderr,
-                  flush=True)
-            for o in ot:
-                grom_amd.lib().grom_out_free(ctypes.byref(o))
-            for d in reversed(dv):
-                d.close()
-    F = max(1, min(args.inflight, 8))
-    devs = [grom_amd.Device(local, params, slot=local + 8 * k) for k in range(F)]
-    outs = [grom_amd.Out() for _ in devs]
-    pile_ms, pile_bytes, cnv_ms = [], [], []
-    rows = {}
-
-    def scanner(k, record):
-        def scan(i):
-            vcf_len, st = devs[k].scan(res[i].chrom, res[i].reads, device_resident=True, out=outs[k])
-            if record is not None:
-                with lock:
-                    record.append((i, st.ms_pileup, st.ms_cnv))
-            else:
-                rows[i] = ctypes.string_at(outs[k].vcf, vcf_len).count(b"\n")
-        return scan
-
-    # warmup passes (the first also counts each chromosome's VCF rows)
-    for w in range(args.warmup):
-        run_queue([scanner(k, None if w == 0 else []) for k in range(F)], order)
-    # the pileup kernel alone (nothing else on the GPU), on the largest chromosome
-    _, st_alone = devs[0].scan(res[order[0]].chrom, res[order[0]].reads, device_resident=True, out=outs[0])
+    from grom_amd.shard import assign_chromosomes, max_over_ranks, merge_rank_outputs
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    rec = []
+    genome = args.workload == "genome"
+    if genome:
+        knobs, flags = C3, list(GENOME_FLAGS)
+        names = [n for n, _ in GRCH38]
+        lengths = [max(int(L * args.scale), 1_000_000) for _, L in GRCH38]
+    else:
+        knobs, flags = C2, []
+        names = ["chr1"]
+        lengths = [max(int(100_000_000 * args.scale), 1_000_000)]
+    total = sum(lengths)
+    shares = assign_chromosomes(lengths, world)
+    mine = shares[rank]
+
+    # one shared directory on this node (rank 0 writes the BAM)
+    work = args.workdir or os.path.join(tempfile.gettempdir(), f"grom_bench_{os.environ.get('MASTER_PORT', 'solo')}")
+    if rank == 0:
+        shutil.rmtree(work, ignore_errors=True)
+        os.makedirs(work, exist_ok=True)
+        bam, fa, t_synth = write_genome(work, knobs, lengths, names)
+    barrier()
+    bam, fa = os.path.join(work, "genome.bam"), os.path.join(work, "genome.fa")
+
+    # the rank's CLI: its chromosomes, its GPU, its share of the CPUs
+    cpus = cpu_quota()
+    env = {"GROM_DEVICE": str(local)}
+    if world > 1:
+        env.update(GROM_CHROMS=",".join(names[i].lower() for i in mine),
+                   GROM_DECODE_THREADS=str(max(1, cpus // world)),
+                   GROM_CTX_RAW=os.path.join(work, f"rank{rank}.ctxraw"))
+    out = os.path.join(work, f"rank{rank}.vcf")
+    hdr_names = names  # BAM target names (the CTX post-pass maps mate ids to them)
+
+    def step():
+        dt, so = whole_run(work, bam, fa, out, flags, env)
+        if world > 1:
+            barrier()
+            if rank == 0:
+                m = open(bam + ".mean").read().split()  # insert mean, lseq, min, max (save_insert_mean)
+                vcf, bnd = merge_rank_outputs([os.path.join(work, f"rank{r}.vcf") for r in range(world)],
+                                              [os.path.join(work, f"rank{r}.ctxraw") for r in range(world)],
+                                              [n.lower() for n in names], hdr_names, int(m[3]), int(m[1]))
+                with open(os.path.join(work, "merged.vcf"), "w") as f:
+                    f.write(vcf)
+                with open(os.path.join(work, "merged.ctx.vcf"), "w") as f:
+                    f.write(bnd)
+        return dt, so
+
+    if world > 1 and rank == 0:
+        # the side files every rank's CLI reads (<bam>.mean, <fasta>.info) are
+        # written once here, before the ranks run concurrently (a plan-only run
+        # over no chromosome: the insert-statistics head of the file only)
+        whole_run(work, bam, fa, os.path.join(work, "prewarm.vcf"), flags, {"GROM_PLAN_ONLY": "1", "GROM_CHROMS": "-"})
+    barrier()
+    for w in range(args.warmup):
+        dt, _ = step()
+        log(f"warmup run {w + 1}: {dt:.2f} s")
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run_queue([scanner(k, rec) for k in range(F)], order)
+    runs, last = [], ""
+    for k in range(args.steps):
+        t1 = time.perf_counter()
+        _, last = step()
+        runs.append(time.perf_counter() - t1)
+        log(f"timed run {k + 1}: {runs[-1]:.2f} s")
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, device="cuda")
-    for o in outs:
-        grom_amd.lib().grom_out_free(ctypes.byref(o))
+    value = total * args.steps / dt / 1e6
+    stats = chrom_stats(last)  # this rank's chromosomes, last timed run
+    dec = [ln for ln in last.splitlines() if ln.startswith("streamed decode:")]
+    phases = [ln for ln in last.splitlines() if ln.startswith("cli phases")]
 
-    total_bases = sum(lengths) if genome else lengths[0] * world
-    value = total_bases * args.steps / dt / 1e6
-    launch_bytes = sum(info[i]["bytes"] for i, _, _ in rec)
-    launch_s = sum(ms for _, ms, _ in rec) / 1e3
-    achieved = launch_bytes / launch_s / 1e9
-    bases_launched = sum(lengths[i] for i, _, _ in rec)
-    survey_achieved = SURVEY_BYTES_PER_BASE * bases_launched / launch_s / 1e9
-    big = order[0]
-    alone_ach = info[big]["bytes"] / (st_alone.ms_pileup / 1e3) / 1e9
-    tag = "genome_30x" if genome else f"{lengths[0] // 1_000_000}Mb_30x"
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", f"pmc_{tag}.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get(f"{PILEUP_KERNEL}_hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    launches = [(launch_bytes(s["reads"], s["cigar_ops"], s["bases"], s["len"]), s["ms_pileup"], s["len"])
+                for s in stats.values()]
+    resident, alone = None, None
+    if rank == 0 and world == 1:
+        remaining = args.budget_s - (time.perf_counter() - t_start)
+        est = 0.55 * (t_synth if genome else 30.0) + 20.0  # host generation (no compression) + passes
+        if args.no_resident:
+            resident = {"skipped": "--no-resident"}
+        elif est > remaining:
+            resident = {"skipped": f"time budget (--budget-s {args.budget_s:g}: {remaining:.0f} s left, the leg "
+                                   f"takes about {est:.0f} s)"}
+        else:
+            resident, alone, rl = resident_leg(local, knobs, lengths, names, bam, out, args.resident_steps,
+                                               max(1, min(args.inflight, 8)))
+            log(f"device-resident: {resident['value']} Mbases/s, rows identical: "
+                f"{resident['rows_identical_to_whole_run']}/{resident['ctx_identical_to_whole_run']}")
     if rank == 0:
         cpu = conc = None
         if world == 1 and not args.no_cpu_baseline:
             with tempfile.TemporaryDirectory() as d:
                 cpu, conc = cpu_baseline_and_concordance(d, knobs, flags)
-        cli_info = cli_whole_run_finish(cli_state) if cli_state else None
-        if cli_dir:
-            cli_dir.cleanup()
+        n_rows, _ = rows_digest(out if world == 1 else os.path.join(work, "merged.vcf"))
         wl = ("BASELINE configs[2]: synthetic 30x 2x150 bp human-shape genome, 24 GRCh38 contigs "
-              f"({sum(lengths) / 1e9:.3f} Gb), SNV/indel, {knobs['sv_per_mb']:.2f} breakpoint SVs/Mb "
-              "(DEL/DUP/INV/INS/CTX with split reads + discordant pairs), 500 CNVs/3.1 Gb, 5% PCR duplicates, -M"
-              + ("; chromosomes LPT-sharded over ranks (configs[3])" if world > 1 else "")
-              if genome else
-              "BASELINE configs[1]: one 100 Mb chromosome per GPU, 30x 2x150 bp, SNV/indel")
+              f"({total / 1e9:.3f} Gb), SNV/indel, {knobs['sv_per_mb']:.2f} breakpoint SVs/Mb "
+              "(DEL/DUP/INV/INS/CTX with split reads + discordant pairs), 500 CNVs/3.1 Gb, 5% PCR duplicates, "
+              "flags -M -g 1" + ("; chromosomes LPT-sharded over ranks, one CLI process per GPU (configs[3])"
+                                 if world > 1 else "")
+              if genome else "BASELINE configs[1]: one 100 Mb chromosome, 30x 2x150 bp, SNV/indel")
         line = {
             "metric": "Mbases/sec scanned (whole genome) + VCF concordance vs ref",
             "value": round(value, 3),
@@ -394,48 +481,36 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong" if genome else "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (seeded generator grom_amd/csrc/synth.c, inputs resident in HBM)",
+            "data": "synthetic (seeded generator grom_amd/csrc/synth.c, written as BAM + BAI + FASTA by grom_synth)",
             "config": {
-                "workload": wl + "; step = every chromosome through grom_scan_chrom_device (pileup/SNV, "
-                                 "duplicate filter, breakpoint evidence + tests, SV/INDEL rows, CTX records, "
-                                 "read-depth CNV path + rows)",
-                "genome_bases": total_bases, "chromosomes": len(lengths), "chromosomes_rank0": len(mine),
+                "workload": wl + "; step = one whole run of the drop-in CLI (grom_amd/bin/grom, a fresh process): "
+                                 "BAM index, BGZF decode on the host into pinned pieces, host->HBM copies, every "
+                                 "chromosome's scan (pileup/SNV, duplicate filter, breakpoint evidence + tests, "
+                                 "SV/INDEL rows, CTX records, read-depth CNV path + rows), VCF + CTX post-pass",
+                "genome_bases": total, "chromosomes": len(lengths), "chromosomes_rank0": len(mine),
                 "coverage": knobs["coverage"], "read_len": READ_LEN, "flags": " ".join(flags),
-                "reads_rank0": sum(info[i]["reads"] for i in mine),
-                "vcf_rows_rank0": sum(rows.values()),
-                "hbm_resident_gb_rank0": round(sum(info[i]["resident_bytes"] for i in mine) / 1e9, 1),
-                "host_generate_s": round(t_gen, 1), "generator_threads": workers,
-                "scans_in_flight_per_gpu": F,
-                "cnv_ms_per_step_rank0": round(sum(c for _, _, c in rec) / args.steps, 1),
+                "bam_bytes": os.path.getsize(bam), "synth_s": round(t_synth, 1),
+                "run_s": [round(x, 3) for x in runs],
+                "vcf_rows": n_rows,
+                "host_cpus": cpus, "decode_threads": int(env.get("GROM_DECODE_THREADS", cpus)),
+                "decode_rank0": dec[-1] if dec else None,
+                "phases_rank0": phases[-1] if phases else None,
+                "reads_rank0": sum(s["reads"] for s in stats.values()),
+                "pileup_ms_rank0": round(sum(s["ms_pileup"] for s in stats.values()), 1),
+                "cnv_ms_rank0": round(sum(s["ms_cnv"] for s in stats.values()), 1),
             },
-            "roofline": {
-                "bound": "hbm", "kernel": PILEUP_KERNEL,
-                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "bytes_model": "this build (DESIGN.md 6): read records + CIGAR + 1.5 B per read base + 13 B per "
-                               "reference base, summed over the timed launches",
-                "launches": len(rec), "launch_ms_mean": round(launch_s * 1e3 / len(rec), 3),
-                "bytes_per_100mb": round(launch_bytes / bases_launched * 1e8),
-                "survey_bytes_per_base": SURVEY_BYTES_PER_BASE,
-                "survey_achieved": round(survey_achieved, 1),
-                "survey_frac": round(survey_achieved / HBM_PEAK_GBS, 4),
-                "alone": {"chrom": names[big], "launch_ms": round(st_alone.ms_pileup, 3),
-                          "achieved": round(alone_ach, 1), "frac": round(alone_ach / HBM_PEAK_GBS, 4),
-                          "survey_frac": round(SURVEY_BYTES_PER_BASE * lengths[big] / (st_alone.ms_pileup / 1e3)
-                                               / 1e9 / HBM_PEAK_GBS, 4)},
-            },
+            "roofline": roofline_of(launches, alone) if launches else None,
             "cpu_baseline": cpu,
             "concordance": conc,
-            "cli_whole_run": cli_info,
+            "device_resident": resident,
         }
         print(json.dumps(line), flush=True)
-    for d in reversed(devs):
-        d.close()
-    for r in res.values():
-        r.close()
+    barrier()
+    if rank == 0 and not args.workdir:
+        shutil.rmtree(work, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
 

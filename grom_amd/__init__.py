@@ -132,6 +132,8 @@ _SIGS = {
     "grom_synth_batch": (C.c_void_p, [C.c_int64, C.c_double, C.c_int32, C.c_double, C.c_double, C.c_uint64,
                                       C.POINTER(Params)]),
     "grom_synth_chrom": (C.c_void_p, [C.POINTER(SynthSpec), C.POINTER(Params)]),
+    "grom_synth_chrom_stream": (C.c_void_p, [C.POINTER(SynthSpec), C.POINTER(Params)]),  # ABI 7
+    "grom_reads_digest": (C.c_uint64, [C.POINTER(Reads)]),
     "grom_resident_new": (C.c_void_p, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Chrom),
                                        C.POINTER(Reads)]),
     "grom_resident_bytes": (C.c_int64, [C.c_void_p]),
@@ -301,17 +303,21 @@ class SynthBatch:
     def genome_chrom(cls, lengths, chrom: int, params: Params, names=None, coverage: float = 30.0,
                      read_len: int = 150, ploidy: int = 2, insert_mean: float = 500.0, insert_sd: float = 50.0,
                      dup_frac: float = 0.0, sv_per_mb: float = 0.0, cnv_rate: float = 0.0,
-                     cnv_range=(0, 0), chr_cov=None, munmap_frac: float = 0.002, seed: int = 2) -> "SynthBatch":
+                     cnv_range=(0, 0), chr_cov=None, munmap_frac: float = 0.002, seed: int = 2,
+                     stream: bool = False) -> "SynthBatch":
         """Chromosome `chrom` of a multi-chromosome synthetic genome (grom_synth_chrom).
-        `params` keeps genome-wide insert statistics once set (see include/grom_amd.h)."""
+        `params` keeps genome-wide insert statistics once set (see include/grom_amd.h).
+        stream=True: as the chromosome's scan sees it inside the genome's BAM
+        (grom_synth_chrom_stream: the serial stream's Q1 drops and pending-record length)."""
         arr = (C.c_int64 * len(lengths))(*lengths)
         cov = (C.c_double * len(lengths))(*chr_cov) if chr_cov is not None else None
         sp = SynthSpec(len(lengths), chrom, arr, ",".join(names).encode() if names else None, coverage, read_len,
                        ploidy, insert_mean, insert_sd, dup_frac, sv_per_mb, cnv_rate, cnv_range[0], cnv_range[1],
                        cov, munmap_frac, seed)
-        h = lib().grom_synth_chrom(C.byref(sp), C.byref(params))
+        fn = lib().grom_synth_chrom_stream if stream else lib().grom_synth_chrom
+        h = fn(C.byref(sp), C.byref(params))
         if not h:
-            raise RuntimeError(f"grom_synth_chrom failed for chromosome {chrom}")
+            raise RuntimeError(f"grom_synth_chrom failed for chromosome {chrom}: {last_error()}")
         return cls(lengths[chrom], params=params, _handle=h)
 
     def close(self):

@@ -411,6 +411,8 @@ static void write_dumps(int slot, const chrom_plan *cp, const grom_chrom *ch, co
     free(caf);
 }
 
+static int chrom_wanted(const char *name);
+
 static uint32_t chrom_seed(void) {
     /* srand(time()) per chromosome, GROM.c:1584; GROM_SEED pins it */
     const char *e = getenv("GROM_SEED");
@@ -422,6 +424,7 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     chrom_plan *cp = j->cp;
     j->text = j->ctx_text = NULL;
     j->text_len = j->ctx_len = 0;
+    if (!chrom_wanted(cp->name)) return GROM_OK; /* serial path: another rank's chromosome */
     grom_chrom ch;
     memset(&ch, 0, sizeof(ch));
     grom_reads rd;
@@ -442,6 +445,13 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
         grom_batch_view(b, &rd);
         n_reads = b->n;
     } else {
+        if (g_plan_only) { /* streamed plan-only (host tests): the decoder's host mirror */
+            pd_mirror_view(j->pd, j->k, &rd);
+            printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d lseq_tail=%d digest=%016llx\n", cp->name, cp->tid,
+                   (long long)j->facts.n_reads, j->facts.n_skip, j->facts.p_last, j->facts.lseq_tail,
+                   (unsigned long long)pd_digest(&rd));
+            return GROM_OK;
+        }
         ch.lseq_tail = j->facts.lseq_tail;
         ch.n_skip = j->facts.n_skip;
         ch.p_last = j->facts.p_last;
@@ -484,9 +494,22 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     }
     free(out.side);
     if (getenv("GROM_DUMP")) write_dumps(slot, cp, &ch, &rd, j->has_batch ? NULL : j->stage, P);
-    if (verbose)
-        printf("%s: %lld reads, %.3f ms on GPU (%.2f Mbases/s)\n", cp->name, (long long)n_reads, st.ms_total,
-               st.ms_total > 0 ? cp->len / (st.ms_total * 1e3) : 0.0);
+    if (verbose) {
+        /* the pileup kernel's launch and its inputs' sizes (bench.py's roofline) */
+        int64_t n_cig = rd.n_cigar_ops, n_b = rd.n_bases;
+        if (!j->has_batch) {
+            grom_chrom dc;
+            grom_reads dr;
+            if (grom_stage_view(j->stage, &ch, &dc, &dr) == GROM_OK) {
+                n_cig = dr.n_cigar_ops;
+                n_b = dr.n_bases;
+            }
+        }
+        printf("%s: %lld reads, %.3f ms on GPU (%.2f Mbases/s); pileup %.3f ms, cnv %.3f ms, cigar_ops %lld, "
+               "bases %lld, len %ld\n", cp->name, (long long)n_reads, st.ms_total,
+               st.ms_total > 0 ? cp->len / (st.ms_total * 1e3) : 0.0, st.ms_pileup, st.ms_cnv, (long long)n_cig,
+               (long long)n_b, (long)cp->len);
+    }
     return GROM_OK;
 }
 
@@ -661,17 +684,25 @@ static int setup_workers(cli_state *S) {
     return 0;
 }
 
+/* set once the streamed run printed the insert lines: a serial rerun after
+ * a late fallback (the index plan contradicted mid-file) does not print them
+ * again, so stdout reads as one run */
+static __thread int t_insert_printed;
+
 static void print_insert(cli_state *S, int imean, int lseq, int imin, int imax, long mapped) {
-    printf("insert_min_size, insert_max_size %d %d\n", imin, imax);
+    const int quiet = t_insert_printed;
+    t_insert_printed = 1;
+    if (!quiet) printf("insert_min_size, insert_max_size %d %d\n", imin, imax);
     char mean_name[4096];
     snprintf(mean_name, sizeof(mean_name), "%s.mean", S->bam_name);
     FILE *mf = fopen(mean_name, "w"); /* save_insert_mean, GROM.c:994-1008 */
     if (mf) {
-        printf("Saving insert_mean et al to %s\n", mean_name);
+        if (!quiet) printf("Saving insert_mean et al to %s\n", mean_name);
         fprintf(mf, "%d %d %d %d %ld\n", imean, lseq, imin, imax, mapped);
         fclose(mf);
     }
     grom_params_set_insert(&S->P, imean, imin, imax, lseq);
+    if (quiet) return;
     printf("insert mean, insert minimum, insert maximum: %d %d %d\n", S->P.insert_mean, imin, imax);
     printf("median read length: %d\n", lseq);
 }
@@ -687,6 +718,14 @@ static int passes_length(const cli_state *S, const chrom_plan *c) {
 }
 
 static void finish_outputs(cli_state *S, textbuf *ctx_all) {
+    const char *raw = getenv("GROM_CTX_RAW"); /* the raw CTX rows, for a merge of several ranks' runs */
+    if (raw) {
+        FILE *f = fopen(raw, "w");
+        if (f) {
+            if (ctx_all->len) fwrite(ctx_all->p, 1, ctx_all->len, f);
+            fclose(f);
+        }
+    }
     /* CTX post-pass (GROM.c:22400-22770): pair the translocation rows of all
      * chromosomes with their mates and write them under the header */
     FILE *ctx = fopen(S->ctx_name, "w");
@@ -902,6 +941,42 @@ static void *fasta_main(void *arg) {
     return NULL;
 }
 
+/* the CPUs this process may use: the cgroup's CPU quota when it has one
+ * (cpu.max "quota period"; a container's share of a large host), else the
+ * online CPUs -- more decoder threads than that only contend */
+static int host_cpus(void) {
+    long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (f) {
+        char q[64] = "";
+        long period = 0;
+        if (fscanf(f, "%63s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const long c = (atol(q) + period - 1) / period;
+            if (c >= 1 && c < ncpu) ncpu = c;
+        }
+        fclose(f);
+    }
+    return ncpu < 1 ? 1 : (int)ncpu;
+}
+
+/* GROM_CHROMS=name[,name...]: scan and write only these chromosomes (one
+ * rank's share of a genome, bench.py --gpus N); the others keep their place
+ * in the plan, so each scanned chromosome gets the records the serial stream
+ * of a whole run would give it */
+static int chrom_wanted(const char *name) {
+    const char *w = getenv("GROM_CHROMS");
+    if (!w || !*w) return 1;
+    const size_t L = strlen(name);
+    for (const char *p = w; *p;) {
+        const char *e = strchr(p, ',');
+        const size_t n = e ? (size_t)(e - p) : strlen(p);
+        if (n == L && strncmp(p, name, n) == 0) return 1;
+        if (!e) break;
+        p = e + 1;
+    }
+    return 0;
+}
+
 static int run_streamed(cli_state *S) {
     grom_params *P = &S->P;
     const double t_start = clock_gettime_s();
@@ -913,8 +988,7 @@ static int run_streamed(cli_state *S) {
         cin[c].target_name = S->plan[c].target;
     }
     const char *dt = getenv("GROM_DECODE_THREADS");
-    long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
-    int n_thr = dt ? atoi(dt) : (int)(ncpu < 16 ? ncpu : 16);
+    int n_thr = dt ? atoi(dt) : host_cpus();
     if (n_thr < 1) n_thr = 1;
     char why[256] = "";
     pd_session *pd = pd_open(S->bam_name, &S->hdr, cin, S->n_cand, P->splitread, P->read_name_len, n_thr, why,
@@ -976,6 +1050,12 @@ static int run_streamed(cli_state *S) {
             pd_add_stage(pd, st, atoi(wd));
         }
     }
+    if (getenv("GROM_CHROMS")) {
+        int *want = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
+        for (int c = 0; c < S->n_cand; c++) want[c] = chrom_wanted(S->plan[c].name);
+        pd_set_wanted(pd, want);
+        free(want);
+    }
     if (pd_start(pd, P->min_mapq, S->n_dev, dev_of, g_plan_only)) {
         fprintf(stderr, "grom: %s\n", pd_error(pd));
         pd_close(pd);
@@ -1004,7 +1084,7 @@ static int run_streamed(cli_state *S) {
     int *pidx = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
     int n_plan = 0;
     for (int c = 0; c < S->n_cand; c++)
-        if ((keep[c] = passes_length(S, &S->plan[c]))) {
+        if ((keep[c] = passes_length(S, &S->plan[c])) && chrom_wanted(S->plan[c].name)) {
             pidx[n_plan] = c;
             plan[n_plan++] = &S->plan[c];
         }
@@ -1034,10 +1114,10 @@ static int run_streamed(cli_state *S) {
     pthread_cond_init(&F.cv, NULL);
     pthread_create(&fthr, NULL, fasta_main, &F);
     fasta_started = 1;
-    if (!g_plan_only) {
-        pool_start(&pool, S, n_plan, &workers, &tids);
-        started = 1;
-    }
+    /* (plan-only: the workers print each chromosome's plan line, so the host
+     * tests run the pool beside the streamed decoder) */
+    pool_start(&pool, S, n_plan, &workers, &tids);
+    started = 1;
     for (int k = 0; k < n_plan; k++) {
         grom_stage *st = NULL;
         pd_chrom_facts facts;
@@ -1049,24 +1129,18 @@ static int run_streamed(cli_state *S) {
             status = 1;
             break;
         }
-        if (g_plan_only) {
-            grom_reads rd;
-            pd_mirror_view(pd, pidx[k], &rd);
-            printf("plan %s tid=%d reads=%lld n_skip=%d p_last=%d lseq_tail=%d digest=%016llx\n", plan[k]->name,
-                   plan[k]->tid, (long long)facts.n_reads, facts.n_skip, facts.p_last, facts.lseq_tail,
-                   (unsigned long long)pd_digest(&rd));
-            continue;
-        }
-        pthread_mutex_lock(&F.mu);
-        while (F.loaded <= k) pthread_cond_wait(&F.cv, &F.mu);
-        F.consumed = k + 1;
-        pthread_cond_broadcast(&F.cv);
-        pthread_mutex_unlock(&F.mu);
-        if (!plan[k]->ref || grom_stage_set_ref(st, plan[k]->ref, plan[k]->len) != GROM_OK) {
-            fprintf(stderr, "grom: staging the reference of %s failed: %s\n", plan[k]->name, grom_last_error());
-            status = 1;
-            pd_release_stage(pd, st);
-            break;
+        if (!g_plan_only) {
+            pthread_mutex_lock(&F.mu);
+            while (F.loaded <= k) pthread_cond_wait(&F.cv, &F.mu);
+            F.consumed = k + 1;
+            pthread_cond_broadcast(&F.cv);
+            pthread_mutex_unlock(&F.mu);
+            if (!plan[k]->ref || grom_stage_set_ref(st, plan[k]->ref, plan[k]->len) != GROM_OK) {
+                fprintf(stderr, "grom: staging the reference of %s failed: %s\n", plan[k]->name, grom_last_error());
+                status = 1;
+                pd_release_stage(pd, st);
+                break;
+            }
         }
         pthread_mutex_lock(&pool.mu);
         grom_job *j = &pool.jobs[k];
@@ -1089,8 +1163,9 @@ done:
         pthread_cond_broadcast(&F.cv);
         pthread_mutex_unlock(&F.mu);
         pthread_join(fthr, NULL);
-        for (int k = 0; k < n_plan; k++)
-            if (plan[k]->ref && (fallback || status)) { free(plan[k]->ref); plan[k]->ref = NULL; }
+        /* references loaded but never handed to a worker are freed with the
+         * plan at the end of cli_run, after the workers are joined (a worker
+         * frees its own job's reference when its scan ends) */
         pthread_mutex_destroy(&F.mu);
         pthread_cond_destroy(&F.cv);
     }
@@ -1104,9 +1179,9 @@ done:
         pd_counters pc;
         pd_get_counters(pd, &pc);
         printf("streamed decode: %lld records in %lld pieces, %d threads (%s), %.2f GB inflated, %.2f GB to HBM, "
-               "decoder busy %.2f s (inflate %.2f s), uploader %.2f s (waiting %.2f s), wall %.2f s\n",
+               "decoder busy %.2f s (inflate %.2f s, file reads %.2f s), uploader %.2f s (waiting %.2f s), wall %.2f s\n",
                (long long)pc.records, (long long)pc.pieces, pc.threads, pc.libdeflate ? "libdeflate" : "zlib",
-               pc.inflated_bytes / 1e9, pc.h2d_bytes / 1e9, pc.decode_thread_s, pc.inflate_s, pc.upload_s, pc.wait_s,
+               pc.inflated_bytes / 1e9, pc.h2d_bytes / 1e9, pc.decode_thread_s, pc.inflate_s, pc.io_s, pc.upload_s, pc.wait_s,
                clock_gettime_s() - t_start);
     }
     S->t_scans = clock_gettime_s();
@@ -1290,6 +1365,7 @@ out_hdr:
 }
 
 int grom_cli_main(int argc, char **argv) {
+    t_insert_printed = 0;
     int rc = cli_run(argc, argv, 0);
     if (rc == CLI_FALLBACK) {
         if (getenv("GROM_VERBOSE")) printf("reading the BAM serially\n");

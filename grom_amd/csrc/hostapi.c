@@ -9,6 +9,7 @@
 
 #include "../../include/grom_amd.h"
 #include "stream.h"
+#include "pdecode.h"
 #include "synth.h"
 
 struct grom_batch_handle {
@@ -137,7 +138,30 @@ static void on_record_direct(void *ctx, const bam_rec *r) {
     grom_batch_add(d->b, r, d->s0);
 }
 
-grom_batch_handle *grom_synth_chrom(const grom_synth_spec *sp, grom_params *P) {
+/* the stream of one chromosome inside a whole genome's BAM (every chromosome
+ * processed, in order): the previous chromosome's loop took its first two
+ * records (GROM.c:5740, 14960-14976) */
+struct stream_ctx { grom_batch *b; int32_t s0; int64_t drop; };
+static void on_record_stream(void *ctx, const bam_rec *r) {
+    struct stream_ctx *d = (struct stream_ctx *)ctx;
+    if (d->drop > 0) { d->drop--; return; }
+    grom_batch_add(d->b, r, d->s0);
+}
+static void on_first_record(void *ctx, const bam_rec *r) { *(int32_t *)ctx = r->l_qseq; }
+
+static grom_batch_handle *synth_chrom(const grom_synth_spec *sp, grom_params *P, int stream);
+
+grom_batch_handle *grom_synth_chrom(const grom_synth_spec *sp, grom_params *P) { return synth_chrom(sp, P, 0); }
+
+grom_batch_handle *grom_synth_chrom_stream(const grom_synth_spec *sp, grom_params *P) {
+    if (!P || P->half_one_base_rd_len <= 0) {
+        grom_set_last_error("grom_synth_chrom_stream: set the insert statistics first (grom_params_set_insert)");
+        return NULL;
+    }
+    return synth_chrom(sp, P, 1);
+}
+
+static grom_batch_handle *synth_chrom(const grom_synth_spec *sp, grom_params *P, int stream) {
     if (!sp || !P || sp->n_chr < 1 || sp->n_chr > SYNTH_MAX_CHR || sp->chrom < 0 || sp->chrom >= sp->n_chr ||
         !sp->chr_len)
         return NULL;
@@ -186,7 +210,18 @@ grom_batch_handle *grom_synth_chrom(const grom_synth_spec *sp, grom_params *P) {
     h->ref = synth_reference(&c, ci);
     grom_batch_init(&h->b, ci, P->read_name_len);
     grom_batch_set_sv(&h->b, c.chr_name[ci], P->splitread);
-    if (P->half_one_base_rd_len > 0) {
+    if (stream) {
+        struct stream_ctx d = {&h->b, P->one_base_rd_len / 4 + 1, ci > 0 ? 2 : 0};
+        synth_reads(&c, ci, h->ref, on_record_stream, &d);
+        if (ci + 1 < c.n_chr) { /* the record that ends the stream: the next chromosome's first */
+            synth_cfg c1 = c;
+            c1.max_emit = 1;
+            char *r1 = synth_reference(&c1, ci + 1);
+            int32_t lq = -1;
+            if (r1 && synth_reads(&c1, ci + 1, r1, on_first_record, &lq) == 1 && h->b.n_seen > 0) h->b.lseq_tail = lq;
+            free(r1);
+        }
+    } else if (P->half_one_base_rd_len > 0) {
         struct direct_ctx d = {&h->b, P->one_base_rd_len / 4 + 1};
         synth_reads(&c, ci, h->ref, on_record_direct, &d);
     } else {
@@ -202,6 +237,8 @@ grom_batch_handle *grom_synth_chrom(const grom_synth_spec *sp, grom_params *P) {
     grom_batch_finish(&h->b, P->one_base_rd_len / 4 + 1, P->overlap_mult, P->insert_max_size);
     return h;
 }
+
+uint64_t grom_reads_digest(const grom_reads *r) { return pd_digest(r); }
 
 int grom_batch_get(grom_batch_handle *h, grom_chrom *ch, grom_reads *rd) {
     if (!h) return GROM_E_ARG;

@@ -82,7 +82,7 @@ __global__ void k_prep(int64_t n, ReadArrays R, ReadMeta *__restrict__ meta, int
         m.a = make_uint4((uint32_t)p, (uint32_t)(p + span), (uint32_t)lq, R.name_id[i]);
         m.b = make_uint4(cb, (ce - cb) | (fl << 16),
                          mq | (keep << 8) | (fast ? MK_FAST : 0u) | ((fl & 0x10u) ? MK_REV : 0u) |
-                             (mq >= (uint32_t)min_mapq ? MK_HQ : 0u),
+                             ((int32_t)mq >= min_mapq ? MK_HQ : 0u),  // signed, as tally_base (-q may be < 0)
                          (uint32_t)(bo & 0xffffffffu));
         m.c = make_uint4((uint32_t)((uint64_t)bo >> 32), (uint32_t)R.mtid[i], (uint32_t)R.mpos[i],
                          (uint32_t)R.isize[i]);
@@ -657,7 +657,7 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
             if (rm.b.z & MK_FAST) {
                 const int32_t lo = max(p0, t0) - t0, hi = min(p0 + len, t0 + TG) - t0;
                 if (lo < hi) {
-                    const uint32_t inc = (mq >= (uint32_t)a.rd_min_mapq) ? 1u : 65536u;
+                    const uint32_t inc = ((int32_t)mq >= a.rd_min_mapq) ? 1u : 65536u;  // signed, as the oracle
                     atomicAdd(&L.dmq[lo], (int32_t)mq);
                     atomicSub(&L.dmq[hi], (int32_t)mq);
                     atomicAdd(&L.dcnt[lo], inc);

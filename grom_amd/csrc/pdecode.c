@@ -130,13 +130,14 @@ static int rd_fetch(pd_reader *r, int64_t off, int64_t need) {
     if (off + want > r->file_size) want = r->file_size - off;
     if (want < need) return -1;
     int64_t got = 0;
+    const double t0 = now_s();
     while (got < want) {
         ssize_t k = pread(r->fd, r->cbuf + got, (size_t)(want - got), (off_t)(off + got));
         if (k <= 0) break;
         got += k;
     }
+    r->t_io += now_s() - t0;
     if (got < need) return -1;
-    r->t_io += 0;
     r->cbuf_off = off;
     r->cbuf_len = got;
     return 0;
@@ -402,6 +403,8 @@ struct pd_session {
     int walk_set, final_pending, final_applied;
     int next_final, finalizing; /* the uploader's finalisation cursor */
     int *keep;             /* final plan (per preliminary chromosome) */
+    int *want;             /* scanned by this process (GROM_CHROMS): unwanted plan chromosomes keep their
+                              place in the serial stream's plan but are neither decoded nor staged */
     int32_t index_start, overlap_mult, insert_max;
     /* devices and stages (pd_stream_chrom's caller owns the stages) */
     int plan_only, no_mirror;
@@ -413,12 +416,13 @@ struct pd_session {
     int n_stage, cap_stage, extra_stages;
     /* counters */
     int64_t c_records, c_inflated, c_compressed, c_h2d;
-    double c_dec_s, c_upl_s, c_wait_s, c_inflate_s;
+    double c_dec_s, c_upl_s, c_wait_s, c_inflate_s, c_io_s;
     /* GROM_TRACE */
     char *trace_path;
     double t0;
     struct { double t; int64_t a, b; int ev, thr; } *tr;
     int64_t tr_n, tr_cap;
+    int test_soft_abort;   /* GROM_TEST_SOFT_ABORT=<piece>: contradict the plan at that piece (tests) */
     /* uploader scratch */
     uint32_t *remap;
     int64_t remap_cap;
@@ -989,6 +993,7 @@ static void *decoder_main(void *arg) {
     s->c_dec_s += secs;
     s->c_inflated += r.inflated;
     s->c_inflate_s += r.t_inflate;
+    s->c_io_s += r.t_io;
     s->c_compressed += r.compressed;
     pthread_mutex_unlock(&s->mu);
     rd_free(&r);
@@ -1452,7 +1457,11 @@ static int chrom_finalize(pd_session *s, int k) {
         dp = s->plan_only ? (int32_t *)malloc(4 * (size_t)ndr) : (int32_t *)grom_pinned_alloc(4 * (size_t)ndr);
         dl = s->plan_only ? (int32_t *)malloc(4 * (size_t)ndr) : (int32_t *)grom_pinned_alloc(4 * (size_t)ndr);
         db = s->plan_only ? (int64_t *)malloc(8 * (size_t)ndr) : (int64_t *)grom_pinned_alloc(8 * (size_t)ndr);
-        if (!dp || !dl || !db) return -1;
+        if (!dp || !dl || !db) {
+            if (s->plan_only) { free(dp); free(dl); free(db); }
+            else { grom_pinned_free(dp); grom_pinned_free(dl); grom_pinned_free(db); }
+            return -1;
+        }
         for (int64_t d = 0; d < ndr; d++) {
             const drop_rec *q = &c->drops[sd + d];
             dp[d] = q->pos;
@@ -1535,7 +1544,9 @@ static int finalize_ready(pd_session *s) {
     int rc = 0;
     for (;;) {
         pthread_mutex_lock(&s->mu);
-        while (s->next_final < s->n_plan && s->final_applied && !s->ch[s->next_final].kept) s->next_final++;
+        while (s->next_final < s->n_plan && s->final_applied &&
+               (!s->ch[s->next_final].kept || !s->want[s->next_final]))
+            s->next_final++;
         const int k = s->next_final;
         const int ok = !s->abort && k < s->n_plan && s->stats_done && s->final_applied &&
                        (s->ch[k].run < 0 || s->ch[k].uploaded);
@@ -1575,13 +1586,19 @@ static void *uploader_main(void *arg) {
             /* the walk parameters may still be on their way */
             pthread_mutex_lock(&s->mu);
             while (!s->abort && s->next_final < s->n_plan && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
-            while (s->next_final < s->n_plan && s->final_applied && !s->ch[s->next_final].kept) s->next_final++;
+            while (s->next_final < s->n_plan && s->final_applied &&
+                   (!s->ch[s->next_final].kept || !s->want[s->next_final]))
+                s->next_final++;
             const int more = !s->abort && s->next_final < s->n_plan;
             pthread_mutex_unlock(&s->mu);
             if (more) { idx--; continue; } /* loop back to finalise */
             break;
         }
         pd_piece *p = &s->pieces[idx];
+        if (s->test_soft_abort >= 0 && idx == s->test_soft_abort && idx > 0) { /* test hook: a late contradiction */
+            sess_abort(s, 1, "test hook: the index plan is contradicted here (GROM_TEST_SOFT_ABORT)");
+            break;
+        }
         const double tw = now_s();
         pthread_mutex_lock(&s->mu);
         while (!s->abort && (p->state == 0 || p->state == 1)) {
@@ -1736,7 +1753,7 @@ static void apply_final(pd_session *s, int idx) {
             r->chrom = rc[i];
             r->j0 = rj[i];
             for (int q = r->first_piece; q < r->first_piece + r->n_pieces; q++)
-                if (q >= s->next_piece) s->pieces[q].full = rc[i] >= 0;
+                if (q >= s->next_piece) s->pieces[q].full = rc[i] >= 0 && s->want[rc[i]];
         }
         for (int k = 0; k < s->n_plan; k++) {
             pd_chrom *c = &s->ch[k];
@@ -1870,6 +1887,8 @@ pd_session *pd_open(const char *bam_path, const bam_hdr *hdr, const pd_chrom_in 
     s->plan = (pd_chrom_in *)calloc((size_t)(n_plan > 0 ? n_plan : 1), sizeof(pd_chrom_in));
     s->ch = (pd_chrom *)calloc((size_t)(n_plan > 0 ? n_plan : 1), sizeof(pd_chrom));
     s->keep = (int *)calloc((size_t)(n_plan > 0 ? n_plan : 1), sizeof(int));
+    s->want = (int *)calloc((size_t)(n_plan > 0 ? n_plan : 1), sizeof(int));
+    for (int k = 0; k < n_plan; k++) s->want[k] = 1;
     memcpy(s->plan, plan, sizeof(pd_chrom_in) * (size_t)n_plan);
     {
         int *rc = (int *)malloc(sizeof(int) * (size_t)(s->n_runs + 1));
@@ -1959,6 +1978,7 @@ fail:
     free(s->ch);
     free(s->plan);
     free(s->keep);
+    free(s->want);
     free(s->runs);
     free(s->pieces);
     free(s->s_ins);
@@ -1968,9 +1988,19 @@ fail:
 #undef FAIL
 }
 
+void pd_set_wanted(pd_session *s, const int *want) {
+    for (int k = 0; k < s->n_plan; k++) s->want[k] = want ? (want[k] != 0) : 1;
+    for (int i = 0; i < s->n_runs; i++) {
+        const pd_run *r = &s->runs[i];
+        for (int q = r->first_piece; q < r->first_piece + r->n_pieces; q++)
+            s->pieces[q].full = r->chrom >= 0 && s->want[r->chrom];
+    }
+}
+
 int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan_only) {
     s->min_mapq_stats = min_mapq;
     s->plan_only = plan_only;
+    s->test_soft_abort = getenv("GROM_TEST_SOFT_ABORT") ? atoi(getenv("GROM_TEST_SOFT_ABORT")) : -1;
     s->no_mirror = plan_only && getenv("GROM_DECODE_ONLY") != NULL; /* time the decode alone */
     s->n_dev = n_dev < 1 ? 1 : n_dev;
     for (int k = 0; k < s->n_plan; k++) s->ch[k].device = dev_of ? dev_of[k] : 0;
@@ -2085,6 +2115,7 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
     c->decode_thread_s = s->c_dec_s;
     c->h2d_bytes = s->c_h2d;
     c->inflate_s = s->c_inflate_s;
+    c->io_s = s->c_io_s;
     c->upload_s = s->c_upl_s;
     c->wait_s = s->c_wait_s;
     c->threads = s->n_threads;
@@ -2158,6 +2189,7 @@ void pd_close(pd_session *s) {
     free(s->ch);
     free(s->plan);
     free(s->keep);
+    free(s->want);
     free(s->runs);
     free(s->pieces);
     free(s->s_ins);

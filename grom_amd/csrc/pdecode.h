@@ -58,6 +58,11 @@ typedef struct pd_chrom_facts {
  * plan needs (the caller then reads serially). */
 pd_session *pd_open(const char *bam_path, const bam_hdr *hdr, const pd_chrom_in *plan, int n_plan, int splitread,
                     int read_name_len, int n_threads, char *why, int why_len);
+/* before pd_start: only the plan chromosomes with want[k] != 0 are decoded,
+ * staged and handed out (GROM_CHROMS: one rank's share of the genome); the
+ * others keep their place in the serial stream's plan (their records still
+ * decide Q1/Q21 for the rest) but are skipped */
+void pd_set_wanted(pd_session *s, const int *want);
 /* start the decoder threads and the uploader.  dev_of[k]: the GPU of plan
  * chromosome k.  plan_only: no device; chromosomes go to host mirrors. */
 int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan_only);
@@ -86,7 +91,7 @@ int pd_mirror_view(pd_session *s, int k, grom_reads *out);
  * decoders (summed over threads) and in the uploader's fix-up/append loop */
 typedef struct pd_counters {
     int64_t records, pieces, inflated_bytes, compressed_bytes, h2d_bytes;
-    double decode_thread_s, inflate_s, upload_s, wait_s;
+    double decode_thread_s, inflate_s, upload_s, wait_s, io_s;
     int threads, libdeflate;
 } pd_counters;
 void pd_get_counters(pd_session *s, pd_counters *c);

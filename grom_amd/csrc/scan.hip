@@ -308,8 +308,11 @@ static int check_params(const grom_params &p) {
         set_err("insert-size parameters not set (grom_params_set_insert)");
         return GROM_E_ARG;
     }
-    if (p.ploidy < 1 || p.ploidy > 50) {
-        set_err("ploidy %d outside 1..50", p.ploidy);
+    // any -p >= 1, as GROM.c:22003 takes it (the reference's 100-byte GT
+    // text, GROM.c:1477, overflows above 50; the rows print the whole string).
+    // Below 1 the reference prints an unset GT (undefined), so it is refused.
+    if (p.ploidy < 1) {
+        set_err("ploidy %d below 1", p.ploidy);
         return GROM_E_ARG;
     }
     return GROM_OK;
@@ -491,9 +494,15 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         else if (P.min_snv <= 8) GROM_LAUNCH_TILE(8);
         else if (P.min_snv <= 16) GROM_LAUNCH_TILE(16);
         else GROM_LAUNCH_TILE(GROM_MAX_NAME_SLOTS);
-        {
-            const unsigned mg = (unsigned)std::min<int64_t>(n_tiles, GROM_MEM_SLOT_BLOCKS);
+        // (no tile can hold more than pack_max reads when the chromosome has
+        // no more: then the heavy-tile pass is not launched at all)
+        if (mem_all || pack_max < 0 || n > pack_max) {
+            // the grid walks the tiles with a stride, so any grid size is
+            // correct: cap its name-slot scratch ([-n][256] words per
+            // workgroup) at GROM_MEM_SLOT_BUDGET bytes
             const size_t ns = (size_t)std::max(P.min_snv, 1);
+            const int64_t by_mem = std::max<int64_t>(1, (int64_t)(GROM_MEM_SLOT_BUDGET / (sizeof(uint32_t) * ns * GROM_TILE)));
+            const unsigned mg = (unsigned)std::max<int64_t>(1, std::min<int64_t>({n_tiles, (int64_t)GROM_MEM_SLOT_BLOCKS, by_mem}));
             if ((rc = ensure(C.slots, sizeof(uint32_t) * (size_t)mg * ns * GROM_TILE))) return rc;
             hipLaunchKernelGGL(k_scan_tile_mem, dim3(mg), dim3(GROM_TILE), 0, st, a, ch->ref, ra,
                                (const ReadMeta *)C.meta.p, (const int32_t *)C.tlo.p, (const int32_t *)C.thi.p, po,
@@ -665,7 +674,26 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
                 // the CNV path runs on the GPU
                 svt = std::thread([&P, ch, href, &cs, hits, nh, &sv_text, &ctx_text] {
                     SvRowsInput ri{&P, ch->name, href, ch->len, &CafSum::call, &cs};
-                    sv_rows(ri, hits, nh, sv_text, ctx_text);
+                    static const char *rec_prefix = getenv("GROM_SV_HITS_DUMP");  // test hook (sv.h)
+                    if (!rec_prefix) {
+                        sv_rows(ri, hits, nh, sv_text, ctx_text);
+                        return;
+                    }
+                    struct Rec {
+                        CafSum *cs;
+                        std::vector<SvCafRec> q;
+                        static double call(void *u, int64_t lo, int64_t hi) {
+                            Rec &r = *(Rec *)u;
+                            const double v = CafSum::call(r.cs, lo, hi);
+                            r.q.push_back({lo, hi, v});
+                            return v;
+                        }
+                    } rec{&cs, {}};
+                    SvRowsInput rr{&P, ch->name, href, ch->len, &Rec::call, &rec};
+                    sv_rows(rr, hits, nh, sv_text, ctx_text);
+                    std::string path = std::string(rec_prefix) + "." + ch->name + ".svh";
+                    if (sv_rows_record_write(path.c_str(), rr, hits, nh, rec.q, sv_text, ctx_text))
+                        fprintf(stderr, "grom: writing %s failed\n", path.c_str());
                 });
             }
         }

@@ -15,6 +15,7 @@
  * the gather kernel is also built with GROM_FEW_NAME_SLOTS for -n up to that */
 #define GROM_MAX_NAME_SLOTS 32 /* register builds for 4, 8, 16 and 32 slots */
 #define GROM_MEM_SLOT_BLOCKS 2048 /* -n above 32: workgroups of the global-slot kernel */
+#define GROM_MEM_SLOT_BUDGET ((size_t)256 << 20) /* at most this much name-slot scratch (bytes) */
 #define GROM_FEW_NAME_SLOTS 4
 
 /* order of the GROM_NCOUNT int32 per-base counters exported by

@@ -119,3 +119,21 @@ struct SvRowsInput {
     void *u;
 };
 void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::string &vcf, std::string &ctx);
+
+// Test hook (GROM_SV_HITS_DUMP=<prefix>): one chromosome's sv_rows inputs and
+// outputs as recorded by a GPU scan -- parameters, reference, hits, every
+// caf_sum query with its answer, the VCF and CTX text -- in <prefix>.<chr>.svh.
+// sv_rows_record_write writes it; grom_sv_rows_replay (C ABI below) runs
+// sv_rows on it again (host only: the sanitizer tests) and compares.
+struct SvCafRec {
+    int64_t lo, hi;
+    double v;
+};
+int sv_rows_record_write(const char *path, const SvRowsInput &in, const SvHit *hits, size_t n_hits,
+                         const std::vector<SvCafRec> &caf, const std::string &vcf, const std::string &ctx);
+extern "C" {
+// 0: sv_rows on the recorded inputs gives the recorded rows; 1: they differ;
+// negative: unreadable record or a caf_sum query that was not recorded
+int grom_sv_rows_replay(const char *path);
+}
+

@@ -691,3 +691,71 @@ void sv_rows(const SvRowsInput &in, const SvHit *hits, size_t n_hits, std::strin
                 n_hits, (long long)L.n_ii, (long long)L.n_id, (long long)L.n_ins, (long long)L.n_pr[0],
                 (long long)L.n_pr[1], (long long)L.n_pr[2], (long long)L.n_pr[3], l2[PR_DEL].size());
 }
+
+// ---------------- test hook: recorded sv_rows inputs (sv.h) ----------------
+namespace {
+constexpr char SVH_MAGIC[8] = {'G', 'S', 'V', 'H', '1', 0, 0, 0};
+
+struct Replay {
+    const std::vector<SvCafRec> *caf;
+    bool missing = false;
+    static double call(void *u, int64_t lo, int64_t hi) {
+        Replay &r = *(Replay *)u;
+        for (const SvCafRec &c : *r.caf)
+            if (c.lo == lo && c.hi == hi) return c.v;
+        r.missing = true;
+        return 0.0;
+    }
+};
+
+bool put(FILE *f, const void *p, size_t n) { return n == 0 || fwrite(p, 1, n, f) == n; }
+bool get(FILE *f, void *p, size_t n) { return n == 0 || fread(p, 1, n, f) == n; }
+bool put_blob(FILE *f, const void *p, uint64_t n) { return put(f, &n, 8) && put(f, p, n); }
+bool get_blob(FILE *f, std::string &out) {
+    uint64_t n;
+    if (!get(f, &n, 8) || n > ((uint64_t)1 << 34)) return false;
+    out.resize((size_t)n);
+    return get(f, out.empty() ? nullptr : &out[0], (size_t)n);
+}
+}  // namespace
+
+int sv_rows_record_write(const char *path, const SvRowsInput &in, const SvHit *hits, size_t n_hits,
+                         const std::vector<SvCafRec> &caf, const std::string &vcf, const std::string &ctx) {
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    const char *nm = in.chr_name ? in.chr_name : "";
+    const uint64_t sz[2] = {sizeof(grom_params), sizeof(SvHit)};
+    bool ok = put(f, SVH_MAGIC, 8) && put(f, sz, 16) && put(f, in.P, sizeof(grom_params)) && put(f, &in.len, 8) &&
+              put_blob(f, nm, strlen(nm)) && put_blob(f, in.ref, (uint64_t)in.len) &&
+              put_blob(f, hits, sizeof(SvHit) * n_hits) && put_blob(f, caf.data(), sizeof(SvCafRec) * caf.size()) &&
+              put_blob(f, vcf.data(), vcf.size()) && put_blob(f, ctx.data(), ctx.size());
+    ok = (fclose(f) == 0) && ok;
+    return ok ? 0 : -1;
+}
+
+extern "C" int grom_sv_rows_replay(const char *path) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return -1;
+    char magic[8];
+    uint64_t sz[2];
+    grom_params P;
+    int64_t len = 0;
+    std::string name, ref, hits, caf, vcf, ctx;
+    const bool ok = get(f, magic, 8) && memcmp(magic, SVH_MAGIC, 8) == 0 && get(f, sz, 16) &&
+                    sz[0] == sizeof(grom_params) && sz[1] == sizeof(SvHit) && get(f, &P, sizeof(P)) &&
+                    get(f, &len, 8) && get_blob(f, name) && get_blob(f, ref) && get_blob(f, hits) &&
+                    get_blob(f, caf) && get_blob(f, vcf) && get_blob(f, ctx);
+    fclose(f);
+    if (!ok || (int64_t)ref.size() != len || hits.size() % sizeof(SvHit) || caf.size() % sizeof(SvCafRec)) return -2;
+    std::vector<SvHit> H(hits.size() / sizeof(SvHit));
+    if (!H.empty()) memcpy(H.data(), hits.data(), hits.size());
+    std::vector<SvCafRec> C(caf.size() / sizeof(SvCafRec));
+    if (!C.empty()) memcpy(C.data(), caf.data(), caf.size());
+    Replay rp{&C};
+    SvRowsInput in{&P, name.c_str(), ref.data(), len, &Replay::call, &rp};
+    std::string v, c;
+    sv_rows(in, H.data(), H.size(), v, c);
+    if (rp.missing) return -3;
+    return (v == vcf && c == ctx) ? 0 : 1;
+}
+

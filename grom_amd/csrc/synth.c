@@ -841,12 +841,13 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
         int ndup = (xunif(&r) < c->dup_frac) ? 2 : 1;
         frag_id++;
         /* flush everything that now sorts before this fragment */
-        while (heap.n > 0 && heap.a[0].pos < start) {
+        while (heap.n > 0 && heap.a[0].pos < start && !(c->max_emit > 0 && emitted >= c->max_emit)) {
             hent e = hpop(&heap);
             emit(ctx, &e.rec);
             free(e.rec.data);
             emitted++;
         }
+        if (c->max_emit > 0 && emitted >= c->max_emit) break;
         for (int dup = 0; dup < ndup; dup++) {
             int cl1 = 0, cr2 = 0;
             if (xunif(&r) < c->softclip_frac) cl1 = 5 + (int)xint(&r, 26);
@@ -886,9 +887,11 @@ long synth_reads(const synth_cfg *c, int ci, const char *ref, synth_emit_fn emit
     }
     while (heap.n > 0) {
         hent e = hpop(&heap);
-        emit(ctx, &e.rec);
+        if (!(c->max_emit > 0 && emitted >= c->max_emit)) {
+            emit(ctx, &e.rec);
+            emitted++;
+        }
         free(e.rec.data);
-        emitted++;
     }
     free(heap.a);
     free(creg);
@@ -952,9 +955,17 @@ static void q_push(swriter *w, sblock *b) {
     pthread_mutex_unlock(&w->mu);
 }
 
+/* BGZF compression level: 6 (zlib's and samtools' default) unless
+ * GROM_SYNTH_LEVEL says otherwise (the bench's large BAMs) */
+static int synth_level(void) {
+    const char *e = getenv("GROM_SYNTH_LEVEL");
+    const int l = e ? atoi(e) : 6;
+    return l < 1 ? 1 : (l > 9 ? 9 : l);
+}
+
 static int compress_one(sblock *b) {
     unsigned char out[65536 + 64];
-    const int n = bgzf_block_compress(b->raw, b->len, out, 6);
+    const int n = bgzf_block_compress(b->raw, b->len, out, synth_level());
     if (n < 0) return -1;
     b->comp = (unsigned char *)malloc((size_t)n);
     if (!b->comp) return -1;
@@ -1142,7 +1153,7 @@ int synth_write_files(const synth_cfg *c, const char *fasta_path, const char *ba
     vm.base = (int64_t *)calloc((size_t)c->n_chr + 1, sizeof(int64_t));
     vm.coff = (int64_t **)calloc((size_t)c->n_chr, sizeof(int64_t *));
     bgzf_writer bw;
-    if (rc == 0 && bgzf_open_write(&bw, bam_path, 6) != 0) rc = -1;
+    if (rc == 0 && bgzf_open_write(&bw, bam_path, synth_level()) != 0) rc = -1;
     if (rc == 0) {
         rc = bam_write_header(&bw, &h);
         if (rc == 0 && bgzf_flush_block(&bw) != 0) rc = -1;

@@ -65,6 +65,8 @@ typedef struct synth_cfg {
                              variants sit on a random non-empty subset, so
                              allele fractions are k/ploidy */
     uint64_t seed;
+    long max_emit;        /* > 0: synth_reads stops after this many records
+                             (the first records of a chromosome, cheaply) */
 } synth_cfg;
 
 void synth_default_cfg(synth_cfg *c);

@@ -157,3 +157,35 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def merge_rank_outputs(vcf_paths: Sequence[str], raw_ctx_paths: Sequence[str], chrom_order: Sequence[str],
+                       target_names: Sequence[str], insert_max: int, lseq: int):
+    """Join several ranks' drop-in CLI runs over disjoint chromosome shares
+    (GROM_CHROMS, each with GROM_CTX_RAW) into one run's output: the VCF
+    header of the first file, every chromosome's rows in `chrom_order` (the
+    order a one-process run writes them: GROM's loop over the BAM targets),
+    and the translocation post-pass (grom_ctx_postpass, GROM.c:22400-22770)
+    over all ranks' raw CTX rows in the same order.  Rows are grouped by their
+    chromosome column (VCF column 1, raw CTX column 2).  Returns
+    (vcf_text, bnd_rows)."""
+    from . import ctx_postpass
+    header, rows, raw = [], {}, {}
+    for k, path in enumerate(vcf_paths):
+        with open(path) as f:
+            for line in f:
+                if line.startswith("#"):
+                    if k == 0:
+                        header.append(line)
+                    continue
+                rows.setdefault(line.split("\t", 1)[0], []).append(line)
+    for path in raw_ctx_paths:
+        with open(path) as f:
+            for line in f:
+                raw.setdefault(line.split("\t", 2)[1], []).append(line)
+    unknown = (set(rows) | set(raw)) - set(chrom_order)
+    if unknown:
+        raise ValueError(f"rows of chromosomes outside the plan: {sorted(unknown)[:5]}")
+    vcf = "".join(header) + "".join("".join(rows.get(c, [])) for c in chrom_order)
+    bnd = ctx_postpass("".join("".join(raw.get(c, [])) for c in chrom_order), list(target_names), insert_max, lseq)
+    return vcf, bnd

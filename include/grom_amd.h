@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GROM_AMD_ABI_VERSION 6
+#define GROM_AMD_ABI_VERSION 7
 #define GROM_MAX_TRIALS 1000 /* max_trials, GROM.c:631 */
 
 enum {
@@ -446,6 +446,18 @@ typedef struct grom_synth_spec {
     uint64_t seed;
 } grom_synth_spec;
 grom_batch_handle *grom_synth_chrom(const grom_synth_spec *spec, grom_params *params);
+/* ABI 7: chromosome `chrom` as its scan sees it inside the whole genome's BAM
+ * (grom_synth's file, every chromosome processed in order, as the CLI's
+ * serial-stream plan gives it): the previous chromosome's loop consumed its
+ * first two records (GROM.c:5740, 14960-14976), and lseq_tail is
+ * the next chromosome's first record's length (GROM.c:12047).  The insert
+ * statistics must already be set in *params.  bench.py scans these resident
+ * and compares the rows with the CLI's whole run over the BAM. */
+grom_batch_handle *grom_synth_chrom_stream(const grom_synth_spec *spec, grom_params *params);
+/* ABI 7: the digest the CLI's plan-only mode prints for a chromosome's input
+ * (every array, CIGAR/base/quality/SA-XP contents, dropped records, which
+ * overlapping reads share a name id); host arrays.  Test helper. */
+uint64_t grom_reads_digest(const grom_reads *reads);
 /* views into the handle (valid until grom_batch_release) */
 int grom_batch_get(grom_batch_handle *h, grom_chrom *chrom, grom_reads *reads);
 void grom_batch_release(grom_batch_handle *h);

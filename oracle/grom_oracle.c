@@ -501,7 +501,10 @@ static void snv_flush(snv_list *l, const char *fasta, long chr_len, const int32_
     }
     double ave_rd = (double)*rc_total / (double)*base_total;
     *last_group_pos = range_end;
-    char gt[128];
+    /* GROM.c:1477 keeps the GT text in 100 bytes: -p above 50 writes past
+     * it (undefined); both sides print the whole 2*p-1 character string */
+    char *gt = (char *)malloc(2 * (size_t)(g_ploidy > 0 ? g_ploidy : 1) + 2);
+    gt[0] = 0;
     for (int a = 0; a < l->n; a++) {
         if (!(l->rc_all[a] <= round(g_snv_rd_min_factor * ave_rd) || l->ratio[a] >= g_high_cov_min_snv_ratio)) continue;
         int b = l->base[a];
@@ -544,6 +547,7 @@ static void snv_flush(snv_list *l, const char *fasta, long chr_len, const int32_
             fprintf(vcf, "\t%e\t%e\n", l->binom[a], l->hez[a]);
         }
     }
+    free(gt);
     l->n = 0;
 }
 

@@ -63,6 +63,11 @@ CASES = {
     # come from chromosome-wide prefixes (k_cnv_gc_global)
     "huge_insert": ["-L", "2500000", "-s", "23", "-m", "20000", "-d", "1500", "-V", "0.000003", "-W", "60000,300000",
                     "-Q", "0.05"],
+    # amplicon depth: tiles of 256 positions holding about 60-72k reads, on both
+    # sides of the register builds' 16-bit counter bound (PACK_MAX_READS,
+    # 65,535: heavier tiles go to k_scan_tile_mem); contig ends ramp the depth
+    # down through the bound
+    "amplicon": ["-L", "30000,20000", "-c", "24500,23000", "-s", "51"],
     "wide_insert": ["-L", "1500000", "-s", "19", "-m", "2200", "-d", "200", "-V", "0.000004", "-W", "20000,150000",
                     "-Q", "0.05", "-X", "5"],
 }

@@ -57,6 +57,11 @@ RUNS = [
     ("sv", ["-f"]),
     ("c3_genome", ["-M", "-V", "1", "-f"]),
     ("one_chr", ["-G", "40", "-f"]),
+    # any -p >= 1 (GROM.c:22003; the reference's 100-byte GT text overflows
+    # above 50, both sides print the whole 119-character genotype)
+    ("one_chr", ["-p", "60"]),
+    # a negative -q: every read is high quality on every path (signed compares)
+    ("lowmapq_clip", ["-q", "-1"]),
 ]
 
 # read-depth CNV path (detect_del_dup, GROM.c:18228): -V 1 keeps every call
@@ -76,6 +81,7 @@ CNV_RUNS = [
     # window straddles up to six sampling passes of its block (GROM.c:18967-19018)
     ("cnv_multi", ["-V", "1", "-X", "2500000", "-A", "20", "-W", "100"]),
     ("cnv", ["-V", "1", "-X", "40000", "-A", "9"]),
+    ("cnv", ["-V", "1", "-p", "60"]),
 ]
 
 
@@ -342,6 +348,118 @@ def test_serial_reader_path(datadir, case, extra):
         assert open(datadir / f"o_{tag}{ext}").read() == open(datadir / f"g_{tag}{ext}").read(), ext
 
 
+def test_amplicon_depth_tiles(datadir):
+    """Tiles on both sides of the 16-bit packed-counter bound: the register
+    build takes the tiles of at most PACK_MAX_READS reads, k_scan_tile_mem
+    the heavier ones (with 32-bit counters), and every per-base counter, caf
+    value and VCF byte is the oracle's."""
+    bam, fa = synth(datadir, "amplicon", CASES["amplicon"])
+    hits = _tile_read_counts(bam)
+    pack_max = 65535  # PACK_MAX_READS, grom_amd/csrc/scan_common.h
+    assert (hits <= pack_max).any() and (hits > pack_max).any(), (hits.min(), hits.max())
+    _check_counters(datadir, "amplicon", [], "amplicon")
+
+
+def _tile_read_counts(bam, halo=151, tile=256):
+    """Reads whose start lies in [t0 - halo, t0 + tile) for every 256-base
+    tile (k_tile_ranges' read range; 2x150 bp reads without clips), from the
+    BAM's records (BGZF members are gzip members)."""
+    import gzip
+    import struct
+    raw = gzip.decompress(open(bam, "rb").read())
+    o = 4
+    (l_text,) = struct.unpack_from("<i", raw, o)
+    o += 4 + l_text
+    (n_ref,) = struct.unpack_from("<i", raw, o)
+    o += 4
+    for _ in range(n_ref):
+        (l_name,) = struct.unpack_from("<i", raw, o)
+        o += 8 + l_name
+    keys = []
+    while o + 12 <= len(raw):
+        bs, tid, pos = struct.unpack_from("<iii", raw, o)
+        keys.append(tid * (1 << 32) + pos)
+        o += 4 + bs
+    k = np.array(keys, dtype=np.int64)
+    out = []
+    for tid in np.unique(k >> 32):
+        p = np.sort(k[(k >> 32) == tid] & 0xffffffff)
+        t0 = np.arange(0, int(p[-1]) + 1, tile)
+        out.append(np.searchsorted(p, t0 + tile) - np.searchsorted(p, t0 - halo))
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("case,extra", [("sv", ["-d", "2", "-k", "8", "-v", "0.01", "-j", "0.02"]),
+                                        ("c3_genome", ["-M", "-V", "1", "-N", "5000"]),
+                                        ("cnv_multi", ["-V", "1", "-p", "3", "-q", "10", "-S"])],
+                         ids=["sv_opts", "c3_genome", "cnv_multi"])
+def test_integration_stub(datadir, case, extra):
+    """INTEGRATION.md section 2's GROM.c binding, compiled as written
+    (tools/gromc_binding.c), scanning every chromosome through grom_scan_chrom
+    with the globals it copies: the same VCF rows and BND rows as the CLI."""
+    import subprocess
+    from _util import FILEDATE, GROM_BIN, SEED
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"stub_{case}"
+    env = dict(os.environ, GROM_FILEDATE=FILEDATE, GROM_SEED=SEED)
+    exe = os.path.join(os.path.dirname(GROM_BIN), "gromc_binding")
+    r = subprocess.run([exe, "-i", bam, "-r", fa, "-o", f"b_{tag}.vcf"] + extra, cwd=str(datadir), env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    run_grom(datadir, bam, fa, f"g_{tag}.vcf", extra)
+
+    def rows(path):
+        return [ln for ln in open(path) if not ln.startswith("#")]
+    g = rows(datadir / f"g_{tag}.vcf")
+    assert len(g) > 40 and rows(datadir / f"b_{tag}.vcf") == g
+    assert rows(datadir / f"b_{tag}.vcf.ctx.vcf") == rows(datadir / f"g_{tag}.ctx.vcf")
+
+
+def test_rank_shares_merge_to_one_run(datadir):
+    """bench.py --gpus N's whole run: each rank's CLI scans its share of the
+    chromosomes (GROM_CHROMS, raw CTX rows kept with GROM_CTX_RAW); rank 0's
+    merge (grom_amd.shard.merge_rank_outputs: rows in chromosome order, one
+    translocation post-pass) is byte-identical to a one-process run."""
+    from grom_amd.shard import assign_chromosomes, merge_rank_outputs
+    names = ["chr1", "chr2", "chrX", "chrY"]
+    lengths = [700_000, 600_000, 500_000, 400_000]
+    bam, fa = synth(datadir, "shares", ["-L", ",".join(map(str, lengths)), "-n", ",".join(names), "-s", "6", "-X", "6",
+                                        "-D", "0.05", "-V", "2e-6", "-W", "20000,80000"])
+    flags = ["-M", "-g", "1"]
+    run_grom(datadir, bam, fa, "one.vcf", flags)
+    shares = assign_chromosomes(lengths, 3)
+    for r, share in enumerate(shares):
+        run_grom(datadir, bam, fa, f"r{r}.vcf", flags,
+                 env_extra={"GROM_CHROMS": ",".join(names[i].lower() for i in share),
+                            "GROM_CTX_RAW": str(datadir / f"r{r}.raw")})
+    m = open(bam + ".mean").read().split()
+    vcf, bnd = merge_rank_outputs([str(datadir / f"r{r}.vcf") for r in range(3)],
+                                  [str(datadir / f"r{r}.raw") for r in range(3)], [n.lower() for n in names], names,
+                                  int(m[3]), int(m[1]))
+    one = open(datadir / "one.vcf").read()
+    assert one.count("\n") > 100 and vcf == one
+    one_ctx = "".join(l for l in open(datadir / "one.ctx.vcf") if not l.startswith("#"))
+    assert bnd == one_ctx and bnd.count("SVTYPE=BND") >= 2
+
+
+def test_late_fallback_to_serial_reader(datadir, capfd):
+    """The streamed decoder's plan contradicted partway through the file
+    (GROM_TEST_SOFT_ABORT: at a later piece, after chromosomes were handed to
+    the scans): the CLI reruns through the serial reader, the outputs are the
+    oracle's, and stdout carries the insert-size lines once."""
+    bam, fa = synth(datadir, "three_chr", CASES["three_chr"])
+    run_oracle(datadir, bam, fa, "o_late.vcf")
+    capfd.readouterr()
+    run_grom(datadir, bam, fa, "g_late.vcf", env_extra={"GROM_PIECE_RECS": "2000", "GROM_TEST_SOFT_ABORT": "20",
+                                                         "GROM_VERBOSE": "1"})
+    out = capfd.readouterr().out
+    assert "reading the BAM serially" in out, out[-2000:]
+    assert out.count("insert_min_size, insert_max_size") == 1, out[-2000:]
+    assert out.count("median read length") == 1
+    for ext in (".vcf", ".ctx.vcf"):
+        assert open(datadir / f"o_late{ext}").read() == open(datadir / f"g_late{ext}").read(), ext
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case,extra", [("cnv", ["-N", "1000"]), ("cnv_multi", ["-V", "1", "-N", "777"]),
                                         ("three_chr", ["-N", "5000"])])
@@ -510,3 +628,45 @@ def test_two_ranks_sharded_genome_matches_one_rank():
     assert vcf.count("\n") > 100 and "chrx" in vcf
     # the translocation rows of the whole genome, paired across the ranks' chromosomes
     assert bnd.count("SVTYPE=BND") >= 2, bnd
+
+
+def test_device_inflate_matches_zlib(datadir, tmp_path):
+    """The GPU BGZF inflater (ddecode.hip, one block per lane) against zlib
+    on every block: synthetic BAMs compressed by libdeflate (levels 1, 6, 9)
+    and by zlib, and BGZF files of stored, fixed-Huffman, Huffman-only,
+    run-length and overlapping-match blocks (the CPU test's chunks)."""
+    import ctypes
+    import zlib
+    from test_host import _bgzf_blocks
+    lib = grom_amd.lib()
+    f = lib.grom_inflate_device_selftest
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    paths = []
+    for lv, nolib in (("1", False), ("6", False), ("9", False), ("6", True)):
+        env = dict(os.environ, GROM_SYNTH_LEVEL=lv)
+        if nolib:
+            env["GROM_NO_LIBDEFLATE"] = "1"
+        prefix = str(tmp_path / f"inf{lv}{int(nolib)}")
+        import subprocess
+        from _util import SYNTH_BIN
+        r = subprocess.run([SYNTH_BIN, "-o", prefix, "-L", "1500000", "-s", "9", "-X", "20", "-D", "0.1"], env=env,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        paths.append(prefix + ".bam")
+    import random
+    rng = random.Random(5)
+    chunks = [b"", b"A", bytes(rng.getrandbits(8) for _ in range(65280))]
+    for period in (1, 2, 3, 5, 8, 9, 31, 300):
+        unit = bytes(rng.getrandbits(8) for _ in range(period))
+        chunks.append((unit * (60000 // period + 1))[:60000])
+    for level, strategy in ((0, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_FIXED), (6, zlib.Z_HUFFMAN_ONLY),
+                            (6, zlib.Z_RLE), (9, zlib.Z_DEFAULT_STRATEGY)):
+        p = tmp_path / f"chunks{level}_{strategy}.bgzf"
+        p.write_bytes(_bgzf_blocks(chunks, level, strategy) * 3)
+        paths.append(str(p))
+    for path in paths:
+        ms, nb, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        bad = f(path.encode(), 0, 0, 1, ctypes.byref(ms), ctypes.byref(nb), ctypes.byref(by))
+        assert bad == 0 and nb.value > 10, (path, bad, nb.value)

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 15
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.grom_abi_version() == 6
+    assert lib.grom_abi_version() == 7
     # the ctypes mirror has the C layout of every ABI struct
     for i, st in enumerate((grom_amd.Params, grom_amd.Chrom, grom_amd.Reads, grom_amd.Out, grom_amd.Stats,
                               grom_amd.IndelRec, grom_amd.Aux, grom_amd.SvRec)):
@@ -114,6 +114,30 @@ def test_streamed_decode_matches_serial_reader(datadir, case, extra):
         assert got == want, (thr, got, want)
 
 
+@pytest.mark.parametrize("case,subsets", [("three_chr", ["chr2", "chr1,chr3"]), ("empty_middle", ["chr3", "chr1"]),
+                                          ("sv", ["chr2"])])
+def test_chromosome_subset_keeps_serial_facts(datadir, case, subsets):
+    """GROM_CHROMS (one rank's share in bench.py --gpus N): the chosen
+    chromosomes get exactly the input a whole run gives them (Q1/Q21 follow the
+    full plan), through the streamed decoder and the serial reader; the
+    others are not decoded."""
+    bam, fa = synth(datadir, case, CASES[case])
+    base = ["-i", bam, "-r", fa, "-o", f"sub_{case}.vcf"]
+    full = {l.split()[1]: l for l in run(GROM_BIN, base, str(datadir), {"GROM_PLAN_ONLY": "1"}).stdout.splitlines()
+            if l.startswith("plan ")}
+    assert full
+    for sub in subsets:
+        names = sub.split(",")
+        for extra in ({"GROM_PIECE_RECS": "1500"}, {"GROM_SERIAL_DECODE": "1"}):
+            r = run(GROM_BIN, base, str(datadir), dict(extra, GROM_PLAN_ONLY="1", GROM_CHROMS=sub))
+            got = {l.split()[1]: l for l in r.stdout.splitlines() if l.startswith("plan ")}
+            if "GROM_SERIAL_DECODE" not in extra:
+                assert sorted(got) == sorted(n for n in names if n in full), (sub, got)
+            for n, line in got.items():
+                if n in names:
+                    assert line == full[n], (sub, extra, line, full[n])
+
+
 def test_q21_empty_chromosome_starves_later_ones(datadir):
     bam, fa = synth(datadir, "empty_middle", CASES["empty_middle"])
     r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "q21.vcf"], str(datadir), {"GROM_PLAN_ONLY": "1"})
@@ -184,3 +208,116 @@ def test_fasta_info_cache_written_and_trusted(datadir, tmp_path):
     open(fa + ".info", "w").write("3 1\n0 x\n")
     run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "c.vcf"], str(tmp_path), {"GROM_PLAN_ONLY": "1"})
     assert open(fa + ".info").read().splitlines()[1:] == want.splitlines()[1:]
+
+
+def test_integration_stub_is_the_compiled_text():
+    """INTEGRATION.md section 2 shows exactly the stub that
+    tools/gromc_binding.c compiles (between its BEGIN/END markers), and the
+    built program links against the library and starts (usage exit)."""
+    import re
+    import subprocess
+    src = open(os.path.join(REPO, "tools", "gromc_binding.c")).read()
+    a = src.index("/* ---- BEGIN INTEGRATION.md §2 stub ---- */\n")
+    a = src.index("\n", a) + 1
+    b = src.index("/* ---- END INTEGRATION.md §2 stub ---- */")
+    md = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```c\n(.*?)```", md, flags=re.S)
+    assert src[a:b] in blocks
+    stub = src[a:b]
+    # every option-set global of the scan reaches grom_params (GROM.c:21908-22103)
+    for g in ("g_min_disc", "g_max_split_loss", "g_min_sr_len", "g_max_homopolymer", "g_max_ins_range",
+              "g_pval_threshold", "g_pval_insertion", "g_min_sv_ratio", "g_min_indel_ratio", "g_max_evidence_ratio",
+              "g_1000gen_window", "g_sv_list2_len", "lseq_tail"):
+        assert g in stub, g
+    exe = os.path.join(REPO, "grom_amd", "bin", "gromc_binding")
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_synth_stream_batches_match_the_cli_plan(datadir):
+    """grom_synth_chrom_stream (what bench.py keeps resident) gives each
+    chromosome exactly the input the CLI's streamed decoder stages from the
+    genome's BAM (-g 1: every contig processed): same stream facts and digest,
+    so the resident pass and the whole CLI run can be compared row for row."""
+    import ctypes
+    import grom_amd
+    lengths, names = [700_000, 500_000, 400_000, 300_000], ["chr1", "chr2", "chrX", "chrY"]
+    args = ["-L", ",".join(map(str, lengths)), "-n", ",".join(names), "-s", "3", "-X", "5", "-D", "0.05",
+            "-V", "2e-06", "-W", "20000,80000"]
+    bam, fa = synth(datadir, "gstream", args)
+    r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "gs.vcf", "-M", "-g", "1"], str(datadir), {"GROM_PLAN_ONLY": "1"})
+    plan = parse_plan(r.stdout)
+    assert sorted(plan) == sorted(n.lower() for n in names), plan
+    imean, lseq, imin, imax = (int(x) for x in open(bam + ".mean").read().split()[:4])
+    p = grom_amd.default_params()
+    p.rmdup = 1
+    grom_amd.lib().grom_params_set_insert(ctypes.byref(p), imean, imin, imax, lseq)
+    for i, name in enumerate(names):
+        b = grom_amd.SynthBatch.genome_chrom(lengths, i, p, names=names, sv_per_mb=5.0, dup_frac=0.05, cnv_rate=2e-6,
+                                             cnv_range=(20_000, 80_000), seed=3, stream=True)
+        try:
+            got = {"reads": b.reads.n, "n_skip": b.chrom.n_skip, "p_last": b.chrom.p_last,
+                   "lseq_tail": b.chrom.lseq_tail,
+                   "digest": grom_amd.lib().grom_reads_digest(ctypes.byref(b.reads))}
+        finally:
+            b.close()
+        want = plan[name.lower()]
+        assert got == {k: want[k] for k in got}, (name, got, want)
+
+
+def _bgzf_blocks(chunks, level, strategy):
+    """BGZF blocks (gzip members with the BC extra field) of each chunk, raw
+    DEFLATE at the given zlib level/strategy."""
+    import struct
+    import zlib
+    out = bytearray()
+    for data in chunks:
+        c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, strategy)
+        body = c.compress(data) + c.flush()
+        bsize = 18 + len(body) + 8 - 1
+        out += bytes([0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, ord("B"), ord("C"), 2, 0]) + struct.pack("<H", bsize)
+        out += body + struct.pack("<II", zlib.crc32(data) & 0xffffffff, len(data))
+    return bytes(out)
+
+
+def test_inflate_twin_matches_zlib(tmp_path):
+    """The device BGZF inflater's decoder (inflate.h), compiled for the host,
+    against zlib on every kind of DEFLATE block: stored (level 0 and
+    incompressible data), fixed Huffman, dynamic Huffman at levels 1-9, the
+    Huffman-only and run-length strategies, matches overlapping their source
+    at periods 1-300 (the pattern and chunked copy paths), empty and 64 KiB
+    blocks, and corrupted streams (both must fail)."""
+    import ctypes
+    import random
+    import zlib
+    import grom_amd
+    rng = random.Random(5)
+    chunks = [b"", b"A", bytes(rng.getrandbits(8) for _ in range(65280)), b"ACGT" * 16320]
+    for period in (1, 2, 3, 5, 8, 9, 31, 300):
+        unit = bytes(rng.getrandbits(8) for _ in range(period))
+        chunks.append((unit * (60000 // period + 1))[:60000])
+    chunks.append(bytes(rng.choice(b"ACGTN") for _ in range(50000)))
+    chunks.append(b"".join(b"read%07d\t" % i + bytes(rng.choice(b"#+5?AEI") for _ in range(150)) for i in range(300)))
+    lib = grom_amd.lib()
+    f = lib.grom_inflate_selftest
+    f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                             ctypes.POINTER(ctypes.c_int64)]
+    cases = [(0, zlib.Z_DEFAULT_STRATEGY)] + [(lv, zlib.Z_DEFAULT_STRATEGY) for lv in (1, 6, 9)] + \
+            [(6, zlib.Z_FIXED), (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_RLE), (9, zlib.Z_FILTERED)]
+    for level, strategy in cases:
+        path = tmp_path / f"b{level}_{strategy}.bgzf"
+        path.write_bytes(_bgzf_blocks(chunks, level, strategy))
+        nb, by = ctypes.c_int64(), ctypes.c_int64()
+        assert f(str(path).encode(), 0, ctypes.byref(nb), ctypes.byref(by)) == 0, (level, strategy)
+        assert nb.value == len(chunks) and by.value == sum(map(len, chunks))
+    # corrupted blocks: flipped bytes inside the DEFLATE data; both decoders
+    # must agree that each block fails or succeeds (and on its bytes)
+    good = bytearray(_bgzf_blocks(chunks[2:8], 6, zlib.Z_DEFAULT_STRATEGY))
+    for k in range(40):
+        bad = bytearray(good)
+        i = 18 + rng.randrange(200)
+        bad[i] ^= 1 << rng.randrange(8)
+        path = tmp_path / f"bad{k}.bgzf"
+        path.write_bytes(bytes(bad))
+        nb, by = ctypes.c_int64(), ctypes.c_int64()
+        assert f(str(path).encode(), 1, ctypes.byref(nb), ctypes.byref(by)) == 0, k

@@ -12,10 +12,20 @@ uninstrumented and never called) and grom_synth.  The runs cover:
     reader (GROM_SERIAL_DECODE);
   - BAI region queries against a linear scan, the SNV row formatter, the
     synthetic-batch builder and the translocation post-pass.
-Not covered here: the scan worker pool and svcall.cpp's list logic, which
-run only after device scans (GPU tests).  Any sanitizer report fails the test
-(UBSan is built with -fno-sanitize-recover, ASan/TSan exit non-zero).
+  - the scan worker pool: in plan-only mode the streamed decoder hands every
+    chromosome to the pool's threads, which print its plan line;
+  - svcall.cpp's candidate lists, SV assembly and rows (sv_rows) on inputs
+    recorded from real GPU scans of the "sv" parity case (tests/golden/
+    svh_*.svh.gz, written by tools/record_sv_hits.sh with GROM_SV_HITS_DUMP:
+    parameters, reference, the per-base hits, every INV depth query with its
+    answer, and the rows the GPU run wrote), replayed on concurrent threads,
+    four rounds each, and compared with the recorded rows;
+  - the device BGZF inflater's host twin (inflate.h) on the synthetic BAM.
+Any sanitizer report fails the test (UBSan is built with
+-fno-sanitize-recover, ASan/TSan exit non-zero).
 """
+import glob
+import gzip
 import os
 import shutil
 import subprocess
@@ -61,7 +71,18 @@ def test_host_code_under_sanitizer(san, tmp_path):
                    dict(env, GROM_PLAN_ONLY="1"))
         plans.append(sorted(line for line in out.splitlines() if line.startswith("plan ")))
     assert len(plans[0]) == 3 and plans[0] == plans[1] == plans[2], plans
+    # svcall.cpp on recorded GPU-scan inputs, every record on its own thread
+    recs = []
+    for gz in sorted(glob.glob(os.path.join(REPO, "tests", "golden", "svh_*.svh.gz"))):
+        path = os.path.join(d, os.path.basename(gz)[:-3])
+        with gzip.open(gz, "rb") as fi, open(path, "wb") as fo:
+            fo.write(fi.read())
+        recs.append(path)
+    assert len(recs) >= 2
+    out = _run([driver, "svrows"] + recs, d)
+    assert out.count(": rc 0") == len(recs), out
     if san == "asan":  # single-threaded helpers: once is enough
+        assert "0 mismatches" in _run([driver, "inflate", "s.bam"], d)
         assert "0 mismatches" in _run([driver, "bai", "s.bam", "3000"], d)
         assert "0 mismatches" in _run([driver, "fmt", "20000"], d)
         assert "reads on a" in _run([driver, "synth", "200000"], d)

@@ -14,7 +14,14 @@
  *   synth <len>          one synthetic chromosome batch (synth.c, hostapi.c)
  *   ctx                  the translocation post-pass (grom_main.c) on a few
  *                        raw CTX rows
+ *   inflate <bam>        the device BGZF inflater's host twin against zlib on
+ *                        every block (inflate_host.cpp)
+ *   svrows <rec>...      svcall.cpp's candidate lists, SV assembly and rows on
+ *                        recorded GPU-scan inputs (GROM_SV_HITS_DUMP), every
+ *                        record on its own thread, four rounds, outputs
+ *                        compared with the recorded rows
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -85,9 +92,49 @@ static int cmd_ctx(void) {
     return rc < 0;
 }
 
+int grom_sv_rows_replay(const char *path); /* svcall.cpp test hook (sv.h) */
+int64_t grom_inflate_selftest(const char *bam_path, int64_t max_blocks, int64_t *n_blocks, int64_t *bytes);
+
+static int cmd_inflate(const char *bam) {
+    int64_t nb = 0, by = 0;
+    const int64_t bad = grom_inflate_selftest(bam, 0, &nb, &by);
+    printf("inflate selftest: %lld mismatches over %lld blocks (%lld bytes)\n", (long long)bad, (long long)nb,
+           (long long)by);
+    return bad != 0;
+}
+
+typedef struct {
+    const char *path;
+    int rc;
+} replay_job;
+
+static void *replay_main(void *arg) {
+    replay_job *j = (replay_job *)arg;
+    for (int r = 0; r < 4 && j->rc == 0; r++) j->rc = grom_sv_rows_replay(j->path);
+    return NULL;
+}
+
+static int cmd_svrows(int n, char **paths) {
+    replay_job *jobs = calloc((size_t)n, sizeof(replay_job));
+    pthread_t *t = calloc((size_t)n, sizeof(pthread_t));
+    for (int i = 0; i < n; i++) {
+        jobs[i].path = paths[i];
+        pthread_create(&t[i], NULL, replay_main, &jobs[i]);
+    }
+    int bad = 0;
+    for (int i = 0; i < n; i++) {
+        pthread_join(t[i], NULL);
+        printf("svrows %s: rc %d\n", paths[i], jobs[i].rc);
+        bad += jobs[i].rc != 0;
+    }
+    free(jobs);
+    free(t);
+    return bad != 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) {
-        fprintf(stderr, "usage: san_driver cli|bai|fmt|synth|ctx ...\n");
+        fprintf(stderr, "usage: san_driver cli|bai|fmt|synth|ctx|svrows|inflate ...\n");
         return 2;
     }
     if (!strcmp(argv[1], "cli")) return grom_cli_main(argc - 1, argv + 1);
@@ -95,6 +142,8 @@ int main(int argc, char **argv) {
     if (!strcmp(argv[1], "fmt") && argc >= 3) return cmd_fmt(atoll(argv[2]));
     if (!strcmp(argv[1], "synth") && argc >= 3) return cmd_synth(atoll(argv[2]));
     if (!strcmp(argv[1], "ctx")) return cmd_ctx();
+    if (!strcmp(argv[1], "svrows") && argc >= 3) return cmd_svrows(argc - 2, argv + 2);
+    if (!strcmp(argv[1], "inflate") && argc >= 3) return cmd_inflate(argv[2]);
     fprintf(stderr, "bad arguments\n");
     return 2;
 }
