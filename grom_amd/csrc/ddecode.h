@@ -7,6 +7,8 @@
 
 #include <stdint.h>
 
+#include "../../include/grom_amd.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -14,10 +16,11 @@ extern "C" {
 /* one BGZF block of a compressed range: its DEFLATE data in the range, and
  * where its ISIZE bytes go in the inflated stream */
 typedef struct DdBlock {
-    int64_t in_off;
-    int64_t out_off;
+    int64_t in_off;   /* its DEFLATE data in the range */
+    int64_t out_off;  /* its first byte in the inflated stream */
     uint32_t in_len;
-    uint32_t out_len;
+    uint32_t out_len; /* ISIZE */
+    int64_t c_off;    /* the block's own start in the range */
 } DdBlock;
 
 /* the blocks of buf[0..len) (whole BGZF blocks): returns their number (and
@@ -30,6 +33,54 @@ int64_t dd_block_table(const uint8_t *buf, int64_t len, DdBlock *out, int64_t ca
  * of two launches timed with HIP events */
 int64_t grom_inflate_device_selftest(const char *bam_path, int device, int64_t max_bytes, int check, double *ms_kernel,
                                      int64_t *n_blocks, int64_t *bytes);
+
+/* ---- one run (a chromosome's records in the file) on the device ---- */
+typedef struct dd_ctx dd_ctx;
+dd_ctx *dd_ctx_new(int device);
+void dd_ctx_free(dd_ctx *c);
+/* summed HIP-event times of the parsed runs: inflate, record walk, parse */
+void dd_ctx_times(const dd_ctx *c, double ms[3]);
+/* inflate a run's blocks (h_comp pinned, 64 readable bytes past comp_len;
+ * h_blk its block table, ubytes the inflated size) and find its records from
+ * the record starts h_starts (offsets into the inflated stream, the first
+ * being the run's first record) up to u_end: *n_rec records.  0; -2 when
+ * the data contradicts the index plan (the CLI then reads serially); -1 */
+int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
+                int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int64_t *n_rec, char *err,
+                int errlen);
+/* find_insert_mean's sample from every record of the loaded run (file order):
+ * at most cap_left (insert, l_qseq) pairs into h_ins/h_lq, the mapped-bases
+ * sum up to the pair that completes the cap (or over the run) */
+int dd_run_stats(dd_ctx *c, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq, int64_t *n_taken,
+                 int64_t *m_contrib, char *err, int errlen);
+typedef struct dd_parse_out {
+    int64_t n_rec, n_kept, n_drop, n_cig, n_bases, n_auxc;
+    int32_t last_pos, last_lq, last_hclip, last_kept;
+    /* the split-read candidates (host, valid until the next parse): record
+     * bytes (block_size first) at aux_bytes + aux_off[a], kept index aux_kidx[a] */
+    const uint8_t *aux_bytes;
+    const int64_t *aux_off, *aux_kidx;
+} dd_parse_out;
+/* the loaded run's records j0.. parsed into `stage` (grom_stage_fill_begin):
+ * every array of the chromosome, untrimmed, aux_idx all -1 */
+int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len, grom_stage *stage,
+                 dd_parse_out *out, char *err, int errlen);
+/* kept reads and dropped records at positions below s0 (the walk's skip
+ * prefix) in a staged chromosome (positions sorted) */
+int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64_t *sd);
+
+/* stage helpers for device-side fills (scan.hip) */
+/* a stage holding exactly sz's counts (n_aux = capacity, the count starts at
+ * 0), its device arrays in *dev (writable); waits for its earlier copies */
+int grom_stage_fill_begin(grom_stage *s, const grom_stage_sizes *sz, grom_reads *dev);
+/* n split-read alignments: aux[k] for kept read kidx[k] (host arrays) */
+int grom_stage_put_aux(grom_stage *s, const grom_aux *aux, const int64_t *kidx, int64_t n);
+/* drop the first sd dropped records and count kept reads after the first sk */
+int grom_stage_trim_drops(grom_stage *s, int64_t sd, int64_t sk);
+/* the stage's device arrays, untrimmed (no reference check) */
+int grom_stage_dev_reads(grom_stage *s, grom_reads *dev);
+/* n bytes from device memory of `device` (synchronous); 0 or -1 */
+int grom_copy_d2h(void *dst, const void *src, size_t n, int device);
 
 #ifdef __cplusplus
 }

@@ -72,6 +72,7 @@ extern "C" int64_t dd_block_table(const uint8_t *buf, int64_t len, DdBlock *out,
             out[n].in_len = (uint32_t)(blen - 12 - xlen - 8);
             out[n].out_off = ob;
             out[n].out_len = isize;
+            out[n].c_off = off;
         }
         n++;
         ob += isize;
@@ -181,4 +182,769 @@ done:
     (void)hipFree(d_blk);
     (void)hipFree(d_bad);
     return bad;
+}
+
+// ===========================================================================
+// Records of one run (a chromosome's records in the file) on the device.
+//
+// The run's blocks are inflated into one contiguous stream U.  Record
+// boundaries: the BAI's linear index names a record start every 16 kb of the
+// reference (the first record overlapping each window), so the run is cut at
+// those offsets into chunks, one lane walks each chunk's block_size chain
+// (counting, then writing every record's offset), and a chunk must end
+// exactly where the next one starts -- else the plan falls back to the host
+// decoder.  Then one lane per record parses the fixed fields into the
+// stage's structure-of-arrays, prefix sums place the CIGAR words, bases,
+// qualities, dropped records and split-read candidates, one wave per read
+// copies its packed bases and qualities, and read names become ids by a
+// radix sort of 64-bit name hashes with every member of an equal-hash run
+// compared byte for byte against the run's first (a collision falls back).
+// This is the work pdecode.c's decode_piece + upload_piece do on the host,
+// with the same results (tests/test_gpu_parity.py compares the digests).
+// ===========================================================================
+#include <hipcub/hipcub.hpp>
+
+#include "bamio.h"
+
+namespace {
+
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+int dgrow(DBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return 0;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    const size_t want = bytes + bytes / 8 + 256;
+    if (hipMalloc(&b.p, want) != hipSuccess) return -1;
+    b.cap = want;
+    return 0;
+}
+
+template <class T> T *P(DBuf &b) { return (T *)b.p; }
+
+// bad-state bits
+enum : uint32_t { DB_INFLATE = 1, DB_CHAIN = 2, DB_RECORD = 4, DB_TID = 8, DB_UNSORTED = 16, DB_NAMES = 32 };
+
+__device__ __forceinline__ uint32_t ldu32(const uint8_t *U, int64_t o) {
+    return (uint32_t)U[o] | (uint32_t)U[o + 1] << 8 | (uint32_t)U[o + 2] << 16 | (uint32_t)U[o + 3] << 24;
+}
+
+// the 36-byte record header at o (block_size .. tlen) as 9 words, from 10
+// aligned word loads
+struct RecHdr {
+    uint32_t w[9];
+    __device__ int32_t bs() const { return (int32_t)w[0]; }
+    __device__ int32_t tid() const { return (int32_t)w[1]; }
+    __device__ int32_t pos() const { return (int32_t)w[2]; }
+    __device__ int l_qname() const { return (int)(w[3] & 0xff); }
+    __device__ int mapq() const { return (int)((w[3] >> 8) & 0xff); }
+    __device__ int n_cigar() const { return (int)(w[4] & 0xffff); }
+    __device__ int flag() const { return (int)(w[4] >> 16); }
+    __device__ int32_t lq() const { return (int32_t)w[5]; }
+    __device__ int32_t mtid() const { return (int32_t)w[6]; }
+    __device__ int32_t mpos() const { return (int32_t)w[7]; }
+    __device__ int32_t isz() const { return (int32_t)w[8]; }
+};
+
+__device__ __forceinline__ void load_hdr(const uint8_t *U, int64_t o, RecHdr &h) {
+    const uint32_t *a = (const uint32_t *)(U + (o & ~(int64_t)3));
+    const uint32_t sh = (uint32_t)(o & 3) * 8;
+    uint32_t raw[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) raw[k] = a[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) h.w[k] = sh ? (raw[k] >> sh) | (raw[k + 1] << (32 - sh)) : raw[k];
+}
+
+__device__ __forceinline__ int32_t ld_bs(const uint8_t *U, int64_t o) {
+    const uint32_t *a = (const uint32_t *)(U + (o & ~(int64_t)3));
+    const uint32_t sh = (uint32_t)(o & 3) * 8;
+    const uint32_t w0 = a[0], w1 = a[1];
+    return (int32_t)(sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0);
+}
+
+#define DD_MAX_REC (256 << 20)
+
+// one lane per chunk: count its records (off == nullptr) or write their
+// offsets from base[c] on
+__global__ void k_walk(const uint8_t *__restrict__ U, const int64_t *__restrict__ S, int64_t n_chunks,
+                       uint32_t *__restrict__ cnt, const uint32_t *__restrict__ base, int64_t *__restrict__ off,
+                       uint32_t *__restrict__ bad) {
+    const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    int64_t o = S[c];
+    const int64_t e = S[c + 1];
+    uint32_t n = 0;
+    int64_t w = off ? (int64_t)base[c] : 0;
+    while (o < e) {
+        const int32_t bs = ld_bs(U, o);
+        if (bs < 32 || bs > DD_MAX_REC) { atomicOr(bad, DB_RECORD); return; }
+        if (off) off[w++] = o;
+        o += 4 + (int64_t)bs;
+        n++;
+    }
+    if (o != e) { atomicOr(bad, DB_CHAIN); return; }
+    if (!off) cnt[c] = n;
+}
+
+// which characters are 'Z'/'H' terminated, and the fixed sizes (bamio.c aux_type_size)
+__device__ __forceinline__ int aux_sz(uint8_t t) {
+    return (t == 'A' || t == 'c' || t == 'C') ? 1 : (t == 's' || t == 'S') ? 2 : (t == 'i' || t == 'I' || t == 'f') ? 4
+         : (t == 'd') ? 8 : -1;
+}
+
+// bam_aux_find(b, "XP") || bam_aux_find(b, "SA") with bamio.c's skip rules
+__device__ bool has_split_tag(const uint8_t *U, int64_t s, int64_t end) {
+    while (s + 3 <= end) {
+        const uint8_t t0 = U[s], t1 = U[s + 1], t = U[s + 2];
+        if ((t0 == 'X' && t1 == 'P') || (t0 == 'S' && t1 == 'A')) return true;
+        s += 3;
+        if (t == 'Z' || t == 'H') {
+            while (s < end && U[s]) s++;
+            s++;
+        } else if (t == 'B') {
+            if (s + 5 > end) return false;
+            const int sz = aux_sz(U[s]);
+            const uint32_t n = ldu32(U, s + 1);
+            if (sz < 0) return false;
+            s += 5 + (int64_t)sz * n;
+        } else {
+            const int sz = aux_sz(t);
+            if (sz < 0) return false;
+            s += sz;
+        }
+    }
+    return false;
+}
+
+// per record (file order, r >= j0 only): kept / dropped (GROM.c:6418),
+// CIGAR words and bases of the kept, split-read candidates (0 < l_aux < 100
+// and an XP/SA tag: grom_parse_aux's precondition, GROM.c:5763), positions
+__global__ void k_rec_meta(const uint8_t *__restrict__ U, const int64_t *__restrict__ off, int64_t R, int64_t j0,
+                           int32_t tid, uint32_t *__restrict__ keep, uint32_t *__restrict__ drop,
+                           uint32_t *__restrict__ auxc, uint32_t *__restrict__ ncig, int64_t *__restrict__ nb,
+                           int32_t *__restrict__ rpos, uint32_t *__restrict__ bad) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = off[r];
+        RecHdr h;
+        load_hdr(U, o, h);
+        const int32_t lq = h.lq();
+        const int lqn = h.l_qname(), nc = h.n_cigar();
+        if (lq < 0 || lqn < 1 || 32 + (int64_t)lqn + 4 * (int64_t)nc + (lq + 1) / 2 + lq > (int64_t)h.bs())
+            atomicOr(bad, DB_RECORD);
+        if (h.tid() != tid) atomicOr(bad, DB_TID);
+        rpos[r] = h.pos();
+        const bool in = r >= j0;
+        const bool dropped = (h.flag() & GF_UNMAP) || (h.flag() & GF_DUP);
+        const bool k = in && !dropped;
+        keep[r] = k;
+        drop[r] = in && dropped;
+        ncig[r] = k ? (uint32_t)nc : 0u;
+        nb[r] = k ? (((int64_t)lq + 1) & ~1LL) : 0;
+        bool cand = false;
+        if (k) {
+            const int64_t data = o + 36, end = o + 4 + h.bs();
+            const int64_t aux = data + lqn + 4 * (int64_t)nc + (lq + 1) / 2 + lq;
+            const int64_t l_aux = end - aux;
+            cand = l_aux > 0 && l_aux < 100 && has_split_tag(U, aux, end);
+        }
+        auxc[r] = cand;
+    }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+struct StageOut {
+    int32_t *pos, *mtid, *mpos, *isize, *lq, *aidx;
+    uint16_t *flag;
+    uint8_t *mapq;
+    uint32_t *coff, *cig, *nid;
+    int64_t *boff;
+    int32_t *dpos, *dlq;
+    int64_t *dbef;
+};
+
+// the kept reads' fields, CIGAR words and name hashes; the dropped records;
+// the split-read candidates' record indices; the stream's last record
+__global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__restrict__ off, int64_t R, int64_t j0,
+                            const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kidx,
+                            const uint32_t *__restrict__ drop, const uint32_t *__restrict__ didx,
+                            const uint32_t *__restrict__ auxc, const uint32_t *__restrict__ aidx,
+                            const uint32_t *__restrict__ coff_s, const int64_t *__restrict__ boff_s,
+                            const int32_t *__restrict__ rpos, StageOut so, int64_t *__restrict__ krec,
+                            uint64_t *__restrict__ keys, uint32_t *__restrict__ vals, int64_t *__restrict__ acand,
+                            int32_t read_name_len, int32_t *__restrict__ last, uint32_t *__restrict__ bad) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
+        if (r > j0 && rpos[r] < rpos[r - 1]) atomicOr(bad, DB_UNSORTED);
+        const int64_t o = off[r];
+        RecHdr h;
+        load_hdr(U, o, h);
+        int32_t hc = 0;
+        const int lqn = h.l_qname(), nc = h.n_cigar();
+        if (keep[r]) {
+            const uint32_t i = kidx[r];
+            so.pos[i] = h.pos();
+            so.flag[i] = (uint16_t)h.flag();
+            so.mapq[i] = (uint8_t)h.mapq();
+            so.mtid[i] = h.mtid();
+            so.mpos[i] = h.mpos();
+            so.isize[i] = h.isz();
+            so.lq[i] = h.lq();
+            so.coff[i] = coff_s[r];
+            so.boff[i] = boff_s[r];
+            so.aidx[i] = -1;
+            krec[i] = r;
+            const int64_t cg = o + 36 + lqn;
+            for (int c = 0; c < nc; c++) {
+                const uint32_t op = ldu32(U, cg + 4 * c);
+                so.cig[coff_s[r] + c] = op;
+                if ((op & 15u) == GC_HARD_CLIP) hc += (int32_t)(op >> 4);
+            }
+            // name: up to its NUL (pdecode.c buf_intern); empty or >= read_name_len: id 0 (GROM.c:6813)
+            uint64_t hs = 0xcbf29ce484222325ULL;
+            int L = 0;
+            while (L < lqn && U[o + 36 + L]) {
+                hs = (hs ^ U[o + 36 + L]) * 0x100000001b3ULL;
+                L++;
+            }
+            keys[i] = (L == 0 || L >= read_name_len) ? 0ull : (mix64(hs ^ (uint64_t)L * 0x9e3779b97f4a7c15ULL) | 1ull);
+            vals[i] = i;
+            if (auxc[r]) acand[aidx[r]] = r;
+        } else if (drop[r]) {
+            const uint32_t d = didx[r];
+            so.dpos[d] = h.pos();
+            so.dlq[d] = h.lq();
+            so.dbef[d] = (int64_t)kidx[r];  // kept reads before it (exclusive scan)
+        }
+        if (r == R - 1) {  // the stream's last record: position, length, hard clips, kept
+            if (!keep[r]) {
+                const int64_t cg = o + 36 + lqn;
+                for (int c = 0; c < nc; c++) {
+                    const uint32_t op = ldu32(U, cg + 4 * c);
+                    if ((op & 15u) == GC_HARD_CLIP) hc += (int32_t)(op >> 4);
+                }
+            }
+            last[0] = h.pos();
+            last[1] = h.lq();
+            last[2] = hc;
+            last[3] = keep[r] ? 1 : 0;
+        }
+    }
+}
+
+// one wave per kept read (grid-stride): its packed bases and qualities, and
+// the zero pad byte after an odd-length read's qualities
+__global__ void k_copy_bases(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
+                             const int64_t *__restrict__ krec, int64_t n, const int64_t *__restrict__ boff,
+                             uint8_t *__restrict__ seq, uint8_t *__restrict__ qual) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t i = w0; i < n; i += nw) {
+        const int64_t o = off[krec[i]];
+        const int lqn = U[o + 12], nc = (int)(U[o + 16] | (U[o + 17] << 8));
+        const int32_t lq = (int32_t)ldu32(U, o + 20);
+        const int64_t s = o + 36 + lqn + 4 * (int64_t)nc;
+        const int64_t ns = (lq + 1) / 2;
+        const int64_t b = boff[i];
+        for (int64_t k = lane; k < ns; k += 64) seq[b / 2 + k] = U[s + k];
+        for (int64_t k = lane; k < lq; k += 64) qual[b + k] = U[s + ns + k];
+        if ((lq & 1) && lane == 0) qual[b + lq] = 0;
+    }
+}
+
+// equal-hash runs: every member's name equal to the run head's; ids = head + 1
+__global__ void k_name_ids(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
+                           const int64_t *__restrict__ krec, const uint64_t *__restrict__ keys,
+                           const uint32_t *__restrict__ vals, const uint32_t *__restrict__ head, int64_t n,
+                           uint32_t *__restrict__ nid, uint32_t *__restrict__ bad) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = vals[p];
+        if (keys[p] == 0) { nid[i] = 0; continue; }
+        const uint32_t hp = head[p];
+        nid[i] = hp + 1;
+        if (hp == (uint32_t)p) continue;
+        const int64_t a = off[krec[i]] + 36, b = off[krec[vals[hp]]] + 36;
+        for (int k = 0;; k++) {
+            const uint8_t x = U[a + k], y = U[b + k];
+            if (x != y) { atomicOr(bad, DB_NAMES); break; }
+            if (!x) break;
+        }
+    }
+}
+
+__global__ void k_seg_head(const uint64_t *__restrict__ keys, int64_t n, uint32_t *__restrict__ head) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x)
+        head[p] = (p == 0 || keys[p] != keys[p - 1]) ? (uint32_t)p : 0u;
+}
+
+// find_insert_mean's per-record test (GROM.c:1226-1317), every record of the run
+__global__ void k_stats(const uint8_t *__restrict__ U, const int64_t *__restrict__ off, int64_t R, int32_t min_mapq,
+                        uint32_t *__restrict__ q, int32_t *__restrict__ v, int32_t *__restrict__ lqo,
+                        int64_t *__restrict__ m) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
+        RecHdr h;
+        load_hdr(U, off[r], h);
+        const int fl = h.flag();
+        const bool dropped = (fl & GF_UNMAP) || (fl & GF_DUP);
+        bool take = false;
+        int32_t val = 0;
+        if (!dropped) {
+            if (!(fl & GF_PAIRED)) { take = true; val = h.lq(); }
+            else if (!(fl & GF_MUNMAP) && h.tid() == h.mtid() && h.pos() < h.mpos() && (fl & GF_PROPER) && h.isz() > 0) {
+                take = true;
+                val = h.isz();
+            }
+        }
+        q[r] = take;
+        v[r] = val;
+        lqo[r] = h.lq();
+        m[r] = (!dropped && h.mapq() >= min_mapq) ? (int64_t)h.lq() : 0;
+    }
+}
+
+__global__ void k_stats_take(const uint32_t *__restrict__ q, const uint32_t *__restrict__ qi,
+                             const int32_t *__restrict__ v, const int32_t *__restrict__ lq,
+                             const int64_t *__restrict__ m_incl, int64_t R, int64_t cap, int32_t *__restrict__ ins_out,
+                             int32_t *__restrict__ lq_out, int64_t *__restrict__ m_at_cap) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
+        if (!q[r] || qi[r] >= cap) continue;
+        ins_out[qi[r]] = v[r];
+        lq_out[qi[r]] = lq[r];
+        if (qi[r] == cap - 1) *m_at_cap = m_incl[r];
+    }
+}
+
+// pack the split-read candidates' records (their full bytes) for the host parse
+__global__ void k_aux_pack(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
+                           const int64_t *__restrict__ acand, const int64_t *__restrict__ pk_off, int64_t n,
+                           uint8_t *__restrict__ out) {
+    for (int64_t a = blockIdx.x; a < n; a += gridDim.x) {
+        const int64_t o = off[acand[a]];
+        const int64_t len = pk_off[a + 1] - pk_off[a];
+        for (int64_t k = threadIdx.x; k < len; k += blockDim.x) out[pk_off[a] + k] = U[o + k];
+    }
+}
+
+__global__ void k_aux_len(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
+                          const int64_t *__restrict__ acand, int64_t n, int64_t *__restrict__ len,
+                          const uint32_t *__restrict__ kidx, int64_t *__restrict__ akidx) {
+    for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < n; a += (int64_t)gridDim.x * blockDim.x) {
+        len[a] = 4 + (int64_t)ld_bs(U, off[acand[a]]);
+        akidx[a] = kidx[acand[a]];
+    }
+}
+
+inline unsigned grid_for(int64_t n, int per = 256, unsigned cap = 65536) {
+    int64_t g = (n + per - 1) / per;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+}  // namespace
+
+// totals of the exclusive scans (last element + its input), and the CIGAR
+// offsets' closing entry
+__global__ void k_totals(const uint32_t *keep, const uint32_t *kidx, const uint32_t *drop, const uint32_t *didx,
+                         const uint32_t *auxc, const uint32_t *aidx, const uint32_t *ncig, const uint32_t *coff,
+                         const int64_t *nb, const int64_t *boff, int64_t R, int64_t *tot) {
+    if (blockIdx.x || threadIdx.x) return;
+    if (R == 0) {
+        for (int k = 0; k < 5; k++) tot[k] = 0;
+        return;
+    }
+    const int64_t r = R - 1;
+    tot[0] = (int64_t)kidx[r] + keep[r];
+    tot[1] = (int64_t)didx[r] + drop[r];
+    tot[2] = (int64_t)aidx[r] + auxc[r];
+    tot[3] = (int64_t)coff[r] + ncig[r];
+    tot[4] = boff[r] + nb[r];
+}
+
+__global__ void k_set_u32(uint32_t *p, uint32_t v) {
+    if (!blockIdx.x && !threadIdx.x) *p = v;
+}
+
+// first index with a[i] >= x in a sorted array (one lane)
+__global__ void k_lower_bound(const int32_t *a, int64_t n, int32_t x, int64_t *out) {
+    if (blockIdx.x || threadIdx.x) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    *out = lo;
+}
+
+struct dd_ctx {
+    int device = -1;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[4] = {};
+    DBuf comp, blk, U, status, misc, S, ccnt, cbase, off;
+    DBuf keep, kidx, drop, didx, auxc, aidx, ncig, coff, nb, boff, rpos, krec, keys, vals, keys2, vals2, head, tmp;
+    DBuf sq, sqi, sv, slq, sm, s_ins, s_lq, acand, alen, aoff, akidx, apack;
+    int64_t R = 0, nblk = 0, ubytes = 0;
+    int64_t *h_small = nullptr;  // pinned: totals and scalars
+    uint8_t *h_aux = nullptr;    // pinned: packed split-read candidate records
+    size_t h_aux_cap = 0;
+    float ms_inflate = 0, ms_walk = 0, ms_parse = 0;
+};
+
+#define DCK(x)                                                                                       \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) {                                                                      \
+            if (err) snprintf(err, (size_t)errlen, "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, \
+                              __LINE__);                                                             \
+            return -1;                                                                               \
+        }                                                                                            \
+    } while (0)
+#define DGROW(b, bytes)                                                                              \
+    do {                                                                                             \
+        if (dgrow((b), (bytes))) {                                                                   \
+            if (err) snprintf(err, (size_t)errlen, "device decode: hipMalloc(%zu) failed", (size_t)(bytes)); \
+            return -1;                                                                               \
+        }                                                                                            \
+    } while (0)
+
+extern "C" dd_ctx *dd_ctx_new(int device) {
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    dd_ctx *c = new dd_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return nullptr; }
+    for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
+    if (hipHostMalloc((void **)&c->h_small, 64 * sizeof(int64_t), 0) != hipSuccess) c->h_small = nullptr;
+    return c;
+}
+
+extern "C" void dd_ctx_free(dd_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    DBuf *all[] = {&c->comp, &c->blk, &c->U, &c->status, &c->misc, &c->S, &c->ccnt, &c->cbase, &c->off, &c->keep,
+                   &c->kidx, &c->drop, &c->didx, &c->auxc, &c->aidx, &c->ncig, &c->coff, &c->nb, &c->boff, &c->rpos,
+                   &c->krec, &c->keys, &c->vals, &c->keys2, &c->vals2, &c->head, &c->tmp, &c->sq, &c->sqi, &c->sv,
+                   &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack};
+    for (DBuf *b : all)
+        if (b->p) (void)hipFree(b->p);
+    for (int k = 0; k < 4; k++)
+        if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_aux) (void)hipHostFree(c->h_aux);
+    if (c->st) (void)hipStreamDestroy(c->st);
+    delete c;
+}
+
+extern "C" void dd_ctx_times(const dd_ctx *c, double *ms) {
+    ms[0] = c->ms_inflate;
+    ms[1] = c->ms_walk;
+    ms[2] = c->ms_parse;
+}
+
+// inflate a run's blocks (h_comp: pinned, readable 64 bytes past comp_len)
+// and find its records: starts[0..n_starts) are record offsets in the
+// inflated stream (the first = the run's first record), u_end its end
+extern "C" int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
+                           int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int64_t *n_rec,
+                           char *err, int errlen) {
+    DCK(hipSetDevice(c->device));
+    hipStream_t st = c->st;
+    DGROW(c->comp, (size_t)comp_len + 64);
+    DGROW(c->blk, sizeof(DdBlock) * (size_t)(nblk + 1));
+    DGROW(c->U, (size_t)ubytes + 64);
+    DGROW(c->status, (size_t)nblk + 1);
+    DGROW(c->misc, 256);
+    DGROW(c->S, sizeof(int64_t) * (size_t)(n_starts + 1));
+    DGROW(c->ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
+    DGROW(c->cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
+    DCK(hipMemcpyAsync(c->comp.p, h_comp, (size_t)comp_len + 64, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(c->blk.p, h_blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(c->S.p, h_starts, sizeof(int64_t) * (size_t)n_starts, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(P<int64_t>(c->S) + n_starts, &u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
+    uint32_t *bad = P<uint32_t>(c->misc);
+    DCK(hipEventRecord(c->ev[0], st));
+    if (dd_inflate_launch(st, P<uint8_t>(c->comp), P<DdBlock>(c->blk), nblk, P<uint8_t>(c->U), P<uint8_t>(c->status),
+                          bad + 1)) {
+        if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
+        return -1;
+    }
+    DCK(hipEventRecord(c->ev[1], st));
+    // records: count per chunk, place, write offsets
+    hipLaunchKernelGGL(k_walk, dim3(grid_for(n_starts, 128, 1u << 30)), dim3(128), 0, st, P<uint8_t>(c->U),
+                       P<int64_t>(c->S), n_starts, P<uint32_t>(c->ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr,
+                       bad);
+    size_t tb = 0;
+    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->ccnt), P<uint32_t>(c->cbase), (int)n_starts, st));
+    DGROW(c->tmp, tb);
+    DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->ccnt), P<uint32_t>(c->cbase), (int)n_starts, st));
+    DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(c->cbase) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(c->ccnt) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)c->h_small + 8, bad, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipStreamSynchronize(st));
+    const uint32_t *hs = (const uint32_t *)c->h_small;
+    if (hs[3]) {
+        if (err) snprintf(err, (size_t)errlen, "device inflate: %u blocks failed", hs[3]);
+        return -2;
+    }
+    if (hs[2]) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: record chain (%#x) does not follow the index", hs[2]);
+        return -2;
+    }
+    const int64_t R = (int64_t)hs[0] + hs[1];
+    DGROW(c->off, sizeof(int64_t) * (size_t)(R + 1));
+    hipLaunchKernelGGL(k_walk, dim3(grid_for(n_starts, 128, 1u << 30)), dim3(128), 0, st, P<uint8_t>(c->U),
+                       P<int64_t>(c->S), n_starts, (uint32_t *)nullptr, P<uint32_t>(c->cbase), P<int64_t>(c->off), bad);
+    DCK(hipEventRecord(c->ev[2], st));
+    DCK(hipGetLastError());
+    c->R = R;
+    c->nblk = nblk;
+    c->ubytes = ubytes;
+    *n_rec = R;
+    return 0;
+}
+
+// find_insert_mean's sample from the loaded run, all of its records in file
+// order: at most cap_left (insert, l_qseq) pairs, and the mapped-bases sum up
+// to the record that completes the cap (or over the whole run)
+extern "C" int dd_run_stats(dd_ctx *c, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq,
+                            int64_t *n_taken, int64_t *m_contrib, char *err, int errlen) {
+    DCK(hipSetDevice(c->device));
+    hipStream_t st = c->st;
+    const int64_t R = c->R;
+    *n_taken = 0;
+    *m_contrib = 0;
+    if (R == 0 || cap_left <= 0) return 0;
+    DGROW(c->sq, 4 * (size_t)R);
+    DGROW(c->sqi, 4 * (size_t)R);
+    DGROW(c->sv, 4 * (size_t)R);
+    DGROW(c->slq, 4 * (size_t)R);
+    DGROW(c->sm, 8 * (size_t)R);
+    const int64_t take_cap = std::min<int64_t>(cap_left, R);
+    DGROW(c->s_ins, 4 * (size_t)take_cap);
+    DGROW(c->s_lq, 4 * (size_t)take_cap);
+    hipLaunchKernelGGL(k_stats, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off), R, min_mapq,
+                       P<uint32_t>(c->sq), P<int32_t>(c->sv), P<int32_t>(c->slq), P<int64_t>(c->sm));
+    size_t tb = 0, tb2 = 0;
+    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->sq), P<uint32_t>(c->sqi), (int)R, st));
+    DCK(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, P<int64_t>(c->sm), P<int64_t>(c->sm), (int)R, st));
+    DGROW(c->tmp, std::max(tb, tb2));
+    DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->sq), P<uint32_t>(c->sqi), (int)R, st));
+    DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, tb2, P<int64_t>(c->sm), P<int64_t>(c->sm), (int)R, st));
+    int64_t *mcap = (int64_t *)((char *)c->misc.p + 64);
+    DCK(hipMemsetAsync(mcap, 0xff, 8, st));
+    hipLaunchKernelGGL(k_stats_take, dim3(grid_for(R)), dim3(256), 0, st, P<uint32_t>(c->sq), P<uint32_t>(c->sqi),
+                       P<int32_t>(c->sv), P<int32_t>(c->slq), P<int64_t>(c->sm), R, take_cap, P<int32_t>(c->s_ins),
+                       P<int32_t>(c->s_lq), mcap);
+    // qualifying total, m total, m at the cap
+    DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(c->sqi) + R - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(c->sq) + R - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync(c->h_small + 1, P<int64_t>(c->sm) + R - 1, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync(c->h_small + 2, mcap, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipStreamSynchronize(st));
+    const uint32_t *hs = (const uint32_t *)c->h_small;
+    const int64_t nq = (int64_t)hs[0] + hs[1];
+    const int64_t n = std::min<int64_t>(nq, cap_left);
+    if (n > 0) {
+        DCK(hipMemcpyAsync(h_ins, c->s_ins.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+        DCK(hipMemcpyAsync(h_lq, c->s_lq.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+        DCK(hipStreamSynchronize(st));
+    }
+    *n_taken = n;
+    *m_contrib = (nq >= cap_left) ? c->h_small[2] : c->h_small[1];
+    return 0;
+}
+
+// the loaded run parsed into `stage` (records j0.. of the run): fields,
+// CIGAR words, bases, qualities, name ids, dropped records; the split-read
+// candidates' record bytes come back to the host (dd_run_aux)
+extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len,
+                            grom_stage *stage, dd_parse_out *po, char *err, int errlen) {
+    DCK(hipSetDevice(c->device));
+    hipStream_t st = c->st;
+    const int64_t R = c->R;
+    memset(po, 0, sizeof(*po));
+    const size_t r4 = 4 * (size_t)(R + 1), r8 = 8 * (size_t)(R + 1);
+    DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
+    DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
+    DGROW(c->rpos, r4);
+    uint32_t *bad = P<uint32_t>(c->misc);
+    int64_t *tot = (int64_t *)((char *)c->misc.p + 128);
+    if (R > 0)
+        hipLaunchKernelGGL(k_rec_meta, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off), R, j0,
+                           tid, P<uint32_t>(c->keep), P<uint32_t>(c->drop), P<uint32_t>(c->auxc), P<uint32_t>(c->ncig),
+                           P<int64_t>(c->nb), P<int32_t>(c->rpos), bad);
+    if (R > 0) {
+        size_t tb = 0, t2 = 0;
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->keep), P<uint32_t>(c->kidx), (int)R, st));
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, P<int64_t>(c->nb), P<int64_t>(c->boff), (int)R, st));
+        DGROW(c->tmp, std::max(tb, t2));
+        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->keep), P<uint32_t>(c->kidx), (int)R, st));
+        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->drop), P<uint32_t>(c->didx), (int)R, st));
+        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), (int)R, st));
+        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->ncig), P<uint32_t>(c->coff), (int)R, st));
+        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t2, P<int64_t>(c->nb), P<int64_t>(c->boff), (int)R, st));
+    }
+    hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, st, P<uint32_t>(c->keep), P<uint32_t>(c->kidx),
+                       P<uint32_t>(c->drop), P<uint32_t>(c->didx), P<uint32_t>(c->auxc), P<uint32_t>(c->aidx),
+                       P<uint32_t>(c->ncig), P<uint32_t>(c->coff), P<int64_t>(c->nb), P<int64_t>(c->boff), R, tot);
+    DCK(hipMemcpyAsync(c->h_small, tot, 5 * 8, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync(c->h_small + 5, bad, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipStreamSynchronize(st));
+    const int64_t n = c->h_small[0], nd = c->h_small[1], na = c->h_small[2], ncg = c->h_small[3], nbs = c->h_small[4];
+    const uint32_t b0 = ((const uint32_t *)(c->h_small + 5))[0];
+    if (b0) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: records do not parse as the run's (%#x)", b0);
+        return -2;
+    }
+    // the stage: exact sizes, then every array written in place
+    grom_stage_sizes sz;
+    memset(&sz, 0, sizeof(sz));
+    sz.n = n;
+    sz.n_cigar_ops = ncg;
+    sz.n_bases = nbs;
+    sz.n_aux = na + 1;  // + the -S patch
+    sz.n_drop = nd;
+    sz.ref_len = ref_len;
+    grom_reads dv;
+    if (grom_stage_fill_begin(stage, &sz, &dv) != GROM_OK) {
+        if (err) snprintf(err, (size_t)errlen, "%s", grom_last_error());
+        return -1;
+    }
+    StageOut so;
+    so.pos = (int32_t *)dv.pos; so.mtid = (int32_t *)dv.mtid; so.mpos = (int32_t *)dv.mpos;
+    so.isize = (int32_t *)dv.isize; so.lq = (int32_t *)dv.l_qseq; so.aidx = (int32_t *)dv.aux_idx;
+    so.flag = (uint16_t *)dv.flag; so.mapq = (uint8_t *)dv.mapq; so.coff = (uint32_t *)dv.cigar_off;
+    so.cig = (uint32_t *)dv.cigar; so.nid = (uint32_t *)dv.name_id; so.boff = (int64_t *)dv.base_off;
+    so.dpos = (int32_t *)dv.drop_pos; so.dlq = (int32_t *)dv.drop_lq; so.dbef = (int64_t *)dv.drop_before;
+    DGROW(c->krec, 8 * (size_t)(n + 1));
+    DGROW(c->keys, 8 * (size_t)(n + 1)); DGROW(c->vals, 4 * (size_t)(n + 1));
+    DGROW(c->keys2, 8 * (size_t)(n + 1)); DGROW(c->vals2, 4 * (size_t)(n + 1)); DGROW(c->head, 4 * (size_t)(n + 1));
+    DGROW(c->acand, 8 * (size_t)(na + 2)); DGROW(c->alen, 8 * (size_t)(na + 2)); DGROW(c->aoff, 8 * (size_t)(na + 2));
+    DGROW(c->akidx, 8 * (size_t)(na + 2));
+    int32_t *last = (int32_t *)((char *)c->misc.p + 192);
+    // (grom_stage_fill_begin waited for the stage's earlier copies; the
+    // arrays are written on this context's stream, synchronised below before
+    // the chromosome is handed to a scan)
+    if (R > 0)
+        hipLaunchKernelGGL(k_rec_write, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off), R, j0,
+                           P<uint32_t>(c->keep), P<uint32_t>(c->kidx), P<uint32_t>(c->drop), P<uint32_t>(c->didx),
+                           P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), P<uint32_t>(c->coff), P<int64_t>(c->boff),
+                           P<int32_t>(c->rpos), so, P<int64_t>(c->krec), P<uint64_t>(c->keys), P<uint32_t>(c->vals),
+                           P<int64_t>(c->acand), read_name_len, last, bad);
+    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, st, so.coff + n, (uint32_t)ncg);
+    if (n > 0) {
+        hipLaunchKernelGGL(k_copy_bases, dim3(grid_for(n * 64, 256, 1u << 16)), dim3(256), 0, st, P<uint8_t>(c->U),
+                           P<int64_t>(c->off), P<int64_t>(c->krec), n, (const int64_t *)so.boff, (uint8_t *)dv.seq,
+                           (uint8_t *)dv.qual);
+        // read-name ids: sort the hashes, check each equal-hash run byte for byte
+        size_t tb = 0, t2 = 0;
+        DCK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, P<uint64_t>(c->keys), P<uint64_t>(c->keys2),
+                                               P<uint32_t>(c->vals), P<uint32_t>(c->vals2), (int)n, 0, 64, st));
+        DCK(hipcub::DeviceScan::InclusiveScan(nullptr, t2, P<uint32_t>(c->head), P<uint32_t>(c->head),
+                                              hipcub::Max(), (int)n, st));
+        DGROW(c->tmp, std::max(tb, t2));
+        DCK(hipcub::DeviceRadixSort::SortPairs(c->tmp.p, tb, P<uint64_t>(c->keys), P<uint64_t>(c->keys2),
+                                               P<uint32_t>(c->vals), P<uint32_t>(c->vals2), (int)n, 0, 64, st));
+        hipLaunchKernelGGL(k_seg_head, dim3(grid_for(n)), dim3(256), 0, st, P<uint64_t>(c->keys2), n,
+                           P<uint32_t>(c->head));
+        DCK(hipcub::DeviceScan::InclusiveScan(c->tmp.p, t2, P<uint32_t>(c->head), P<uint32_t>(c->head), hipcub::Max(),
+                                              (int)n, st));
+        hipLaunchKernelGGL(k_name_ids, dim3(grid_for(n)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off),
+                           P<int64_t>(c->krec), P<uint64_t>(c->keys2), P<uint32_t>(c->vals2), P<uint32_t>(c->head), n,
+                           so.nid, bad);
+    }
+    // split-read candidates: lengths, offsets, kept indices, packed bytes -> host
+    int64_t apack = 0;
+    if (na > 0) {
+        hipLaunchKernelGGL(k_aux_len, dim3(grid_for(na)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off),
+                           P<int64_t>(c->acand), na, P<int64_t>(c->alen), P<uint32_t>(c->kidx), P<int64_t>(c->akidx));
+        size_t tb = 0;
+        DCK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
+        DGROW(c->tmp, tb);
+        DCK(hipMemsetAsync(c->aoff.p, 0, 8, st));
+        DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, tb, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
+    }
+    DCK(hipMemcpyAsync(c->h_small, last, 16, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync(c->h_small + 2, bad, 8, hipMemcpyDeviceToHost, st));
+    if (na > 0) DCK(hipMemcpyAsync(c->h_small + 3, P<int64_t>(c->aoff) + na, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipStreamSynchronize(st));
+    const int32_t *hl = (const int32_t *)c->h_small;
+    const uint32_t b1 = ((const uint32_t *)(c->h_small + 2))[0];
+    if (b1) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: %s (%#x)",
+                          (b1 & DB_NAMES) ? "read-name hash collision" : (b1 & DB_UNSORTED) ? "records are not sorted by position"
+                                                                                               : "record check failed",
+                          b1);
+        return -2;
+    }
+    po->n_rec = R;
+    po->n_kept = n;
+    po->n_drop = nd;
+    po->n_cig = ncg;
+    po->n_bases = nbs;
+    po->n_auxc = na;
+    po->last_pos = hl[0];
+    po->last_lq = hl[1];
+    po->last_hclip = hl[2];
+    po->last_kept = hl[3];
+    if (na > 0) {
+        apack = c->h_small[3];
+        DGROW(c->apack, (size_t)apack + 16);
+        hipLaunchKernelGGL(k_aux_pack, dim3(grid_for(na, 1, 65536)), dim3(64), 0, st, P<uint8_t>(c->U),
+                           P<int64_t>(c->off), P<int64_t>(c->acand), P<int64_t>(c->aoff), na, P<uint8_t>(c->apack));
+        const size_t need = (((size_t)apack + 15) & ~(size_t)15) + 16 * (size_t)(na + 1) + 64;
+        if (need > c->h_aux_cap) {
+            if (c->h_aux) (void)hipHostFree(c->h_aux);
+            c->h_aux = nullptr;
+            c->h_aux_cap = need + need / 4;
+            DCK(hipHostMalloc((void **)&c->h_aux, c->h_aux_cap, 0));
+        }
+        // host buffer: [packed records][offsets, na + 1][kept index of each]
+        int64_t *ho = (int64_t *)(c->h_aux + (((size_t)apack + 15) & ~(size_t)15));
+        DCK(hipMemcpyAsync(c->h_aux, c->apack.p, (size_t)apack, hipMemcpyDeviceToHost, st));
+        DCK(hipMemcpyAsync(ho, c->aoff.p, 8 * (size_t)(na + 1), hipMemcpyDeviceToHost, st));
+        DCK(hipMemcpyAsync(ho + na + 1, c->akidx.p, 8 * (size_t)na, hipMemcpyDeviceToHost, st));
+        DCK(hipStreamSynchronize(st));
+        po->aux_bytes = c->h_aux;
+        po->aux_off = ho;
+        po->aux_kidx = ho + na + 1;
+    }
+    DCK(hipEventRecord(c->ev[3], st));
+    DCK(hipStreamSynchronize(st));
+    float a = 0, b = 0, d = 0;
+    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    c->ms_inflate += a;
+    c->ms_walk += b;
+    c->ms_parse += d;
+    return 0;
+}
+
+extern "C" int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64_t *sd) {
+    if (hipSetDevice(c->device) != hipSuccess) return -1;
+    grom_reads dv;
+    if (grom_stage_dev_reads(stage, &dv) != GROM_OK) return -1;
+    int64_t *o = (int64_t *)((char *)c->misc.p + 224);
+    hipLaunchKernelGGL(k_lower_bound, dim3(1), dim3(1), 0, c->st, dv.pos, dv.n, s0, o);
+    hipLaunchKernelGGL(k_lower_bound, dim3(1), dim3(1), 0, c->st, dv.drop_pos, dv.n_drop, s0, o + 1);
+    if (hipMemcpyAsync(c->h_small, o, 16, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+        hipStreamSynchronize(c->st) != hipSuccess)
+        return -1;
+    *sk = c->h_small[0];
+    *sd = c->h_small[1];
+    return 0;
 }

@@ -23,6 +23,7 @@
 #include "bamio.h"
 #include "stream.h"
 #include "pdecode.h"
+#include "ddecode.h"
 
 static const char *VERSION = "GROM, Version 1.0.1\n"; /* g_version_name, GROM.c:690 */
 
@@ -419,6 +420,45 @@ static uint32_t chrom_seed(void) {
     return e ? (uint32_t)strtoul(e, NULL, 10) : (uint32_t)time(NULL);
 }
 
+/* test hook (GROM_STAGE_DIGEST): the staged input of a chromosome, copied
+ * back to the host, as the plan-only line prints it (the device decoder's
+ * output against the host decoder's, tests/test_gpu_parity.py) */
+static void stage_digest_line(grom_stage *st, const grom_chrom *ch, int device) {
+    grom_chrom dc;
+    grom_reads d, h;
+    if (grom_stage_view(st, ch, &dc, &d) != GROM_OK) return;
+    memset(&h, 0, sizeof(h));
+    h.n = d.n;
+    h.n_cigar_ops = d.n_cigar_ops;
+    h.n_bases = d.n_bases;
+    h.n_aux = d.n_aux;
+    h.n_drop = d.n_drop;
+    const int64_t n = d.n, nd = d.n_drop;
+#define DL(f, T, cnt)                                                                     \
+    T *f##_h = (T *)malloc(sizeof(T) * (size_t)((cnt) > 0 ? (cnt) : 1));                   \
+    if ((cnt) > 0 && d.f) grom_copy_d2h(f##_h, d.f, sizeof(T) * (size_t)(cnt), device);   \
+    h.f = f##_h;
+    DL(pos, int32_t, n) DL(flag, uint16_t, n) DL(mapq, uint8_t, n) DL(mtid, int32_t, n) DL(mpos, int32_t, n)
+    DL(isize, int32_t, n) DL(l_qseq, int32_t, n) DL(cigar_off, uint32_t, n + 1) DL(base_off, int64_t, n)
+    DL(name_id, uint32_t, n) DL(drop_pos, int32_t, nd) DL(drop_lq, int32_t, nd) DL(drop_before, int64_t, nd)
+    /* absolute offsets: the whole CIGAR / base arrays */
+    DL(cigar, uint32_t, d.n_cigar_ops) DL(qual, uint8_t, d.n_bases) DL(seq, uint8_t, d.n_bases / 2)
+    DL(aux, grom_aux, d.n_aux)
+#undef DL
+    int32_t *ai = NULL;
+    if (d.aux_idx) {
+        ai = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+        if (n > 0) grom_copy_d2h(ai, d.aux_idx, sizeof(int32_t) * (size_t)n, device);
+        h.aux_idx = ai;
+    }
+    printf("stage %s tid=%d reads=%lld n_skip=%d p_last=%d lseq_tail=%d digest=%016llx\n", ch->name, ch->tid,
+           (long long)n, ch->n_skip, ch->p_last, ch->lseq_tail, (unsigned long long)pd_digest(&h));
+    free((void *)h.pos); free((void *)h.flag); free((void *)h.mapq); free((void *)h.mtid); free((void *)h.mpos);
+    free((void *)h.isize); free((void *)h.l_qseq); free((void *)h.cigar_off); free((void *)h.base_off);
+    free((void *)h.name_id); free((void *)h.drop_pos); free((void *)h.drop_lq); free((void *)h.drop_before);
+    free((void *)h.cigar); free((void *)h.qual); free((void *)h.seq); free((void *)h.aux); free(ai);
+}
+
 /* Scan one chromosome on context `slot`; its VCF rows go to j->text (malloc'd). */
 static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     chrom_plan *cp = j->cp;
@@ -463,6 +503,7 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     ch.tid = cp->tid;
     ch.cnv = cp->tid >= 0; /* detect_del_dup runs for a matched target, GROM.c:16633 */
     ch.seed = chrom_seed();
+    if (!j->has_batch && getenv("GROM_STAGE_DIGEST")) stage_digest_line(j->stage, &ch, j->device);
     grom_out out = {0};
     grom_stats st = {0};
     if (j->pd) pd_trace(j->pd, PD_EV_SCAN, j->k, 0);
@@ -986,6 +1027,7 @@ static int run_streamed(cli_state *S) {
     for (int c = 0; c < S->n_cand; c++) {
         cin[c].tid = S->plan[c].tid;
         cin[c].target_name = S->plan[c].target;
+        cin[c].len = S->plan[c].len;
     }
     const char *dt = getenv("GROM_DECODE_THREADS");
     int n_thr = dt ? atoi(dt) : host_cpus();
@@ -1055,6 +1097,12 @@ static int run_streamed(cli_state *S) {
         for (int c = 0; c < S->n_cand; c++) want[c] = chrom_wanted(S->plan[c].name);
         pd_set_wanted(pd, want);
         free(want);
+    }
+    /* BAM decode on the GPUs (ddecode.hip) with GROM_DEVICE_DECODE=1; the
+     * host decoder threads otherwise (plan-only runs always use them) */
+    {
+        const char *dd = getenv("GROM_DEVICE_DECODE");
+        pd_set_device_mode(pd, !g_plan_only && dd && atoi(dd) != 0);
     }
     if (pd_start(pd, P->min_mapq, S->n_dev, dev_of, g_plan_only)) {
         fprintf(stderr, "grom: %s\n", pd_error(pd));
@@ -1178,6 +1226,13 @@ done:
                t_started - S->t_cli0, t_stats - S->t_cli0, t_ctx - S->t_cli0, t_loop - S->t_cli0, t_end - S->t_cli0);
         pd_counters pc;
         pd_get_counters(pd, &pc);
+        if (pc.device)
+            printf("device decode: %lld records, %.2f GB compressed read and copied to HBM, %.2f GB inflated on the GPU; "
+                   "file reads %.2f s, device work %.2f s (GPU inflate %.3f s, record walk %.3f s, parse %.3f s), "
+                   "per-chromosome decode + finalise %.2f s, wall %.2f s\n",
+                   (long long)pc.records, pc.compressed_bytes / 1e9, pc.inflated_bytes / 1e9, pc.io_s, pc.decode_thread_s,
+                   pc.gpu_ms[0] / 1e3, pc.gpu_ms[1] / 1e3, pc.gpu_ms[2] / 1e3, pc.upload_s, clock_gettime_s() - t_start);
+        else
         printf("streamed decode: %lld records in %lld pieces, %d threads (%s), %.2f GB inflated, %.2f GB to HBM, "
                "decoder busy %.2f s (inflate %.2f s, file reads %.2f s), uploader %.2f s (waiting %.2f s), wall %.2f s\n",
                (long long)pc.records, (long long)pc.pieces, pc.threads, pc.libdeflate ? "libdeflate" : "zlib",

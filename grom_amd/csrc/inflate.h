@@ -57,26 +57,54 @@ GI_FN uint32_t gi_rev15(uint32_t x) {
 #endif
 }
 
-// LSB-first bit reader over the block's DEFLATE data.  A BGZF block's data is
-// followed by its 8-byte trailer (CRC32, ISIZE), and the reader never holds
-// more than 8 bytes it has not consumed, so it may load past the data's end;
-// the caller checks that no more than the data was consumed.
+// LSB-first bit reader over the block's DEFLATE data, fed by aligned 32-bit
+// words with the next word loaded one refill ahead (the load's latency hides
+// behind the symbols decoded meanwhile).  A BGZF block's data is followed by
+// its 8-byte trailer (CRC32, ISIZE) and then the next block or the buffer's
+// padding, so reading up to 15 bytes past the data is safe; the caller checks
+// that no more than the data was consumed.
 struct GiBits {
-    const uint8_t *p;
+    const uint32_t *wp;  // the word after `nxt`
+    uint32_t nxt;        // the next word to merge (already loaded)
     uint64_t buf;
-    int cnt;
+    int cnt;             // valid bits in buf
+    int sh0;             // bits of the first word before the data
+    int64_t merged;      // words merged into buf so far
 };
 
-GI_FN uint32_t gi_load4(const uint8_t *p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+GI_FN uint32_t gi_ldw(const uint32_t *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *p;
+#else
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+#endif
+}
+
+GI_FN void gi_open(GiBits &b, const uint8_t *in) {
+    // (pointer arithmetic on `in`, not an integer round trip: the compiler
+    // keeps the global address space, so the loads are global_load, not flat
+    // loads that an LDS wait would also wait for)
+    const int mis = (int)((uintptr_t)in & 3);
+    b.wp = (const uint32_t *)(in - mis);
+    b.sh0 = mis * 8;
+    const uint32_t w0 = gi_ldw(b.wp);
+    b.nxt = gi_ldw(b.wp + 1);
+    b.wp += 2;
+    b.buf = (uint64_t)(w0 >> b.sh0);
+    b.cnt = 32 - b.sh0;
+    b.merged = 1;
 }
 
 // at least 32 bits in the buffer
 GI_FN void gi_refill(GiBits &b) {
     if (b.cnt < 32) {
-        b.buf |= (uint64_t)gi_load4(b.p) << b.cnt;
-        b.p += 4;
+        b.buf |= (uint64_t)b.nxt << b.cnt;
         b.cnt += 32;
+        b.nxt = gi_ldw(b.wp);
+        b.wp++;
+        b.merged++;
     }
 }
 
@@ -177,9 +205,7 @@ GI_FN void gi_dist_code(int d, int &base, int &extra) {  // d = 0..29
 template <int LANES>
 GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len, uint16_t *sym, int lane) {
     GiBits b;
-    b.p = in;
-    b.buf = 0;
-    b.cnt = 0;
+    gi_open(b, in);
     uint32_t o = 0;
     GiHuff lit, dist;
     for (;;) {
@@ -294,20 +320,28 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
                 if (dd > o) return GI_E_DIST;
                 if (o + len > out_len) return GI_E_OVERRUN;
                 uint8_t *q = out + o;
-                if (dd >= len) {  // source and destination do not overlap
-                    for (uint32_t k = 0; k < len; k++) q[k] = q[(int64_t)k - dd];
-                } else if (dd <= 8) {  // a short repeating pattern: from registers
+                if (dd < len && dd <= 8) {  // a short repeating pattern: loaded once, stored from registers
                     uint64_t pat = 0;
-                    for (uint32_t k = 0; k < dd; k++) pat |= (uint64_t)q[(int64_t)k - dd] << (8 * k);
+                    GI_UNROLL
+                    for (uint32_t k = 0; k < 8; k++)
+                        if (k < dd) pat |= (uint64_t)q[(int64_t)k - dd] << (8 * k);
                     uint32_t r = 0;
                     for (uint32_t k = 0; k < len; k++) {
                         q[k] = (uint8_t)(pat >> (8 * r));
                         r = (r + 1 == dd) ? 0 : r + 1;
                     }
-                } else {  // overlapping, period > 8: chunks of dd bytes
-                    for (uint32_t k = 0; k < len; k += dd) {
-                        const uint32_t m = (len - k < dd) ? len - k : dd;
-                        for (uint32_t j = 0; j < m; j++) q[k + j] = q[(int64_t)(k + j) - dd];
+                } else {  // chunks of up to 16 bytes whose sources are final: all loads, then the stores
+                    for (uint32_t k = 0; k < len;) {
+                        uint32_t m = len - k;
+                        m = m < 16u ? m : 16u;
+                        m = m < dd ? m : dd;
+                        uint8_t t[16];
+                        GI_UNROLL
+                        for (uint32_t j = 0; j < 16; j++) t[j] = j < m ? q[(int64_t)(k + j) - dd] : 0;
+                        GI_UNROLL
+                        for (uint32_t j = 0; j < 16; j++)
+                            if (j < m) q[k + j] = t[j];
+                        k += m;
                     }
                 }
                 o += len;
@@ -317,9 +351,9 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
         }
         if (bfinal) break;
     }
-    // consumed: everything loaded minus the whole bytes still buffered
-    const int64_t used = (int64_t)(b.p - in) - (int64_t)(b.cnt >> 3);
-    if (used > (int64_t)in_len) return GI_E_INPUT;
+    // consumed bits: every merged word minus the first word's lead and the buffer
+    const int64_t used_bits = b.merged * 32 - b.sh0 - b.cnt;
+    if (used_bits > 8 * (int64_t)in_len) return GI_E_INPUT;
     if (o != out_len) return GI_E_SIZE;
     return GI_OK;
 }

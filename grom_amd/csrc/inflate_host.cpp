@@ -29,7 +29,7 @@ extern "C" int64_t grom_inflate_selftest(const char *bam_path, int64_t max_block
     fseek(f, 0, SEEK_END);
     const long size = ftell(f);
     fseek(f, 0, SEEK_SET);
-    std::vector<uint8_t> file((size_t)size + 16);
+    std::vector<uint8_t> file((size_t)size + 64);
     if (fread(file.data(), 1, (size_t)size, f) != (size_t)size) {
         fclose(f);
         return -1;

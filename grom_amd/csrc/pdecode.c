@@ -25,6 +25,7 @@
 #include <unistd.h>
 #include <zlib.h>
 
+#include "ddecode.h"
 #include "stream.h"
 
 #define PD_INSERT_CAP 10000000 /* insert_sample_size, GROM.c:913 */
@@ -423,6 +424,16 @@ struct pd_session {
     struct { double t; int64_t a, b; int ev, thr; } *tr;
     int64_t tr_n, tr_cap;
     int test_soft_abort;   /* GROM_TEST_SOFT_ABORT=<piece>: contradict the plan at that piece (tests) */
+    /* device mode (pd_start with GROM_DEVICE_DECODE): whole runs inflated and
+     * parsed on the GPUs (ddecode.hip) by one worker thread per device */
+    int dev_mode;
+    uint64_t **lin;        /* per target: the BAI's linear index (record starts every 16 kb) */
+    int *n_lin;
+    int n_tgt;
+    pthread_t *dw;
+    int n_dw, dw_started;
+    double c_gpu_ms[3];    /* inflate, record walk, parse (HIP events, summed) */
+    int io_threads;
     /* uploader scratch */
     uint32_t *remap;
     int64_t remap_cap;
@@ -1951,6 +1962,20 @@ pd_session *pd_open(const char *bam_path, const bam_hdr *hdr, const pd_chrom_in 
             r->n_pieces = s->n_pieces - r->first_piece;
         }
     }
+    /* device mode cuts runs at the linear index's record starts: keep it */
+    s->n_tgt = idx.n_ref;
+    s->lin = (uint64_t **)calloc((size_t)(idx.n_ref > 0 ? idx.n_ref : 1), sizeof(uint64_t *));
+    s->n_lin = (int *)calloc((size_t)(idx.n_ref > 0 ? idx.n_ref : 1), sizeof(int));
+    for (int t = 0; t < idx.n_ref; t++) {
+        const bai_ref *R = &idx.ref[t];
+        if (R->n_intv > 0) {
+            s->lin[t] = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)R->n_intv);
+            if (s->lin[t]) {
+                memcpy(s->lin[t], R->ioff, sizeof(uint64_t) * (size_t)R->n_intv);
+                s->n_lin[t] = R->n_intv;
+            }
+        }
+    }
     bai_free(&idx);
     have_idx = 0;
     s->splitread = splitread;
@@ -1988,6 +2013,8 @@ fail:
 #undef FAIL
 }
 
+void pd_set_device_mode(pd_session *s, int on) { s->dev_mode = on; }
+
 void pd_set_wanted(pd_session *s, const int *want) {
     for (int k = 0; k < s->n_plan; k++) s->want[k] = want ? (want[k] != 0) : 1;
     for (int i = 0; i < s->n_runs; i++) {
@@ -1997,6 +2024,366 @@ void pd_set_wanted(pd_session *s, const int *want) {
     }
 }
 
+/* ================= device mode: whole runs decoded on the GPUs ================= */
+typedef struct {
+    pd_session *s;
+    int device, first;       /* first: this worker also gathers the insert statistics */
+    dd_ctx *dd;
+    uint8_t *comp;           /* pinned compressed run (+64 readable bytes) */
+    int64_t comp_cap;
+    DdBlock *blk;
+    int64_t blk_cap;
+    int64_t *starts;
+    int64_t starts_cap;
+    int loaded;              /* run index whose records dd holds, -1 none */
+    int64_t loaded_R;
+} dd_worker;
+
+typedef struct {
+    int fd;
+    uint8_t *buf;
+    int64_t len, off;
+    int ok;
+} pread_part;
+
+static void *pread_main(void *arg) {
+    pread_part *p = (pread_part *)arg;
+    int64_t got = 0;
+    while (got < p->len) {
+        const ssize_t k = pread(p->fd, p->buf + got, (size_t)(p->len - got), (off_t)(p->off + got));
+        if (k <= 0) break;
+        got += k;
+    }
+    p->ok = got == p->len;
+    return NULL;
+}
+
+/* read [off, off+len) on up to nt threads */
+static int pread_par(int fd, uint8_t *buf, int64_t len, int64_t off, int nt) {
+    if (nt < 1) nt = 1;
+    if (len < ((int64_t)8 << 20)) nt = 1;
+    pread_part parts[32];
+    pthread_t th[32];
+    if (nt > 32) nt = 32;
+    const int64_t step = (len + nt - 1) / nt;
+    int started = 0;
+    for (int t = 0; t < nt; t++) {
+        const int64_t a = t * step, b = a + step < len ? a + step : len;
+        parts[t].fd = fd;
+        parts[t].buf = buf + a;
+        parts[t].len = b > a ? b - a : 0;
+        parts[t].off = off + a;
+        parts[t].ok = 0;
+        if (t == nt - 1 || pthread_create(&th[t], NULL, pread_main, &parts[t]) != 0) pread_main(&parts[t]);
+        else started |= 1 << t;
+    }
+    int ok = 1;
+    for (int t = 0; t < nt; t++) {
+        if (started & (1 << t)) pthread_join(th[t], NULL);
+        ok &= parts[t].ok;
+    }
+    return ok ? 0 : -1;
+}
+
+static int cmp_i64(const void *a, const void *b) {
+    const int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* a run's compressed bytes into the worker's pinned buffer, its block table
+ * and record starts, then dd_run_load (inflate + record walk on the GPU) */
+static int dw_load(dd_worker *w, int ri, char *err, int errlen) {
+    pd_session *s = w->s;
+    const pd_run *r = &s->runs[ri];
+    const int64_t c0 = (int64_t)(r->vbeg >> 16);
+    int64_t c1;
+    if (r->vend == UINT64_MAX) {
+        c1 = s->file_size;
+    } else {
+        c1 = (int64_t)(r->vend >> 16);
+        if ((r->vend & 0xffff) != 0) { /* the block holding the end is part of the range */
+            uint8_t h[18];
+            if (pread(s->fd, h, 18, (off_t)c1) != 18) { snprintf(err, (size_t)errlen, "cannot read a block header"); return -2; }
+            const int xlen = h[10] | (h[11] << 8);
+            if (xlen < 6 || h[12] != 'B' || h[13] != 'C') { snprintf(err, (size_t)errlen, "not a BGZF block at %lld", (long long)c1); return -2; }
+            c1 += (int64_t)(h[16] | (h[17] << 8)) + 1;
+        }
+    }
+    const int64_t len = c1 - c0;
+    if (len <= 0 || c1 > s->file_size) { snprintf(err, (size_t)errlen, "bad run range"); return -2; }
+    if (len + 64 > w->comp_cap) {
+        grom_pinned_free(w->comp);
+        w->comp_cap = len + len / 8 + 4096;
+        w->comp = (uint8_t *)grom_pinned_alloc((size_t)w->comp_cap);
+        if (!w->comp) { w->comp_cap = 0; snprintf(err, (size_t)errlen, "no pinned memory for a run"); return -1; }
+    }
+    const double t0 = now_s();
+    if (pread_par(s->fd, w->comp, len, c0, s->io_threads)) { snprintf(err, (size_t)errlen, "reading the BAM failed"); return -1; }
+    memset(w->comp + len, 0, 64);
+    const double t1 = now_s();
+    int64_t ub = 0;
+    int64_t nb = dd_block_table(w->comp, len, NULL, 0, &ub);
+    if (nb <= 0) { snprintf(err, (size_t)errlen, "the run is not whole BGZF blocks"); return -2; }
+    if (nb > w->blk_cap) {
+        free(w->blk);
+        w->blk_cap = nb + nb / 4 + 16;
+        w->blk = (DdBlock *)malloc(sizeof(DdBlock) * (size_t)w->blk_cap);
+        if (!w->blk) { w->blk_cap = 0; return -1; }
+    }
+    dd_block_table(w->comp, len, w->blk, nb, &ub);
+    /* record starts: the run's first record, then every linear-index offset inside the run */
+    const int64_t u0 = (int64_t)(r->vbeg & 0xffff);
+    int64_t u_end = ub;
+    if (r->vend != UINT64_MAX && (r->vend & 0xffff) != 0) u_end = w->blk[nb - 1].out_off + (int64_t)(r->vend & 0xffff);
+    const int nl = (r->tid >= 0 && r->tid < s->n_tgt) ? s->n_lin[r->tid] : 0;
+    if (nl + 2 > w->starts_cap) {
+        free(w->starts);
+        w->starts_cap = nl + 64;
+        w->starts = (int64_t *)malloc(sizeof(int64_t) * (size_t)w->starts_cap);
+        if (!w->starts) { w->starts_cap = 0; return -1; }
+    }
+    int64_t ns = 0;
+    w->starts[ns++] = u0;
+    for (int k = 0; k < nl; k++) {
+        const uint64_t v = s->lin[r->tid][k];
+        if (v < r->vbeg || v >= r->vend) continue;
+        const int64_t cb = (int64_t)(v >> 16) - c0;
+        int64_t lo = 0, hi = nb - 1; /* the block starting at cb */
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) / 2;
+            if (w->blk[mid].c_off <= cb) lo = mid;
+            else hi = mid - 1;
+        }
+        if (w->blk[lo].c_off != cb) continue;
+        const int64_t u = w->blk[lo].out_off + (int64_t)(v & 0xffff);
+        if (u > u0 && u < u_end) w->starts[ns++] = u;
+    }
+    qsort(w->starts, (size_t)ns, sizeof(int64_t), cmp_i64);
+    int64_t m = 0;
+    for (int64_t k = 0; k < ns; k++)
+        if (m == 0 || w->starts[k] != w->starts[m - 1]) w->starts[m++] = w->starts[k];
+    int64_t R = 0;
+    const int rc = dd_run_load(w->dd, w->comp, len, w->blk, nb, ub, w->starts, m, u_end, &R, err, errlen);
+    if (rc) return rc;
+    if (r->count >= 0 && R != r->count) {
+        snprintf(err, (size_t)errlen, "target %d: %lld records decoded, the index counts %lld", r->tid, (long long)R,
+                 (long long)r->count);
+        return -2;
+    }
+    pthread_mutex_lock(&s->mu);
+    s->c_records += R;
+    s->c_inflated += ub;
+    s->c_compressed += len;
+    s->c_io_s += t1 - t0;
+    s->c_dec_s += now_s() - t1;
+    pthread_mutex_unlock(&s->mu);
+    w->loaded = ri;
+    w->loaded_R = R;
+    return 0;
+}
+
+/* find_insert_mean's sample, runs in file order until the cap (worker of the
+ * first device) */
+static int dw_stats(dd_worker *w, char *err, int errlen) {
+    pd_session *s = w->s;
+    for (int i = 0; i < s->n_runs && s->s_n < PD_INSERT_CAP && !s->abort; i++) {
+        if (s->runs[i].tid < 0) continue; /* unplaced: unmapped records only */
+        int rc = dw_load(w, i, err, errlen);
+        if (rc) return rc;
+        int64_t taken = 0, m = 0;
+        rc = dd_run_stats(w->dd, s->min_mapq_stats, PD_INSERT_CAP - s->s_n, s->s_ins + s->s_n, s->s_lq + s->s_n, &taken,
+                          &m, err, errlen);
+        if (rc) return rc;
+        s->s_n += taken;
+        s->s_m += m;
+    }
+    mark_stats_done(s);
+    return 0;
+}
+
+/* one processed chromosome: its run parsed into a stage, the split-read
+ * alignments parsed on the host, the walk's trims (chrom_finalize's facts) */
+static int dw_chrom(dd_worker *w, int k, char *err, int errlen) {
+    pd_session *s = w->s;
+    pd_chrom *c = &s->ch[k];
+    if (stage_acquire(s, w->device, k, &c->stage)) { snprintf(err, (size_t)errlen, "no stage"); return -1; }
+    const int ri = c->run;
+    dd_parse_out po;
+    memset(&po, 0, sizeof(po));
+    int64_t j0 = 0;
+    if (ri >= 0) {
+        int rc = (w->loaded == ri) ? 0 : dw_load(w, ri, err, errlen);
+        if (rc) return rc;
+        j0 = s->runs[ri].j0;
+        rc = dd_run_parse(w->dd, j0, s->runs[ri].tid, s->read_name_len, s->plan[k].len, c->stage, &po, err, errlen);
+        if (rc) return rc;
+        w->loaded = -1; /* the parse reuses the load's buffers */
+    } else {
+        grom_stage_sizes sz;
+        grom_reads dv;
+        memset(&sz, 0, sizeof(sz));
+        sz.ref_len = s->plan[k].len;
+        if (grom_stage_fill_begin(c->stage, &sz, &dv) != GROM_OK) { snprintf(err, (size_t)errlen, "%s", grom_last_error()); return -1; }
+    }
+    /* the split-read alignments, parsed as decode_piece parses them */
+    const char *target = s->plan[k].target_name ? s->plan[k].target_name : "";
+    grom_aux *ax = NULL;
+    int64_t *ak = NULL, na = 0;
+    if (po.n_auxc > 0) {
+        ax = (grom_aux *)malloc(sizeof(grom_aux) * (size_t)po.n_auxc);
+        ak = (int64_t *)malloc(sizeof(int64_t) * (size_t)po.n_auxc);
+        if (!ax || !ak) { free(ax); free(ak); return -1; }
+        for (int64_t a = 0; a < po.n_auxc; a++) {
+            const uint8_t *q = po.aux_bytes + po.aux_off[a] + 4;
+            const int32_t bs = (int32_t)(po.aux_off[a + 1] - po.aux_off[a] - 4);
+            bam_rec rv;
+            memset(&rv, 0, sizeof(rv));
+            rv.tid = ldi32(q);
+            rv.pos = ldi32(q + 4);
+            rv.l_qname = q[8];
+            rv.n_cigar = ld16(q + 12);
+            rv.l_qseq = ldi32(q + 16);
+            rv.data = (uint8_t *)q + 32;
+            rv.data_len = bs - 32;
+            if (grom_parse_aux(&rv, target, &ax[na])) ak[na++] = po.aux_kidx[a];
+        }
+    }
+    int rc = 0;
+    if (s->splitread && na > 0 && grom_stage_put_aux(c->stage, ax, ak, na) != GROM_OK) rc = -1;
+    /* the walk's facts: wait for the insert statistics and the final plan */
+    pthread_mutex_lock(&s->mu);
+    while (!s->abort && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
+    const int ab = s->abort;
+    pthread_mutex_unlock(&s->mu);
+    if (ab) { free(ax); free(ak); return -3; }
+    const int32_t s0 = s->index_start;
+    int64_t sk = 0, sd = 0;
+    if (rc == 0 && ri >= 0 && dd_stage_prefix(w->dd, c->stage, s0, &sk, &sd)) rc = -1;
+    /* -S: the first ingested record keeps its SA/XP if it is a kept read */
+    int64_t first_drop_before = -1;
+    if (rc == 0 && !s->splitread && sd < po.n_drop) {
+        grom_reads dv;
+        grom_stage_dev_reads(c->stage, &dv);
+        if (grom_copy_d2h(&first_drop_before, dv.drop_before + sd, sizeof(int64_t), w->device)) rc = -1;
+    }
+    if (rc == 0 && ri >= 0 && grom_stage_trim_drops(c->stage, sd, sk) != GROM_OK) rc = -1;
+    if (rc == 0 && grom_stage_trim(c->stage, sk) != GROM_OK) rc = -1;
+    const int any = (po.n_kept + po.n_drop) > (sk + sd);
+    pd_chrom_facts *f = &c->facts;
+    memset(f, 0, sizeof(*f));
+    f->n_skip = (int32_t)(sk + sd);
+    f->n_reads = po.n_kept - sk;
+    f->n_drop = po.n_drop - sd;
+    if (any) {
+        const int32_t p = po.last_pos - s->overlap_mult * s->insert_max;
+        f->p_last = p > s0 ? p : s0;
+    } else {
+        f->p_last = -1;
+    }
+    const int64_t n_seen = ri >= 0 ? po.n_rec - j0 : 0;
+    if (n_seen > 0 && s->runs[ri].has_next) f->lseq_tail = s->runs[ri].next_lq;
+    else if (any) f->lseq_tail = po.last_lq + (po.last_kept ? po.last_hclip : 0);
+    else f->lseq_tail = 0;
+    if (rc == 0 && !s->splitread && any) {
+        const int first_is_drop = sd < po.n_drop && first_drop_before == sk;
+        if (!first_is_drop)
+            for (int64_t a = 0; a < na; a++)
+                if (ak[a] == sk) {
+                    if (grom_stage_patch_aux(c->stage, sk, &ax[a]) != GROM_OK) rc = -1;
+                    break;
+                }
+    }
+    free(ax);
+    free(ak);
+    pthread_mutex_lock(&s->mu);
+    s->c_h2d += 0;
+    pthread_mutex_unlock(&s->mu);
+    return rc;
+}
+
+static void *dw_main(void *arg) {
+    dd_worker *w = (dd_worker *)arg;
+    pd_session *s = w->s;
+    char err[300] = "";
+    int rc = 0;
+    w->dd = dd_ctx_new(w->device);
+    if (!w->dd) { rc = -1; snprintf(err, sizeof(err), "device decode: no context on device %d", w->device); }
+    if (rc == 0 && w->first) rc = dw_stats(w, err, (int)sizeof(err));
+    /* the final plan (which chromosomes, which records each one's run starts with) */
+    if (rc == 0) {
+        pthread_mutex_lock(&s->mu);
+        while (!s->abort && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
+        pthread_mutex_unlock(&s->mu);
+        if (!s->abort) {
+            pthread_mutex_lock(&s->mu);
+            const int need = !s->final_applied;
+            pthread_mutex_unlock(&s->mu);
+            if (need) apply_final(s, 0);
+        }
+    }
+    for (int k = 0; rc == 0 && k < s->n_plan && !s->abort; k++) {
+        pd_chrom *c = &s->ch[k];
+        if (!s->keep[k] || !s->want[k] || c->device != w->device) continue;
+        const double t0 = now_s();
+        pd_trace(s, PD_EV_UPLOAD, k, 0);
+        rc = dw_chrom(w, k, err, (int)sizeof(err));
+        pd_trace(s, PD_EV_UPLOAD, k, 1);
+        pthread_mutex_lock(&s->mu);
+        s->c_upl_s += now_s() - t0;
+        c->rc = rc;
+        c->final = 1;
+        c->begun = 1;
+        pd_trace(s, PD_EV_FINAL, k, 0);
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+    }
+    if (rc == -2 || rc == -1) sess_abort(s, rc == -2, err);
+    if (w->dd) {
+        double ms[3];
+        dd_ctx_times(w->dd, ms);
+        pthread_mutex_lock(&s->mu);
+        for (int q = 0; q < 3; q++) s->c_gpu_ms[q] += ms[q];
+        pthread_mutex_unlock(&s->mu);
+    }
+    /* the scans may still read the stages; the decode context goes now */
+    dd_ctx_free(w->dd);
+    grom_pinned_free(w->comp);
+    free(w->blk);
+    free(w->starts);
+    free(w);
+    return NULL;
+}
+
+static int pd_start_device(pd_session *s) {
+    int devs[64], nd = 0;
+    for (int k = 0; k < s->n_plan; k++) {
+        int seen = 0;
+        for (int q = 0; q < nd; q++) seen |= devs[q] == s->ch[k].device;
+        if (!seen && nd < 64) devs[nd++] = s->ch[k].device;
+    }
+    if (nd == 0) devs[nd++] = 0;
+    const char *it = getenv("GROM_DECODE_THREADS");
+    s->io_threads = it && atoi(it) > 0 ? atoi(it) / nd : 8;
+    if (s->io_threads < 1) s->io_threads = 1;
+    if (s->io_threads > 16) s->io_threads = 16;
+    s->dw = (pthread_t *)calloc((size_t)nd, sizeof(pthread_t));
+    for (int q = 0; q < nd; q++) {
+        dd_worker *w = (dd_worker *)calloc(1, sizeof(dd_worker));
+        w->s = s;
+        w->device = devs[q];
+        w->first = q == 0;
+        w->loaded = -1;
+        if (pthread_create(&s->dw[q], NULL, dw_main, w) != 0) {
+            free(w);
+            sess_abort(s, 0, "cannot start device decode workers");
+            return -1;
+        }
+        s->dw_started = q + 1;
+    }
+    s->n_threads = 0;
+    return 0;
+}
+
 int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan_only) {
     s->min_mapq_stats = min_mapq;
     s->plan_only = plan_only;
@@ -2004,6 +2391,7 @@ int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan
     s->no_mirror = plan_only && getenv("GROM_DECODE_ONLY") != NULL; /* time the decode alone */
     s->n_dev = n_dev < 1 ? 1 : n_dev;
     for (int k = 0; k < s->n_plan; k++) s->ch[k].device = dev_of ? dev_of[k] : 0;
+    if (!plan_only && s->dev_mode) return pd_start_device(s);
     s->thr = (pthread_t *)calloc((size_t)s->n_threads, sizeof(pthread_t));
     for (int t = 0; t < s->n_threads; t++)
         if (pthread_create(&s->thr[t], NULL, decoder_main, s) != 0) {
@@ -2115,6 +2503,8 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
     c->decode_thread_s = s->c_dec_s;
     c->h2d_bytes = s->c_h2d;
     c->inflate_s = s->c_inflate_s;
+    c->device = s->dev_mode;
+    for (int q = 0; q < 3; q++) c->gpu_ms[q] = s->c_gpu_ms[q];
     c->io_s = s->c_io_s;
     c->upload_s = s->c_upl_s;
     c->wait_s = s->c_wait_s;
@@ -2149,6 +2539,7 @@ void pd_close(pd_session *s) {
     pthread_mutex_unlock(&s->mu);
     for (int t = 0; t < s->n_threads && s->thr; t++) pthread_join(s->thr[t], NULL);
     if (s->upl_started) pthread_join(s->upl, NULL);
+    for (int t = 0; t < s->dw_started; t++) pthread_join(s->dw[t], NULL);
     /* buffers: wait for their copies, then free */
     while (s->inflight_head) {
         pd_buf *b = s->inflight_head;
@@ -2173,6 +2564,10 @@ void pd_close(pd_session *s) {
         free(s->ch[k].lowpos);
         free(s->ch[k].saux);
     }
+    for (int t = 0; t < s->n_tgt && s->lin; t++) free(s->lin[t]);
+    free(s->lin);
+    free(s->n_lin);
+    free(s->dw);
     free(s->T.e);
     free(s->T.arena);
     free(s->T.ht);

@@ -43,6 +43,7 @@ typedef struct pd_session pd_session;
 typedef struct pd_chrom_in {
     int32_t tid;             /* BAM target (-1: none) */
     const char *target_name; /* the SA/XP chromosome test's name (GROM.c:1894-1961) */
+    int64_t len;             /* its reference length (device mode reserves the stage's room for it) */
 } pd_chrom_in;
 
 /* what the serial stream gives one chromosome (grom_chrom's stream facts) */
@@ -63,6 +64,10 @@ pd_session *pd_open(const char *bam_path, const bam_hdr *hdr, const pd_chrom_in 
  * others keep their place in the serial stream's plan (their records still
  * decide Q1/Q21 for the rest) but are skipped */
 void pd_set_wanted(pd_session *s, const int *want);
+/* before pd_start: decode on the GPUs (ddecode.hip: each device's worker
+ * reads its chromosomes' compressed runs, inflates and parses them into the
+ * stages) instead of the host decoder threads; same results, same API */
+void pd_set_device_mode(pd_session *s, int on);
 /* start the decoder threads and the uploader.  dev_of[k]: the GPU of plan
  * chromosome k.  plan_only: no device; chromosomes go to host mirrors. */
 int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan_only);
@@ -93,6 +98,8 @@ typedef struct pd_counters {
     int64_t records, pieces, inflated_bytes, compressed_bytes, h2d_bytes;
     double decode_thread_s, inflate_s, upload_s, wait_s, io_s;
     int threads, libdeflate;
+    int device;          /* runs decoded on the GPU (device mode) */
+    double gpu_ms[3];    /* device mode: inflate, record walk, parse (HIP events, summed) */
 } pd_counters;
 void pd_get_counters(pd_session *s, pd_counters *c);
 void pd_close(pd_session *s);

@@ -35,6 +35,7 @@
 
 #include "../../include/grom_amd.h"
 #include "cnv.h"
+#include "ddecode.h"
 #include "sv.h"
 #include "scan_common.h"
 #include "snvfmt.h"
@@ -1356,6 +1357,130 @@ int grom_stage_patch_aux(grom_stage *s, int64_t read_index, const grom_aux *aux)
     HIPCHK(hipMemcpyAsync(s->a(SA_AIDX) + 4 * read_index, &s->patch_idx, 4, hipMemcpyHostToDevice, s->st));
     HIPCHK(hipStreamSynchronize(s->st));
     s->n_aux++;
+    return GROM_OK;
+}
+
+// ---- device-side fills (ddecode.hip: the BAM decoded on the GPU) ----
+__global__ void k_stage_aux_idx(int32_t *aidx, const int64_t *kidx, int64_t n, int32_t first) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        aidx[kidx[k]] = first + (int32_t)k;
+}
+
+__global__ void k_stage_trim_drops(int32_t *dpos, int32_t *dlq, int64_t *dbef, const int32_t *spos, const int32_t *slq,
+                                   const int64_t *sbef, int64_t n, int64_t sk) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        dpos[k] = spos[k];
+        dlq[k] = slq[k];
+        dbef[k] = sbef[k] >= sk ? sbef[k] - sk : 0;
+    }
+}
+
+static void stage_dev_view(grom_stage *s, grom_reads *d) {
+    memset(d, 0, sizeof(*d));
+    d->n = s->n;
+    d->n_cigar_ops = s->n_cig;
+    d->n_bases = s->n_bases;
+    d->pos = (const int32_t *)s->a(SA_POS);
+    d->flag = (const uint16_t *)s->a(SA_FLAG);
+    d->mapq = (const uint8_t *)s->a(SA_MAPQ);
+    d->mtid = (const int32_t *)s->a(SA_MTID);
+    d->mpos = (const int32_t *)s->a(SA_MPOS);
+    d->isize = (const int32_t *)s->a(SA_ISIZE);
+    d->l_qseq = (const int32_t *)s->a(SA_LQ);
+    d->cigar_off = (const uint32_t *)s->a(SA_COFF);
+    d->cigar = (const uint32_t *)s->a(SA_CIG);
+    d->base_off = (const int64_t *)s->a(SA_BOFF);
+    d->seq = (const uint8_t *)s->a(SA_SEQ);
+    d->qual = (const uint8_t *)s->a(SA_QUAL);
+    d->name_id = (const uint32_t *)s->a(SA_NID);
+    d->n_aux = s->n_aux;
+    d->aux_idx = (const int32_t *)s->a(SA_AIDX);
+    d->aux = (const grom_aux *)s->a(SA_AUX);
+    d->n_drop = s->n_drop;
+    d->drop_pos = (const int32_t *)s->a(SA_DPOS);
+    d->drop_lq = (const int32_t *)s->a(SA_DLQ);
+    d->drop_before = (const int64_t *)s->a(SA_DBEF);
+}
+
+int grom_stage_fill_begin(grom_stage *s, const grom_stage_sizes *sz, grom_reads *dev) {
+    if (!s || !sz || !dev) { set_err("grom_stage_fill_begin: null argument"); return GROM_E_ARG; }
+    int rc = grom_stage_begin(s, nullptr);
+    if (rc) return rc;
+    grom_stage want = {};
+    want.n = sz->n;
+    want.n_cig = sz->n_cigar_ops;
+    want.n_bases = sz->n_bases;
+    want.n_aux = sz->n_aux;
+    want.n_drop = sz->n_drop;
+    want.ref_len = std::max<int64_t>(sz->ref_len, 16);
+    size_t need[SA_N], keep[SA_N] = {};
+    stage_used(&want, need);
+    need[SA_AUX] += sizeof(grom_aux);  // the -S patch
+    if ((rc = stage_reserve(s, need, keep))) return rc;
+    s->n = sz->n;
+    s->n_cig = sz->n_cigar_ops;
+    s->n_bases = sz->n_bases;
+    s->n_aux = 0;
+    s->n_drop = sz->n_drop;
+    s->bytes_h2d = 0;
+    stage_dev_view(s, dev);
+    return GROM_OK;
+}
+
+int grom_stage_put_aux(grom_stage *s, const grom_aux *aux, const int64_t *kidx, int64_t n) {
+    if (!s || n < 0 || (n > 0 && (!aux || !kidx))) { set_err("grom_stage_put_aux: bad argument"); return GROM_E_ARG; }
+    if (n == 0) return GROM_OK;
+    HIPCHK(hipSetDevice(s->device));
+    size_t need[SA_N], keep[SA_N];
+    stage_used(s, keep);
+    stage_used(s, need);
+    need[SA_AUX] = sizeof(grom_aux) * (size_t)(s->n_aux + n + 1);
+    int rc = stage_reserve(s, need, keep);
+    if (rc) return rc;
+    int64_t *d_k = nullptr;
+    HIPCHK(hipMalloc((void **)&d_k, sizeof(int64_t) * (size_t)n));
+    HIPCHK(hipMemcpyAsync(s->a(SA_AUX) + sizeof(grom_aux) * s->n_aux, aux, sizeof(grom_aux) * (size_t)n,
+                          hipMemcpyHostToDevice, s->st));
+    HIPCHK(hipMemcpyAsync(d_k, kidx, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, s->st));
+    hipLaunchKernelGGL(k_stage_aux_idx, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s->st,
+                       (int32_t *)s->a(SA_AIDX), d_k, n, (int32_t)s->n_aux);
+    HIPCHK(hipStreamSynchronize(s->st));
+    (void)hipFree(d_k);
+    s->n_aux += n;
+    return GROM_OK;
+}
+
+int grom_stage_trim_drops(grom_stage *s, int64_t sd, int64_t sk) {
+    if (!s || sd < 0 || sd > s->n_drop || sk < 0) { set_err("grom_stage_trim_drops: bad argument"); return GROM_E_ARG; }
+    HIPCHK(hipSetDevice(s->device));
+    const int64_t n = s->n_drop - sd;
+    if (n > 0) {
+        // through a scratch copy: the source and destination ranges overlap
+        char *tmp = nullptr;
+        HIPCHK(hipMalloc((void **)&tmp, 16 * (size_t)n));
+        int32_t *tp = (int32_t *)tmp, *tl = tp + n;
+        int64_t *tb = (int64_t *)(tmp + 8 * (size_t)n);
+        HIPCHK(hipMemcpyAsync(tp, (int32_t *)s->a(SA_DPOS) + sd, 4 * (size_t)n, hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(tl, (int32_t *)s->a(SA_DLQ) + sd, 4 * (size_t)n, hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(tb, (int64_t *)s->a(SA_DBEF) + sd, 8 * (size_t)n, hipMemcpyDeviceToDevice, s->st));
+        hipLaunchKernelGGL(k_stage_trim_drops, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                           s->st, (int32_t *)s->a(SA_DPOS), (int32_t *)s->a(SA_DLQ), (int64_t *)s->a(SA_DBEF), tp, tl,
+                           tb, n, sk);
+        HIPCHK(hipStreamSynchronize(s->st));
+        (void)hipFree(tmp);
+    }
+    s->n_drop = n;
+    return GROM_OK;
+}
+
+int grom_copy_d2h(void *dst, const void *src, size_t n, int device) {
+    if (hipSetDevice(device) != hipSuccess) return -1;
+    return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+
+int grom_stage_dev_reads(grom_stage *s, grom_reads *dev) {
+    if (!s || !dev) { set_err("grom_stage_dev_reads: null argument"); return GROM_E_ARG; }
+    stage_dev_view(s, dev);
     return GROM_OK;
 }
 

@@ -670,3 +670,32 @@ def test_device_inflate_matches_zlib(datadir, tmp_path):
         ms, nb, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
         bad = f(path.encode(), 0, 0, 1, ctypes.byref(ms), ctypes.byref(nb), ctypes.byref(by))
         assert bad == 0 and nb.value > 10, (path, bad, nb.value)
+
+
+@pytest.mark.parametrize("case,extra", [("three_chr", []), ("sv", ["-S"]), ("sv", []), ("dups", ["-M"]),
+                                        ("empty_middle", []), ("c3_genome", ["-M", "-V", "1"]), ("indels", []),
+                                        ("c5_tetra_male", ["-p", "4", "-g", "1"]), ("lowmapq_clip", [])],
+                         ids=["three_chr", "sv_S", "sv", "dups_M", "empty_middle", "c3_genome", "indels", "c5",
+                              "lowmapq_clip"])
+def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
+    """BAM decode on the GPU (ddecode.hip: the runs inflated, walked and
+    parsed on the device; the CLI's default) stages, for every chromosome,
+    exactly the input the host decoder threads (pdecode.c) stage: same stream
+    facts and the same digest of every array, CIGAR/base/quality/SA-XP
+    content, dropped record and name-id relation; and the outputs are the
+    oracle's."""
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"dd_{case}{''.join(extra).replace('-', '_')}"
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    lines = {}
+    for mode in ("0", "1"):
+        capfd.readouterr()
+        run_grom(datadir, bam, fa, f"g{mode}_{tag}.vcf", extra,
+                 env_extra={"GROM_DEVICE_DECODE": mode, "GROM_STAGE_DIGEST": "1", "GROM_VERBOSE": "1"})
+        out = capfd.readouterr().out
+        assert ("device decode:" in out) == (mode == "1"), out[-1500:]
+        lines[mode] = sorted(l for l in out.splitlines() if l.startswith("stage "))
+    assert lines["1"] and lines["0"] == lines["1"], (lines["0"], lines["1"])
+    for mode in ("0", "1"):
+        for ext in (".vcf", ".ctx.vcf"):
+            assert open(datadir / f"o_{tag}{ext}").read() == open(datadir / f"g{mode}_{tag}{ext}").read(), (mode, ext)
