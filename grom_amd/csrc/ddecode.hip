@@ -26,11 +26,11 @@
 __global__ void __launch_bounds__(DD_LANES) k_inflate(const uint8_t *__restrict__ comp, const DdBlock *__restrict__ blk,
                                                       int64_t n_blk, uint8_t *__restrict__ out,
                                                       uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad) {
-    extern __shared__ uint16_t dd_sym[];  // GI_LANE_BYTES x DD_LANES: rows element-major across the lanes
+    extern __shared__ uint32_t dd_tab[];  // GI_LANE_DWORDS x DD_LANES: rows element-major across the lanes
     const int64_t j = (int64_t)blockIdx.x * DD_LANES + threadIdx.x;
     if (j >= n_blk) return;
     const DdBlock b = blk[j];
-    const int rc = gi_inflate<DD_LANES>(comp + b.in_off, b.in_len, out + b.out_off, b.out_len, dd_sym, threadIdx.x);
+    const int rc = gi_inflate<DD_LANES>(comp + b.in_off, b.in_len, out + b.out_off, b.out_len, dd_tab, threadIdx.x);
     status[j] = (uint8_t)rc;
     if (rc) atomicAdd(n_bad, 1u);
 }

@@ -7,14 +7,31 @@
 // with their own Huffman trees, so a chromosome's 10^4-10^5 blocks fill the
 // chip without any cross-lane work.
 //
+// The decoder is a flat state machine that takes one bounded STEP per loop
+// trip -- a block header, or one symbol plus at most 16 bytes of a match --
+// so the 64 lanes of a wave, each in its own block, stay in step: no lane
+// waits for another's long match or for the end of another's DEFLATE block
+// (a nested per-block/per-match loop makes the whole wave wait for its
+// slowest lane at every level).  A match step is one 16-byte load and one
+// 16-byte store (unaligned dwordx4): the bytes past the match's end that the
+// store also writes are garbage that this lane overwrites later, since a
+// block's output is produced front to back; near the end of the block's
+// output the step falls back to single bytes.  A match whose distance is
+// below 16 copies its first distance bytes, then doubles the distance (the
+// output is periodic with the distance, so any multiple of it is a valid
+// source): 1, 2, 4, 8, 16, 16, ... bytes per step for a run of one byte.
+//
 // Per lane, the Huffman tables are canonical: for each code length l the
 // left-justified end of its code range (lim[l]) and the offset from a code to
 // its symbol's index in the sorted-symbol array (base[l]) sit in registers;
 // the length of the code at the stream's front is the number of lim[l] at or
 // below the next 15 bits (bit-reversed), found by one unrolled compare chain,
-// and only the sorted symbols live in LDS (element-major across the lanes, so
-// any per-lane index is bank-conflict free).  No table of 2^n entries per
-// block: the 64 blocks of a wave need 43 KiB of LDS in all.
+// and only the sorted symbols live in LDS, one byte each (plus a bit per
+// literal/length entry for symbols >= 256), interleaved across the lanes a
+// dword at a time so any per-lane index is bank-conflict free.  A dynamic
+// header's run-length-coded code lengths are decoded twice -- once to count
+// the lengths, once to place the symbols -- so they need no storage.  376
+// bytes of LDS per lane: 6 waves of 64 blocks per CU.
 //
 // The same code is compiled for the host (LANES = 1, plain arrays) as the
 // library's test twin (grom_inflate_selftest), checked against zlib on the CPU.
@@ -34,18 +51,18 @@
 #define GI_UNROLL _Pragma("GCC unroll 16")
 #endif
 
-// sorted-symbol rows per lane: literal/length (288), distance (32), code-length (19)
-#define GI_ROW_LIT 0
-#define GI_ROW_DIST 288
-#define GI_ROW_CL 320
-#define GI_ROWS 339
-// 4-bit code-length cells of a dynamic block's 286 + 30 symbols, after the rows
-#define GI_NIB_ROWS 160
-// storage per lane (bytes): the symbol rows (uint16) and the length cells
-#define GI_LANE_BYTES (GI_ROWS * 2 + GI_NIB_ROWS)
+// sorted-symbol tables per lane, in dwords of 4 one-byte cells: literal/length
+// (288 cells), its >= 256 bitmap (288 bits), distance (32), code-length (19)
+#define GI_T_LIT 0
+#define GI_T_LITHI 72
+#define GI_T_DIST 81
+#define GI_T_CL 89
+#define GI_LANE_DWORDS 94
+#define GI_LANE_BYTES (GI_LANE_DWORDS * 4)
 
 enum { GI_OK = 0, GI_E_HEADER = 1, GI_E_TREE = 2, GI_E_CODE = 3, GI_E_DIST = 4, GI_E_OVERRUN = 5, GI_E_INPUT = 6,
        GI_E_SIZE = 7 };
+enum { GI_M_HDR = 0, GI_M_SYM = 1, GI_M_COPY = 2, GI_M_STORED = 3, GI_M_DONE = 4 };
 
 GI_FN uint32_t gi_rev15(uint32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -115,77 +132,114 @@ GI_FN uint32_t gi_bits(GiBits &b, int n) {  // n <= 32, after a refill that cove
     return v;
 }
 
-// a canonical Huffman code: code lengths 1..15
-struct GiHuff {
-    uint32_t lim[16];  // lim[l]: left-justified (15-bit) end of the codes of length <= l
-    int32_t base[16];  // symbol index of a length-l code c: base[l] + c
-};
+// cell r of the table at dword t0 in the lane's column
+template <int LANES>
+GI_FN uint8_t *gi_cell(uint32_t *tab, int t0, int r, int lane) {
+    return (uint8_t *)(tab + (t0 + (r >> 2)) * LANES + lane) + (r & 3);
+}
 
-// Build from n code lengths (len[i] for symbol i, read through `get`): the
-// sorted symbols go to rows row0.. of the lane's column.  Returns GI_OK, or
-// GI_E_TREE for an over-subscribed set.  allow_incomplete: DEFLATE permits an
-// incomplete distance tree (a single code) -- any code outside the tree fails
-// at decode time.
-template <int LANES, class Get>
-GI_FN int gi_build(GiHuff &h, uint16_t *sym, int lane, int row0, int n, Get get) {
-    uint32_t cnt[16];
-GI_UNROLL
-    for (int l = 0; l < 16; l++) cnt[l] = 0;
-    for (int i = 0; i < n; i++) {
-        const uint32_t L = get(i);
-GI_UNROLL
-        for (int l = 1; l < 16; l++) cnt[l] += (L == (uint32_t)l) ? 1u : 0u;
-    }
-    // Kraft check, first codes, offsets
+// A canonical Huffman code with code lengths 1..N, one register per length:
+// e[l] = lim[l] << 16 | (uint16)base[l], where lim[l] is the left-justified
+// (15-bit) end of the codes of length <= l and a length-l code c is the
+// symbol at sorted index base[l] + c.  With the bit-reversed next 15 bits
+// `rev`, key = rev << 16 | 0xffff is >= e[l] exactly when rev >= lim[l], so
+// one unsigned compare per length finds the code length.
+template <int N>
+struct GiHuffT {
+    uint32_t e[N + 1];
+};
+typedef GiHuffT<15> GiHuff;   // literal/length and distance codes
+typedef GiHuffT<7> GiHuffCL;  // the code-length code
+
+// Kraft check and the code's entries from its length counts, the 16-bit field
+// at bit `sh` of cnt[l] (l = 1..N), which then becomes the first sorted index
+// of the length-l symbols.  GI_E_TREE for an over-subscribed set (DEFLATE
+// permits an incomplete one: a code outside the tree fails at decode time).
+template <int N>
+GI_FN int gi_code(GiHuffT<N> &h, uint32_t *cnt, int sh) {
     int32_t left = 1;
-    uint32_t code = 0, off = 0, off_l[16];
+    uint32_t code = 0, off = 0;
 GI_UNROLL
-    for (int l = 1; l < 16; l++) {
-        left = (left << 1) - (int32_t)cnt[l];
+    for (int l = 1; l <= N; l++) {
+        const uint32_t c = (cnt[l] >> sh) & 0xffffu;
+        left = (left << 1) - (int32_t)c;
         if (left < 0) return GI_E_TREE;
-        off_l[l] = off;
-        h.base[l] = (int32_t)off - (int32_t)code;
-        code += cnt[l];
-        h.lim[l] = code << (15 - l);
-        off += cnt[l];
-        code <<= 1;
+        cnt[l] = (cnt[l] & ~(0xffffu << sh)) | (off << sh);
+        h.e[l] = (((code + c) << (15 - l)) << 16) | ((off - code) & 0xffffu);
+        code = (code + c) << 1;
+        off += c;
     }
-    h.base[0] = 0;
-    h.lim[0] = 0;
-    // place the symbols in code order (stable in symbol order)
+    h.e[0] = 0;
+    return GI_OK;
+}
+
+// symbol i of code length L (1..N) into its sorted cell (stable in symbol
+// order); the 16-bit fields at bit `sh` of off[] are the next free indices
+template <int LANES, int N, bool HI>
+GI_FN void gi_place(uint32_t *tab, int t0, int lane, uint32_t *off, int sh, uint32_t L, int i) {
+    uint32_t o = 0;
+GI_UNROLL
+    for (int l = 1; l <= N; l++) {
+        o = (L == (uint32_t)l) ? off[l] : o;
+        off[l] += (L == (uint32_t)l) ? (1u << sh) : 0u;
+    }
+    o = (o >> sh) & 0xffffu;
+    *gi_cell<LANES>(tab, t0, (int)o, lane) = (uint8_t)i;
+    if (HI && i >= 256) tab[(GI_T_LITHI + (int)(o >> 5)) * LANES + lane] |= 1u << (o & 31);
+}
+
+template <int LANES, bool HI>
+GI_FN void gi_clear_hi(uint32_t *tab, int lane) {
+    if (HI) {
+GI_UNROLL
+        for (int w = 0; w < 9; w++) tab[(GI_T_LITHI + w) * LANES + lane] = 0;
+    }
+}
+
+// Build from n code lengths (len[i] for symbol i, read through `get`)
+template <int LANES, int N, bool HI, class Get>
+GI_FN int gi_build(GiHuffT<N> &h, uint32_t *tab, int lane, int t0, int n, Get get) {
+    uint32_t cnt[N + 1];
+GI_UNROLL
+    for (int l = 0; l <= N; l++) cnt[l] = 0;
     for (int i = 0; i < n; i++) {
         const uint32_t L = get(i);
-        uint32_t o = 0;
 GI_UNROLL
-        for (int l = 1; l < 16; l++) {
-            o = (L == (uint32_t)l) ? off_l[l] : o;
-            off_l[l] += (L == (uint32_t)l) ? 1u : 0u;
-        }
-        if (L) sym[(row0 + (int)o) * LANES + lane] = (uint16_t)i;
+        for (int l = 1; l <= N; l++) cnt[l] += (L == (uint32_t)l) ? 1u : 0u;
+    }
+    const int rc = gi_code<N>(h, cnt, 0);
+    if (rc) return rc;
+    gi_clear_hi<LANES, HI>(tab, lane);
+    for (int i = 0; i < n; i++) {
+        const uint32_t L = get(i);
+        if (L) gi_place<LANES, N, HI>(tab, t0, lane, cnt, 0, L, i);
     }
     return GI_OK;
 }
 
 // decode one symbol; -1 for a code outside the tree
-template <int LANES>
-GI_FN int gi_decode(GiBits &b, const GiHuff &h, const uint16_t *sym, int lane, int row0) {
+template <int LANES, int N, bool HI>
+GI_FN int gi_decode(GiBits &b, const GiHuffT<N> &h, const uint32_t *tab, int lane, int t0) {
     const uint32_t rev = gi_rev15((uint32_t)b.buf);
+    const uint32_t key = rev << 16 | 0xffffu;
     int L = 1;
-    int32_t bs = h.base[1];
+    uint32_t bs = h.e[1];
 GI_UNROLL
-    for (int l = 1; l < 15; l++) {
-        const bool ge = rev >= h.lim[l];
+    for (int l = 1; l < N; l++) {
+        const bool ge = key >= h.e[l];
         L += ge ? 1 : 0;
-        bs = ge ? h.base[l + 1] : bs;
+        bs = ge ? h.e[l + 1] : bs;
         // keep the chain of selects (the compiler would otherwise fold it into
-        // base[L], a dynamic index that moves the tables to scratch memory)
+        // e[L], a dynamic index that moves the table to scratch memory)
         GI_KEEP(bs);
     }
-    if (rev >= h.lim[15]) return -1;
-    const int idx = bs + (int)(rev >> (15 - L));
+    if (key >= h.e[N]) return -1;
+    const int idx = (int)(int16_t)(uint16_t)bs + (int)(rev >> (15 - L));
     b.buf >>= L;
     b.cnt -= L;
-    return sym[(row0 + idx) * LANES + lane];
+    int s = *gi_cell<LANES>((uint32_t *)tab, t0, idx, lane);
+    if (HI) s |= (int)((tab[(GI_T_LITHI + (idx >> 5)) * LANES + lane] >> (idx & 31)) & 1u) << 8;
+    return s;
 }
 
 // the RFC 1951 length / distance bases, computed (no tables)
@@ -199,158 +253,208 @@ GI_FN void gi_dist_code(int d, int &base, int &extra) {  // d = 0..29
     else { extra = (d >> 1) - 1; base = ((2 + (d & 1)) << extra) + 1; }
 }
 
-// Inflate one block's raw DEFLATE data (in[0..in_len)) into out[0..out_len).
-// `sym` is the LDS (device) or local (host) sorted-symbol storage of GI_ROWS
-// rows x LANES columns.  Every output byte is written exactly once.
+// one repeat item of the code-length code: its value and repeat count, or -1
+GI_FN int gi_cl_item(GiBits &b, int s, int prev, int &val) {
+    if (s < 16) { val = s; return 1; }
+    if (s == 16) { val = prev; return prev < 0 ? -1 : 3 + (int)gi_bits(b, 2); }
+    val = 0;
+    return s == 17 ? 3 + (int)gi_bits(b, 3) : 11 + (int)gi_bits(b, 7);
+}
+
+// A block header (after a refill): the next mode (GI_M_SYM with lit/dist
+// built, or GI_M_STORED with *rem bytes), or -GI_E_*.
 template <int LANES>
-GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len, uint16_t *sym, int lane) {
+GI_FN int gi_header(GiBits &b, GiHuff &lit, GiHuff &dist, uint32_t *tab, int lane, uint32_t &bfinal, uint32_t &rem) {
+    const uint32_t hdr = gi_bits(b, 3);
+    bfinal = hdr & 1;
+    const uint32_t btype = hdr >> 1;
+    if (btype == 0) {  // stored: to the byte boundary, LEN, NLEN, bytes
+        gi_bits(b, b.cnt & 7);
+        gi_refill(b);
+        const uint32_t len = gi_bits(b, 16);
+        gi_refill(b);
+        const uint32_t nlen = gi_bits(b, 16);
+        if ((len ^ 0xffffu) != nlen) return -GI_E_HEADER;
+        rem = len;
+        return len ? GI_M_STORED : (bfinal ? GI_M_DONE : GI_M_HDR);
+    }
+    if (btype == 1) {  // fixed codes
+        int rc = gi_build<LANES, 15, true>(lit, tab, lane, GI_T_LIT, 288, [](int i) -> uint32_t {
+            return i < 144 ? 8u : (i < 256 ? 9u : (i < 280 ? 7u : 8u));
+        });
+        if (rc) return -rc;
+        rc = gi_build<LANES, 15, false>(dist, tab, lane, GI_T_DIST, 30, [](int) -> uint32_t { return 5u; });
+        return rc ? -rc : GI_M_SYM;
+    }
+    if (btype != 2) return -GI_E_HEADER;
+    // dynamic codes
+    const int nlit = (int)gi_bits(b, 5) + 257;
+    const int ndist = (int)gi_bits(b, 5) + 1;
+    const int ncl = (int)gi_bits(b, 4) + 4;
+    if (nlit > 286 || ndist > 30) return -GI_E_HEADER;
+    // code-length code lengths, 3 bits each in the order
+    // 16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15 (5 bits per entry in two
+    // words), packed 3 bits per symbol
+    const uint64_t ord_lo = 16ull | 17ull << 5 | 18ull << 10 | 0ull << 15 | 8ull << 20 | 7ull << 25 | 9ull << 30 |
+                            6ull << 35 | 10ull << 40 | 5ull << 45 | 11ull << 50 | 4ull << 55;
+    const uint64_t ord_hi = 12ull | 3ull << 5 | 13ull << 10 | 2ull << 15 | 14ull << 20 | 1ull << 25 | 15ull << 30;
+    uint64_t cl = 0;
+    for (int k = 0; k < ncl; k++) {
+        gi_refill(b);
+        const uint32_t v = gi_bits(b, 3);
+        const int s = (int)((k < 12 ? ord_lo >> (5 * k) : ord_hi >> (5 * (k - 12))) & 31u);
+        cl |= (uint64_t)v << (3 * s);
+    }
+    GiHuffCL clh;
+    int rc = gi_build<LANES, 7, false>(clh, tab, lane, GI_T_CL, 19,
+                                       [cl](int i) -> uint32_t { return (uint32_t)(cl >> (3 * i)) & 7u; });
+    if (rc) return -rc;
+    // the literal/length and distance code lengths, run-length coded: counted
+    // in a first pass (literal/length counts in the low, distance counts in
+    // the high 16 bits of cn[l]), then decoded again to place the symbols
+    const int ntot = nlit + ndist;
+    const GiBits at = b;
+    uint32_t cn[16];
+GI_UNROLL
+    for (int l = 0; l < 16; l++) cn[l] = 0;
+    int n = 0, prev = -1;
+    bool eob = false;
+    while (n < ntot) {
+        gi_refill(b);
+        const int s = gi_decode<LANES, 7, false>(b, clh, tab, lane, GI_T_CL);
+        if (s < 0) return -GI_E_TREE;
+        int val;
+        const int rep = gi_cl_item(b, s, prev, val);
+        if (rep < 0 || n + rep > ntot) return -GI_E_TREE;
+        int rl = nlit - n;
+        rl = rl < 0 ? 0 : (rl > rep ? rep : rl);
+        const uint32_t add = (uint32_t)rl | (uint32_t)(rep - rl) << 16;
+GI_UNROLL
+        for (int l = 1; l < 16; l++) cn[l] += (val == l) ? add : 0u;
+        if (val && n <= 256 && 256 < n + rep) eob = true;
+        n += rep;
+        prev = val;
+    }
+    if (!eob) return -GI_E_TREE;  // no end-of-block code (zlib refuses it too)
+    rc = gi_code<15>(lit, cn, 0);
+    if (rc) return -rc;
+    rc = gi_code<15>(dist, cn, 16);
+    if (rc) return -rc;
+    gi_clear_hi<LANES, true>(tab, lane);
+    b = at;
+    n = 0;
+    prev = -1;
+    while (n < ntot) {
+        gi_refill(b);
+        const int s = gi_decode<LANES, 7, false>(b, clh, tab, lane, GI_T_CL);
+        int val;
+        const int rep = gi_cl_item(b, s, prev, val);
+        if (val) {
+            for (int k = 0; k < rep; k++) {
+                const int i = n + k;
+                if (i < nlit) gi_place<LANES, 15, true>(tab, GI_T_LIT, lane, cn, 0, (uint32_t)val, i);
+                else gi_place<LANES, 15, false>(tab, GI_T_DIST, lane, cn, 16, (uint32_t)val, i - nlit);
+            }
+        }
+        n += rep;
+        prev = val;
+    }
+    return GI_M_SYM;
+}
+
+// Inflate one block's raw DEFLATE data (in[0..in_len)) into out[0..out_len).
+// `tab` is the LDS (device) or local (host) table storage of GI_LANE_DWORDS
+// rows x LANES columns.  Bytes outside out[0..out_len) are never written.
+template <int LANES>
+GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len, uint32_t *tab, int lane) {
+    typedef uint32_t gi_u32x4 __attribute__((vector_size(16)));
     GiBits b;
     gi_open(b, in);
-    uint32_t o = 0;
-    GiHuff lit, dist;
-    for (;;) {
+    GiHuff lit = {}, dist = {};
+    uint32_t o = 0, bfinal = 0;
+    uint32_t rem = 0;  // bytes left of the match or stored block
+    uint32_t D = 0;    // the match's current source distance (a multiple of its distance)
+    int mode = GI_M_HDR, rc = GI_OK;
+    while (mode != GI_M_DONE) {
         gi_refill(b);
-        const uint32_t hdr = gi_bits(b, 3);
-        const uint32_t bfinal = hdr & 1, btype = hdr >> 1;
-        if (btype == 0) {  // stored: to the byte boundary, LEN, NLEN, bytes
-            gi_bits(b, b.cnt & 7);
-            gi_refill(b);
-            const uint32_t len = gi_bits(b, 16);
-            gi_refill(b);
-            const uint32_t nlen = gi_bits(b, 16);
-            if ((len ^ 0xffffu) != nlen) return GI_E_HEADER;
-            if (o + len > out_len) return GI_E_OVERRUN;
-            for (uint32_t k = 0; k < len; k++) {
-                if (b.cnt < 8) gi_refill(b);
-                out[o++] = (uint8_t)gi_bits(b, 8);
+        if (mode == GI_M_HDR) {
+            const int m = gi_header<LANES>(b, lit, dist, tab, lane, bfinal, rem);
+            if (m < 0) {
+                rc = -m;
+                break;
             }
-        } else if (btype == 1 || btype == 2) {
-            int nlit = 288, ndist = 30;
-            if (btype == 1) {  // fixed codes
-                int rc = gi_build<LANES>(lit, sym, lane, GI_ROW_LIT, 288, [](int i) -> uint32_t {
-                    return i < 144 ? 8u : (i < 256 ? 9u : (i < 280 ? 7u : 8u));
-                });
-                if (rc) return rc;
-                rc = gi_build<LANES>(dist, sym, lane, GI_ROW_DIST, 30, [](int) -> uint32_t { return 5u; });
-                if (rc) return rc;
-            } else {  // dynamic codes
-                gi_refill(b);
-                nlit = (int)gi_bits(b, 5) + 257;
-                ndist = (int)gi_bits(b, 5) + 1;
-                const int ncl = (int)gi_bits(b, 4) + 4;
-                if (nlit > 286 || ndist > 30) return GI_E_HEADER;
-                // code-length code lengths, 3 bits each in the order
-                // 16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15 (5 bits per
-                // entry in two words), packed 3 bits per symbol
-                const uint64_t ord_lo = 16ull | 17ull << 5 | 18ull << 10 | 0ull << 15 | 8ull << 20 | 7ull << 25 |
-                                        9ull << 30 | 6ull << 35 | 10ull << 40 | 5ull << 45 | 11ull << 50 | 4ull << 55;
-                const uint64_t ord_hi = 12ull | 3ull << 5 | 13ull << 10 | 2ull << 15 | 14ull << 20 | 1ull << 25 |
-                                        15ull << 30;
-                uint64_t cl = 0;
-                for (int k = 0; k < ncl; k++) {
-                    gi_refill(b);
-                    const uint32_t v = gi_bits(b, 3);
-                    const int s = (int)((k < 12 ? ord_lo >> (5 * k) : ord_hi >> (5 * (k - 12))) & 31u);
-                    cl |= (uint64_t)v << (3 * s);
-                }
-                GiHuff clh;
-                int rc = gi_build<LANES>(clh, sym, lane, GI_ROW_CL, 19,
-                                         [cl](int i) -> uint32_t { return (uint32_t)(cl >> (3 * i)) & 7u; });
-                if (rc) return rc;
-                // the literal/length and distance code lengths, run-length
-                // coded: into 4-bit cells after the symbol rows (GI_NIB_ROWS
-                // rows of two lengths per lane), then both trees from them
-                uint8_t *nib = (uint8_t *)(sym + GI_ROWS * LANES);
-                const int ntot = nlit + ndist;
-                int n = 0, prev = -1;
-                while (n < ntot) {
-                    gi_refill(b);
-                    const int s = gi_decode<LANES>(b, clh, sym, lane, GI_ROW_CL);
-                    if (s < 0) return GI_E_TREE;
-                    int rep = 1, val = s;
-                    if (s == 16) {
-                        if (prev < 0) return GI_E_TREE;
-                        rep = 3 + (int)gi_bits(b, 2);
-                        val = prev;
-                    } else if (s == 17) {
-                        rep = 3 + (int)gi_bits(b, 3);
-                        val = 0;
-                    } else if (s == 18) {
-                        rep = 11 + (int)gi_bits(b, 7);
-                        val = 0;
-                    }
-                    if (n + rep > ntot) return GI_E_TREE;
-                    for (int k = 0; k < rep; k++, n++) {
-                        uint8_t *c = nib + (n >> 1) * LANES + lane;
-                        *c = (n & 1) ? (uint8_t)(*c | (val << 4)) : (uint8_t)val;
-                    }
-                    prev = val;
-                }
-                rc = gi_build<LANES>(lit, sym, lane, GI_ROW_LIT, nlit, [nib, lane](int i) -> uint32_t {
-                    return (uint32_t)(nib[(i >> 1) * LANES + lane] >> (4 * (i & 1))) & 15u;
-                });
-                if (rc) return rc;
-                rc = gi_build<LANES>(dist, sym, lane, GI_ROW_DIST, ndist, [nib, lane, nlit](int i) -> uint32_t {
-                    const int k = i + nlit;
-                    return (uint32_t)(nib[(k >> 1) * LANES + lane] >> (4 * (k & 1))) & 15u;
-                });
-                if (rc) return rc;
+            if (m == GI_M_STORED && o + rem > out_len) {
+                rc = GI_E_OVERRUN;
+                break;
             }
-            // the block's symbols
-            for (;;) {
-                gi_refill(b);
-                const int s = gi_decode<LANES>(b, lit, sym, lane, GI_ROW_LIT);
-                if (s < 0) return GI_E_CODE;
-                if (s < 256) {
-                    if (o >= out_len) return GI_E_OVERRUN;
-                    out[o++] = (uint8_t)s;
-                    continue;
+            mode = m;
+        } else if (mode == GI_M_SYM) {
+            const int s = gi_decode<LANES, 15, true>(b, lit, tab, lane, GI_T_LIT);
+            if (s < 0 || s > 285) {
+                rc = GI_E_CODE;
+                break;
+            }
+            if (s < 256) {
+                if (o >= out_len) {
+                    rc = GI_E_OVERRUN;
+                    break;
                 }
-                if (s == 256) break;
-                if (s > 285) return GI_E_CODE;
+                out[o++] = (uint8_t)s;
+            } else if (s == 256) {
+                mode = bfinal ? GI_M_DONE : GI_M_HDR;
+            } else {
                 int lb, le;
                 gi_len_code(s, lb, le);
                 const uint32_t len = (uint32_t)lb + gi_bits(b, le);
                 gi_refill(b);
-                const int d = gi_decode<LANES>(b, dist, sym, lane, GI_ROW_DIST);
-                if (d < 0 || d > 29) return GI_E_DIST;
+                const int d = gi_decode<LANES, 15, false>(b, dist, tab, lane, GI_T_DIST);
+                if (d < 0 || d > 29) {
+                    rc = GI_E_DIST;
+                    break;
+                }
                 int db, de;
                 gi_dist_code(d, db, de);
                 const uint32_t dd = (uint32_t)db + gi_bits(b, de);
-                if (dd > o) return GI_E_DIST;
-                if (o + len > out_len) return GI_E_OVERRUN;
-                uint8_t *q = out + o;
-                if (dd < len && dd <= 8) {  // a short repeating pattern: loaded once, stored from registers
-                    uint64_t pat = 0;
-                    GI_UNROLL
-                    for (uint32_t k = 0; k < 8; k++)
-                        if (k < dd) pat |= (uint64_t)q[(int64_t)k - dd] << (8 * k);
-                    uint32_t r = 0;
-                    for (uint32_t k = 0; k < len; k++) {
-                        q[k] = (uint8_t)(pat >> (8 * r));
-                        r = (r + 1 == dd) ? 0 : r + 1;
-                    }
-                } else {  // chunks of up to 16 bytes whose sources are final: all loads, then the stores
-                    for (uint32_t k = 0; k < len;) {
-                        uint32_t m = len - k;
-                        m = m < 16u ? m : 16u;
-                        m = m < dd ? m : dd;
-                        uint8_t t[16];
-                        GI_UNROLL
-                        for (uint32_t j = 0; j < 16; j++) t[j] = j < m ? q[(int64_t)(k + j) - dd] : 0;
-                        GI_UNROLL
-                        for (uint32_t j = 0; j < 16; j++)
-                            if (j < m) q[k + j] = t[j];
-                        k += m;
-                    }
+                if (dd > o) {
+                    rc = GI_E_DIST;
+                    break;
                 }
-                o += len;
+                if (o + len > out_len) {
+                    rc = GI_E_OVERRUN;
+                    break;
+                }
+                rem = len;
+                D = dd;
+                mode = GI_M_COPY;
             }
-        } else {
-            return GI_E_HEADER;
         }
-        if (bfinal) break;
+        // (a match starts copying in the step that decoded it)
+        if (mode == GI_M_COPY) {
+            uint32_t m = rem < 16u ? rem : 16u;
+            m = m < D ? m : D;
+            uint8_t *q = out + o;
+            if (o + 16 <= out_len) {  // sources all final: o - D + m <= o
+                gi_u32x4 v;
+                __builtin_memcpy(&v, q - D, 16);
+                __builtin_memcpy(q, &v, 16);
+            } else {
+                for (uint32_t j = 0; j < m; j++) q[j] = q[(int64_t)j - D];
+            }
+            o += m;
+            rem -= m;
+            if (m == D && D < 16) D <<= 1;
+            if (!rem) mode = GI_M_SYM;
+        } else if (mode == GI_M_STORED) {
+            // byte-aligned: up to 4 bytes from the bit buffer per step
+            gi_refill(b);
+            const uint32_t m = rem < 4u ? rem : 4u;
+            for (uint32_t j = 0; j < m; j++) out[o + j] = (uint8_t)gi_bits(b, 8);
+            o += m;
+            rem -= m;
+            if (!rem) mode = bfinal ? GI_M_DONE : GI_M_HDR;
+        }
     }
+    if (rc) return rc;
     // consumed bits: every merged word minus the first word's lead and the buffer
     const int64_t used_bits = b.merged * 32 - b.sh0 - b.cnt;
     if (used_bits > 8 * (int64_t)in_len) return GI_E_INPUT;

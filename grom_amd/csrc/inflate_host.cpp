@@ -12,8 +12,8 @@
 #include "inflate.h"
 
 extern "C" int grom_inflate_block_host(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len) {
-    thread_local uint16_t sym[GI_LANE_BYTES / 2 + 1];
-    return gi_inflate<1>(in, in_len, out, out_len, sym, 0);
+    thread_local uint32_t tab[GI_LANE_DWORDS];
+    return gi_inflate<1>(in, in_len, out, out_len, tab, 0);
 }
 
 static uint16_t rd16(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }

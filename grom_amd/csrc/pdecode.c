@@ -2028,6 +2028,7 @@ void pd_set_wanted(pd_session *s, const int *want) {
 typedef struct {
     pd_session *s;
     int device, first;       /* first: this worker also gathers the insert statistics */
+    int sub, nsub;           /* this device's chromosomes taken in turn by nsub workers */
     dd_ctx *dd;
     uint8_t *comp;           /* pinned compressed run (+64 readable bytes) */
     int64_t comp_cap;
@@ -2321,9 +2322,10 @@ static void *dw_main(void *arg) {
             if (need) apply_final(s, 0);
         }
     }
-    for (int k = 0; rc == 0 && k < s->n_plan && !s->abort; k++) {
+    for (int k = 0, ord = 0; rc == 0 && k < s->n_plan && !s->abort; k++) {
         pd_chrom *c = &s->ch[k];
         if (!s->keep[k] || !s->want[k] || c->device != w->device) continue;
+        if (ord++ % w->nsub != w->sub) continue;
         const double t0 = now_s();
         pd_trace(s, PD_EV_UPLOAD, k, 0);
         rc = dw_chrom(w, k, err, (int)sizeof(err));
@@ -2362,15 +2364,21 @@ static int pd_start_device(pd_session *s) {
         if (!seen && nd < 64) devs[nd++] = s->ch[k].device;
     }
     if (nd == 0) devs[nd++] = 0;
+    /* GROM_DD_WORKERS per GPU (one reads a run while another's is on the GPU) */
+    const char *ws = getenv("GROM_DD_WORKERS");
+    int per = ws && atoi(ws) > 0 ? atoi(ws) : 1;
+    if (per > 8) per = 8;
     const char *it = getenv("GROM_DECODE_THREADS");
-    s->io_threads = it && atoi(it) > 0 ? atoi(it) / nd : 8;
+    s->io_threads = it && atoi(it) > 0 ? atoi(it) / (nd * per) : 8;
     if (s->io_threads < 1) s->io_threads = 1;
     if (s->io_threads > 16) s->io_threads = 16;
-    s->dw = (pthread_t *)calloc((size_t)nd, sizeof(pthread_t));
-    for (int q = 0; q < nd; q++) {
+    s->dw = (pthread_t *)calloc((size_t)(nd * per), sizeof(pthread_t));
+    for (int q = 0; q < nd * per; q++) {
         dd_worker *w = (dd_worker *)calloc(1, sizeof(dd_worker));
         w->s = s;
-        w->device = devs[q];
+        w->device = devs[q / per];
+        w->sub = q % per;
+        w->nsub = per;
         w->first = q == 0;
         w->loaded = -1;
         if (pthread_create(&s->dw[q], NULL, dw_main, w) != 0) {

@@ -679,23 +679,58 @@ def test_device_inflate_matches_zlib(datadir, tmp_path):
                               "lowmapq_clip"])
 def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
     """BAM decode on the GPU (ddecode.hip: the runs inflated, walked and
-    parsed on the device; the CLI's default) stages, for every chromosome,
+    parsed on the device; GROM_DEVICE_DECODE=1) stages, for every chromosome,
     exactly the input the host decoder threads (pdecode.c) stage: same stream
     facts and the same digest of every array, CIGAR/base/quality/SA-XP
     content, dropped record and name-id relation; and the outputs are the
-    oracle's."""
+    oracle's.  Mode "3w" splits the GPU's chromosomes over three device
+    decode workers (GROM_DD_WORKERS), each with its own decode context, as
+    the per-GPU workers of -P n on a multi-GPU node do."""
     bam, fa = synth(datadir, case, CASES[case])
     tag = f"dd_{case}{''.join(extra).replace('-', '_')}"
     run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
     lines = {}
-    for mode in ("0", "1"):
+    modes = {"0": {"GROM_DEVICE_DECODE": "0"}, "1": {"GROM_DEVICE_DECODE": "1"},
+             "3w": {"GROM_DEVICE_DECODE": "1", "GROM_DD_WORKERS": "3"}}
+    for mode, env in modes.items():
         capfd.readouterr()
         run_grom(datadir, bam, fa, f"g{mode}_{tag}.vcf", extra,
-                 env_extra={"GROM_DEVICE_DECODE": mode, "GROM_STAGE_DIGEST": "1", "GROM_VERBOSE": "1"})
+                 env_extra=dict(env, GROM_STAGE_DIGEST="1", GROM_VERBOSE="1"))
         out = capfd.readouterr().out
-        assert ("device decode:" in out) == (mode == "1"), out[-1500:]
+        assert ("device decode:" in out) == (mode != "0"), out[-1500:]
         lines[mode] = sorted(l for l in out.splitlines() if l.startswith("stage "))
-    assert lines["1"] and lines["0"] == lines["1"], (lines["0"], lines["1"])
-    for mode in ("0", "1"):
+    assert lines["1"] and lines["0"] == lines["1"] == lines["3w"], (lines["0"], lines["1"], lines["3w"])
+    for mode in modes:
         for ext in (".vcf", ".ctx.vcf"):
             assert open(datadir / f"o_{tag}{ext}").read() == open(datadir / f"g{mode}_{tag}{ext}").read(), (mode, ext)
+
+
+def _sha_rows(path):
+    import hashlib
+    h = hashlib.sha256()
+    rows = 0
+    with open(path, "rb") as f:
+        for line in f:
+            h.update(line)
+            rows += not line.startswith(b"#")
+    return h.hexdigest(), rows
+
+
+@pytest.mark.parametrize("case", ["c4_20mb_60x", "genome_s010"])
+def test_oracle_digest_cases(datadir, case):
+    """Inputs too large for the oracle inside a GPU test, checked against the
+    oracle's digests (tests/golden/oracle_<case>.json, written on the CPU by
+    tools/make_golden_genome.py): BASELINE configs[4]'s shape at 20 Mb (60x
+    tetraploid male donor, -p 4 -g 1 -M -V 1) and a 24-contig genome at 0.1 of
+    GRCh38's lengths (configs[2]'s shape, -M -g 1).  The BAM is written here
+    by the same deterministic grom_synth call; VCF and .ctx.vcf must hash to
+    the oracle's."""
+    import json
+    from _util import REPO
+    rec = json.load(open(os.path.join(REPO, "tests", "golden", f"oracle_{case}.json")))
+    d = datadir / case
+    d.mkdir(exist_ok=True)
+    synth(d, "genome", rec["synth_args"])
+    run_grom(d, "genome.bam", "genome.fa", "o.vcf", rec["cli_flags"])
+    assert _sha_rows(d / "o.vcf") == (rec["vcf_sha256"], rec["vcf_rows"])
+    assert _sha_rows(d / "o.ctx.vcf") == (rec["ctx_sha256"], rec["ctx_rows"])
