@@ -441,7 +441,7 @@ def main():
     dt = max_over_ranks(time.perf_counter() - t0, device="cuda")
     value = total * args.steps / dt / 1e6
     stats = chrom_stats(last)  # this rank's chromosomes, last timed run
-    dec = [ln for ln in last.splitlines() if ln.startswith("streamed decode:")]
+    dec = [ln for ln in last.splitlines() if ln.startswith(("streamed decode:", "device decode:"))]
     phases = [ln for ln in last.splitlines() if ln.startswith("cli phases")]
 
     launches = [(launch_bytes(s["reads"], s["cigar_ops"], s["bases"], s["len"]), s["ms_pileup"], s["len"])
@@ -487,7 +487,7 @@ def main():
             "data": "synthetic (seeded generator grom_amd/csrc/synth.c, written as BAM + BAI + FASTA by grom_synth)",
             "config": {
                 "workload": wl + "; step = one whole run of the drop-in CLI (grom_amd/bin/grom, a fresh process): "
-                                 "BAM index, BGZF decode on the host into pinned pieces, host->HBM copies, every "
+                                 "BAM index, compressed BGZF runs copied to HBM and inflated + parsed on the GPU, every "
                                  "chromosome's scan (pileup/SNV, duplicate filter, breakpoint evidence + tests, "
                                  "SV/INDEL rows, CTX records, read-depth CNV path + rows), VCF + CTX post-pass",
                 "genome_bases": total, "chromosomes": len(lengths), "chromosomes_rank0": len(mine),
@@ -495,7 +495,7 @@ def main():
                 "bam_bytes": os.path.getsize(bam), "synth_s": round(t_synth, 1),
                 "run_s": [round(x, 3) for x in runs],
                 "vcf_rows": n_rows,
-                "host_cpus": cpus, "decode_threads": int(env.get("GROM_DECODE_THREADS", cpus)),
+                "host_cpus": cpus, "decode": "device (GPU inflate + parse)" if dec and dec[-1].startswith("device") else "host threads",
                 "decode_rank0": dec[-1] if dec else None,
                 "phases_rank0": phases[-1] if phases else None,
                 "reads_rank0": sum(s["reads"] for s in stats.values()),

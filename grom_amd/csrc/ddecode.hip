@@ -270,26 +270,137 @@ __device__ __forceinline__ int32_t ld_bs(const uint8_t *U, int64_t o) {
 
 #define DD_MAX_REC (256 << 20)
 
-// one lane per chunk: count its records (off == nullptr) or write their
-// offsets from base[c] on
-__global__ void k_walk(const uint8_t *__restrict__ U, const int64_t *__restrict__ S, int64_t n_chunks,
-                       uint32_t *__restrict__ cnt, const uint32_t *__restrict__ base, int64_t *__restrict__ off,
-                       uint32_t *__restrict__ bad) {
-    const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
-    int64_t o = S[c];
-    const int64_t e = S[c + 1];
-    uint32_t n = 0;
-    int64_t w = off ? (int64_t)base[c] : 0;
-    while (o < e) {
+// ---- record starts, many short chains per chunk (guess, then verify) ----
+//
+// A chunk between two index-named record starts holds ~3,000 records at 30x;
+// walking its block_size chain on one lane is 3,000 dependent loads from HBM.
+// Instead one workgroup takes the chunk, cut into sub-chunks of WS_G bytes:
+// each lane guesses the first record start in its sub-chunk (a header whose
+// fields fit the run -- block_size, target id, a NUL-terminated name, field
+// sizes within block_size -- and whose successor's block_size and target id
+// fit too) and walks the chain to the sub-chunk's end.  Then lane 0 follows
+// the true chain across the sub-chunks: sub-chunk q's walk is taken when its
+// guess equals the true chain's first start in it (the exit of sub-chunk
+// q-1's accepted walk; sub-chunk 0 starts at the chunk's known start), by
+// induction every accepted walk is the true chain's; any other sub-chunk is
+// walked again from the true position.  A wrong guess costs one re-walk and
+// never changes the result.
+#define WS_G 4096
+#define WS_T 256
+
+__device__ __forceinline__ bool ws_plausible(const uint8_t *U, int64_t p, int64_t end, int32_t tid) {
+    if (p + 40 > end) return false;
+    const uint32_t *a = (const uint32_t *)(U + (p & ~(int64_t)3));
+    const uint32_t sh = (uint32_t)(p & 3) * 8;
+    uint32_t raw[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) raw[k] = a[k];
+    uint32_t w[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = sh ? (raw[k] >> sh) | (raw[k + 1] << (32 - sh)) : raw[k];
+    const int32_t bs = (int32_t)w[0];
+    if (bs < 34 || bs > (1 << 20) || (int32_t)w[1] != tid) return false;
+    const int lqn = (int)(w[3] & 0xff), nc = (int)(w[4] & 0xffff);
+    const int32_t lq = (int32_t)w[5];
+    if (lqn < 1 || lq < 0 || 32 + (int64_t)lqn + 4 * (int64_t)nc + (lq + 1) / 2 + lq > (int64_t)bs) return false;
+    if (p + 36 + lqn > end || U[p + 36 + lqn - 1] != 0) return false;
+    const int64_t q = p + 4 + (int64_t)bs;
+    if (q + 8 <= end) {
+        const int32_t bs2 = ld_bs(U, q), tid2 = ld_bs(U, q + 4);
+        if (bs2 < 34 || bs2 > (1 << 20) || tid2 != tid) return false;
+    }
+    return true;
+}
+
+// walk from o while o < hi: records counted (and written from *w when off)
+// and the exit; -1 exit for a block_size outside the record limits
+__device__ __forceinline__ int64_t ws_walk(const uint8_t *U, int64_t o, int64_t hi, uint32_t &n, int64_t *off,
+                                           int64_t w) {
+    n = 0;
+    while (o < hi) {
         const int32_t bs = ld_bs(U, o);
-        if (bs < 32 || bs > DD_MAX_REC) { atomicOr(bad, DB_RECORD); return; }
-        if (off) off[w++] = o;
+        if (bs < 32 || bs > DD_MAX_REC) return -1;
+        if (off) off[w + n] = o;
         o += 4 + (int64_t)bs;
         n++;
     }
-    if (o != e) { atomicOr(bad, DB_CHAIN); return; }
-    if (!off) cnt[c] = n;
+    return o;
+}
+
+// one workgroup per chunk [S[c], S[c+1]): counts per chunk (off == nullptr) or
+// the record offsets from base[c] on
+__global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U, const int64_t *__restrict__ S,
+                                                   int64_t n_chunks, int32_t tid, int guess,
+                                                   uint32_t *__restrict__ cnt,
+                                                   const uint32_t *__restrict__ base, int64_t *__restrict__ off,
+                                                   uint32_t *__restrict__ bad) {
+    __shared__ int64_t s_start[WS_T], s_exit[WS_T];
+    __shared__ uint32_t s_n[WS_T], s_pre[WS_T];
+    __shared__ int64_t s_carry;
+    __shared__ uint32_t s_total;
+    __shared__ int s_fail;
+    const int64_t c = blockIdx.x;
+    if (c >= n_chunks) return;
+    const int t = threadIdx.x;
+    const int64_t c0 = S[c], c1 = S[c + 1];
+    const int64_t nsub = c1 > c0 ? (c1 - c0 + WS_G - 1) / WS_G : 0;
+    if (t == 0) { s_carry = c0; s_total = 0; s_fail = 0; }
+    __syncthreads();
+    for (int64_t r0 = 0; r0 < nsub; r0 += WS_T) {
+        const int64_t q = r0 + t;
+        const int64_t lo = c0 + q * WS_G, hi = lo + WS_G < c1 ? lo + WS_G : c1;
+        int64_t st = -1, ex = -1;
+        uint32_t n = 0;
+        if (q < nsub) {
+            if (q == 0) st = c0;
+            else if (guess == 2) st = lo;  // test hook: guesses that are mostly wrong
+            else if (guess == 1)
+                for (int64_t p = lo; p < hi; p++)
+                    if (ws_plausible(U, p, c1, tid)) { st = p; break; }
+            if (st >= 0) ex = ws_walk(U, st, hi, n, nullptr, 0);
+        }
+        s_start[t] = st;
+        s_exit[t] = ex;
+        s_n[t] = n;
+        __syncthreads();
+        if (t == 0) {  // the true chain across this round's sub-chunks
+            int64_t carry = s_carry;
+            const int m = (int)(nsub - r0 < WS_T ? nsub - r0 : WS_T);
+            for (int k = 0; k < m && !s_fail; k++) {
+                const int64_t khi = c0 + (r0 + k) * WS_G + WS_G < c1 ? c0 + (r0 + k) * WS_G + WS_G : c1;
+                if (!(s_start[k] == carry && s_exit[k] >= 0)) {
+                    uint32_t kn = 0;
+                    const int64_t kex = ws_walk(U, carry, khi, kn, nullptr, 0);
+                    if (kex < 0) { atomicOr(bad, DB_RECORD); s_fail = 1; break; }
+                    s_start[k] = carry;
+                    s_exit[k] = kex;
+                    s_n[k] = kn;
+                }
+                carry = s_exit[k];
+            }
+            s_carry = carry;
+        }
+        __syncthreads();
+        if (s_fail) return;
+        // exclusive prefix of this round's counts (lane 0; 256 adds)
+        if (t == 0) {
+            const int m = (int)(nsub - r0 < WS_T ? nsub - r0 : WS_T);
+            uint32_t acc = s_total;
+            for (int k = 0; k < m; k++) { s_pre[k] = acc; acc += s_n[k]; }
+            s_total = acc;
+        }
+        __syncthreads();
+        if (off && q < nsub && s_n[t]) {
+            uint32_t n2 = 0;
+            ws_walk(U, s_start[t], c0 + q * WS_G + WS_G < c1 ? c0 + q * WS_G + WS_G : c1, n2, off,
+                    (int64_t)base[c] + s_pre[t]);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        if (s_carry != c1) atomicOr(bad, DB_CHAIN);
+        if (!off) cnt[c] = s_total;
+    }
 }
 
 // which characters are 'Z'/'H' terminated, and the fixed sizes (bamio.c aux_type_size)
@@ -600,6 +711,7 @@ struct dd_ctx {
     uint8_t *h_aux = nullptr;    // pinned: packed split-read candidate records
     size_t h_aux_cap = 0;
     float ms_inflate = 0, ms_walk = 0, ms_parse = 0;
+    int ws_guess = 1;  // record-start guesses: 1 plausible headers, 0 none, 2 sub-chunk starts (GROM_WS_GUESS, tests)
 };
 
 #define DCK(x)                                                                                       \
@@ -623,6 +735,7 @@ extern "C" dd_ctx *dd_ctx_new(int device) {
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     dd_ctx *c = new dd_ctx();
     c->device = device;
+    if (getenv("GROM_WS_GUESS")) c->ws_guess = atoi(getenv("GROM_WS_GUESS"));
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return nullptr; }
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
     if (hipHostMalloc((void **)&c->h_small, 64 * sizeof(int64_t), 0) != hipSuccess) c->h_small = nullptr;
@@ -657,8 +770,8 @@ extern "C" void dd_ctx_times(const dd_ctx *c, double *ms) {
 // and find its records: starts[0..n_starts) are record offsets in the
 // inflated stream (the first = the run's first record), u_end its end
 extern "C" int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
-                           int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int64_t *n_rec,
-                           char *err, int errlen) {
+                           int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int32_t tid,
+                           int64_t *n_rec, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
     hipStream_t st = c->st;
     DGROW(c->comp, (size_t)comp_len + 64);
@@ -683,9 +796,8 @@ extern "C" int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, c
     }
     DCK(hipEventRecord(c->ev[1], st));
     // records: count per chunk, place, write offsets
-    hipLaunchKernelGGL(k_walk, dim3(grid_for(n_starts, 128, 1u << 30)), dim3(128), 0, st, P<uint8_t>(c->U),
-                       P<int64_t>(c->S), n_starts, P<uint32_t>(c->ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr,
-                       bad);
+    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(c->U), P<int64_t>(c->S),
+                       n_starts, tid, c->ws_guess, P<uint32_t>(c->ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, bad);
     size_t tb = 0;
     DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->ccnt), P<uint32_t>(c->cbase), (int)n_starts, st));
     DGROW(c->tmp, tb);
@@ -705,8 +817,8 @@ extern "C" int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, c
     }
     const int64_t R = (int64_t)hs[0] + hs[1];
     DGROW(c->off, sizeof(int64_t) * (size_t)(R + 1));
-    hipLaunchKernelGGL(k_walk, dim3(grid_for(n_starts, 128, 1u << 30)), dim3(128), 0, st, P<uint8_t>(c->U),
-                       P<int64_t>(c->S), n_starts, (uint32_t *)nullptr, P<uint32_t>(c->cbase), P<int64_t>(c->off), bad);
+    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(c->U), P<int64_t>(c->S),
+                       n_starts, tid, c->ws_guess, (uint32_t *)nullptr, P<uint32_t>(c->cbase), P<int64_t>(c->off), bad);
     DCK(hipEventRecord(c->ev[2], st));
     DCK(hipGetLastError());
     c->R = R;

@@ -973,7 +973,8 @@ static void *fasta_main(void *arg) {
         if (stop) break;
         chrom_plan *c = F->plan[k];
         c->ref = malloc(c->len + 1);
-        if (c->ref) grom_fasta_load(&F->S->fa, c->fasta_idx, c->ref, c->len);
+        if (c->ref && grom_fasta_load_at(&F->S->fa, c->fasta_idx, c->ref, c->len) < 0)
+            grom_fasta_load(&F->S->fa, c->fasta_idx, c->ref, c->len);
         pthread_mutex_lock(&F->mu);
         F->loaded = k + 1;
         pthread_cond_broadcast(&F->cv);
@@ -1098,11 +1099,11 @@ static int run_streamed(cli_state *S) {
         pd_set_wanted(pd, want);
         free(want);
     }
-    /* BAM decode on the GPUs (ddecode.hip) with GROM_DEVICE_DECODE=1; the
-     * host decoder threads otherwise (plan-only runs always use them) */
+    /* BAM decode on the GPUs (ddecode.hip) by default; the host decoder
+     * threads with GROM_DEVICE_DECODE=0 (plan-only runs always use them) */
     {
         const char *dd = getenv("GROM_DEVICE_DECODE");
-        pd_set_device_mode(pd, !g_plan_only && dd && atoi(dd) != 0);
+        pd_set_device_mode(pd, !g_plan_only && !(dd && atoi(dd) == 0));
     }
     if (pd_start(pd, P->min_mapq, S->n_dev, dev_of, g_plan_only)) {
         fprintf(stderr, "grom: %s\n", pd_error(pd));
@@ -1366,13 +1367,34 @@ static int cli_run(int argc, char **argv, int force_serial) {
     /* candidate chromosomes in BAM header order (GROM.c:20826-21050); the
      * length test that needs the insert size comes later */
     S->plan = calloc(S->hdr.n_ref > 0 ? S->hdr.n_ref : 1, sizeof(chrom_plan));
+    /* the loader's length of every matched FASTA entry (find_disc_svs loads
+     * each chromosome, GROM.c:21009-21045), several entries at once */
+    int *fi_of = malloc(sizeof(int) * (S->hdr.n_ref > 0 ? S->hdr.n_ref : 1));
+    int *fi_list = malloc(sizeof(int) * (S->hdr.n_ref > 0 ? S->hdr.n_ref : 1));
+    long *fi_len = calloc(S->fa.n > 0 ? S->fa.n : 1, sizeof(long));
+    int n_fi = 0;
     for (int t = 0; t < S->hdr.n_ref; t++) {
         int fi = grom_match_target(&S->fa, S->hdr.ref_name[t]);
         char lc[GROM_MAX_CHR_NAMES];
         int bl = grom_target_name_lc(S->hdr.ref_name[t], lc, (int)sizeof(lc));
         if (P->gender == 0 && ((bl == 4 && strncmp(lc, "chry", 4) == 0) || (bl == 1 && lc[0] == 'y'))) fi = -1;
+        fi_of[t] = fi;
         if (fi < 0) continue;
-        long len = grom_fasta_load(&S->fa, fi, NULL, 0);
+        int seen = 0;
+        for (int a = 0; a < n_fi && !seen; a++) seen = fi_list[a] == fi;
+        if (!seen) fi_list[n_fi++] = fi;
+    }
+    {
+        long *lens = calloc(n_fi > 0 ? n_fi : 1, sizeof(long));
+        const int thr = host_cpus() < 16 ? host_cpus() : 16;
+        const int ok = getenv("GROM_FASTA_SERIAL") == NULL && grom_fasta_lengths(&S->fa, fi_list, n_fi, lens, thr) == 0;
+        for (int a = 0; a < n_fi; a++) fi_len[fi_list[a]] = ok ? lens[a] : grom_fasta_load(&S->fa, fi_list[a], NULL, 0);
+        free(lens);
+    }
+    for (int t = 0; t < S->hdr.n_ref; t++) {
+        const int fi = fi_of[t];
+        if (fi < 0) continue;
+        long len = fi_len[fi];
         /* count_discordant_pairs re-derives the BAM target from the FASTA name
          * (GROM.c:1894-1961): the first target matching it */
         int32_t tid2 = -1;
@@ -1386,6 +1408,9 @@ static int cli_run(int argc, char **argv, int force_serial) {
         c->target = strdup(S->hdr.n_ref > 0 ? S->hdr.ref_name[tid2 >= 0 ? tid2 : S->hdr.n_ref - 1] : "");
         snprintf(c->name, sizeof(c->name), "%.*s", S->fa.name_len[fi], S->fa.names[fi]);
     }
+    free(fi_of);
+    free(fi_list);
+    free(fi_len);
     S->t_cand = clock_gettime_s();
     {
         size_t ol = strlen(S->out_name);

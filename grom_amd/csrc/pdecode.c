@@ -2164,7 +2164,7 @@ static int dw_load(dd_worker *w, int ri, char *err, int errlen) {
     for (int64_t k = 0; k < ns; k++)
         if (m == 0 || w->starts[k] != w->starts[m - 1]) w->starts[m++] = w->starts[k];
     int64_t R = 0;
-    const int rc = dd_run_load(w->dd, w->comp, len, w->blk, nb, ub, w->starts, m, u_end, &R, err, errlen);
+    const int rc = dd_run_load(w->dd, w->comp, len, w->blk, nb, ub, w->starts, m, u_end, r->tid, &R, err, errlen);
     if (rc) return rc;
     if (r->count >= 0 && R != r->count) {
         snprintf(err, (size_t)errlen, "target %d: %lld records decoded, the index counts %lld", r->tid, (long long)R,

@@ -5,6 +5,8 @@
 
 #include <ctype.h>
 #include <math.h>
+#include <pthread.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -167,6 +169,103 @@ long grom_fasta_load(grom_fasta *f, int i, char *buf, long cap) {
         len += f->loader_alpha_len;
     }
     return len;
+}
+
+/* grom_fasta_load's result without the shared stream: the chromosome's bytes
+ * by pread into a private buffer and fgets(line, 1000)'s chunks found with
+ * memchr (a chunk ends after its newline or at 999 bytes), so chromosomes
+ * load on several threads at once.  -2 when the chromosome holds a NUL byte
+ * (strlen would cut the chunk; the caller takes grom_fasta_load). */
+long grom_fasta_load_at(const grom_fasta *f, int i, char *buf, long cap) {
+    enum { BLK = 1 << 22 };
+    char *b = malloc((size_t)BLK + 1024);
+    if (!b) return -1;
+    const int fd = fileno(f->fh);
+    off_t off = (off_t)f->file_pos[i];
+    size_t have = 0, p = 0;
+    int eof = 0, prev_l = -1, alpha = 0;
+    long len = 0;
+    for (;;) {
+        if (have - p < 1000 && !eof) {
+            memmove(b, b + p, have - p);
+            have -= p;
+            p = 0;
+            const ssize_t k = pread(fd, b + have, BLK, off);
+            if (k < 0) { free(b); return -1; }
+            if (k == 0) eof = 1;
+            if (k > 0 && memchr(b + have, 0, (size_t)k)) { free(b); return -2; }
+            have += (size_t)k;
+            off += k;
+            continue;
+        }
+        if (p >= have) break; /* fgets at end of file */
+        const size_t avail = have - p, lim = avail < 999 ? avail : 999;
+        const char *line = b + p;
+        const char *nl = memchr(line, '\n', lim);
+        const int L = (int)(nl ? (size_t)(nl - line) + 1 : lim);
+        if (line[0] == '>') break;
+        if (len == 0 || L != prev_l) {
+            prev_l = L;
+            int w = L - 1;
+            while (!isalpha((unsigned char)line[w]) && w > 0) w--;
+            alpha = w + 1;
+        }
+        if (buf && len + alpha <= cap) memcpy(buf + len, line, (size_t)alpha);
+        len += alpha;
+        p += (size_t)L;
+    }
+    free(b);
+    return len;
+}
+
+typedef struct {
+    const grom_fasta *f;
+    const int *idx;
+    long *out;
+    int n, next, bad;
+    pthread_mutex_t mu;
+} fasta_len_job;
+
+static void *fasta_len_main(void *arg) {
+    fasta_len_job *j = (fasta_len_job *)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        const int k = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (k >= j->n) break;
+        const long L = grom_fasta_load_at(j->f, j->idx[k], NULL, 0);
+        if (L < 0) {
+            pthread_mutex_lock(&j->mu);
+            j->bad = 1;
+            pthread_mutex_unlock(&j->mu);
+        }
+        j->out[k] = L;
+    }
+    return NULL;
+}
+
+int grom_fasta_lengths(const grom_fasta *f, const int *idx, int n, long *out, int threads) {
+    if (n <= 0) return 0;
+    if (threads > n) threads = n;
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    fasta_len_job j;
+    memset(&j, 0, sizeof(j));
+    j.f = f;
+    j.idx = idx;
+    j.out = out;
+    j.n = n;
+    pthread_mutex_init(&j.mu, NULL);
+    pthread_t th[64];
+    int started = 0;
+    for (int t = 1; t < threads; t++) {
+        if (pthread_create(&th[started], NULL, fasta_len_main, &j) != 0) break;
+        started++;
+    }
+    fasta_len_main(&j);
+    for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&j.mu);
+    return j.bad ? -1 : 0;
 }
 
 int grom_target_name_lc(const char *target, char *out, int cap) {

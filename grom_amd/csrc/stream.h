@@ -45,6 +45,12 @@ int grom_fasta_open_cached(grom_fasta *f, const char *path);
 void grom_fasta_close(grom_fasta *f);
 /* load chromosome `i` into buf (capacity cap); returns its length */
 long grom_fasta_load(grom_fasta *f, int i, char *buf, long cap);
+/* the same load without the shared stream (thread-safe, pread + memchr);
+ * -2 when the chromosome holds a NUL byte (use grom_fasta_load), -1 on error */
+long grom_fasta_load_at(const grom_fasta *f, int i, char *buf, long cap);
+/* lengths of chromosomes idx[0..n) (grom_fasta_load_at) on up to `threads`
+ * threads; -1 if any failed (out[k] < 0 for those) */
+int grom_fasta_lengths(const grom_fasta *f, const int *idx, int n, long *out, int threads);
 
 /* FASTA index of a BAM target under find_disc_svs' name rules
  * (GROM.c:20898-20975), -1 if none */

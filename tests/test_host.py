@@ -321,3 +321,63 @@ def test_inflate_twin_matches_zlib(tmp_path):
         path.write_bytes(bytes(bad))
         nb, by = ctypes.c_int64(), ctypes.c_int64()
         assert f(str(path).encode(), 1, ctypes.byref(nb), ctypes.byref(by)) == 0, k
+
+
+def test_fasta_pread_loader_matches_fgets_loader(tmp_path):
+    """grom_fasta_load_at (pread + memchr chunks, several chromosomes at once)
+    gives grom_fasta_load's bytes and lengths (fgets(line, 1000) per chunk,
+    the alpha cut re-measured only when a chunk's length changes;
+    GROM.c:21009-21045) on awkward files: lines over 999 bytes (split into
+    fgets chunks, one starting with '>'), changing widths, trailing spaces and
+    digits, CRLF, no final newline, empty entries; a NUL byte returns -2."""
+    import random
+    import grom_amd
+    lib = grom_amd.lib()
+    lib.grom_fasta_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.grom_fasta_load.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_long]
+    lib.grom_fasta_load.restype = ctypes.c_long
+    lib.grom_fasta_load_at.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_long]
+    lib.grom_fasta_load_at.restype = ctypes.c_long
+    lib.grom_fasta_lengths.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_long), ctypes.c_int]
+    lib.grom_fasta_close.argtypes = [ctypes.c_void_p]
+    rng = random.Random(11)
+
+    def seq(n):
+        return "".join(rng.choice("ACGTNacgtn") for _ in range(n))
+
+    entries = [
+        ">c1 desc\n" + "".join(seq(60) + "\n" for _ in range(300)) + seq(17) + "\n",
+        ">c2\n" + seq(2500) + "\n" + seq(80) + "  \n" + seq(80) + "12\n" + seq(3) + "\n",
+        ">c3\r\n" + "".join(seq(70) + "\r\n" for _ in range(50)),
+        ">c4\n" + seq(998) + ">" + seq(500) + "\n" + seq(60) + "\n",  # a chunk starting with '>'
+        ">empty\n",
+        ">c5\n" + seq(999) + "\n" + seq(1000) + "\n" + seq(1998) + "\n" + "".join(seq(rng.randint(1, 120)) + "\n" for _ in range(400)),
+        ">c6\n" + "".join(seq(50) + "\n" for _ in range(100000)),
+        ">last\n" + seq(61) + "\n" + seq(61),  # no final newline
+    ]
+    path = tmp_path / "odd.fa"
+    path.write_text("".join(entries))
+    f = ctypes.create_string_buffer(256)
+    assert lib.grom_fasta_open(f, str(path).encode()) == 0
+    n = ctypes.c_int.from_buffer(f, 8).value
+    assert n == len(entries)
+    lens_want = []
+    for i in range(n):
+        L = lib.grom_fasta_load(f, i, None, 0)
+        buf_a = ctypes.create_string_buffer(L + 1)
+        buf_b = ctypes.create_string_buffer(L + 1)
+        assert lib.grom_fasta_load(f, i, buf_a, L) == L
+        assert lib.grom_fasta_load_at(f, i, buf_b, L) == L, i
+        assert buf_a.raw == buf_b.raw, i
+        lens_want.append(L)
+    idx = (ctypes.c_int * n)(*range(n))
+    out = (ctypes.c_long * n)()
+    assert lib.grom_fasta_lengths(f, idx, n, out, 4) == 0
+    assert list(out) == lens_want
+    lib.grom_fasta_close(f)
+    nul = tmp_path / "nul.fa"
+    nul.write_bytes(b">a\nACGT\x00ACGT\n")
+    assert lib.grom_fasta_open(f, str(nul).encode()) == 0
+    assert lib.grom_fasta_load_at(f, 0, None, 0) == -2
+    lib.grom_fasta_close(f)
