@@ -40,13 +40,17 @@ dd_ctx *dd_ctx_new(int device);
 void dd_ctx_free(dd_ctx *c);
 /* summed HIP-event times of the parsed runs: inflate, record walk, parse */
 void dd_ctx_times(const dd_ctx *c, double ms[3]);
-/* inflate a run's blocks (h_comp pinned, 64 readable bytes past comp_len;
- * h_blk its block table, ubytes the inflated size) and find its records from
+/* a run's compressed bytes (h_comp pinned, 64 readable bytes past comp_len)
+ * copied into device slot 0/1 on the context's copy stream; returns at once,
+ * h_comp must stay untouched until a dd_run_load of the slot has returned */
+int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_t comp_len, char *err, int errlen);
+/* inflate a run's blocks (uploaded to `slot`; h_blk its block table, ubytes
+ * the inflated size) and find its records from
  * the record starts h_starts (offsets into the inflated stream, the first
  * being the run's first record) up to u_end: *n_rec records (tid: the run's
  * target, for the record-start guesses).  0; -2 when
  * the data contradicts the index plan (the CLI then reads serially); -1 */
-int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
+int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
                 int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int32_t tid, int64_t *n_rec,
                 char *err, int errlen);
 /* find_insert_mean's sample from every record of the loaded run (file order):

@@ -20,6 +20,7 @@
 #include "inflate.h"
 
 #define DD_LANES 64
+#define DD_SLOTS 2
 
 // One BGZF block per lane: blk[j] = {offset of its DEFLATE data in `comp`,
 // its length, offset of its output in `out`, ISIZE}.  status[j] = GI_* code.
@@ -702,8 +703,12 @@ __global__ void k_lower_bound(const int32_t *a, int64_t n, int32_t x, int64_t *o
 struct dd_ctx {
     int device = -1;
     hipStream_t st = nullptr;
+    hipStream_t cst = nullptr;  // compressed runs' host->device copies (dd_comp_upload, the prefetch thread)
+    DBuf dcomp[DD_SLOTS];
+    hipEvent_t cev[DD_SLOTS] = {};
+    int64_t dcomp_len[DD_SLOTS] = {};
     hipEvent_t ev[4] = {};
-    DBuf comp, blk, U, status, misc, S, ccnt, cbase, off;
+    DBuf blk, U, status, misc, S, ccnt, cbase, off;
     DBuf keep, kidx, drop, didx, auxc, aidx, ncig, coff, nb, boff, rpos, krec, keys, vals, keys2, vals2, head, tmp;
     DBuf sq, sqi, sv, slq, sm, s_ins, s_lq, acand, alen, aoff, akidx, apack;
     int64_t R = 0, nblk = 0, ubytes = 0;
@@ -737,7 +742,9 @@ extern "C" dd_ctx *dd_ctx_new(int device) {
     c->device = device;
     if (getenv("GROM_WS_GUESS")) c->ws_guess = atoi(getenv("GROM_WS_GUESS"));
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return nullptr; }
+    if (hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) c->cst = nullptr;
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
+    for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming);
     if (hipHostMalloc((void **)&c->h_small, 64 * sizeof(int64_t), 0) != hipSuccess) c->h_small = nullptr;
     return c;
 }
@@ -746,7 +753,12 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DBuf *all[] = {&c->comp, &c->blk, &c->U, &c->status, &c->misc, &c->S, &c->ccnt, &c->cbase, &c->off, &c->keep,
+    if (c->cst) (void)hipStreamSynchronize(c->cst);
+    for (int k = 0; k < DD_SLOTS; k++) {
+        if (c->dcomp[k].p) (void)hipFree(c->dcomp[k].p);
+        if (c->cev[k]) (void)hipEventDestroy(c->cev[k]);
+    }
+    DBuf *all[] = {&c->blk, &c->U, &c->status, &c->misc, &c->S, &c->ccnt, &c->cbase, &c->off, &c->keep,
                    &c->kidx, &c->drop, &c->didx, &c->auxc, &c->aidx, &c->ncig, &c->coff, &c->nb, &c->boff, &c->rpos,
                    &c->krec, &c->keys, &c->vals, &c->keys2, &c->vals2, &c->head, &c->tmp, &c->sq, &c->sqi, &c->sv,
                    &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack};
@@ -757,6 +769,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_aux) (void)hipHostFree(c->h_aux);
     if (c->st) (void)hipStreamDestroy(c->st);
+    if (c->cst) (void)hipStreamDestroy(c->cst);
     delete c;
 }
 
@@ -766,15 +779,32 @@ extern "C" void dd_ctx_times(const dd_ctx *c, double *ms) {
     ms[2] = c->ms_parse;
 }
 
-// inflate a run's blocks (h_comp: pinned, readable 64 bytes past comp_len)
-// and find its records: starts[0..n_starts) are record offsets in the
-// inflated stream (the first = the run's first record), u_end its end
-extern "C" int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
+// a run's compressed bytes (pinned, readable 64 bytes past comp_len) into the
+// device slot, on the copy stream: returns at once; the host buffer must stay
+// untouched until a dd_run_load of the slot has returned
+extern "C" int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_t comp_len, char *err, int errlen) {
+    if (slot < 0 || slot >= DD_SLOTS) return -1;
+    DCK(hipSetDevice(c->device));
+    hipStream_t cs = c->cst ? c->cst : c->st;
+    DGROW(c->dcomp[slot], (size_t)comp_len + 64);
+    DCK(hipMemcpyAsync(c->dcomp[slot].p, h_comp, (size_t)comp_len + 64, hipMemcpyHostToDevice, cs));
+    DCK(hipEventRecord(c->cev[slot], cs));
+    c->dcomp_len[slot] = comp_len;
+    return 0;
+}
+
+// inflate a run's blocks (uploaded to `slot` by dd_comp_upload) and find its
+// records: starts[0..n_starts) are record offsets in the inflated stream (the
+// first = the run's first record), u_end its end
+extern "C" int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
                            int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int32_t tid,
                            int64_t *n_rec, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
     hipStream_t st = c->st;
-    DGROW(c->comp, (size_t)comp_len + 64);
+    if (slot < 0 || slot >= DD_SLOTS || c->dcomp_len[slot] != comp_len) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: slot %d does not hold the run", slot);
+        return -1;
+    }
     DGROW(c->blk, sizeof(DdBlock) * (size_t)(nblk + 1));
     DGROW(c->U, (size_t)ubytes + 64);
     DGROW(c->status, (size_t)nblk + 1);
@@ -782,14 +812,14 @@ extern "C" int dd_run_load(dd_ctx *c, const uint8_t *h_comp, int64_t comp_len, c
     DGROW(c->S, sizeof(int64_t) * (size_t)(n_starts + 1));
     DGROW(c->ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
     DGROW(c->cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
-    DCK(hipMemcpyAsync(c->comp.p, h_comp, (size_t)comp_len + 64, hipMemcpyHostToDevice, st));
+    DCK(hipStreamWaitEvent(st, c->cev[slot], 0));
     DCK(hipMemcpyAsync(c->blk.p, h_blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
     DCK(hipMemcpyAsync(c->S.p, h_starts, sizeof(int64_t) * (size_t)n_starts, hipMemcpyHostToDevice, st));
     DCK(hipMemcpyAsync(P<int64_t>(c->S) + n_starts, &u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
     DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
     uint32_t *bad = P<uint32_t>(c->misc);
     DCK(hipEventRecord(c->ev[0], st));
-    if (dd_inflate_launch(st, P<uint8_t>(c->comp), P<DdBlock>(c->blk), nblk, P<uint8_t>(c->U), P<uint8_t>(c->status),
+    if (dd_inflate_launch(st, P<uint8_t>(c->dcomp[slot]), P<DdBlock>(c->blk), nblk, P<uint8_t>(c->U), P<uint8_t>(c->status),
                           bad + 1)) {
         if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
         return -1;

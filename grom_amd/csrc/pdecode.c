@@ -434,6 +434,8 @@ struct pd_session {
     int n_dw, dw_started;
     double c_gpu_ms[3];    /* inflate, record walk, parse (HIP events, summed) */
     int io_threads;
+    int64_t insert_cap;    /* PD_INSERT_CAP (GROM_TEST_INSERT_CAP: tests of both decoders against each other) */
+    int64_t prefix_records; /* GROM_TEST_PREFIX_RECORDS: the stats prefix's record target (tests) */
     /* uploader scratch */
     uint32_t *remap;
     int64_t remap_cap;
@@ -1242,13 +1244,13 @@ static int stage_acquire(pd_session *s, int dev, int k, grom_stage **out) {
 
 static void stats_take(pd_session *s, pd_piece *p) {
     if (s->stats_done || !p->stats) return;
-    for (int64_t i = 0; i < p->st_n && s->s_n < PD_INSERT_CAP; i++) {
+    for (int64_t i = 0; i < p->st_n && s->s_n < s->insert_cap; i++) {
         s->s_ins[s->s_n] = p->st_ins[i];
         s->s_lq[s->s_n] = p->st_lq[i];
         s->s_n++;
-        if (s->s_n == PD_INSERT_CAP) s->s_m += p->st_m[i];
+        if (s->s_n == s->insert_cap) s->s_m += p->st_m[i];
     }
-    if (s->s_n < PD_INSERT_CAP) s->s_m += p->m_total;
+    if (s->s_n < s->insert_cap) s->s_m += p->m_total;
 }
 
 static void piece_free_stats(pd_piece *p) {
@@ -1639,7 +1641,7 @@ static void *uploader_main(void *arg) {
             s->c_records += p->n_rec;
             stats_take(s, p);
             piece_free_stats(p);
-            if (!s->stats_done && s->s_n >= PD_INSERT_CAP) mark_stats_done(s);
+            if (!s->stats_done && s->s_n >= s->insert_cap) mark_stats_done(s);
         }
         const pd_run *run = &s->runs[p->run];
         if (p->buf && run->chrom < 0) { /* decoded for a chromosome the final plan dropped */
@@ -1983,8 +1985,12 @@ pd_session *pd_open(const char *bam_path, const bam_hdr *hdr, const pd_chrom_in 
     s->n_threads = n_threads < 1 ? 1 : n_threads;
     s->window = 2 * s->n_threads + 4;
     s->max_bufs = s->window + s->n_threads / 2 + 8;
-    s->s_ins = (int32_t *)malloc(sizeof(int32_t) * PD_INSERT_CAP);
-    s->s_lq = (int32_t *)malloc(sizeof(int32_t) * PD_INSERT_CAP);
+    s->insert_cap = PD_INSERT_CAP;
+    if (getenv("GROM_TEST_INSERT_CAP") && atoll(getenv("GROM_TEST_INSERT_CAP")) > 0)
+        s->insert_cap = atoll(getenv("GROM_TEST_INSERT_CAP"));
+    if (getenv("GROM_TEST_PREFIX_RECORDS")) s->prefix_records = atoll(getenv("GROM_TEST_PREFIX_RECORDS"));
+    s->s_ins = (int32_t *)malloc(sizeof(int32_t) * (size_t)s->insert_cap);
+    s->s_lq = (int32_t *)malloc(sizeof(int32_t) * (size_t)s->insert_cap);
     if (!s->s_ins || !s->s_lq) FAIL("out of memory");
     pthread_mutex_init(&s->mu, NULL);
     pthread_cond_init(&s->cv, NULL);
@@ -2025,17 +2031,35 @@ void pd_set_wanted(pd_session *s, const int *want) {
 }
 
 /* ================= device mode: whole runs decoded on the GPUs ================= */
+/* A worker's compressed runs are read one ahead by its prefetch thread: the
+ * run's bytes by pread into a pinned slot, its block table and record starts
+ * on the host, and the copy to the device slot of the same number started on
+ * the decode context's copy stream -- all while the GPU inflates and parses
+ * the run before it.  The worker takes a slot, loads it (dd_run_load) and
+ * releases it; a run nobody takes is simply read again when needed. */
+enum { PF_FREE = 0, PF_WANTED = 1, PF_READY = 2, PF_USED = 3 };
+typedef struct {
+    int ri, state, rc;
+    char err[200];
+    uint8_t *comp;           /* pinned compressed run (+64 readable bytes) */
+    int64_t comp_cap, len;
+    DdBlock *blk;
+    int64_t blk_cap, nb, ub;
+    int64_t *starts;
+    int64_t starts_cap, m, u_end;
+    double t_io;
+} pf_slot;
+
 typedef struct {
     pd_session *s;
     int device, first;       /* first: this worker also gathers the insert statistics */
     int sub, nsub;           /* this device's chromosomes taken in turn by nsub workers */
     dd_ctx *dd;
-    uint8_t *comp;           /* pinned compressed run (+64 readable bytes) */
-    int64_t comp_cap;
-    DdBlock *blk;
-    int64_t blk_cap;
-    int64_t *starts;
-    int64_t starts_cap;
+    pf_slot slot[2];
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    pthread_t pf_thr;
+    int pf_started, pf_stop;
     int loaded;              /* run index whose records dd holds, -1 none */
     int64_t loaded_R;
 } dd_worker;
@@ -2091,18 +2115,49 @@ static int cmp_i64(const void *a, const void *b) {
     return x < y ? -1 : x > y;
 }
 
-/* a run's compressed bytes into the worker's pinned buffer, its block table
- * and record starts, then dd_run_load (inflate + record walk on the GPU) */
-static int dw_load(dd_worker *w, int ri, char *err, int errlen) {
-    pd_session *s = w->s;
+/* The insert statistics need the first PD_INSERT_CAP qualifying records in
+ * file order (find_insert_mean, GROM.c:1205-1318) -- about half of the
+ * records qualify (one mate of each proper pair), so at 30x the first 40% of
+ * chr1's run.  The first stats load is that prefix of the run: its end a
+ * linear-index record start (a record boundary the index names) at the share
+ * of the run's 16 kb windows that holds ~2.6x the cap's records.  UINT64_MAX:
+ * no prefix (the run is small, or the index gives no cut inside it). */
+static uint64_t stats_prefix_end(const pd_session *s, int ri) {
     const pd_run *r = &s->runs[ri];
+    const int64_t want = s->prefix_records > 0 ? s->prefix_records : (int64_t)(2.6 * s->insert_cap);
+    if (r->tid < 0 || r->tid >= s->n_tgt || r->count < 0 || r->count <= want + want / 4) return UINT64_MAX;
+    const int nl = s->n_lin[r->tid];
+    int lo = -1, hi = -1; /* the run's linear entries */
+    for (int k = 0; k < nl; k++) {
+        const uint64_t v = s->lin[r->tid][k];
+        if (v <= r->vbeg || v >= r->vend) continue;
+        if (lo < 0) lo = k;
+        hi = k;
+    }
+    if (lo < 0) return UINT64_MAX;
+    const int k = lo + (int)((double)(hi - lo) * (double)want / (double)r->count);
+    for (int q = k; q <= hi; q++) { /* the first entry at or after k inside the run */
+        const uint64_t v = s->lin[r->tid][q];
+        if (v > r->vbeg && v < r->vend) return v;
+    }
+    return UINT64_MAX;
+}
+
+/* a run's compressed bytes into a pinned slot, its block table and record
+ * starts, and the slot's copy to the device started (prefetch thread); key =
+ * the run, or -(run + 2) for its insert-statistics prefix */
+static int pf_read(dd_worker *w, pf_slot *sl, int slot_no, int key, char *err, int errlen) {
+    pd_session *s = w->s;
+    const int ri = key >= 0 ? key : -key - 2;
+    const pd_run *r = &s->runs[ri];
+    const uint64_t vend = key >= 0 ? r->vend : stats_prefix_end(s, ri);
     const int64_t c0 = (int64_t)(r->vbeg >> 16);
     int64_t c1;
-    if (r->vend == UINT64_MAX) {
+    if (vend == UINT64_MAX) {
         c1 = s->file_size;
     } else {
-        c1 = (int64_t)(r->vend >> 16);
-        if ((r->vend & 0xffff) != 0) { /* the block holding the end is part of the range */
+        c1 = (int64_t)(vend >> 16);
+        if ((vend & 0xffff) != 0) { /* the block holding the end is part of the range */
             uint8_t h[18];
             if (pread(s->fd, h, 18, (off_t)c1) != 18) { snprintf(err, (size_t)errlen, "cannot read a block header"); return -2; }
             const int xlen = h[10] | (h[11] << 8);
@@ -2112,61 +2167,171 @@ static int dw_load(dd_worker *w, int ri, char *err, int errlen) {
     }
     const int64_t len = c1 - c0;
     if (len <= 0 || c1 > s->file_size) { snprintf(err, (size_t)errlen, "bad run range"); return -2; }
-    if (len + 64 > w->comp_cap) {
-        grom_pinned_free(w->comp);
-        w->comp_cap = len + len / 8 + 4096;
-        w->comp = (uint8_t *)grom_pinned_alloc((size_t)w->comp_cap);
-        if (!w->comp) { w->comp_cap = 0; snprintf(err, (size_t)errlen, "no pinned memory for a run"); return -1; }
+    if (len + 64 > sl->comp_cap) {
+        grom_pinned_free(sl->comp);
+        sl->comp_cap = len + len / 8 + 4096;
+        sl->comp = (uint8_t *)grom_pinned_alloc((size_t)sl->comp_cap);
+        if (!sl->comp) { sl->comp_cap = 0; snprintf(err, (size_t)errlen, "no pinned memory for a run"); return -1; }
     }
     const double t0 = now_s();
-    if (pread_par(s->fd, w->comp, len, c0, s->io_threads)) { snprintf(err, (size_t)errlen, "reading the BAM failed"); return -1; }
-    memset(w->comp + len, 0, 64);
-    const double t1 = now_s();
+    if (pread_par(s->fd, sl->comp, len, c0, s->io_threads)) { snprintf(err, (size_t)errlen, "reading the BAM failed"); return -1; }
+    memset(sl->comp + len, 0, 64);
+    sl->t_io = now_s() - t0;
     int64_t ub = 0;
-    int64_t nb = dd_block_table(w->comp, len, NULL, 0, &ub);
+    int64_t nb = dd_block_table(sl->comp, len, NULL, 0, &ub);
     if (nb <= 0) { snprintf(err, (size_t)errlen, "the run is not whole BGZF blocks"); return -2; }
-    if (nb > w->blk_cap) {
-        free(w->blk);
-        w->blk_cap = nb + nb / 4 + 16;
-        w->blk = (DdBlock *)malloc(sizeof(DdBlock) * (size_t)w->blk_cap);
-        if (!w->blk) { w->blk_cap = 0; return -1; }
+    if (nb > sl->blk_cap) {
+        free(sl->blk);
+        sl->blk_cap = nb + nb / 4 + 16;
+        sl->blk = (DdBlock *)malloc(sizeof(DdBlock) * (size_t)sl->blk_cap);
+        if (!sl->blk) { sl->blk_cap = 0; return -1; }
     }
-    dd_block_table(w->comp, len, w->blk, nb, &ub);
+    dd_block_table(sl->comp, len, sl->blk, nb, &ub);
     /* record starts: the run's first record, then every linear-index offset inside the run */
     const int64_t u0 = (int64_t)(r->vbeg & 0xffff);
     int64_t u_end = ub;
-    if (r->vend != UINT64_MAX && (r->vend & 0xffff) != 0) u_end = w->blk[nb - 1].out_off + (int64_t)(r->vend & 0xffff);
+    if (vend != UINT64_MAX && (vend & 0xffff) != 0) u_end = sl->blk[nb - 1].out_off + (int64_t)(vend & 0xffff);
     const int nl = (r->tid >= 0 && r->tid < s->n_tgt) ? s->n_lin[r->tid] : 0;
-    if (nl + 2 > w->starts_cap) {
-        free(w->starts);
-        w->starts_cap = nl + 64;
-        w->starts = (int64_t *)malloc(sizeof(int64_t) * (size_t)w->starts_cap);
-        if (!w->starts) { w->starts_cap = 0; return -1; }
+    if (nl + 2 > sl->starts_cap) {
+        free(sl->starts);
+        sl->starts_cap = nl + 64;
+        sl->starts = (int64_t *)malloc(sizeof(int64_t) * (size_t)sl->starts_cap);
+        if (!sl->starts) { sl->starts_cap = 0; return -1; }
     }
     int64_t ns = 0;
-    w->starts[ns++] = u0;
+    sl->starts[ns++] = u0;
     for (int k = 0; k < nl; k++) {
         const uint64_t v = s->lin[r->tid][k];
-        if (v < r->vbeg || v >= r->vend) continue;
+        if (v < r->vbeg || v >= vend) continue;
         const int64_t cb = (int64_t)(v >> 16) - c0;
         int64_t lo = 0, hi = nb - 1; /* the block starting at cb */
         while (lo < hi) {
             const int64_t mid = (lo + hi + 1) / 2;
-            if (w->blk[mid].c_off <= cb) lo = mid;
+            if (sl->blk[mid].c_off <= cb) lo = mid;
             else hi = mid - 1;
         }
-        if (w->blk[lo].c_off != cb) continue;
-        const int64_t u = w->blk[lo].out_off + (int64_t)(v & 0xffff);
-        if (u > u0 && u < u_end) w->starts[ns++] = u;
+        if (sl->blk[lo].c_off != cb) continue;
+        const int64_t u = sl->blk[lo].out_off + (int64_t)(v & 0xffff);
+        if (u > u0 && u < u_end) sl->starts[ns++] = u;
     }
-    qsort(w->starts, (size_t)ns, sizeof(int64_t), cmp_i64);
+    qsort(sl->starts, (size_t)ns, sizeof(int64_t), cmp_i64);
     int64_t m = 0;
     for (int64_t k = 0; k < ns; k++)
-        if (m == 0 || w->starts[k] != w->starts[m - 1]) w->starts[m++] = w->starts[k];
+        if (m == 0 || sl->starts[k] != sl->starts[m - 1]) sl->starts[m++] = sl->starts[k];
+    sl->len = len;
+    sl->nb = nb;
+    sl->ub = ub;
+    sl->m = m;
+    sl->u_end = u_end;
+    return dd_comp_upload(w->dd, slot_no, sl->comp, len, err, errlen) ? -1 : 0;
+}
+
+static void *pf_main(void *arg) {
+    dd_worker *w = (dd_worker *)arg;
+    pthread_mutex_lock(&w->mu);
+    for (;;) {
+        int q = -1;
+        for (int k = 0; k < 2 && q < 0; k++)
+            if (w->slot[k].state == PF_WANTED) q = k;
+        if (q < 0) {
+            if (w->pf_stop) break;
+            pthread_cond_wait(&w->cv, &w->mu);
+            continue;
+        }
+        pf_slot *sl = &w->slot[q];
+        const int ri = sl->ri;
+        pthread_mutex_unlock(&w->mu);
+        char err[200] = "";
+        pd_trace(w->s, PD_EV_PHASE, 101, 0);
+        const int rc = pf_read(w, sl, q, ri, err, (int)sizeof(err));
+        pd_trace(w->s, PD_EV_PHASE, 101, 1);
+        pthread_mutex_lock(&w->mu);
+        sl->rc = rc;
+        snprintf(sl->err, sizeof(sl->err), "%s", err);
+        sl->state = PF_READY;
+        pthread_cond_broadcast(&w->cv);
+    }
+    pthread_mutex_unlock(&w->mu);
+    return NULL;
+}
+
+/* ask for run ri to be read ahead (no-op when it is already asked for or no
+ * slot is free) */
+static void pf_want(dd_worker *w, int ri) {
+    if (ri < 0) return;
+    pthread_mutex_lock(&w->mu);
+    int have = 0, q = -1;
+    for (int k = 0; k < 2; k++) {
+        if (w->slot[k].ri == ri && w->slot[k].state != PF_FREE) have = 1;
+        if (q < 0 && (w->slot[k].state == PF_FREE || w->slot[k].state == PF_READY)) q = k;
+    }
+    if (!have && q >= 0) {
+        w->slot[q].ri = ri;
+        w->slot[q].state = PF_WANTED;
+        pthread_cond_broadcast(&w->cv);
+    }
+    pthread_mutex_unlock(&w->mu);
+}
+
+/* the slot holding run ri, read (waits); NULL with err set on failure */
+static pf_slot *pf_take(dd_worker *w, int ri, int *slot_no, int *rc, char *err, int errlen) {
+    pthread_mutex_lock(&w->mu);
+    int q = -1;
+    for (;;) {
+        q = -1;
+        for (int k = 0; k < 2; k++)
+            if (w->slot[k].ri == ri && (w->slot[k].state == PF_WANTED || w->slot[k].state == PF_READY)) q = k;
+        if (q >= 0) break;
+        for (int k = 0; k < 2 && q < 0; k++)
+            if (w->slot[k].state == PF_FREE || w->slot[k].state == PF_READY) q = k;
+        if (q >= 0) {
+            w->slot[q].ri = ri;
+            w->slot[q].state = PF_WANTED;
+            pthread_cond_broadcast(&w->cv);
+            break;
+        }
+        pthread_cond_wait(&w->cv, &w->mu); /* both slots busy: wait for a release */
+    }
+    while (w->slot[q].state == PF_WANTED) pthread_cond_wait(&w->cv, &w->mu);
+    pf_slot *sl = &w->slot[q];
+    sl->state = PF_USED;
+    *rc = sl->rc;
+    if (sl->rc) snprintf(err, (size_t)errlen, "%s", sl->err);
+    pthread_mutex_unlock(&w->mu);
+    *slot_no = q;
+    return sl;
+}
+
+static void pf_release(dd_worker *w, pf_slot *sl) {
+    pthread_mutex_lock(&w->mu);
+    sl->state = PF_FREE;
+    sl->ri = -1;
+    pthread_cond_broadcast(&w->cv);
+    pthread_mutex_unlock(&w->mu);
+}
+
+/* a run's records loaded on the device (inflate + record walk), its
+ * compressed bytes from the prefetcher; then `next` (the run this worker
+ * needs after it, -1 none) is asked for */
+static int dw_load(dd_worker *w, int key, int next, char *err, int errlen) {
+    pd_session *s = w->s;
+    const int ri = key >= 0 ? key : -key - 2;
+    const pd_run *r = &s->runs[ri];
+    int q = 0, rc = 0;
+    const double tw = now_s();
+    pf_slot *sl = pf_take(w, key, &q, &rc, err, errlen);
+    const double t1 = now_s();
+    if (rc) { pf_release(w, sl); return rc; }
+    pf_want(w, next);
     int64_t R = 0;
-    const int rc = dd_run_load(w->dd, w->comp, len, w->blk, nb, ub, w->starts, m, u_end, r->tid, &R, err, errlen);
+    pd_trace(s, PD_EV_PHASE, 102, 0);
+    rc = dd_run_load(w->dd, q, sl->len, sl->blk, sl->nb, sl->ub, sl->starts, sl->m, sl->u_end, r->tid, &R, err, errlen);
+    pd_trace(s, PD_EV_PHASE, 102, 1);
+    const int64_t len = sl->len, ub = sl->ub;
+    const double tio = sl->t_io;
+    pf_release(w, sl);
     if (rc) return rc;
-    if (r->count >= 0 && R != r->count) {
+    if (key >= 0 && r->count >= 0 && R != r->count) {
         snprintf(err, (size_t)errlen, "target %d: %lld records decoded, the index counts %lld", r->tid, (long long)R,
                  (long long)r->count);
         return -2;
@@ -2175,28 +2340,47 @@ static int dw_load(dd_worker *w, int ri, char *err, int errlen) {
     s->c_records += R;
     s->c_inflated += ub;
     s->c_compressed += len;
-    s->c_io_s += t1 - t0;
+    s->c_io_s += tio;
+    s->c_wait_s += t1 - tw;
     s->c_dec_s += now_s() - t1;
     pthread_mutex_unlock(&s->mu);
-    w->loaded = ri;
+    w->loaded = key;  /* a prefix (key < -1) is never taken for the whole run */
     w->loaded_R = R;
     return 0;
+}
+
+/* the next run (tid >= 0) after ri in file order, -1 none */
+static int next_placed_run(const pd_session *s, int ri) {
+    for (int i = ri + 1; i < s->n_runs; i++)
+        if (s->runs[i].tid >= 0) return i;
+    return -1;
 }
 
 /* find_insert_mean's sample, runs in file order until the cap (worker of the
  * first device) */
 static int dw_stats(dd_worker *w, char *err, int errlen) {
     pd_session *s = w->s;
-    for (int i = 0; i < s->n_runs && s->s_n < PD_INSERT_CAP && !s->abort; i++) {
+    int first = 1;
+    for (int i = 0; i < s->n_runs && s->s_n < s->insert_cap && !s->abort; i++) {
         if (s->runs[i].tid < 0) continue; /* unplaced: unmapped records only */
-        int rc = dw_load(w, i, err, errlen);
-        if (rc) return rc;
-        int64_t taken = 0, m = 0;
-        rc = dd_run_stats(w->dd, s->min_mapq_stats, PD_INSERT_CAP - s->s_n, s->s_ins + s->s_n, s->s_lq + s->s_n, &taken,
-                          &m, err, errlen);
-        if (rc) return rc;
-        s->s_n += taken;
-        s->s_m += m;
+        /* the first run: its prefix, then (if the cap was not reached there)
+         * the whole run, counted from its start again */
+        const int pre = first && stats_prefix_end(s, i) != UINT64_MAX;
+        first = 0;
+        for (int pass = pre ? 0 : 1; pass < 2; pass++) {
+            int rc = dw_load(w, pass == 0 ? -i - 2 : i, pass == 0 ? i : next_placed_run(s, i), err, errlen);
+            if (rc) return rc;
+            int64_t taken = 0, m = 0;
+            const int64_t left = s->insert_cap - s->s_n;
+            pd_trace(s, PD_EV_PHASE, 103, i);
+            rc = dd_run_stats(w->dd, s->min_mapq_stats, left, s->s_ins + s->s_n, s->s_lq + s->s_n, &taken, &m, err,
+                              errlen);
+            if (rc) return rc;
+            if (pass == 0 && taken < left) continue; /* the prefix held too few: the whole run */
+            s->s_n += taken;
+            s->s_m += m;
+            break;
+        }
     }
     mark_stats_done(s);
     return 0;
@@ -2204,7 +2388,7 @@ static int dw_stats(dd_worker *w, char *err, int errlen) {
 
 /* one processed chromosome: its run parsed into a stage, the split-read
  * alignments parsed on the host, the walk's trims (chrom_finalize's facts) */
-static int dw_chrom(dd_worker *w, int k, char *err, int errlen) {
+static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
     pd_session *s = w->s;
     pd_chrom *c = &s->ch[k];
     if (stage_acquire(s, w->device, k, &c->stage)) { snprintf(err, (size_t)errlen, "no stage"); return -1; }
@@ -2213,7 +2397,9 @@ static int dw_chrom(dd_worker *w, int k, char *err, int errlen) {
     memset(&po, 0, sizeof(po));
     int64_t j0 = 0;
     if (ri >= 0) {
-        int rc = (w->loaded == ri) ? 0 : dw_load(w, ri, err, errlen);
+        int rc = 0;
+        if (w->loaded == ri) pf_want(w, next_run);
+        else rc = dw_load(w, ri, next_run, err, errlen);
         if (rc) return rc;
         j0 = s->runs[ri].j0;
         rc = dd_run_parse(w->dd, j0, s->runs[ri].tid, s->read_name_len, s->plan[k].len, c->stage, &po, err, errlen);
@@ -2307,8 +2493,19 @@ static void *dw_main(void *arg) {
     pd_session *s = w->s;
     char err[300] = "";
     int rc = 0;
+    pd_trace(s, PD_EV_PHASE, 100, 0);
     w->dd = dd_ctx_new(w->device);
+    pd_trace(s, PD_EV_PHASE, 100, 1);
     if (!w->dd) { rc = -1; snprintf(err, sizeof(err), "device decode: no context on device %d", w->device); }
+    if (rc == 0) w->pf_started = pthread_create(&w->pf_thr, NULL, pf_main, w) == 0;
+    if (rc == 0 && !w->pf_started) { rc = -1; snprintf(err, sizeof(err), "device decode: no prefetch thread"); }
+    /* this worker's chromosomes in order (the final plan's keep[] only drops some) */
+    int *mine = (int *)malloc(sizeof(int) * (size_t)(s->n_plan > 0 ? s->n_plan : 1)), n_mine = 0;
+    for (int k = 0, ord = 0; k < s->n_plan; k++) {
+        if (!s->want[k] || s->ch[k].device != w->device) continue;
+        if (ord++ % w->nsub == w->sub) mine[n_mine++] = k;
+    }
+    if (rc == 0 && !w->first && n_mine > 0) pf_want(w, s->ch[mine[0]].run);
     if (rc == 0 && w->first) rc = dw_stats(w, err, (int)sizeof(err));
     /* the final plan (which chromosomes, which records each one's run starts with) */
     if (rc == 0) {
@@ -2322,13 +2519,16 @@ static void *dw_main(void *arg) {
             if (need) apply_final(s, 0);
         }
     }
-    for (int k = 0, ord = 0; rc == 0 && k < s->n_plan && !s->abort; k++) {
+    for (int i = 0; rc == 0 && i < n_mine && !s->abort; i++) {
+        const int k = mine[i];
         pd_chrom *c = &s->ch[k];
-        if (!s->keep[k] || !s->want[k] || c->device != w->device) continue;
-        if (ord++ % w->nsub != w->sub) continue;
+        if (!s->keep[k]) continue;
+        int next_run = -1;
+        for (int j = i + 1; j < n_mine && next_run < 0; j++)
+            if (s->keep[mine[j]]) next_run = s->ch[mine[j]].run;
         const double t0 = now_s();
         pd_trace(s, PD_EV_UPLOAD, k, 0);
-        rc = dw_chrom(w, k, err, (int)sizeof(err));
+        rc = dw_chrom(w, k, next_run, err, (int)sizeof(err));
         pd_trace(s, PD_EV_UPLOAD, k, 1);
         pthread_mutex_lock(&s->mu);
         s->c_upl_s += now_s() - t0;
@@ -2347,11 +2547,23 @@ static void *dw_main(void *arg) {
         for (int q = 0; q < 3; q++) s->c_gpu_ms[q] += ms[q];
         pthread_mutex_unlock(&s->mu);
     }
+    free(mine);
+    if (w->pf_started) {
+        pthread_mutex_lock(&w->mu);
+        w->pf_stop = 1;
+        pthread_cond_broadcast(&w->cv);
+        pthread_mutex_unlock(&w->mu);
+        pthread_join(w->pf_thr, NULL);
+    }
     /* the scans may still read the stages; the decode context goes now */
     dd_ctx_free(w->dd);
-    grom_pinned_free(w->comp);
-    free(w->blk);
-    free(w->starts);
+    for (int q = 0; q < 2; q++) {
+        grom_pinned_free(w->slot[q].comp);
+        free(w->slot[q].blk);
+        free(w->slot[q].starts);
+    }
+    pthread_mutex_destroy(&w->mu);
+    pthread_cond_destroy(&w->cv);
     free(w);
     return NULL;
 }
@@ -2381,6 +2593,9 @@ static int pd_start_device(pd_session *s) {
         w->nsub = per;
         w->first = q == 0;
         w->loaded = -1;
+        w->slot[0].ri = w->slot[1].ri = -1;
+        pthread_mutex_init(&w->mu, NULL);
+        pthread_cond_init(&w->cv, NULL);
         if (pthread_create(&s->dw[q], NULL, dw_main, w) != 0) {
             free(w);
             sess_abort(s, 0, "cannot start device decode workers");

@@ -739,3 +739,31 @@ def test_oracle_digest_cases(datadir, case):
     run_grom(d, "genome.bam", "genome.fa", "o.vcf", rec["cli_flags"])
     assert _sha_rows(d / "o.vcf") == (rec["vcf_sha256"], rec["vcf_rows"])
     assert _sha_rows(d / "o.ctx.vcf") == (rec["ctx_sha256"], rec["ctx_rows"])
+
+
+def test_device_decode_stats_prefix(datadir, capfd):
+    """The device decoder takes the insert statistics (find_insert_mean,
+    GROM.c:1205-1318: the first 10^7 qualifying records in file order) from a
+    prefix of the first run, cut at a linear-index record start, and falls back
+    to the whole run when the prefix holds too few.  With the cap lowered for
+    the test (GROM_TEST_INSERT_CAP, read by both decoders) a prefix that holds
+    the cap and one that does not both give the host decoder's insert line,
+    staged inputs and outputs."""
+    bam, fa = synth(datadir, "c3_genome", CASES["c3_genome"])
+    extra = ["-M", "-V", "1"]
+    common = {"GROM_TEST_INSERT_CAP": "20000", "GROM_STAGE_DIGEST": "1", "GROM_VERBOSE": "1"}
+    modes = {"host": {"GROM_DEVICE_DECODE": "0"},
+             "prefix_holds": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_PREFIX_RECORDS": "60000"},
+             "prefix_short": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_PREFIX_RECORDS": "15000"}}
+    got = {}
+    for mode, env in modes.items():
+        capfd.readouterr()
+        run_grom(datadir, bam, fa, f"pfx_{mode}.vcf", extra, env_extra=dict(common, **env))
+        out = capfd.readouterr().out
+        ins = [l for l in out.splitlines() if l.startswith(("insert mean", "insert_min_size", "median read"))]
+        stages = sorted(l for l in out.splitlines() if l.startswith("stage "))
+        vcf = open(datadir / f"pfx_{mode}.vcf").read() + open(datadir / f"pfx_{mode}.ctx.vcf").read()
+        got[mode] = (ins, stages, vcf)
+    assert got["host"][0] and got["host"][1]
+    for mode in modes:
+        assert got[mode] == got["host"], mode
