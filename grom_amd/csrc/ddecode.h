@@ -38,8 +38,12 @@ int64_t grom_inflate_device_selftest(const char *bam_path, int device, int64_t m
 typedef struct dd_ctx dd_ctx;
 dd_ctx *dd_ctx_new(int device);
 void dd_ctx_free(dd_ctx *c);
-/* summed HIP-event times of the parsed runs: inflate, record walk, parse */
-void dd_ctx_times(const dd_ctx *c, double ms[3]);
+/* summed HIP-event times of the parsed runs: inflate, record walk, parse;
+ * ms[3]: wall time of decode buffer growth so far (every context) */
+void dd_ctx_times(const dd_ctx *c, double ms[4]);
+/* the per-run device buffers sized for a run of `ubytes` inflated bytes and
+ * `recs` records (growth later frees buffers, which waits for the device) */
+int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, char *err, int errlen);
 /* a run's compressed bytes (h_comp pinned, 64 readable bytes past comp_len)
  * copied into device slot 0/1 on the context's copy stream; returns at once,
  * h_comp must stay untouched until a dd_run_load of the slot has returned */
@@ -73,6 +77,9 @@ int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_name_len, int6
 /* kept reads and dropped records at positions below s0 (the walk's skip
  * prefix) in a staged chromosome (positions sorted) */
 int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64_t *sd);
+
+/* wall time of a device allocation (stage growth), added to dd_ctx_times' ms[3] */
+void grom_note_alloc_ns(int64_t ns);
 
 /* stage helpers for device-side fills (scan.hip) */
 /* a stage holding exactly sz's counts (n_aux = capacity, the count starts at

@@ -8,6 +8,7 @@
 // as they are (20 GB per genome) and the GPU inflates them.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -214,14 +215,19 @@ struct DBuf {
     size_t cap = 0;
 };
 
+std::atomic<int64_t> g_dgrow_ns{0};  // time in buffer growth (hipFree + hipMalloc), all contexts and stages
+
 int dgrow(DBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.cap = 0;
     const size_t want = bytes + bytes / 8 + 256;
-    if (hipMalloc(&b.p, want) != hipSuccess) return -1;
+    const hipError_t e = hipMalloc(&b.p, want);
+    g_dgrow_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (e != hipSuccess) return -1;
     b.cap = want;
     return 0;
 }
@@ -234,6 +240,14 @@ enum : uint32_t { DB_INFLATE = 1, DB_CHAIN = 2, DB_RECORD = 4, DB_TID = 8, DB_UN
 __device__ __forceinline__ uint32_t ldu32(const uint8_t *U, int64_t o) {
     return (uint32_t)U[o] | (uint32_t)U[o + 1] << 8 | (uint32_t)U[o + 2] << 16 | (uint32_t)U[o + 3] << 24;
 }
+
+__device__ __forceinline__ uint32_t ldu32a(const uint8_t *U, int64_t p) {  // unaligned, from aligned words
+    const uint32_t *a = (const uint32_t *)(U + (p & ~(int64_t)3));
+    const uint32_t sh = (uint32_t)(p & 3) * 8;
+    const uint32_t w0 = a[0], w1 = a[1];
+    return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+}
+
 
 // the 36-byte record header at o (block_size .. tlen) as 9 words, from 10
 // aligned word loads
@@ -488,6 +502,42 @@ struct StageOut {
     int64_t *dbef;
 };
 
+// FNV-1a of a read name (up to lqn bytes, stopping at its NUL) and its
+// length; the bytes come 32 at a time from eight independent word loads
+__device__ __forceinline__ int name_hash(const uint8_t *U, int64_t p, int lqn, uint64_t &hs) {
+    hs = 0xcbf29ce484222325ULL;
+    int L = 0;
+    for (int base = 0; base < lqn; base += 32) {
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[k] = ldu32a(U, p + base + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+            if (base + k >= lqn || c == 0) return L;
+            hs = (hs ^ c) * 0x100000001b3ULL;
+            L++;
+        }
+    }
+    return L;
+}
+
+// names at a and b equal up to their NUL (or lqn bytes of a)
+__device__ __forceinline__ bool name_equal(const uint8_t *U, int64_t a, int64_t b, int lqn) {
+    for (int base = 0; base < 256; base += 32) {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) { x[k] = ldu32a(U, a + base + 4 * k); y[k] = ldu32a(U, b + base + 4 * k); }
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            const uint32_t cx = (x[k >> 2] >> (8 * (k & 3))) & 0xffu, cy = (y[k >> 2] >> (8 * (k & 3))) & 0xffu;
+            if (cx != cy) return false;
+            if (cx == 0 || base + k + 1 >= lqn) return true;
+        }
+    }
+    return true;
+}
+
 // the kept reads' fields, CIGAR words and name hashes; the dropped records;
 // the split-read candidates' record indices; the stream's last record
 __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__restrict__ off, int64_t R, int64_t j0,
@@ -525,12 +575,8 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
                 if ((op & 15u) == GC_HARD_CLIP) hc += (int32_t)(op >> 4);
             }
             // name: up to its NUL (pdecode.c buf_intern); empty or >= read_name_len: id 0 (GROM.c:6813)
-            uint64_t hs = 0xcbf29ce484222325ULL;
-            int L = 0;
-            while (L < lqn && U[o + 36 + L]) {
-                hs = (hs ^ U[o + 36 + L]) * 0x100000001b3ULL;
-                L++;
-            }
+            uint64_t hs = 0;
+            const int L = name_hash(U, o + 36, lqn, hs);
             keys[i] = (L == 0 || L >= read_name_len) ? 0ull : (mix64(hs ^ (uint64_t)L * 0x9e3779b97f4a7c15ULL) | 1ull);
             vals[i] = i;
             if (auxc[r]) acand[aidx[r]] = r;
@@ -556,24 +602,69 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
     }
 }
 
-// one wave per kept read (grid-stride): its packed bases and qualities, and
-// the zero pad byte after an odd-length read's qualities
-__global__ void k_copy_bases(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
-                             const int64_t *__restrict__ krec, int64_t n, const int64_t *__restrict__ boff,
-                             uint8_t *__restrict__ seq, uint8_t *__restrict__ qual) {
+// Packed bases and qualities of the kept reads.  A read's regions tile the
+// stage arrays with no gaps (quality bytes [b, b + nb), bases [b/2, b/2 +
+// nb/2), nb = l_qseq rounded up to even, the pad quality byte 0), so a wave
+// takes 64 reads at once: each lane loads one read's header fields, then the
+// wave copies the reads one after another, a lane per destination dword --
+// aligned source dwords joined by a byte shift, whole dwords stored; only the
+// dwords a region shares with its neighbours take byte stores.
+// dest bytes [dst, dst + len) from src; dword k of the region's dword span for
+// lane k (k < n_dw); `pad`: byte len - 1 is the zero pad, not a source byte
+__device__ __forceinline__ void cp_region(const uint8_t *U, int64_t src, uint8_t *dst_base, int64_t dst, int64_t len,
+                                          int64_t k, bool pad) {
+    const int64_t d0 = dst & ~(int64_t)3;
+    const int64_t D = d0 + 4 * k;
+    const int64_t lo = D < dst ? dst : D, hi = D + 4 < dst + len ? D + 4 : dst + len;
+    if (lo >= hi) return;
+    uint32_t v = ldu32a(U, src + (D - dst));
+    if (pad && hi == dst + len) v &= ~(0xffu << (8 * (uint32_t)(dst + len - 1 - D)));
+    if (lo == D && hi == D + 4) {
+        *(uint32_t *)(dst_base + D) = v;
+    } else {
+        for (int64_t x = lo; x < hi; x++) dst_base[x] = (uint8_t)(v >> (8 * (uint32_t)(x - D)));
+    }
+}
+
+__device__ __forceinline__ int64_t rl64(int64_t v, int j) {  // lane j's value (j wave-uniform)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__global__ void __launch_bounds__(256) k_copy_bases(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
+                                                    const int64_t *__restrict__ krec, int64_t n,
+                                                    const int64_t *__restrict__ boff, uint8_t *__restrict__ seq,
+                                                    uint8_t *__restrict__ qual) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t i = w0; i < n; i += nw) {
-        const int64_t o = off[krec[i]];
-        const int lqn = U[o + 12], nc = (int)(U[o + 16] | (U[o + 17] << 8));
-        const int32_t lq = (int32_t)ldu32(U, o + 20);
-        const int64_t s = o + 36 + lqn + 4 * (int64_t)nc;
-        const int64_t ns = (lq + 1) / 2;
-        const int64_t b = boff[i];
-        for (int64_t k = lane; k < ns; k += 64) seq[b / 2 + k] = U[s + k];
-        for (int64_t k = lane; k < lq; k += 64) qual[b + k] = U[s + ns + k];
-        if ((lq & 1) && lane == 0) qual[b + lq] = 0;
+    for (int64_t g = w0 * 64; g < n; g += nw * 64) {
+        // lane j: read g + j's source offset, length and destination
+        const int64_t i = g + lane;
+        int64_t src = 0, b = 0;
+        int32_t lq = 0;
+        if (i < n) {
+            const int64_t o = off[krec[i]];
+            const uint32_t h3 = ldu32a(U, o + 12), h4 = ldu32a(U, o + 16);
+            lq = (int32_t)ldu32a(U, o + 20);
+            src = o + 36 + (int64_t)(h3 & 0xff) + 4 * (int64_t)(h4 & 0xffff);
+            b = boff[i];
+        }
+        const int m = n - g < 64 ? (int)(n - g) : 64;
+        for (int j = 0; j < m; j++) {
+            const int64_t s_j = rl64(src, j), b_j = rl64(b, j);
+            const int32_t lq_j = __builtin_amdgcn_readlane(lq, j);
+            const int64_t ns = (lq_j + 1) / 2, nb = 2 * ns;
+            // bases: dst b/2, ns bytes; qualities: dst b, nb bytes (the last a pad when lq is odd)
+            const int64_t sd0 = (b_j / 2) & ~(int64_t)3, sdn = ((b_j / 2 + ns + 3) & ~(int64_t)3) - sd0;
+            const int64_t qd0 = b_j & ~(int64_t)3, qdn = ((b_j + nb + 3) & ~(int64_t)3) - qd0;
+            const int64_t n_s = sdn / 4, n_q = qdn / 4;
+            for (int64_t k = lane; k < n_s + n_q; k += 64) {
+                if (k < n_s) cp_region(U, s_j, seq, b_j / 2, ns, k, false);
+                else cp_region(U, s_j + ns, qual, b_j, nb, k - n_s, (lq_j & 1) != 0);
+            }
+        }
     }
 }
 
@@ -588,12 +679,8 @@ __global__ void k_name_ids(const uint8_t *__restrict__ U, const int64_t *__restr
         const uint32_t hp = head[p];
         nid[i] = hp + 1;
         if (hp == (uint32_t)p) continue;
-        const int64_t a = off[krec[i]] + 36, b = off[krec[vals[hp]]] + 36;
-        for (int k = 0;; k++) {
-            const uint8_t x = U[a + k], y = U[b + k];
-            if (x != y) { atomicOr(bad, DB_NAMES); break; }
-            if (!x) break;
-        }
+        const int64_t oa = off[krec[i]];
+        if (!name_equal(U, oa + 36, off[krec[vals[hp]]] + 36, U[oa + 12])) atomicOr(bad, DB_NAMES);
     }
 }
 
@@ -773,10 +860,28 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     delete c;
 }
 
+extern "C" void grom_note_alloc_ns(int64_t ns) { g_dgrow_ns += ns; }
+
 extern "C" void dd_ctx_times(const dd_ctx *c, double *ms) {
     ms[0] = c->ms_inflate;
     ms[1] = c->ms_walk;
     ms[2] = c->ms_parse;
+    ms[3] = (double)g_dgrow_ns.load() / 1e6;
+}
+
+// the per-run buffers sized once for the largest run (ubytes inflated bytes,
+// recs records): growing them later frees the old buffer, which waits for the
+// whole device
+extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, char *err, int errlen) {
+    DCK(hipSetDevice(c->device));
+    DGROW(c->U, (size_t)ubytes + 64);
+    const size_t r4 = 4 * (size_t)(recs + 1), r8 = 8 * (size_t)(recs + 1);
+    DGROW(c->off, r8);
+    DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
+    DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
+    DGROW(c->rpos, r4); DGROW(c->krec, r8); DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8);
+    DGROW(c->vals2, r4); DGROW(c->head, r4);
+    return 0;
 }
 
 // a run's compressed bytes (pinned, readable 64 bytes past comp_len) into the

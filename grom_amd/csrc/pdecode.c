@@ -432,7 +432,7 @@ struct pd_session {
     int n_tgt;
     pthread_t *dw;
     int n_dw, dw_started;
-    double c_gpu_ms[3];    /* inflate, record walk, parse (HIP events, summed) */
+    double c_gpu_ms[4];    /* inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
     int io_threads;
     int64_t insert_cap;    /* PD_INSERT_CAP (GROM_TEST_INSERT_CAP: tests of both decoders against each other) */
     int64_t prefix_records; /* GROM_TEST_PREFIX_RECORDS: the stats prefix's record target (tests) */
@@ -2349,6 +2349,48 @@ static int dw_load(dd_worker *w, int key, int next, char *err, int errlen) {
     return 0;
 }
 
+static int next_placed_run(const pd_session *s, int ri);
+
+/* The decode buffers sized once, while the first run is read: the largest
+ * record count the index gives for a run this worker may load, and its
+ * largest compressed span times the inflate ratio of the BAM's first blocks
+ * (+15%).  A run beyond the estimate still grows the buffers. */
+static int dw_reserve(dd_worker *w, char *err, int errlen) {
+    pd_session *s = w->s;
+    int64_t recs = 0, span = 0;
+    for (int i = 0; i < s->n_runs; i++) {
+        const pd_run *r = &s->runs[i];
+        if (r->tid < 0) continue;
+        if (r->count > recs) recs = r->count;
+        const int64_t c1 = r->vend == UINT64_MAX ? s->file_size : (int64_t)(r->vend >> 16) + 65536;
+        const int64_t sp = c1 - (int64_t)(r->vbeg >> 16);
+        if (sp > span) span = sp;
+    }
+    if (recs == 0 || span == 0) return 0;
+    /* the inflate ratio of up to 1 MB of whole blocks from the first run's start */
+    const int r0 = next_placed_run(s, -1);
+    if (r0 < 0) return 0;
+    const int64_t c0 = (int64_t)(s->runs[r0].vbeg >> 16);
+    int64_t n = s->file_size - c0 < ((int64_t)1 << 20) ? s->file_size - c0 : ((int64_t)1 << 20);
+    uint8_t *b = (uint8_t *)malloc((size_t)n);
+    if (!b) return 0;
+    int64_t got = pread(s->fd, b, (size_t)n, (off_t)c0), csum = 0, usum = 0;
+    for (int64_t o = 0; got > 0 && o + 18 <= got;) {
+        const uint8_t *h = b + o;
+        if (h[0] != 0x1f || h[1] != 0x8b || h[12] != 'B' || h[13] != 'C') break;
+        const int64_t bl = (int64_t)(h[16] | (h[17] << 8)) + 1;
+        if (o + bl > got) break;
+        csum += bl;
+        usum += (int64_t)((uint32_t)b[o + bl - 4] | (uint32_t)b[o + bl - 3] << 8 | (uint32_t)b[o + bl - 2] << 16 |
+                          (uint32_t)b[o + bl - 1] << 24);
+        o += bl;
+    }
+    free(b);
+    if (csum <= 0 || usum <= 0) return 0;
+    const int64_t ub = (int64_t)((double)span * (double)usum / (double)csum * 1.15);
+    return dd_reserve(w->dd, ub, recs + recs / 20, err, errlen);
+}
+
 /* the next run (tid >= 0) after ri in file order, -1 none */
 static int next_placed_run(const pd_session *s, int ri) {
     for (int i = ri + 1; i < s->n_runs; i++)
@@ -2506,6 +2548,11 @@ static void *dw_main(void *arg) {
         if (ord++ % w->nsub == w->sub) mine[n_mine++] = k;
     }
     if (rc == 0 && !w->first && n_mine > 0) pf_want(w, s->ch[mine[0]].run);
+    if (rc == 0 && w->first) { /* the stats prefix first: start its read now */
+        const int r0 = next_placed_run(s, -1);
+        if (r0 >= 0) pf_want(w, stats_prefix_end(s, r0) != UINT64_MAX ? -r0 - 2 : r0);
+    }
+    if (rc == 0 && dw_reserve(w, err, (int)sizeof(err))) rc = -1;
     if (rc == 0 && w->first) rc = dw_stats(w, err, (int)sizeof(err));
     /* the final plan (which chromosomes, which records each one's run starts with) */
     if (rc == 0) {
@@ -2541,10 +2588,11 @@ static void *dw_main(void *arg) {
     }
     if (rc == -2 || rc == -1) sess_abort(s, rc == -2, err);
     if (w->dd) {
-        double ms[3];
+        double ms[4];
         dd_ctx_times(w->dd, ms);
         pthread_mutex_lock(&s->mu);
         for (int q = 0; q < 3; q++) s->c_gpu_ms[q] += ms[q];
+        s->c_gpu_ms[3] = ms[3];
         pthread_mutex_unlock(&s->mu);
     }
     free(mine);
@@ -2727,7 +2775,7 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
     c->h2d_bytes = s->c_h2d;
     c->inflate_s = s->c_inflate_s;
     c->device = s->dev_mode;
-    for (int q = 0; q < 3; q++) c->gpu_ms[q] = s->c_gpu_ms[q];
+    for (int q = 0; q < 4; q++) c->gpu_ms[q] = s->c_gpu_ms[q];
     c->io_s = s->c_io_s;
     c->upload_s = s->c_upl_s;
     c->wait_s = s->c_wait_s;

@@ -99,7 +99,7 @@ typedef struct pd_counters {
     double decode_thread_s, inflate_s, upload_s, wait_s, io_s;
     int threads, libdeflate;
     int device;          /* runs decoded on the GPU (device mode) */
-    double gpu_ms[3];    /* device mode: inflate, record walk, parse (HIP events, summed) */
+    double gpu_ms[4];    /* device mode: inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
 } pd_counters;
 void pd_get_counters(pd_session *s, pd_counters *c);
 void pd_close(pd_session *s);

@@ -1107,6 +1107,7 @@ static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t ke
         tot += (cap[k] + 255) & ~(size_t)255;
     }
     char *nb = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     if (hipMalloc((void **)&nb, tot) != hipSuccess) {
         set_err("grom_stage: hipMalloc(%zu) failed", tot);
         return GROM_E_NOMEM;
@@ -1117,6 +1118,7 @@ static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t ke
         HIPCHK(hipStreamSynchronize(s->st));
         (void)hipFree(s->blk);
     }
+    grom_note_alloc_ns(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
     s->blk = nb;
     s->blk_cap = tot;
     memcpy(s->off, off, sizeof(off));

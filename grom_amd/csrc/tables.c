@@ -9,10 +9,12 @@
  * full precision and passed through the same "%e" round trip here.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "../../include/grom_amd.h"
 
@@ -70,15 +72,17 @@ static double through_text(double v) {
     return strtod(b, NULL);
 }
 
-void grom_build_tables(int32_t min_mapq, double *hez, double *mq) {
-    memset(hez, 0, sizeof(double) * NT * NT);
-    memset(mq, 0, sizeof(double) * NT * NT);
+/* One row of both tables: the upper tails, GROM's clamps, the mq tails and
+ * the text round trip.  Rows depend only on themselves (the clamp reads the
+ * row's next tail and its own clamped previous column, the mq stop rule the
+ * row's previous columns), so rows are built on threads. */
+static void build_row(int r, double p, double *hez, double *mq) {
 #define H(r, c) hez[(size_t)(r) * NT + (c)]
 #define M(r, c) mq[(size_t)(r) * NT + (c)]
-    for (int64_t n = 1; n < NT; n++)
-        for (int64_t s = 0; s <= n; s++) H(n, s) = upper_tail(n, s, 0.5, 17);
+    if (r >= 1)
+        for (int64_t s = 0; s <= r; s++) H(r, s) = upper_tail(r, s, 0.5, 17);
     /* turn the upper tail into P(X <= c) with GROM's clamps (GROM.c:21309-21324) */
-    for (int r = 0; r < GROM_MAX_TRIALS; r++) {
+    if (r < GROM_MAX_TRIALS) {
         for (int c = 0; c < GROM_MAX_TRIALS; c++) {
             double v = 1.0 - H(r, c + 1);
             if (v < 0) v = 0;
@@ -87,18 +91,58 @@ void grom_build_tables(int32_t min_mapq, double *hez, double *mq) {
         }
         H(r, GROM_MAX_TRIALS) = 1.0;
     }
-    double p = pow(10, (-min_mapq / 10.0)); /* g_mq_prob, GROM.c:21616 */
-    for (int64_t n = 1; n < NT; n++)
-        for (int64_t s = 0; s <= n; s++) {
-            int stop = (s > 0 && M(n, s - 1) == 0) || (s > 1 && M(n, s - 1) == M(n, s - 2));
-            M(n, s) = stop ? 0 : upper_tail(n, s, p, 20);
+    if (r >= 1)
+        for (int64_t s = 0; s <= r; s++) {
+            int stop = (s > 0 && M(r, s - 1) == 0) || (s > 1 && M(r, s - 1) == M(r, s - 2));
+            M(r, s) = stop ? 0 : upper_tail(r, s, p, 20);
         }
-    for (size_t i = 0; i < (size_t)NT * NT; i++) {
+    for (size_t i = (size_t)r * NT; i < (size_t)(r + 1) * NT; i++) {
         hez[i] = through_text(hez[i]);
         mq[i] = through_text(mq[i]);
     }
 #undef H
 #undef M
+}
+
+typedef struct {
+    double p, *hez, *mq;
+    int next;
+    pthread_mutex_t mu;
+} table_job;
+
+static void *table_main(void *arg) {
+    table_job *j = (table_job *)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        const int r = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (r >= NT) break;
+        /* rows taken longest first (row r costs ~r entries) */
+        build_row(NT - 1 - r, j->p, j->hez, j->mq);
+    }
+    return NULL;
+}
+
+void grom_build_tables(int32_t min_mapq, double *hez, double *mq) {
+    memset(hez, 0, sizeof(double) * NT * NT);
+    memset(mq, 0, sizeof(double) * NT * NT);
+    table_job j;
+    j.p = pow(10, (-min_mapq / 10.0)); /* g_mq_prob, GROM.c:21616 */
+    j.hez = hez;
+    j.mq = mq;
+    j.next = 0;
+    pthread_mutex_init(&j.mu, NULL);
+    long nc = sysconf(_SC_NPROCESSORS_ONLN);
+    int nt = nc < 1 ? 1 : (nc > 16 ? 16 : (int)nc);
+    pthread_t th[16];
+    int started = 0;
+    for (int t = 1; t < nt; t++) {
+        if (pthread_create(&th[started], NULL, table_main, &j) != 0) break;
+        started++;
+    }
+    table_main(&j);
+    for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&j.mu);
 }
 
 void grom_default_params(grom_params *p) {
