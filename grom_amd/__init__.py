@@ -113,6 +113,7 @@ _SIGS = {
     "grom_dev_init": (C.c_int, [C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
     "grom_dev_fini": (None, [C.c_int]),
     "grom_ctx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(Params), C.c_void_p, C.c_void_p]),
+    "grom_ctx_set_params": (C.c_int, [C.c_int, C.POINTER(Params)]),
     "grom_scan_chrom": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Out), C.POINTER(Stats)]),
     "grom_scan_chrom_device": (C.c_int, [C.c_int, C.POINTER(Chrom), C.POINTER(Reads), C.POINTER(Out),
                                          C.POINTER(Stats)]),

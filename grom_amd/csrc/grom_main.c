@@ -1116,6 +1116,9 @@ static int run_streamed(cli_state *S) {
     int lseq = 0, imin = 0, imax = 0;
     long mapped = 0;
     const double t_started = clock_gettime_s();
+    /* the scan contexts while the head of the BAM is decoded (their insert
+     * parameters are set once the statistics are known) */
+    const int ws_fail = setup_workers(S);
     const int imean = pd_insert_stats(pd, grom_prob2(S->num_sd), P->min_mapq, &lseq, &imin, &imax, &mapped);
     if (imean < 0) {
         const int fallback = imean == -2;
@@ -1149,7 +1152,9 @@ static int run_streamed(cli_state *S) {
     pthread_t fthr;
     int fasta_started = 0;
     double t_ctx = 0.0;
-    if (setup_workers(S)) { status = 1; goto done; }
+    if (ws_fail) { status = 1; goto done; }
+    for (int d = 0; d < S->n_init; d++)
+        if (grom_ctx_set_params(d, &S->P) != GROM_OK) { status = 1; goto done; }
     t_ctx = clock_gettime_s();
     vcf = fopen(S->out_name, "w");
     if (!vcf) { printf("Error opening file %s\n", S->out_name); status = 1; goto done; }

@@ -2351,6 +2351,72 @@ static int dw_load(dd_worker *w, int key, int next, char *err, int errlen) {
 
 static int next_placed_run(const pd_session *s, int ri);
 
+/* Stages reserved ahead: the first chromosomes' stages would otherwise be
+ * allocated (hipMalloc of ~15 GB each at 30x) on the decode's critical path.
+ * A helper thread sizes every stage of the device for the largest run while
+ * the insert statistics load: reads from the index's record count, bases and
+ * CIGAR words per record from the first 2,000 records of the file. */
+typedef struct {
+    pd_session *s;
+    int device;
+} stres_job;
+
+static void *stres_main(void *arg) {
+    stres_job *j = (stres_job *)arg;
+    pd_session *s = j->s;
+    int64_t recs = 0, ref = 0;
+    for (int i = 0; i < s->n_runs; i++)
+        if (s->runs[i].tid >= 0 && s->runs[i].count > recs) recs = s->runs[i].count;
+    for (int k = 0; k < s->n_plan; k++)
+        if (s->ch[k].device == j->device && s->want[k] && s->plan[k].len > ref) ref = s->plan[k].len;
+    const int r0 = next_placed_run(s, -1);
+    if (recs <= 0 || r0 < 0) return NULL;
+    pd_reader r;
+    memset(&r, 0, sizeof(r));
+    inf_init(&r.inf);
+    int64_t n = 0, lq = 0, nc = 0;
+    if (rd_open(&r, s->fd, s->file_size, s->runs[r0].vbeg, UINT64_MAX) == 0) {
+        while (n < 2000 && rd_avail(&r, 4) == 1) {
+            const int32_t bs = ldi32(r.ub + r.ub_pos);
+            if (bs < 32 || rd_avail(&r, 4 + (int64_t)bs) != 1) break;
+            const uint8_t *q = r.ub + r.ub_pos + 4;
+            lq += ldi32(q + 16) > 0 ? ldi32(q + 16) : 0;
+            nc += ld16(q + 12);
+            n++;
+            r.ub_pos += 4 + (int64_t)bs;
+        }
+    }
+    rd_free(&r);
+    if (n == 0) return NULL;
+    grom_stage_sizes est;
+    memset(&est, 0, sizeof(est));
+    est.n = recs;
+    est.n_drop = recs / 4 + 1024;
+    est.n_bases = (int64_t)((double)recs * ((double)lq / (double)n + 1.0) * 1.05);
+    est.n_cigar_ops = (int64_t)((double)recs * (double)nc / (double)n * 1.1) + 1024;
+    est.n_aux = recs / 16 + 1024;
+    est.ref_len = ref;
+    pthread_mutex_lock(&s->mu);
+    int ns = s->n_stage;
+    grom_stage *mine[64];
+    int m = 0;
+    for (int i = 0; i < ns && m < 64; i++)
+        if (s->stage_dev[i] == j->device && !s->stage_busy[i]) mine[m++] = s->stages[i];
+    pthread_mutex_unlock(&s->mu);
+    /* a stage's bytes, roughly: the read SoA, CIGAR words,
+     * qualities + packed bases, dropped records, the reference; stages are
+     * reserved while the device keeps room for the scan contexts (two
+     * chromosome scratches) beside them */
+    const double bytes = 48.0 * (double)est.n + 4.0 * (double)est.n_cigar_ops + 1.5 * (double)est.n_bases +
+                         16.0 * (double)est.n_drop + (double)est.ref_len;
+    for (int i = 0; i < m; i++) {
+        const int64_t fr = grom_device_mem_free(j->device);
+        if (fr < 0 || (double)fr < bytes + 3.0 * bytes + (double)((int64_t)32 << 30)) break;
+        (void)grom_stage_begin(mine[i], &est);
+    }
+    return NULL;
+}
+
 /* The decode buffers sized once, while the first run is read: the largest
  * record count the index gives for a run this worker may load, and its
  * largest compressed span times the inflate ratio of the BAM's first blocks
@@ -2552,8 +2618,13 @@ static void *dw_main(void *arg) {
         const int r0 = next_placed_run(s, -1);
         if (r0 >= 0) pf_want(w, stats_prefix_end(s, r0) != UINT64_MAX ? -r0 - 2 : r0);
     }
+    pthread_t stres_thr;
+    stres_job sj = {s, w->device};
+    const int stres = rc == 0 && w->sub == 0 && getenv("GROM_NO_STAGE_RESERVE") == NULL &&
+                      pthread_create(&stres_thr, NULL, stres_main, &sj) == 0;
     if (rc == 0 && dw_reserve(w, err, (int)sizeof(err))) rc = -1;
     if (rc == 0 && w->first) rc = dw_stats(w, err, (int)sizeof(err));
+    if (stres) pthread_join(stres_thr, NULL); /* the stages are the worker's again */
     /* the final plan (which chromosomes, which records each one's run starts with) */
     if (rc == 0) {
         pthread_mutex_lock(&s->mu);

@@ -882,6 +882,15 @@ int grom_ctx_init(int slot, int device, const grom_params *params, const double 
     return GROM_OK;
 }
 
+int grom_ctx_set_params(int slot, const grom_params *params) {
+    if (slot < 0 || slot >= 64 || !params || !g_ctx[slot].init) {
+        set_err("grom_ctx_set_params: bad argument");
+        return GROM_E_ARG;
+    }
+    g_ctx[slot].prm = *params;
+    return GROM_OK;
+}
+
 int grom_dev_init(int device, const grom_params *params, const double *hez, const double *mq) {
     return grom_ctx_init(device, device, params, hez, mq);
 }

@@ -242,6 +242,9 @@ int grom_dev_init(int device, const grom_params *params, const double *hez_table
  * threads (two chromosomes in flight per GPU).  Device-resident reads from
  * grom_upload in one slot may be scanned from another slot on the same GPU. */
 int grom_ctx_init(int slot, int device, const grom_params *params, const double *hez_table, const double *mq_table);
+/* replace an initialised context's parameters (e.g. once the insert statistics
+ * are known: the CLI creates its contexts while the BAM's head is decoded) */
+int grom_ctx_set_params(int slot, const grom_params *params);
 void grom_dev_fini(int device);
 
 /* Scan one chromosome whose reads are in host memory; appends its VCF rows to
