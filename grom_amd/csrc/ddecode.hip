@@ -25,7 +25,7 @@
 
 // One BGZF block per lane: blk[j] = {offset of its DEFLATE data in `comp`,
 // its length, offset of its output in `out`, ISIZE}.  status[j] = GI_* code.
-__global__ void __launch_bounds__(DD_LANES) k_inflate(const uint8_t *__restrict__ comp, const DdBlock *__restrict__ blk,
+__global__ void __launch_bounds__(DD_LANES, 2) k_inflate(const uint8_t *__restrict__ comp, const DdBlock *__restrict__ blk,
                                                       int64_t n_blk, uint8_t *__restrict__ out,
                                                       uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad) {
     extern __shared__ uint32_t dd_tab[];  // GI_LANE_DWORDS x DD_LANES: rows element-major across the lanes

@@ -62,7 +62,7 @@
 
 enum { GI_OK = 0, GI_E_HEADER = 1, GI_E_TREE = 2, GI_E_CODE = 3, GI_E_DIST = 4, GI_E_OVERRUN = 5, GI_E_INPUT = 6,
        GI_E_SIZE = 7 };
-enum { GI_M_HDR = 0, GI_M_SYM = 1, GI_M_COPY = 2, GI_M_STORED = 3, GI_M_DONE = 4 };
+enum { GI_M_HDR = 0, GI_M_SYM = 1, GI_M_COPY = 2, GI_M_STORED = 3, GI_M_DONE = 4, GI_M_P1 = 5, GI_M_P2 = 6 };
 
 GI_FN uint32_t gi_rev15(uint32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -261,10 +261,73 @@ GI_FN int gi_cl_item(GiBits &b, int s, int prev, int &val) {
     return s == 17 ? 3 + (int)gi_bits(b, 3) : 11 + (int)gi_bits(b, 7);
 }
 
-// A block header (after a refill): the next mode (GI_M_SYM with lit/dist
-// built, or GI_M_STORED with *rem bytes), or -GI_E_*.
+// The fixed codes (RFC 1951 3.2.6) straight into the tables: literal/length
+// code lengths 8 (0-143), 9 (144-255), 7 (256-279), 8 (280-287), so the
+// sorted order is 256-279, 0-143, 280-287, 144-255; distances all 5 bits.
 template <int LANES>
-GI_FN int gi_header(GiBits &b, GiHuff &lit, GiHuff &dist, uint32_t *tab, int lane, uint32_t &bfinal, uint32_t &rem) {
+GI_FN int gi_fixed(GiHuff &lit, GiHuff &dist, uint32_t *tab, int lane) {
+GI_UNROLL
+    for (int w = 0; w < 72; w++) {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; k++) {
+            const int i = 4 * w + k;
+            const int sym = i < 24 ? 256 + i : i < 168 ? i - 24 : i < 176 ? 280 + (i - 168) : 144 + (i - 176);
+            v |= (uint32_t)(sym & 0xff) << (8 * k);
+        }
+        tab[(GI_T_LIT + w) * LANES + lane] = v;
+    }
+GI_UNROLL
+    for (int w = 0; w < 9; w++) tab[(GI_T_LITHI + w) * LANES + lane] = w == 0 ? 0x00ffffffu : (w == 5 ? 0x0000ff00u : 0u);
+GI_UNROLL
+    for (int w = 0; w < 8; w++)
+        tab[(GI_T_DIST + w) * LANES + lane] = (uint32_t)(4 * w) | (uint32_t)(4 * w + 1) << 8 | (uint32_t)(4 * w + 2) << 16 |
+                                              (uint32_t)(4 * w + 3) << 24;
+    uint32_t cn[16];
+GI_UNROLL
+    for (int l = 0; l < 16; l++) cn[l] = (l == 7 ? 24u : l == 8 ? 152u : l == 9 ? 112u : 0u) | (l == 5 ? 30u << 16 : 0u);
+    int rc = gi_code<15>(lit, cn, 0);
+    if (!rc) rc = gi_code<15>(dist, cn, 16);
+    return rc;
+}
+
+// A dynamic block's header in progress.  Its code lengths are read one
+// run-length item per step, twice: pass 1 counts the literal/length (low 16
+// bits of cn[l]) and distance (high 16 bits) code lengths; the counts are
+// checked and become each length's first sorted index; pass 2 reads the same
+// items again (from bit `at`) and places the symbols, leaving each length's
+// end index, from which the codes are formed.  A lane in a header thus takes
+// a few hundred short steps beside its wave's symbol steps, instead of holding
+// the whole wave for the header's length.  cn[] is the literal/length code's
+// register array (lit.e), which a header does not otherwise need.
+struct GiHdr {
+    GiHuffCL clh;
+    int at;  // bit offset of the code lengths in the block's data
+    int n, ntot, nlit, prev, eob;
+};
+
+// the bit reader positioned at bit `pos` of the data starting at `in`
+GI_FN void gi_seek(GiBits &b, const uint8_t *in, int pos) {
+    const int mis = (int)((uintptr_t)in & 3);
+    const uint32_t *base = (const uint32_t *)(in - mis);
+    const int abs = mis * 8 + pos, k = abs >> 5, r = abs & 31;
+    b.sh0 = mis * 8;
+    b.wp = base + k;
+    const uint32_t w0 = gi_ldw(b.wp);
+    b.nxt = gi_ldw(b.wp + 1);
+    b.wp += 2;
+    b.buf = (uint64_t)(w0 >> r);
+    b.cnt = 32 - r;
+    b.merged = k + 1;
+}
+
+// bits consumed so far
+GI_FN int64_t gi_used(const GiBits &b) { return b.merged * 32 - b.sh0 - b.cnt; }
+
+// the 3-bit block header and, for a dynamic block, its counts and the
+// code-length code (after a refill): the next mode or -GI_E_*
+template <int LANES>
+GI_FN int gi_header(GiBits &b, GiHuff &lit, GiHuff &dist, GiHdr &H, uint32_t *tab, int lane, uint32_t &bfinal,
+                    uint32_t &rem) {
     const uint32_t hdr = gi_bits(b, 3);
     bfinal = hdr & 1;
     const uint32_t btype = hdr >> 1;
@@ -279,19 +342,14 @@ GI_FN int gi_header(GiBits &b, GiHuff &lit, GiHuff &dist, uint32_t *tab, int lan
         return len ? GI_M_STORED : (bfinal ? GI_M_DONE : GI_M_HDR);
     }
     if (btype == 1) {  // fixed codes
-        int rc = gi_build<LANES, 15, true>(lit, tab, lane, GI_T_LIT, 288, [](int i) -> uint32_t {
-            return i < 144 ? 8u : (i < 256 ? 9u : (i < 280 ? 7u : 8u));
-        });
-        if (rc) return -rc;
-        rc = gi_build<LANES, 15, false>(dist, tab, lane, GI_T_DIST, 30, [](int) -> uint32_t { return 5u; });
+        const int rc = gi_fixed<LANES>(lit, dist, tab, lane);
         return rc ? -rc : GI_M_SYM;
     }
     if (btype != 2) return -GI_E_HEADER;
-    // dynamic codes
-    const int nlit = (int)gi_bits(b, 5) + 257;
+    H.nlit = (int)gi_bits(b, 5) + 257;
     const int ndist = (int)gi_bits(b, 5) + 1;
     const int ncl = (int)gi_bits(b, 4) + 4;
-    if (nlit > 286 || ndist > 30) return -GI_E_HEADER;
+    if (H.nlit > 286 || ndist > 30) return -GI_E_HEADER;
     // code-length code lengths, 3 bits each in the order
     // 16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15 (5 bits per entry in two
     // words), packed 3 bits per symbol
@@ -305,61 +363,82 @@ GI_FN int gi_header(GiBits &b, GiHuff &lit, GiHuff &dist, uint32_t *tab, int lan
         const int s = (int)((k < 12 ? ord_lo >> (5 * k) : ord_hi >> (5 * (k - 12))) & 31u);
         cl |= (uint64_t)v << (3 * s);
     }
-    GiHuffCL clh;
-    int rc = gi_build<LANES, 7, false>(clh, tab, lane, GI_T_CL, 19,
-                                       [cl](int i) -> uint32_t { return (uint32_t)(cl >> (3 * i)) & 7u; });
+    const int rc = gi_build<LANES, 7, false>(H.clh, tab, lane, GI_T_CL, 19,
+                                             [cl](int i) -> uint32_t { return (uint32_t)(cl >> (3 * i)) & 7u; });
     if (rc) return -rc;
-    // the literal/length and distance code lengths, run-length coded: counted
-    // in a first pass (literal/length counts in the low, distance counts in
-    // the high 16 bits of cn[l]), then decoded again to place the symbols
-    const int ntot = nlit + ndist;
-    const GiBits at = b;
-    uint32_t cn[16];
+    H.ntot = H.nlit + ndist;
+    H.at = (int)gi_used(b);
 GI_UNROLL
-    for (int l = 0; l < 16; l++) cn[l] = 0;
-    int n = 0, prev = -1;
-    bool eob = false;
-    while (n < ntot) {
-        gi_refill(b);
-        const int s = gi_decode<LANES, 7, false>(b, clh, tab, lane, GI_T_CL);
-        if (s < 0) return -GI_E_TREE;
-        int val;
-        const int rep = gi_cl_item(b, s, prev, val);
-        if (rep < 0 || n + rep > ntot) return -GI_E_TREE;
-        int rl = nlit - n;
+    for (int l = 0; l < 16; l++) lit.e[l] = 0;
+    H.n = 0;
+    H.prev = -1;
+    H.eob = 0;
+    return GI_M_P1;
+}
+
+// Kraft check of the 16-bit counts at bit `sh` of cnt[1..15] (an
+// over-subscribed set is GI_E_TREE; DEFLATE permits an incomplete one)
+GI_FN int gi_kraft(const uint32_t *cnt, int sh) {
+    int32_t left = 1;
+GI_UNROLL
+    for (int l = 1; l <= 15; l++) {
+        left = (left << 1) - (int32_t)((cnt[l] >> sh) & 0xffffu);
+        if (left < 0) return GI_E_TREE;
+    }
+    return GI_OK;
+}
+
+// one run-length item of the code lengths (after a refill): pass 1 or 2
+template <int LANES, bool PASS2>
+GI_FN int gi_cl_step(GiBits &b, const uint8_t *in, GiHuff &lit, GiHuff &dist, GiHdr &H, uint32_t *tab, int lane) {
+    uint32_t *cn = lit.e;
+    const int s = gi_decode<LANES, 7, false>(b, H.clh, tab, lane, GI_T_CL);
+    if (s < 0) return -GI_E_TREE;
+    int val;
+    const int rep = gi_cl_item(b, s, H.prev, val);
+    if (rep < 0 || H.n + rep > H.ntot) return -GI_E_TREE;
+    if (!PASS2) {
+        int rl = H.nlit - H.n;
         rl = rl < 0 ? 0 : (rl > rep ? rep : rl);
         const uint32_t add = (uint32_t)rl | (uint32_t)(rep - rl) << 16;
 GI_UNROLL
         for (int l = 1; l < 16; l++) cn[l] += (val == l) ? add : 0u;
-        if (val && n <= 256 && 256 < n + rep) eob = true;
-        n += rep;
-        prev = val;
-    }
-    if (!eob) return -GI_E_TREE;  // no end-of-block code (zlib refuses it too)
-    rc = gi_code<15>(lit, cn, 0);
-    if (rc) return -rc;
-    rc = gi_code<15>(dist, cn, 16);
-    if (rc) return -rc;
-    gi_clear_hi<LANES, true>(tab, lane);
-    b = at;
-    n = 0;
-    prev = -1;
-    while (n < ntot) {
-        gi_refill(b);
-        const int s = gi_decode<LANES, 7, false>(b, clh, tab, lane, GI_T_CL);
-        int val;
-        const int rep = gi_cl_item(b, s, prev, val);
-        if (val) {
-            for (int k = 0; k < rep; k++) {
-                const int i = n + k;
-                if (i < nlit) gi_place<LANES, 15, true>(tab, GI_T_LIT, lane, cn, 0, (uint32_t)val, i);
-                else gi_place<LANES, 15, false>(tab, GI_T_DIST, lane, cn, 16, (uint32_t)val, i - nlit);
-            }
+        if (val && H.n <= 256 && 256 < H.n + rep) H.eob = 1;
+    } else if (val) {
+        for (int k = 0; k < rep; k++) {
+            const int i = H.n + k;
+            if (i < H.nlit) gi_place<LANES, 15, true>(tab, GI_T_LIT, lane, cn, 0, (uint32_t)val, i);
+            else gi_place<LANES, 15, false>(tab, GI_T_DIST, lane, cn, 16, (uint32_t)val, i - H.nlit);
         }
-        n += rep;
-        prev = val;
     }
-    return GI_M_SYM;
+    H.n += rep;
+    H.prev = val;
+    if (H.n < H.ntot) return PASS2 ? GI_M_P2 : GI_M_P1;
+    if (PASS2) {
+        // cn[l] = each length's end index: the counts again, then both codes
+        // (the distance code first: the literal code is formed in place)
+        for (int l = 15; l >= 1; l--) cn[l] -= cn[l - 1];
+        int rc = gi_code<15>(dist, cn, 16);
+        if (!rc) rc = gi_code<15>(lit, cn, 0);
+        return rc ? -rc : GI_M_SYM;
+    }
+    // pass 1 done: the counts checked and turned into first sorted indices,
+    // then the items again from their start
+    if (!H.eob) return -GI_E_TREE;  // no end-of-block code (zlib refuses it too)
+    if (gi_kraft(cn, 0) || gi_kraft(cn, 16)) return -GI_E_TREE;
+    uint32_t off = 0;
+GI_UNROLL
+    for (int l = 1; l <= 15; l++) {
+        const uint32_t c = cn[l];
+        cn[l] = off;
+        off += c;  // both 16-bit fields at once: neither exceeds 286
+    }
+    cn[0] = 0;
+    gi_clear_hi<LANES, true>(tab, lane);
+    gi_seek(b, in, H.at);
+    H.n = 0;
+    H.prev = -1;
+    return GI_M_P2;
 }
 
 // Inflate one block's raw DEFLATE data (in[0..in_len)) into out[0..out_len).
@@ -371,6 +450,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
     GiBits b;
     gi_open(b, in);
     GiHuff lit = {}, dist = {};
+    GiHdr H = {};
     uint32_t o = 0, bfinal = 0;
     uint32_t rem = 0;  // bytes left of the match or stored block
     uint32_t D = 0;    // the match's current source distance (a multiple of its distance)
@@ -378,13 +458,21 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
     while (mode != GI_M_DONE) {
         gi_refill(b);
         if (mode == GI_M_HDR) {
-            const int m = gi_header<LANES>(b, lit, dist, tab, lane, bfinal, rem);
+            const int m = gi_header<LANES>(b, lit, dist, H, tab, lane, bfinal, rem);
             if (m < 0) {
                 rc = -m;
                 break;
             }
             if (m == GI_M_STORED && o + rem > out_len) {
                 rc = GI_E_OVERRUN;
+                break;
+            }
+            mode = m;
+        } else if (mode == GI_M_P1 || mode == GI_M_P2) {
+            const int m = mode == GI_M_P1 ? gi_cl_step<LANES, false>(b, in, lit, dist, H, tab, lane)
+                                          : gi_cl_step<LANES, true>(b, in, lit, dist, H, tab, lane);
+            if (m < 0) {
+                rc = -m;
                 break;
             }
             mode = m;
@@ -456,7 +544,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
     }
     if (rc) return rc;
     // consumed bits: every merged word minus the first word's lead and the buffer
-    const int64_t used_bits = b.merged * 32 - b.sh0 - b.cnt;
+    const int64_t used_bits = gi_used(b);
     if (used_bits > 8 * (int64_t)in_len) return GI_E_INPUT;
     if (o != out_len) return GI_E_SIZE;
     return GI_OK;
