@@ -632,6 +632,8 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int j) {  // lane j's value (
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+#define CP_UNROLL 8
+
 __global__ void __launch_bounds__(256) k_copy_bases(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
                                                     const int64_t *__restrict__ krec, int64_t n,
                                                     const int64_t *__restrict__ boff, uint8_t *__restrict__ seq,
@@ -652,17 +654,57 @@ __global__ void __launch_bounds__(256) k_copy_bases(const uint8_t *__restrict__ 
             b = boff[i];
         }
         const int m = n - g < 64 ? (int)(n - g) : 64;
-        for (int j = 0; j < m; j++) {
-            const int64_t s_j = rl64(src, j), b_j = rl64(b, j);
-            const int32_t lq_j = __builtin_amdgcn_readlane(lq, j);
-            const int64_t ns = (lq_j + 1) / 2, nb = 2 * ns;
-            // bases: dst b/2, ns bytes; qualities: dst b, nb bytes (the last a pad when lq is odd)
-            const int64_t sd0 = (b_j / 2) & ~(int64_t)3, sdn = ((b_j / 2 + ns + 3) & ~(int64_t)3) - sd0;
-            const int64_t qd0 = b_j & ~(int64_t)3, qdn = ((b_j + nb + 3) & ~(int64_t)3) - qd0;
-            const int64_t n_s = sdn / 4, n_q = qdn / 4;
-            for (int64_t k = lane; k < n_s + n_q; k += 64) {
-                if (k < n_s) cp_region(U, s_j, seq, b_j / 2, ns, k, false);
-                else cp_region(U, s_j + ns, qual, b_j, nb, k - n_s, (lq_j & 1) != 0);
+        // CP_UNROLL reads at a time: every source load of the group issued
+        // before its stores (the copies are latency-bound one read at a time)
+        for (int j0 = 0; j0 < m; j0 += CP_UNROLL) {
+            int64_t dst_[CP_UNROLL], len_[CP_UNROLL], sb_[CP_UNROLL], k_[CP_UNROLL];
+            uint8_t *base_[CP_UNROLL];
+            bool pad_[CP_UNROLL], on_[CP_UNROLL];
+            uint32_t w0_[CP_UNROLL], w1_[CP_UNROLL];
+#pragma unroll
+            for (int u = 0; u < CP_UNROLL; u++) {
+                const int j = j0 + u < m ? j0 + u : m - 1;
+                const int64_t s_j = rl64(src, j), b_j = rl64(b, j);
+                const int32_t lq_j = __builtin_amdgcn_readlane(lq, j);
+                const int64_t ns = (lq_j + 1) / 2, nb = 2 * ns;
+                // bases: dst b/2, ns bytes; qualities: dst b, nb bytes (the last a pad when lq is odd)
+                const int64_t n_s = (((b_j / 2 + ns + 3) & ~(int64_t)3) - ((b_j / 2) & ~(int64_t)3)) / 4;
+                const int64_t n_q = (((b_j + nb + 3) & ~(int64_t)3) - (b_j & ~(int64_t)3)) / 4;
+                const int64_t k = lane;
+                const bool sq = k < n_s;
+                dst_[u] = sq ? b_j / 2 : b_j;
+                len_[u] = sq ? ns : nb;
+                sb_[u] = sq ? s_j : s_j + ns;
+                k_[u] = sq ? k : k - n_s;
+                base_[u] = sq ? seq : qual;
+                pad_[u] = !sq && (lq_j & 1) != 0;
+                on_[u] = j0 + u < m && k < n_s + n_q && n_s + n_q <= 64;
+                const int64_t p = sb_[u] + ((dst_[u] & ~(int64_t)3) + 4 * k_[u] - dst_[u]);
+                const uint32_t *a = (const uint32_t *)(U + (p & ~(int64_t)3));
+                w0_[u] = on_[u] ? a[0] : 0u;
+                w1_[u] = on_[u] ? a[1] : 0u;
+                if (j0 + u < m && n_s + n_q > 64)  // a read over 64 dwords (l_qseq > ~250): plain loop
+                    for (int64_t kk = lane; kk < n_s + n_q; kk += 64) {
+                        if (kk < n_s) cp_region(U, s_j, seq, b_j / 2, ns, kk, false);
+                        else cp_region(U, s_j + ns, qual, b_j, nb, kk - n_s, (lq_j & 1) != 0);
+                    }
+            }
+#pragma unroll
+            for (int u = 0; u < CP_UNROLL; u++) {
+                if (!on_[u]) continue;
+                const int64_t d = dst_[u], L = len_[u];
+                const int64_t D = (d & ~(int64_t)3) + 4 * k_[u];
+                const int64_t lo = D < d ? d : D, hi = D + 4 < d + L ? D + 4 : d + L;
+                if (lo >= hi) continue;
+                const int64_t p = sb_[u] + (D - d);
+                const uint32_t sh = (uint32_t)(p & 3) * 8;
+                uint32_t v = sh ? (w0_[u] >> sh) | (w1_[u] << (32 - sh)) : w0_[u];
+                if (pad_[u] && hi == d + L) v &= ~(0xffu << (8 * (uint32_t)(d + L - 1 - D)));
+                if (lo == D && hi == D + 4) {
+                    *(uint32_t *)(base_[u] + D) = v;
+                } else {
+                    for (int64_t x = lo; x < hi; x++) base_[u][x] = (uint8_t)(v >> (8 * (uint32_t)(x - D)));
+                }
             }
         }
     }
