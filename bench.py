@@ -167,6 +167,9 @@ def whole_run(work, bam, fa, out, flags, env_extra=None, timeout=900):
     dt = time.perf_counter() - t0
     if r.returncode != 0:
         raise RuntimeError(f"grom failed ({r.returncode}): {r.stdout[-3000:]} {r.stderr[-3000:]}")
+    slow = [ln for ln in r.stderr.splitlines() if ln.startswith("grom:") and " took " in ln]
+    if slow:
+        log(f"{len(slow)} slow device allocations in the run: " + "; ".join(ln[6:] for ln in slow[:12]))
     return dt, r.stdout
 
 

@@ -79,7 +79,7 @@ int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_name_len, int6
 int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64_t *sd);
 
 /* wall time of a device allocation (stage growth), added to dd_ctx_times' ms[3] */
-void grom_note_alloc_ns(int64_t ns);
+void grom_note_alloc_ns(int64_t ns, size_t bytes);
 
 /* stage helpers for device-side fills (scan.hip) */
 /* a stage holding exactly sz's counts (n_aux = capacity, the count starts at

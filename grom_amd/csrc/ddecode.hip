@@ -226,7 +226,10 @@ int dgrow(DBuf &b, size_t bytes) {
     b.cap = 0;
     const size_t want = bytes + bytes / 8 + 256;
     const hipError_t e = hipMalloc(&b.p, want);
-    g_dgrow_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    g_dgrow_ns += ns;
+    if (ns > 20000000 && getenv("GROM_VERBOSE"))
+        fprintf(stderr, "grom: device buffer of %.2f GB took %.1f ms\n", (double)want / 1e9, ns / 1e6);
     if (e != hipSuccess) return -1;
     b.cap = want;
     return 0;
@@ -902,7 +905,11 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     delete c;
 }
 
-extern "C" void grom_note_alloc_ns(int64_t ns) { g_dgrow_ns += ns; }
+extern "C" void grom_note_alloc_ns(int64_t ns, size_t bytes) {
+    g_dgrow_ns += ns;
+    if (ns > 20000000 && getenv("GROM_VERBOSE"))
+        fprintf(stderr, "grom: stage buffer of %.2f GB took %.1f ms\n", (double)bytes / 1e9, ns / 1e6);
+}
 
 extern "C" void dd_ctx_times(const dd_ctx *c, double *ms) {
     ms[0] = c->ms_inflate;

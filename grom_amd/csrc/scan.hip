@@ -1127,7 +1127,8 @@ static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t ke
         HIPCHK(hipStreamSynchronize(s->st));
         (void)hipFree(s->blk);
     }
-    grom_note_alloc_ns(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+    grom_note_alloc_ns(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
+                       tot);
     s->blk = nb;
     s->blk_cap = tot;
     memcpy(s->off, off, sizeof(off));
