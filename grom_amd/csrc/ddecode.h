@@ -41,9 +41,10 @@ void dd_ctx_free(dd_ctx *c);
 /* summed HIP-event times of the parsed runs: inflate, record walk, parse;
  * ms[3]: wall time of decode buffer growth so far (every context) */
 void dd_ctx_times(const dd_ctx *c, double ms[4]);
-/* the per-run device buffers sized for a run of `ubytes` inflated bytes and
- * `recs` records (growth later frees buffers, which waits for the device) */
-int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, char *err, int errlen);
+/* the per-run device buffers sized for a run of `ubytes` inflated bytes,
+ * `recs` records and `n_starts` index-named record starts (growth later frees
+ * buffers, which waits for the device) */
+int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, char *err, int errlen);
 /* a run's compressed bytes (h_comp pinned, 64 readable bytes past comp_len)
  * copied into device slot 0/1 on the context's copy stream; returns at once,
  * h_comp must stay untouched until a dd_run_load of the slot has returned */

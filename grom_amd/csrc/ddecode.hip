@@ -921,15 +921,37 @@ extern "C" void dd_ctx_times(const dd_ctx *c, double *ms) {
 // the per-run buffers sized once for the largest run (ubytes inflated bytes,
 // recs records): growing them later frees the old buffer, which waits for the
 // whole device
-extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, char *err, int errlen) {
+extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
     DGROW(c->U, (size_t)ubytes + 64);
+    // the small buffers too: a small hipMalloc waits behind any large one in
+    // flight on another thread (the stage reservations), ~0.4 s at 30x
+    const int64_t nblk = ubytes / 60000 + 1024;
+    DGROW(c->blk, sizeof(DdBlock) * (size_t)(nblk + 1));
+    DGROW(c->status, (size_t)nblk + 1);
+    DGROW(c->misc, 256);
+    DGROW(c->S, sizeof(int64_t) * (size_t)(n_starts + 1));
+    DGROW(c->ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
+    DGROW(c->cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
+    {
+        size_t tb = 0, t2 = 0, t3 = 0, t4 = 0;
+        const int r = (int)std::min<int64_t>(recs + 1, INT32_MAX);
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, r, c->st));
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (int64_t *)nullptr, (int64_t *)nullptr, r, c->st));
+        DCK(hipcub::DeviceRadixSort::SortPairs(nullptr, t3, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                               (uint32_t *)nullptr, r, 0, 64, c->st));
+        DCK(hipcub::DeviceScan::InclusiveScan(nullptr, t4, (uint32_t *)nullptr, (uint32_t *)nullptr, hipcub::Max(), r,
+                                              c->st));
+        DGROW(c->tmp, std::max(std::max(tb, t2), std::max(t3, t4)));
+    }
     const size_t r4 = 4 * (size_t)(recs + 1), r8 = 8 * (size_t)(recs + 1);
     DGROW(c->off, r8);
     DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
     DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
     DGROW(c->rpos, r4); DGROW(c->krec, r8); DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8);
     DGROW(c->vals2, r4); DGROW(c->head, r4);
+    // the insert statistics' arrays (dd_run_stats)
+    DGROW(c->sq, r4); DGROW(c->sqi, r4); DGROW(c->sv, r4); DGROW(c->slq, r4); DGROW(c->sm, r8);
     return 0;
 }
 

@@ -2454,7 +2454,10 @@ static int dw_reserve(dd_worker *w, char *err, int errlen) {
     free(b);
     if (csum <= 0 || usum <= 0) return 0;
     const int64_t ub = (int64_t)((double)span * (double)usum / (double)csum * 1.15);
-    return dd_reserve(w->dd, ub, recs + recs / 20, err, errlen);
+    int64_t nst = 0;
+    for (int t = 0; t < s->n_tgt; t++)
+        if (s->n_lin[t] > nst) nst = s->n_lin[t];
+    return dd_reserve(w->dd, ub, recs + recs / 20, nst + 2, err, errlen);
 }
 
 /* the next run (tid >= 0) after ri in file order, -1 none */
@@ -2618,11 +2621,13 @@ static void *dw_main(void *arg) {
         const int r0 = next_placed_run(s, -1);
         if (r0 >= 0) pf_want(w, stats_prefix_end(s, r0) != UINT64_MAX ? -r0 - 2 : r0);
     }
+    if (rc == 0 && dw_reserve(w, err, (int)sizeof(err))) rc = -1;
+    /* (after the worker's own buffers: a small allocation waits behind any
+     * large one in flight) */
     pthread_t stres_thr;
     stres_job sj = {s, w->device};
     const int stres = rc == 0 && w->sub == 0 && getenv("GROM_NO_STAGE_RESERVE") == NULL &&
                       pthread_create(&stres_thr, NULL, stres_main, &sj) == 0;
-    if (rc == 0 && dw_reserve(w, err, (int)sizeof(err))) rc = -1;
     if (rc == 0 && w->first) rc = dw_stats(w, err, (int)sizeof(err));
     if (stres) pthread_join(stres_thr, NULL); /* the stages are the worker's again */
     /* the final plan (which chromosomes, which records each one's run starts with) */
