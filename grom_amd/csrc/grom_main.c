@@ -579,6 +579,7 @@ typedef struct {
     int n_jobs, closing;
     const grom_params *P;
     int verbose;
+    const int *pos; /* pos[k]: the job of the k-th chromosome in BAM order (NULL: job k) */
 } grom_pool;
 
 typedef struct {
@@ -783,8 +784,9 @@ static void finish_outputs(cli_state *S, textbuf *ctx_all) {
 
 /* rows of finished jobs, in chromosome order (caller holds pool.mu) */
 static void drain_rows(grom_pool *pool, int *next_write, int upto, FILE *vcf, textbuf *ctx_all, int *status) {
-    while (*next_write < upto && pool->jobs[*next_write].done) {
-        grom_job *j = &pool->jobs[(*next_write)++];
+    while (*next_write < upto && pool->jobs[pool->pos ? pool->pos[*next_write] : *next_write].done) {
+        grom_job *j = &pool->jobs[pool->pos ? pool->pos[*next_write] : *next_write];
+        (*next_write)++;
         pthread_mutex_unlock(&pool->mu);
         if (j->rc != GROM_OK) *status = 1;
         take_rows(j, vcf, ctx_all);
@@ -819,7 +821,7 @@ static void pool_finish(grom_pool *pool, cli_state *S, grom_worker *workers, pth
     for (;;) {
         drain_rows(pool, next_write, pool->n_jobs, vcf, ctx_all, status);
         int busy = 0;
-        for (int j = *next_write; j < pool->n_jobs; j++)
+        for (int j = 0; j < pool->n_jobs; j++)
             if (pool->jobs[j].ready && !pool->jobs[j].done) busy = 1;
         if (!busy) break;
         pthread_cond_wait(&pool->cv, &pool->mu);
@@ -1147,6 +1149,8 @@ static int run_streamed(cli_state *S) {
     pthread_t *tids = NULL;
     textbuf ctx_all = {0};
     int next_write = 0, started = 0, fallback = 0;
+    int *qord = NULL, *qpos = NULL;
+    chrom_plan **qplan = NULL;
     fasta_feed F;
     memset(&F, 0, sizeof(F));
     pthread_t fthr;
@@ -1160,8 +1164,25 @@ static int run_streamed(cli_state *S) {
     if (!vcf) { printf("Error opening file %s\n", S->out_name); status = 1; goto done; }
     if (P->vcf == 1) header(vcf, S->fasta_name, 0);
     else tab_header(vcf, P);
+    /* the order chromosomes are taken in: the device decoder's (longest
+     * first), else BAM order; rows are written in BAM order either way */
+    qord = malloc(sizeof(int) * (n_plan > 0 ? n_plan : 1));
+    qpos = malloc(sizeof(int) * (n_plan > 0 ? n_plan : 1));
+    qplan = malloc(sizeof(chrom_plan *) * (n_plan > 0 ? n_plan : 1));
+    for (int k = 0; k < n_plan; k++) qord[k] = k;
+    if (pd_device_mode(pd))
+        for (int a = 1; a < n_plan; a++)
+            for (int b = a; b > 0 && plan[qord[b]]->len > plan[qord[b - 1]]->len; b--) {
+                const int t = qord[b];
+                qord[b] = qord[b - 1];
+                qord[b - 1] = t;
+            }
+    for (int q = 0; q < n_plan; q++) {
+        qpos[qord[q]] = q;
+        qplan[q] = plan[qord[q]];
+    }
     F.S = S;
-    F.plan = plan;
+    F.plan = qplan;
     F.n_plan = g_plan_only ? 0 : n_plan;
     F.ahead = 3;
     pthread_mutex_init(&F.mu, NULL);
@@ -1171,8 +1192,10 @@ static int run_streamed(cli_state *S) {
     /* (plan-only: the workers print each chromosome's plan line, so the host
      * tests run the pool beside the streamed decoder) */
     pool_start(&pool, S, n_plan, &workers, &tids);
+    pool.pos = qpos;
     started = 1;
-    for (int k = 0; k < n_plan; k++) {
+    for (int q = 0; q < n_plan; q++) {
+        const int k = qord[q];
         grom_stage *st = NULL;
         pd_chrom_facts facts;
         const int rc = pd_wait_chrom(pd, pidx[k], &st, &facts);
@@ -1185,8 +1208,8 @@ static int run_streamed(cli_state *S) {
         }
         if (!g_plan_only) {
             pthread_mutex_lock(&F.mu);
-            while (F.loaded <= k) pthread_cond_wait(&F.cv, &F.mu);
-            F.consumed = k + 1;
+            while (F.loaded <= q) pthread_cond_wait(&F.cv, &F.mu);
+            F.consumed = q + 1;
             pthread_cond_broadcast(&F.cv);
             pthread_mutex_unlock(&F.mu);
             if (!plan[k]->ref || grom_stage_set_ref(st, plan[k]->ref, plan[k]->len) != GROM_OK) {
@@ -1197,7 +1220,7 @@ static int run_streamed(cli_state *S) {
             }
         }
         pthread_mutex_lock(&pool.mu);
-        grom_job *j = &pool.jobs[k];
+        grom_job *j = &pool.jobs[q];
         j->cp = plan[k];
         j->stage = st;
         j->facts = facts;
@@ -1207,7 +1230,7 @@ static int run_streamed(cli_state *S) {
         pd_trace(pd, PD_EV_HANDED, pidx[k], 0);
         j->ready = 1;
         pthread_cond_broadcast(&pool.cv);
-        drain_rows(&pool, &next_write, k + 1, vcf, &ctx_all, &status);
+        drain_rows(&pool, &next_write, n_plan, vcf, &ctx_all, &status);
         pthread_mutex_unlock(&pool.mu);
     }
 done:
@@ -1258,6 +1281,9 @@ done:
     free(pidx);
     free(keep);
     free(dev_of);
+    free(qord);
+    free(qpos);
+    free(qplan);
     if (fallback) {
         for (int d = 0; d < S->n_init; d++) grom_dev_fini(d);
         S->n_init = 0;

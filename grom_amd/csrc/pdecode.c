@@ -2020,6 +2020,7 @@ fail:
 }
 
 void pd_set_device_mode(pd_session *s, int on) { s->dev_mode = on; }
+int pd_device_mode(const pd_session *s) { return s->dev_mode; }
 
 void pd_set_wanted(pd_session *s, const int *want) {
     for (int k = 0; k < s->n_plan; k++) s->want[k] = want ? (want[k] != 0) : 1;
@@ -2610,12 +2611,22 @@ static void *dw_main(void *arg) {
     if (!w->dd) { rc = -1; snprintf(err, sizeof(err), "device decode: no context on device %d", w->device); }
     if (rc == 0) w->pf_started = pthread_create(&w->pf_thr, NULL, pf_main, w) == 0;
     if (rc == 0 && !w->pf_started) { rc = -1; snprintf(err, sizeof(err), "device decode: no prefetch thread"); }
-    /* this worker's chromosomes in order (the final plan's keep[] only drops some) */
+    /* this worker's chromosomes, longest first (the CLI hands them to the
+     * scans in the same order, so the last scans are the short chromosomes';
+     * the final plan's keep[] only drops some) */
     int *mine = (int *)malloc(sizeof(int) * (size_t)(s->n_plan > 0 ? s->n_plan : 1)), n_mine = 0;
-    for (int k = 0, ord = 0; k < s->n_plan; k++) {
-        if (!s->want[k] || s->ch[k].device != w->device) continue;
-        if (ord++ % w->nsub == w->sub) mine[n_mine++] = k;
-    }
+    int *lo = (int *)malloc(sizeof(int) * (size_t)(s->n_plan > 0 ? s->n_plan : 1)), n_lo = 0;
+    for (int k = 0; k < s->n_plan; k++)
+        if (s->want[k] && s->ch[k].device == w->device) lo[n_lo++] = k;
+    for (int a = 1; a < n_lo; a++) /* insertion sort: length descending, plan order on ties */
+        for (int b = a; b > 0 && s->plan[lo[b]].len > s->plan[lo[b - 1]].len; b--) {
+            const int t = lo[b];
+            lo[b] = lo[b - 1];
+            lo[b - 1] = t;
+        }
+    for (int a = 0; a < n_lo; a++)
+        if (a % w->nsub == w->sub) mine[n_mine++] = lo[a];
+    free(lo);
     if (rc == 0 && !w->first && n_mine > 0) pf_want(w, s->ch[mine[0]].run);
     if (rc == 0 && w->first) { /* the stats prefix first: start its read now */
         const int r0 = next_placed_run(s, -1);

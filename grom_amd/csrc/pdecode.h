@@ -68,6 +68,9 @@ void pd_set_wanted(pd_session *s, const int *want);
  * reads its chromosomes' compressed runs, inflates and parses them into the
  * stages) instead of the host decoder threads; same results, same API */
 void pd_set_device_mode(pd_session *s, int on);
+/* device mode: each GPU's chromosomes are decoded longest first (plan order
+ * among equal lengths); the caller takes them in that order */
+int pd_device_mode(const pd_session *s);
 /* start the decoder threads and the uploader.  dev_of[k]: the GPU of plan
  * chromosome k.  plan_only: no device; chromosomes go to host mirrors. */
 int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan_only);
