@@ -2063,6 +2063,7 @@ typedef struct {
     int pf_started, pf_stop;
     int loaded;              /* run index whose records dd holds, -1 none */
     int64_t loaded_R;
+    int test_abort, n_done;  /* GROM_TEST_DD_ABORT=n: -2 at the n-th chromosome (tests) */
 } dd_worker;
 
 typedef struct {
@@ -2503,6 +2504,11 @@ static int dw_stats(dd_worker *w, char *err, int errlen) {
 static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
     pd_session *s = w->s;
     pd_chrom *c = &s->ch[k];
+    /* test hook: the plan contradicted at this worker's n-th chromosome */
+    if (w->test_abort >= 0 && w->n_done++ == w->test_abort) {
+        snprintf(err, (size_t)errlen, "test: the device decode plan contradicted (GROM_TEST_DD_ABORT)");
+        return -2;
+    }
     if (stage_acquire(s, w->device, k, &c->stage)) { snprintf(err, (size_t)errlen, "no stage"); return -1; }
     const int ri = c->run;
     dd_parse_out po;
@@ -2728,6 +2734,7 @@ static int pd_start_device(pd_session *s) {
         w->nsub = per;
         w->first = q == 0;
         w->loaded = -1;
+        w->test_abort = getenv("GROM_TEST_DD_ABORT") ? atoi(getenv("GROM_TEST_DD_ABORT")) : -1;
         w->slot[0].ri = w->slot[1].ri = -1;
         pthread_mutex_init(&w->mu, NULL);
         pthread_cond_init(&w->cv, NULL);

@@ -442,16 +442,20 @@ def test_rank_shares_merge_to_one_run(datadir):
     assert bnd == one_ctx and bnd.count("SVTYPE=BND") >= 2
 
 
-def test_late_fallback_to_serial_reader(datadir, capfd):
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_late_fallback_to_serial_reader(datadir, capfd, mode):
     """The streamed decoder's plan contradicted partway through the file
-    (GROM_TEST_SOFT_ABORT: at a later piece, after chromosomes were handed to
-    the scans): the CLI reruns through the serial reader, the outputs are the
-    oracle's, and stdout carries the insert-size lines once."""
+    (host decoder: GROM_TEST_SOFT_ABORT at a later piece; device decoder:
+    GROM_TEST_DD_ABORT at the second chromosome it decodes -- both after
+    chromosomes were handed to the scans): the CLI reruns through the serial
+    reader, the outputs are the oracle's, and stdout carries the insert-size
+    lines once."""
     bam, fa = synth(datadir, "three_chr", CASES["three_chr"])
     run_oracle(datadir, bam, fa, "o_late.vcf")
     capfd.readouterr()
-    run_grom(datadir, bam, fa, "g_late.vcf", env_extra={"GROM_PIECE_RECS": "2000", "GROM_TEST_SOFT_ABORT": "20",
-                                                         "GROM_VERBOSE": "1"})
+    env = ({"GROM_DEVICE_DECODE": "0", "GROM_PIECE_RECS": "2000", "GROM_TEST_SOFT_ABORT": "20"} if mode == "host"
+           else {"GROM_DEVICE_DECODE": "1", "GROM_TEST_DD_ABORT": "1"})
+    run_grom(datadir, bam, fa, "g_late.vcf", env_extra=dict(env, GROM_VERBOSE="1"))
     out = capfd.readouterr().out
     assert "reading the BAM serially" in out, out[-2000:]
     assert out.count("insert_min_size, insert_max_size") == 1, out[-2000:]
