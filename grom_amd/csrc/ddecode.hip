@@ -330,6 +330,30 @@ __device__ __forceinline__ bool ws_plausible(const uint8_t *U, int64_t p, int64_
     return true;
 }
 
+// the first plausible record start in [lo, hi), -1 none: a sliding window of
+// three aligned words gives each position's block_size and target id from
+// registers (one new word per four positions); only positions whose two
+// fields fit take the full test
+__device__ __forceinline__ int64_t ws_guess(const uint8_t *U, int64_t lo, int64_t hi, int64_t end, int32_t tid) {
+    int64_t a = lo & ~(int64_t)3;
+    const uint32_t *wp = (const uint32_t *)(U + a);
+    uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
+    for (; a < hi; a += 4) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int64_t p = a + k;
+            const uint32_t bs = k ? (w0 >> (8 * k)) | (w1 << (32 - 8 * k)) : w0;
+            const uint32_t td = k ? (w1 >> (8 * k)) | (w2 << (32 - 8 * k)) : w1;
+            if (p >= lo && p < hi && bs >= 34u && bs <= (1u << 20) && (int32_t)td == tid && ws_plausible(U, p, end, tid))
+                return p;
+        }
+        w0 = w1;
+        w1 = w2;
+        w2 = wp[(a - (lo & ~(int64_t)3)) / 4 + 3];
+    }
+    return -1;
+}
+
 // walk from o while o < hi: records counted (and written from *w when off)
 // and the exit; -1 exit for a block_size outside the record limits
 __device__ __forceinline__ int64_t ws_walk(const uint8_t *U, int64_t o, int64_t hi, uint32_t &n, int64_t *off,
@@ -373,8 +397,7 @@ __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U
             if (q == 0) st = c0;
             else if (guess == 2) st = lo;  // test hook: guesses that are mostly wrong
             else if (guess == 1)
-                for (int64_t p = lo; p < hi; p++)
-                    if (ws_plausible(U, p, c1, tid)) { st = p; break; }
+                st = ws_guess(U, lo, hi, c1, tid);
             if (st >= 0) ex = ws_walk(U, st, hi, n, nullptr, 0);
         }
         s_start[t] = st;
@@ -549,6 +572,7 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
                             const uint32_t *__restrict__ auxc, const uint32_t *__restrict__ aidx,
                             const uint32_t *__restrict__ coff_s, const int64_t *__restrict__ boff_s,
                             const int32_t *__restrict__ rpos, StageOut so, int64_t *__restrict__ krec,
+                            int64_t *__restrict__ srcs,
                             uint64_t *__restrict__ keys, uint32_t *__restrict__ vals, int64_t *__restrict__ acand,
                             int32_t read_name_len, int32_t *__restrict__ last, uint32_t *__restrict__ bad) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
@@ -571,6 +595,7 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
             so.boff[i] = boff_s[r];
             so.aidx[i] = -1;
             krec[i] = r;
+            srcs[i] = o + 36 + lqn + 4 * (int64_t)nc;  // the packed bases in U (the qualities follow)
             const int64_t cg = o + 36 + lqn;
             for (int c = 0; c < nc; c++) {
                 const uint32_t op = ldu32(U, cg + 4 * c);
@@ -607,109 +632,97 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
 
 // Packed bases and qualities of the kept reads.  A read's regions tile the
 // stage arrays with no gaps (quality bytes [b, b + nb), bases [b/2, b/2 +
-// nb/2), nb = l_qseq rounded up to even, the pad quality byte 0), so a wave
-// takes 64 reads at once: each lane loads one read's header fields, then the
-// wave copies the reads one after another, a lane per destination dword --
-// aligned source dwords joined by a byte shift, whole dwords stored; only the
-// dwords a region shares with its neighbours take byte stores.
-// dest bytes [dst, dst + len) from src; dword k of the region's dword span for
-// lane k (k < n_dw); `pad`: byte len - 1 is the zero pad, not a source byte
-__device__ __forceinline__ void cp_region(const uint8_t *U, int64_t src, uint8_t *dst_base, int64_t dst, int64_t len,
-                                          int64_t k, bool pad) {
-    const int64_t d0 = dst & ~(int64_t)3;
-    const int64_t D = d0 + 4 * k;
-    const int64_t lo = D < dst ? dst : D, hi = D + 4 < dst + len ? D + 4 : dst + len;
-    if (lo >= hi) return;
-    uint32_t v = ldu32a(U, src + (D - dst));
-    if (pad && hi == dst + len) v &= ~(0xffu << (8 * (uint32_t)(dst + len - 1 - D)));
-    if (lo == D && hi == D + 4) {
-        *(uint32_t *)(dst_base + D) = v;
-    } else {
-        for (int64_t x = lo; x < hi; x++) dst_base[x] = (uint8_t)(v >> (8 * (uint32_t)(x - D)));
+// nb/2), nb = l_qseq rounded up to even, the pad quality byte 0), so the copy
+// is driven by the destination: fixed tiles of it, each with the reads that
+// touch it.
+#define CP_T 1024  // destination bytes per tile (one workgroup, 4 per thread)
+#define CP_R 544   // reads a tile may touch, staged in LDS (more: the tile searches global memory)
+
+// the read holding each tile's first destination byte: read i's region of
+// qualities is [b, b + nb) and of bases [b/2, b/2 + nb/2) (b = boff[i], nb =
+// l_qseq rounded up to even); tiles start every CP_T bytes
+__global__ void k_tile_first(const int64_t *__restrict__ boff, const int32_t *__restrict__ lq, int64_t n,
+                             int64_t *__restrict__ tfq, int64_t *__restrict__ tfs) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = boff[i], nb = ((int64_t)lq[i] + 1) & ~1LL;
+        if (nb <= 0) continue;
+        for (int64_t t = (b + CP_T - 1) / CP_T; t * CP_T < b + nb; t++) tfq[t] = i;
+        for (int64_t t = (b / 2 + CP_T - 1) / CP_T; t * CP_T < b / 2 + nb / 2; t++) tfs[t] = i;
     }
 }
 
-__device__ __forceinline__ int64_t rl64(int64_t v, int j) {  // lane j's value (j wave-uniform)
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
-#define CP_UNROLL 8
-
-__global__ void __launch_bounds__(256) k_copy_bases(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
-                                                    const int64_t *__restrict__ krec, int64_t n,
-                                                    const int64_t *__restrict__ boff, uint8_t *__restrict__ seq,
-                                                    uint8_t *__restrict__ qual) {
-    const int lane = threadIdx.x & 63;
-    const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t g = w0 * 64; g < n; g += nw * 64) {
-        // lane j: read g + j's source offset, length and destination
-        const int64_t i = g + lane;
-        int64_t src = 0, b = 0;
-        int32_t lq = 0;
-        if (i < n) {
-            const int64_t o = off[krec[i]];
-            const uint32_t h3 = ldu32a(U, o + 12), h4 = ldu32a(U, o + 16);
-            lq = (int32_t)ldu32a(U, o + 20);
-            src = o + 36 + (int64_t)(h3 & 0xff) + 4 * (int64_t)(h4 & 0xffff);
-            b = boff[i];
-        }
-        const int m = n - g < 64 ? (int)(n - g) : 64;
-        // CP_UNROLL reads at a time: every source load of the group issued
-        // before its stores (the copies are latency-bound one read at a time)
-        for (int j0 = 0; j0 < m; j0 += CP_UNROLL) {
-            int64_t dst_[CP_UNROLL], len_[CP_UNROLL], sb_[CP_UNROLL], k_[CP_UNROLL];
-            uint8_t *base_[CP_UNROLL];
-            bool pad_[CP_UNROLL], on_[CP_UNROLL];
-            uint32_t w0_[CP_UNROLL], w1_[CP_UNROLL];
-#pragma unroll
-            for (int u = 0; u < CP_UNROLL; u++) {
-                const int j = j0 + u < m ? j0 + u : m - 1;
-                const int64_t s_j = rl64(src, j), b_j = rl64(b, j);
-                const int32_t lq_j = __builtin_amdgcn_readlane(lq, j);
-                const int64_t ns = (lq_j + 1) / 2, nb = 2 * ns;
-                // bases: dst b/2, ns bytes; qualities: dst b, nb bytes (the last a pad when lq is odd)
-                const int64_t n_s = (((b_j / 2 + ns + 3) & ~(int64_t)3) - ((b_j / 2) & ~(int64_t)3)) / 4;
-                const int64_t n_q = (((b_j + nb + 3) & ~(int64_t)3) - (b_j & ~(int64_t)3)) / 4;
-                const int64_t k = lane;
-                const bool sq = k < n_s;
-                dst_[u] = sq ? b_j / 2 : b_j;
-                len_[u] = sq ? ns : nb;
-                sb_[u] = sq ? s_j : s_j + ns;
-                k_[u] = sq ? k : k - n_s;
-                base_[u] = sq ? seq : qual;
-                pad_[u] = !sq && (lq_j & 1) != 0;
-                on_[u] = j0 + u < m && k < n_s + n_q && n_s + n_q <= 64;
-                const int64_t p = sb_[u] + ((dst_[u] & ~(int64_t)3) + 4 * k_[u] - dst_[u]);
-                const uint32_t *a = (const uint32_t *)(U + (p & ~(int64_t)3));
-                w0_[u] = on_[u] ? a[0] : 0u;
-                w1_[u] = on_[u] ? a[1] : 0u;
-                if (j0 + u < m && n_s + n_q > 64)  // a read over 64 dwords (l_qseq > ~250): plain loop
-                    for (int64_t kk = lane; kk < n_s + n_q; kk += 64) {
-                        if (kk < n_s) cp_region(U, s_j, seq, b_j / 2, ns, kk, false);
-                        else cp_region(U, s_j + ns, qual, b_j, nb, kk - n_s, (lq_j & 1) != 0);
-                    }
+// One workgroup per CP_T destination bytes of the qualities (QUAL) or the
+// packed bases: every dword of the tile stored whole and coalesced; each
+// thread finds its read among the tile's (staged in LDS), then takes its
+// four bytes from the read's source in U (two aligned words and a shift when
+// all four come from one read, else byte by byte; an odd-length read's pad
+// quality byte is 0).  Replaces a wave-per-64-reads copy whose per-read
+// boundary dwords and serial loop left it latency-bound.
+template <bool QUAL>
+__global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ U, const int64_t *__restrict__ srcs,
+                                                    const int64_t *__restrict__ boff, const int32_t *__restrict__ lq,
+                                                    int64_t n, const int64_t *__restrict__ tf, int64_t n_tiles,
+                                                    int64_t total, uint8_t *__restrict__ dst) {
+    __shared__ int64_t s_beg[CP_R], s_src[CP_R];
+    __shared__ int32_t s_len[CP_R];
+    __shared__ int s_odd[CP_R];
+    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const int64_t r0 = tf[t], r1 = t + 1 < n_tiles ? tf[t + 1] : n - 1;
+        const int64_t nr = r1 - r0 + 1;
+        const bool staged = nr <= CP_R;
+        __syncthreads();
+        if (staged)
+            for (int64_t k = threadIdx.x; k < nr; k += blockDim.x) {
+                const int64_t i = r0 + k, nb = ((int64_t)lq[i] + 1) & ~1LL;
+                s_beg[k] = QUAL ? boff[i] : boff[i] / 2;
+                s_len[k] = (int32_t)(QUAL ? nb : nb / 2);
+                s_src[k] = QUAL ? srcs[i] + nb / 2 : srcs[i];
+                s_odd[k] = (int)(lq[i] & 1);
             }
-#pragma unroll
-            for (int u = 0; u < CP_UNROLL; u++) {
-                if (!on_[u]) continue;
-                const int64_t d = dst_[u], L = len_[u];
-                const int64_t D = (d & ~(int64_t)3) + 4 * k_[u];
-                const int64_t lo = D < d ? d : D, hi = D + 4 < d + L ? D + 4 : d + L;
-                if (lo >= hi) continue;
-                const int64_t p = sb_[u] + (D - d);
-                const uint32_t sh = (uint32_t)(p & 3) * 8;
-                uint32_t v = sh ? (w0_[u] >> sh) | (w1_[u] << (32 - sh)) : w0_[u];
-                if (pad_[u] && hi == d + L) v &= ~(0xffu << (8 * (uint32_t)(d + L - 1 - D)));
-                if (lo == D && hi == D + 4) {
-                    *(uint32_t *)(base_[u] + D) = v;
-                } else {
-                    for (int64_t x = lo; x < hi; x++) base_[u][x] = (uint8_t)(v >> (8 * (uint32_t)(x - D)));
+        __syncthreads();
+        const int64_t x = t * CP_T + 4 * (int64_t)threadIdx.x;
+        if (x >= total) continue;
+        auto beg = [&](int64_t k) { return staged ? s_beg[k] : (QUAL ? boff[r0 + k] : boff[r0 + k] / 2); };
+        auto len = [&](int64_t k) -> int64_t {
+            if (staged) return s_len[k];
+            const int64_t nb = ((int64_t)lq[r0 + k] + 1) & ~1LL;
+            return QUAL ? nb : nb / 2;
+        };
+        auto src = [&](int64_t k) -> int64_t {
+            if (staged) return s_src[k];
+            const int64_t nb = ((int64_t)lq[r0 + k] + 1) & ~1LL;
+            return QUAL ? srcs[r0 + k] + nb / 2 : srcs[r0 + k];
+        };
+        auto odd = [&](int64_t k) -> bool { return staged ? s_odd[k] != 0 : (lq[r0 + k] & 1) != 0; };
+        // the last read starting at or before x (reads in destination order)
+        int64_t lo = 0, hi = nr - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) / 2;
+            if (beg(mid) <= x) lo = mid;
+            else hi = mid - 1;
+        }
+        int64_t k = lo;
+        int64_t b0 = beg(k), L = len(k);
+        uint32_t v;
+        const bool pad_in = QUAL && odd(k) && x + 3 >= b0 + L - 1;
+        if (x + 4 <= b0 + L && !pad_in) {
+            v = ldu32a(U, src(k) + (x - b0));
+        } else {
+            v = 0;
+            for (int j = 0; j < 4; j++) {
+                const int64_t y = x + j;
+                if (y >= total) break;
+                while (y >= b0 + L && k + 1 < nr) {
+                    k++;
+                    b0 = beg(k);
+                    L = len(k);
                 }
+                uint32_t byte = 0;
+                if (!(QUAL && odd(k) && y == b0 + L - 1)) byte = U[src(k) + (y - b0)];
+                v |= byte << (8 * j);
             }
         }
+        *(uint32_t *)(dst + x) = v;
     }
 }
 
@@ -842,6 +855,7 @@ struct dd_ctx {
     hipEvent_t ev[4] = {};
     DBuf blk, U, status, misc, S, ccnt, cbase, off;
     DBuf keep, kidx, drop, didx, auxc, aidx, ncig, coff, nb, boff, rpos, krec, keys, vals, keys2, vals2, head, tmp;
+    DBuf srcs, tfq, tfs;  // per kept read: its bases' offset in U; per copy tile: its first read
     DBuf sq, sqi, sv, slq, sm, s_ins, s_lq, acand, alen, aoff, akidx, apack;
     int64_t R = 0, nblk = 0, ubytes = 0;
     int64_t *h_small = nullptr;  // pinned: totals and scalars
@@ -893,6 +907,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     DBuf *all[] = {&c->blk, &c->U, &c->status, &c->misc, &c->S, &c->ccnt, &c->cbase, &c->off, &c->keep,
                    &c->kidx, &c->drop, &c->didx, &c->auxc, &c->aidx, &c->ncig, &c->coff, &c->nb, &c->boff, &c->rpos,
                    &c->krec, &c->keys, &c->vals, &c->keys2, &c->vals2, &c->head, &c->tmp, &c->sq, &c->sqi, &c->sv,
+                   &c->srcs, &c->tfq, &c->tfs,
                    &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack};
     for (DBuf *b : all)
         if (b->p) (void)hipFree(b->p);
@@ -948,7 +963,7 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_sta
     DGROW(c->off, r8);
     DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
     DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
-    DGROW(c->rpos, r4); DGROW(c->krec, r8); DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8);
+    DGROW(c->rpos, r4); DGROW(c->krec, r8); DGROW(c->srcs, r8); DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8);
     DGROW(c->vals2, r4); DGROW(c->head, r4);
     // the insert statistics' arrays (dd_run_stats)
     DGROW(c->sq, r4); DGROW(c->sqi, r4); DGROW(c->sv, r4); DGROW(c->slq, r4); DGROW(c->sm, r8);
@@ -1148,6 +1163,7 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
     so.cig = (uint32_t *)dv.cigar; so.nid = (uint32_t *)dv.name_id; so.boff = (int64_t *)dv.base_off;
     so.dpos = (int32_t *)dv.drop_pos; so.dlq = (int32_t *)dv.drop_lq; so.dbef = (int64_t *)dv.drop_before;
     DGROW(c->krec, 8 * (size_t)(n + 1));
+    DGROW(c->srcs, 8 * (size_t)(n + 1));
     DGROW(c->keys, 8 * (size_t)(n + 1)); DGROW(c->vals, 4 * (size_t)(n + 1));
     DGROW(c->keys2, 8 * (size_t)(n + 1)); DGROW(c->vals2, 4 * (size_t)(n + 1)); DGROW(c->head, 4 * (size_t)(n + 1));
     DGROW(c->acand, 8 * (size_t)(na + 2)); DGROW(c->alen, 8 * (size_t)(na + 2)); DGROW(c->aoff, 8 * (size_t)(na + 2));
@@ -1160,13 +1176,26 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
         hipLaunchKernelGGL(k_rec_write, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off), R, j0,
                            P<uint32_t>(c->keep), P<uint32_t>(c->kidx), P<uint32_t>(c->drop), P<uint32_t>(c->didx),
                            P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), P<uint32_t>(c->coff), P<int64_t>(c->boff),
-                           P<int32_t>(c->rpos), so, P<int64_t>(c->krec), P<uint64_t>(c->keys), P<uint32_t>(c->vals),
+                           P<int32_t>(c->rpos), so, P<int64_t>(c->krec), P<int64_t>(c->srcs), P<uint64_t>(c->keys),
+                           P<uint32_t>(c->vals),
                            P<int64_t>(c->acand), read_name_len, last, bad);
     hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, st, so.coff + n, (uint32_t)ncg);
     if (n > 0) {
-        hipLaunchKernelGGL(k_copy_bases, dim3(grid_for(n * 64, 256, 1u << 16)), dim3(256), 0, st, P<uint8_t>(c->U),
-                           P<int64_t>(c->off), P<int64_t>(c->krec), n, (const int64_t *)so.boff, (uint8_t *)dv.seq,
-                           (uint8_t *)dv.qual);
+        {
+            const int64_t nt_q = (nbs + CP_T - 1) / CP_T, nt_s = (nbs / 2 + CP_T - 1) / CP_T;
+            DGROW(c->tfq, 8 * (size_t)(nt_q + 1));
+            DGROW(c->tfs, 8 * (size_t)(nt_s + 1));
+            hipLaunchKernelGGL(k_tile_first, dim3(grid_for(n)), dim3(256), 0, st, (const int64_t *)so.boff,
+                               (const int32_t *)so.lq, n, P<int64_t>(c->tfq), P<int64_t>(c->tfs));
+            if (nt_q > 0)
+                hipLaunchKernelGGL(k_copy_tiles<true>, dim3((unsigned)std::min<int64_t>(nt_q, 1 << 20)), dim3(256), 0, st,
+                                   P<uint8_t>(c->U), P<int64_t>(c->srcs), (const int64_t *)so.boff, (const int32_t *)so.lq,
+                                   n, P<int64_t>(c->tfq), nt_q, nbs, (uint8_t *)dv.qual);
+            if (nt_s > 0)
+                hipLaunchKernelGGL(k_copy_tiles<false>, dim3((unsigned)std::min<int64_t>(nt_s, 1 << 20)), dim3(256), 0,
+                                   st, P<uint8_t>(c->U), P<int64_t>(c->srcs), (const int64_t *)so.boff,
+                                   (const int32_t *)so.lq, n, P<int64_t>(c->tfs), nt_s, nbs / 2, (uint8_t *)dv.seq);
+        }
         // read-name ids: sort the hashes, check each equal-hash run byte for byte
         size_t tb = 0, t2 = 0;
         DCK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, P<uint64_t>(c->keys), P<uint64_t>(c->keys2),
