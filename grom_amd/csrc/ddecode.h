@@ -41,6 +41,8 @@ void dd_ctx_free(dd_ctx *c);
 /* summed HIP-event times of the parsed runs: inflate, record walk, parse;
  * ms[3]: wall time of decode buffer growth so far (every context) */
 void dd_ctx_times(const dd_ctx *c, double ms[4]);
+/* record-walk sub-chunks whose guessed start was wrong (re-walked) / all */
+void dd_ctx_counts(const dd_ctx *c, int64_t *rewalked, int64_t *subchunks);
 /* the per-run device buffers sized for a run of `ubytes` inflated bytes,
  * `recs` records and `n_starts` index-named record starts (growth later frees
  * buffers, which waits for the device) */

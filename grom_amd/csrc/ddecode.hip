@@ -373,7 +373,7 @@ __device__ __forceinline__ int64_t ws_walk(const uint8_t *U, int64_t o, int64_t 
 // the record offsets from base[c] on
 __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U, const int64_t *__restrict__ S,
                                                    int64_t n_chunks, int32_t tid, int guess,
-                                                   uint32_t *__restrict__ cnt,
+                                                   uint32_t *__restrict__ q0_stats, uint32_t *__restrict__ cnt,
                                                    const uint32_t *__restrict__ base, int64_t *__restrict__ off,
                                                    uint32_t *__restrict__ bad) {
     __shared__ int64_t s_start[WS_T], s_exit[WS_T];
@@ -410,6 +410,7 @@ __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U
             for (int k = 0; k < m && !s_fail; k++) {
                 const int64_t khi = c0 + (r0 + k) * WS_G + WS_G < c1 ? c0 + (r0 + k) * WS_G + WS_G : c1;
                 if (!(s_start[k] == carry && s_exit[k] >= 0)) {
+                    if (!off && q0_stats) atomicAdd(q0_stats, 1u);  // GROM_VERBOSE: re-walked sub-chunks
                     uint32_t kn = 0;
                     const int64_t kex = ws_walk(U, carry, khi, kn, nullptr, 0);
                     if (kex < 0) { atomicOr(bad, DB_RECORD); s_fail = 1; break; }
@@ -635,8 +636,9 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
 // nb/2), nb = l_qseq rounded up to even, the pad quality byte 0), so the copy
 // is driven by the destination: fixed tiles of it, each with the reads that
 // touch it.
-#define CP_T 1024  // destination bytes per tile (one workgroup, 4 per thread)
-#define CP_R 544   // reads a tile may touch, staged in LDS (more: the tile searches global memory)
+#define CP_T 8192  // destination bytes per tile: one workgroup, 8 dwords per thread
+#define CP_J (CP_T / 1024)
+#define CP_R 1024   // reads a tile may touch, staged in LDS (more: the tile reads them from global memory)
 
 // the read holding each tile's first destination byte: read i's region of
 // qualities is [b, b + nb) and of bases [b/2, b/2 + nb/2) (b = boff[i], nb =
@@ -652,24 +654,25 @@ __global__ void k_tile_first(const int64_t *__restrict__ boff, const int32_t *__
 }
 
 // One workgroup per CP_T destination bytes of the qualities (QUAL) or the
-// packed bases: every dword of the tile stored whole and coalesced; each
-// thread finds its read among the tile's (staged in LDS), then takes its
-// four bytes from the read's source in U (two aligned words and a shift when
-// all four come from one read, else byte by byte; an odd-length read's pad
-// quality byte is 0).  Replaces a wave-per-64-reads copy whose per-read
-// boundary dwords and serial loop left it latency-bound.
+// packed bases: every dword of the tile stored whole and coalesced.  The
+// tile's reads are staged in LDS; each thread finds the read of each of its
+// dwords, issues all of their source loads (two aligned words and a shift
+// when the four bytes come from one read), then stores; a dword across a read
+// boundary (or an odd-length read's pad quality byte, 0) is built byte by
+// byte.  The tile is large so the per-tile chain of dependent loads (its
+// first read, the staged fields) is paid once per 16 KB.
 template <bool QUAL>
 __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ U, const int64_t *__restrict__ srcs,
                                                     const int64_t *__restrict__ boff, const int32_t *__restrict__ lq,
                                                     int64_t n, const int64_t *__restrict__ tf, int64_t n_tiles,
-                                                    int64_t total, uint8_t *__restrict__ dst) {
+                                                    int64_t total, int stage_cap, uint8_t *__restrict__ dst) {
     __shared__ int64_t s_beg[CP_R], s_src[CP_R];
     __shared__ int32_t s_len[CP_R];
-    __shared__ int s_odd[CP_R];
+    __shared__ uint8_t s_odd[CP_R];
     for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         const int64_t r0 = tf[t], r1 = t + 1 < n_tiles ? tf[t + 1] : n - 1;
         const int64_t nr = r1 - r0 + 1;
-        const bool staged = nr <= CP_R;
+        const bool staged = nr <= stage_cap;
         __syncthreads();
         if (staged)
             for (int64_t k = threadIdx.x; k < nr; k += blockDim.x) {
@@ -677,52 +680,90 @@ __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ 
                 s_beg[k] = QUAL ? boff[i] : boff[i] / 2;
                 s_len[k] = (int32_t)(QUAL ? nb : nb / 2);
                 s_src[k] = QUAL ? srcs[i] + nb / 2 : srcs[i];
-                s_odd[k] = (int)(lq[i] & 1);
+                s_odd[k] = (uint8_t)(lq[i] & 1);
             }
         __syncthreads();
-        const int64_t x = t * CP_T + 4 * (int64_t)threadIdx.x;
-        if (x >= total) continue;
-        auto beg = [&](int64_t k) { return staged ? s_beg[k] : (QUAL ? boff[r0 + k] : boff[r0 + k] / 2); };
-        auto len = [&](int64_t k) -> int64_t {
-            if (staged) return s_len[k];
-            const int64_t nb = ((int64_t)lq[r0 + k] + 1) & ~1LL;
-            return QUAL ? nb : nb / 2;
-        };
-        auto src = [&](int64_t k) -> int64_t {
-            if (staged) return s_src[k];
-            const int64_t nb = ((int64_t)lq[r0 + k] + 1) & ~1LL;
-            return QUAL ? srcs[r0 + k] + nb / 2 : srcs[r0 + k];
-        };
-        auto odd = [&](int64_t k) -> bool { return staged ? s_odd[k] != 0 : (lq[r0 + k] & 1) != 0; };
-        // the last read starting at or before x (reads in destination order)
-        int64_t lo = 0, hi = nr - 1;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi + 1) / 2;
-            if (beg(mid) <= x) lo = mid;
-            else hi = mid - 1;
-        }
-        int64_t k = lo;
-        int64_t b0 = beg(k), L = len(k);
-        uint32_t v;
-        const bool pad_in = QUAL && odd(k) && x + 3 >= b0 + L - 1;
-        if (x + 4 <= b0 + L && !pad_in) {
-            v = ldu32a(U, src(k) + (x - b0));
-        } else {
-            v = 0;
-            for (int j = 0; j < 4; j++) {
-                const int64_t y = x + j;
-                if (y >= total) break;
-                while (y >= b0 + L && k + 1 < nr) {
-                    k++;
-                    b0 = beg(k);
-                    L = len(k);
+        if (!staged) {  // more reads than LDS holds (tiny reads): each dword searched in global memory
+            for (int j = 0; j < CP_J; j++) {
+                const int64_t x = t * CP_T + 4 * (int64_t)(threadIdx.x + 256 * j);
+                if (x >= total) continue;
+                int64_t lo = r0, hi = r1;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi + 1) / 2;
+                    if ((QUAL ? boff[mid] : boff[mid] / 2) <= x) lo = mid;
+                    else hi = mid - 1;
                 }
-                uint32_t byte = 0;
-                if (!(QUAL && odd(k) && y == b0 + L - 1)) byte = U[src(k) + (y - b0)];
-                v |= byte << (8 * j);
+                uint32_t v = 0;
+                int64_t q = lo;
+                for (int jj = 0; jj < 4; jj++) {
+                    const int64_t y = x + jj;
+                    if (y >= total) break;
+                    int64_t nb = ((int64_t)lq[q] + 1) & ~1LL;
+                    while (y >= (QUAL ? boff[q] + nb : boff[q] / 2 + nb / 2) && q < r1) {
+                        q++;
+                        nb = ((int64_t)lq[q] + 1) & ~1LL;
+                    }
+                    const int64_t b0 = QUAL ? boff[q] : boff[q] / 2, L = QUAL ? nb : nb / 2;
+                    uint32_t byte = 0;
+                    if (!(QUAL && (lq[q] & 1) && y == b0 + L - 1)) byte = U[(QUAL ? srcs[q] + nb / 2 : srcs[q]) + (y - b0)];
+                    v |= byte << (8 * jj);
+                }
+                *(uint32_t *)(dst + x) = v;
             }
+            continue;
         }
-        *(uint32_t *)(dst + x) = v;
+        uint32_t w0[CP_J], w1[CP_J], fastm = 0, shp = 0;  // shp: 2 bits per dword, its source's byte offset
+        int k = 0;  // reads are in destination order: each search starts from the previous dword's read
+        const int64_t t0 = t * CP_T;
+#pragma unroll
+        for (int j = 0; j < CP_J; j++) {
+            const int32_t xr = 4 * (threadIdx.x + 256 * j);  // offset in the tile
+            const int64_t x = t0 + xr;
+            int lo = k, hi = (int)nr - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2;
+                if (s_beg[mid] <= x) lo = mid;
+                else hi = mid - 1;
+            }
+            k = lo;
+            const int64_t b0 = s_beg[k], L = s_len[k];
+            const bool fast = x + 4 <= b0 + L && !(QUAL && s_odd[k] && x + 3 >= b0 + L - 1) && x + 4 <= total;
+            const int64_t p = s_src[k] + (x - b0);
+            const uint32_t *a = (const uint32_t *)(U + (p & ~(int64_t)3));
+            fastm |= (uint32_t)fast << j;
+            shp |= (uint32_t)(p & 3) << (2 * j);
+            w0[j] = fast ? a[0] : 0u;
+            w1[j] = fast && (p & 3) ? a[1] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < CP_J; j++) {
+            const int64_t x = t0 + 4 * (threadIdx.x + 256 * j);
+            if (x >= total) continue;
+            uint32_t v;
+            if ((fastm >> j) & 1u) {
+                const uint32_t sh = ((shp >> (2 * j)) & 3u) * 8;
+                v = sh ? (w0[j] >> sh) | (w1[j] << (32 - sh)) : w0[j];
+            } else {
+                // a read boundary or the pad byte in this dword: the read again, then byte by byte
+                int lo = 0, hi = (int)nr - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) / 2;
+                    if (s_beg[mid] <= x) lo = mid;
+                    else hi = mid - 1;
+                }
+                v = 0;
+                int q = lo;
+                for (int jj = 0; jj < 4; jj++) {
+                    const int64_t y = x + jj;
+                    if (y >= total) break;
+                    while (y >= s_beg[q] + s_len[q] && q + 1 < (int)nr) q++;
+                    uint32_t byte = 0;
+                    if (!(QUAL && s_odd[q] && y == s_beg[q] + s_len[q] - 1)) byte = U[s_src[q] + (y - s_beg[q])];
+                    v |= byte << (8 * jj);
+                }
+            }
+            *(uint32_t *)(dst + x) = v;
+        }
     }
 }
 
@@ -862,6 +903,8 @@ struct dd_ctx {
     uint8_t *h_aux = nullptr;    // pinned: packed split-read candidate records
     size_t h_aux_cap = 0;
     float ms_inflate = 0, ms_walk = 0, ms_parse = 0;
+    int64_t n_rewalk = 0, n_sub = 0;
+    int cp_cap = CP_R;  // copy tiles staged in LDS up to this many reads (GROM_TEST_CP_UNSTAGED: 0, tests)  // sub-chunks re-walked by the verifying lane / all sub-chunks
     int ws_guess = 1;  // record-start guesses: 1 plausible headers, 0 none, 2 sub-chunk starts (GROM_WS_GUESS, tests)
 };
 
@@ -887,6 +930,7 @@ extern "C" dd_ctx *dd_ctx_new(int device) {
     dd_ctx *c = new dd_ctx();
     c->device = device;
     if (getenv("GROM_WS_GUESS")) c->ws_guess = atoi(getenv("GROM_WS_GUESS"));
+    if (getenv("GROM_TEST_CP_UNSTAGED")) c->cp_cap = 0;
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return nullptr; }
     if (hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) c->cst = nullptr;
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
@@ -931,6 +975,11 @@ extern "C" void dd_ctx_times(const dd_ctx *c, double *ms) {
     ms[1] = c->ms_walk;
     ms[2] = c->ms_parse;
     ms[3] = (double)g_dgrow_ns.load() / 1e6;
+}
+
+extern "C" void dd_ctx_counts(const dd_ctx *c, int64_t *rewalked, int64_t *subchunks) {
+    *rewalked = c->n_rewalk;
+    *subchunks = c->n_sub;
 }
 
 // the per-run buffers sized once for the largest run (ubytes inflated bytes,
@@ -1018,7 +1067,7 @@ extern "C" int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock 
     DCK(hipEventRecord(c->ev[1], st));
     // records: count per chunk, place, write offsets
     hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(c->U), P<int64_t>(c->S),
-                       n_starts, tid, c->ws_guess, P<uint32_t>(c->ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, bad);
+                       n_starts, tid, c->ws_guess, bad + 4, P<uint32_t>(c->ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, bad);
     size_t tb = 0;
     DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->ccnt), P<uint32_t>(c->cbase), (int)n_starts, st));
     DGROW(c->tmp, tb);
@@ -1026,8 +1075,11 @@ extern "C" int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock 
     DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(c->cbase) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
     DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(c->ccnt) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
     DCK(hipMemcpyAsync((char *)c->h_small + 8, bad, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)c->h_small + 16, bad + 4, 4, hipMemcpyDeviceToHost, st));
     DCK(hipStreamSynchronize(st));
     const uint32_t *hs = (const uint32_t *)c->h_small;
+    c->n_rewalk += hs[4];
+    c->n_sub += (ubytes + WS_G - 1) / WS_G;
     if (hs[3]) {
         if (err) snprintf(err, (size_t)errlen, "device inflate: %u blocks failed", hs[3]);
         return -2;
@@ -1039,7 +1091,7 @@ extern "C" int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock 
     const int64_t R = (int64_t)hs[0] + hs[1];
     DGROW(c->off, sizeof(int64_t) * (size_t)(R + 1));
     hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(c->U), P<int64_t>(c->S),
-                       n_starts, tid, c->ws_guess, (uint32_t *)nullptr, P<uint32_t>(c->cbase), P<int64_t>(c->off), bad);
+                       n_starts, tid, c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(c->cbase), P<int64_t>(c->off), bad);
     DCK(hipEventRecord(c->ev[2], st));
     DCK(hipGetLastError());
     c->R = R;
@@ -1188,13 +1240,13 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
             hipLaunchKernelGGL(k_tile_first, dim3(grid_for(n)), dim3(256), 0, st, (const int64_t *)so.boff,
                                (const int32_t *)so.lq, n, P<int64_t>(c->tfq), P<int64_t>(c->tfs));
             if (nt_q > 0)
-                hipLaunchKernelGGL(k_copy_tiles<true>, dim3((unsigned)std::min<int64_t>(nt_q, 1 << 20)), dim3(256), 0, st,
+                hipLaunchKernelGGL(k_copy_tiles<true>, dim3((unsigned)std::min<int64_t>(nt_q, 1 << 16)), dim3(256), 0, st,
                                    P<uint8_t>(c->U), P<int64_t>(c->srcs), (const int64_t *)so.boff, (const int32_t *)so.lq,
-                                   n, P<int64_t>(c->tfq), nt_q, nbs, (uint8_t *)dv.qual);
+                                   n, P<int64_t>(c->tfq), nt_q, nbs, c->cp_cap, (uint8_t *)dv.qual);
             if (nt_s > 0)
-                hipLaunchKernelGGL(k_copy_tiles<false>, dim3((unsigned)std::min<int64_t>(nt_s, 1 << 20)), dim3(256), 0,
+                hipLaunchKernelGGL(k_copy_tiles<false>, dim3((unsigned)std::min<int64_t>(nt_s, 1 << 16)), dim3(256), 0,
                                    st, P<uint8_t>(c->U), P<int64_t>(c->srcs), (const int64_t *)so.boff,
-                                   (const int32_t *)so.lq, n, P<int64_t>(c->tfs), nt_s, nbs / 2, (uint8_t *)dv.seq);
+                                   (const int32_t *)so.lq, n, P<int64_t>(c->tfs), nt_s, nbs / 2, c->cp_cap, (uint8_t *)dv.seq);
         }
         // read-name ids: sort the hashes, check each equal-hash run byte for byte
         size_t tb = 0, t2 = 0;

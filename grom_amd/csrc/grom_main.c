@@ -1258,10 +1258,12 @@ done:
         if (pc.device)
             printf("device decode: %lld records, %.2f GB compressed read and copied to HBM, %.2f GB inflated on the GPU; "
                    "file reads %.2f s (read ahead; waited for %.2f s), device work %.2f s (GPU inflate %.3f s, record walk %.3f s, "
-                   "parse %.3f s), device buffer growth %.3f s, per-chromosome decode + finalise %.2f s, wall %.2f s\n",
+                   "parse %.3f s; %lld of %lld walk sub-chunks re-walked), device buffer growth %.3f s, per-chromosome decode + "
+                   "finalise %.2f s, wall %.2f s\n",
                    (long long)pc.records, pc.compressed_bytes / 1e9, pc.inflated_bytes / 1e9, pc.io_s, pc.wait_s,
                    pc.decode_thread_s,
-                   pc.gpu_ms[0] / 1e3, pc.gpu_ms[1] / 1e3, pc.gpu_ms[2] / 1e3, pc.gpu_ms[3] / 1e3, pc.upload_s, clock_gettime_s() - t_start);
+                   pc.gpu_ms[0] / 1e3, pc.gpu_ms[1] / 1e3, pc.gpu_ms[2] / 1e3, (long long)pc.rewalked, (long long)pc.subchunks,
+                   pc.gpu_ms[3] / 1e3, pc.upload_s, clock_gettime_s() - t_start);
         else
         printf("streamed decode: %lld records in %lld pieces, %d threads (%s), %.2f GB inflated, %.2f GB to HBM, "
                "decoder busy %.2f s (inflate %.2f s, file reads %.2f s), uploader %.2f s (waiting %.2f s), wall %.2f s\n",

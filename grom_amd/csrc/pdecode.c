@@ -433,6 +433,7 @@ struct pd_session {
     pthread_t *dw;
     int n_dw, dw_started;
     double c_gpu_ms[4];    /* inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
+    int64_t c_rewalk, c_subchunks; /* record walk: sub-chunks re-walked / all */
     int io_threads;
     int64_t insert_cap;    /* PD_INSERT_CAP (GROM_TEST_INSERT_CAP: tests of both decoders against each other) */
     int64_t prefix_records; /* GROM_TEST_PREFIX_RECORDS: the stats prefix's record target (tests) */
@@ -2686,6 +2687,10 @@ static void *dw_main(void *arg) {
         pthread_mutex_lock(&s->mu);
         for (int q = 0; q < 3; q++) s->c_gpu_ms[q] += ms[q];
         s->c_gpu_ms[3] = ms[3];
+        int64_t rw = 0, sc = 0;
+        dd_ctx_counts(w->dd, &rw, &sc);
+        s->c_rewalk += rw;
+        s->c_subchunks += sc;
         pthread_mutex_unlock(&s->mu);
     }
     free(mine);
@@ -2870,6 +2875,8 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
     c->inflate_s = s->c_inflate_s;
     c->device = s->dev_mode;
     for (int q = 0; q < 4; q++) c->gpu_ms[q] = s->c_gpu_ms[q];
+    c->rewalked = s->c_rewalk;
+    c->subchunks = s->c_subchunks;
     c->io_s = s->c_io_s;
     c->upload_s = s->c_upl_s;
     c->wait_s = s->c_wait_s;

@@ -102,6 +102,7 @@ typedef struct pd_counters {
     double decode_thread_s, inflate_s, upload_s, wait_s, io_s;
     int threads, libdeflate;
     int device;          /* runs decoded on the GPU (device mode) */
+    int64_t rewalked, subchunks; /* device mode: record-walk sub-chunks re-walked / all */
     double gpu_ms[4];    /* device mode: inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
 } pd_counters;
 void pd_get_counters(pd_session *s, pd_counters *c);

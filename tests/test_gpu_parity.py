@@ -692,7 +692,9 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
     the per-GPU workers of -P n on a multi-GPU node do.  Modes "g0"/"g2" run
     the record walk's guess-then-verify (k_walk_sub) with no guesses and with
     guesses at raw sub-chunk offsets (almost all wrong): every sub-chunk is
-    then walked again from the true chain, with the same result."""
+    then walked again from the true chain, with the same result.  Mode "cu"
+    copies every base/quality tile through its global-memory path (the one
+    tiles with more reads than LDS holds take)."""
     bam, fa = synth(datadir, case, CASES[case])
     tag = f"dd_{case}{''.join(extra).replace('-', '_')}"
     run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
@@ -700,7 +702,8 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
     modes = {"0": {"GROM_DEVICE_DECODE": "0"}, "1": {"GROM_DEVICE_DECODE": "1"},
              "3w": {"GROM_DEVICE_DECODE": "1", "GROM_DD_WORKERS": "3"},
              "g0": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "0"},
-             "g2": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "2"}}
+             "g2": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "2"},
+             "cu": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_CP_UNSTAGED": "1"}}
     for mode, env in modes.items():
         capfd.readouterr()
         run_grom(datadir, bam, fa, f"g{mode}_{tag}.vcf", extra,
