@@ -77,6 +77,8 @@ typedef struct dd_parse_out {
  * every array of the chromosome, untrimmed, aux_idx all -1 */
 int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len, grom_stage *stage,
                  dd_parse_out *out, char *err, int errlen);
+/* n <= 512 bytes of device memory to the host after the context's work */
+int dd_copy_d2h(dd_ctx *c, void *dst, const void *src, size_t n);
 /* kept reads and dropped records at positions below s0 (the walk's skip
  * prefix) in a staged chromosome (positions sorted) */
 int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64_t *sd);

@@ -1333,6 +1333,16 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
     return 0;
 }
 
+// n bytes of device memory to the host, ordered after this context's work
+extern "C" int dd_copy_d2h(dd_ctx *c, void *dst, const void *src, size_t n) {
+    if (hipSetDevice(c->device) != hipSuccess || n > 64 * sizeof(int64_t) ||
+        hipMemcpyAsync(c->h_small, src, n, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+        hipStreamSynchronize(c->st) != hipSuccess)
+        return -1;
+    memcpy(dst, c->h_small, n);
+    return 0;
+}
+
 extern "C" int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64_t *sd) {
     if (hipSetDevice(c->device) != hipSuccess) return -1;
     grom_reads dv;

@@ -2570,7 +2570,7 @@ static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
     if (rc == 0 && !s->splitread && sd < po.n_drop) {
         grom_reads dv;
         grom_stage_dev_reads(c->stage, &dv);
-        if (grom_copy_d2h(&first_drop_before, dv.drop_before + sd, sizeof(int64_t), w->device)) rc = -1;
+        if (dd_copy_d2h(w->dd, &first_drop_before, dv.drop_before + sd, sizeof(int64_t))) rc = -1;
     }
     if (rc == 0 && ri >= 0 && grom_stage_trim_drops(c->stage, sd, sk) != GROM_OK) rc = -1;
     if (rc == 0 && grom_stage_trim(c->stage, sk) != GROM_OK) rc = -1;

@@ -1090,8 +1090,26 @@ struct grom_stage {
     int64_t tickets = 0;  // appends issued (ticket t uses ev[t % GROM_STAGE_EVENTS])
     int64_t done_upto = 0; // every ticket below this is known complete
     int64_t bytes_h2d = 0;
+    // scratch of the stage's own operations (put_aux, trim_drops): grows, is
+    // kept (a hipMalloc/hipFree pair per chromosome would wait for the device)
+    char *scratch = nullptr;
+    size_t scratch_cap = 0;
     char *a(int k) const { return blk + off[k]; }
 };
+
+static char *stage_scratch(grom_stage *s, size_t bytes) {
+    if (bytes <= s->scratch_cap) return s->scratch;
+    if (s->scratch) {
+        (void)hipStreamSynchronize(s->st);
+        (void)hipFree(s->scratch);
+    }
+    s->scratch = nullptr;
+    s->scratch_cap = 0;
+    const size_t want = bytes + bytes / 2 + 4096;
+    if (hipMalloc((void **)&s->scratch, want) != hipSuccess) return nullptr;
+    s->scratch_cap = want;
+    return s->scratch;
+}
 
 // bytes each array holds now (kept when the block grows)
 static void stage_used(const grom_stage *s, size_t u[SA_N]) {
@@ -1163,6 +1181,7 @@ void grom_stage_free(grom_stage *s) {
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->blk) (void)hipFree(s->blk);
+    if (s->scratch) (void)hipFree(s->scratch);
     for (int k = 0; k < GROM_STAGE_EVENTS; k++)
         if (s->ev[k]) (void)hipEventDestroy(s->ev[k]);
     if (s->all_ev) (void)hipEventDestroy(s->all_ev);
@@ -1186,7 +1205,12 @@ int grom_stage_begin(grom_stage *s, const grom_stage_sizes *est) {
                              sizeof(grom_aux) * (size_t)std::max<int64_t>(est->n_aux, 1), 4 * nd, 4 * nd, 8 * nd,
                              (size_t)std::max<int64_t>(est->ref_len, 16)};
         const size_t keep[SA_N] = {};
-        return stage_reserve(s, need, keep);
+        const int rc = stage_reserve(s, need, keep);
+        if (rc == GROM_OK && !stage_scratch(s, std::max(16 * nd, 8 * (size_t)std::max<int64_t>(est->n_aux, 1)))) {
+            set_err("grom_stage_begin: no device scratch");
+            return GROM_E_NOMEM;
+        }
+        return rc;
     }
     return GROM_OK;
 }
@@ -1449,15 +1473,14 @@ int grom_stage_put_aux(grom_stage *s, const grom_aux *aux, const int64_t *kidx, 
     need[SA_AUX] = sizeof(grom_aux) * (size_t)(s->n_aux + n + 1);
     int rc = stage_reserve(s, need, keep);
     if (rc) return rc;
-    int64_t *d_k = nullptr;
-    HIPCHK(hipMalloc((void **)&d_k, sizeof(int64_t) * (size_t)n));
+    int64_t *d_k = (int64_t *)stage_scratch(s, sizeof(int64_t) * (size_t)n);
+    if (!d_k) { set_err("grom_stage_put_aux: no device scratch"); return GROM_E_NOMEM; }
     HIPCHK(hipMemcpyAsync(s->a(SA_AUX) + sizeof(grom_aux) * s->n_aux, aux, sizeof(grom_aux) * (size_t)n,
                           hipMemcpyHostToDevice, s->st));
     HIPCHK(hipMemcpyAsync(d_k, kidx, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, s->st));
     hipLaunchKernelGGL(k_stage_aux_idx, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s->st,
                        (int32_t *)s->a(SA_AIDX), d_k, n, (int32_t)s->n_aux);
     HIPCHK(hipStreamSynchronize(s->st));
-    (void)hipFree(d_k);
     s->n_aux += n;
     return GROM_OK;
 }
@@ -1468,8 +1491,8 @@ int grom_stage_trim_drops(grom_stage *s, int64_t sd, int64_t sk) {
     const int64_t n = s->n_drop - sd;
     if (n > 0) {
         // through a scratch copy: the source and destination ranges overlap
-        char *tmp = nullptr;
-        HIPCHK(hipMalloc((void **)&tmp, 16 * (size_t)n));
+        char *tmp = stage_scratch(s, 16 * (size_t)n);
+        if (!tmp) { set_err("grom_stage_trim_drops: no device scratch"); return GROM_E_NOMEM; }
         int32_t *tp = (int32_t *)tmp, *tl = tp + n;
         int64_t *tb = (int64_t *)(tmp + 8 * (size_t)n);
         HIPCHK(hipMemcpyAsync(tp, (int32_t *)s->a(SA_DPOS) + sd, 4 * (size_t)n, hipMemcpyDeviceToDevice, s->st));
@@ -1479,7 +1502,6 @@ int grom_stage_trim_drops(grom_stage *s, int64_t sd, int64_t sk) {
                            s->st, (int32_t *)s->a(SA_DPOS), (int32_t *)s->a(SA_DLQ), (int64_t *)s->a(SA_DBEF), tp, tl,
                            tb, n, sk);
         HIPCHK(hipStreamSynchronize(s->st));
-        (void)hipFree(tmp);
     }
     s->n_drop = n;
     return GROM_OK;
