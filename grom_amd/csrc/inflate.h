@@ -12,14 +12,15 @@
 // so the 64 lanes of a wave, each in its own block, stay in step: no lane
 // waits for another's long match or for the end of another's DEFLATE block
 // (a nested per-block/per-match loop makes the whole wave wait for its
-// slowest lane at every level).  A match step is one 16-byte load and one
-// 16-byte store (unaligned dwordx4): the bytes past the match's end that the
-// store also writes are garbage that this lane overwrites later, since a
-// block's output is produced front to back; near the end of the block's
-// output the step falls back to single bytes.  A match whose distance is
-// below 16 copies its first distance bytes, then doubles the distance (the
-// output is periodic with the distance, so any multiple of it is a valid
-// source): 1, 2, 4, 8, 16, 16, ... bytes per step for a run of one byte.
+// slowest lane at every level).  A match step is four 16-byte loads and four
+// 16-byte stores (unaligned dwordx4; one wait for the loads per 64 bytes):
+// the bytes past the match's end that the stores also write are garbage
+// that this lane overwrites later, since a block's output is produced front
+// to back; near the end of the block's output the step falls back to single
+// bytes.  A match whose distance is below 64 copies its first distance bytes,
+// then doubles the distance (the output is periodic with the distance, so any
+// multiple of it is a valid source): 1, 2, 4, ..., 64, 64, ... bytes per step
+// for a run of one byte.
 //
 // Per lane, the Huffman tables are canonical: for each code length l the
 // left-justified end of its code range (lim[l]) and the offset from a code to
@@ -59,6 +60,9 @@
 #define GI_T_CL 89
 #define GI_LANE_DWORDS 94
 #define GI_LANE_BYTES (GI_LANE_DWORDS * 4)
+
+// bytes a match step copies: four 16-byte loads, then four stores
+#define GI_COPY 64u
 
 enum { GI_OK = 0, GI_E_HEADER = 1, GI_E_TREE = 2, GI_E_CODE = 3, GI_E_DIST = 4, GI_E_OVERRUN = 5, GI_E_INPUT = 6,
        GI_E_SIZE = 7 };
@@ -518,19 +522,25 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
         }
         // (a match starts copying in the step that decoded it)
         if (mode == GI_M_COPY) {
-            uint32_t m = rem < 16u ? rem : 16u;
+            uint32_t m = rem < GI_COPY ? rem : GI_COPY;
             m = m < D ? m : D;
             uint8_t *q = out + o;
-            if (o + 16 <= out_len) {  // sources all final: o - D + m <= o
-                gi_u32x4 v;
-                __builtin_memcpy(&v, q - D, 16);
-                __builtin_memcpy(q, &v, 16);
+            if (o + GI_COPY <= out_len) {  // sources all final: o - D + m <= o
+                gi_u32x4 v0, v1, v2, v3;
+                __builtin_memcpy(&v0, q - D, 16);
+                __builtin_memcpy(&v1, q - D + 16, 16);
+                __builtin_memcpy(&v2, q - D + 32, 16);
+                __builtin_memcpy(&v3, q - D + 48, 16);
+                __builtin_memcpy(q, &v0, 16);
+                __builtin_memcpy(q + 16, &v1, 16);
+                __builtin_memcpy(q + 32, &v2, 16);
+                __builtin_memcpy(q + 48, &v3, 16);
             } else {
                 for (uint32_t j = 0; j < m; j++) q[j] = q[(int64_t)j - D];
             }
             o += m;
             rem -= m;
-            if (m == D && D < 16) D <<= 1;
+            if (m == D && D < GI_COPY) D <<= 1;
             if (!rem) mode = GI_M_SYM;
         } else if (mode == GI_M_STORED) {
             // byte-aligned: up to 4 bytes from the bit buffer per step
