@@ -2602,11 +2602,19 @@ __device__ __forceinline__ int first_passage(uint64_t P, int n, int e, const Cls
 // the reference's order; any base whose window could pass within a margin
 // far above that difference is UNDECIDED and computed exactly (k_cnv_pre or
 // the walk), so the jumps and no-ops written are exact.
+//
+// The work per candidate ranges from one word (a jump near its start) to
+// L/64 = 157 words (a no-op window), so the lanes do not stay with one
+// candidate: each takes one segment per step and, when its candidate is
+// decided, the next candidate from the wave's share of a global queue (one
+// atomic per refill of the wave's idle lanes).  A wave runs until the queue
+// is empty and its lanes are idle, instead of waiting at every candidate for
+// its slowest lane.
 template <int KIND>
 __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand,
                                                       CandWords C, const double *__restrict__ wsdmin,
                                                       int32_t *__restrict__ nxt, int64_t *__restrict__ und,
-                                                      uint32_t *n_und, uint32_t und_cap) {
+                                                      uint32_t *n_und, uint32_t und_cap, uint32_t *__restrict__ qhead) {
     __shared__ ClsTabs T;
     // GROM_TIMING counters (W.stats + 24): candidates, phase-A jumps, first
     // window undecided, passing bases tested one by one, segments settled by
@@ -2615,67 +2623,91 @@ __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *_
     cls_tabs_build(T);
     if (W.stats && threadIdx.x < 8) cst[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long c_steps = 0, c_skip = 0, c_wstep = 0;
-    int c_out = -1;  // 0 jump, 1 first-window undecided, 2 B undecided, -1 no-op
-    if (i < n_cand) {
-        const int64_t p = cand[i] >> 1;
-        const int m = (int)(cand[i] & 1);
-        const int64_t L = W.L, ML = W.min_len, end = W.end, nw = C.n_words;
-        const double sgn = KIND == 0 ? 1.0 : -1.0;
+    const int lane = threadIdx.x & 63;
+    const int64_t L = W.L, ML = W.min_len, end = W.end, nw = C.n_words;
+    const double sgn = KIND == 0 ? 1.0 : -1.0;
+    unsigned long long c_steps = 0, c_skip = 0, c_wstep = 0, c_n[4] = {0, 0, 0, 0};  // jump, first undecided, B undecided, no-op
+    // the lane's candidate
+    uint32_t ci = 0;
+    bool busy = false;
+    int64_t p = 0, lo = 0, wl = 0, cnt = 0;
+    int m = 0, E = 0, phase = 0;  // phase 0: A, 1: B
+    bool defined = false;
+    double R = 0.0, A = 0.0;
+    bool drained = false;
+    for (;;) {
+        // refill the idle lanes from the queue
+        const unsigned long long idle = __ballot(!busy);
+        if (idle && !drained) {
+            const uint32_t k = (uint32_t)__popcll(idle);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(qhead, k);
+            base = (uint32_t)__shfl((int)base, 0);
+            if (base >= n_cand) drained = true;
+            if (!busy) {
+                const uint32_t mine = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1));
+                if (mine < n_cand) {
+                    ci = mine;
+                    busy = true;
+                    p = cand[ci] >> 1;
+                    m = (int)(cand[ci] & 1);
+                    lo = p;
+                    wl = cnt = 0;
+                    E = 0;
+                    phase = 0;
+                    defined = false;
+                    R = A = 0.0;
+                }
+            }
+        }
+        if (!__ballot(busy)) break;
+        if (!busy) continue;
+        // one segment of the lane's candidate
         const uint64_t *pmw = C.pm + (KIND * 2 + m) * nw, *pkw = C.pk + KIND * nw;
-        bool defined = false;
-        // the pass bits of a segment (mask M of word w) under the class rule
-        auto pass_bits = [&](int64_t w, uint64_t M) -> uint64_t {
-            if (defined) return pkw[w] & M;
-            const uint64_t dw = C.def[w] & M;
-            if (!dw) return pmw[w] & M;
-            const uint64_t below = (dw & (0 - dw)) - 1;
-            defined = true;
-            return ((pmw[w] & below) | (pkw[w] & ~below)) & M;
-        };
+        int outcome = -2;  // -2 running, 0 jump (out set), 1 first-window undecided, 2 B undecided, 3 no-op
         int32_t out = (int32_t)p;
-        bool undecided = false;
-        int E = 0;  // 2*cnt2 - wl
-        int64_t wl = 0, cnt = 0;
-        double R = 0.0, A = 0.0;
-        // phase A: the first ML bases (GROM.c:19370-19400)
-        for (int64_t lo = p; lo < p + ML;) {
-            const int64_t w = lo >> 6, hi = min(p + ML, (w + 1) << 6);
+        const int64_t lim = phase == 0 ? p + ML : min(p + L, end);
+        if (lo >= lim) {
+            outcome = 3;  // phase B reached its end (or an empty window): no stop, no call
+        } else {
+            const int64_t w = lo >> 6, hi = min(lim, (w + 1) << 6);
             const int s0 = (int)(lo & 63), n = (int)(hi - lo);
             const uint64_t M = low_bits(n) << s0;
-            const uint64_t P = pass_bits(w, M);
+            uint64_t P;
+            if (defined) {
+                P = pkw[w] & M;
+            } else {
+                const uint64_t dw = C.def[w] & M;
+                if (!dw) {
+                    P = pmw[w] & M;
+                } else {
+                    const uint64_t below = (dw & (0 - dw)) - 1;
+                    defined = true;
+                    P = ((pmw[w] & below) | (pkw[w] & ~below)) & M;
+                }
+            }
             const int j = first_passage(P >> s0, n, E, T);
-            if (j < n) {  // the stop: the walk jumps here
-                out = (int32_t)(lo + j);
-                c_out = 0;
-                goto done;
-            }
-            E += 2 * (int)__popcll(P) - n;
-            wl += n;
-            cnt += __popcll(C.nl[w] & M);
-            R += sgn * (C.rsa[hi - 1] - (s0 ? C.rsa[lo - 1] : 0.0));
-            A += C.babs[w];
-            lo = hi;
-        }
-        // the first window's z test (every base's z, nonlow count)
-        if (cnt > 0 && W.wsd[ML] > 0) {
-            const double d = (double)cnt * W.wsd[ML];
-            if (!(R + 1e-9 * (A + fabs(R)) + 1e-300 < 3.0 * d * (1.0 - 1e-15))) {
-                undecided = true;
-                c_out = 1;
-                goto done;
-            }
-        }
-        // phase B: extension to L (GROM.c:19405-19470); reaching `end` stops it
-        {
-            const int64_t xlim = min(p + L, end);
-            for (int64_t lo = p + ML; lo < xlim;) {
-                const int64_t w = lo >> 6, hi = min(xlim, (w + 1) << 6);
-                const int s0 = (int)(lo & 63), n = (int)(hi - lo);
-                const uint64_t M = low_bits(n) << s0;
-                const uint64_t P = pass_bits(w, M);
-                const int j = first_passage(P >> s0, n, E, T);
+            if (phase == 0) {
+                if (j < n) {  // the stop: the walk jumps here
+                    out = (int32_t)(lo + j);
+                    outcome = 0;
+                } else {
+                    E += 2 * (int)__popcll(P) - n;
+                    wl += n;
+                    cnt += __popcll(C.nl[w] & M);
+                    R += sgn * (C.rsa[hi - 1] - (s0 ? C.rsa[lo - 1] : 0.0));
+                    A += C.babs[w];
+                    lo = hi;
+                    if (lo == p + ML) {
+                        // the first window's z test (every base's z, nonlow count)
+                        if (cnt > 0 && W.wsd[ML] > 0) {
+                            const double d = (double)cnt * W.wsd[ML];
+                            if (!(R + 1e-9 * (A + fabs(R)) + 1e-300 < 3.0 * d * (1.0 - 1e-15))) outcome = 1;
+                        }
+                        phase = 1;
+                    }
+                }
+            } else {
                 const uint64_t Pr = (P >> s0) & low_bits(j);  // passing bases before the stop
                 const double base = s0 ? C.rsn[lo - 1] : 0.0;
                 if (Pr) {
@@ -2696,39 +2728,47 @@ __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *_
                             if (ws > 0) {
                                 const double d = (double)ck * ws;
                                 if (!(Rk + 1e-9 * (A + C.babs[w] + fabs(Rk)) + 1e-300 < 3.0 * d * (1.0 - 1e-15))) {
-                                    undecided = true;
-                                    c_out = 2;
-                                    goto done;
+                                    outcome = 2;
+                                    break;
                                 }
                             }
                         }
                     }
                 }
-                if (j < n) goto done;  // phase B stops without a call: no-op
-                E += 2 * (int)__popcll(P) - n;
-                wl += n;
-                cnt += __popcll(C.nl[w] & M);
-                R += sgn * (C.rsn[hi - 1] - base);
-                A += C.babs[w];
-                lo = hi;
+                if (outcome < 0) {
+                    if (j < n) {
+                        outcome = 3;  // phase B stops without a call: no-op
+                    } else {
+                        E += 2 * (int)__popcll(P) - n;
+                        wl += n;
+                        cnt += __popcll(C.nl[w] & M);
+                        R += sgn * (C.rsn[hi - 1] - base);
+                        A += C.babs[w];
+                        lo = hi;
+                    }
+                }
             }
         }
-    done:
-        if (undecided) {
-            out = NXT_UNDECIDED;
-            const uint32_t k = atomicAdd(n_und, 1u);
-            if (k < und_cap) und[k] = cand[i];
+        if (outcome >= 0) {
+            if (outcome == 1 || outcome == 2) {
+                out = NXT_UNDECIDED;
+                const uint32_t k = atomicAdd(n_und, 1u);
+                if (k < und_cap) und[k] = cand[ci];
+            }
+            nxt[m * W.len + p] = out;
+            c_n[outcome]++;
+            busy = false;
         }
-        nxt[m * W.len + p] = out;
     }
     if (W.stats) {
-        if (i < n_cand) {
-            atomicAdd(&cst[0], 1ull);
-            atomicAdd(&cst[c_out < 0 ? 6 : c_out == 0 ? 1 : c_out == 1 ? 2 : 5], 1ull);
-            atomicAdd(&cst[3], c_steps);
-            atomicAdd(&cst[4], c_skip);
-            atomicAdd(&cst[7], c_wstep);
-        }
+        atomicAdd(&cst[0], c_n[0] + c_n[1] + c_n[2] + c_n[3]);
+        atomicAdd(&cst[1], c_n[0]);
+        atomicAdd(&cst[2], c_n[1]);
+        atomicAdd(&cst[5], c_n[2]);
+        atomicAdd(&cst[6], c_n[3]);
+        atomicAdd(&cst[3], c_steps);
+        atomicAdd(&cst[4], c_skip);
+        atomicAdd(&cst[7], c_wstep);
         __syncthreads();
         if (threadIdx.x < 8) atomicAdd(W.stats + 24 + threadIdx.x, cst[threadIdx.x]);
     }
@@ -3802,11 +3842,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         if ((rc = grow(K.und, 8 * (size_t)ncand, err, errlen))) return rc;
                         int64_t *und = (int64_t *)K.und.p;
                         uint32_t *n_und = n_pre + 3;
-                        CK(hipMemsetAsync(n_und, 0, 4, st));
+                        uint32_t *qhead = n_pre + 4;  // the classification's work queue
+                        CK(hipMemsetAsync(n_und, 0, 8, st));  // n_und, qhead
+                        // a fixed grid of waves pulling candidates (k_cnv_classify): enough
+                        // to fill the chip, never more than the candidates need
+                        const unsigned gcls = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ncand + 255) / 256, 2048));
                         if (kind == 0)
-                            hipLaunchKernelGGL(k_cnv_classify<0>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand);
+                            hipLaunchKernelGGL(k_cnv_classify<0>, dim3(gcls), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand, qhead);
                         else
-                            hipLaunchKernelGGL(k_cnv_classify<1>, dim3((ncand + 255) / 256), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand);
+                            hipLaunchKernelGGL(k_cnv_classify<1>, dim3(gcls), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand, qhead);
                         CK(hipGetLastError());
                         uint32_t nu = 0;
                         CK(hipMemcpyAsync(&nu, n_und, 4, hipMemcpyDeviceToHost, st));
