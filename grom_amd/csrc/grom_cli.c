@@ -3,6 +3,7 @@
  * against grom_amd/lib/libgrom_amd.so) before the process ends. */
 #include <execinfo.h>
 #include <signal.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -25,5 +26,9 @@ int main(int argc, char **argv) {
     sigaction(SIGBUS, &sa, NULL);
     sigaction(SIGSEGV, &sa, NULL);
     sigaction(SIGABRT, &sa, NULL);
+    /* a whole-process run: the library may end the process once the outputs
+     * are written instead of freeing its device memory (GROM_CLI_PROCESS=0
+     * keeps the teardown) */
+    setenv("GROM_CLI_PROCESS", "1", 0);
     return grom_cli_main(argc, argv);
 }
