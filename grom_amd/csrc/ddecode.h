@@ -44,27 +44,29 @@ void dd_ctx_times(const dd_ctx *c, double ms[4]);
 /* record-walk sub-chunks whose guessed start was wrong (re-walked) / all */
 void dd_ctx_counts(const dd_ctx *c, int64_t *rewalked, int64_t *subchunks);
 /* the per-run device buffers sized for a run of `ubytes` inflated bytes,
- * `recs` records and `n_starts` index-named record starts (growth later frees
- * buffers, which waits for the device) */
-int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, char *err, int errlen);
+ * `recs` records and `n_starts` index-named record starts, in run slots
+ * 0..n_slots-1 (growth later frees buffers, which waits for the device) */
+int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, int n_slots, char *err, int errlen);
 /* a run's compressed bytes (h_comp pinned, 64 readable bytes past comp_len)
  * copied into device slot 0/1 on the context's copy stream; returns at once,
  * h_comp must stay untouched until a dd_run_load of the slot has returned */
 int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_t comp_len, char *err, int errlen);
 /* inflate a run's blocks (uploaded to `slot`; h_blk its block table, ubytes
- * the inflated size) and find its records from
- * the record starts h_starts (offsets into the inflated stream, the first
- * being the run's first record) up to u_end: *n_rec records (tid: the run's
- * target, for the record-start guesses).  0; -2 when
- * the data contradicts the index plan (the CLI then reads serially); -1 */
-int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
+ * the inflated size) into run slot `rslot` and find its records from the
+ * record starts h_starts (offsets into the inflated stream, the first being
+ * the run's first record) up to u_end: *n_rec records (tid: the run's target,
+ * for the record-start guesses).  Runs on the run slot's own stream and
+ * returns with the work done, so a second thread may load one run slot while
+ * the context parses the other.  0; -2 when the data contradicts the index
+ * plan (the CLI then reads serially); -1 */
+int dd_run_load(dd_ctx *c, int slot, int rslot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
                 int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int32_t tid, int64_t *n_rec,
                 char *err, int errlen);
-/* find_insert_mean's sample from every record of the loaded run (file order):
- * at most cap_left (insert, l_qseq) pairs into h_ins/h_lq, the mapped-bases
- * sum up to the pair that completes the cap (or over the run) */
-int dd_run_stats(dd_ctx *c, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq, int64_t *n_taken,
-                 int64_t *m_contrib, char *err, int errlen);
+/* find_insert_mean's sample from every record of the run in run slot rslot
+ * (file order): at most cap_left (insert, l_qseq) pairs into h_ins/h_lq, the
+ * mapped-bases sum up to the pair that completes the cap (or over the run) */
+int dd_run_stats(dd_ctx *c, int rslot, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq,
+                 int64_t *n_taken, int64_t *m_contrib, char *err, int errlen);
 typedef struct dd_parse_out {
     int64_t n_rec, n_kept, n_drop, n_cig, n_bases, n_auxc;
     int32_t last_pos, last_lq, last_hclip, last_kept;
@@ -73,9 +75,10 @@ typedef struct dd_parse_out {
     const uint8_t *aux_bytes;
     const int64_t *aux_off, *aux_kidx;
 } dd_parse_out;
-/* the loaded run's records j0.. parsed into `stage` (grom_stage_fill_begin):
- * every array of the chromosome, untrimmed, aux_idx all -1 */
-int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len, grom_stage *stage,
+/* the records j0.. of the run in run slot rslot parsed into `stage`
+ * (grom_stage_fill_begin): every array of the chromosome, untrimmed, aux_idx
+ * all -1 */
+int dd_run_parse(dd_ctx *c, int rslot, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len, grom_stage *stage,
                  dd_parse_out *out, char *err, int errlen);
 /* n <= 512 bytes of device memory to the host after the context's work */
 int dd_copy_d2h(dd_ctx *c, void *dst, const void *src, size_t n);

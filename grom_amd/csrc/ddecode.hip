@@ -886,25 +886,36 @@ __global__ void k_lower_bound(const int32_t *a, int64_t n, int32_t x, int64_t *o
     *out = lo;
 }
 
+// one loaded run: its inflated bytes and record offsets, loaded on the slot's
+// own stream (the prefetch thread inflates and walks run k+1 while the worker
+// parses run k on the context's stream)
+struct RunSlot {
+    DBuf U, blk, status, misc, S, ccnt, cbase, off, tmp;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[3] = {};
+    int64_t *h_small = nullptr;  // pinned
+    int64_t R = 0, nblk = 0, ubytes = 0;
+};
+
 struct dd_ctx {
     int device = -1;
+    RunSlot rs[DD_SLOTS];
     hipStream_t st = nullptr;
     hipStream_t cst = nullptr;  // compressed runs' host->device copies (dd_comp_upload, the prefetch thread)
     DBuf dcomp[DD_SLOTS];
     hipEvent_t cev[DD_SLOTS] = {};
     int64_t dcomp_len[DD_SLOTS] = {};
     hipEvent_t ev[4] = {};
-    DBuf blk, U, status, misc, S, ccnt, cbase, off;
+    DBuf misc;  // the parse's and the statistics' flags and scalars
     DBuf keep, kidx, drop, didx, auxc, aidx, ncig, coff, nb, boff, rpos, krec, keys, vals, keys2, vals2, head, tmp;
     DBuf srcs, tfq, tfs;  // per kept read: its bases' offset in U; per copy tile: its first read
     DBuf sq, sqi, sv, slq, sm, s_ins, s_lq, acand, alen, aoff, akidx, apack;
-    int64_t R = 0, nblk = 0, ubytes = 0;
     int64_t *h_small = nullptr;  // pinned: totals and scalars
     uint8_t *h_aux = nullptr;    // pinned: packed split-read candidate records
     size_t h_aux_cap = 0;
     float ms_inflate = 0, ms_walk = 0, ms_parse = 0;
-    int64_t n_rewalk = 0, n_sub = 0;
-    int cp_cap = CP_R;  // copy tiles staged in LDS up to this many reads (GROM_TEST_CP_UNSTAGED: 0, tests)  // sub-chunks re-walked by the verifying lane / all sub-chunks
+    int64_t n_rewalk = 0, n_sub = 0;  // record-walk sub-chunks re-walked by the verifying lane / all
+    int cp_cap = CP_R;  // copy tiles staged in LDS up to this many reads (GROM_TEST_CP_UNSTAGED: 0, tests)
     int ws_guess = 1;  // record-start guesses: 1 plausible headers, 0 none, 2 sub-chunk starts (GROM_WS_GUESS, tests)
 };
 
@@ -925,6 +936,8 @@ struct dd_ctx {
         }                                                                                            \
     } while (0)
 
+extern "C" void dd_ctx_free(dd_ctx *c);
+
 extern "C" dd_ctx *dd_ctx_new(int device) {
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     dd_ctx *c = new dd_ctx();
@@ -936,6 +949,13 @@ extern "C" dd_ctx *dd_ctx_new(int device) {
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
     for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming);
     if (hipHostMalloc((void **)&c->h_small, 64 * sizeof(int64_t), 0) != hipSuccess) c->h_small = nullptr;
+    for (int k = 0; k < DD_SLOTS; k++) {
+        RunSlot &r = c->rs[k];
+        if (hipStreamCreateWithFlags(&r.st, hipStreamNonBlocking) != hipSuccess) r.st = nullptr;
+        for (int e = 0; e < 3; e++) (void)hipEventCreate(&r.ev[e]);
+        if (hipHostMalloc((void **)&r.h_small, 16 * sizeof(int64_t), 0) != hipSuccess) r.h_small = nullptr;
+        if (!r.st || !r.h_small) { dd_ctx_free(c); return nullptr; }
+    }
     return c;
 }
 
@@ -948,7 +968,18 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
         if (c->dcomp[k].p) (void)hipFree(c->dcomp[k].p);
         if (c->cev[k]) (void)hipEventDestroy(c->cev[k]);
     }
-    DBuf *all[] = {&c->blk, &c->U, &c->status, &c->misc, &c->S, &c->ccnt, &c->cbase, &c->off, &c->keep,
+    for (int k = 0; k < DD_SLOTS; k++) {
+        RunSlot &r = c->rs[k];
+        if (r.st) (void)hipStreamSynchronize(r.st);
+        DBuf *rb[] = {&r.U, &r.blk, &r.status, &r.misc, &r.S, &r.ccnt, &r.cbase, &r.off, &r.tmp};
+        for (DBuf *b : rb)
+            if (b->p) (void)hipFree(b->p);
+        for (int e = 0; e < 3; e++)
+            if (r.ev[e]) (void)hipEventDestroy(r.ev[e]);
+        if (r.h_small) (void)hipHostFree(r.h_small);
+        if (r.st) (void)hipStreamDestroy(r.st);
+    }
+    DBuf *all[] = {&c->misc, &c->keep,
                    &c->kidx, &c->drop, &c->didx, &c->auxc, &c->aidx, &c->ncig, &c->coff, &c->nb, &c->boff, &c->rpos,
                    &c->krec, &c->keys, &c->vals, &c->keys2, &c->vals2, &c->head, &c->tmp, &c->sq, &c->sqi, &c->sv,
                    &c->srcs, &c->tfq, &c->tfs,
@@ -985,18 +1016,28 @@ extern "C" void dd_ctx_counts(const dd_ctx *c, int64_t *rewalked, int64_t *subch
 // the per-run buffers sized once for the largest run (ubytes inflated bytes,
 // recs records): growing them later frees the old buffer, which waits for the
 // whole device
-extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, char *err, int errlen) {
+extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, int n_slots, char *err,
+                          int errlen) {
     DCK(hipSetDevice(c->device));
-    DGROW(c->U, (size_t)ubytes + 64);
     // the small buffers too: a small hipMalloc waits behind any large one in
     // flight on another thread (the stage reservations), ~0.4 s at 30x
     const int64_t nblk = ubytes / 60000 + 1024;
-    DGROW(c->blk, sizeof(DdBlock) * (size_t)(nblk + 1));
-    DGROW(c->status, (size_t)nblk + 1);
+    for (int k = 0; k < n_slots && k < DD_SLOTS; k++) {
+        RunSlot &r = c->rs[k];
+        DGROW(r.U, (size_t)ubytes + 64);
+        DGROW(r.blk, sizeof(DdBlock) * (size_t)(nblk + 1));
+        DGROW(r.status, (size_t)nblk + 1);
+        DGROW(r.misc, 256);
+        DGROW(r.S, sizeof(int64_t) * (size_t)(n_starts + 1));
+        DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
+        DGROW(r.cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
+        DGROW(r.off, 8 * (size_t)(recs + 1));
+        size_t tb = 0;
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(n_starts + 1),
+                                             r.st));
+        DGROW(r.tmp, tb);
+    }
     DGROW(c->misc, 256);
-    DGROW(c->S, sizeof(int64_t) * (size_t)(n_starts + 1));
-    DGROW(c->ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
-    DGROW(c->cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
     {
         size_t tb = 0, t2 = 0, t3 = 0, t4 = 0;
         const int r = (int)std::min<int64_t>(recs + 1, INT32_MAX);
@@ -1009,7 +1050,6 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_sta
         DGROW(c->tmp, std::max(std::max(tb, t2), std::max(t3, t4)));
     }
     const size_t r4 = 4 * (size_t)(recs + 1), r8 = 8 * (size_t)(recs + 1);
-    DGROW(c->off, r8);
     DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
     DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
     DGROW(c->rpos, r4); DGROW(c->krec, r8); DGROW(c->srcs, r8); DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8);
@@ -1036,48 +1076,49 @@ extern "C" int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_
 // inflate a run's blocks (uploaded to `slot` by dd_comp_upload) and find its
 // records: starts[0..n_starts) are record offsets in the inflated stream (the
 // first = the run's first record), u_end its end
-extern "C" int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
+extern "C" int dd_run_load(dd_ctx *c, int slot, int rslot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
                            int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int32_t tid,
                            int64_t *n_rec, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
-    hipStream_t st = c->st;
-    if (slot < 0 || slot >= DD_SLOTS || c->dcomp_len[slot] != comp_len) {
+    if (slot < 0 || slot >= DD_SLOTS || rslot < 0 || rslot >= DD_SLOTS || c->dcomp_len[slot] != comp_len) {
         if (err) snprintf(err, (size_t)errlen, "device decode: slot %d does not hold the run", slot);
         return -1;
     }
-    DGROW(c->blk, sizeof(DdBlock) * (size_t)(nblk + 1));
-    DGROW(c->U, (size_t)ubytes + 64);
-    DGROW(c->status, (size_t)nblk + 1);
-    DGROW(c->misc, 256);
-    DGROW(c->S, sizeof(int64_t) * (size_t)(n_starts + 1));
-    DGROW(c->ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
-    DGROW(c->cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
+    RunSlot &r = c->rs[rslot];
+    hipStream_t st = r.st;
+    DGROW(r.blk, sizeof(DdBlock) * (size_t)(nblk + 1));
+    DGROW(r.U, (size_t)ubytes + 64);
+    DGROW(r.status, (size_t)nblk + 1);
+    DGROW(r.misc, 256);
+    DGROW(r.S, sizeof(int64_t) * (size_t)(n_starts + 1));
+    DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
+    DGROW(r.cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
     DCK(hipStreamWaitEvent(st, c->cev[slot], 0));
-    DCK(hipMemcpyAsync(c->blk.p, h_blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(c->S.p, h_starts, sizeof(int64_t) * (size_t)n_starts, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(P<int64_t>(c->S) + n_starts, &u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
-    uint32_t *bad = P<uint32_t>(c->misc);
-    DCK(hipEventRecord(c->ev[0], st));
-    if (dd_inflate_launch(st, P<uint8_t>(c->dcomp[slot]), P<DdBlock>(c->blk), nblk, P<uint8_t>(c->U), P<uint8_t>(c->status),
+    DCK(hipMemcpyAsync(r.blk.p, h_blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(r.S.p, h_starts, sizeof(int64_t) * (size_t)n_starts, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(P<int64_t>(r.S) + n_starts, &u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    DCK(hipMemsetAsync(r.misc.p, 0, 256, st));
+    uint32_t *bad = P<uint32_t>(r.misc);
+    DCK(hipEventRecord(r.ev[0], st));
+    if (dd_inflate_launch(st, P<uint8_t>(c->dcomp[slot]), P<DdBlock>(r.blk), nblk, P<uint8_t>(r.U), P<uint8_t>(r.status),
                           bad + 1)) {
         if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
         return -1;
     }
-    DCK(hipEventRecord(c->ev[1], st));
+    DCK(hipEventRecord(r.ev[1], st));
     // records: count per chunk, place, write offsets
-    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(c->U), P<int64_t>(c->S),
-                       n_starts, tid, c->ws_guess, bad + 4, P<uint32_t>(c->ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, bad);
+    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(r.U), P<int64_t>(r.S),
+                       n_starts, tid, c->ws_guess, bad + 4, P<uint32_t>(r.ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, bad);
     size_t tb = 0;
-    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->ccnt), P<uint32_t>(c->cbase), (int)n_starts, st));
-    DGROW(c->tmp, tb);
-    DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->ccnt), P<uint32_t>(c->cbase), (int)n_starts, st));
-    DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(c->cbase) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(c->ccnt) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)c->h_small + 8, bad, 8, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)c->h_small + 16, bad + 4, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)n_starts, st));
+    DGROW(r.tmp, tb);
+    DCK(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)n_starts, st));
+    DCK(hipMemcpyAsync(r.h_small, P<uint32_t>(r.cbase) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)r.h_small + 4, P<uint32_t>(r.ccnt) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)r.h_small + 8, bad, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)r.h_small + 16, bad + 4, 4, hipMemcpyDeviceToHost, st));
     DCK(hipStreamSynchronize(st));
-    const uint32_t *hs = (const uint32_t *)c->h_small;
+    const uint32_t *hs = (const uint32_t *)r.h_small;
     c->n_rewalk += hs[4];
     c->n_sub += (ubytes + WS_G - 1) / WS_G;
     if (hs[3]) {
@@ -1089,14 +1130,22 @@ extern "C" int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock 
         return -2;
     }
     const int64_t R = (int64_t)hs[0] + hs[1];
-    DGROW(c->off, sizeof(int64_t) * (size_t)(R + 1));
-    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(c->U), P<int64_t>(c->S),
-                       n_starts, tid, c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(c->cbase), P<int64_t>(c->off), bad);
-    DCK(hipEventRecord(c->ev[2], st));
+    DGROW(r.off, sizeof(int64_t) * (size_t)(R + 1));
+    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(r.U), P<int64_t>(r.S),
+                       n_starts, tid, c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), bad);
+    DCK(hipEventRecord(r.ev[2], st));
     DCK(hipGetLastError());
-    c->R = R;
-    c->nblk = nblk;
-    c->ubytes = ubytes;
+    // the run is complete before the slot is handed on (its caller may be the
+    // prefetch thread, the parse then runs on the context's own stream)
+    DCK(hipStreamSynchronize(st));
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, r.ev[0], r.ev[1]);
+    (void)hipEventElapsedTime(&b, r.ev[1], r.ev[2]);
+    c->ms_inflate += a;
+    c->ms_walk += b;
+    r.R = R;
+    r.nblk = nblk;
+    r.ubytes = ubytes;
     *n_rec = R;
     return 0;
 }
@@ -1104,11 +1153,13 @@ extern "C" int dd_run_load(dd_ctx *c, int slot, int64_t comp_len, const DdBlock 
 // find_insert_mean's sample from the loaded run, all of its records in file
 // order: at most cap_left (insert, l_qseq) pairs, and the mapped-bases sum up
 // to the record that completes the cap (or over the whole run)
-extern "C" int dd_run_stats(dd_ctx *c, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq,
+extern "C" int dd_run_stats(dd_ctx *c, int slot, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq,
                             int64_t *n_taken, int64_t *m_contrib, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
     hipStream_t st = c->st;
-    const int64_t R = c->R;
+    if (slot < 0 || slot >= DD_SLOTS) return -1;
+    RunSlot &rs = c->rs[slot];
+    const int64_t R = rs.R;
     *n_taken = 0;
     *m_contrib = 0;
     if (R == 0 || cap_left <= 0) return 0;
@@ -1120,7 +1171,7 @@ extern "C" int dd_run_stats(dd_ctx *c, int32_t min_mapq, int64_t cap_left, int32
     const int64_t take_cap = std::min<int64_t>(cap_left, R);
     DGROW(c->s_ins, 4 * (size_t)take_cap);
     DGROW(c->s_lq, 4 * (size_t)take_cap);
-    hipLaunchKernelGGL(k_stats, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off), R, min_mapq,
+    hipLaunchKernelGGL(k_stats, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off), R, min_mapq,
                        P<uint32_t>(c->sq), P<int32_t>(c->sv), P<int32_t>(c->slq), P<int64_t>(c->sm));
     size_t tb = 0, tb2 = 0;
     DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->sq), P<uint32_t>(c->sqi), (int)R, st));
@@ -1128,6 +1179,7 @@ extern "C" int dd_run_stats(dd_ctx *c, int32_t min_mapq, int64_t cap_left, int32
     DGROW(c->tmp, std::max(tb, tb2));
     DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->sq), P<uint32_t>(c->sqi), (int)R, st));
     DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, tb2, P<int64_t>(c->sm), P<int64_t>(c->sm), (int)R, st));
+    DGROW(c->misc, 256);
     int64_t *mcap = (int64_t *)((char *)c->misc.p + 64);
     DCK(hipMemsetAsync(mcap, 0xff, 8, st));
     hipLaunchKernelGGL(k_stats_take, dim3(grid_for(R)), dim3(256), 0, st, P<uint32_t>(c->sq), P<uint32_t>(c->sqi),
@@ -1155,20 +1207,25 @@ extern "C" int dd_run_stats(dd_ctx *c, int32_t min_mapq, int64_t cap_left, int32
 // the loaded run parsed into `stage` (records j0.. of the run): fields,
 // CIGAR words, bases, qualities, name ids, dropped records; the split-read
 // candidates' record bytes come back to the host (dd_run_aux)
-extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len,
+extern "C" int dd_run_parse(dd_ctx *c, int slot, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len,
                             grom_stage *stage, dd_parse_out *po, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
     hipStream_t st = c->st;
-    const int64_t R = c->R;
+    if (slot < 0 || slot >= DD_SLOTS) return -1;
+    RunSlot &rs = c->rs[slot];
+    const int64_t R = rs.R;
     memset(po, 0, sizeof(*po));
     const size_t r4 = 4 * (size_t)(R + 1), r8 = 8 * (size_t)(R + 1);
     DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
     DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
     DGROW(c->rpos, r4);
+    DGROW(c->misc, 256);
     uint32_t *bad = P<uint32_t>(c->misc);
     int64_t *tot = (int64_t *)((char *)c->misc.p + 128);
+    DCK(hipEventRecord(c->ev[2], st));
+    DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
     if (R > 0)
-        hipLaunchKernelGGL(k_rec_meta, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off), R, j0,
+        hipLaunchKernelGGL(k_rec_meta, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off), R, j0,
                            tid, P<uint32_t>(c->keep), P<uint32_t>(c->drop), P<uint32_t>(c->auxc), P<uint32_t>(c->ncig),
                            P<int64_t>(c->nb), P<int32_t>(c->rpos), bad);
     if (R > 0) {
@@ -1225,7 +1282,7 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
     // arrays are written on this context's stream, synchronised below before
     // the chromosome is handed to a scan)
     if (R > 0)
-        hipLaunchKernelGGL(k_rec_write, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off), R, j0,
+        hipLaunchKernelGGL(k_rec_write, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off), R, j0,
                            P<uint32_t>(c->keep), P<uint32_t>(c->kidx), P<uint32_t>(c->drop), P<uint32_t>(c->didx),
                            P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), P<uint32_t>(c->coff), P<int64_t>(c->boff),
                            P<int32_t>(c->rpos), so, P<int64_t>(c->krec), P<int64_t>(c->srcs), P<uint64_t>(c->keys),
@@ -1241,11 +1298,11 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
                                (const int32_t *)so.lq, n, P<int64_t>(c->tfq), P<int64_t>(c->tfs));
             if (nt_q > 0)
                 hipLaunchKernelGGL(k_copy_tiles<true>, dim3((unsigned)std::min<int64_t>(nt_q, 1 << 16)), dim3(256), 0, st,
-                                   P<uint8_t>(c->U), P<int64_t>(c->srcs), (const int64_t *)so.boff, (const int32_t *)so.lq,
+                                   P<uint8_t>(rs.U), P<int64_t>(c->srcs), (const int64_t *)so.boff, (const int32_t *)so.lq,
                                    n, P<int64_t>(c->tfq), nt_q, nbs, c->cp_cap, (uint8_t *)dv.qual);
             if (nt_s > 0)
                 hipLaunchKernelGGL(k_copy_tiles<false>, dim3((unsigned)std::min<int64_t>(nt_s, 1 << 16)), dim3(256), 0,
-                                   st, P<uint8_t>(c->U), P<int64_t>(c->srcs), (const int64_t *)so.boff,
+                                   st, P<uint8_t>(rs.U), P<int64_t>(c->srcs), (const int64_t *)so.boff,
                                    (const int32_t *)so.lq, n, P<int64_t>(c->tfs), nt_s, nbs / 2, c->cp_cap, (uint8_t *)dv.seq);
         }
         // read-name ids: sort the hashes, check each equal-hash run byte for byte
@@ -1261,14 +1318,14 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
                            P<uint32_t>(c->head));
         DCK(hipcub::DeviceScan::InclusiveScan(c->tmp.p, t2, P<uint32_t>(c->head), P<uint32_t>(c->head), hipcub::Max(),
                                               (int)n, st));
-        hipLaunchKernelGGL(k_name_ids, dim3(grid_for(n)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off),
+        hipLaunchKernelGGL(k_name_ids, dim3(grid_for(n)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off),
                            P<int64_t>(c->krec), P<uint64_t>(c->keys2), P<uint32_t>(c->vals2), P<uint32_t>(c->head), n,
                            so.nid, bad);
     }
     // split-read candidates: lengths, offsets, kept indices, packed bytes -> host
     int64_t apack = 0;
     if (na > 0) {
-        hipLaunchKernelGGL(k_aux_len, dim3(grid_for(na)), dim3(256), 0, st, P<uint8_t>(c->U), P<int64_t>(c->off),
+        hipLaunchKernelGGL(k_aux_len, dim3(grid_for(na)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off),
                            P<int64_t>(c->acand), na, P<int64_t>(c->alen), P<uint32_t>(c->kidx), P<int64_t>(c->akidx));
         size_t tb = 0;
         DCK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
@@ -1302,8 +1359,8 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
     if (na > 0) {
         apack = c->h_small[3];
         DGROW(c->apack, (size_t)apack + 16);
-        hipLaunchKernelGGL(k_aux_pack, dim3(grid_for(na, 1, 65536)), dim3(64), 0, st, P<uint8_t>(c->U),
-                           P<int64_t>(c->off), P<int64_t>(c->acand), P<int64_t>(c->aoff), na, P<uint8_t>(c->apack));
+        hipLaunchKernelGGL(k_aux_pack, dim3(grid_for(na, 1, 65536)), dim3(64), 0, st, P<uint8_t>(rs.U),
+                           P<int64_t>(rs.off), P<int64_t>(c->acand), P<int64_t>(c->aoff), na, P<uint8_t>(c->apack));
         const size_t need = (((size_t)apack + 15) & ~(size_t)15) + 16 * (size_t)(na + 1) + 64;
         if (need > c->h_aux_cap) {
             if (c->h_aux) (void)hipHostFree(c->h_aux);
@@ -1323,12 +1380,8 @@ extern "C" int dd_run_parse(dd_ctx *c, int64_t j0, int32_t tid, int32_t read_nam
     }
     DCK(hipEventRecord(c->ev[3], st));
     DCK(hipStreamSynchronize(st));
-    float a = 0, b = 0, d = 0;
-    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    float d = 0;
     (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
-    c->ms_inflate += a;
-    c->ms_walk += b;
     c->ms_parse += d;
     return 0;
 }

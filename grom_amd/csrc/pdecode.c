@@ -2038,7 +2038,13 @@ void pd_set_wanted(pd_session *s, const int *want) {
  * on the host, and the copy to the device slot of the same number started on
  * the decode context's copy stream -- all while the GPU inflates and parses
  * the run before it.  The worker takes a slot, loads it (dd_run_load) and
- * releases it; a run nobody takes is simply read again when needed. */
+ * releases it; a run nobody takes is simply read again when needed.
+ *
+ * With room on the device for two runs (w->preload) the prefetch thread also
+ * loads the run -- inflate and record walk into the run slot of the same
+ * number, on that slot's stream -- while the worker parses the run before it
+ * from the other run slot; the worker then holds its slot until the parse is
+ * done. */
 enum { PF_FREE = 0, PF_WANTED = 1, PF_READY = 2, PF_USED = 3 };
 typedef struct {
     int ri, state, rc;
@@ -2050,6 +2056,9 @@ typedef struct {
     int64_t *starts;
     int64_t starts_cap, m, u_end;
     double t_io;
+    int loaded;              /* preload: the run is in the run slot of this number */
+    int64_t R;
+    double t_load;
 } pf_slot;
 
 typedef struct {
@@ -2064,6 +2073,9 @@ typedef struct {
     int pf_started, pf_stop;
     int loaded;              /* run index whose records dd holds, -1 none */
     int64_t loaded_R;
+    int loaded_slot;         /* ... in this run slot */
+    int preload;             /* the prefetch thread loads runs too (two run slots reserved) */
+    pf_slot *held;           /* preload: the slot whose run the worker is using */
     int test_abort, n_done;  /* GROM_TEST_DD_ABORT=n: -2 at the n-th chromosome (tests) */
 } dd_worker;
 
@@ -2246,8 +2258,19 @@ static void *pf_main(void *arg) {
         pthread_mutex_unlock(&w->mu);
         char err[200] = "";
         pd_trace(w->s, PD_EV_PHASE, 101, 0);
-        const int rc = pf_read(w, sl, q, ri, err, (int)sizeof(err));
+        int rc = pf_read(w, sl, q, ri, err, (int)sizeof(err));
         pd_trace(w->s, PD_EV_PHASE, 101, 1);
+        sl->loaded = 0;
+        if (rc == 0 && __atomic_load_n(&w->preload, __ATOMIC_ACQUIRE)) {
+            const int rk = ri >= 0 ? ri : -ri - 2;
+            const double t0 = now_s();
+            pd_trace(w->s, PD_EV_PHASE, 102, 0);
+            rc = dd_run_load(w->dd, q, q, sl->len, sl->blk, sl->nb, sl->ub, sl->starts, sl->m, sl->u_end,
+                             w->s->runs[rk].tid, &sl->R, err, (int)sizeof(err));
+            pd_trace(w->s, PD_EV_PHASE, 102, 1);
+            sl->t_load = now_s() - t0;
+            sl->loaded = rc == 0;
+        }
         pthread_mutex_lock(&w->mu);
         sl->rc = rc;
         snprintf(sl->err, sizeof(sl->err), "%s", err);
@@ -2316,23 +2339,40 @@ static void pf_release(dd_worker *w, pf_slot *sl) {
 /* a run's records loaded on the device (inflate + record walk), its
  * compressed bytes from the prefetcher; then `next` (the run this worker
  * needs after it, -1 none) is asked for */
+static void dw_unhold(dd_worker *w) {
+    if (w->held) pf_release(w, w->held);
+    w->held = NULL;
+}
+
 static int dw_load(dd_worker *w, int key, int next, char *err, int errlen) {
     pd_session *s = w->s;
     const int ri = key >= 0 ? key : -key - 2;
     const pd_run *r = &s->runs[ri];
     int q = 0, rc = 0;
+    dw_unhold(w);
+    w->loaded = -1;
     const double tw = now_s();
     pf_slot *sl = pf_take(w, key, &q, &rc, err, errlen);
     const double t1 = now_s();
     if (rc) { pf_release(w, sl); return rc; }
     pf_want(w, next);
     int64_t R = 0;
-    pd_trace(s, PD_EV_PHASE, 102, 0);
-    rc = dd_run_load(w->dd, q, sl->len, sl->blk, sl->nb, sl->ub, sl->starts, sl->m, sl->u_end, r->tid, &R, err, errlen);
-    pd_trace(s, PD_EV_PHASE, 102, 1);
+    const int rs = w->preload ? q : 0;
+    double tdec = 0;
+    if (sl->loaded) {
+        R = sl->R;
+        tdec = sl->t_load;
+    } else {
+        pd_trace(s, PD_EV_PHASE, 102, 0);
+        rc = dd_run_load(w->dd, q, rs, sl->len, sl->blk, sl->nb, sl->ub, sl->starts, sl->m, sl->u_end, r->tid, &R, err,
+                         errlen);
+        pd_trace(s, PD_EV_PHASE, 102, 1);
+        tdec = now_s() - t1;
+    }
     const int64_t len = sl->len, ub = sl->ub;
     const double tio = sl->t_io;
-    pf_release(w, sl);
+    if (w->preload && rc == 0) w->held = sl; /* the run slot stays this run's until it is parsed */
+    else pf_release(w, sl);
     if (rc) return rc;
     if (key >= 0 && r->count >= 0 && R != r->count) {
         snprintf(err, (size_t)errlen, "target %d: %lld records decoded, the index counts %lld", r->tid, (long long)R,
@@ -2345,10 +2385,11 @@ static int dw_load(dd_worker *w, int key, int next, char *err, int errlen) {
     s->c_compressed += len;
     s->c_io_s += tio;
     s->c_wait_s += t1 - tw;
-    s->c_dec_s += now_s() - t1;
+    s->c_dec_s += tdec;
     pthread_mutex_unlock(&s->mu);
     w->loaded = key;  /* a prefix (key < -1) is never taken for the whole run */
     w->loaded_R = R;
+    w->loaded_slot = rs;
     return 0;
 }
 
@@ -2460,7 +2501,18 @@ static int dw_reserve(dd_worker *w, char *err, int errlen) {
     int64_t nst = 0;
     for (int t = 0; t < s->n_tgt; t++)
         if (s->n_lin[t] > nst) nst = s->n_lin[t];
-    return dd_reserve(w->dd, ub, recs + recs / 20, nst + 2, err, errlen);
+    /* two run slots (loads overlap parses) only on request (GROM_DD_PRELOAD=1)
+     * and when the device keeps room for them beside the stages: measured on
+     * the configs[2] whole run, the second slot's allocation and the reads
+     * serialised behind loads cost more than the overlap gains (DESIGN.md
+     * 4.5), the GPU being busy with the scans meanwhile */
+    const char *pe = getenv("GROM_DD_PRELOAD");
+    const int64_t fr = grom_device_mem_free(w->device);
+    const double need = 2.0 * ((double)ub + 8.0 * (double)recs) + (double)((int64_t)64 << 30);
+    const int two = pe && atoi(pe) != 0 && fr > 0 && (double)fr >= need;
+    const int rc = dd_reserve(w->dd, ub, recs + recs / 20, nst + 2, two ? 2 : 1, err, errlen);
+    if (rc == 0 && two) __atomic_store_n(&w->preload, 1, __ATOMIC_RELEASE);
+    return rc;
 }
 
 /* the next run (tid >= 0) after ri in file order, -1 none */
@@ -2487,7 +2539,7 @@ static int dw_stats(dd_worker *w, char *err, int errlen) {
             int64_t taken = 0, m = 0;
             const int64_t left = s->insert_cap - s->s_n;
             pd_trace(s, PD_EV_PHASE, 103, i);
-            rc = dd_run_stats(w->dd, s->min_mapq_stats, left, s->s_ins + s->s_n, s->s_lq + s->s_n, &taken, &m, err,
+            rc = dd_run_stats(w->dd, w->loaded_slot, s->min_mapq_stats, left, s->s_ins + s->s_n, s->s_lq + s->s_n, &taken, &m, err,
                               errlen);
             if (rc) return rc;
             if (pass == 0 && taken < left) continue; /* the prefix held too few: the whole run */
@@ -2521,9 +2573,11 @@ static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
         else rc = dw_load(w, ri, next_run, err, errlen);
         if (rc) return rc;
         j0 = s->runs[ri].j0;
-        rc = dd_run_parse(w->dd, j0, s->runs[ri].tid, s->read_name_len, s->plan[k].len, c->stage, &po, err, errlen);
+        rc = dd_run_parse(w->dd, w->loaded_slot, j0, s->runs[ri].tid, s->read_name_len, s->plan[k].len, c->stage, &po,
+                          err, errlen);
+        w->loaded = -1;
+        dw_unhold(w); /* its run slot is free for the run after the next */
         if (rc) return rc;
-        w->loaded = -1; /* the parse reuses the load's buffers */
     } else {
         grom_stage_sizes sz;
         grom_reads dv;
@@ -2681,6 +2735,7 @@ static void *dw_main(void *arg) {
         pthread_mutex_unlock(&s->mu);
     }
     if (rc == -2 || rc == -1) sess_abort(s, rc == -2, err);
+    dw_unhold(w);
     if (w->dd) {
         double ms[4];
         dd_ctx_times(w->dd, ms);

@@ -694,7 +694,10 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
     guesses at raw sub-chunk offsets (almost all wrong): every sub-chunk is
     then walked again from the true chain, with the same result.  Mode "cu"
     copies every base/quality tile through its global-memory path (the one
-    tiles with more reads than LDS holds take)."""
+    tiles with more reads than LDS holds take).  Mode "p1" loads each run on
+    the prefetch thread into a second run slot while the run before it is
+    parsed (GROM_DD_PRELOAD=1); the default keeps one run slot and loads on
+    the worker."""
     bam, fa = synth(datadir, case, CASES[case])
     tag = f"dd_{case}{''.join(extra).replace('-', '_')}"
     run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
@@ -703,7 +706,8 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
              "3w": {"GROM_DEVICE_DECODE": "1", "GROM_DD_WORKERS": "3"},
              "g0": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "0"},
              "g2": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "2"},
-             "cu": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_CP_UNSTAGED": "1"}}
+             "cu": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_CP_UNSTAGED": "1"},
+             "p1": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PRELOAD": "1"}}
     for mode, env in modes.items():
         capfd.readouterr()
         run_grom(datadir, bam, fa, f"g{mode}_{tag}.vcf", extra,

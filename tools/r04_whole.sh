@@ -3,7 +3,8 @@
 # optional GPU tests first, then a configs[2]-shape genome at SCALE of GRCh38's
 # lengths written by grom_synth and RUNS whole-run CLI calls (the first one
 # writes <fasta>.info), each timed, with the CLI's phase/decode lines; the
-# runs' outputs must be identical.  Everything goes to gpurun_out/OUT.
+# runs' outputs must be identical.  ALT_ENV="K=V ...": the last run with
+# that environment (e.g. a decode variant, checked against the others).  Everything goes to gpurun_out/OUT.
 set -o pipefail
 out=gpurun_out/$1
 scale=$2
@@ -28,7 +29,8 @@ timeout -k 10 400 $repo/grom_amd/bin/grom_synth -o $work/g -L $L -n $N $SY > /de
 echo "synth $(python3 -c "print(round($(date +%s.%N) - $t0, 1))") s, $(stat -c %s $work/g.bam) bytes"
 cd $work
 for r in $(seq 1 $runs); do
-  { time GROM_VERBOSE=1 GROM_TRACE=$repo/$out/trace_$r.csv timeout -k 10 120 $repo/grom_amd/bin/grom \
+  alt=""; [ $r -eq $runs ] && [ -n "$ALT_ENV" ] && alt="$ALT_ENV" && echo "== run $r with $ALT_ENV"
+  { time env $alt GROM_VERBOSE=1 GROM_TRACE=$repo/$out/trace_$r.csv timeout -k 10 120 $repo/grom_amd/bin/grom \
       -i g.bam -r g.fa -o w_$r.vcf -M -g 1 ${GROM_EXTRA_FLAGS} > $repo/$out/whole_$r.log 2>&1 ; } 2> $repo/$out/whole_$r.time \
       || { tail $repo/$out/whole_$r.log; exit 1; }
   echo "== run $r: $(cat $repo/$out/whole_$r.time)"
