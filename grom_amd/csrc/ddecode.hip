@@ -938,20 +938,32 @@ struct dd_ctx {
 
 extern "C" void dd_ctx_free(dd_ctx *c);
 
+// The decode is the whole run's critical path while the scans of earlier
+// chromosomes share the GPU: its streams ask for the device's highest queue
+// priority (GROM_DD_PRIORITY=0: the default priority)
+static hipError_t dd_stream_new(hipStream_t *st) {
+    const char *e = getenv("GROM_DD_PRIORITY");
+    int least = 0, greatest = 0;
+    if ((e == nullptr || atoi(e) != 0) && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+        greatest != least)
+        return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
 extern "C" dd_ctx *dd_ctx_new(int device) {
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     dd_ctx *c = new dd_ctx();
     c->device = device;
     if (getenv("GROM_WS_GUESS")) c->ws_guess = atoi(getenv("GROM_WS_GUESS"));
     if (getenv("GROM_TEST_CP_UNSTAGED")) c->cp_cap = 0;
-    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { delete c; return nullptr; }
-    if (hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) c->cst = nullptr;
+    if (dd_stream_new(&c->st) != hipSuccess) { delete c; return nullptr; }
+    if (dd_stream_new(&c->cst) != hipSuccess) c->cst = nullptr;
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
     for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming);
     if (hipHostMalloc((void **)&c->h_small, 64 * sizeof(int64_t), 0) != hipSuccess) c->h_small = nullptr;
     for (int k = 0; k < DD_SLOTS; k++) {
         RunSlot &r = c->rs[k];
-        if (hipStreamCreateWithFlags(&r.st, hipStreamNonBlocking) != hipSuccess) r.st = nullptr;
+        if (dd_stream_new(&r.st) != hipSuccess) r.st = nullptr;
         for (int e = 0; e < 3; e++) (void)hipEventCreate(&r.ev[e]);
         if (hipHostMalloc((void **)&r.h_small, 16 * sizeof(int64_t), 0) != hipSuccess) r.h_small = nullptr;
         if (!r.st || !r.h_small) { dd_ctx_free(c); return nullptr; }
