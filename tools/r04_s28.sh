@@ -26,7 +26,7 @@ for r in 1 2 3 4 5; do
   [ $r -gt 1 ] && { cmp w_1.vcf w_$r.vcf && cmp w_1.ctx.vcf w_$r.ctx.vcf || exit 1; }
 done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $repo/$out/prof -o run -- \
+GROM_EXIT_HANDLERS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $repo/$out/prof -o run -- \
     $repo/grom_amd/bin/grom -i $work/g.bam -r $work/g.fa -o $work/p.vcf -M -g 1 > $repo/$out/prof_run.log 2>&1 || { tail $repo/$out/prof_run.log; exit 1; }
 cd $repo
 db=$(find $out/prof -name "*.db" | head -1)
