@@ -2607,9 +2607,13 @@ __device__ __forceinline__ int first_passage(uint64_t P, int n, int e, const Cls
 // L/64 = 157 words (a no-op window), so the lanes do not stay with one
 // candidate: each takes one segment per step and, when its candidate is
 // decided, the next candidate from the wave's share of a global queue (one
-// atomic per refill of the wave's idle lanes).  A wave runs until the queue
+// atomic per CLS_GRAB candidates).  A wave runs until the queue
 // is empty and its lanes are idle, instead of waiting at every candidate for
 // its slowest lane.
+
+// candidates a wave takes from the global queue at a time
+constexpr uint32_t CLS_GRAB = 128;
+
 template <int KIND>
 __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand,
                                                       CandWords C, const double *__restrict__ wsdmin,
@@ -2635,30 +2639,39 @@ __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *_
     bool defined = false;
     double R = 0.0, A = 0.0;
     bool drained = false;
+    uint32_t qb = 0, qe = 0;  // the wave's share of the queue not yet handed to a lane (wave-uniform)
     for (;;) {
-        // refill the idle lanes from the queue
-        const unsigned long long idle = __ballot(!busy);
-        if (idle && !drained) {
-            const uint32_t k = (uint32_t)__popcll(idle);
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(qhead, k);
-            base = (uint32_t)__shfl((int)base, 0);
-            if (base >= n_cand) drained = true;
-            if (!busy) {
-                const uint32_t mine = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1));
-                if (mine < n_cand) {
-                    ci = mine;
-                    busy = true;
-                    p = cand[ci] >> 1;
-                    m = (int)(cand[ci] & 1);
-                    lo = p;
-                    wl = cnt = 0;
-                    E = 0;
-                    phase = 0;
-                    defined = false;
-                    R = A = 0.0;
+        // refill the idle lanes: from the wave's share, then (one atomic per
+        // CLS_GRAB candidates) a new share
+        unsigned long long idle = __ballot(!busy);
+        for (int pass = 0; pass < 2 && idle && !drained; pass++) {
+            if (qb >= qe) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(qhead, (uint32_t)CLS_GRAB);
+                base = (uint32_t)__shfl((int)base, 0);
+                if (base >= n_cand) {
+                    drained = true;
+                    break;
                 }
+                qb = base;
+                qe = min(base + (uint32_t)CLS_GRAB, n_cand);
             }
+            const uint32_t avail = qe - qb, n_idle = (uint32_t)__popcll(idle);
+            const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane) - 1));
+            if (!busy && rank < avail) {
+                ci = qb + rank;
+                busy = true;
+                p = cand[ci] >> 1;
+                m = (int)(cand[ci] & 1);
+                lo = p;
+                wl = cnt = 0;
+                E = 0;
+                phase = 0;
+                defined = false;
+                R = A = 0.0;
+            }
+            qb += min(n_idle, avail);
+            idle = __ballot(!busy);
         }
         if (!__ballot(busy)) break;
         if (!busy) continue;
