@@ -2787,6 +2787,141 @@ __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *_
     }
 }
 
+// The same classification with one lane per candidate for its whole window
+// (GROM_CNV_CLS=0): lanes of a wave walk neighbouring candidates in step, so
+// their word loads coalesce, but a wave waits for its longest candidate.
+template <int KIND>
+__global__ __launch_bounds__(256) void k_cnv_classify_lane(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand,
+                                                      CandWords C, const double *__restrict__ wsdmin,
+                                                      int32_t *__restrict__ nxt, int64_t *__restrict__ und,
+                                                      uint32_t *n_und, uint32_t und_cap) {
+    __shared__ ClsTabs T;
+    // GROM_TIMING counters (W.stats + 24): candidates, phase-A jumps, first
+    // window undecided, passing bases tested one by one, segments settled by
+    // the bound, phase-B undecided, no-ops, segments tested base by base
+    __shared__ unsigned long long cst[8];
+    cls_tabs_build(T);
+    if (W.stats && threadIdx.x < 8) cst[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long c_steps = 0, c_skip = 0, c_wstep = 0;
+    int c_out = -1;  // 0 jump, 1 first-window undecided, 2 B undecided, -1 no-op
+    if (i < n_cand) {
+        const int64_t p = cand[i] >> 1;
+        const int m = (int)(cand[i] & 1);
+        const int64_t L = W.L, ML = W.min_len, end = W.end, nw = C.n_words;
+        const double sgn = KIND == 0 ? 1.0 : -1.0;
+        const uint64_t *pmw = C.pm + (KIND * 2 + m) * nw, *pkw = C.pk + KIND * nw;
+        bool defined = false;
+        // the pass bits of a segment (mask M of word w) under the class rule
+        auto pass_bits = [&](int64_t w, uint64_t M) -> uint64_t {
+            if (defined) return pkw[w] & M;
+            const uint64_t dw = C.def[w] & M;
+            if (!dw) return pmw[w] & M;
+            const uint64_t below = (dw & (0 - dw)) - 1;
+            defined = true;
+            return ((pmw[w] & below) | (pkw[w] & ~below)) & M;
+        };
+        int32_t out = (int32_t)p;
+        bool undecided = false;
+        int E = 0;  // 2*cnt2 - wl
+        int64_t wl = 0, cnt = 0;
+        double R = 0.0, A = 0.0;
+        // phase A: the first ML bases (GROM.c:19370-19400)
+        for (int64_t lo = p; lo < p + ML;) {
+            const int64_t w = lo >> 6, hi = min(p + ML, (w + 1) << 6);
+            const int s0 = (int)(lo & 63), n = (int)(hi - lo);
+            const uint64_t M = low_bits(n) << s0;
+            const uint64_t P = pass_bits(w, M);
+            const int j = first_passage(P >> s0, n, E, T);
+            if (j < n) {  // the stop: the walk jumps here
+                out = (int32_t)(lo + j);
+                c_out = 0;
+                goto done;
+            }
+            E += 2 * (int)__popcll(P) - n;
+            wl += n;
+            cnt += __popcll(C.nl[w] & M);
+            R += sgn * (C.rsa[hi - 1] - (s0 ? C.rsa[lo - 1] : 0.0));
+            A += C.babs[w];
+            lo = hi;
+        }
+        // the first window's z test (every base's z, nonlow count)
+        if (cnt > 0 && W.wsd[ML] > 0) {
+            const double d = (double)cnt * W.wsd[ML];
+            if (!(R + 1e-9 * (A + fabs(R)) + 1e-300 < 3.0 * d * (1.0 - 1e-15))) {
+                undecided = true;
+                c_out = 1;
+                goto done;
+            }
+        }
+        // phase B: extension to L (GROM.c:19405-19470); reaching `end` stops it
+        {
+            const int64_t xlim = min(p + L, end);
+            for (int64_t lo = p + ML; lo < xlim;) {
+                const int64_t w = lo >> 6, hi = min(xlim, (w + 1) << 6);
+                const int s0 = (int)(lo & 63), n = (int)(hi - lo);
+                const uint64_t M = low_bits(n) << s0;
+                const uint64_t P = pass_bits(w, M);
+                const int j = first_passage(P >> s0, n, E, T);
+                const uint64_t Pr = (P >> s0) & low_bits(j);  // passing bases before the stop
+                const double base = s0 ? C.rsn[lo - 1] : 0.0;
+                if (Pr) {
+                    const double ub = KIND == 0 ? R + (C.bmax[w] - base) : R - (C.bmin[w] - base);
+                    const double dlo = (double)(cnt + 1) * wsdmin[wl + 1];
+                    const double slack = 1e-9 * (A + C.babs[w] + fabs(ub)) + 1e-300;
+                    if (dlo > 0 && ub + slack < 3.0 * dlo * (1.0 - 1e-15)) {
+                        c_skip++;
+                    } else {
+                        c_wstep++;
+                        const uint64_t nlr = C.nl[w] >> s0;
+                        for (uint64_t q = Pr; q; q &= q - 1) {
+                            const int k = __ffsll((long long)q) - 1;
+                            const double Rk = R + sgn * (C.rsn[lo + k] - base);
+                            const int64_t ck = cnt + __popcll(nlr & low_bits(k + 1));
+                            const double ws = W.wsd[wl + k + 1];
+                            c_steps++;
+                            if (ws > 0) {
+                                const double d = (double)ck * ws;
+                                if (!(Rk + 1e-9 * (A + C.babs[w] + fabs(Rk)) + 1e-300 < 3.0 * d * (1.0 - 1e-15))) {
+                                    undecided = true;
+                                    c_out = 2;
+                                    goto done;
+                                }
+                            }
+                        }
+                    }
+                }
+                if (j < n) goto done;  // phase B stops without a call: no-op
+                E += 2 * (int)__popcll(P) - n;
+                wl += n;
+                cnt += __popcll(C.nl[w] & M);
+                R += sgn * (C.rsn[hi - 1] - base);
+                A += C.babs[w];
+                lo = hi;
+            }
+        }
+    done:
+        if (undecided) {
+            out = NXT_UNDECIDED;
+            const uint32_t k = atomicAdd(n_und, 1u);
+            if (k < und_cap) und[k] = cand[i];
+        }
+        nxt[m * W.len + p] = out;
+    }
+    if (W.stats) {
+        if (i < n_cand) {
+            atomicAdd(&cst[0], 1ull);
+            atomicAdd(&cst[c_out < 0 ? 6 : c_out == 0 ? 1 : c_out == 1 ? 2 : 5], 1ull);
+            atomicAdd(&cst[3], c_steps);
+            atomicAdd(&cst[4], c_skip);
+            atomicAdd(&cst[7], c_wstep);
+        }
+        __syncthreads();
+        if (threadIdx.x < 8) atomicAdd(W.stats + 24 + threadIdx.x, cst[threadIdx.x]);
+    }
+}
+
 // a call is on the true walk iff its start was visited in its class
 // (chunks the true walk jumps over entirely are flagged in `skipped`)
 __global__ void k_cnv_calls_valid(const CallRec *calls, uint32_t n, const uint8_t *vis, const uint8_t *skipped,
@@ -3860,7 +3995,17 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         // a fixed grid of waves pulling candidates (k_cnv_classify): enough
                         // to fill the chip, never more than the candidates need
                         const unsigned gcls = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ncand + 255) / 256, 2048));
-                        if (kind == 0)
+                        static const int cls_queue = [] {
+                            const char *e = getenv("GROM_CNV_CLS");
+                            return e ? atoi(e) : 1;
+                        }();
+                        if (!cls_queue) {
+                            const unsigned gl = (unsigned)((ncand + 255) / 256);
+                            if (kind == 0)
+                                hipLaunchKernelGGL(k_cnv_classify_lane<0>, dim3(gl), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand);
+                            else
+                                hipLaunchKernelGGL(k_cnv_classify_lane<1>, dim3(gl), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand);
+                        } else if (kind == 0)
                             hipLaunchKernelGGL(k_cnv_classify<0>, dim3(gcls), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand, qhead);
                         else
                             hipLaunchKernelGGL(k_cnv_classify<1>, dim3(gcls), dim3(256), 0, st, WK, cand, ncand, CW, (const double *)S->wsdmin.p, nxt, und, n_und, ncand, qhead);
