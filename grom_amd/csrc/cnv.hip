@@ -2788,8 +2788,9 @@ __global__ __launch_bounds__(256) void k_cnv_classify(WalkIn W, const int64_t *_
 }
 
 // The same classification with one lane per candidate for its whole window
-// (GROM_CNV_CLS=0): lanes of a wave walk neighbouring candidates in step, so
-// their word loads coalesce, but a wave waits for its longest candidate.
+// (the default; GROM_CNV_CLS=1 takes the queue kernel above): lanes of a wave
+// walk neighbouring candidates in step, so their word loads coalesce, but a
+// wave waits for its longest candidate.  Measured faster than the queue.
 template <int KIND>
 __global__ __launch_bounds__(256) void k_cnv_classify_lane(WalkIn W, const int64_t *__restrict__ cand, uint32_t n_cand,
                                                       CandWords C, const double *__restrict__ wsdmin,
@@ -3996,8 +3997,10 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         // to fill the chip, never more than the candidates need
                         const unsigned gcls = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ncand + 255) / 256, 2048));
                         static const int cls_queue = [] {
+                            // default: lane per candidate (150 Mb chromosome, walks
+                            // 32-34 ms against 40-41 ms with the queue)
                             const char *e = getenv("GROM_CNV_CLS");
-                            return e ? atoi(e) : 1;
+                            return e ? atoi(e) : 0;
                         }();
                         if (!cls_queue) {
                             const unsigned gl = (unsigned)((ncand + 255) / 256);

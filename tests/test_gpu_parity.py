@@ -265,6 +265,21 @@ def test_cnv_wave_window_search(datadir, case, extra):
     assert ov == gv
 
 
+@pytest.mark.parametrize("case,extra", [("cnv", ["-V", "1"]), ("cnv_long", ["-V", "1", "-M"]),
+                                        ("cnv_multi", ["-V", "1", "-p", "3"])],
+                         ids=["cnv_V1", "cnv_long_V1_M", "cnv_multi_V1_p3"])
+def test_cnv_classify_queue(datadir, case, extra):
+    """The candidate classification as a per-wave work queue (k_cnv_classify,
+    GROM_CNV_CLS=1: lanes refill from the wave's queue share when their
+    candidate is decided) instead of one lane per candidate (the default,
+    faster on the 150 Mb timing case): the same rows as the oracle's."""
+    bam, fa, tag = _oracle_once(datadir, case, extra)
+    run_grom(datadir, bam, fa, f"gq_{tag}.vcf", extra, env_extra={"GROM_CNV_CLS": "1"})
+    ov, gv = open(datadir / f"o_{tag}.vcf").read(), open(datadir / f"gq_{tag}.vcf").read()
+    assert ov.count("<DEL>") + ov.count("<DUP>") > 0
+    assert ov == gv
+
+
 @pytest.mark.parametrize("case,extra", [("cnv", ["-V", "1"]), ("cnv_multi", ["-V", "1", "-p", "3"])],
                          ids=["cnv_V1", "cnv_multi_V1_p3"])
 def test_cnv_serial_stdev_path(datadir, case, extra):
