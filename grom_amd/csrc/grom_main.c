@@ -1021,9 +1021,9 @@ static int chrom_wanted(const char *name) {
     return 0;
 }
 
-/* GROM_CLI_PROCESS=1 (set by the `grom` executable's main, not by in-process
- * callers such as the Python binding): the process ends once a streamed run's
- * outputs are written */
+/* GROM_CLI_PROCESS=1 (opt-in, for a `grom` process; never for in-process
+ * callers such as the Python binding): the process ends once a streamed
+ * run's outputs are written */
 static int cli_process_exit(void) {
     const char *e = getenv("GROM_CLI_PROCESS");
     return e && atoi(e) == 1;
