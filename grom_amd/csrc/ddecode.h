@@ -86,6 +86,9 @@ int dd_copy_d2h(dd_ctx *c, void *dst, const void *src, size_t n);
  * prefix) in a staged chromosome (positions sorted) */
 int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64_t *sd);
 
+/* the device's first allocation of the process (its memory set up), done
+ * ahead on a start-up thread */
+void dd_device_warm(int device);
 /* wall time of a device allocation (stage growth), added to dd_ctx_times' ms[3] */
 void grom_note_alloc_ns(int64_t ns, size_t bytes);
 

@@ -21,6 +21,7 @@
 
 #include "../../include/grom_amd.h"
 #include "bamio.h"
+#include "ddecode.h"
 #include "stream.h"
 #include "pdecode.h"
 #include "ddecode.h"
@@ -649,8 +650,9 @@ typedef struct {
 } cli_state;
 
 static void *hip_init_main(void *arg) {
-    (void)arg;
+    const int device = *(const int *)arg;
     (void)grom_device_count();
+    if (getenv("GROM_NO_WARM") == NULL) dd_device_warm(device);
     return NULL;
 }
 
@@ -1414,7 +1416,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
         goto out_hdr;
     }
     g_plan_only = getenv("GROM_PLAN_ONLY") != NULL;
-    if (!g_plan_only) S->hip_started = pthread_create(&S->hip_thr, NULL, hip_init_main, NULL) == 0;
+    if (!g_plan_only) S->hip_started = pthread_create(&S->hip_thr, NULL, hip_init_main, &S->device) == 0;
     /* tables (read_binom_tables, GROM.c:22234) on a thread beside the decode */
     {
         size_t tn = (size_t)(GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);
