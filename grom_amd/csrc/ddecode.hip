@@ -1079,6 +1079,26 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_sta
     DGROW(c->vals2, r4); DGROW(c->head, r4);
     // the insert statistics' arrays (dd_run_stats)
     DGROW(c->sq, r4); DGROW(c->sqi, r4); DGROW(c->sv, r4); DGROW(c->slq, r4); DGROW(c->sm, r8);
+    const size_t take = 4 * (size_t)std::min<int64_t>(recs + 1, (int64_t)1 << 24);
+    DGROW(c->s_ins, take); DGROW(c->s_lq, take);
+    // the parse's small arrays too (a small allocation made while the stage
+    // helper's 20 GB ones are in flight waited 0.3-0.4 s): copy-tile starts
+    // (bases <= inflated bytes) and the split-read candidates (generously:
+    // one record in 8, 512 bytes per packed record for one in 64)
+    DGROW(c->tfq, 8 * (size_t)(ubytes / CP_T + 2));
+    DGROW(c->tfs, 8 * (size_t)(ubytes / 2 / CP_T + 2));
+    const size_t na = (size_t)(recs / 8 + 2);
+    DGROW(c->acand, 8 * na); DGROW(c->alen, 8 * na); DGROW(c->aoff, 8 * na); DGROW(c->akidx, 8 * na);
+    DGROW(c->apack, (size_t)(recs / 64 + 1) * 512);
+    if (c->h_aux_cap < ((size_t)16 << 20)) {  // their host copy: a few MB per chromosome at 30x
+        if (c->h_aux) (void)hipHostFree(c->h_aux);
+        c->h_aux = nullptr;
+        c->h_aux_cap = (size_t)16 << 20;
+        if (hipHostMalloc((void **)&c->h_aux, c->h_aux_cap, 0) != hipSuccess) {
+            c->h_aux = nullptr;
+            c->h_aux_cap = 0;
+        }
+    }
     return 0;
 }
 
