@@ -645,6 +645,7 @@ typedef struct {
     int wdev[64], n_work, n_init;
     double t_cli0, t_cand; /* CLI start, candidates (FASTA lengths) done */
     double t_scans, t_pdclose, t_outputs; /* scans done, decoder closed, outputs written */
+    double t_decclose;                     /* the decoder's host side closed */
     pthread_t hip_thr;     /* HIP runtime start-up, beside the header/FASTA/index work */
     int hip_started;
 } cli_state;
@@ -1031,6 +1032,11 @@ static int cli_process_exit(void) {
     return e && atoi(e) == 1;
 }
 
+static void *stage_free_main(void *arg) {
+    grom_stage_free((grom_stage *)arg);
+    return NULL;
+}
+
 static int run_streamed(cli_state *S) {
     grom_params *P = &S->P;
     const double t_start = clock_gettime_s();
@@ -1303,7 +1309,20 @@ done:
         _exit(0);
     }
     pd_close(pd);
-    for (int i = 0; i < n_stages; i++) grom_stage_free(stages[i]);
+    S->t_decclose = clock_gettime_s();
+    if (getenv("GROM_PAR_FREE") && atoi(getenv("GROM_PAR_FREE")) == 1 && n_stages > 1) {
+        /* (timing probe) the stages freed on threads of their own */
+        pthread_t th[64];
+        int started[64] = {0};
+        for (int i = 0; i < n_stages && i < 64; i++)
+            started[i] = pthread_create(&th[i], NULL, stage_free_main, stages[i]) == 0;
+        for (int i = 0; i < n_stages; i++) {
+            if (i < 64 && started[i]) pthread_join(th[i], NULL);
+            else grom_stage_free(stages[i]);
+        }
+    } else {
+        for (int i = 0; i < n_stages; i++) grom_stage_free(stages[i]);
+    }
     S->t_pdclose = clock_gettime_s();
     free(ctx_all.p);
     free(plan);
@@ -1486,9 +1505,9 @@ static int cli_run(int argc, char **argv, int force_serial) {
     tables_join(S);
     for (int d = 0; d < S->n_init; d++) grom_dev_fini(d);
     if (S->verbose && S->t_outputs > 0)
-        printf("cli teardown (s from start): scans done %.3f, outputs %.3f, decoder + stages freed %.3f, contexts "
-               "freed %.3f\n", S->t_scans - S->t_cli0, S->t_outputs - S->t_cli0, S->t_pdclose - S->t_cli0,
-               clock_gettime_s() - S->t_cli0);
+        printf("cli teardown (s from start): scans done %.3f, outputs %.3f, decoder closed %.3f, stages freed %.3f, "
+               "contexts freed %.3f\n", S->t_scans - S->t_cli0, S->t_outputs - S->t_cli0, S->t_decclose - S->t_cli0,
+               S->t_pdclose - S->t_cli0, clock_gettime_s() - S->t_cli0);
     for (int i = 0; i < S->n_cand; i++) {
         free(S->plan[i].target);
         free(S->plan[i].ref);
