@@ -2698,7 +2698,8 @@ static void *dw_main(void *arg) {
      * large one in flight) */
     pthread_t stres_thr;
     stres_job sj = {s, w->device};
-    const int stres = rc == 0 && w->sub == 0 && getenv("GROM_NO_STAGE_RESERVE") == NULL &&
+    const char *nsr = getenv("GROM_NO_STAGE_RESERVE");
+    const int stres = rc == 0 && w->sub == 0 && !(nsr && atoi(nsr) == 1) &&
                       pthread_create(&stres_thr, NULL, stres_main, &sj) == 0;
     if (rc == 0 && w->first) rc = dw_stats(w, err, (int)sizeof(err));
     if (stres) pthread_join(stres_thr, NULL); /* the stages are the worker's again */
