@@ -52,6 +52,7 @@
 #include <vector>
 
 #include "cnv.h"
+#include "ddecode.h"
 
 namespace {
 
@@ -2979,7 +2980,10 @@ namespace {
 static int grow(Buf &b, size_t bytes, char *err, size_t errlen) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return GROM_OK;
-    if (b.p) (void)hipFree(b.p);
+    if (b.p) {
+        (void)hipFree(b.p);
+        grom_dev_note(GROM_DEVCAT_CNV, -(int64_t)b.cap);
+    }
     b.p = nullptr;
     b.cap = 0;
     size_t want = bytes + bytes / 8 + 256;
@@ -2988,6 +2992,7 @@ static int grow(Buf &b, size_t bytes, char *err, size_t errlen) {
         return GROM_E_NOMEM;
     }
     b.cap = want;
+    grom_dev_note(GROM_DEVCAT_CNV, (int64_t)want);
     return GROM_OK;
 }
 
@@ -3233,11 +3238,17 @@ void cnv_scratch_free(CnvScratch *S) {
                   &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover, &S->cwords, &S->cw_seg,
                   &S->cw_carry, &S->wsdmin, &S->gen1000, &S->gpre, &S->gtmp};
     for (Buf *b : all)
-        if (b->p) (void)hipFree(b->p);
+        if (b->p) {
+            (void)hipFree(b->p);
+            grom_dev_note(GROM_DEVCAT_CNV, -(int64_t)b->cap);
+        }
     for (KindBufs &K : S->kb) {
         Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und, &K.skip, &K.pend, &K.plist};
         for (Buf *b : kall)
-            if (b->p) (void)hipFree(b->p);
+            if (b->p) {
+                (void)hipFree(b->p);
+                grom_dev_note(GROM_DEVCAT_CNV, -(int64_t)b->cap);
+            }
         if (K.st) (void)hipStreamDestroy(K.st);
     }
     if (S->walk_in) (void)hipEventDestroy(S->walk_in);

@@ -91,6 +91,15 @@ int dd_stage_prefix(dd_ctx *c, grom_stage *stage, int32_t s0, int64_t *sk, int64
 void dd_device_warm(int device);
 /* wall time of a device allocation (stage growth), added to dd_ctx_times' ms[3] */
 void grom_note_alloc_ns(int64_t ns, size_t bytes);
+/* grom_scan_chrom_staged calls fn(arg, s) once its scan no longer reads the
+ * stage (before the CNV path): the stage may take the next chromosome then */
+void grom_stage_on_consumed(grom_stage *s, void (*fn)(void *, grom_stage *), void *arg);
+/* device memory accounting per category (the CLI's "device buffers" line) */
+enum { GROM_DEVCAT_SCAN, GROM_DEVCAT_SV, GROM_DEVCAT_CNV, GROM_DEVCAT_STAGE, GROM_DEVCAT_DECODE, GROM_DEVCAT_OTHER,
+       GROM_DEVCAT_N };
+void grom_dev_note(int cat, int64_t delta);
+/* peak[k] / now[k] for k < GROM_DEVCAT_N, [GROM_DEVCAT_N] = their sum */
+void grom_dev_peaks(int64_t *peak, int64_t *now);
 
 /* stage helpers for device-side fills (scan.hip) */
 /* a stage holding exactly sz's counts (n_aux = capacity, the count starts at

@@ -221,7 +221,10 @@ int dgrow(DBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return 0;
     const auto t0 = std::chrono::steady_clock::now();
-    if (b.p) (void)hipFree(b.p);
+    if (b.p) {
+        (void)hipFree(b.p);
+        grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)b.cap);
+    }
     b.p = nullptr;
     b.cap = 0;
     const size_t want = bytes + bytes / 8 + 256;
@@ -232,6 +235,7 @@ int dgrow(DBuf &b, size_t bytes) {
         fprintf(stderr, "grom: device buffer of %.2f GB took %.1f ms\n", (double)want / 1e9, ns / 1e6);
     if (e != hipSuccess) return -1;
     b.cap = want;
+    grom_dev_note(GROM_DEVCAT_DECODE, (int64_t)want);
     return 0;
 }
 
@@ -988,7 +992,10 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->cst) (void)hipStreamSynchronize(c->cst);
     for (int k = 0; k < DD_SLOTS; k++) {
-        if (c->dcomp[k].p) (void)hipFree(c->dcomp[k].p);
+        if (c->dcomp[k].p) {
+            (void)hipFree(c->dcomp[k].p);
+            grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)c->dcomp[k].cap);
+        }
         if (c->cev[k]) (void)hipEventDestroy(c->cev[k]);
     }
     for (int k = 0; k < DD_SLOTS; k++) {
@@ -996,7 +1003,10 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
         if (r.st) (void)hipStreamSynchronize(r.st);
         DBuf *rb[] = {&r.U, &r.blk, &r.status, &r.misc, &r.S, &r.ccnt, &r.cbase, &r.off, &r.tmp};
         for (DBuf *b : rb)
-            if (b->p) (void)hipFree(b->p);
+            if (b->p) {
+                (void)hipFree(b->p);
+                grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)b->cap);
+            }
         for (int e = 0; e < 3; e++)
             if (r.ev[e]) (void)hipEventDestroy(r.ev[e]);
         if (r.h_small) (void)hipHostFree(r.h_small);
@@ -1008,7 +1018,10 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
                    &c->srcs, &c->tfq, &c->tfs,
                    &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack};
     for (DBuf *b : all)
-        if (b->p) (void)hipFree(b->p);
+        if (b->p) {
+            (void)hipFree(b->p);
+            grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)b->cap);
+        }
     for (int k = 0; k < 4; k++)
         if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -1016,6 +1029,26 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     if (c->st) (void)hipStreamDestroy(c->st);
     if (c->cst) (void)hipStreamDestroy(c->cst);
     delete c;
+}
+
+// device bytes held per category (scan, breakpoint, CNV, stage, decode), now
+// and at their peak, and the peak of their sum (the CLI's "device buffers" line)
+static std::atomic<int64_t> g_dev_now[GROM_DEVCAT_N + 1], g_dev_peak[GROM_DEVCAT_N + 1];
+
+extern "C" void grom_dev_note(int cat, int64_t delta) {
+    if (cat < 0 || cat >= GROM_DEVCAT_N) cat = GROM_DEVCAT_N - 1;
+    const int64_t v = (g_dev_now[cat] += delta), t = (g_dev_now[GROM_DEVCAT_N] += delta);
+    int64_t p = g_dev_peak[cat].load();
+    while (v > p && !g_dev_peak[cat].compare_exchange_weak(p, v)) {}
+    p = g_dev_peak[GROM_DEVCAT_N].load();
+    while (t > p && !g_dev_peak[GROM_DEVCAT_N].compare_exchange_weak(p, t)) {}
+}
+
+extern "C" void grom_dev_peaks(int64_t *peak, int64_t *now) {
+    for (int k = 0; k <= GROM_DEVCAT_N; k++) {
+        if (peak) peak[k] = g_dev_peak[k].load();
+        if (now) now[k] = g_dev_now[k].load();
+    }
 }
 
 extern "C" void grom_note_alloc_ns(int64_t ns, size_t bytes) {

@@ -12,6 +12,7 @@
  * the implemented scan rows are accepted and recorded.
  */
 #include <ctype.h>
+#include <dirent.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -357,6 +358,7 @@ typedef struct {
     grom_stage *stage;
     pd_chrom_facts facts;
     pd_session *pd;        /* releases the stage after the scan */
+    int stage_released;    /* the scan gave the stage back before its CNV path */
     int k;                 /* plan index (trace) */
     int device;            /* the GPU the stage lives on, -1: any */
     char *text, *ctx_text;
@@ -461,6 +463,14 @@ static void stage_digest_line(grom_stage *st, const grom_chrom *ch, int device) 
 }
 
 /* Scan one chromosome on context `slot`; its VCF rows go to j->text (malloc'd). */
+/* the scan no longer reads the job's stage: the decoder may refill it while
+ * the CNV path runs (grom_stage_on_consumed) */
+static void job_stage_consumed(void *arg, grom_stage *st) {
+    grom_job *j = (grom_job *)arg;
+    j->stage_released = 1;
+    pd_release_stage(j->pd, st);
+}
+
 static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     chrom_plan *cp = j->cp;
     j->text = j->ctx_text = NULL;
@@ -507,6 +517,18 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     if (!j->has_batch && getenv("GROM_STAGE_DIGEST")) stage_digest_line(j->stage, &ch, j->device);
     grom_out out = {0};
     grom_stats st = {0};
+    /* the pileup's input sizes (the verbose line) before the stage is given back */
+    int64_t n_cig = rd.n_cigar_ops, n_b = rd.n_bases;
+    if (!j->has_batch) {
+        grom_chrom dc;
+        grom_reads dr;
+        if (grom_stage_view(j->stage, &ch, &dc, &dr) == GROM_OK) {
+            n_cig = dr.n_cigar_ops;
+            n_b = dr.n_bases;
+        }
+        /* (GROM_DUMP reads the stage after the scan: it keeps it) */
+        grom_stage_on_consumed(j->stage, j->pd && !getenv("GROM_DUMP") ? job_stage_consumed : NULL, j);
+    }
     if (j->pd) pd_trace(j->pd, PD_EV_SCAN, j->k, 0);
     int rc = j->has_batch ? grom_scan_chrom(slot, &ch, &rd, &out, &st)
                           : grom_scan_chrom_staged(slot, j->stage, &ch, &out, &st);
@@ -538,15 +560,6 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
     if (getenv("GROM_DUMP")) write_dumps(slot, cp, &ch, &rd, j->has_batch ? NULL : j->stage, P);
     if (verbose) {
         /* the pileup kernel's launch and its inputs' sizes (bench.py's roofline) */
-        int64_t n_cig = rd.n_cigar_ops, n_b = rd.n_bases;
-        if (!j->has_batch) {
-            grom_chrom dc;
-            grom_reads dr;
-            if (grom_stage_view(j->stage, &ch, &dc, &dr) == GROM_OK) {
-                n_cig = dr.n_cigar_ops;
-                n_b = dr.n_bases;
-            }
-        }
         printf("%s: %lld reads, %.3f ms on GPU (%.2f Mbases/s); pileup %.3f ms, cnv %.3f ms, cigar_ops %lld, "
                "bases %lld, len %ld\n", cp->name, (long long)n_reads, st.ms_total,
                st.ms_total > 0 ? cp->len / (st.ms_total * 1e3) : 0.0, st.ms_pileup, st.ms_cnv, (long long)n_cig,
@@ -616,7 +629,7 @@ static void *grom_worker_main(void *arg) {
         free(j->cp->ref);
         j->cp->ref = NULL;
         if (j->has_batch) grom_batch_free(&j->batch);
-        if (j->stage && j->pd) pd_release_stage(j->pd, j->stage);
+        if (j->stage && j->pd && !j->stage_released) pd_release_stage(j->pd, j->stage);
         j->stage = NULL;
         pthread_mutex_lock(&pl->mu);
         j->rc = rc;
@@ -649,6 +662,93 @@ typedef struct {
     pthread_t hip_thr;     /* HIP runtime start-up, beside the header/FASTA/index work */
     int hip_started;
 } cli_state;
+
+/* Peak device memory of this process (GROM_VERBOSE): the kernel driver's
+ * per-process VRAM count (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu>), sampled
+ * every 5 ms; without it, the device-wide use above the start's.  Printed as
+ * the "footprint:" line, which bench.py reports. */
+typedef struct {
+    pthread_t thr;
+    int started, stop, device, kfd;
+    int64_t peak, base;
+    double t_peak;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+} fp_sampler;
+
+static int64_t fp_kfd_bytes(void) {
+    char dir[96], path[384], buf[64];
+    snprintf(dir, sizeof(dir), "/sys/class/kfd/kfd/proc/%d", (int)getpid());
+    DIR *d = opendir(dir);
+    if (!d) return -1;
+    int64_t tot = 0;
+    int any = 0;
+    struct dirent *e;
+    while ((e = readdir(d)) != NULL) {
+        if (strncmp(e->d_name, "vram_", 5) != 0) continue;
+        snprintf(path, sizeof(path), "%s/%s", dir, e->d_name);
+        FILE *f = fopen(path, "r");
+        if (!f) continue;
+        if (fgets(buf, sizeof(buf), f)) { tot += atoll(buf); any = 1; }
+        fclose(f);
+    }
+    closedir(d);
+    return any ? tot : -1;
+}
+
+static int64_t fp_sample(fp_sampler *F) {
+    if (F->kfd) return fp_kfd_bytes();
+    const int64_t fr = grom_device_mem_free(F->device);
+    return fr < 0 ? -1 : F->base - fr; /* base: free bytes at the start */
+}
+
+static void *fp_main(void *arg) {
+    fp_sampler *F = (fp_sampler *)arg;
+    F->kfd = fp_kfd_bytes() >= 0;
+    if (!F->kfd) F->base = grom_device_mem_free(F->device);
+    const double t0 = clock_gettime_s();
+    pthread_mutex_lock(&F->mu);
+    while (!F->stop) {
+        pthread_mutex_unlock(&F->mu);
+        const int64_t v = fp_sample(F);
+        pthread_mutex_lock(&F->mu);
+        if (v > F->peak) { F->peak = v; F->t_peak = clock_gettime_s() - t0; }
+        struct timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        ts.tv_nsec += 5000000;
+        if (ts.tv_nsec >= 1000000000) { ts.tv_sec++; ts.tv_nsec -= 1000000000; }
+        if (!F->stop) pthread_cond_timedwait(&F->cv, &F->mu, &ts);
+    }
+    pthread_mutex_unlock(&F->mu);
+    return NULL;
+}
+
+static void fp_start(fp_sampler *F, int device) {
+    memset(F, 0, sizeof(*F));
+    F->device = device;
+    pthread_mutex_init(&F->mu, NULL);
+    pthread_cond_init(&F->cv, NULL);
+    F->started = pthread_create(&F->thr, NULL, fp_main, F) == 0;
+}
+
+static void fp_stop(fp_sampler *F, double since_start) {
+    if (!F->started) return;
+    pthread_mutex_lock(&F->mu);
+    F->stop = 1;
+    pthread_cond_broadcast(&F->cv);
+    pthread_mutex_unlock(&F->mu);
+    pthread_join(F->thr, NULL);
+    int64_t pk[GROM_DEVCAT_N + 1];
+    grom_dev_peaks(pk, NULL);
+    printf("footprint: peak %.2f GB of device memory (%s), at %.3f s of %.3f s; buffers: peak %.2f GB together, "
+           "per kind scan %.2f, breakpoint %.2f, CNV %.2f, stages %.2f, decode %.2f GB\n", F->peak / 1e9,
+           F->kfd ? "this process, kfd" : "device-wide use above the start's", F->t_peak, since_start,
+           pk[GROM_DEVCAT_N] / 1e9, pk[GROM_DEVCAT_SCAN] / 1e9, pk[GROM_DEVCAT_SV] / 1e9, pk[GROM_DEVCAT_CNV] / 1e9,
+           pk[GROM_DEVCAT_STAGE] / 1e9, pk[GROM_DEVCAT_DECODE] / 1e9);
+    pthread_mutex_destroy(&F->mu);
+    pthread_cond_destroy(&F->cv);
+    F->started = 0;
+}
 
 static void *hip_init_main(void *arg) {
     const int device = *(const int *)arg;
@@ -1049,7 +1149,9 @@ static int run_streamed(cli_state *S) {
         cin[c].len = S->plan[c].len;
     }
     const char *dt = getenv("GROM_DECODE_THREADS");
-    int n_thr = dt ? atoi(dt) : host_cpus();
+    /* the host decoder's threads (GROM_DEVICE_DECODE=0 and plan-only runs):
+     * the CPU share, at most 32 (its piece window grows with the count) */
+    int n_thr = dt ? atoi(dt) : (host_cpus() < 32 ? host_cpus() : 32);
     if (n_thr < 1) n_thr = 1;
     char why[256] = "";
     pd_session *pd = pd_open(S->bam_name, &S->hdr, cin, S->n_cand, P->splitread, P->read_name_len, n_thr, why,
@@ -1436,6 +1538,9 @@ static int cli_run(int argc, char **argv, int force_serial) {
     }
     g_plan_only = getenv("GROM_PLAN_ONLY") != NULL;
     if (!g_plan_only) S->hip_started = pthread_create(&S->hip_thr, NULL, hip_init_main, &S->device) == 0;
+    fp_sampler fps;
+    memset(&fps, 0, sizeof(fps));
+    if (!g_plan_only && S->verbose) fp_start(&fps, S->device);
     /* tables (read_binom_tables, GROM.c:22234) on a thread beside the decode */
     {
         size_t tn = (size_t)(GROM_MAX_TRIALS + 1) * (GROM_MAX_TRIALS + 1);
@@ -1508,6 +1613,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
         printf("cli teardown (s from start): scans done %.3f, outputs %.3f, decoder closed %.3f, stages freed %.3f, "
                "contexts freed %.3f\n", S->t_scans - S->t_cli0, S->t_outputs - S->t_cli0, S->t_decclose - S->t_cli0,
                S->t_pdclose - S->t_cli0, clock_gettime_s() - S->t_cli0);
+    if (fps.started) fp_stop(&fps, clock_gettime_s() - S->t_cli0);
     for (int i = 0; i < S->n_cand; i++) {
         free(S->plan[i].target);
         free(S->plan[i].ref);

@@ -1211,6 +1211,12 @@ static int stage_acquire(pd_session *s, int dev, int k, grom_stage **out) {
                 pd_trace(s, PD_EV_STAGE, k, 1);
                 return 0;
             }
+        int reserving = 0;
+        for (int i = 0; i < s->n_stage; i++) reserving |= s->stage_busy[i] && s->stage_owner[i] == -2;
+        if (reserving) { /* stres_main is growing this device's stages: wait for them */
+            pthread_cond_wait(&s->cv, &s->mu);
+            continue;
+        }
         int unsafe = s->n_stage < 1;
         for (int i = 0; i < s->n_stage && !unsafe; i++)
             if (s->stage_busy[i] && (s->stage_owner[i] < 0 || !s->ch[s->stage_owner[i]].final)) unsafe = 1;
@@ -2443,9 +2449,17 @@ static void *stres_main(void *arg) {
     pthread_mutex_lock(&s->mu);
     int ns = s->n_stage;
     grom_stage *mine[64];
-    int m = 0;
+    int mi[64], m = 0;
+    /* the stages being reserved are busy (owner -2) until their blocks exist:
+     * a worker's stage_acquire waits for them (a second worker on
+     * the device could otherwise fill a stage this thread is growing) */
     for (int i = 0; i < ns && m < 64; i++)
-        if (s->stage_dev[i] == j->device && !s->stage_busy[i]) mine[m++] = s->stages[i];
+        if (s->stage_dev[i] == j->device && !s->stage_busy[i]) {
+            s->stage_busy[i] = 1;
+            s->stage_owner[i] = -2;
+            mi[m] = i;
+            mine[m++] = s->stages[i];
+        }
     pthread_mutex_unlock(&s->mu);
     /* a stage's bytes, roughly: the read SoA, CIGAR words,
      * qualities + packed bases, dropped records, the reference; stages are
@@ -2458,6 +2472,13 @@ static void *stres_main(void *arg) {
         if (fr < 0 || (double)fr < bytes + 3.0 * bytes + (double)((int64_t)32 << 30)) break;
         (void)grom_stage_begin(mine[i], &est);
     }
+    pthread_mutex_lock(&s->mu);
+    for (int i = 0; i < m; i++) {
+        s->stage_busy[mi[i]] = 0;
+        s->stage_owner[mi[i]] = -1;
+    }
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
     return NULL;
 }
 
@@ -2728,6 +2749,14 @@ static void *dw_main(void *arg) {
         pd_trace(s, PD_EV_UPLOAD, k, 1);
         pthread_mutex_lock(&s->mu);
         s->c_upl_s += now_s() - t0;
+        if ((rc == -2 || rc == -1) && !s->abort) {
+            /* the session's abort is published with the chromosome's final
+             * state, under one lock: a waiter on this chromosome sees the
+             * abort (soft for -2: the serial reader reruns), never a bare rc */
+            s->abort = 1;
+            s->abort_soft = rc == -2;
+            snprintf(s->abort_msg, sizeof(s->abort_msg), "%s", err);
+        }
         c->rc = rc;
         c->final = 1;
         c->begun = 1;

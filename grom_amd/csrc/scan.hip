@@ -204,7 +204,10 @@ struct DevBuf {
 static int ensure(DevBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return GROM_OK;
-    if (b.p) (void)hipFree(b.p);
+    if (b.p) {
+        (void)hipFree(b.p);
+        grom_dev_note(GROM_DEVCAT_SCAN, -(int64_t)b.cap);
+    }
     b.p = nullptr;
     b.cap = 0;
     size_t want = bytes + bytes / 8 + 64;  // slack: kernels read whole 16-byte words
@@ -213,6 +216,7 @@ static int ensure(DevBuf &b, size_t bytes) {
         return GROM_E_NOMEM;
     }
     b.cap = want;
+    grom_dev_note(GROM_DEVCAT_SCAN, (int64_t)want);
     return GROM_OK;
 }
 
@@ -320,8 +324,13 @@ static int check_params(const grom_params &p) {
 }
 
 // the scan proper on device-resident reads
+// reads_done (optional): called once the scan no longer reads R or ch->ref
+// (after the breakpoint tests; the CNV path then reads the context's own
+// copy of the reference), so a stage can take the next chromosome while this
+// one's CNV path runs
 static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_out *out, grom_stats *stats,
-                       int32_t *dbg_first, int32_t *dbg_counts, int64_t dbg_cap, int32_t *dbg_caf) {
+                       int32_t *dbg_first, int32_t *dbg_counts, int64_t dbg_cap, int32_t *dbg_caf,
+                       void (*reads_done)(void *) = nullptr, void *reads_done_arg = nullptr) {
     const grom_params &P = C.prm;
     int rc = check_params(P);
     if (rc) return rc;
@@ -395,6 +404,14 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     unsigned long long *d_facc = (unsigned long long *)(misc + 32);
     unsigned long long *d_macc = (unsigned long long *)(misc + 64);
 
+    // the CNV path's reference: the context's own copy when the caller takes
+    // the input back before the CNV path (reads_done)
+    const char *cnv_ref = ch->ref;
+    if (reads_done && ch->cnv && !want_dbg) {
+        if ((rc = ensure(C.ref, (size_t)ch->len))) return rc;
+        HIPCHK(hipMemcpyAsync(C.ref.p, ch->ref, (size_t)ch->len, hipMemcpyDeviceToDevice, st));
+        cnv_ref = (const char *)C.ref.p;
+    }
     // device-resident reference: its host copy for the breakpoint rows,
     // overlapped with the pileup on the copy stream
     bool ref_copy_pending = false;
@@ -414,7 +431,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     if (ch->cnv && !want_dbg) {
         if (!C.cnv) C.cnv = cnv_scratch_new();
         char cerr[512] = {0};
-        if ((rc = cnv_prelaunch(C.cnv, st, P, ch->ref, ch->len, cerr, sizeof(cerr)))) {
+        if ((rc = cnv_prelaunch(C.cnv, st, P, cnv_ref, ch->len, cerr, sizeof(cerr)))) {
             set_err("%s", cerr);
             return rc;
         }
@@ -699,6 +716,15 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             }
         }
         const double t_sv = ms_since(t_start);
+        if (reads_done) {
+            // every kernel that reads the input has finished (sv_evaluate
+            // waited for the stream) and so has the reference's host copy
+            if (ref_copy_pending) {
+                HIPCHK(hipEventSynchronize(C.ref_ev));
+                ref_copy_pending = false;
+            }
+            reads_done(reads_done_arg);
+        }
 
         // read-depth CNV path after the SV rows (GROM.c:16633-17300); the
         // reference runs it only when the FASTA name matched a BAM target
@@ -708,7 +734,7 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             if (!C.cnv) C.cnv = cnv_scratch_new();
             std::string crow, side;
             char cerr[512] = {0};
-            rc = cnv_chrom(C.cnv, st, P, ch->seed, ch->name, ch->ref, ch->len, (int32_t *)C.caf_mq.p,
+            rc = cnv_chrom(C.cnv, st, P, ch->seed, ch->name, cnv_ref, ch->len, (int32_t *)C.caf_mq.p,
                            (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, crow, &ct, cerr, sizeof(cerr),
                            P.gen1000_window > 0 ? &side : nullptr);
             if (rc != GROM_OK) {
@@ -905,7 +931,12 @@ void grom_dev_fini(int device) {
                      &C.runb, &C.runc, &C.segs, &C.fpart, &C.tlo, &C.thi, &C.caf_mq, &C.caf_rd, &C.caf_low, &C.cands,
                      &C.misc, &C.dbg, &C.slots, &C.r_aidx, &C.r_aux, &C.r_dpos, &C.r_dlq, &C.r_dbef};
     for (DevBuf *b : all)
-        if (b->p) (void)hipFree(b->p);
+        if (b->p) {
+            (void)hipFree(b->p);
+            grom_dev_note(GROM_DEVCAT_SCAN, -(int64_t)b->cap);
+            b->p = nullptr;
+            b->cap = 0;
+        }
     if (C.h_cands) (void)hipHostFree(C.h_cands);
     if (C.st_copy) (void)hipStreamSynchronize(C.st_copy);
     if (C.h_ref) (void)hipHostFree(C.h_ref);
@@ -1094,20 +1125,32 @@ struct grom_stage {
     // kept (a hipMalloc/hipFree pair per chromosome would wait for the device)
     char *scratch = nullptr;
     size_t scratch_cap = 0;
+    // called by grom_scan_chrom_staged once the scan no longer reads the
+    // stage (grom_stage_on_consumed)
+    void (*consumed)(void *, grom_stage *) = nullptr;
+    void *consumed_arg = nullptr;
     char *a(int k) const { return blk + off[k]; }
 };
+
+void grom_stage_on_consumed(grom_stage *s, void (*fn)(void *, grom_stage *), void *arg) {
+    if (!s) return;
+    s->consumed = fn;
+    s->consumed_arg = arg;
+}
 
 static char *stage_scratch(grom_stage *s, size_t bytes) {
     if (bytes <= s->scratch_cap) return s->scratch;
     if (s->scratch) {
         (void)hipStreamSynchronize(s->st);
         (void)hipFree(s->scratch);
+        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->scratch_cap);
     }
     s->scratch = nullptr;
     s->scratch_cap = 0;
     const size_t want = bytes + bytes / 2 + 4096;
     if (hipMalloc((void **)&s->scratch, want) != hipSuccess) return nullptr;
     s->scratch_cap = want;
+    grom_dev_note(GROM_DEVCAT_STAGE, (int64_t)want);
     return s->scratch;
 }
 
@@ -1144,7 +1187,9 @@ static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t ke
             if (keep[k]) HIPCHK(hipMemcpyAsync(nb + off[k], s->a(k), keep[k], hipMemcpyDeviceToDevice, s->st));
         HIPCHK(hipStreamSynchronize(s->st));
         (void)hipFree(s->blk);
+        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->blk_cap);
     }
+    grom_dev_note(GROM_DEVCAT_STAGE, (int64_t)tot);
     grom_note_alloc_ns(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
                        tot);
     s->blk = nb;
@@ -1180,8 +1225,14 @@ void grom_stage_free(grom_stage *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
-    if (s->blk) (void)hipFree(s->blk);
-    if (s->scratch) (void)hipFree(s->scratch);
+    if (s->blk) {
+        (void)hipFree(s->blk);
+        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->blk_cap);
+    }
+    if (s->scratch) {
+        (void)hipFree(s->scratch);
+        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->scratch_cap);
+    }
     for (int k = 0; k < GROM_STAGE_EVENTS; k++)
         if (s->ev[k]) (void)hipEventDestroy(s->ev[k]);
     if (s->all_ev) (void)hipEventDestroy(s->all_ev);
@@ -1535,7 +1586,14 @@ int grom_scan_chrom_staged(int slot, grom_stage *s, const grom_chrom *chrom, gro
     HIPCHK(hipEventRecord(s->all_ev, s->st));
     HIPCHK(hipStreamWaitEvent(C->st, s->all_ev, 0));
     C->host_ref = chrom->ref;
-    rc = scan_device(*C, &dch, &dr, out, stats, nullptr, nullptr, 0, nullptr);
+    struct Done {
+        grom_stage *s;
+        static void call(void *u) {
+            grom_stage *s = ((Done *)u)->s;
+            s->consumed(s->consumed_arg, s);
+        }
+    } done{s};
+    rc = scan_device(*C, &dch, &dr, out, stats, nullptr, nullptr, 0, nullptr, s->consumed ? &Done::call : nullptr, &done);
     C->host_ref = nullptr;
     return rc;
 }

@@ -47,6 +47,7 @@
 #include <cstring>
 
 #include "sv.h"
+#include "ddecode.h"
 
 namespace {
 
@@ -937,7 +938,10 @@ struct SvScratch {
 static int sbuf(Buf &b, size_t bytes, char *err, size_t errlen) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return GROM_OK;
-    if (b.p) (void)hipFree(b.p);
+    if (b.p) {
+        (void)hipFree(b.p);
+        grom_dev_note(GROM_DEVCAT_SV, -(int64_t)b.cap);
+    }
     b.p = nullptr;
     b.cap = 0;
     const size_t want = bytes + bytes / 8 + 64;
@@ -946,6 +950,7 @@ static int sbuf(Buf &b, size_t bytes, char *err, size_t errlen) {
         return GROM_E_NOMEM;
     }
     b.cap = want;
+    grom_dev_note(GROM_DEVCAT_SV, (int64_t)want);
     return GROM_OK;
 }
 
@@ -958,7 +963,10 @@ void sv_scratch_free(SvScratch *s) {
                   &s->o_cand, &s->o_ind, &s->o_dbg, &s->rec, &s->irec_c, &s->irec, &s->drec, &s->ctx, &s->ctx2,
                   &s->ckeys, &s->ckeys2, &s->cvals, &s->cvals2, &s->n_ctx, &s->hits, &s->n_hits, &s->hits2};
     for (Buf *b : all)
-        if (b->p) (void)hipFree(b->p);
+        if (b->p) {
+            (void)hipFree(b->p);
+            grom_dev_note(GROM_DEVCAT_SV, -(int64_t)b->cap);
+        }
     if (s->h_hits) (void)hipHostFree(s->h_hits);
     if (s->e0) (void)hipEventDestroy(s->e0);
     if (s->e1) (void)hipEventDestroy(s->e1);

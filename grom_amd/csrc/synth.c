@@ -976,6 +976,28 @@ static int compress_one(sblock *b) {
     return 0;
 }
 
+static int compress_one(sblock *b);
+
+/* a generator that gets ahead of the compressors compresses queued blocks
+ * itself until at most SYNTH_QUEUE_MAX wait (the raw blocks of a 30x genome
+ * would otherwise pile up: 190 GB); which thread compresses a block does not
+ * change its bytes */
+#define SYNTH_QUEUE_MAX 2048
+
+static void q_help(swriter *w) {
+    for (;;) {
+        pthread_mutex_lock(&w->mu);
+        if (w->q_tail - w->q_head <= SYNTH_QUEUE_MAX) {
+            pthread_mutex_unlock(&w->mu);
+            return;
+        }
+        sblock *b = w->q[w->q_head % w->q_cap];
+        w->q_head++;
+        pthread_mutex_unlock(&w->mu);
+        if (compress_one(b)) w->err = 1;
+    }
+}
+
 static void sc_flush(schrom *c) {
     if (c->cur_len == 0) return;
     sblock *b = (sblock *)calloc(1, sizeof(sblock));
@@ -989,6 +1011,7 @@ static void sc_flush(schrom *c) {
     c->cur = (unsigned char *)malloc(BGZF_PAYLOAD);
     c->cur_len = 0;
     q_push(c->w, b);
+    q_help(c->w);
 }
 
 static void sc_write(schrom *c, const void *src, int n) {
