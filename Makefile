@@ -10,9 +10,9 @@ LIBDIR  = grom_amd/lib
 BINDIR  = grom_amd/bin
 
 HOST_SRC = grom_amd/csrc/bamio.c grom_amd/csrc/stream.c grom_amd/csrc/tables.c grom_amd/csrc/synth.c grom_amd/csrc/hostapi.c grom_amd/csrc/grom_main.c grom_amd/csrc/pdecode.c
-HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC)) build/snvfmt.o build/svcall.o build/inflate_host.o
+HOST_OBJ = $(patsubst grom_amd/csrc/%.c,build/%.o,$(HOST_SRC)) build/snvfmt.o build/svcall.o build/inflate_host.o build/devmem.o
 DEV_OBJ = build/scan.o build/cnv.o build/sv.o build/ddecode.o
-HDRS = include/grom_amd.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h grom_amd/csrc/pdecode.h grom_amd/csrc/ddecode.h
+HDRS = include/grom_amd.h grom_amd/csrc/devmem.h grom_amd/csrc/scan_common.h grom_amd/csrc/bamio.h grom_amd/csrc/stream.h grom_amd/csrc/synth.h grom_amd/csrc/pdecode.h grom_amd/csrc/ddecode.h
 KHDRS = grom_amd/csrc/k_scan_tile.h grom_amd/csrc/device_common.h grom_amd/csrc/snvfmt.h
 
 all: $(LIBDIR)/libgrom_amd.so $(BINDIR)/grom $(BINDIR)/grom_synth $(BINDIR)/gromc_binding oracle
@@ -48,6 +48,11 @@ build/cnv.o: grom_amd/csrc/cnv.hip grom_amd/csrc/cnv.h $(HDRS)
 build/sv.o: grom_amd/csrc/sv.hip grom_amd/csrc/sv.h $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -ffp-contract=off -c $< -o $@
+
+# device allocations: accounting, reclaim / wait / retry (host code on the HIP runtime)
+build/devmem.o: grom_amd/csrc/devmem.cpp $(HDRS)
+	@mkdir -p build
+	$(HIPCC) -O2 -g -Wall -fPIC -std=c++17 -c $< -o $@
 
 # host list logic and SV rows (needs only the HIP runtime headers)
 build/svcall.o: grom_amd/csrc/svcall.cpp grom_amd/csrc/sv.h $(HDRS)
@@ -118,8 +123,14 @@ $(SANDIR)/svcall.o: grom_amd/csrc/svcall.cpp grom_amd/csrc/sv.h $(HDRS)
 	$(CXX) -O1 -g -fno-omit-frame-pointer -Wall -fPIC -std=c++17 -pthread -ffp-contract=off -I/opt/rocm/include \
 	    -D__HIP_PLATFORM_AMD__ $(SANFLAGS) -c $< -o $@
 
-$(SANDIR)/san_driver: tools/san_driver.c $(SAN_OBJ) $(SANDIR)/svcall.o $(DEV_OBJ)
-	$(CXX) -O1 -g -fno-omit-frame-pointer $(SANFLAGS) -x c tools/san_driver.c -x none $(SAN_OBJ) $(SANDIR)/svcall.o $(DEV_OBJ) \
+# the device allocations (host code on the HIP runtime API)
+$(SANDIR)/devmem.o: grom_amd/csrc/devmem.cpp $(HDRS)
+	@mkdir -p $(SANDIR)
+	$(CXX) -O1 -g -fno-omit-frame-pointer -Wall -fPIC -std=c++17 -pthread -I/opt/rocm/include \
+	    -D__HIP_PLATFORM_AMD__ $(SANFLAGS) -c $< -o $@
+
+$(SANDIR)/san_driver: tools/san_driver.c $(SAN_OBJ) $(SANDIR)/svcall.o $(SANDIR)/devmem.o $(DEV_OBJ)
+	$(CXX) -O1 -g -fno-omit-frame-pointer $(SANFLAGS) -x c tools/san_driver.c -x none $(SAN_OBJ) $(SANDIR)/svcall.o $(SANDIR)/devmem.o $(DEV_OBJ) \
 	    -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -lz -lm -ldl -lpthread -o $@
 
 $(SANDIR)/grom_synth: tools/grom_synth.c $(SANDIR)/synth.o $(SANDIR)/bamio.o

@@ -1,6 +1,7 @@
 // cnv.h -- internal interface of the read-depth CNV path (SURVEY.md §8 rows
 // A14-A16) between the scan driver (scan.hip) and cnv.hip.
 #pragma once
+#include "devmem.h"
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -12,6 +13,11 @@
 struct CnvScratch;
 CnvScratch *cnv_scratch_new();
 void cnv_scratch_free(CnvScratch *s);
+// a new CNV phase (scan.hip): with an arena every buffer but the GC windows is
+// carved from the phase; without one the buffers are the scratch's own
+void cnv_scratch_phase(CnvScratch *s, grom_arena *ar);
+// wait for the CNV path's own streams (before its arena phase is reused)
+void cnv_scratch_sync(CnvScratch *s);
 
 // Start the reference-only GC/ACGT window kernel of a chromosome on the CNV
 // path's own stream (to overlap the pileup); the next cnv_chrom with the same

@@ -2938,6 +2938,8 @@ __global__ void k_cnv_calls_valid(const CallRec *calls, uint32_t n, const uint8_
 struct Buf {
     void *p = nullptr;
     size_t cap = 0;
+    bool own = false;          // p is this buffer's own allocation (else a piece of `ar`'s phase)
+    grom_arena *ar = nullptr;  // the context's phase arena (cnv_scratch_phase), or none
 };
 
 }  // namespace
@@ -2980,19 +2982,21 @@ namespace {
 static int grow(Buf &b, size_t bytes, char *err, size_t errlen) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return GROM_OK;
-    if (b.p) {
-        (void)hipFree(b.p);
-        grom_dev_note(GROM_DEVCAT_CNV, -(int64_t)b.cap);
-    }
+    if (b.p && b.own) grom_dev_free(b.p, b.cap, GROM_DEVCAT_CNV);
     b.p = nullptr;
     b.cap = 0;
+    b.own = false;
     size_t want = bytes + bytes / 8 + 256;
-    if (hipMalloc(&b.p, want) != hipSuccess) {
+    if (b.ar && (b.p = grom_arena_take(b.ar, want)) != nullptr) {
+        b.cap = want;
+        return GROM_OK;
+    }
+    if (grom_dev_malloc(&b.p, want, GROM_DEVCAT_CNV)) {
         snprintf(err, errlen, "hipMalloc(%zu) failed in the CNV path", want);
         return GROM_E_NOMEM;
     }
     b.cap = want;
-    grom_dev_note(GROM_DEVCAT_CNV, (int64_t)want);
+    b.own = true;
     return GROM_OK;
 }
 
@@ -3230,25 +3234,52 @@ int cnv_prelaunch(CnvScratch *S, hipStream_t after, const grom_params &P, const 
     return GROM_OK;
 }
 
+#define CNV_PHASE_BUFS(S)                                                                                             \
+    {&S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre, &S->prepos, &S->ppos, &S->rep, &S->misc,       \
+     &S->blk, &S->hist, &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows,           \
+     &S->rowlen, &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover, &S->cwords, &S->cw_seg, &S->cw_carry,      \
+     &S->wsdmin, &S->gen1000, &S->gpre, &S->gtmp}
+#define CNV_KIND_BUFS(K) \
+    {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und, &K.skip, &K.pend, &K.plist}
+
+// a new CNV phase (scan.hip): with an arena every buffer but the GC windows
+// (written beside the pileup by cnv_prelaunch) is carved from it
+void cnv_scratch_phase(CnvScratch *S, grom_arena *ar) {
+    auto reset = [ar](Buf *b) {
+        if (b->own && ar) grom_dev_free(b->p, b->cap, GROM_DEVCAT_CNV);  // (an overflow of the last phase)
+        if (!b->own || ar) {
+            b->p = nullptr;
+            b->cap = 0;
+            b->own = false;
+        }
+        b->ar = ar;
+    };
+    Buf *all[] = CNV_PHASE_BUFS(S);
+    for (Buf *b : all) reset(b);
+    for (KindBufs &K : S->kb) {
+        Buf *kall[] = CNV_KIND_BUFS(K);
+        for (Buf *b : kall) reset(b);
+    }
+}
+
+void cnv_scratch_sync(CnvScratch *S) {
+    if (!S) return;
+    for (KindBufs &K : S->kb)
+        if (K.st) (void)hipStreamSynchronize(K.st);
+}
+
 void cnv_scratch_free(CnvScratch *S) {
     if (!S) return;
-    Buf *all[] = {&S->gcw, &S->acw, &S->rtype, &S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre,
-                  &S->prepos, &S->ppos, &S->rep, &S->misc, &S->blk, &S->hist,
-                  &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows, &S->rowlen,
-                  &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover, &S->cwords, &S->cw_seg,
-                  &S->cw_carry, &S->wsdmin, &S->gen1000, &S->gpre, &S->gtmp};
+    Buf *all[] = CNV_PHASE_BUFS(S);
     for (Buf *b : all)
-        if (b->p) {
-            (void)hipFree(b->p);
-            grom_dev_note(GROM_DEVCAT_CNV, -(int64_t)b->cap);
-        }
+        if (b->p && b->own) grom_dev_free(b->p, b->cap, GROM_DEVCAT_CNV);
+    Buf *gc[] = {&S->gcw, &S->acw, &S->rtype};
+    for (Buf *b : gc)
+        if (b->p && b->own) grom_dev_free(b->p, b->cap, GROM_DEVCAT_CNV);
     for (KindBufs &K : S->kb) {
-        Buf *kall[] = {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und, &K.skip, &K.pend, &K.plist};
+        Buf *kall[] = CNV_KIND_BUFS(K);
         for (Buf *b : kall)
-            if (b->p) {
-                (void)hipFree(b->p);
-                grom_dev_note(GROM_DEVCAT_CNV, -(int64_t)b->cap);
-            }
+            if (b->p && b->own) grom_dev_free(b->p, b->cap, GROM_DEVCAT_CNV);
         if (K.st) (void)hipStreamDestroy(K.st);
     }
     if (S->walk_in) (void)hipEventDestroy(S->walk_in);

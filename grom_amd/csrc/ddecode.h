@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "../../include/grom_amd.h"
+#include "devmem.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -94,12 +95,12 @@ void grom_note_alloc_ns(int64_t ns, size_t bytes);
 /* grom_scan_chrom_staged calls fn(arg, s) once its scan no longer reads the
  * stage (before the CNV path): the stage may take the next chromosome then */
 void grom_stage_on_consumed(grom_stage *s, void (*fn)(void *, grom_stage *), void *arg);
-/* device memory accounting per category (the CLI's "device buffers" line) */
-enum { GROM_DEVCAT_SCAN, GROM_DEVCAT_SV, GROM_DEVCAT_CNV, GROM_DEVCAT_STAGE, GROM_DEVCAT_DECODE, GROM_DEVCAT_OTHER,
-       GROM_DEVCAT_N };
-void grom_dev_note(int cat, int64_t delta);
-/* peak[k] / now[k] for k < GROM_DEVCAT_N, [GROM_DEVCAT_N] = their sum */
-void grom_dev_peaks(int64_t *peak, int64_t *now);
+/* free a stage's device block (an idle stage under memory pressure): the bytes
+ * freed; the stage is empty and grows again when it is next filled */
+int64_t grom_stage_drop(grom_stage *s);
+/* device bytes a stage holds */
+int64_t grom_stage_held(const grom_stage *s);
+
 
 /* stage helpers for device-side fills (scan.hip) */
 /* a stage holding exactly sz's counts (n_aux = capacity, the count starts at

@@ -221,21 +221,19 @@ int dgrow(DBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return 0;
     const auto t0 = std::chrono::steady_clock::now();
-    if (b.p) {
-        (void)hipFree(b.p);
-        grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)b.cap);
-    }
+    if (b.p) grom_dev_free(b.p, b.cap, GROM_DEVCAT_DECODE);
     b.p = nullptr;
     b.cap = 0;
-    const size_t want = bytes + bytes / 8 + 256;
-    const hipError_t e = hipMalloc(&b.p, want);
+    // growth slack: an eighth for small buffers, 1/64 for the run-sized ones
+    // (reserved from estimates that carry their own margin)
+    const size_t want = bytes + (bytes >= ((size_t)64 << 20) ? bytes / 64 : bytes / 8) + 256;
+    const int e = grom_dev_malloc(&b.p, want, GROM_DEVCAT_DECODE);
     const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     g_dgrow_ns += ns;
     if (ns > 20000000 && getenv("GROM_VERBOSE"))
         fprintf(stderr, "grom: device buffer of %.2f GB took %.1f ms\n", (double)want / 1e9, ns / 1e6);
-    if (e != hipSuccess) return -1;
+    if (e != 0) return -1;
     b.cap = want;
-    grom_dev_note(GROM_DEVCAT_DECODE, (int64_t)want);
     return 0;
 }
 
@@ -992,10 +990,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->cst) (void)hipStreamSynchronize(c->cst);
     for (int k = 0; k < DD_SLOTS; k++) {
-        if (c->dcomp[k].p) {
-            (void)hipFree(c->dcomp[k].p);
-            grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)c->dcomp[k].cap);
-        }
+        if (c->dcomp[k].p) grom_dev_free(c->dcomp[k].p, c->dcomp[k].cap, GROM_DEVCAT_DECODE);
         if (c->cev[k]) (void)hipEventDestroy(c->cev[k]);
     }
     for (int k = 0; k < DD_SLOTS; k++) {
@@ -1003,10 +998,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
         if (r.st) (void)hipStreamSynchronize(r.st);
         DBuf *rb[] = {&r.U, &r.blk, &r.status, &r.misc, &r.S, &r.ccnt, &r.cbase, &r.off, &r.tmp};
         for (DBuf *b : rb)
-            if (b->p) {
-                (void)hipFree(b->p);
-                grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)b->cap);
-            }
+            if (b->p) grom_dev_free(b->p, b->cap, GROM_DEVCAT_DECODE);
         for (int e = 0; e < 3; e++)
             if (r.ev[e]) (void)hipEventDestroy(r.ev[e]);
         if (r.h_small) (void)hipHostFree(r.h_small);
@@ -1018,10 +1010,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
                    &c->srcs, &c->tfq, &c->tfs,
                    &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack};
     for (DBuf *b : all)
-        if (b->p) {
-            (void)hipFree(b->p);
-            grom_dev_note(GROM_DEVCAT_DECODE, -(int64_t)b->cap);
-        }
+        if (b->p) grom_dev_free(b->p, b->cap, GROM_DEVCAT_DECODE);
     for (int k = 0; k < 4; k++)
         if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -1029,26 +1018,6 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     if (c->st) (void)hipStreamDestroy(c->st);
     if (c->cst) (void)hipStreamDestroy(c->cst);
     delete c;
-}
-
-// device bytes held per category (scan, breakpoint, CNV, stage, decode), now
-// and at their peak, and the peak of their sum (the CLI's "device buffers" line)
-static std::atomic<int64_t> g_dev_now[GROM_DEVCAT_N + 1], g_dev_peak[GROM_DEVCAT_N + 1];
-
-extern "C" void grom_dev_note(int cat, int64_t delta) {
-    if (cat < 0 || cat >= GROM_DEVCAT_N) cat = GROM_DEVCAT_N - 1;
-    const int64_t v = (g_dev_now[cat] += delta), t = (g_dev_now[GROM_DEVCAT_N] += delta);
-    int64_t p = g_dev_peak[cat].load();
-    while (v > p && !g_dev_peak[cat].compare_exchange_weak(p, v)) {}
-    p = g_dev_peak[GROM_DEVCAT_N].load();
-    while (t > p && !g_dev_peak[GROM_DEVCAT_N].compare_exchange_weak(p, t)) {}
-}
-
-extern "C" void grom_dev_peaks(int64_t *peak, int64_t *now) {
-    for (int k = 0; k <= GROM_DEVCAT_N; k++) {
-        if (peak) peak[k] = g_dev_peak[k].load();
-        if (now) now[k] = g_dev_now[k].load();
-    }
 }
 
 extern "C" void grom_note_alloc_ns(int64_t ns, size_t bytes) {
@@ -1110,8 +1079,7 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_sta
     DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
     DGROW(c->rpos, r4); DGROW(c->krec, r8); DGROW(c->srcs, r8); DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8);
     DGROW(c->vals2, r4); DGROW(c->head, r4);
-    // the insert statistics' arrays (dd_run_stats)
-    DGROW(c->sq, r4); DGROW(c->sqi, r4); DGROW(c->sv, r4); DGROW(c->slq, r4); DGROW(c->sm, r8);
+    // (the insert statistics' arrays are the parse's: dd_run_stats)
     const size_t take = 4 * (size_t)std::min<int64_t>(recs + 1, (int64_t)1 << 24);
     DGROW(c->s_ins, take); DGROW(c->s_lq, take);
     // the parse's small arrays too (a small allocation made while the stage
@@ -1239,32 +1207,35 @@ extern "C" int dd_run_stats(dd_ctx *c, int slot, int32_t min_mapq, int64_t cap_l
     *n_taken = 0;
     *m_contrib = 0;
     if (R == 0 || cap_left <= 0) return 0;
-    DGROW(c->sq, 4 * (size_t)R);
-    DGROW(c->sqi, 4 * (size_t)R);
-    DGROW(c->sv, 4 * (size_t)R);
-    DGROW(c->slq, 4 * (size_t)R);
-    DGROW(c->sm, 8 * (size_t)R);
+    // the parse's per-record arrays serve the statistics (both run on c->st,
+    // one after the other): sq, sqi, sv, slq, sm
+    DGROW(c->keep, 4 * (size_t)(R + 1));
+    DGROW(c->kidx, 4 * (size_t)(R + 1));
+    DGROW(c->drop, 4 * (size_t)(R + 1));
+    DGROW(c->didx, 4 * (size_t)(R + 1));
+    DGROW(c->nb, 8 * (size_t)(R + 1));
+    DBuf &sq = c->keep, &sqi = c->kidx, &sv = c->drop, &slq = c->didx, &sm = c->nb;
     const int64_t take_cap = std::min<int64_t>(cap_left, R);
     DGROW(c->s_ins, 4 * (size_t)take_cap);
     DGROW(c->s_lq, 4 * (size_t)take_cap);
     hipLaunchKernelGGL(k_stats, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off), R, min_mapq,
-                       P<uint32_t>(c->sq), P<int32_t>(c->sv), P<int32_t>(c->slq), P<int64_t>(c->sm));
+                       P<uint32_t>(sq), P<int32_t>(sv), P<int32_t>(slq), P<int64_t>(sm));
     size_t tb = 0, tb2 = 0;
-    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->sq), P<uint32_t>(c->sqi), (int)R, st));
-    DCK(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, P<int64_t>(c->sm), P<int64_t>(c->sm), (int)R, st));
+    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(sq), P<uint32_t>(sqi), (int)R, st));
+    DCK(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, P<int64_t>(sm), P<int64_t>(sm), (int)R, st));
     DGROW(c->tmp, std::max(tb, tb2));
-    DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->sq), P<uint32_t>(c->sqi), (int)R, st));
-    DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, tb2, P<int64_t>(c->sm), P<int64_t>(c->sm), (int)R, st));
+    DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(sq), P<uint32_t>(sqi), (int)R, st));
+    DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, tb2, P<int64_t>(sm), P<int64_t>(sm), (int)R, st));
     DGROW(c->misc, 256);
     int64_t *mcap = (int64_t *)((char *)c->misc.p + 64);
     DCK(hipMemsetAsync(mcap, 0xff, 8, st));
-    hipLaunchKernelGGL(k_stats_take, dim3(grid_for(R)), dim3(256), 0, st, P<uint32_t>(c->sq), P<uint32_t>(c->sqi),
-                       P<int32_t>(c->sv), P<int32_t>(c->slq), P<int64_t>(c->sm), R, take_cap, P<int32_t>(c->s_ins),
+    hipLaunchKernelGGL(k_stats_take, dim3(grid_for(R)), dim3(256), 0, st, P<uint32_t>(sq), P<uint32_t>(sqi),
+                       P<int32_t>(sv), P<int32_t>(slq), P<int64_t>(sm), R, take_cap, P<int32_t>(c->s_ins),
                        P<int32_t>(c->s_lq), mcap);
     // qualifying total, m total, m at the cap
-    DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(c->sqi) + R - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(c->sq) + R - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync(c->h_small + 1, P<int64_t>(c->sm) + R - 1, 8, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(sqi) + R - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(sq) + R - 1, 4, hipMemcpyDeviceToHost, st));
+    DCK(hipMemcpyAsync(c->h_small + 1, P<int64_t>(sm) + R - 1, 8, hipMemcpyDeviceToHost, st));
     DCK(hipMemcpyAsync(c->h_small + 2, mcap, 8, hipMemcpyDeviceToHost, st));
     DCK(hipStreamSynchronize(st));
     const uint32_t *hs = (const uint32_t *)c->h_small;

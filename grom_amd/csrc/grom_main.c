@@ -738,13 +738,16 @@ static void fp_stop(fp_sampler *F, double since_start) {
     pthread_cond_broadcast(&F->cv);
     pthread_mutex_unlock(&F->mu);
     pthread_join(F->thr, NULL);
-    int64_t pk[GROM_DEVCAT_N + 1];
+    int64_t pk[GROM_DEVCAT_N + 1], nw = 0;
+    double sw = 0;
     grom_dev_peaks(pk, NULL);
+    grom_dev_waits(&nw, &sw);
     printf("footprint: peak %.2f GB of device memory (%s), at %.3f s of %.3f s; buffers: peak %.2f GB together, "
-           "per kind scan %.2f, breakpoint %.2f, CNV %.2f, stages %.2f, decode %.2f GB\n", F->peak / 1e9,
+           "per kind scan %.2f, breakpoint %.2f, CNV %.2f, stages %.2f, decode %.2f, phase arenas %.2f GB; %lld "
+           "allocations waited %.3f s for memory\n", F->peak / 1e9,
            F->kfd ? "this process, kfd" : "device-wide use above the start's", F->t_peak, since_start,
            pk[GROM_DEVCAT_N] / 1e9, pk[GROM_DEVCAT_SCAN] / 1e9, pk[GROM_DEVCAT_SV] / 1e9, pk[GROM_DEVCAT_CNV] / 1e9,
-           pk[GROM_DEVCAT_STAGE] / 1e9, pk[GROM_DEVCAT_DECODE] / 1e9);
+           pk[GROM_DEVCAT_STAGE] / 1e9, pk[GROM_DEVCAT_DECODE] / 1e9, pk[GROM_DEVCAT_ARENA] / 1e9, (long long)nw, sw);
     pthread_mutex_destroy(&F->mu);
     pthread_cond_destroy(&F->cv);
     F->started = 0;
@@ -1199,8 +1202,13 @@ static int run_streamed(cli_state *S) {
     if (!g_plan_only) {
         int per_gpu = getenv("GROM_SCANS_PER_GPU") ? atoi(getenv("GROM_SCANS_PER_GPU")) : 2;
         if (per_gpu < 1) per_gpu = 1;
+        /* one stage per scan plus the one being decoded: a scan gives its
+         * stage back before its CNV path (grom_stage_on_consumed);
+         * GROM_STAGES overrides */
+        int n_st = getenv("GROM_STAGES") ? atoi(getenv("GROM_STAGES")) : per_gpu + 1;
+        if (n_st < 1) n_st = 1;
         for (int d = 0; d < S->n_dev && !wd; d++)
-            for (int k = 0; k < per_gpu + 2 && n_stages < 256; k++) {
+            for (int k = 0; k < n_st && n_stages < 256; k++) {
                 grom_stage *st = grom_stage_new(S->device + d);
                 if (!st) break;
                 stages[n_stages++] = st;
@@ -1212,6 +1220,21 @@ static int run_streamed(cli_state *S) {
             stages[n_stages++] = st;
             pd_add_stage(pd, st, atoi(wd));
         }
+    }
+    /* a share of a multi-process run (GROM_CHROMS, bench.py --gpus N) reads
+     * the insert statistics from <bam>.mean as the reference's -c children do
+     * (load_insert_mean, GROM.c:1011-1026, 22253-22257) */
+    int given = 0, g_mean = 0, g_lseq = 0, g_min = 0, g_max = 0;
+    long g_mapped = 0;
+    char mean_name[4096];
+    snprintf(mean_name, sizeof(mean_name), "%s.mean", S->bam_name);
+    if (getenv("GROM_CHROMS") && !g_plan_only) {
+        FILE *mf = fopen(mean_name, "r");
+        if (mf) {
+            given = fscanf(mf, "%d %d %d %d %ld", &g_mean, &g_lseq, &g_min, &g_max, &g_mapped) == 5 && g_mean > 0;
+            fclose(mf);
+        }
+        if (given) pd_stats_given(pd);
     }
     if (getenv("GROM_CHROMS")) {
         int *want = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
@@ -1239,7 +1262,16 @@ static int run_streamed(cli_state *S) {
     /* the scan contexts while the head of the BAM is decoded (their insert
      * parameters are set once the statistics are known) */
     const int ws_fail = setup_workers(S);
-    const int imean = pd_insert_stats(pd, grom_prob2(S->num_sd), P->min_mapq, &lseq, &imin, &imax, &mapped);
+    int imean;
+    if (given) {
+        imean = g_mean;
+        lseq = g_lseq;
+        imin = g_min;
+        imax = g_max;
+        mapped = g_mapped;
+    } else {
+        imean = pd_insert_stats(pd, grom_prob2(S->num_sd), P->min_mapq, &lseq, &imin, &imax, &mapped);
+    }
     if (imean < 0) {
         const int fallback = imean == -2;
         if (!fallback) printf("ERROR: no reads to estimate the insert size from\n");
@@ -1249,7 +1281,15 @@ static int run_streamed(cli_state *S) {
         free(dev_of);
         return fallback ? CLI_FALLBACK : 1;
     }
-    print_insert(S, imean, lseq, imin, imax, mapped);
+    if (given) {
+        printf("Loading insert_mean et al from %s\n", mean_name);
+        t_insert_printed = 1;
+        grom_params_set_insert(&S->P, imean, imin, imax, lseq);
+        printf("insert mean, insert minimum, insert maximum: %d %d %d\n", S->P.insert_mean, imin, imax);
+        printf("median read length: %d\n", lseq);
+    } else {
+        print_insert(S, imean, lseq, imin, imax, mapped);
+    }
     const double t_stats = clock_gettime_s();
     int *keep = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
     chrom_plan **plan = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(chrom_plan *));
@@ -1377,11 +1417,11 @@ done:
             printf("device decode: %lld records, %.2f GB compressed read and copied to HBM, %.2f GB inflated on the GPU; "
                    "file reads %.2f s (read ahead; waited for %.2f s), device work %.2f s (GPU inflate %.3f s, record walk %.3f s, "
                    "parse %.3f s; %lld of %lld walk sub-chunks re-walked), device buffer growth %.3f s, per-chromosome decode + "
-                   "finalise %.2f s, wall %.2f s\n",
+                   "finalise %.2f s, idle stage blocks reclaimed %lld, wall %.2f s\n",
                    (long long)pc.records, pc.compressed_bytes / 1e9, pc.inflated_bytes / 1e9, pc.io_s, pc.wait_s,
                    pc.decode_thread_s,
                    pc.gpu_ms[0] / 1e3, pc.gpu_ms[1] / 1e3, pc.gpu_ms[2] / 1e3, (long long)pc.rewalked, (long long)pc.subchunks,
-                   pc.gpu_ms[3] / 1e3, pc.upload_s, clock_gettime_s() - t_start);
+                   pc.gpu_ms[3] / 1e3, pc.upload_s, (long long)pc.reclaimed, clock_gettime_s() - t_start);
         else
         printf("streamed decode: %lld records in %lld pieces, %d threads (%s), %.2f GB inflated, %.2f GB to HBM, "
                "decoder busy %.2f s (inflate %.2f s, file reads %.2f s), uploader %.2f s (waiting %.2f s), wall %.2f s\n",

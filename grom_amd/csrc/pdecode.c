@@ -433,6 +433,9 @@ struct pd_session {
     pthread_t *dw;
     int n_dw, dw_started;
     double c_gpu_ms[4];    /* inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
+    int64_t c_reclaimed;   /* idle stage blocks freed for a waiting allocation */
+    int stats_given;       /* the insert statistics come from <bam>.mean (pd_stats_given) */
+    int reclaim_on;        /* pd_reclaim_stages is registered (devmem.h) */
     int64_t c_rewalk, c_subchunks; /* record walk: sub-chunks re-walked / all */
     int io_threads;
     int64_t insert_cap;    /* PD_INSERT_CAP (GROM_TEST_INSERT_CAP: tests of both decoders against each other) */
@@ -2403,24 +2406,55 @@ static int next_placed_run(const pd_session *s, int ri);
 
 /* Stages reserved ahead: the first chromosomes' stages would otherwise be
  * allocated (hipMalloc of ~15 GB each at 30x) on the decode's critical path.
- * A helper thread sizes every stage of the device for the largest run while
- * the insert statistics load: reads from the index's record count, bases and
- * CIGAR words per record from the first 2,000 records of the file. */
+ * The decode hands chromosomes out longest first and a stage's later
+ * chromosomes are never larger than its first, so stage i is sized for the
+ * i-th largest run of this device: its record count from the index, bases and
+ * CIGAR words per record from the first 2,000 records of the file, and that
+ * chromosome's reference. */
 typedef struct {
     pd_session *s;
     int device;
 } stres_job;
 
+static void *stres_body(stres_job *j);
+
 static void *stres_main(void *arg) {
     stres_job *j = (stres_job *)arg;
+    pd_trace(j->s, PD_EV_PHASE, 105, 0);
+    void *r = stres_body(j);
+    pd_trace(j->s, PD_EV_PHASE, 105, 1);
+    return r;
+}
+
+static void *stres_body(stres_job *j) {
     pd_session *s = j->s;
-    int64_t recs = 0, ref = 0;
-    for (int i = 0; i < s->n_runs; i++)
-        if (s->runs[i].tid >= 0 && s->runs[i].count > recs) recs = s->runs[i].count;
+    /* this device's wanted chromosomes by record count, largest first */
+    int64_t recs[64], refl[64];
+    int nw = 0;
+    for (int k = 0; k < s->n_plan; k++) {
+        if (s->ch[k].device != j->device || !s->want[k] || s->ch[k].run < 0) continue;
+        const int64_t c = s->runs[s->ch[k].run].count;
+        if (c <= 0) continue;
+        /* insertion into the top 64 (more stages than that are never made) */
+        int at = nw;
+        if (nw == 64) {
+            if (recs[63] >= c) continue;
+            at = 63;
+        } else {
+            nw++;
+        }
+        for (; at > 0 && recs[at - 1] < c; at--) {
+            recs[at] = recs[at - 1];
+            refl[at] = refl[at - 1];
+        }
+        recs[at] = c;
+        refl[at] = s->plan[k].len;
+    }
+    int64_t ref_max = 0;
     for (int k = 0; k < s->n_plan; k++)
-        if (s->ch[k].device == j->device && s->want[k] && s->plan[k].len > ref) ref = s->plan[k].len;
+        if (s->ch[k].device == j->device && s->want[k] && s->plan[k].len > ref_max) ref_max = s->plan[k].len;
     const int r0 = next_placed_run(s, -1);
-    if (recs <= 0 || r0 < 0) return NULL;
+    if (nw == 0 || r0 < 0) return NULL;
     pd_reader r;
     memset(&r, 0, sizeof(r));
     inf_init(&r.inf);
@@ -2438,14 +2472,6 @@ static void *stres_main(void *arg) {
     }
     rd_free(&r);
     if (n == 0) return NULL;
-    grom_stage_sizes est;
-    memset(&est, 0, sizeof(est));
-    est.n = recs;
-    est.n_drop = recs / 4 + 1024;
-    est.n_bases = (int64_t)((double)recs * ((double)lq / (double)n + 1.0) * 1.05);
-    est.n_cigar_ops = (int64_t)((double)recs * (double)nc / (double)n * 1.1) + 1024;
-    est.n_aux = recs / 16 + 1024;
-    est.ref_len = ref;
     pthread_mutex_lock(&s->mu);
     int ns = s->n_stage;
     grom_stage *mine[64];
@@ -2461,15 +2487,18 @@ static void *stres_main(void *arg) {
             mine[m++] = s->stages[i];
         }
     pthread_mutex_unlock(&s->mu);
-    /* a stage's bytes, roughly: the read SoA, CIGAR words,
-     * qualities + packed bases, dropped records, the reference; stages are
-     * reserved while the device keeps room for the scan contexts (two
-     * chromosome scratches) beside them */
-    const double bytes = 48.0 * (double)est.n + 4.0 * (double)est.n_cigar_ops + 1.5 * (double)est.n_bases +
-                         16.0 * (double)est.n_drop + (double)est.ref_len;
     for (int i = 0; i < m; i++) {
-        const int64_t fr = grom_device_mem_free(j->device);
-        if (fr < 0 || (double)fr < bytes + 3.0 * bytes + (double)((int64_t)32 << 30)) break;
+        const int64_t rc = recs[i < nw ? i : nw - 1];
+        grom_stage_sizes est;
+        memset(&est, 0, sizeof(est));
+        est.n = rc;
+        est.n_drop = rc / 4 + 1024;
+        est.n_bases = (int64_t)((double)rc * ((double)lq / (double)n + 1.0) * 1.05);
+        est.n_cigar_ops = (int64_t)((double)rc * (double)nc / (double)n * 1.1) + 1024;
+        est.n_aux = rc / 16 + 1024;
+        /* the reference: this chromosome's, at least the largest's share that
+         * a later, shorter run with a longer sequence would need */
+        est.ref_len = refl[i < nw ? i : nw - 1] > ref_max / 2 ? refl[i < nw ? i : nw - 1] : ref_max / 2;
         (void)grom_stage_begin(mine[i], &est);
     }
     pthread_mutex_lock(&s->mu);
@@ -2485,7 +2514,7 @@ static void *stres_main(void *arg) {
 /* The decode buffers sized once, while the first run is read: the largest
  * record count the index gives for a run this worker may load, and its
  * largest compressed span times the inflate ratio of the BAM's first blocks
- * (+15%).  A run beyond the estimate still grows the buffers. */
+ * (+4%).  A run beyond the estimate still grows the buffers. */
 static int dw_reserve(dd_worker *w, char *err, int errlen) {
     pd_session *s = w->s;
     int64_t recs = 0, span = 0;
@@ -2518,7 +2547,7 @@ static int dw_reserve(dd_worker *w, char *err, int errlen) {
     }
     free(b);
     if (csum <= 0 || usum <= 0) return 0;
-    const int64_t ub = (int64_t)((double)span * (double)usum / (double)csum * 1.15);
+    const int64_t ub = (int64_t)((double)span * (double)usum / (double)csum * 1.04);
     int64_t nst = 0;
     for (int t = 0; t < s->n_tgt; t++)
         if (s->n_lin[t] > nst) nst = s->n_lin[t];
@@ -2709,12 +2738,15 @@ static void *dw_main(void *arg) {
     for (int a = 0; a < n_lo; a++)
         if (a % w->nsub == w->sub) mine[n_mine++] = lo[a];
     free(lo);
-    if (rc == 0 && !w->first && n_mine > 0) pf_want(w, s->ch[mine[0]].run);
-    if (rc == 0 && w->first) { /* the stats prefix first: start its read now */
+    const int stats_here = w->first && !s->stats_given;
+    if (rc == 0 && !stats_here && n_mine > 0) pf_want(w, s->ch[mine[0]].run);
+    if (rc == 0 && stats_here) { /* the stats prefix first: start its read now */
         const int r0 = next_placed_run(s, -1);
         if (r0 >= 0) pf_want(w, stats_prefix_end(s, r0) != UINT64_MAX ? -r0 - 2 : r0);
     }
+    pd_trace(s, PD_EV_PHASE, 104, 0);
     if (rc == 0 && dw_reserve(w, err, (int)sizeof(err))) rc = -1;
+    pd_trace(s, PD_EV_PHASE, 104, 1);
     /* (after the worker's own buffers: a small allocation waits behind any
      * large one in flight) */
     pthread_t stres_thr;
@@ -2722,7 +2754,8 @@ static void *dw_main(void *arg) {
     const char *nsr = getenv("GROM_NO_STAGE_RESERVE");
     const int stres = rc == 0 && w->sub == 0 && !(nsr && atoi(nsr) == 1) &&
                       pthread_create(&stres_thr, NULL, stres_main, &sj) == 0;
-    if (rc == 0 && w->first) rc = dw_stats(w, err, (int)sizeof(err));
+    if (rc == 0 && stats_here) rc = dw_stats(w, err, (int)sizeof(err));
+    else if (rc == 0 && w->first) mark_stats_done(s);
     if (stres) pthread_join(stres_thr, NULL); /* the stages are the worker's again */
     /* the final plan (which chromosomes, which records each one's run starts with) */
     if (rc == 0) {
@@ -2839,6 +2872,8 @@ static int pd_start_device(pd_session *s) {
     return 0;
 }
 
+static int64_t pd_reclaim_stages(void *arg, int device, size_t want);
+
 int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan_only) {
     s->min_mapq_stats = min_mapq;
     s->plan_only = plan_only;
@@ -2846,6 +2881,10 @@ int pd_start(pd_session *s, int min_mapq, int n_dev, const int *dev_of, int plan
     s->no_mirror = plan_only && getenv("GROM_DECODE_ONLY") != NULL; /* time the decode alone */
     s->n_dev = n_dev < 1 ? 1 : n_dev;
     for (int k = 0; k < s->n_plan; k++) s->ch[k].device = dev_of ? dev_of[k] : 0;
+    if (!plan_only) { /* an allocation short of device memory may take idle stages' blocks */
+        grom_dev_add_reclaim(pd_reclaim_stages, s);
+        s->reclaim_on = 1;
+    }
     if (!plan_only && s->dev_mode) return pd_start_device(s);
     s->thr = (pthread_t *)calloc((size_t)s->n_threads, sizeof(pthread_t));
     for (int t = 0; t < s->n_threads; t++)
@@ -2886,6 +2925,8 @@ int pd_insert_stats(pd_session *s, double prob2, int min_mapq, int *lseq, int *i
     return mean;
 }
 
+void pd_stats_given(pd_session *s) { s->stats_given = 1; }
+
 void pd_set_walk(pd_session *s, int32_t index_start, int32_t overlap_mult, int32_t insert_max, const int *keep) {
     pthread_mutex_lock(&s->mu);
     for (int k = 0; k < s->n_plan; k++) s->keep[k] = keep ? (keep[k] != 0) : 1;
@@ -2917,6 +2958,37 @@ void pd_release_stage(pd_session *s, grom_stage *st) {
         if (s->stages[i] == st) { s->stage_busy[i] = 0; s->stage_owner[i] = -1; }
     pthread_cond_broadcast(&s->cv);
     pthread_mutex_unlock(&s->mu);
+    grom_dev_release_notify(); /* an allocation waiting for memory may take its block */
+}
+
+/* devmem.h reclaim hook: the blocks of this device's idle stages (no
+ * chromosome holds them), largest first, until `want` bytes are free */
+static int64_t pd_reclaim_stages(void *arg, int device, size_t want) {
+    pd_session *s = (pd_session *)arg;
+    int64_t got = 0;
+    for (;;) {
+        pthread_mutex_lock(&s->mu);
+        int pick = -1;
+        for (int i = 0; i < s->n_stage; i++)
+            if (!s->stage_busy[i] && s->stage_dev[i] == device && grom_stage_held(s->stages[i]) > 0 &&
+                (pick < 0 || grom_stage_held(s->stages[i]) > grom_stage_held(s->stages[pick])))
+                pick = i;
+        if (pick >= 0) {
+            s->stage_busy[pick] = 1;
+            s->stage_owner[pick] = -3;
+        }
+        pthread_mutex_unlock(&s->mu);
+        if (pick < 0) break;
+        got += grom_stage_drop(s->stages[pick]);
+        pthread_mutex_lock(&s->mu);
+        s->stage_busy[pick] = 0;
+        s->stage_owner[pick] = -1;
+        s->c_reclaimed++;
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+        if (got >= (int64_t)want) break;
+    }
+    return got;
 }
 
 int pd_add_stage(pd_session *s, grom_stage *st, int device) {
@@ -2964,6 +3036,7 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
     c->subchunks = s->c_subchunks;
     c->io_s = s->c_io_s;
     c->upload_s = s->c_upl_s;
+    c->reclaimed = s->c_reclaimed;
     c->wait_s = s->c_wait_s;
     c->threads = s->n_threads;
     pthread_mutex_unlock(&s->mu);
@@ -2973,6 +3046,7 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
 
 void pd_close(pd_session *s) {
     if (!s) return;
+    if (s->reclaim_on) grom_dev_remove_reclaim(pd_reclaim_stages, s);
     if (s->tr && s->trace_path) {
         FILE *f = fopen(s->trace_path, "w");
         if (f) {

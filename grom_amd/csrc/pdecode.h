@@ -84,6 +84,9 @@ int pd_insert_stats(pd_session *s, double prob2, int min_mapq, int *lseq, int *i
 /* the walk's index start (cdp_one_base_index_start, GROM.c:2918), the facts
  * grom_batch_finish needs, and the final plan: keep[k] = 0 drops preliminary
  * chromosome k (the length test of find_disc_svs needs the insert size) */
+/* before pd_start: the caller has the insert statistics (<bam>.mean, as the
+ * reference's -c children load them, GROM.c:22253-22257); no statistics pass */
+void pd_stats_given(pd_session *s);
 void pd_set_walk(pd_session *s, int32_t index_start, int32_t overlap_mult, int32_t insert_max, const int *keep);
 /* wait for plan chromosome k (kept, in order) to be staged and finalised:
  * 0 with its stage and facts; 1 if the index-based plan was contradicted by
@@ -104,6 +107,7 @@ typedef struct pd_counters {
     int device;          /* runs decoded on the GPU (device mode) */
     int64_t rewalked, subchunks; /* device mode: record-walk sub-chunks re-walked / all */
     double gpu_ms[4];    /* device mode: inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
+    int64_t reclaimed;   /* idle stage blocks freed for allocations short of device memory */
 } pd_counters;
 void pd_get_counters(pd_session *s, pd_counters *c);
 void pd_close(pd_session *s);

@@ -199,30 +199,35 @@ namespace {
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    bool own = false;          // p is this buffer's own allocation (else a piece of `ar`'s phase)
+    grom_arena *ar = nullptr;  // the context's phase arena, for the pileup phase's per-read buffers
 };
 
 static int ensure(DevBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return GROM_OK;
-    if (b.p) {
-        (void)hipFree(b.p);
-        grom_dev_note(GROM_DEVCAT_SCAN, -(int64_t)b.cap);
-    }
+    if (b.p && b.own) grom_dev_free(b.p, b.cap, GROM_DEVCAT_SCAN);
     b.p = nullptr;
     b.cap = 0;
+    b.own = false;
     size_t want = bytes + bytes / 8 + 64;  // slack: kernels read whole 16-byte words
-    if (hipMalloc(&b.p, want) != hipSuccess) {
+    if (b.ar && (b.p = grom_arena_take(b.ar, want)) != nullptr) {
+        b.cap = want;
+        return GROM_OK;
+    }
+    if (grom_dev_malloc(&b.p, want, GROM_DEVCAT_SCAN)) {
         set_err("hipMalloc(%zu) failed", want);
         return GROM_E_NOMEM;
     }
     b.cap = want;
-    grom_dev_note(GROM_DEVCAT_SCAN, (int64_t)want);
+    b.own = true;
     return GROM_OK;
 }
 
 struct Ctx {
     bool init = false;
     int device = -1;
+    grom_arena *ar = nullptr;  // the phase arena (devmem.h): pileup/breakpoint phase, then CNV phase
     hipStream_t st = nullptr;
     grom_params prm{};
     double *d_mq = nullptr, *d_hez = nullptr;
@@ -379,6 +384,32 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     // scratch
     const bool want_dbg = dbg_counts != nullptr;
     const bool sv_debug = getenv("GROM_SV_DEBUG") != nullptr;  // keep the breakpoint records for grom_debug_sv
+    // The pileup/breakpoint phase: its per-read records and breakpoint
+    // buffers are carved from the context's phase arena, which the CNV phase
+    // takes over after the breakpoint tests (devmem.h).  Callers that read
+    // those buffers after the scan (the debug dumps) keep them separate.
+    const bool use_arena = !want_dbg && !sv_debug && !getenv("GROM_DUMP") && !getenv("GROM_NO_ARENA");
+    grom_arena *par = nullptr;
+    if (use_arena) {
+        if (!C.ar) C.ar = grom_arena_new(GROM_DEVCAT_ARENA);
+        cnv_scratch_sync(C.cnv);  // (the last CNV phase's streams are done with the arena)
+        if (grom_arena_begin(C.ar)) {
+            set_err("phase arena: device memory allocation failed");
+            return GROM_E_NOMEM;
+        }
+        par = C.ar;
+    }
+    if (!C.sv) C.sv = sv_scratch_new();
+    sv_scratch_phase(C.sv, par);
+    for (DevBuf *b : {&C.meta, &C.keep}) {
+        if (b->own && par) grom_dev_free(b->p, b->cap, GROM_DEVCAT_SCAN);
+        if (!b->own || par) {
+            b->p = nullptr;
+            b->cap = 0;
+            b->own = false;
+        }
+        b->ar = par;
+    }
     int64_t n_eval = (a.eval_hi >= a.eval_lo) ? (int64_t)a.eval_hi - a.eval_lo + 1 : 0;
     if ((rc = ensure(C.tlo, sizeof(int32_t) * n_tiles)) || (rc = ensure(C.thi, sizeof(int32_t) * n_tiles)) ||
         (rc = ensure(C.caf_mq, sizeof(int32_t) * ch->len)) || (rc = ensure(C.caf_rd, sizeof(int32_t) * ch->len)) ||
@@ -716,6 +747,16 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
             }
         }
         const double t_sv = ms_since(t_start);
+        if (ch->cnv && !want_dbg) {
+            // the CNV phase: the arena's pileup/breakpoint buffers are dead
+            // (sv_evaluate waited for the stream; the rows read pinned copies)
+            if (!C.cnv) C.cnv = cnv_scratch_new();
+            if (par && grom_arena_begin(par)) {
+                set_err("phase arena: device memory allocation failed");
+                return GROM_E_NOMEM;
+            }
+            cnv_scratch_phase(C.cnv, par);
+        }
         if (reads_done) {
             // every kernel that reads the input has finished (sv_evaluate
             // waited for the stream) and so has the reference's host copy
@@ -932,8 +973,7 @@ void grom_dev_fini(int device) {
                      &C.misc, &C.dbg, &C.slots, &C.r_aidx, &C.r_aux, &C.r_dpos, &C.r_dlq, &C.r_dbef};
     for (DevBuf *b : all)
         if (b->p) {
-            (void)hipFree(b->p);
-            grom_dev_note(GROM_DEVCAT_SCAN, -(int64_t)b->cap);
+            if (b->own) grom_dev_free(b->p, b->cap, GROM_DEVCAT_SCAN);
             b->p = nullptr;
             b->cap = 0;
         }
@@ -944,6 +984,7 @@ void grom_dev_fini(int device) {
     if (C.st_copy) (void)hipStreamDestroy(C.st_copy);
     cnv_scratch_free(C.cnv);
     sv_scratch_free(C.sv);
+    grom_arena_free(C.ar);
     (void)hipFree(C.d_mq);
     (void)hipFree(C.d_hez);
     (void)hipEventDestroy(C.e0);
@@ -1132,6 +1173,26 @@ struct grom_stage {
     char *a(int k) const { return blk + off[k]; }
 };
 
+int64_t grom_stage_held(const grom_stage *s) { return s ? (int64_t)(s->blk_cap + s->scratch_cap) : 0; }
+
+int64_t grom_stage_drop(grom_stage *s) {
+    if (!s || (!s->blk && !s->scratch)) return 0;
+    (void)hipSetDevice(s->device);
+    (void)hipStreamSynchronize(s->st);
+    const int64_t freed = (int64_t)(s->blk_cap + s->scratch_cap);
+    if (s->blk) grom_dev_free(s->blk, s->blk_cap, GROM_DEVCAT_STAGE);
+    if (s->scratch) grom_dev_free(s->scratch, s->scratch_cap, GROM_DEVCAT_STAGE);
+    s->blk = nullptr;
+    s->blk_cap = 0;
+    s->scratch = nullptr;
+    s->scratch_cap = 0;
+    memset(s->cap, 0, sizeof(s->cap));
+    memset(s->off, 0, sizeof(s->off));
+    s->n = s->n_cig = s->n_bases = s->n_aux = s->n_drop = s->ref_len = 0;
+    s->front = 0;
+    return freed;
+}
+
 void grom_stage_on_consumed(grom_stage *s, void (*fn)(void *, grom_stage *), void *arg) {
     if (!s) return;
     s->consumed = fn;
@@ -1142,15 +1203,13 @@ static char *stage_scratch(grom_stage *s, size_t bytes) {
     if (bytes <= s->scratch_cap) return s->scratch;
     if (s->scratch) {
         (void)hipStreamSynchronize(s->st);
-        (void)hipFree(s->scratch);
-        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->scratch_cap);
+        grom_dev_free(s->scratch, s->scratch_cap, GROM_DEVCAT_STAGE);
     }
     s->scratch = nullptr;
     s->scratch_cap = 0;
     const size_t want = bytes + bytes / 2 + 4096;
-    if (hipMalloc((void **)&s->scratch, want) != hipSuccess) return nullptr;
+    if (grom_dev_malloc((void **)&s->scratch, want, GROM_DEVCAT_STAGE)) return nullptr;
     s->scratch_cap = want;
-    grom_dev_note(GROM_DEVCAT_STAGE, (int64_t)want);
     return s->scratch;
 }
 
@@ -1165,20 +1224,30 @@ static void stage_used(const grom_stage *s, size_t u[SA_N]) {
 
 // make every array hold need[a] bytes (+64 slack), keeping keep[a] bytes of
 // its contents: one new block when anything is short (copies on the stage
-// stream), else nothing
-static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t keep[SA_N]) {
+// stream), else nothing.  A short array gets need + need/grow: appends grow
+// by a quarter (grow 4, amortised), exact or estimated sizes by 1/64.
+static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t keep[SA_N], size_t grow = 64) {
     bool ok = s->blk != nullptr;
     for (int k = 0; k < SA_N && ok; k++) ok = s->cap[k] >= need[k] + 64;
     if (ok) return GROM_OK;
     size_t cap[SA_N], off[SA_N], tot = 0;
     for (int k = 0; k < SA_N; k++) {
-        cap[k] = s->cap[k] >= need[k] + 64 ? s->cap[k] : need[k] + need[k] / 4 + 4096;
+        cap[k] = s->cap[k] >= need[k] + 64 ? s->cap[k] : need[k] + need[k] / grow + 4096;
         off[k] = tot;
         tot += (cap[k] + 255) & ~(size_t)255;
     }
     char *nb = nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    if (hipMalloc((void **)&nb, tot) != hipSuccess) {
+    bool kept = false;
+    for (int k = 0; k < SA_N; k++) kept |= keep[k] != 0;
+    if (s->blk && !kept) {  // nothing to carry over: the old block goes first
+        HIPCHK(hipStreamSynchronize(s->st));
+        grom_dev_free(s->blk, s->blk_cap, GROM_DEVCAT_STAGE);
+        s->blk = nullptr;
+        s->blk_cap = 0;
+        memset(s->cap, 0, sizeof(s->cap));
+    }
+    if (grom_dev_malloc((void **)&nb, tot, GROM_DEVCAT_STAGE)) {
         set_err("grom_stage: hipMalloc(%zu) failed", tot);
         return GROM_E_NOMEM;
     }
@@ -1186,10 +1255,8 @@ static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t ke
         for (int k = 0; k < SA_N; k++)
             if (keep[k]) HIPCHK(hipMemcpyAsync(nb + off[k], s->a(k), keep[k], hipMemcpyDeviceToDevice, s->st));
         HIPCHK(hipStreamSynchronize(s->st));
-        (void)hipFree(s->blk);
-        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->blk_cap);
+        grom_dev_free(s->blk, s->blk_cap, GROM_DEVCAT_STAGE);
     }
-    grom_dev_note(GROM_DEVCAT_STAGE, (int64_t)tot);
     grom_note_alloc_ns(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
                        tot);
     s->blk = nb;
@@ -1225,14 +1292,8 @@ void grom_stage_free(grom_stage *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
-    if (s->blk) {
-        (void)hipFree(s->blk);
-        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->blk_cap);
-    }
-    if (s->scratch) {
-        (void)hipFree(s->scratch);
-        grom_dev_note(GROM_DEVCAT_STAGE, -(int64_t)s->scratch_cap);
-    }
+    if (s->blk) grom_dev_free(s->blk, s->blk_cap, GROM_DEVCAT_STAGE);
+    if (s->scratch) grom_dev_free(s->scratch, s->scratch_cap, GROM_DEVCAT_STAGE);
     for (int k = 0; k < GROM_STAGE_EVENTS; k++)
         if (s->ev[k]) (void)hipEventDestroy(s->ev[k]);
     if (s->all_ev) (void)hipEventDestroy(s->all_ev);
@@ -1313,7 +1374,7 @@ int64_t grom_stage_append(grom_stage *s, const grom_reads *p) {
     size_t need[SA_N], keep[SA_N];
     stage_used(&after, need);
     stage_used(s, keep);
-    int rc = stage_reserve(s, need, keep);
+    int rc = stage_reserve(s, need, keep, 4);
     if (rc) return rc;
     int64_t bytes = 0;
     auto cp = [&](int arr, int64_t off_bytes, const void *src, int64_t nbytes) -> int {

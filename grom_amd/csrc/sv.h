@@ -11,6 +11,7 @@
 
 #include "../../include/grom_amd.h"
 #include "scan_common.h"
+#include "devmem.h"
 
 // cluster types in the order of the reference's OTHER_* codes minus one
 // (GROM.c:668-681)
@@ -53,6 +54,10 @@ struct SvHit {
 struct SvScratch;
 SvScratch *sv_scratch_new();
 void sv_scratch_free(SvScratch *s);
+// a new pileup/breakpoint phase (scan.hip): with an arena, every buffer is
+// carved from its phase (their contents are dead); without one, the buffers
+// are the scratch's own and persist
+void sv_scratch_phase(SvScratch *s, grom_arena *ar);
 
 // device views of the reads the breakpoint pass walks
 struct SvInput {

@@ -919,6 +919,8 @@ __global__ void k_ctx_gather(const grom_sv_ctx *__restrict__ src, const uint32_t
 struct Buf {
     void *p = nullptr;
     size_t cap = 0;
+    bool own = false;          // p is this buffer's own allocation (else a piece of `ar`'s phase)
+    grom_arena *ar = nullptr;  // the context's phase arena (sv_scratch_phase), or none
 };
 
 }  // namespace
@@ -938,35 +940,50 @@ struct SvScratch {
 static int sbuf(Buf &b, size_t bytes, char *err, size_t errlen) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return GROM_OK;
-    if (b.p) {
-        (void)hipFree(b.p);
-        grom_dev_note(GROM_DEVCAT_SV, -(int64_t)b.cap);
-    }
+    if (b.p && b.own) grom_dev_free(b.p, b.cap, GROM_DEVCAT_SV);
     b.p = nullptr;
     b.cap = 0;
+    b.own = false;
     const size_t want = bytes + bytes / 8 + 64;
-    if (hipMalloc(&b.p, want) != hipSuccess) {
+    if (b.ar && (b.p = grom_arena_take(b.ar, want)) != nullptr) {
+        b.cap = want;
+        return GROM_OK;
+    }
+    if (grom_dev_malloc(&b.p, want, GROM_DEVCAT_SV)) {
         snprintf(err, errlen, "breakpoint pass: hipMalloc(%zu) failed", want);
         return GROM_E_NOMEM;
     }
     b.cap = want;
-    grom_dev_note(GROM_DEVCAT_SV, (int64_t)want);
+    b.own = true;
     return GROM_OK;
 }
 
 SvScratch *sv_scratch_new() { return new SvScratch(); }
 
+#define SV_ALL_BUFS(s)                                                                                                \
+    {&s->cnt, &s->off, &s->keys, &s->vals, &s->keys2, &s->vals2, &s->ev, &s->run_pos, &s->run_len, &s->run_off,       \
+     &s->n_runs, &s->tmp, &s->sums, &s->bits, &s->f_cand, &s->f_ind, &s->f_dbg, &s->o_cand, &s->o_ind, &s->o_dbg,      \
+     &s->rec, &s->irec_c, &s->irec, &s->drec, &s->ctx, &s->ctx2, &s->ckeys, &s->ckeys2, &s->cvals, &s->cvals2,         \
+     &s->n_ctx, &s->hits, &s->n_hits, &s->hits2}
+
+void sv_scratch_phase(SvScratch *s, grom_arena *ar) {
+    Buf *all[] = SV_ALL_BUFS(s);
+    for (Buf *b : all) {
+        if (b->own && ar) grom_dev_free(b->p, b->cap, GROM_DEVCAT_SV);  // (an overflow of the last phase)
+        if (!b->own || ar) {
+            b->p = nullptr;
+            b->cap = 0;
+            b->own = false;
+        }
+        b->ar = ar;
+    }
+}
+
 void sv_scratch_free(SvScratch *s) {
     if (!s) return;
-    Buf *all[] = {&s->cnt, &s->off, &s->keys, &s->vals, &s->keys2, &s->vals2, &s->ev, &s->run_pos, &s->run_len,
-                  &s->run_off, &s->n_runs, &s->tmp, &s->sums, &s->bits, &s->f_cand, &s->f_ind, &s->f_dbg,
-                  &s->o_cand, &s->o_ind, &s->o_dbg, &s->rec, &s->irec_c, &s->irec, &s->drec, &s->ctx, &s->ctx2,
-                  &s->ckeys, &s->ckeys2, &s->cvals, &s->cvals2, &s->n_ctx, &s->hits, &s->n_hits, &s->hits2};
+    Buf *all[] = SV_ALL_BUFS(s);
     for (Buf *b : all)
-        if (b->p) {
-            (void)hipFree(b->p);
-            grom_dev_note(GROM_DEVCAT_SV, -(int64_t)b->cap);
-        }
+        if (b->p && b->own) grom_dev_free(b->p, b->cap, GROM_DEVCAT_SV);
     if (s->h_hits) (void)hipHostFree(s->h_hits);
     if (s->e0) (void)hipEventDestroy(s->e0);
     if (s->e1) (void)hipEventDestroy(s->e1);

@@ -6,6 +6,8 @@ base), the three whole-chromosome read-depth arrays, and the VCF bytes (with
 ##fileDate pinned; ##reference is the same path for both)."""
 import filecmp
 import os
+import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -793,3 +795,37 @@ def test_device_decode_stats_prefix(datadir, capfd):
     assert got["host"][0] and got["host"][1]
     for mode in modes:
         assert got[mode] == got["host"], mode
+
+
+_FOOT = re.compile(r"buffers: peak ([\d.]+) GB together, per kind scan ([\d.]+), breakpoint ([\d.]+), CNV ([\d.]+), "
+                   r"stages ([\d.]+), decode ([\d.]+) GB; (\d+) allocations waited")
+
+
+def test_hbm_cap_waits_for_memory(datadir):
+    """Running short of device memory does not fail the run (devmem.h): with a
+    test-only cap on this process's device memory (GROM_TEST_HBM_CAP) below
+    what the run holds uncapped -- room for the scan contexts, the decoder and
+    about one and a half input stages -- allocations first free idle stages'
+    blocks and then wait for a scan to give its stage back.  The rows must
+    still be the oracle's."""
+    from _util import FILEDATE, GROM_BIN, SEED
+    case, extra = "c3_genome", ["-M", "-V", "1"]
+    bam, fa, tag = _oracle_once(datadir, case, extra)
+    env = dict(os.environ, GROM_FILEDATE=FILEDATE, GROM_SEED=SEED, GROM_VERBOSE="1")
+
+    def run(out, more):
+        r = subprocess.run([GROM_BIN, "-i", bam, "-r", fa, "-o", out] + extra, env=dict(env, **more),
+                           cwd=str(datadir), capture_output=True, text=True, timeout=150)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        m = _FOOT.search(r.stdout)
+        assert m, r.stdout[-2000:]
+        return [float(x) for x in m.groups()[:6]], int(m.group(7)), r.stdout
+
+    (tot, _, _, _, stages, _), _, _ = run("g_cap_free.vcf", {})
+    cap = (tot - stages + 0.5 * stages) * 1e9
+    (tot2, *_), waits, out = run("g_cap.vcf", {"GROM_TEST_HBM_CAP": str(int(cap)), "GROM_ALLOC_WAIT_S": "40"})
+    reclaimed = int(re.search(r"idle stage blocks reclaimed (\d+)", out).group(1))
+    assert waits + reclaimed > 0, out[-1500:]
+    assert tot2 * 1e9 <= cap * 1.0001
+    for ext in (".vcf", ".ctx.vcf"):
+        assert open(datadir / f"o_{tag}{ext}").read() == open(datadir / f"g_cap{ext}").read()

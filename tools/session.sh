@@ -51,7 +51,7 @@ step_whole() {
   local runs=$1; shift
   ( cd $work
     for r in $(seq 1 $runs); do
-      { time env "$@" GROM_VERBOSE=1 timeout -k 10 180 $repo/grom_amd/bin/grom -i g.bam -r g.fa -o w_$r.vcf $FLAGS \
+      { time env "$@" GROM_VERBOSE=1 GROM_TRACE=$repo/$out/trace_$r.csv timeout -k 10 180 $repo/grom_amd/bin/grom -i g.bam -r g.fa -o w_$r.vcf $FLAGS \
           > $repo/$out/whole_$r.log 2>&1 ; } 2> $repo/$out/whole_$r.time || { tail $repo/$out/whole_$r.log; exit 1; }
       echo "== run $r: $(cat $repo/$out/whole_$r.time)"
       grep -h "decode:\|cli \|footprint\|took" $repo/$out/whole_$r.log
