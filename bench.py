@@ -11,24 +11,32 @@ a BAM + BAI + FASTA by grom_synth, and scanned with `-M -g 1` (the male
 genome: chrY is processed too, so all 24 contigs are scanned).
 
 One step = one whole run of the drop-in CLI (grom_amd/bin/grom) as a fresh
-process: BAM index, parallel BGZF decode on the host's CPU share into pinned
-pieces, host->HBM copies, every chromosome's scan (pileup/SNV, duplicate
-filter, breakpoint evidence and tests, SV/INDEL rows, CTX records, read-depth
-CNV path and rows), the VCF and the translocation post-pass (.ctx.vcf).  The
-BAM sits in the page cache (the first warmup run reads it from disk).
+process: BAM index, each chromosome's compressed BGZF run read ahead into
+pinned memory and copied to HBM, inflated and parsed on the GPU piece by
+piece (ddecode.hip; the insert statistics from the first run's pieces),
+every chromosome's scan (pileup/SNV, duplicate filter, breakpoint evidence
+and tests, SV/INDEL rows, CTX records, read-depth CNV path and rows), the VCF
+and the translocation post-pass (.ctx.vcf).  The BAM sits in the page cache
+(the first warmup run reads it from disk).
 value = genome bases * steps / (time of the steps).
 
 --gpus N (torch.distributed.run, one rank per GPU): the chromosomes are
 assigned longest-processing-time-first to ranks (configs[3]); each rank runs
 its own CLI process on its GPU over its share (GROM_CHROMS: the serial
 stream's plan is kept, so each chromosome gets exactly a one-process run's
-input), with its own decoder threads (the CPU quota split over the ranks);
+input; the insert statistics come from <bam>.mean, which a plan-only run of
+rank 0 writes first, as the reference's -c children load it);
 after a barrier rank 0 joins the shares in chromosome order and runs the
 translocation post-pass over all raw CTX rows (grom_amd.shard.merge_rank_outputs)
 -- inside the timed step.  The step time is the max over ranks.  There is no
 data-path collective: chromosomes are independent.
 
-The JSON line also carries (rank 0, N=1):
+The JSON line also carries:
+  identical_to_oracle_full_scale  the timed run's VCF and .ctx.vcf rows against
+                  the oracle's on the same full-scale genome (sha256 of the
+                  non-header rows, tests/golden/oracle_genome_s100.json);
+  footprint_rank0 the run's peak device memory (the CLI's footprint line);
+and (rank 0, N=1):
   roofline        the pileup kernel (k_scan_tile) in the timed whole runs:
                   algorithmic bytes of every launch (read records, CIGAR,
                   packed bases + qualities, reference, caf arrays)
@@ -83,6 +91,9 @@ C3 = dict(coverage=30.0, dup_frac=0.05, sv_per_mb=2200 / 3088.3, cnv_rate=500 / 
 C2 = dict(coverage=30.0, dup_frac=0.0, sv_per_mb=0.0, cnv_rate=0.0, cnv_range=(0, 0), seed=2)
 GENOME_FLAGS = ["-M", "-g", "1"]
 
+FOOTPRINT = re.compile(r"^footprint: peak ([\d.]+) GB of device memory \(([^)]*)\).*buffers: peak ([\d.]+) GB together.*"
+                       r"; (\d+) allocations waited ([\d.]+) s")
+ORACLE_FULL = os.path.join(REPO, "tests", "golden", "oracle_genome_s100.json")
 CHROM_LINE = re.compile(r"^(\S+): (\d+) reads, ([\d.]+) ms on GPU .*; pileup ([\d.]+) ms, cnv ([\d.]+) ms, "
                         r"cigar_ops (\d+), bases (\d+), len (\d+)$")
 
@@ -182,6 +193,30 @@ def chrom_stats(stdout):
                                    ms_cnv=float(m.group(5)), cigar_ops=int(m.group(6)), bases=int(m.group(7)),
                                    len=int(m.group(8)))
     return out
+
+
+def footprint(stdout):
+    """the CLI's footprint line (GROM_VERBOSE): peak device memory of the run"""
+    for line in stdout.splitlines():
+        m = FOOTPRINT.match(line)
+        if m:
+            return {"peak_gb": float(m.group(1)), "measured_as": m.group(2), "buffers_peak_gb": float(m.group(3)),
+                    "allocations_waited": int(m.group(4)), "wait_s": float(m.group(5))}
+    return None
+
+
+def oracle_full_scale(vcf, ctx):
+    """The timed whole run's rows against the oracle's at the same full-scale
+    workload (tests/golden/oracle_genome_s100.json, tools/make_golden_genome.py:
+    the oracle, one thread, about three hours in the build container)."""
+    if not os.path.exists(ORACLE_FULL):
+        return None
+    g = json.load(open(ORACLE_FULL))
+    nv, dv = rows_digest(vcf)
+    nc, dc = rows_digest(ctx)
+    return {"identical": (nv, dv, nc, dc) == (g["vcf_rows"], g["vcf_rows_sha256"], g["ctx_rows"], g["ctx_rows_sha256"]),
+            "vcf_rows": nv, "ctx_rows": nc, "oracle_vcf_rows": g["vcf_rows"], "oracle_ctx_rows": g["ctx_rows"],
+            "oracle_seconds": g.get("oracle_seconds"), "golden": os.path.relpath(ORACLE_FULL, REPO)}
 
 
 def rows_digest(path):
@@ -434,16 +469,19 @@ def main():
         log(f"warmup run {w + 1}: {dt:.2f} s")
     barrier()
     t0 = time.perf_counter()
-    runs, last = [], ""
+    runs, last, run_out = [], "", []
     for k in range(args.steps):
         t1 = time.perf_counter()
         _, last = step()
         runs.append(time.perf_counter() - t1)
+        run_out.append(last)
         log(f"timed run {k + 1}: {runs[-1]:.2f} s")
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, device="cuda")
     value = total * args.steps / dt / 1e6
     stats = chrom_stats(last)  # this rank's chromosomes, last timed run
+    feet = [footprint(so) for so in run_out]
+    feet = [f for f in feet if f]
     dec = [ln for ln in last.splitlines() if ln.startswith(("streamed decode:", "device decode:"))]
     phases = [ln for ln in last.splitlines() if ln.startswith("cli phases")]
 
@@ -468,7 +506,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             with tempfile.TemporaryDirectory() as d:
                 cpu, conc = cpu_baseline_and_concordance(d, knobs, flags)
-        n_rows, _ = rows_digest(out if world == 1 else os.path.join(work, "merged.vcf"))
+        final_vcf = out if world == 1 else os.path.join(work, "merged.vcf")
+        n_rows, _ = rows_digest(final_vcf)
+        full = (oracle_full_scale(final_vcf, final_vcf[:-4] + ".ctx.vcf")
+                if genome and args.scale == 1.0 else None)
         wl = ("BASELINE configs[2]: synthetic 30x 2x150 bp human-shape genome, 24 GRCh38 contigs "
               f"({total / 1e9:.3f} Gb), SNV/indel, {knobs['sv_per_mb']:.2f} breakpoint SVs/Mb "
               "(DEL/DUP/INV/INS/CTX with split reads + discordant pairs), 500 CNVs/3.1 Gb, 5% PCR duplicates, "
@@ -504,7 +545,14 @@ def main():
                 "reads_rank0": sum(s["reads"] for s in stats.values()),
                 "pileup_ms_rank0": round(sum(s["ms_pileup"] for s in stats.values()), 1),
                 "cnv_ms_rank0": round(sum(s["ms_cnv"] for s in stats.values()), 1),
+                "footprint_rank0": {"peak_gb_max": max(f["peak_gb"] for f in feet),
+                                    "buffers_peak_gb_max": max(f["buffers_peak_gb"] for f in feet),
+                                    "measured_as": feet[0]["measured_as"],
+                                    "allocations_waited": sum(f["allocations_waited"] for f in feet),
+                                    "wait_s": round(sum(f["wait_s"] for f in feet), 3)} if feet else None,
             },
+            "identical_to_oracle_full_scale": full["identical"] if full else None,
+            "oracle_full_scale": full,
             "roofline": roofline_of(launches, alone) if launches else None,
             "cpu_baseline": cpu,
             "concordance": conc,

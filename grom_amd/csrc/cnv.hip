@@ -2400,10 +2400,69 @@ __global__ __launch_bounds__(64) void k_cnv_walk_resume(WalkIn W, const int32_t 
 // in cs[k].status whether it met one (ST_MERGED) or walked the chunk to its
 // end (ST_NOMERGE, exit in x2/l2)
 template <int KIND>
+__device__ __forceinline__ void walk_fix(WalkIn W, const int32_t *nxt, const PreAB *pre, int64_t k, int64_t chunk,
+                                         int64_t x, int l, uint8_t *__restrict__ vis, ChunkState *__restrict__ cs,
+                                         CallRec *calls, uint32_t *n_calls, uint32_t cap);
+
+template <int KIND>
 __global__ __launch_bounds__(64) void k_cnv_walk_fix(WalkIn W, const int32_t *nxt, const PreAB *pre, int64_t k,
                                                      int64_t chunk, int64_t x, int l, uint8_t *__restrict__ vis,
                                                      ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
                                                      uint32_t cap) {
+    walk_fix<KIND>(W, nxt, pre, k, chunk, x, l, vis, cs, calls, n_calls, cap);
+}
+
+// The reconcile of the chunked walk on the device (one wave): the true exit
+// of each chunk in order -- GROM.c's walk is one pass -- repairing (walk_fix)
+// a chunk whose speculative entry was wrong and marking the chunks the true
+// walk jumps over (skipped[k] = 1).  The host reconcile it replaces read every
+// chunk state back and waited for each repair; here one launch does them all.
+template <int KIND>
+__global__ __launch_bounds__(64) void k_cnv_reconcile(WalkIn W, const int32_t *nxt, const PreAB *pre, int64_t n_ch,
+                                                      int64_t chunk, uint8_t *__restrict__ vis,
+                                                      ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
+                                                      uint32_t cap, uint8_t *__restrict__ skipped,
+                                                      uint32_t *__restrict__ n_fix) {
+    __shared__ ChunkState s_prev, s_cur;
+    if (threadIdx.x == 0) s_prev = cs[0];
+    for (int64_t k = threadIdx.x; k < n_ch; k += 64) skipped[k] = 0;
+    __syncthreads();
+    int64_t tx = s_prev.x1;
+    int tl = s_prev.l1;
+    uint32_t fixes = 0;
+    for (int64_t k = 1; k < n_ch; k++) {
+        if (threadIdx.x == 0) s_cur = cs[k];
+        __syncthreads();
+        const ChunkState h = s_cur, hp = s_prev;  // (the fix of chunk k writes only its own state)
+        __syncthreads();
+        if (threadIdx.x == 0) s_prev = h;
+        const bool entry_ok = tx == hp.x1 && tl == hp.l1;
+        const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
+        const int64_t ex = h.status == ST_NOMERGE ? h.x2 : h.x1;
+        const int el = h.status == ST_NOMERGE ? h.l2 : h.l1;
+        if (entry_ok && h.status != ST_PASSTHRU) { tx = ex; tl = el; continue; }
+        if (tx >= c1) {  // the true walk jumps over this chunk
+            if (threadIdx.x == 0) skipped[k] = 1;
+            continue;
+        }
+        walk_fix<KIND>(W, nxt, pre, k, chunk, tx, tl, vis, cs, calls, n_calls, cap);
+        fixes++;
+        __threadfence_block();
+        __syncthreads();
+        if (threadIdx.x == 0) s_cur = cs[k];
+        __syncthreads();
+        const ChunkState one = s_cur;
+        __syncthreads();
+        if (one.status == ST_MERGED && h.status != ST_PASSTHRU) { tx = ex; tl = el; }
+        else { tx = one.x2; tl = one.l2; }
+    }
+    if (threadIdx.x == 0) *n_fix = fixes;
+}
+
+template <int KIND>
+__device__ __forceinline__ void walk_fix(WalkIn W, const int32_t *nxt, const PreAB *pre, int64_t k, int64_t chunk,
+                                         int64_t x, int l, uint8_t *__restrict__ vis, ChunkState *__restrict__ cs,
+                                         CallRec *calls, uint32_t *n_calls, uint32_t cap) {
     if (W.stats) W.stats += 10;  // the repair walks' own counters (GROM_TIMING)
     const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
     int64_t merge;
@@ -4148,36 +4207,18 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 else
                     hipLaunchKernelGGL(k_cnv_walk<1>, dim3(gch), dim3(64), 0, st, WK, nxt, pre, 1, n_ch, WALK_CHUNK, vis, dcs, pend, dcalls, n_calls, call_cap);
                 CK(hipGetLastError());
-                CK(hipMemcpyAsync(hcs.data(), dcs, sizeof(ChunkState) * n_ch, hipMemcpyDeviceToHost, st));
-                CK(hipStreamSynchronize(st));
-                std::vector<uint8_t> skipped((size_t)n_ch, 0);
-                // reconcile: the true exit of each chunk, in order (GROM.c's walk is one pass)
-                int64_t tx = hcs[0].x1;
-                int tl_ = hcs[0].l1;
+                // reconcile (k_cnv_reconcile, one wave): the true exit of each
+                // chunk in order, repairs, the chunks the walk jumps over
+                if ((rc = grow(K.skip, (size_t)n_ch, err, errlen))) return rc;
+                uint32_t *d_nfix = n_calls + 8;  // (a free word of the counters, byte 32)
+                if (kind == 0)
+                    hipLaunchKernelGGL(k_cnv_reconcile<0>, dim3(1), dim3(64), 0, st, WK, nxt, pre, n_ch, WALK_CHUNK, vis, dcs,
+                                       dcalls, n_calls, call_cap, (uint8_t *)K.skip.p, d_nfix);
+                else
+                    hipLaunchKernelGGL(k_cnv_reconcile<1>, dim3(1), dim3(64), 0, st, WK, nxt, pre, n_ch, WALK_CHUNK, vis, dcs,
+                                       dcalls, n_calls, call_cap, (uint8_t *)K.skip.p, d_nfix);
+                CK(hipGetLastError());
                 int64_t n_fix = 0;
-                for (int64_t k = 1; k < n_ch; k++) {
-                    const bool entry_ok = tx == hcs[k - 1].x1 && tl_ == hcs[k - 1].l1;
-                    const int64_t c0 = WK.start + k * WALK_CHUNK, c1 = std::min<int64_t>(WK.end, c0 + WALK_CHUNK);
-                    // the exit of the walk whose marks this chunk holds after its mode-1 pass
-                    const int64_t ex = hcs[k].status == ST_NOMERGE ? hcs[k].x2 : hcs[k].x1;
-                    const int el = hcs[k].status == ST_NOMERGE ? hcs[k].l2 : hcs[k].l1;
-                    if (entry_ok && hcs[k].status != ST_PASSTHRU) { tx = ex; tl_ = el; continue; }
-                    if (tx >= c1) {  // the true walk jumps over this chunk
-                        skipped[k] = 1;
-                        continue;
-                    }
-                    if (kind == 0)
-                        hipLaunchKernelGGL(k_cnv_walk_fix<0>, dim3(1), dim3(64), 0, st, WK, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
-                    else
-                        hipLaunchKernelGGL(k_cnv_walk_fix<1>, dim3(1), dim3(64), 0, st, WK, nxt, pre, k, WALK_CHUNK, tx, tl_, vis, dcs, dcalls, n_calls, call_cap);
-                    CK(hipGetLastError());
-                    ChunkState one;
-                    CK(hipMemcpyAsync(&one, dcs + k, sizeof(ChunkState), hipMemcpyDeviceToHost, st));
-                    CK(hipStreamSynchronize(st));
-                    n_fix++;
-                    if (one.status == ST_MERGED && hcs[k].status != ST_PASSTHRU) { tx = ex; tl_ = el; }
-                    else { tx = one.x2; tl_ = one.l2; }
-                }
                 if (tmg) {
                     uint32_t np_[3] = {0, 0, 0};
                     (void)hipMemcpy(np_, n_pre, 12, hipMemcpyDeviceToHost);
@@ -4203,12 +4244,13 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                             kind == 0 ? "DEL" : "DUP", (long long)n_ch, (long long)n_fix, ncand, np_[0], np_[2], ws[4],
                             ws[0], ws[1], ws[2], ws[3]);
                 }
-                uint32_t nc = 0;
-                CK(hipMemcpyAsync(&nc, n_calls, 4, hipMemcpyDeviceToHost, st));
+                // n_calls, n_pre (adjacent) and the repairs in one copy
+                uint32_t hn[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                CK(hipMemcpyAsync(hn, n_calls, sizeof(hn), hipMemcpyDeviceToHost, st));
                 CK(hipStreamSynchronize(st));
-                uint32_t npre = 0;
-                CK(hipMemcpyAsync(&npre, n_pre, 4, hipMemcpyDeviceToHost, st));
-                CK(hipStreamSynchronize(st));
+                const uint32_t nc = hn[0], npre = hn[1];
+                n_fix = hn[8];
+                (void)n_fix;
                 if (npre > pre_cap || nc > call_cap) {
                     pre_cap = std::max(pre_cap, npre + npre / 4 + 1024);
                     call_cap = std::max(call_cap, nc + nc / 4 + 1024);
@@ -4218,8 +4260,6 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 std::vector<CallRec> hc(nc);
                 std::vector<uint8_t> ok(nc);
                 if (nc) {
-                    if ((rc = grow(K.skip, (size_t)n_ch, err, errlen))) return rc;
-                    CK(hipMemcpyAsync(K.skip.p, skipped.data(), (size_t)n_ch, hipMemcpyHostToDevice, st));
                     hipLaunchKernelGGL(k_cnv_calls_valid, dim3((nc + 255) / 256), dim3(256), 0, st, dcalls, nc, vis,
                                        (const uint8_t *)K.skip.p, WK.start, WALK_CHUNK, (uint8_t *)K.ok.p);
                     CK(hipMemcpyAsync(hc.data(), dcalls, sizeof(CallRec) * nc, hipMemcpyDeviceToHost, st));

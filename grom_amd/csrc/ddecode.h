@@ -44,43 +44,50 @@ void dd_ctx_free(dd_ctx *c);
 void dd_ctx_times(const dd_ctx *c, double ms[4]);
 /* record-walk sub-chunks whose guessed start was wrong (re-walked) / all */
 void dd_ctx_counts(const dd_ctx *c, int64_t *rewalked, int64_t *subchunks);
-/* the per-run device buffers sized for a run of `ubytes` inflated bytes,
- * `recs` records and `n_starts` index-named record starts, in run slots
- * 0..n_slots-1 (growth later frees buffers, which waits for the device) */
-int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, int n_slots, char *err, int errlen);
+/* the device buffers sized for the largest run (`ubytes` inflated bytes, a
+ * compressed span of `span`, `recs` records, `n_starts` index-named record
+ * starts): the two piece slots and the chromosome-wide name arrays (growth
+ * later frees buffers, which waits for the device) */
+int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs, int64_t n_starts, char *err, int errlen);
 /* a run's compressed bytes (h_comp pinned, 64 readable bytes past comp_len)
  * copied into device slot 0/1 on the context's copy stream; returns at once,
- * h_comp must stay untouched until a dd_run_load of the slot has returned */
+ * h_comp must stay untouched until a dd_run_decode of the slot has returned */
 int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_t comp_len, char *err, int errlen);
-/* inflate a run's blocks (uploaded to `slot`; h_blk its block table, ubytes
- * the inflated size) into run slot `rslot` and find its records from the
- * record starts h_starts (offsets into the inflated stream, the first being
- * the run's first record) up to u_end: *n_rec records (tid: the run's target,
- * for the record-start guesses).  Runs on the run slot's own stream and
- * returns with the work done, so a second thread may load one run slot while
- * the context parses the other.  0; -2 when the data contradicts the index
- * plan (the CLI then reads serially); -1 */
-int dd_run_load(dd_ctx *c, int slot, int rslot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
-                int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int32_t tid, int64_t *n_rec,
-                char *err, int errlen);
-/* find_insert_mean's sample from every record of the run in run slot rslot
- * (file order): at most cap_left (insert, l_qseq) pairs into h_ins/h_lq, the
- * mapped-bases sum up to the pair that completes the cap (or over the run) */
-int dd_run_stats(dd_ctx *c, int rslot, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq,
-                 int64_t *n_taken, int64_t *m_contrib, char *err, int errlen);
 typedef struct dd_parse_out {
     int64_t n_rec, n_kept, n_drop, n_cig, n_bases, n_auxc;
     int32_t last_pos, last_lq, last_hclip, last_kept;
-    /* the split-read candidates (host, valid until the next parse): record
+    /* the split-read candidates (host, valid until the next run): record
      * bytes (block_size first) at aux_bytes + aux_off[a], kept index aux_kidx[a] */
     const uint8_t *aux_bytes;
     const int64_t *aux_off, *aux_kidx;
 } dd_parse_out;
-/* the records j0.. of the run in run slot rslot parsed into `stage`
- * (grom_stage_fill_begin): every array of the chromosome, untrimmed, aux_idx
- * all -1 */
-int dd_run_parse(dd_ctx *c, int rslot, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len, grom_stage *stage,
-                 dd_parse_out *out, char *err, int errlen);
+/* one run on the device, piece by piece (~GROM_DD_PIECE_MB of inflated bytes,
+ * whole record-start chunks): inflate, record walk, the insert statistics'
+ * sample while stats_left > 0 (file order; stats_cb after each piece with
+ * what it took), and with a stage the records j0.. parsed into it: every
+ * array of the chromosome, untrimmed, aux_idx all -1 */
+typedef struct dd_run_req {
+    int slot;                 /* the compressed bytes' device slot (dd_comp_upload) */
+    int64_t comp_len;
+    const DdBlock *blk;       /* the run's BGZF blocks (host) */
+    int64_t nblk;
+    const int64_t *starts;    /* record starts in the inflated run: its first record, then the index's */
+    int64_t n_starts, u_end;  /* ... and the run's end */
+    int32_t tid;              /* the run's target (record-start guesses, the record check) */
+    int64_t j0;               /* the run's first record to take */
+    int32_t read_name_len;
+    int64_t ref_len;
+    int64_t count;            /* the index's record count for the run (-1: unknown): sizes the stage */
+    grom_stage *stage;        /* NULL: the insert statistics only */
+    int64_t stats_left;       /* insert-size pairs still wanted (0: none) */
+    int32_t min_mapq;
+    int32_t *h_ins, *h_lq;    /* the sample continues here */
+    void (*stats_cb)(void *arg, int64_t taken, int64_t m_contrib, int complete);
+    void *stats_arg;
+} dd_run_req;
+/* 0; -2 when the data contradicts the index plan (the CLI then reads
+ * serially); -1.  *n_rec: the records walked (all of the run's with a stage) */
+int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *out, int64_t *n_rec, char *err, int errlen);
 /* n <= 512 bytes of device memory to the host after the context's work */
 int dd_copy_d2h(dd_ctx *c, void *dst, const void *src, size_t n);
 /* kept reads and dropped records at positions below s0 (the walk's skip
@@ -106,6 +113,11 @@ int64_t grom_stage_held(const grom_stage *s);
 /* a stage holding exactly sz's counts (n_aux = capacity, the count starts at
  * 0), its device arrays in *dev (writable); waits for its earlier copies */
 int grom_stage_fill_begin(grom_stage *s, const grom_stage_sizes *sz, grom_reads *dev);
+/* the piece-wise decode: room for `need` in every array keeping the first
+ * `have` entries (earlier pieces), the device arrays in *dev; then the final
+ * counts (grom_stage_fill_set) */
+int grom_stage_fill_ensure(grom_stage *s, const grom_stage_sizes *need, const grom_stage_sizes *have, grom_reads *dev);
+int grom_stage_fill_set(grom_stage *s, const grom_stage_sizes *sz);
 /* n split-read alignments: aux[k] for kept read kidx[k] (host arrays) */
 int grom_stage_put_aux(grom_stage *s, const grom_aux *aux, const int64_t *kidx, int64_t n);
 /* drop the first sd dropped records and count kept reads after the first sk */

@@ -24,25 +24,31 @@
 #define DD_SLOTS 2
 
 // One BGZF block per lane: blk[j] = {offset of its DEFLATE data in `comp`,
-// its length, offset of its output in `out`, ISIZE}.  status[j] = GI_* code.
+// its length, offset of its output, ISIZE}; the output goes to out +
+// (out_off - out_base) (a piece of a run: out holds the piece).  status[j] =
+// GI_* code.
 __global__ void __launch_bounds__(DD_LANES, 2) k_inflate(const uint8_t *__restrict__ comp, const DdBlock *__restrict__ blk,
-                                                      int64_t n_blk, uint8_t *__restrict__ out,
-                                                      uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad) {
+                                                      int64_t n_blk, uint8_t *__restrict__ out, int64_t out_base,
+                                                      uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad,
+                                                      int hdr_batch) {
     extern __shared__ uint32_t dd_tab[];  // GI_LANE_DWORDS x DD_LANES: rows element-major across the lanes
     const int64_t j = (int64_t)blockIdx.x * DD_LANES + threadIdx.x;
     if (j >= n_blk) return;
     const DdBlock b = blk[j];
-    const int rc = gi_inflate<DD_LANES>(comp + b.in_off, b.in_len, out + b.out_off, b.out_len, dd_tab, threadIdx.x);
+    const int rc = gi_inflate<DD_LANES>(comp + b.in_off, b.in_len, out + (b.out_off - out_base), b.out_len, dd_tab,
+                                        threadIdx.x, hdr_batch);
     status[j] = (uint8_t)rc;
     if (rc) atomicAdd(n_bad, 1u);
 }
 
 extern "C" int dd_inflate_launch(hipStream_t st, const uint8_t *d_comp, const DdBlock *d_blk, int64_t n_blk,
-                                 uint8_t *d_out, uint8_t *d_status, uint32_t *d_bad) {
+                                 uint8_t *d_out, int64_t out_base, uint8_t *d_status, uint32_t *d_bad) {
     if (n_blk <= 0) return 0;
     const unsigned grid = (unsigned)((n_blk + DD_LANES - 1) / DD_LANES);
+    // GROM_INFLATE_BATCH: header-trip batching (inflate.h), lanes per header trip
+    static const int batch = getenv("GROM_INFLATE_BATCH") ? atoi(getenv("GROM_INFLATE_BATCH")) : 0;
     hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES, st, d_comp, d_blk,
-                       n_blk, d_out, d_status, d_bad);
+                       n_blk, d_out, out_base, d_status, d_bad, batch);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -138,7 +144,7 @@ extern "C" int64_t grom_inflate_device_selftest(const char *bam_path, int device
         // a warm launch, then the timed one
         for (int rep = 0; rep < 2; rep++) {
             (void)hipEventRecord(e0, st);
-            if (dd_inflate_launch(st, d_comp, d_blk, nb, d_out, d_status, d_bad)) goto done;
+            if (dd_inflate_launch(st, d_comp, d_blk, nb, d_out, 0, d_status, d_bad)) goto done;
             (void)hipEventRecord(e1, st);
         }
         if (hipStreamSynchronize(st) != hipSuccess) goto done;
@@ -217,7 +223,7 @@ struct DBuf {
 
 std::atomic<int64_t> g_dgrow_ns{0};  // time in buffer growth (hipFree + hipMalloc), all contexts and stages
 
-int dgrow(DBuf &b, size_t bytes) {
+int dgrow(DBuf &b, size_t bytes, const char *what = nullptr) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return 0;
     const auto t0 = std::chrono::steady_clock::now();
@@ -231,7 +237,7 @@ int dgrow(DBuf &b, size_t bytes) {
     const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     g_dgrow_ns += ns;
     if (ns > 20000000 && getenv("GROM_VERBOSE"))
-        fprintf(stderr, "grom: device buffer of %.2f GB took %.1f ms\n", (double)want / 1e9, ns / 1e6);
+        fprintf(stderr, "grom: device buffer %s of %.3f GB took %.1f ms\n", what ? what : "", (double)want / 1e9, ns / 1e6);
     if (e != 0) return -1;
     b.cap = want;
     return 0;
@@ -240,7 +246,8 @@ int dgrow(DBuf &b, size_t bytes) {
 template <class T> T *P(DBuf &b) { return (T *)b.p; }
 
 // bad-state bits
-enum : uint32_t { DB_INFLATE = 1, DB_CHAIN = 2, DB_RECORD = 4, DB_TID = 8, DB_UNSORTED = 16, DB_NAMES = 32 };
+enum : uint32_t { DB_INFLATE = 1, DB_CHAIN = 2, DB_RECORD = 4, DB_TID = 8, DB_UNSORTED = 16, DB_NAMES = 32,
+                  DB_OFFCAP = 64 };
 
 __device__ __forceinline__ uint32_t ldu32(const uint8_t *U, int64_t o) {
     return (uint32_t)U[o] | (uint32_t)U[o + 1] << 8 | (uint32_t)U[o + 2] << 16 | (uint32_t)U[o + 3] << 24;
@@ -356,15 +363,16 @@ __device__ __forceinline__ int64_t ws_guess(const uint8_t *U, int64_t lo, int64_
     return -1;
 }
 
-// walk from o while o < hi: records counted (and written from *w when off)
-// and the exit; -1 exit for a block_size outside the record limits
+// walk from o while o < hi: records counted (and written from *w when off,
+// below off_cap) and the exit; -1 exit for a block_size outside the record
+// limits
 __device__ __forceinline__ int64_t ws_walk(const uint8_t *U, int64_t o, int64_t hi, uint32_t &n, int64_t *off,
-                                           int64_t w) {
+                                           int64_t w, int64_t off_cap = INT64_MAX) {
     n = 0;
     while (o < hi) {
         const int32_t bs = ld_bs(U, o);
         if (bs < 32 || bs > DD_MAX_REC) return -1;
-        if (off) off[w + n] = o;
+        if (off && w + n < off_cap) off[w + n] = o;
         o += 4 + (int64_t)bs;
         n++;
     }
@@ -374,10 +382,10 @@ __device__ __forceinline__ int64_t ws_walk(const uint8_t *U, int64_t o, int64_t 
 // one workgroup per chunk [S[c], S[c+1]): counts per chunk (off == nullptr) or
 // the record offsets from base[c] on
 __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U, const int64_t *__restrict__ S,
-                                                   int64_t n_chunks, int32_t tid, int guess,
+                                                   int64_t sbase, int64_t n_chunks, int32_t tid, int guess,
                                                    uint32_t *__restrict__ q0_stats, uint32_t *__restrict__ cnt,
                                                    const uint32_t *__restrict__ base, int64_t *__restrict__ off,
-                                                   uint32_t *__restrict__ bad) {
+                                                   uint32_t *__restrict__ bad, int64_t off_cap = INT64_MAX) {
     __shared__ int64_t s_start[WS_T], s_exit[WS_T];
     __shared__ uint32_t s_n[WS_T], s_pre[WS_T];
     __shared__ int64_t s_carry;
@@ -386,7 +394,7 @@ __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U
     const int64_t c = blockIdx.x;
     if (c >= n_chunks) return;
     const int t = threadIdx.x;
-    const int64_t c0 = S[c], c1 = S[c + 1];
+    const int64_t c0 = S[c] - sbase, c1 = S[c + 1] - sbase;  // chunk bounds in U (a piece from sbase on)
     const int64_t nsub = c1 > c0 ? (c1 - c0 + WS_G - 1) / WS_G : 0;
     if (t == 0) { s_carry = c0; s_total = 0; s_fail = 0; }
     __syncthreads();
@@ -436,8 +444,9 @@ __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U
         __syncthreads();
         if (off && q < nsub && s_n[t]) {
             uint32_t n2 = 0;
-            ws_walk(U, s_start[t], c0 + q * WS_G + WS_G < c1 ? c0 + q * WS_G + WS_G : c1, n2, off,
-                    (int64_t)base[c] + s_pre[t]);
+            const int64_t w0 = (int64_t)base[c] + s_pre[t];
+            ws_walk(U, s_start[t], c0 + q * WS_G + WS_G < c1 ? c0 + q * WS_G + WS_G : c1, n2, off, w0, off_cap);
+            if (w0 + n2 > off_cap) atomicOr(bad, DB_OFFCAP);
         }
         __syncthreads();
     }
@@ -483,7 +492,7 @@ __device__ bool has_split_tag(const uint8_t *U, int64_t s, int64_t end) {
 __global__ void k_rec_meta(const uint8_t *__restrict__ U, const int64_t *__restrict__ off, int64_t R, int64_t j0,
                            int32_t tid, uint32_t *__restrict__ keep, uint32_t *__restrict__ drop,
                            uint32_t *__restrict__ auxc, uint32_t *__restrict__ ncig, int64_t *__restrict__ nb,
-                           int32_t *__restrict__ rpos, uint32_t *__restrict__ bad) {
+                           uint32_t *__restrict__ nml, int32_t *__restrict__ rpos, uint32_t *__restrict__ bad) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
         const int64_t o = off[r];
         RecHdr h;
@@ -501,6 +510,7 @@ __global__ void k_rec_meta(const uint8_t *__restrict__ U, const int64_t *__restr
         drop[r] = in && dropped;
         ncig[r] = k ? (uint32_t)nc : 0u;
         nb[r] = k ? (((int64_t)lq + 1) & ~1LL) : 0;
+        nml[r] = k ? (uint32_t)lqn : 0u;
         bool cand = false;
         if (k) {
             const int64_t data = o + 36, end = o + 4 + h.bs();
@@ -551,42 +561,40 @@ __device__ __forceinline__ int name_hash(const uint8_t *U, int64_t p, int lqn, u
     return L;
 }
 
-// names at a and b equal up to their NUL (or lqn bytes of a)
-__device__ __forceinline__ bool name_equal(const uint8_t *U, int64_t a, int64_t b, int lqn) {
-    for (int base = 0; base < 256; base += 32) {
-        uint32_t x[8], y[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) { x[k] = ldu32a(U, a + base + 4 * k); y[k] = ldu32a(U, b + base + 4 * k); }
-#pragma unroll
-        for (int k = 0; k < 32; k++) {
-            const uint32_t cx = (x[k >> 2] >> (8 * (k & 3))) & 0xffu, cy = (y[k >> 2] >> (8 * (k & 3))) & 0xffu;
-            if (cx != cy) return false;
-            if (cx == 0 || base + k + 1 >= lqn) return true;
-        }
-    }
-    return true;
-}
+// What the pieces of a run before this one wrote: the offsets a piece's own
+// exclusive scans start from in the chromosome's arrays, and the last
+// record's position (the sort check across the piece boundary)
+struct Carry {
+    int64_t k, d, cig, b, nm;  // kept reads, dropped records, CIGAR words, bases, name bytes
+    int32_t prev_pos;          // position of the record before the piece (unset: the piece starts the run)
+    int32_t has_prev;
+};
 
-// the kept reads' fields, CIGAR words and name hashes; the dropped records;
-// the split-read candidates' record indices; the stream's last record
+// the kept reads' fields, CIGAR words, names (into the chromosome's name
+// bytes) and name hashes; the dropped records; the split-read candidates'
+// record indices; the piece's last record.  r is a record of the piece (its
+// offset off[r] in U), j0 the run's first record to take, relative to the
+// piece (negative: the piece starts past it).
 __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__restrict__ off, int64_t R, int64_t j0,
                             const uint32_t *__restrict__ keep, const uint32_t *__restrict__ kidx,
                             const uint32_t *__restrict__ drop, const uint32_t *__restrict__ didx,
                             const uint32_t *__restrict__ auxc, const uint32_t *__restrict__ aidx,
                             const uint32_t *__restrict__ coff_s, const int64_t *__restrict__ boff_s,
-                            const int32_t *__restrict__ rpos, StageOut so, int64_t *__restrict__ krec,
-                            int64_t *__restrict__ srcs,
+                            const uint32_t *__restrict__ nmo_s, const int32_t *__restrict__ rpos, StageOut so, Carry car,
+                            int64_t *__restrict__ srcs, uint8_t *__restrict__ nm, int64_t *__restrict__ nmoff,
                             uint64_t *__restrict__ keys, uint32_t *__restrict__ vals, int64_t *__restrict__ acand,
                             int32_t read_name_len, int32_t *__restrict__ last, uint32_t *__restrict__ bad) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
-        if (r > j0 && rpos[r] < rpos[r - 1]) atomicOr(bad, DB_UNSORTED);
+        if (r > j0 && (r > 0 ? rpos[r] < rpos[r - 1] : (car.has_prev && rpos[0] < car.prev_pos)))
+            atomicOr(bad, DB_UNSORTED);
         const int64_t o = off[r];
         RecHdr h;
         load_hdr(U, o, h);
         int32_t hc = 0;
         const int lqn = h.l_qname(), nc = h.n_cigar();
         if (keep[r]) {
-            const uint32_t i = kidx[r];
+            const int64_t i = car.k + kidx[r];
+            const int64_t cg0 = car.cig + coff_s[r];
             so.pos[i] = h.pos();
             so.flag[i] = (uint16_t)h.flag();
             so.mapq[i] = (uint8_t)h.mapq();
@@ -594,30 +602,34 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
             so.mpos[i] = h.mpos();
             so.isize[i] = h.isz();
             so.lq[i] = h.lq();
-            so.coff[i] = coff_s[r];
-            so.boff[i] = boff_s[r];
+            so.coff[i] = (uint32_t)cg0;
+            so.boff[i] = car.b + boff_s[r];
             so.aidx[i] = -1;
-            krec[i] = r;
-            srcs[i] = o + 36 + lqn + 4 * (int64_t)nc;  // the packed bases in U (the qualities follow)
+            srcs[kidx[r]] = o + 36 + lqn + 4 * (int64_t)nc;  // the packed bases in U (the qualities follow)
             const int64_t cg = o + 36 + lqn;
             for (int c = 0; c < nc; c++) {
                 const uint32_t op = ldu32(U, cg + 4 * c);
-                so.cig[coff_s[r] + c] = op;
+                so.cig[cg0 + c] = op;
                 if ((op & 15u) == GC_HARD_CLIP) hc += (int32_t)(op >> 4);
             }
+            // the name's bytes (l_qname, its NUL included) for the id check
+            // after the last piece (k_name_ids)
+            const int64_t nb0 = car.nm + nmo_s[r];
+            nmoff[i] = nb0;
+            for (int c = 0; c < lqn; c++) nm[nb0 + c] = U[o + 36 + c];
             // name: up to its NUL (pdecode.c buf_intern); empty or >= read_name_len: id 0 (GROM.c:6813)
             uint64_t hs = 0;
             const int L = name_hash(U, o + 36, lqn, hs);
             keys[i] = (L == 0 || L >= read_name_len) ? 0ull : (mix64(hs ^ (uint64_t)L * 0x9e3779b97f4a7c15ULL) | 1ull);
-            vals[i] = i;
+            vals[i] = (uint32_t)i;
             if (auxc[r]) acand[aidx[r]] = r;
         } else if (drop[r]) {
-            const uint32_t d = didx[r];
+            const int64_t d = car.d + didx[r];
             so.dpos[d] = h.pos();
             so.dlq[d] = h.lq();
-            so.dbef[d] = (int64_t)kidx[r];  // kept reads before it (exclusive scan)
+            so.dbef[d] = car.k + (int64_t)kidx[r];  // kept reads before it (exclusive scan)
         }
-        if (r == R - 1) {  // the stream's last record: position, length, hard clips, kept
+        if (r == R - 1) {  // the piece's last record: position, length, hard clips, kept
             if (!keep[r]) {
                 const int64_t cg = o + 36 + lqn;
                 for (int c = 0; c < nc; c++) {
@@ -642,16 +654,22 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
 #define CP_J (CP_T / 1024)
 #define CP_R 1024   // reads a tile may touch, staged in LDS (more: the tile reads them from global memory)
 
-// the read holding each tile's first destination byte: read i's region of
-// qualities is [b, b + nb) and of bases [b/2, b/2 + nb/2) (b = boff[i], nb =
-// l_qseq rounded up to even); tiles start every CP_T bytes
-__global__ void k_tile_first(const int64_t *__restrict__ boff, const int32_t *__restrict__ lq, int64_t n,
-                             int64_t *__restrict__ tfq, int64_t *__restrict__ tfs) {
+// the read holding each tile's first destination byte, for the tiles of one
+// piece: its reads are kept reads k0.. (n of them) whose regions fill the
+// destination [lo, hi) of the qualities and [lo/2, hi/2) of the packed bases
+// (read i's qualities [b, b + nb), bases [b/2, b/2 + nb/2), b = boff[i], nb =
+// l_qseq rounded up to even); tile t (every CP_T bytes) is entry t - lo /
+// CP_T, read indices relative to k0; entry 0 (a tile that starts before the
+// piece) is the piece's first read
+__global__ void k_tile_first(const int64_t *__restrict__ boff, const int32_t *__restrict__ lq, int64_t k0, int64_t n,
+                             int64_t lo, int64_t *__restrict__ tfq, int64_t *__restrict__ tfs) {
+    const int64_t tq0 = lo / CP_T, ts0 = (lo / 2) / CP_T;
+    if (blockIdx.x == 0 && threadIdx.x == 0) tfq[0] = tfs[0] = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t b = boff[i], nb = ((int64_t)lq[i] + 1) & ~1LL;
+        const int64_t b = boff[k0 + i], nb = ((int64_t)lq[k0 + i] + 1) & ~1LL;
         if (nb <= 0) continue;
-        for (int64_t t = (b + CP_T - 1) / CP_T; t * CP_T < b + nb; t++) tfq[t] = i;
-        for (int64_t t = (b / 2 + CP_T - 1) / CP_T; t * CP_T < b / 2 + nb / 2; t++) tfs[t] = i;
+        for (int64_t t = (b + CP_T - 1) / CP_T; t * CP_T < b + nb; t++) tfq[t - tq0] = i;
+        for (int64_t t = (b / 2 + CP_T - 1) / CP_T; t * CP_T < b / 2 + nb / 2; t++) tfs[t - ts0] = i;
     }
 }
 
@@ -662,55 +680,68 @@ __global__ void k_tile_first(const int64_t *__restrict__ boff, const int32_t *__
 // when the four bytes come from one read), then stores; a dword across a read
 // boundary (or an odd-length read's pad quality byte, 0) is built byte by
 // byte.  The tile is large so the per-tile chain of dependent loads (its
-// first read, the staged fields) is paid once per 16 KB.
+// first read, the staged fields) is paid once per 16 KB.  A piece writes only
+// its destination bytes [dlo, dhi): the dwords it shares with the pieces
+// either side take byte stores.
 template <bool QUAL>
 __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ U, const int64_t *__restrict__ srcs,
                                                     const int64_t *__restrict__ boff, const int32_t *__restrict__ lq,
-                                                    int64_t n, const int64_t *__restrict__ tf, int64_t n_tiles,
-                                                    int64_t total, int stage_cap, uint8_t *__restrict__ dst) {
+                                                    int64_t k0, int64_t n, const int64_t *__restrict__ tf,
+                                                    int64_t n_tiles, int64_t dlo, int64_t dhi, int stage_cap,
+                                                    uint8_t *__restrict__ dst) {
     __shared__ int64_t s_beg[CP_R], s_src[CP_R];
     __shared__ int32_t s_len[CP_R];
     __shared__ uint8_t s_odd[CP_R];
-    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-        const int64_t r0 = tf[t], r1 = t + 1 < n_tiles ? tf[t + 1] : n - 1;
+    const int64_t t_first = dlo / CP_T;
+    // byte y of the destination (dlo <= y < dhi): read q (local) holds it
+    auto byte_at = [&](int64_t y, int64_t q) -> uint32_t {
+        const int64_t i = k0 + q, nb = ((int64_t)lq[i] + 1) & ~1LL;
+        const int64_t b0 = QUAL ? boff[i] : boff[i] / 2, L = QUAL ? nb : nb / 2;
+        if (QUAL && (lq[i] & 1) && y == b0 + L - 1) return 0u;
+        return U[(QUAL ? srcs[q] + nb / 2 : srcs[q]) + (y - b0)];
+    };
+    for (int64_t tt = blockIdx.x; tt < n_tiles; tt += gridDim.x) {
+        const int64_t t = t_first + tt;
+        const int64_t r0 = tf[tt], r1 = tt + 1 < n_tiles ? tf[tt + 1] : n - 1;
         const int64_t nr = r1 - r0 + 1;
         const bool staged = nr <= stage_cap;
         __syncthreads();
         if (staged)
             for (int64_t k = threadIdx.x; k < nr; k += blockDim.x) {
-                const int64_t i = r0 + k, nb = ((int64_t)lq[i] + 1) & ~1LL;
+                const int64_t q = r0 + k, i = k0 + q, nb = ((int64_t)lq[i] + 1) & ~1LL;
                 s_beg[k] = QUAL ? boff[i] : boff[i] / 2;
                 s_len[k] = (int32_t)(QUAL ? nb : nb / 2);
-                s_src[k] = QUAL ? srcs[i] + nb / 2 : srcs[i];
+                s_src[k] = QUAL ? srcs[q] + nb / 2 : srcs[q];
                 s_odd[k] = (uint8_t)(lq[i] & 1);
             }
         __syncthreads();
         if (!staged) {  // more reads than LDS holds (tiny reads): each dword searched in global memory
             for (int j = 0; j < CP_J; j++) {
                 const int64_t x = t * CP_T + 4 * (int64_t)(threadIdx.x + 256 * j);
-                if (x >= total) continue;
+                if (x + 4 <= dlo || x >= dhi) continue;
                 int64_t lo = r0, hi = r1;
+                const int64_t x0 = x < dlo ? dlo : x;
                 while (lo < hi) {
                     const int64_t mid = (lo + hi + 1) / 2;
-                    if ((QUAL ? boff[mid] : boff[mid] / 2) <= x) lo = mid;
+                    if ((QUAL ? boff[k0 + mid] : boff[k0 + mid] / 2) <= x0) lo = mid;
                     else hi = mid - 1;
                 }
-                uint32_t v = 0;
                 int64_t q = lo;
+                const bool whole = x >= dlo && x + 4 <= dhi;
+                uint32_t v = 0;
                 for (int jj = 0; jj < 4; jj++) {
                     const int64_t y = x + jj;
-                    if (y >= total) break;
-                    int64_t nb = ((int64_t)lq[q] + 1) & ~1LL;
-                    while (y >= (QUAL ? boff[q] + nb : boff[q] / 2 + nb / 2) && q < r1) {
+                    if (y < dlo || y >= dhi) continue;
+                    int64_t nb = ((int64_t)lq[k0 + q] + 1) & ~1LL;
+                    while (y >= (QUAL ? boff[k0 + q] + nb : boff[k0 + q] / 2 + nb / 2) && q < r1) {
                         q++;
-                        nb = ((int64_t)lq[q] + 1) & ~1LL;
+                        nb = ((int64_t)lq[k0 + q] + 1) & ~1LL;
                     }
-                    const int64_t b0 = QUAL ? boff[q] : boff[q] / 2, L = QUAL ? nb : nb / 2;
-                    uint32_t byte = 0;
-                    if (!(QUAL && (lq[q] & 1) && y == b0 + L - 1)) byte = U[(QUAL ? srcs[q] + nb / 2 : srcs[q]) + (y - b0)];
-                    v |= byte << (8 * jj);
+                    const uint32_t byte = byte_at(y, q);
+                    if (whole) v |= byte << (8 * jj);
+                    else dst[y] = (uint8_t)byte;
                 }
-                *(uint32_t *)(dst + x) = v;
+                if (whole) *(uint32_t *)(dst + x) = v;
             }
             continue;
         }
@@ -721,15 +752,16 @@ __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ 
         for (int j = 0; j < CP_J; j++) {
             const int32_t xr = 4 * (threadIdx.x + 256 * j);  // offset in the tile
             const int64_t x = t0 + xr;
+            const int64_t x0 = x < dlo ? dlo : x;
             int lo = k, hi = (int)nr - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) / 2;
-                if (s_beg[mid] <= x) lo = mid;
+                if (s_beg[mid] <= x0) lo = mid;
                 else hi = mid - 1;
             }
             k = lo;
             const int64_t b0 = s_beg[k], L = s_len[k];
-            const bool fast = x + 4 <= b0 + L && !(QUAL && s_odd[k] && x + 3 >= b0 + L - 1) && x + 4 <= total;
+            const bool fast = x >= dlo && x + 4 <= b0 + L && !(QUAL && s_odd[k] && x + 3 >= b0 + L - 1) && x + 4 <= dhi;
             const int64_t p = s_src[k] + (x - b0);
             const uint32_t *a = (const uint32_t *)(U + (p & ~(int64_t)3));
             fastm |= (uint32_t)fast << j;
@@ -740,48 +772,59 @@ __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ 
 #pragma unroll
         for (int j = 0; j < CP_J; j++) {
             const int64_t x = t0 + 4 * (threadIdx.x + 256 * j);
-            if (x >= total) continue;
-            uint32_t v;
+            if (x + 4 <= dlo || x >= dhi) continue;
             if ((fastm >> j) & 1u) {
                 const uint32_t sh = ((shp >> (2 * j)) & 3u) * 8;
-                v = sh ? (w0[j] >> sh) | (w1[j] << (32 - sh)) : w0[j];
-            } else {
-                // a read boundary or the pad byte in this dword: the read again, then byte by byte
-                int lo = 0, hi = (int)nr - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) / 2;
-                    if (s_beg[mid] <= x) lo = mid;
-                    else hi = mid - 1;
-                }
-                v = 0;
-                int q = lo;
-                for (int jj = 0; jj < 4; jj++) {
-                    const int64_t y = x + jj;
-                    if (y >= total) break;
-                    while (y >= s_beg[q] + s_len[q] && q + 1 < (int)nr) q++;
-                    uint32_t byte = 0;
-                    if (!(QUAL && s_odd[q] && y == s_beg[q] + s_len[q] - 1)) byte = U[s_src[q] + (y - s_beg[q])];
-                    v |= byte << (8 * jj);
-                }
+                *(uint32_t *)(dst + x) = sh ? (w0[j] >> sh) | (w1[j] << (32 - sh)) : w0[j];
+                continue;
             }
-            *(uint32_t *)(dst + x) = v;
+            // a read boundary, the pad byte or a piece edge in this dword:
+            // the read again, then byte by byte
+            const int64_t x0 = x < dlo ? dlo : x;
+            int lo = 0, hi = (int)nr - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2;
+                if (s_beg[mid] <= x0) lo = mid;
+                else hi = mid - 1;
+            }
+            const bool whole = x >= dlo && x + 4 <= dhi;
+            uint32_t v = 0;
+            int q = lo;
+            for (int jj = 0; jj < 4; jj++) {
+                const int64_t y = x + jj;
+                if (y < dlo || y >= dhi) continue;
+                while (y >= s_beg[q] + s_len[q] && q + 1 < (int)nr) q++;
+                uint32_t byte = 0;
+                if (!(QUAL && s_odd[q] && y == s_beg[q] + s_len[q] - 1)) byte = U[s_src[q] + (y - s_beg[q])];
+                if (whole) v |= byte << (8 * jj);
+                else dst[y] = (uint8_t)byte;
+            }
+            if (whole) *(uint32_t *)(dst + x) = v;
         }
     }
 }
 
-// equal-hash runs: every member's name equal to the run head's; ids = head + 1
-__global__ void k_name_ids(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
-                           const int64_t *__restrict__ krec, const uint64_t *__restrict__ keys,
-                           const uint32_t *__restrict__ vals, const uint32_t *__restrict__ head, int64_t n,
-                           uint32_t *__restrict__ nid, uint32_t *__restrict__ bad) {
+// equal-hash runs: every member's name equal to the run head's (the names'
+// bytes, nmoff[i]..nmoff[i + 1], up to the NUL); ids = head + 1
+__global__ void k_name_ids(const uint8_t *__restrict__ nm, const int64_t *__restrict__ nmoff,
+                           const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                           const uint32_t *__restrict__ head, int64_t n, uint32_t *__restrict__ nid,
+                           uint32_t *__restrict__ bad) {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t i = vals[p];
         if (keys[p] == 0) { nid[i] = 0; continue; }
         const uint32_t hp = head[p];
         nid[i] = hp + 1;
         if (hp == (uint32_t)p) continue;
-        const int64_t oa = off[krec[i]];
-        if (!name_equal(U, oa + 36, off[krec[vals[hp]]] + 36, U[oa + 12])) atomicOr(bad, DB_NAMES);
+        const uint32_t h = vals[hp];
+        const int64_t a0 = nmoff[i], la = nmoff[i + 1] - a0, b0 = nmoff[h], lb = nmoff[h + 1] - b0;
+        bool eq = true;
+        for (int64_t c = 0; eq; c++) {
+            const uint8_t x = c < la ? nm[a0 + c] : 0, y = c < lb ? nm[b0 + c] : 0;
+            if (x != y) eq = false;
+            else if (x == 0 || c + 1 >= la) break;
+        }
+        if (!eq) atomicOr(bad, DB_NAMES);
     }
 }
 
@@ -858,10 +901,11 @@ inline unsigned grid_for(int64_t n, int per = 256, unsigned cap = 65536) {
 // offsets' closing entry
 __global__ void k_totals(const uint32_t *keep, const uint32_t *kidx, const uint32_t *drop, const uint32_t *didx,
                          const uint32_t *auxc, const uint32_t *aidx, const uint32_t *ncig, const uint32_t *coff,
-                         const int64_t *nb, const int64_t *boff, int64_t R, int64_t *tot) {
+                         const int64_t *nb, const int64_t *boff, const uint32_t *nml, const uint32_t *nmo, int64_t R,
+                         int64_t *tot) {
     if (blockIdx.x || threadIdx.x) return;
     if (R == 0) {
-        for (int k = 0; k < 5; k++) tot[k] = 0;
+        for (int k = 0; k < 6; k++) tot[k] = 0;
         return;
     }
     const int64_t r = R - 1;
@@ -870,6 +914,7 @@ __global__ void k_totals(const uint32_t *keep, const uint32_t *kidx, const uint3
     tot[2] = (int64_t)aidx[r] + auxc[r];
     tot[3] = (int64_t)coff[r] + ncig[r];
     tot[4] = boff[r] + nb[r];
+    tot[5] = (int64_t)nmo[r] + nml[r];
 }
 
 __global__ void k_set_u32(uint32_t *p, uint32_t v) {
@@ -892,7 +937,7 @@ __global__ void k_lower_bound(const int32_t *a, int64_t n, int32_t x, int64_t *o
 // own stream (the prefetch thread inflates and walks run k+1 while the worker
 // parses run k on the context's stream)
 struct RunSlot {
-    DBuf U, blk, status, misc, S, ccnt, cbase, off, tmp;
+    DBuf U, blk, status, misc, S, ccnt, cbase, off, tmp;  // (blk, S: unused by the piece decode)
     hipStream_t st = nullptr;
     hipEvent_t ev[3] = {};
     int64_t *h_small = nullptr;  // pinned
@@ -908,10 +953,20 @@ struct dd_ctx {
     hipEvent_t cev[DD_SLOTS] = {};
     int64_t dcomp_len[DD_SLOTS] = {};
     hipEvent_t ev[4] = {};
+    hipEvent_t pev[DD_SLOTS] = {};  // the piece in slot k is parsed (its U and record offsets are free)
     DBuf misc;  // the parse's and the statistics' flags and scalars
     DBuf keep, kidx, drop, didx, auxc, aidx, ncig, coff, nb, boff, rpos, krec, keys, vals, keys2, vals2, head, tmp;
     DBuf srcs, tfq, tfs;  // per kept read: its bases' offset in U; per copy tile: its first read
     DBuf sq, sqi, sv, slq, sm, s_ins, s_lq, acand, alen, aoff, akidx, apack;
+    DBuf rblk, rS;          // the run's BGZF block table and record starts
+    DBuf nml, nmo, nm, nmoff;  // per piece record: name length, its offset; per chromosome: name bytes, offsets
+    // inflated bytes per piece (GROM_DD_PIECE_MB): a launch of k_inflate takes
+    // at least the time one lane needs for one block, so a piece must hold
+    // about half a chip's worth of blocks (two pieces are in flight): 3 GB is
+    // ~48 k blocks, ~750 waves
+    int64_t piece_bytes = (int64_t)3 << 30;
+    std::vector<uint8_t> aux_bytes;  // the last run's split-read candidates (dd_parse_out)
+    std::vector<int64_t> aux_off, aux_kidx;
     int64_t *h_small = nullptr;  // pinned: totals and scalars
     uint8_t *h_aux = nullptr;    // pinned: packed split-read candidate records
     size_t h_aux_cap = 0;
@@ -932,7 +987,7 @@ struct dd_ctx {
     } while (0)
 #define DGROW(b, bytes)                                                                              \
     do {                                                                                             \
-        if (dgrow((b), (bytes))) {                                                                   \
+        if (dgrow((b), (bytes), #b)) {                                                               \
             if (err) snprintf(err, (size_t)errlen, "device decode: hipMalloc(%zu) failed", (size_t)(bytes)); \
             return -1;                                                                               \
         }                                                                                            \
@@ -969,10 +1024,13 @@ extern "C" dd_ctx *dd_ctx_new(int device) {
     c->device = device;
     if (getenv("GROM_WS_GUESS")) c->ws_guess = atoi(getenv("GROM_WS_GUESS"));
     if (getenv("GROM_TEST_CP_UNSTAGED")) c->cp_cap = 0;
+    if (getenv("GROM_DD_PIECE_MB") && atof(getenv("GROM_DD_PIECE_MB")) > 0)
+        c->piece_bytes = std::max<int64_t>((int64_t)(atof(getenv("GROM_DD_PIECE_MB")) * 1048576.0), 4096);
     if (dd_stream_new(&c->st) != hipSuccess) { delete c; return nullptr; }
     if (dd_stream_new(&c->cst) != hipSuccess) c->cst = nullptr;
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
     for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming);
+    for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->pev[k], hipEventDisableTiming);
     if (hipHostMalloc((void **)&c->h_small, 64 * sizeof(int64_t), 0) != hipSuccess) c->h_small = nullptr;
     for (int k = 0; k < DD_SLOTS; k++) {
         RunSlot &r = c->rs[k];
@@ -992,6 +1050,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     for (int k = 0; k < DD_SLOTS; k++) {
         if (c->dcomp[k].p) grom_dev_free(c->dcomp[k].p, c->dcomp[k].cap, GROM_DEVCAT_DECODE);
         if (c->cev[k]) (void)hipEventDestroy(c->cev[k]);
+        if (c->pev[k]) (void)hipEventDestroy(c->pev[k]);
     }
     for (int k = 0; k < DD_SLOTS; k++) {
         RunSlot &r = c->rs[k];
@@ -1008,7 +1067,8 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
                    &c->kidx, &c->drop, &c->didx, &c->auxc, &c->aidx, &c->ncig, &c->coff, &c->nb, &c->boff, &c->rpos,
                    &c->krec, &c->keys, &c->vals, &c->keys2, &c->vals2, &c->head, &c->tmp, &c->sq, &c->sqi, &c->sv,
                    &c->srcs, &c->tfq, &c->tfs,
-                   &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack};
+                   &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack,
+                   &c->rblk, &c->rS, &c->nml, &c->nmo, &c->nm, &c->nmoff};
     for (DBuf *b : all)
         if (b->p) grom_dev_free(b->p, b->cap, GROM_DEVCAT_DECODE);
     for (int k = 0; k < 4; k++)
@@ -1038,25 +1098,28 @@ extern "C" void dd_ctx_counts(const dd_ctx *c, int64_t *rewalked, int64_t *subch
     *subchunks = c->n_sub;
 }
 
-// the per-run buffers sized once for the largest run (ubytes inflated bytes,
-// recs records): growing them later frees the old buffer, which waits for the
-// whole device
-extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_starts, int n_slots, char *err,
+// The buffers of one piece (the piece slots, ~GROM_DD_PIECE_MB of inflated
+// bytes each) and the chromosome-wide ones, sized once for the largest run
+// (recs records, n_starts record starts, its compressed span): a later run
+// beyond the estimate still grows them.  Growing a buffer frees the old one,
+// which waits for the whole device.
+extern "C" int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs, int64_t n_starts, char *err,
                           int errlen) {
     DCK(hipSetDevice(c->device));
-    // the small buffers too: a small hipMalloc waits behind any large one in
-    // flight on another thread (the stage reservations), ~0.4 s at 30x
+    const int64_t pb = std::min<int64_t>(c->piece_bytes, ubytes) + (4 << 20);  // a piece ends past the target
+    const int64_t pr = pb / 34 + 1024;  // records in a piece: at least 34 bytes each
     const int64_t nblk = ubytes / 60000 + 1024;
-    for (int k = 0; k < n_slots && k < DD_SLOTS; k++) {
+    (void)span;  // (the compressed slots grow on the prefetch thread, dd_comp_upload)
+    DGROW(c->rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
+    DGROW(c->rS, sizeof(int64_t) * (size_t)(n_starts + 2));
+    for (int k = 0; k < DD_SLOTS; k++) {
         RunSlot &r = c->rs[k];
-        DGROW(r.U, (size_t)ubytes + 64);
-        DGROW(r.blk, sizeof(DdBlock) * (size_t)(nblk + 1));
-        DGROW(r.status, (size_t)nblk + 1);
+        DGROW(r.U, (size_t)pb + 64);
+        DGROW(r.status, (size_t)(pb / 16384 + 1024));
         DGROW(r.misc, 256);
-        DGROW(r.S, sizeof(int64_t) * (size_t)(n_starts + 1));
         DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
         DGROW(r.cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
-        DGROW(r.off, 8 * (size_t)(recs + 1));
+        DGROW(r.off, 8 * (size_t)(pr + 1));
         size_t tb = 0;
         DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(n_starts + 1),
                                              r.st));
@@ -1065,47 +1128,39 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t ubytes, int64_t recs, int64_t n_sta
     DGROW(c->misc, 256);
     {
         size_t tb = 0, t2 = 0, t3 = 0, t4 = 0;
-        const int r = (int)std::min<int64_t>(recs + 1, INT32_MAX);
-        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, r, c->st));
-        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (int64_t *)nullptr, (int64_t *)nullptr, r, c->st));
+        const int rp = (int)std::min<int64_t>(pr + 1, INT32_MAX), rn = (int)std::min<int64_t>(recs + 1, INT32_MAX);
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, rp, c->st));
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (int64_t *)nullptr, (int64_t *)nullptr, rp, c->st));
         DCK(hipcub::DeviceRadixSort::SortPairs(nullptr, t3, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
-                                               (uint32_t *)nullptr, r, 0, 64, c->st));
-        DCK(hipcub::DeviceScan::InclusiveScan(nullptr, t4, (uint32_t *)nullptr, (uint32_t *)nullptr, hipcub::Max(), r,
+                                               (uint32_t *)nullptr, rn, 0, 64, c->st));
+        DCK(hipcub::DeviceScan::InclusiveScan(nullptr, t4, (uint32_t *)nullptr, (uint32_t *)nullptr, hipcub::Max(), rn,
                                               c->st));
         DGROW(c->tmp, std::max(std::max(tb, t2), std::max(t3, t4)));
     }
+    // per piece record
+    const size_t p4 = 4 * (size_t)(pr + 1), p8 = 8 * (size_t)(pr + 1);
+    DGROW(c->keep, p4); DGROW(c->kidx, p4); DGROW(c->drop, p4); DGROW(c->didx, p4); DGROW(c->auxc, p4);
+    DGROW(c->aidx, p4); DGROW(c->ncig, p4); DGROW(c->coff, p4); DGROW(c->nml, p4); DGROW(c->nmo, p4);
+    DGROW(c->nb, p8); DGROW(c->boff, p8); DGROW(c->rpos, p4); DGROW(c->srcs, p8);
+    DGROW(c->tfq, 8 * (size_t)(pb / CP_T + 4));
+    DGROW(c->tfs, 8 * (size_t)(pb / 2 / CP_T + 4));
+    const size_t na = (size_t)(pr / 8 + 2);
+    DGROW(c->acand, 8 * na); DGROW(c->alen, 8 * na); DGROW(c->aoff, 8 * na); DGROW(c->akidx, 8 * na);
+    DGROW(c->apack, (size_t)(pr / 64 + 1) * 512);
+    // per chromosome: name hashes and their sort, the names' bytes
     const size_t r4 = 4 * (size_t)(recs + 1), r8 = 8 * (size_t)(recs + 1);
-    DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
-    DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
-    DGROW(c->rpos, r4); DGROW(c->krec, r8); DGROW(c->srcs, r8); DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8);
-    DGROW(c->vals2, r4); DGROW(c->head, r4);
-    // (the insert statistics' arrays are the parse's: dd_run_stats)
+    DGROW(c->keys, r8); DGROW(c->vals, r4); DGROW(c->keys2, r8); DGROW(c->vals2, r4); DGROW(c->head, r4);
+    DGROW(c->nmoff, r8);
+    DGROW(c->nm, (size_t)recs * 24 + 4096);
+    // the insert statistics' sample (the cap's worth)
     const size_t take = 4 * (size_t)std::min<int64_t>(recs + 1, (int64_t)1 << 24);
     DGROW(c->s_ins, take); DGROW(c->s_lq, take);
-    // the parse's small arrays too (a small allocation made while the stage
-    // helper's 20 GB ones are in flight waited 0.3-0.4 s): copy-tile starts
-    // (bases <= inflated bytes) and the split-read candidates (generously:
-    // one record in 8, 512 bytes per packed record for one in 64)
-    DGROW(c->tfq, 8 * (size_t)(ubytes / CP_T + 2));
-    DGROW(c->tfs, 8 * (size_t)(ubytes / 2 / CP_T + 2));
-    const size_t na = (size_t)(recs / 8 + 2);
-    DGROW(c->acand, 8 * na); DGROW(c->alen, 8 * na); DGROW(c->aoff, 8 * na); DGROW(c->akidx, 8 * na);
-    DGROW(c->apack, (size_t)(recs / 64 + 1) * 512);
-    if (c->h_aux_cap < ((size_t)16 << 20)) {  // their host copy: a few MB per chromosome at 30x
-        if (c->h_aux) (void)hipHostFree(c->h_aux);
-        c->h_aux = nullptr;
-        c->h_aux_cap = (size_t)16 << 20;
-        if (hipHostMalloc((void **)&c->h_aux, c->h_aux_cap, 0) != hipSuccess) {
-            c->h_aux = nullptr;
-            c->h_aux_cap = 0;
-        }
-    }
     return 0;
 }
 
 // a run's compressed bytes (pinned, readable 64 bytes past comp_len) into the
 // device slot, on the copy stream: returns at once; the host buffer must stay
-// untouched until a dd_run_load of the slot has returned
+// untouched until a dd_run_decode of the slot has returned
 extern "C" int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_t comp_len, char *err, int errlen) {
     if (slot < 0 || slot >= DD_SLOTS) return -1;
     DCK(hipSetDevice(c->device));
@@ -1117,247 +1172,423 @@ extern "C" int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_
     return 0;
 }
 
-// inflate a run's blocks (uploaded to `slot` by dd_comp_upload) and find its
-// records: starts[0..n_starts) are record offsets in the inflated stream (the
-// first = the run's first record), u_end its end
-extern "C" int dd_run_load(dd_ctx *c, int slot, int rslot, int64_t comp_len, const DdBlock *h_blk, int64_t nblk,
-                           int64_t ubytes, const int64_t *h_starts, int64_t n_starts, int64_t u_end, int32_t tid,
-                           int64_t *n_rec, char *err, int errlen) {
-    DCK(hipSetDevice(c->device));
-    if (slot < 0 || slot >= DD_SLOTS || rslot < 0 || rslot >= DD_SLOTS || c->dcomp_len[slot] != comp_len) {
-        if (err) snprintf(err, (size_t)errlen, "device decode: slot %d does not hold the run", slot);
-        return -1;
+// A DBuf grown to `bytes` keeping its first `keep` bytes (a copy on `st`)
+static int dgrow_keep(DBuf &b, size_t bytes, size_t keep, hipStream_t st) {
+    if (b.cap >= bytes) return 0;
+    DBuf nb;
+    if (dgrow(nb, bytes + bytes / 8)) return -1;
+    if (keep && b.p) {
+        if (hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return -1;
     }
-    RunSlot &r = c->rs[rslot];
-    hipStream_t st = r.st;
-    DGROW(r.blk, sizeof(DdBlock) * (size_t)(nblk + 1));
-    DGROW(r.U, (size_t)ubytes + 64);
-    DGROW(r.status, (size_t)nblk + 1);
-    DGROW(r.misc, 256);
-    DGROW(r.S, sizeof(int64_t) * (size_t)(n_starts + 1));
-    DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
-    DGROW(r.cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
-    DCK(hipStreamWaitEvent(st, c->cev[slot], 0));
-    DCK(hipMemcpyAsync(r.blk.p, h_blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(r.S.p, h_starts, sizeof(int64_t) * (size_t)n_starts, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(P<int64_t>(r.S) + n_starts, &u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    DCK(hipMemsetAsync(r.misc.p, 0, 256, st));
-    uint32_t *bad = P<uint32_t>(r.misc);
-    DCK(hipEventRecord(r.ev[0], st));
-    if (dd_inflate_launch(st, P<uint8_t>(c->dcomp[slot]), P<DdBlock>(r.blk), nblk, P<uint8_t>(r.U), P<uint8_t>(r.status),
-                          bad + 1)) {
-        if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
-        return -1;
-    }
-    DCK(hipEventRecord(r.ev[1], st));
-    // records: count per chunk, place, write offsets
-    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(r.U), P<int64_t>(r.S),
-                       n_starts, tid, c->ws_guess, bad + 4, P<uint32_t>(r.ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, bad);
-    size_t tb = 0;
-    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)n_starts, st));
-    DGROW(r.tmp, tb);
-    DCK(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)n_starts, st));
-    DCK(hipMemcpyAsync(r.h_small, P<uint32_t>(r.cbase) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)r.h_small + 4, P<uint32_t>(r.ccnt) + n_starts - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)r.h_small + 8, bad, 8, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)r.h_small + 16, bad + 4, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipStreamSynchronize(st));
-    const uint32_t *hs = (const uint32_t *)r.h_small;
-    c->n_rewalk += hs[4];
-    c->n_sub += (ubytes + WS_G - 1) / WS_G;
-    if (hs[3]) {
-        if (err) snprintf(err, (size_t)errlen, "device inflate: %u blocks failed", hs[3]);
-        return -2;
-    }
-    if (hs[2]) {
-        if (err) snprintf(err, (size_t)errlen, "device decode: record chain (%#x) does not follow the index", hs[2]);
-        return -2;
-    }
-    const int64_t R = (int64_t)hs[0] + hs[1];
-    DGROW(r.off, sizeof(int64_t) * (size_t)(R + 1));
-    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)n_starts), dim3(WS_T), 0, st, P<uint8_t>(r.U), P<int64_t>(r.S),
-                       n_starts, tid, c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), bad);
-    DCK(hipEventRecord(r.ev[2], st));
-    DCK(hipGetLastError());
-    // the run is complete before the slot is handed on (its caller may be the
-    // prefetch thread, the parse then runs on the context's own stream)
-    DCK(hipStreamSynchronize(st));
-    float a = 0, b = 0;
-    (void)hipEventElapsedTime(&a, r.ev[0], r.ev[1]);
-    (void)hipEventElapsedTime(&b, r.ev[1], r.ev[2]);
-    c->ms_inflate += a;
-    c->ms_walk += b;
-    r.R = R;
-    r.nblk = nblk;
-    r.ubytes = ubytes;
-    *n_rec = R;
+    if (b.p) grom_dev_free(b.p, b.cap, GROM_DEVCAT_DECODE);
+    b = nb;
     return 0;
 }
 
-// find_insert_mean's sample from the loaded run, all of its records in file
-// order: at most cap_left (insert, l_qseq) pairs, and the mapped-bases sum up
-// to the record that completes the cap (or over the whole run)
-extern "C" int dd_run_stats(dd_ctx *c, int slot, int32_t min_mapq, int64_t cap_left, int32_t *h_ins, int32_t *h_lq,
-                            int64_t *n_taken, int64_t *m_contrib, char *err, int errlen) {
+// ---- a run decoded piece by piece ----
+//
+// A chromosome's run inflates to ~15 GB at 30x (chr1).  It is decoded in
+// pieces of whole record-start chunks (the index's 16 kb windows: a chunk
+// boundary is a record start, so no record crosses a piece), each ~piece_bytes
+// of inflated data: the piece's BGZF blocks are inflated into a piece slot,
+// its records walked, the insert statistics taken from it while they are
+// wanted, and its records parsed straight into the stage at the offsets the
+// earlier pieces reached (the carries).  The read names go to a chromosome-wide
+// byte array, so the read-name ids (a sort of the name hashes and a byte
+// check of every equal-hash run) come after the last piece.
+extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, int64_t *n_rec, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
-    hipStream_t st = c->st;
-    if (slot < 0 || slot >= DD_SLOTS) return -1;
-    RunSlot &rs = c->rs[slot];
-    const int64_t R = rs.R;
-    *n_taken = 0;
-    *m_contrib = 0;
-    if (R == 0 || cap_left <= 0) return 0;
-    // the parse's per-record arrays serve the statistics (both run on c->st,
-    // one after the other): sq, sqi, sv, slq, sm
-    DGROW(c->keep, 4 * (size_t)(R + 1));
-    DGROW(c->kidx, 4 * (size_t)(R + 1));
-    DGROW(c->drop, 4 * (size_t)(R + 1));
-    DGROW(c->didx, 4 * (size_t)(R + 1));
-    DGROW(c->nb, 8 * (size_t)(R + 1));
-    DBuf &sq = c->keep, &sqi = c->kidx, &sv = c->drop, &slq = c->didx, &sm = c->nb;
-    const int64_t take_cap = std::min<int64_t>(cap_left, R);
-    DGROW(c->s_ins, 4 * (size_t)take_cap);
-    DGROW(c->s_lq, 4 * (size_t)take_cap);
-    hipLaunchKernelGGL(k_stats, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off), R, min_mapq,
-                       P<uint32_t>(sq), P<int32_t>(sv), P<int32_t>(slq), P<int64_t>(sm));
-    size_t tb = 0, tb2 = 0;
-    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(sq), P<uint32_t>(sqi), (int)R, st));
-    DCK(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, P<int64_t>(sm), P<int64_t>(sm), (int)R, st));
-    DGROW(c->tmp, std::max(tb, tb2));
-    DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(sq), P<uint32_t>(sqi), (int)R, st));
-    DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, tb2, P<int64_t>(sm), P<int64_t>(sm), (int)R, st));
-    DGROW(c->misc, 256);
-    int64_t *mcap = (int64_t *)((char *)c->misc.p + 64);
-    DCK(hipMemsetAsync(mcap, 0xff, 8, st));
-    hipLaunchKernelGGL(k_stats_take, dim3(grid_for(R)), dim3(256), 0, st, P<uint32_t>(sq), P<uint32_t>(sqi),
-                       P<int32_t>(sv), P<int32_t>(slq), P<int64_t>(sm), R, take_cap, P<int32_t>(c->s_ins),
-                       P<int32_t>(c->s_lq), mcap);
-    // qualifying total, m total, m at the cap
-    DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(sqi) + R - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(sq) + R - 1, 4, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync(c->h_small + 1, P<int64_t>(sm) + R - 1, 8, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync(c->h_small + 2, mcap, 8, hipMemcpyDeviceToHost, st));
-    DCK(hipStreamSynchronize(st));
-    const uint32_t *hs = (const uint32_t *)c->h_small;
-    const int64_t nq = (int64_t)hs[0] + hs[1];
-    const int64_t n = std::min<int64_t>(nq, cap_left);
-    if (n > 0) {
-        DCK(hipMemcpyAsync(h_ins, c->s_ins.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
-        DCK(hipMemcpyAsync(h_lq, c->s_lq.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
-        DCK(hipStreamSynchronize(st));
-    }
-    *n_taken = n;
-    *m_contrib = (nq >= cap_left) ? c->h_small[2] : c->h_small[1];
-    return 0;
-}
-
-// the loaded run parsed into `stage` (records j0.. of the run): fields,
-// CIGAR words, bases, qualities, name ids, dropped records; the split-read
-// candidates' record bytes come back to the host (dd_run_aux)
-extern "C" int dd_run_parse(dd_ctx *c, int slot, int64_t j0, int32_t tid, int32_t read_name_len, int64_t ref_len,
-                            grom_stage *stage, dd_parse_out *po, char *err, int errlen) {
-    DCK(hipSetDevice(c->device));
-    hipStream_t st = c->st;
-    if (slot < 0 || slot >= DD_SLOTS) return -1;
-    RunSlot &rs = c->rs[slot];
-    const int64_t R = rs.R;
     memset(po, 0, sizeof(*po));
-    const size_t r4 = 4 * (size_t)(R + 1), r8 = 8 * (size_t)(R + 1);
-    DGROW(c->keep, r4); DGROW(c->kidx, r4); DGROW(c->drop, r4); DGROW(c->didx, r4); DGROW(c->auxc, r4);
-    DGROW(c->aidx, r4); DGROW(c->ncig, r4); DGROW(c->coff, r4); DGROW(c->nb, r8); DGROW(c->boff, r8);
-    DGROW(c->rpos, r4);
-    DGROW(c->misc, 256);
-    uint32_t *bad = P<uint32_t>(c->misc);
-    int64_t *tot = (int64_t *)((char *)c->misc.p + 128);
-    DCK(hipEventRecord(c->ev[2], st));
-    DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
-    if (R > 0)
-        hipLaunchKernelGGL(k_rec_meta, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off), R, j0,
-                           tid, P<uint32_t>(c->keep), P<uint32_t>(c->drop), P<uint32_t>(c->auxc), P<uint32_t>(c->ncig),
-                           P<int64_t>(c->nb), P<int32_t>(c->rpos), bad);
-    if (R > 0) {
-        size_t tb = 0, t2 = 0;
-        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(c->keep), P<uint32_t>(c->kidx), (int)R, st));
-        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, P<int64_t>(c->nb), P<int64_t>(c->boff), (int)R, st));
-        DGROW(c->tmp, std::max(tb, t2));
-        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->keep), P<uint32_t>(c->kidx), (int)R, st));
-        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->drop), P<uint32_t>(c->didx), (int)R, st));
-        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), (int)R, st));
-        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tb, P<uint32_t>(c->ncig), P<uint32_t>(c->coff), (int)R, st));
-        DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t2, P<int64_t>(c->nb), P<int64_t>(c->boff), (int)R, st));
+    *n_rec = 0;
+    if (q->slot < 0 || q->slot >= DD_SLOTS || c->dcomp_len[q->slot] != q->comp_len) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: slot %d does not hold the run", q->slot);
+        return -1;
     }
-    hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, st, P<uint32_t>(c->keep), P<uint32_t>(c->kidx),
-                       P<uint32_t>(c->drop), P<uint32_t>(c->didx), P<uint32_t>(c->auxc), P<uint32_t>(c->aidx),
-                       P<uint32_t>(c->ncig), P<uint32_t>(c->coff), P<int64_t>(c->nb), P<int64_t>(c->boff), R, tot);
-    DCK(hipMemcpyAsync(c->h_small, tot, 5 * 8, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync(c->h_small + 5, bad, 8, hipMemcpyDeviceToHost, st));
-    DCK(hipStreamSynchronize(st));
-    const int64_t n = c->h_small[0], nd = c->h_small[1], na = c->h_small[2], ncg = c->h_small[3], nbs = c->h_small[4];
-    const uint32_t b0 = ((const uint32_t *)(c->h_small + 5))[0];
-    if (b0) {
-        if (err) snprintf(err, (size_t)errlen, "device decode: records do not parse as the run's (%#x)", b0);
-        return -2;
+    hipStream_t st = c->st;
+    const int64_t nblk = q->nblk, ns = q->n_starts;
+    // the run's block table and record starts (+ its end) on the device
+    DGROW(c->rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
+    DGROW(c->rS, sizeof(int64_t) * (size_t)(ns + 2));
+    DCK(hipStreamWaitEvent(st, c->cev[q->slot], 0));
+    DCK(hipMemcpyAsync(c->rblk.p, q->blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(c->rS.p, q->starts, sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(P<int64_t>(c->rS) + ns, &q->u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    // pieces: consecutive chunks [ca, cb) of about piece_bytes
+    auto block_of = [&](int64_t u) {  // the block whose output holds inflated offset u
+        int64_t lo = 0, hi = nblk - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) / 2;
+            if (q->blk[mid].out_off <= u) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    struct Piece {
+        int64_t ca, cb, u_lo, u_hi, bf, bl, base, pbytes;
+    };
+    std::vector<Piece> pcs;
+    for (int64_t ca = 0; ca < ns;) {
+        int64_t cb = ca + 1;
+        while (cb < ns && q->starts[cb] - q->starts[ca] < c->piece_bytes) cb++;
+        Piece pc;
+        pc.ca = ca;
+        pc.cb = cb;
+        pc.u_lo = q->starts[ca];
+        pc.u_hi = cb < ns ? q->starts[cb] : q->u_end;
+        if (pc.u_hi > pc.u_lo) {
+            pc.bf = block_of(pc.u_lo);
+            pc.bl = block_of(pc.u_hi - 1);
+            pc.base = q->blk[pc.bf].out_off;
+            pc.pbytes = q->blk[pc.bl].out_off + q->blk[pc.bl].out_len - pc.base;
+            pcs.push_back(pc);
+        }
+        ca = cb;
     }
-    // the stage: exact sizes, then every array written in place
-    grom_stage_sizes sz;
-    memset(&sz, 0, sizeof(sz));
-    sz.n = n;
-    sz.n_cigar_ops = ncg;
-    sz.n_bases = nbs;
-    sz.n_aux = na + 1;  // + the -S patch
-    sz.n_drop = nd;
-    sz.ref_len = ref_len;
-    grom_reads dv;
-    if (grom_stage_fill_begin(stage, &sz, &dv) != GROM_OK) {
+    const bool parse = q->stage != nullptr;
+    Carry car{};
+    int64_t R_tot = 0, n_aux = 0, apack_tot = 0;
+    int64_t stats_left = q->stats_left;
+    int32_t *h_ins = q->h_ins, *h_lq = q->h_lq;
+    grom_stage_sizes have{}, cap{};
+    grom_reads dv{};
+    std::vector<uint8_t> aux_bytes;
+    std::vector<int64_t> aux_off(1, 0), aux_kidx;
+    int32_t last[4] = {0, 0, 0, 0};
+    if (parse && grom_stage_begin(q->stage, nullptr) != GROM_OK) {
         if (err) snprintf(err, (size_t)errlen, "%s", grom_last_error());
         return -1;
     }
-    StageOut so;
-    so.pos = (int32_t *)dv.pos; so.mtid = (int32_t *)dv.mtid; so.mpos = (int32_t *)dv.mpos;
-    so.isize = (int32_t *)dv.isize; so.lq = (int32_t *)dv.l_qseq; so.aidx = (int32_t *)dv.aux_idx;
-    so.flag = (uint16_t *)dv.flag; so.mapq = (uint8_t *)dv.mapq; so.coff = (uint32_t *)dv.cigar_off;
-    so.cig = (uint32_t *)dv.cigar; so.nid = (uint32_t *)dv.name_id; so.boff = (int64_t *)dv.base_off;
-    so.dpos = (int32_t *)dv.drop_pos; so.dlq = (int32_t *)dv.drop_lq; so.dbef = (int64_t *)dv.drop_before;
-    DGROW(c->krec, 8 * (size_t)(n + 1));
-    DGROW(c->srcs, 8 * (size_t)(n + 1));
-    DGROW(c->keys, 8 * (size_t)(n + 1)); DGROW(c->vals, 4 * (size_t)(n + 1));
-    DGROW(c->keys2, 8 * (size_t)(n + 1)); DGROW(c->vals2, 4 * (size_t)(n + 1)); DGROW(c->head, 4 * (size_t)(n + 1));
-    DGROW(c->acand, 8 * (size_t)(na + 2)); DGROW(c->alen, 8 * (size_t)(na + 2)); DGROW(c->aoff, 8 * (size_t)(na + 2));
-    DGROW(c->akidx, 8 * (size_t)(na + 2));
-    int32_t *last = (int32_t *)((char *)c->misc.p + 192);
-    // (grom_stage_fill_begin waited for the stage's earlier copies; the
-    // arrays are written on this context's stream, synchronised below before
-    // the chromosome is handed to a scan)
-    if (R > 0)
-        hipLaunchKernelGGL(k_rec_write, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off), R, j0,
-                           P<uint32_t>(c->keep), P<uint32_t>(c->kidx), P<uint32_t>(c->drop), P<uint32_t>(c->didx),
-                           P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), P<uint32_t>(c->coff), P<int64_t>(c->boff),
-                           P<int32_t>(c->rpos), so, P<int64_t>(c->krec), P<int64_t>(c->srcs), P<uint64_t>(c->keys),
-                           P<uint32_t>(c->vals),
-                           P<int64_t>(c->acand), read_name_len, last, bad);
-    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, st, so.coff + n, (uint32_t)ncg);
-    if (n > 0) {
-        {
-            const int64_t nt_q = (nbs + CP_T - 1) / CP_T, nt_s = (nbs / 2 + CP_T - 1) / CP_T;
-            DGROW(c->tfq, 8 * (size_t)(nt_q + 1));
-            DGROW(c->tfs, 8 * (size_t)(nt_s + 1));
-            hipLaunchKernelGGL(k_tile_first, dim3(grid_for(n)), dim3(256), 0, st, (const int64_t *)so.boff,
-                               (const int32_t *)so.lq, n, P<int64_t>(c->tfq), P<int64_t>(c->tfs));
-            if (nt_q > 0)
-                hipLaunchKernelGGL(k_copy_tiles<true>, dim3((unsigned)std::min<int64_t>(nt_q, 1 << 16)), dim3(256), 0, st,
-                                   P<uint8_t>(rs.U), P<int64_t>(c->srcs), (const int64_t *)so.boff, (const int32_t *)so.lq,
-                                   n, P<int64_t>(c->tfq), nt_q, nbs, c->cp_cap, (uint8_t *)dv.qual);
-            if (nt_s > 0)
-                hipLaunchKernelGGL(k_copy_tiles<false>, dim3((unsigned)std::min<int64_t>(nt_s, 1 << 16)), dim3(256), 0,
-                                   st, P<uint8_t>(rs.U), P<int64_t>(c->srcs), (const int64_t *)so.boff,
-                                   (const int32_t *)so.lq, n, P<int64_t>(c->tfs), nt_s, nbs / 2, c->cp_cap, (uint8_t *)dv.seq);
+    DGROW(c->misc, 256);
+    uint32_t *bad = P<uint32_t>(c->misc);
+    int64_t *tot = (int64_t *)((char *)c->misc.p + 128);
+    int32_t *d_last = (int32_t *)((char *)c->misc.p + 192);
+    DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
+    DCK(hipEventRecord(c->pev[0], st));
+    DCK(hipEventRecord(c->pev[1], st));
+    // The load of piece p (inflate, record walk) runs on piece slot p % 2's
+    // own stream, issued one piece ahead: it overlaps the statistics and the
+    // parse of piece p - 1 on the context's stream.  A slot is reused once
+    // the parse of the piece before in it is done (pev).  The offsets walk
+    // writes up to the slot's record capacity; a piece with more records is
+    // walked again after its buffer grows.
+    auto issue = [&](size_t p) -> int {
+        const Piece &pc = pcs[p];
+        RunSlot &r = c->rs[p % DD_SLOTS];
+        hipStream_t ls = r.st;
+        DCK(hipStreamWaitEvent(ls, c->pev[p % DD_SLOTS], 0));
+        DCK(hipStreamWaitEvent(ls, c->cev[q->slot], 0));
+        DGROW(r.U, (size_t)pc.pbytes + 64);
+        DGROW(r.status, (size_t)(pc.bl - pc.bf + 2));
+        DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
+        DGROW(r.cbase, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
+        DGROW(r.misc, 256);
+        const int64_t ocap = std::max<int64_t>((int64_t)(r.off.cap / 8) - 1, pc.pbytes / 34 + 1024);
+        DGROW(r.off, 8 * (size_t)(ocap + 1));
+        uint32_t *rb = P<uint32_t>(r.misc);
+        DCK(hipMemsetAsync(r.misc.p, 0, 64, ls));
+        DCK(hipEventRecord(r.ev[0], ls));
+        if (dd_inflate_launch(ls, P<uint8_t>(c->dcomp[q->slot]), P<DdBlock>(c->rblk) + pc.bf, pc.bl - pc.bf + 1,
+                              P<uint8_t>(r.U), pc.base, P<uint8_t>(r.status), rb + 1)) {
+            if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
+            return -1;
         }
-        // read-name ids: sort the hashes, check each equal-hash run byte for byte
+        DCK(hipEventRecord(r.ev[1], ls));
+        const int64_t nch = pc.cb - pc.ca;
+        const int64_t *Sp = P<int64_t>(c->rS) + pc.ca;
+        hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
+                           c->ws_guess, rb + 4, P<uint32_t>(r.ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, rb,
+                           (int64_t)INT64_MAX);
+        size_t tb = 0;
+        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
+        DGROW(r.tmp, tb);
+        DCK(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
+        hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
+                           c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off),
+                           rb, ocap);
+        DCK(hipGetLastError());
+        DCK(hipMemcpyAsync(r.h_small, P<uint32_t>(r.cbase) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
+        DCK(hipMemcpyAsync((char *)r.h_small + 4, P<uint32_t>(r.ccnt) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
+        DCK(hipMemcpyAsync((char *)r.h_small + 8, rb, 8, hipMemcpyDeviceToHost, ls));
+        DCK(hipMemcpyAsync((char *)r.h_small + 16, rb + 4, 4, hipMemcpyDeviceToHost, ls));
+        DCK(hipEventRecord(r.ev[2], ls));
+        return 0;
+    };
+    if (!pcs.empty() && issue(0)) return -1;
+    for (size_t p = 0; p < pcs.size(); p++) {
+        const Piece &pc = pcs[p];
+        RunSlot &r = c->rs[p % DD_SLOTS];
+        const bool ahead = parse || stats_left > 0;  // (statistics only: stop at the cap)
+        if (p + 1 < pcs.size() && ahead && issue(p + 1)) return -1;
+        DCK(hipEventSynchronize(r.ev[2]));
+        const uint32_t *hs = (const uint32_t *)r.h_small;
+        const int64_t R = (int64_t)hs[0] + hs[1];
+        c->n_rewalk += hs[4];
+        c->n_sub += (pc.u_hi - pc.u_lo + WS_G - 1) / WS_G;
+        if (hs[3]) {
+            if (err) snprintf(err, (size_t)errlen, "device inflate: %u blocks failed", hs[3]);
+            return -2;
+        }
+        if (hs[2] & ~DB_OFFCAP) {
+            if (err) snprintf(err, (size_t)errlen, "device decode: record chain (%#x) does not follow the index", hs[2]);
+            return -2;
+        }
+        if (hs[2] & DB_OFFCAP) {  // more records than the slot's capacity: the offsets again
+            DGROW(r.off, 8 * (size_t)(R + 1));
+            DCK(hipMemsetAsync(r.misc.p, 0, 4, r.st));
+            hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)(pc.cb - pc.ca)), dim3(WS_T), 0, r.st, P<uint8_t>(r.U),
+                               P<int64_t>(c->rS) + pc.ca, pc.base, pc.cb - pc.ca, q->tid, c->ws_guess, (uint32_t *)nullptr,
+                               (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), P<uint32_t>(r.misc),
+                               (int64_t)INT64_MAX);
+            DCK(hipEventRecord(r.ev[2], r.st));
+            DCK(hipEventSynchronize(r.ev[2]));
+        }
+        {
+            float a = 0, b = 0;
+            (void)hipEventElapsedTime(&a, r.ev[0], r.ev[1]);
+            (void)hipEventElapsedTime(&b, r.ev[1], r.ev[2]);
+            c->ms_inflate += a;
+            c->ms_walk += b;
+        }
+        DCK(hipStreamWaitEvent(st, r.ev[2], 0));
+        // ---- insert statistics (find_insert_mean's sample, file order) ----
+        if (stats_left > 0 && R > 0) {
+            DGROW(c->keep, 4 * (size_t)(R + 1));
+            DGROW(c->kidx, 4 * (size_t)(R + 1));
+            DGROW(c->drop, 4 * (size_t)(R + 1));
+            DGROW(c->didx, 4 * (size_t)(R + 1));
+            DGROW(c->nb, 8 * (size_t)(R + 1));
+            DBuf &sq = c->keep, &sqi = c->kidx, &sv = c->drop, &slq = c->didx, &sm = c->nb;
+            const int64_t take_cap = std::min<int64_t>(stats_left, R);
+            DGROW(c->s_ins, 4 * (size_t)take_cap);
+            DGROW(c->s_lq, 4 * (size_t)take_cap);
+            hipLaunchKernelGGL(k_stats, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(r.off), R,
+                               q->min_mapq, P<uint32_t>(sq), P<int32_t>(sv), P<int32_t>(slq), P<int64_t>(sm));
+            size_t t1 = 0, t2 = 0;
+            DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, P<uint32_t>(sq), P<uint32_t>(sqi), (int)R, st));
+            DCK(hipcub::DeviceScan::InclusiveSum(nullptr, t2, P<int64_t>(sm), P<int64_t>(sm), (int)R, st));
+            DGROW(c->tmp, std::max(t1, t2));
+            DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t1, P<uint32_t>(sq), P<uint32_t>(sqi), (int)R, st));
+            DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, t2, P<int64_t>(sm), P<int64_t>(sm), (int)R, st));
+            int64_t *mcap = (int64_t *)((char *)c->misc.p + 64);
+            DCK(hipMemsetAsync(mcap, 0xff, 8, st));
+            hipLaunchKernelGGL(k_stats_take, dim3(grid_for(R)), dim3(256), 0, st, P<uint32_t>(sq), P<uint32_t>(sqi),
+                               P<int32_t>(sv), P<int32_t>(slq), P<int64_t>(sm), R, take_cap, P<int32_t>(c->s_ins),
+                               P<int32_t>(c->s_lq), mcap);
+            DCK(hipMemcpyAsync(c->h_small, P<uint32_t>(sqi) + R - 1, 4, hipMemcpyDeviceToHost, st));
+            DCK(hipMemcpyAsync((char *)c->h_small + 4, P<uint32_t>(sq) + R - 1, 4, hipMemcpyDeviceToHost, st));
+            DCK(hipMemcpyAsync(c->h_small + 1, P<int64_t>(sm) + R - 1, 8, hipMemcpyDeviceToHost, st));
+            DCK(hipMemcpyAsync(c->h_small + 2, mcap, 8, hipMemcpyDeviceToHost, st));
+            DCK(hipStreamSynchronize(st));
+            const uint32_t *hs = (const uint32_t *)c->h_small;
+            const int64_t nq = (int64_t)hs[0] + hs[1];
+            const int64_t n = std::min<int64_t>(nq, stats_left);
+            if (n > 0) {
+                DCK(hipMemcpyAsync(h_ins, c->s_ins.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+                DCK(hipMemcpyAsync(h_lq, c->s_lq.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+                DCK(hipStreamSynchronize(st));
+            }
+            const int complete = nq >= stats_left;
+            const int64_t m = complete ? c->h_small[2] : c->h_small[1];
+            stats_left -= n;
+            h_ins += n;
+            h_lq += n;
+            if (q->stats_cb) q->stats_cb(q->stats_arg, n, m, complete);
+        }
+        // ---- parse into the stage ----
+        if (parse && R > 0) {
+            const int64_t j0l = q->j0 - R_tot;  // the run's first record to take, in this piece
+            const size_t p4 = 4 * (size_t)(R + 1), p8 = 8 * (size_t)(R + 1);
+            DGROW(c->keep, p4); DGROW(c->kidx, p4); DGROW(c->drop, p4); DGROW(c->didx, p4); DGROW(c->auxc, p4);
+            DGROW(c->aidx, p4); DGROW(c->ncig, p4); DGROW(c->coff, p4); DGROW(c->nml, p4); DGROW(c->nmo, p4);
+            DGROW(c->nb, p8); DGROW(c->boff, p8); DGROW(c->rpos, p4);
+            hipLaunchKernelGGL(k_rec_meta, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(r.off), R,
+                               std::max<int64_t>(j0l, 0), q->tid, P<uint32_t>(c->keep), P<uint32_t>(c->drop),
+                               P<uint32_t>(c->auxc), P<uint32_t>(c->ncig), P<int64_t>(c->nb), P<uint32_t>(c->nml),
+                               P<int32_t>(c->rpos), bad);
+            size_t t1 = 0, t2 = 0;
+            DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, P<uint32_t>(c->keep), P<uint32_t>(c->kidx), (int)R, st));
+            DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, P<int64_t>(c->nb), P<int64_t>(c->boff), (int)R, st));
+            DGROW(c->tmp, std::max(t1, t2));
+            DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t1, P<uint32_t>(c->keep), P<uint32_t>(c->kidx), (int)R, st));
+            DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t1, P<uint32_t>(c->drop), P<uint32_t>(c->didx), (int)R, st));
+            DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t1, P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), (int)R, st));
+            DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t1, P<uint32_t>(c->ncig), P<uint32_t>(c->coff), (int)R, st));
+            DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t1, P<uint32_t>(c->nml), P<uint32_t>(c->nmo), (int)R, st));
+            DCK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, t2, P<int64_t>(c->nb), P<int64_t>(c->boff), (int)R, st));
+            hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, st, P<uint32_t>(c->keep), P<uint32_t>(c->kidx),
+                               P<uint32_t>(c->drop), P<uint32_t>(c->didx), P<uint32_t>(c->auxc), P<uint32_t>(c->aidx),
+                               P<uint32_t>(c->ncig), P<uint32_t>(c->coff), P<int64_t>(c->nb), P<int64_t>(c->boff),
+                               P<uint32_t>(c->nml), P<uint32_t>(c->nmo), R, tot);
+            DCK(hipMemcpyAsync(c->h_small, tot, 6 * 8, hipMemcpyDeviceToHost, st));
+            DCK(hipMemcpyAsync(c->h_small + 6, bad, 8, hipMemcpyDeviceToHost, st));
+            DCK(hipStreamSynchronize(st));
+            const int64_t n = c->h_small[0], nd = c->h_small[1], na = c->h_small[2], ncg = c->h_small[3];
+            const int64_t nbs = c->h_small[4], nmb = c->h_small[5];
+            if (((const uint32_t *)(c->h_small + 6))[0]) {
+                if (err) snprintf(err, (size_t)errlen, "device decode: records do not parse as the run's (%#x)",
+                                  ((const uint32_t *)(c->h_small + 6))[0]);
+                return -2;
+            }
+            // the stage: the first piece sizes it for the whole run from its
+            // own shares (+6%), later pieces grow it when the run outgrows that
+            grom_stage_sizes need{};
+            need.n = have.n + n;
+            need.n_drop = have.n_drop + nd;
+            need.n_cigar_ops = have.n_cigar_ops + ncg;
+            need.n_bases = have.n_bases + nbs;
+            need.n_aux = 1;
+            need.ref_len = q->ref_len;
+            if (p == 0 && q->count > R) {
+                const double f = (double)q->count / (double)R * 1.02;
+                cap.n = (int64_t)(f * (double)n) + 1024;
+                cap.n_drop = (int64_t)(f * (double)nd) + 1024;
+                cap.n_cigar_ops = (int64_t)(f * (double)ncg) + 1024;
+                cap.n_bases = ((int64_t)(f * (double)nbs) + 1024) & ~(int64_t)1;
+                cap.n_aux = 1;
+                cap.ref_len = q->ref_len;
+            }
+            if (need.n > cap.n || need.n_drop > cap.n_drop || need.n_cigar_ops > cap.n_cigar_ops ||
+                need.n_bases > cap.n_bases || p == 0) {
+                cap.n = std::max(cap.n, need.n);
+                cap.n_drop = std::max(cap.n_drop, need.n_drop);
+                cap.n_cigar_ops = std::max(cap.n_cigar_ops, need.n_cigar_ops);
+                cap.n_bases = std::max(cap.n_bases, need.n_bases);
+                cap.n_aux = 1;
+                cap.ref_len = q->ref_len;
+                if (grom_stage_fill_ensure(q->stage, &cap, &have, &dv) != GROM_OK) {
+                    if (err) snprintf(err, (size_t)errlen, "%s", grom_last_error());
+                    return -1;
+                }
+            }
+            // the chromosome's name bytes and hash arrays
+            const int64_t nm_cap = p == 0 && q->count > R ? (int64_t)((double)nmb * (double)q->count / (double)R * 1.02)
+                                                          : car.nm + nmb;
+            if (dgrow_keep(c->nm, (size_t)std::max<int64_t>(nm_cap, car.nm + nmb) + 64, (size_t)car.nm, st) ||
+                dgrow_keep(c->nmoff, 8 * (size_t)(cap.n + 2), 8 * (size_t)car.k, st) ||
+                dgrow_keep(c->keys, 8 * (size_t)(cap.n + 1), 8 * (size_t)car.k, st) ||
+                dgrow_keep(c->vals, 4 * (size_t)(cap.n + 1), 4 * (size_t)car.k, st)) {
+                if (err) snprintf(err, (size_t)errlen, "device decode: hipMalloc failed (name arrays)");
+                return -1;
+            }
+            DGROW(c->srcs, 8 * (size_t)(n + 1));
+            DGROW(c->acand, 8 * (size_t)(na + 2)); DGROW(c->alen, 8 * (size_t)(na + 2)); DGROW(c->aoff, 8 * (size_t)(na + 2));
+            DGROW(c->akidx, 8 * (size_t)(na + 2));
+            StageOut so;
+            so.pos = (int32_t *)dv.pos; so.mtid = (int32_t *)dv.mtid; so.mpos = (int32_t *)dv.mpos;
+            so.isize = (int32_t *)dv.isize; so.lq = (int32_t *)dv.l_qseq; so.aidx = (int32_t *)dv.aux_idx;
+            so.flag = (uint16_t *)dv.flag; so.mapq = (uint8_t *)dv.mapq; so.coff = (uint32_t *)dv.cigar_off;
+            so.cig = (uint32_t *)dv.cigar; so.nid = (uint32_t *)dv.name_id; so.boff = (int64_t *)dv.base_off;
+            so.dpos = (int32_t *)dv.drop_pos; so.dlq = (int32_t *)dv.drop_lq; so.dbef = (int64_t *)dv.drop_before;
+            hipLaunchKernelGGL(k_rec_write, dim3(grid_for(R)), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(r.off), R,
+                               j0l, P<uint32_t>(c->keep), P<uint32_t>(c->kidx), P<uint32_t>(c->drop), P<uint32_t>(c->didx),
+                               P<uint32_t>(c->auxc), P<uint32_t>(c->aidx), P<uint32_t>(c->coff), P<int64_t>(c->boff),
+                               P<uint32_t>(c->nmo), P<int32_t>(c->rpos), so, car, P<int64_t>(c->srcs),
+                               P<uint8_t>(c->nm), P<int64_t>(c->nmoff), P<uint64_t>(c->keys), P<uint32_t>(c->vals),
+                               P<int64_t>(c->acand), q->read_name_len, d_last, bad);
+            if (n > 0) {  // the bases and qualities of the piece's kept reads
+                const int64_t lo = car.b, hi = car.b + nbs;
+                const int64_t nt_q = (hi + CP_T - 1) / CP_T - lo / CP_T, nt_s = (hi / 2 + CP_T - 1) / CP_T - (lo / 2) / CP_T;
+                DGROW(c->tfq, 8 * (size_t)(nt_q + 1));
+                DGROW(c->tfs, 8 * (size_t)(nt_s + 1));
+                hipLaunchKernelGGL(k_tile_first, dim3(grid_for(n)), dim3(256), 0, st, (const int64_t *)so.boff,
+                                   (const int32_t *)so.lq, car.k, n, lo, P<int64_t>(c->tfq), P<int64_t>(c->tfs));
+                if (nt_q > 0)
+                    hipLaunchKernelGGL(k_copy_tiles<true>, dim3((unsigned)std::min<int64_t>(nt_q, 1 << 16)), dim3(256), 0, st,
+                                       P<uint8_t>(r.U), P<int64_t>(c->srcs), (const int64_t *)so.boff, (const int32_t *)so.lq,
+                                       car.k, n, P<int64_t>(c->tfq), nt_q, lo, hi, c->cp_cap, (uint8_t *)dv.qual);
+                if (nt_s > 0)
+                    hipLaunchKernelGGL(k_copy_tiles<false>, dim3((unsigned)std::min<int64_t>(nt_s, 1 << 16)), dim3(256), 0,
+                                       st, P<uint8_t>(r.U), P<int64_t>(c->srcs), (const int64_t *)so.boff,
+                                       (const int32_t *)so.lq, car.k, n, P<int64_t>(c->tfs), nt_s, lo / 2, hi / 2,
+                                       c->cp_cap, (uint8_t *)dv.seq);
+            }
+            // split-read candidates: lengths, offsets, kept indices, packed bytes -> host
+            if (na > 0) {
+                hipLaunchKernelGGL(k_aux_len, dim3(grid_for(na)), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(r.off),
+                                   P<int64_t>(c->acand), na, P<int64_t>(c->alen), P<uint32_t>(c->kidx),
+                                   P<int64_t>(c->akidx));
+                size_t t3 = 0;
+                DCK(hipcub::DeviceScan::InclusiveSum(nullptr, t3, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
+                DGROW(c->tmp, t3);
+                DCK(hipMemsetAsync(c->aoff.p, 0, 8, st));
+                DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, t3, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
+                DCK(hipMemcpyAsync(c->h_small + 8, P<int64_t>(c->aoff) + na, 8, hipMemcpyDeviceToHost, st));
+            }
+            DCK(hipMemcpyAsync(c->h_small, d_last, 16, hipMemcpyDeviceToHost, st));
+            DCK(hipMemcpyAsync(c->h_small + 2, bad, 8, hipMemcpyDeviceToHost, st));
+            DCK(hipStreamSynchronize(st));
+            memcpy(last, c->h_small, 16);
+            if (((const uint32_t *)(c->h_small + 2))[0]) {
+                const uint32_t b1 = ((const uint32_t *)(c->h_small + 2))[0];
+                if (err) snprintf(err, (size_t)errlen, "device decode: %s (%#x)",
+                                  (b1 & DB_UNSORTED) ? "records are not sorted by position" : "record check failed", b1);
+                return -2;
+            }
+            if (na > 0) {
+                const int64_t apack = c->h_small[8];
+                DGROW(c->apack, (size_t)apack + 16);
+                hipLaunchKernelGGL(k_aux_pack, dim3(grid_for(na, 1, 65536)), dim3(64), 0, st, P<uint8_t>(r.U),
+                                   P<int64_t>(r.off), P<int64_t>(c->acand), P<int64_t>(c->aoff), na, P<uint8_t>(c->apack));
+                const size_t ab0 = aux_bytes.size(), ao0 = aux_off.size(), ak0 = aux_kidx.size();
+                aux_bytes.resize(ab0 + (size_t)apack);
+                aux_off.resize(ao0 + (size_t)na);
+                aux_kidx.resize(ak0 + (size_t)na);
+                DCK(hipMemcpyAsync(aux_bytes.data() + ab0, c->apack.p, (size_t)apack, hipMemcpyDeviceToHost, st));
+                DCK(hipMemcpyAsync(aux_off.data() + ao0, P<int64_t>(c->aoff) + 1, 8 * (size_t)na, hipMemcpyDeviceToHost, st));
+                DCK(hipMemcpyAsync(aux_kidx.data() + ak0, c->akidx.p, 8 * (size_t)na, hipMemcpyDeviceToHost, st));
+                DCK(hipStreamSynchronize(st));
+                for (size_t k = ao0; k < ao0 + (size_t)na; k++) aux_off[k] += apack_tot;  // run-wide offsets
+                for (size_t k = ak0; k < ak0 + (size_t)na; k++) aux_kidx[k] += car.k;    // kept index in the chromosome
+                apack_tot += apack;
+                n_aux += na;
+            }
+            // the carries for the next piece
+            car.k += n;
+            car.d += nd;
+            car.cig += ncg;
+            car.b += nbs;
+            car.nm += nmb;
+            car.prev_pos = last[0];
+            car.has_prev = 1;
+            have.n = car.k;
+            have.n_drop = car.d;
+            have.n_cigar_ops = car.cig;
+            have.n_bases = car.b;
+        }
+        DCK(hipEventRecord(c->pev[p % DD_SLOTS], st));  // the slot's piece is done with
+        R_tot += R;
+        if (!parse && stats_left <= 0) break;  // statistics only: the cap is reached
+    }
+    for (int k = 0; k < DD_SLOTS; k++) DCK(hipStreamSynchronize(c->rs[k].st));  // (a load issued ahead)
+    *n_rec = R_tot;
+    po->n_rec = R_tot;
+    if (!parse) return 0;
+    // ---- after the last piece: the stage's final counts, the name ids ----
+    const int64_t n = car.k;
+    DCK(hipEventRecord(c->ev[2], st));
+    grom_stage_sizes fin{};
+    fin.n = n;
+    fin.n_drop = car.d;
+    fin.n_cigar_ops = car.cig;
+    fin.n_bases = car.b;
+    fin.ref_len = q->ref_len;
+    if (grom_stage_fill_ensure(q->stage, &fin, &have, &dv) != GROM_OK || grom_stage_fill_set(q->stage, &fin) != GROM_OK) {
+        if (err) snprintf(err, (size_t)errlen, "%s", grom_last_error());
+        return -1;
+    }
+    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, st, (uint32_t *)dv.cigar_off + n, (uint32_t)car.cig);
+    if (n > 0) {
+        DCK(hipMemcpyAsync(P<int64_t>(c->nmoff) + n, &car.nm, 8, hipMemcpyHostToDevice, st));
+        DGROW(c->keys2, 8 * (size_t)(n + 1));
+        DGROW(c->vals2, 4 * (size_t)(n + 1));
+        DGROW(c->head, 4 * (size_t)(n + 1));
         size_t tb = 0, t2 = 0;
         DCK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, P<uint64_t>(c->keys), P<uint64_t>(c->keys2),
                                                P<uint32_t>(c->vals), P<uint32_t>(c->vals2), (int)n, 0, 64, st));
-        DCK(hipcub::DeviceScan::InclusiveScan(nullptr, t2, P<uint32_t>(c->head), P<uint32_t>(c->head),
-                                              hipcub::Max(), (int)n, st));
+        DCK(hipcub::DeviceScan::InclusiveScan(nullptr, t2, P<uint32_t>(c->head), P<uint32_t>(c->head), hipcub::Max(),
+                                              (int)n, st));
         DGROW(c->tmp, std::max(tb, t2));
         DCK(hipcub::DeviceRadixSort::SortPairs(c->tmp.p, tb, P<uint64_t>(c->keys), P<uint64_t>(c->keys2),
                                                P<uint32_t>(c->vals), P<uint32_t>(c->vals2), (int)n, 0, 64, st));
@@ -1365,71 +1596,36 @@ extern "C" int dd_run_parse(dd_ctx *c, int slot, int64_t j0, int32_t tid, int32_
                            P<uint32_t>(c->head));
         DCK(hipcub::DeviceScan::InclusiveScan(c->tmp.p, t2, P<uint32_t>(c->head), P<uint32_t>(c->head), hipcub::Max(),
                                               (int)n, st));
-        hipLaunchKernelGGL(k_name_ids, dim3(grid_for(n)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off),
-                           P<int64_t>(c->krec), P<uint64_t>(c->keys2), P<uint32_t>(c->vals2), P<uint32_t>(c->head), n,
-                           so.nid, bad);
+        hipLaunchKernelGGL(k_name_ids, dim3(grid_for(n)), dim3(256), 0, st, P<uint8_t>(c->nm), P<int64_t>(c->nmoff),
+                           P<uint64_t>(c->keys2), P<uint32_t>(c->vals2), P<uint32_t>(c->head), n,
+                           (uint32_t *)dv.name_id, bad);
     }
-    // split-read candidates: lengths, offsets, kept indices, packed bytes -> host
-    int64_t apack = 0;
-    if (na > 0) {
-        hipLaunchKernelGGL(k_aux_len, dim3(grid_for(na)), dim3(256), 0, st, P<uint8_t>(rs.U), P<int64_t>(rs.off),
-                           P<int64_t>(c->acand), na, P<int64_t>(c->alen), P<uint32_t>(c->kidx), P<int64_t>(c->akidx));
-        size_t tb = 0;
-        DCK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
-        DGROW(c->tmp, tb);
-        DCK(hipMemsetAsync(c->aoff.p, 0, 8, st));
-        DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, tb, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
-    }
-    DCK(hipMemcpyAsync(c->h_small, last, 16, hipMemcpyDeviceToHost, st));
-    DCK(hipMemcpyAsync(c->h_small + 2, bad, 8, hipMemcpyDeviceToHost, st));
-    if (na > 0) DCK(hipMemcpyAsync(c->h_small + 3, P<int64_t>(c->aoff) + na, 8, hipMemcpyDeviceToHost, st));
-    DCK(hipStreamSynchronize(st));
-    const int32_t *hl = (const int32_t *)c->h_small;
-    const uint32_t b1 = ((const uint32_t *)(c->h_small + 2))[0];
-    if (b1) {
-        if (err) snprintf(err, (size_t)errlen, "device decode: %s (%#x)",
-                          (b1 & DB_NAMES) ? "read-name hash collision" : (b1 & DB_UNSORTED) ? "records are not sorted by position"
-                                                                                               : "record check failed",
-                          b1);
-        return -2;
-    }
-    po->n_rec = R;
-    po->n_kept = n;
-    po->n_drop = nd;
-    po->n_cig = ncg;
-    po->n_bases = nbs;
-    po->n_auxc = na;
-    po->last_pos = hl[0];
-    po->last_lq = hl[1];
-    po->last_hclip = hl[2];
-    po->last_kept = hl[3];
-    if (na > 0) {
-        apack = c->h_small[3];
-        DGROW(c->apack, (size_t)apack + 16);
-        hipLaunchKernelGGL(k_aux_pack, dim3(grid_for(na, 1, 65536)), dim3(64), 0, st, P<uint8_t>(rs.U),
-                           P<int64_t>(rs.off), P<int64_t>(c->acand), P<int64_t>(c->aoff), na, P<uint8_t>(c->apack));
-        const size_t need = (((size_t)apack + 15) & ~(size_t)15) + 16 * (size_t)(na + 1) + 64;
-        if (need > c->h_aux_cap) {
-            if (c->h_aux) (void)hipHostFree(c->h_aux);
-            c->h_aux = nullptr;
-            c->h_aux_cap = need + need / 4;
-            DCK(hipHostMalloc((void **)&c->h_aux, c->h_aux_cap, 0));
-        }
-        // host buffer: [packed records][offsets, na + 1][kept index of each]
-        int64_t *ho = (int64_t *)(c->h_aux + (((size_t)apack + 15) & ~(size_t)15));
-        DCK(hipMemcpyAsync(c->h_aux, c->apack.p, (size_t)apack, hipMemcpyDeviceToHost, st));
-        DCK(hipMemcpyAsync(ho, c->aoff.p, 8 * (size_t)(na + 1), hipMemcpyDeviceToHost, st));
-        DCK(hipMemcpyAsync(ho + na + 1, c->akidx.p, 8 * (size_t)na, hipMemcpyDeviceToHost, st));
-        DCK(hipStreamSynchronize(st));
-        po->aux_bytes = c->h_aux;
-        po->aux_off = ho;
-        po->aux_kidx = ho + na + 1;
-    }
+    DCK(hipMemcpyAsync(c->h_small, bad, 8, hipMemcpyDeviceToHost, st));
     DCK(hipEventRecord(c->ev[3], st));
     DCK(hipStreamSynchronize(st));
+    if (((const uint32_t *)c->h_small)[0] & DB_NAMES) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: read-name hash collision (%#x)", ((const uint32_t *)c->h_small)[0]);
+        return -2;
+    }
     float d = 0;
     (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
     c->ms_parse += d;
+    po->n_kept = n;
+    po->n_drop = car.d;
+    po->n_cig = car.cig;
+    po->n_bases = car.b;
+    po->n_auxc = n_aux;
+    po->last_pos = last[0];
+    po->last_lq = last[1];
+    po->last_hclip = last[2];
+    po->last_kept = last[3];
+    // the split-read candidates (host): the context keeps them until the next run
+    c->aux_bytes.swap(aux_bytes);
+    c->aux_off.swap(aux_off);
+    c->aux_kidx.swap(aux_kidx);
+    po->aux_bytes = c->aux_bytes.data();
+    po->aux_off = c->aux_off.data();
+    po->aux_kidx = c->aux_kidx.data();
     return 0;
 }
 

@@ -353,12 +353,25 @@ __device__ __forceinline__ bool fast_read(const ReadView &v) {
     return v.ncig == 1 && (op == 0 || op == 7 || op == 8);
 }
 
+// Byte b of a staged LDS array, read as its whole dword and shifted: lanes
+// of a wave look up consecutive bytes of one read (consecutive positions),
+// and whole-dword reads of one address broadcast, where byte reads of
+// neighbouring bytes of a dword are told apart by address (GROM_LDS_BYTE=1:
+// the byte reads, for A/B)
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t *w, int32_t b) {
+#if defined(GROM_LDS_BYTE) && GROM_LDS_BYTE
+    return reinterpret_cast<const uint8_t *>(w)[b];
+#else
+    return (w[b >> 2] >> ((b & 3) << 3)) & 0xffu;
+#endif
+}
+
 // quality byte and 4-bit base (BAM nibble order) of staged base `rel`
 // (relative to the window start, which is a multiple of 16)
-__device__ __forceinline__ void staged_base(const uint8_t *lq8, const uint8_t *ls8, int32_t soff, int32_t rel,
+__device__ __forceinline__ void staged_base(const uint32_t *lq, const uint32_t *ls, int32_t soff, int32_t rel,
                                             uint32_t &q, uint32_t &sbyte) {
-    q = lq8[rel];
-    sbyte = ls8[soff + (rel >> 1)];
+    q = lds_byte(lq, rel);
+    sbyte = lds_byte(ls, soff + (rel >> 1));
 }
 
 // The outputs of position x (one lane per position; every lane of the
@@ -578,8 +591,8 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
     // the fast path's lane position: outside the evaluated range no read's
     // offset (x - pos, unsigned) falls inside it, so no base is tallied
     const int32_t xe = evals ? x : (int32_t)(INT32_MIN / 2);
-    const uint8_t *lq8 = reinterpret_cast<const uint8_t *>(L.qual);
-    const uint8_t *ls8 = reinterpret_cast<const uint8_t *>(L.seq);
+    const uint32_t *lq32 = reinterpret_cast<const uint32_t *>(L.qual);
+    const uint32_t *ls32 = reinterpret_cast<const uint32_t *>(L.seq);
 
     typename std::conditional<PK, PackedCounts, LaneCounts>::type c = {};
     MatchCounts mc = {0, 0, 0, 0};
@@ -737,8 +750,8 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
                         fdx[k] = (uint32_t)(xe - fp[k]);
                         fhit[k] = fdx[k] < (uint32_t)fl[k];
                         const int32_t r = fhit[k] ? fb[k] + (int32_t)fdx[k] : 0;
-                        fq[k] = lq8[r];
-                        fs4[k] = (uint32_t)ls8[soff + (r >> 1)] >> ((((uint32_t)r & 1u) ^ 1u) << 2);
+                        fq[k] = lds_byte(lq32, r);
+                        fs4[k] = lds_byte(ls32, soff + (r >> 1)) >> ((((uint32_t)r & 1u) ^ 1u) << 2);
                     }
 #pragma unroll
                     for (int k = 0; k < FR; k++) {
@@ -893,7 +906,7 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
                         int odd = (u.bo + hit_qi) & 1;
                         {
                             if (staged) {
-                                staged_base(lq8, ls8, soff, u.bo + hit_qi, qb, sbv);
+                                staged_base(lq32, ls32, soff, u.bo + hit_qi, qb, sbv);
                             } else {
                                 const int64_t nib = qb0 + u.bo + (int64_t)hit_qi;
                                 qb = R.qual[nib];

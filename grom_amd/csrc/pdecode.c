@@ -2045,15 +2045,10 @@ void pd_set_wanted(pd_session *s, const int *want) {
 /* A worker's compressed runs are read one ahead by its prefetch thread: the
  * run's bytes by pread into a pinned slot, its block table and record starts
  * on the host, and the copy to the device slot of the same number started on
- * the decode context's copy stream -- all while the GPU inflates and parses
- * the run before it.  The worker takes a slot, loads it (dd_run_load) and
- * releases it; a run nobody takes is simply read again when needed.
- *
- * With room on the device for two runs (w->preload) the prefetch thread also
- * loads the run -- inflate and record walk into the run slot of the same
- * number, on that slot's stream -- while the worker parses the run before it
- * from the other run slot; the worker then holds its slot until the parse is
- * done. */
+ * the decode context's copy stream -- all while the GPU decodes the run
+ * before it.  The worker takes a slot, decodes the run piece by piece
+ * (dd_run_decode) and releases it; a run nobody takes is simply read again
+ * when needed. */
 enum { PF_FREE = 0, PF_WANTED = 1, PF_READY = 2, PF_USED = 3 };
 typedef struct {
     int ri, state, rc;
@@ -2065,9 +2060,6 @@ typedef struct {
     int64_t *starts;
     int64_t starts_cap, m, u_end;
     double t_io;
-    int loaded;              /* preload: the run is in the run slot of this number */
-    int64_t R;
-    double t_load;
 } pf_slot;
 
 typedef struct {
@@ -2080,11 +2072,6 @@ typedef struct {
     pthread_cond_t cv;
     pthread_t pf_thr;
     int pf_started, pf_stop;
-    int loaded;              /* run index whose records dd holds, -1 none */
-    int64_t loaded_R;
-    int loaded_slot;         /* ... in this run slot */
-    int preload;             /* the prefetch thread loads runs too (two run slots reserved) */
-    pf_slot *held;           /* preload: the slot whose run the worker is using */
     int test_abort, n_done;  /* GROM_TEST_DD_ABORT=n: -2 at the n-th chromosome (tests) */
 } dd_worker;
 
@@ -2139,42 +2126,12 @@ static int cmp_i64(const void *a, const void *b) {
     return x < y ? -1 : x > y;
 }
 
-/* The insert statistics need the first PD_INSERT_CAP qualifying records in
- * file order (find_insert_mean, GROM.c:1205-1318) -- about half of the
- * records qualify (one mate of each proper pair), so at 30x the first 40% of
- * chr1's run.  The first stats load is that prefix of the run: its end a
- * linear-index record start (a record boundary the index names) at the share
- * of the run's 16 kb windows that holds ~2.6x the cap's records.  UINT64_MAX:
- * no prefix (the run is small, or the index gives no cut inside it). */
-static uint64_t stats_prefix_end(const pd_session *s, int ri) {
-    const pd_run *r = &s->runs[ri];
-    const int64_t want = s->prefix_records > 0 ? s->prefix_records : (int64_t)(2.6 * s->insert_cap);
-    if (r->tid < 0 || r->tid >= s->n_tgt || r->count < 0 || r->count <= want + want / 4) return UINT64_MAX;
-    const int nl = s->n_lin[r->tid];
-    int lo = -1, hi = -1; /* the run's linear entries */
-    for (int k = 0; k < nl; k++) {
-        const uint64_t v = s->lin[r->tid][k];
-        if (v <= r->vbeg || v >= r->vend) continue;
-        if (lo < 0) lo = k;
-        hi = k;
-    }
-    if (lo < 0) return UINT64_MAX;
-    const int k = lo + (int)((double)(hi - lo) * (double)want / (double)r->count);
-    for (int q = k; q <= hi; q++) { /* the first entry at or after k inside the run */
-        const uint64_t v = s->lin[r->tid][q];
-        if (v > r->vbeg && v < r->vend) return v;
-    }
-    return UINT64_MAX;
-}
-
 /* a run's compressed bytes into a pinned slot, its block table and record
- * starts, and the slot's copy to the device started (prefetch thread); key =
- * the run, or -(run + 2) for its insert-statistics prefix */
-static int pf_read(dd_worker *w, pf_slot *sl, int slot_no, int key, char *err, int errlen) {
+ * starts, and the slot's copy to the device started (prefetch thread) */
+static int pf_read(dd_worker *w, pf_slot *sl, int slot_no, int ri, char *err, int errlen) {
     pd_session *s = w->s;
-    const int ri = key >= 0 ? key : -key - 2;
     const pd_run *r = &s->runs[ri];
-    const uint64_t vend = key >= 0 ? r->vend : stats_prefix_end(s, ri);
+    const uint64_t vend = r->vend;
     const int64_t c0 = (int64_t)(r->vbeg >> 16);
     int64_t c1;
     if (vend == UINT64_MAX) {
@@ -2267,19 +2224,8 @@ static void *pf_main(void *arg) {
         pthread_mutex_unlock(&w->mu);
         char err[200] = "";
         pd_trace(w->s, PD_EV_PHASE, 101, 0);
-        int rc = pf_read(w, sl, q, ri, err, (int)sizeof(err));
+        const int rc = pf_read(w, sl, q, ri, err, (int)sizeof(err));
         pd_trace(w->s, PD_EV_PHASE, 101, 1);
-        sl->loaded = 0;
-        if (rc == 0 && __atomic_load_n(&w->preload, __ATOMIC_ACQUIRE)) {
-            const int rk = ri >= 0 ? ri : -ri - 2;
-            const double t0 = now_s();
-            pd_trace(w->s, PD_EV_PHASE, 102, 0);
-            rc = dd_run_load(w->dd, q, q, sl->len, sl->blk, sl->nb, sl->ub, sl->starts, sl->m, sl->u_end,
-                             w->s->runs[rk].tid, &sl->R, err, (int)sizeof(err));
-            pd_trace(w->s, PD_EV_PHASE, 102, 1);
-            sl->t_load = now_s() - t0;
-            sl->loaded = rc == 0;
-        }
         pthread_mutex_lock(&w->mu);
         sl->rc = rc;
         snprintf(sl->err, sizeof(sl->err), "%s", err);
@@ -2345,60 +2291,77 @@ static void pf_release(dd_worker *w, pf_slot *sl) {
     pthread_mutex_unlock(&w->mu);
 }
 
-/* a run's records loaded on the device (inflate + record walk), its
- * compressed bytes from the prefetcher; then `next` (the run this worker
- * needs after it, -1 none) is asked for */
-static void dw_unhold(dd_worker *w) {
-    if (w->held) pf_release(w, w->held);
-    w->held = NULL;
+/* the statistics' progress (dd_run_decode's callback, the first worker):
+ * find_insert_mean's sample grows by `taken` pairs; complete: the cap */
+static void dw_stats_cb(void *arg, int64_t taken, int64_t m, int complete) {
+    pd_session *s = (pd_session *)arg;
+    pthread_mutex_lock(&s->mu);
+    s->s_n += taken;
+    s->s_m += m;
+    pthread_mutex_unlock(&s->mu);
+    if (complete) mark_stats_done(s);
 }
 
-static int dw_load(dd_worker *w, int key, int next, char *err, int errlen) {
+/* run ri decoded on the device from the prefetcher's compressed bytes (then
+ * `next`, the run this worker needs after it, -1 none, is asked for): parsed
+ * into `stage` (NULL: the insert statistics only), the statistics' sample
+ * taken from it while `stats` and the cap is not reached */
+static int dw_decode(dd_worker *w, int ri, int next, grom_stage *stage, int64_t j0, int64_t ref_len, int stats,
+                     dd_parse_out *po, int64_t *n_rec, char *err, int errlen) {
     pd_session *s = w->s;
-    const int ri = key >= 0 ? key : -key - 2;
     const pd_run *r = &s->runs[ri];
     int q = 0, rc = 0;
-    dw_unhold(w);
-    w->loaded = -1;
     const double tw = now_s();
-    pf_slot *sl = pf_take(w, key, &q, &rc, err, errlen);
+    pf_slot *sl = pf_take(w, ri, &q, &rc, err, errlen);
     const double t1 = now_s();
     if (rc) { pf_release(w, sl); return rc; }
     pf_want(w, next);
-    int64_t R = 0;
-    const int rs = w->preload ? q : 0;
-    double tdec = 0;
-    if (sl->loaded) {
-        R = sl->R;
-        tdec = sl->t_load;
-    } else {
-        pd_trace(s, PD_EV_PHASE, 102, 0);
-        rc = dd_run_load(w->dd, q, rs, sl->len, sl->blk, sl->nb, sl->ub, sl->starts, sl->m, sl->u_end, r->tid, &R, err,
-                         errlen);
-        pd_trace(s, PD_EV_PHASE, 102, 1);
-        tdec = now_s() - t1;
+    dd_run_req rq;
+    memset(&rq, 0, sizeof(rq));
+    rq.slot = q;
+    rq.comp_len = sl->len;
+    rq.blk = sl->blk;
+    rq.nblk = sl->nb;
+    rq.starts = sl->starts;
+    rq.n_starts = sl->m;
+    rq.u_end = sl->u_end;
+    rq.tid = r->tid;
+    rq.j0 = j0;
+    rq.read_name_len = s->read_name_len;
+    rq.ref_len = ref_len;
+    rq.count = r->count;
+    rq.stage = stage;
+    if (stats && !s->stats_done) {
+        rq.stats_left = s->insert_cap - s->s_n;
+        rq.min_mapq = s->min_mapq_stats;
+        rq.h_ins = s->s_ins + s->s_n;
+        rq.h_lq = s->s_lq + s->s_n;
+        rq.stats_cb = dw_stats_cb;
+        rq.stats_arg = s;
     }
+    int64_t R = 0;
+    pd_trace(s, PD_EV_PHASE, 102, 0);
+    rc = dd_run_decode(w->dd, &rq, po, &R, err, errlen);
+    pd_trace(s, PD_EV_PHASE, 102, 1);
+    const double tdec = now_s() - t1;
     const int64_t len = sl->len, ub = sl->ub;
     const double tio = sl->t_io;
-    if (w->preload && rc == 0) w->held = sl; /* the run slot stays this run's until it is parsed */
-    else pf_release(w, sl);
+    pf_release(w, sl);
     if (rc) return rc;
-    if (key >= 0 && r->count >= 0 && R != r->count) {
+    if (stage && r->count >= 0 && R != r->count) {
         snprintf(err, (size_t)errlen, "target %d: %lld records decoded, the index counts %lld", r->tid, (long long)R,
                  (long long)r->count);
         return -2;
     }
     pthread_mutex_lock(&s->mu);
-    s->c_records += R;
+    s->c_records += stage ? R : 0;
     s->c_inflated += ub;
     s->c_compressed += len;
     s->c_io_s += tio;
     s->c_wait_s += t1 - tw;
     s->c_dec_s += tdec;
     pthread_mutex_unlock(&s->mu);
-    w->loaded = key;  /* a prefix (key < -1) is never taken for the whole run */
-    w->loaded_R = R;
-    w->loaded_slot = rs;
+    *n_rec = R;
     return 0;
 }
 
@@ -2514,7 +2477,8 @@ static void *stres_body(stres_job *j) {
 /* The decode buffers sized once, while the first run is read: the largest
  * record count the index gives for a run this worker may load, and its
  * largest compressed span times the inflate ratio of the BAM's first blocks
- * (+4%).  A run beyond the estimate still grows the buffers. */
+ * (+4%): the piece slots and the chromosome-wide name arrays (dd_reserve).
+ * A run beyond the estimate still grows the buffers. */
 static int dw_reserve(dd_worker *w, char *err, int errlen) {
     pd_session *s = w->s;
     int64_t recs = 0, span = 0;
@@ -2551,18 +2515,7 @@ static int dw_reserve(dd_worker *w, char *err, int errlen) {
     int64_t nst = 0;
     for (int t = 0; t < s->n_tgt; t++)
         if (s->n_lin[t] > nst) nst = s->n_lin[t];
-    /* two run slots (loads overlap parses) only on request (GROM_DD_PRELOAD=1)
-     * and when the device keeps room for them beside the stages: measured on
-     * the configs[2] whole run, the second slot's allocation and the reads
-     * serialised behind loads cost more than the overlap gains (DESIGN.md
-     * 4.5), the GPU being busy with the scans meanwhile */
-    const char *pe = getenv("GROM_DD_PRELOAD");
-    const int64_t fr = grom_device_mem_free(w->device);
-    const double need = 2.0 * ((double)ub + 8.0 * (double)recs) + (double)((int64_t)64 << 30);
-    const int two = pe && atoi(pe) != 0 && fr > 0 && (double)fr >= need;
-    const int rc = dd_reserve(w->dd, ub, recs + recs / 20, nst + 2, two ? 2 : 1, err, errlen);
-    if (rc == 0 && two) __atomic_store_n(&w->preload, 1, __ATOMIC_RELEASE);
-    return rc;
+    return dd_reserve(w->dd, span, ub, recs + recs / 20, nst + 2, err, errlen);
 }
 
 /* the next run (tid >= 0) after ri in file order, -1 none */
@@ -2572,39 +2525,27 @@ static int next_placed_run(const pd_session *s, int ri) {
     return -1;
 }
 
-/* find_insert_mean's sample, runs in file order until the cap (worker of the
- * first device) */
-static int dw_stats(dd_worker *w, char *err, int errlen) {
+/* find_insert_mean's sample from the runs in file order, from run `from`,
+ * until the cap (the first worker, when the statistics' runs are not among
+ * the ones it parses): pieces of each run, the statistics only */
+static int dw_stats_only(dd_worker *w, int from, char *err, int errlen) {
     pd_session *s = w->s;
-    int first = 1;
-    for (int i = 0; i < s->n_runs && s->s_n < s->insert_cap && !s->abort; i++) {
-        if (s->runs[i].tid < 0) continue; /* unplaced: unmapped records only */
-        /* the first run: its prefix, then (if the cap was not reached there)
-         * the whole run, counted from its start again */
-        const int pre = first && stats_prefix_end(s, i) != UINT64_MAX;
-        first = 0;
-        for (int pass = pre ? 0 : 1; pass < 2; pass++) {
-            int rc = dw_load(w, pass == 0 ? -i - 2 : i, pass == 0 ? i : next_placed_run(s, i), err, errlen);
-            if (rc) return rc;
-            int64_t taken = 0, m = 0;
-            const int64_t left = s->insert_cap - s->s_n;
-            pd_trace(s, PD_EV_PHASE, 103, i);
-            rc = dd_run_stats(w->dd, w->loaded_slot, s->min_mapq_stats, left, s->s_ins + s->s_n, s->s_lq + s->s_n, &taken, &m, err,
-                              errlen);
-            if (rc) return rc;
-            if (pass == 0 && taken < left) continue; /* the prefix held too few: the whole run */
-            s->s_n += taken;
-            s->s_m += m;
-            break;
-        }
+    for (int i = from; i >= 0 && i < s->n_runs && !s->stats_done && !s->abort; i = next_placed_run(s, i)) {
+        dd_parse_out po;
+        int64_t R = 0;
+        pd_trace(s, PD_EV_PHASE, 103, i);
+        const int rc = dw_decode(w, i, next_placed_run(s, i), NULL, 0, 0, 1, &po, &R, err, errlen);
+        if (rc) return rc;
     }
-    mark_stats_done(s);
+    if (!s->stats_done) mark_stats_done(s);
     return 0;
 }
 
+static void dw_final(pd_session *s);
+
 /* one processed chromosome: its run parsed into a stage, the split-read
  * alignments parsed on the host, the walk's trims (chrom_finalize's facts) */
-static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
+static int dw_chrom(dd_worker *w, int k, int next_run, int stats, char *err, int errlen) {
     pd_session *s = w->s;
     pd_chrom *c = &s->ch[k];
     /* test hook: the plan contradicted at this worker's n-th chromosome */
@@ -2618,16 +2559,12 @@ static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
     memset(&po, 0, sizeof(po));
     int64_t j0 = 0;
     if (ri >= 0) {
-        int rc = 0;
-        if (w->loaded == ri) pf_want(w, next_run);
-        else rc = dw_load(w, ri, next_run, err, errlen);
-        if (rc) return rc;
         j0 = s->runs[ri].j0;
-        rc = dd_run_parse(w->dd, w->loaded_slot, j0, s->runs[ri].tid, s->read_name_len, s->plan[k].len, c->stage, &po,
-                          err, errlen);
-        w->loaded = -1;
-        dw_unhold(w); /* its run slot is free for the run after the next */
+        int64_t R = 0;
+        int rc = dw_decode(w, ri, next_run, c->stage, j0, s->plan[k].len, stats, &po, &R, err, errlen);
         if (rc) return rc;
+        /* the cap not reached in this run: the runs after it in file order */
+        if (stats && !s->stats_done && (rc = dw_stats_only(w, next_placed_run(s, ri), err, errlen))) return rc;
     } else {
         grom_stage_sizes sz;
         grom_reads dv;
@@ -2661,11 +2598,8 @@ static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
     int rc = 0;
     if (s->splitread && na > 0 && grom_stage_put_aux(c->stage, ax, ak, na) != GROM_OK) rc = -1;
     /* the walk's facts: wait for the insert statistics and the final plan */
-    pthread_mutex_lock(&s->mu);
-    while (!s->abort && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
-    const int ab = s->abort;
-    pthread_mutex_unlock(&s->mu);
-    if (ab) { free(ax); free(ak); return -3; }
+    dw_final(s);
+    if (s->abort) { free(ax); free(ak); return -3; }
     const int32_t s0 = s->index_start;
     int64_t sk = 0, sd = 0;
     if (rc == 0 && ri >= 0 && dd_stage_prefix(w->dd, c->stage, s0, &sk, &sd)) rc = -1;
@@ -2711,6 +2645,16 @@ static int dw_chrom(dd_worker *w, int k, int next_run, char *err, int errlen) {
     return rc;
 }
 
+/* wait for the walk's facts (the CLI's pd_set_walk, after the insert
+ * statistics) and apply the final plan once */
+static void dw_final(pd_session *s) {
+    pthread_mutex_lock(&s->mu);
+    while (!s->abort && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
+    const int need = !s->abort && !s->final_applied;
+    pthread_mutex_unlock(&s->mu);
+    if (need) apply_final(s, 0);
+}
+
 static void *dw_main(void *arg) {
     dd_worker *w = (dd_worker *)arg;
     pd_session *s = w->s;
@@ -2738,48 +2682,61 @@ static void *dw_main(void *arg) {
     for (int a = 0; a < n_lo; a++)
         if (a % w->nsub == w->sub) mine[n_mine++] = lo[a];
     free(lo);
+    /* The insert statistics (the first worker): find_insert_mean's sample is
+     * the first records in file order, so the chromosome of the first placed
+     * run is decoded first and the sample taken from its pieces as they are
+     * decoded; a worker that does not parse that run reads the statistics
+     * from it (and the runs after it) alone first. */
     const int stats_here = w->first && !s->stats_given;
-    if (rc == 0 && !stats_here && n_mine > 0) pf_want(w, s->ch[mine[0]].run);
-    if (rc == 0 && stats_here) { /* the stats prefix first: start its read now */
-        const int r0 = next_placed_run(s, -1);
-        if (r0 >= 0) pf_want(w, stats_prefix_end(s, r0) != UINT64_MAX ? -r0 - 2 : r0);
-    }
+    const int r0 = stats_here ? next_placed_run(s, -1) : -1;
+    int k0 = -1;
+    for (int i = 0; r0 >= 0 && i < n_mine && k0 < 0; i++)
+        if (s->ch[mine[i]].run == r0) {
+            k0 = mine[i];
+            for (int j = i; j > 0; j--) mine[j] = mine[j - 1];
+            mine[0] = k0;
+        }
+    const int stats_pass = stats_here && r0 >= 0 && k0 < 0;
+    if (rc == 0) pf_want(w, stats_pass ? r0 : (n_mine > 0 ? s->ch[mine[0]].run : -1));
     pd_trace(s, PD_EV_PHASE, 104, 0);
     if (rc == 0 && dw_reserve(w, err, (int)sizeof(err))) rc = -1;
     pd_trace(s, PD_EV_PHASE, 104, 1);
     /* (after the worker's own buffers: a small allocation waits behind any
-     * large one in flight) */
+     * large one in flight; a stage being reserved makes stage_acquire wait) */
     pthread_t stres_thr;
     stres_job sj = {s, w->device};
     const char *nsr = getenv("GROM_NO_STAGE_RESERVE");
     const int stres = rc == 0 && w->sub == 0 && !(nsr && atoi(nsr) == 1) &&
                       pthread_create(&stres_thr, NULL, stres_main, &sj) == 0;
-    if (rc == 0 && stats_here) rc = dw_stats(w, err, (int)sizeof(err));
-    else if (rc == 0 && w->first) mark_stats_done(s);
-    if (stres) pthread_join(stres_thr, NULL); /* the stages are the worker's again */
-    /* the final plan (which chromosomes, which records each one's run starts with) */
-    if (rc == 0) {
-        pthread_mutex_lock(&s->mu);
-        while (!s->abort && !s->walk_set) pthread_cond_wait(&s->cv, &s->mu);
-        pthread_mutex_unlock(&s->mu);
-        if (!s->abort) {
-            pthread_mutex_lock(&s->mu);
-            const int need = !s->final_applied;
-            pthread_mutex_unlock(&s->mu);
-            if (need) apply_final(s, 0);
-        }
-    }
+    if (rc == 0 && stats_pass) rc = dw_stats_only(w, r0, err, (int)sizeof(err));
+    else if (rc == 0 && w->first && (!stats_here || r0 < 0)) mark_stats_done(s);
     for (int i = 0; rc == 0 && i < n_mine && !s->abort; i++) {
         const int k = mine[i];
         pd_chrom *c = &s->ch[k];
-        if (!s->keep[k]) continue;
+        const int with_stats = stats_here && k == k0;
+        /* the final plan (which chromosomes, which records each one's run
+         * starts with) needs the statistics: the statistics' own chromosome
+         * is decoded before it (its run starts with its first record in
+         * any plan) */
+        if (!with_stats) {
+            dw_final(s);
+            if (s->abort) break;
+            if (!s->keep[k]) continue;
+        }
         int next_run = -1;
         for (int j = i + 1; j < n_mine && next_run < 0; j++)
-            if (s->keep[mine[j]]) next_run = s->ch[mine[j]].run;
+            if (!s->final_applied || s->keep[mine[j]]) next_run = s->ch[mine[j]].run;
         const double t0 = now_s();
         pd_trace(s, PD_EV_UPLOAD, k, 0);
-        rc = dw_chrom(w, k, next_run, err, (int)sizeof(err));
+        rc = dw_chrom(w, k, next_run, with_stats, err, (int)sizeof(err));
         pd_trace(s, PD_EV_UPLOAD, k, 1);
+        if (rc == 0 && with_stats) {
+            dw_final(s);
+            if (!s->abort && !s->keep[k]) { /* the final plan drops it: nobody scans it */
+                pd_release_stage(s, c->stage);
+                c->stage = NULL;
+            }
+        }
         pthread_mutex_lock(&s->mu);
         s->c_upl_s += now_s() - t0;
         if ((rc == -2 || rc == -1) && !s->abort) {
@@ -2797,8 +2754,8 @@ static void *dw_main(void *arg) {
         pthread_cond_broadcast(&s->cv);
         pthread_mutex_unlock(&s->mu);
     }
+    if (stres) pthread_join(stres_thr, NULL);
     if (rc == -2 || rc == -1) sess_abort(s, rc == -2, err);
-    dw_unhold(w);
     if (w->dd) {
         double ms[4];
         dd_ctx_times(w->dd, ms);
@@ -2856,7 +2813,6 @@ static int pd_start_device(pd_session *s) {
         w->sub = q % per;
         w->nsub = per;
         w->first = q == 0;
-        w->loaded = -1;
         w->test_abort = getenv("GROM_TEST_DD_ABORT") ? atoi(getenv("GROM_TEST_DD_ABORT")) : -1;
         w->slot[0].ri = w->slot[1].ri = -1;
         pthread_mutex_init(&w->mu, NULL);

@@ -1575,6 +1575,52 @@ int grom_stage_fill_begin(grom_stage *s, const grom_stage_sizes *sz, grom_reads 
     return GROM_OK;
 }
 
+// the piece-wise device decode (ddecode.hip): room for `need` in every array,
+// keeping what the earlier pieces wrote (`have`); the stage's counts become
+// `need` until grom_stage_fill_set gives the final ones
+int grom_stage_fill_ensure(grom_stage *s, const grom_stage_sizes *need, const grom_stage_sizes *have, grom_reads *dev) {
+    if (!s || !need || !have || !dev) { set_err("grom_stage_fill_ensure: null argument"); return GROM_E_ARG; }
+    HIPCHK(hipSetDevice(s->device));
+    grom_stage w = {}, h = {};
+    w.n = need->n;
+    w.n_cig = need->n_cigar_ops;
+    w.n_bases = need->n_bases;
+    w.n_aux = need->n_aux;
+    w.n_drop = need->n_drop;
+    w.ref_len = std::max<int64_t>(need->ref_len, 16);
+    h.n = have->n;
+    h.n_cig = have->n_cigar_ops;
+    h.n_bases = have->n_bases;
+    h.n_drop = have->n_drop;
+    size_t nd[SA_N], kp[SA_N];
+    stage_used(&w, nd);
+    nd[SA_AUX] += sizeof(grom_aux);  // the -S patch
+    stage_used(&h, kp);
+    kp[SA_COFF] = h.n > 0 ? 4 * (size_t)h.n : 0;  // (the closing entry is written last)
+    kp[SA_AUX] = 0;
+    kp[SA_REF] = 0;
+    int rc = stage_reserve(s, nd, kp, 32);
+    if (rc) return rc;
+    s->n = w.n;
+    s->n_cig = w.n_cig;
+    s->n_bases = w.n_bases;
+    s->n_aux = 0;
+    s->n_drop = w.n_drop;
+    s->bytes_h2d = 0;
+    stage_dev_view(s, dev);
+    return GROM_OK;
+}
+
+int grom_stage_fill_set(grom_stage *s, const grom_stage_sizes *sz) {
+    if (!s || !sz) { set_err("grom_stage_fill_set: null argument"); return GROM_E_ARG; }
+    s->n = sz->n;
+    s->n_cig = sz->n_cigar_ops;
+    s->n_bases = sz->n_bases;
+    s->n_aux = 0;
+    s->n_drop = sz->n_drop;
+    return GROM_OK;
+}
+
 int grom_stage_put_aux(grom_stage *s, const grom_aux *aux, const int64_t *kidx, int64_t n) {
     if (!s || n < 0 || (n > 0 && (!aux || !kidx))) { set_err("grom_stage_put_aux: bad argument"); return GROM_E_ARG; }
     if (n == 0) return GROM_OK;

@@ -711,10 +711,12 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
     guesses at raw sub-chunk offsets (almost all wrong): every sub-chunk is
     then walked again from the true chain, with the same result.  Mode "cu"
     copies every base/quality tile through its global-memory path (the one
-    tiles with more reads than LDS holds take).  Mode "p1" loads each run on
-    the prefetch thread into a second run slot while the run before it is
-    parsed (GROM_DD_PRELOAD=1); the default keeps one run slot and loads on
-    the worker."""
+    tiles with more reads than LDS holds take).  Modes "pc"/"pcu" decode each
+    run in pieces of 64 kB of inflated records (GROM_DD_PIECE_MB; the default
+    is 1 GB, one piece per run at these sizes): many piece boundaries, the
+    carries of every stage array across them, copy tiles shared by two
+    pieces (their shared dwords stored byte by byte), "pcu" with the
+    global-memory tile path as well."""
     bam, fa = synth(datadir, case, CASES[case])
     tag = f"dd_{case}{''.join(extra).replace('-', '_')}"
     run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
@@ -724,7 +726,8 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
              "g0": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "0"},
              "g2": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "2"},
              "cu": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_CP_UNSTAGED": "1"},
-             "p1": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PRELOAD": "1"}}
+             "pc": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PIECE_MB": "0.0625"},
+             "pcu": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PIECE_MB": "0.0625", "GROM_TEST_CP_UNSTAGED": "1"}}
     for mode, env in modes.items():
         capfd.readouterr()
         run_grom(datadir, bam, fa, f"g{mode}_{tag}.vcf", extra,
@@ -769,28 +772,34 @@ def test_oracle_digest_cases(datadir, case):
     assert _sha_rows(d / "o.ctx.vcf") == (rec["ctx_sha256"], rec["ctx_rows"])
 
 
-def test_device_decode_stats_prefix(datadir, capfd):
+@pytest.mark.parametrize("case,cap", [("c3_genome", "20000"), ("c3_genome", "150000"), ("cnv_multi", "20000")],
+                         ids=["cap_in_first_run", "cap_past_first_run", "first_run_not_longest"])
+def test_device_decode_stats_prefix(datadir, capfd, case, cap):
     """The device decoder takes the insert statistics (find_insert_mean,
-    GROM.c:1205-1318: the first 10^7 qualifying records in file order) from a
-    prefix of the first run, cut at a linear-index record start, and falls back
-    to the whole run when the prefix holds too few.  With the cap lowered for
-    the test (GROM_TEST_INSERT_CAP, read by both decoders) a prefix that holds
-    the cap and one that does not both give the host decoder's insert line,
-    staged inputs and outputs."""
-    bam, fa = synth(datadir, "c3_genome", CASES["c3_genome"])
+    GROM.c:1205-1318: the first 10^7 qualifying records in file order) from
+    the pieces of the first run as they are decoded for its chromosome, and
+    goes on into the runs after it (the statistics alone) when the first run
+    holds too few.  With the cap lowered for the test (GROM_TEST_INSERT_CAP,
+    read by both decoders): a cap the first run holds (reached in its first
+    pieces with 64 kB pieces) and one past it.  cnv_multi's first contig is
+    not its longest: one worker decodes it first anyway (the sample is in file
+    order), and of two workers the one that gathers the statistics does not
+    parse it (a statistics-only pass over it)."""
+    bam, fa = synth(datadir, case, CASES[case])
     extra = ["-M", "-V", "1"]
-    common = {"GROM_TEST_INSERT_CAP": "20000", "GROM_STAGE_DIGEST": "1", "GROM_VERBOSE": "1"}
+    common = {"GROM_TEST_INSERT_CAP": cap, "GROM_STAGE_DIGEST": "1", "GROM_VERBOSE": "1"}
     modes = {"host": {"GROM_DEVICE_DECODE": "0"},
-             "prefix_holds": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_PREFIX_RECORDS": "60000"},
-             "prefix_short": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_PREFIX_RECORDS": "15000"}}
+             "device": {"GROM_DEVICE_DECODE": "1"},
+             "pieces": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PIECE_MB": "0.0625"},
+             "workers": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PIECE_MB": "0.25", "GROM_DD_WORKERS": "2"}}
     got = {}
     for mode, env in modes.items():
         capfd.readouterr()
-        run_grom(datadir, bam, fa, f"pfx_{mode}.vcf", extra, env_extra=dict(common, **env))
+        run_grom(datadir, bam, fa, f"pfx_{case}_{cap}_{mode}.vcf", extra, env_extra=dict(common, **env))
         out = capfd.readouterr().out
         ins = [l for l in out.splitlines() if l.startswith(("insert mean", "insert_min_size", "median read"))]
         stages = sorted(l for l in out.splitlines() if l.startswith("stage "))
-        vcf = open(datadir / f"pfx_{mode}.vcf").read() + open(datadir / f"pfx_{mode}.ctx.vcf").read()
+        vcf = open(datadir / f"pfx_{case}_{cap}_{mode}.vcf").read() + open(datadir / f"pfx_{case}_{cap}_{mode}.ctx.vcf").read()
         got[mode] = (ins, stages, vcf)
     assert got["host"][0] and got["host"][1]
     for mode in modes:
@@ -798,7 +807,7 @@ def test_device_decode_stats_prefix(datadir, capfd):
 
 
 _FOOT = re.compile(r"buffers: peak ([\d.]+) GB together, per kind scan ([\d.]+), breakpoint ([\d.]+), CNV ([\d.]+), "
-                   r"stages ([\d.]+), decode ([\d.]+) GB; (\d+) allocations waited")
+                   r"stages ([\d.]+), decode ([\d.]+), phase arenas ([\d.]+) GB; (\d+) allocations waited")
 
 
 def test_hbm_cap_waits_for_memory(datadir):
@@ -819,9 +828,9 @@ def test_hbm_cap_waits_for_memory(datadir):
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
         m = _FOOT.search(r.stdout)
         assert m, r.stdout[-2000:]
-        return [float(x) for x in m.groups()[:6]], int(m.group(7)), r.stdout
+        return [float(x) for x in m.groups()[:7]], int(m.group(8)), r.stdout
 
-    (tot, _, _, _, stages, _), _, _ = run("g_cap_free.vcf", {})
+    (tot, _, _, _, stages, _, _), _, _ = run("g_cap_free.vcf", {})
     cap = (tot - stages + 0.5 * stages) * 1e9
     (tot2, *_), waits, out = run("g_cap.vcf", {"GROM_TEST_HBM_CAP": str(int(cap)), "GROM_ALLOC_WAIT_S": "40"})
     reclaimed = int(re.search(r"idle stage blocks reclaimed (\d+)", out).group(1))

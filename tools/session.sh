@@ -17,6 +17,8 @@
 #   pmc NAME "CTRS" [K=V ...]  one rocprofv3 --pmc pass (CTRS: one pass's
 #                              counters) over a whole run; NAME.csv per kernel
 #   bench [bench args]         python bench.py ... > bench.json
+#   probe CHECK [K=V ...]      the GPU inflater alone on /tmp/gw/g.bam
+#                              (tools/inflate_probe.py; CHECK=1: against zlib)
 #
 # environment: OUT (subdirectory of gpurun_out), FLAGS (CLI flags, default
 # "-M -g 1"), SYNTH (extra grom_synth args, e.g. coverage for configs[4]).
@@ -83,6 +85,11 @@ step_pmc() {
   db=$(find $out/pmc_$name -name "*.db" | head -1)
   [ -n "$db" ] && python3 tools/pmc_summary.py $db $out/pmc_$name.csv | head -12
   rm -rf $out/pmc_$name
+}
+
+step_probe() {
+  local check=$1; shift
+  env "$@" timeout -k 10 300 python3 tools/inflate_probe.py $work/g.bam 0 $check | tee -a $out/probe.jsonl
 }
 
 step_bench() {
