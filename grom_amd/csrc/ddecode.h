@@ -27,6 +27,10 @@ typedef struct DdBlock {
 /* the blocks of buf[0..len) (whole BGZF blocks): returns their number (and
  * fills out[0..cap) and *out_bytes), or -1 if the range is not whole blocks */
 int64_t dd_block_table(const uint8_t *buf, int64_t len, DdBlock *out, int64_t cap, int64_t *out_bytes);
+/* the whole blocks at the front of buf[0..len) (a block that does not end in
+ * the buffer ends the table): their number, *consumed their bytes */
+int64_t dd_block_table_prefix(const uint8_t *buf, int64_t len, DdBlock *out, int64_t cap, int64_t *out_bytes,
+                              int64_t *consumed);
 
 /* test hook: every whole block in the first max_bytes (<= 0: all) of a BAM
  * inflated on `device` and (check != 0) compared with zlib: the number of
@@ -53,6 +57,13 @@ int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs, int64_t n_
  * copied into device slot 0/1 on the context's copy stream; returns at once,
  * h_comp must stay untouched until a dd_run_decode of the slot has returned */
 int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_t comp_len, char *err, int errlen);
+/* the same in chunks from a ring of two pinned buffers: begin (device slot
+ * sized), per chunk wait for its ring buffer, read into it, copy it to
+ * dst_off; end (the slot complete, for dd_run_decode) */
+int dd_comp_begin(dd_ctx *c, int slot, int64_t comp_len, char *err, int errlen);
+int dd_comp_ring_wait(dd_ctx *c, int ring);
+int dd_comp_chunk(dd_ctx *c, int slot, int ring, const uint8_t *h_buf, int64_t dst_off, int64_t n, char *err, int errlen);
+int dd_comp_end(dd_ctx *c, int slot, int64_t comp_len, char *err, int errlen);
 typedef struct dd_parse_out {
     int64_t n_rec, n_kept, n_drop, n_cig, n_bases, n_auxc;
     int32_t last_pos, last_lq, last_hclip, last_kept;

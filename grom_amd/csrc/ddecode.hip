@@ -21,7 +21,8 @@
 #include "inflate.h"
 
 #define DD_LANES 64
-#define DD_SLOTS 2
+#define DD_SLOTS 2   // compressed runs on the device (the prefetch thread's slots)
+#define DD_RSLOTS 4  // piece slots (inflated bytes, record offsets): at most this many pieces in flight
 
 // One BGZF block per lane: blk[j] = {offset of its DEFLATE data in `comp`,
 // its length, offset of its output, ISIZE}; the output goes to out +
@@ -29,14 +30,13 @@
 // GI_* code.
 __global__ void __launch_bounds__(DD_LANES, 2) k_inflate(const uint8_t *__restrict__ comp, const DdBlock *__restrict__ blk,
                                                       int64_t n_blk, uint8_t *__restrict__ out, int64_t out_base,
-                                                      uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad,
-                                                      int hdr_batch) {
+                                                      uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad) {
     extern __shared__ uint32_t dd_tab[];  // GI_LANE_DWORDS x DD_LANES: rows element-major across the lanes
     const int64_t j = (int64_t)blockIdx.x * DD_LANES + threadIdx.x;
     if (j >= n_blk) return;
     const DdBlock b = blk[j];
     const int rc = gi_inflate<DD_LANES>(comp + b.in_off, b.in_len, out + (b.out_off - out_base), b.out_len, dd_tab,
-                                        threadIdx.x, hdr_batch);
+                                        threadIdx.x);
     status[j] = (uint8_t)rc;
     if (rc) atomicAdd(n_bad, 1u);
 }
@@ -45,10 +45,8 @@ extern "C" int dd_inflate_launch(hipStream_t st, const uint8_t *d_comp, const Dd
                                  uint8_t *d_out, int64_t out_base, uint8_t *d_status, uint32_t *d_bad) {
     if (n_blk <= 0) return 0;
     const unsigned grid = (unsigned)((n_blk + DD_LANES - 1) / DD_LANES);
-    // GROM_INFLATE_BATCH: header-trip batching (inflate.h), lanes per header trip
-    static const int batch = getenv("GROM_INFLATE_BATCH") ? atoi(getenv("GROM_INFLATE_BATCH")) : 0;
     hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES, st, d_comp, d_blk,
-                       n_blk, d_out, out_base, d_status, d_bad, batch);
+                       n_blk, d_out, out_base, d_status, d_bad);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -59,9 +57,20 @@ static uint32_t rd32(const uint8_t *p) {
 }
 
 extern "C" int64_t dd_block_table(const uint8_t *buf, int64_t len, DdBlock *out, int64_t cap, int64_t *out_bytes) {
+    return dd_block_table_prefix(buf, len, out, cap, out_bytes, nullptr);
+}
+
+// the whole blocks at the front of buf[0..len): with `consumed` a block that
+// does not end inside the buffer ends the table (*consumed: the bytes of the
+// whole blocks), without it that is an error
+extern "C" int64_t dd_block_table_prefix(const uint8_t *buf, int64_t len, DdBlock *out, int64_t cap, int64_t *out_bytes,
+                                         int64_t *consumed) {
     int64_t off = 0, n = 0, ob = 0;
     while (off < len) {
-        if (off + 18 > len) return -1;
+        if (off + 18 > len) {
+            if (consumed) break;
+            return -1;
+        }
         const uint8_t *h = buf + off;
         if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return -1;
         const int xlen = rd16(h + 10);
@@ -72,7 +81,11 @@ extern "C" int64_t dd_block_table(const uint8_t *buf, int64_t len, DdBlock *out,
             o += 4 + sl;
         }
         const int64_t blen = (int64_t)bsize + 1;
-        if (bsize < 0 || blen < 12 + xlen + 8 || off + blen > len) return -1;
+        if (bsize < 0 || blen < 12 + xlen + 8) return -1;
+        if (off + blen > len) {
+            if (consumed) break;
+            return -1;
+        }
         const uint32_t isize = rd32(h + blen - 4);
         if (isize > 65536) return -1;
         if (out && n < cap) {
@@ -87,6 +100,7 @@ extern "C" int64_t dd_block_table(const uint8_t *buf, int64_t len, DdBlock *out,
         off += blen;
     }
     if (out_bytes) *out_bytes = ob;
+    if (consumed) *consumed = off;
     return n;
 }
 
@@ -946,14 +960,16 @@ struct RunSlot {
 
 struct dd_ctx {
     int device = -1;
-    RunSlot rs[DD_SLOTS];
+    RunSlot rs[DD_RSLOTS];
+    int depth = 2;  // pieces in flight (GROM_DD_DEPTH, 1..DD_RSLOTS)
     hipStream_t st = nullptr;
     hipStream_t cst = nullptr;  // compressed runs' host->device copies (dd_comp_upload, the prefetch thread)
     DBuf dcomp[DD_SLOTS];
     hipEvent_t cev[DD_SLOTS] = {};
     int64_t dcomp_len[DD_SLOTS] = {};
     hipEvent_t ev[4] = {};
-    hipEvent_t pev[DD_SLOTS] = {};  // the piece in slot k is parsed (its U and record offsets are free)
+    hipEvent_t pev[DD_RSLOTS] = {};  // the piece in slot k is parsed (its U and record offsets are free)
+    hipEvent_t rev[2] = {};         // the copy out of pinned ring buffer k is done (dd_comp_chunk)
     DBuf misc;  // the parse's and the statistics' flags and scalars
     DBuf keep, kidx, drop, didx, auxc, aidx, ncig, coff, nb, boff, rpos, krec, keys, vals, keys2, vals2, head, tmp;
     DBuf srcs, tfq, tfs;  // per kept read: its bases' offset in U; per copy tile: its first read
@@ -1026,13 +1042,15 @@ extern "C" dd_ctx *dd_ctx_new(int device) {
     if (getenv("GROM_TEST_CP_UNSTAGED")) c->cp_cap = 0;
     if (getenv("GROM_DD_PIECE_MB") && atof(getenv("GROM_DD_PIECE_MB")) > 0)
         c->piece_bytes = std::max<int64_t>((int64_t)(atof(getenv("GROM_DD_PIECE_MB")) * 1048576.0), 4096);
+    if (getenv("GROM_DD_DEPTH")) c->depth = std::min(std::max(atoi(getenv("GROM_DD_DEPTH")), 1), DD_RSLOTS);
     if (dd_stream_new(&c->st) != hipSuccess) { delete c; return nullptr; }
     if (dd_stream_new(&c->cst) != hipSuccess) c->cst = nullptr;
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
     for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming);
-    for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->pev[k], hipEventDisableTiming);
+    for (int k = 0; k < DD_RSLOTS; k++) (void)hipEventCreateWithFlags(&c->pev[k], hipEventDisableTiming);
+    for (int k = 0; k < 2; k++) (void)hipEventCreateWithFlags(&c->rev[k], hipEventDisableTiming);
     if (hipHostMalloc((void **)&c->h_small, 64 * sizeof(int64_t), 0) != hipSuccess) c->h_small = nullptr;
-    for (int k = 0; k < DD_SLOTS; k++) {
+    for (int k = 0; k < DD_RSLOTS; k++) {
         RunSlot &r = c->rs[k];
         if (dd_stream_new(&r.st) != hipSuccess) r.st = nullptr;
         for (int e = 0; e < 3; e++) (void)hipEventCreate(&r.ev[e]);
@@ -1050,9 +1068,10 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
     for (int k = 0; k < DD_SLOTS; k++) {
         if (c->dcomp[k].p) grom_dev_free(c->dcomp[k].p, c->dcomp[k].cap, GROM_DEVCAT_DECODE);
         if (c->cev[k]) (void)hipEventDestroy(c->cev[k]);
-        if (c->pev[k]) (void)hipEventDestroy(c->pev[k]);
+        if (k < 2 && c->rev[k]) (void)hipEventDestroy(c->rev[k]);
     }
-    for (int k = 0; k < DD_SLOTS; k++) {
+    for (int k = 0; k < DD_RSLOTS; k++) {
+        if (c->pev[k]) (void)hipEventDestroy(c->pev[k]);
         RunSlot &r = c->rs[k];
         if (r.st) (void)hipStreamSynchronize(r.st);
         DBuf *rb[] = {&r.U, &r.blk, &r.status, &r.misc, &r.S, &r.ccnt, &r.cbase, &r.off, &r.tmp};
@@ -1106,13 +1125,16 @@ extern "C" void dd_ctx_counts(const dd_ctx *c, int64_t *rewalked, int64_t *subch
 extern "C" int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs, int64_t n_starts, char *err,
                           int errlen) {
     DCK(hipSetDevice(c->device));
-    const int64_t pb = std::min<int64_t>(c->piece_bytes, ubytes) + (4 << 20);  // a piece ends past the target
-    const int64_t pr = pb / 34 + 1024;  // records in a piece: at least 34 bytes each
-    const int64_t nblk = ubytes / 60000 + 1024;
+    // a piece ends past its target (at a chunk boundary, on whole blocks)
+    const int64_t pb = std::min<int64_t>(c->piece_bytes, ubytes) * 11 / 10 + (4 << 20);
+    // records in a piece at the run's mean record size (+25%); a piece with
+    // more grows its offsets (dd_run_decode)
+    const int64_t pr = (int64_t)((double)pb * (double)recs / (double)std::max<int64_t>(ubytes, 1) * 1.25) + 4096;
+    const int64_t nblk = ubytes / 32768 + 4096;  // BGZF blocks hold at most 64 KiB
     (void)span;  // (the compressed slots grow on the prefetch thread, dd_comp_upload)
     DGROW(c->rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
     DGROW(c->rS, sizeof(int64_t) * (size_t)(n_starts + 2));
-    for (int k = 0; k < DD_SLOTS; k++) {
+    for (int k = 0; k < c->depth; k++) {
         RunSlot &r = c->rs[k];
         DGROW(r.U, (size_t)pb + 64);
         DGROW(r.status, (size_t)(pb / 16384 + 1024));
@@ -1167,6 +1189,45 @@ extern "C" int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_
     hipStream_t cs = c->cst ? c->cst : c->st;
     DGROW(c->dcomp[slot], (size_t)comp_len + 64);
     DCK(hipMemcpyAsync(c->dcomp[slot].p, h_comp, (size_t)comp_len + 64, hipMemcpyHostToDevice, cs));
+    DCK(hipEventRecord(c->cev[slot], cs));
+    c->dcomp_len[slot] = comp_len;
+    return 0;
+}
+
+// A run's compressed bytes in chunks (the prefetch thread reads them into a
+// ring of two pinned buffers): dd_comp_begin sizes the device slot, each
+// dd_comp_chunk copies one buffer to its place on the copy stream (the ring
+// buffer is free again once dd_comp_ring_wait returns), dd_comp_end marks the
+// slot complete for dd_run_decode
+extern "C" int dd_comp_begin(dd_ctx *c, int slot, int64_t comp_len, char *err, int errlen) {
+    if (slot < 0 || slot >= DD_SLOTS) return -1;
+    DCK(hipSetDevice(c->device));
+    hipStream_t cs = c->cst ? c->cst : c->st;
+    c->dcomp_len[slot] = -1;
+    DGROW(c->dcomp[slot], (size_t)comp_len + 64);
+    DCK(hipMemsetAsync(P<uint8_t>(c->dcomp[slot]) + comp_len, 0, 64, cs));
+    return 0;
+}
+
+extern "C" int dd_comp_ring_wait(dd_ctx *c, int ring) {
+    if (ring < 0 || ring > 1 || !c->rev[ring]) return 0;
+    return hipEventSynchronize(c->rev[ring]) == hipSuccess ? 0 : -1;
+}
+
+extern "C" int dd_comp_chunk(dd_ctx *c, int slot, int ring, const uint8_t *h_buf, int64_t dst_off, int64_t n, char *err,
+                             int errlen) {
+    if (slot < 0 || slot >= DD_SLOTS || ring < 0 || ring > 1) return -1;
+    DCK(hipSetDevice(c->device));
+    hipStream_t cs = c->cst ? c->cst : c->st;
+    DCK(hipMemcpyAsync(P<uint8_t>(c->dcomp[slot]) + dst_off, h_buf, (size_t)n, hipMemcpyHostToDevice, cs));
+    DCK(hipEventRecord(c->rev[ring], cs));
+    return 0;
+}
+
+extern "C" int dd_comp_end(dd_ctx *c, int slot, int64_t comp_len, char *err, int errlen) {
+    if (slot < 0 || slot >= DD_SLOTS) return -1;
+    DCK(hipSetDevice(c->device));
+    hipStream_t cs = c->cst ? c->cst : c->st;
     DCK(hipEventRecord(c->cev[slot], cs));
     c->dcomp_len[slot] = comp_len;
     return 0;
@@ -1229,6 +1290,9 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
         int64_t ca, cb, u_lo, u_hi, bf, bl, base, pbytes;
     };
     std::vector<Piece> pcs;
+    // records per inflated byte of the run (the index's count)
+    const double rpb = q->count > 0 && q->u_end > q->starts[0] ? (double)q->count / (double)(q->u_end - q->starts[0])
+                                                                 : 1.0 / 34.0;
     for (int64_t ca = 0; ca < ns;) {
         int64_t cb = ca + 1;
         while (cb < ns && q->starts[cb] - q->starts[ca] < c->piece_bytes) cb++;
@@ -1265,26 +1329,30 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
     int64_t *tot = (int64_t *)((char *)c->misc.p + 128);
     int32_t *d_last = (int32_t *)((char *)c->misc.p + 192);
     DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
-    DCK(hipEventRecord(c->pev[0], st));
-    DCK(hipEventRecord(c->pev[1], st));
-    // The load of piece p (inflate, record walk) runs on piece slot p % 2's
-    // own stream, issued one piece ahead: it overlaps the statistics and the
-    // parse of piece p - 1 on the context's stream.  A slot is reused once
+    const int D = c->depth;
+    for (int k = 0; k < D; k++) DCK(hipEventRecord(c->pev[k], st));
+    // The load of piece p (inflate, record walk) runs on piece slot p % D's
+    // own stream, issued D - 1 pieces ahead: it overlaps the statistics and
+    // the parse of the pieces before on the context's stream, and the loads
+    // in flight together fill the chip (a launch of k_inflate takes at least
+    // one lane's time for one block, whatever its size).  A slot is reused once
     // the parse of the piece before in it is done (pev).  The offsets walk
     // writes up to the slot's record capacity; a piece with more records is
     // walked again after its buffer grows.
     auto issue = [&](size_t p) -> int {
         const Piece &pc = pcs[p];
-        RunSlot &r = c->rs[p % DD_SLOTS];
+        RunSlot &r = c->rs[p % D];
         hipStream_t ls = r.st;
-        DCK(hipStreamWaitEvent(ls, c->pev[p % DD_SLOTS], 0));
+        DCK(hipStreamWaitEvent(ls, c->pev[p % D], 0));
         DCK(hipStreamWaitEvent(ls, c->cev[q->slot], 0));
         DGROW(r.U, (size_t)pc.pbytes + 64);
         DGROW(r.status, (size_t)(pc.bl - pc.bf + 2));
         DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
         DGROW(r.cbase, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
         DGROW(r.misc, 256);
-        const int64_t ocap = std::max<int64_t>((int64_t)(r.off.cap / 8) - 1, pc.pbytes / 34 + 1024);
+        // record offsets: the run's mean record size (+30%); a piece with more
+        // is walked again below
+        const int64_t ocap = std::max<int64_t>((int64_t)(r.off.cap / 8) - 1, (int64_t)((double)pc.pbytes * rpb * 1.3) + 4096);
         DGROW(r.off, 8 * (size_t)(ocap + 1));
         uint32_t *rb = P<uint32_t>(r.misc);
         DCK(hipMemsetAsync(r.misc.p, 0, 64, ls));
@@ -1315,12 +1383,13 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
         DCK(hipEventRecord(r.ev[2], ls));
         return 0;
     };
-    if (!pcs.empty() && issue(0)) return -1;
+    for (size_t p = 0; p + 1 < (size_t)D && p < pcs.size(); p++)
+        if (issue(p)) return -1;
     for (size_t p = 0; p < pcs.size(); p++) {
         const Piece &pc = pcs[p];
-        RunSlot &r = c->rs[p % DD_SLOTS];
+        RunSlot &r = c->rs[p % D];
         const bool ahead = parse || stats_left > 0;  // (statistics only: stop at the cap)
-        if (p + 1 < pcs.size() && ahead && issue(p + 1)) return -1;
+        if (p + D - 1 < pcs.size() && ahead && issue(p + D - 1)) return -1;
         DCK(hipEventSynchronize(r.ev[2]));
         const uint32_t *hs = (const uint32_t *)r.h_small;
         const int64_t R = (int64_t)hs[0] + hs[1];
@@ -1446,7 +1515,9 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                 cap.n_drop = (int64_t)(f * (double)nd) + 1024;
                 cap.n_cigar_ops = (int64_t)(f * (double)ncg) + 1024;
                 cap.n_bases = ((int64_t)(f * (double)nbs) + 1024) & ~(int64_t)1;
-                cap.n_aux = 1;
+                // the split-read records the host appends after the run
+                // (at most one per candidate)
+                cap.n_aux = (int64_t)(f * 1.5 * (double)na) + 1024;
                 cap.ref_len = q->ref_len;
             }
             if (need.n > cap.n || need.n_drop > cap.n_drop || need.n_cigar_ops > cap.n_cigar_ops ||
@@ -1455,7 +1526,7 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                 cap.n_drop = std::max(cap.n_drop, need.n_drop);
                 cap.n_cigar_ops = std::max(cap.n_cigar_ops, need.n_cigar_ops);
                 cap.n_bases = std::max(cap.n_bases, need.n_bases);
-                cap.n_aux = 1;
+                cap.n_aux = std::max<int64_t>(cap.n_aux, n_aux + na + 1024);
                 cap.ref_len = q->ref_len;
                 if (grom_stage_fill_ensure(q->stage, &cap, &have, &dv) != GROM_OK) {
                     if (err) snprintf(err, (size_t)errlen, "%s", grom_last_error());
@@ -1557,11 +1628,11 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
             have.n_cigar_ops = car.cig;
             have.n_bases = car.b;
         }
-        DCK(hipEventRecord(c->pev[p % DD_SLOTS], st));  // the slot's piece is done with
+        DCK(hipEventRecord(c->pev[p % D], st));  // the slot's piece is done with
         R_tot += R;
         if (!parse && stats_left <= 0) break;  // statistics only: the cap is reached
     }
-    for (int k = 0; k < DD_SLOTS; k++) DCK(hipStreamSynchronize(c->rs[k].st));  // (a load issued ahead)
+    for (int k = 0; k < D; k++) DCK(hipStreamSynchronize(c->rs[k].st));  // (loads issued ahead)
     *n_rec = R_tot;
     po->n_rec = R_tot;
     if (!parse) return 0;

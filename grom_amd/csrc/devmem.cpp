@@ -177,6 +177,11 @@ extern "C" int grom_arena_begin(grom_arena *a) {
     return 0;
 }
 
+extern "C" void grom_arena_hint(grom_arena *a, size_t bytes) {
+    std::lock_guard<std::mutex> lk(a->mu);
+    if (bytes > a->high) a->high = bytes;
+}
+
 extern "C" void *grom_arena_take(grom_arena *a, size_t bytes) {
     std::lock_guard<std::mutex> lk(a->mu);
     const size_t b = (bytes + 255) & ~(size_t)255;

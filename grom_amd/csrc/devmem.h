@@ -53,6 +53,10 @@ int grom_arena_begin(grom_arena *a);
  * the caller then allocates on its own (grom_dev_malloc) and the arena grows
  * to hold it at the next begin */
 void *grom_arena_take(grom_arena *a, size_t bytes);
+/* grom_arena_hint: the next grom_arena_begin sizes the arena for at least
+ * this many bytes (an estimate of the phase to come; a phase that needs more
+ * overflows into allocations of its own, and the arena grows after it). */
+void grom_arena_hint(grom_arena *a, size_t bytes);
 int64_t grom_arena_bytes(const grom_arena *a);
 
 /* accounting only (allocations made elsewhere) */

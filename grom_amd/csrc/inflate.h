@@ -482,15 +482,8 @@ GI_FN void gi_lit(uint8_t *out, uint32_t &o, uint64_t &pend, uint32_t &pn, uint3
 // Inflate one block's raw DEFLATE data (in[0..in_len)) into out[0..out_len).
 // `tab` is the LDS (device) or local (host) table storage of GI_LANE_DWORDS
 // rows x LANES columns.  Bytes outside out[0..out_len) are never written.
-// hdr_batch (the device, 64 lanes): a wave runs a trip of header steps
-// (block headers, the two passes over a dynamic header's code lengths) only
-// when at least hdr_batch of its lanes wait for one or none has data to
-// decode, else a trip of data steps (symbols, matches, stored bytes); a lane
-// of the other kind sits the trip out.  Without it (0) every trip executes
-// both kinds of code whenever any lane needs the other.
 template <int LANES>
-GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len, uint32_t *tab, int lane,
-                     int hdr_batch = 0) {
+GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len, uint32_t *tab, int lane) {
     typedef uint32_t gi_u32x4 __attribute__((vector_size(16)));
     GiBits b;
     gi_open(b, in);
@@ -503,14 +496,6 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
     uint32_t pn = 0;
     int mode = GI_M_HDR, rc = GI_OK;
     while (mode != GI_M_DONE) {
-#if defined(__HIP_DEVICE_COMPILE__)
-        if (hdr_batch > 0) {
-            const bool hdr = mode == GI_M_HDR || mode == GI_M_P1 || mode == GI_M_P2;
-            const uint64_t mh = __ballot(hdr), ml = __ballot(1);
-            const bool hdr_trip = (ml & ~mh) == 0 || __popcll(mh) >= hdr_batch;
-            if (hdr != hdr_trip) continue;  // (the lane's state is unchanged)
-        }
-#endif
         gi_refill(b);
         if (mode == GI_M_HDR) {
             const int m = gi_header<LANES>(b, lit, dist, H, tab, lane, bfinal, rem);

@@ -2053,8 +2053,7 @@ enum { PF_FREE = 0, PF_WANTED = 1, PF_READY = 2, PF_USED = 3 };
 typedef struct {
     int ri, state, rc;
     char err[200];
-    uint8_t *comp;           /* pinned compressed run (+64 readable bytes) */
-    int64_t comp_cap, len;
+    int64_t len;             /* the compressed run's bytes (copied to the device slot of the same number) */
     DdBlock *blk;
     int64_t blk_cap, nb, ub;
     int64_t *starts;
@@ -2072,8 +2071,11 @@ typedef struct {
     pthread_cond_t cv;
     pthread_t pf_thr;
     int pf_started, pf_stop;
+    uint8_t *ring[2];        /* pinned read ring of the prefetch thread (PF_CHUNK bytes each) */
     int test_abort, n_done;  /* GROM_TEST_DD_ABORT=n: -2 at the n-th chromosome (tests) */
 } dd_worker;
+
+#define PF_CHUNK ((int64_t)64 << 20)
 
 typedef struct {
     int fd;
@@ -2148,26 +2150,50 @@ static int pf_read(dd_worker *w, pf_slot *sl, int slot_no, int ri, char *err, in
     }
     const int64_t len = c1 - c0;
     if (len <= 0 || c1 > s->file_size) { snprintf(err, (size_t)errlen, "bad run range"); return -2; }
-    if (len + 64 > sl->comp_cap) {
-        grom_pinned_free(sl->comp);
-        sl->comp_cap = len + len / 8 + 4096;
-        sl->comp = (uint8_t *)grom_pinned_alloc((size_t)sl->comp_cap);
-        if (!sl->comp) { sl->comp_cap = 0; snprintf(err, (size_t)errlen, "no pinned memory for a run"); return -1; }
-    }
+    /* the compressed run in chunks of whole blocks through a ring of two
+     * pinned buffers (PF_CHUNK each: pinning a whole 1.6 GB run per process
+     * cost ~0.4 s and held up the device allocations made meanwhile), each
+     * copied to the device slot while the next is read; the block table is
+     * built chunk by chunk */
+    for (int k = 0; k < 2; k++)
+        if (!w->ring[k]) {
+            w->ring[k] = (uint8_t *)grom_pinned_alloc(PF_CHUNK);
+            if (!w->ring[k]) { snprintf(err, (size_t)errlen, "no pinned memory for the read ring"); return -1; }
+        }
+    if (dd_comp_begin(w->dd, slot_no, len, err, errlen)) return -1;
     const double t0 = now_s();
-    if (pread_par(s->fd, sl->comp, len, c0, s->io_threads)) { snprintf(err, (size_t)errlen, "reading the BAM failed"); return -1; }
-    memset(sl->comp + len, 0, 64);
-    sl->t_io = now_s() - t0;
-    int64_t ub = 0;
-    int64_t nb = dd_block_table(sl->comp, len, NULL, 0, &ub);
-    if (nb <= 0) { snprintf(err, (size_t)errlen, "the run is not whole BGZF blocks"); return -2; }
-    if (nb > sl->blk_cap) {
-        free(sl->blk);
-        sl->blk_cap = nb + nb / 4 + 16;
-        sl->blk = (DdBlock *)malloc(sizeof(DdBlock) * (size_t)sl->blk_cap);
-        if (!sl->blk) { sl->blk_cap = 0; return -1; }
+    int64_t off = 0, ub = 0, nb = 0;
+    for (int ring = 0; off < len; ring ^= 1) {
+        const int64_t want = len - off < PF_CHUNK ? len - off : PF_CHUNK;
+        if (dd_comp_ring_wait(w->dd, ring)) { snprintf(err, (size_t)errlen, "device copy failed"); return -1; }
+        if (pread_par(s->fd, w->ring[ring], want, c0 + off, s->io_threads)) {
+            snprintf(err, (size_t)errlen, "reading the BAM failed");
+            return -1;
+        }
+        int64_t used = 0, cb = 0;
+        const int64_t n = dd_block_table_prefix(w->ring[ring], want, NULL, 0, &cb, &used);
+        if (n <= 0 || (off + want == len && used != want)) {
+            snprintf(err, (size_t)errlen, "the run is not whole BGZF blocks");
+            return -2;
+        }
+        if (nb + n > sl->blk_cap) {
+            sl->blk_cap = (nb + n) + (nb + n) / 2 + 16;
+            DdBlock *nbk = (DdBlock *)realloc(sl->blk, sizeof(DdBlock) * (size_t)sl->blk_cap);
+            if (!nbk) { sl->blk_cap = 0; return -1; }
+            sl->blk = nbk;
+        }
+        dd_block_table_prefix(w->ring[ring], used, sl->blk + nb, n, &cb, NULL);
+        for (int64_t k = nb; k < nb + n; k++) { /* offsets in the whole run */
+            sl->blk[k].in_off += off;
+            sl->blk[k].c_off += off;
+            sl->blk[k].out_off += ub;
+        }
+        if (dd_comp_chunk(w->dd, slot_no, ring, w->ring[ring], off, used, err, errlen)) return -1;
+        nb += n;
+        ub += cb;
+        off += used;
     }
-    dd_block_table(sl->comp, len, sl->blk, nb, &ub);
+    sl->t_io = now_s() - t0;
     /* record starts: the run's first record, then every linear-index offset inside the run */
     const int64_t u0 = (int64_t)(r->vbeg & 0xffff);
     int64_t u_end = ub;
@@ -2204,7 +2230,7 @@ static int pf_read(dd_worker *w, pf_slot *sl, int slot_no, int ri, char *err, in
     sl->ub = ub;
     sl->m = m;
     sl->u_end = u_end;
-    return dd_comp_upload(w->dd, slot_no, sl->comp, len, err, errlen) ? -1 : 0;
+    return dd_comp_end(w->dd, slot_no, len, err, errlen) ? -1 : 0;
 }
 
 static void *pf_main(void *arg) {
@@ -2779,7 +2805,7 @@ static void *dw_main(void *arg) {
     /* the scans may still read the stages; the decode context goes now */
     dd_ctx_free(w->dd);
     for (int q = 0; q < 2; q++) {
-        grom_pinned_free(w->slot[q].comp);
+        grom_pinned_free(w->ring[q]);
         free(w->slot[q].blk);
         free(w->slot[q].starts);
     }

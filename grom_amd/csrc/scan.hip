@@ -393,6 +393,14 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
     if (use_arena) {
         if (!C.ar) C.ar = grom_arena_new(GROM_DEVCAT_ARENA);
         cnv_scratch_sync(C.cnv);  // (the last CNV phase's streams are done with the arena)
+        // Size the arena for this chromosome's phases before the first one,
+        // so that the first chromosome (the longest) does not overflow into
+        // separate allocations: the pileup/breakpoint phase holds ~34 bytes
+        // per base and ~56 per read, the CNV phase ~83 per base (measured on
+        // the 30x genome)
+        const double p_est = 34.0 * (double)ch->len + 56.0 * (double)n;
+        const double c_est = ch->cnv ? 83.0 * (double)ch->len : 0.0;
+        grom_arena_hint(C.ar, (size_t)(std::max(p_est, c_est) + (64 << 20)));
         if (grom_arena_begin(C.ar)) {
             set_err("phase arena: device memory allocation failed");
             return GROM_E_NOMEM;
@@ -1235,6 +1243,13 @@ static int stage_reserve(grom_stage *s, const size_t need[SA_N], const size_t ke
         cap[k] = s->cap[k] >= need[k] + 64 ? s->cap[k] : need[k] + need[k] / grow + 4096;
         off[k] = tot;
         tot += (cap[k] + 255) & ~(size_t)255;
+    }
+    static const bool log = getenv("GROM_STAGE_LOG") != nullptr;
+    if (log) {  // which arrays outgrew the block
+        fprintf(stderr, "grom: stage %p block %.3f -> %.3f GB:", (void *)s, s->blk_cap / 1e9, tot / 1e9);
+        for (int k = 0; k < SA_N; k++)
+            if (s->cap[k] < need[k] + 64) fprintf(stderr, " [%d] %zu<%zu", k, s->cap[k], need[k]);
+        fputc('\n', stderr);
     }
     char *nb = nullptr;
     const auto t0 = std::chrono::steady_clock::now();

@@ -381,3 +381,42 @@ def test_fasta_pread_loader_matches_fgets_loader(tmp_path):
     assert lib.grom_fasta_open(f, str(nul).encode()) == 0
     assert lib.grom_fasta_load_at(f, 0, None, 0) == -2
     lib.grom_fasta_close(f)
+
+
+def test_block_table_in_chunks(tmp_path):
+    """The prefetch thread builds a run's BGZF block table chunk by chunk
+    (pdecode.c pf_read: a ring of pinned buffers, each holding the whole
+    blocks that fit): the tables of every chunk, shifted by the chunk's
+    offsets, must equal the table of the whole range, for chunk sizes that cut
+    blocks anywhere, down to one block per chunk."""
+    import zlib
+    import grom_amd
+    rng = __import__("random").Random(9)
+    chunks = [bytes(rng.choice(b"ACGT#+5?") for _ in range(rng.randrange(1, 65280))) for _ in range(60)]
+    data = _bgzf_blocks(chunks, 6, zlib.Z_DEFAULT_STRATEGY)
+
+    class Blk(ctypes.Structure):
+        _fields_ = [("in_off", ctypes.c_int64), ("out_off", ctypes.c_int64), ("in_len", ctypes.c_uint32),
+                    ("out_len", ctypes.c_uint32), ("c_off", ctypes.c_int64)]
+    lib = grom_amd.lib()
+    tab, pre = lib.dd_block_table, lib.dd_block_table_prefix
+    tab.restype = pre.restype = ctypes.c_int64
+    tab.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(Blk), ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    pre.argtypes = tab.argtypes + [ctypes.POINTER(ctypes.c_int64)]
+    whole = (Blk * 100)()
+    ub = ctypes.c_int64()
+    n = tab(data, len(data), whole, 100, ctypes.byref(ub))
+    assert n == len(chunks) and ub.value == sum(map(len, chunks))
+    ref = [(b.in_off, b.out_off, b.in_len, b.out_len, b.c_off) for b in whole[:n]]
+    for size in (70000, 100000, 250000, 1 << 20):
+        got, off, ob = [], 0, 0
+        while off < len(data):
+            buf = data[off:off + size]
+            part = (Blk * 100)()
+            cb, used = ctypes.c_int64(), ctypes.c_int64()
+            k = pre(buf, len(buf), part, 100, ctypes.byref(cb), ctypes.byref(used))
+            assert k > 0 and used.value > 0
+            got += [(b.in_off + off, b.out_off + ob, b.in_len, b.out_len, b.c_off + off) for b in part[:k]]
+            off += used.value
+            ob += cb.value
+        assert got == ref, size

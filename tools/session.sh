@@ -49,15 +49,20 @@ step_genome() {
   echo "synth $(python3 -c "print(round($(date +%s.%N) - $t0, 1))") s, $(stat -c %s $work/g.bam) bytes"
 }
 
+WN=0
 step_whole() {
   local runs=$1; shift
+  WN=$((WN + 1))
+  local pre=""
+  [ $WN -gt 1 ] && pre="w${WN}_"
   ( cd $work
-    for r in $(seq 1 $runs); do
+    for r0 in $(seq 1 $runs); do
+      r="${pre}${r0}"
       { time env "$@" GROM_VERBOSE=1 GROM_TRACE=$repo/$out/trace_$r.csv timeout -k 10 180 $repo/grom_amd/bin/grom -i g.bam -r g.fa -o w_$r.vcf $FLAGS \
           > $repo/$out/whole_$r.log 2>&1 ; } 2> $repo/$out/whole_$r.time || { tail $repo/$out/whole_$r.log; exit 1; }
       echo "== run $r: $(cat $repo/$out/whole_$r.time)"
       grep -h "decode:\|cli \|footprint\|took" $repo/$out/whole_$r.log
-      if [ $r -gt 1 ]; then cmp w_1.vcf w_$r.vcf && cmp w_1.ctx.vcf w_$r.ctx.vcf || exit 1; fi
+      if [ "$r" != "1" ]; then cmp w_1.vcf w_$r.vcf && cmp w_1.ctx.vcf w_$r.ctx.vcf || exit 1; fi
     done
     sha256sum w_1.vcf w_1.ctx.vcf | tee $repo/$out/sha.txt
     echo "rows $(grep -vc '^#' w_1.vcf)" )
