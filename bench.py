@@ -475,7 +475,10 @@ def main():
         _, last = step()
         runs.append(time.perf_counter() - t1)
         run_out.append(last)
-        log(f"timed run {k + 1}: {runs[-1]:.2f} s")
+        ph = [ln[len("cli phases (s from start): "):] for ln in last.splitlines() if ln.startswith("cli phases")]
+        rd = re.search(r"file reads ([\d.]+) s \(read ahead; waited for ([\d.]+) s\)", last)
+        log(f"timed run {k + 1}: {runs[-1]:.2f} s" + (f"; {ph[0]}" if ph else "") +
+            (f"; file reads {rd.group(1)} s, waited {rd.group(2)} s" if rd else ""))
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, device="cuda")
     value = total * args.steps / dt / 1e6

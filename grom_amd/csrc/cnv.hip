@@ -2423,19 +2423,25 @@ __global__ __launch_bounds__(64) void k_cnv_reconcile(WalkIn W, const int32_t *n
                                                       ChunkState *__restrict__ cs, CallRec *calls, uint32_t *n_calls,
                                                       uint32_t cap, uint8_t *__restrict__ skipped,
                                                       uint32_t *__restrict__ n_fix) {
-    __shared__ ChunkState s_prev, s_cur;
+    // the chunk states come in batches of 64, one load per lane (a serial
+    // load per chunk made the launch ~6 ms on a 250 Mb chromosome); a repair
+    // rewrites only its own chunk's state, which is read again after it
+    __shared__ ChunkState s_prev, s_cur, s_bat[64];
     if (threadIdx.x == 0) s_prev = cs[0];
     for (int64_t k = threadIdx.x; k < n_ch; k += 64) skipped[k] = 0;
     __syncthreads();
-    int64_t tx = s_prev.x1;
-    int tl = s_prev.l1;
+    ChunkState prev = s_prev;
+    int64_t tx = prev.x1;
+    int tl = prev.l1;
     uint32_t fixes = 0;
     for (int64_t k = 1; k < n_ch; k++) {
-        if (threadIdx.x == 0) s_cur = cs[k];
-        __syncthreads();
-        const ChunkState h = s_cur, hp = s_prev;  // (the fix of chunk k writes only its own state)
-        __syncthreads();
-        if (threadIdx.x == 0) s_prev = h;
+        if (((k - 1) & 63) == 0) {  // the next batch: chunks k .. k + 63
+            __syncthreads();
+            if (k + threadIdx.x < n_ch) s_bat[threadIdx.x] = cs[k + threadIdx.x];
+            __syncthreads();
+        }
+        const ChunkState h = s_bat[(k - 1) & 63], hp = prev;
+        prev = h;  // (chunk k's state before any repair of it)
         const bool entry_ok = tx == hp.x1 && tl == hp.l1;
         const int64_t c0 = W.start + k * chunk, c1 = min(W.end, c0 + chunk);
         const int64_t ex = h.status == ST_NOMERGE ? h.x2 : h.x1;

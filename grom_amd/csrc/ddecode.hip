@@ -666,6 +666,7 @@ __global__ void k_rec_write(const uint8_t *__restrict__ U, const int64_t *__rest
 // touch it.
 #define CP_T 8192  // destination bytes per tile: one workgroup, 8 dwords per thread
 #define CP_J (CP_T / 1024)
+#define CP_G 4  // dwords whose loads are in flight together
 #define CP_R 1024   // reads a tile may touch, staged in LDS (more: the tile reads them from global memory)
 
 // the read holding each tile's first destination byte, for the tiles of one
@@ -759,11 +760,22 @@ __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ 
             }
             continue;
         }
-        uint32_t w0[CP_J], w1[CP_J], fastm = 0, shp = 0;  // shp: 2 bits per dword, its source's byte offset
+        // Each dword takes its bytes from at most two reads: A, the read that
+        // holds its first byte (nA bytes, the last of them possibly an odd
+        // read's pad byte, 0), and B, the next read (the other 4 - nA).  The
+        // loads of both (two aligned words each) are issued for all of the
+        // thread's dwords before any is stored.  A dword at a piece edge, or
+        // one that touches a third read or B's pad byte, goes byte by byte.
+        // (in groups of CP_G dwords: all of a thread's eight at once took ~200
+        // registers, two waves per SIMD)
         int k = 0;  // reads are in destination order: each search starts from the previous dword's read
         const int64_t t0 = t * CP_T;
+        for (int g = 0; g < CP_J; g += CP_G) {
+        uint32_t wa0[CP_G], wa1[CP_G], wb0[CP_G], wb1[CP_G];
+        uint32_t gen = 0, sha = 0, shb = 0, nam = 0, padm = 0;
 #pragma unroll
-        for (int j = 0; j < CP_J; j++) {
+        for (int jg = 0; jg < CP_G; jg++) {
+            const int j = g + jg;
             const int32_t xr = 4 * (threadIdx.x + 256 * j);  // offset in the tile
             const int64_t x = t0 + xr;
             const int64_t x0 = x < dlo ? dlo : x;
@@ -774,26 +786,49 @@ __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ 
                 else hi = mid - 1;
             }
             k = lo;
-            const int64_t b0 = s_beg[k], L = s_len[k];
-            const bool fast = x >= dlo && x + 4 <= b0 + L && !(QUAL && s_odd[k] && x + 3 >= b0 + L - 1) && x + 4 <= dhi;
-            const int64_t p = s_src[k] + (x - b0);
-            const uint32_t *a = (const uint32_t *)(U + (p & ~(int64_t)3));
-            fastm |= (uint32_t)fast << j;
-            shp |= (uint32_t)(p & 3) << (2 * j);
-            w0[j] = fast ? a[0] : 0u;
-            w1[j] = fast && (p & 3) ? a[1] : 0u;
+            const int64_t e = s_beg[k] + s_len[k];  // the end of read A's bytes
+            const int64_t nA = e - x < 4 ? e - x : 4;
+            const bool padA = QUAL && s_odd[k] && e - 1 <= x + 3;
+            bool ok = x >= dlo && x + 4 <= dhi && nA > 0;
+            int64_t pb = 0;
+            if (ok && nA < 4) {
+                const int k2 = k + 1;
+                ok = k2 < (int)nr && s_beg[k2] == e && x + 4 <= e + s_len[k2] &&
+                     !(QUAL && s_odd[k2] && e + s_len[k2] - 1 <= x + 3);
+                if (ok) pb = s_src[k2] + (x - e);
+            }
+            const int64_t pa = s_src[k] + (x - s_beg[k]);
+            const uint32_t *a = (const uint32_t *)(U + (pa & ~(int64_t)3));
+            const uint32_t *bb = (const uint32_t *)(U + (pb & ~(int64_t)3));
+            const bool two = ok && nA < 4;
+            gen |= (uint32_t)ok << jg;
+            sha |= (uint32_t)(pa & 3) << (2 * jg);
+            shb |= (uint32_t)(pb & 3) << (2 * jg);
+            nam |= (uint32_t)(nA & 7) << (3 * jg);
+            padm |= (uint32_t)padA << jg;
+            wa0[jg] = ok ? a[0] : 0u;
+            wa1[jg] = ok && (pa & 3) ? a[1] : 0u;
+            wb0[jg] = two ? bb[0] : 0u;
+            wb1[jg] = two && (pb & 3) ? bb[1] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < CP_J; j++) {
+        for (int jg = 0; jg < CP_G; jg++) {
+            const int j = g + jg;
             const int64_t x = t0 + 4 * (threadIdx.x + 256 * j);
             if (x + 4 <= dlo || x >= dhi) continue;
-            if ((fastm >> j) & 1u) {
-                const uint32_t sh = ((shp >> (2 * j)) & 3u) * 8;
-                *(uint32_t *)(dst + x) = sh ? (w0[j] >> sh) | (w1[j] << (32 - sh)) : w0[j];
+            if ((gen >> jg) & 1u) {
+                const uint32_t s1 = ((sha >> (2 * jg)) & 3u) * 8, s2 = ((shb >> (2 * jg)) & 3u) * 8;
+                const uint32_t va = s1 ? (wa0[jg] >> s1) | (wa1[jg] << (32 - s1)) : wa0[jg];
+                const uint32_t vb = s2 ? (wb0[jg] >> s2) | (wb1[jg] << (32 - s2)) : wb0[jg];
+                const uint32_t nA = (nam >> (3 * jg)) & 7u;
+                const uint32_t ma = nA >= 4 ? 0xffffffffu : (1u << (8 * nA)) - 1u;
+                uint32_t v = (va & ma) | (vb & ~ma);
+                if ((padm >> jg) & 1u) v &= ~(0xffu << (8 * (nA - 1)));  // A's pad byte
+                *(uint32_t *)(dst + x) = v;
                 continue;
             }
-            // a read boundary, the pad byte or a piece edge in this dword:
-            // the read again, then byte by byte
+            // a piece edge, a third read or B's pad byte in this dword: the
+            // read again, then byte by byte
             const int64_t x0 = x < dlo ? dlo : x;
             int lo = 0, hi = (int)nr - 1;
             while (lo < hi) {
@@ -815,6 +850,40 @@ __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ 
             }
             if (whole) *(uint32_t *)(dst + x) = v;
         }
+        }
+    }
+}
+
+// The same copy driven by the reads: 16 lanes per kept read, lane l moving
+// bytes [16 l, 16 l + 16) of its quality (QUAL) or packed-base region with
+// one unaligned 16-byte load and store, the read's last few bytes singly
+// (16-byte stores past a read's end would write the next read's bytes,
+// another lane's); an odd-length read's pad quality byte is 0.  A wave's
+// loads and stores cover four reads' regions, contiguous in both arrays.
+template <bool QUAL>
+__global__ void __launch_bounds__(256) k_copy_reads(const uint8_t *__restrict__ U, const int64_t *__restrict__ srcs,
+                                                    const int64_t *__restrict__ boff, const int32_t *__restrict__ lq,
+                                                    int64_t k0, int64_t n, uint8_t *__restrict__ dst) {
+    typedef uint32_t u32x4 __attribute__((vector_size(16)));
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t q = gid >> 4;
+    if (q >= n) return;
+    const int32_t l = lq[k0 + q];
+    const int64_t nb = ((int64_t)l + 1) & ~1LL;
+    const int64_t L = QUAL ? nb : nb / 2;
+    const int64_t off = 16 * (gid & 15);
+    for (int64_t o = off; o < L; o += 256) {
+        const uint8_t *src = U + (QUAL ? srcs[q] + nb / 2 : srcs[q]) + o;
+        uint8_t *d = dst + (QUAL ? boff[k0 + q] : boff[k0 + q] / 2) + o;
+        const int64_t m = L - o < 16 ? L - o : 16;
+        const bool pad = QUAL && (l & 1) && o + m == L;  // the region's last byte is the pad
+        if (m == 16 && !pad) {
+            u32x4 v;
+            __builtin_memcpy(&v, src, 16);
+            __builtin_memcpy(d, &v, 16);
+        } else {
+            for (int64_t j = 0; j < m; j++) d[j] = (pad && j == m - 1) ? 0 : src[j];
+        }
     }
 }
 
@@ -832,11 +901,39 @@ __global__ void k_name_ids(const uint8_t *__restrict__ nm, const int64_t *__rest
         if (hp == (uint32_t)p) continue;
         const uint32_t h = vals[hp];
         const int64_t a0 = nmoff[i], la = nmoff[i + 1] - a0, b0 = nmoff[h], lb = nmoff[h + 1] - b0;
-        bool eq = true;
-        for (int64_t c = 0; eq; c++) {
-            const uint8_t x = c < la ? nm[a0 + c] : 0, y = c < lb ? nm[b0 + c] : 0;
-            if (x != y) eq = false;
-            else if (x == 0 || c + 1 >= la) break;
+        // Names of equal length: 32 bytes at a time, the nine aligned words
+        // that cover each side's 32 loaded at once (a name's bytes are
+        // scattered over the chromosome's name array; a byte loop touched
+        // each of its lines ~25 times).  A mismatch -- or names of different
+        // lengths -- is settled by the byte loop (a NUL ends a name).
+        bool eq = true, slow = la != lb;
+        for (int64_t c = 0; !slow && c < la; c += 32) {
+            const uint8_t *pa = nm + a0 + c, *pb = nm + b0 + c;
+            const uint32_t *wa = (const uint32_t *)((uintptr_t)pa & ~(uintptr_t)3);
+            const uint32_t *wb = (const uint32_t *)((uintptr_t)pb & ~(uintptr_t)3);
+            const uint32_t sa = (uint32_t)((uintptr_t)pa & 3) * 8, sb = (uint32_t)((uintptr_t)pb & 3) * 8;
+            uint32_t A[9], B[9];
+#pragma unroll
+            for (int w = 0; w < 9; w++) {
+                A[w] = wa[w];
+                B[w] = wb[w];
+            }
+            const int64_t m = la - c < 32 ? la - c : 32;
+#pragma unroll
+            for (int w = 0; w < 8; w++) {
+                const uint32_t x = (uint32_t)((((uint64_t)A[w + 1] << 32) | A[w]) >> sa);
+                const uint32_t y = (uint32_t)((((uint64_t)B[w + 1] << 32) | B[w]) >> sb);
+                const int64_t left = m - 4 * w;
+                const uint32_t mk = left >= 4 ? 0xffffffffu : left <= 0 ? 0u : (1u << (8 * left)) - 1u;
+                slow |= ((x ^ y) & mk) != 0;
+            }
+        }
+        if (slow) {
+            for (int64_t c = 0; eq; c++) {
+                const uint8_t x = c < la ? nm[a0 + c] : 0, y = c < lb ? nm[b0 + c] : 0;
+                if (x != y) eq = false;
+                else if (x == 0 || c + 1 >= la) break;
+            }
         }
         if (!eq) atomicOr(bad, DB_NAMES);
     }
@@ -1129,7 +1226,7 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs,
     const int64_t pb = std::min<int64_t>(c->piece_bytes, ubytes) * 11 / 10 + (4 << 20);
     // records in a piece at the run's mean record size (+25%); a piece with
     // more grows its offsets (dd_run_decode)
-    const int64_t pr = (int64_t)((double)pb * (double)recs / (double)std::max<int64_t>(ubytes, 1) * 1.25) + 4096;
+    const int64_t pr = (int64_t)((double)pb * (double)recs / (double)std::max<int64_t>(ubytes, 1) * 1.3) + 4096;
     const int64_t nblk = ubytes / 32768 + 4096;  // BGZF blocks hold at most 64 KiB
     (void)span;  // (the compressed slots grow on the prefetch thread, dd_comp_upload)
     DGROW(c->rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
@@ -1310,6 +1407,32 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
         }
         ca = cb;
     }
+    // The piece slots sized once for the run's largest piece: a buffer that
+    // grows inside the loop frees its old block, and a free waits for the
+    // whole device (the loads in flight, the scans), which serialises the
+    // pipeline below
+    const int D = c->depth;
+    {
+        int64_t mx_pb = 0, mx_blk = 0, mx_ch = 0, mx_oc = 0;
+        for (const Piece &pc : pcs) {
+            mx_pb = std::max(mx_pb, pc.pbytes);
+            mx_blk = std::max(mx_blk, pc.bl - pc.bf + 2);
+            mx_ch = std::max(mx_ch, pc.cb - pc.ca + 1);
+            mx_oc = std::max(mx_oc, (int64_t)((double)pc.pbytes * rpb * 1.3) + 4096);
+        }
+        for (int k = 0; k < D && k < (int)pcs.size(); k++) {
+            RunSlot &r = c->rs[k];
+            DGROW(r.U, (size_t)mx_pb + 64);
+            DGROW(r.status, (size_t)mx_blk);
+            DGROW(r.ccnt, sizeof(uint32_t) * (size_t)mx_ch);
+            DGROW(r.cbase, sizeof(uint32_t) * (size_t)mx_ch);
+            DGROW(r.misc, 256);
+            DGROW(r.off, 8 * (size_t)(mx_oc + 1));
+            size_t tb = 0;
+            DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)mx_ch, r.st));
+            DGROW(r.tmp, tb);
+        }
+    }
     const bool parse = q->stage != nullptr;
     Carry car{};
     int64_t R_tot = 0, n_aux = 0, apack_tot = 0;
@@ -1329,7 +1452,6 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
     int64_t *tot = (int64_t *)((char *)c->misc.p + 128);
     int32_t *d_last = (int32_t *)((char *)c->misc.p + 192);
     DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
-    const int D = c->depth;
     for (int k = 0; k < D; k++) DCK(hipEventRecord(c->pev[k], st));
     // The load of piece p (inflate, record walk) runs on piece slot p % D's
     // own stream, issued D - 1 pieces ahead: it overlaps the statistics and
@@ -1558,7 +1680,14 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                                P<uint32_t>(c->nmo), P<int32_t>(c->rpos), so, car, P<int64_t>(c->srcs),
                                P<uint8_t>(c->nm), P<int64_t>(c->nmoff), P<uint64_t>(c->keys), P<uint32_t>(c->vals),
                                P<int64_t>(c->acand), q->read_name_len, d_last, bad);
-            if (n > 0) {  // the bases and qualities of the piece's kept reads
+            static const bool tiles = getenv("GROM_COPY_TILES") != nullptr;  // (A/B of the two copies)
+            if (n > 0 && !tiles) {  // the bases and qualities of the piece's kept reads
+                const unsigned g = (unsigned)((16 * n + 255) / 256);
+                hipLaunchKernelGGL(k_copy_reads<true>, dim3(g), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(c->srcs),
+                                   (const int64_t *)so.boff, (const int32_t *)so.lq, car.k, n, (uint8_t *)dv.qual);
+                hipLaunchKernelGGL(k_copy_reads<false>, dim3(g), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(c->srcs),
+                                   (const int64_t *)so.boff, (const int32_t *)so.lq, car.k, n, (uint8_t *)dv.seq);
+            } else if (n > 0) {
                 const int64_t lo = car.b, hi = car.b + nbs;
                 const int64_t nt_q = (hi + CP_T - 1) / CP_T - lo / CP_T, nt_s = (hi / 2 + CP_T - 1) / CP_T - (lo / 2) / CP_T;
                 DGROW(c->tfq, 8 * (size_t)(nt_q + 1));

@@ -61,6 +61,12 @@
 #define GI_LANE_DWORDS 94
 #define GI_LANE_BYTES (GI_LANE_DWORDS * 4)
 
+// per-trip statistics hooks (tools/inflate_trips.cpp); nothing by default
+#ifndef GI_TRIP
+#define GI_TRIP(mode) (void)0
+#define GI_BYTES(kind, n) (void)0
+#endif
+
 // bytes a match step copies: four 16-byte loads, then four stores
 #define GI_COPY 64u
 
@@ -496,6 +502,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
     uint32_t pn = 0;
     int mode = GI_M_HDR, rc = GI_OK;
     while (mode != GI_M_DONE) {
+        GI_TRIP(mode);
         gi_refill(b);
         if (mode == GI_M_HDR) {
             const int m = gi_header<LANES>(b, lit, dist, H, tab, lane, bfinal, rem);
@@ -528,6 +535,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
                     break;
                 }
                 gi_lit(out, o, pend, pn, (uint32_t)s);
+                GI_BYTES(0, 1);
             } else if (s == 256) {
                 mode = bfinal ? GI_M_DONE : GI_M_HDR;
             } else {
@@ -579,6 +587,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
             }
             o += m;
             rem -= m;
+            GI_BYTES(1, m);
             if (m == D && D < GI_COPY) D <<= 1;
             if (!rem) mode = GI_M_SYM;
         } else if (mode == GI_M_STORED) {
@@ -586,6 +595,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
             gi_refill(b);
             const uint32_t m = rem < 4u ? rem : 4u;
             for (uint32_t j = 0; j < m; j++) gi_lit(out, o, pend, pn, gi_bits(b, 8));
+            GI_BYTES(2, m);
             rem -= m;
             if (!rem) mode = bfinal ? GI_M_DONE : GI_M_HDR;
         }

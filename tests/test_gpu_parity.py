@@ -725,9 +725,9 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
              "3w": {"GROM_DEVICE_DECODE": "1", "GROM_DD_WORKERS": "3"},
              "g0": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "0"},
              "g2": {"GROM_DEVICE_DECODE": "1", "GROM_WS_GUESS": "2"},
-             "cu": {"GROM_DEVICE_DECODE": "1", "GROM_TEST_CP_UNSTAGED": "1"},
+             "cu": {"GROM_DEVICE_DECODE": "1", "GROM_COPY_TILES": "1", "GROM_TEST_CP_UNSTAGED": "1"},
              "pc": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PIECE_MB": "0.0625"},
-             "pcu": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PIECE_MB": "0.0625", "GROM_TEST_CP_UNSTAGED": "1"}}
+             "pcu": {"GROM_DEVICE_DECODE": "1", "GROM_DD_PIECE_MB": "0.0625", "GROM_COPY_TILES": "1"}}
     for mode, env in modes.items():
         capfd.readouterr()
         run_grom(datadir, bam, fa, f"g{mode}_{tag}.vcf", extra,
@@ -752,13 +752,15 @@ def _sha_rows(path):
     return h.hexdigest(), rows
 
 
-@pytest.mark.parametrize("case", ["c4_20mb_60x", "genome_s010"])
+@pytest.mark.parametrize("case", ["c4_20mb_60x", "genome_s010", "genome_s100"])
 def test_oracle_digest_cases(datadir, case):
     """Inputs too large for the oracle inside a GPU test, checked against the
     oracle's digests (tests/golden/oracle_<case>.json, written on the CPU by
     tools/make_golden_genome.py): BASELINE configs[4]'s shape at 20 Mb (60x
-    tetraploid male donor, -p 4 -g 1 -M -V 1) and a 24-contig genome at 0.1 of
-    GRCh38's lengths (configs[2]'s shape, -M -g 1).  The BAM is written here
+    tetraploid male donor, -p 4 -g 1 -M -V 1), a 24-contig genome at 0.1 of
+    GRCh38's lengths (configs[2]'s shape, -M -g 1), and the bench's own
+    full-scale configs[2] genome (3.09 Gb, a 20 GB BAM; the oracle took 2.6 h
+    on one core, 3,178,516 rows).  The BAM is written here
     by the same deterministic grom_synth call; VCF and .ctx.vcf must hash to
     the oracle's."""
     import json

@@ -15,3 +15,18 @@ for name, n, tot, avg in rows:
 print("\n".join(lines))
 if len(sys.argv) > 2:
     open(sys.argv[2], "w").write("\n".join(lines) + "\n")
+
+# optional: every launch (short name, start/end in ms from the first launch,
+# stream and queue ids where the database has them), for timelines
+if len(sys.argv) > 3:
+    cols = [d[0] for d in c.execute("select * from kernels limit 1").description]
+    extra = [k for k in ("stream_id", "queue_id") if k in cols]
+    q = "select name, start, end" + "".join(", " + k for k in extra) + " from kernels order by start"
+    launches = c.execute(q).fetchall()
+    t0 = launches[0][1] if launches else 0
+    with open(sys.argv[3], "w") as f:
+        f.write("kernel,start_ms,end_ms" + "".join("," + k for k in extra) + "\n")
+        for r in launches:
+            short = r[0].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+            short = short.split("<rocprim")[0].replace(",", ";")[:60]
+            f.write(f"{short},{(r[1] - t0) / 1e6:.4f},{(r[2] - t0) / 1e6:.4f}" + "".join(f",{v}" for v in r[3:]) + "\n")

@@ -65,6 +65,8 @@ step_whole() {
       if [ "$r" != "1" ]; then cmp w_1.vcf w_$r.vcf && cmp w_1.ctx.vcf w_$r.ctx.vcf || exit 1; fi
     done
     sha256sum w_1.vcf w_1.ctx.vcf | tee $repo/$out/sha.txt
+    echo "rows sha256 vcf $(grep -v '^#' w_1.vcf | sha256sum | cut -c1-64) ctx $(grep -v '^#' w_1.ctx.vcf | sha256sum | cut -c1-64)" \
+        | tee -a $repo/$out/sha.txt
     echo "rows $(grep -vc '^#' w_1.vcf)" )
 }
 
@@ -75,7 +77,7 @@ step_trace() {
         || { tail $repo/$out/trace_run.log; exit 1; } )
   local db
   db=$(find $out/trace -name "*.db" | head -1)
-  python3 tools/kstats.py $db $out/kernel_stats.csv | head -30
+  python3 tools/kstats.py $db $out/kernel_stats.csv $out/launches.csv | head -30
   find $out/trace -name "*kernel_stats.csv" -exec cp {} $out/rocprof_kernel_stats.csv \;
   rm -rf $out/trace
 }
