@@ -92,7 +92,7 @@ C2 = dict(coverage=30.0, dup_frac=0.0, sv_per_mb=0.0, cnv_rate=0.0, cnv_range=(0
 GENOME_FLAGS = ["-M", "-g", "1"]
 
 FOOTPRINT = re.compile(r"^footprint: peak ([\d.]+) GB of device memory \(([^)]*)\).*buffers: peak ([\d.]+) GB together.*"
-                       r"; (\d+) allocations waited ([\d.]+) s")
+                       r"; (\d+) allocations waited ([\d.]+) s(?:.*; (\d+) slow hipMalloc calls ([\d.]+) s)?")
 ORACLE_FULL = os.path.join(REPO, "tests", "golden", "oracle_genome_s100.json")
 CHROM_LINE = re.compile(r"^(\S+): (\d+) reads, ([\d.]+) ms on GPU .*; pileup ([\d.]+) ms, cnv ([\d.]+) ms, "
                         r"cigar_ops (\d+), bases (\d+), len (\d+)$")
@@ -201,7 +201,8 @@ def footprint(stdout):
         m = FOOTPRINT.match(line)
         if m:
             return {"peak_gb": float(m.group(1)), "measured_as": m.group(2), "buffers_peak_gb": float(m.group(3)),
-                    "allocations_waited": int(m.group(4)), "wait_s": float(m.group(5))}
+                    "allocations_waited": int(m.group(4)), "wait_s": float(m.group(5)),
+                    "slow_hipmalloc": int(m.group(6) or 0), "slow_hipmalloc_s": float(m.group(7) or 0.0)}
     return None
 
 
@@ -552,7 +553,10 @@ def main():
                                     "buffers_peak_gb_max": max(f["buffers_peak_gb"] for f in feet),
                                     "measured_as": feet[0]["measured_as"],
                                     "allocations_waited": sum(f["allocations_waited"] for f in feet),
-                                    "wait_s": round(sum(f["wait_s"] for f in feet), 3)} if feet else None,
+                                    "wait_s": round(sum(f["wait_s"] for f in feet), 3),
+                                    "slow_hipmalloc_runs": sum(1 for f in feet if f["slow_hipmalloc"]),
+                                    "slow_hipmalloc_s": round(sum(f["slow_hipmalloc_s"] for f in feet), 3)}
+                if feet else None,
             },
             "identical_to_oracle_full_scale": full["identical"] if full else None,
             "oracle_full_scale": full,

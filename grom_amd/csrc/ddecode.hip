@@ -1074,10 +1074,11 @@ struct dd_ctx {
     DBuf rblk, rS;          // the run's BGZF block table and record starts
     DBuf nml, nmo, nm, nmoff;  // per piece record: name length, its offset; per chromosome: name bytes, offsets
     // inflated bytes per piece (GROM_DD_PIECE_MB): a launch of k_inflate takes
-    // at least the time one lane needs for one block, so a piece must hold
-    // about half a chip's worth of blocks (two pieces are in flight): 3 GB is
-    // ~48 k blocks, ~750 waves
-    int64_t piece_bytes = (int64_t)3 << 30;
+    // at least the time one lane needs for one block, so a piece must hold a
+    // good part of a chip's worth of blocks (two pieces are in flight): 2 GB
+    // is ~32 k blocks, ~500 waves (1 GB pieces made the inflate 2.7x slower;
+    // 2 GB ran as fast as 3 GB and saves 3 GB of HBM, profiles/r05r)
+    int64_t piece_bytes = (int64_t)2 << 30;
     std::vector<uint8_t> aux_bytes;  // the last run's split-read candidates (dd_parse_out)
     std::vector<int64_t> aux_off, aux_kidx;
     int64_t *h_small = nullptr;  // pinned: totals and scalars

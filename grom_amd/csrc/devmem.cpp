@@ -15,7 +15,11 @@
 namespace {
 
 std::atomic<int64_t> g_now[GROM_DEVCAT_N + 1], g_peak[GROM_DEVCAT_N + 1];
-std::atomic<int64_t> g_waits{0}, g_wait_ns{0};
+std::atomic<int64_t> g_waits{0}, g_wait_ns{0}, g_slow{0}, g_slow_ns{0};
+const char *cat_name(int cat) {
+    static const char *n[] = {"scan", "breakpoint", "CNV", "stage", "decode", "phase arena", "other"};
+    return cat >= 0 && cat < GROM_DEVCAT_N ? n[cat] : "other";
+}
 
 std::mutex g_mu;  // reclaim hooks, release epoch
 std::condition_variable g_cv;
@@ -68,6 +72,11 @@ extern "C" void grom_dev_waits(int64_t *n, double *secs) {
     if (secs) *secs = (double)g_wait_ns.load() / 1e9;
 }
 
+extern "C" void grom_dev_slow(int64_t *n, double *secs) {
+    if (n) *n = g_slow.load();
+    if (secs) *secs = (double)g_slow_ns.load() / 1e9;
+}
+
 extern "C" void grom_dev_release_notify(void) {
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -104,7 +113,20 @@ extern "C" int grom_dev_malloc(void **p, size_t bytes, int cat) {
     for (;;) {
         const bool capped = cap > 0 && (double)(g_now[GROM_DEVCAT_N].load() + (int64_t)bytes) > cap;
         if (!capped) {
-            if (hipMalloc(p, bytes) == hipSuccess) {
+            const auto c0 = std::chrono::steady_clock::now();
+            const hipError_t e = hipMalloc(p, bytes);
+            const int64_t cns =
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - c0).count();
+            if (cns > 100000000) {
+                // one hipMalloc call that took long although the memory was
+                // there: on a freshly started process, the driver still
+                // clearing what an earlier process released
+                g_slow++;
+                g_slow_ns += cns;
+                fprintf(stderr, "grom: hipMalloc of %.2f GB (%s) took %.1f ms\n", (double)bytes / 1e9, cat_name(cat),
+                        cns / 1e6);
+            }
+            if (e == hipSuccess) {
                 grom_dev_note(cat, (int64_t)bytes);
                 if (waited) {
                     const int64_t ns =

@@ -65,6 +65,8 @@ void grom_dev_note(int cat, int64_t delta);
 void grom_dev_peaks(int64_t *peak, int64_t *now);
 /* allocations that waited, and the seconds they waited */
 void grom_dev_waits(int64_t *n, double *secs);
+/* hipMalloc calls that took over 0.1 s (each is also logged to stderr) */
+void grom_dev_slow(int64_t *n, double *secs);
 
 #ifdef __cplusplus
 }

@@ -738,16 +738,18 @@ static void fp_stop(fp_sampler *F, double since_start) {
     pthread_cond_broadcast(&F->cv);
     pthread_mutex_unlock(&F->mu);
     pthread_join(F->thr, NULL);
-    int64_t pk[GROM_DEVCAT_N + 1], nw = 0;
-    double sw = 0;
+    int64_t pk[GROM_DEVCAT_N + 1], nw = 0, ns = 0;
+    double sw = 0, ss = 0;
     grom_dev_peaks(pk, NULL);
     grom_dev_waits(&nw, &sw);
+    grom_dev_slow(&ns, &ss);
     printf("footprint: peak %.2f GB of device memory (%s), at %.3f s of %.3f s; buffers: peak %.2f GB together, "
            "per kind scan %.2f, breakpoint %.2f, CNV %.2f, stages %.2f, decode %.2f, phase arenas %.2f GB; %lld "
-           "allocations waited %.3f s for memory\n", F->peak / 1e9,
+           "allocations waited %.3f s for memory; %lld slow hipMalloc calls %.3f s\n", F->peak / 1e9,
            F->kfd ? "this process, kfd" : "device-wide use above the start's", F->t_peak, since_start,
            pk[GROM_DEVCAT_N] / 1e9, pk[GROM_DEVCAT_SCAN] / 1e9, pk[GROM_DEVCAT_SV] / 1e9, pk[GROM_DEVCAT_CNV] / 1e9,
-           pk[GROM_DEVCAT_STAGE] / 1e9, pk[GROM_DEVCAT_DECODE] / 1e9, pk[GROM_DEVCAT_ARENA] / 1e9, (long long)nw, sw);
+           pk[GROM_DEVCAT_STAGE] / 1e9, pk[GROM_DEVCAT_DECODE] / 1e9, pk[GROM_DEVCAT_ARENA] / 1e9, (long long)nw, sw,
+           (long long)ns, ss);
     pthread_mutex_destroy(&F->mu);
     pthread_cond_destroy(&F->cv);
     F->started = 0;
@@ -1202,10 +1204,13 @@ static int run_streamed(cli_state *S) {
     if (!g_plan_only) {
         int per_gpu = getenv("GROM_SCANS_PER_GPU") ? atoi(getenv("GROM_SCANS_PER_GPU")) : 2;
         if (per_gpu < 1) per_gpu = 1;
-        /* one stage per scan plus the one being decoded: a scan gives its
-         * stage back before its CNV path (grom_stage_on_consumed);
-         * GROM_STAGES overrides */
-        int n_st = getenv("GROM_STAGES") ? atoi(getenv("GROM_STAGES")) : per_gpu + 1;
+        /* one stage per scan: a scan gives its stage back before its CNV
+         * path (grom_stage_on_consumed), so the next chromosome decodes into
+         * it while the CNV path runs.  A third stage (GROM_STAGES=3, the
+         * round-4/5 default) let the decode run one chromosome further ahead
+         * for 15.5 GB more at 30x, and the whole run was no faster
+         * (profiles/r05r: 4.03-4.04 s against 4.00-4.12 s) */
+        int n_st = getenv("GROM_STAGES") ? atoi(getenv("GROM_STAGES")) : per_gpu;
         if (n_st < 1) n_st = 1;
         for (int d = 0; d < S->n_dev && !wd; d++)
             for (int k = 0; k < n_st && n_stages < 256; k++) {

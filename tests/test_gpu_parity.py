@@ -818,11 +818,13 @@ def test_hbm_cap_waits_for_memory(datadir):
     what the run holds uncapped -- room for the scan contexts, the decoder and
     about one and a half input stages -- allocations first free idle stages'
     blocks and then wait for a scan to give its stage back.  The rows must
-    still be the oracle's."""
+    still be the oracle's.  Three stages (the CLI's default is one per scan
+    context, two): the cap leaves room for one and a half of them, so a scan
+    can always go on while another waits."""
     from _util import FILEDATE, GROM_BIN, SEED
     case, extra = "c3_genome", ["-M", "-V", "1"]
     bam, fa, tag = _oracle_once(datadir, case, extra)
-    env = dict(os.environ, GROM_FILEDATE=FILEDATE, GROM_SEED=SEED, GROM_VERBOSE="1")
+    env = dict(os.environ, GROM_FILEDATE=FILEDATE, GROM_SEED=SEED, GROM_VERBOSE="1", GROM_STAGES="3")
 
     def run(out, more):
         r = subprocess.run([GROM_BIN, "-i", bam, "-r", fa, "-o", out] + extra, env=dict(env, **more),

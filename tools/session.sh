@@ -17,6 +17,9 @@
 #   pmc NAME "CTRS" [K=V ...]  one rocprofv3 --pmc pass (CTRS: one pass's
 #                              counters) over a whole run; NAME.csv per kernel
 #   bench [bench args]         python bench.py ... > bench.json
+#   share CHROMS RUNS          a multi-GPU rank's share: the plan-only run that
+#                              writes <bam>.mean, then RUNS runs over the
+#                              chromosomes CHROMS (GROM_CHROMS, as bench.py's ranks)
 #   probe CHECK [K=V ...]      the GPU inflater alone on /tmp/gw/g.bam
 #                              (tools/inflate_probe.py; CHECK=1: against zlib)
 #
@@ -92,6 +95,20 @@ step_pmc() {
   db=$(find $out/pmc_$name -name "*.db" | head -1)
   [ -n "$db" ] && python3 tools/pmc_summary.py $db $out/pmc_$name.csv | head -12
   rm -rf $out/pmc_$name
+}
+
+step_share() {
+  local chroms=$1 runs=$2
+  ( cd $work
+    GROM_PLAN_ONLY=1 GROM_CHROMS=- timeout -k 10 300 $repo/grom_amd/bin/grom -i g.bam -r g.fa -o prewarm.vcf $FLAGS \
+        > $repo/$out/share_prewarm.log 2>&1 || { tail $repo/$out/share_prewarm.log; exit 1; }
+    for r in $(seq 1 $runs); do
+      { time env GROM_CHROMS=$chroms GROM_VERBOSE=1 timeout -k 10 300 $repo/grom_amd/bin/grom -i g.bam -r g.fa -o s_$r.vcf $FLAGS \
+          > $repo/$out/share_$r.log 2>&1 ; } 2> $repo/$out/share_$r.time || { tail $repo/$out/share_$r.log; exit 1; }
+      echo "== share run $r: $(cat $repo/$out/share_$r.time)"
+      grep -h "decode:\|cli \|footprint\|took\|Loading" $repo/$out/share_$r.log
+    done
+    echo "rows $(grep -vc '^#' s_1.vcf)" )
 }
 
 step_probe() {
