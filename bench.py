@@ -405,7 +405,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import grom_amd
-    from grom_amd.shard import assign_chromosomes, max_over_ranks, merge_rank_outputs
+    from grom_amd.shard import all_gather_objects, assign_chromosomes, max_over_ranks, merge_rank_outputs_parallel
 
     def barrier():
         if world > 1:
@@ -440,23 +440,24 @@ def main():
     if world > 1:
         env.update(GROM_CHROMS=",".join(names[i].lower() for i in mine),
                    GROM_DECODE_THREADS=str(max(1, cpus // world)),
-                   GROM_CTX_RAW=os.path.join(work, f"rank{rank}.ctxraw"))
+                   GROM_CTX_RAW=os.path.join(work, f"rank{rank}.ctxraw"),
+                   GROM_VCF_SEGS=os.path.join(work, f"rank{rank}.segs"))
     out = os.path.join(work, f"rank{rank}.vcf")
     hdr_names = names  # BAM target names (the CTX post-pass maps mate ids to them)
 
     def step():
         dt, so = whole_run(work, bam, fa, out, flags, env)
         if world > 1:
+            # every rank copies its own chromosomes' rows into the merged VCF
+            # at their offsets (the CLI's segment index, an all-gather of the
+            # segment sizes); rank 0 adds the header and the CTX post-pass
             barrier()
-            if rank == 0:
-                m = open(bam + ".mean").read().split()  # insert mean, lseq, min, max (save_insert_mean)
-                vcf, bnd = merge_rank_outputs([os.path.join(work, f"rank{r}.vcf") for r in range(world)],
-                                              [os.path.join(work, f"rank{r}.ctxraw") for r in range(world)],
-                                              [n.lower() for n in names], hdr_names, int(m[3]), int(m[1]))
-                with open(os.path.join(work, "merged.vcf"), "w") as f:
-                    f.write(vcf)
-                with open(os.path.join(work, "merged.ctx.vcf"), "w") as f:
-                    f.write(bnd)
+            m = open(bam + ".mean").read().split()  # insert mean, lseq, min, max (save_insert_mean)
+            merge_rank_outputs_parallel(rank, out, [names[i].lower() for i in mine], [n.lower() for n in names],
+                                        os.path.join(work, "merged.vcf"), all_gather_objects, barrier,
+                                        [os.path.join(work, f"rank{r}.ctxraw") for r in range(world)], hdr_names,
+                                        int(m[3]), int(m[1]), os.path.join(work, "merged.ctx.vcf"),
+                                        segs_path=os.path.join(work, f"rank{rank}.segs"))
         return dt, so
 
     if world > 1 and rank == 0:

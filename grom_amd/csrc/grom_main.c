@@ -576,8 +576,22 @@ static int scan_job(int slot, grom_job *j, const grom_params *P, int verbose) {
  * counts) and scanned by one of that GPU's workers.  Rows are written in
  * chromosome order, so the VCF is the same bytes as a one-GPU run. */
 
+/* GROM_VCF_SEGS (a multi-GPU rank's run): where each chromosome's rows lie
+ * in the VCF, "chromosome<TAB>offset<TAB>bytes" per line, so a merge of the
+ * ranks' files copies byte ranges without reading the rows
+ * (grom_amd.shard.merge_rank_outputs_parallel) */
+static textbuf g_vcf_segs;
+
 /* a finished chromosome: its VCF rows go out, its raw CTX rows are kept */
 static void take_rows(grom_job *j, FILE *vcf, textbuf *ctx_all) {
+    if (j->text_len && getenv("GROM_VCF_SEGS")) {
+        const char *tab = memchr(j->text, '\t', j->text_len);
+        char line[320];
+        const int nl = tab ? (int)(tab - j->text) : 0;
+        const int k = snprintf(line, sizeof(line), "%.*s\t%ld\t%zu\n", nl < 256 ? nl : 256, j->text, ftell(vcf),
+                               (size_t)j->text_len);
+        if (k > 0) textbuf_add(&g_vcf_segs, line, (size_t)k);
+    }
     if (j->text_len) fwrite(j->text, 1, j->text_len, vcf);
     free(j->text);
     j->text = NULL;
@@ -868,6 +882,16 @@ static int passes_length(const cli_state *S, const chrom_plan *c) {
 }
 
 static void finish_outputs(cli_state *S, textbuf *ctx_all) {
+    const char *segs = getenv("GROM_VCF_SEGS");
+    if (segs) {
+        FILE *f = fopen(segs, "w");
+        if (f) {
+            if (g_vcf_segs.len) fwrite(g_vcf_segs.p, 1, g_vcf_segs.len, f);
+            fclose(f);
+        }
+        free(g_vcf_segs.p);
+        memset(&g_vcf_segs, 0, sizeof(g_vcf_segs));
+    }
     const char *raw = getenv("GROM_CTX_RAW"); /* the raw CTX rows, for a merge of several ranks' runs */
     if (raw) {
         FILE *f = fopen(raw, "w");

@@ -448,7 +448,8 @@ def test_rank_shares_merge_to_one_run(datadir):
     for r, share in enumerate(shares):
         run_grom(datadir, bam, fa, f"r{r}.vcf", flags,
                  env_extra={"GROM_CHROMS": ",".join(names[i].lower() for i in share),
-                            "GROM_CTX_RAW": str(datadir / f"r{r}.raw")})
+                            "GROM_CTX_RAW": str(datadir / f"r{r}.raw"),
+                            "GROM_VCF_SEGS": str(datadir / f"r{r}.segs")})
     m = open(bam + ".mean").read().split()
     vcf, bnd = merge_rank_outputs([str(datadir / f"r{r}.vcf") for r in range(3)],
                                   [str(datadir / f"r{r}.raw") for r in range(3)], [n.lower() for n in names], names,
@@ -457,6 +458,37 @@ def test_rank_shares_merge_to_one_run(datadir):
     assert one.count("\n") > 100 and vcf == one
     one_ctx = "".join(l for l in open(datadir / "one.ctx.vcf") if not l.startswith("#"))
     assert bnd == one_ctx and bnd.count("SVTYPE=BND") >= 2
+    # bench.py's merge: every rank copies its rows to their offsets from the
+    # CLI's segment index (three threads stand in for the ranks)
+    import threading
+    from grom_amd.shard import merge_rank_outputs_parallel
+    bar, got = threading.Barrier(3), [None] * 3
+
+    def gather_of(r):
+        def g(obj):
+            got[r] = obj
+            bar.wait()
+            return list(got)
+        return g
+    errs = []
+
+    def rank_main(r):
+        try:
+            merge_rank_outputs_parallel(r, str(datadir / f"r{r}.vcf"), [names[i].lower() for i in shares[r]],
+                                        [n.lower() for n in names], str(datadir / "par.vcf"), gather_of(r), bar.wait,
+                                        [str(datadir / f"r{k}.raw") for k in range(3)], names, int(m[3]), int(m[1]),
+                                        str(datadir / "par.ctx.vcf"), segs_path=str(datadir / f"r{r}.segs"))
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errs.append(e)
+            bar.abort()
+    ths = [threading.Thread(target=rank_main, args=(r,)) for r in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    assert open(datadir / "par.vcf").read() == one
+    assert open(datadir / "par.ctx.vcf").read() == bnd
 
 
 @pytest.mark.parametrize("mode", ["host", "device"])

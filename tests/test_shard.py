@@ -166,3 +166,84 @@ def test_ctx_postpass_pairs_translocations():
     rows = text.splitlines()
     assert len(rows) == 2 and all("SVTYPE=BND" in r for r in rows), text
     assert rows[0].startswith("chr1\t1001\t") and "chr2:5000" in rows[0]
+
+
+# ---- the parallel merge of the ranks' VCFs (bench.py --gpus N) ----
+
+_MERGE_CHROMS = ["chr1", "chr2", "chr3", "chr4", "chr5"]
+
+
+def _rank_vcf(path, chroms, seg_path=None):
+    """A rank's CLI output: the header, then each of its chromosomes' rows
+    together (different row counts per chromosome; chr4 has none)."""
+    hdr = "##fileformat=VCFv4.1\n#CHROM\tPOS\tID\tREF\tALT\n"
+    rows = {c: "".join(f"{c}\t{p}\t.\tA\tT\n" for p in range(1, 1 + 3 * (i + 1)))
+            for i, c in enumerate(_MERGE_CHROMS) if c != "chr4"}
+    body, segs, at = "", [], len(hdr)
+    for c in chroms:
+        t = rows.get(c, "")
+        if t:
+            segs.append(f"{c}\t{at}\t{len(t)}\n")
+        body += t
+        at += len(t)
+    with open(path, "w") as f:
+        f.write(hdr + body)
+    if seg_path:
+        with open(seg_path, "w") as f:
+            f.write("".join(segs))
+
+
+def _merge_worker(rank, world, port, d, use_segs, q):
+    import torch.distributed as dist
+    from grom_amd.shard import all_gather_objects, merge_rank_outputs_parallel
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = [c for i, c in enumerate(_MERGE_CHROMS) if i % world == rank]
+        merge_rank_outputs_parallel(rank, os.path.join(d, f"r{rank}.vcf"), mine, _MERGE_CHROMS,
+                                    os.path.join(d, "merged.vcf"), all_gather_objects, dist.barrier,
+                                    segs_path=os.path.join(d, f"r{rank}.segs") if use_segs else None)
+        q.put((rank, "ok"))
+    except BaseException as e:  # noqa: BLE001 -- reported to the test
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("use_segs", [True, False], ids=["segment_index", "scan"])
+def test_gloo_world2_parallel_merge_matches_rank0_merge(tmp_path, use_segs):
+    """bench.py's N>1 merge: every rank copies its chromosomes' rows to their
+    offsets in the merged VCF (from the CLI's GROM_VCF_SEGS index, or by
+    scanning its file); the bytes equal rank 0's merge_rank_outputs join."""
+    import torch.multiprocessing as mp
+    from grom_amd.shard import merge_rank_outputs
+    world = 2
+    for r in range(world):
+        mine = [c for i, c in enumerate(_MERGE_CHROMS) if i % world == r]
+        _rank_vcf(tmp_path / f"r{r}.vcf", mine, tmp_path / f"r{r}.segs")
+        (tmp_path / f"r{r}.ctxraw").write_text("")
+    want, _ = merge_rank_outputs([str(tmp_path / f"r{r}.vcf") for r in range(world)],
+                                 [str(tmp_path / f"r{r}.ctxraw") for r in range(world)], _MERGE_CHROMS,
+                                 _MERGE_CHROMS, 600, 150)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_merge_worker, args=(r, world, port, str(tmp_path), use_segs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: "ok", 1: "ok"}, res
+    assert (tmp_path / "merged.vcf").read_text() == want
+    assert want.count("\n") == 2 + 3 + 6 + 9 + 15
+
+
+def test_vcf_segments_rejects_interleaved_rows():
+    from grom_amd.shard import vcf_segments
+    data = b"#h\nchr1\t1\nchr2\t1\nchr1\t2\n"
+    with pytest.raises(RuntimeError):
+        vcf_segments(data, ["chr1", "chr2"])
+    assert vcf_segments(b"#h\nchr1\t1\nchr1\t2\nchr2\t1\n", ["chr1", "chr2"]) == (3, {"chr1": (3, 17), "chr2": (17, 24)})
