@@ -99,8 +99,13 @@ struct TileTail {
     uint32_t cbase;          // the tile's first candidate slot
 };
 
+// the chunk's records in LDS at a stride of 13 words: a lane per record reads
+// and writes them, and the plain 12-word stride put every 8th lane of a
+// 32-lane half on the same bank (4-way conflicts; 13 is odd: none)
+#define META_W 13
+
 struct __align__(16) ScanLds {
-    ReadMeta meta[RCHUNK];
+    uint32_t meta[RCHUNK * META_W];
     uint4 qual[QV + 1];  // + a slot the clamped loads past the window are stored to
     uint4 seq[SV + 1];
     uint32_t cig[CIGCAP];
@@ -118,6 +123,22 @@ struct __align__(16) ScanLds {
 // tiles with more reads than this keep the per-lane interval updates (the
 // packed 16-bit caf counts could overflow)
 #define DIFF_MAX_READS 30000
+
+__device__ __forceinline__ ReadMeta meta_ld(const ScanLds &L, int i) {
+    const uint32_t *p = L.meta + META_W * i;
+    ReadMeta r;
+    r.a = make_uint4(p[0], p[1], p[2], p[3]);
+    r.b = make_uint4(p[4], p[5], p[6], p[7]);
+    r.c = make_uint4(p[8], p[9], p[10], p[11]);
+    return r;
+}
+
+__device__ __forceinline__ void meta_st(ScanLds &L, int i, const ReadMeta &r) {
+    uint32_t *p = L.meta + META_W * i;
+    p[0] = r.a.x; p[1] = r.a.y; p[2] = r.a.z; p[3] = r.a.w;
+    p[4] = r.b.x; p[5] = r.b.y; p[6] = r.b.z; p[7] = r.b.w;
+    p[8] = r.c.x; p[9] = r.c.y; p[10] = r.c.z; p[11] = r.c.w;
+}
 
 // per-lane counters of one position (cdp_one_base_*)
 struct LaneCounts {
@@ -619,7 +640,7 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
         // ---- stage the packed records; find the prefix within the budgets ----
         if (tid < m) {
             const ReadMeta rm = meta[c0 + tid];
-            L.meta[tid] = rm;
+            meta_st(L, tid, rm);
             const ReadMeta f = meta[c0];
             const int64_t bo = ((int64_t)rm.c.x << 32) | rm.b.w, b0 = ((int64_t)f.c.x << 32) | f.b.w;
             const uint32_t ce = rm.b.x + (rm.b.y & 0xffffu);
@@ -631,7 +652,7 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
         int32_t m2 = min(L.m2, m);
         const bool staged = m2 > 0;
         if (!staged) m2 = 1;  // one oversized read: served from global memory
-        const ReadMeta &first = L.meta[0], &last = L.meta[m2 - 1];
+        const ReadMeta first = meta_ld(L, 0), last = meta_ld(L, m2 - 1);
         const int64_t b0 = ((int64_t)first.c.x << 32) | first.b.w;
         const int64_t bend = (((int64_t)last.c.x << 32) | last.b.w) + (int32_t)last.a.z;
         const uint32_t cf = first.b.x, cl = last.b.x + (last.b.y & 0xffffu);
@@ -663,20 +684,47 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
         // single-op staged reads: their caf and physical-depth intervals go
         // to the tile's difference arrays (one lane per read), so the fold
         // below skips those per-lane updates (GROM.c:6605-6671, 7173-7181)
-        if (use_diff && staged && tid < m2) {
-            const ReadMeta &rm = L.meta[tid];
-            const int32_t p0 = (int32_t)rm.a.x, len = (int32_t)rm.a.z;
-            const uint32_t mq = rm.b.z & 255u;
-            if (rm.b.z & MK_FAST) {
-                const int32_t lo = max(p0, t0) - t0, hi = min(p0 + len, t0 + TG) - t0;
-                if (lo < hi) {
-                    const uint32_t inc = ((int32_t)mq >= a.rd_min_mapq) ? 1u : 65536u;  // signed, as the oracle
-                    atomicAdd(&L.dmq[lo], (int32_t)mq);
-                    atomicSub(&L.dmq[hi], (int32_t)mq);
-                    atomicAdd(&L.dcnt[lo], inc);
-                    atomicSub(&L.dcnt[hi], inc);
+        // Reads that start before the tile all add at index 0 and those that
+        // end past it all subtract at TG, which the scan never reads: one
+        // wave-summed add at 0 instead of up to a chunk of same-address
+        // atomics (most of the kernel's LDS bank-conflict cycles), and no
+        // update at TG.
+        if (use_diff && staged) {
+            int32_t mq0 = 0;
+            uint32_t inc0 = 0;
+            if (tid < m2) {
+                const uint32_t bz = L.meta[META_W * tid + 6];
+                const int32_t p0 = (int32_t)L.meta[META_W * tid], len = (int32_t)L.meta[META_W * tid + 2];
+                const uint32_t mq = bz & 255u;
+                if (bz & MK_FAST) {
+                    const int32_t lo = max(p0, t0) - t0, hi = min(p0 + len, t0 + TG) - t0;
+                    if (lo < hi) {
+                        const uint32_t inc = ((int32_t)mq >= a.rd_min_mapq) ? 1u : 65536u;  // signed, as the oracle
+                        if (lo > 0) {
+                            atomicAdd(&L.dmq[lo], (int32_t)mq);
+                            atomicAdd(&L.dcnt[lo], inc);
+                        } else {
+                            mq0 = (int32_t)mq;
+                            inc0 = inc;
+                        }
+                        if (hi < TG) {
+                            atomicSub(&L.dmq[hi], (int32_t)mq);
+                            atomicSub(&L.dcnt[hi], inc);
+                        }
+                    }
+                    L.meta[META_W * tid + 6] = bz | DIFFED;  // read by the fold, written only here
                 }
-                L.meta[tid].b.z = rm.b.z | DIFFED;  // read by the fold, written only here
+            }
+            if (__ballot(mq0 != 0 || inc0 != 0)) {  // (wave-uniform)
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    mq0 += __shfl_xor(mq0, o, 64);
+                    inc0 += (uint32_t)__shfl_xor((int)inc0, o, 64);
+                }
+                if (lane == 0) {
+                    atomicAdd(&L.dmq[0], mq0);
+                    atomicAdd(&L.dcnt[0], inc0);
+                }
             }
         }
         __syncthreads();
@@ -691,7 +739,7 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
             GroupRegs G = {0, 0, 0, 0, 0, 0, 0, 0};
             bool rel = false;
             if (j < m2) {
-                const ReadMeta rm = L.meta[j];
+                const ReadMeta rm = meta_ld(L, j);
                 G.p0 = rm.a.x;
                 G.lq = rm.a.z;
                 G.nid = rm.a.w;
@@ -870,7 +918,8 @@ __device__ __forceinline__ void scan_tile_gather(ScanLds &L, SLOTS &slot, int64_
                     const bool at_l = start_adj >= a.sc_min && x == p0 - 1;
                     const bool at_r = end_adj >= a.sc_min && x == E;
                     if (evals && (at_l || at_r)) {
-                        const uint4 mate = L.meta[g + u.i].c;
+                        const uint32_t *mw = L.meta + META_W * (g + u.i) + 8;
+                        const uint4 mate = make_uint4(mw[0], mw[1], mw[2], mw[3]);
                         const uint32_t fl = u.fl;
                         const bool paired = fl & 0x1, munmap = fl & 0x8, rev = fl & 0x10;
                         const bool same_chr = (int32_t)mate.y == a.chr_tid;
