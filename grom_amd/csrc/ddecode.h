@@ -95,6 +95,12 @@ typedef struct dd_run_req {
     int32_t *h_ins, *h_lq;    /* the sample continues here */
     void (*stats_cb)(void *arg, int64_t taken, int64_t m_contrib, int complete);
     void *stats_arg;
+    /* the next run this context will decode, if its compressed bytes are on
+     * the device already: fills *next (slot, comp_len, blk, nblk, starts,
+     * n_starts, u_end, tid, count) and returns 1, its slot then held for
+     * that run; its first piece is loaded while this run finishes */
+    int (*next_cb)(void *arg, struct dd_run_req *next);
+    void *next_arg;
 } dd_run_req;
 /* 0; -2 when the data contradicts the index plan (the CLI then reads
  * serially); -1.  *n_rec: the records walked (all of the run's with a stage) */

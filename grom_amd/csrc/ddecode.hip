@@ -1059,6 +1059,13 @@ struct dd_ctx {
     int device = -1;
     RunSlot rs[DD_RSLOTS];
     int depth = 2;  // pieces in flight (GROM_DD_DEPTH, 1..DD_RSLOTS)
+    // the next run's first piece, issued while this run's last pieces parse
+    // (dd_run_decode's next_cb): its compressed slot, length, first record
+    // start and the piece slot it went to
+    struct {
+        int valid, comp_slot, rslot;
+        int64_t comp_len, u_lo;
+    } pre = {};
     hipStream_t st = nullptr;
     hipStream_t cst = nullptr;  // compressed runs' host->device copies (dd_comp_upload, the prefetch thread)
     DBuf dcomp[DD_SLOTS];
@@ -1071,7 +1078,7 @@ struct dd_ctx {
     DBuf keep, kidx, drop, didx, auxc, aidx, ncig, coff, nb, boff, rpos, krec, keys, vals, keys2, vals2, head, tmp;
     DBuf srcs, tfq, tfs;  // per kept read: its bases' offset in U; per copy tile: its first read
     DBuf sq, sqi, sv, slq, sm, s_ins, s_lq, acand, alen, aoff, akidx, apack;
-    DBuf rblk, rS;          // the run's BGZF block table and record starts
+    DBuf rblk[DD_SLOTS], rS[DD_SLOTS];  // per compressed slot: the run's BGZF block table and record starts
     DBuf nml, nmo, nm, nmoff;  // per piece record: name length, its offset; per chromosome: name bytes, offsets
     // inflated bytes per piece (GROM_DD_PIECE_MB): a launch of k_inflate takes
     // at least the time one lane needs for one block, so a piece must hold a
@@ -1185,7 +1192,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
                    &c->krec, &c->keys, &c->vals, &c->keys2, &c->vals2, &c->head, &c->tmp, &c->sq, &c->sqi, &c->sv,
                    &c->srcs, &c->tfq, &c->tfs,
                    &c->slq, &c->sm, &c->s_ins, &c->s_lq, &c->acand, &c->alen, &c->aoff, &c->akidx, &c->apack,
-                   &c->rblk, &c->rS, &c->nml, &c->nmo, &c->nm, &c->nmoff};
+                   &c->rblk[0], &c->rS[0], &c->rblk[1], &c->rS[1], &c->nml, &c->nmo, &c->nm, &c->nmoff};
     for (DBuf *b : all)
         if (b->p) grom_dev_free(b->p, b->cap, GROM_DEVCAT_DECODE);
     for (int k = 0; k < 4; k++)
@@ -1230,8 +1237,10 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs,
     const int64_t pr = (int64_t)((double)pb * (double)recs / (double)std::max<int64_t>(ubytes, 1) * 1.3) + 4096;
     const int64_t nblk = ubytes / 32768 + 4096;  // BGZF blocks hold at most 64 KiB
     (void)span;  // (the compressed slots grow on the prefetch thread, dd_comp_upload)
-    DGROW(c->rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
-    DGROW(c->rS, sizeof(int64_t) * (size_t)(n_starts + 2));
+    for (int k = 0; k < DD_SLOTS; k++) {
+        DGROW(c->rblk[k], sizeof(DdBlock) * (size_t)(nblk + 1));
+        DGROW(c->rS[k], sizeof(int64_t) * (size_t)(n_starts + 2));
+    }
     for (int k = 0; k < c->depth; k++) {
         RunSlot &r = c->rs[k];
         DGROW(r.U, (size_t)pb + 64);
@@ -1357,24 +1366,14 @@ static int dgrow_keep(DBuf &b, size_t bytes, size_t keep, hipStream_t st) {
 // earlier pieces reached (the carries).  The read names go to a chromosome-wide
 // byte array, so the read-name ids (a sort of the name hashes and a byte
 // check of every equal-hash run) come after the last piece.
-extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, int64_t *n_rec, char *err, int errlen) {
-    DCK(hipSetDevice(c->device));
-    memset(po, 0, sizeof(*po));
-    *n_rec = 0;
-    if (q->slot < 0 || q->slot >= DD_SLOTS || c->dcomp_len[q->slot] != q->comp_len) {
-        if (err) snprintf(err, (size_t)errlen, "device decode: slot %d does not hold the run", q->slot);
-        return -1;
-    }
-    hipStream_t st = c->st;
+struct Piece {
+    int64_t ca, cb, u_lo, u_hi, bf, bl, base, pbytes;
+};
+
+// a run's pieces: consecutive record-start chunks [ca, cb) of about
+// piece_bytes of inflated data each, on whole BGZF blocks
+static void plan_pieces(const dd_run_req *q, int64_t piece_bytes, std::vector<Piece> &pcs) {
     const int64_t nblk = q->nblk, ns = q->n_starts;
-    // the run's block table and record starts (+ its end) on the device
-    DGROW(c->rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
-    DGROW(c->rS, sizeof(int64_t) * (size_t)(ns + 2));
-    DCK(hipStreamWaitEvent(st, c->cev[q->slot], 0));
-    DCK(hipMemcpyAsync(c->rblk.p, q->blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(c->rS.p, q->starts, sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(P<int64_t>(c->rS) + ns, &q->u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    // pieces: consecutive chunks [ca, cb) of about piece_bytes
     auto block_of = [&](int64_t u) {  // the block whose output holds inflated offset u
         int64_t lo = 0, hi = nblk - 1;
         while (lo < hi) {
@@ -1384,16 +1383,10 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
         }
         return lo;
     };
-    struct Piece {
-        int64_t ca, cb, u_lo, u_hi, bf, bl, base, pbytes;
-    };
-    std::vector<Piece> pcs;
-    // records per inflated byte of the run (the index's count)
-    const double rpb = q->count > 0 && q->u_end > q->starts[0] ? (double)q->count / (double)(q->u_end - q->starts[0])
-                                                                 : 1.0 / 34.0;
+    pcs.clear();
     for (int64_t ca = 0; ca < ns;) {
         int64_t cb = ca + 1;
-        while (cb < ns && q->starts[cb] - q->starts[ca] < c->piece_bytes) cb++;
+        while (cb < ns && q->starts[cb] - q->starts[ca] < piece_bytes) cb++;
         Piece pc;
         pc.ca = ca;
         pc.cb = cb;
@@ -1408,32 +1401,127 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
         }
         ca = cb;
     }
-    // The piece slots sized once for the run's largest piece: a buffer that
-    // grows inside the loop frees its old block, and a free waits for the
-    // whole device (the loads in flight, the scans), which serialises the
-    // pipeline below
-    const int D = c->depth;
-    {
-        int64_t mx_pb = 0, mx_blk = 0, mx_ch = 0, mx_oc = 0;
-        for (const Piece &pc : pcs) {
-            mx_pb = std::max(mx_pb, pc.pbytes);
-            mx_blk = std::max(mx_blk, pc.bl - pc.bf + 2);
-            mx_ch = std::max(mx_ch, pc.cb - pc.ca + 1);
-            mx_oc = std::max(mx_oc, (int64_t)((double)pc.pbytes * rpb * 1.3) + 4096);
-        }
-        for (int k = 0; k < D && k < (int)pcs.size(); k++) {
-            RunSlot &r = c->rs[k];
-            DGROW(r.U, (size_t)mx_pb + 64);
-            DGROW(r.status, (size_t)mx_blk);
-            DGROW(r.ccnt, sizeof(uint32_t) * (size_t)mx_ch);
-            DGROW(r.cbase, sizeof(uint32_t) * (size_t)mx_ch);
-            DGROW(r.misc, 256);
-            DGROW(r.off, 8 * (size_t)(mx_oc + 1));
-            size_t tb = 0;
-            DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)mx_ch, r.st));
-            DGROW(r.tmp, tb);
-        }
+}
+
+// records per inflated byte of the run (the index's count)
+static double run_rpb(const dd_run_req *q) {
+    return q->count > 0 && q->u_end > q->starts[0] ? (double)q->count / (double)(q->u_end - q->starts[0]) : 1.0 / 34.0;
+}
+
+// the run's block table and record starts (+ its end) into its compressed
+// slot's device buffers (host copies from pageable memory: done on return)
+static int upload_run_tables(dd_ctx *c, const dd_run_req *q, hipStream_t st, char *err, int errlen) {
+    const int64_t nblk = q->nblk, ns = q->n_starts;
+    DBuf &rblk = c->rblk[q->slot], &rS = c->rS[q->slot];
+    DGROW(rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
+    DGROW(rS, sizeof(int64_t) * (size_t)(ns + 2));
+    DCK(hipMemcpyAsync(rblk.p, q->blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(rS.p, q->starts, sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice, st));
+    DCK(hipMemcpyAsync(P<int64_t>(rS) + ns, &q->u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    return 0;
+}
+
+// A piece slot sized once for the run's largest piece: a buffer that grows
+// inside the piece loop frees its old block, and a free waits for the whole
+// device (the loads in flight, the scans), which serialised the pipeline
+static int size_slot(RunSlot &r, const std::vector<Piece> &pcs, double rpb, char *err, int errlen) {
+    int64_t mx_pb = 0, mx_blk = 0, mx_ch = 0, mx_oc = 0;
+    for (const Piece &pc : pcs) {
+        mx_pb = std::max(mx_pb, pc.pbytes);
+        mx_blk = std::max(mx_blk, pc.bl - pc.bf + 2);
+        mx_ch = std::max(mx_ch, pc.cb - pc.ca + 1);
+        mx_oc = std::max(mx_oc, (int64_t)((double)pc.pbytes * rpb * 1.3) + 4096);
     }
+    DGROW(r.U, (size_t)mx_pb + 64);
+    DGROW(r.status, (size_t)mx_blk);
+    DGROW(r.ccnt, sizeof(uint32_t) * (size_t)mx_ch);
+    DGROW(r.cbase, sizeof(uint32_t) * (size_t)mx_ch);
+    DGROW(r.misc, 256);
+    DGROW(r.off, 8 * (size_t)(mx_oc + 1));
+    size_t tb = 0;
+    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)mx_ch, r.st));
+    DGROW(r.tmp, tb);
+    return 0;
+}
+
+// The load of one piece (inflate, record walk) on piece slot k's own stream.
+// The slot is reused once the parse of the piece before in it is done (pev);
+// the offsets walk writes up to the slot's record capacity (a piece with more
+// records is walked again by the caller after its buffer grows).
+static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, double rpb, char *err, int errlen) {
+    RunSlot &r = c->rs[k];
+    hipStream_t ls = r.st;
+    DCK(hipStreamWaitEvent(ls, c->pev[k], 0));
+    DCK(hipStreamWaitEvent(ls, c->cev[q->slot], 0));
+    DGROW(r.U, (size_t)pc.pbytes + 64);
+    DGROW(r.status, (size_t)(pc.bl - pc.bf + 2));
+    DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
+    DGROW(r.cbase, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
+    DGROW(r.misc, 256);
+    // record offsets: the run's mean record size (+30%)
+    const int64_t ocap = std::max<int64_t>((int64_t)(r.off.cap / 8) - 1, (int64_t)((double)pc.pbytes * rpb * 1.3) + 4096);
+    DGROW(r.off, 8 * (size_t)(ocap + 1));
+    uint32_t *rb = P<uint32_t>(r.misc);
+    DCK(hipMemsetAsync(r.misc.p, 0, 64, ls));
+    DCK(hipEventRecord(r.ev[0], ls));
+    if (dd_inflate_launch(ls, P<uint8_t>(c->dcomp[q->slot]), P<DdBlock>(c->rblk[q->slot]) + pc.bf, pc.bl - pc.bf + 1,
+                          P<uint8_t>(r.U), pc.base, P<uint8_t>(r.status), rb + 1)) {
+        if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
+        return -1;
+    }
+    DCK(hipEventRecord(r.ev[1], ls));
+    const int64_t nch = pc.cb - pc.ca;
+    const int64_t *Sp = P<int64_t>(c->rS[q->slot]) + pc.ca;
+    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
+                       c->ws_guess, rb + 4, P<uint32_t>(r.ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, rb,
+                       (int64_t)INT64_MAX);
+    size_t tb = 0;
+    DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
+    DGROW(r.tmp, tb);
+    DCK(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
+    hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
+                       c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), rb,
+                       ocap);
+    DCK(hipGetLastError());
+    DCK(hipMemcpyAsync(r.h_small, P<uint32_t>(r.cbase) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
+    DCK(hipMemcpyAsync((char *)r.h_small + 4, P<uint32_t>(r.ccnt) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
+    DCK(hipMemcpyAsync((char *)r.h_small + 8, rb, 8, hipMemcpyDeviceToHost, ls));
+    DCK(hipMemcpyAsync((char *)r.h_small + 16, rb + 4, 4, hipMemcpyDeviceToHost, ls));
+    DCK(hipEventRecord(r.ev[2], ls));
+    return 0;
+}
+
+extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, int64_t *n_rec, char *err, int errlen) {
+    DCK(hipSetDevice(c->device));
+    memset(po, 0, sizeof(*po));
+    *n_rec = 0;
+    if (q->slot < 0 || q->slot >= DD_SLOTS || c->dcomp_len[q->slot] != q->comp_len) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: slot %d does not hold the run", q->slot);
+        return -1;
+    }
+    hipStream_t st = c->st;
+    std::vector<Piece> pcs;
+    plan_pieces(q, c->piece_bytes, pcs);
+    const double rpb = run_rpb(q);
+    const int D = c->depth;
+    // This run's first piece already loading (issued by the run before, while
+    // its last pieces parsed)?  Its piece slot is then the base of this run's
+    // slot order; a piece issued for a run that is not this one is drained.
+    int base = 0;
+    bool pre = false;
+    if (c->pre.valid) {
+        if (c->pre.comp_slot == q->slot && c->pre.comp_len == q->comp_len && !pcs.empty() && pcs[0].u_lo == c->pre.u_lo) {
+            base = c->pre.rslot;
+            pre = true;
+        } else {
+            DCK(hipStreamSynchronize(c->rs[c->pre.rslot].st));
+        }
+        c->pre.valid = 0;
+    }
+    if (!pre && upload_run_tables(c, q, st, err, errlen)) return -1;
+    DCK(hipStreamWaitEvent(st, c->cev[q->slot], 0));
+    for (int k = 0; k < D && k < (int)pcs.size(); k++)
+        if (!(pre && k == 0) && size_slot(c->rs[(base + k) % D], pcs, rpb, err, errlen)) return -1;
     const bool parse = q->stage != nullptr;
     Carry car{};
     int64_t R_tot = 0, n_aux = 0, apack_tot = 0;
@@ -1454,65 +1542,43 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
     int32_t *d_last = (int32_t *)((char *)c->misc.p + 192);
     DCK(hipMemsetAsync(c->misc.p, 0, 256, st));
     for (int k = 0; k < D; k++) DCK(hipEventRecord(c->pev[k], st));
-    // The load of piece p (inflate, record walk) runs on piece slot p % D's
-    // own stream, issued D - 1 pieces ahead: it overlaps the statistics and
-    // the parse of the pieces before on the context's stream, and the loads
-    // in flight together fill the chip (a launch of k_inflate takes at least
-    // one lane's time for one block, whatever its size).  A slot is reused once
-    // the parse of the piece before in it is done (pev).  The offsets walk
-    // writes up to the slot's record capacity; a piece with more records is
-    // walked again after its buffer grows.
-    auto issue = [&](size_t p) -> int {
-        const Piece &pc = pcs[p];
-        RunSlot &r = c->rs[p % D];
-        hipStream_t ls = r.st;
-        DCK(hipStreamWaitEvent(ls, c->pev[p % D], 0));
-        DCK(hipStreamWaitEvent(ls, c->cev[q->slot], 0));
-        DGROW(r.U, (size_t)pc.pbytes + 64);
-        DGROW(r.status, (size_t)(pc.bl - pc.bf + 2));
-        DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
-        DGROW(r.cbase, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
-        DGROW(r.misc, 256);
-        // record offsets: the run's mean record size (+30%); a piece with more
-        // is walked again below
-        const int64_t ocap = std::max<int64_t>((int64_t)(r.off.cap / 8) - 1, (int64_t)((double)pc.pbytes * rpb * 1.3) + 4096);
-        DGROW(r.off, 8 * (size_t)(ocap + 1));
-        uint32_t *rb = P<uint32_t>(r.misc);
-        DCK(hipMemsetAsync(r.misc.p, 0, 64, ls));
-        DCK(hipEventRecord(r.ev[0], ls));
-        if (dd_inflate_launch(ls, P<uint8_t>(c->dcomp[q->slot]), P<DdBlock>(c->rblk) + pc.bf, pc.bl - pc.bf + 1,
-                              P<uint8_t>(r.U), pc.base, P<uint8_t>(r.status), rb + 1)) {
-            if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
+    // The load of piece p (inflate, record walk) runs on piece slot
+    // (base + p) % D's own stream, issued D - 1 pieces ahead: it overlaps the
+    // statistics and the parse of the pieces before on the context's stream,
+    // and the loads in flight together fill the chip (a launch of k_inflate
+    // takes at least one lane's time for one block, whatever its size).  When
+    // this run issues no more pieces, the next run's first piece (next_cb: its
+    // compressed bytes already on the device) goes to the slot that frees
+    // next, so its inflate overlaps this run's last parses and name ids
+    // instead of waiting for them (24 such drains per genome).
+    auto issue = [&](size_t p) -> int { return issue_piece(c, q, pcs[p], (int)((base + p) % D), rpb, err, errlen); };
+    auto issue_next = [&](int k) -> int {
+        dd_run_req nq;
+        memset(&nq, 0, sizeof(nq));
+        if (!q->next_cb || !q->next_cb(q->next_arg, &nq)) return 0;
+        if (nq.slot < 0 || nq.slot >= DD_SLOTS || nq.slot == q->slot || c->dcomp_len[nq.slot] != nq.comp_len) return 0;
+        std::vector<Piece> np;
+        plan_pieces(&nq, c->piece_bytes, np);
+        if (np.empty()) return 0;
+        const double nrpb = run_rpb(&nq);
+        if (upload_run_tables(c, &nq, c->rs[k].st, err, errlen) || size_slot(c->rs[k], np, nrpb, err, errlen) ||
+            issue_piece(c, &nq, np[0], k, nrpb, err, errlen))
             return -1;
-        }
-        DCK(hipEventRecord(r.ev[1], ls));
-        const int64_t nch = pc.cb - pc.ca;
-        const int64_t *Sp = P<int64_t>(c->rS) + pc.ca;
-        hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
-                           c->ws_guess, rb + 4, P<uint32_t>(r.ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, rb,
-                           (int64_t)INT64_MAX);
-        size_t tb = 0;
-        DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
-        DGROW(r.tmp, tb);
-        DCK(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
-        hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
-                           c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off),
-                           rb, ocap);
-        DCK(hipGetLastError());
-        DCK(hipMemcpyAsync(r.h_small, P<uint32_t>(r.cbase) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
-        DCK(hipMemcpyAsync((char *)r.h_small + 4, P<uint32_t>(r.ccnt) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
-        DCK(hipMemcpyAsync((char *)r.h_small + 8, rb, 8, hipMemcpyDeviceToHost, ls));
-        DCK(hipMemcpyAsync((char *)r.h_small + 16, rb + 4, 4, hipMemcpyDeviceToHost, ls));
-        DCK(hipEventRecord(r.ev[2], ls));
+        c->pre.valid = 1;
+        c->pre.comp_slot = nq.slot;
+        c->pre.comp_len = nq.comp_len;
+        c->pre.u_lo = np[0].u_lo;
+        c->pre.rslot = k;
         return 0;
     };
-    for (size_t p = 0; p + 1 < (size_t)D && p < pcs.size(); p++)
+    for (size_t p = pre ? 1 : 0; p + 1 < (size_t)D && p < pcs.size(); p++)
         if (issue(p)) return -1;
     for (size_t p = 0; p < pcs.size(); p++) {
         const Piece &pc = pcs[p];
-        RunSlot &r = c->rs[p % D];
+        RunSlot &r = c->rs[(base + p) % D];
         const bool ahead = parse || stats_left > 0;  // (statistics only: stop at the cap)
         if (p + D - 1 < pcs.size() && ahead && issue(p + D - 1)) return -1;
+        if (p + D - 1 == pcs.size() && ahead && D > 1 && issue_next((int)((base + pcs.size()) % D))) return -1;
         DCK(hipEventSynchronize(r.ev[2]));
         const uint32_t *hs = (const uint32_t *)r.h_small;
         const int64_t R = (int64_t)hs[0] + hs[1];
@@ -1530,7 +1596,7 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
             DGROW(r.off, 8 * (size_t)(R + 1));
             DCK(hipMemsetAsync(r.misc.p, 0, 4, r.st));
             hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)(pc.cb - pc.ca)), dim3(WS_T), 0, r.st, P<uint8_t>(r.U),
-                               P<int64_t>(c->rS) + pc.ca, pc.base, pc.cb - pc.ca, q->tid, c->ws_guess, (uint32_t *)nullptr,
+                               P<int64_t>(c->rS[q->slot]) + pc.ca, pc.base, pc.cb - pc.ca, q->tid, c->ws_guess, (uint32_t *)nullptr,
                                (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), P<uint32_t>(r.misc),
                                (int64_t)INT64_MAX);
             DCK(hipEventRecord(r.ev[2], r.st));
@@ -1758,11 +1824,12 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
             have.n_cigar_ops = car.cig;
             have.n_bases = car.b;
         }
-        DCK(hipEventRecord(c->pev[p % D], st));  // the slot's piece is done with
+        DCK(hipEventRecord(c->pev[(base + p) % D], st));  // the slot's piece is done with
         R_tot += R;
         if (!parse && stats_left <= 0) break;  // statistics only: the cap is reached
     }
-    for (int k = 0; k < D; k++) DCK(hipStreamSynchronize(c->rs[k].st));  // (loads issued ahead)
+    for (int k = 0; k < D; k++)  // (loads issued ahead; the next run's first piece goes on)
+        if (!(c->pre.valid && k == c->pre.rslot)) DCK(hipStreamSynchronize(c->rs[k].st));
     *n_rec = R_tot;
     po->n_rec = R_tot;
     if (!parse) return 0;

@@ -2049,7 +2049,9 @@ void pd_set_wanted(pd_session *s, const int *want) {
  * before it.  The worker takes a slot, decodes the run piece by piece
  * (dd_run_decode) and releases it; a run nobody takes is simply read again
  * when needed. */
-enum { PF_FREE = 0, PF_WANTED = 1, PF_READY = 2, PF_USED = 3 };
+/* PF_HELD: read, and promised to the worker's next dw_decode (its first piece
+ * is already loading on the device, dd_run_req.next_cb) */
+enum { PF_FREE = 0, PF_WANTED = 1, PF_READY = 2, PF_USED = 3, PF_HELD = 4 };
 typedef struct {
     int ri, state, rc;
     char err[200];
@@ -2287,7 +2289,9 @@ static pf_slot *pf_take(dd_worker *w, int ri, int *slot_no, int *rc, char *err, 
     for (;;) {
         q = -1;
         for (int k = 0; k < 2; k++)
-            if (w->slot[k].ri == ri && (w->slot[k].state == PF_WANTED || w->slot[k].state == PF_READY)) q = k;
+            if (w->slot[k].ri == ri &&
+                (w->slot[k].state == PF_WANTED || w->slot[k].state == PF_READY || w->slot[k].state == PF_HELD))
+                q = k;
         if (q >= 0) break;
         for (int k = 0; k < 2 && q < 0; k++)
             if (w->slot[k].state == PF_FREE || w->slot[k].state == PF_READY) q = k;
@@ -2315,6 +2319,39 @@ static void pf_release(dd_worker *w, pf_slot *sl) {
     sl->ri = -1;
     pthread_cond_broadcast(&w->cv);
     pthread_mutex_unlock(&w->mu);
+}
+
+/* dd_run_decode's next_cb: run `next` of this worker, if its slot is read
+ * (without waiting), held for the worker's next dw_decode */
+typedef struct {
+    dd_worker *w;
+    int next;
+} dw_next_arg;
+
+static int dw_next_cb(void *arg, dd_run_req *nq) {
+    const dw_next_arg *a = (const dw_next_arg *)arg;
+    dd_worker *w = a->w;
+    if (a->next < 0) return 0;
+    int got = 0;
+    pthread_mutex_lock(&w->mu);
+    for (int k = 0; k < 2 && !got; k++) {
+        pf_slot *sl = &w->slot[k];
+        if (sl->ri != a->next || sl->state != PF_READY || sl->rc != 0) continue;
+        const pd_run *r = &w->s->runs[a->next];
+        sl->state = PF_HELD;
+        nq->slot = k;
+        nq->comp_len = sl->len;
+        nq->blk = sl->blk;
+        nq->nblk = sl->nb;
+        nq->starts = sl->starts;
+        nq->n_starts = sl->m;
+        nq->u_end = sl->u_end;
+        nq->tid = r->tid;
+        nq->count = r->count;
+        got = 1;
+    }
+    pthread_mutex_unlock(&w->mu);
+    return got;
 }
 
 /* the statistics' progress (dd_run_decode's callback, the first worker):
@@ -2364,6 +2401,14 @@ static int dw_decode(dd_worker *w, int ri, int next, grom_stage *stage, int64_t 
         rq.h_lq = s->s_lq + s->s_n;
         rq.stats_cb = dw_stats_cb;
         rq.stats_arg = s;
+    }
+    dw_next_arg na = {w, next};
+    /* the next run's first piece loads while this one finishes (not in the
+     * statistics-only pass: the run after it is not necessarily the next
+     * one this worker decodes, and a held slot reads nothing ahead) */
+    if (stage && !getenv("GROM_DD_NO_AHEAD")) {
+        rq.next_cb = dw_next_cb;
+        rq.next_arg = &na;
     }
     int64_t R = 0;
     pd_trace(s, PD_EV_PHASE, 102, 0);
