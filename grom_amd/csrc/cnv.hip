@@ -53,6 +53,7 @@
 
 #include "cnv.h"
 #include "ddecode.h"
+#include "copystats.h"  // (GROM_COPY_STATS, last: it wraps the runtime copy calls)
 
 namespace {
 
@@ -3191,13 +3192,16 @@ static int gather(CnvScratch *S, hipStream_t st, const std::vector<GatherRange> 
     hipLaunchKernelGGL(k_cnv_gather, dim3(g_), dim3(256), 0, st, (const GatherRange *)S->gat_rg.p, (int)rg.size(), gcw,
                        acw, mq, rd, low, flag, total, o_gc, o_ac, o_mq, o_rd, o_low, o_f);
     CK(hipGetLastError());
-    CK(hipMemcpyAsync(g.mq.data(), o_mq, 4 * total, hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(g.rd.data(), o_rd, 4 * total, hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(g.low.data(), o_low, 4 * total, hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(g.gc.data(), o_gc, total, hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(g.ac.data(), o_ac, total, hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(g.flag.data(), o_f, total, hipMemcpyDeviceToHost, st));
+    // the six gathered arrays lie back to back: one copy, split on the host
+    std::vector<uint8_t> hb((size_t)total * 15);
+    CK(hipMemcpyAsync(hb.data(), o, (size_t)total * 15, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
+    memcpy(g.mq.data(), hb.data(), 4 * (size_t)total);
+    memcpy(g.rd.data(), hb.data() + 4 * (size_t)total, 4 * (size_t)total);
+    memcpy(g.low.data(), hb.data() + 8 * (size_t)total, 4 * (size_t)total);
+    memcpy(g.gc.data(), hb.data() + 12 * (size_t)total, (size_t)total);
+    memcpy(g.ac.data(), hb.data() + 13 * (size_t)total, (size_t)total);
+    memcpy(g.flag.data(), hb.data() + 14 * (size_t)total, (size_t)total);
     for (int64_t i = 0; i < total; i++) g.rt[i] = g.rd[i] + g.low[i];
     return GROM_OK;
 }
@@ -4061,13 +4065,14 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 ChunkState *dcs = (ChunkState *)K.tiles.p;
                 CallRec *dcalls = (CallRec *)K.calls.p;
                 uint8_t *vis = (uint8_t *)K.vis.p;
-                CK(hipMemsetAsync(n_calls, 0, 8, st));  // n_calls, n_pre
+                // the kind's counters in one fill: n_calls, n_pre, n_cand, the
+                // capped call starts, n_und, the queue head (n_calls[0..5])
+                CK(hipMemsetAsync(n_calls, 0, 24, st));
                 CK(hipMemsetAsync(vis, 0, len, st));
                 int32_t *nxt = (int32_t *)K.nxt.p;
                 PreAB *pre = (PreAB *)K.pre.p;
                 const unsigned gpre = (unsigned)((span + 255) / 256);
                 uint32_t *n_cand = n_pre + 1;
-                CK(hipMemsetAsync(n_cand, 0, 8, st));  // candidates, capped call starts
                 int64_t *cand = (int64_t *)K.prepos.p;
                 if (kind == 0)
                     hipLaunchKernelGGL(k_cnv_cand<0>, dim3(gpre), dim3(256), 0, st, WK, nxt, cand, n_cand, cand_cap);
@@ -4099,7 +4104,6 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         int64_t *und = (int64_t *)K.und.p;
                         uint32_t *n_und = n_pre + 3;
                         uint32_t *qhead = n_pre + 4;  // the classification's work queue
-                        CK(hipMemsetAsync(n_und, 0, 8, st));  // n_und, qhead
                         // a fixed grid of waves pulling candidates (k_cnv_classify): enough
                         // to fill the chip, never more than the candidates need
                         const unsigned gcls = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ncand + 255) / 256, 2048));

@@ -82,7 +82,8 @@ typedef struct dd_run_req {
     int64_t comp_len;
     const DdBlock *blk;       /* the run's BGZF blocks (host) */
     int64_t nblk;
-    const int64_t *starts;    /* record starts in the inflated run: its first record, then the index's */
+    const int64_t *starts;    /* record starts in the inflated run: its first record, then the index's;
+                                 starts[n_starts] = u_end */
     int64_t n_starts, u_end;  /* ... and the run's end */
     int32_t tid;              /* the run's target (record-start guesses, the record check) */
     int64_t j0;               /* the run's first record to take */

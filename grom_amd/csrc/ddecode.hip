@@ -227,6 +227,7 @@ done:
 #include <hipcub/hipcub.hpp>
 
 #include "bamio.h"
+#include "copystats.h"  // (GROM_COPY_STATS, last: it wraps the runtime copy calls)
 
 namespace {
 
@@ -994,7 +995,8 @@ __global__ void k_aux_pack(const uint8_t *__restrict__ U, const int64_t *__restr
 
 __global__ void k_aux_len(const uint8_t *__restrict__ U, const int64_t *__restrict__ off,
                           const int64_t *__restrict__ acand, int64_t n, int64_t *__restrict__ len,
-                          const uint32_t *__restrict__ kidx, int64_t *__restrict__ akidx) {
+                          const uint32_t *__restrict__ kidx, int64_t *__restrict__ akidx, int64_t *__restrict__ aoff0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *aoff0 = 0;  // (the offsets' inclusive scan starts at aoff0 + 1)
     for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < n; a += (int64_t)gridDim.x * blockDim.x) {
         len[a] = 4 + (int64_t)ld_bs(U, off[acand[a]]);
         akidx[a] = kidx[acand[a]];
@@ -1051,7 +1053,9 @@ struct RunSlot {
     DBuf U, blk, status, misc, S, ccnt, cbase, off, tmp;  // (blk, S: unused by the piece decode)
     hipStream_t st = nullptr;
     hipEvent_t ev[3] = {};
-    int64_t *h_small = nullptr;  // pinned
+    int64_t *h_small = nullptr;  // pinned, mapped: k_piece_summary writes it
+    int64_t *d_small = nullptr;  // its device address
+    bool misc_clean = false;     // misc's flag words are zero (k_piece_summary clears them)
     int64_t R = 0, nblk = 0, ubytes = 0;
 };
 
@@ -1159,7 +1163,9 @@ extern "C" dd_ctx *dd_ctx_new(int device) {
         RunSlot &r = c->rs[k];
         if (dd_stream_new(&r.st) != hipSuccess) r.st = nullptr;
         for (int e = 0; e < 3; e++) (void)hipEventCreate(&r.ev[e]);
-        if (hipHostMalloc((void **)&r.h_small, 16 * sizeof(int64_t), 0) != hipSuccess) r.h_small = nullptr;
+        if (hipHostMalloc((void **)&r.h_small, 16 * sizeof(int64_t), hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&r.d_small, r.h_small, 0) != hipSuccess)
+            r.h_small = nullptr;
         if (!r.st || !r.h_small) { dd_ctx_free(c); return nullptr; }
     }
     return c;
@@ -1274,7 +1280,7 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs,
     DGROW(c->tfq, 8 * (size_t)(pb / CP_T + 4));
     DGROW(c->tfs, 8 * (size_t)(pb / 2 / CP_T + 4));
     const size_t na = (size_t)(pr / 8 + 2);
-    DGROW(c->acand, 8 * na); DGROW(c->alen, 8 * na); DGROW(c->aoff, 8 * na); DGROW(c->akidx, 8 * na);
+    DGROW(c->acand, 8 * na); DGROW(c->alen, 8 * na); DGROW(c->aoff, 16 * na);  // (aoff also holds the kept indices)
     DGROW(c->apack, (size_t)(pr / 64 + 1) * 512);
     // per chromosome: name hashes and their sort, the names' bytes
     const size_t r4 = 4 * (size_t)(recs + 1), r8 = 8 * (size_t)(recs + 1);
@@ -1416,8 +1422,8 @@ static int upload_run_tables(dd_ctx *c, const dd_run_req *q, hipStream_t st, cha
     DGROW(rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
     DGROW(rS, sizeof(int64_t) * (size_t)(ns + 2));
     DCK(hipMemcpyAsync(rblk.p, q->blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(rS.p, q->starts, sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice, st));
-    DCK(hipMemcpyAsync(P<int64_t>(rS) + ns, &q->u_end, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    // (starts[ns] holds the run's end, dd_run_req)
+    DCK(hipMemcpyAsync(rS.p, q->starts, sizeof(int64_t) * (size_t)(ns + 1), hipMemcpyHostToDevice, st));
     return 0;
 }
 
@@ -1444,6 +1450,23 @@ static int size_slot(RunSlot &r, const std::vector<Piece> &pcs, double rpb, char
     return 0;
 }
 
+// a piece's load results for the host, written straight to the slot's mapped
+// pinned words (four runtime copies per piece before): the records walked
+// (the last chunk's base and count), the flag words and the re-walk count;
+// the flag words are cleared for the slot's next piece
+__global__ void k_piece_summary(const uint32_t *__restrict__ cbase, const uint32_t *__restrict__ ccnt, int64_t nch,
+                                uint32_t *__restrict__ rb, uint32_t *__restrict__ out) {
+    if (threadIdx.x == 0) {
+        out[0] = cbase[nch - 1];
+        out[1] = ccnt[nch - 1];
+        out[2] = rb[0];
+        out[3] = rb[1];
+        out[4] = rb[4];
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) rb[threadIdx.x] = 0;
+}
+
 // The load of one piece (inflate, record walk) on piece slot k's own stream.
 // The slot is reused once the parse of the piece before in it is done (pev);
 // the offsets walk writes up to the slot's record capacity (a piece with more
@@ -1462,7 +1485,8 @@ static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, d
     const int64_t ocap = std::max<int64_t>((int64_t)(r.off.cap / 8) - 1, (int64_t)((double)pc.pbytes * rpb * 1.3) + 4096);
     DGROW(r.off, 8 * (size_t)(ocap + 1));
     uint32_t *rb = P<uint32_t>(r.misc);
-    DCK(hipMemsetAsync(r.misc.p, 0, 64, ls));
+    if (!r.misc_clean) DCK(hipMemsetAsync(r.misc.p, 0, 64, ls));
+    r.misc_clean = true;
     DCK(hipEventRecord(r.ev[0], ls));
     if (dd_inflate_launch(ls, P<uint8_t>(c->dcomp[q->slot]), P<DdBlock>(c->rblk[q->slot]) + pc.bf, pc.bl - pc.bf + 1,
                           P<uint8_t>(r.U), pc.base, P<uint8_t>(r.status), rb + 1)) {
@@ -1483,10 +1507,9 @@ static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, d
                        c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), rb,
                        ocap);
     DCK(hipGetLastError());
-    DCK(hipMemcpyAsync(r.h_small, P<uint32_t>(r.cbase) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
-    DCK(hipMemcpyAsync((char *)r.h_small + 4, P<uint32_t>(r.ccnt) + nch - 1, 4, hipMemcpyDeviceToHost, ls));
-    DCK(hipMemcpyAsync((char *)r.h_small + 8, rb, 8, hipMemcpyDeviceToHost, ls));
-    DCK(hipMemcpyAsync((char *)r.h_small + 16, rb + 4, 4, hipMemcpyDeviceToHost, ls));
+    hipLaunchKernelGGL(k_piece_summary, dim3(1), dim3(64), 0, ls, P<uint32_t>(r.cbase), P<uint32_t>(r.ccnt), nch, rb,
+                       (uint32_t *)r.d_small);
+    DCK(hipGetLastError());
     DCK(hipEventRecord(r.ev[2], ls));
     return 0;
 }
@@ -1599,6 +1622,7 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                                P<int64_t>(c->rS[q->slot]) + pc.ca, pc.base, pc.cb - pc.ca, q->tid, c->ws_guess, (uint32_t *)nullptr,
                                (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), P<uint32_t>(r.misc),
                                (int64_t)INT64_MAX);
+            r.misc_clean = false;  // (the re-walk's flag words stay)
             DCK(hipEventRecord(r.ev[2], r.st));
             DCK(hipEventSynchronize(r.ev[2]));
         }
@@ -1679,14 +1703,15 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                                P<uint32_t>(c->drop), P<uint32_t>(c->didx), P<uint32_t>(c->auxc), P<uint32_t>(c->aidx),
                                P<uint32_t>(c->ncig), P<uint32_t>(c->coff), P<int64_t>(c->nb), P<int64_t>(c->boff),
                                P<uint32_t>(c->nml), P<uint32_t>(c->nmo), R, tot);
-            DCK(hipMemcpyAsync(c->h_small, tot, 6 * 8, hipMemcpyDeviceToHost, st));
-            DCK(hipMemcpyAsync(c->h_small + 6, bad, 8, hipMemcpyDeviceToHost, st));
+            // the flag words (misc + 0) and the totals (misc + 128) in one copy
+            int64_t *hm = c->h_small + 16;
+            DCK(hipMemcpyAsync(hm, c->misc.p, 176, hipMemcpyDeviceToHost, st));
             DCK(hipStreamSynchronize(st));
-            const int64_t n = c->h_small[0], nd = c->h_small[1], na = c->h_small[2], ncg = c->h_small[3];
-            const int64_t nbs = c->h_small[4], nmb = c->h_small[5];
-            if (((const uint32_t *)(c->h_small + 6))[0]) {
+            const int64_t n = hm[16], nd = hm[17], na = hm[18], ncg = hm[19];
+            const int64_t nbs = hm[20], nmb = hm[21];
+            if (((const uint32_t *)hm)[0]) {
                 if (err) snprintf(err, (size_t)errlen, "device decode: records do not parse as the run's (%#x)",
-                                  ((const uint32_t *)(c->h_small + 6))[0]);
+                                  ((const uint32_t *)hm)[0]);
                 return -2;
             }
             // the stage: the first piece sizes it for the whole run from its
@@ -1733,8 +1758,10 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                 return -1;
             }
             DGROW(c->srcs, 8 * (size_t)(n + 1));
-            DGROW(c->acand, 8 * (size_t)(na + 2)); DGROW(c->alen, 8 * (size_t)(na + 2)); DGROW(c->aoff, 8 * (size_t)(na + 2));
-            DGROW(c->akidx, 8 * (size_t)(na + 2));
+            // aoff: the candidates' offsets [0, na] and right after them their
+            // kept indices (akidx), so one copy brings both back
+            DGROW(c->acand, 8 * (size_t)(na + 2)); DGROW(c->alen, 8 * (size_t)(na + 2)); DGROW(c->aoff, 16 * (size_t)(na + 2));
+            int64_t *akidx = P<int64_t>(c->aoff) + na + 1;
             StageOut so;
             so.pos = (int32_t *)dv.pos; so.mtid = (int32_t *)dv.mtid; so.mpos = (int32_t *)dv.mpos;
             so.isize = (int32_t *)dv.isize; so.lq = (int32_t *)dv.l_qseq; so.aidx = (int32_t *)dv.aux_idx;
@@ -1774,21 +1801,20 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
             // split-read candidates: lengths, offsets, kept indices, packed bytes -> host
             if (na > 0) {
                 hipLaunchKernelGGL(k_aux_len, dim3(grid_for(na)), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(r.off),
-                                   P<int64_t>(c->acand), na, P<int64_t>(c->alen), P<uint32_t>(c->kidx),
-                                   P<int64_t>(c->akidx));
+                                   P<int64_t>(c->acand), na, P<int64_t>(c->alen), P<uint32_t>(c->kidx), akidx,
+                                   P<int64_t>(c->aoff));
                 size_t t3 = 0;
                 DCK(hipcub::DeviceScan::InclusiveSum(nullptr, t3, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
                 DGROW(c->tmp, t3);
-                DCK(hipMemsetAsync(c->aoff.p, 0, 8, st));
                 DCK(hipcub::DeviceScan::InclusiveSum(c->tmp.p, t3, P<int64_t>(c->alen), P<int64_t>(c->aoff) + 1, (int)na, st));
                 DCK(hipMemcpyAsync(c->h_small + 8, P<int64_t>(c->aoff) + na, 8, hipMemcpyDeviceToHost, st));
             }
-            DCK(hipMemcpyAsync(c->h_small, d_last, 16, hipMemcpyDeviceToHost, st));
-            DCK(hipMemcpyAsync(c->h_small + 2, bad, 8, hipMemcpyDeviceToHost, st));
+            // the flag words and the piece's last record (misc + 192) in one copy
+            DCK(hipMemcpyAsync(hm, c->misc.p, 208, hipMemcpyDeviceToHost, st));
             DCK(hipStreamSynchronize(st));
-            memcpy(last, c->h_small, 16);
-            if (((const uint32_t *)(c->h_small + 2))[0]) {
-                const uint32_t b1 = ((const uint32_t *)(c->h_small + 2))[0];
+            memcpy(last, hm + 24, 16);
+            if (((const uint32_t *)hm)[0]) {
+                const uint32_t b1 = ((const uint32_t *)hm)[0];
                 if (err) snprintf(err, (size_t)errlen, "device decode: %s (%#x)",
                                   (b1 & DB_UNSORTED) ? "records are not sorted by position" : "record check failed", b1);
                 return -2;
@@ -1803,9 +1829,11 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                 aux_off.resize(ao0 + (size_t)na);
                 aux_kidx.resize(ak0 + (size_t)na);
                 DCK(hipMemcpyAsync(aux_bytes.data() + ab0, c->apack.p, (size_t)apack, hipMemcpyDeviceToHost, st));
-                DCK(hipMemcpyAsync(aux_off.data() + ao0, P<int64_t>(c->aoff) + 1, 8 * (size_t)na, hipMemcpyDeviceToHost, st));
-                DCK(hipMemcpyAsync(aux_kidx.data() + ak0, c->akidx.p, 8 * (size_t)na, hipMemcpyDeviceToHost, st));
+                std::vector<int64_t> ok2(2 * (size_t)na);  // offsets [1, na], then the kept indices
+                DCK(hipMemcpyAsync(ok2.data(), P<int64_t>(c->aoff) + 1, 16 * (size_t)na, hipMemcpyDeviceToHost, st));
                 DCK(hipStreamSynchronize(st));
+                memcpy(aux_off.data() + ao0, ok2.data(), 8 * (size_t)na);
+                memcpy(aux_kidx.data() + ak0, ok2.data() + na, 8 * (size_t)na);
                 for (size_t k = ao0; k < ao0 + (size_t)na; k++) aux_off[k] += apack_tot;  // run-wide offsets
                 for (size_t k = ak0; k < ak0 + (size_t)na; k++) aux_kidx[k] += car.k;    // kept index in the chromosome
                 apack_tot += apack;

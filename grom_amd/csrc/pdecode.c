@@ -2077,7 +2077,7 @@ typedef struct {
     int test_abort, n_done;  /* GROM_TEST_DD_ABORT=n: -2 at the n-th chromosome (tests) */
 } dd_worker;
 
-#define PF_CHUNK ((int64_t)64 << 20)
+#define PF_CHUNK ((int64_t)128 << 20)
 
 typedef struct {
     int fd;
@@ -2227,6 +2227,7 @@ static int pf_read(dd_worker *w, pf_slot *sl, int slot_no, int ri, char *err, in
     int64_t m = 0;
     for (int64_t k = 0; k < ns; k++)
         if (m == 0 || sl->starts[k] != sl->starts[m - 1]) sl->starts[m++] = sl->starts[k];
+    sl->starts[m] = u_end; /* (dd_run_req: the run's end after its starts) */
     sl->len = len;
     sl->nb = nb;
     sl->ub = ub;

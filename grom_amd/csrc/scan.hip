@@ -151,6 +151,7 @@ __global__ void k_rmdup(int64_t n, int32_t tid, const int32_t *__restrict__ pos,
 // k_scan_tile: the tile kernel (k_scan_tile.h)
 // ---------------------------------------------------------------------------
 #include "k_scan_tile.h"
+#include "copystats.h"  // (GROM_COPY_STATS, last: it wraps the runtime copy calls)
 
 // the per-tile flush sums of the pileup kernels into acc[0..1]
 __global__ __launch_bounds__(256) void k_flush_reduce(int64_t n_tiles, const unsigned long long *__restrict__ part,
@@ -237,6 +238,7 @@ struct Ctx {
     // scan scratch
     DevBuf keep, meta, tlo, thi, caf_mq, caf_rd, caf_low, cands, cands2, runb, runc, segs, misc, dbg, fpart, slots;
     grom_snv_cand *h_cands = nullptr;  // pinned host copy of the ordered candidates
+    unsigned long long *h_cafsum = nullptr, *d_cafsum = nullptr;  // mapped pinned word: k_caf_range_sum's result
     const char *host_ref = nullptr;    // the caller's host reference during grom_scan_chrom
     // device-resident scans: the breakpoint rows read reference bases on the
     // host, so the reference is copied into this pinned buffer on a side
@@ -263,26 +265,45 @@ static Ctx *ctx_of(int device) {
 
 // sum of caf_rd + caf_low over [lo, hi) of the device arrays, as the INV
 // depth check reads them (GROM.c:15816-15826): int per base, double total
+// One block sums rd[i] + low[i] over [lo, hi) as int64 into a mapped pinned
+// word: the host's double total of int sums is the same number (each partial
+// sum is an integer below 2^53)
+__global__ __launch_bounds__(1024) void k_caf_range_sum(const int32_t *__restrict__ rd, const int32_t *__restrict__ low,
+                                                        int64_t lo, int64_t hi, unsigned long long *out) {
+    __shared__ long long part[16];
+    long long s = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) s += (long long)rd[i] + (long long)low[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += part[w];
+        *out = (unsigned long long)t;
+    }
+}
+
+// sum of caf_rd + caf_low over [lo, hi) of the device arrays, as the INV
+// depth check reads them (GROM.c:15816-15826): int per base, double total.
+// Summed on the device (round 4 copied both ranges to the host: two blits and
+// up to megabytes per query, the largest source of runtime copies)
 struct CafSum {
     hipStream_t st;
     const int32_t *rd, *low;
     int64_t len;
     int rc;
+    unsigned long long *h, *d;  // mapped pinned result word
     static double call(void *u, int64_t lo, int64_t hi) {
         CafSum &c = *(CafSum *)u;
         const int64_t a = std::max<int64_t>(lo, 0), b = std::min<int64_t>(hi, c.len);
         if (a >= b || c.rc != GROM_OK) return 0.0;
-        std::vector<int32_t> r((size_t)(b - a)), l((size_t)(b - a));
-        if (hipMemcpyAsync(r.data(), c.rd + a, sizeof(int32_t) * r.size(), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
-            hipMemcpyAsync(l.data(), c.low + a, sizeof(int32_t) * l.size(), hipMemcpyDeviceToHost, c.st) != hipSuccess ||
-            hipStreamSynchronize(c.st) != hipSuccess) {
-            set_err("INV depth check: device copy failed");
+        hipLaunchKernelGGL(k_caf_range_sum, dim3(1), dim3(1024), 0, c.st, c.rd, c.low, a, b, c.d);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c.st) != hipSuccess) {
+            set_err("INV depth check: device sum failed");
             c.rc = GROM_E_HIP;
             return 0.0;
         }
-        double s = 0;
-        for (size_t k = 0; k < r.size(); k++) s += r[k] + l[k];
-        return s;
+        return (double)(long long)*(volatile unsigned long long *)c.h;
     }
 };
 
@@ -702,7 +723,12 @@ static int scan_device(Ctx &C, const grom_chrom *ch, const grom_reads *R, grom_o
         // the rows' INV depth sums read caf_rd/caf_low on the copy stream, so
         // the row thread never waits behind the CNV kernels on `st` (the CNV
         // path only rewrites caf_mq)
-        CafSum cs{C.st_copy, (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, ch->len, GROM_OK};
+        if (!C.h_cafsum) {
+            HIPCHK(hipHostMalloc((void **)&C.h_cafsum, 64, hipHostMallocMapped));
+            HIPCHK(hipHostGetDevicePointer((void **)&C.d_cafsum, C.h_cafsum, 0));
+        }
+        CafSum cs{C.st_copy, (const int32_t *)C.caf_rd.p, (const int32_t *)C.caf_low.p, ch->len, GROM_OK, C.h_cafsum,
+                  C.d_cafsum};
         const char *href = nullptr;
         std::thread svt;
         Joiner sv_join{svt};
@@ -986,6 +1012,7 @@ void grom_dev_fini(int device) {
             b->cap = 0;
         }
     if (C.h_cands) (void)hipHostFree(C.h_cands);
+    if (C.h_cafsum) (void)hipHostFree(C.h_cafsum);
     if (C.st_copy) (void)hipStreamSynchronize(C.st_copy);
     if (C.h_ref) (void)hipHostFree(C.h_ref);
     if (C.ref_ev) (void)hipEventDestroy(C.ref_ev);

@@ -48,6 +48,7 @@
 
 #include "sv.h"
 #include "ddecode.h"
+#include "copystats.h"  // (GROM_COPY_STATS, last: it wraps the runtime copy calls)
 
 namespace {
 
