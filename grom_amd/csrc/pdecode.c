@@ -2874,7 +2874,9 @@ static int pd_start_device(pd_session *s) {
     int per = ws && atoi(ws) > 0 ? atoi(ws) : 1;
     if (per > 8) per = 8;
     const char *it = getenv("GROM_DECODE_THREADS");
-    s->io_threads = it && atoi(it) > 0 ? atoi(it) / (nd * per) : 8;
+    /* the read-ahead's pread threads per worker: 16 read chr1's 1.75 GB in
+     * 0.18 s from the page cache against 0.28 s with 8 (profiles/r05aa) */
+    s->io_threads = it && atoi(it) > 0 ? atoi(it) / (nd * per) : 16;
     if (s->io_threads < 1) s->io_threads = 1;
     if (s->io_threads > 16) s->io_threads = 16;
     s->dw = (pthread_t *)calloc((size_t)(nd * per), sizeof(pthread_t));
