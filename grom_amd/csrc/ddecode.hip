@@ -45,7 +45,10 @@ extern "C" int dd_inflate_launch(hipStream_t st, const uint8_t *d_comp, const Dd
                                  uint8_t *d_out, int64_t out_base, uint8_t *d_status, uint32_t *d_bad) {
     if (n_blk <= 0) return 0;
     const unsigned grid = (unsigned)((n_blk + DD_LANES - 1) / DD_LANES);
-    hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES, st, d_comp, d_blk,
+    // GROM_INFLATE_LDS_PAD (probe only): extra LDS bytes per wave, to measure
+    // how the kernel's speed follows its occupancy
+    static const int pad = getenv("GROM_INFLATE_LDS_PAD") ? atoi(getenv("GROM_INFLATE_LDS_PAD")) : 0;
+    hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES + pad, st, d_comp, d_blk,
                        n_blk, d_out, out_base, d_status, d_bad);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
