@@ -196,6 +196,32 @@ static double clock_gettime_s(void) {
     return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
 }
 
+/* seconds from this process's start (the kernel's start time, clock ticks
+ * since boot) to now: what loading the program and the library took before
+ * the CLI's first line; -1 when /proc does not say */
+static double since_process_start(void) {
+    FILE *f = fopen("/proc/self/stat", "r");
+    if (!f) return -1.0;
+    char buf[2048];
+    const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    const char *p = strrchr(buf, ')'); /* (the command name may hold spaces) */
+    if (!p) return -1.0;
+    unsigned long long start = 0;
+    int field = 2;
+    for (const char *q = p + 1; *q && field < 22; q++)
+        if (*q == ' ') {
+            field++;
+            if (field == 22) start = strtoull(q + 1, NULL, 10);
+        }
+    struct timespec t;
+    clock_gettime(CLOCK_BOOTTIME, &t);
+    const long hz = sysconf(_SC_CLK_TCK);
+    if (start == 0 || hz <= 0) return -1.0;
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec - (double)start / (double)hz;
+}
+
 typedef struct {
     char *p;
     size_t len, cap;
@@ -671,6 +697,7 @@ typedef struct {
     char ctx_name[4096];
     int wdev[64], n_work, n_init;
     double t_cli0, t_cand; /* CLI start, candidates (FASTA lengths) done */
+    double t_load;         /* process start to the CLI's start (program and library loading) */
     double t_scans, t_pdclose, t_outputs; /* scans done, decoder closed, outputs written */
     double t_decclose;                     /* the decoder's host side closed */
     pthread_t hip_thr;     /* HIP runtime start-up, beside the header/FASTA/index work */
@@ -1438,8 +1465,9 @@ done:
     if (!fallback && status == 0 && S->verbose) {
         const double t_end = clock_gettime_s();
         printf("cli phases (s from start): candidates/FASTA lengths %.3f, decoder open %.3f, insert statistics %.3f, "
-               "contexts %.3f, last chromosome handed %.3f, scans done %.3f\n", S->t_cand - S->t_cli0,
-               t_started - S->t_cli0, t_stats - S->t_cli0, t_ctx - S->t_cli0, t_loop - S->t_cli0, t_end - S->t_cli0);
+               "contexts %.3f, last chromosome handed %.3f, scans done %.3f; process start to CLI start %.3f\n",
+               S->t_cand - S->t_cli0, t_started - S->t_cli0, t_stats - S->t_cli0, t_ctx - S->t_cli0, t_loop - S->t_cli0,
+               t_end - S->t_cli0, S->t_load);
         pd_counters pc;
         pd_get_counters(pd, &pc);
         if (pc.device)
@@ -1516,6 +1544,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
     setlinebuf(stdout);
     cli_state *S = calloc(1, sizeof(cli_state));
     S->t_cli0 = clock_gettime_s();
+    S->t_load = since_process_start();
     grom_params *P = &S->P;
     grom_default_params(P);
     S->max_chr_len = 300000000; /* g_max_chr_fasta_len, GROM.c:946 */
