@@ -400,9 +400,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GROM_BENCH_ONE_GPU=1 (a rehearsal of the multi-rank path on a one-GPU
+    # box): every rank runs its CLI on GPU 0 and the ranks talk over gloo
+    # (RCCL refuses two ranks on one GPU)
+    one_gpu = os.environ.get("GROM_BENCH_ONE_GPU") == "1"
+    if one_gpu:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import grom_amd
     from grom_amd.shard import all_gather_objects, assign_chromosomes, max_over_ranks, merge_rank_outputs_parallel
@@ -482,7 +491,7 @@ def main():
         log(f"timed run {k + 1}: {runs[-1]:.2f} s" + (f"; {ph[0]}" if ph else "") +
             (f"; file reads {rd.group(1)} s, waited {rd.group(2)} s" if rd else ""))
     barrier()
-    dt = max_over_ranks(time.perf_counter() - t0, device="cuda")
+    dt = max_over_ranks(time.perf_counter() - t0, device="cpu" if one_gpu else "cuda")
     value = total * args.steps / dt / 1e6
     stats = chrom_stats(last)  # this rank's chromosomes, last timed run
     feet = [footprint(so) for so in run_out]
