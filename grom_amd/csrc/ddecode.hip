@@ -1777,7 +1777,7 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
                                P<uint32_t>(c->nmo), P<int32_t>(c->rpos), so, car, P<int64_t>(c->srcs),
                                P<uint8_t>(c->nm), P<int64_t>(c->nmoff), P<uint64_t>(c->keys), P<uint32_t>(c->vals),
                                P<int64_t>(c->acand), q->read_name_len, d_last, bad);
-            static const bool tiles = getenv("GROM_COPY_TILES") != nullptr;  // (A/B of the two copies)
+            const bool tiles = getenv("GROM_COPY_TILES") != nullptr;  // (A/B of the two copies)
             if (n > 0 && !tiles) {  // the bases and qualities of the piece's kept reads
                 const unsigned g = (unsigned)((16 * n + 255) / 256);
                 hipLaunchKernelGGL(k_copy_reads<true>, dim3(g), dim3(256), 0, st, P<uint8_t>(r.U), P<int64_t>(c->srcs),

@@ -17,6 +17,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -1539,7 +1541,27 @@ done:
     return status;
 }
 
+/* GROM_SEGV_TRACE=1 (diagnostics for in-process callers such as the Python
+ * binding, which have no handler of the grom executable's): a fatal signal
+ * prints the host stack before the process ends */
+static void on_fatal_trace(int sig) {
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    static const char msg[] = "grom: fatal signal, host stack:\n";
+    if (write(2, msg, sizeof(msg) - 1) < 0) { /* nothing more to do */ }
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 static int cli_run(int argc, char **argv, int force_serial) {
+    if (getenv("GROM_SEGV_TRACE")) {
+        struct sigaction sa;
+        memset(&sa, 0, sizeof(sa));
+        sa.sa_handler = on_fatal_trace;
+        sigaction(SIGSEGV, &sa, NULL);
+        sigaction(SIGBUS, &sa, NULL);
+    }
     optind = 0; /* GNU getopt: 0 fully re-initialises, so this is callable again */
     setlinebuf(stdout);
     cli_state *S = calloc(1, sizeof(cli_state));
