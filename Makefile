@@ -81,11 +81,13 @@ oracle:
 
 # kernel tuning variants, loaded with GROM_AMD_LIB=...:
 #   make variant V=w4 VFLAGS=-DGROM_WAVES_PER_EU=4  ->  grom_amd/lib/variants/libgrom_amd_w4.so
-variant: $(HOST_OBJ) build/sv.o build/ddecode.o
+#   make variant V=q0 VFLAGS=-DGI_QUAD=0            (the inflater's bit reader)
+variant: $(HOST_OBJ) build/sv.o
 	@mkdir -p build/variants $(LIBDIR)/variants
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c grom_amd/csrc/scan.hip -o build/variants/scan_$(V).o
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -ffp-contract=off -c grom_amd/csrc/cnv.hip -o build/variants/cnv_$(V).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(LIBDIR)/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/variants/cnv_$(V).o build/sv.o build/ddecode.o $(HOST_OBJ) -lz -lm
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c grom_amd/csrc/ddecode.hip -o build/variants/ddecode_$(V).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(LIBDIR)/variants/libgrom_amd_$(V).so build/variants/scan_$(V).o build/variants/cnv_$(V).o build/sv.o build/variants/ddecode_$(V).o $(HOST_OBJ) -lz -lm
 
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR)

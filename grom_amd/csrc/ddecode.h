@@ -42,6 +42,8 @@ int64_t grom_inflate_device_selftest(const char *bam_path, int device, int64_t m
 /* ---- one run (a chromosome's records in the file) on the device ---- */
 typedef struct dd_ctx dd_ctx;
 dd_ctx *dd_ctx_new(int device);
+void dd_ctx_prepare(int device); /* one context made ahead (taken by the next dd_ctx_new on the device) */
+void dd_ctx_drop_prepared(void); /* frees a prepared context nobody took */
 void dd_ctx_free(dd_ctx *c);
 /* summed HIP-event times of the parsed runs: inflate, record walk, parse;
  * ms[3]: wall time of decode buffer growth so far (every context) */

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 #include <zlib.h>
 
@@ -1146,7 +1147,46 @@ static hipError_t dd_stream_new(hipStream_t *st) {
     return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
 }
 
+// A context made ahead (dd_ctx_prepare, the CLI's HIP start-up thread, while
+// the host reads the FASTA lengths and the BAI): making one takes ~0.1 s
+// (streams, events, pinned words) that otherwise sat on the run's critical
+// path before the first chromosome's read.  The first dd_ctx_new on its
+// device takes it; dd_ctx_drop_prepared frees one nobody took.
+static std::mutex g_prep_mu;
+static dd_ctx *g_prep = nullptr;
+static dd_ctx *dd_ctx_make(int device);
+
+extern "C" void dd_ctx_prepare(int device) {
+    dd_ctx *c = dd_ctx_make(device);
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    if (g_prep) dd_ctx_free(c);
+    else g_prep = c;
+}
+
+extern "C" void dd_ctx_drop_prepared(void) {
+    dd_ctx *c;
+    {
+        std::lock_guard<std::mutex> lk(g_prep_mu);
+        c = g_prep;
+        g_prep = nullptr;
+    }
+    dd_ctx_free(c);
+}
+
 extern "C" dd_ctx *dd_ctx_new(int device) {
+    {
+        std::lock_guard<std::mutex> lk(g_prep_mu);
+        if (g_prep && g_prep->device == device) {
+            dd_ctx *c = g_prep;
+            g_prep = nullptr;
+            if (hipSetDevice(device) != hipSuccess) { dd_ctx_free(c); return nullptr; }
+            return c;
+        }
+    }
+    return dd_ctx_make(device);
+}
+
+static dd_ctx *dd_ctx_make(int device) {
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     dd_ctx *c = new dd_ctx();
     c->device = device;

@@ -802,6 +802,14 @@ static void *hip_init_main(void *arg) {
     const int device = *(const int *)arg;
     (void)grom_device_count();
     if (getenv("GROM_NO_WARM") == NULL) dd_device_warm(device);
+    /* the device decoder's first context, made while the host reads the
+     * FASTA lengths and the BAI (GROM_NO_CTX_PREPARE=1: made by the worker).
+     * Not with several decode workers per GPU (GROM_DD_WORKERS > 1): that
+     * mode's GPU tests once gave a stage digest unlike the host decoder's
+     * with the context ready early, so it keeps its timing */
+    const char *dd = getenv("GROM_DEVICE_DECODE"), *np = getenv("GROM_NO_CTX_PREPARE"),
+               *wk = getenv("GROM_DD_WORKERS");
+    if (!(dd && atoi(dd) == 0) && !(np && atoi(np) == 1) && !(wk && atoi(wk) > 1)) dd_ctx_prepare(device);
     return NULL;
 }
 
@@ -1745,6 +1753,7 @@ static int cli_run(int argc, char **argv, int force_serial) {
 out_hdr:
     tables_join(S);
     hip_ready(S);
+    dd_ctx_drop_prepared();
     bam_free_header(&S->hdr);
     free(S);
     return ret;

@@ -84,15 +84,30 @@ GI_FN uint32_t gi_rev15(uint32_t x) {
 #endif
 }
 
-// LSB-first bit reader over the block's DEFLATE data, fed by aligned 32-bit
-// words with the next word loaded one refill ahead (the load's latency hides
-// behind the symbols decoded meanwhile).  A BGZF block's data is followed by
-// its 8-byte trailer (CRC32, ISIZE) and then the next block or the buffer's
-// padding, so reading up to 15 bytes past the data is safe; the caller checks
-// that no more than the data was consumed.
+// LSB-first bit reader over the block's DEFLATE data.  A BGZF block's data is
+// followed by its 8-byte trailer (CRC32, ISIZE) and then the next block or the
+// buffer's padding (>= 64 bytes), so reading a little past the data is safe;
+// the caller checks that no more than the data was consumed.
+//
+// Aligned 32-bit words with the next word loaded one refill ahead.  GI_QUAD=1
+// (a variant, off): 16-byte loads with the next quad loaded a whole quad
+// ahead, so a refill waits for a load issued about four refills earlier;
+// measured 20% slower on the 140 k-block probe (46.5 against 38.6 ms,
+// profiles/r05ao/probe.jsonl).  It reads at most 40 bytes past the consumed
+// bits.
+#ifndef GI_QUAD
+#define GI_QUAD 0
+#endif
 struct GiBits {
+#if GI_QUAD
+    const uint32_t *wp;  // the next quad to load
+    uint32_t q0, q1, q2, q3;  // the current quad's words not yet merged, q0 next
+    uint32_t n0, n1, n2, n3;  // the next quad (loaded)
+    int kq;                   // words left in the current quad (1..4)
+#else
     const uint32_t *wp;  // the word after `nxt`
     uint32_t nxt;        // the next word to merge (already loaded)
+#endif
     uint64_t buf;
     int cnt;             // valid bits in buf
     int sh0;             // bits of the first word before the data
@@ -109,28 +124,79 @@ GI_FN uint32_t gi_ldw(const uint32_t *p) {
 #endif
 }
 
+#if GI_QUAD
+GI_FN void gi_ldq(const uint32_t *p, uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef uint32_t gi_q4 __attribute__((ext_vector_type(4), aligned(4)));
+    const gi_q4 v = *(const gi_q4 *)p;  // one dwordx4 load
+    a = v.x;
+    b = v.y;
+    c = v.z;
+    d = v.w;
+#else
+    uint32_t v[4];
+    __builtin_memcpy(v, p, 16);
+    a = v[0];
+    b = v[1];
+    c = v[2];
+    d = v[3];
+#endif
+}
+#endif
+
+// the reader at word `k` of `base` (4-byte aligned), bit r of that word
+GI_FN void gi_start(GiBits &b, const uint32_t *base, int k, int r) {
+#if GI_QUAD
+    gi_ldq(base + k, b.q0, b.q1, b.q2, b.q3);
+    gi_ldq(base + k + 4, b.n0, b.n1, b.n2, b.n3);
+    b.wp = base + k + 8;
+    b.buf = (uint64_t)(b.q0 >> r);
+    b.q0 = b.q1;
+    b.q1 = b.q2;
+    b.q2 = b.q3;
+    b.kq = 3;
+#else
+    const uint32_t w0 = gi_ldw(base + k);
+    b.nxt = gi_ldw(base + k + 1);
+    b.wp = base + k + 2;
+    b.buf = (uint64_t)(w0 >> r);
+#endif
+    b.cnt = 32 - r;
+    b.merged = k + 1;
+}
+
 GI_FN void gi_open(GiBits &b, const uint8_t *in) {
     // (pointer arithmetic on `in`, not an integer round trip: the compiler
     // keeps the global address space, so the loads are global_load, not flat
     // loads that an LDS wait would also wait for)
     const int mis = (int)((uintptr_t)in & 3);
-    b.wp = (const uint32_t *)(in - mis);
     b.sh0 = mis * 8;
-    const uint32_t w0 = gi_ldw(b.wp);
-    b.nxt = gi_ldw(b.wp + 1);
-    b.wp += 2;
-    b.buf = (uint64_t)(w0 >> b.sh0);
-    b.cnt = 32 - b.sh0;
-    b.merged = 1;
+    gi_start(b, (const uint32_t *)(in - mis), 0, b.sh0);
 }
 
 // at least 32 bits in the buffer
 GI_FN void gi_refill(GiBits &b) {
     if (b.cnt < 32) {
+#if GI_QUAD
+        b.buf |= (uint64_t)b.q0 << b.cnt;
+        b.q0 = b.q1;
+        b.q1 = b.q2;
+        b.q2 = b.q3;
+        if (--b.kq == 0) {
+            b.q0 = b.n0;
+            b.q1 = b.n1;
+            b.q2 = b.n2;
+            b.q3 = b.n3;
+            gi_ldq(b.wp, b.n0, b.n1, b.n2, b.n3);
+            b.wp += 4;
+            b.kq = 4;
+        }
+#else
         b.buf |= (uint64_t)b.nxt << b.cnt;
-        b.cnt += 32;
         b.nxt = gi_ldw(b.wp);
         b.wp++;
+#endif
+        b.cnt += 32;
         b.merged++;
     }
 }
@@ -309,25 +375,24 @@ GI_UNROLL
 // a few hundred short steps beside its wave's symbol steps, instead of holding
 // the whole wave for the header's length.  cn[] is the literal/length code's
 // register array (lit.e), which a header does not otherwise need.
+// GI_P2ONE (the default): pass 2 places one symbol per step (a variant
+// with 0: a whole repeat item, up to 6 placements, per step)
+#ifndef GI_P2ONE
+#define GI_P2ONE 1
+#endif
 struct GiHdr {
     GiHuffCL clh;
     int at;  // bit offset of the code lengths in the block's data
     int n, ntot, nlit, prev, eob;
+    int rl;  // pass 2 (GI_P2ONE): symbols of the current repeat item still to place
 };
 
 // the bit reader positioned at bit `pos` of the data starting at `in`
 GI_FN void gi_seek(GiBits &b, const uint8_t *in, int pos) {
     const int mis = (int)((uintptr_t)in & 3);
-    const uint32_t *base = (const uint32_t *)(in - mis);
-    const int abs = mis * 8 + pos, k = abs >> 5, r = abs & 31;
+    const int abs = mis * 8 + pos;
     b.sh0 = mis * 8;
-    b.wp = base + k;
-    const uint32_t w0 = gi_ldw(b.wp);
-    b.nxt = gi_ldw(b.wp + 1);
-    b.wp += 2;
-    b.buf = (uint64_t)(w0 >> r);
-    b.cnt = 32 - r;
-    b.merged = k + 1;
+    gi_start(b, (const uint32_t *)(in - mis), abs >> 5, abs & 31);
 }
 
 // bits consumed so far
@@ -402,6 +467,34 @@ GI_UNROLL
 template <int LANES, bool PASS2>
 GI_FN int gi_cl_step(GiBits &b, const uint8_t *in, GiHuff &lit, GiHuff &dist, GiHdr &H, uint32_t *tab, int lane) {
     uint32_t *cn = lit.e;
+#if GI_P2ONE
+    if (PASS2) {
+        // one symbol placed per step: a repeat item's symbols over several
+        // steps, so no step holds its wave for a whole item
+        if (H.rl == 0) {
+            const int s = gi_decode<LANES, 7, false>(b, H.clh, tab, lane, GI_T_CL);
+            if (s < 0) return -GI_E_TREE;
+            int val;
+            const int rep = gi_cl_item(b, s, H.prev, val);
+            if (rep < 0 || H.n + rep > H.ntot) return -GI_E_TREE;
+            H.prev = val;
+            if (val) H.rl = rep;
+            else H.n += rep;
+        }
+        if (H.rl > 0) {
+            const int i = H.n;
+            if (i < H.nlit) gi_place<LANES, 15, true>(tab, GI_T_LIT, lane, cn, 0, (uint32_t)H.prev, i);
+            else gi_place<LANES, 15, false>(tab, GI_T_DIST, lane, cn, 16, (uint32_t)H.prev, i - H.nlit);
+            H.n++;
+            H.rl--;
+        }
+        if (H.n < H.ntot) return GI_M_P2;
+        for (int l = 15; l >= 1; l--) cn[l] -= cn[l - 1];
+        int rc = gi_code<15>(dist, cn, 16);
+        if (!rc) rc = gi_code<15>(lit, cn, 0);
+        return rc ? -rc : GI_M_SYM;
+    }
+#endif
     const int s = gi_decode<LANES, 7, false>(b, H.clh, tab, lane, GI_T_CL);
     if (s < 0) return -GI_E_TREE;
     int val;
@@ -448,6 +541,7 @@ GI_UNROLL
     gi_seek(b, in, H.at);
     H.n = 0;
     H.prev = -1;
+    H.rl = 0;
     return GI_M_P2;
 }
 
@@ -485,6 +579,19 @@ GI_FN void gi_lit(uint8_t *out, uint32_t &o, uint64_t &pend, uint32_t &pn, uint3
     }
 }
 
+// A match step's stores wait for its loads (an L2 round trip).  GI_DEFER
+// (the default): the step issues its loads and leaves the stores to the next
+// trip, which stores them after its own refill and symbol decode (LDS work)
+// and before its first output access -- a literal group's store, a flush, or
+// the next match step's loads (whose source may be the pending bytes) -- so
+// the round trip overlaps the next symbol's decode.  Stores keep their
+// program order: the pending chunk's store (and its garbage tail past m)
+// always precedes every later store.  36.7 against 38.6 ms on the 140 k-block
+// probe (profiles/r05ao/probe.jsonl).
+#ifndef GI_DEFER
+#define GI_DEFER 1
+#endif
+
 // Inflate one block's raw DEFLATE data (in[0..in_len)) into out[0..out_len).
 // `tab` is the LDS (device) or local (host) table storage of GI_LANE_DWORDS
 // rows x LANES columns.  Bytes outside out[0..out_len) are never written.
@@ -500,6 +607,19 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
     uint32_t D = 0;    // the match's current source distance (a multiple of its distance)
     uint64_t pend = 0; // literals not yet stored: the output bytes [o - pn, o)
     uint32_t pn = 0;
+    gi_u32x4 v0 = {}, v1 = {}, v2 = {}, v3 = {};
+    uint32_t cq = 0, cm = 0;  // GI_DEFER: a loaded match chunk of cm bytes (0: none) for out + cq
+    // the pending chunk's stores (16-byte pieces that cover its cm bytes)
+    auto commit = [&]() {
+        if (cm) {
+            uint8_t *q = out + cq;
+            __builtin_memcpy(q, &v0, 16);
+            if (cm > 16) __builtin_memcpy(q + 16, &v1, 16);
+            if (cm > 32) __builtin_memcpy(q + 32, &v2, 16);
+            if (cm > 48) __builtin_memcpy(q + 48, &v3, 16);
+            cm = 0;
+        }
+    };
     int mode = GI_M_HDR, rc = GI_OK;
     while (mode != GI_M_DONE) {
         GI_TRIP(mode);
@@ -534,6 +654,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
                     rc = GI_E_OVERRUN;
                     break;
                 }
+                if (pn == 7) commit();  // (this literal completes a group: its store follows the chunk's)
                 gi_lit(out, o, pend, pn, (uint32_t)s);
                 GI_BYTES(0, 1);
             } else if (s == 256) {
@@ -562,26 +683,28 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
                 rem = len;
                 D = dd;
                 mode = GI_M_COPY;
+                commit();
                 gi_flush(out, o, out_len, pend, pn);  // the match reads final bytes
             }
         }
         // (a match starts copying in the step that decoded it)
         if (mode == GI_M_COPY) {
+            commit();  // (its bytes may be this step's source)
             uint32_t m = rem < GI_COPY ? rem : GI_COPY;
             m = m < D ? m : D;
             uint8_t *q = out + o;
             // 16-byte pieces that cover m bytes (sources all final: o - D + m <= o)
             const uint32_t span = (m + 15u) & ~15u;
             if (o + span <= out_len) {
-                gi_u32x4 v0, v1, v2, v3;
                 __builtin_memcpy(&v0, q - D, 16);
                 if (m > 16) __builtin_memcpy(&v1, q - D + 16, 16);
                 if (m > 32) __builtin_memcpy(&v2, q - D + 32, 16);
                 if (m > 48) __builtin_memcpy(&v3, q - D + 48, 16);
-                __builtin_memcpy(q, &v0, 16);
-                if (m > 16) __builtin_memcpy(q + 16, &v1, 16);
-                if (m > 32) __builtin_memcpy(q + 32, &v2, 16);
-                if (m > 48) __builtin_memcpy(q + 48, &v3, 16);
+                cq = o;
+                cm = m;
+#if !GI_DEFER
+                commit();
+#endif
             } else {
                 for (uint32_t j = 0; j < m; j++) q[j] = q[(int64_t)j - D];
             }
@@ -592,6 +715,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
             if (!rem) mode = GI_M_SYM;
         } else if (mode == GI_M_STORED) {
             // byte-aligned: up to 4 bytes from the bit buffer per step
+            commit();
             gi_refill(b);
             const uint32_t m = rem < 4u ? rem : 4u;
             for (uint32_t j = 0; j < m; j++) gi_lit(out, o, pend, pn, gi_bits(b, 8));
@@ -601,6 +725,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
         }
     }
     if (rc) return rc;
+    commit();
     gi_flush(out, o, out_len, pend, pn);
     // consumed bits: every merged word minus the first word's lead and the buffer
     const int64_t used_bits = gi_used(b);

@@ -7,6 +7,7 @@
 #
 # steps (outputs under gpurun_out/$OUT, OUT defaults to "s"):
 #   suite [pytest args]        the GPU suite in one pytest process
+#   ksuite TAG K [K=V ...]     the GPU tests matching K under the environment K=V
 #   genome SCALE               a configs[2]-shape genome at SCALE of GRCh38's
 #                              lengths (grom_synth) in /tmp/gw (kept for the
 #                              following steps of this call)
@@ -21,7 +22,8 @@
 #                              writes <bam>.mean, then RUNS runs over the
 #                              chromosomes CHROMS (GROM_CHROMS, as bench.py's ranks)
 #   probe CHECK [K=V ...]      the GPU inflater alone on /tmp/gw/g.bam
-#                              (tools/inflate_probe.py; CHECK=1: against zlib)
+#                              (tools/inflate_probe.py; CHECK=1: against zlib;
+#                              PROBE_MAX: a prefix of that many compressed bytes)
 #
 # environment: OUT (subdirectory of gpurun_out), FLAGS (CLI flags, default
 # "-M -g 1"), SYNTH (extra grom_synth args, e.g. coverage for configs[4]).
@@ -38,6 +40,18 @@ step_suite() {
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
       > $out/gputest.log 2>&1 || { tail -40 $out/gputest.log; return 1; }
   tail -3 $out/gputest.log
+}
+
+# the GPU suite's tests matching K under an environment (TAG names the log)
+step_ksuite() {
+  local tag=$1 k=$2; shift 2
+  env "$@" timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$k" \
+      > $out/gputest_$tag.log 2>&1
+  local rc=$?
+  tail -1 $out/gputest_$tag.log
+  # (a failed assertion goes on to the next step; a crash or time limit ends the chain)
+  [ $rc -ge 2 ] && return $rc
+  return 0
 }
 
 step_genome() {
@@ -113,7 +127,7 @@ step_share() {
 
 step_probe() {
   local check=$1; shift
-  env "$@" timeout -k 10 300 python3 tools/inflate_probe.py $work/g.bam 0 $check | tee -a $out/probe.jsonl
+  env "$@" timeout -k 10 300 python3 tools/inflate_probe.py $work/g.bam ${PROBE_MAX:-0} $check | tee -a $out/probe.jsonl
 }
 
 step_bench() {
