@@ -57,8 +57,20 @@
 #define GI_T_LIT 0
 #define GI_T_LITHI 72
 #define GI_T_DIST 81
+// GI_CLREG (a variant, off): the code-length code's 19 sorted symbols in
+// four registers of the header state (5 bits each) instead of 5 LDS rows, so
+// that 89 dwords per lane let 7 waves of 64 blocks share a CU's LDS instead
+// of 6: measured slower (38.5 against 36.7 ms on the 140 k-block probe,
+// profiles/r05ar)
+#ifndef GI_CLREG
+#define GI_CLREG 0
+#endif
+#if GI_CLREG
+#define GI_LANE_DWORDS 89
+#else
 #define GI_T_CL 89
 #define GI_LANE_DWORDS 94
+#endif
 #define GI_LANE_BYTES (GI_LANE_DWORDS * 4)
 
 // per-trip statistics hooks (tools/inflate_trips.cpp); nothing by default
@@ -293,12 +305,13 @@ GI_UNROLL
     return GI_OK;
 }
 
-// decode one symbol; -1 for a code outside the tree
-template <int LANES, int N, bool HI>
-GI_FN int gi_decode(GiBits &b, const GiHuffT<N> &h, const uint32_t *tab, int lane, int t0) {
+// the symbol at the front of the stream and its code length L (nothing
+// consumed); -1 for a code outside the tree
+template <int N>
+GI_FN int gi_index(const GiBits &b, const GiHuffT<N> &h, int &L) {
     const uint32_t rev = gi_rev15((uint32_t)b.buf);
     const uint32_t key = rev << 16 | 0xffffu;
-    int L = 1;
+    L = 1;
     uint32_t bs = h.e[1];
 GI_UNROLL
     for (int l = 1; l < N; l++) {
@@ -310,11 +323,26 @@ GI_UNROLL
         GI_KEEP(bs);
     }
     if (key >= h.e[N]) return -1;
-    const int idx = (int)(int16_t)(uint16_t)bs + (int)(rev >> (15 - L));
-    b.buf >>= L;
-    b.cnt -= L;
+    return (int)(int16_t)(uint16_t)bs + (int)(rev >> (15 - L));
+}
+
+template <int LANES, int N, bool HI>
+GI_FN int gi_lookup(const GiBits &b, const GiHuffT<N> &h, const uint32_t *tab, int lane, int t0, int &L) {
+    const int idx = gi_index<N>(b, h, L);
+    if (idx < 0) return -1;
     int s = *gi_cell<LANES>((uint32_t *)tab, t0, idx, lane);
     if (HI) s |= (int)((tab[(GI_T_LITHI + (idx >> 5)) * LANES + lane] >> (idx & 31)) & 1u) << 8;
+    return s;
+}
+
+// decode one symbol; -1 for a code outside the tree
+template <int LANES, int N, bool HI>
+GI_FN int gi_decode(GiBits &b, const GiHuffT<N> &h, const uint32_t *tab, int lane, int t0) {
+    int L;
+    const int s = gi_lookup<LANES, N, HI>(b, h, tab, lane, t0, L);
+    if (s < 0) return -1;
+    b.buf >>= L;
+    b.cnt -= L;
     return s;
 }
 
@@ -382,6 +410,9 @@ GI_UNROLL
 #endif
 struct GiHdr {
     GiHuffCL clh;
+#if GI_CLREG
+    uint32_t clt[4];  // the code-length code's sorted symbols, 5 bits each, 6 per word
+#endif
     int at;  // bit offset of the code lengths in the block's data
     int n, ntot, nlit, prev, eob;
     int rl;  // pass 2 (GI_P2ONE): symbols of the current repeat item still to place
@@ -397,6 +428,63 @@ GI_FN void gi_seek(GiBits &b, const uint8_t *in, int pos) {
 
 // bits consumed so far
 GI_FN int64_t gi_used(const GiBits &b) { return b.merged * 32 - b.sh0 - b.cnt; }
+
+#if GI_CLREG
+// the code-length code from its 19 3-bit lengths (cl, symbol i at bit 3i)
+GI_FN int gi_build_cl(GiHdr &H, uint64_t cl) {
+    uint32_t cnt[8];
+GI_UNROLL
+    for (int l = 0; l < 8; l++) cnt[l] = 0;
+GI_UNROLL
+    for (int i = 0; i < 19; i++) {
+        const uint32_t L = (uint32_t)(cl >> (3 * i)) & 7u;
+GI_UNROLL
+        for (int l = 1; l <= 7; l++) cnt[l] += (L == (uint32_t)l) ? 1u : 0u;
+    }
+    const int rc = gi_code<7>(H.clh, cnt, 0);
+    if (rc) return rc;
+    H.clt[0] = H.clt[1] = H.clt[2] = H.clt[3] = 0;
+GI_UNROLL
+    for (int i = 0; i < 19; i++) {
+        const uint32_t L = (uint32_t)(cl >> (3 * i)) & 7u;
+        if (!L) continue;
+        uint32_t o = 0;
+GI_UNROLL
+        for (int l = 1; l <= 7; l++) {
+            o = (L == (uint32_t)l) ? cnt[l] : o;
+            cnt[l] += (L == (uint32_t)l) ? 1u : 0u;
+        }
+        const uint32_t r = o / 6u, v = (uint32_t)i << (5u * (o - 6u * r));
+        H.clt[0] |= r == 0 ? v : 0u;
+        H.clt[1] |= r == 1 ? v : 0u;
+        H.clt[2] |= r == 2 ? v : 0u;
+        H.clt[3] |= r == 3 ? v : 0u;
+    }
+    return GI_OK;
+}
+
+// decode one code-length symbol; -1 for a code outside the tree
+GI_FN int gi_decode_cl(GiBits &b, const GiHdr &H) {
+    int L;
+    const int idx = gi_index<7>(b, H.clh, L);
+    if (idx < 0) return -1;
+    b.buf >>= L;
+    b.cnt -= L;
+    const uint32_t r = (uint32_t)idx / 6u;
+    // (selects kept apart: folded, they become a dynamic index into H,
+    // which moves the header state to scratch memory)
+    uint32_t w = H.clt[0];
+    w = r == 1 ? H.clt[1] : w;
+    GI_KEEP(w);
+    w = r == 2 ? H.clt[2] : w;
+    GI_KEEP(w);
+    w = r == 3 ? H.clt[3] : w;
+    return (int)((w >> (5u * ((uint32_t)idx - 6u * r))) & 31u);
+}
+#define GI_CL_DECODE(b, H) gi_decode_cl(b, H)
+#else
+#define GI_CL_DECODE(b, H) gi_decode<LANES, 7, false>(b, (H).clh, tab, lane, GI_T_CL)
+#endif
 
 // the 3-bit block header and, for a dynamic block, its counts and the
 // code-length code (after a refill): the next mode or -GI_E_*
@@ -438,8 +526,12 @@ GI_FN int gi_header(GiBits &b, GiHuff &lit, GiHuff &dist, GiHdr &H, uint32_t *ta
         const int s = (int)((k < 12 ? ord_lo >> (5 * k) : ord_hi >> (5 * (k - 12))) & 31u);
         cl |= (uint64_t)v << (3 * s);
     }
+#if GI_CLREG
+    const int rc = gi_build_cl(H, cl);
+#else
     const int rc = gi_build<LANES, 7, false>(H.clh, tab, lane, GI_T_CL, 19,
                                              [cl](int i) -> uint32_t { return (uint32_t)(cl >> (3 * i)) & 7u; });
+#endif
     if (rc) return -rc;
     H.ntot = H.nlit + ndist;
     H.at = (int)gi_used(b);
@@ -472,7 +564,7 @@ GI_FN int gi_cl_step(GiBits &b, const uint8_t *in, GiHuff &lit, GiHuff &dist, Gi
         // one symbol placed per step: a repeat item's symbols over several
         // steps, so no step holds its wave for a whole item
         if (H.rl == 0) {
-            const int s = gi_decode<LANES, 7, false>(b, H.clh, tab, lane, GI_T_CL);
+            const int s = GI_CL_DECODE(b, H);
             if (s < 0) return -GI_E_TREE;
             int val;
             const int rep = gi_cl_item(b, s, H.prev, val);
@@ -495,7 +587,7 @@ GI_FN int gi_cl_step(GiBits &b, const uint8_t *in, GiHuff &lit, GiHuff &dist, Gi
         return rc ? -rc : GI_M_SYM;
     }
 #endif
-    const int s = gi_decode<LANES, 7, false>(b, H.clh, tab, lane, GI_T_CL);
+    const int s = GI_CL_DECODE(b, H);
     if (s < 0) return -GI_E_TREE;
     int val;
     const int rep = gi_cl_item(b, s, H.prev, val);
@@ -591,6 +683,16 @@ GI_FN void gi_lit(uint8_t *out, uint32_t &o, uint64_t &pend, uint32_t &pn, uint3
 #ifndef GI_DEFER
 #define GI_DEFER 1
 #endif
+// GI_DEFER2: a match's later chunk whose source lies wholly before the
+// pending chunk loads before the pending chunk's stores (a variant)
+#ifndef GI_DEFER2
+#define GI_DEFER2 0
+#endif
+// GI_LIT2: a literal step also takes a second literal when the bit buffer
+// holds its code (a variant)
+#ifndef GI_LIT2
+#define GI_LIT2 0
+#endif
 
 // Inflate one block's raw DEFLATE data (in[0..in_len)) into out[0..out_len).
 // `tab` is the LDS (device) or local (host) table storage of GI_LANE_DWORDS
@@ -657,6 +759,20 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
                 if (pn == 7) commit();  // (this literal completes a group: its store follows the chunk's)
                 gi_lit(out, o, pend, pn, (uint32_t)s);
                 GI_BYTES(0, 1);
+#if GI_LIT2
+                // a second literal in the same step when the buffer holds its code
+                if (b.cnt >= 15 && o < out_len) {
+                    int L2;
+                    const int s2 = gi_lookup<LANES, 15, true>(b, lit, tab, lane, GI_T_LIT, L2);
+                    if (s2 >= 0 && s2 < 256) {
+                        b.buf >>= L2;
+                        b.cnt -= L2;
+                        if (pn == 7) commit();
+                        gi_lit(out, o, pend, pn, (uint32_t)s2);
+                        GI_BYTES(0, 1);
+                    }
+                }
+#endif
             } else if (s == 256) {
                 mode = bfinal ? GI_M_DONE : GI_M_HDR;
             } else {
@@ -689,13 +805,31 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
         }
         // (a match starts copying in the step that decoded it)
         if (mode == GI_M_COPY) {
-            commit();  // (its bytes may be this step's source)
             uint32_t m = rem < GI_COPY ? rem : GI_COPY;
             m = m < D ? m : D;
             uint8_t *q = out + o;
             // 16-byte pieces that cover m bytes (sources all final: o - D + m <= o)
             const uint32_t span = (m + 15u) & ~15u;
+#if GI_DEFER2
+            if (cm && D >= m + cm && o + span <= out_len) {
+                // the source lies before the pending chunk (which ends at o):
+                // this chunk's loads go out before the pending chunk's stores
+                gi_u32x4 w0 = {}, w1 = {}, w2 = {}, w3 = {};
+                __builtin_memcpy(&w0, q - D, 16);
+                if (m > 16) __builtin_memcpy(&w1, q - D + 16, 16);
+                if (m > 32) __builtin_memcpy(&w2, q - D + 32, 16);
+                if (m > 48) __builtin_memcpy(&w3, q - D + 48, 16);
+                commit();
+                v0 = w0;
+                v1 = w1;
+                v2 = w2;
+                v3 = w3;
+                cq = o;
+                cm = m;
+            } else
+#endif
             if (o + span <= out_len) {
+                commit();  // (its bytes may be this step's source)
                 __builtin_memcpy(&v0, q - D, 16);
                 if (m > 16) __builtin_memcpy(&v1, q - D + 16, 16);
                 if (m > 32) __builtin_memcpy(&v2, q - D + 32, 16);
@@ -706,6 +840,7 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
                 commit();
 #endif
             } else {
+                commit();
                 for (uint32_t j = 0; j < m; j++) q[j] = q[(int64_t)j - D];
             }
             o += m;
