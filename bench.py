@@ -278,8 +278,18 @@ def cpu_baseline_and_concordance(work_dir, knobs, flags):
                      f"(grom_synth {' '.join(synth_args(knobs, CPU_SAMPLE_LENS))}), flags {' '.join(flags) or '-'}; "
                      f"whole oracle run (BAM decode + scan + VCF) in {dt:.2f} s, 1 thread"}
     t0 = time.perf_counter()
-    rc = cli_main(["-i", bam, "-r", fa, "-o", "gpu.vcf"] + flags, env={"GROM_FILEDATE": FILEDATE, "GROM_SEED": SEED},
-                  cwd=work_dir)
+    # (the in-process CLI prints its report on fd 1: sent to stderr, so that
+    # stdout holds only the bench's one JSON line)
+    sys.stdout.flush()
+    saved_fd = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        rc = cli_main(["-i", bam, "-r", fa, "-o", "gpu.vcf"] + flags,
+                      env={"GROM_FILEDATE": FILEDATE, "GROM_SEED": SEED}, cwd=work_dir)
+    finally:
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(saved_fd, 1)
+        os.close(saved_fd)
     dt_gpu = time.perf_counter() - t0
     if rc != 0:
         raise RuntimeError(f"GPU CLI failed on the concordance sample: {last_error()}")
