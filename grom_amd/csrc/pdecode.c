@@ -2873,6 +2873,17 @@ static int pd_start_device(pd_session *s) {
     const char *ws = getenv("GROM_DD_WORKERS");
     int per = ws && atoi(ws) > 0 ? atoi(ws) : 1;
     if (per > 8) per = 8;
+    /* Several decode workers on ONE GPU are disabled: at the end of round 5
+     * that mode faulted the device intermittently (an illegal memory access,
+     * test_device_decode_stats_prefix run first in a fresh process, its
+     * 0.25 MB-piece "workers" mode: 3 runs of 4), a race not yet found
+     * (DESIGN.md 4.5).  GROM_DD_WORKERS_UNSAFE=1 keeps the mode for that
+     * investigation.  One worker per GPU is the default and is unaffected. */
+    const char *wu = getenv("GROM_DD_WORKERS_UNSAFE");
+    if (per > 1 && !(wu && atoi(wu) == 1)) {
+        fprintf(stderr, "grom: GROM_DD_WORKERS=%d ignored: one decode worker per GPU (DESIGN.md 4.5)\n", per);
+        per = 1;
+    }
     const char *it = getenv("GROM_DECODE_THREADS");
     /* the read-ahead's pread threads per worker: 16 read chr1's 1.75 GB in
      * 0.18 s from the page cache against 0.28 s with 8 (profiles/r05aa) */

@@ -736,9 +736,10 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
     exactly the input the host decoder threads (pdecode.c) stage: same stream
     facts and the same digest of every array, CIGAR/base/quality/SA-XP
     content, dropped record and name-id relation; and the outputs are the
-    oracle's.  Mode "3w" splits the GPU's chromosomes over three device
-    decode workers (GROM_DD_WORKERS), each with its own decode context, as
-    the per-GPU workers of -P n on a multi-GPU node do.  Modes "g0"/"g2" run
+    oracle's.  Mode "3w" asks for three device decode workers on the GPU
+    (GROM_DD_WORKERS); several workers on one GPU are disabled since the end
+    of round 5 (an intermittent device fault), so it runs one
+    worker and checks that the request is ignored safely.  Modes "g0"/"g2" run
     the record walk's guess-then-verify (k_walk_sub) with no guesses and with
     guesses at raw sub-chunk offsets (almost all wrong): every sub-chunk is
     then walked again from the true chain, with the same result.  Mode "cu"
@@ -818,7 +819,11 @@ def test_device_decode_stats_prefix(datadir, capfd, case, cap):
     pieces with 64 kB pieces) and one past it.  cnv_multi's first contig is
     not its longest: one worker decodes it first anyway (the sample is in file
     order), and of two workers the one that gathers the statistics does not
-    parse it (a statistics-only pass over it)."""
+    parse it (a statistics-only pass over it).  The "workers" mode asks for
+    two workers on the GPU; that is disabled since the end of round 5 (an
+    intermittent device fault in exactly this mode), so it
+    runs one worker with 0.25 MB pieces; GROM_DD_WORKERS_UNSAFE=1 restores
+    the two workers for the investigation."""
     bam, fa = synth(datadir, case, CASES[case])
     extra = ["-M", "-V", "1"]
     common = {"GROM_TEST_INSERT_CAP": cap, "GROM_STAGE_DIGEST": "1", "GROM_VERBOSE": "1"}
