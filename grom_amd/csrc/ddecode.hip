@@ -10,6 +10,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,29 +29,44 @@
 // One BGZF block per lane: blk[j] = {offset of its DEFLATE data in `comp`,
 // its length, offset of its output, ISIZE}; the output goes to out +
 // (out_off - out_base) (a piece of a run: out holds the piece).  status[j] =
-// GI_* code.
-__global__ void __launch_bounds__(DD_LANES, 2) k_inflate(const uint8_t *__restrict__ comp, const DdBlock *__restrict__ blk,
-                                                      int64_t n_blk, uint8_t *__restrict__ out, int64_t out_base,
-                                                      uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad) {
+// GI_* code.  A block whose input is not inside comp[0, comp_cap) or whose
+// output is not inside out[0, out_cap) is not touched: status GI_E_BOUNDS and
+// bit 1 in *bounds (a block table that does not belong to the compressed
+// slot or the piece is an error the host reports, never a wild access).
+#define GI_E_BOUNDS 8
+__global__ void __launch_bounds__(DD_LANES, 2) k_inflate(const uint8_t *__restrict__ comp, int64_t comp_cap,
+                                                      const DdBlock *__restrict__ blk, int64_t n_blk,
+                                                      uint8_t *__restrict__ out, int64_t out_base, int64_t out_cap,
+                                                      uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad,
+                                                      uint32_t *__restrict__ bounds) {
     extern __shared__ uint32_t dd_tab[];  // GI_LANE_DWORDS x DD_LANES: rows element-major across the lanes
     const int64_t j = (int64_t)blockIdx.x * DD_LANES + threadIdx.x;
     if (j >= n_blk) return;
     const DdBlock b = blk[j];
-    const int rc = gi_inflate<DD_LANES>(comp + b.in_off, b.in_len, out + (b.out_off - out_base), b.out_len, dd_tab,
-                                        threadIdx.x);
+    const int64_t o = b.out_off - out_base;
+    const bool inb = b.in_off >= 0 && b.in_off + (int64_t)b.in_len <= comp_cap && o >= 0 && b.out_len <= 65536u &&
+                     o + (int64_t)b.out_len <= out_cap;
+    if (!inb) {
+        status[j] = (uint8_t)GI_E_BOUNDS;
+        atomicAdd(n_bad, 1u);
+        atomicOr(bounds, 1u);
+        return;
+    }
+    const int rc = gi_inflate<DD_LANES>(comp + b.in_off, b.in_len, out + o, b.out_len, dd_tab, threadIdx.x);
     status[j] = (uint8_t)rc;
     if (rc) atomicAdd(n_bad, 1u);
 }
 
-extern "C" int dd_inflate_launch(hipStream_t st, const uint8_t *d_comp, const DdBlock *d_blk, int64_t n_blk,
-                                 uint8_t *d_out, int64_t out_base, uint8_t *d_status, uint32_t *d_bad) {
+extern "C" int dd_inflate_launch(hipStream_t st, const uint8_t *d_comp, int64_t comp_cap, const DdBlock *d_blk,
+                                 int64_t n_blk, uint8_t *d_out, int64_t out_base, int64_t out_cap, uint8_t *d_status,
+                                 uint32_t *d_bad, uint32_t *d_bounds) {
     if (n_blk <= 0) return 0;
     const unsigned grid = (unsigned)((n_blk + DD_LANES - 1) / DD_LANES);
     // GROM_INFLATE_LDS_PAD (probe only): extra LDS bytes per wave, to measure
     // how the kernel's speed follows its occupancy
     static const int pad = getenv("GROM_INFLATE_LDS_PAD") ? atoi(getenv("GROM_INFLATE_LDS_PAD")) : 0;
-    hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES + pad, st, d_comp, d_blk,
-                       n_blk, d_out, out_base, d_status, d_bad);
+    hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES + pad, st, d_comp, comp_cap,
+                       d_blk, n_blk, d_out, out_base, out_cap, d_status, d_bad, d_bounds);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -152,17 +168,18 @@ extern "C" int64_t grom_inflate_device_selftest(const char *bam_path, int device
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipMalloc(&d_comp, (size_t)used + 64) != hipSuccess || hipMalloc(&d_out, (size_t)ob + 64) != hipSuccess ||
         hipMalloc(&d_status, (size_t)nb + 1) != hipSuccess || hipMalloc(&d_blk, sizeof(DdBlock) * (size_t)(nb + 1)) != hipSuccess ||
-        hipMalloc(&d_bad, 4) != hipSuccess || hipStreamCreate(&st) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipMalloc(&d_bad, 8) != hipSuccess || hipStreamCreate(&st) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
         hipEventCreate(&e1) != hipSuccess)
         goto done;
     {
         (void)hipMemcpyAsync(d_comp, file.data(), (size_t)used + 64, hipMemcpyHostToDevice, st);
         (void)hipMemcpyAsync(d_blk, tab.data(), sizeof(DdBlock) * (size_t)nb, hipMemcpyHostToDevice, st);
-        (void)hipMemsetAsync(d_bad, 0, 4, st);
+        (void)hipMemsetAsync(d_bad, 0, 8, st);
         // a warm launch, then the timed one
         for (int rep = 0; rep < 2; rep++) {
             (void)hipEventRecord(e0, st);
-            if (dd_inflate_launch(st, d_comp, d_blk, nb, d_out, 0, d_status, d_bad)) goto done;
+            if (dd_inflate_launch(st, d_comp, used + 64, d_blk, nb, d_out, 0, ob + 64, d_status, d_bad, d_bad + 1))
+                goto done;
             (void)hipEventRecord(e1, st);
         }
         if (hipStreamSynchronize(st) != hipSuccess) goto done;
@@ -266,7 +283,7 @@ template <class T> T *P(DBuf &b) { return (T *)b.p; }
 
 // bad-state bits
 enum : uint32_t { DB_INFLATE = 1, DB_CHAIN = 2, DB_RECORD = 4, DB_TID = 8, DB_UNSORTED = 16, DB_NAMES = 32,
-                  DB_OFFCAP = 64 };
+                  DB_OFFCAP = 64, DB_BOUNDS = 128 };
 
 __device__ __forceinline__ uint32_t ldu32(const uint8_t *U, int64_t o) {
     return (uint32_t)U[o] | (uint32_t)U[o + 1] << 8 | (uint32_t)U[o + 2] << 16 | (uint32_t)U[o + 3] << 24;
@@ -404,7 +421,7 @@ __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U
                                                    int64_t sbase, int64_t n_chunks, int32_t tid, int guess,
                                                    uint32_t *__restrict__ q0_stats, uint32_t *__restrict__ cnt,
                                                    const uint32_t *__restrict__ base, int64_t *__restrict__ off,
-                                                   uint32_t *__restrict__ bad, int64_t off_cap = INT64_MAX) {
+                                                   uint32_t *__restrict__ bad, int64_t off_cap, int64_t ulen) {
     __shared__ int64_t s_start[WS_T], s_exit[WS_T];
     __shared__ uint32_t s_n[WS_T], s_pre[WS_T];
     __shared__ int64_t s_carry;
@@ -414,6 +431,10 @@ __global__ void __launch_bounds__(WS_T) k_walk_sub(const uint8_t *__restrict__ U
     if (c >= n_chunks) return;
     const int t = threadIdx.x;
     const int64_t c0 = S[c] - sbase, c1 = S[c + 1] - sbase;  // chunk bounds in U (a piece from sbase on)
+    if (c0 < 0 || c1 < c0 || c1 > ulen) {  // record starts that are not this piece's: reported, never walked
+        if (t == 0) atomicOr(bad, DB_BOUNDS);
+        return;
+    }
     const int64_t nsub = c1 > c0 ? (c1 - c0 + WS_G - 1) / WS_G : 0;
     if (t == 0) { s_carry = c0; s_total = 0; s_fail = 0; }
     __syncthreads();
@@ -1076,6 +1097,20 @@ struct dd_ctx {
     } pre = {};
     hipStream_t st = nullptr;
     hipStream_t cst = nullptr;  // compressed runs' host->device copies (dd_comp_upload, the prefetch thread)
+    // Compressed-slot ownership between the prefetch thread (which fills a
+    // slot) and the worker (which decodes from it).  comp_gen[k] counts the
+    // fills of slot k (dd_comp_begin); tab_gen[k] is the fill whose block table
+    // and record starts rblk[k]/rS[k] hold (upload_run_tables); a piece is
+    // issued only when they agree.  slot_busy[k]: a run's pieces may still
+    // read slot k (set by dd_run_decode and the next-run issue, cleared once
+    // its streams are drained); a refill waits for it.
+    std::atomic<uint64_t> comp_gen[DD_SLOTS] = {};
+    uint64_t tab_gen[DD_SLOTS] = {};
+    std::mutex slot_mu;
+    std::condition_variable slot_cv;
+    int slot_busy[DD_SLOTS] = {};
+    hipEvent_t tev = nullptr;  // the next run's tables uploaded on its piece slot's stream (issue_next)
+    int trace = 0;             // GROM_DD_TRACE: one stderr line per fill and piece
     DBuf dcomp[DD_SLOTS];
     hipEvent_t cev[DD_SLOTS] = {};
     int64_t dcomp_len[DD_SLOTS] = {};
@@ -1195,7 +1230,9 @@ static dd_ctx *dd_ctx_make(int device) {
     if (getenv("GROM_DD_PIECE_MB") && atof(getenv("GROM_DD_PIECE_MB")) > 0)
         c->piece_bytes = std::max<int64_t>((int64_t)(atof(getenv("GROM_DD_PIECE_MB")) * 1048576.0), 4096);
     if (getenv("GROM_DD_DEPTH")) c->depth = std::min(std::max(atoi(getenv("GROM_DD_DEPTH")), 1), DD_RSLOTS);
+    c->trace = getenv("GROM_DD_TRACE") != nullptr;
     if (dd_stream_new(&c->st) != hipSuccess) { delete c; return nullptr; }
+    (void)hipEventCreateWithFlags(&c->tev, hipEventDisableTiming);
     if (dd_stream_new(&c->cst) != hipSuccess) c->cst = nullptr;
     for (int k = 0; k < 4; k++) (void)hipEventCreate(&c->ev[k]);
     for (int k = 0; k < DD_SLOTS; k++) (void)hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming);
@@ -1217,8 +1254,13 @@ static dd_ctx *dd_ctx_make(int device) {
 extern "C" void dd_ctx_free(dd_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    // every stream drained before any buffer is freed: a next-run piece issued
+    // ahead (issue_next) may still be reading a compressed slot
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->cst) (void)hipStreamSynchronize(c->cst);
+    for (int k = 0; k < DD_RSLOTS; k++)
+        if (c->rs[k].st) (void)hipStreamSynchronize(c->rs[k].st);
+    if (c->tev) (void)hipEventDestroy(c->tev);
     for (int k = 0; k < DD_SLOTS; k++) {
         if (c->dcomp[k].p) grom_dev_free(c->dcomp[k].p, c->dcomp[k].cap, GROM_DEVCAT_DECODE);
         if (c->cev[k]) (void)hipEventDestroy(c->cev[k]);
@@ -1343,6 +1385,14 @@ extern "C" int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_
     if (slot < 0 || slot >= DD_SLOTS) return -1;
     DCK(hipSetDevice(c->device));
     hipStream_t cs = c->cst ? c->cst : c->st;
+    {
+        std::lock_guard<std::mutex> lk(c->slot_mu);
+        if (c->slot_busy[slot]) {
+            if (err) snprintf(err, (size_t)errlen, "device decode: compressed slot %d refilled while its run decodes", slot);
+            return -1;
+        }
+        c->comp_gen[slot]++;
+    }
     DGROW(c->dcomp[slot], (size_t)comp_len + 64);
     DCK(hipMemcpyAsync(c->dcomp[slot].p, h_comp, (size_t)comp_len + 64, hipMemcpyHostToDevice, cs));
     DCK(hipEventRecord(c->cev[slot], cs));
@@ -1358,8 +1408,23 @@ extern "C" int dd_comp_upload(dd_ctx *c, int slot, const uint8_t *h_comp, int64_
 extern "C" int dd_comp_begin(dd_ctx *c, int slot, int64_t comp_len, char *err, int errlen) {
     if (slot < 0 || slot >= DD_SLOTS) return -1;
     DCK(hipSetDevice(c->device));
+    {
+        // the slot's last run must be drained before it is refilled (the
+        // prefetch protocol guarantees it; a wait here is reported)
+        std::unique_lock<std::mutex> lk(c->slot_mu);
+        if (c->slot_busy[slot]) {
+            fprintf(stderr, "grom: device decode: compressed slot %d asked for while its run decodes (waiting)\n", slot);
+            if (!c->slot_cv.wait_for(lk, std::chrono::seconds(60), [&] { return !c->slot_busy[slot]; })) {
+                if (err) snprintf(err, (size_t)errlen, "device decode: compressed slot %d never drained", slot);
+                return -1;
+            }
+        }
+        c->comp_gen[slot]++;
+    }
     hipStream_t cs = c->cst ? c->cst : c->st;
     c->dcomp_len[slot] = -1;
+    if (c->trace) fprintf(stderr, "ddtrace ctx=%p fill slot=%d gen=%llu len=%lld\n", (void *)c, slot,
+                          (unsigned long long)c->comp_gen[slot].load(), (long long)comp_len);
     DGROW(c->dcomp[slot], (size_t)comp_len + 64);
     DCK(hipMemsetAsync(P<uint8_t>(c->dcomp[slot]) + comp_len, 0, 64, cs));
     return 0;
@@ -1462,6 +1527,7 @@ static double run_rpb(const dd_run_req *q) {
 static int upload_run_tables(dd_ctx *c, const dd_run_req *q, hipStream_t st, char *err, int errlen) {
     const int64_t nblk = q->nblk, ns = q->n_starts;
     DBuf &rblk = c->rblk[q->slot], &rS = c->rS[q->slot];
+    c->tab_gen[q->slot] = c->comp_gen[q->slot].load();
     DGROW(rblk, sizeof(DdBlock) * (size_t)(nblk + 1));
     DGROW(rS, sizeof(int64_t) * (size_t)(ns + 2));
     DCK(hipMemcpyAsync(rblk.p, q->blk, sizeof(DdBlock) * (size_t)nblk, hipMemcpyHostToDevice, st));
@@ -1505,6 +1571,7 @@ __global__ void k_piece_summary(const uint32_t *__restrict__ cbase, const uint32
         out[2] = rb[0];
         out[3] = rb[1];
         out[4] = rb[4];
+        out[5] = rb[5];
     }
     __syncthreads();
     if (threadIdx.x < 16) rb[threadIdx.x] = 0;
@@ -1517,6 +1584,19 @@ __global__ void k_piece_summary(const uint32_t *__restrict__ cbase, const uint32
 static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, double rpb, char *err, int errlen) {
     RunSlot &r = c->rs[k];
     hipStream_t ls = r.st;
+    // the compressed slot still holds this run, and its tables are this fill's
+    if (c->dcomp_len[q->slot] != q->comp_len || c->tab_gen[q->slot] != c->comp_gen[q->slot].load() ||
+        pc.bf < 0 || pc.bl >= q->nblk || pc.bl < pc.bf || pc.cb > q->n_starts) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: piece of target %d issued against compressed slot %d "
+                          "(length %lld, run %lld; table fill %llu, slot fill %llu)", q->tid, q->slot,
+                          (long long)c->dcomp_len[q->slot], (long long)q->comp_len, (unsigned long long)c->tab_gen[q->slot],
+                          (unsigned long long)c->comp_gen[q->slot].load());
+        return -1;
+    }
+    if (c->trace)
+        fprintf(stderr, "ddtrace ctx=%p piece tid=%d slot=%d gen=%llu rslot=%d chunks=%lld-%lld blocks=%lld-%lld u=%lld-%lld\n",
+                (void *)c, q->tid, q->slot, (unsigned long long)c->tab_gen[q->slot], k, (long long)pc.ca, (long long)pc.cb,
+                (long long)pc.bf, (long long)pc.bl, (long long)pc.u_lo, (long long)pc.u_hi);
     DCK(hipStreamWaitEvent(ls, c->pev[k], 0));
     DCK(hipStreamWaitEvent(ls, c->cev[q->slot], 0));
     DGROW(r.U, (size_t)pc.pbytes + 64);
@@ -1531,8 +1611,8 @@ static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, d
     if (!r.misc_clean) DCK(hipMemsetAsync(r.misc.p, 0, 64, ls));
     r.misc_clean = true;
     DCK(hipEventRecord(r.ev[0], ls));
-    if (dd_inflate_launch(ls, P<uint8_t>(c->dcomp[q->slot]), P<DdBlock>(c->rblk[q->slot]) + pc.bf, pc.bl - pc.bf + 1,
-                          P<uint8_t>(r.U), pc.base, P<uint8_t>(r.status), rb + 1)) {
+    if (dd_inflate_launch(ls, P<uint8_t>(c->dcomp[q->slot]), q->comp_len, P<DdBlock>(c->rblk[q->slot]) + pc.bf,
+                          pc.bl - pc.bf + 1, P<uint8_t>(r.U), pc.base, pc.pbytes, P<uint8_t>(r.status), rb + 1, rb + 5)) {
         if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
         return -1;
     }
@@ -1541,14 +1621,14 @@ static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, d
     const int64_t *Sp = P<int64_t>(c->rS[q->slot]) + pc.ca;
     hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
                        c->ws_guess, rb + 4, P<uint32_t>(r.ccnt), (const uint32_t *)nullptr, (int64_t *)nullptr, rb,
-                       (int64_t)INT64_MAX);
+                       (int64_t)INT64_MAX, pc.pbytes);
     size_t tb = 0;
     DCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
     DGROW(r.tmp, tb);
     DCK(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, P<uint32_t>(r.ccnt), P<uint32_t>(r.cbase), (int)nch, ls));
     hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)nch), dim3(WS_T), 0, ls, P<uint8_t>(r.U), Sp, pc.base, nch, q->tid,
                        c->ws_guess, (uint32_t *)nullptr, (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), rb,
-                       ocap);
+                       ocap, pc.pbytes);
     DCK(hipGetLastError());
     hipLaunchKernelGGL(k_piece_summary, dim3(1), dim3(64), 0, ls, P<uint32_t>(r.cbase), P<uint32_t>(r.ccnt), nch, rb,
                        (uint32_t *)r.d_small);
@@ -1557,7 +1637,37 @@ static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, d
     return 0;
 }
 
+static void slot_busy_set(dd_ctx *c, int slot, int busy) {
+    std::lock_guard<std::mutex> lk(c->slot_mu);
+    c->slot_busy[slot] = busy;
+    if (!busy) c->slot_cv.notify_all();
+}
+
+static int run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, int64_t *n_rec, char *err, int errlen);
+
+// One run, its compressed slot held busy until every stream that may read it
+// is drained -- on an error too (pieces issued ahead are then still in flight)
 extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, int64_t *n_rec, char *err, int errlen) {
+    if (q->slot < 0 || q->slot >= DD_SLOTS) {
+        if (err) snprintf(err, (size_t)errlen, "device decode: no compressed slot %d", q->slot);
+        return -1;
+    }
+    slot_busy_set(c, q->slot, 1);
+    const int rc = run_decode(c, q, po, n_rec, err, errlen);
+    if (rc != 0) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->st);
+        for (int k = 0; k < DD_RSLOTS; k++) (void)hipStreamSynchronize(c->rs[k].st);
+        if (c->pre.valid) {  // (a next-run piece issued before the error: drained above)
+            c->pre.valid = 0;
+            slot_busy_set(c, c->pre.comp_slot, 0);
+        }
+    }
+    if (!(c->pre.valid && c->pre.comp_slot == q->slot)) slot_busy_set(c, q->slot, 0);
+    return rc;
+}
+
+static int run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, int64_t *n_rec, char *err, int errlen) {
     DCK(hipSetDevice(c->device));
     memset(po, 0, sizeof(*po));
     *n_rec = 0;
@@ -1576,11 +1686,17 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
     int base = 0;
     bool pre = false;
     if (c->pre.valid) {
-        if (c->pre.comp_slot == q->slot && c->pre.comp_len == q->comp_len && !pcs.empty() && pcs[0].u_lo == c->pre.u_lo) {
+        if (c->pre.comp_slot == q->slot && c->pre.comp_len == q->comp_len && !pcs.empty() && pcs[0].u_lo == c->pre.u_lo &&
+            c->tab_gen[q->slot] == c->comp_gen[q->slot].load()) {
             base = c->pre.rslot;
             pre = true;
+            // this run's later pieces (other slots' streams, ordered after the
+            // context stream's events below) read the tables the next-run issue
+            // uploaded on the first piece's stream
+            DCK(hipStreamWaitEvent(st, c->tev, 0));
         } else {
             DCK(hipStreamSynchronize(c->rs[c->pre.rslot].st));
+            if (c->pre.comp_slot != q->slot) slot_busy_set(c, c->pre.comp_slot, 0);
         }
         c->pre.valid = 0;
     }
@@ -1627,9 +1743,13 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
         plan_pieces(&nq, c->piece_bytes, np);
         if (np.empty()) return 0;
         const double nrpb = run_rpb(&nq);
-        if (upload_run_tables(c, &nq, c->rs[k].st, err, errlen) || size_slot(c->rs[k], np, nrpb, err, errlen) ||
-            issue_piece(c, &nq, np[0], k, nrpb, err, errlen))
-            return -1;
+        slot_busy_set(c, nq.slot, 1);
+        c->pre.valid = 1;  // (set first: an error below drains and releases it)
+        c->pre.comp_slot = nq.slot;
+        c->pre.rslot = k;
+        if (upload_run_tables(c, &nq, c->rs[k].st, err, errlen)) return -1;
+        DCK(hipEventRecord(c->tev, c->rs[k].st));
+        if (size_slot(c->rs[k], np, nrpb, err, errlen) || issue_piece(c, &nq, np[0], k, nrpb, err, errlen)) return -1;
         c->pre.valid = 1;
         c->pre.comp_slot = nq.slot;
         c->pre.comp_len = nq.comp_len;
@@ -1650,6 +1770,13 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
         const int64_t R = (int64_t)hs[0] + hs[1];
         c->n_rewalk += hs[4];
         c->n_sub += (pc.u_hi - pc.u_lo + WS_G - 1) / WS_G;
+        if (hs[5] || (hs[2] & DB_BOUNDS)) {  // a block table or record starts outside the piece: a bug, reported
+            if (err) snprintf(err, (size_t)errlen, "device decode: piece %zu of target %d reads outside its buffers "
+                              "(inflate %u, walk %#x; compressed slot %d fill %llu)", p, q->tid, hs[5], hs[2], q->slot,
+                              (unsigned long long)c->tab_gen[q->slot]);
+            fprintf(stderr, "grom: %s\n", err ? err : "device decode: bounds");
+            return -1;
+        }
         if (hs[3]) {
             if (err) snprintf(err, (size_t)errlen, "device inflate: %u blocks failed", hs[3]);
             return -2;
@@ -1664,7 +1791,7 @@ extern "C" int dd_run_decode(dd_ctx *c, const dd_run_req *q, dd_parse_out *po, i
             hipLaunchKernelGGL(k_walk_sub, dim3((unsigned)(pc.cb - pc.ca)), dim3(WS_T), 0, r.st, P<uint8_t>(r.U),
                                P<int64_t>(c->rS[q->slot]) + pc.ca, pc.base, pc.cb - pc.ca, q->tid, c->ws_guess, (uint32_t *)nullptr,
                                (uint32_t *)nullptr, P<uint32_t>(r.cbase), P<int64_t>(r.off), P<uint32_t>(r.misc),
-                               (int64_t)INT64_MAX);
+                               (int64_t)INT64_MAX, pc.pbytes);
             r.misc_clean = false;  // (the re-walk's flag words stay)
             DCK(hipEventRecord(r.ev[2], r.st));
             DCK(hipEventSynchronize(r.ev[2]));

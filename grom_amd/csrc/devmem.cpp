@@ -29,23 +29,33 @@ struct Hook {
     void *arg;
 };
 std::vector<Hook> g_hooks;
+int g_reclaiming = 0;  // reclaim() calls running hooks (grom_dev_remove_reclaim waits for them)
 
 double env_d(const char *name, double dflt) {
     const char *e = getenv(name);
     return e && *e ? atof(e) : dflt;
 }
 
+// The hooks run outside g_mu (they take their owners' locks and free device
+// memory); g_reclaiming keeps a hook's owner alive meanwhile: removing a hook
+// waits until no reclaim() is running one.
 int64_t reclaim(int device, size_t want) {
     std::vector<Hook> hooks;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         hooks = g_hooks;
+        g_reclaiming++;
     }
     int64_t got = 0;
     for (const Hook &h : hooks) {
         got += h.fn(h.arg, device, want);
         if (got >= (int64_t)want) break;
     }
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_reclaiming--;
+    }
+    g_cv.notify_all();
     return got;
 }
 
@@ -91,12 +101,14 @@ extern "C" void grom_dev_add_reclaim(grom_reclaim_fn fn, void *arg) {
 }
 
 extern "C" void grom_dev_remove_reclaim(grom_reclaim_fn fn, void *arg) {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::unique_lock<std::mutex> lk(g_mu);
     for (size_t i = 0; i < g_hooks.size(); i++)
         if (g_hooks[i].fn == fn && g_hooks[i].arg == arg) {
             g_hooks.erase(g_hooks.begin() + (long)i);
             break;
         }
+    // a reclaim() that copied the list before the erase may still call it
+    g_cv.wait(lk, [] { return g_reclaiming == 0; });
 }
 
 extern "C" int grom_dev_malloc(void **p, size_t bytes, int cat) {
@@ -141,6 +153,11 @@ extern "C" int grom_dev_malloc(void **p, size_t bytes, int cat) {
             }
             (void)hipGetLastError();  // the failure is handled here, not left sticky
             *p = nullptr;
+            if (e != hipErrorOutOfMemory) {  // (a device fault, not memory: no reclaim, no wait)
+                fprintf(stderr, "grom: hipMalloc of %.2f GB (%s) failed: %s\n", (double)bytes / 1e9, cat_name(cat),
+                        hipGetErrorString(e));
+                return -1;
+            }
         }
         // idle memory of this process first (stages no chromosome holds)
         if (reclaim(device, bytes) > 0) continue;

@@ -804,12 +804,11 @@ static void *hip_init_main(void *arg) {
     if (getenv("GROM_NO_WARM") == NULL) dd_device_warm(device);
     /* the device decoder's first context, made while the host reads the
      * FASTA lengths and the BAI (GROM_NO_CTX_PREPARE=1: made by the worker).
-     * Not with several decode workers per GPU (GROM_DD_WORKERS > 1): that
-     * mode's GPU tests once gave a stage digest unlike the host decoder's
-     * with the context ready early, so it keeps its timing */
-    const char *dd = getenv("GROM_DEVICE_DECODE"), *np = getenv("GROM_NO_CTX_PREPARE"),
-               *wk = getenv("GROM_DD_WORKERS");
-    if (!(dd && atoi(dd) == 0) && !(np && atoi(np) == 1) && !(wk && atoi(wk) > 1)) dd_ctx_prepare(device);
+     * One context is prepared: with several decode workers per GPU
+     * (GROM_DD_WORKERS > 1) the first to start takes it, the others make
+     * their own */
+    const char *dd = getenv("GROM_DEVICE_DECODE"), *np = getenv("GROM_NO_CTX_PREPARE");
+    if (!(dd && atoi(dd) == 0) && !(np && atoi(np) == 1)) dd_ctx_prepare(device);
     return NULL;
 }
 
@@ -1484,11 +1483,12 @@ done:
             printf("device decode: %lld records, %.2f GB compressed read and copied to HBM, %.2f GB inflated on the GPU; "
                    "file reads %.2f s (read ahead; waited for %.2f s), device work %.2f s (GPU inflate %.3f s, record walk %.3f s, "
                    "parse %.3f s; %lld of %lld walk sub-chunks re-walked), device buffer growth %.3f s, per-chromosome decode + "
-                   "finalise %.2f s, idle stage blocks reclaimed %lld, wall %.2f s\n",
+                   "finalise %.2f s, idle stage blocks reclaimed %lld, %d decode workers, %lld statistics-only runs, wall %.2f s\n",
                    (long long)pc.records, pc.compressed_bytes / 1e9, pc.inflated_bytes / 1e9, pc.io_s, pc.wait_s,
                    pc.decode_thread_s,
                    pc.gpu_ms[0] / 1e3, pc.gpu_ms[1] / 1e3, pc.gpu_ms[2] / 1e3, (long long)pc.rewalked, (long long)pc.subchunks,
-                   pc.gpu_ms[3] / 1e3, pc.upload_s, (long long)pc.reclaimed, clock_gettime_s() - t_start);
+                   pc.gpu_ms[3] / 1e3, pc.upload_s, (long long)pc.reclaimed, pc.dd_workers, (long long)pc.stats_only_runs,
+                   clock_gettime_s() - t_start);
         else
         printf("streamed decode: %lld records in %lld pieces, %d threads (%s), %.2f GB inflated, %.2f GB to HBM, "
                "decoder busy %.2f s (inflate %.2f s, file reads %.2f s), uploader %.2f s (waiting %.2f s), wall %.2f s\n",

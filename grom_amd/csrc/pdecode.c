@@ -434,6 +434,7 @@ struct pd_session {
     int n_dw, dw_started;
     double c_gpu_ms[4];    /* inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
     int64_t c_reclaimed;   /* idle stage blocks freed for a waiting allocation */
+    int64_t c_stats_only;  /* device mode: runs decoded for the statistics alone */
     int stats_given;       /* the insert statistics come from <bam>.mean (pd_stats_given) */
     int reclaim_on;        /* pd_reclaim_stages is registered (devmem.h) */
     int64_t c_rewalk, c_subchunks; /* record walk: sub-chunks re-walked / all */
@@ -2608,6 +2609,9 @@ static int dw_stats_only(dd_worker *w, int from, char *err, int errlen) {
         pd_trace(s, PD_EV_PHASE, 103, i);
         const int rc = dw_decode(w, i, next_placed_run(s, i), NULL, 0, 0, 1, &po, &R, err, errlen);
         if (rc) return rc;
+        pthread_mutex_lock(&s->mu);
+        s->c_stats_only++;
+        pthread_mutex_unlock(&s->mu);
     }
     if (!s->stats_done) mark_stats_done(s);
     return 0;
@@ -2861,6 +2865,12 @@ static void *dw_main(void *arg) {
     return NULL;
 }
 
+int pd_dd_workers(void) {
+    const char *ws = getenv("GROM_DD_WORKERS");
+    int per = ws && atoi(ws) > 0 ? atoi(ws) : 1;
+    return per > 8 ? 8 : per;
+}
+
 static int pd_start_device(pd_session *s) {
     int devs[64], nd = 0;
     for (int k = 0; k < s->n_plan; k++) {
@@ -2870,20 +2880,7 @@ static int pd_start_device(pd_session *s) {
     }
     if (nd == 0) devs[nd++] = 0;
     /* GROM_DD_WORKERS per GPU (one reads a run while another's is on the GPU) */
-    const char *ws = getenv("GROM_DD_WORKERS");
-    int per = ws && atoi(ws) > 0 ? atoi(ws) : 1;
-    if (per > 8) per = 8;
-    /* Several decode workers on ONE GPU are disabled: at the end of round 5
-     * that mode faulted the device intermittently (an illegal memory access,
-     * test_device_decode_stats_prefix run first in a fresh process, its
-     * 0.25 MB-piece "workers" mode: 3 runs of 4), a race not yet found
-     * (DESIGN.md 4.5).  GROM_DD_WORKERS_UNSAFE=1 keeps the mode for that
-     * investigation.  One worker per GPU is the default and is unaffected. */
-    const char *wu = getenv("GROM_DD_WORKERS_UNSAFE");
-    if (per > 1 && !(wu && atoi(wu) == 1)) {
-        fprintf(stderr, "grom: GROM_DD_WORKERS=%d ignored: one decode worker per GPU (DESIGN.md 4.5)\n", per);
-        per = 1;
-    }
+    const int per = pd_dd_workers();
     const char *it = getenv("GROM_DECODE_THREADS");
     /* the read-ahead's pread threads per worker: 16 read chr1's 1.75 GB in
      * 0.18 s from the page cache against 0.28 s with 8 (profiles/r05aa) */
@@ -3078,6 +3075,8 @@ void pd_get_counters(pd_session *s, pd_counters *c) {
     c->io_s = s->c_io_s;
     c->upload_s = s->c_upl_s;
     c->reclaimed = s->c_reclaimed;
+    c->dd_workers = s->dw_started;
+    c->stats_only_runs = s->c_stats_only;
     c->wait_s = s->c_wait_s;
     c->threads = s->n_threads;
     pthread_mutex_unlock(&s->mu);

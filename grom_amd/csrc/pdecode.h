@@ -68,6 +68,9 @@ void pd_set_wanted(pd_session *s, const int *want);
  * reads its chromosomes' compressed runs, inflates and parses them into the
  * stages) instead of the host decoder threads; same results, same API */
 void pd_set_device_mode(pd_session *s, int on);
+/* device decode workers per GPU (GROM_DD_WORKERS, 1..8; default 1): the one
+ * place that decides it (pd_start_device, the CLI's start-up thread) */
+int pd_dd_workers(void);
 /* device mode: each GPU's chromosomes are decoded longest first (plan order
  * among equal lengths); the caller takes them in that order */
 int pd_device_mode(const pd_session *s);
@@ -108,6 +111,8 @@ typedef struct pd_counters {
     int64_t rewalked, subchunks; /* device mode: record-walk sub-chunks re-walked / all */
     double gpu_ms[4];    /* device mode: inflate, record walk, parse (HIP events, summed); buffer growth (wall) */
     int64_t reclaimed;   /* idle stage blocks freed for allocations short of device memory */
+    int dd_workers;      /* device mode: decode workers (all GPUs) */
+    int64_t stats_only_runs; /* device mode: runs decoded for the insert statistics alone */
 } pd_counters;
 void pd_get_counters(pd_session *s, pd_counters *c);
 void pd_close(pd_session *s);

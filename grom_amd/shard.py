@@ -263,18 +263,33 @@ def merge_rank_outputs_parallel(rank: int, vcf_path: str, chroms_mine: Sequence[
     merge_rank_outputs; rank 0 no longer reads and re-joins the genome's
     ~440 MB of rows alone (4.4 s in Python)."""
     import os
-    size = os.path.getsize(vcf_path)
-    if segs_path is not None:
-        hdr_end, segs = read_vcf_segments(segs_path, size)
-        missing = set(segs) - set(chroms_mine)
-        if missing:
-            raise RuntimeError(f"rows of chromosomes outside the rank's share: {sorted(missing)[:5]}")
-    else:
-        with open(vcf_path, "rb") as f:
-            hdr_end, segs = vcf_segments(f.read(), chroms_mine)
-    info = all_gather((rank, hdr_end, {c: e - s for c, (s, e) in segs.items()}))
+
+    def agree(ok_err, payload=None):
+        """all_gather of (rank, error or None, payload): a rank that failed makes
+        every rank raise at once (a rank that raised alone would leave the
+        others waiting in the next collective until its timeout)."""
+        got = all_gather((rank, ok_err, payload))
+        bad = [(r, e) for r, e, _ in got if e is not None]
+        if bad:
+            raise RuntimeError("merge failed on rank(s) " + "; ".join(f"{r}: {e}" for r, e in bad))
+        return got
+
+    hdr_end, segs, err = 0, {}, None
+    try:
+        size = os.path.getsize(vcf_path)
+        if segs_path is not None:
+            hdr_end, segs = read_vcf_segments(segs_path, size)
+            missing = set(segs) - set(chroms_mine)
+            if missing:
+                raise RuntimeError(f"rows of chromosomes outside the rank's share: {sorted(missing)[:5]}")
+        else:
+            with open(vcf_path, "rb") as f:
+                hdr_end, segs = vcf_segments(f.read(), chroms_mine)
+    except (OSError, RuntimeError, ValueError) as e:
+        err = f"{type(e).__name__}: {e}"
+    info = agree(err, (hdr_end, {c: e - s for c, (s, e) in segs.items()}))
     hdr_len, sizes = 0, {}
-    for r, h, d in info:
+    for r, _, (h, d) in info:
         if r == 0:
             hdr_len = h
         for c, n in d.items():
@@ -288,27 +303,35 @@ def merge_rank_outputs_parallel(rank: int, vcf_path: str, chroms_mine: Sequence[
     for c in chrom_order:
         off[c] = base
         base += sizes.get(c, 0)
-    src = os.open(vcf_path, os.O_RDONLY)
+    err = None
     try:
         if rank == 0:
-            with open(out_vcf, "wb") as f:
-                f.write(os.pread(src, hdr_end, 0))
+            with open(out_vcf, "wb") as f, open(vcf_path, "rb") as g:
+                f.write(g.read(hdr_end))
                 f.truncate(base)
-        barrier()
-        dst = os.open(out_vcf, os.O_WRONLY)
+    except OSError as e:
+        err = f"OSError: {e}"
+    agree(err)
+    err = None
+    try:
+        src = os.open(vcf_path, os.O_RDONLY)
         try:
-            for c, (s, e) in segs.items():
-                done = 0
-                while done < e - s:
-                    k = os.copy_file_range(src, dst, e - s - done, s + done, off[c] + done)
-                    if k <= 0:
-                        raise OSError(f"copy_file_range returned {k}")
-                    done += k
+            dst = os.open(out_vcf, os.O_WRONLY)
+            try:
+                for c, (s, e) in segs.items():
+                    done = 0
+                    while done < e - s:
+                        k = os.copy_file_range(src, dst, e - s - done, s + done, off[c] + done)
+                        if k <= 0:
+                            raise OSError(f"copy_file_range returned {k}")
+                        done += k
+            finally:
+                os.close(dst)
         finally:
-            os.close(dst)
-    finally:
-        os.close(src)
-    barrier()
+            os.close(src)
+    except OSError as e:
+        err = f"OSError: {e}"
+    agree(err)
     if rank == 0 and out_ctx is not None:
         from . import ctx_postpass
         raw = {}

@@ -736,10 +736,10 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
     exactly the input the host decoder threads (pdecode.c) stage: same stream
     facts and the same digest of every array, CIGAR/base/quality/SA-XP
     content, dropped record and name-id relation; and the outputs are the
-    oracle's.  Mode "3w" asks for three device decode workers on the GPU
-    (GROM_DD_WORKERS); several workers on one GPU are disabled since the end
-    of round 5 (an intermittent device fault), so it runs one
-    worker and checks that the request is ignored safely.  Modes "g0"/"g2" run
+    oracle's.  Mode "3w" runs three device decode workers on the GPU
+    (GROM_DD_WORKERS), each with its own decode context, prefetch thread and
+    chromosomes, sharing the stages (the in-process shape of the reference's
+    concurrent -P children, GROM.c:549-599).  Modes "g0"/"g2" run
     the record walk's guess-then-verify (k_walk_sub) with no guesses and with
     guesses at raw sub-chunk offsets (almost all wrong): every sub-chunk is
     then walked again from the true chain, with the same result.  Mode "cu"
@@ -767,6 +767,8 @@ def test_device_decode_matches_host_decode(datadir, capfd, case, extra):
                  env_extra=dict(env, GROM_STAGE_DIGEST="1", GROM_VERBOSE="1"))
         out = capfd.readouterr().out
         assert ("device decode:" in out) == (mode != "0"), out[-1500:]
+        if mode == "3w":
+            assert " 3 decode workers," in out, out[-1500:]
         lines[mode] = sorted(l for l in out.splitlines() if l.startswith("stage "))
     assert lines["1"] and all(lines[m] == lines["0"] for m in modes), {m: lines[m][:3] for m in modes}
     for mode in modes:
@@ -819,11 +821,10 @@ def test_device_decode_stats_prefix(datadir, capfd, case, cap):
     pieces with 64 kB pieces) and one past it.  cnv_multi's first contig is
     not its longest: one worker decodes it first anyway (the sample is in file
     order), and of two workers the one that gathers the statistics does not
-    parse it (a statistics-only pass over it).  The "workers" mode asks for
-    two workers on the GPU; that is disabled since the end of round 5 (an
-    intermittent device fault in exactly this mode), so it
-    runs one worker with 0.25 MB pieces; GROM_DD_WORKERS_UNSAFE=1 restores
-    the two workers for the investigation."""
+    parse it (a statistics-only pass over it).  The "workers" mode runs two
+    workers on the GPU with 0.25 MB pieces: the mode that faulted the device
+    in round 5 (the next run's block table read before its upload landed,
+    DESIGN.md 4.5)."""
     bam, fa = synth(datadir, case, CASES[case])
     extra = ["-M", "-V", "1"]
     common = {"GROM_TEST_INSERT_CAP": cap, "GROM_STAGE_DIGEST": "1", "GROM_VERBOSE": "1"}
@@ -836,6 +837,10 @@ def test_device_decode_stats_prefix(datadir, capfd, case, cap):
         capfd.readouterr()
         run_grom(datadir, bam, fa, f"pfx_{case}_{cap}_{mode}.vcf", extra, env_extra=dict(common, **env))
         out = capfd.readouterr().out
+        if mode == "workers":
+            assert " 2 decode workers," in out, out[-1500:]
+            if case == "cnv_multi":  # the gatherer (worker 0) does not own the first run: a statistics-only pass
+                assert int(re.search(r"(\d+) statistics-only runs", out).group(1)) >= 1, out[-1500:]
         ins = [l for l in out.splitlines() if l.startswith(("insert mean", "insert_min_size", "median read"))]
         stages = sorted(l for l in out.splitlines() if l.startswith("stage "))
         vcf = open(datadir / f"pfx_{case}_{cap}_{mode}.vcf").read() + open(datadir / f"pfx_{case}_{cap}_{mode}.ctx.vcf").read()
@@ -843,6 +848,41 @@ def test_device_decode_stats_prefix(datadir, capfd, case, cap):
     assert got["host"][0] and got["host"][1]
     for mode in modes:
         assert got[mode] == got["host"], mode
+
+
+@pytest.mark.parametrize("case,extra,env", [
+    ("cnv_multi", ["-V", "1", "-M"], {"GROM_DD_WORKERS": "2"}),
+    ("cnv_multi", ["-V", "1", "-M"], {"GROM_DD_WORKERS": "2", "GROM_DD_PIECE_MB": "0.125"}),
+    ("c3_genome", ["-M", "-V", "1"], {"GROM_DD_WORKERS": "3", "GROM_DD_PIECE_MB": "0.25"})],
+    ids=["cnv_multi_2w", "cnv_multi_2w_pieces", "c3_genome_3w_pieces"])
+def test_decode_workers_share_session(datadir, capfd, case, extra, env):
+    """Several device decode workers in one session on one GPU: the shape
+    `grom -P n` runs across n GPUs (one decode worker per GPU, pdecode.c
+    dw_main), mapped onto the one GPU of the test box.  Worker 0 gathers the
+    insert statistics (find_insert_mean, GROM.c:1205-1318) but, with
+    cnv_multi's longer second contig dealt to it first, does not own the
+    first run in file order: it reads the statistics from that run (and the
+    next) alone, while worker 1 parses it.  Each worker issues its next run's
+    first piece ahead; the workers share the stages.  Full statistics cap,
+    default and small pieces; every staged chromosome's digest equals the host
+    decoder's and the VCF/.ctx.vcf the oracle's, at the full insert-sample
+    cap."""
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"dw_{case}_{'_'.join(f'{k}{v}' for k, v in env.items())}".replace(".", "")
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    stages = {}
+    for mode, e in {"host": {"GROM_DEVICE_DECODE": "0"}, "dev": dict(env, GROM_DEVICE_DECODE="1")}.items():
+        capfd.readouterr()
+        run_grom(datadir, bam, fa, f"{mode}_{tag}.vcf", extra, env_extra=dict(e, GROM_STAGE_DIGEST="1", GROM_VERBOSE="1"))
+        out = capfd.readouterr().out
+        stages[mode] = sorted(l for l in out.splitlines() if l.startswith("stage "))
+        if mode == "dev":
+            assert f" {env['GROM_DD_WORKERS']} decode workers," in out, out[-1500:]
+            if case == "cnv_multi":
+                assert int(re.search(r"(\d+) statistics-only runs", out).group(1)) >= 1, out[-1500:]
+        for ext in (".vcf", ".ctx.vcf"):
+            assert open(datadir / f"o_{tag}{ext}").read() == open(datadir / f"{mode}_{tag}{ext}").read(), (mode, ext)
+    assert stages["host"] and stages["dev"] == stages["host"]
 
 
 _FOOT = re.compile(r"buffers: peak ([\d.]+) GB together, per kind scan ([\d.]+), breakpoint ([\d.]+), CNV ([\d.]+), "

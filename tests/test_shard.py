@@ -247,3 +247,29 @@ def test_vcf_segments_rejects_interleaved_rows():
     with pytest.raises(RuntimeError):
         vcf_segments(data, ["chr1", "chr2"])
     assert vcf_segments(b"#h\nchr1\t1\nchr1\t2\nchr2\t1\n", ["chr1", "chr2"]) == (3, {"chr1": (3, 17), "chr2": (17, 24)})
+
+
+def test_gloo_world2_merge_fails_fast_on_every_rank(tmp_path):
+    """A rank whose segment index does not validate (it used to
+    raise alone, leaving the other rank in the next collective until the
+    process-group timeout): both ranks raise within seconds."""
+    import time
+
+    import torch.multiprocessing as mp
+    world = 2
+    for r in range(world):
+        mine = [c for i, c in enumerate(_MERGE_CHROMS) if i % world == r]
+        _rank_vcf(tmp_path / f"r{r}.vcf", mine, tmp_path / f"r{r}.segs")
+    (tmp_path / "r1.segs").write_text("chr2\t0\t5\n")  # does not tile rank 1's file
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    t0 = time.time()
+    procs = [ctx.Process(target=_merge_worker, args=(r, world, port, str(tmp_path), True, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert time.time() - t0 < 100
+    assert all("merge failed on rank(s) 1" in res[r] for r in range(world)), res
