@@ -32,9 +32,11 @@ translocation post-pass over all raw CTX rows (grom_amd.shard.merge_rank_outputs
 data-path collective: chromosomes are independent.
 
 The JSON line also carries:
-  identical_to_oracle_full_scale  the timed run's VCF and .ctx.vcf rows against
-                  the oracle's on the same full-scale genome (sha256 of the
-                  non-header rows, tests/golden/oracle_genome_s100.json);
+  identical_to_oracle_full_scale  every timed run's VCF and .ctx.vcf rows
+                  against the oracle's on the same full-scale genome (sha256
+                  of the non-header rows, tests/golden/oracle_genome_s100.json;
+                  each step writes its own files, hashed after the timed
+                  region: oracle_full_scale.identical_runs "k/K");
   footprint_rank0 the run's peak device memory (the CLI's footprint line);
 and (rank 0, N=1):
   roofline        the pileup kernel (k_scan_tile) in the timed whole runs:
@@ -453,18 +455,28 @@ def main():
     barrier()
     bam, fa = os.path.join(work, "genome.bam"), os.path.join(work, "genome.fa")
 
-    # the rank's CLI: its chromosomes, its GPU, its share of the CPUs
+    # the rank's CLI: its chromosomes, its GPU, its share of the CPUs.  The
+    # CLI sees only its own GPU (HIP_VISIBLE_DEVICES): a process that could
+    # see all eight would initialise the HIP runtime over all of them, a fixed
+    # cost every rank pays inside the timed step
     cpus = cpu_quota()
-    env = {"GROM_DEVICE": str(local)}
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    vis_list = [v for v in vis.split(",") if v.strip()] if vis else []
+    env = {"GROM_DEVICE": "0", "HIP_VISIBLE_DEVICES": vis_list[local] if local < len(vis_list) else str(local)}
     if world > 1:
         env.update(GROM_CHROMS=",".join(names[i].lower() for i in mine),
                    GROM_DECODE_THREADS=str(max(1, cpus // world)),
                    GROM_CTX_RAW=os.path.join(work, f"rank{rank}.ctxraw"),
                    GROM_VCF_SEGS=os.path.join(work, f"rank{rank}.segs"))
-    out = os.path.join(work, f"rank{rank}.vcf")
     hdr_names = names  # BAM target names (the CTX post-pass maps mate ids to them)
 
-    def step():
+    def outs(k):
+        """step k's output files (each timed step keeps its own, so every
+        step's rows are compared with the oracle after the timed region)"""
+        return os.path.join(work, f"rank{rank}_s{k}.vcf"), os.path.join(work, f"merged_s{k}.vcf")
+
+    def step(k):
+        out, merged = outs(k)
         dt, so = whole_run(work, bam, fa, out, flags, env)
         if world > 1:
             # every rank copies its own chromosomes' rows into the merged VCF
@@ -473,11 +485,17 @@ def main():
             barrier()
             m = open(bam + ".mean").read().split()  # insert mean, lseq, min, max (save_insert_mean)
             merge_rank_outputs_parallel(rank, out, [names[i].lower() for i in mine], [n.lower() for n in names],
-                                        os.path.join(work, "merged.vcf"), all_gather_objects, barrier,
+                                        merged, all_gather_objects, barrier,
                                         [os.path.join(work, f"rank{r}.ctxraw") for r in range(world)], hdr_names,
-                                        int(m[3]), int(m[1]), os.path.join(work, "merged.ctx.vcf"),
+                                        int(m[3]), int(m[1]), merged[:-4] + ".ctx.vcf",
                                         segs_path=os.path.join(work, f"rank{rank}.segs"))
         return dt, so
+
+    def drop(k):
+        for p in outs(k):
+            for q in (p, p[:-4] + ".ctx.vcf"):
+                if os.path.exists(q):
+                    os.remove(q)
 
     if world > 1 and rank == 0:
         # the side files every rank's CLI reads (<bam>.mean, <fasta>.info) are
@@ -486,14 +504,15 @@ def main():
         whole_run(work, bam, fa, os.path.join(work, "prewarm.vcf"), flags, {"GROM_PLAN_ONLY": "1", "GROM_CHROMS": "-"})
     barrier()
     for w in range(args.warmup):
-        dt, _ = step()
+        dt, _ = step(-1 - w)
+        drop(-1 - w)
         log(f"warmup run {w + 1}: {dt:.2f} s")
     barrier()
     t0 = time.perf_counter()
     runs, last, run_out = [], "", []
     for k in range(args.steps):
         t1 = time.perf_counter()
-        _, last = step()
+        _, last = step(k)
         runs.append(time.perf_counter() - t1)
         run_out.append(last)
         ph = [ln[len("cli phases (s from start): "):] for ln in last.splitlines() if ln.startswith("cli phases")]
@@ -521,7 +540,7 @@ def main():
             resident = {"skipped": f"time budget (--budget-s {args.budget_s:g}: {remaining:.0f} s left, the leg "
                                    f"takes about {est:.0f} s)"}
         else:
-            resident, alone, rl = resident_leg(local, knobs, lengths, names, bam, out, args.resident_steps,
+            resident, alone, rl = resident_leg(local, knobs, lengths, names, bam, outs(args.steps - 1)[0], args.resident_steps,
                                                max(1, min(args.inflight, 8)))
             log(f"device-resident: {resident['value']} Mbases/s, rows identical: "
                 f"{resident['rows_identical_to_whole_run']}/{resident['ctx_identical_to_whole_run']}")
@@ -530,10 +549,23 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             with tempfile.TemporaryDirectory() as d:
                 cpu, conc = cpu_baseline_and_concordance(d, knobs, flags)
-        final_vcf = out if world == 1 else os.path.join(work, "merged.vcf")
+        # every timed step's rows against the oracle's full-scale digest
+        # (after the timed region; each step wrote its own files)
+        final_of = [outs(k)[0] if world == 1 else outs(k)[1] for k in range(args.steps)]
+        final_vcf = final_of[-1]
         n_rows, _ = rows_digest(final_vcf)
-        full = (oracle_full_scale(final_vcf, final_vcf[:-4] + ".ctx.vcf")
-                if genome and args.scale == 1.0 else None)
+        full = None
+        if genome and args.scale == 1.0:
+            per = [oracle_full_scale(v, v[:-4] + ".ctx.vcf") for v in final_of]
+            full = per[-1]
+            if full is not None:
+                full["identical_runs"] = f"{sum(1 for p in per if p and p['identical'])}/{len(per)}"
+                full["identical"] = all(p and p["identical"] for p in per)
+        else:
+            # a reduced workload has no oracle digest: the steps' rows must at least agree with each other
+            d0 = [rows_digest(v) + rows_digest(v[:-4] + ".ctx.vcf") for v in final_of]
+            full_steps_agree = all(d == d0[0] for d in d0)
+            log(f"timed steps' rows identical to each other: {full_steps_agree}")
         wl = ("BASELINE configs[2]: synthetic 30x 2x150 bp human-shape genome, 24 GRCh38 contigs "
               f"({total / 1e9:.3f} Gb), SNV/indel, {knobs['sv_per_mb']:.2f} breakpoint SVs/Mb "
               "(DEL/DUP/INV/INS/CTX with split reads + discordant pairs), 500 CNVs/3.1 Gb, 5% PCR duplicates, "
@@ -585,8 +617,12 @@ def main():
             "concordance": conc,
             "device_resident": resident,
         }
+        if full is None and not (genome and args.scale == 1.0):
+            line["steps_rows_identical"] = full_steps_agree
         print(json.dumps(line), flush=True)
     barrier()
+    for k in range(args.steps):
+        drop(k)
     if rank == 0 and not args.workdir:
         shutil.rmtree(work, ignore_errors=True)
     if world > 1:

@@ -704,6 +704,11 @@ typedef struct {
     double t_decclose;                     /* the decoder's host side closed */
     pthread_t hip_thr;     /* HIP runtime start-up, beside the header/FASTA/index work */
     int hip_started;
+    /* -P n (1..256, GROM.c:21923-21927): every chromosome reads its own
+     * target's records (bam_fetch, GROM.c:21051-21064 and the -c children of
+     * GROM.c:549-599) -- pd_set_fetch_mode; GROM_P_SERIAL=1 keeps the serial
+     * stream's input (a one-process run's rows) on n GPUs */
+    int fetch;
 } cli_state;
 
 /* Peak device memory of this process (GROM_VERBOSE): the kernel driver's
@@ -1095,7 +1100,29 @@ static int run_serial(cli_state *S) {
                 batch_ended = 0;                                                                   \
             }                                                                                      \
         } while (0)
-    while (cur < n_plan && bam_read_rec(&br, &rec) > 0) {
+    while (S->fetch && cur < n_plan && bam_read_rec(&br, &rec) > 0) {
+        /* -P: chromosome `cur` is given its own target's placed records
+         * (bam_fetch over [0, MAX_REGION), GROM.c:320) and its stream ends at
+         * its last one; a record of a later plan chromosome completes every
+         * chromosome before it.  The file is coordinate-sorted (bam_fetch's
+         * precondition): a record of an earlier target cannot follow. */
+        if (rec.pos < 0 || rec.pos >= 300000000) continue;
+        int k = -1;
+        for (int j = cur; j < n_plan && k < 0; j++)
+            if (order[j] == rec.tid) k = j;
+        if (k < 0) {
+            for (int j = 0; j < cur; j++)
+                if (order[j] == rec.tid) {
+                    fprintf(stderr, "grom: -P needs a coordinate-sorted BAM (target %d after a later one)\n", rec.tid);
+                    status = 1;
+                }
+            if (status) break;
+            continue;
+        }
+        while (cur < k) SUBMIT_CUR();
+        grom_batch_add(&batch, &rec, s0);
+    }
+    while (!S->fetch && cur < n_plan && bam_read_rec(&br, &rec) > 0) {
         /* cdp_lseq after the chromosome: the l_qseq of the record that ended
          * it (the R-side edge tests of its last bases read it, GROM.c:12047) */
         if (!batch_ended && batch.n_seen > 0 && rec.tid != order[cur]) {
@@ -1301,6 +1328,7 @@ static int run_streamed(cli_state *S) {
         }
         if (given) pd_stats_given(pd);
     }
+    if (S->fetch) pd_set_fetch_mode(pd, 1);
     if (getenv("GROM_CHROMS")) {
         int *want = calloc(S->n_cand > 0 ? S->n_cand : 1, sizeof(int));
         for (int c = 0; c < S->n_cand; c++) want[c] = chrom_wanted(S->plan[c].name);
@@ -1604,7 +1632,13 @@ static int cli_run(int argc, char **argv, int force_serial) {
         case 'a': P->min_snv_ratio = atof(optarg); break;
         case 'f': P->vcf = 0; break;
         case 'x': P->min_ave_bq = atof(optarg); break;
-        case 'P': S->n_dev = atoi(optarg); break; /* -P threads -> GPUs, GROM.c:21930 */
+        case 'P': { /* -P processes -> GPUs; 0 or beyond 256: serial, one GPU (GROM.c:21923-21927) */
+            const int n = atoi(optarg);
+            const char *ps = getenv("GROM_P_SERIAL");
+            S->fetch = n >= 1 && n <= 256 && !(ps && atoi(ps) == 1);
+            S->n_dev = n >= 1 && n <= 256 ? n : 1;
+            break;
+        }
         case 'Z': P->block_min = atol(optarg); break;
         case 'W': P->min_rd_window_len = atol(optarg); break;
         case 'X': P->max_rd_window_len = atol(optarg); break;

@@ -436,6 +436,7 @@ struct pd_session {
     int64_t c_reclaimed;   /* idle stage blocks freed for a waiting allocation */
     int64_t c_stats_only;  /* device mode: runs decoded for the statistics alone */
     int stats_given;       /* the insert statistics come from <bam>.mean (pd_stats_given) */
+    int fetch_mode;        /* GROM -P n: every chromosome its own records (bam_fetch), pd_set_fetch_mode */
     int reclaim_on;        /* pd_reclaim_stages is registered (devmem.h) */
     int64_t c_rewalk, c_subchunks; /* record walk: sub-chunks re-walked / all */
     int io_threads;
@@ -1468,7 +1469,8 @@ static int chrom_finalize(pd_session *s, int k) {
     } else {
         f->p_last = -1;
     }
-    if (c->n_seen > 0 && c->run >= 0 && s->runs[c->run].has_next) f->lseq_tail = s->runs[c->run].next_lq;
+    /* (-P: the chromosome's stream ends at its own last record) */
+    if (c->n_seen > 0 && c->run >= 0 && s->runs[c->run].has_next && !s->fetch_mode) f->lseq_tail = s->runs[c->run].next_lq;
     else if (any) f->lseq_tail = c->last_lq + (c->last_kept == 1 ? c->last_hclip : 0);
     else f->lseq_tail = 0;
     /* drops after the prefix, counting kept reads after the trim */
@@ -1722,6 +1724,24 @@ static void plan_runs(const pd_session *s, const int *keep, int *rc, int64_t *rj
     for (int i = 0; i < s->n_runs; i++) {
         rc[i] = -1;
         rj[i] = 0;
+    }
+    if (s->fetch_mode) {
+        /* -P: each chromosome reads its own target's records through
+         * bam_fetch (GROM.c:21051-21064, 304-324): its whole run, nothing
+         * consumed by the chromosome before it, nothing starved */
+        for (int k = 0; k < s->n_plan; k++) {
+            chr[k] = -1;
+            if (keep && !keep[k]) continue;
+            for (int i = 0; i < s->n_runs && s->plan[k].tid >= 0; i++)
+                if (s->runs[i].tid == s->plan[k].tid) {
+                    if (rc[i] < 0) {
+                        rc[i] = k;
+                        chr[k] = i;
+                    }
+                    break;
+                }
+        }
+        return;
     }
     int cr = 0, stuck = 0;
     int64_t co = 0;
@@ -2031,6 +2051,31 @@ fail:
 }
 
 void pd_set_device_mode(pd_session *s, int on) { s->dev_mode = on; }
+
+void pd_set_fetch_mode(pd_session *s, int on) {
+    s->fetch_mode = on != 0;
+    /* the initial plan again (pd_open made the serial stream's) */
+    int *rc = (int *)malloc(sizeof(int) * (size_t)(s->n_runs + 1));
+    int64_t *rj = (int64_t *)malloc(sizeof(int64_t) * (size_t)(s->n_runs + 1));
+    int *chr = (int *)malloc(sizeof(int) * (size_t)(s->n_plan + 1));
+    plan_runs(s, NULL, rc, rj, chr);
+    for (int i = 0; i < s->n_runs; i++) {
+        s->runs[i].chrom = rc[i];
+        s->runs[i].j0 = rj[i];
+    }
+    for (int k = 0; k < s->n_plan; k++) {
+        s->ch[k].run = chr[k];
+        s->ch[k].j_left = chr[k] >= 0 ? rj[chr[k]] : 0;
+    }
+    for (int i = 0; i < s->n_runs; i++) {
+        const pd_run *r = &s->runs[i];
+        for (int q = r->first_piece; q < r->first_piece + r->n_pieces; q++)
+            s->pieces[q].full = r->chrom >= 0 && s->want[r->chrom];
+    }
+    free(rc);
+    free(rj);
+    free(chr);
+}
 int pd_device_mode(const pd_session *s) { return s->dev_mode; }
 
 void pd_set_wanted(pd_session *s, const int *want) {
@@ -2701,7 +2746,7 @@ static int dw_chrom(dd_worker *w, int k, int next_run, int stats, char *err, int
         f->p_last = -1;
     }
     const int64_t n_seen = ri >= 0 ? po.n_rec - j0 : 0;
-    if (n_seen > 0 && s->runs[ri].has_next) f->lseq_tail = s->runs[ri].next_lq;
+    if (n_seen > 0 && s->runs[ri].has_next && !s->fetch_mode) f->lseq_tail = s->runs[ri].next_lq;
     else if (any) f->lseq_tail = po.last_lq + (po.last_kept ? po.last_hclip : 0);
     else f->lseq_tail = 0;
     if (rc == 0 && !s->splitread && any) {

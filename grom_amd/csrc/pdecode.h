@@ -68,6 +68,12 @@ void pd_set_wanted(pd_session *s, const int *want);
  * reads its chromosomes' compressed runs, inflates and parses them into the
  * stages) instead of the host decoder threads; same results, same API */
 void pd_set_device_mode(pd_session *s, int on);
+/* before pd_set_wanted / pd_start: GROM -P n semantics (GROM.c:21051-21064,
+ * 549-599): every chromosome is given its own target's records as bam_fetch
+ * returns them -- no records consumed by the chromosome before it (no Q1
+ * drops), no starvation after an empty one (no Q21), its stream ending at its
+ * own last record -- instead of the serial stream's */
+void pd_set_fetch_mode(pd_session *s, int on);
 /* device decode workers per GPU (GROM_DD_WORKERS, 1..8; default 1): the one
  * place that decides it (pd_start_device, the CLI's start-up thread) */
 int pd_dd_workers(void);

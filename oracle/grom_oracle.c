@@ -198,10 +198,21 @@ typedef struct {
     bgzf_reader bg;
     bam_hdr hdr;
     int open;
+    int only_tid; /* -1: every record (the serial stream); else bam_fetch's records of that target */
 } stream_t;
+
+/* -P n (1 <= n <= 256, GROM.c:21923-21927): every chromosome reads its own
+ * records through bam_fetch over [g_sub_region_start, g_sub_region_end - 1] =
+ * [0, MAX_REGION) (the reader thread of find_disc_svs, GROM.c:21051-21064,
+ * single_chromosome_read GROM.c:304-324; the -c children of -P n > 1 do the
+ * same, GROM.c:549-599): the target's records with a position, in file
+ * order, then the end of the stream -- no records of the next chromosome are
+ * consumed (no Q1 drops) and an empty chromosome starves nothing (no Q21). */
+static int g_fetch_mode = 0;
 
 static int stream_open(stream_t *s, const char *path) {
     memset(s, 0, sizeof(*s));
+    s->only_tid = -1;
     if (bgzf_open_read(&s->bg, path) != 0) return -1;
     if (bam_read_header(&s->bg, &s->hdr) != 0) return -1;
     s->open = 1;
@@ -214,8 +225,14 @@ static void stream_close(stream_t *s) {
     s->open = 0;
 }
 static int my_samread(stream_t *s, bam_rec *b) {
-    int rc = bam_read_rec(&s->bg, b);
-    return rc > 0 ? 1 : -1;
+    for (;;) {
+        int rc = bam_read_rec(&s->bg, b);
+        if (rc <= 0) return -1;
+        /* bam_fetch over [0, MAX_REGION): the target's records that overlap
+         * it, i.e. every one with a position (an unmapped read placed at its
+         * mate's position included) */
+        if (s->only_tid < 0 || (b->tid == s->only_tid && b->pos >= 0 && b->pos < 300000000)) return 1;
+    }
 }
 
 /* ---------------- find_insert_mean (GROM.c:1205-1318) ---------------- */
@@ -1232,6 +1249,7 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
     optind = 0; /* GNU getopt: full re-initialisation */
     int opt;
     g_1000gen_window = 0;
+    g_fetch_mode = 0;
     /* getopt string of GROM.c:21908 */
     while ((opt = getopt(argc, argv,
                          "Z:W:X:Q:A:Y:B:D:E:K:N:V:U:L:F:SP:c:R:MG:i:r:o:p:q:s:v:g:l:d:b:n:a:y:z:e:fj:k:m:u:w:x:h")) != -1) {
@@ -1276,6 +1294,7 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
         case 'U': g_chr_rd_threshold_factor = atoi(optarg); break;
         case 'L': g_dup_threshold_factor = atol(optarg); break;
         case 'F': g_mapq_factor = atof(optarg); break;
+        case 'P': { const int n = atoi(optarg); g_fetch_mode = n >= 1 && n <= 256; break; } /* GROM.c:21923 */
         case 'h': return 0;
         case '?': return 1;
         default: break; /* options outside this restatement's scope */
@@ -1395,8 +1414,21 @@ int grom_oracle_main(int argc, char **argv, const char *dump_prefix) {
             snprintf(path, sizeof(path), "%s.%s.sv", g_dump_prefix, cname);
             dump_sv = fopen(path, "wb");
         }
-        scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, ctx, dump_cnt, dump_ind,
-                        dump_sv);
+        if (g_fetch_mode) {
+            /* this chromosome's own stream (bam_fetch), from a fresh record */
+            stream_t fst;
+            cur_t fcur;
+            memset(&fcur, 0, sizeof(fcur));
+            if (stream_open(&fst, bam_file_name) != 0) return 1;
+            fst.only_tid = chr_match;
+            scan_chromosome(&fst, &fcur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, ctx, dump_cnt,
+                            dump_ind, dump_sv);
+            bam_free_rec(&fcur.b);
+            stream_close(&fst);
+        } else {
+            scan_chromosome(&st, &cur, target_name, chr_match, chr_fasta, chr_len, cname, vcf, ctx, dump_cnt, dump_ind,
+                            dump_sv);
+        }
         if (dump_cnt) fclose(dump_cnt);
         if (dump_ind) fclose(dump_ind);
         if (dump_sv) fclose(dump_sv);

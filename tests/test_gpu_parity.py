@@ -555,17 +555,49 @@ def test_device_resident_path_matches_host_path():
 def test_sharded_cli_matches_one_gpu(datadir, workers, extra):
     """Chromosomes scanned by several device workers (GROM_WORKER_DEVICES maps
     workers onto this box's one GPU; on an 8-GPU node -P 8 gives one per GPU)
-    give the byte-identical VCF, rows in chromosome order."""
+    give the byte-identical VCF, rows in chromosome order -- the oracle's
+    under the same -P 8 (each chromosome its own records, as the reference's
+    -c children read them)."""
     import grom_amd
     from _util import FILEDATE, SEED
     case = "three_chr" if not extra else "cnv_multi"
     bam, fa = synth(datadir, case, CASES[case])
     tag = f"shard_{workers.replace(',', '')}"
-    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra + ["-P", "8"])
     env = {"GROM_FILEDATE": FILEDATE, "GROM_SEED": SEED, "GROM_WORKER_DEVICES": workers}
     rc = grom_amd.cli_main(["-i", bam, "-r", fa, "-o", f"g_{tag}.vcf", "-P", "8"] + extra, env=env, cwd=str(datadir))
     assert rc == 0, grom_amd.last_error()
     assert open(datadir / f"o_{tag}.vcf").read() == open(datadir / f"g_{tag}.vcf").read()
+
+
+@pytest.mark.parametrize("case,extra", [("three_chr", ["-P", "2"]), ("empty_middle", ["-P", "2"]),
+                                        ("sv", ["-P", "1", "-S"]), ("c3_genome", ["-P", "3", "-M", "-V", "1"])],
+                         ids=["three_chr_P2", "empty_middle_P2", "sv_P1_S", "c3_genome_P3"])
+def test_p_reference_semantics(datadir, case, extra):
+    """GROM -P n: the reference reads every chromosome through bam_fetch
+    (GROM.c:21051-21064; -P n > 1 forks -c children that do the same,
+    549-599), so no chromosome loses the two records at its start that the
+    serial stream consumes (Q1) and an empty chromosome starves nothing (Q21):
+    its rows differ from a serial run's.  The CLI's -P n gives the oracle's -P
+    rows byte for byte (device decode, the host decoder threads and the serial
+    reader); GROM_P_SERIAL=1 keeps the serial stream's rows on n GPUs."""
+    bam, fa = synth(datadir, case, CASES[case])
+    tag = f"pref_{case}{''.join(extra).replace('-', '_')}"
+    run_oracle(datadir, bam, fa, f"o_{tag}.vcf", extra)
+    flags = [x for x in extra if x not in ("-P",) and not x.isdigit()]
+    run_oracle(datadir, bam, fa, f"os_{tag}.vcf", flags)
+    outs = {}
+    for mode, env in (("dev", {}), ("host", {"GROM_DEVICE_DECODE": "0"}), ("serial_reader", {"GROM_SERIAL_DECODE": "1"}),
+                      ("p_serial", {"GROM_P_SERIAL": "1"})):
+        run_grom(datadir, bam, fa, f"g{mode}_{tag}.vcf", extra, env_extra=env)
+        outs[mode] = open(datadir / f"g{mode}_{tag}.vcf").read() + open(datadir / f"g{mode}_{tag}.ctx.vcf").read()
+    want = open(datadir / f"o_{tag}.vcf").read() + open(datadir / f"o_{tag}.ctx.vcf").read()
+    serial = open(datadir / f"os_{tag}.vcf").read() + open(datadir / f"os_{tag}.ctx.vcf").read()
+    for mode in ("dev", "host", "serial_reader"):
+        assert outs[mode] == want, mode
+    assert outs["p_serial"] == serial
+    if case == "empty_middle":  # chr3's rows exist only without Q21's starvation
+        assert "\nchr3\t" in want and "\nchr3\t" not in serial
 
 
 def test_two_contexts_scan_concurrently():

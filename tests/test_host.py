@@ -67,15 +67,23 @@ def parse_meta(path):
     return d
 
 
-@pytest.mark.parametrize("case", ["one_chr", "three_chr", "empty_middle", "lowmapq_clip"])
-def test_stream_plan_matches_oracle_walk(datadir, case):
+@pytest.mark.parametrize("case,extra", [("one_chr", []), ("three_chr", []), ("empty_middle", []), ("lowmapq_clip", []),
+                                        ("three_chr", ["-P", "2"]), ("empty_middle", ["-P", "2"]),
+                                        ("lowmapq_clip", ["-P", "1"])],
+                         ids=["one_chr", "three_chr", "empty_middle", "lowmapq_clip", "three_chr_P2", "empty_middle_P2",
+                              "lowmapq_clip_P1"])
+def test_stream_plan_matches_oracle_walk(datadir, case, extra):
     """The per-chromosome record plan (skip prefix, last base reached) equals what
     the oracle's serial walk did, including the two records lost at every
-    chromosome boundary (Q1) and the empty chromosome swallowing the file (Q21)."""
+    chromosome boundary (Q1) and the empty chromosome swallowing the file (Q21).
+    With -P n each chromosome reads its own records (bam_fetch, GROM.c:21051-
+    21064 / the -c children, 549-599): no Q1 drops, no Q21 starvation, in the
+    CLI and in the oracle alike."""
     bam, fa = synth(datadir, case, CASES[case])
-    dump = str(datadir / f"plan_{case}")
-    run_oracle(datadir, bam, fa, f"plan_{case}.vcf", dump=dump)
-    r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", f"plan_{case}_g.vcf"], str(datadir), {"GROM_PLAN_ONLY": "1"})
+    tag = case + "".join(extra).replace("-", "_")
+    dump = str(datadir / f"plan_{tag}")
+    run_oracle(datadir, bam, fa, f"plan_{tag}.vcf", extra, dump=dump)
+    r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", f"plan_{tag}_g.vcf"] + extra, str(datadir), {"GROM_PLAN_ONLY": "1"})
     plan = parse_plan(r.stdout)
     assert plan, r.stdout
     for name, p in plan.items():
@@ -144,6 +152,35 @@ def test_q21_empty_chromosome_starves_later_ones(datadir):
     plan = parse_plan(r.stdout)
     assert plan["chr1"]["reads"] > 0
     assert plan["chr2"]["reads"] == 0 and plan["chr3"]["reads"] == 0
+
+
+@pytest.mark.parametrize("case", ["three_chr", "empty_middle", "sv", "dups"])
+def test_p_fetch_streamed_matches_serial_reader(datadir, case):
+    """-P n (the reference's per-chromosome bam_fetch input): the streamed
+    decoder and the serial reader hand every chromosome the same input (facts
+    and digests); it differs from the serial stream's exactly at the
+    chromosome boundaries -- no chromosome after the first loses records (Q1)
+    and an empty chromosome starves nothing (Q21); GROM_P_SERIAL=1 restores
+    the serial stream's input."""
+    bam, fa = synth(datadir, case, CASES[case])
+    base = ["-i", bam, "-r", fa, "-o", f"pf_{case}.vcf"]
+    plans = {}
+    for mode, args, env in (("serial", [], {}), ("fetch", ["-P", "2"], {}), ("fetch_reader", ["-P", "2"], {"GROM_SERIAL_DECODE": "1"}),
+                            ("fetch_pieces", ["-P", "2"], {"GROM_PIECE_RECS": "777", "GROM_DECODE_THREADS": "3"}),
+                            ("p_serial", ["-P", "2"], {"GROM_P_SERIAL": "1"})):
+        r = run(GROM_BIN, base + args, str(datadir), dict(env, GROM_PLAN_ONLY="1"))
+        plans[mode] = parse_plan(r.stdout)
+    assert plans["fetch"] and plans["fetch"] == plans["fetch_reader"] == plans["fetch_pieces"]
+    assert plans["p_serial"] == plans["serial"]
+    first = min(plans["serial"], key=lambda n: plans["serial"][n]["tid"])
+    for n, p in plans["fetch"].items():
+        q = plans["serial"][n]
+        if n == first or (case == "empty_middle" and n == "chr2"):
+            assert p == q, (n, p, q)
+        elif case == "empty_middle":
+            assert q["reads"] == 0 and p["reads"] > 0, (n, p, q)  # Q21 in the serial stream only
+        else:
+            assert p["reads"] >= q["reads"] and p != q, (n, p, q)  # the two records Q1 drops
 
 
 def test_fmt_2f_matches_printf():
