@@ -709,6 +709,15 @@ typedef struct {
      * GROM.c:549-599) -- pd_set_fetch_mode; GROM_P_SERIAL=1 keeps the serial
      * stream's input (a one-process run's rows) on n GPUs */
     int fetch;
+    /* -c chr,sub,start,end (GROM.c:21928-21930): one child of a -P n run --
+     * BAM target `one_chrom` alone, read through bam_fetch, its rows to
+     * OUT.<target>-<sub> and its raw CTX rows to OUT.<target>-<sub>.ctx, no
+     * header, no translocation post-pass (the parent concatenates and pairs,
+     * GROM.c:603-624, 22400), the insert statistics from <bam>.mean
+     * (GROM.c:22253-22257).  Whole chromosomes only (start 0, end at or past
+     * the chromosome's end: the children -P n forks without -R). */
+    int one_chrom, sub_child, sub_start, sub_end;
+    char part_name[4096];
 } cli_state;
 
 /* Peak device memory of this process (GROM_VERBOSE): the kernel driver's
@@ -933,6 +942,14 @@ static void finish_outputs(cli_state *S, textbuf *ctx_all) {
         free(g_vcf_segs.p);
         memset(&g_vcf_segs, 0, sizeof(g_vcf_segs));
     }
+    if (S->one_chrom >= 0) { /* -c: the raw CTX rows; the parent pairs them (GROM.c:22400) */
+        FILE *f = fopen(S->ctx_name, "w");
+        if (f) {
+            if (ctx_all->len) fwrite(ctx_all->p, 1, ctx_all->len, f);
+            fclose(f);
+        }
+        return;
+    }
     const char *raw = getenv("GROM_CTX_RAW"); /* the raw CTX rows, for a merge of several ranks' runs */
     if (raw) {
         FILE *f = fopen(raw, "w");
@@ -1040,8 +1057,10 @@ static int run_serial(cli_state *S) {
         }
     FILE *vcf = fopen(S->out_name, "w");
     if (!vcf) { printf("Error opening file %s\n", S->out_name); free(plan); free(order); return 1; }
-    if (P->vcf == 1) header(vcf, S->fasta_name, 0);
-    else tab_header(vcf, P);
+    if (S->one_chrom < 0) { /* (-c: rows only, the parent wrote the header) */
+        if (P->vcf == 1) header(vcf, S->fasta_name, 0);
+        else tab_header(vcf, P);
+    }
     /* one serial pass over the records, split per chromosome (stream.h);
      * finished chromosomes go to the GPU workers, rows are written in order */
     if (bgzf_open_read(&br, S->bam_name) != 0) { fclose(vcf); free(plan); free(order); return 1; }
@@ -1320,7 +1339,7 @@ static int run_streamed(cli_state *S) {
     long g_mapped = 0;
     char mean_name[4096];
     snprintf(mean_name, sizeof(mean_name), "%s.mean", S->bam_name);
-    if (getenv("GROM_CHROMS") && !g_plan_only) {
+    if ((getenv("GROM_CHROMS") || S->one_chrom >= 0) && !g_plan_only) {
         FILE *mf = fopen(mean_name, "r");
         if (mf) {
             given = fscanf(mf, "%d %d %d %d %ld", &g_mean, &g_lseq, &g_min, &g_max, &g_mapped) == 5 && g_mean > 0;
@@ -1413,8 +1432,10 @@ static int run_streamed(cli_state *S) {
     t_ctx = clock_gettime_s();
     vcf = fopen(S->out_name, "w");
     if (!vcf) { printf("Error opening file %s\n", S->out_name); status = 1; goto done; }
-    if (P->vcf == 1) header(vcf, S->fasta_name, 0);
-    else tab_header(vcf, P);
+    if (S->one_chrom < 0) { /* (-c: rows only, the parent wrote the header) */
+        if (P->vcf == 1) header(vcf, S->fasta_name, 0);
+        else tab_header(vcf, P);
+    }
     /* the order chromosomes are taken in: the device decoder's (longest
      * first), else BAM order; rows are written in BAM order either way */
     qord = malloc(sizeof(int) * (n_plan > 0 ? n_plan : 1));
@@ -1609,6 +1630,8 @@ static int cli_run(int argc, char **argv, int force_serial) {
     S->num_sd = 3;
     S->verbose = getenv("GROM_VERBOSE") != NULL;
     S->n_dev = 1;
+    S->one_chrom = -1;
+    S->sub_end = 300000000; /* MAX_REGION, GROM.c:78 */
     if (getenv("GROM_DEVICE")) S->device = atoi(getenv("GROM_DEVICE"));
     int opt, ret = 1;
     /* getopt string of GROM.c:21908 */
@@ -1632,6 +1655,10 @@ static int cli_run(int argc, char **argv, int force_serial) {
         case 'a': P->min_snv_ratio = atof(optarg); break;
         case 'f': P->vcf = 0; break;
         case 'x': P->min_ave_bq = atof(optarg); break;
+        case 'c':
+            if (sscanf(optarg, "%d,%d,%d,%d", &S->one_chrom, &S->sub_child, &S->sub_start, &S->sub_end) < 1)
+                S->one_chrom = -1;
+            break;
         case 'P': { /* -P processes -> GPUs; 0 or beyond 256: serial, one GPU (GROM.c:21923-21927) */
             const int n = atoi(optarg);
             const char *ps = getenv("GROM_P_SERIAL");
@@ -1688,7 +1715,17 @@ static int cli_run(int argc, char **argv, int force_serial) {
     }
     if (!bai_loads(S->bam_name)) { printf("Could not open BAM indexing file\n"); goto out_hdr; }
     if (!S->out_name) { printf("ERROR: No output file specified.\n"); goto out_hdr; }
-    {
+    if (S->one_chrom >= 0) {
+        if (S->one_chrom >= S->hdr.n_ref) { printf("ERROR: -c %d: the BAM has %d targets\n", S->one_chrom, S->hdr.n_ref); goto out_hdr; }
+        if (S->sub_start != 0) {
+            printf("ERROR: -c with a sub-region (start %d): only whole-chromosome children are supported (-R is not)\n",
+                   S->sub_start);
+            goto out_hdr;
+        }
+        S->fetch = 1; /* g_parallel_mode = 1, GROM.c:22104 */
+        snprintf(S->part_name, sizeof(S->part_name), "%s.%s-%d", S->out_name, S->hdr.ref_name[S->one_chrom], S->sub_child);
+        S->out_name = S->part_name;
+    } else {
         FILE *probe = fopen(S->out_name, "w");
         if (!probe) { printf("\nCould not open %s\n", S->out_name); goto out_hdr; }
         fclose(probe);
@@ -1721,6 +1758,10 @@ static int cli_run(int argc, char **argv, int force_serial) {
     long *fi_len = calloc(S->fa.n > 0 ? S->fa.n : 1, sizeof(long));
     int n_fi = 0;
     for (int t = 0; t < S->hdr.n_ref; t++) {
+        if (S->one_chrom >= 0 && t != S->one_chrom) { /* -c: loop_start = g_one_chromosome, GROM.c:20821 */
+            fi_of[t] = -1;
+            continue;
+        }
         int fi = grom_match_target(&S->fa, S->hdr.ref_name[t]);
         char lc[GROM_MAX_CHR_NAMES];
         int bl = grom_target_name_lc(S->hdr.ref_name[t], lc, (int)sizeof(lc));
@@ -1742,6 +1783,12 @@ static int cli_run(int argc, char **argv, int force_serial) {
         const int fi = fi_of[t];
         if (fi < 0) continue;
         long len = fi_len[fi];
+        if (S->one_chrom >= 0 && len > S->sub_end) {
+            printf("ERROR: -c region end %d is inside the chromosome (%ld bases): -R sub-regions are not supported\n",
+                   S->sub_end, len);
+            free(fi_of); free(fi_list); free(fi_len);
+            goto out_hdr;
+        }
         /* count_discordant_pairs re-derives the BAM target from the FASTA name
          * (GROM.c:1894-1961): the first target matching it */
         int32_t tid2 = -1;
@@ -1761,7 +1808,9 @@ static int cli_run(int argc, char **argv, int force_serial) {
     S->t_cand = clock_gettime_s();
     {
         size_t ol = strlen(S->out_name);
-        if (ol > 4 && strcmp(S->out_name + ol - 4, ".vcf") == 0)
+        if (S->one_chrom >= 0) /* the child's partial CTX file, GROM.c:20686 */
+            snprintf(S->ctx_name, sizeof(S->ctx_name), "%s.ctx", S->out_name);
+        else if (ol > 4 && strcmp(S->out_name + ol - 4, ".vcf") == 0)
             snprintf(S->ctx_name, sizeof(S->ctx_name), "%.*s.ctx.vcf", (int)(ol - 4), S->out_name);
         else
             snprintf(S->ctx_name, sizeof(S->ctx_name), "%s.ctx", S->out_name);

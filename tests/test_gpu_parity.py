@@ -598,6 +598,21 @@ def test_p_reference_semantics(datadir, case, extra):
     assert outs["p_serial"] == serial
     if case == "empty_middle":  # chr3's rows exist only without Q21's starvation
         assert "\nchr3\t" in want and "\nchr3\t" not in serial
+    if case == "three_chr":
+        # the -c children -P n forks (GROM.c:549-599): target t alone, rows to
+        # OUT.<target>-0 and raw CTX rows to OUT.<target>-0.ctx; the parent's
+        # header followed by the children's rows in target order is -P's VCF
+        import grom_amd
+        base = f"c_{tag}.vcf"
+        parts = []
+        for t, name in enumerate(["chr1", "chr2", "chr3"]):
+            run_grom(datadir, bam, fa, base, ["-c", f"{t},0,0,300000000"])
+            parts.append(open(datadir / f"{base}.{name}-0").read())
+            assert os.path.exists(datadir / f"{base}.{name}-0.ctx")
+        got = open(datadir / f"gdev_{tag}.vcf").read()
+        hdr = "".join(l for l in got.splitlines(keepends=True) if l.startswith("#"))
+        assert hdr + "".join(parts) == got
+        assert not os.path.exists(datadir / base)  # a child writes no full results file
 
 
 def test_two_contexts_scan_concurrently():

@@ -457,3 +457,25 @@ def test_block_table_in_chunks(tmp_path):
             off += used.value
             ob += cb.value
         assert got == ref, size
+
+
+def test_c_child_plans_match_p(datadir):
+    """-c t,0,0,end (the child -P n forks per chromosome, GROM.c:549-599,
+    21928-21930): target t alone, with the same bam_fetch input -P gives it;
+    partial outputs OUT.<target>-0 (+ .ctx) and no full results file; a
+    sub-region (-R) child is refused."""
+    case = "three_chr"
+    bam, fa = synth(datadir, case, CASES[case])
+    p = parse_plan(run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "cp.vcf", "-P", "2"], str(datadir),
+                       {"GROM_PLAN_ONLY": "1"}).stdout)
+    for t, name in enumerate(["chr1", "chr2", "chr3"]):
+        r = run(GROM_BIN, ["-i", bam, "-r", fa, "-o", "cc.vcf", "-c", f"{t},0,0,300000000"], str(datadir),
+                {"GROM_PLAN_ONLY": "1"})
+        got = parse_plan(r.stdout)
+        assert got == {name: p[name]}, (t, got)
+        assert os.path.exists(os.path.join(str(datadir), f"cc.vcf.{name}-0.ctx"))
+    assert not os.path.exists(os.path.join(str(datadir), "cc.vcf"))
+    import subprocess
+    r = subprocess.run([GROM_BIN, "-i", bam, "-r", fa, "-o", "cr.vcf", "-c", "1,1,100000,200000"], cwd=str(datadir),
+                       capture_output=True, text=True, env=dict(os.environ, GROM_PLAN_ONLY="1"))
+    assert r.returncode != 0 and "sub-region" in r.stdout
