@@ -34,19 +34,25 @@
 // bit 1 in *bounds (a block table that does not belong to the compressed
 // slot or the piece is an error the host reports, never a wild access).
 #define GI_E_BOUNDS 8
+__device__ __forceinline__ bool dd_blk_inb(const DdBlock &b, int64_t o, int64_t comp_cap, int64_t out_cap) {
+    return b.in_off >= 0 && b.in_off + (int64_t)b.in_len <= comp_cap && o >= 0 && b.out_len <= 65536u &&
+           o + (int64_t)b.out_len <= out_cap;
+}
+
+// only_tokcap: the fallback launch of the two-phase inflate -- only the
+// blocks phase 1 refused for their token count (status GI_E_TOKCAP)
 __global__ void __launch_bounds__(DD_LANES, 2) k_inflate(const uint8_t *__restrict__ comp, int64_t comp_cap,
                                                       const DdBlock *__restrict__ blk, int64_t n_blk,
                                                       uint8_t *__restrict__ out, int64_t out_base, int64_t out_cap,
                                                       uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad,
-                                                      uint32_t *__restrict__ bounds) {
+                                                      uint32_t *__restrict__ bounds, int only_tokcap) {
     extern __shared__ uint32_t dd_tab[];  // GI_LANE_DWORDS x DD_LANES: rows element-major across the lanes
     const int64_t j = (int64_t)blockIdx.x * DD_LANES + threadIdx.x;
     if (j >= n_blk) return;
+    if (only_tokcap && status[j] != (uint8_t)GI_E_TOKCAP) return;
     const DdBlock b = blk[j];
     const int64_t o = b.out_off - out_base;
-    const bool inb = b.in_off >= 0 && b.in_off + (int64_t)b.in_len <= comp_cap && o >= 0 && b.out_len <= 65536u &&
-                     o + (int64_t)b.out_len <= out_cap;
-    if (!inb) {
+    if (!dd_blk_inb(b, o, comp_cap, out_cap)) {
         status[j] = (uint8_t)GI_E_BOUNDS;
         atomicAdd(n_bad, 1u);
         atomicOr(bounds, 1u);
@@ -57,16 +63,179 @@ __global__ void __launch_bounds__(DD_LANES, 2) k_inflate(const uint8_t *__restri
     if (rc) atomicAdd(n_bad, 1u);
 }
 
+// Phase 1 of the two-phase inflate (inflate.h, gi_tokens): one block per
+// lane, its tokens to tok + j * tokcap, their count to ntok[j], its literals
+// packed at the front of its output region.  A block over the token cap is
+// left for the fallback launch (status GI_E_TOKCAP, not counted as bad).
+__global__ void __launch_bounds__(DD_LANES, 2) k_huff(const uint8_t *__restrict__ comp, int64_t comp_cap,
+                                                   const DdBlock *__restrict__ blk, int64_t n_blk,
+                                                   uint8_t *__restrict__ out, int64_t out_base, int64_t out_cap,
+                                                   uint32_t *__restrict__ tok, uint32_t *__restrict__ ntok,
+                                                   uint32_t tokcap, uint8_t *__restrict__ status,
+                                                   uint32_t *__restrict__ n_bad, uint32_t *__restrict__ bounds) {
+    extern __shared__ uint32_t dd_tab[];
+    const int64_t j = (int64_t)blockIdx.x * DD_LANES + threadIdx.x;
+    if (j >= n_blk) return;
+    const DdBlock b = blk[j];
+    const int64_t o = b.out_off - out_base;
+    if (!dd_blk_inb(b, o, comp_cap, out_cap)) {
+        status[j] = (uint8_t)GI_E_BOUNDS;
+        atomicAdd(n_bad, 1u);
+        atomicOr(bounds, 1u);
+        return;
+    }
+    const int rc = gi_tokens<DD_LANES>(comp + b.in_off, b.in_len, out + o, b.out_len, tok + (size_t)j * tokcap, tokcap,
+                                       ntok + j, dd_tab, threadIdx.x);
+    status[j] = (uint8_t)rc;
+    if (rc && rc != GI_E_TOKCAP) atomicAdd(n_bad, 1u);
+}
+
+// Phase 2: one wave per block (GROM_LZ_LANE=1: one lane per block, gi_lz).
+// One lane per block put ~10^5 blocks' recent output in flight at once and
+// the match sources (half of them 256-1024 bytes back) fell out of L2
+// (26 ms for 140 k blocks); a wave per block keeps a block's last few KB
+// hot in its CU.  Tokens are taken 64 at a time: a prefix sum places each
+// token's literals (already in place) and match, then the matches copy in
+// rounds: a match copies once no unresolved match of the group writes into
+// its source (the first round: sources below the group's lowest unresolved
+// match; the lowest one always qualifies, its own overlap handled by
+// gi_match's doubling).  Lanes of one wave share the CU's L1, so a round's
+// stores are visible to the next round's loads after a workgroup-scope
+// release/acquire (a wait for the stores).
+__device__ __forceinline__ uint32_t lz_wave_incl(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t lz_wave_min(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
+
+__global__ void __launch_bounds__(64) k_lz77(const DdBlock *__restrict__ blk, int64_t n_blk, uint8_t *__restrict__ out,
+                                             int64_t out_base, const uint32_t *__restrict__ tok,
+                                             const uint32_t *__restrict__ ntok, uint32_t tokcap,
+                                             uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad) {
+    const int64_t j = blockIdx.x;
+    if (j >= n_blk || status[j] != 0) return;  // (uniform: one wave per block)
+    const int lane = threadIdx.x;
+    const DdBlock b = blk[j];
+    uint8_t *dst = out + (b.out_off - out_base);
+    const uint32_t n = ntok[j], olen = b.out_len;
+    const uint32_t *tk = tok + (size_t)j * tokcap;
+    uint32_t obase = 0;
+    bool bad = false;
+    for (uint32_t c0 = 0; c0 < n && !bad; c0 += 64) {
+        const uint32_t k = c0 + (uint32_t)lane;
+        const uint32_t t = k < n ? tk[k] : GI_TOK_LITONLY;
+        const bool hm = !(t & GI_TOK_LITONLY);
+        const uint32_t lc = t & 255u, len = hm ? ((t >> 8) & 255u) + 3u : 0u, d = ((t >> 16) & 0x7fffu) + 1u;
+        const uint32_t span = lc + len;
+        const uint32_t inc = lz_wave_incl(span, lane);
+        const uint32_t m = obase + inc - len;  // the match's first byte
+        obase += __shfl(inc, 63, 64);
+        bool pend = hm;
+        if (__any((hm && d > m) || obase > olen)) {  // (phase 1 checked these: a wrong table or token area)
+            bad = true;
+            break;
+        }
+        const uint32_t src = m - d, se = src + (len < d ? len : d);
+        for (;;) {
+            const uint64_t pm = __ballot(pend);
+            if (pm == 0) break;
+            const uint32_t P = lz_wave_min(pend ? m : 0xffffffffu);
+            bool ready = pend && se <= P;
+            if (__ballot(ready) != pm) {
+                // the rest: blocked only by a pending match that writes into the source
+                bool blocked = false;
+                for (uint64_t q = pm; q; q &= q - 1) {
+                    const int jl = __builtin_ctzll(q);
+                    const uint32_t mj = __builtin_amdgcn_readlane(m, jl);
+                    const uint32_t ej = mj + __builtin_amdgcn_readlane(len, jl);
+                    blocked = blocked || (mj < se && ej > src);
+                }
+                ready = pend && !blocked;
+            }
+            if (ready) {
+                gi_match(dst, m, len, d);
+                pend = false;
+            }
+            // this round's stores before the next round's loads (one CU, one L1)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+    }
+    if (lane == 0 && (bad || obase != olen)) {
+        status[j] = (uint8_t)GI_E_SIZE;
+        atomicAdd(n_bad, 1u);
+    }
+}
+
+// the one-lane-per-block variant (GROM_LZ_LANE=1)
+__global__ void __launch_bounds__(DD_LANES) k_lz77_lane(const DdBlock *__restrict__ blk, int64_t n_blk,
+                                                        uint8_t *__restrict__ out, int64_t out_base,
+                                                        const uint32_t *__restrict__ tok,
+                                                        const uint32_t *__restrict__ ntok, uint32_t tokcap,
+                                                        uint8_t *__restrict__ status, uint32_t *__restrict__ n_bad) {
+    const int64_t j = (int64_t)blockIdx.x * DD_LANES + threadIdx.x;
+    if (j >= n_blk || status[j] != 0) return;
+    const DdBlock b = blk[j];
+    const int rc = gi_lz(tok + (size_t)j * tokcap, ntok[j], out + (b.out_off - out_base), b.out_len);
+    if (rc) {
+        status[j] = (uint8_t)rc;
+        atomicAdd(n_bad, 1u);
+    }
+}
+
+// tokens per block of the two-phase inflate (GROM_INFLATE_TOKCAP, a multiple
+// of 4; 0: the one-phase k_inflate alone)
+static uint32_t dd_tokcap() {
+    static const uint32_t cap = [] {
+        const char *e = getenv("GROM_INFLATE_TOKCAP");
+        long v = e ? atol(e) : 0;
+        if (v < 0) v = 0;
+        if (v > 65536) v = 65536;
+        return (uint32_t)(v & ~3L);
+    }();
+    return cap;
+}
+
+// bytes of the token buffer the two-phase inflate of n_blk blocks needs (0: one-phase)
+extern "C" size_t dd_inflate_tok_bytes(int64_t n_blk) {
+    const uint32_t cap = dd_tokcap();
+    return cap ? (size_t)n_blk * ((size_t)cap + 1) * 4 + 64 : 0;
+}
+
 extern "C" int dd_inflate_launch(hipStream_t st, const uint8_t *d_comp, int64_t comp_cap, const DdBlock *d_blk,
                                  int64_t n_blk, uint8_t *d_out, int64_t out_base, int64_t out_cap, uint8_t *d_status,
-                                 uint32_t *d_bad, uint32_t *d_bounds) {
+                                 uint32_t *d_bad, uint32_t *d_bounds, uint32_t *d_tok, size_t tok_bytes) {
     if (n_blk <= 0) return 0;
     const unsigned grid = (unsigned)((n_blk + DD_LANES - 1) / DD_LANES);
     // GROM_INFLATE_LDS_PAD (probe only): extra LDS bytes per wave, to measure
     // how the kernel's speed follows its occupancy
     static const int pad = getenv("GROM_INFLATE_LDS_PAD") ? atoi(getenv("GROM_INFLATE_LDS_PAD")) : 0;
+    const uint32_t cap = dd_tokcap();
+    if (cap == 0 || d_tok == nullptr || tok_bytes < dd_inflate_tok_bytes(n_blk)) {
+        hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES + pad, st, d_comp, comp_cap,
+                           d_blk, n_blk, d_out, out_base, out_cap, d_status, d_bad, d_bounds, 0);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    uint32_t *ntok = d_tok + (size_t)n_blk * cap;
+    hipLaunchKernelGGL(k_huff, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES + pad, st, d_comp, comp_cap, d_blk,
+                       n_blk, d_out, out_base, out_cap, d_tok, ntok, cap, d_status, d_bad, d_bounds);
+    static const bool lane_lz = getenv("GROM_LZ_LANE") && atoi(getenv("GROM_LZ_LANE")) != 0;
+    if (lane_lz)
+        hipLaunchKernelGGL(k_lz77_lane, dim3(grid), dim3(DD_LANES), 0, st, d_blk, n_blk, d_out, out_base, d_tok, ntok,
+                           cap, d_status, d_bad);
+    else
+        hipLaunchKernelGGL(k_lz77, dim3((unsigned)n_blk), dim3(64), 0, st, d_blk, n_blk, d_out, out_base, d_tok, ntok,
+                           cap, d_status, d_bad);
     hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(DD_LANES), GI_LANE_BYTES * DD_LANES + pad, st, d_comp, comp_cap,
-                       d_blk, n_blk, d_out, out_base, out_cap, d_status, d_bad, d_bounds);
+                       d_blk, n_blk, d_out, out_base, out_cap, d_status, d_bad, d_bounds, 1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -162,13 +331,15 @@ extern "C" int64_t grom_inflate_device_selftest(const char *bam_path, int device
     if (hipSetDevice(device) != hipSuccess) return -3;
     uint8_t *d_comp = nullptr, *d_out = nullptr, *d_status = nullptr;
     DdBlock *d_blk = nullptr;
-    uint32_t *d_bad = nullptr;
+    uint32_t *d_bad = nullptr, *d_tok = nullptr;
+    const size_t tok_bytes = dd_inflate_tok_bytes(nb);
     int64_t bad = -4;
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipMalloc(&d_comp, (size_t)used + 64) != hipSuccess || hipMalloc(&d_out, (size_t)ob + 64) != hipSuccess ||
         hipMalloc(&d_status, (size_t)nb + 1) != hipSuccess || hipMalloc(&d_blk, sizeof(DdBlock) * (size_t)(nb + 1)) != hipSuccess ||
-        hipMalloc(&d_bad, 8) != hipSuccess || hipStreamCreate(&st) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipMalloc(&d_bad, 8) != hipSuccess || (tok_bytes && hipMalloc(&d_tok, tok_bytes) != hipSuccess) ||
+        hipStreamCreate(&st) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
         hipEventCreate(&e1) != hipSuccess)
         goto done;
     {
@@ -178,7 +349,8 @@ extern "C" int64_t grom_inflate_device_selftest(const char *bam_path, int device
         // a warm launch, then the timed one
         for (int rep = 0; rep < 2; rep++) {
             (void)hipEventRecord(e0, st);
-            if (dd_inflate_launch(st, d_comp, used + 64, d_blk, nb, d_out, 0, ob + 64, d_status, d_bad, d_bad + 1))
+            if (dd_inflate_launch(st, d_comp, used + 64, d_blk, nb, d_out, 0, ob + 64, d_status, d_bad, d_bad + 1, d_tok,
+                                  tok_bytes))
                 goto done;
             (void)hipEventRecord(e1, st);
         }
@@ -224,6 +396,7 @@ done:
     (void)hipFree(d_status);
     (void)hipFree(d_blk);
     (void)hipFree(d_bad);
+    (void)hipFree(d_tok);
     return bad;
 }
 
@@ -1076,6 +1249,7 @@ __global__ void k_lower_bound(const int32_t *a, int64_t n, int32_t x, int64_t *o
 // parses run k on the context's stream)
 struct RunSlot {
     DBuf U, blk, status, misc, S, ccnt, cbase, off, tmp;  // (blk, S: unused by the piece decode)
+    DBuf tok;  // the two-phase inflate's tokens and per-block counts (dd_inflate_tok_bytes)
     hipStream_t st = nullptr;
     hipEvent_t ev[3] = {};
     int64_t *h_small = nullptr;  // pinned, mapped: k_piece_summary writes it
@@ -1125,10 +1299,12 @@ struct dd_ctx {
     DBuf nml, nmo, nm, nmoff;  // per piece record: name length, its offset; per chromosome: name bytes, offsets
     // inflated bytes per piece (GROM_DD_PIECE_MB): a launch of k_inflate takes
     // at least the time one lane needs for one block, so a piece must hold a
-    // good part of a chip's worth of blocks (two pieces are in flight): 2 GB
-    // is ~32 k blocks, ~500 waves (1 GB pieces made the inflate 2.7x slower;
-    // 2 GB ran as fast as 3 GB and saves 3 GB of HBM, profiles/r05r)
-    int64_t piece_bytes = (int64_t)2 << 30;
+    // good part of a chip's worth of blocks (two pieces are in flight): 3 GB
+    // is ~48 k blocks, ~750 waves.  Round 5 measured 2 GB as fast as 3 GB
+    // (profiles/r05r) while the one FASTA loader thread set the run's pace;
+    // with that fixed, 3 GB pieces cut the inflate's event time 1.88 ->
+    // 1.49 s and the run 3.8 -> 3.55 s for 3 GB more HBM (profiles/r06g, r06i)
+    int64_t piece_bytes = (int64_t)3 << 30;
     std::vector<uint8_t> aux_bytes;  // the last run's split-read candidates (dd_parse_out)
     std::vector<int64_t> aux_off, aux_kidx;
     int64_t *h_small = nullptr;  // pinned: totals and scalars
@@ -1270,7 +1446,7 @@ extern "C" void dd_ctx_free(dd_ctx *c) {
         if (c->pev[k]) (void)hipEventDestroy(c->pev[k]);
         RunSlot &r = c->rs[k];
         if (r.st) (void)hipStreamSynchronize(r.st);
-        DBuf *rb[] = {&r.U, &r.blk, &r.status, &r.misc, &r.S, &r.ccnt, &r.cbase, &r.off, &r.tmp};
+        DBuf *rb[] = {&r.U, &r.blk, &r.status, &r.misc, &r.S, &r.ccnt, &r.cbase, &r.off, &r.tmp, &r.tok};
         for (DBuf *b : rb)
             if (b->p) grom_dev_free(b->p, b->cap, GROM_DEVCAT_DECODE);
         for (int e = 0; e < 3; e++)
@@ -1336,6 +1512,9 @@ extern "C" int dd_reserve(dd_ctx *c, int64_t span, int64_t ubytes, int64_t recs,
         RunSlot &r = c->rs[k];
         DGROW(r.U, (size_t)pb + 64);
         DGROW(r.status, (size_t)(pb / 16384 + 1024));
+        // (a piece's blocks: at most ~pb / 32 KiB, BGZF writers fill blocks to
+        // ~64 KiB; a piece beyond the estimate grows it in issue_piece)
+        if (dd_inflate_tok_bytes(1)) DGROW(r.tok, dd_inflate_tok_bytes(pb / 60000 + 64));
         DGROW(r.misc, 256);
         DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(n_starts + 1));
         DGROW(r.cbase, sizeof(uint32_t) * (size_t)(n_starts + 1));
@@ -1601,6 +1780,7 @@ static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, d
     DCK(hipStreamWaitEvent(ls, c->cev[q->slot], 0));
     DGROW(r.U, (size_t)pc.pbytes + 64);
     DGROW(r.status, (size_t)(pc.bl - pc.bf + 2));
+    if (dd_inflate_tok_bytes(1)) DGROW(r.tok, dd_inflate_tok_bytes(pc.bl - pc.bf + 1));
     DGROW(r.ccnt, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
     DGROW(r.cbase, sizeof(uint32_t) * (size_t)(pc.cb - pc.ca + 1));
     DGROW(r.misc, 256);
@@ -1612,7 +1792,8 @@ static int issue_piece(dd_ctx *c, const dd_run_req *q, const Piece &pc, int k, d
     r.misc_clean = true;
     DCK(hipEventRecord(r.ev[0], ls));
     if (dd_inflate_launch(ls, P<uint8_t>(c->dcomp[q->slot]), q->comp_len, P<DdBlock>(c->rblk[q->slot]) + pc.bf,
-                          pc.bl - pc.bf + 1, P<uint8_t>(r.U), pc.base, pc.pbytes, P<uint8_t>(r.status), rb + 1, rb + 5)) {
+                          pc.bl - pc.bf + 1, P<uint8_t>(r.U), pc.base, pc.pbytes, P<uint8_t>(r.status), rb + 1, rb + 5,
+                          P<uint32_t>(r.tok), r.tok.cap)) {
         if (err) snprintf(err, (size_t)errlen, "inflate launch failed");
         return -1;
     }

@@ -21,6 +21,7 @@
 #include <signal.h>
 #include <time.h>
 #include <unistd.h>
+#include <sys/mman.h>
 
 #include "../../include/grom_amd.h"
 #include "bamio.h"
@@ -1173,26 +1174,53 @@ typedef struct {
     int n_plan;
     pthread_mutex_t mu;
     pthread_cond_t cv;
-    int loaded, consumed, stop; /* refs loaded ahead of the consumer, at most `ahead` */
+    int loaded, consumed, stop; /* refs loaded (a prefix of the plan) ahead of the consumer, at most `ahead` */
     int ahead;
+    int next;         /* the next chromosome a loader thread takes */
+    char *done;       /* per chromosome: its reference is loaded */
 } fasta_feed;
 
+#define FASTA_THREADS_MAX 8
+
+/* A chromosome's reference buffer: 2 MB aligned and advised for huge pages,
+ * so the first touch of a 250 MB chromosome is ~125 faults instead of ~61 k
+ * (half of a single thread's load time went to page faults) */
+static char *ref_alloc(long len) {
+    const size_t huge = (size_t)2 << 20, n = ((size_t)len + 1 + huge - 1) / huge * huge;
+    void *p = NULL;
+    if (posix_memalign(&p, huge, n) != 0) return NULL;
+#ifdef MADV_HUGEPAGE
+    (void)madvise(p, n, MADV_HUGEPAGE);
+#endif
+    return (char *)p;
+}
+
 /* find_disc_svs loads each chromosome in order (GROM.c:21009-21045); here a
- * thread does it ahead of the scans */
+ * few threads do it ahead of the scans (one thread at ~0.9 GB/s of FASTA was
+ * slower than the GPU decode: the whole run waited on it), each taking the
+ * next chromosome of the plan; `loaded` counts the plan's loaded prefix */
 static void *fasta_main(void *arg) {
     fasta_feed *F = (fasta_feed *)arg;
-    for (int k = 0; k < F->n_plan; k++) {
+    for (;;) {
         pthread_mutex_lock(&F->mu);
-        while (!F->stop && k >= F->consumed + F->ahead) pthread_cond_wait(&F->cv, &F->mu);
-        const int stop = F->stop;
+        const int k = F->next;
+        if (k < F->n_plan) F->next++;
+        while (!F->stop && k < F->n_plan && k >= F->consumed + F->ahead) pthread_cond_wait(&F->cv, &F->mu);
+        const int stop = F->stop || k >= F->n_plan;
         pthread_mutex_unlock(&F->mu);
         if (stop) break;
         chrom_plan *c = F->plan[k];
-        c->ref = malloc(c->len + 1);
-        if (c->ref && grom_fasta_load_at(&F->S->fa, c->fasta_idx, c->ref, c->len) < 0)
+        c->ref = ref_alloc(c->len);
+        if (c->ref && grom_fasta_load_at(&F->S->fa, c->fasta_idx, c->ref, c->len) < 0) {
+            /* (the shared-stream loader: one thread at a time) */
+            static pthread_mutex_t fmu = PTHREAD_MUTEX_INITIALIZER;
+            pthread_mutex_lock(&fmu);
             grom_fasta_load(&F->S->fa, c->fasta_idx, c->ref, c->len);
+            pthread_mutex_unlock(&fmu);
+        }
         pthread_mutex_lock(&F->mu);
-        F->loaded = k + 1;
+        F->done[k] = 1;
+        while (F->loaded < F->n_plan && F->done[F->loaded]) F->loaded++;
         pthread_cond_broadcast(&F->cv);
         pthread_mutex_unlock(&F->mu);
     }
@@ -1423,8 +1451,8 @@ static int run_streamed(cli_state *S) {
     chrom_plan **qplan = NULL;
     fasta_feed F;
     memset(&F, 0, sizeof(F));
-    pthread_t fthr;
-    int fasta_started = 0;
+    pthread_t fthr[FASTA_THREADS_MAX];
+    int fasta_started = 0, n_fthr = 0;
     double t_ctx = 0.0;
     if (ws_fail) { status = 1; goto done; }
     for (int d = 0; d < S->n_init; d++)
@@ -1456,10 +1484,24 @@ static int run_streamed(cli_state *S) {
     F.S = S;
     F.plan = qplan;
     F.n_plan = g_plan_only ? 0 : n_plan;
-    F.ahead = 3;
+    F.ahead = 4;
+    F.done = calloc((size_t)(n_plan > 0 ? n_plan : 1), 1);
     pthread_mutex_init(&F.mu, NULL);
     pthread_cond_init(&F.cv, NULL);
-    pthread_create(&fthr, NULL, fasta_main, &F);
+    /* GROM_FASTA_THREADS (default 3) */
+    n_fthr = getenv("GROM_FASTA_THREADS") ? atoi(getenv("GROM_FASTA_THREADS")) : 3;
+    if (n_fthr < 1) n_fthr = 1;
+    if (n_fthr > FASTA_THREADS_MAX) n_fthr = FASTA_THREADS_MAX;
+    for (int t = 0; t < n_fthr; t++)
+        if (pthread_create(&fthr[t], NULL, fasta_main, &F) != 0) {
+            n_fthr = t;
+            break;
+        }
+    if (n_fthr == 0) {
+        fprintf(stderr, "grom: no FASTA loader thread\n");
+        status = 1;
+        goto done;
+    }
     fasta_started = 1;
     /* (plan-only: the workers print each chromosome's plan line, so the host
      * tests run the pool beside the streamed decoder) */
@@ -1511,13 +1553,14 @@ done:
         F.stop = 1;
         pthread_cond_broadcast(&F.cv);
         pthread_mutex_unlock(&F.mu);
-        pthread_join(fthr, NULL);
+        for (int t = 0; t < n_fthr; t++) pthread_join(fthr[t], NULL);
         /* references loaded but never handed to a worker are freed with the
          * plan at the end of cli_run, after the workers are joined (a worker
          * frees its own job's reference when its scan ends) */
         pthread_mutex_destroy(&F.mu);
         pthread_cond_destroy(&F.cv);
     }
+    free(F.done);
     const double t_loop = clock_gettime_s();
     if (started) pool_finish(&pool, S, workers, tids, &next_write, vcf, &ctx_all, &status);
     if (!fallback && status == 0 && S->verbose) {

@@ -868,3 +868,241 @@ GI_FN int gi_inflate(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t 
     if (o != out_len) return GI_E_SIZE;
     return GI_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Two-phase inflate (round 6).  gi_inflate above copies every match from the
+// block's own output in global memory inside the decode loop: the match's
+// loads are an L2 round trip on the lane's chain (its stores before them
+// must land first: one in-order memory counter), and a wave carries the
+// union of the header, symbol and copy paths every trip.  Split:
+//   phase 1 (gi_tokens, one block per lane, LDS code tables): the Huffman
+//     decode alone.  Literals go to their final places in the block's output
+//     (8-byte groups, as gi_inflate's); each match becomes a 32-bit token in
+//     the block's token area; no output byte is read back.
+//   phase 2 (gi_lz, one block per lane, no LDS, few registers: a full chip
+//     of waves): the tokens replayed -- each match copied from the output
+//     before it, 16-byte pieces, the match's last piece cut to its bytes so
+//     the literals already in place after it are never touched.
+// Token: bits 0-7 the literals before it (lc), bit 31 set: literals only
+// (the block's last token, or a run of 255), else bits 8-15 the match length
+// - 3 and bits 16-30 its distance - 1.  A block with more than `tokcap`
+// tokens is GI_E_TOKCAP: the caller inflates it with gi_inflate instead.
+// ---------------------------------------------------------------------------
+enum { GI_E_TOKCAP = 9 };
+#define GI_TOK_LITONLY 0x80000000u
+
+template <int LANES>
+GI_FN int gi_tokens(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len, uint32_t *tok, uint32_t tokcap,
+                    uint32_t *ntok, uint32_t *tab, int lane) {
+    typedef uint32_t gi_u32x4 __attribute__((vector_size(16)));
+    GiBits b;
+    gi_open(b, in);
+    GiHuff lit_h = {}, dist_h = {};
+    GiHdr H = {};
+    uint32_t o = 0, bfinal = 0, rem = 0;
+    uint64_t pend = 0;   // literals not yet stored: the output bytes [o - pn, o)
+    uint32_t pn = 0;
+    uint32_t lc = 0;     // literals since the last token
+    uint32_t nt = 0;     // tokens so far
+    gi_u32x4 tv = {};    // the current group of four tokens, oldest in [0] once full
+    int mode = GI_M_HDR, rc = GI_OK;
+    // one token into the group; a full group leaves as one 16-byte store
+    auto emit = [&](uint32_t t) -> bool {
+        if (nt >= tokcap) return false;
+        tv = (gi_u32x4){tv[1], tv[2], tv[3], t};
+        nt++;
+        if ((nt & 3u) == 0) __builtin_memcpy(tok + (nt - 4), &tv, 16);
+        return true;
+    };
+    auto put_lit = [&](uint32_t s) -> bool {
+        gi_lit(out, o, pend, pn, s);
+        if (++lc == 255) {
+            lc = 0;
+            return emit(GI_TOK_LITONLY | 255u);
+        }
+        return true;
+    };
+    while (mode != GI_M_DONE) {
+        GI_TRIP(mode);
+        gi_refill(b);
+        if (mode == GI_M_HDR) {
+            const int m = gi_header<LANES>(b, lit_h, dist_h, H, tab, lane, bfinal, rem);
+            if (m < 0) {
+                rc = -m;
+                break;
+            }
+            if (m == GI_M_STORED && o + rem > out_len) {
+                rc = GI_E_OVERRUN;
+                break;
+            }
+            mode = m;
+        } else if (mode == GI_M_P1 || mode == GI_M_P2) {
+            const int m = mode == GI_M_P1 ? gi_cl_step<LANES, false>(b, in, lit_h, dist_h, H, tab, lane)
+                                          : gi_cl_step<LANES, true>(b, in, lit_h, dist_h, H, tab, lane);
+            if (m < 0) {
+                rc = -m;
+                break;
+            }
+            mode = m;
+        } else if (mode == GI_M_SYM) {
+            const int s = gi_decode<LANES, 15, true>(b, lit_h, tab, lane, GI_T_LIT);
+            if (s < 0 || s > 285) {
+                rc = GI_E_CODE;
+                break;
+            }
+            if (s < 256) {
+                if (o >= out_len) {
+                    rc = GI_E_OVERRUN;
+                    break;
+                }
+                if (!put_lit((uint32_t)s)) {
+                    rc = GI_E_TOKCAP;
+                    break;
+                }
+                GI_BYTES(0, 1);
+            } else if (s == 256) {
+                mode = bfinal ? GI_M_DONE : GI_M_HDR;
+            } else {
+                int lb, le;
+                gi_len_code(s, lb, le);
+                const uint32_t len = (uint32_t)lb + gi_bits(b, le);
+                gi_refill(b);
+                const int d = gi_decode<LANES, 15, false>(b, dist_h, tab, lane, GI_T_DIST);
+                if (d < 0 || d > 29) {
+                    rc = GI_E_DIST;
+                    break;
+                }
+                int db, de;
+                gi_dist_code(d, db, de);
+                const uint32_t dd = (uint32_t)db + gi_bits(b, de);
+                if (dd > o) {
+                    rc = GI_E_DIST;
+                    break;
+                }
+                if (o + len > out_len) {
+                    rc = GI_E_OVERRUN;
+                    break;
+                }
+                if (!emit(lc | (len - 3u) << 8 | (dd - 1u) << 16)) {
+                    rc = GI_E_TOKCAP;
+                    break;
+                }
+                lc = 0;
+                // the pending literals out (their garbage tail lands in this
+                // match's bytes, which phase 2 writes)
+                gi_flush(out, o, out_len, pend, pn);
+                o += len;
+                GI_BYTES(1, len);
+            }
+        } else if (mode == GI_M_STORED) {
+            // byte-aligned: up to 4 bytes from the bit buffer per step
+            const uint32_t m = rem < 4u ? rem : 4u;
+            bool ok = true;
+            for (uint32_t j = 0; j < m; j++) ok = put_lit(gi_bits(b, 8)) && ok;
+            if (!ok) {
+                rc = GI_E_TOKCAP;
+                break;
+            }
+            GI_BYTES(2, m);
+            rem -= m;
+            if (!rem) mode = bfinal ? GI_M_DONE : GI_M_HDR;
+        }
+    }
+    if (rc) return rc;
+    if (lc && !emit(GI_TOK_LITONLY | lc)) return GI_E_TOKCAP;
+    gi_flush(out, o, out_len, pend, pn);
+    // the last group, shifted down to its start
+    const uint32_t tail = nt & 3u;
+    if (tail) {
+        for (uint32_t k = tail; k < 4; k++) tv = (gi_u32x4){tv[1], tv[2], tv[3], 0u};
+        __builtin_memcpy(tok + (nt - tail), &tv, 16);
+    }
+    *ntok = nt;
+    const int64_t used_bits = gi_used(b);
+    if (used_bits > 8 * (int64_t)in_len) return GI_E_INPUT;
+    if (o != out_len) return GI_E_SIZE;
+    return GI_OK;
+}
+
+// the first n (< 16) bytes of a 16-byte piece, exactly: 8, 4, 2, 1-byte stores
+GI_FN void gi_put_part(uint8_t *q, const uint32_t *w, uint32_t n) {
+    uint32_t k = 0;  // words done
+    if (n & 8) {
+        const uint64_t v = (uint64_t)w[0] | (uint64_t)w[1] << 32;
+        __builtin_memcpy(q, &v, 8);
+        k = 2;
+    }
+    uint32_t x = w[k], y = w[k + 1];
+    // (select, not a dynamic index: the piece stays in registers)
+    if (n & 4) {
+        __builtin_memcpy(q + (n & 8), &x, 4);
+        x = y;
+    }
+    const uint32_t at = n & 12u;
+    if (n & 2) {
+        const uint16_t h = (uint16_t)x;
+        __builtin_memcpy(q + at, &h, 2);
+        x >>= 16;
+    }
+    if (n & 1) q[at + (n & 2)] = (uint8_t)x;
+}
+
+// One match: out[o, o + rem) from D bytes back (all of it before o final).
+// A step copies up to 64 bytes (at most the current source distance D,
+// doubled after each step that copies D bytes: the output is periodic with
+// the distance) in 16-byte pieces; the pieces are cut at the match's end, so
+// whatever follows the match (literals already in place) is never touched.
+GI_FN void gi_match(uint8_t *out, uint32_t o, uint32_t rem, uint32_t D) {
+    typedef uint32_t gi_u32x4 __attribute__((vector_size(16)));
+    while (rem) {
+        uint32_t m = rem < GI_COPY ? rem : GI_COPY;
+        m = m < D ? m : D;
+        uint8_t *q = out + o;
+        const uint8_t *src = q - D;
+        gi_u32x4 v0 = {}, v1 = {}, v2 = {}, v3 = {};
+        __builtin_memcpy(&v0, src, 16);
+        if (m > 16) __builtin_memcpy(&v1, src + 16, 16);
+        if (m > 32) __builtin_memcpy(&v2, src + 32, 16);
+        if (m > 48) __builtin_memcpy(&v3, src + 48, 16);
+        // (bytes past m but inside the match are garbage the next step overwrites)
+        const uint32_t span = (m + 15u) & ~15u;
+        const uint32_t lim = rem < span ? rem : span;
+        const uint32_t full = lim >> 4, part = lim & 15u;
+        if (full > 0) __builtin_memcpy(q, &v0, 16);
+        if (full > 1) __builtin_memcpy(q + 16, &v1, 16);
+        if (full > 2) __builtin_memcpy(q + 32, &v2, 16);
+        if (full > 3) __builtin_memcpy(q + 48, &v3, 16);
+        if (part) {
+            const gi_u32x4 lp = full == 0 ? v0 : full == 1 ? v1 : full == 2 ? v2 : v3;
+            uint32_t w[4] = {lp[0], lp[1], lp[2], lp[3]};
+            gi_put_part(q + 16 * full, w, part);
+        }
+        o += m;
+        rem -= m;
+        if (m == D && D < GI_COPY) D <<= 1;
+    }
+}
+
+// Phase 2 for one block on one lane (the host twin's; the device's takes a
+// wave per block, ddecode.hip k_lz77): the tokens tok[0..n) over
+// out[0..out_len), whose literal bytes are already in place, in order.
+// Tokens come four per load.
+GI_FN int gi_lz(const uint32_t *tok, uint32_t n, uint8_t *out, uint32_t out_len) {
+    typedef uint32_t gi_u32x4 __attribute__((vector_size(16)));
+    uint32_t o = 0;
+    gi_u32x4 g = {};
+    for (uint32_t k = 0; k < n; k++) {
+        if ((k & 3u) == 0) __builtin_memcpy(&g, tok + k, 16);
+        const uint32_t t = g[0];
+        g = (gi_u32x4){g[1], g[2], g[3], 0u};
+        o += t & 255u;
+        if (o > out_len) return GI_E_OVERRUN;
+        if (t & GI_TOK_LITONLY) continue;
+        const uint32_t len = ((t >> 8) & 255u) + 3u, d = ((t >> 16) & 0x7fffu) + 1u;
+        if (d > o) return GI_E_DIST;
+        if (o + len > out_len) return GI_E_OVERRUN;
+        gi_match(out, o, len, d);
+        o += len;
+    }
+    return o == out_len ? GI_OK : GI_E_SIZE;
+}

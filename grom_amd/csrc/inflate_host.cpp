@@ -16,6 +16,18 @@ extern "C" int grom_inflate_block_host(const uint8_t *in, uint32_t in_len, uint8
     return gi_inflate<1>(in, in_len, out, out_len, tab, 0);
 }
 
+// the two-phase decoder (gi_tokens, then the tokens replayed): the same bytes
+// as gi_inflate, or GI_E_TOKCAP for a block with more than tokcap tokens
+extern "C" int grom_inflate_block_host2(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t out_len,
+                                        uint32_t tokcap) {
+    thread_local uint32_t tab[GI_LANE_DWORDS];
+    thread_local std::vector<uint32_t> tok;
+    tok.assign(((size_t)tokcap + 3) & ~(size_t)3, 0);
+    uint32_t nt = 0;
+    const int rc = gi_tokens<1>(in, in_len, out, out_len, tok.data(), tokcap & ~3u, &nt, tab, 0);
+    return rc ? rc : gi_lz(tok.data(), nt, out, out_len);
+}
+
 static uint16_t rd16(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 static uint32_t rd32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 
@@ -68,7 +80,12 @@ extern "C" int64_t grom_inflate_selftest(const char *bam_path, int64_t max_block
         // the twin
         memset(b.data(), 0xa5, b.size());
         const int rc = grom_inflate_block_host(data, dlen, b.data(), isize);
-        const bool same = zok ? (rc == GI_OK && memcmp(a.data(), b.data(), isize) == 0) : (rc != GI_OK);
+        bool same = zok ? (rc == GI_OK && memcmp(a.data(), b.data(), isize) == 0) : (rc != GI_OK);
+        // the two-phase decoder: the same bytes, or a refusal (a block over
+        // the token cap) that the one-phase decoder then covers
+        memset(b.data(), 0x5a, b.size());
+        const int rc2 = grom_inflate_block_host2(data, dlen, b.data(), isize, 65536);
+        same = same && (zok ? (rc2 == GI_OK && memcmp(a.data(), b.data(), isize) == 0) : (rc2 != GI_OK));
         if (!same) {
             if (bad < 5) fprintf(stderr, "inflate selftest: block at %ld (isize %u): zlib %d, twin %d\n", off, isize, zrc, rc);
             bad++;

@@ -466,9 +466,13 @@ def test_rank_shares_merge_to_one_run(datadir):
 
     def gather_of(r):
         def g(obj):
+            # (the merge gathers several times: the second wait keeps a fast
+            # rank's next entry out of got until every rank has its copy)
             got[r] = obj
             bar.wait()
-            return list(got)
+            res = list(got)
+            bar.wait()
+            return res
         return g
     errs = []
 
