@@ -329,7 +329,7 @@ __global__ void k_cnv_gather(const GatherRange *__restrict__ rg, int n_rg, const
                              const uint8_t *__restrict__ acw, const int32_t *__restrict__ mq,
                              const int32_t *__restrict__ rd, const int32_t *__restrict__ low,
                              const uint8_t *__restrict__ flag, int64_t total, uint8_t *o_gc, uint8_t *o_ac,
-                             int32_t *o_mq, int32_t *o_rd, int32_t *o_low, uint8_t *o_flag) {
+                             int32_t *o_mq, int32_t *o_rd, int32_t *o_low, int32_t *o_rt, uint8_t *o_flag) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         int lo = 0, hi = n_rg - 1;
         while (lo < hi) {  // range holding output slot i
@@ -343,7 +343,34 @@ __global__ void k_cnv_gather(const GatherRange *__restrict__ rg, int n_rg, const
         o_mq[i] = mq[p];
         o_rd[i] = rd[p];
         o_low[i] = low[p];
+        o_rt[i] = rd[p] + low[p];
         o_flag[i] = flag ? flag[p] : 0;
+    }
+}
+
+// The copy number's per-base ratios (GROM.c:20100-20160) for output slot i
+// of the kept calls' ranges: rt / ave[mapq class][gc], or +inf for a base
+// the reference leaves out (a low base or an empty bin).  8 bytes per base
+// to the host instead of the six gathered arrays' 15 (and their host split).
+__global__ void k_cnv_cn_ratio(const GatherRange *__restrict__ rg, int n_rg, const uint8_t *__restrict__ gcw,
+                               const int32_t *__restrict__ mq, const int32_t *__restrict__ rd,
+                               const int32_t *__restrict__ low, const uint8_t *__restrict__ flag,
+                               const Tables *__restrict__ T, int32_t min_mapq, int64_t total, double *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = n_rg - 1;
+        while (lo < hi) {  // range holding output slot i
+            int mid = (lo + hi + 1) / 2;
+            if (rg[mid].out <= i) lo = mid; else hi = mid - 1;
+        }
+        const GatherRange r = rg[lo];
+        const int64_t p = r.start + (i - r.out) * r.stride;
+        double v = HUGE_VAL;
+        if (!(flag[p] & F_LOW)) {
+            const int k = mq[p] >= min_mapq ? 0 : 1;
+            const double a = T->ave[k][gcw[p]];
+            if (a > 0) v = (double)(rd[p] + low[p]) / a;
+        }
+        out[i] = v;
     }
 }
 
@@ -2523,9 +2550,29 @@ struct CandWords {
     double *bsum, *bmax, *bmin, *babs;  // per word: sum z (nonlow), max/min running sum, sum |z|
     int8_t *kend;        // per word: the last defining class at its end
     double *rsn, *rsa;   // per base: running sum of z inside its word, nonlow bases / all bases
+    double *bmax4, *bmin4;  // per word and quarter (16 bases): max/min of rsn (the classification's finer bound)
     uint64_t *defa, *c1a, *c1n;  // class-defining bases (any / their class-1 bits), class-1 bits of `def`
     uint64_t *pa;        // [kind][class][word]: passing with the class fixed, low bases included
     int64_t n_words;
+    struct SuperW *sup;        // per 8 words (k_cnv_super): phase B's block skip
+    const double *wsdmin512;   // min wsd over 512 window lengths from each length
+    int64_t n_sup;
+};
+
+// Per CW_SUP words (512 bases), for phase B of the classification: a
+// candidate whose class is defined (pass bits pk) at a block's start skips
+// the block in one step when its walk cannot reach -1 inside it (level +
+// the block's lowest walk prefix >= 0) and the block's z bound (largest
+// running sum, at least one more nonlow base, the smallest wsd over the
+// block's lengths) is settled -- the same bound as a word's, over 8 words.
+#define CW_SUP 8
+struct SuperW {
+    // per kind and pass-bit source (0: pk, the class defined; 1 + m: pm with
+    // class m fixed, for a candidate whose class is not defined yet): the pass
+    // walk's change over the block and its lowest prefix
+    int32_t d[2][3], mp[2][3];
+    int32_t nlc, hasdef;      // nonlow bases; any class-defining base (a candidate not yet defined becomes defined inside)
+    double zs, zmx, zmn, za;  // z over nonlow bases: sum, largest/smallest running sum from the block's start; sum |z|
 };
 
 // last defining class per segment of CW_SEG words (for the carry scan)
@@ -2580,6 +2627,15 @@ __global__ __launch_bounds__(256) void k_cnv_words(const uint16_t *__restrict__ 
             if (lane >= d) ps += t;
         }
         double mx = ps, mn = ps, ab = fabs(in ? sd[p] : 0.0);  // |z| of every base: a slack bound for both phases
+        // (per quarter first: lanes 16q..16q+15)
+        for (int o = 8; o > 0; o >>= 1) {
+            mx = fmax(mx, __shfl_xor(mx, o));
+            mn = fmin(mn, __shfl_xor(mn, o));
+        }
+        if ((lane & 15) == 0) {
+            C.bmax4[wi * 4 + (lane >> 4)] = mx;
+            C.bmin4[wi * 4 + (lane >> 4)] = mn;
+        }
         for (int o = 32; o > 0; o >>= 1) {
             mx = fmax(mx, __shfl_xor(mx, o));
             mn = fmin(mn, __shfl_xor(mn, o));
@@ -2641,6 +2697,62 @@ __device__ __forceinline__ void cls_tabs_build(ClsTabs &T) {
         T.minp[by] = (int8_t)mn;
         for (int e = 0; e < 8; e++) T.first[by][e] = f[e];
     }
+}
+
+__global__ __launch_bounds__(256) void k_cnv_super(CandWords C) {
+    __shared__ ClsTabs T;
+    cls_tabs_build(T);
+    __syncthreads();
+    const int64_t sg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sg >= C.n_sup) return;
+    const int64_t nw = C.n_words, w0 = sg * CW_SUP;
+    SuperW o;
+    if (w0 + CW_SUP > nw) {  // a partial block is never skipped
+        for (int k = 0; k < 2; k++)
+            for (int v = 0; v < 3; v++) {
+                o.d[k][v] = 0;
+                o.mp[k][v] = -(1 << 30);
+            }
+        o.nlc = 0;
+        o.hasdef = 1;
+        o.zs = o.zmx = o.zmn = o.za = 0.0;
+        C.sup[sg] = o;
+        return;
+    }
+    int lv[2][3] = {}, mn[2][3], nlc = 0;
+    uint64_t anydef = 0;
+    for (int k = 0; k < 2; k++)
+        for (int v = 0; v < 3; v++) mn[k][v] = 1 << 30;
+    double z = 0.0, mx = -HUGE_VAL, mnz = HUGE_VAL, a = 0.0;
+    for (int64_t w = w0; w < w0 + CW_SUP; w++) {
+        for (int k = 0; k < 2; k++)
+            for (int v = 0; v < 3; v++) {
+                const uint64_t P = v == 0 ? C.pk[k * nw + w] : C.pm[(k * 2 + (v - 1)) * nw + w];
+                for (int b = 0; b < 64; b += 8) {
+                    const uint32_t by = (uint32_t)(P >> b) & 0xffu;
+                    mn[k][v] = min(mn[k][v], lv[k][v] + (int)T.minp[by]);
+                    lv[k][v] += 2 * (int)__popc(by) - 8;
+                }
+            }
+        anydef |= C.def[w];
+        nlc += (int)__popcll(C.nl[w]);
+        mx = fmax(mx, z + C.bmax[w]);
+        mnz = fmin(mnz, z + C.bmin[w]);
+        z += C.bsum[w];
+        a += C.babs[w];
+    }
+    for (int k = 0; k < 2; k++)
+        for (int v = 0; v < 3; v++) {
+            o.d[k][v] = lv[k][v];
+            o.mp[k][v] = mn[k][v];
+        }
+    o.nlc = nlc;
+    o.hasdef = anydef != 0;
+    o.zs = z;
+    o.zmx = mx;
+    o.zmn = mnz;
+    o.za = a;
+    C.sup[sg] = o;
 }
 
 // the first step j in [0, n) at which the walk from level e >= 0 (+1 on a set
@@ -2873,6 +2985,8 @@ __global__ __launch_bounds__(256) void k_cnv_classify_lane(WalkIn W, const int64
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long c_steps = 0, c_skip = 0, c_wstep = 0;
+    // GROM_TIMING, slots 32-35: aligned blocks reached, with the class defined, walk clear, skipped
+    unsigned long long c_blk[4] = {0, 0, 0, 0};
     int c_out = -1;  // 0 jump, 1 first-window undecided, 2 B undecided, -1 no-op
     if (i < n_cand) {
         const int64_t p = cand[i] >> 1;
@@ -2927,6 +3041,31 @@ __global__ __launch_bounds__(256) void k_cnv_classify_lane(WalkIn W, const int64
         {
             const int64_t xlim = min(p + L, end);
             for (int64_t lo = p + ML; lo < xlim;) {
+                if ((lo & (64 * CW_SUP - 1)) == 0 && lo + 64 * CW_SUP <= xlim) {
+                    // (the pass bits over the block: pk once defined, else pm of
+                    // the candidate's class while the block defines nothing)
+                    const SuperW &B = C.sup[lo / (64 * CW_SUP)];
+                    const int v = defined ? 0 : B.hasdef ? -1 : 1 + m;
+                    c_blk[0]++;
+                    if (v >= 0) c_blk[1]++;
+                    if (v >= 0 && E + B.mp[KIND][v] >= 0) {
+                        c_blk[2]++;
+                        const double ub = KIND == 0 ? R + B.zmx : R - B.zmn;
+                        const double dlo = (double)(cnt + 1) * C.wsdmin512[wl + 1];
+                        const double slack = 1e-9 * (A + B.za + fabs(ub)) + 1e-300;
+                        if (dlo > 0 && ub + slack < 3.0 * dlo * (1.0 - 1e-15)) {
+                            c_blk[3]++;
+                            c_skip += CW_SUP;
+                            E += B.d[KIND][v];
+                            wl += 64 * CW_SUP;
+                            cnt += B.nlc;
+                            R += sgn * B.zs;
+                            A += B.za;
+                            lo += 64 * CW_SUP;
+                            continue;
+                        }
+                    }
+                }
                 const int64_t w = lo >> 6, hi = min(xlim, (w + 1) << 6);
                 const int s0 = (int)(lo & 63), n = (int)(hi - lo);
                 const uint64_t M = low_bits(n) << s0;
@@ -2943,8 +3082,29 @@ __global__ __launch_bounds__(256) void k_cnv_classify_lane(WalkIn W, const int64
                     } else {
                         c_wstep++;
                         const uint64_t nlr = C.nl[w] >> s0;
+                        // the same bound per quarter word (16 bases) before its
+                        // passing bases are tested one by one: a quarter's
+                        // largest running sum, at least the nonlow bases before
+                        // it plus its own first, and the smallest wsd from there
+                        uint64_t qdone = 0;  // quarters settled or tested
                         for (uint64_t q = Pr; q; q &= q - 1) {
                             const int k = __ffsll((long long)q) - 1;
+                            const int qi = (s0 + k) >> 4;
+                            if (!((qdone >> qi) & 1)) {
+                                qdone |= 1ull << qi;
+                                const int kq = max((qi << 4) - s0, 0);  // the quarter's first step in the segment
+                                const double ubq = KIND == 0 ? R + (C.bmax4[w * 4 + qi] - base)
+                                                             : R - (C.bmin4[w * 4 + qi] - base);
+                                const double dq = (double)(cnt + __popcll(nlr & low_bits(kq)) + 1) * wsdmin[wl + kq + 1];
+                                const double sq = 1e-9 * (A + C.babs[w] + fabs(ubq)) + 1e-300;
+                                if (dq > 0 && ubq + sq < 3.0 * dq * (1.0 - 1e-15)) {
+                                    // settled: skip the quarter's passing bases
+                                    const int qe = ((qi + 1) << 4) - s0;
+                                    q &= ~low_bits(qe);
+                                    q |= 1ull << k;  // (cleared by the loop step)
+                                    continue;
+                                }
+                            }
                             const double Rk = R + sgn * (C.rsn[lo + k] - base);
                             const int64_t ck = cnt + __popcll(nlr & low_bits(k + 1));
                             const double ws = W.wsd[wl + k + 1];
@@ -2984,6 +3144,8 @@ __global__ __launch_bounds__(256) void k_cnv_classify_lane(WalkIn W, const int64
             atomicAdd(&cst[3], c_steps);
             atomicAdd(&cst[4], c_skip);
             atomicAdd(&cst[7], c_wstep);
+            for (int q = 0; q < 4; q++)
+                if (c_blk[q]) atomicAdd(W.stats + 32 + q, c_blk[q]);
         }
         __syncthreads();
         if (threadIdx.x < 8) atomicAdd(W.stats + 24 + threadIdx.x, cst[threadIdx.x]);
@@ -3031,6 +3193,15 @@ struct CnvScratch {
     Buf gpre, gtmp;                        // insert means above GC_MMAX: chromosome-wide GC/ACGT prefixes
     Buf gcw, acw, rtype, flag, sd, vis, wbits, ztab, nxt, pre, prepos, ppos, rep, misc, blk, hist, tiles, carry, tabs, samples, gat_rg, gat, wd, rows,
         rowlen, wtot, wcnt, wsd, calls, ok;
+    Buf cn_v;                // the copy number's per-base ratios of the kept calls
+    double *h_cn = nullptr;  // pinned: their host copy
+    size_t h_cn_cap = 0;
+    // pinned host buffers of the gathers (gather(): at most three alive at once)
+    struct PinBuf {
+        uint8_t *p = nullptr;
+        size_t cap = 0;
+        bool busy = false;
+    } pin[4];
     hipEvent_t e0 = nullptr, e1 = nullptr;
 };
 
@@ -3164,45 +3335,70 @@ static void sort_depths(std::vector<int> &v) {
         for (uint32_t c = 0; c < h[x]; c++) v[k++] = x;
 }
 
+// Per-position values of gathered ranges on the host, views of one pinned
+// buffer the device copy lands in (round 5 copied 15 bytes per position into
+// a zero-filled pageable vector and split it into six more: 54-74 ms per
+// chromosome for the copy numbers' ~6 M positions); rt = rd + low is made on
+// the device.  The buffer goes back to the scratch's pool with the view.
 struct Gathered {
-    std::vector<uint8_t> gc, ac, flag;
-    std::vector<int32_t> mq, rt, rd, low;
+    const uint8_t *gc = nullptr, *ac = nullptr, *flag = nullptr;
+    const int32_t *mq = nullptr, *rd = nullptr, *low = nullptr, *rt = nullptr;
+    CnvScratch::PinBuf *pb = nullptr;
+    Gathered() = default;
+    Gathered(const Gathered &) = delete;
+    Gathered &operator=(const Gathered &) = delete;
+    ~Gathered() {
+        if (pb) pb->busy = false;
+    }
 };
 
 static int gather(CnvScratch *S, hipStream_t st, const std::vector<GatherRange> &rg, int64_t total, const uint8_t *gcw,
                   const uint8_t *acw, const int32_t *mq, const int32_t *rd, const int32_t *low, const uint8_t *flag,
                   Gathered &g, char *err, size_t errlen) {
-    g.gc.resize(total);
-    g.ac.resize(total);
-    g.flag.resize(total);
-    g.mq.resize(total);
-    g.rt.resize(total);
-    g.rd.resize(total);
-    g.low.resize(total);
     if (total == 0 || rg.empty()) return GROM_OK;
     int rc;
-    if ((rc = grow(S->gat_rg, sizeof(GatherRange) * rg.size(), err, errlen)) ||
-        (rc = grow(S->gat, (size_t)total * 15, err, errlen)))
+    const size_t bytes = (size_t)total * 19;
+    if ((rc = grow(S->gat_rg, sizeof(GatherRange) * rg.size(), err, errlen)) || (rc = grow(S->gat, bytes, err, errlen)))
         return rc;
+    CnvScratch::PinBuf *pb = nullptr;
+    for (auto &b : S->pin)
+        if (!b.busy) {
+            pb = &b;
+            break;
+        }
+    if (!pb) {
+        snprintf(err, errlen, "CNV gather: no free pinned buffer");
+        return GROM_E_NOMEM;
+    }
+    if (pb->cap < bytes) {
+        if (pb->p) (void)hipHostFree(pb->p);
+        pb->p = nullptr;
+        pb->cap = 0;
+        const size_t want = bytes + bytes / 4 + 4096;
+        CK(hipHostMalloc((void **)&pb->p, want, 0));
+        pb->cap = want;
+    }
+    pb->busy = true;
+    g.pb = pb;
     CK(hipMemcpyAsync(S->gat_rg.p, rg.data(), sizeof(GatherRange) * rg.size(), hipMemcpyHostToDevice, st));
     uint8_t *o = (uint8_t *)S->gat.p;
-    int32_t *o_mq = (int32_t *)o, *o_rd = o_mq + total, *o_low = o_rd + total;
-    uint8_t *o_gc = (uint8_t *)(o_low + total), *o_ac = o_gc + total, *o_f = o_ac + total;
+    int32_t *o_mq = (int32_t *)o, *o_rd = o_mq + total, *o_low = o_rd + total, *o_rt = o_low + total;
+    uint8_t *o_gc = (uint8_t *)(o_rt + total), *o_ac = o_gc + total, *o_f = o_ac + total;
     int g_ = (int)std::min<int64_t>((total + 255) / 256, 16384);
     hipLaunchKernelGGL(k_cnv_gather, dim3(g_), dim3(256), 0, st, (const GatherRange *)S->gat_rg.p, (int)rg.size(), gcw,
-                       acw, mq, rd, low, flag, total, o_gc, o_ac, o_mq, o_rd, o_low, o_f);
+                       acw, mq, rd, low, flag, total, o_gc, o_ac, o_mq, o_rd, o_low, o_rt, o_f);
     CK(hipGetLastError());
-    // the six gathered arrays lie back to back: one copy, split on the host
-    std::vector<uint8_t> hb((size_t)total * 15);
-    CK(hipMemcpyAsync(hb.data(), o, (size_t)total * 15, hipMemcpyDeviceToHost, st));
+    // the seven arrays lie back to back: one copy, viewed in place
+    CK(hipMemcpyAsync(pb->p, o, bytes, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
-    memcpy(g.mq.data(), hb.data(), 4 * (size_t)total);
-    memcpy(g.rd.data(), hb.data() + 4 * (size_t)total, 4 * (size_t)total);
-    memcpy(g.low.data(), hb.data() + 8 * (size_t)total, 4 * (size_t)total);
-    memcpy(g.gc.data(), hb.data() + 12 * (size_t)total, (size_t)total);
-    memcpy(g.ac.data(), hb.data() + 13 * (size_t)total, (size_t)total);
-    memcpy(g.flag.data(), hb.data() + 14 * (size_t)total, (size_t)total);
-    for (int64_t i = 0; i < total; i++) g.rt[i] = g.rd[i] + g.low[i];
+    const int32_t *h = (const int32_t *)pb->p;
+    g.mq = h;
+    g.rd = h + total;
+    g.low = h + 2 * total;
+    g.rt = h + 3 * total;
+    g.gc = (const uint8_t *)(h + 4 * total);
+    g.ac = g.gc + total;
+    g.flag = g.ac + total;
     return GROM_OK;
 }
 
@@ -3307,7 +3503,7 @@ int cnv_prelaunch(CnvScratch *S, hipStream_t after, const grom_params &P, const 
     {&S->flag, &S->sd, &S->vis, &S->wbits, &S->ztab, &S->nxt, &S->pre, &S->prepos, &S->ppos, &S->rep, &S->misc,       \
      &S->blk, &S->hist, &S->tiles, &S->carry, &S->tabs, &S->samples, &S->gat_rg, &S->gat, &S->wd, &S->rows,           \
      &S->rowlen, &S->wtot, &S->wcnt, &S->wsd, &S->calls, &S->ok, &S->zover, &S->cwords, &S->cw_seg, &S->cw_carry,      \
-     &S->wsdmin, &S->gen1000, &S->gpre, &S->gtmp}
+     &S->wsdmin, &S->gen1000, &S->gpre, &S->gtmp, &S->cn_v}
 #define CNV_KIND_BUFS(K) \
     {&K.nxt, &K.pre, &K.prepos, &K.ppos, &K.calls, &K.ok, &K.tiles, &K.vis, &K.cnt, &K.und, &K.skip, &K.pend, &K.plist}
 
@@ -3339,6 +3535,10 @@ void cnv_scratch_sync(CnvScratch *S) {
 
 void cnv_scratch_free(CnvScratch *S) {
     if (!S) return;
+    if (S->h_cn) (void)hipHostFree(S->h_cn);
+    S->h_cn = nullptr;
+    for (auto &b : S->pin)
+        if (b.p) (void)hipHostFree(b.p);
     Buf *all[] = CNV_PHASE_BUFS(S);
     for (Buf *b : all)
         if (b->p && b->own) grom_dev_free(b->p, b->cap, GROM_DEVCAT_CNV);
@@ -3980,7 +4180,9 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
         CandWords CW{};
         {
             const int64_t n_words = (len + 63) / 64 + 1, n_seg = (n_words + CW_SEG - 1) / CW_SEG;
-            const size_t wbytes = (size_t)n_words * (15 * 8 + 4 * 8 + 1) + 256 + 2 * 8 * (size_t)n_words * 64;
+            const int64_t n_sup = (n_words + CW_SUP - 1) / CW_SUP;
+            const size_t wbytes = (size_t)n_words * (15 * 8 + 4 * 8 + 8 * 8 + 1) + 256 + 2 * 8 * (size_t)n_words * 64 +
+                                  sizeof(SuperW) * (size_t)n_sup + 8 * (size_t)(L + 2) + 64;
             if ((rc = grow(S->cwords, wbytes, err, errlen)) || (rc = grow(S->cw_seg, (size_t)n_seg, err, errlen)) ||
                 (rc = grow(S->cw_carry, (size_t)n_seg, err, errlen)) || (rc = grow(S->wsdmin, 8 * (size_t)(L + 2), err, errlen)))
                 return rc;
@@ -4001,7 +4203,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             CW.babs = dd + 3 * n_words;
             CW.rsn = dd + 4 * n_words;
             CW.rsa = CW.rsn + n_words * 64;
-            CW.kend = (int8_t *)(CW.rsa + n_words * 64);
+            CW.bmax4 = CW.rsa + n_words * 64;
+            CW.bmin4 = CW.bmax4 + 4 * n_words;
+            CW.kend = (int8_t *)(CW.bmin4 + 4 * n_words);
+            {
+                uintptr_t q = ((uintptr_t)(CW.kend + n_words) + 63) & ~(uintptr_t)63;
+                CW.sup = (SuperW *)q;
+                CW.n_sup = n_sup;
+                CW.wsdmin512 = (const double *)(CW.sup + n_sup);
+            }
             const unsigned gs = (unsigned)((n_seg * 64 + 255) / 256);
             hipLaunchKernelGGL(k_cnv_cls_seg, dim3(gs), dim3(256), 0, st, (const uint16_t *)S->wbits.p, len, n_seg,
                                (int8_t *)S->cw_seg.p);
@@ -4018,6 +4228,16 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
             }
             wmin[L + 1] = 0.0;
             CK(hipMemcpyAsync(S->wsdmin.p, wmin.data(), 8 * (L + 2), hipMemcpyHostToDevice, st));
+            // the same over 512 lengths (phase B's block skip), from the 64-length minima
+            std::vector<double> wmin512((size_t)L + 2, 0.0);
+            for (int64_t a = 0; a <= L; a++) {
+                double v = wmin[a];
+                for (int64_t b2 = a + 64; b2 <= std::min<int64_t>(a + 511, L); b2 += 64) v = std::min(v, wmin[b2]);
+                wmin512[a] = v;
+            }
+            CK(hipMemcpyAsync((void *)CW.wsdmin512, wmin512.data(), 8 * (L + 2), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_cnv_super, dim3((unsigned)((n_sup + 255) / 256)), dim3(256), 0, st, CW);
+            CK(hipGetLastError());
             CK(hipStreamSynchronize(st));  // wmin is released on scope exit
         }
         const int64_t span = std::max<int64_t>(0, WI.end - WI.start);
@@ -4135,6 +4355,10 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                         if (tmg) {
                             unsigned long long cs8[8];
                             (void)hipMemcpy(cs8, WK.stats + 24, sizeof(cs8), hipMemcpyDeviceToHost);
+                            unsigned long long cb4[4];
+                            (void)hipMemcpy(cb4, WK.stats + 32, sizeof(cb4), hipMemcpyDeviceToHost);
+                            fprintf(stderr, "cnv classify %s blocks: %llu reached, %llu with known pass bits, %llu walk clear, %llu skipped\n",
+                                    kind == 0 ? "DEL" : "DUP", cb4[0], cb4[1], cb4[2], cb4[3]);
                             fprintf(stderr, "cnv classify %s: %u candidates, %u undecided (%s); jumps %llu, first-window "
                                     "undecided %llu, B undecided %llu, no-ops %llu, bases tested %llu, segments settled by the bound %llu, "
                                     "segments tested %llu\n", kind == 0 ? "DEL" : "DUP", ncand, nu,
@@ -4338,19 +4562,38 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 rg.push_back(GatherRange{c.p, n, 1, tot});
                 tot += n;
             }
-            Gathered g;
-            if ((rc = gather(S, st, rg, tot, gcw, acw, d_mq, d_rd, d_low, flag, g, err, errlen))) return rc;
+            const auto tg0 = std::chrono::steady_clock::now();
+            if (tot > 0) {
+                const size_t nb = (size_t)tot;
+                if ((rc = grow(S->gat_rg, sizeof(GatherRange) * rg.size(), err, errlen)) ||
+                    (rc = grow(S->cn_v, 8 * nb, err, errlen)))
+                    return rc;
+                if (S->h_cn_cap < nb) {
+                    if (S->h_cn) (void)hipHostFree(S->h_cn);
+                    S->h_cn = nullptr;
+                    S->h_cn_cap = 0;
+                    const size_t want = nb + nb / 4 + 4096;
+                    CK(hipHostMalloc((void **)&S->h_cn, 8 * want, 0));
+                    S->h_cn_cap = want;
+                }
+                CK(hipMemcpyAsync(S->gat_rg.p, rg.data(), sizeof(GatherRange) * rg.size(), hipMemcpyHostToDevice, st));
+                const int g_ = (int)std::min<int64_t>((tot + 255) / 256, 16384);
+                hipLaunchKernelGGL(k_cnv_cn_ratio, dim3(g_), dim3(256), 0, st, (const GatherRange *)S->gat_rg.p,
+                                   (int)rg.size(), gcw, d_mq, d_rd, d_low, flag, dT, (int32_t)P.rd_min_mapq, tot,
+                                   (double *)S->cn_v.p);
+                CK(hipGetLastError());
+                CK(hipMemcpyAsync(S->h_cn, S->cn_v.p, 8 * nb, hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+            }
+            const auto tg1 = std::chrono::steady_clock::now();
             // copy number of every kept call (GROM.c:20100-20160): independent per
             // call, so host threads share them; the rows are then written in order
             std::vector<double> cnv_cn(keep.size(), -1.0), cnv_cs(keep.size(), 0.0);
             auto cn_of = [&](size_t j, std::vector<double> &pl, std::vector<double> &tmp) {
                 pl.clear();
-                for (int64_t i = 0; i < rg[j].count; i++) {
-                    const int64_t o = rg[j].out + i;
-                    if (g.flag[o] & F_LOW) continue;
-                    const int k = g.mq[o] >= P.rd_min_mapq ? 0 : 1;
-                    if (T.ave[k][g.gc[o]] > 0) pl.push_back((double)g.rt[o] / T.ave[k][g.gc[o]]);
-                }
+                const double *v = S->h_cn + rg[j].out;
+                for (int64_t i = 0; i < rg[j].count; i++)
+                    if (v[i] < HUGE_VAL) pl.push_back(v[i]);  // (the reference's list, in base order)
                 double cn = -1, cns = 0;
                 const long pc = (long)pl.size();
                 if (pc > 0) {
@@ -4382,6 +4625,15 @@ int cnv_chrom(CnvScratch *S, hipStream_t st, const grom_params &P, uint32_t seed
                 for (unsigned t = 1; t < nt; t++) th.emplace_back(worker);
                 worker();
                 for (auto &t : th) t.join();
+                if (tmg) {
+                    const auto tg2 = std::chrono::steady_clock::now();
+                    int64_t mx = 0;
+                    for (size_t j = 0; j < keep.size(); j++) mx = std::max<int64_t>(mx, rg[j].count);
+                    fprintf(stderr, "cnv rows %s: %zu calls, %lld bases (largest %lld), %u threads; gather %.1f ms, copy number %.1f ms\n",
+                            kind == 0 ? "DEL" : "DUP", keep.size(), (long long)tot, (long long)mx, nt,
+                            std::chrono::duration<double, std::milli>(tg1 - tg0).count(),
+                            std::chrono::duration<double, std::milli>(tg2 - tg1).count());
+                }
             }
             // -f: a column header before each kind's rows (GROM.c:17242-17245,
             // 17378), rows named by caf_del_text / caf_dup_text (GROM.c:1575)

@@ -486,12 +486,13 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
     memset(&d, 0, sizeof(d));
     d.pos = x;
     bool any_indel = false;
+    // the "other" slots in use are a prefix [0, n_used) (a slot is never
+    // emptied again), so none is initialised until it is first taken: the
+    // 300 scratch stores per base of round 5 were most of the fold's time
     int32_t ocnt[OTHER_LEN], omchr[OTHER_LEN], ors[OTHER_LEN], ore[OTHER_LEN];
     double odist[OTHER_LEN];
     uint8_t otype[OTHER_LEN];
-    for (int o = 0; o < OTHER_LEN; o++) {
-        ocnt[o] = 0; omchr[o] = 0; ors[o] = 0; ore[o] = 0; odist[o] = 0.0; otype[o] = OT_EMPTY;
-    }
+    int n_used = 0;
     const uint32_t b = run_off[r], e_end = b + run_len[r];
     for (uint32_t j = b; j < e_end; j++) {
         const SvEv E = ev[order[j]];
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
                 *cnt += add;
             } else {
                 bool found = false;
-                for (int o = 0; o < OTHER_LEN; o++) {
+                for (int o = 0; o < n_used; o++) {
                     if (otype[o] == E.type) {
                         if ((uint32_t)E.len == (uint32_t)(odist[o] + 0.5)) {
                             found = true;
@@ -532,13 +533,16 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
                             }
                             break;
                         }
-                    } else if (otype[o] == OT_EMPTY) {
-                        found = true;
-                        ocnt[o] = add;
-                        otype[o] = E.type;
-                        odist[o] = (double)E.len;
-                        break;
                     }
+                }
+                if (!found && n_used < OTHER_LEN) {  // the first empty slot
+                    const int o = n_used++;
+                    found = true;
+                    ocnt[o] = add;
+                    otype[o] = E.type;
+                    odist[o] = (double)E.len;
+                    omchr[o] = 0;
+                    ors[o] = ore[o] = 0;
                 }
                 if (!found) {
                     for (int o = 0; o < OTHER_LEN; o++) {
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
             // an "other" slot write leaves the group's flags alone but moves no
             // primary data, so it cannot strand DUP evidence
             bool found = false;
-            for (int o = 0; o < OTHER_LEN; o++) {
+            for (int o = 0; o < n_used; o++) {
                 if (otype[o] == (uint8_t)E.type) {
                     if (compat(E, odist[o], ocnt[o], omchr[o])) {
                         found = true;
@@ -597,15 +601,16 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
                         }
                         break;
                     }
-                } else if (otype[o] == OT_EMPTY) {
-                    found = true;
-                    ocnt[o] = E.w;
-                    otype[o] = E.type;
-                    odist[o] = E.v;
-                    if (pm) omchr[o] = E.mchr;
-                    ors[o] = ore[o] = E.rp;
-                    break;
                 }
+            }
+            if (!found && n_used < OTHER_LEN) {  // the first empty slot
+                const int o = n_used++;
+                found = true;
+                ocnt[o] = E.w;
+                otype[o] = E.type;
+                odist[o] = E.v;
+                omchr[o] = pm ? E.mchr : 0;
+                ors[o] = ore[o] = E.rp;
             }
             if (!found) {
                 for (int o = 0; o < OTHER_LEN; o++) {
@@ -621,9 +626,7 @@ __global__ __launch_bounds__(64) void k_sv_fold(uint32_t n_runs, const uint32_t 
             }
         }
     }
-    int other_len = OTHER_LEN;  // GROM.c:11415-11425
-    for (int o = 0; o < OTHER_LEN; o++)
-        if (otype[o] == OT_EMPTY) { other_len = o; break; }
+    const int other_len = n_used;  // the first empty slot, GROM.c:11415-11425
     d.other_len = other_len;
     const int32_t thr = AF * O.min_disc;  // count / 6 >= g_min_disc
     bool cand = d.ins >= thr || d.del_f >= thr || d.del_r >= thr;
