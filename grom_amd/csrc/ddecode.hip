@@ -1055,10 +1055,12 @@ __global__ void __launch_bounds__(256) k_copy_tiles(const uint8_t *__restrict__ 
 
 // The same copy driven by the reads: 16 lanes per kept read, lane l moving
 // bytes [16 l, 16 l + 16) of its quality (QUAL) or packed-base region with
-// one unaligned 16-byte load and store, the read's last few bytes singly
-// (16-byte stores past a read's end would write the next read's bytes,
-// another lane's); an odd-length read's pad quality byte is 0.  A wave's
-// loads and stores cover four reads' regions, contiguous in both arrays.
+// one unaligned 16-byte load and store; the region's last partial piece is
+// loaded whole too (U has slack past every record) and stored exactly, as
+// 8/4/2/1-byte stores (a 16-byte store past a read's end would write the
+// next read's bytes, another lane's; round 5 moved those bytes one by one);
+// an odd-length read's pad quality byte is 0.  A wave's loads and stores
+// cover four reads' regions, contiguous in both arrays.
 template <bool QUAL>
 __global__ void __launch_bounds__(256) k_copy_reads(const uint8_t *__restrict__ U, const int64_t *__restrict__ srcs,
                                                     const int64_t *__restrict__ boff, const int32_t *__restrict__ lq,
@@ -1076,12 +1078,21 @@ __global__ void __launch_bounds__(256) k_copy_reads(const uint8_t *__restrict__ 
         uint8_t *d = dst + (QUAL ? boff[k0 + q] : boff[k0 + q] / 2) + o;
         const int64_t m = L - o < 16 ? L - o : 16;
         const bool pad = QUAL && (l & 1) && o + m == L;  // the region's last byte is the pad
-        if (m == 16 && !pad) {
-            u32x4 v;
-            __builtin_memcpy(&v, src, 16);
+        u32x4 v;
+        __builtin_memcpy(&v, src, 16);
+        if (pad) {  // byte m - 1 of the piece: 0
+            const int pb = (int)m - 1;
+            const uint32_t keep = ~(0xffu << (8 * (pb & 3)));
+            v[0] &= (pb >> 2) == 0 ? keep : 0xffffffffu;
+            v[1] &= (pb >> 2) == 1 ? keep : 0xffffffffu;
+            v[2] &= (pb >> 2) == 2 ? keep : 0xffffffffu;
+            v[3] &= (pb >> 2) == 3 ? keep : 0xffffffffu;
+        }
+        if (m == 16) {
             __builtin_memcpy(d, &v, 16);
         } else {
-            for (int64_t j = 0; j < m; j++) d[j] = (pad && j == m - 1) ? 0 : src[j];
+            uint32_t w[4] = {v[0], v[1], v[2], v[3]};
+            gi_put_part(d, w, (uint32_t)m);
         }
     }
 }
