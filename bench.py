@@ -233,6 +233,28 @@ def rows_digest(path):
     return n, h.hexdigest()
 
 
+def inflate_roofline(dec_line):
+    """The GPU BGZF inflater (k_inflate, the largest event time of a whole
+    run) beside the pileup's roofline: algorithmic bytes = the compressed
+    bytes read + the inflated bytes written, over the CLI's summed HIP-event
+    time of the inflate launches (the decode line of the last timed run)."""
+    if not dec_line or not dec_line.startswith("device decode"):
+        return None
+    m = re.search(r"([\d.]+) GB compressed.*?([\d.]+) GB inflated.*?GPU inflate ([\d.]+) s", dec_line)
+    if not m:
+        return None
+    comp, infl, sec = float(m.group(1)), float(m.group(2)), float(m.group(3))
+    if sec <= 0:
+        return None
+    achieved = (comp + infl) / sec
+    return {"bound": "hbm", "kernel": "k_inflate", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_model": "compressed bytes read + inflated bytes written per genome (DESIGN.md 4.5)",
+            "event_s": sec, "gb_in": comp, "gb_out": infl,
+            "note": "latency-bound (one DEFLATE block per lane, each match an L2 round trip); its launches "
+                    "share the chip with the scans"}
+
+
 def roofline_of(per_launch, alone=None):
     """per_launch: [(bytes, ms, chrom_len)] of the pileup kernel's launches."""
     byt = sum(b for b, _, _ in per_launch)
@@ -613,6 +635,7 @@ def main():
             "identical_to_oracle_full_scale": full["identical"] if full else None,
             "oracle_full_scale": full,
             "roofline": roofline_of(launches, alone) if launches else None,
+            "roofline_inflate": inflate_roofline(dec[-1] if dec else None),
             "cpu_baseline": cpu,
             "concordance": conc,
             "device_resident": resident,
