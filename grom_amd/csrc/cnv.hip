@@ -1729,8 +1729,14 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
     int64_t pa = s.pa, cnt = s.cnt, last_good = s.last_good, ce = s.ce;
     double tot = s.tot;
     // the largest good ratio per lane; max is exact and order-free, so the
-    // wave's maximum is taken once, when the slide ends or pauses
-    double lmax = 0.0;
+    // wave's maximum is taken once, when the slide ends or pauses.  Kept as
+    // the step's (tot, divisor) with the largest exact quotient (compared by
+    // exact cross products, two-product FMAs) and divided once at the end:
+    // rounding is monotonic, so RN of the largest quotient is the largest of
+    // the reference's RN(tot / divisor), without a division per good step
+    // (the division was most of the slide's work after the sum chain)
+    double bt = 0.0, bd = 1.0;
+    bool bany = false;
     int mqi = s.mqi, mqb = s.mqb;
     bool finished = true;
     const long long ck_start = W.stats ? clock64() : 0;
@@ -1800,11 +1806,11 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
         pc_chain += ck1 - ck0;
         pc_before += ck0 - ckt;
         bool good[4];
-        double ts[4];
+        double dv[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            good[i] = inl[i] && cj[i] > 0 && wsdL > 0 && ratio_ge_min(tj[i], cj[i] * wsdL) && LOW_FRAC_OK;
-            ts[i] = good[i] ? tj[i] / (cj[i] * wsdL) : 0.0;
+            dv[i] = cj[i] * wsdL;  // (the reference's divisor, rounded as it is)
+            good[i] = inl[i] && cj[i] > 0 && wsdL > 0 && ratio_ge_min(tj[i], dv[i]) && LOW_FRAC_OK;
         }
         // the loop test of step j (GROM.c:19492) sees the last good step
         // before it; no step of the round can fail it while pa + 255 is
@@ -1836,7 +1842,15 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
         for (int i = 0; i < 4; i++) {
             const bool eg = good[i] && 4 * lane + i < js;
             eg_last = eg ? 4 * lane + i : eg_last;
-            lmax = (eg && ts[i] > lmax) ? ts[i] : lmax;
+            // tj / dv > bt / bd  <=>  tj * bd > bt * dv (both divisors > 0), exactly
+            const double p1 = tj[i] * bd, e1 = fma(tj[i], bd, -p1);
+            const double p2 = bt * dv[i], e2 = fma(bt, dv[i], -p2);
+            const bool gt = !bany || p1 > p2 || (p1 == p2 && e1 > e2);
+            if (eg && gt) {
+                bt = tj[i];
+                bd = dv[i];
+                bany = true;
+            }
         }
         const unsigned long long gm = __ballot(eg_last >= 0);
         if (gm) last_good = ce = pa + __builtin_amdgcn_readlane(eg_last, 63 - __clzll(gm));
@@ -1878,6 +1892,7 @@ __device__ bool slide_run(const WalkIn &W, SlideState &s, int64_t cap) {
     s.last_good = last_good;
     s.ce = ce;
     s.tot = tot;
+    const double lmax = bany ? bt / bd : 0.0;
     const double mx = dpp_max_pos(lmax);  // ratios are >= 3 > 0; lanes without one hold 0
     if (mx > s.stdevs) s.stdevs = mx;
     s.mqi = mqi;
