@@ -8,6 +8,7 @@ import filecmp
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -735,19 +736,12 @@ def test_two_ranks_sharded_genome_matches_one_rank():
     assert bnd.count("SVTYPE=BND") >= 2, bnd
 
 
-def test_device_inflate_matches_zlib(datadir, tmp_path):
-    """The GPU BGZF inflater (ddecode.hip, one block per lane) against zlib
-    on every block: synthetic BAMs compressed by libdeflate (levels 1, 6, 9)
-    and by zlib, and BGZF files of stored, fixed-Huffman, Huffman-only,
-    run-length and overlapping-match blocks (the CPU test's chunks)."""
-    import ctypes
+def _inflate_inputs(tmp_path):
+    """synthetic BAMs compressed by libdeflate (levels 1, 6, 9) and by zlib,
+    and BGZF files of stored, fixed-Huffman, Huffman-only, run-length and
+    overlapping-match blocks (the CPU test's chunks)"""
     import zlib
     from test_host import _bgzf_blocks
-    lib = grom_amd.lib()
-    f = lib.grom_inflate_device_selftest
-    f.restype = ctypes.c_int64
-    f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
-                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     paths = []
     for lv, nolib in (("1", False), ("6", False), ("9", False), ("6", True)):
         env = dict(os.environ, GROM_SYNTH_LEVEL=lv)
@@ -771,10 +765,57 @@ def test_device_inflate_matches_zlib(datadir, tmp_path):
         p = tmp_path / f"chunks{level}_{strategy}.bgzf"
         p.write_bytes(_bgzf_blocks(chunks, level, strategy) * 3)
         paths.append(str(p))
+    return paths
+
+
+_INFLATE_SELFTEST = """
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+import grom_amd
+f = grom_amd.lib().grom_inflate_device_selftest
+f.restype = ctypes.c_int64
+f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+for path in sys.argv[2:]:
+    ms, nb, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+    bad = f(path.encode(), 0, 0, 1, ctypes.byref(ms), ctypes.byref(nb), ctypes.byref(by))
+    print(path, bad, nb.value, flush=True)
+"""
+
+
+def test_device_inflate_matches_zlib(datadir, tmp_path):
+    """The GPU BGZF inflater (ddecode.hip, one block per lane) against zlib
+    on every block of _inflate_inputs."""
+    import ctypes
+    lib = grom_amd.lib()
+    f = lib.grom_inflate_device_selftest
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    paths = _inflate_inputs(tmp_path)
     for path in paths:
         ms, nb, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
         bad = f(path.encode(), 0, 0, 1, ctypes.byref(ms), ctypes.byref(nb), ctypes.byref(by))
         assert bad == 0 and nb.value > 10, (path, bad, nb.value)
+
+
+@pytest.mark.parametrize("tokcap", ["4096", "64"])
+def test_two_phase_inflate_matches_zlib(tmp_path, tokcap):
+    """The two-phase inflate variant (GROM_INFLATE_TOKCAP, DESIGN.md 4.5:
+    Huffman tokens, then the wave-per-block LZ77 replay) against zlib on the
+    same inputs; a cap of 64 tokens sends nearly every block of the BAMs to
+    the one-phase fallback launch (status GI_E_TOKCAP).  A child process: the
+    cap is read once per process."""
+    paths = _inflate_inputs(tmp_path)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _INFLATE_SELFTEST, repo] + paths, capture_output=True, text=True,
+                       env=dict(os.environ, GROM_INFLATE_TOKCAP=tokcap), timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.split("\n")
+    got = [l.rsplit(" ", 2) for l in lines if l.strip()]
+    assert len(got) == len(paths), r.stdout
+    for path, bad, nb in got:
+        assert int(bad) == 0 and int(nb) > 10, (path, bad, nb)
 
 
 @pytest.mark.parametrize("case,extra", [("three_chr", []), ("sv", ["-S"]), ("sv", []), ("dups", ["-M"]),
